@@ -1,0 +1,137 @@
+/* mitty_hip.h — C ABI of libmitty_hip.so, the MI355X (gfx950) generate-reads engine.
+ *
+ * Plain C types only (pointers + sizes); no torch / HIP types cross this boundary.  Every call returns an int32
+ * status (MH_OK == 0, negative = error) and leaves a message in mh_last_error(ctx).  The Python package
+ * mitty_amd binds this with ctypes (mitty_amd/_native.py); INTEGRATION.md shows the binding a maintainer of the
+ * reference would add.
+ *
+ * Which reference interface each entry point replaces (paths relative to the reference repo root):
+ *   mh_upload_contig      pysam.FastaFile.fetch of a BED region          mitty/simulation/readgenerate.py:181,186
+ *   mh_build_haplotype    rpc.create_node_list (+ rpc.Node)              mitty/simulation/rpc.py:5-116
+ *                         fed by vcfio.split_copies/parse per copy       mitty/lib/vcfio.py:67-126
+ *   mh_sample_templates   illumina.generate_reads                        mitty/simulation/illumina.py:43-110
+ *   mh_set_templates      (the template arrays a read module returns)   mitty/simulation/illumina.py:238-269
+ *   mh_get_templates      (same arrays back to the host)
+ *   mh_emit_reads         read_generating_worker loop + fastq_lines      mitty/simulation/readgenerate.py:184-230
+ *   mh_read_batch         rpc.get_begin_end_nodes + rpc.generate_read    mitty/simulation/rpc.py:119-160
+ *   mh_set_corruption     illumina.corrupt_template (Philox mode)        mitty/simulation/illumina.py:113-162
+ *                         + readcorrupt.multi_process's worker loop        mitty/simulation/readcorrupt.py:73-93
+ *   mh_work_units         readgenerate.get_data_for_workers              mitty/simulation/readgenerate.py:129-159
+ *   mh_read_model_params  illumina.read_model_params                     mitty/simulation/illumina.py:12-40
+ *
+ * Threading: one mh_ctx per GPU and per host thread; a context owns one HIP stream and all device buffers.
+ * Calls are synchronous at return (device work is ordered on the context's stream; results copied back are
+ * complete).  Outputs of mh_emit_reads stay device-resident in the context's FASTQ arenas until fetched.
+ */
+#ifndef MITTY_HIP_H
+#define MITTY_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mh_ctx mh_ctx;
+
+enum {
+  MH_OK = 0,
+  MH_E_ARG = -1,              /* bad argument (ValueError in the Python facade) */
+  MH_E_HIP = -2,              /* HIP runtime error */
+  MH_E_OOM = -3,              /* device allocation failed */
+  MH_E_CAPACITY = -4,         /* caller buffer too small: *used / *needed says how much */
+  MH_E_COMPLEX_VARIANT = -5,  /* a variant that is not SNP/INS/DEL (vcfio.py:124 ValueError) */
+  MH_E_SEED = -6,             /* seed outside 0..2^32-1 (illumina.py:53-54 ValueError) */
+  MH_E_STATE = -7,            /* call out of order (e.g. emit before sampling) */
+  MH_E_NO_DEVICE = -8         /* no HIP device */
+};
+
+enum { MH_RNG_MITTY = 0, MH_RNG_PHILOX = 1 };
+
+/* ---- context ------------------------------------------------------------------------------------------- */
+int32_t mh_version(void);
+int32_t mh_device_count(int32_t *out);
+int32_t mh_create(int32_t device, mh_ctx **out);
+int32_t mh_destroy(mh_ctx *ctx);
+const char *mh_last_error(const mh_ctx *ctx);
+/* Synchronise the context's stream. */
+int32_t mh_sync(mh_ctx *ctx);
+
+/* ---- host-side helpers that mirror the reference's scalar logic ---------------------------------------- */
+int32_t mh_read_model_params(int64_t mean_rlen, double coverage, double *p, int64_t *passes);
+/* Work units in the reference's shuffled order; arrays sized sum(ploidy) * passes. */
+int32_t mh_work_units(uint64_t seed, const int32_t *ploidy, int64_t n_regions, int64_t passes,
+                      int32_t *out_region, int32_t *out_cpy, uint32_t *out_seed, int64_t *out_n);
+
+/* ---- reference sequence and haplotypes ----------------------------------------------------------------- */
+/* Upload (or replace) contig `contig_id` — the bytes of one BED region as fetched from the FASTA. */
+int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_t len);
+/* Splice one chromosome copy on the device: variants (1-based pos, op 'X'/'I'/'D', oplen, alt bytes in
+ * alt_pool[alt_off .. +alt_len)) applied to contig `contig_id`, whose first base has 1-based coordinate
+ * ref_start_pos.  Result kept in haplotype slot `slot`.  Outputs: node count, p_min, p_max (rpc/readgenerate.py:192). */
+int32_t mh_build_haplotype(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos,
+                           const int64_t *v_pos, const uint8_t *v_op, const int64_t *v_oplen,
+                           const int64_t *v_alt_off, const int64_t *v_alt_len, const char *alt_pool,
+                           int64_t alt_pool_len, int64_t n_var,
+                           int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max);
+/* Copy a slot's node list back (arrays sized n_nodes; seq bytes of node k = hap[ps[k]-p_min .. +oplen) for
+ * non-'D' nodes).  Any pointer may be NULL. */
+int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_t *op, int64_t *oplen,
+                     char *hap, int64_t hap_cap, int64_t *hap_len);
+int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot);
+
+/* ---- templates ----------------------------------------------------------------------------------------- */
+/* illumina.generate_reads for haplotype `slot` (p_min/p_max from the slot).  rng_mode MH_RNG_MITTY reproduces
+ * numpy's MT19937 streams bit for bit; MH_RNG_PHILOX is the counter-based fast mode. */
+int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, const double *cum_tlen,
+                            int32_t n_tlen, uint64_t seed, int32_t rng_mode, int64_t *out_n_templates);
+/* Same, for an explicit [p_min, p_max) span with no haplotype (the plugin-level generate_reads). */
+int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen,
+                                 const double *cum_tlen, int32_t n_tlen, uint64_t seed, int32_t rng_mode,
+                                 int64_t *out_n_templates);
+int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, const int64_t *pos1, int64_t n,
+                         int32_t rlen);
+int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1, int64_t cap, int64_t *n);
+
+/* ---- read emission ------------------------------------------------------------------------------------- */
+/* Turn the current templates into FASTQ text for both files, appended to the device arenas.
+ * serial_stub = "{sample}:{worker}:{ps}" (readgenerate.py:195).  unit_key keys the corruption stream (ignored when
+ * corruption is off; pass the unit's rng_seed).  Outputs: kept templates, bytes appended. */
+int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                      int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_bytes1,
+                      int64_t *out_bytes2);
+int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);
+/* Copy arena bytes [offset, offset+len) of file 1 / file 2 to host (either host pointer may be NULL). */
+int32_t mh_output_fetch(mh_ctx *ctx, int64_t offset1, char *fq1, int64_t len1, int64_t offset2, char *fq2,
+                        int64_t len2);
+int32_t mh_output_reset(mh_ctx *ctx);
+
+/* rpc.generate_read for a batch of (p, l) on haplotype `slot`: positions, start/end nodes and the text fields.
+ * Text outputs are concatenated; *_off arrays (n+1 entries) index them.  MH_E_CAPACITY if a text buffer is short
+ * (needed sizes returned in *cigar_used / *vlist_used / *seq_used). */
+int32_t mh_read_batch(mh_ctx *ctx, int32_t slot, const int64_t *p, const int64_t *l, int64_t n,
+                      int64_t *out_pos, int64_t *out_n0, int64_t *out_n1,
+                      char *cigar, int64_t cigar_cap, int64_t *cigar_off, int64_t *cigar_used,
+                      char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
+                      char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used);
+
+/* ---- corruption (Philox mode) -------------------------------------------------------------------------- */
+/* Configure the empirical-BQ corruption (illumina.corrupt_template, illumina.py:113-162) that mh_emit_reads then
+ * applies while it writes each record: per base bq = min(searchsorted(cum_bq[file][n], U1), 93), the base replaced
+ * by one of the other three ('NNN' for non-ACGT) when U2 < phred_p[bq], quality chr(bq + 33) instead of '~'.
+ * U1/U2/choice come from Philox4x32-10 keyed by (seed, unit_key) and counted by (template, file, base), so the
+ * output does not depend on GPU count or launch geometry.  cum_bq: f64[2][max_bp][n_bq]; phred_p: f64[100]
+ * (pass the reference's own 10 ** (-arange(100) / 10)).  enable = 0 turns it off. */
+int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int32_t max_bp, int32_t n_bq,
+                          const double *phred_p, uint64_t seed);
+
+/* ---- timing / profiling hooks ------------------------------------------------------------------------- */
+/* Per-stage device time of the most recent mh_emit_reads / mh_sample_templates / mh_build_haplotype calls,
+ * measured with HIP events on the context's stream (milliseconds); names are static strings. */
+int32_t mh_stage_times(mh_ctx *ctx, const char **names, double *ms, int32_t cap, int32_t *n);
+int32_t mh_enable_timing(mh_ctx *ctx, int32_t on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,281 @@
+"""ctypes binding of libmitty_hip.so (include/mitty_hip.h).
+
+There is no CPU fallback: if the library is missing or no HIP device is present, the product path raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libmitty_hip.so')
+
+MH_OK, MH_E_ARG, MH_E_HIP, MH_E_OOM, MH_E_CAPACITY, MH_E_COMPLEX_VARIANT, MH_E_SEED, MH_E_STATE, MH_E_NO_DEVICE = \
+  0, -1, -2, -3, -4, -5, -6, -7, -8
+MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
+
+# Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
+EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
+           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_get_nodes',
+           'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
+           'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
+           'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing']
+
+
+class NativeError(RuntimeError):
+  pass
+
+
+class NativeUnavailable(NativeError):
+  pass
+
+
+_lib = None
+
+c_i32, c_i64, c_u64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p
+P_i64 = ctypes.POINTER(c_i64)
+
+
+def _sig(L, name, args, res=c_i32):
+  f = getattr(L, name)
+  f.argtypes = args
+  f.restype = res
+
+
+def lib():
+  """Load the library (raises NativeUnavailable when it has not been built)."""
+  global _lib
+  if _lib is not None:
+    return _lib
+  if not os.path.exists(LIB_PATH):
+    raise NativeUnavailable('libmitty_hip.so not built ({}); run __graft_entry__.build() or make -C '
+                            'mitty_amd/csrc'.format(LIB_PATH))
+  L = ctypes.CDLL(LIB_PATH)
+  _sig(L, 'mh_version', [])
+  _sig(L, 'mh_device_count', [ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_create', [c_i32, ctypes.POINTER(c_vp)])
+  _sig(L, 'mh_destroy', [c_vp])
+  _sig(L, 'mh_last_error', [c_vp], ctypes.c_char_p)
+  _sig(L, 'mh_sync', [c_vp])
+  _sig(L, 'mh_read_model_params', [c_i64, c_dbl, ctypes.POINTER(c_dbl), P_i64])
+  _sig(L, 'mh_work_units', [c_u64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, P_i64])
+  _sig(L, 'mh_upload_contig', [c_vp, c_i32, c_vp, c_i64])
+  _sig(L, 'mh_build_haplotype', [c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                 P_i64, P_i64, P_i64])
+  _sig(L, 'mh_get_nodes', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_release_haplotype', [c_vp, c_i32])
+  _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
+  _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
+  _sig(L, 'mh_set_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32])
+  _sig(L, 'mh_get_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
+  _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
+  _sig(L, 'mh_output_reset', [c_vp])
+  _sig(L, 'mh_read_batch', [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                            c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64])
+  _sig(L, 'mh_set_corruption', [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_u64])
+  _sig(L, 'mh_stage_times', [c_vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_dbl), c_i32,
+                             ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_enable_timing', [c_vp, c_i32])
+  _lib = L
+  return L
+
+
+def device_count():
+  n = c_i32(0)
+  lib().mh_device_count(ctypes.byref(n))
+  return n.value
+
+
+def _ptr(a):
+  return a.ctypes.data_as(c_vp) if a is not None else None
+
+
+def _raise(rc, msg):
+  if rc in (MH_E_ARG, MH_E_COMPLEX_VARIANT, MH_E_SEED):
+    raise ValueError(msg)
+  if rc == MH_E_OOM:
+    raise MemoryError(msg)
+  if rc == MH_E_NO_DEVICE:
+    raise NativeUnavailable('no HIP device visible: ' + msg)
+  raise NativeError('libmitty_hip error {}: {}'.format(rc, msg))
+
+
+def read_model_params(mean_rlen, coverage):
+  p, passes = c_dbl(), c_i64()
+  rc = lib().mh_read_model_params(int(mean_rlen), float(coverage), ctypes.byref(p), ctypes.byref(passes))
+  if rc:
+    _raise(rc, 'bad read model parameters')
+  return p.value, passes.value
+
+
+def work_units(seed, ploidy, passes):
+  ploidy = np.ascontiguousarray(ploidy, dtype=np.int32)
+  n = int(ploidy.sum()) * int(passes)
+  r, c, s = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.uint32)
+  nn = c_i64()
+  rc = lib().mh_work_units(int(seed), _ptr(ploidy), len(ploidy), int(passes), _ptr(r), _ptr(c), _ptr(s),
+                           ctypes.byref(nn))
+  if rc:
+    _raise(rc, 'Seed must be between 0 and 2**32 - 1')
+  return [(int(a), int(b), int(x)) for a, b, x in zip(r[:n], c[:n], s[:n])]
+
+
+class Context:
+  """One device context (one GPU, one stream).  Wraps mh_ctx."""
+
+  def __init__(self, device=0):
+    L = lib()
+    h = c_vp()
+    rc = L.mh_create(int(device), ctypes.byref(h))
+    if rc:
+      _raise(rc, 'mh_create(device={}) failed'.format(device))
+    self._h = h
+    self._L = L
+    self.device = device
+
+  def close(self):
+    if self._h:
+      self._L.mh_destroy(self._h)
+      self._h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def _chk(self, rc):
+    if rc:
+      _raise(rc, self._L.mh_last_error(self._h).decode(errors='replace'))
+
+  # ---- contigs / haplotypes ----------------------------------------------------------------------------
+  def upload_contig(self, contig_id, seq):
+    buf = np.frombuffer(seq, dtype=np.uint8) if len(seq) else np.zeros(1, np.uint8)
+    self._chk(self._L.mh_upload_contig(self._h, contig_id, _ptr(buf), len(seq)))
+
+  def build_haplotype(self, slot, contig_id, ref_start_pos, vsoa):
+    """vsoa: dict with pos i64, op u8, oplen i64, alt_off i64, alt_len i64, alt_pool bytes."""
+    n = len(vsoa['pos'])
+    pool = vsoa['alt_pool']
+    pool_arr = np.frombuffer(pool, dtype=np.uint8) if len(pool) else np.zeros(1, np.uint8)
+    nn, pmin, pmax = c_i64(), c_i64(), c_i64()
+    arrs = [np.ascontiguousarray(vsoa[k], dtype=dt) for k, dt in
+            (('pos', np.int64), ('op', np.uint8), ('oplen', np.int64), ('alt_off', np.int64), ('alt_len', np.int64))]
+    self._chk(self._L.mh_build_haplotype(self._h, slot, contig_id, int(ref_start_pos), *[_ptr(a) for a in arrs],
+                                         _ptr(pool_arr), len(pool), n, ctypes.byref(nn), ctypes.byref(pmin),
+                                         ctypes.byref(pmax)))
+    return nn.value, pmin.value, pmax.value
+
+  def get_nodes(self, slot, n_nodes, with_hap=True):
+    ps, pr, ol = (np.empty(max(n_nodes, 1), np.int64) for _ in range(3))
+    op = np.empty(max(n_nodes, 1), np.uint8)
+    hl = c_i64()
+    self._chk(self._L.mh_get_nodes(self._h, slot, None, None, None, None, None, 0, ctypes.byref(hl)))
+    hap = np.empty(max(hl.value, 1), np.uint8) if with_hap else None
+    self._chk(self._L.mh_get_nodes(self._h, slot, _ptr(ps), _ptr(pr), _ptr(op), _ptr(ol), _ptr(hap),
+                                   hl.value if with_hap else 0, ctypes.byref(hl)))
+    return ps[:n_nodes], pr[:n_nodes], op[:n_nodes], ol[:n_nodes], (hap[:hl.value].tobytes() if with_hap else None)
+
+  def release_haplotype(self, slot):
+    self._chk(self._L.mh_release_haplotype(self._h, slot))
+
+  # ---- templates ---------------------------------------------------------------------------------------
+  def sample_templates(self, slot, p, rlen, cum_tlen, seed, rng_mode=MH_RNG_MITTY):
+    ct = np.ascontiguousarray(cum_tlen, dtype=np.float64)
+    n = c_i64()
+    self._chk(self._L.mh_sample_templates(self._h, slot, float(p), int(rlen), _ptr(ct), len(ct), int(seed),
+                                          int(rng_mode), ctypes.byref(n)))
+    return n.value
+
+  def sample_templates_span(self, p_min, p_max, p, rlen, cum_tlen, seed, rng_mode=MH_RNG_MITTY):
+    if not (0 <= int(seed) <= 0xffffffff):
+      raise ValueError('Seed value {} is out of range 0 - {}'.format(seed, 0xffffffff))
+    ct = np.ascontiguousarray(cum_tlen, dtype=np.float64)
+    n = c_i64()
+    self._chk(self._L.mh_sample_templates_span(self._h, int(p_min), int(p_max), float(p), int(rlen), _ptr(ct),
+                                               len(ct), int(seed), int(rng_mode), ctypes.byref(n)))
+    return n.value
+
+  def set_templates(self, fo0, pos0, pos1, rlen):
+    fo0 = np.ascontiguousarray(fo0, dtype=np.int8)
+    pos0 = np.ascontiguousarray(pos0, dtype=np.int64)
+    pos1 = np.ascontiguousarray(pos1, dtype=np.int64)
+    self._chk(self._L.mh_set_templates(self._h, _ptr(fo0), _ptr(pos0), _ptr(pos1), len(fo0), int(rlen)))
+
+  def get_templates(self):
+    n = c_i64()
+    self._L.mh_get_templates(self._h, None, None, None, 0, ctypes.byref(n))
+    m = n.value
+    fo0, p0, p1 = np.empty(max(m, 1), np.int8), np.empty(max(m, 1), np.int64), np.empty(max(m, 1), np.int64)
+    self._chk(self._L.mh_get_templates(self._h, _ptr(fo0), _ptr(p0), _ptr(p1), max(m, 1), ctypes.byref(n)))
+    return fo0[:m], p0[:m], p1[:m]
+
+  # ---- emission ----------------------------------------------------------------------------------------
+  def emit_reads(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+    k, b1, b2 = c_i64(), c_i64(), c_i64()
+    self._chk(self._L.mh_emit_reads(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                    1 if write_fastq2 else 0, int(unit_key), ctypes.byref(k), ctypes.byref(b1),
+                                    ctypes.byref(b2)))
+    return k.value, b1.value, b2.value
+
+  def output_size(self):
+    a, b = c_i64(), c_i64()
+    self._chk(self._L.mh_output_size(self._h, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
+
+  def fetch_output(self, off1=0, len1=None, off2=0, len2=None):
+    u1, u2 = self.output_size()
+    len1 = u1 - off1 if len1 is None else len1
+    len2 = u2 - off2 if len2 is None else len2
+    b1 = np.empty(max(len1, 1), np.uint8)
+    b2 = np.empty(max(len2, 1), np.uint8)
+    self._chk(self._L.mh_output_fetch(self._h, off1, _ptr(b1), len1, off2, _ptr(b2) if len2 > 0 else None, len2))
+    return b1[:len1].tobytes(), b2[:len2].tobytes()
+
+  def reset_output(self):
+    self._chk(self._L.mh_output_reset(self._h))
+
+  def read_batch(self, slot, p, l):
+    p = np.ascontiguousarray(p, dtype=np.int64)
+    l = np.ascontiguousarray(l, dtype=np.int64)
+    n = len(p)
+    pos, n0, n1 = (np.empty(max(n, 1), np.int64) for _ in range(3))
+    offs = [np.empty(n + 1, np.int64) for _ in range(3)]
+    used = [c_i64() for _ in range(3)]
+    caps = [max(64, 64 * n), max(64, 16 * n), max(64, int(l.sum()) + 16 if n else 64)]
+    for _ in range(2):
+      bufs = [np.empty(c, np.uint8) for c in caps]
+      rc = self._L.mh_read_batch(self._h, slot, _ptr(p), _ptr(l), n, _ptr(pos), _ptr(n0), _ptr(n1),
+                                 _ptr(bufs[0]), caps[0], _ptr(offs[0]), ctypes.byref(used[0]),
+                                 _ptr(bufs[1]), caps[1], _ptr(offs[1]), ctypes.byref(used[1]),
+                                 _ptr(bufs[2]), caps[2], _ptr(offs[2]), ctypes.byref(used[2]))
+      if rc == MH_E_CAPACITY:
+        caps = [max(c, u.value + 16) for c, u in zip(caps, used)]
+        continue
+      self._chk(rc)
+      break
+    texts = [b[:u.value].tobytes().decode('latin-1') for b, u in zip(bufs, used)]
+    return pos[:n], n0[:n], n1[:n], texts, offs
+
+  def set_corruption(self, enable, cum_bq=None, phred_p=None, seed=0):
+    if not enable:
+      self._chk(self._L.mh_set_corruption(self._h, 0, None, 0, 0, None, 0))
+      return
+    cb = np.ascontiguousarray(cum_bq, dtype=np.float64)
+    ph = np.ascontiguousarray(phred_p, dtype=np.float64)
+    self._chk(self._L.mh_set_corruption(self._h, 1, _ptr(cb), cb.shape[1], cb.shape[2], _ptr(ph), int(seed)))
+
+  def enable_timing(self, on=True):
+    self._chk(self._L.mh_enable_timing(self._h, 1 if on else 0))
+
+  def stage_times(self):
+    n = c_i32()
+    self._L.mh_stage_times(self._h, None, None, 0, ctypes.byref(n))
+    names = (ctypes.c_char_p * max(n.value, 1))()
+    ms = (c_dbl * max(n.value, 1))()
+    self._L.mh_stage_times(self._h, names, ms, n.value, ctypes.byref(n))
+    return [(names[i].decode(), ms[i]) for i in range(n.value)]
+
+  def sync(self):
+    self._chk(self._L.mh_sync(self._h))

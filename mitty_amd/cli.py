@@ -1,0 +1,91 @@
+"""`mitty` command line (reference mitty/cli.py), MI355X build.
+
+Implemented: generate-reads (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
+--rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Out of scope for this build (not on the
+generate-reads path): filter-variants, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
+"""
+import logging
+import os
+
+import click
+
+
+@click.group()
+@click.version_option('2.7.3.dev0+mi355x')
+@click.option('-v', '--verbose', type=int, default=0)
+def cli(verbose):
+  """A genomic data simulator for testing and debugging bio-informatics tools"""
+  logging.basicConfig(level=[logging.ERROR, logging.WARNING, logging.INFO, logging.DEBUG][min(verbose, 3)])
+
+
+@cli.command('list-read-models')
+@click.option('-d', type=click.Path(exists=True), help='List models in this directory')
+def list_read_models(d):
+  """List read models"""
+  import glob
+  from mitty_amd import readmodel
+  if d is None:
+    files = [os.path.join(readmodel.BUILTIN_DIR, f) for f in sorted(os.listdir(readmodel.BUILTIN_DIR))]
+  else:
+    files = glob.glob(os.path.join(d, '*'))
+  for f in files:
+    try:
+      m = readmodel.load_model_file(f)
+      name = os.path.basename(f)
+      if name.endswith('.npz'):
+        name = name[:-4] + '.pkl'
+      click.echo('\n----------\n{}:\n{}\n=========='.format(name, m['model_description']))
+    except Exception:
+      logging.debug('Skipping {}. Not a read model file'.format(f))
+
+
+@cli.command()
+def qname():
+  """Display qname format"""
+  from mitty_amd.simulation import readgenerate
+  click.echo(readgenerate.__qname_format_details__)
+
+
+def print_qname(ctx, param, value):
+  if not value or ctx.resilient_parsing:
+    return
+  from mitty_amd.simulation import readgenerate
+  click.echo(readgenerate.__qname_format_details__)
+  ctx.exit()
+
+
+@cli.command('generate-reads', short_help='Generate simulated reads.')
+@click.argument('fasta')
+@click.argument('vcf')
+@click.argument('sample_name')
+@click.argument('bed')
+@click.argument('modelfile')
+@click.argument('coverage', type=float)
+@click.argument('seed', type=int)
+@click.argument('fastq1', type=click.Path())
+@click.option('--fastq2', type=click.Path())
+@click.option('--threads', default=2, help='Accepted for compatibility; the work runs on the GPU')
+@click.option('--qname', is_flag=True, callback=print_qname, expose_value=False, is_eager=True,
+              help='Print documentation for information encoded in qname')
+@click.option('--device', default=0, help='HIP device ordinal')
+@click.option('--rng', type=click.Choice(['mitty', 'philox']), default='mitty',
+              help='mitty: bit-exact with the reference; philox: counter-based fast mode')
+@click.option('--corrupt-seed', type=int, default=None, help='Apply the BQ corruption model while writing')
+def generate_reads(fasta, vcf, sample_name, bed, modelfile, coverage, seed, fastq1, fastq2, threads, device, rng,
+                   corrupt_seed):
+  """Generate simulated reads"""
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  read_module, model = get_read_model(modelfile)
+  stats = readgenerate.process_multi_threaded(fasta, vcf, sample_name, bed, read_module, model, coverage, fastq1,
+                                              fastq2, threads=threads, seed=seed, device=device, rng=rng,
+                                              corrupt_seed=corrupt_seed)
+  logging.info('generate-reads: {}'.format(stats))
+
+
+def main():
+  cli()
+
+
+if __name__ == '__main__':
+  main()

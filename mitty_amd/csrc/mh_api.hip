@@ -1,0 +1,421 @@
+// mh_api.hip — the C ABI (include/mitty_hip.h): context, buffers, argument checks, dispatch to the subsystems.
+#include <cmath>
+#include <cstring>
+
+#include "mh_internal.h"
+
+namespace mh {
+
+int32_t hip_fail(mh_ctx *ctx, hipError_t e, const char *what, const char *file, int line) {
+  if (ctx) {
+    ctx->err = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") in " + what + " at " +
+               file + ":" + std::to_string(line);
+  }
+  return e == hipErrorOutOfMemory ? MH_E_OOM : MH_E_HIP;
+}
+
+int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return MH_OK;
+  if (b.p) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t c = bytes + bytes / 8 + 256;
+  hipError_t e = hipMalloc(&b.p, c);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    (void)hipGetLastError();
+    return arg_fail(ctx, MH_E_OOM, "device allocation of " + std::to_string(c) + " bytes failed");
+  }
+  b.cap = c;
+  return MH_OK;
+}
+
+int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
+  if (b.cap >= bytes) return MH_OK;
+  DevBuf nb;
+  MH_TRY(ensure(ctx, nb, bytes + bytes / 2));
+  if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (b.p) HIPCHK(ctx, hipFree(b.p));
+  b = nb;
+  return MH_OK;
+}
+
+void release(DevBuf &b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+}
+
+void stage_begin(mh_ctx *ctx, const char *name) {
+  if (!ctx->timing) return;
+  StageTime s{name, nullptr, nullptr};
+  (void)hipEventCreate(&s.a);
+  (void)hipEventCreate(&s.b);
+  (void)hipEventRecord(s.a, ctx->stream);
+  ctx->stages.push_back(s);
+}
+
+void stage_end(mh_ctx *ctx) {
+  if (!ctx->timing || ctx->stages.empty()) return;
+  StageTime s = ctx->stages.back();
+  ctx->stages.pop_back();
+  (void)hipEventRecord(s.b, ctx->stream);   // resolved later by stages_collect: no host sync here
+  ctx->pending.push_back(s);
+}
+
+void stages_collect(mh_ctx *ctx) {
+  for (auto &s : ctx->pending) {
+    (void)hipEventSynchronize(s.b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, s.a, s.b);
+    ctx->last_times.emplace_back(s.name, (double)ms);
+    (void)hipEventDestroy(s.a);
+    (void)hipEventDestroy(s.b);
+  }
+  ctx->pending.clear();
+}
+
+}  // namespace mh
+
+using namespace mh;
+
+#define CTX_GUARD(ctx)                                                     \
+  do {                                                                     \
+    if (!(ctx)) return MH_E_ARG;                                           \
+    hipError_t _e = hipSetDevice((ctx)->device);                           \
+    if (_e != hipSuccess) return hip_fail((ctx), _e, "hipSetDevice", __FILE__, __LINE__); \
+  } while (0)
+
+extern "C" {
+
+int32_t mh_version(void) { return 1; }
+
+int32_t mh_device_count(int32_t *out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  *out = n;
+  return MH_OK;
+}
+
+int32_t mh_create(int32_t device, mh_ctx **out) {
+  if (!out) return MH_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    (void)hipGetLastError();
+    return MH_E_NO_DEVICE;
+  }
+  if (device < 0 || device >= n) return MH_E_ARG;
+  mh_ctx *ctx = new mh_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return MH_E_HIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->max_cu = prop.multiProcessorCount;
+  *out = ctx;
+  return MH_OK;
+}
+
+int32_t mh_destroy(mh_ctx *ctx) {
+  if (!ctx) return MH_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &kv : ctx->contigs) release(kv.second.seq);
+  for (auto &kv : ctx->haps) {
+    Hap &h = kv.second;
+    release(h.hap); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
+    release(h.nrun_s); release(h.nrun_e);
+  }
+  release(ctx->t_fo0); release(ctx->t_pos0); release(ctx->t_pos1);
+  for (auto &b : ctx->s) release(b);
+  release(ctx->scan_partials); release(ctx->d_small);
+  release(ctx->corrupt_cum); release(ctx->corrupt_phred);
+  release(ctx->out1); release(ctx->out2);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return MH_OK;
+}
+
+const char *mh_last_error(const mh_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int32_t mh_sync(mh_ctx *ctx) {
+  CTX_GUARD(ctx);
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+// illumina.read_model_params (illumina.py:12-40)
+int32_t mh_read_model_params(int64_t mean_rlen, double coverage, double *p_out, int64_t *passes_out) {
+  if (!p_out || !passes_out || mean_rlen <= 0) return MH_E_ARG;
+  double p = 1.0;
+  int64_t passes = 1;
+  while (p > 0.1) {
+    passes *= 2;
+    p = 0.5 * coverage / (double)(2 * mean_rlen * passes);
+  }
+  *p_out = p;
+  *passes_out = passes;
+  return MH_OK;
+}
+
+// readgenerate.get_data_for_workers (readgenerate.py:129-159)
+int32_t mh_work_units(uint64_t seed, const int32_t *ploidy, int64_t n_regions, int64_t passes, int32_t *out_region,
+                      int32_t *out_cpy, uint32_t *out_seed, int64_t *out_n) {
+  if (seed > 0xffffffffull) return MH_E_SEED;
+  if (n_regions < 0 || passes < 0 || (n_regions && !ploidy)) return MH_E_ARG;
+  HostMT s;
+  s.seed((uint32_t)seed);
+  uint32_t shuffle_seed = (uint32_t)s.interval(0xfffffffeull);
+  int64_t n = 0;
+  for (int64_t r = 0; r < n_regions; r++)
+    for (int32_t c = 0; c < ploidy[r]; c++)
+      for (int64_t k = 0; k < passes; k++) {
+        out_region[n] = (int32_t)r;
+        out_cpy[n] = c;
+        out_seed[n] = (uint32_t)s.interval(0xfffffffeull);
+        n++;
+      }
+  HostMT sh;
+  sh.seed(shuffle_seed);
+  for (int64_t i = n - 1; i >= 1; i--) {
+    int64_t j = (int64_t)sh.interval((uint64_t)i);
+    std::swap(out_region[i], out_region[j]);
+    std::swap(out_cpy[i], out_cpy[j]);
+    std::swap(out_seed[i], out_seed[j]);
+  }
+  *out_n = n;
+  return MH_OK;
+}
+
+int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_t len) {
+  CTX_GUARD(ctx);
+  if (len < 0 || (len > 0 && !seq)) return arg_fail(ctx, MH_E_ARG, "bad contig");
+  Contig &c = ctx->contigs[contig_id];
+  MH_TRY(ensure(ctx, c.seq, len + 16));
+  if (len) HIPCHK(ctx, hipMemcpyAsync(c.seq.p, seq, len, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  c.len = len;
+  return MH_OK;
+}
+
+int32_t mh_build_haplotype(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, const int64_t *v_pos,
+                           const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
+                           const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var,
+                           int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
+  CTX_GUARD(ctx);
+  auto it = ctx->contigs.find(contig_id);
+  if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+  if (n_var < 0 || (n_var > 0 && (!v_pos || !v_op || !v_oplen || !v_alt_off || !v_alt_len)))
+    return arg_fail(ctx, MH_E_ARG, "bad variant arrays");
+  Hap &h = ctx->haps[slot];
+  h.valid = false;
+  MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v_pos, v_op, v_oplen, v_alt_off, v_alt_len, alt_pool,
+                      alt_pool_len, n_var));
+  if (out_n_nodes) *out_n_nodes = h.n_nodes;
+  if (out_p_min) *out_p_min = h.p_min;
+  if (out_p_max) *out_p_max = h.p_max;
+  return MH_OK;
+}
+
+int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_t *op, int64_t *oplen, char *hap,
+                     int64_t hap_cap, int64_t *hap_len) {
+  CTX_GUARD(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  Hap &h = it->second;
+  hipStream_t st = ctx->stream;
+  size_t n = (size_t)h.n_nodes;
+  if (ps) HIPCHK(ctx, hipMemcpyAsync(ps, h.ps.p, 8 * n, hipMemcpyDeviceToHost, st));
+  if (pr) HIPCHK(ctx, hipMemcpyAsync(pr, h.pr.p, 8 * n, hipMemcpyDeviceToHost, st));
+  if (op) HIPCHK(ctx, hipMemcpyAsync(op, h.op.p, n, hipMemcpyDeviceToHost, st));
+  if (oplen) HIPCHK(ctx, hipMemcpyAsync(oplen, h.oplen.p, 8 * n, hipMemcpyDeviceToHost, st));
+  if (hap_len) *hap_len = h.hap_len;
+  if (hap) {
+    if (hap_cap < h.hap_len) {
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      return arg_fail(ctx, MH_E_CAPACITY, "haplotype buffer too small");
+    }
+    if (h.hap_len) HIPCHK(ctx, hipMemcpyAsync(hap, h.hap.p, h.hap_len, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return MH_OK;
+}
+
+int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
+  CTX_GUARD(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end()) return MH_OK;
+  Hap &h = it->second;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  release(h.hap); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
+  release(h.nrun_s); release(h.nrun_e);
+  ctx->haps.erase(it);
+  return MH_OK;
+}
+
+int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                            uint64_t seed, int32_t rng_mode, int64_t *out_n) {
+  CTX_GUARD(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0)) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return sample_templates(ctx, it->second.p_min, it->second.p_max, p, rlen, cum_tlen, n_tlen, seed, rng_mode, out_n);
+}
+
+int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen,
+                                 const double *cum_tlen, int32_t n_tlen, uint64_t seed, int32_t rng_mode,
+                                 int64_t *out_n) {
+  CTX_GUARD(ctx);
+  if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0) || p_max < p_min)
+    return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return sample_templates(ctx, p_min, p_max, p, rlen, cum_tlen, n_tlen, seed, rng_mode, out_n);
+}
+
+int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, const int64_t *pos1, int64_t n,
+                         int32_t rlen) {
+  CTX_GUARD(ctx);
+  if (n < 0 || rlen <= 0 || (n > 0 && (!fo0 || !pos0 || !pos1))) return arg_fail(ctx, MH_E_ARG, "bad templates");
+  for (int64_t i = 0; i < n; i++)
+    if (fo0[i] != 0 && fo0[i] != 1) return arg_fail(ctx, MH_E_ARG, "file_order must be 0/1");
+  MH_TRY(ensure(ctx, ctx->t_fo0, n + 1));
+  MH_TRY(ensure(ctx, ctx->t_pos0, 8 * (n + 1)));
+  MH_TRY(ensure(ctx, ctx->t_pos1, 8 * (n + 1)));
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->t_fo0.p, fo0, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->t_pos0.p, pos0, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->t_pos1.p, pos1, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->n_tpl = n;
+  ctx->rlen = rlen;
+  ctx->have_tpl = true;
+  return MH_OK;
+}
+
+int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1, int64_t cap, int64_t *n) {
+  CTX_GUARD(ctx);
+  if (!ctx->have_tpl) return arg_fail(ctx, MH_E_STATE, "no templates");
+  if (n) *n = ctx->n_tpl;
+  if (cap < ctx->n_tpl) return arg_fail(ctx, MH_E_CAPACITY, "template buffers too small");
+  size_t m = (size_t)ctx->n_tpl;
+  if (m) {
+    if (fo0) HIPCHK(ctx, hipMemcpyAsync(fo0, ctx->t_fo0.p, m, hipMemcpyDeviceToHost, ctx->stream));
+    if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ctx->t_pos0.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ctx->t_pos1.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                      int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+  CTX_GUARD(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
+  return emit_reads(ctx, it->second, serial_stub, chrom, cpy, write_fastq2, unit_key, out_kept, out_b1, out_b2);
+}
+
+int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
+  if (!ctx) return MH_E_ARG;
+  if (b1) *b1 = ctx->used1;
+  if (b2) *b2 = ctx->used2;
+  return MH_OK;
+}
+
+int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2, int64_t len2) {
+  CTX_GUARD(ctx);
+  if ((fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
+      (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
+    return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
+  if (fq1 && len1) HIPCHK(ctx, hipMemcpyAsync(fq1, (char *)ctx->out1.p + off1, len1, hipMemcpyDeviceToHost, ctx->stream));
+  if (fq2 && len2) HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_output_reset(mh_ctx *ctx) {
+  if (!ctx) return MH_E_ARG;
+  ctx->used1 = ctx->used2 = 0;
+  return MH_OK;
+}
+
+int32_t mh_read_batch(mh_ctx *ctx, int32_t slot, const int64_t *p, const int64_t *l, int64_t n, int64_t *out_pos,
+                      int64_t *out_n0, int64_t *out_n1, char *cigar, int64_t cigar_cap, int64_t *cigar_off,
+                      int64_t *cigar_used, char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
+                      char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used) {
+  CTX_GUARD(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (n < 0 || !cigar_used || !vlist_used || !seq_used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return read_batch(ctx, it->second, p, l, n, out_pos, out_n0, out_n1, cigar, cigar_cap, cigar_off, cigar_used, vlist,
+                    vlist_cap, vlist_off, vlist_used, seq, seq_cap, seq_off, seq_used);
+}
+
+int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int32_t max_bp, int32_t n_bq,
+                          const double *phred_p, uint64_t seed) {
+  CTX_GUARD(ctx);
+  if (!enable) {
+    ctx->corrupt_on = false;
+    return MH_OK;
+  }
+  if (!cum_bq || !phred_p || max_bp <= 0 || n_bq <= 0 || n_bq > 4096)
+    return arg_fail(ctx, MH_E_ARG, "bad corruption model");
+  if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
+  std::vector<float> f((size_t)2 * max_bp * n_bq);
+  for (size_t i = 0; i < f.size(); i++) f[i] = (float)cum_bq[i];
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, 4 * f.size()));
+  MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_cum.p, f.data(), 4 * f.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->corrupt_on = true;
+  ctx->corrupt_max_bp = max_bp;
+  ctx->corrupt_n_bq = n_bq;
+  ctx->corrupt_seed = seed;
+  return MH_OK;
+}
+
+int32_t mh_enable_timing(mh_ctx *ctx, int32_t on) {
+  if (!ctx) return MH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  stages_collect(ctx);
+  ctx->timing = on != 0;
+  ctx->last_times.clear();
+  return MH_OK;
+}
+
+int32_t mh_stage_times(mh_ctx *ctx, const char **names, double *ms, int32_t cap, int32_t *n) {
+  if (!ctx || !n) return MH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  stages_collect(ctx);
+  int32_t k = 0;
+  for (auto &t : ctx->last_times) {
+    if (k < cap) {
+      if (names) names[k] = t.first;
+      if (ms) ms[k] = t.second;
+    }
+    k++;
+  }
+  *n = k;
+  if (names || ms) ctx->last_times.clear();   // a size query (both NULL) keeps them
+  return MH_OK;
+}
+
+}  // extern "C"

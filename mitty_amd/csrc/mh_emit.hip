@@ -1,0 +1,663 @@
+// mh_emit.hip — read emission (reference readgenerate.read_generating_worker + rpc.generate_read + fastq_lines,
+// mitty/simulation/readgenerate.py:184-230, mitty/simulation/rpc.py:119-160).
+//
+// Per template the reference: finds each mate's start/end node (searchsorted 'right' on node keys, rpc.py:127-130),
+// derives POS, CIGAR, the variant-size list and the sequence (rpc.py:144-160), drops the pair if either read has
+// more than two 'N' (readgenerate.py:204), reverse-complements mate 1 (:205-206) and writes the qname
+// '@{sample}:{worker}:{ps}:{cnt}|{chrom}|{cpy}|{strand}|{pos}|{rlen}|{cigar}|{v,..}|...' into both FASTQ files
+// (:222-230), cnt counting only kept templates.
+//
+// Device plan (two passes over the template arrays, one over the bases):
+//   k_emit_measure  one thread per template: node search, CIGAR/v-list text lengths, N count from the haplotype's
+//                   N runs (no base reads), keep flag, per-file record length without the cnt digits.
+//   scan            (kept, bytes1, bytes2) -> cnt and exact byte offsets; the cnt digits are added in closed form
+//                   (sum_{c<=K} digits(c)), so one scan suffices.
+//   k_emit_write    64 templates per 256-thread workgroup: owner threads format the qnames into two LDS images
+//                   (one per FASTQ file), all threads gather the bases from the haplotype (reverse complement for
+//                   mate 1) and fill '~' qualities, then the images leave LDS as 16-byte aligned stores into the
+//                   file arenas (byte stores only at the two ragged edges of a workgroup's range).
+// The sequence of a read is hap[p - p_min, min(p + l, hap_end) - p_min): non-'D' nodes tile sample coordinates
+// contiguously, so the reference's per-node slice concatenation (rpc.py:146) is one contiguous range.
+#include "mh_internal.h"
+#include "mh_scan.h"
+
+namespace mh {
+
+namespace {
+
+struct HapView {
+  const int64_t *keys, *ps, *pr, *oplen;
+  const uint8_t *op;
+  int64_t n_nodes;
+  const uint8_t *hap;
+  int64_t p_min, hap_len;
+  const int64_t *nrs, *nre;
+  int64_t n_runs;
+};
+
+__device__ __forceinline__ int64_t upper_bound(const int64_t *a, int64_t n, int64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int ndig_u(uint64_t v) {
+  int d = 1;
+  while (v >= 10) { v /= 10; d++; }
+  return d;
+}
+__device__ __forceinline__ int ndig_s(int64_t v) { return v < 0 ? 1 + ndig_u((uint64_t)(-v)) : ndig_u((uint64_t)v); }
+
+__device__ __forceinline__ char *put_u(char *d, uint64_t v) {
+  int nd = ndig_u(v);
+  if (v <= 0xffffffffull) {
+    uint32_t x = (uint32_t)v;
+    for (int i = nd - 1; i >= 0; i--) { d[i] = (char)('0' + x % 10u); x /= 10u; }
+  } else {
+    for (int i = nd - 1; i >= 0; i--) { d[i] = (char)('0' + v % 10u); v /= 10u; }
+  }
+  return d + nd;
+}
+__device__ __forceinline__ char *put_s(char *d, int64_t v) {
+  if (v < 0) { *d++ = '-'; return put_u(d, (uint64_t)(-v)); }
+  return put_u(d, (uint64_t)v);
+}
+__device__ __forceinline__ char *put_str(char *d, const char *s, int n) {
+  for (int i = 0; i < n; i++) d[i] = s[i];
+  return d + n;
+}
+
+struct ReadInfo {
+  int64_t n0, n1, pos, hap_a;
+  int32_t cigar_len, vlist_len, seq_len;
+  bool special;
+};
+
+__device__ __forceinline__ int64_t node_count(const HapView &h, int64_t k, int64_t p, int64_t l) {
+  int64_t ps = h.ps[k], ol = h.oplen[k];
+  if (h.op[k] == 'D') return ol;
+  int64_t hi = p + l - ps < ol ? p + l - ps : ol;
+  int64_t lo = p - ps > 0 ? p - ps : 0;
+  return hi - lo;
+}
+__device__ __forceinline__ int64_t node_v(const HapView &h, int64_t k) {
+  uint8_t o = h.op[k];
+  return o == 'X' ? 0 : (o == 'I' ? h.oplen[k] : -h.oplen[k]);
+}
+
+// rpc.get_begin_end_nodes + the lengths of rpc.generate_read's outputs.  Requires p >= p_min (n0 >= 0).
+__device__ void read_info(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
+  r.n0 = upper_bound(h.keys, h.n_nodes, p) - 1;
+  r.n1 = upper_bound(h.keys, h.n_nodes, p + l - 1) - 1;
+  int32_t cl = 0, vl = 0;
+  bool first = true;
+  for (int64_t k = r.n0; k <= r.n1; k++) {
+    cl += ndig_s(node_count(h, k, p, l)) + 1;
+    if (h.op[k] != '=') {
+      vl += ndig_s(node_v(h, k)) + (first ? 0 : 1);
+      first = false;
+    }
+  }
+  r.special = false;
+  const uint8_t o0 = h.op[r.n0];
+  if (o0 == 'I') {
+    if (r.n0 == r.n1) {
+      r.special = true;
+      r.pos = h.pr[r.n0] - 1;
+      cl = 1 + ndig_s(p - h.ps[r.n0]) + 1 + ndig_s(l) + 1;
+    } else {
+      r.pos = h.pr[r.n0];
+    }
+  } else {
+    r.pos = p - h.ps[r.n0] + h.pr[r.n0];
+  }
+  r.cigar_len = cl;
+  r.vlist_len = vl;
+  int64_t a = p - h.p_min, b = p + l - h.p_min;
+  if (b > h.hap_len) b = h.hap_len;
+  r.hap_a = a;
+  r.seq_len = (int32_t)(b > a ? b - a : 0);
+}
+
+__device__ char *write_cigar(char *d, const HapView &h, int64_t p, int64_t l, const ReadInfo &r) {
+  if (r.special) {
+    *d++ = '>';
+    d = put_s(d, p - h.ps[r.n0]);
+    *d++ = ':';
+    d = put_s(d, l);
+    *d++ = 'I';
+    return d;
+  }
+  for (int64_t k = r.n0; k <= r.n1; k++) {
+    d = put_s(d, node_count(h, k, p, l));
+    *d++ = (char)h.op[k];
+  }
+  return d;
+}
+__device__ char *write_vlist(char *d, const HapView &h, const ReadInfo &r) {
+  bool first = true;
+  for (int64_t k = r.n0; k <= r.n1; k++) {
+    if (h.op[k] == '=') continue;
+    if (!first) *d++ = ',';
+    d = put_s(d, node_v(h, k));
+    first = false;
+  }
+  return d;
+}
+
+// Number of 'N' in hap[a, b), capped at 3 (the filter only needs > 2).
+__device__ int count_N(const HapView &h, int64_t a, int64_t b) {
+  if (h.n_runs == 0 || b <= a) return 0;
+  int64_t r = upper_bound(h.nre, h.n_runs, a);   // first run with end > a
+  int64_t c = 0;
+  for (; r < h.n_runs && h.nrs[r] < b && c <= 2; r++) {
+    int64_t s = h.nrs[r] > a ? h.nrs[r] : a, e = h.nre[r] < b ? h.nre[r] : b;
+    if (e > s) c += e - s;
+  }
+  return (int)(c > 3 ? 3 : c);
+}
+
+struct Rec {
+  int32_t keep, len1, len2, pad;
+};
+struct E3 {
+  int64_t kept, b1, b2;
+  __device__ E3 operator+(const E3 &o) const { return E3{kept + o.kept, b1 + o.b1, b2 + o.b2}; }
+};
+
+// Sum of digits(c) for c = 1..K  ((K+1)*nd - (10^nd - 1)/9, nd = digits(K)).
+__device__ __forceinline__ int64_t digit_sum(int64_t K) {
+  if (K <= 0) return 0;
+  int nd = ndig_u((uint64_t)K);
+  int64_t rep = 0;
+  for (int i = 0; i < nd; i++) rep = rep * 10 + 1;
+  return (K + 1) * nd - rep;
+}
+
+struct QFixed {
+  const char *prefix;   // "@{stub}:"
+  const char *mid;      // "|{chrom}|{cpy}"
+  int32_t prefix_len, mid_len;
+};
+
+__device__ __forceinline__ int32_t qname_len_wo_cnt(const QFixed &q, const ReadInfo *r, int64_t rlen) {
+  int32_t n = q.prefix_len + q.mid_len;
+  for (int s = 0; s < 2; s++)
+    n += 2 + 1 + ndig_s(r[s].pos) + 1 + ndig_s(rlen) + 1 + r[s].cigar_len + 1 + r[s].vlist_len;
+  return n;
+}
+
+__global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
+                                                      const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
+                                                      Rec *recs, int32_t *max_rec) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t local_max = 0;
+  if (t < m) {
+  ReadInfo r[2];
+  read_info(h, pos0[t], rlen, r[0]);
+  read_info(h, pos1[t], rlen, r[1]);
+  int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+             count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+  Rec out{0, 0, 0, 0};
+  if (keep) {
+    int32_t ql = qname_len_wo_cnt(q, r, rlen);
+    int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
+    int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
+    int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
+    int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
+    out = Rec{1, ql + 1 + s_f1 + 3 + q1 + 1, ql + 1 + s_f2 + 3 + q2 + 1, 0};
+    local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+  }
+  recs[t] = out;
+  }
+  // one atomic per wave
+  for (int d = 32; d >= 1; d >>= 1) {
+    int32_t o = __shfl_xor(local_max, d, 64);
+    local_max = o > local_max ? o : local_max;
+  }
+  if ((threadIdx.x & 63) == 0 && local_max > 0) atomicMax(max_rec, local_max);
+}
+
+struct LoadRec {
+  const Rec *recs; int64_t m;
+  __device__ E3 operator()(int64_t t) const {
+    if (t >= m) return E3{0, 0, 0};
+    Rec r = recs[t];
+    return r.keep ? E3{1, r.len1, r.len2} : E3{0, 0, 0};
+  }
+};
+struct StoreOff {
+  E3 *off;
+  __device__ void operator()(int64_t t, E3, E3 excl) const {
+    int64_t ds = digit_sum(excl.kept);
+    off[t] = E3{excl.kept, excl.b1 + ds, excl.b2 + ds};
+  }
+};
+
+constexpr int EW_T = 64;        // templates per workgroup
+constexpr int EW_THREADS = 256;
+
+struct TplMeta {
+  int32_t loc[2];       // record offset inside each LDS image
+  int32_t qlen;         // qname length (with cnt)
+  int32_t seq_len[2];   // per file
+  int32_t keep;
+  int64_t hap_a[2];     // per file
+  int32_t mate[2];      // per file
+};
+
+__device__ __forceinline__ uint8_t comp(uint8_t c) {
+  // str.maketrans('ATCGN', 'TAGCN'): everything else passes through
+  return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
+}
+
+struct CorruptCfg {
+  int32_t enable;
+  const float *cum;      // [2][max_bp][n_bq] cumulative BQ tables (f32)
+  const double *phred;   // [100]
+  int32_t max_bp, n_bq;
+  uint32_t k0, k1, c3;   // Philox key and the constant counter word
+};
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// illumina.corrupt_single_read for one base (illumina.py:155-160), Philox-driven.
+__device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, int f, int n, uint8_t &b, uint8_t &q) {
+  uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ((uint32_t)f << 16) | (uint32_t)n, cc.c3),
+                          make_uint2(cc.k0, cc.k1));
+  const float u1 = (float)(r.x >> 8) * (1.0f / 16777216.0f);
+  const float *row = cc.cum + ((int64_t)f * cc.max_bp + n) * cc.n_bq;
+  int lo = 0, hi = cc.n_bq;                 // np.searchsorted(bq_mat[n, :], U1) (side='left')
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (row[mid] < u1) lo = mid + 1; else hi = mid;
+  }
+  const int bq = lo < 93 ? lo : 93;
+  const double u2 = (double)r.y * (1.0 / 4294967296.0);
+  if (u2 < cc.phred[bq]) {
+    const uint32_t ch = __umulhi(r.z, 3u);  // randint(0, 3)
+    const char *rot = b == 'A' ? "CTG" : b == 'C' ? "ATG" : b == 'T' ? "ACG" : b == 'G' ? "ACT" : "NNN";
+    b = (uint8_t)rot[ch];
+  }
+  q = (uint8_t)(bq + 33);
+}
+
+__global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m, const int64_t *pos0,
+                                                           const int64_t *pos1, const int8_t *fo0, int64_t rlen,
+                                                           QFixed q, const Rec *recs, const E3 *off, char *out1,
+                                                           char *out2, int write2, int32_t cap, CorruptCfg cc,
+                                                           int32_t *err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  TplMeta *meta = (TplMeta *)smem;                                        // EW_T entries
+  char *img[2];
+  img[0] = smem + ((sizeof(TplMeta) * EW_T + 15) / 16) * 16;
+  img[1] = img[0] + cap + 16;
+  __shared__ int64_t s_sb_end;
+
+  const int64_t t0 = (int64_t)blockIdx.x * EW_T;
+  const int64_t t1 = t0 + EW_T < m ? t0 + EW_T : m;
+  const int nfile = write2 ? 2 : 1;
+  char *outs[2] = {out1, out2};
+
+  int64_t sb = t0;
+  while (sb < t1) {
+    // ---- sub-batch [sb, sb_end): the largest prefix whose two images fit `cap` bytes ----------------------
+    {
+      int64_t t = sb + 1 + threadIdx.x;
+      int fits = 0;
+      if (threadIdx.x < EW_T && t <= t1) {
+        E3 a = off[sb], b = off[t];
+        fits = (b.b1 - a.b1 <= cap) && (!write2 || b.b2 - a.b2 <= cap);
+      }
+      int cnt = __syncthreads_count(fits);
+      if (threadIdx.x == 0) s_sb_end = sb + cnt;
+      __syncthreads();
+    }
+    const int64_t sb_end = s_sb_end;
+    if (sb_end == sb) {   // one record larger than the image (host sizes cap from the measured maximum)
+      if (threadIdx.x == 0) atomicOr(err, 1);
+      return;
+    }
+    const E3 base = off[sb];
+    const int64_t g0[2] = {base.b1, base.b2};
+    const int al[2] = {(int)(g0[0] & 15), (int)(g0[1] & 15)};
+
+    // ---- phase A: owner threads format qnames and record metadata ------------------------------------------
+    if (threadIdx.x < sb_end - sb) {
+      const int64_t t = sb + threadIdx.x;
+      TplMeta &mt = meta[threadIdx.x];
+      Rec rc = recs[t];
+      mt.keep = rc.keep;
+      if (rc.keep) {
+        ReadInfo r[2];
+        const int64_t p[2] = {pos0[t], pos1[t]};
+        read_info(h, p[0], rlen, r[0]);
+        read_info(h, p[1], rlen, r[1]);
+        const E3 o = off[t];
+        const int64_t cnt = o.kept + 1;
+        const int f0 = fo0[t];
+        int32_t qlen = 0;
+        for (int f = 0; f < nfile; f++) {
+          const int64_t go = f == 0 ? o.b1 : o.b2;
+          const int loc = (int)(go - g0[f]) + al[f];
+          char *d = img[f] + loc;
+          char *d0 = d;
+          d = put_str(d, q.prefix, q.prefix_len);
+          d = put_s(d, cnt);
+          d = put_str(d, q.mid, q.mid_len);
+          for (int fr = 0; fr < 2; fr++) {            // reads in file order
+            const int s = fr == f0 ? 0 : 1;           // reads[fo] = mate s, fo0 for mate 0
+            *d++ = '|'; *d++ = (char)('0' + s);
+            *d++ = '|'; d = put_s(d, r[s].pos);
+            *d++ = '|'; d = put_s(d, rlen);
+            *d++ = '|'; d = write_cigar(d, h, p[s], rlen, r[s]);
+            *d++ = '|'; d = write_vlist(d, h, r[s]);
+          }
+          qlen = (int32_t)(d - d0);
+          const int s = f == f0 ? 0 : 1;
+          mt.loc[f] = loc;
+          mt.mate[f] = s;
+          mt.seq_len[f] = r[s].seq_len;
+          mt.hap_a[f] = r[s].hap_a;
+        }
+        mt.qlen = qlen;
+      }
+    }
+    __syncthreads();
+
+    // ---- phase B: bases, separators and qualities, all threads -------------------------------------------
+    for (int64_t t = sb; t < sb_end; t++) {
+      const TplMeta &mt = meta[t - sb];
+      if (!mt.keep) continue;
+      for (int f = 0; f < nfile; f++) {
+        const int S = mt.seq_len[f];
+        const int Q = cc.enable ? S : (int)rlen;       // corrupt_single_read emits len(seq) qualities
+        char *d = img[f] + mt.loc[f] + mt.qlen;         // '\n' seq '\n+\n' qual '\n'
+        const uint8_t *src = h.hap + mt.hap_a[f];
+        const bool rc = mt.mate[f] == 1;
+        for (int n = threadIdx.x; n < S; n += EW_THREADS) {
+          uint8_t b = rc ? comp(src[S - 1 - n]) : src[n];
+          if (cc.enable) {
+            uint8_t qq;
+            corrupt_base(cc, t, f, n, b, qq);
+            d[4 + S + n] = (char)qq;
+          }
+          d[1 + n] = (char)b;
+        }
+        if (!cc.enable)
+          for (int n = threadIdx.x; n < Q; n += EW_THREADS) d[4 + S + n] = '~';
+        if (threadIdx.x == 0) {
+          d[0] = '\n';
+          d[1 + S] = '\n';
+          d[2 + S] = '+';
+          d[3 + S] = '\n';
+          d[4 + S + Q] = '\n';
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- phase C: images -> file arenas (16-byte aligned stores; byte stores at the ragged edges) ---------
+    {
+      const E3 endo = off[sb_end];
+      const int64_t g1[2] = {endo.b1, endo.b2};
+      for (int f = 0; f < nfile; f++) {
+        const int64_t G0 = g0[f], G1 = g1[f];
+        if (G1 <= G0) continue;
+        char *out = outs[f];
+        const char *im = img[f] + al[f];   // im[g - G0] is global byte g
+        int64_t A0 = (G0 + 15) & ~(int64_t)15, A1 = G1 & ~(int64_t)15;
+        if (A0 > G1) A0 = G1;
+        if (A1 < A0) A1 = A0;
+        for (int64_t g = G0 + threadIdx.x; g < A0; g += EW_THREADS) out[g] = im[g - G0];
+        const int64_t nvec = (A1 - A0) >> 4;
+        for (int64_t v = threadIdx.x; v < nvec; v += EW_THREADS) {
+          const int64_t g = A0 + (v << 4);
+          *(uint4 *)(out + g) = *(const uint4 *)(im + (g - G0));
+        }
+        for (int64_t g = A1 + threadIdx.x; g < G1; g += EW_THREADS) out[g] = im[g - G0];
+      }
+    }
+    __syncthreads();
+    sb = sb_end;
+  }
+}
+
+// ---- rpc.generate_read facade: per-read text into host-visible buffers ------------------------------------
+__global__ void k_rb_measure(HapView h, int64_t n, const int64_t *p, const int64_t *l, int64_t *pos, int64_t *n0,
+                             int64_t *n1, int64_t *lens, int32_t *err) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (p[i] < h.p_min || l[i] < 1) {
+    atomicOr(err, 1);
+    lens[3 * i] = lens[3 * i + 1] = lens[3 * i + 2] = 0;
+    pos[i] = n0[i] = n1[i] = -1;
+    return;
+  }
+  ReadInfo r;
+  read_info(h, p[i], l[i], r);
+  pos[i] = r.pos;
+  n0[i] = r.n0;
+  n1[i] = r.n1;
+  lens[3 * i] = r.cigar_len;
+  lens[3 * i + 1] = r.vlist_len;
+  lens[3 * i + 2] = r.seq_len;
+}
+__global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t *l, const int64_t *offs, char *cigar,
+                           char *vlist, char *seq) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || p[i] < h.p_min || l[i] < 1) return;
+  ReadInfo r;
+  read_info(h, p[i], l[i], r);
+  write_cigar(cigar + offs[3 * i], h, p[i], l[i], r);
+  write_vlist(vlist + offs[3 * i + 1], h, r);
+  char *d = seq + offs[3 * i + 2];
+  for (int k = 0; k < r.seq_len; k++) d[k] = (char)h.hap[r.hap_a + k];
+}
+
+HapView view_of(const Hap &h) {
+  return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
+                 (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p, h.p_min,
+                 h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
+}
+
+}  // namespace
+
+int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+                   int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+  if (!ctx->have_tpl) return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates first");
+  hipStream_t st = ctx->stream;
+  const int64_t m = ctx->n_tpl;
+  const int64_t rlen = ctx->rlen;
+  std::string prefix = std::string("@") + serial_stub + ":";
+  std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
+  if (prefix.size() + mid.size() > 4000) return arg_fail(ctx, MH_E_ARG, "sample/chrom names too long");
+  *out_kept = 0;
+  *out_b1 = 0;
+  *out_b2 = 0;
+  if (m == 0) return MH_OK;
+
+  stage_begin(ctx, "emit");
+  MH_TRY(ensure(ctx, ctx->s[14], sizeof(Rec) * m));
+  MH_TRY(ensure(ctx, ctx->s[15], sizeof(E3) * (m + 1)));
+  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(E3) * scan_partials_count(m + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  char *small = (char *)ctx->d_small.p;
+  E3 *tot = (E3 *)small;                 // [0, 24)
+  int32_t *max_rec = (int32_t *)(small + 32);
+  int32_t *err = (int32_t *)(small + 36);
+  char *d_prefix = small + 256;
+  char *d_mid = small + 256 + 4096;
+  HIPCHK(ctx, hipMemsetAsync(small, 0, 64, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
+  QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
+  HapView hv = view_of(h);
+  Rec *recs = (Rec *)ctx->s[14].p;
+  E3 *off = (E3 *)ctx->s[15].p;
+
+  stage_begin(ctx, "emit_measure");
+  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m,
+                     (const int64_t *)ctx->t_pos0.p, (const int64_t *)ctx->t_pos1.p, (const int8_t *)ctx->t_fo0.p,
+                     rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  stage_begin(ctx, "emit_scan");
+  HIPCHK(ctx, device_scan<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off}, OpSum{}, E3{0, 0, 0},
+                              (E3 *)ctx->scan_partials.p, tot));
+  stage_end(ctx);
+  E3 ht;
+  int32_t hmax = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&hmax, max_rec, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+
+  // arenas: append after what is already there
+  const int64_t need1 = ctx->used1 + ht.b1, need2 = ctx->used2 + (write_fastq2 ? ht.b2 : 0);
+  MH_TRY(ensure_keep(ctx, ctx->out1, need1 + 64, ctx->used1));
+  if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, need2 + 64, ctx->used2));
+
+  int32_t cap = 24 * 1024;
+  while (cap < hmax) cap *= 2;
+  if (cap > 72 * 1024) {
+    stage_end(ctx);
+    return arg_fail(ctx, MH_E_CAPACITY, "a FASTQ record exceeds 72 KiB");
+  }
+  size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + 2 * (size_t)(cap + 16);
+  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0};
+  if (ctx->corrupt_on) {
+    if (rlen > ctx->corrupt_max_bp) {
+      stage_end(ctx);
+      return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
+    }
+    cc = CorruptCfg{1, (const float *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
+                    ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
+                    (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u};
+  }
+  const int64_t nblk = (m + EW_T - 1) / EW_T;
+  stage_begin(ctx, "emit_write");
+  hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
+                     (const int64_t *)ctx->t_pos0.p, (const int64_t *)ctx->t_pos1.p, (const int8_t *)ctx->t_fo0.p,
+                     rlen, q, (const Rec *)recs, (const E3 *)off, (char *)ctx->out1.p + ctx->used1,
+                     write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr, write_fastq2, cap, cc, err);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  int32_t herr = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  stage_end(ctx);
+  if (herr) return arg_fail(ctx, MH_E_CAPACITY, "FASTQ record larger than the LDS staging image");
+  ctx->used1 += ht.b1;
+  if (write_fastq2) ctx->used2 += ht.b2;
+  *out_kept = ht.kept;
+  *out_b1 = ht.b1;
+  *out_b2 = write_fastq2 ? ht.b2 : 0;
+  return MH_OK;
+}
+
+int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l, int64_t n, int64_t *out_pos,
+                   int64_t *out_n0, int64_t *out_n1, char *cigar, int64_t cigar_cap, int64_t *cigar_off,
+                   int64_t *cigar_used, char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
+                   char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used) {
+  hipStream_t st = ctx->stream;
+  if (n <= 0) {
+    *cigar_used = *vlist_used = *seq_used = 0;
+    if (cigar_off) cigar_off[0] = 0;
+    if (vlist_off) vlist_off[0] = 0;
+    if (seq_off) seq_off[0] = 0;
+    return MH_OK;
+  }
+  DevBuf b;
+  size_t sz = 8 * (size_t)n * (2 + 3 + 3 + 3) + 64;
+  HIPCHK(ctx, hipMalloc(&b.p, sz));
+  int64_t *dp = (int64_t *)b.p, *dl = dp + n, *dpos = dl + n, *dn0 = dpos + n, *dn1 = dn0 + n, *lens = dn1 + n,
+          *offs = lens + 3 * n;
+  int32_t *derr = (int32_t *)(offs + 3 * n);
+  HapView hv = view_of(h);
+  int32_t herr = 0;
+  std::vector<int64_t> hl(3 * n), ho(3 * n);
+  int32_t rc = MH_OK;
+  char *dtxt = nullptr;
+  do {
+    if (hipMemcpyAsync(dp, p, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(dl, l, 8 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(derr, 0, 4, st) != hipSuccess) {
+      rc = hip_fail(ctx, hipGetLastError(), "read_batch upload", __FILE__, __LINE__);
+      break;
+    }
+    hipLaunchKernelGGL(k_rb_measure, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, hv, n, dp, dl, dpos, dn0,
+                       dn1, lens, derr);
+    if (hipMemcpyAsync(hl.data(), lens, 24 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      rc = hip_fail(ctx, hipGetLastError(), "read_batch measure", __FILE__, __LINE__);
+      break;
+    }
+    if (herr) {
+      rc = arg_fail(ctx, MH_E_ARG, "read start before the first node (p < p_min) or non-positive length");
+      break;
+    }
+    int64_t acc[3] = {0, 0, 0};
+    for (int64_t i = 0; i < n; i++)
+      for (int k = 0; k < 3; k++) {
+        ho[3 * i + k] = acc[k];
+        acc[k] += hl[3 * i + k];
+      }
+    *cigar_used = acc[0];
+    *vlist_used = acc[1];
+    *seq_used = acc[2];
+    if (acc[0] > cigar_cap || acc[1] > vlist_cap || acc[2] > seq_cap) {
+      rc = arg_fail(ctx, MH_E_CAPACITY, "read_batch text buffers too small");
+      break;
+    }
+    for (int64_t i = 0; i < n; i++) {
+      cigar_off[i] = ho[3 * i];
+      vlist_off[i] = ho[3 * i + 1];
+      seq_off[i] = ho[3 * i + 2];
+    }
+    cigar_off[n] = acc[0];
+    vlist_off[n] = acc[1];
+    seq_off[n] = acc[2];
+    // offsets relative to three device text regions
+    int64_t tot = acc[0] + acc[1] + acc[2] + 3;
+    if (hipMalloc(&dtxt, tot) != hipSuccess) {
+      rc = arg_fail(ctx, MH_E_OOM, "read_batch text");
+      break;
+    }
+    char *dc = dtxt, *dv = dtxt + acc[0] + 1, *ds = dv + acc[1] + 1;
+    if (hipMemcpyAsync(offs, ho.data(), 24 * n, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = hip_fail(ctx, hipGetLastError(), "read_batch offsets", __FILE__, __LINE__);
+      break;
+    }
+    hipLaunchKernelGGL(k_rb_write, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, hv, n, dp, dl, offs, dc, dv,
+                       ds);
+    if ((acc[0] && hipMemcpyAsync(cigar, dc, acc[0], hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        (acc[1] && hipMemcpyAsync(vlist, dv, acc[1], hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        (acc[2] && hipMemcpyAsync(seq, ds, acc[2], hipMemcpyDeviceToHost, st) != hipSuccess) ||
+        hipMemcpyAsync(out_pos, dpos, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(out_n0, dn0, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(out_n1, dn1, 8 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      rc = hip_fail(ctx, hipGetLastError(), "read_batch write", __FILE__, __LINE__);
+      break;
+    }
+  } while (0);
+  if (dtxt) (void)hipFree(dtxt);
+  (void)hipFree(b.p);
+  return rc;
+}
+
+}  // namespace mh

@@ -1,0 +1,150 @@
+// mh_internal.h — shared definitions for libmitty_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/mitty_hip.h"
+
+namespace mh {
+
+// ---------------------------------------------------------------------------------------------------------------
+// Error handling: every HIP call is checked; failures set ctx->err and return MH_E_HIP up the stack.
+// ---------------------------------------------------------------------------------------------------------------
+struct Status {
+  int32_t code = MH_OK;
+  std::string msg;
+};
+
+#define MH_TRY(expr)                        \
+  do {                                      \
+    int32_t _rc = (expr);                   \
+    if (_rc != MH_OK) return _rc;           \
+  } while (0)
+
+// A grow-only device buffer.
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+// Haplotype (one chromosome copy of one BED region) resident on the device.  SURVEY.md §8(a) A9.
+// Sample coordinates are the reference's 1-based `ps`; hap[k] is the base at sample position p_min + k.
+struct Hap {
+  bool valid = false;
+  DevBuf hap, keys, ps, pr, op, oplen, nrun_s, nrun_e;
+  int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
+};
+
+struct Contig {
+  DevBuf seq;
+  int64_t len = 0;
+};
+
+struct StageTime {
+  const char *name;
+  hipEvent_t a, b;
+};
+
+}  // namespace mh
+
+struct mh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int32_t max_cu = 256;
+
+  std::map<int32_t, mh::Contig> contigs;
+  std::map<int32_t, mh::Hap> haps;
+
+  // current template set (illumina.generate_reads output, device-resident)
+  mh::DevBuf t_fo0, t_pos0, t_pos1;
+  int64_t n_tpl = 0;
+  int32_t rlen = 0;
+  bool have_tpl = false;
+
+  // scratch (grow-only), reused by all stages
+  mh::DevBuf s[16];
+  mh::DevBuf scan_partials;
+  mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
+  mh::DevBuf d_small;        // device small scalars
+
+  // fused corruption (mh_set_corruption)
+  bool corrupt_on = false;
+  mh::DevBuf corrupt_cum, corrupt_phred;
+  int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
+  uint64_t corrupt_seed = 0;
+
+  // FASTQ arenas
+  mh::DevBuf out1, out2;
+  int64_t used1 = 0, used2 = 0;
+
+  // timing
+  bool timing = false;
+  std::vector<mh::StageTime> stages;    // open (begun, not ended)
+  std::vector<mh::StageTime> pending;   // ended, not yet resolved
+  std::vector<std::pair<const char *, double>> last_times;
+};
+
+namespace mh {
+
+int32_t hip_fail(mh_ctx *ctx, hipError_t e, const char *what, const char *file, int line);
+int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg);
+
+#define HIPCHK(ctx, call)                                                     \
+  do {                                                                        \
+    hipError_t _e = (call);                                                   \
+    if (_e != hipSuccess) return ::mh::hip_fail((ctx), _e, #call, __FILE__, __LINE__); \
+  } while (0)
+
+// Grow `b` to hold at least `bytes`; contents are NOT preserved.
+int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);
+// Grow preserving the first `keep` bytes (stream-ordered copy).
+int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep);
+void release(DevBuf &b);
+
+// Stage timing (HIP events on ctx->stream).
+void stage_begin(mh_ctx *ctx, const char *name);
+void stage_end(mh_ctx *ctx);
+void stages_collect(mh_ctx *ctx);
+
+// Launch helpers
+inline unsigned grid_for(int64_t n, int threads, int64_t cap = 1 << 20) {
+  int64_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---- subsystem entry points (host side, called from mh_api.cpp) -----------------------------------------------
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const int64_t *v_pos,
+                     const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
+                     const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var);
+
+int32_t sample_templates(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen, const double *cum_tlen,
+                         int32_t n_tlen, uint64_t seed, int32_t rng_mode, int64_t *out_n);
+
+int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+                   int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
+
+int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l, int64_t n, int64_t *out_pos,
+                   int64_t *out_n0, int64_t *out_n1, char *cigar, int64_t cigar_cap, int64_t *cigar_off,
+                   int64_t *cigar_used, char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
+                   char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used);
+
+
+// Host-side MT19937 (numpy RandomState seeding), used for seed derivation and the rare exact fix-ups.
+struct HostMT {
+  uint32_t key[624];
+  int pos;
+  void seed(uint32_t s);
+  uint32_t next();
+  double next_double();
+  uint64_t interval(uint64_t max);
+};
+
+}  // namespace mh

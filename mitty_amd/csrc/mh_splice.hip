@@ -1,0 +1,357 @@
+// mh_splice.hip — haplotype splice on the device (reference rpc.create_node_list, mitty/simulation/rpc.py:38-116).
+//
+// The reference walks the variant list with two cursors (samp_pos, ref_pos) and skips a variant whose position is
+// before the ref cursor left by the last ACCEPTED variant (rpc.py:55) — a sequential chain.  Here:
+//   1. max-scan of variant ends  -> "anchor" = pos >= every earlier end, accepted whatever happened before;
+//   2. k_resolve                 -> one thread per anchor walks its (short) run of non-anchors sequentially;
+//   3. max-scan of accepted ends -> ref cursor before each variant (accepted ends are strictly increasing);
+//   4. sum-scan of (nodes, sample length) -> every node's index and ps, written straight from the scan's Store;
+//   5. piece copy                -> haplotype bytes (hap[k] = base at sample position p_min + k) gathered from the
+//                                   resident contig / alt pool, 4 KiB pieces, one wave each;
+//   6. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
+// Node arrays are SoA in HBM: keys (search key, ps+1 for 'D' as rpc.py:127), ps, pr, op, oplen.
+#include "mh_internal.h"
+#include "mh_scan.h"
+
+namespace mh {
+
+namespace {
+
+constexpr int64_t PIECE = 4096;
+constexpr int64_t ALT_FLAG = (int64_t)1 << 62;
+
+__device__ __forceinline__ int64_t var_end(int64_t pos, uint8_t op, int64_t oplen) {
+  return pos + 1 + (op == 'D' ? oplen : 0);
+}
+
+struct LoadEnd {
+  const int64_t *pos; const uint8_t *op; const int64_t *oplen;
+  __device__ int64_t operator()(int64_t i) const { return var_end(pos[i], op[i], oplen[i]); }
+};
+struct StoreAnchor {
+  const int64_t *pos; uint8_t *anchor; int64_t rs;
+  __device__ void operator()(int64_t i, int64_t, int64_t excl) const {
+    int64_t m = excl > rs ? excl : rs;
+    anchor[i] = pos[i] >= m;
+  }
+};
+
+__global__ void k_resolve(int64_t n, const int64_t *pos, const uint8_t *op, const int64_t *oplen,
+                          const uint8_t *anchor, uint8_t *accepted, int64_t rs) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t cur;
+  int64_t k;
+  if (anchor[i]) {
+    accepted[i] = 1;
+    cur = var_end(pos[i], op[i], oplen[i]);
+    k = i + 1;
+  } else if (i == 0) {
+    cur = rs;
+    k = 0;
+  } else {
+    return;
+  }
+  for (; k < n && !anchor[k]; k++) {
+    uint8_t a = pos[k] >= cur;
+    accepted[k] = a;
+    if (a) cur = var_end(pos[k], op[k], oplen[k]);
+  }
+}
+
+struct LoadAccEnd {
+  const int64_t *pos; const uint8_t *op; const int64_t *oplen; const uint8_t *accepted; int64_t rs;
+  __device__ int64_t operator()(int64_t i) const { return accepted[i] ? var_end(pos[i], op[i], oplen[i]) : rs; }
+};
+struct StoreRefBefore {
+  int64_t *ref_before; int64_t rs;
+  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { ref_before[i] = excl > rs ? excl : rs; }
+};
+
+struct NS {
+  int64_t nodes, samp;
+  __device__ NS operator+(const NS &o) const { return NS{nodes + o.nodes, samp + o.samp}; }
+};
+
+struct LoadNS {
+  const int64_t *pos; const uint8_t *op; const int64_t *oplen; const uint8_t *accepted; const int64_t *ref_before;
+  __device__ NS operator()(int64_t i) const {
+    if (!accepted[i]) return NS{0, 0};
+    uint8_t o = op[i];
+    int64_t delta = (o == 'X') ? pos[i] - ref_before[i] : pos[i] + 1 - ref_before[i];
+    int64_t eq = delta > 0 ? 1 : 0;
+    int64_t sl = (delta > 0 ? delta : 0) + (o == 'X' ? 1 : (o == 'I' ? oplen[i] : 0));
+    return NS{eq + 1, sl};
+  }
+};
+
+struct StoreNodes {
+  const int64_t *pos; const uint8_t *op; const int64_t *oplen; const uint8_t *accepted; const int64_t *ref_before;
+  const int64_t *alt_off; const int64_t *alt_len;
+  int64_t *keys, *ps, *pr, *nl, *src; uint8_t *nop;
+  int64_t rs, ref_len; int32_t *err;
+  __device__ void operator()(int64_t i, NS, NS excl) const {
+    if (!accepted[i]) return;
+    uint8_t o = op[i];
+    int64_t vp = pos[i], rb = ref_before[i];
+    int64_t sp = rs + excl.samp, k = excl.nodes;
+    int64_t delta = (o == 'X') ? vp - rb : vp + 1 - rb;
+    if (delta > 0) {                                  // '=' node (rpc.py:78-81, 93-96, 108-111)
+      keys[k] = sp; ps[k] = sp; pr[k] = rb; nop[k] = '='; nl[k] = delta; src[k] = rb - rs;
+      if (rb - rs + delta > ref_len) atomicOr(err, 1);
+      k++;
+      sp += delta;
+    }
+    if (o == 'X') {                                   // rpc.py:84
+      keys[k] = sp; ps[k] = sp; pr[k] = vp; nop[k] = 'X'; nl[k] = 1; src[k] = ALT_FLAG | alt_off[i];
+      if (alt_len[i] != 1) atomicOr(err, 2);
+    } else if (o == 'I') {                            // rpc.py:98-100
+      keys[k] = sp; ps[k] = sp; pr[k] = vp + 1; nop[k] = 'I'; nl[k] = oplen[i]; src[k] = ALT_FLAG | (alt_off[i] + 1);
+      if (alt_len[i] - 1 != oplen[i]) atomicOr(err, 2);
+    } else {                                          // rpc.py:113-115
+      keys[k] = sp; ps[k] = sp - 1; pr[k] = vp + 1 + oplen[i]; nop[k] = 'D'; nl[k] = oplen[i]; src[k] = -1;
+    }
+  }
+};
+
+__global__ void k_trailing(int64_t k, int64_t sp, int64_t rp, int64_t rs, int64_t len, int64_t *keys, int64_t *ps,
+                           int64_t *pr, int64_t *nl, int64_t *src, uint8_t *nop) {
+  keys[k] = sp; ps[k] = sp; pr[k] = rp; nop[k] = '='; nl[k] = len; src[k] = rp - rs;
+}
+
+struct LoadPieces {
+  const uint8_t *nop; const int64_t *nl;
+  __device__ int64_t operator()(int64_t i) const { return nop[i] == 'D' ? 0 : (nl[i] + PIECE - 1) / PIECE; }
+};
+struct StorePieceOff {
+  int64_t *off;
+  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { off[i] = excl; }
+};
+
+__device__ __forceinline__ int64_t upper_bound_i64(const int64_t *a, int64_t n, int64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) k_hap_copy(int64_t total_pieces, int64_t n_nodes, const int64_t *piece_off,
+                                                  const int64_t *ps, const int64_t *nl, const int64_t *src,
+                                                  const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap,
+                                                  int64_t p_min) {
+  int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= total_pieces) return;
+  int64_t node = upper_bound_i64(piece_off, n_nodes, w) - 1;
+  int64_t q = w - piece_off[node];
+  int64_t b0 = q * PIECE, b1 = b0 + PIECE;
+  if (b1 > nl[node]) b1 = nl[node];
+  int64_t s = src[node];
+  const uint8_t *sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
+  uint8_t *dp = hap + (ps[node] - p_min);
+  for (int64_t b = b0 + lane; b < b1; b += 64) dp[b] = sp[b];
+}
+
+// ---- N runs ---------------------------------------------------------------------------------------------------
+constexpr int64_t NCHUNK = 16;
+
+struct RunCnt {
+  int64_t starts, ends;
+  __device__ RunCnt operator+(const RunCnt &o) const { return RunCnt{starts + o.starts, ends + o.ends}; }
+};
+
+// Element c covers byte positions k in [c*16, c*16+16) ∩ [0, len]; start at k if hap[k]=='N' && prev != 'N';
+// end at k (exclusive) if hap[k-1]=='N' && (k == len || hap[k] != 'N').
+__device__ __forceinline__ void run_flags(const uint8_t *hap, int64_t len, int64_t k, bool &st, bool &en) {
+  bool cur = k < len && hap[k] == 'N';
+  bool prev = k > 0 && hap[k - 1] == 'N';
+  st = cur && !prev;
+  en = prev && !cur;
+}
+
+struct LoadRuns {
+  const uint8_t *hap; int64_t len;
+  __device__ RunCnt operator()(int64_t c) const {
+    RunCnt r{0, 0};
+    int64_t k0 = c * NCHUNK, k1 = k0 + NCHUNK;
+    if (k1 > len + 1) k1 = len + 1;
+    for (int64_t k = k0; k < k1; k++) {
+      bool st, en;
+      run_flags(hap, len, k, st, en);
+      r.starts += st;
+      r.ends += en;
+    }
+    return r;
+  }
+};
+struct StoreRuns {
+  const uint8_t *hap; int64_t len; int64_t *rs_out; int64_t *re_out;
+  __device__ void operator()(int64_t c, RunCnt, RunCnt excl) const {
+    int64_t k0 = c * NCHUNK, k1 = k0 + NCHUNK;
+    if (k1 > len + 1) k1 = len + 1;
+    int64_t a = excl.starts, b = excl.ends;
+    for (int64_t k = k0; k < k1; k++) {
+      bool st, en;
+      run_flags(hap, len, k, st, en);
+      if (st) rs_out[a++] = k;
+      if (en) re_out[b++] = k;
+    }
+  }
+};
+
+}  // namespace
+
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int64_t *v_pos, const uint8_t *v_op,
+                     const int64_t *v_oplen, const int64_t *v_alt_off, const int64_t *v_alt_len,
+                     const char *alt_pool, int64_t alt_pool_len, int64_t n_var) {
+  hipStream_t st = ctx->stream;
+  for (int64_t i = 0; i < n_var; i++)
+    if (v_op[i] != 'X' && v_op[i] != 'I' && v_op[i] != 'D')
+      return arg_fail(ctx, MH_E_COMPLEX_VARIANT, "Complex variants present in VCF. Please filter or refactor these.");
+  for (int64_t i = 0; i < n_var; i++)
+    if (v_alt_off[i] < 0 || v_alt_len[i] < 0 || v_alt_off[i] + v_alt_len[i] > alt_pool_len)
+      return arg_fail(ctx, MH_E_ARG, "variant alt bytes outside alt_pool");
+  const int64_t nv = n_var > 0 ? n_var : 1;
+  const int64_t node_cap = 2 * n_var + 1;
+
+  stage_begin(ctx, "splice");
+  // --- inputs to the device (scratch 0..5) -----------------------------------------------------------------
+  MH_TRY(ensure(ctx, ctx->s[0], 8 * nv));
+  MH_TRY(ensure(ctx, ctx->s[1], nv));
+  MH_TRY(ensure(ctx, ctx->s[2], 8 * nv));
+  MH_TRY(ensure(ctx, ctx->s[3], 8 * nv));
+  MH_TRY(ensure(ctx, ctx->s[4], 8 * nv));
+  MH_TRY(ensure(ctx, ctx->s[5], alt_pool_len > 0 ? alt_pool_len : 1));
+  int64_t *d_pos = (int64_t *)ctx->s[0].p, *d_oplen = (int64_t *)ctx->s[2].p;
+  int64_t *d_aoff = (int64_t *)ctx->s[3].p, *d_alen = (int64_t *)ctx->s[4].p;
+  uint8_t *d_op = (uint8_t *)ctx->s[1].p, *d_pool = (uint8_t *)ctx->s[5].p;
+  if (n_var > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(d_pos, v_pos, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_op, v_op, n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_oplen, v_oplen, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_aoff, v_alt_off, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_alen, v_alt_len, 8 * n_var, hipMemcpyHostToDevice, st));
+  }
+  if (alt_pool_len > 0) HIPCHK(ctx, hipMemcpyAsync(d_pool, alt_pool, alt_pool_len, hipMemcpyHostToDevice, st));
+
+  // --- scratch: anchor(6) accepted(7) ref_before(8) node src(9) piece_off(10) small(d_small) -----------------
+  MH_TRY(ensure(ctx, ctx->s[6], nv));
+  MH_TRY(ensure(ctx, ctx->s[7], nv));
+  MH_TRY(ensure(ctx, ctx->s[8], 8 * nv));
+  MH_TRY(ensure(ctx, ctx->s[9], 8 * node_cap));
+  MH_TRY(ensure(ctx, ctx->s[10], 8 * node_cap));
+  MH_TRY(ensure(ctx, ctx->d_small, 256));
+  MH_TRY(ensure(ctx, ctx->scan_partials, 32 * scan_partials_count(node_cap > nv ? node_cap : nv) + 64));
+  uint8_t *anchor = (uint8_t *)ctx->s[6].p, *accepted = (uint8_t *)ctx->s[7].p;
+  int64_t *ref_before = (int64_t *)ctx->s[8].p, *nsrc = (int64_t *)ctx->s[9].p, *poff = (int64_t *)ctx->s[10].p;
+  char *small = (char *)ctx->d_small.p;
+  int64_t *tot_i64 = (int64_t *)small;           // [0]
+  NS *tot_ns = (NS *)(small + 16);                // [16..32)
+  int32_t *err = (int32_t *)(small + 64);
+  int64_t *tot_pieces = (int64_t *)(small + 80);
+  HIPCHK(ctx, hipMemsetAsync(small, 0, 256, st));
+
+  MH_TRY(ensure(ctx, h.keys, 8 * node_cap));
+  MH_TRY(ensure(ctx, h.ps, 8 * node_cap));
+  MH_TRY(ensure(ctx, h.pr, 8 * node_cap));
+  MH_TRY(ensure(ctx, h.oplen, 8 * node_cap));
+  MH_TRY(ensure(ctx, h.op, node_cap));
+
+  int64_t *keys = (int64_t *)h.keys.p, *ps = (int64_t *)h.ps.p, *pr = (int64_t *)h.pr.p, *nl = (int64_t *)h.oplen.p;
+  uint8_t *nop = (uint8_t *)h.op.p;
+
+  int64_t final_ref = rs;
+  NS tot{0, 0};
+  if (n_var > 0) {
+    HIPCHK(ctx, device_scan<int64_t>(st, n_var, LoadEnd{d_pos, d_op, d_oplen}, StoreAnchor{d_pos, anchor, rs}, OpMax{},
+                                     INT64_MIN, (int64_t *)ctx->scan_partials.p, tot_i64));
+    HIPCHK(ctx, hipMemsetAsync(accepted, 0, n_var, st));
+    hipLaunchKernelGGL(k_resolve, dim3(grid_for(n_var, 256)), dim3(256), 0, st, n_var, d_pos, d_op, d_oplen, anchor,
+                       accepted, rs);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, device_scan<int64_t>(st, n_var, LoadAccEnd{d_pos, d_op, d_oplen, accepted, rs},
+                                     StoreRefBefore{ref_before, rs}, OpMax{}, INT64_MIN,
+                                     (int64_t *)ctx->scan_partials.p, tot_i64));
+    HIPCHK(ctx, device_scan<NS>(st, n_var, LoadNS{d_pos, d_op, d_oplen, accepted, ref_before},
+                                StoreNodes{d_pos, d_op, d_oplen, accepted, ref_before, d_aoff, d_alen, keys, ps, pr, nl,
+                                           nsrc, nop, rs, c.len, err},
+                                OpSum{}, NS{0, 0}, (NS *)ctx->scan_partials.p, tot_ns));
+    int64_t hb[2];
+    HIPCHK(ctx, hipMemcpyAsync(&final_ref, tot_i64, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hb, tot_ns, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (final_ref < rs) final_ref = rs;
+    tot = NS{hb[0], hb[1]};
+  }
+  int64_t n_nodes = tot.nodes, samp_end = rs + tot.samp, hap_len = tot.samp;
+  int64_t offset = final_ref - rs;
+  if (offset <= c.len) {                                   // trailing '=' node, rpc.py:59-61
+    int64_t len = c.len - offset;
+    hipLaunchKernelGGL(k_trailing, dim3(1), dim3(1), 0, st, n_nodes, samp_end, final_ref, rs, len, keys, ps, pr, nl,
+                       nsrc, nop);
+    HIPCHK(ctx, hipGetLastError());
+    n_nodes++;
+    hap_len += len;
+  }
+  // p_min / p_max (readgenerate.py:192): ps of the first node; ps + oplen of the last
+  int64_t ps0, psl, nll;
+  HIPCHK(ctx, hipMemcpyAsync(&ps0, ps, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&psl, ps + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&nll, nl + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
+
+  // --- haplotype bytes ---------------------------------------------------------------------------------------
+  HIPCHK(ctx, device_scan<int64_t>(st, n_nodes, LoadPieces{nop, nl}, StorePieceOff{poff}, OpSum{}, (int64_t)0,
+                                   (int64_t *)ctx->scan_partials.p, tot_pieces));
+  int64_t pieces = 0;
+  int32_t herr = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&pieces, tot_pieces, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (herr) {
+    stage_end(ctx);
+    return arg_fail(ctx, MH_E_ARG, herr & 1 ? "variant beyond the end of the fetched reference region"
+                                            : "SNP/INS alt length inconsistent with its op");
+  }
+  int64_t p_min = ps0;
+  MH_TRY(ensure(ctx, h.hap, hap_len > 0 ? hap_len : 1));
+  if (pieces > 0) {
+    stage_begin(ctx, "splice_hap_copy");
+    int64_t threads = pieces * 64;
+    hipLaunchKernelGGL(k_hap_copy, dim3(grid_for(threads, 256, INT32_MAX)), dim3(256), 0, st, pieces, n_nodes, poff,
+                       ps, nl, nsrc, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p, p_min);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+  }
+  // --- N runs -----------------------------------------------------------------------------------------------
+  int64_t nchunks = (hap_len + 1 + NCHUNK - 1) / NCHUNK;
+  RunCnt *rtot = (RunCnt *)(small + 128);
+  // count first (sizes the run arrays), then the same scan again to write them
+  MH_TRY(ensure(ctx, ctx->scan_partials, 16 * scan_partials_count(nchunks) + 64));
+  HIPCHK(ctx, device_reduce<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len}, OpSum{}, RunCnt{0, 0},
+                                    (RunCnt *)ctx->scan_partials.p, rtot));
+  RunCnt hr;
+  HIPCHK(ctx, hipMemcpyAsync(&hr, rtot, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  h.n_runs = hr.starts;
+  MH_TRY(ensure(ctx, h.nrun_s, 8 * (hr.starts + 1)));
+  MH_TRY(ensure(ctx, h.nrun_e, 8 * (hr.ends + 1)));
+  if (hr.starts > 0) {
+    HIPCHK(ctx, device_scan<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len},
+                                    StoreRuns{(const uint8_t *)h.hap.p, hap_len, (int64_t *)h.nrun_s.p,
+                                              (int64_t *)h.nrun_e.p},
+                                    OpSum{}, RunCnt{0, 0}, (RunCnt *)ctx->scan_partials.p, rtot));
+  }
+  stage_end(ctx);
+
+  h.n_nodes = n_nodes;
+  h.p_min = p_min;
+  h.p_max = psl + nll;
+  h.hap_len = hap_len;
+  h.ref_start_pos = rs;
+  h.valid = true;
+  return MH_OK;
+}
+
+}  // namespace mh

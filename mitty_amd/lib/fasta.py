@@ -1,0 +1,28 @@
+"""FASTA access for read generation (replaces pysam.FastaFile.fetch, reference readgenerate.py:181,186)."""
+import gzip
+
+
+def read_fasta(fname, names=None):
+  """{contig name (first word of the header): bytes}.  If `names` is given, other contigs are skipped."""
+  with open(fname, 'rb') as fp:
+    gz = fp.read(2) == b'\x1f\x8b'
+  seqs, name, chunks, keep = {}, None, [], True
+  with (gzip.open(fname, 'rb') if gz else open(fname, 'rb')) as fp:
+    for line in fp:
+      if line.startswith(b'>'):
+        if name is not None and keep:
+          seqs[name] = b''.join(chunks)
+        name = line[1:].split()[0].decode()
+        chunks = []
+        keep = names is None or name in names
+      elif keep:
+        chunks.append(line.rstrip(b'\r\n'))
+  if name is not None and keep:
+    seqs[name] = b''.join(chunks)
+  return seqs
+
+
+def fetch(seqs, reference, start, end):
+  """pysam FastaFile.fetch semantics: clamp [start, end) to the contig."""
+  s = seqs[reference]
+  return s[max(0, start):max(0, min(end, len(s)))]

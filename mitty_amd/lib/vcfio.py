@@ -1,0 +1,188 @@
+"""VCF / BED loading for read generation (reference mitty/lib/vcfio.py:19-168).
+
+Semantics follow the reference + htslib exactly:
+* read_bed: whitespace split, (chrom, int start0, int end) per line (vcfio.py:45-46).
+* records fetched for a BED region are those on the region's contig with pos-1 < end and pos-1+len(REF) > start,
+  in file order (tabix overlap query).
+* ploidy = number of GT entries of the region's first record, 2 for an empty region (vcfio.py:74-79).
+* per copy c: records with GT[c] != 0; alt = (REF,)+ALTs indexed by GT[c]; classified X / I / D by REF/ALT
+  lengths; anything else raises ValueError (vcfio.py:116-124).
+
+The engine consumes the structure-of-arrays form (`load_variants_soa`); `load_variant_file` returns the reference's
+list-of-Variant form for API compatibility.
+"""
+import gzip
+import logging
+
+import numpy as np
+
+logger = logging.getLogger(__name__)
+
+
+class Variant(object):
+  __slots__ = ('pos', 'ref', 'alt', 'cigarop', 'oplen')
+
+  def __init__(self, pos, ref, alt, cigarop, oplen):
+    self.pos = pos
+    self.ref = ref
+    self.alt = alt
+    self.cigarop = cigarop
+    self.oplen = oplen
+
+  def tuple(self):
+    return self.pos, self.ref, self.alt, self.cigarop, self.oplen
+
+  def __repr__(self):
+    return self.tuple().__repr__()
+
+
+def read_bed(bed_fname):
+  with open(bed_fname, 'r') as fp:
+    return [(x[0], int(x[1]), int(x[2])) for x in (ln.split() for ln in fp.readlines())]
+
+
+def _open(fname):
+  with open(fname, 'rb') as fp:
+    gz = fp.read(2) == b'\x1f\x8b'
+  return gzip.open(fname, 'rb') if gz else open(fname, 'rb')
+
+
+class _Records:
+  """All data lines of one sample, grouped by contig, in file order."""
+
+  def __init__(self, fname, sample):
+    col = None
+    by_chrom = {}
+    with _open(fname) as fp:
+      for line in fp:
+        if line.startswith(b'##'):
+          continue
+        if line.startswith(b'#CHROM'):
+          names = line.rstrip(b'\r\n').split(b'\t')
+          try:
+            col = names.index(sample.encode())
+          except ValueError:
+            raise ValueError('invalid sample name: {}'.format(sample))
+          continue
+        if col is None:
+          raise ValueError('VCF has no #CHROM header line')
+        f = line.rstrip(b'\r\n').split(b'\t', col + 1)
+        lst = by_chrom.get(f[0])
+        if lst is None:
+          lst = by_chrom[f[0]] = []
+        fmt = f[8].split(b':')
+        gi = fmt.index(b'GT') if b'GT' in fmt else -1
+        gt = f[col].split(b':')[gi] if gi >= 0 else b'.'
+        lst.append((int(f[1]), f[3], f[4], gt))
+    self.by_chrom = {}
+    for ch, lst in by_chrom.items():
+      pos = np.fromiter((r[0] for r in lst), dtype=np.int64, count=len(lst))
+      rl = np.fromiter((len(r[1]) for r in lst), dtype=np.int64, count=len(lst))
+      self.by_chrom[ch.decode()] = (pos, rl, lst)
+
+  def fetch(self, chrom, start, stop):
+    ent = self.by_chrom.get(chrom)
+    if ent is None:
+      return []
+    pos, rl, lst = ent
+    beg = pos - 1
+    idx = np.nonzero((beg < stop) & (beg + rl > start))[0]
+    return [lst[i] for i in idx]
+
+
+def _gt_tuple(gt):
+  return tuple(None if g in (b'.', b'') else int(g) for g in gt.replace(b'/', b'|').split(b'|'))
+
+
+def _split_soa(region, recs):
+  """split_copies + parse for one region -> (ploidy, [soa per copy])."""
+  if not recs:
+    logger.warning('Empty region ({}), assuming diploid'.format(region))
+    ploidy = 2
+  else:
+    ploidy = len(_gt_tuple(recs[0][3]))
+  copies = []
+  for cpy in range(ploidy):
+    pos, op, oplen, alts = [], [], [], []
+    for p1, ref, alt_field, gt in recs:
+      g = _gt_tuple(gt)
+      if cpy >= len(g):
+        raise ValueError('record at {}:{} has fewer GT entries than the region ploidy'.format(region[0], p1))
+      if g[cpy] == 0:
+        continue
+      if g[cpy] is None:
+        raise ValueError('missing genotype at {}:{}'.format(region[0], p1))
+      alleles = [ref] + ([] if alt_field == b'.' else alt_field.split(b','))
+      alt = alleles[g[cpy]]
+      l_r, l_a = len(ref), len(alt)
+      if l_r == 1:
+        o, ol = (b'X', 0) if l_a == 1 else (b'I', l_a - l_r)
+      elif l_a == 1:
+        o, ol = b'D', l_r - l_a
+      else:
+        raise ValueError('Complex variants present in VCF. Please filter or refactor these.')
+      pos.append(p1)
+      op.append(o)
+      oplen.append(ol)
+      alts.append(alt)
+    alt_len = np.array([len(a) for a in alts], dtype=np.int64)
+    alt_off = np.zeros(len(alts), dtype=np.int64)
+    if len(alts):
+      alt_off[1:] = np.cumsum(alt_len)[:-1]
+    copies.append({'pos': np.array(pos, dtype=np.int64),
+                   'op': np.frombuffer(b''.join(op), dtype=np.uint8).copy() if op else np.zeros(0, np.uint8),
+                   'oplen': np.array(oplen, dtype=np.int64), 'alt_off': alt_off, 'alt_len': alt_len,
+                   'alt_pool': b''.join(alts)})
+  return ploidy, copies
+
+
+def load_variants_soa(fname, sample, bed_fname):
+  """[{'region': (chrom, s0, e), 'ploidy': k, 'copies': [soa, ...]}] in BED order."""
+  recs = _Records(fname, sample)
+  out = []
+  for region in read_bed(bed_fname):
+    rl = recs.fetch(*region)
+    ploidy, copies = _split_soa(region, rl)
+    out.append({'region': region, 'ploidy': ploidy, 'copies': copies, '_recs': rl})
+  return out
+
+
+def load_variant_file(fname, sample, bed_fname):
+  """Reference-compatible form: [{'region': region, 'v': [[Variant, ...] per copy]}] (vcfio.py:51-64)."""
+  out = []
+  for reg in load_variants_soa(fname, sample, bed_fname):
+    recs = reg['_recs']
+    v = []
+    for cpy in range(reg['ploidy']):
+      lst = []
+      for p1, ref, alt_field, gt in recs:
+        g = _gt_tuple(gt)
+        if g[cpy] == 0:
+          continue
+        alleles = [ref] + ([] if alt_field == b'.' else alt_field.split(b','))
+        alt = alleles[g[cpy]].decode()
+        l_r, l_a = len(ref), len(alt)
+        op, ol = (('X', 0) if l_a == 1 else ('I', l_a - l_r)) if l_r == 1 else ('D', l_r - l_a)
+        lst.append(Variant(p1, ref.decode(), alt, op, ol))
+      v.append(lst)
+    out.append({'region': reg['region'], 'v': v})
+  return out
+
+
+def split_copies(region, vl):
+  """vcfio.split_copies over records given as (pos, ref, alts, gt) tuples."""
+  ploidy, copies = _split_soa(region, vl)
+  return {'region': region, 'v': copies}
+
+
+def soa_from_variants(vl):
+  """Structure-of-arrays from a list of Variant (used by the rpc facade)."""
+  alts = [v.alt.encode() if isinstance(v.alt, str) else v.alt for v in vl]
+  alt_len = np.array([len(a) for a in alts], dtype=np.int64)
+  alt_off = np.zeros(len(alts), dtype=np.int64)
+  if len(alts):
+    alt_off[1:] = np.cumsum(alt_len)[:-1]
+  return {'pos': np.array([v.pos for v in vl], dtype=np.int64),
+          'op': np.frombuffer(''.join(v.cigarop for v in vl).encode(), dtype=np.uint8).copy(),
+          'oplen': np.array([v.oplen for v in vl], dtype=np.int64), 'alt_off': alt_off, 'alt_len': alt_len,
+          'alt_pool': b''.join(alts)}

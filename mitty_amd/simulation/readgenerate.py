@@ -1,0 +1,157 @@
+"""generate-reads orchestration, qname codec (reference mitty/simulation/readgenerate.py).
+
+`process_multi_threaded` keeps the reference's signature (readgenerate.py:76-78).  The per-unit work runs on the
+GPU (mitty_amd.engine); the host only parses inputs, walks the reference's work-unit order and streams the device
+FASTQ arenas to the output files in that order.  Output is byte-identical to the reference run with --threads 1
+(worker id 0, ps = index of the unit in the shuffled list): the reference's own multi-process output differs from
+that only in the serial's worker/ps fields and in record order (SURVEY.md Finding 2).  `threads` is accepted for
+CLI compatibility; `gpus` > 1 is handled by mitty_amd.distributed.
+"""
+import logging
+import re
+import time
+from collections import namedtuple
+
+from mitty_amd import _native
+from mitty_amd.engine import Engine
+from mitty_amd.lib import fasta as mfasta
+from mitty_amd.lib import vcfio
+
+logger = logging.getLogger(__name__)
+
+SEED_MAX = (1 << 32) - 1
+DNA_complement = str.maketrans('ATCGN', 'TAGCN')
+
+__qname_format__ = '@read_serial|chrom|copy|strand|pos|rlen|cigar|vs1,vs2,...|strand|pos|rlen|cigar|vs1,vs2,...'
+__qname_format_details__ = """
+@read_serial|chrom|copy|strand|pos|rlen|cigar|vs1,vs2,...|strand|pos|rlen|cigar|vs1,vs2,...
+    |          |     |    |     |    |    |        |         |                      |
+ unique        |     |    |     | read    |        |         ---- repeated for ------
+ code for      |     |    |     | len     |        |          other read in template
+ template      |     |    |     |         |        |
+               |     |    |     |     cigar    comma separated
+      chrom read     |    |     |              list of sizes of
+  was taken from     |    |     |              variants this read
+       One based     |    |     |              covers
+                     |    |     |
+                     |    |     |
+    copy of chrom read    |     |
+ was taken from (0, 1)    |     |
+                          |     |
+         forward strand (0)     |
+      or reverse strand (1)     |
+                                |
+                      pos of read
+                        One based
+
+The chrom and pos are one based to make comparing qname info in genome browser easier
+
+For reads from inside a long insertion the CIGAR has the following format:
+
+  '>p:nI'
+
+where:
+
+ '>' is the unique key that indicates a read inside a long insertion
+ 'p' is how many bases into the insertion branch the read starts
+ 'n' is simply the length of the read
+"""
+
+
+def get_data_for_workers(model, vcf, seed):
+  """Work units in the reference's order (readgenerate.py:129-159).  `vcf` entries need 'ploidy' or 'v'."""
+  ploidy = [v['ploidy'] if 'ploidy' in v else len(v['v']) for v in vcf]
+  for r, c, s in _native.work_units(seed, ploidy, model['passes']):
+    yield {'region_idx': r, 'region_cpy': c, 'rng_seed': s}
+
+
+def _write_all(fp, data):
+  mv = memoryview(data)
+  while len(mv):
+    n = fp.write(mv)
+    mv = mv[n:]
+
+
+def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
+                           fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
+                           flush_bytes=1 << 30):
+  """Generate reads for every (region, copy, pass) unit and write FASTQ (reference readgenerate.py:76-126).
+
+  Returns a stats dict (templates sampled, kept, bytes, seconds).
+  """
+  t0 = time.time()
+  read_model = read_module.read_model_params(model, coverage)
+  vdf = vcfio.load_variants_soa(vcf_fname, sample_name, bed_fname)
+  seqs = mfasta.read_fasta(fasta_fname, names={r['region'][0] for r in vdf})
+  units = list(get_data_for_workers(read_model, vdf, seed))
+  logger.debug('{} passes will be made'.format(len(units)))
+  eng = Engine(device)
+  if corrupt_seed is not None:
+    import numpy as np
+    eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), corrupt_seed)
+  for ri, reg in enumerate(vdf):
+    chrom, s0, e = reg['region']
+    eng.load_region(ri, reg['region'], mfasta.fetch(seqs, chrom, s0, e))
+  stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0}
+  write2 = fastq2_fname is not None
+  fp1 = open(fastq1_fname, 'wb')
+  fp2 = open(fastq2_fname, 'wb') if write2 else None
+  try:
+    for ps, wd in enumerate(units):
+      ri, cpy, rs = wd['region_idx'], wd['region_cpy'], wd['rng_seed']
+      t1 = time.time()
+      n, kept, b1, b2 = eng.run_unit(ps, ri, cpy, rs, vdf[ri]['copies'][cpy], read_model['p'], read_model['rlen'],
+                                     read_model['cum_tlen'], sample_name, 0, write2, rng)
+      stats['templates'] += n
+      stats['kept'] += kept
+      stats['bytes1'] += b1
+      stats['bytes2'] += b2
+      logger.debug('Unit {} ({}, copy {}): {} templates in {:0.3f}s'.format(ps, vdf[ri]['region'], cpy, kept,
+                                                                         time.time() - t1))
+      u1, u2 = eng.ctx.output_size()
+      if u1 + u2 >= flush_bytes or ps == len(units) - 1:
+        d1, d2 = eng.ctx.fetch_output()
+        _write_all(fp1, d1)
+        if write2:
+          _write_all(fp2, d2)
+        eng.ctx.reset_output()
+  finally:
+    fp1.close()
+    if fp2:
+      fp2.close()
+    eng.close()
+  stats['seconds'] = time.time() - t0
+  return stats
+
+
+def fastq_lines(n, chrom, cpy, reads):
+  """readgenerate.fastq_lines (readgenerate.py:222-230) — host-side formatter for single templates."""
+  qname = '@{}|{}|{}'.format(n, chrom, cpy)
+  for r in reads:
+    qname += '|{}|{}|{}|{}|{}'.format(r[0], r[1], r[2], r[3], ','.join(str(int(v)) for v in r[4]))
+  return [qname + '\n' + r[5] + '\n+\n' + '~' * int(r[2]) + '\n' for r in reads]
+
+
+ri = namedtuple('ReadInfo', ['sample', 'rid', 'chrom', 'cpy', 'strand', 'pos', 'rlen', 'cigar', 'special_cigar',
+                             'v_list'])
+
+
+def parse_qname(qname):
+  """readgenerate.parse_qname (readgenerate.py:259-291)."""
+  def _parse_(_cigar, _v_list):
+    if _cigar[0] == '>':
+      _special_cigar = _cigar
+      _cigar = _cigar.split(':')[-1]
+    else:
+      _special_cigar = None
+    return _cigar, _special_cigar, [int(v) for v in _v_list.split(',') if v != '']
+
+  d = qname.split('|')
+  rid, chrom, cpy = d[:3]
+  sample, _ = rid.split(':', 1)
+  cpy = int(cpy)
+  return [ri(sample, rid, chrom, cpy, int(strand), int(pos), int(rlen), *_parse_(cigar, v_list))
+          for strand, pos, rlen, cigar, v_list in zip(d[3::5], d[4::5], d[5::5], d[6::5], d[7::5])]
+
+
+cigar_parser = re.compile(r'(\d+)(\D)')

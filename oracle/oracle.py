@@ -218,6 +218,30 @@ def generate_unit(ref_seq, region_start0, vl, p, rlen, cum_tlen, rng_seed, seria
   return n, b1, b2
 
 
+def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, serial_stub, chrom, cpy):
+  """generate_unit for variants already in structure-of-arrays form (pos, op, oplen, alt_off, alt_len, alt_pool)."""
+  pos = np.ascontiguousarray(soa['pos'], dtype=np.int64)
+  op = np.ascontiguousarray(soa['op'], dtype=np.uint8)
+  oplen = np.ascontiguousarray(soa['oplen'], dtype=np.int64)
+  aoff = np.ascontiguousarray(soa['alt_off'], dtype=np.int64)
+  alen = np.ascontiguousarray(soa['alt_len'], dtype=np.int64)
+  pool = soa['alt_pool'] or b'\0'
+  if len(op) == 0:
+    op = np.zeros(1, np.uint8)
+  cum_tlen = np.ascontiguousarray(cum_tlen, dtype=np.float64)
+  o1, o2 = ctypes.c_void_p(), ctypes.c_void_p()
+  l1, l2 = ctypes.c_int64(), ctypes.c_int64()
+  n = lib().mo_generate_unit(ref_seq, len(ref_seq), region_start0, _p(pos), _p(op), _p(oplen), _p(aoff), _p(alen),
+                             pool, len(pos), p, rlen, _p(cum_tlen), len(cum_tlen), rng_seed, serial_stub.encode(),
+                             chrom.encode(), cpy, ctypes.byref(o1), ctypes.byref(l1), ctypes.byref(o2),
+                             ctypes.byref(l2))
+  b1 = ctypes.string_at(o1, l1.value) if l1.value else b''
+  b2 = ctypes.string_at(o2, l2.value) if l2.value else b''
+  lib().mo_free(o1)
+  lib().mo_free(o2)
+  return n, b1, b2
+
+
 def generate_reads_fastq(fasta, vcf, sample, bed, model, coverage, seed, max_units=None):
   """readgenerate.process_multi_threaded(..., threads=1): returns (r1_bytes, r2_bytes, n_templates)."""
   seqs = read_fasta(fasta) if isinstance(fasta, str) else fasta

@@ -1,0 +1,319 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the CPU oracle.
+
+Bar: bit-exact (integer / byte work).  Sizes: golden fixtures (reference-captured), oracle comparisons up to a few
+Mbp, and size-independent properties at larger sizes.
+"""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from tests import golden_io as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def native():
+  from mitty_amd import _native
+  if _native.device_count() == 0:
+    pytest.fail('no HIP device: GPU tests must run on an MI355X')
+  return _native
+
+
+@pytest.fixture(scope='module')
+def ctx(native):
+  c = native.Context(0)
+  yield c
+  c.close()
+
+
+# ---- template sampling (illumina.generate_reads) ---------------------------------------------------------------
+def test_templates_golden(native):
+  from mitty_amd.simulation import illumina
+  t = G.templates()
+  keys = sorted({k.rsplit('|', 1)[0] for k in t.files})
+  assert len(keys) == 12
+  for key in keys:
+    m, seed, p_min, p_max = key.split('|')
+    rm = illumina.read_model_params(G.model(m), 30.0)
+    r = illumina.generate_reads(rm, int(p_min), int(p_max), int(seed))
+    assert np.array_equal(r[0]['file_order'], t[key + '|fo0']), key
+    assert np.array_equal(r[0]['pos'], t[key + '|pos0']), key
+    assert np.array_equal(r[1]['pos'], t[key + '|pos1']), key
+    assert r[0]['file_order'].dtype == np.int8 and r[0]['pos'].dtype == np.int64 and r[0]['len'].dtype == np.uint32
+    assert np.array_equal(r[1]['file_order'], 1 - t[key + '|fo0'])
+
+
+@pytest.mark.parametrize('span,seed', [(3_000_000, 7), (20_000_000, 99), (61_000, 4294967295), (41, 3), (1, 5)])
+@pytest.mark.parametrize('model', G.MODELS)
+def test_templates_vs_oracle(native, model, span, seed):
+  """Larger spans than the golden set (exercise the shuffle decode / permutation at millions of draws)."""
+  from mitty_amd.simulation import illumina
+  from oracle import oracle as O
+  mdl = G.model(model)
+  rm = illumina.read_model_params(mdl, 30.0)
+  r = illumina.generate_reads(rm, 1000, 1000 + span, seed)
+  fo, p0, p1 = O.generate_templates(rm['p'], int(rm['rlen']), mdl['cum_tlen'], 1000, 1000 + span, seed)
+  assert np.array_equal(r[0]['file_order'], fo)
+  assert np.array_equal(r[0]['pos'], p0)
+  assert np.array_equal(r[1]['pos'], p1)
+
+
+def test_templates_high_coverage_vs_oracle(native):
+  """p close to 0.1 (coverage 60, 2x150 -> passes 4, p = 0.025 ... use a direct p) and tiny rlen."""
+  from mitty_amd.simulation import illumina
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  for p in (0.1, 0.0999, 0.05, 0.4, 0.9):
+    rm = {'p': p, 'rlen': 30, 'cum_tlen': mdl['cum_tlen']}
+    r = illumina.generate_reads(rm, 0, 400_000, 11)
+    fo, p0, p1 = O.generate_templates(p, 30, mdl['cum_tlen'], 0, 400_000, 11)
+    assert np.array_equal(r[0]['pos'], p0) and np.array_equal(r[1]['pos'], p1)
+    assert np.array_equal(r[0]['file_order'], fo)
+
+
+def test_seed_out_of_range(native):
+  from mitty_amd.simulation import illumina
+  rm = illumina.read_model_params(G.model('hiseq-X-v2.5-Garvan'), 30.0)
+  with pytest.raises(ValueError):
+    illumina.generate_reads(rm, 0, 1000, 1 << 32)
+  with pytest.raises(ValueError):
+    illumina.generate_reads(rm, 0, 1000, -1)
+
+
+# ---- splice / read derivation (rpc) ----------------------------------------------------------------------------
+def _seqs():
+  from mitty_amd.lib import fasta
+  return {'syn': fasta.read_fasta(G.path('data/syn.fa')), 'tiny': fasta.read_fasta(G.path('data/tiny.fasta'))}
+
+
+def test_node_lists_golden(native):
+  from mitty_amd.lib import vcfio
+  from mitty_amd.simulation import rpc
+  seqs = _seqs()
+  for key, d in G.load_json('nodes.json').items():
+    tag = key.split('|')[0]
+    chrom, s0, e = d['region']
+    vl = [vcfio.Variant(*v) for v in d['variants']]
+    nodes = rpc.create_node_list(seqs[tag][chrom][s0:e].decode(), s0 + 1, vl)
+    assert [list(n.tuple()) for n in nodes] == d['nodes'], key
+
+
+def test_reads_golden(native):
+  from mitty_amd.lib import vcfio
+  from mitty_amd.simulation import rpc
+  seqs = _seqs()
+  nodes_g = G.load_json('nodes.json')
+  reads = G.load_json('reads.json.gz')
+  total = 0
+  for key, rows in reads.items():
+    d = nodes_g[key]
+    tag = key.split('|')[0]
+    chrom, s0, e = d['region']
+    nodes = rpc.create_node_list(seqs[tag][chrom][s0:e].decode(), s0 + 1, [vcfio.Variant(*v) for v in d['variants']])
+    pl = [r[0] for r in rows]
+    ll = [r[1] for r in rows]
+    got, n0, n1 = rpc.generate_reads_batch(pl, ll, nodes)
+    for r, g, a, b in zip(rows, got, n0, n1):
+      assert [r[2], r[3]] == [int(a), int(b)], (key, r[:2])
+      assert [r[4], r[5], r[6], r[7]] == [g[0], g[1], g[2], g[3]], (key, r[:2])
+    total += len(rows)
+  assert total > 5000
+
+
+def test_reference_rpc_known_answers(native):
+  """mitty/test/simulation/test_rpc.py:111-180 restated against the device path."""
+  from mitty_amd.lib import vcfio
+  from mitty_amd.simulation import rpc
+  ref_seq = open(G.path('data/tiny.fasta')).readlines()[1]
+  vdf = vcfio.load_variant_file(G.path('data/tiny.vcf'), 'g0_s0', G.path('data/tiny.whole.bed'))
+  nodes = rpc.create_node_list(ref_seq, 1, vdf[0]['v'][1])
+  assert len(nodes) == 9
+  assert nodes[0] == (1, 1, '=', 4, 'ATGA', None)
+  assert nodes[3] == (9, 9, 'I', 3, 'TTT', 3)
+  assert nodes[5] == (14, 14, 'D', 2, '', -2)
+  assert nodes[7] == (21, 25, 'D', 4, '', -4)
+  assert nodes[8] == (22, 25, '=', 1, 'C', None)
+  nse = rpc.get_begin_end_nodes(np.arange(1, 16), 10, nodes)
+  assert nse[0].tolist() == [0, 0, 0, 0, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4, 6]
+  assert nse[1].tolist() == [3, 3, 4, 4, 4, 6, 6, 6, 6, 6, 6, 6, 8, 8, 8]
+  assert rpc.generate_read(1, 10, 0, 3, nodes) == (1, '4=1X3=2I', [0, 3], 'ATGATGTATT')
+  assert rpc.generate_read(6, 10, 2, 6, nodes) == (6, '3=3I3=2D1=', [3, -2], 'GTATTTTCCG')
+  assert rpc.generate_read(10, 10, 3, 6, nodes) == (9, '2I3=2D5=', [3, -2], 'TTTCCGGAGG')
+  assert rpc.generate_read(13, 10, 4, 8, nodes) == (10, '2=2D7=4D1=', [-2, -4], 'CCGGAGGCGC')
+  assert rpc.generate_read(15, 8, 6, 8, nodes) == (14, '7=4D1=', [-4], 'GGAGGCGC')
+  assert rpc.generate_read(9, 2, 3, 3, nodes) == (8, '>0:2I', [3], 'TT')
+  nodes0 = rpc.create_node_list(ref_seq, 1, vdf[0]['v'][0])
+  assert rpc.generate_read(5, 10, 0, 1, nodes0) == (5, '9=1X', [0], 'CGTATCCAAT')
+  assert rpc.generate_read(6, 10, 0, 2, nodes0) == (6, '8=1X1=', [0], 'GTATCCAATG')
+
+
+def test_survey_edge_cases(native):
+  """SURVEY.md Appendix B1-B5 node-list quirks."""
+  from mitty_amd.lib.vcfio import Variant
+  from mitty_amd.simulation import rpc
+  ref = 'ACGTACGTAC' * 3
+  nodes = rpc.create_node_list(ref, 1, [Variant(27, 'CGTACG', 'C', 'D', 5)])           # B1
+  assert [n.tuple()[:4] for n in nodes] == [(1, 1, '=', 27), (27, 33, 'D', 5)]
+  ref = 'ACGTA' + 'C' * 25
+  nodes = rpc.create_node_list(ref, 1, [Variant(5, 'A', 'A' + 'T' * 20, 'I', 20)])     # B2
+  assert rpc.generate_read(6, 5, 1, 1, nodes) == (5, '>0:5I', [20], 'TTTTT')
+  assert rpc.generate_read(8, 5, 1, 1, nodes) == (5, '>2:5I', [20], 'TTTTT')
+  assert rpc.generate_read(3, 5, 0, 1, nodes) == (3, '3=2I', [20], 'GTATT')
+  assert rpc.generate_read(20, 8, 1, 2, nodes) == (6, '6I2=', [20], 'TTTTTTCC')
+  ref = 'ACGTACGTACGTACGTACGTACGTAC'
+  vl = [Variant(5, 'ACGT', 'A', 'D', 3), Variant(6, 'C', 'T', 'X', 0), Variant(9, 'A', 'T', 'X', 0),
+        Variant(9, 'A', 'AG', 'I', 1)]                                                       # B3
+  nodes = rpc.create_node_list(ref, 1, vl)
+  assert [n.tuple()[:4] for n in nodes] == [(1, 1, '=', 5), (5, 9, 'D', 3), (6, 9, 'X', 1), (7, 10, '=', 17)]
+
+
+# ---- end to end --------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize('model', G.MODELS)
+def test_e2e_fastq_byte_identical_to_reference(native, model, tmp_path):
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  c = G.load_json('e2e_config.json')[model]
+  mod, mdl = get_read_model(model + '.pkl')
+  f1, f2 = str(tmp_path / 'r1.fq'), str(tmp_path / 'r2.fq')
+  readgenerate.process_multi_threaded(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], f1, f2, threads=2, seed=c['seed'])
+  assert open(f1, 'rb').read() == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
+  assert open(f2, 'rb').read() == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+
+
+def test_e2e_single_file_and_cli(native, tmp_path):
+  """--fastq2 omitted: file 1 only (readgenerate.py:244-245), through the click CLI."""
+  from click.testing import CliRunner
+  from mitty_amd.cli import cli
+  c = G.load_json('e2e_config.json')['hiseq-X-v2.5-Garvan']
+  f1 = str(tmp_path / 'r1.fq')
+  res = CliRunner().invoke(cli, ['generate-reads', G.path(c['fasta']), G.path(c['vcf']), c['sample'],
+                                 G.path(c['bed']), 'hiseq-X-v2.5-Garvan.pkl', str(c['coverage']), str(c['seed']), f1])
+  assert res.exit_code == 0, res.output + repr(res.exception)
+  assert open(f1, 'rb').read() == G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
+
+
+def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(0, 1)):
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model(model)
+  p, _ = _native.read_model_params(mdl['mean_rlen'], 30.0)
+  seq = synth.contig(length, n_seed)
+  recs = synth.variants(seq, n_seed + 1, rate=rate)
+  copies = synth.copies_soa(recs, start0, length)
+  ref = seq[start0:]
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('7', start0, length), ref)
+    for cpy in cpys:
+      eng.ctx.reset_output()
+      n, kept, b1, b2 = eng.run_unit(3, 0, cpy, seed + cpy, copies[cpy], p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')
+      d1, d2 = eng.ctx.fetch_output()
+      k, o1, o2 = O.generate_unit_soa(ref, start0, copies[cpy], p, int(mdl['mean_rlen']), mdl['cum_tlen'], seed + cpy,
+                                      'SYN:0:3', '7', cpy)
+      assert kept == k
+      assert d1 == o1, 'file 1 differs (copy {})'.format(cpy)
+      assert d2 == o2, 'file 2 differs (copy {})'.format(cpy)
+  finally:
+    eng.close()
+  return kept
+
+
+@pytest.mark.parametrize('model', G.MODELS)
+def test_unit_vs_oracle_2mbp(native, model):
+  assert _unit_vs_oracle(2_000_000, 7, model) > 10000
+
+
+def test_unit_vs_oracle_dense_variants_offset_region(native):
+  _unit_vs_oracle(1_500_000, 4000000000, 'hiseq-X-v2.5-Garvan', n_seed=5, rate=8e-3, start0=123_457)
+
+
+def test_unit_vs_oracle_no_variants(native):
+  _unit_vs_oracle(600_000, 1, '1kg-pcr-free', n_seed=9, rate=0.0)
+
+
+# ---- size-independent properties at full chromosome scale -------------------------------------------------------
+def test_chr1_scale_properties(native):
+  """One chr1-sized unit (249 Mbp): every record parses, POS/CIGAR are consistent with the sequence length, every
+  read sequence equals the haplotype slice its qname implies, cnt runs 1..kept."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from mitty_amd.simulation.readgenerate import parse_qname
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  L = 249_250_621
+  seq = synth.contig(L, 1)
+  recs = synth.variants(seq, 2)
+  copies = synth.copies_soa(recs)
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('1', 0, L), seq)
+    n, kept, b1, b2 = eng.run_unit(0, 0, 1, 12345, copies[1], p, 150, mdl['cum_tlen'], 'SYN')
+    assert n > 7_000_000 and kept > 0.8 * n
+    slot, n_nodes, p_min, p_max = eng.haplotype(0, 1, copies[1])
+    ps, pr, op, ol, hap = eng.ctx.get_nodes(slot, n_nodes)
+    # sample a slice of records from the arena
+    d1, d2 = eng.ctx.fetch_output(0, min(b1, 40_000_000), 0, min(b2, 40_000_000))
+  finally:
+    eng.close()
+  assert b1 == b2 or abs(b1 - b2) < b1 // 1000
+  lines = d1.split(b'\n')
+  n_rec = (len(lines) - 1) // 4
+  assert n_rec > 50000
+  for i in range(0, n_rec - 1, 97):
+    qn, s, q = lines[4 * i][1:].decode(), lines[4 * i + 1], lines[4 * i + 3]
+    ri = parse_qname(qn)
+    assert int(qn.split('|')[0].split(':')[3]) == i + 1
+    assert len(q) == 150 and set(q) == {ord('~')}
+    r = ri[0]
+    if r.special_cigar is None:
+      import re
+      consumed = sum(int(a) for a, o in re.findall(r'(\d+)([=XID])', r.cigar) if o in '=XI')
+      assert consumed == len(s) == 150
+
+
+# ---- corruption (Philox mode) ----------------------------------------------------------------------------------
+def test_corruption_statistics(native, tmp_path):
+  """Qnames unchanged; qualities follow the model's per-position BQ distribution; substitution rate follows the
+  phred error probability; substitutions are to a different base."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  seq = synth.contig(3_000_000, 3)
+  copies = synth.copies_soa(synth.variants(seq, 4))
+  outs = []
+  for corrupt in (False, True):
+    eng = Engine(0)
+    try:
+      if corrupt:
+        eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 7)
+      eng.load_region(0, ('1', 0, len(seq)), seq)
+      eng.run_unit(0, 0, 0, 77, copies[0], p, 150, mdl['cum_tlen'], 'S')
+      outs.append(eng.ctx.fetch_output())
+    finally:
+      eng.close()
+  (a1, a2), (c1, c2) = outs
+  for a, c, mate in ((a1, c1, 0), (a2, c2, 1)):
+    la, lc = a.split(b'\n'), c.split(b'\n')
+    assert len(la) == len(lc)
+    assert la[0::4] == lc[0::4]                      # qnames untouched
+    seq_a, seq_c, qual = la[1::4], lc[1::4], lc[3::4]
+    n = len(qual) - 1
+    Q = np.frombuffer(b''.join(qual[:n]), np.uint8).reshape(n, 150).astype(np.int64) - 33
+    SA = np.frombuffer(b''.join(seq_a[:n]), np.uint8).reshape(n, 150)
+    SC = np.frombuffer(b''.join(seq_c[:n]), np.uint8).reshape(n, 150)
+    # BQ histogram at a few positions vs the model's pmf
+    for pos in (0, 75, 149):
+      pmf = np.diff(np.concatenate([[0.0], mdl['cum_bq_mat'][mate, pos, :]]))
+      h = np.bincount(Q[:, pos], minlength=94)[:94] / n
+      assert np.abs(h - pmf).max() < 0.02, (mate, pos)
+    err = SA != SC
+    exp = (10 ** (-Q / 10.0)).mean()
+    assert abs(err.mean() - exp) < 0.1 * exp + 1e-4
+    changed = SC[err]
+    assert not np.any(changed == SA[err])

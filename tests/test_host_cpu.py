@@ -1,0 +1,140 @@
+"""CPU-side checks: the C-ABI library loads and exports every declared symbol; host-side logic (model loading,
+VCF parsing, work units, qname codec) against the reference's golden vectors.  No GPU compute here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mitty_amd import _native, readmodel
+from mitty_amd.lib import vcfio
+from mitty_amd.simulation import readgenerate
+from tests import golden_io as G
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+  with open(os.path.join(REPO, 'include', 'mitty_hip.h')) as fp:
+    txt = fp.read()
+  return sorted(set(re.findall(r'\b(mh_[a-z_0-9]+)\s*\(', txt)))
+
+
+def test_header_matches_binding_list():
+  assert _declared() == sorted(_native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+  import ctypes
+  L = _native.lib()
+  for name in _declared():
+    assert hasattr(L, name), name
+    assert isinstance(getattr(L, name), ctypes._CFuncPtr)
+  assert L.mh_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+  import subprocess
+  out = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-objdump', '--offloading', _native.LIB_PATH],
+                       capture_output=True, text=True, cwd='/tmp')
+  if out.returncode != 0:
+    pytest.skip('llvm-objdump --offloading unavailable')
+  assert 'gfx950' in out.stdout + out.stderr
+
+
+def test_work_units_host_abi():
+  for key, d in G.load_json('units.json').items():
+    seed, passes = map(int, key.split(':'))
+    got = [list(u) for u in _native.work_units(seed, d['ploidy'], passes)]
+    assert got == d['units'], key
+
+
+def test_read_model_params_host_abi():
+  rng = G.load_json('rng.json')
+  for m, by_cov in rng['read_model_params'].items():
+    mdl = G.model(m)
+    for cov, want in by_cov.items():
+      p, passes = _native.read_model_params(mdl['mean_rlen'], float(cov))
+      assert p.hex() == want['p'] and passes == want['passes']
+
+
+def test_work_units_bad_seed():
+  with pytest.raises(ValueError):
+    _native.work_units(1 << 32, [2], 2)
+
+
+def test_safe_model_parser_matches_builtin():
+  mods = readmodel.builtin_models()
+  assert 'hiseq-X-v2.5-Garvan.pkl' in mods and '1kg-pcr-free.pkl' in mods and len(mods) == 5
+  _, m = readmodel.get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  assert m['mean_rlen'] == 150 and m['cum_bq_mat'].shape == (2, 300, 94) and m['cum_tlen'][-1] == 1.0
+  _, m = readmodel.get_read_model('1kg-pcr-free.pkl')
+  assert m['mean_rlen'] == 250
+
+
+def test_safe_model_parser_refuses_code(tmp_path):
+  import pickle
+
+  class Evil:
+    def __reduce__(self):
+      return (os.system, ('echo pwned',))
+  p = tmp_path / 'evil.pkl'
+  p.write_bytes(pickle.dumps({'x': Evil()}, protocol=3))
+  with pytest.raises(readmodel.UnsafeModelError):
+    readmodel.load_model_file(str(p))
+
+
+def test_safe_model_parser_roundtrip(tmp_path):
+  import pickle
+  m = {'model_class': 'illumina', 'model_description': 'x', 'mean_rlen': 100, 'r_cnt': 10 ** 12,
+       'cum_tlen': np.linspace(0, 1, 7), 'bq_mat': np.arange(24, dtype=np.uint64).reshape(2, 3, 4)}
+  p = tmp_path / 'm.pkl'
+  p.write_bytes(pickle.dumps(m, protocol=3))
+  got = readmodel.load_model_file(str(p))
+  assert got['mean_rlen'] == 100 and got['r_cnt'] == 10 ** 12 and got['model_class'] == 'illumina'
+  assert np.array_equal(got['cum_tlen'], m['cum_tlen']) and np.array_equal(got['bq_mat'], m['bq_mat'])
+
+
+def test_vcf_loading_matches_reference():
+  nodes = G.load_json('nodes.json')
+  for vcf in ('syn.vcf', 'syn.vcf.gz'):
+    vdf = vcfio.load_variant_file(G.path('data', vcf), 'S1', G.path('data/syn.bed'))
+    for ri, reg in enumerate(vdf):
+      for cpy, vl in enumerate(reg['v']):
+        assert [list(v.tuple()) for v in vl] == nodes['syn|{}|{}'.format(ri, cpy)]['variants']
+  soa = vcfio.load_variants_soa(G.path('data/syn.vcf'), 'S1', G.path('data/syn.bed'))
+  assert [r['ploidy'] for r in soa] == [2, 2, 2, 1]
+
+
+def test_vcfio_reference_unit_tests():
+  """mitty/test/lib/test_vcfio.py:9-62 restated."""
+  v = vcfio.load_variant_file(G.path('data/tiny.vcf'), 'g0_s0', G.path('data/tiny.8-14.bed'))
+  assert v[0]['v'][1][0].tuple() == (11, 'CAA', 'C', 'D', 2)
+  assert v[0]['v'][0][0].tuple() == (14, 'G', 'T', 'X', 0)
+  assert len(v[0]['v'][0]) == 1
+  with pytest.raises(ValueError):
+    vcfio.load_variants_soa(G.path('data/flawed-tiny.vcf'), 'g0_s0', G.path('data/tiny.whole.bed'))
+  v = vcfio.load_variant_file(G.path('data/tiny.vcf'), 'g0_s0', G.path('data/tiny.whole.bed'))
+  assert (v[0]['v'][1][0].cigarop, v[0]['v'][1][0].oplen) == ('X', 0)
+  assert (v[0]['v'][1][1].cigarop, v[0]['v'][1][1].oplen) == ('I', 3)
+  assert (v[0]['v'][1][2].cigarop, v[0]['v'][1][2].oplen) == ('D', 2)
+
+
+def test_parse_qname_matches_reference():
+  for qn, want in G.load_json('qnames.json'):
+    got = [list(r) for r in readgenerate.parse_qname(qn)]
+    assert got == want
+
+
+def test_native_fails_loudly_without_library(monkeypatch):
+  monkeypatch.setattr(_native, '_lib', None)
+  monkeypatch.setattr(_native, 'LIB_PATH', '/nonexistent/libmitty_hip.so')
+  with pytest.raises(_native.NativeUnavailable):
+    _native.Context(0)
+
+
+def test_no_device_raises_here():
+  if _native.device_count() > 0:
+    pytest.skip('a GPU is visible')
+  with pytest.raises(_native.NativeUnavailable):
+    _native.Context(0)
