@@ -8,14 +8,20 @@
 // (:222-230), cnt counting only kept templates.
 //
 // Device plan (two passes over the template arrays, one over the bases):
-//   k_emit_measure  one thread per template: node search, CIGAR/v-list text lengths, N count from the haplotype's
-//                   N runs (no base reads), keep flag, per-file record length without the cnt digits.
+//   k_emit_measure  one thread per template: node search (start/end node of both mates, kept for pass 2),
+//                   CIGAR / v-list text lengths, N count from the haplotype's N runs (no base reads), keep flag,
+//                   per-file record length without the cnt digits.
 //   scan            (kept, bytes1, bytes2) -> cnt and exact byte offsets; the cnt digits are added in closed form
 //                   (sum_{c<=K} digits(c)), so one scan suffices.
-//   k_emit_write    64 templates per 256-thread workgroup: owner threads format the qnames into two LDS images
-//                   (one per FASTQ file), all threads gather the bases from the haplotype (reverse complement for
-//                   mate 1) and fill '~' qualities, then the images leave LDS as 16-byte aligned stores into the
-//                   file arenas (byte stores only at the two ragged edges of a workgroup's range).
+//   k_emit_write    32 templates per 256-thread workgroup:
+//                     B0  every thread issues its 16-byte haplotype gathers (both mates of every template) into an
+//                         LDS window buffer — all gathers of the tile in flight at once;
+//                     A   one owner thread per template formats the qname into the file-1 LDS image;
+//                     B1  one wave per (template, file) copies the qname into the file-2 image and writes
+//                         '\n' seq '\n+\n' qual '\n' from the LDS windows (reverse complement for mate 1, fused
+//                         BQ corruption when enabled);
+//                     C   both images leave LDS as 16-byte aligned stores (byte stores only at the ragged edges of
+//                         the workgroup's output range; neighbouring workgroups own disjoint byte ranges).
 // The sequence of a read is hap[p - p_min, min(p + l, hap_end) - p_min): non-'D' nodes tile sample coordinates
 // contiguously, so the reference's per-node slice concatenation (rpc.py:146) is one contiguous range.
 #include "mh_internal.h"
@@ -45,6 +51,11 @@ __device__ __forceinline__ int64_t upper_bound(const int64_t *a, int64_t n, int6
 }
 
 __device__ __forceinline__ int ndig_u(uint64_t v) {
+  if (v <= 0xffffffffull) {
+    uint32_t x = (uint32_t)v;
+    return x < 10u ? 1 : x < 100u ? 2 : x < 1000u ? 3 : x < 10000u ? 4 : x < 100000u ? 5 : x < 1000000u ? 6
+         : x < 10000000u ? 7 : x < 100000000u ? 8 : x < 1000000000u ? 9 : 10;
+  }
   int d = 1;
   while (v >= 10) { v /= 10; d++; }
   return d;
@@ -88,6 +99,26 @@ __device__ __forceinline__ int64_t node_v(const HapView &h, int64_t k) {
   return o == 'X' ? 0 : (o == 'I' ? h.oplen[k] : -h.oplen[k]);
 }
 
+// POS / special-CIGAR / sequence range of a read whose start and end nodes are known (rpc.py:144-160).
+__device__ __forceinline__ void read_place(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
+  r.special = false;
+  const uint8_t o0 = h.op[r.n0];
+  if (o0 == 'I') {
+    if (r.n0 == r.n1) {
+      r.special = true;
+      r.pos = h.pr[r.n0] - 1;
+    } else {
+      r.pos = h.pr[r.n0];
+    }
+  } else {
+    r.pos = p - h.ps[r.n0] + h.pr[r.n0];
+  }
+  int64_t a = p - h.p_min, b = p + l - h.p_min;
+  if (b > h.hap_len) b = h.hap_len;
+  r.hap_a = a;
+  r.seq_len = (int32_t)(b > a ? b - a : 0);
+}
+
 // rpc.get_begin_end_nodes + the lengths of rpc.generate_read's outputs.  Requires p >= p_min (n0 >= 0).
 __device__ void read_info(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
   r.n0 = upper_bound(h.keys, h.n_nodes, p) - 1;
@@ -101,25 +132,10 @@ __device__ void read_info(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
       first = false;
     }
   }
-  r.special = false;
-  const uint8_t o0 = h.op[r.n0];
-  if (o0 == 'I') {
-    if (r.n0 == r.n1) {
-      r.special = true;
-      r.pos = h.pr[r.n0] - 1;
-      cl = 1 + ndig_s(p - h.ps[r.n0]) + 1 + ndig_s(l) + 1;
-    } else {
-      r.pos = h.pr[r.n0];
-    }
-  } else {
-    r.pos = p - h.ps[r.n0] + h.pr[r.n0];
-  }
+  read_place(h, p, l, r);
+  if (r.special) cl = 1 + ndig_s(p - h.ps[r.n0]) + 1 + ndig_s(l) + 1;
   r.cigar_len = cl;
   r.vlist_len = vl;
-  int64_t a = p - h.p_min, b = p + l - h.p_min;
-  if (b > h.hap_len) b = h.hap_len;
-  r.hap_a = a;
-  r.seq_len = (int32_t)(b > a ? b - a : 0);
 }
 
 __device__ char *write_cigar(char *d, const HapView &h, int64_t p, int64_t l, const ReadInfo &r) {
@@ -162,6 +178,7 @@ __device__ int count_N(const HapView &h, int64_t a, int64_t b) {
 
 struct Rec {
   int32_t keep, len1, len2, pad;
+  int32_t n0[2], n1[2];   // start / end node per mate (pass 2 skips the searches)
 };
 struct E3 {
   int64_t kept, b1, b2;
@@ -196,25 +213,26 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int32_t local_max = 0;
   if (t < m) {
-  ReadInfo r[2];
-  read_info(h, pos0[t], rlen, r[0]);
-  read_info(h, pos1[t], rlen, r[1]);
-  int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
-             count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
-  Rec out{0, 0, 0, 0};
-  if (keep) {
-    int32_t ql = qname_len_wo_cnt(q, r, rlen);
-    int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-    int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
-    int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
-    int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
-    out = Rec{1, ql + 1 + s_f1 + 3 + q1 + 1, ql + 1 + s_f2 + 3 + q2 + 1, 0};
-    local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+    ReadInfo r[2];
+    read_info(h, pos0[t], rlen, r[0]);
+    read_info(h, pos1[t], rlen, r[1]);
+    int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+               count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
+    if (keep) {
+      int32_t ql = qname_len_wo_cnt(q, r, rlen);
+      int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
+      int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
+      int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
+      int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
+      out.keep = 1;
+      out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
+      out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
+      local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+    }
+    recs[t] = out;
   }
-  recs[t] = out;
-  }
-  // one atomic per wave
-  for (int d = 32; d >= 1; d >>= 1) {
+  for (int d = 32; d >= 1; d >>= 1) {   // one atomic per wave
     int32_t o = __shfl_xor(local_max, d, 64);
     local_max = o > local_max ? o : local_max;
   }
@@ -225,7 +243,7 @@ struct LoadRec {
   const Rec *recs; int64_t m;
   __device__ E3 operator()(int64_t t) const {
     if (t >= m) return E3{0, 0, 0};
-    Rec r = recs[t];
+    const Rec &r = recs[t];
     return r.keep ? E3{1, r.len1, r.len2} : E3{0, 0, 0};
   }
 };
@@ -237,16 +255,16 @@ struct StoreOff {
   }
 };
 
-constexpr int EW_T = 64;        // templates per workgroup
+constexpr int EW_T = 32;        // templates per workgroup
 constexpr int EW_THREADS = 256;
+constexpr int EW_WAVES = EW_THREADS / 64;
 
 struct TplMeta {
   int32_t loc[2];       // record offset inside each LDS image
   int32_t qlen;         // qname length (with cnt)
-  int32_t seq_len[2];   // per file
-  int32_t keep;
-  int64_t hap_a[2];     // per file
-  int32_t mate[2];      // per file
+  int32_t keep;         // bit 0: kept; bit 1: fo0 (file 0 holds mate fo0)
+  int32_t seq_len[2];   // per mate
+  int32_t win[2];       // per mate: offset of the first read base inside the LDS window buffer
 };
 
 __device__ __forceinline__ uint8_t comp(uint8_t c) {
@@ -295,26 +313,29 @@ __device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, in
   q = (uint8_t)(bq + 33);
 }
 
+// LDS: meta[EW_T] | windows[EW_T][2][win_stride] | image 0 [cap+16] | image 1 [cap+16]
 __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m, const int64_t *pos0,
                                                            const int64_t *pos1, const int8_t *fo0, int64_t rlen,
                                                            QFixed q, const Rec *recs, const E3 *off, char *out1,
-                                                           char *out2, int write2, int32_t cap, CorruptCfg cc,
-                                                           int32_t *err) {
+                                                           char *out2, int write2, int32_t cap, int32_t win_stride,
+                                                           CorruptCfg cc, int32_t *err) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  TplMeta *meta = (TplMeta *)smem;                                        // EW_T entries
+  TplMeta *meta = (TplMeta *)smem;
+  uint8_t *wins = (uint8_t *)smem + ((sizeof(TplMeta) * EW_T + 15) / 16) * 16;
   char *img[2];
-  img[0] = smem + ((sizeof(TplMeta) * EW_T + 15) / 16) * 16;
+  img[0] = (char *)wins + (size_t)EW_T * 2 * win_stride;
   img[1] = img[0] + cap + 16;
   __shared__ int64_t s_sb_end;
 
   const int64_t t0 = (int64_t)blockIdx.x * EW_T;
   const int64_t t1 = t0 + EW_T < m ? t0 + EW_T : m;
   const int nfile = write2 ? 2 : 1;
-  char *outs[2] = {out1, out2};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunks = win_stride / 16;      // 16-byte gathers per mate window
 
   int64_t sb = t0;
   while (sb < t1) {
-    // ---- sub-batch [sb, sb_end): the largest prefix whose two images fit `cap` bytes ----------------------
+    // ---- sub-batch [sb, sb_end): the largest prefix whose images fit `cap` bytes (normally the whole tile) --
     {
       int64_t t = sb + 1 + threadIdx.x;
       int fits = 0;
@@ -331,93 +352,108 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
       if (threadIdx.x == 0) atomicOr(err, 1);
       return;
     }
+    const int nb = (int)(sb_end - sb);
     const E3 base = off[sb];
     const int64_t g0[2] = {base.b1, base.b2};
     const int al[2] = {(int)(g0[0] & 15), (int)(g0[1] & 15)};
 
-    // ---- phase A: owner threads format qnames and record metadata ------------------------------------------
-    if (threadIdx.x < sb_end - sb) {
+    // ---- B0: gather both mates' haplotype windows of every template into LDS (all loads in flight) --------
+    for (int it = threadIdx.x; it < nb * 2 * chunks; it += EW_THREADS) {
+      const int j = it / (2 * chunks), rem = it - j * 2 * chunks, s = rem / chunks, c = rem - s * chunks;
+      const int64_t t = sb + j;
+      const int64_t p = s ? pos1[t] : pos0[t];
+      int64_t a = p - h.p_min;
+      if (a > h.hap_len) a = h.hap_len;
+      const int64_t a16 = a & ~(int64_t)15;
+      if (a16 + 16 * c < a + rlen && recs[t].keep) {
+        uint4 v = *(const uint4 *)(h.hap + a16 + 16 * c);
+        *(uint4 *)(wins + (size_t)(j * 2 + s) * win_stride + 16 * c) = v;
+      }
+    }
+
+    // ---- A: owner threads format the qname into image 0 and record metadata ------------------------------
+    if (threadIdx.x < nb) {
       const int64_t t = sb + threadIdx.x;
       TplMeta &mt = meta[threadIdx.x];
-      Rec rc = recs[t];
+      const Rec rc = recs[t];
       mt.keep = rc.keep;
       if (rc.keep) {
         ReadInfo r[2];
         const int64_t p[2] = {pos0[t], pos1[t]};
-        read_info(h, p[0], rlen, r[0]);
-        read_info(h, p[1], rlen, r[1]);
+        for (int s = 0; s < 2; s++) {
+          r[s].n0 = rc.n0[s];
+          r[s].n1 = rc.n1[s];
+          read_place(h, p[s], rlen, r[s]);
+          mt.seq_len[s] = r[s].seq_len;
+          mt.win[s] = (threadIdx.x * 2 + s) * win_stride + (int)(r[s].hap_a & 15);
+        }
         const E3 o = off[t];
-        const int64_t cnt = o.kept + 1;
         const int f0 = fo0[t];
-        int32_t qlen = 0;
-        for (int f = 0; f < nfile; f++) {
-          const int64_t go = f == 0 ? o.b1 : o.b2;
-          const int loc = (int)(go - g0[f]) + al[f];
-          char *d = img[f] + loc;
-          char *d0 = d;
-          d = put_str(d, q.prefix, q.prefix_len);
-          d = put_s(d, cnt);
-          d = put_str(d, q.mid, q.mid_len);
-          for (int fr = 0; fr < 2; fr++) {            // reads in file order
-            const int s = fr == f0 ? 0 : 1;           // reads[fo] = mate s, fo0 for mate 0
-            *d++ = '|'; *d++ = (char)('0' + s);
-            *d++ = '|'; d = put_s(d, r[s].pos);
-            *d++ = '|'; d = put_s(d, rlen);
-            *d++ = '|'; d = write_cigar(d, h, p[s], rlen, r[s]);
-            *d++ = '|'; d = write_vlist(d, h, r[s]);
-          }
-          qlen = (int32_t)(d - d0);
-          const int s = f == f0 ? 0 : 1;
-          mt.loc[f] = loc;
-          mt.mate[f] = s;
-          mt.seq_len[f] = r[s].seq_len;
-          mt.hap_a[f] = r[s].hap_a;
+        mt.loc[0] = (int)(o.b1 - g0[0]) + al[0];
+        mt.loc[1] = (int)(o.b2 - g0[1]) + al[1];
+        char *d = img[0] + mt.loc[0];
+        char *d0 = d;
+        d = put_str(d, q.prefix, q.prefix_len);
+        d = put_s(d, o.kept + 1);
+        d = put_str(d, q.mid, q.mid_len);
+        for (int fr = 0; fr < 2; fr++) {              // reads in file order: reads[fo] = mate s
+          const int s = fr == f0 ? 0 : 1;
+          *d++ = '|'; *d++ = (char)('0' + s);
+          *d++ = '|'; d = put_s(d, r[s].pos);
+          *d++ = '|'; d = put_s(d, rlen);
+          *d++ = '|'; d = write_cigar(d, h, p[s], rlen, r[s]);
+          *d++ = '|'; d = write_vlist(d, h, r[s]);
         }
-        mt.qlen = qlen;
+        mt.qlen = (int32_t)(d - d0);
+        mt.keep = 1 | (f0 << 1);
       }
     }
     __syncthreads();
 
-    // ---- phase B: bases, separators and qualities, all threads -------------------------------------------
-    for (int64_t t = sb; t < sb_end; t++) {
-      const TplMeta &mt = meta[t - sb];
-      if (!mt.keep) continue;
-      for (int f = 0; f < nfile; f++) {
-        const int S = mt.seq_len[f];
-        const int Q = cc.enable ? S : (int)rlen;       // corrupt_single_read emits len(seq) qualities
-        char *d = img[f] + mt.loc[f] + mt.qlen;         // '\n' seq '\n+\n' qual '\n'
-        const uint8_t *src = h.hap + mt.hap_a[f];
-        const bool rc = mt.mate[f] == 1;
-        for (int n = threadIdx.x; n < S; n += EW_THREADS) {
-          uint8_t b = rc ? comp(src[S - 1 - n]) : src[n];
-          if (cc.enable) {
-            uint8_t qq;
-            corrupt_base(cc, t, f, n, b, qq);
-            d[4 + S + n] = (char)qq;
-          }
-          d[1 + n] = (char)b;
+    // ---- B1: one wave per (template, file): qname copy (file 2), bases, separators, qualities -------------
+    for (int pair = wave; pair < nb * nfile; pair += EW_WAVES) {
+      const int j = pair / nfile, f = pair - j * nfile;
+      const TplMeta &mt = meta[j];
+      if (!(mt.keep & 1)) continue;
+      const int f0 = mt.keep >> 1;
+      const int s = f == f0 ? 0 : 1;                  // mate held by file f
+      const int S = mt.seq_len[s];
+      const int Q = cc.enable ? S : (int)rlen;        // corrupt_single_read emits len(seq) qualities
+      char *d0 = img[f] + mt.loc[f];
+      if (f == 1)
+        for (int i = lane; i < mt.qlen; i += 64) d0[i] = img[0][mt.loc[0] + i];
+      char *d = d0 + mt.qlen;                         // '\n' seq '\n+\n' qual '\n'
+      const uint8_t *w = wins + mt.win[s];
+      const int64_t t = sb + j;
+      for (int n = lane; n < S; n += 64) {
+        uint8_t b = s ? comp(w[S - 1 - n]) : w[n];
+        if (cc.enable) {
+          uint8_t qq;
+          corrupt_base(cc, t, f, n, b, qq);
+          d[4 + S + n] = (char)qq;
         }
-        if (!cc.enable)
-          for (int n = threadIdx.x; n < Q; n += EW_THREADS) d[4 + S + n] = '~';
-        if (threadIdx.x == 0) {
-          d[0] = '\n';
-          d[1 + S] = '\n';
-          d[2 + S] = '+';
-          d[3 + S] = '\n';
-          d[4 + S + Q] = '\n';
-        }
+        d[1 + n] = (char)b;
+      }
+      if (!cc.enable)
+        for (int n = lane; n < Q; n += 64) d[4 + S + n] = '~';
+      if (lane == 0) {
+        d[0] = '\n';
+        d[1 + S] = '\n';
+        d[2 + S] = '+';
+        d[3 + S] = '\n';
+        d[4 + S + Q] = '\n';
       }
     }
     __syncthreads();
 
-    // ---- phase C: images -> file arenas (16-byte aligned stores; byte stores at the ragged edges) ---------
+    // ---- C: images -> file arenas (16-byte aligned stores; byte stores at the ragged edges) --------------
     {
       const E3 endo = off[sb_end];
       const int64_t g1[2] = {endo.b1, endo.b2};
       for (int f = 0; f < nfile; f++) {
         const int64_t G0 = g0[f], G1 = g1[f];
         if (G1 <= G0) continue;
-        char *out = outs[f];
+        char *out = f ? out2 : out1;
         const char *im = img[f] + al[f];   // im[g - G0] is global byte g
         int64_t A0 = (G0 + 15) & ~(int64_t)15, A1 = G1 & ~(int64_t)15;
         if (A0 > G1) A0 = G1;
@@ -530,13 +566,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   MH_TRY(ensure_keep(ctx, ctx->out1, need1 + 64, ctx->used1));
   if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, need2 + 64, ctx->used2));
 
-  int32_t cap = 24 * 1024;
+  int32_t cap = 16 * 1024;
   while (cap < hmax) cap *= 2;
-  if (cap > 72 * 1024) {
+  if (cap > 64 * 1024) {
     stage_end(ctx);
-    return arg_fail(ctx, MH_E_CAPACITY, "a FASTQ record exceeds 72 KiB");
+    return arg_fail(ctx, MH_E_CAPACITY, "a FASTQ record exceeds 64 KiB");
   }
-  size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + 2 * (size_t)(cap + 16);
+  const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
+  size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + (size_t)EW_T * 2 * win_stride + 2 * (size_t)(cap + 16);
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on) {
     if (rlen > ctx->corrupt_max_bp) {
@@ -547,12 +584,16 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
                     ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
                     (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u};
   }
+  if (lds > 160 * 1024) {
+    stage_end(ctx);
+    return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
+  }
   const int64_t nblk = (m + EW_T - 1) / EW_T;
   stage_begin(ctx, "emit_write");
   hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
                      (const int64_t *)ctx->t_pos0.p, (const int64_t *)ctx->t_pos1.p, (const int8_t *)ctx->t_fo0.p,
                      rlen, q, (const Rec *)recs, (const E3 *)off, (char *)ctx->out1.p + ctx->used1,
-                     write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr, write_fastq2, cap, cc, err);
+                     write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr, write_fastq2, cap, win_stride, cc, err);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   int32_t herr = 0;
@@ -631,7 +672,6 @@ int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l
     cigar_off[n] = acc[0];
     vlist_off[n] = acc[1];
     seq_off[n] = acc[2];
-    // offsets relative to three device text regions
     int64_t tot = acc[0] + acc[1] + acc[2] + 3;
     if (hipMalloc(&dtxt, tot) != hipSuccess) {
       rc = arg_fail(ctx, MH_E_OOM, "read_batch text");

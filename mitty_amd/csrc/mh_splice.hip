@@ -315,7 +315,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
                                             : "SNP/INS alt length inconsistent with its op");
   }
   int64_t p_min = ps0;
-  MH_TRY(ensure(ctx, h.hap, hap_len > 0 ? hap_len : 1));
+  MH_TRY(ensure(ctx, h.hap, hap_len + 1024));   // emission gathers whole 16-byte chunks past the last base
   if (pieces > 0) {
     stage_begin(ctx, "splice_hap_copy");
     int64_t threads = pieces * 64;

@@ -253,7 +253,7 @@ def test_chr1_scale_properties(native):
   try:
     eng.load_region(0, ('1', 0, L), seq)
     n, kept, b1, b2 = eng.run_unit(0, 0, 1, 12345, copies[1], p, 150, mdl['cum_tlen'], 'SYN')
-    assert n > 7_000_000 and kept > 0.8 * n
+    assert n > 6_000_000 and kept > 0.9 * n   # n = templates kept by te < p_max (draws ~7.48 M)
     slot, n_nodes, p_min, p_max = eng.haplotype(0, 1, copies[1])
     ps, pr, op, ol, hap = eng.ctx.get_nodes(slot, n_nodes)
     # sample a slice of records from the arena
