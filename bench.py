@@ -83,14 +83,10 @@ def main():
   def step():
     eng.drop_haplotypes()
     eng.ctx.reset_output()
-    kept = b1 = b2 = 0
-    for ps, (ri, cpy, s) in enumerate(units):
-      _, k, x1, x2 = eng.run_unit(ps, ri, cpy, s, copies[cpy], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
-      kept += k
-      b1 += x1
-      b2 += x2
+    res = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p, rlen,
+                        model['cum_tlen'], 'SYN', 0, True, a.rng)
     eng.ctx.sync()
-    return kept, b1, b2
+    return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
 
   def barrier():
     if dist is not None:

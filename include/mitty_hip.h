@@ -10,6 +10,7 @@
  *   mh_build_haplotype    rpc.create_node_list (+ rpc.Node)              mitty/simulation/rpc.py:5-116
  *                         fed by vcfio.split_copies/parse per copy       mitty/lib/vcfio.py:67-126
  *   mh_sample_templates   illumina.generate_reads                        mitty/simulation/illumina.py:43-110
+ *   mh_sample_units       (the same for many units: the worker pool of readgenerate.py:102-115)
  *   mh_set_templates      (the template arrays a read module returns)   mitty/simulation/illumina.py:238-269
  *   mh_get_templates      (same arrays back to the host)
  *   mh_emit_reads         read_generating_worker loop + fastq_lines      mitty/simulation/readgenerate.py:184-230
@@ -89,6 +90,15 @@ int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, c
 int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen,
                                  const double *cum_tlen, int32_t n_tlen, uint64_t seed, int32_t rng_mode,
                                  int64_t *out_n_templates);
+/* Batched form: sample `n_units` work units at once (all their MT19937 streams are generated in parallel
+ * jump-ahead segments).  Unit k uses haplotype slots[k] and seed seeds[k]; its templates are kept as template set
+ * tpl_ids[k] (>= 0) until released.  out_n[k] = templates kept for unit k. */
+int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                        const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                        int32_t rng_mode, int64_t *out_n);
+/* Make template set `tpl_id` the current one (used by mh_emit_reads / mh_get_templates). */
+int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id);
+int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id);
 int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, const int64_t *pos1, int64_t n,
                          int32_t rlen);
 int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1, int64_t cap, int64_t *n);
@@ -130,6 +140,13 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
  * measured with HIP events on the context's stream (milliseconds); names are static strings. */
 int32_t mh_stage_times(mh_ctx *ctx, const char **names, double *ms, int32_t cap, int32_t *n);
 int32_t mh_enable_timing(mh_ctx *ctx, int32_t on);
+
+/* ---- diagnostics --------------------------------------------------------------------------------------- */
+/* Host computation of the MT19937 window (x_J .. x_{J+623}, untempered) of the stream seeded with `seed`, via the
+ * jump polynomial x^J mod P — the same math the device segments use (tests compare it with the plain recurrence). */
+int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624);
+/* Units the context redid on the exact sequential fallback path (decode out of words / near-integer quotient). */
+int32_t mh_fixup_count(mh_ctx *ctx, int64_t *n);
 
 #ifdef __cplusplus
 }

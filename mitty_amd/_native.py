@@ -18,7 +18,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
-           'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing']
+           'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
+           'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count']
 
 
 class NativeError(RuntimeError):
@@ -77,8 +78,22 @@ def lib():
   _sig(L, 'mh_stage_times', [c_vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_dbl), c_i32,
                              ctypes.POINTER(c_i32)])
   _sig(L, 'mh_enable_timing', [c_vp, c_i32])
+  _sig(L, 'mh_sample_units', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32, c_vp])
+  _sig(L, 'mh_use_templates', [c_vp, c_i32])
+  _sig(L, 'mh_release_templates', [c_vp, c_i32])
+  _sig(L, 'mh_mt_window_at', [ctypes.c_uint32, c_u64, c_vp])
+  _sig(L, 'mh_fixup_count', [c_vp, P_i64])
   _lib = L
   return L
+
+
+def mt_window_at(seed, offset):
+  """Host jump-ahead: untempered MT19937 window (x_J .. x_{J+623}) of the stream seeded with `seed`."""
+  out = np.empty(624, np.uint32)
+  rc = lib().mh_mt_window_at(int(seed), int(offset), _ptr(out))
+  if rc:
+    _raise(rc, 'mh_mt_window_at failed')
+  return out
 
 
 def device_count():
@@ -195,6 +210,28 @@ class Context:
     n = c_i64()
     self._chk(self._L.mh_sample_templates_span(self._h, int(p_min), int(p_max), float(p), int(rlen), _ptr(ct),
                                                len(ct), int(seed), int(rng_mode), ctypes.byref(n)))
+    return n.value
+
+  def sample_units(self, tpl_ids, slots, seeds, p, rlen, cum_tlen, rng_mode=MH_RNG_MITTY):
+    """Batched sampling; returns templates kept per unit."""
+    ids = np.ascontiguousarray(tpl_ids, dtype=np.int32)
+    sl = np.ascontiguousarray(slots, dtype=np.int32)
+    sd = np.ascontiguousarray(seeds, dtype=np.uint64)
+    ct = np.ascontiguousarray(cum_tlen, dtype=np.float64)
+    out = np.zeros(max(len(ids), 1), dtype=np.int64)
+    self._chk(self._L.mh_sample_units(self._h, len(ids), _ptr(ids), _ptr(sl), _ptr(sd), float(p), int(rlen),
+                                      _ptr(ct), len(ct), int(rng_mode), _ptr(out)))
+    return out[:len(ids)]
+
+  def use_templates(self, tpl_id):
+    self._chk(self._L.mh_use_templates(self._h, int(tpl_id)))
+
+  def release_templates(self, tpl_id):
+    self._chk(self._L.mh_release_templates(self._h, int(tpl_id)))
+
+  def fixup_count(self):
+    n = c_i64()
+    self._chk(self._L.mh_fixup_count(self._h, ctypes.byref(n)))
     return n.value
 
   def set_templates(self, fo0, pos0, pos1, rlen):

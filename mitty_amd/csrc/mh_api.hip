@@ -5,6 +5,9 @@
 #include "mh_internal.h"
 
 namespace mh {
+namespace jump {
+void window_at(uint32_t seed, uint64_t J, uint32_t *out624);
+}
 
 int32_t hip_fail(mh_ctx *ctx, hipError_t e, const char *what, const char *file, int line) {
   if (ctx) {
@@ -142,7 +145,10 @@ int32_t mh_destroy(mh_ctx *ctx) {
     release(h.hap); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
     release(h.nrun_s); release(h.nrun_e);
   }
-  release(ctx->t_fo0); release(ctx->t_pos0); release(ctx->t_pos1);
+  for (auto &kv : ctx->tsets) {
+    release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1);
+  }
+  release(ctx->jump_polys);
   for (auto &b : ctx->s) release(b);
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
@@ -275,7 +281,11 @@ int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, c
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0)) return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  return sample_templates(ctx, it->second.p_min, it->second.p_max, p, rlen, cum_tlen, n_tlen, seed, rng_mode, out_n);
+  const int32_t id = -1;
+  MH_TRY(sample_units(ctx, 1, &id, &it->second.p_min, &it->second.p_max, &seed, p, rlen, cum_tlen, n_tlen, rng_mode,
+                      out_n));
+  ctx->cur_tpl = id;
+  return MH_OK;
 }
 
 int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen,
@@ -284,7 +294,50 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
   CTX_GUARD(ctx);
   if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0) || p_max < p_min)
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  return sample_templates(ctx, p_min, p_max, p, rlen, cum_tlen, n_tlen, seed, rng_mode, out_n);
+  const int32_t id = -1;
+  MH_TRY(sample_units(ctx, 1, &id, &p_min, &p_max, &seed, p, rlen, cum_tlen, n_tlen, rng_mode, out_n));
+  ctx->cur_tpl = id;
+  return MH_OK;
+}
+
+int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                        const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                        int32_t rng_mode, int64_t *out_n) {
+  CTX_GUARD(ctx);
+  if (n_units < 0 || (n_units > 0 && (!tpl_ids || !slots || !seeds)) || !cum_tlen || rlen <= 0 ||
+      !(p > 0.0 && p <= 1.0))
+    return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  std::vector<int64_t> pmin(n_units), pmax(n_units);
+  for (int32_t u = 0; u < n_units; u++) {
+    if (tpl_ids[u] < 0) return arg_fail(ctx, MH_E_ARG, "template set ids must be >= 0");
+    for (int32_t v = 0; v < u; v++)
+      if (tpl_ids[v] == tpl_ids[u]) return arg_fail(ctx, MH_E_ARG, "duplicate template set id");
+    auto it = ctx->haps.find(slots[u]);
+    if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+    pmin[u] = it->second.p_min;
+    pmax[u] = it->second.p_max;
+  }
+  return sample_units(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen, rng_mode,
+                      out_n);
+}
+
+int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id) {
+  if (!ctx) return MH_E_ARG;
+  auto it = ctx->tsets.find(tpl_id);
+  if (it == ctx->tsets.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  ctx->cur_tpl = tpl_id;
+  return MH_OK;
+}
+
+int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id) {
+  CTX_GUARD(ctx);
+  auto it = ctx->tsets.find(tpl_id);
+  if (it == ctx->tsets.end()) return MH_OK;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  release(it->second.fo0); release(it->second.pos0); release(it->second.pos1);
+  ctx->tsets.erase(it);
+  if (ctx->cur_tpl == tpl_id) ctx->cur_tpl = -1;
+  return MH_OK;
 }
 
 int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, const int64_t *pos1, int64_t n,
@@ -293,31 +346,35 @@ int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, co
   if (n < 0 || rlen <= 0 || (n > 0 && (!fo0 || !pos0 || !pos1))) return arg_fail(ctx, MH_E_ARG, "bad templates");
   for (int64_t i = 0; i < n; i++)
     if (fo0[i] != 0 && fo0[i] != 1) return arg_fail(ctx, MH_E_ARG, "file_order must be 0/1");
-  MH_TRY(ensure(ctx, ctx->t_fo0, n + 1));
-  MH_TRY(ensure(ctx, ctx->t_pos0, 8 * (n + 1)));
-  MH_TRY(ensure(ctx, ctx->t_pos1, 8 * (n + 1)));
+  TplSet &ts = ctx->tsets[-1];
+  MH_TRY(ensure(ctx, ts.fo0, n + 1));
+  MH_TRY(ensure(ctx, ts.pos0, 8 * (n + 1)));
+  MH_TRY(ensure(ctx, ts.pos1, 8 * (n + 1)));
   if (n) {
-    HIPCHK(ctx, hipMemcpyAsync(ctx->t_fo0.p, fo0, n, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->t_pos0.p, pos0, 8 * n, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->t_pos1.p, pos1, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ts.fo0.p, fo0, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ts.pos0.p, pos0, 8 * n, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ts.pos1.p, pos1, 8 * n, hipMemcpyHostToDevice, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  ctx->n_tpl = n;
-  ctx->rlen = rlen;
-  ctx->have_tpl = true;
+  ts.n = n;
+  ts.rlen = rlen;
+  ts.valid = true;
+  ctx->cur_tpl = -1;
   return MH_OK;
 }
 
 int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1, int64_t cap, int64_t *n) {
   CTX_GUARD(ctx);
-  if (!ctx->have_tpl) return arg_fail(ctx, MH_E_STATE, "no templates");
-  if (n) *n = ctx->n_tpl;
-  if (cap < ctx->n_tpl) return arg_fail(ctx, MH_E_CAPACITY, "template buffers too small");
-  size_t m = (size_t)ctx->n_tpl;
+  auto it = ctx->tsets.find(ctx->cur_tpl);
+  if (it == ctx->tsets.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "no templates");
+  const TplSet &ts = it->second;
+  if (n) *n = ts.n;
+  if (cap < ts.n) return arg_fail(ctx, MH_E_CAPACITY, "template buffers too small");
+  size_t m = (size_t)ts.n;
   if (m) {
-    if (fo0) HIPCHK(ctx, hipMemcpyAsync(fo0, ctx->t_fo0.p, m, hipMemcpyDeviceToHost, ctx->stream));
-    if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ctx->t_pos0.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
-    if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ctx->t_pos1.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (fo0) HIPCHK(ctx, hipMemcpyAsync(fo0, ts.fo0.p, m, hipMemcpyDeviceToHost, ctx->stream));
+    if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ts.pos0.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ts.pos1.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
@@ -389,6 +446,22 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   ctx->corrupt_max_bp = max_bp;
   ctx->corrupt_n_bq = n_bq;
   ctx->corrupt_seed = seed;
+  return MH_OK;
+}
+
+int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624) {
+  if (!out624) return MH_E_ARG;
+  try {
+    mh::jump::window_at(seed, offset, out624);
+  } catch (...) {
+    return MH_E_ARG;
+  }
+  return MH_OK;
+}
+
+int32_t mh_fixup_count(mh_ctx *ctx, int64_t *n) {
+  if (!ctx || !n) return MH_E_ARG;
+  *n = ctx->fixups;
   return MH_OK;
 }
 

@@ -514,10 +514,13 @@ HapView view_of(const Hap &h) {
 
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  if (!ctx->have_tpl) return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates first");
+  auto tit = ctx->tsets.find(ctx->cur_tpl);
+  if (tit == ctx->tsets.end() || !tit->second.valid)
+    return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
+  const TplSet &tp = tit->second;
   hipStream_t st = ctx->stream;
-  const int64_t m = ctx->n_tpl;
-  const int64_t rlen = ctx->rlen;
+  const int64_t m = tp.n;
+  const int64_t rlen = tp.rlen;
   std::string prefix = std::string("@") + serial_stub + ":";
   std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
   if (prefix.size() + mid.size() > 4000) return arg_fail(ctx, MH_E_ARG, "sample/chrom names too long");
@@ -547,7 +550,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
 
   stage_begin(ctx, "emit_measure");
   hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m,
-                     (const int64_t *)ctx->t_pos0.p, (const int64_t *)ctx->t_pos1.p, (const int8_t *)ctx->t_fo0.p,
+                     (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p,
                      rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
@@ -591,7 +594,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   const int64_t nblk = (m + EW_T - 1) / EW_T;
   stage_begin(ctx, "emit_write");
   hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
-                     (const int64_t *)ctx->t_pos0.p, (const int64_t *)ctx->t_pos1.p, (const int8_t *)ctx->t_fo0.p,
+                     (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p,
                      rlen, q, (const Rec *)recs, (const E3 *)off, (char *)ctx->out1.p + ctx->used1,
                      write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr, write_fastq2, cap, win_stride, cc, err);
   HIPCHK(ctx, hipGetLastError());

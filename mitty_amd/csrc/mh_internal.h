@@ -40,6 +40,14 @@ struct Hap {
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
 };
 
+// One work unit's templates (illumina.generate_reads output), device-resident.
+struct TplSet {
+  DevBuf fo0, pos0, pos1;
+  int64_t n = 0;
+  int32_t rlen = 0;
+  bool valid = false;
+};
+
 struct Contig {
   DevBuf seq;
   int64_t len = 0;
@@ -61,11 +69,14 @@ struct mh_ctx {
   std::map<int32_t, mh::Contig> contigs;
   std::map<int32_t, mh::Hap> haps;
 
-  // current template set (illumina.generate_reads output, device-resident)
-  mh::DevBuf t_fo0, t_pos0, t_pos1;
-  int64_t n_tpl = 0;
-  int32_t rlen = 0;
-  bool have_tpl = false;
+  // template sets by id; `cur_tpl` is the one mh_emit_reads / mh_get_templates use
+  std::map<int32_t, mh::TplSet> tsets;
+  int32_t cur_tpl = -1;
+
+  // MT19937 jump polynomials on the device (x^(k * SEG_WORDS) mod P, k < jump_k)
+  mh::DevBuf jump_polys;
+  int64_t jump_k = 0;
+  int64_t fixups = 0;   // units redone on the exact fallback path
 
   // scratch (grow-only), reused by all stages
   mh::DevBuf s[16];
@@ -125,8 +136,9 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos
                      const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
                      const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var);
 
-int32_t sample_templates(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen, const double *cum_tlen,
-                         int32_t n_tlen, uint64_t seed, int32_t rng_mode, int64_t *out_n);
+int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
+                     const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                     int32_t rng_mode, int64_t *out_n);
 
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);

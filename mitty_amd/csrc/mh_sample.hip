@@ -1,21 +1,24 @@
 // mh_sample.hip — template sampling on the device (reference illumina.generate_reads, illumina.py:43-110).
 //
-// Parity mode (MH_RNG_MITTY) reproduces numpy's legacy RandomState streams word for word:
-//   seed -> RS(seed).randint(SEED_MAX, 4) = (tloc, tlen, shuffle, file_order) seeds        (host, 4 words)
-//   k_mt_streams     one 256-thread workgroup per MT19937 stream; the 624-word state lives in LDS and is
-//                    advanced in the three dependency phases of the twist ([0,227) [227,454) [454,624)),
-//                    tempered words streamed to HBM (tloc: 2n words, tlen: 2n words, file order: n/4 words)
-//   scan(geometric)  ts = cumsum(ceil(log1p(-U)/log(1-p))) + p_min + 1, the geometric draw computed inside the
-//                    scan's Load; a draw whose quotient lies within 1e-9 of an integer is flagged and recomputed
-//                    with the host libm (the reference's libm) before the scan is redone
-//   k_shuffle_decode Fisher-Yates swap indices j_i = random_interval(i), i = n-1..1: one workgroup per stream
-//                    fuses MT19937 with a block-parallel rejection decode (fixed-point on the accept prefix,
-//                    exact; sequential fallback for the rare non-converging chunk)
-//   k_perm_*         the permutation those swaps produce, without replaying them: bucket the steps by target j,
-//                    then for each output slot p chase  q = j_p -> next step with the same target -> ...
-//                    (see perm_chase below); ts_shuf[p] = ts[q]
-//   k_tlen + scan    tl = searchsorted(cum_tlen (LDS), U) clipped to rlen; keep te < p_max; compaction
-//   k_file_order     fo0[k] = byte (k & 3) of word k >> 2, & 1  (randint(2, dtype=int8) buffering)
+// Parity mode (MH_RNG_MITTY) reproduces numpy's legacy RandomState streams word for word.
+// Per work unit:  seed -> RS(seed).randint(SEED_MAX, 4) = (tloc, tlen, shuffle, file_order) stream seeds (host).
+//   k_mt_segments     every MT19937 stream of every unit in the batch is cut into segments of SEG_WORDS outputs;
+//                     one 256-thread workgroup per segment jumps to the segment start (W_J = XOR_{g_k=1} W_k with
+//                     g = x^J mod P from mh_jump.cpp, the stream's first 20.6k words built in LDS) and then twists
+//                     its segment (three dependency phases of 227/227/170 words) — no sequential chain over a
+//                     stream, all segments of all units run at once
+//   k_shuffle_decode2 Fisher-Yates swap indices j_i = random_interval(i), i = n-1..1, one 1024-thread workgroup
+//                     per unit, 4096 words per step: each thread decides its 4 words given the accepted count
+//                     before it, the block fixes that count by iterating scan -> decide to its (unique) fixed
+//                     point (2 rounds while i >> 4096; bounded, with an exact sequential fallback)
+//   scan(geometric)   ts = cumsum(ceil(log1p(-U)/log(1-p))) + p_min + 1 (numpy legacy inversion, pinned against
+//                     numpy), computed inside the scan's Load; quotients within 1e-12 of an integer are flagged
+//                     and the unit is redone with those draws recomputed by the host libm
+//   k_perm_*          the permutation the swaps produce, without replaying them (see k_perm_gather)
+//   k_tlen + scan     tl = searchsorted(cum_tlen (LDS), U) clipped to rlen; keep te < p_max; compaction
+//   k_file_order      fo0[k] = byte (k & 3) of word k >> 2, & 1 (randint(2, dtype=int8) buffering)
+// The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
+// fallback for a unit whose decode ran out of pre-generated words.
 #include <cmath>
 
 #include "mh_internal.h"
@@ -23,9 +26,15 @@
 
 namespace mh {
 
+namespace jump {
+void jump_poly_words(uint64_t L, int64_t k, uint32_t *out624);
+}
+
 namespace {
 
 constexpr uint32_t MT_UP = 0x80000000u, MT_LO = 0x7fffffffu, MT_A = 0x9908b0dfu;
+constexpr int64_t SEG_WORDS = 624 * 320;     // outputs per segment
+constexpr int EXT_WORDS = 624 * 33;          // x_0 .. x_20591 >= 19936 + 623
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
@@ -79,40 +88,173 @@ __device__ __forceinline__ void mt_twist_block(const uint32_t *o, uint32_t *nw, 
   __syncthreads();
 }
 
-struct MTJob {
-  uint32_t *out;
-  int64_t count;
+// ---- jump-ahead segments ---------------------------------------------------------------------------------------
+struct SegJob {
+  uint32_t *out;      // the stream's output array
+  int64_t start;      // first output index of this segment
+  int64_t count;      // outputs to produce
   uint32_t seed;
-};
-struct MTJobs {
-  MTJob j[8];
+  int32_t k;          // segment index: start = k * SEG_WORDS, jump polynomial polys[k]
 };
 
-__global__ void __launch_bounds__(256) k_mt_streams(MTJobs jobs) {
-  __shared__ uint32_t st[2][624];
-  const MTJob job = jobs.j[blockIdx.x];
-  mt_seed_lds(st[0], job.seed);
-  int cur = 0;
-  for (int64_t base = 0; base < job.count; base += 624) {
-    uint32_t *out = job.out;
-    int64_t cnt = job.count;
-    mt_twist_block(st[cur], st[cur ^ 1], [&](int k, uint32_t w) {
+__global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys) {
+  __shared__ uint32_t x[EXT_WORDS];
+  const SegJob job = jobs[blockIdx.x];
+  const int t = threadIdx.x;
+  mt_seed_lds(x, job.seed);
+  if (job.k > 0) {
+    // x_624 .. x_20591 in place: x[i] = x[i-227] ^ mix(x[i-624], x[i-623])
+    for (int b = 624; b < EXT_WORDS; b += 624) {
+      if (t < 227) { int i = b + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
+      __syncthreads();
+      if (t < 227) { int i = b + 227 + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
+      __syncthreads();
+      if (t < 170) { int i = b + 454 + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
+      __syncthreads();
+    }
+    // W_J[w] = XOR over set bits k of g of x[k + w]
+    const uint32_t *g = polys + (int64_t)job.k * 624;
+    const int w0 = t, w1 = t + 256, w2 = t + 512;
+    const bool h2 = w2 < 624;
+    uint32_t a0 = 0, a1 = 0, a2 = 0;
+    for (int pw = 0; pw < 624; pw++) {
+      uint32_t m = g[pw];
+      const int kb = pw * 32;
+      while (m) {
+        const int k = kb + __builtin_ctz(m);
+        m &= m - 1;
+        a0 ^= x[k + w0];
+        a1 ^= x[k + w1];
+        if (h2) a2 ^= x[k + w2];
+      }
+    }
+    __syncthreads();
+    x[w0] = a0;
+    x[w1] = a1;
+    if (h2) x[w2] = a2;
+    __syncthreads();
+  }
+  uint32_t *st0 = x, *st1 = x + 624;
+  uint32_t *out = job.out + job.start;
+  const int64_t cnt = job.count;
+  for (int64_t base = 0; base < cnt; base += 624) {
+    mt_twist_block(st0, st1, [&](int k, uint32_t w) {
       if (base + k < cnt) out[base + k] = w;
     });
-    cur ^= 1;
+    uint32_t *tmp = st0; st0 = st1; st1 = tmp;
   }
 }
 
 // ---- Fisher-Yates swap indices -------------------------------------------------------------------------------
-constexpr int SD_THREADS = 640;   // 10 waves: one tempered word per thread per twist
-constexpr int SD_WAVES = SD_THREADS / 64;
-
 __device__ __forceinline__ uint32_t interval_mask(uint32_t m) {
   m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
   return m;
 }
 
-// j[i] = random_interval(i) for i = n-1 .. 1 (j[0] = 0), MT19937 seeded with `seed`.
+struct DecJob {
+  const uint32_t *words;   // the unit's shuffle stream (tempered outputs)
+  int64_t n_words;
+  int64_t n;               // draws: i = n-1 .. 1
+  uint32_t *j;
+  int64_t *status;         // remaining i0 (0 = complete)
+};
+
+constexpr int DC_THREADS = 1024;
+constexpr int DC_WAVES = DC_THREADS / 64;
+constexpr int DC_PER = 4;
+constexpr int DC_CHUNK = DC_THREADS * DC_PER;
+
+__global__ void __launch_bounds__(DC_THREADS) k_shuffle_decode2(const DecJob *jobs) {
+  __shared__ int32_t wsum[DC_WAVES];
+  __shared__ int32_t s_tot;
+  const DecJob job = jobs[blockIdx.x];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0 && job.n > 0) job.j[0] = 0;
+  int64_t i0 = job.n - 1;
+  int64_t base = 0;
+  float ratio = 0.75f;
+  while (i0 >= 1 && base < job.n_words) {
+    uint32_t w[DC_PER];
+    bool valid[DC_PER];
+#pragma unroll
+    for (int e = 0; e < DC_PER; e++) {
+      const int64_t idx = base + DC_PER * t + e;
+      valid[e] = idx < job.n_words;
+      w[e] = valid[e] ? job.words[idx] : 0u;
+    }
+    int32_t A = (int32_t)(ratio * (float)(DC_PER * t));
+    int32_t cnt = 0;
+    uint32_t v[DC_PER];
+    bool acc[DC_PER];
+    bool converged = false;
+    for (int it = 0; it < 24; it++) {
+      cnt = 0;
+#pragma unroll
+      for (int e = 0; e < DC_PER; e++) {
+        const int64_t i = i0 - A - cnt;
+        v[e] = (i >= 1) ? (w[e] & interval_mask((uint32_t)i)) : 0u;
+        acc[e] = valid[e] && i >= 1 && v[e] <= (uint32_t)i;
+        cnt += acc[e];
+      }
+      // exclusive block scan of cnt
+      int32_t incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        int32_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      int32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int q = 0; q < DC_WAVES; q++) {
+        const int32_t s = wsum[q];
+        pre += q < wave ? s : 0;
+        tot += s;
+      }
+      const int32_t A2 = pre + incl - cnt;
+      const int same = __syncthreads_and(A2 == A);
+      A = A2;
+      if (t == 0) s_tot = tot;
+      if (same) {
+        converged = true;
+        break;
+      }
+    }
+    if (!converged) {
+      // exact sequential decode of this chunk (only when i0 is comparable to the chunk size)
+      __syncthreads();
+      if (t == 0) {
+        int64_t ii = i0;
+        for (int64_t k = 0; k < DC_CHUNK && base + k < job.n_words && ii >= 1; k++) {
+          const uint32_t vv = job.words[base + k] & interval_mask((uint32_t)ii);
+          if (vv <= (uint32_t)ii) { job.j[ii] = vv; ii--; }
+        }
+        s_tot = (int32_t)(i0 - ii);
+      }
+      __syncthreads();
+    } else {
+      int32_t a = 0;
+#pragma unroll
+      for (int e = 0; e < DC_PER; e++) {
+        if (acc[e]) job.j[i0 - A - a] = v[e];
+        a += acc[e];
+      }
+    }
+    __syncthreads();
+    const int32_t tot = s_tot;
+    i0 -= tot;
+    base += DC_CHUNK;
+    ratio = (float)tot / (float)DC_CHUNK;
+    __syncthreads();
+  }
+  if (t == 0) *job.status = i0 < 1 ? 0 : i0;
+}
+
+// Sequential-stream variant (exact fallback): MT19937 in LDS fused with the decode, one 640-thread workgroup.
+constexpr int SD_THREADS = 640;
+constexpr int SD_WAVES = SD_THREADS / 64;
+
 __global__ void __launch_bounds__(SD_THREADS) k_shuffle_decode(uint32_t seed, int64_t n, uint32_t *j) {
   __shared__ uint32_t st[2][624];
   __shared__ uint32_t words[624];
@@ -129,10 +271,9 @@ __global__ void __launch_bounds__(SD_THREADS) k_shuffle_decode(uint32_t seed, in
   while (i0 >= 1) {
     mt_twist_block(st[cur], st[cur ^ 1], [&](int k, uint32_t w) { words[k] = w; });
     cur ^= 1;
-    // decode the 624 words: lane t holds word t; A = accepted words before t in this twist
     const bool have = t < 624;
     const uint32_t w = have ? words[t] : 0u;
-    int32_t A = t;   // first guess: everything before accepted (decisions barely depend on A while i0 >> 624)
+    int32_t A = t;
     bool acc = false;
     uint32_t v = 0;
     bool converged = false;
@@ -150,7 +291,6 @@ __global__ void __launch_bounds__(SD_THREADS) k_shuffle_decode(uint32_t seed, in
       if (same) { converged = true; break; }
     }
     if (!converged) {
-      // exact sequential decode of this twist (rare: only when i0 is comparable to 624)
       if (t == 0) {
         int64_t ii = i0;
         for (int k = 0; k < 624 && ii >= 1; k++) {
@@ -250,7 +390,7 @@ __device__ __forceinline__ int64_t geometric_draw(double U, double p, double log
   }
   double qv = log1p(-U) / log_q;                      // numpy legacy_random_geometric_inversion
   double r = rint(qv);
-  if (fabs(qv - r) <= 1e-9 * fmax(1.0, fabs(qv))) {   // ceil() could differ from the host libm: flag
+  if (fabs(qv - r) <= 1e-12 * fmax(1.0, fabs(qv))) {  // ceil() could differ from the host libm: flag
     uint32_t s = atomicAdd(fl.count, 1u);
     if (s < fl.cap) fl.idx[s] = k;
   }
@@ -306,9 +446,9 @@ struct StoreCompact {
     pos1[excl] = te[k] - rlen;
   }
 };
-__global__ void k_file_order(int64_t m, const uint32_t *w, int8_t *fo0) {
+__global__ void k_file_order(int64_t n, const int64_t *m_ptr, const uint32_t *w, int8_t *fo0) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < m) fo0[k] = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 1u);
+  if (k < n && k < *m_ptr) fo0[k] = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 1u);
 }
 
 // ---- Philox4x32-10 fast mode ------------------------------------------------------------------------------
@@ -331,6 +471,27 @@ __global__ void k_philox_words(uint32_t *out, int64_t count, uint64_t key, uint3
   uint32_t v[4] = {r.x, r.y, r.z, r.w};
   for (int e = 0; e < 4; e++)
     if (q * 4 + e < count) out[q * 4 + e] = v[e];
+}
+
+// ---- host-side planning ---------------------------------------------------------------------------------------
+// Expected MT words consumed by the shuffle's n-1 random_interval draws, plus a wide margin.
+int64_t shuffle_words_alloc(int64_t n) {
+  if (n <= 1) return DC_CHUNK;
+  double E = 0.0;
+  // draws i in [a, b] share mask M (i in [2^(k-1), 2^k - 1], M = 2^k): sum M/(i+1) = M (H(b+1) - H(a))
+  auto H = [](double x) { return x < 20 ? 0.0 : std::log(x) + 0.5772156649015329 + 1.0 / (2 * x) - 1.0 / (12 * x * x); };
+  for (int64_t a = 1; a <= n - 1; a *= 2) {
+    int64_t b = std::min(2 * a - 1, n - 1);
+    double M = (double)(2 * a);
+    if (b < 64) {
+      for (int64_t i = a; i <= b; i++) E += M / (double)(i + 1);
+    } else {
+      E += M * (H((double)(b + 1)) - H((double)a));
+    }
+  }
+  double sd = 2.0 * std::sqrt((double)n);
+  int64_t w = (int64_t)(E + 12.0 * sd) + 2 * DC_CHUNK;
+  return ((w + DC_CHUNK - 1) / DC_CHUNK) * DC_CHUNK;
 }
 
 }  // namespace
@@ -380,128 +541,59 @@ uint64_t HostMT::interval(uint64_t max) {
   return v;
 }
 
-int32_t sample_templates(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen, const double *cum_tlen,
-                         int32_t n_tlen, uint64_t seed, int32_t rng_mode, int64_t *out_n) {
-  if (seed > 0xffffffffull)
-    return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seed) + " is out of range 0 - 4294967295");
-  if (n_tlen <= 0 || n_tlen > 8192) return arg_fail(ctx, MH_E_ARG, "cum_tlen must have 1..8192 entries");
-  if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
+namespace {
+
+struct UnitPlan {
+  int64_t p_min, p_max, n, n_fo_words, n_shuf_words;
+  uint32_t s_tloc, s_tlen, s_shuf, s_fo;
+  int64_t w_tloc, w_tlen, w_fo, w_shuf;   // word offsets in the batch word buffer
+  int64_t j_off;                          // offset in the batch j buffer
+  TplSet *out;
+};
+
+// Everything after the word streams for one unit: ts (geometric scan), shuffle, tlen + keep + compaction into
+// `out`, file order.  `exact`: materialise the draws and recompute flagged ones on the host (rare path).
+int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
+                    const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
+                    uint32_t *d_flag) {
   hipStream_t st = ctx->stream;
-  HostMT sr;
-  sr.seed((uint32_t)seed);
-  uint32_t s_tloc = (uint32_t)sr.interval(0xfffffffeull), s_tlen = (uint32_t)sr.interval(0xfffffffeull);
-  uint32_t s_shuf = (uint32_t)sr.interval(0xfffffffeull), s_fo = (uint32_t)sr.interval(0xfffffffeull);
-
-  int64_t n = (int64_t)((double)(p_max - p_min) * p * 1.2);   // int((p_max - p_min) * p * 1.2)
-  if (n < 0) n = 0;
-  if (n > ((int64_t)1 << 31) - 2) return arg_fail(ctx, MH_E_ARG, "region too large for one work unit (2^31 draws)");
-  const int64_t nn = n > 0 ? n : 1;
-  const int64_t n_fo_words = (n + 3) / 4 + 1;
-
-  stage_begin(ctx, "sample");
-  // scratch layout: 0 tloc words, 1 tlen words, 2 fo words, 3 j, 4 ts, 5 ts_shuf, 6 te, 7 keep, 8 cnt/fill,
-  //                 9 start, 10 entries, 11 geo flags, 12 g (rare path)
-  MH_TRY(ensure(ctx, ctx->s[0], 8 * nn));
-  MH_TRY(ensure(ctx, ctx->s[1], 8 * nn));
-  MH_TRY(ensure(ctx, ctx->s[2], 4 * n_fo_words));
-  MH_TRY(ensure(ctx, ctx->s[3], 4 * nn));
-  MH_TRY(ensure(ctx, ctx->s[4], 8 * nn));
-  MH_TRY(ensure(ctx, ctx->s[5], 8 * nn));
-  MH_TRY(ensure(ctx, ctx->s[6], 8 * nn));
-  MH_TRY(ensure(ctx, ctx->s[7], nn));
-  MH_TRY(ensure(ctx, ctx->s[8], 4 * (nn + 1)));
-  MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
-  MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
-  MH_TRY(ensure(ctx, ctx->s[11], 8 * 1024));
-  MH_TRY(ensure(ctx, ctx->s[13], 8 * 1024));
-  MH_TRY(ensure(ctx, ctx->d_small, 256));
-  MH_TRY(ensure(ctx, ctx->scan_partials, 16 * scan_partials_count(nn) + 64));
-  MH_TRY(ensure(ctx, ctx->t_pos0, 8 * nn));
-  MH_TRY(ensure(ctx, ctx->t_pos1, 8 * nn));
-  MH_TRY(ensure(ctx, ctx->t_fo0, nn));
-  uint32_t *w_tloc = (uint32_t *)ctx->s[0].p, *w_tlen = (uint32_t *)ctx->s[1].p, *w_fo = (uint32_t *)ctx->s[2].p;
-  uint32_t *jarr = (uint32_t *)ctx->s[3].p;
+  const int64_t n = u.n;
+  const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
   int64_t *ts = (int64_t *)ctx->s[4].p, *ts_shuf = (int64_t *)ctx->s[5].p, *te = (int64_t *)ctx->s[6].p;
   uint8_t *keep = (uint8_t *)ctx->s[7].p;
   int32_t *cnt = (int32_t *)ctx->s[8].p, *start = (int32_t *)ctx->s[9].p, *entries = (int32_t *)ctx->s[10].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
-  double *d_cum = (double *)ctx->s[13].p;
-  char *small = (char *)ctx->d_small.p;
-  int64_t *tot = (int64_t *)small;
-  uint32_t *flag_cnt = (uint32_t *)(small + 32);
-  HIPCHK(ctx, hipMemsetAsync(small, 0, 256, st));
-  HIPCHK(ctx, hipMemcpyAsync(d_cum, cum_tlen, 8 * n_tlen, hipMemcpyHostToDevice, st));
-
-  if (n == 0) {
-    stage_end(ctx);
-    ctx->n_tpl = 0;
-    ctx->rlen = rlen;
-    ctx->have_tpl = true;
-    *out_n = 0;
-    return MH_OK;
-  }
-
-  // 1. word streams
-  if (rng_mode == MH_RNG_MITTY) {
-    MTJobs jobs{};
-    jobs.j[0] = MTJob{w_tloc, 2 * n, s_tloc};
-    jobs.j[1] = MTJob{w_tlen, 2 * n, s_tlen};
-    jobs.j[2] = MTJob{w_fo, n_fo_words, s_fo};
-    stage_begin(ctx, "sample_mt_streams");
-    hipLaunchKernelGGL(k_mt_streams, dim3(3), dim3(256), 0, st, jobs);
-    HIPCHK(ctx, hipGetLastError());
-    stage_end(ctx);
-    stage_begin(ctx, "sample_shuffle_decode");
-    hipLaunchKernelGGL(k_shuffle_decode, dim3(1), dim3(SD_THREADS), 0, st, s_shuf, n, jarr);
-    HIPCHK(ctx, hipGetLastError());
-    stage_end(ctx);
-  } else {
-    uint64_t key = ((uint64_t)s_tloc << 32) | s_tlen;
-    hipLaunchKernelGGL(k_philox_words, dim3(grid_for((2 * n + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st, w_tloc,
-                       2 * n, key, 1u);
-    hipLaunchKernelGGL(k_philox_words, dim3(grid_for((2 * n + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st, w_tlen,
-                       2 * n, key, 2u);
-    hipLaunchKernelGGL(k_philox_words, dim3(grid_for((n_fo_words + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st, w_fo,
-                       n_fo_words, key, 3u);
-    HIPCHK(ctx, hipGetLastError());
-  }
-
-  // 2. ts = cumsum(geometric) + p_min + 1
+  int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128);
   const double log_q = std::log(1.0 - p);
-  GeoFlags fl{flag_idx, flag_cnt, 1024};
+  GeoFlags fl{flag_idx, d_flag, 1024};
+
   stage_begin(ctx, "sample_geometric_scan");
-  HIPCHK(ctx, device_scan<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, p_min + 1}, OpSum{}, (int64_t)0,
-                                   (int64_t *)ctx->scan_partials.p, tot));
-  stage_end(ctx);
-  uint32_t nflag = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&nflag, flag_cnt, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
-  if (nflag > 0) {
-    // rare exact path: materialise the draws, recompute the flagged ones with the host libm, rescan
-    MH_TRY(ensure(ctx, ctx->s[12], 8 * nn));
+  if (!exact) {
+    HIPCHK(ctx, device_scan<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1}, OpSum{},
+                                     (int64_t)0, (int64_t *)ctx->scan_partials.p, tot));
+  } else {
     int64_t *g = (int64_t *)ctx->s[12].p;
-    HIPCHK(ctx, hipMemsetAsync(flag_cnt, 0, 4, st));
+    uint32_t nflag = 0;
+    HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
     hipLaunchKernelGGL(k_geo_array, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, w_tloc, p, log_q, fl, g);
-    HIPCHK(ctx, hipMemcpyAsync(&nflag, flag_cnt, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&nflag, d_flag, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
-    if (nflag > 1024) {
-      stage_end(ctx);
-      return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients (p too coarse?)");
-    }
+    if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
     std::vector<int64_t> idx(nflag);
-    HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
+    if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
     for (int64_t k : idx) {
       uint32_t ww[2];
       HIPCHK(ctx, hipMemcpy(ww, w_tloc + 2 * k, 8, hipMemcpyDeviceToHost));
       double U = (((int32_t)(ww[0] >> 5)) * 67108864.0 + ((int32_t)(ww[1] >> 6))) / 9007199254740992.0;
-      int64_t gv = (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));
+      int64_t gv = (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));   // the reference's libm
       HIPCHK(ctx, hipMemcpy(g + k, &gv, 8, hipMemcpyHostToDevice));
     }
-    HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, p_min + 1}, OpSum{}, (int64_t)0,
+    HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
+    HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
                                      (int64_t *)ctx->scan_partials.p, tot));
   }
+  stage_end(ctx);
 
-  // 3. shuffle
   const int64_t *ts_use = ts;
   if (rng_mode == MH_RNG_MITTY && n > 1) {
     stage_begin(ctx, "sample_permutation");
@@ -519,30 +611,190 @@ int32_t sample_templates(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, in
     ts_use = ts_shuf;
   }
 
-  // 4. template lengths, keep te < p_max, compaction
   stage_begin(ctx, "sample_tlen_compact");
   hipLaunchKernelGGL(k_tlen, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 8 * n_tlen, st, n, w_tlen, d_cum, n_tlen,
-                     (int64_t)rlen, p_max, ts_use, te, keep);
+                     (int64_t)rlen, u.p_max, ts_use, te, keep);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, device_scan<int64_t>(st, n, LoadKeep{keep},
-                                   StoreCompact{keep, ts_use, te, (int64_t *)ctx->t_pos0.p, (int64_t *)ctx->t_pos1.p,
+                                   StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p, (int64_t *)u.out->pos1.p,
                                                 (int64_t)rlen},
-                                   OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p, tot + 2));
+                                   OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p, d_m));
+  hipLaunchKernelGGL(k_file_order, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const int64_t *)d_m,
+                     w_fo, (int8_t *)u.out->fo0.p);
+  HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
-  int64_t m = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&m, tot + 2, 8, hipMemcpyDeviceToHost, st));
+  return MH_OK;
+}
+
+}  // namespace
+
+int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
+                     const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                     int32_t rng_mode, int64_t *out_n) {
+  for (int32_t u = 0; u < n_units; u++)
+    if (seeds[u] > 0xffffffffull)
+      return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seeds[u]) + " is out of range 0 - 4294967295");
+  if (n_tlen <= 0 || n_tlen > 8192) return arg_fail(ctx, MH_E_ARG, "cum_tlen must have 1..8192 entries");
+  if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
+  hipStream_t st = ctx->stream;
+
+  // ---- plan ---------------------------------------------------------------------------------------------------
+  std::vector<UnitPlan> plan(n_units);
+  int64_t words_total = 0, j_total = 0, n_max = 1;
+  for (int32_t u = 0; u < n_units; u++) {
+    UnitPlan &q = plan[u];
+    q.p_min = p_min[u];
+    q.p_max = p_max[u];
+    q.n = (int64_t)((double)(q.p_max - q.p_min) * p * 1.2);   // int((p_max - p_min) * p * 1.2)
+    if (q.n < 0) q.n = 0;
+    if (q.n > ((int64_t)1 << 31) - 2) return arg_fail(ctx, MH_E_ARG, "region too large for one work unit");
+    HostMT sr;
+    sr.seed((uint32_t)seeds[u]);
+    q.s_tloc = (uint32_t)sr.interval(0xfffffffeull);
+    q.s_tlen = (uint32_t)sr.interval(0xfffffffeull);
+    q.s_shuf = (uint32_t)sr.interval(0xfffffffeull);
+    q.s_fo = (uint32_t)sr.interval(0xfffffffeull);
+    q.n_fo_words = (q.n + 3) / 4 + 1;
+    q.n_shuf_words = rng_mode == MH_RNG_MITTY ? shuffle_words_alloc(q.n) : 0;
+    q.w_tloc = words_total; words_total += 2 * q.n + 4;
+    q.w_tlen = words_total; words_total += 2 * q.n + 4;
+    q.w_fo = words_total; words_total += q.n_fo_words + 4;
+    q.w_shuf = words_total; words_total += q.n_shuf_words + 4;
+    words_total = (words_total + 3) & ~(int64_t)3;
+    q.j_off = j_total; j_total += q.n + 4;
+    n_max = std::max(n_max, q.n);
+    TplSet &ts = ctx->tsets[tpl_ids[u]];
+    MH_TRY(ensure(ctx, ts.fo0, q.n + 16));
+    MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
+    MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));
+    ts.valid = false;
+    q.out = &ts;
+  }
+  const int64_t nn = n_max + 1;
+  MH_TRY(ensure(ctx, ctx->s[0], 4 * (size_t)words_total + 64));
+  MH_TRY(ensure(ctx, ctx->s[3], 4 * (size_t)j_total + 64));
+  MH_TRY(ensure(ctx, ctx->s[4], 8 * nn));
+  MH_TRY(ensure(ctx, ctx->s[5], 8 * nn));
+  MH_TRY(ensure(ctx, ctx->s[6], 8 * nn));
+  MH_TRY(ensure(ctx, ctx->s[7], nn));
+  MH_TRY(ensure(ctx, ctx->s[8], 4 * (nn + 1)));
+  MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
+  MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
+  MH_TRY(ensure(ctx, ctx->s[11], 8 * 1024));
+  MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 64));
+  MH_TRY(ensure(ctx, ctx->s[1], 64 * (size_t)n_units + 64));          // per-unit m, flags, decode status
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  MH_TRY(ensure(ctx, ctx->scan_partials, 16 * scan_partials_count(nn + 1) + 64));
+  uint32_t *words = (uint32_t *)ctx->s[0].p, *jall = (uint32_t *)ctx->s[3].p;
+  double *d_cum = (double *)ctx->s[13].p;
+  int64_t *d_m = (int64_t *)ctx->s[1].p;                                // [n_units]
+  int64_t *d_status = d_m + n_units;                                    // [n_units]
+  uint32_t *d_flags = (uint32_t *)(d_status + n_units);                 // [n_units]
+  HIPCHK(ctx, hipMemsetAsync(ctx->s[1].p, 0, 64 * (size_t)n_units + 64, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_cum, cum_tlen, 8 * n_tlen, hipMemcpyHostToDevice, st));
+
+  stage_begin(ctx, "sample");
+  // ---- word streams ------------------------------------------------------------------------------------------
+  if (rng_mode == MH_RNG_MITTY) {
+    std::vector<SegJob> jobs;
+    std::vector<DecJob> dec;
+    int64_t kmax = 0;
+    auto add_stream = [&](uint32_t *out, int64_t count, uint32_t seed) {
+      for (int64_t k = 0; k * SEG_WORDS < count; k++) {
+        int64_t s0 = k * SEG_WORDS;
+        jobs.push_back(SegJob{out, s0, std::min(SEG_WORDS, count - s0), seed, (int32_t)k});
+        kmax = std::max(kmax, k);
+      }
+    };
+    for (int32_t u = 0; u < n_units; u++) {
+      UnitPlan &q = plan[u];
+      if (q.n == 0) continue;
+      add_stream(words + q.w_tloc, 2 * q.n, q.s_tloc);
+      add_stream(words + q.w_tlen, 2 * q.n, q.s_tlen);
+      add_stream(words + q.w_fo, q.n_fo_words, q.s_fo);
+      add_stream(words + q.w_shuf, q.n_shuf_words, q.s_shuf);
+      dec.push_back(DecJob{words + q.w_shuf, q.n_shuf_words, q.n, jall + q.j_off, d_status + u});
+    }
+    if (!jobs.empty()) {
+      // jump polynomials x^(k * SEG_WORDS) mod P, k = 0..kmax (cached on host and device)
+      if (ctx->jump_k < kmax + 1) {
+        std::vector<uint32_t> polys((size_t)(kmax + 1) * 624);
+        for (int64_t k = 0; k <= kmax; k++) jump::jump_poly_words((uint64_t)SEG_WORDS, k, polys.data() + k * 624);
+        MH_TRY(ensure(ctx, ctx->jump_polys, 4 * polys.size()));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->jump_polys.p, polys.data(), 4 * polys.size(), hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        ctx->jump_k = kmax + 1;
+      }
+      MH_TRY(ensure(ctx, ctx->s[2], sizeof(SegJob) * jobs.size() + sizeof(DecJob) * dec.size() + 64));
+      SegJob *d_jobs = (SegJob *)ctx->s[2].p;
+      DecJob *d_dec = (DecJob *)((char *)ctx->s[2].p + ((sizeof(SegJob) * jobs.size() + 15) / 16) * 16);
+      HIPCHK(ctx, hipMemcpyAsync(d_jobs, jobs.data(), sizeof(SegJob) * jobs.size(), hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, hipMemcpyAsync(d_dec, dec.data(), sizeof(DecJob) * dec.size(), hipMemcpyHostToDevice, st));
+      stage_begin(ctx, "sample_mt_segments");
+      hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)d_jobs,
+                         (const uint32_t *)ctx->jump_polys.p);
+      HIPCHK(ctx, hipGetLastError());
+      stage_end(ctx);
+      stage_begin(ctx, "sample_shuffle_decode");
+      hipLaunchKernelGGL(k_shuffle_decode2, dim3((unsigned)dec.size()), dim3(DC_THREADS), 0, st,
+                         (const DecJob *)d_dec);
+      HIPCHK(ctx, hipGetLastError());
+      stage_end(ctx);
+      // keep the job tables alive until the kernels ran
+      HIPCHK(ctx, hipStreamSynchronize(st));
+    }
+  } else {
+    for (int32_t u = 0; u < n_units; u++) {
+      UnitPlan &q = plan[u];
+      if (q.n == 0) continue;
+      uint64_t key = ((uint64_t)q.s_tloc << 32) | q.s_tlen;
+      hipLaunchKernelGGL(k_philox_words, dim3(grid_for((2 * q.n + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st,
+                         words + q.w_tloc, 2 * q.n, key, 1u);
+      hipLaunchKernelGGL(k_philox_words, dim3(grid_for((2 * q.n + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st,
+                         words + q.w_tlen, 2 * q.n, key, 2u);
+      hipLaunchKernelGGL(k_philox_words, dim3(grid_for((q.n_fo_words + 3) / 4, 256, INT32_MAX)), dim3(256), 0, st,
+                         words + q.w_fo, q.n_fo_words, key, 3u);
+      HIPCHK(ctx, hipGetLastError());
+    }
+  }
+
+  // ---- per-unit parallel stages (stream-ordered, shared scratch) ------------------------------------------------
+  for (int32_t u = 0; u < n_units; u++) {
+    if (plan[u].n == 0) continue;
+    MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
+                       d_flags + u));
+  }
+  std::vector<int64_t> hm(n_units), hstat(n_units);
+  std::vector<uint32_t> hflag(n_units);
+  HIPCHK(ctx, hipMemcpyAsync(hm.data(), d_m, 8 * n_units, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hstat.data(), d_status, 8 * n_units, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hflag.data(), d_flags, 4 * n_units, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
-  // 5. file order
-  if (m > 0) {
-    hipLaunchKernelGGL(k_file_order, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, m, w_fo,
-                       (int8_t *)ctx->t_fo0.p);
-    HIPCHK(ctx, hipGetLastError());
+
+  // ---- rare exact fix-ups: decode out of words (sequential stream), near-integer geometric quotients ------------
+  for (int32_t u = 0; u < n_units; u++) {
+    UnitPlan &q = plan[u];
+    if (q.n == 0 || (hstat[u] == 0 && hflag[u] == 0)) continue;
+    if (rng_mode == MH_RNG_MITTY && hstat[u] != 0) {
+      hipLaunchKernelGGL(k_shuffle_decode, dim3(1), dim3(SD_THREADS), 0, st, q.s_shuf, q.n, jall + q.j_off);
+      HIPCHK(ctx, hipGetLastError());
+    }
+    MH_TRY(ensure(ctx, ctx->s[12], 8 * (size_t)nn));
+    HIPCHK(ctx, hipMemsetAsync(d_flags + u, 0, 4, st));
+    MH_TRY(finish_unit(ctx, q, words, jall + q.j_off, p, rlen, d_cum, n_tlen, rng_mode, hflag[u] != 0, d_m + u,
+                       d_flags + u));
+    HIPCHK(ctx, hipMemcpyAsync(&hm[u], d_m + u, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    ctx->fixups++;
   }
   stage_end(ctx);
-  ctx->n_tpl = m;
-  ctx->rlen = rlen;
-  ctx->have_tpl = true;
-  *out_n = m;
+  for (int32_t u = 0; u < n_units; u++) {
+    TplSet &ts = *plan[u].out;
+    ts.n = plan[u].n == 0 ? 0 : hm[u];
+    ts.rlen = rlen;
+    ts.valid = true;
+    if (out_n) out_n[u] = ts.n;
+  }
   return MH_OK;
 }
 

@@ -1,8 +1,9 @@
 """Device-resident generate-reads pipeline for one GPU (the orchestration of reference readgenerate.py:76-218).
 
 One Engine = one HIP context.  Per BED region the fetched reference bytes are uploaded once; per (region, copy)
-the haplotype is spliced on the device once and kept resident for all of that copy's passes; per work unit
-(region, copy, pass) the templates are sampled and the FASTQ records emitted into device arenas.
+the haplotype is spliced on the device once and kept resident for all of that copy's passes; work units
+(region, copy, pass) are sampled in batches — all their MT19937 streams generated at once in jump-ahead
+segments — and then emitted one by one, in the reference's unit order, into the device FASTQ arenas.
 """
 import logging
 
@@ -43,12 +44,28 @@ class Engine:
       self.ctx.release_haplotype(slot)
     self._haps.clear()
 
+  def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
+                on_unit=None):
+    """Sample a batch of work units together, then emit them in order.
+
+    units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
+    unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
+    """
+    slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    ns = self.ctx.sample_units(list(range(len(units))), slots, [u[3] for u in units], p, rlen, cum_tlen,
+                               RNG_MODES[rng])
+    out = []
+    for k, (ps, ri, cpy, seed) in enumerate(units):
+      self.ctx.use_templates(k)
+      kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
+                                         self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
+      out.append((int(ns[k]), kept, b1, b2))
+      if on_unit is not None:
+        on_unit(ps, int(ns[k]), kept, b1, b2)
+    return out
+
   def run_unit(self, ps, ri, cpy, rng_seed, soa, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
                rng='mitty'):
     """One work unit: sample templates, emit FASTQ.  Returns (n_templates, kept, bytes1, bytes2)."""
-    chrom = self._regions[ri][0]
-    slot, _, _, _ = self.haplotype(ri, cpy, soa)
-    n = self.ctx.sample_templates(slot, p, rlen, cum_tlen, rng_seed, RNG_MODES[rng])
-    kept, b1, b2 = self.ctx.emit_reads(slot, '{}:{}:{}'.format(sample_name, worker_id, ps), chrom, cpy,
-                                       write_fastq2, unit_key=rng_seed)
-    return n, kept, b1, b2
+    return self.run_units([(ps, ri, cpy, rng_seed)], lambda a, b: soa, p, rlen, cum_tlen, sample_name, worker_id,
+                          write_fastq2, rng)[0]

@@ -74,7 +74,7 @@ def _write_all(fp, data):
 
 def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                            fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
-                           flush_bytes=1 << 30):
+                           flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000):
   """Generate reads for every (region, copy, pass) unit and write FASTQ (reference readgenerate.py:76-126).
 
   Returns a stats dict (templates sampled, kept, bytes, seconds).
@@ -96,25 +96,34 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   write2 = fastq2_fname is not None
   fp1 = open(fastq1_fname, 'wb')
   fp2 = open(fastq2_fname, 'wb') if write2 else None
+
+  def flush(ps, n, kept, b1, b2):
+    stats['templates'] += n
+    stats['kept'] += kept
+    stats['bytes1'] += b1
+    stats['bytes2'] += b2
+    u1, u2 = eng.ctx.output_size()
+    if u1 + u2 >= flush_bytes or ps == len(units) - 1:
+      d1, d2 = eng.ctx.fetch_output()
+      _write_all(fp1, d1)
+      if write2:
+        _write_all(fp2, d2)
+      eng.ctx.reset_output()
+
   try:
+    # batches of units sampled together (their MT19937 streams run concurrently); order of emission unchanged
+    batch, batch_draws = [], 0
     for ps, wd in enumerate(units):
-      ri, cpy, rs = wd['region_idx'], wd['region_cpy'], wd['rng_seed']
-      t1 = time.time()
-      n, kept, b1, b2 = eng.run_unit(ps, ri, cpy, rs, vdf[ri]['copies'][cpy], read_model['p'], read_model['rlen'],
-                                     read_model['cum_tlen'], sample_name, 0, write2, rng)
-      stats['templates'] += n
-      stats['kept'] += kept
-      stats['bytes1'] += b1
-      stats['bytes2'] += b2
-      logger.debug('Unit {} ({}, copy {}): {} templates in {:0.3f}s'.format(ps, vdf[ri]['region'], cpy, kept,
-                                                                         time.time() - t1))
-      u1, u2 = eng.ctx.output_size()
-      if u1 + u2 >= flush_bytes or ps == len(units) - 1:
-        d1, d2 = eng.ctx.fetch_output()
-        _write_all(fp1, d1)
-        if write2:
-          _write_all(fp2, d2)
-        eng.ctx.reset_output()
+      ri, cpy = wd['region_idx'], wd['region_cpy']
+      reg = vdf[ri]['region']
+      batch.append((ps, ri, cpy, wd['rng_seed']))
+      batch_draws += int((reg[2] - reg[1]) * read_model['p'] * 1.2)
+      if len(batch) >= max_batch_units or batch_draws >= max_batch_draws or ps == len(units) - 1:
+        t1 = time.time()
+        eng.run_units(batch, lambda r, c: vdf[r]['copies'][c], read_model['p'], read_model['rlen'],
+                      read_model['cum_tlen'], sample_name, 0, write2, rng, on_unit=flush)
+        logger.debug('Units {}..{}: {:0.3f}s'.format(batch[0][0], batch[-1][0], time.time() - t1))
+        batch, batch_draws = [], 0
   finally:
     fp1.close()
     if fp2:

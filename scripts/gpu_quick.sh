@@ -1,0 +1,18 @@
+# GPU tests + short bench (+ optional rocprofv3 kernel-trace of the bench)
+mkdir -p gpurun_out
+TAG=${1:-quick}
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -x > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_$TAG.log
+if [ "$rc" != 0 ] && [ "$rc" != 1 ]; then exit $rc; fi
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 --cpu-baseline-mbp 100 > gpurun_out/bench_$TAG.log 2>&1
+rc=$?
+echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench_$TAG.log
+if [ "$rc" != 0 ]; then exit $rc; fi
+if [ "$2" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.log 2>&1
+  echo "rocprof rc=$?"
+  find gpurun_out/prof_$TAG -name '*kernel_stats.csv' -exec head -30 {} \;
+fi

@@ -236,6 +236,42 @@ def test_unit_vs_oracle_no_variants(native):
   _unit_vs_oracle(600_000, 1, '1kg-pcr-free', n_seed=9, rate=0.0)
 
 
+def test_batched_units_vs_oracle(native):
+  """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
+  reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 30.0)
+  regions = [('5', 0, 9_000_000), ('6', 250_000, 4_000_000)]
+  seqs = [synth.contig(9_000_000, 21), synth.contig(4_000_000, 22)]
+  copies = [synth.copies_soa(synth.variants(seqs[0], 23), 0, 9_000_000),
+            synth.copies_soa(synth.variants(seqs[1], 24), 250_000, 4_000_000)]
+  units = _native.work_units(99, [2, 2], passes)
+  eng = Engine(0)
+  try:
+    for ri, (reg, s) in enumerate(zip(regions, seqs)):
+      eng.load_region(ri, reg, s[reg[1]:reg[2]])
+    res = eng.run_units([(ps, ri, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)],
+                        lambda r, c: copies[r][c], p, 150, mdl['cum_tlen'], 'SYN')
+    d1, d2 = eng.ctx.fetch_output()
+    fix = eng.ctx.fixup_count()
+  finally:
+    eng.close()
+  o1, o2, total = [], [], 0
+  for ps, (ri, cpy, sd) in enumerate(units):
+    reg = regions[ri]
+    k, b1, b2 = O.generate_unit_soa(seqs[ri][reg[1]:reg[2]], reg[1], copies[ri][cpy], p, 150, mdl['cum_tlen'], sd,
+                                    'SYN:0:{}'.format(ps), reg[0], cpy)
+    assert res[ps][1] == k
+    o1.append(b1)
+    o2.append(b2)
+  assert d1 == b''.join(o1)
+  assert d2 == b''.join(o2)
+  assert fix <= 1
+
+
 # ---- size-independent properties at full chromosome scale -------------------------------------------------------
 def test_chr1_scale_properties(native):
   """One chr1-sized unit (249 Mbp): every record parses, POS/CIGAR are consistent with the sequence length, every

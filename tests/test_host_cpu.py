@@ -138,3 +138,26 @@ def test_no_device_raises_here():
     pytest.skip('a GPU is visible')
   with pytest.raises(_native.NativeUnavailable):
     _native.Context(0)
+
+
+def _raw_mt(seed, n):
+  x = np.zeros(n, dtype=np.uint64)
+  x[0] = seed
+  for i in range(1, 624):
+    x[i] = (1812433253 * (int(x[i - 1]) ^ (int(x[i - 1]) >> 30)) + i) & 0xffffffff
+  xs = [int(v) for v in x[:624]]
+  for t in range(624, n):
+    y = (xs[t - 624] & 0x80000000) | (xs[t - 623] & 0x7fffffff)
+    xs.append(xs[t - 227] ^ (y >> 1) ^ (0x9908b0df if y & 1 else 0))
+  return xs
+
+
+@pytest.mark.parametrize('seed', [7, 327741615, 4294967295])
+def test_mt19937_jump_ahead_host(seed):
+  """The jump polynomial x^J mod P (host GF(2) math the device segments use) lands on the same window as the plain
+  recurrence, at offsets inside and across twist blocks."""
+  xs = _raw_mt(seed, 200_000 + 624)
+  for J in (0, 1, 623, 624, 1000, 12345, 199_680):
+    w = _native.mt_window_at(seed, J)
+    assert (int(w[0]) >> 31) == (xs[J] >> 31)
+    assert [int(v) for v in w[1:]] == xs[J + 1:J + 624], J
