@@ -152,7 +152,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &b : ctx->s) release(b);
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
-  release(ctx->out1); release(ctx->out2);
+  release(ctx->out1); release(ctx->out2); release(ctx->emit_slots);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return MH_OK;
@@ -456,6 +456,12 @@ int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624) {
   } catch (...) {
     return MH_E_ARG;
   }
+  return MH_OK;
+}
+
+int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode) {
+  if (!ctx || mode < 0 || mode > 1) return MH_E_ARG;
+  ctx->emit_lds_only = mode == 1;
   return MH_OK;
 }
 

@@ -177,8 +177,48 @@ __device__ int count_N(const HapView &h, int64_t a, int64_t b) {
 }
 
 struct Rec {
-  int32_t keep, len1, len2, pad;
-  int32_t n0[2], n1[2];   // start / end node per mate (pass 2 skips the searches)
+  int32_t keep, len1, len2, rest;   // rest: length of the reads part of the qname (formatted into the slot)
+  int32_t n0[2], n1[2];             // start / end node per mate (pass 2 skips the searches)
+};
+
+// Packs bytes into dwords and stores each completed dword (one thread writing its own slot).
+struct ByteWriter {
+  uint32_t *p;
+  uint32_t acc;
+  int nb;
+  __device__ __forceinline__ void put(uint8_t c) {
+    acc |= (uint32_t)c << (8 * nb);
+    if (++nb == 4) {
+      *p++ = acc;
+      acc = 0;
+      nb = 0;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if (nb) *p = acc;
+  }
+  // decimal, most significant digit first: digits packed 4 bits each (LSB-first) then emitted from the top
+  __device__ __forceinline__ void put_u(uint64_t v) {
+    if (v <= 0xffffffffull) {
+      uint32_t x = (uint32_t)v;
+      uint64_t bcd = 0;
+      int nd = 0;
+      do {
+        bcd |= (uint64_t)(x % 10u) << (4 * nd);
+        x /= 10u;
+        nd++;
+      } while (x);
+      for (int i = nd - 1; i >= 0; i--) put((uint8_t)('0' + ((bcd >> (4 * i)) & 15)));
+    } else {
+      char tmp[24];
+      int nd = 0;
+      do { tmp[nd++] = (char)('0' + v % 10u); v /= 10u; } while (v);
+      for (int i = nd - 1; i >= 0; i--) put((uint8_t)tmp[i]);
+    }
+  }
+  __device__ __forceinline__ void put_s(int64_t v) {
+    if (v < 0) { put('-'); put_u((uint64_t)(-v)); } else put_u((uint64_t)v);
+  }
 };
 struct E3 {
   int64_t kept, b1, b2;
@@ -207,15 +247,19 @@ __device__ __forceinline__ int32_t qname_len_wo_cnt(const QFixed &q, const ReadI
   return n;
 }
 
+constexpr int SLOT = 256;   // bytes per template for the reads part of the qname ("|s|pos|rlen|cigar|v,..|...")
+
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
-                                                      Rec *recs, int32_t *max_rec) {
+                                                      Rec *recs, int32_t *max_rec, uint8_t *slots,
+                                                      int32_t *overflow) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int32_t local_max = 0;
   if (t < m) {
     ReadInfo r[2];
-    read_info(h, pos0[t], rlen, r[0]);
-    read_info(h, pos1[t], rlen, r[1]);
+    const int64_t p[2] = {pos0[t], pos1[t]};
+    read_info(h, p[0], rlen, r[0]);
+    read_info(h, p[1], rlen, r[1]);
     int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
                count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
@@ -228,7 +272,40 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       out.keep = 1;
       out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
       out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
+      out.rest = ql - q.prefix_len - q.mid_len;
       local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+      if (slots != nullptr) {
+        if (out.rest > SLOT) {
+          atomicOr(overflow, 1);
+        } else {   // the reads part of the qname, in file order (readgenerate.py:223-225)
+          ByteWriter bw{(uint32_t *)(slots + t * SLOT), 0u, 0};
+          for (int fr = 0; fr < 2; fr++) {
+            const int s = fr == f0 ? 0 : 1;
+            const ReadInfo &ri = r[s];
+            bw.put('|'); bw.put((uint8_t)('0' + s));
+            bw.put('|'); bw.put_s(ri.pos);
+            bw.put('|'); bw.put_s(rlen);
+            bw.put('|');
+            if (ri.special) {
+              bw.put('>'); bw.put_s(p[s] - h.ps[ri.n0]); bw.put(':'); bw.put_s(rlen); bw.put('I');
+            } else {
+              for (int64_t k = ri.n0; k <= ri.n1; k++) {
+                bw.put_s(node_count(h, k, p[s], rlen));
+                bw.put(h.op[k]);
+              }
+            }
+            bw.put('|');
+            bool first = true;
+            for (int64_t k = ri.n0; k <= ri.n1; k++) {
+              if (h.op[k] == '=') continue;
+              if (!first) bw.put(',');
+              bw.put_s(node_v(h, k));
+              first = false;
+            }
+          }
+          bw.flush();
+        }
+      }
     }
     recs[t] = out;
   }
@@ -472,6 +549,221 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
   }
 }
 
+// ---- pull-model assembler ------------------------------------------------------------------------------------
+// Every thread builds whole 16-byte output chunks in registers: it finds the record holding the chunk's first byte
+// and walks the record's fields ('@stub:' | cnt | '|chrom|cpy' | reads part of the qname (slot) | '\n' | bases |
+// '\n+\n' | qualities | '\n'), pulling bytes from LDS (haplotype windows, qname slots) or constants; full chunks
+// leave as one 16-byte aligned store, the two ragged ends of the workgroup's range as byte stores.
+constexpr int EA_T = 32;
+constexpr int EA_THREADS = 256;
+
+struct AMeta {
+  int32_t start[2], len[2];   // record start (workgroup-relative) and length per file; len 0 = dropped
+  int32_t e1, e3;             // end of the cnt digits / of the reads part (record-relative)
+  int32_t S[2], win[2];       // per file: bases, LDS window offset of the read's first base
+  int32_t rc;                 // bit f: file f holds mate 1 (reverse complement)
+  int32_t nd;                 // cnt digits
+  uint32_t bcd_lo, bcd_hi;    // cnt digits, 4 bits each, least significant first
+  int32_t rest_off;           // LDS offset of the slot copy
+  int32_t pad;
+};
+
+struct Emit16 {
+  uint64_t lo, hi;
+  __device__ __forceinline__ void put(int b, uint8_t c) {
+    if (b < 8) lo |= (uint64_t)c << (8 * b); else hi |= (uint64_t)c << (8 * (b - 8));
+  }
+};
+
+__global__ void __launch_bounds__(EA_THREADS) k_emit_assemble(HapView h, int64_t m, const int64_t *pos0,
+                                                              const int64_t *pos1, const int8_t *fo0, int64_t rlen,
+                                                              QFixed q, const Rec *recs, const E3 *off,
+                                                              const uint8_t *slots, char *out1, char *out2,
+                                                              int write2, int32_t win_stride, CorruptCfg cc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  AMeta *meta = (AMeta *)smem;
+  uint8_t *wins = (uint8_t *)smem + ((sizeof(AMeta) * EA_T + 15) / 16) * 16;
+  uint8_t *rests = wins + (size_t)EA_T * 2 * win_stride;
+  char *fixed = (char *)(rests + (size_t)EA_T * SLOT);   // prefix | mid
+  __shared__ int64_t s_g0[2], s_g1[2];
+
+  const int64_t t0 = (int64_t)blockIdx.x * EA_T;
+  const int64_t t1 = t0 + EA_T < m ? t0 + EA_T : m;
+  const int nt = (int)(t1 - t0);
+  const int nfile = write2 ? 2 : 1;
+  const int tid = threadIdx.x;
+  const int Lp = q.prefix_len, Lm = q.mid_len;
+
+  for (int i = tid; i < Lp + Lm; i += EA_THREADS) fixed[i] = i < Lp ? q.prefix[i] : q.mid[i - Lp];
+  if (tid == 0) {
+    const E3 a = off[t0], b = off[t1];
+    s_g0[0] = a.b1; s_g0[1] = a.b2;
+    s_g1[0] = b.b1; s_g1[1] = b.b2;
+  }
+  // ---- per-template metadata ----------------------------------------------------------------------------------
+  if (tid < nt) {
+    const int64_t t = t0 + tid;
+    const Rec rc = recs[t];
+    const E3 o = off[t];
+    const E3 base = off[t0];
+    AMeta mt;
+    mt.start[0] = (int32_t)(o.b1 - base.b1);
+    mt.start[1] = (int32_t)(o.b2 - base.b2);
+    mt.len[0] = rc.keep ? rc.len1 : 0;
+    mt.len[1] = rc.keep ? rc.len2 : 0;
+    mt.rest_off = tid * SLOT;
+    if (rc.keep) {
+      const int64_t cnt = o.kept + 1;
+      uint64_t bcd = 0;
+      int nd = 0;
+      uint64_t x = (uint64_t)cnt;
+      do { bcd |= (uint64_t)(x % 10u) << (4 * nd); x /= 10u; nd++; } while (x && nd < 16);
+      mt.nd = nd;
+      mt.bcd_lo = (uint32_t)bcd;
+      mt.bcd_hi = (uint32_t)(bcd >> 32);
+      mt.e1 = Lp + nd;
+      mt.e3 = mt.e1 + Lm + rc.rest;
+      const int f0 = fo0[t];
+      const int64_t p[2] = {pos0[t], pos1[t]};
+      mt.rc = 0;
+      for (int f = 0; f < 2; f++) {
+        const int s = f == f0 ? 0 : 1;
+        int64_t a = p[s] - h.p_min, e = p[s] + rlen - h.p_min;
+        if (e > h.hap_len) e = h.hap_len;
+        if (a > h.hap_len) a = h.hap_len;
+        mt.S[f] = (int32_t)(e > a ? e - a : 0);
+        mt.win[f] = (tid * 2 + s) * win_stride + (int)(a & 15);
+        mt.rc |= s << f;
+      }
+    } else {
+      mt.nd = 0; mt.bcd_lo = mt.bcd_hi = 0; mt.e1 = mt.e3 = 0; mt.S[0] = mt.S[1] = 0; mt.win[0] = mt.win[1] = 0;
+      mt.rc = 0;
+    }
+    meta[tid] = mt;
+  }
+  __syncthreads();
+  // ---- gathers: both mates' haplotype windows and the qname slots (all loads in flight) ------------------------
+  const int chunks = win_stride / 16;
+  for (int it = tid; it < nt * 2 * chunks; it += EA_THREADS) {
+    const int j = it / (2 * chunks), rem = it - j * 2 * chunks, s = rem / chunks, c = rem - s * chunks;
+    if (meta[j].len[0] == 0) continue;
+    const int64_t t = t0 + j;
+    int64_t a = (s ? pos1[t] : pos0[t]) - h.p_min;
+    if (a > h.hap_len) a = h.hap_len;
+    const int64_t a16 = a & ~(int64_t)15;
+    if (a16 + 16 * c < a + rlen)
+      *(uint4 *)(wins + (size_t)(j * 2 + s) * win_stride + 16 * c) = *(const uint4 *)(h.hap + a16 + 16 * c);
+  }
+  for (int it = tid; it < nt * (SLOT / 16); it += EA_THREADS) {
+    const int j = it / (SLOT / 16), c = it - j * (SLOT / 16);
+    const AMeta &mt = meta[j];
+    if (mt.len[0] == 0 || 16 * c >= mt.e3 - mt.e1 - Lm) continue;
+    *(uint4 *)(rests + mt.rest_off + 16 * c) = *(const uint4 *)(slots + (t0 + j) * SLOT + 16 * c);
+  }
+  __syncthreads();
+
+  // ---- assemble ------------------------------------------------------------------------------------------------
+  for (int f = 0; f < nfile; f++) {
+    const int64_t G0 = s_g0[f], G1 = s_g1[f];
+    if (G1 <= G0) continue;
+    char *out = f ? out2 : out1;
+    int64_t A0 = (G0 + 15) & ~(int64_t)15, A1 = G1 & ~(int64_t)15;
+    if (A0 > G1) A0 = G1;
+    if (A1 < A0) A1 = A0;
+    const int64_t nvec = (A1 - A0) >> 4;
+    // work items: 0 = head [G0, A0), 1 = tail [A1, G1), 2.. = full chunks
+    for (int64_t w = tid; w < nvec + 2; w += EA_THREADS) {
+      int64_t gs, ge;
+      if (w == 0) { gs = G0; ge = A0; }
+      else if (w == 1) { gs = A1; ge = G1; }
+      else { gs = A0 + ((w - 2) << 4); ge = gs + 16; }
+      if (ge <= gs) continue;
+      const int nb = (int)(ge - gs);
+      const int32_t g = (int32_t)(gs - G0);
+      // record holding byte g: the last record whose start <= g (dropped records have length 0)
+      int lo = 0, hi = nt;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (meta[mid].start[f] <= g) lo = mid + 1; else hi = mid;
+      }
+      int j = lo - 1;
+      int r = g - meta[j].start[f];
+      Emit16 e{0, 0};
+      int b = 0;
+      while (b < nb) {
+        while (r >= meta[j].len[f]) { j++; r = 0; }
+        const AMeta &mt = meta[j];
+        const int S = mt.S[f];
+        const int Q = cc.enable ? S : (int)rlen;
+        const int e3 = mt.e3, e5 = e3 + 1 + S, e6 = e5 + 3, e7 = e6 + Q;
+        int n;
+        if (r < Lp) {
+          n = min(nb - b, Lp - r);
+          for (int k = 0; k < n; k++) e.put(b + k, (uint8_t)fixed[r + k]);
+        } else if (r < mt.e1) {
+          n = min(nb - b, mt.e1 - r);
+          const uint64_t bcd = ((uint64_t)mt.bcd_hi << 32) | mt.bcd_lo;
+          for (int k = 0; k < n; k++) {
+            const int di = mt.nd - 1 - (r + k - Lp);
+            e.put(b + k, (uint8_t)('0' + ((bcd >> (4 * di)) & 15)));
+          }
+        } else if (r < mt.e1 + Lm) {
+          n = min(nb - b, mt.e1 + Lm - r);
+          for (int k = 0; k < n; k++) e.put(b + k, (uint8_t)fixed[Lp + r + k - mt.e1]);
+        } else if (r < e3) {
+          n = min(nb - b, e3 - r);
+          const uint8_t *src = rests + mt.rest_off + (r - mt.e1 - Lm);
+          for (int k = 0; k < n; k++) e.put(b + k, src[k]);
+        } else if (r == e3 || r == e5 || r == e5 + 2 || r == e7) {
+          n = 1;
+          e.put(b, '\n');
+        } else if (r == e5 + 1) {
+          n = 1;
+          e.put(b, '+');
+        } else if (r < e5) {
+          const int k0 = r - e3 - 1;
+          n = min(nb - b, e5 - r);
+          const uint8_t *w = wins + mt.win[f];
+          const bool rcf = (mt.rc >> f) & 1;
+          for (int k = 0; k < n; k++) {
+            const int kk = k0 + k;
+            uint8_t c = rcf ? comp(w[S - 1 - kk]) : w[kk];
+            if (cc.enable) {
+              uint8_t qq;
+              corrupt_base(cc, t0 + j, f, kk, c, qq);
+            }
+            e.put(b + k, c);
+          }
+        } else {   // qualities
+          const int k0 = r - e6;
+          n = min(nb - b, e7 - r);
+          if (!cc.enable) {
+            for (int k = 0; k < n; k++) e.put(b + k, '~');
+          } else {
+            const uint8_t *w = wins + mt.win[f];
+            const bool rcf = (mt.rc >> f) & 1;
+            for (int k = 0; k < n; k++) {
+              const int kk = k0 + k;
+              uint8_t c = rcf ? comp(w[S - 1 - kk]) : w[kk], qq;
+              corrupt_base(cc, t0 + j, f, kk, c, qq);
+              e.put(b + k, qq);
+            }
+          }
+        }
+        b += n;
+        r += n;
+      }
+      if (nb == 16 && (gs & 15) == 0) {
+        *(uint4 *)(out + gs) = make_uint4((uint32_t)e.lo, (uint32_t)(e.lo >> 32), (uint32_t)e.hi,
+                                          (uint32_t)(e.hi >> 32));
+      } else {
+        for (int k = 0; k < nb; k++)
+          out[gs + k] = (char)(k < 8 ? (e.lo >> (8 * k)) : (e.hi >> (8 * (k - 8))));
+      }
+    }
+  }
+}
+
 // ---- rpc.generate_read facade: per-read text into host-visible buffers ------------------------------------
 __global__ void k_rb_measure(HapView h, int64_t n, const int64_t *p, const int64_t *l, int64_t *pos, int64_t *n0,
                              int64_t *n1, int64_t *lens, int32_t *err) {
@@ -548,10 +840,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   Rec *recs = (Rec *)ctx->s[14].p;
   E3 *off = (E3 *)ctx->s[15].p;
 
+  const bool assemble = !ctx->emit_lds_only;
+  int32_t *overflow = (int32_t *)(small + 40);
+  if (assemble) MH_TRY(ensure(ctx, ctx->emit_slots, (size_t)SLOT * (m + 1)));
   stage_begin(ctx, "emit_measure");
   hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m,
                      (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p,
-                     rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec);
+                     rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
+                     assemble ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");
@@ -591,12 +887,30 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     stage_end(ctx);
     return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
   }
-  const int64_t nblk = (m + EW_T - 1) / EW_T;
+  int32_t hover = 0;
+  if (assemble) {
+    HIPCHK(ctx, hipMemcpyAsync(&hover, overflow, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+  }
+  char *o1 = (char *)ctx->out1.p + ctx->used1;
+  char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   stage_begin(ctx, "emit_write");
-  hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
-                     (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p,
-                     rlen, q, (const Rec *)recs, (const E3 *)off, (char *)ctx->out1.p + ctx->used1,
-                     write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr, write_fastq2, cap, win_stride, cc, err);
+  if (assemble && !hover) {
+    // pull-model assembler (qname reads part formatted by k_emit_measure into 256-byte slots)
+    const size_t lds_a = ((sizeof(AMeta) * EA_T + 15) / 16) * 16 + (size_t)EA_T * 2 * win_stride +
+                         (size_t)EA_T * SLOT + 4160;
+    const int64_t nblk_a = (m + EA_T - 1) / EA_T;
+    hipLaunchKernelGGL(k_emit_assemble, dim3((unsigned)nblk_a), dim3(EA_THREADS), lds_a, st, hv, m,
+                       (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p, rlen, q,
+                       (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p, o1, o2, write_fastq2,
+                       win_stride, cc);
+  } else {
+    // LDS-image writer: fallback when a qname's reads part exceeds its slot
+    const int64_t nblk = (m + EW_T - 1) / EW_T;
+    hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
+                       (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p, rlen, q,
+                       (const Rec *)recs, (const E3 *)off, o1, o2, write_fastq2, cap, win_stride, cc, err);
+  }
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   int32_t herr = 0;

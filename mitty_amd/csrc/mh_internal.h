@@ -90,6 +90,10 @@ struct mh_ctx {
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
   uint64_t corrupt_seed = 0;
 
+  // emission: per-template qname slots; emit_lds_only forces the LDS-image writer (A/B and fallback testing)
+  mh::DevBuf emit_slots;
+  bool emit_lds_only = false;
+
   // FASTQ arenas
   mh::DevBuf out1, out2;
   int64_t used1 = 0, used2 = 0;

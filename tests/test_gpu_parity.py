@@ -196,7 +196,7 @@ def test_e2e_single_file_and_cli(native, tmp_path):
   assert open(f1, 'rb').read() == G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
 
 
-def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(0, 1)):
+def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(0, 1), emit_mode=0):
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from oracle import oracle as O
@@ -207,6 +207,7 @@ def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(
   copies = synth.copies_soa(recs, start0, length)
   ref = seq[start0:]
   eng = Engine(0)
+  eng.ctx.set_emit_mode(emit_mode)
   try:
     eng.load_region(0, ('7', start0, length), ref)
     for cpy in cpys:
@@ -223,13 +224,21 @@ def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(
   return kept
 
 
+@pytest.mark.parametrize('emit_mode', [0, 1])
 @pytest.mark.parametrize('model', G.MODELS)
-def test_unit_vs_oracle_2mbp(native, model):
-  assert _unit_vs_oracle(2_000_000, 7, model) > 10000
+def test_unit_vs_oracle_2mbp(native, model, emit_mode):
+  assert _unit_vs_oracle(2_000_000, 7, model, emit_mode=emit_mode) > 10000
 
 
-def test_unit_vs_oracle_dense_variants_offset_region(native):
-  _unit_vs_oracle(1_500_000, 4000000000, 'hiseq-X-v2.5-Garvan', n_seed=5, rate=8e-3, start0=123_457)
+@pytest.mark.parametrize('emit_mode', [0, 1])
+def test_unit_vs_oracle_dense_variants_offset_region(native, emit_mode):
+  _unit_vs_oracle(1_500_000, 4000000000, 'hiseq-X-v2.5-Garvan', n_seed=5, rate=8e-3, start0=123_457,
+                  emit_mode=emit_mode)
+
+
+def test_unit_vs_oracle_very_dense_slot_overflow(native):
+  """~1 variant per 8 bp: some qnames exceed the 256-byte slot, the unit falls back to the LDS-image writer."""
+  _unit_vs_oracle(300_000, 11, '1kg-pcr-free', n_seed=13, rate=0.12, cpys=(0,))
 
 
 def test_unit_vs_oracle_no_variants(native):
