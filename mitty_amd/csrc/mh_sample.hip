@@ -173,14 +173,17 @@ __global__ void __launch_bounds__(DC_THREADS) k_shuffle_decode2(const DecJob *jo
   int64_t i0 = job.n - 1;
   int64_t base = 0;
   float ratio = 0.75f;
+  // words of the current chunk; the next chunk's are loaded one step ahead (hides the HBM latency per step)
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (DC_PER * t + 3 < job.n_words) nxt = *(const uint4 *)(job.words + DC_PER * t);
   while (i0 >= 1 && base < job.n_words) {
-    uint32_t w[DC_PER];
+    uint32_t w[DC_PER] = {nxt.x, nxt.y, nxt.z, nxt.w};
     bool valid[DC_PER];
 #pragma unroll
-    for (int e = 0; e < DC_PER; e++) {
-      const int64_t idx = base + DC_PER * t + e;
-      valid[e] = idx < job.n_words;
-      w[e] = valid[e] ? job.words[idx] : 0u;
+    for (int e = 0; e < DC_PER; e++) valid[e] = base + DC_PER * t + e < job.n_words;
+    {
+      const int64_t nb = base + DC_CHUNK + DC_PER * t;
+      if (nb + 3 < job.n_words) nxt = *(const uint4 *)(job.words + nb);
     }
     int32_t A = (int32_t)(ratio * (float)(DC_PER * t));
     int32_t cnt = 0;
@@ -656,11 +659,15 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     q.s_fo = (uint32_t)sr.interval(0xfffffffeull);
     q.n_fo_words = (q.n + 3) / 4 + 1;
     q.n_shuf_words = rng_mode == MH_RNG_MITTY ? shuffle_words_alloc(q.n) : 0;
-    q.w_tloc = words_total; words_total += 2 * q.n + 4;
-    q.w_tlen = words_total; words_total += 2 * q.n + 4;
-    q.w_fo = words_total; words_total += q.n_fo_words + 4;
-    q.w_shuf = words_total; words_total += q.n_shuf_words + 4;
-    words_total = (words_total + 3) & ~(int64_t)3;
+    auto take = [&](int64_t cnt) {   // 16-byte aligned stream offsets (vector loads in the decode)
+      int64_t at = words_total;
+      words_total = (words_total + cnt + 4 + 3) & ~(int64_t)3;
+      return at;
+    };
+    q.w_tloc = take(2 * q.n);
+    q.w_tlen = take(2 * q.n);
+    q.w_fo = take(q.n_fo_words);
+    q.w_shuf = take(q.n_shuf_words);
     q.j_off = j_total; j_total += q.n + 4;
     n_max = std::max(n_max, q.n);
     TplSet &ts = ctx->tsets[tpl_ids[u]];

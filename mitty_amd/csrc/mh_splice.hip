@@ -162,42 +162,49 @@ struct RunCnt {
   __device__ RunCnt operator+(const RunCnt &o) const { return RunCnt{starts + o.starts, ends + o.ends}; }
 };
 
-// Element c covers byte positions k in [c*16, c*16+16) ∩ [0, len]; start at k if hap[k]=='N' && prev != 'N';
-// end at k (exclusive) if hap[k-1]=='N' && (k == len || hap[k] != 'N').
-__device__ __forceinline__ void run_flags(const uint8_t *hap, int64_t len, int64_t k, bool &st, bool &en) {
-  bool cur = k < len && hap[k] == 'N';
-  bool prev = k > 0 && hap[k - 1] == 'N';
-  st = cur && !prev;
-  en = prev && !cur;
+// Element c covers byte positions k in [c*16, c*16+16) ∩ [0, len]; a run starts at k if hap[k]=='N' and
+// hap[k-1] != 'N', and ends (exclusive) at k if hap[k-1]=='N' and (k == len or hap[k] != 'N').
+// 16 bytes per element as one aligned 16-byte load (the haplotype buffer is padded), 'N' found with SWAR.
+__device__ __forceinline__ uint32_t n_bits4(uint32_t w) {
+  const uint32_t t = w ^ 0x4E4E4E4Eu;                                    // zero byte where 'N'
+  const uint32_t nz = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;             // bit 7 of each byte: byte != 0
+  const uint32_t z = ~nz & 0x80808080u;
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+// masks over the 16 positions of element c: starts, ends
+__device__ __forceinline__ void run_masks(const uint8_t *hap, int64_t len, int64_t c, uint32_t &st, uint32_t &en) {
+  const int64_t k0 = c * NCHUNK;
+  uint32_t nm = 0;
+  if (k0 < len) {
+    const uint4 v = *(const uint4 *)(hap + k0);
+    nm = n_bits4(v.x) | (n_bits4(v.y) << 4) | (n_bits4(v.z) << 8) | (n_bits4(v.w) << 12);
+    const int64_t valid = len - k0;                                      // positions >= len are not 'N'
+    if (valid < 16) nm &= (1u << valid) - 1u;
+  }
+  const uint32_t prev = (k0 > 0 && k0 - 1 < len && hap[k0 - 1] == 'N') ? 1u : 0u;
+  const uint32_t sh = ((nm << 1) | prev) & 0xFFFFu;                      // bit i: hap[k0 + i - 1] == 'N'
+  uint32_t pos_mask = 0xFFFFu;                                           // positions k0 + i <= len
+  if (len - k0 < 15) pos_mask = (len - k0 < 0) ? 0u : ((1u << (len - k0 + 1)) - 1u);
+  st = nm & ~sh & pos_mask;
+  en = sh & ~nm & pos_mask;
 }
 
 struct LoadRuns {
   const uint8_t *hap; int64_t len;
   __device__ RunCnt operator()(int64_t c) const {
-    RunCnt r{0, 0};
-    int64_t k0 = c * NCHUNK, k1 = k0 + NCHUNK;
-    if (k1 > len + 1) k1 = len + 1;
-    for (int64_t k = k0; k < k1; k++) {
-      bool st, en;
-      run_flags(hap, len, k, st, en);
-      r.starts += st;
-      r.ends += en;
-    }
-    return r;
+    uint32_t st, en;
+    run_masks(hap, len, c, st, en);
+    return RunCnt{__popc(st), __popc(en)};
   }
 };
 struct StoreRuns {
   const uint8_t *hap; int64_t len; int64_t *rs_out; int64_t *re_out;
   __device__ void operator()(int64_t c, RunCnt, RunCnt excl) const {
-    int64_t k0 = c * NCHUNK, k1 = k0 + NCHUNK;
-    if (k1 > len + 1) k1 = len + 1;
+    uint32_t st, en;
+    run_masks(hap, len, c, st, en);
     int64_t a = excl.starts, b = excl.ends;
-    for (int64_t k = k0; k < k1; k++) {
-      bool st, en;
-      run_flags(hap, len, k, st, en);
-      if (st) rs_out[a++] = k;
-      if (en) re_out[b++] = k;
-    }
+    while (st) { rs_out[a++] = c * NCHUNK + __ffs(st) - 1; st &= st - 1; }
+    while (en) { re_out[b++] = c * NCHUNK + __ffs(en) - 1; en &= en - 1; }
   }
 };
 
