@@ -110,6 +110,15 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_bytes1,
                       int64_t *out_bytes2);
+/* A slice of a unit for multi-GPU sharding: emit only templates [t_begin, t_end) of the current
+ * set, numbering the kept ones from cnt_base + 1 (cnt_base = templates kept before t_begin, e.g. from an all-gather
+ * of mh_count_kept over the ranks' slices).  Concatenating the slices in order reproduces mh_emit_reads byte for
+ * byte, corruption included (its stream is counted by the template's index in the whole unit). */
+int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                            int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
+                            int64_t cnt_base, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2);
+/* Templates in [t_begin, t_end) of the current set that survive the N filter (readgenerate.py:201-204). */
+int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end, int64_t *out_kept);
 int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);
 /* Copy arena bytes [offset, offset+len) of file 1 / file 2 to host (either host pointer may be NULL). */
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t offset1, char *fq1, int64_t len1, int64_t offset2, char *fq2,

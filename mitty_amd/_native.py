@@ -19,7 +19,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
-           'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode']
+           'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
+           'mh_emit_reads_range', 'mh_count_kept']
 
 
 class NativeError(RuntimeError):
@@ -69,6 +70,9 @@ def lib():
   _sig(L, 'mh_set_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32])
   _sig(L, 'mh_get_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
+                                   c_i64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -254,12 +258,26 @@ class Context:
     return fo0[:m], p0[:m], p1[:m]
 
   # ---- emission ----------------------------------------------------------------------------------------
-  def emit_reads(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+  def emit_reads(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, t_range=None, cnt_base=0):
+    """Emit the current templates (or the slice t_range = (t_begin, t_end), kept ones numbered from cnt_base + 1).
+    Returns (kept, bytes1, bytes2)."""
     k, b1, b2 = c_i64(), c_i64(), c_i64()
-    self._chk(self._L.mh_emit_reads(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
-                                    1 if write_fastq2 else 0, int(unit_key), ctypes.byref(k), ctypes.byref(b1),
-                                    ctypes.byref(b2)))
+    if t_range is None:
+      self._chk(self._L.mh_emit_reads(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                      1 if write_fastq2 else 0, int(unit_key), ctypes.byref(k), ctypes.byref(b1),
+                                      ctypes.byref(b2)))
+    else:
+      self._chk(self._L.mh_emit_reads_range(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                            1 if write_fastq2 else 0, int(unit_key), int(t_range[0]),
+                                            int(t_range[1]), int(cnt_base), ctypes.byref(k), ctypes.byref(b1),
+                                            ctypes.byref(b2)))
     return k.value, b1.value, b2.value
+
+  def count_kept(self, slot, t_begin, t_end):
+    """Templates of the current set in [t_begin, t_end) that pass the N filter."""
+    k = c_i64()
+    self._chk(self._L.mh_count_kept(self._h, slot, int(t_begin), int(t_end), ctypes.byref(k)))
+    return k.value
 
   def output_size(self):
     a, b = c_i64(), c_i64()

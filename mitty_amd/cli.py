@@ -1,7 +1,9 @@
 """`mitty` command line (reference mitty/cli.py), MI355X build.
 
 Implemented: generate-reads (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
---rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Out of scope for this build (not on the
+--rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Multi-GPU: launch generate-reads under
+`python -m torch.distributed.run --nproc-per-node N -m mitty_amd.cli generate-reads ...` (one process per GPU,
+RCCL); the output files are identical to the one-GPU run.  Out of scope for this build (not on the
 generate-reads path): filter-variants, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
 """
 import logging
@@ -77,6 +79,19 @@ def generate_reads(fasta, vcf, sample_name, bed, modelfile, coverage, seed, fast
   from mitty_amd.readmodel import get_read_model
   from mitty_amd.simulation import readgenerate
   read_module, model = get_read_model(modelfile)
+  if int(os.environ.get('WORLD_SIZE', '1')) > 1:
+    import torch
+    import torch.distributed as dist
+    from mitty_amd import distributed
+    torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
+    dist.init_process_group('nccl')
+    try:
+      stats = distributed.generate_reads_distributed(fasta, vcf, sample_name, bed, read_module, model, coverage,
+                                                     fastq1, fastq2, seed=seed, rng=rng, corrupt_seed=corrupt_seed)
+    finally:
+      dist.destroy_process_group()
+    logging.info('generate-reads: {}'.format(stats))
+    return
   stats = readgenerate.process_multi_threaded(fasta, vcf, sample_name, bed, read_module, model, coverage, fastq1,
                                               fastq2, threads=threads, seed=seed, device=device, rng=rng,
                                               corrupt_seed=corrupt_seed)

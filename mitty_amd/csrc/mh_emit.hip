@@ -326,9 +326,22 @@ struct LoadRec {
 };
 struct StoreOff {
   E3 *off;
+  int64_t base;   // templates kept before this slice; cnt of the slice's k-th kept template = base + k + 1
   __device__ void operator()(int64_t t, E3, E3 excl) const {
-    int64_t ds = digit_sum(excl.kept);
-    off[t] = E3{excl.kept, excl.b1 + ds, excl.b2 + ds};
+    int64_t ds = digit_sum(base + excl.kept) - digit_sum(base);
+    off[t] = E3{base + excl.kept, excl.b1 + ds, excl.b2 + ds};
+  }
+};
+
+struct LoadKeep {   // N filter only (readgenerate.py:201-204), for mh_count_kept
+  HapView h; const int64_t *pos0, *pos1; int64_t m, rlen;
+  __device__ int64_t operator()(int64_t t) const {
+    if (t >= m) return 0;
+    ReadInfo r[2];
+    read_info(h, pos0[t], rlen, r[0]);
+    read_info(h, pos1[t], rlen, r[1]);
+    return count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+           count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
   }
 };
 
@@ -355,6 +368,7 @@ struct CorruptCfg {
   const double *phred;   // [100]
   int32_t max_bp, n_bq;
   uint32_t k0, k1, c3;   // Philox key and the constant counter word
+  int64_t t_base;        // index of the launch's first template inside its unit (slices: mh_emit_reads_range)
 };
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
@@ -371,6 +385,7 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 
 // illumina.corrupt_single_read for one base (illumina.py:155-160), Philox-driven.
 __device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, int f, int n, uint8_t &b, uint8_t &q) {
+  t += cc.t_base;
   uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ((uint32_t)f << 16) | (uint32_t)n, cc.c3),
                           make_uint2(cc.k0, cc.k1));
   const float u1 = (float)(r.x >> 8) * (1.0f / 16777216.0f);
@@ -804,14 +819,40 @@ HapView view_of(const Hap &h) {
 
 }  // namespace
 
+int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept) {
+  auto tit = ctx->tsets.find(ctx->cur_tpl);
+  if (tit == ctx->tsets.end() || !tit->second.valid)
+    return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
+  const TplSet &tp = tit->second;
+  if (t_end > tp.n) t_end = tp.n;
+  *out_kept = 0;
+  if (t_begin >= t_end) return MH_OK;
+  const int64_t m = t_end - t_begin;
+  hipStream_t st = ctx->stream;
+  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(m) + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int64_t *tot = (int64_t *)ctx->d_small.p;
+  HIPCHK(ctx, device_reduce<int64_t>(st, m, LoadKeep{view_of(h), (const int64_t *)tp.pos0.p + t_begin,
+                                                     (const int64_t *)tp.pos1.p + t_begin, m, tp.rlen},
+                                     OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p, tot));
+  HIPCHK(ctx, hipMemcpyAsync(out_kept, tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return MH_OK;
+}
+
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
-                   int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+                   int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
+                   int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   auto tit = ctx->tsets.find(ctx->cur_tpl);
   if (tit == ctx->tsets.end() || !tit->second.valid)
     return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
   const TplSet &tp = tit->second;
   hipStream_t st = ctx->stream;
-  const int64_t m = tp.n;
+  if (t_end < 0 || t_end > tp.n) t_end = tp.n;
+  if (t_begin > t_end) t_begin = t_end;
+  const int64_t m = t_end - t_begin;
+  const int64_t *pos0 = (const int64_t *)tp.pos0.p + t_begin, *pos1 = (const int64_t *)tp.pos1.p + t_begin;
+  const int8_t *fo0 = (const int8_t *)tp.fo0.p + t_begin;
   const int64_t rlen = tp.rlen;
   std::string prefix = std::string("@") + serial_stub + ":";
   std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
@@ -844,14 +885,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   int32_t *overflow = (int32_t *)(small + 40);
   if (assemble) MH_TRY(ensure(ctx, ctx->emit_slots, (size_t)SLOT * (m + 1)));
   stage_begin(ctx, "emit_measure");
-  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m,
-                     (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p,
+  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
                      rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
                      assemble ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");
-  HIPCHK(ctx, device_scan<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off}, OpSum{}, E3{0, 0, 0},
+  HIPCHK(ctx, device_scan<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, OpSum{}, E3{0, 0, 0},
                               (E3 *)ctx->scan_partials.p, tot));
   stage_end(ctx);
   E3 ht;
@@ -859,6 +899,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipMemcpyAsync(&hmax, max_rec, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  ht.kept -= cnt_base;
 
   // arenas: append after what is already there
   const int64_t need1 = ctx->used1 + ht.b1, need2 = ctx->used2 + (write_fastq2 ? ht.b2 : 0);
@@ -873,7 +914,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   }
   const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
   size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + (size_t)EW_T * 2 * win_stride + 2 * (size_t)(cap + 16);
-  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0};
+  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on) {
     if (rlen > ctx->corrupt_max_bp) {
       stage_end(ctx);
@@ -881,7 +922,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     }
     cc = CorruptCfg{1, (const float *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
                     ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
-                    (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u};
+                    (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u, t_begin};
   }
   if (lds > 160 * 1024) {
     stage_end(ctx);
@@ -901,14 +942,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
                          (size_t)EA_T * SLOT + 4160;
     const int64_t nblk_a = (m + EA_T - 1) / EA_T;
     hipLaunchKernelGGL(k_emit_assemble, dim3((unsigned)nblk_a), dim3(EA_THREADS), lds_a, st, hv, m,
-                       (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p, rlen, q,
+                       pos0, pos1, fo0, rlen, q,
                        (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p, o1, o2, write_fastq2,
                        win_stride, cc);
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot
     const int64_t nblk = (m + EW_T - 1) / EW_T;
     hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
-                       (const int64_t *)tp.pos0.p, (const int64_t *)tp.pos1.p, (const int8_t *)tp.fo0.p, rlen, q,
+                       pos0, pos1, fo0, rlen, q,
                        (const Rec *)recs, (const E3 *)off, o1, o2, write_fastq2, cap, win_stride, cc, err);
   }
   HIPCHK(ctx, hipGetLastError());

@@ -145,7 +145,9 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
                      int32_t rng_mode, int64_t *out_n);
 
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
-                   int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
+                   int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
+                   int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
+int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept);
 
 int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l, int64_t n, int64_t *out_pos,
                    int64_t *out_n0, int64_t *out_n1, char *cigar, int64_t cigar_cap, int64_t *cigar_off,

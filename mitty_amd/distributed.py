@@ -1,0 +1,235 @@
+"""Multi-GPU generate-reads: one process per GPU, torch.distributed over RCCL.
+
+Work units (region, copy, pass) are independent given their rng_seed (reference readgenerate.py:149-154,
+illumina.py:56-58), so the path shards without any data-path collective:
+
+* every rank builds the reference's unit list (A6) itself, so seeds and `ps` do not depend on the GPU count;
+* with at least 2 units per GPU the units are dealt out whole by LPT on region length;
+* with fewer (chr1 = 4 units on 8 GPUs) every rank samples every unit and emits only its slice
+  [m*r/W, m*(r+1)/W) of the unit's templates; the cnt of the slice's first kept template comes from one
+  all-reduce of the per-slice N-filter survivor counts (the only coupling between templates, an exclusive prefix);
+* one more all-reduce of per-piece byte sizes gives every piece its file offset, and each rank pwrites its pieces
+  there, so the files are byte-identical to the single-GPU run (= reference --threads 1) at any GPU count.
+
+The collectives carry a few int64 per piece; no sequence data crosses xGMI.  Outputs must be regular files
+(ranks write at offsets); FIFOs / process substitution need the single-GPU path.
+"""
+import logging
+import os
+import time
+
+from mitty_amd.lib import fasta as mfasta
+from mitty_amd.lib import vcfio
+
+logger = logging.getLogger(__name__)
+
+
+def lpt_assign(weights, world):
+  """Longest-processing-time: items by decreasing weight (ties: lower index first) to the least-loaded rank
+  (ties: lower rank).  Returns owner rank per item."""
+  load = [0] * world
+  owner = [0] * len(weights)
+  for i in sorted(range(len(weights)), key=lambda i: (-weights[i], i)):
+    r = min(range(world), key=lambda r: (load[r], r))
+    owner[i] = r
+    load[r] += weights[i]
+  return owner
+
+
+def plan_pieces(unit_weights, world, layout=None):
+  """Pieces = (unit index, slice, n_slices, owner rank) in output order (unit, slice).
+  layout: None = whole units by LPT when there are >= 2 units per rank, else slices; 'lpt' / 'slice' force one."""
+  n = len(unit_weights)
+  if layout == 'lpt' or (layout is None and (world <= 1 or n >= 2 * world)):
+    owner = lpt_assign(unit_weights, max(world, 1))
+    return [(u, 0, 1, owner[u]) for u in range(n)]
+  return [(u, s, world, s) for u in range(n) for s in range(world)]
+
+
+def slice_range(m, s, n_slices):
+  return m * s // n_slices, m * (s + 1) // n_slices
+
+
+def exclusive_bases(pieces, kept):
+  """cnt base of each piece = templates kept by the earlier slices of the same unit."""
+  base, acc, cur = [], 0, None
+  for (u, s, _, _), k in zip(pieces, kept):
+    if u != cur:
+      cur, acc = u, 0
+    base.append(acc)
+    acc += k
+  return base
+
+
+def file_offsets(sizes):
+  out, acc = [], 0
+  for x in sizes:
+    out.append(acc)
+    acc += x
+  return out, acc
+
+
+def allreduce_i64(vals, group=None):
+  """Sum an int64 vector over ranks (RCCL on GPU tensors under 'nccl', gloo on CPU tensors)."""
+  import torch
+  import torch.distributed as dist
+  if not dist.is_available() or not dist.is_initialized():
+    return [int(v) for v in vals]
+  dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
+  t = torch.tensor([int(v) for v in vals], dtype=torch.int64, device=dev)
+  dist.all_reduce(t, group=group)
+  return [int(v) for v in t.cpu().tolist()]
+
+
+class DeviceBackend:
+  """The per-rank device side: one Engine (HIP context) on this rank's GPU."""
+
+  def __init__(self, device):
+    from mitty_amd.engine import Engine
+    self.eng = Engine(device)
+
+  def set_corruption(self, model, seed):
+    import numpy as np
+    self.eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), seed)
+
+  def load_region(self, ri, region, seq):
+    self.eng.load_region(ri, region, seq)
+
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng):
+    """units: [(ps, ri, cpy, seed)] -> template counts; unit k's set becomes template id k."""
+    from mitty_amd.engine import RNG_MODES
+    self._slots = [self.eng.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    return [int(x) for x in self.eng.ctx.sample_units(list(range(len(units))), self._slots, [u[3] for u in units],
+                                                      p, rlen, cum_tlen, RNG_MODES[rng])]
+
+  def count_kept(self, k, t0, t1):
+    self.eng.ctx.use_templates(k)
+    return self.eng.ctx.count_kept(self._slots[k], t0, t1)
+
+  def emit(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+    """-> (kept, (arena offset, length) for file 1, same for file 2)"""
+    ctx = self.eng.ctx
+    ctx.use_templates(k)
+    u1, u2 = ctx.output_size()
+    kept, b1, b2 = ctx.emit_reads(self._slots[k], stub, chrom, cpy, write2, unit_key, t_range, cnt_base)
+    return kept, (u1, b1), (u2, b2)
+
+  def fetch(self, r1, r2):
+    return self.eng.ctx.fetch_output(r1[0], r1[1], r2[0], r2[1])
+
+  def close(self):
+    self.eng.close()
+
+
+def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
+                               fastq1_fname, fastq2_fname, seed=7, rng='mitty', corrupt_seed=None, backend=None,
+                               group=None, max_batch_draws=200_000_000, layout=None):
+  """process_multi_threaded (readgenerate.py:76-126) over the ranks of the default process group.
+
+  `backend` defaults to DeviceBackend(LOCAL_RANK); tests pass a host stand-in to exercise the orchestration with
+  the gloo backend on CPU.  Returns this rank's stats plus the job totals.
+  """
+  import torch.distributed as dist
+  from mitty_amd.simulation.readgenerate import get_data_for_workers
+  t0 = time.time()
+  rank = dist.get_rank(group) if dist.is_initialized() else 0
+  world = dist.get_world_size(group) if dist.is_initialized() else 1
+  read_model = read_module.read_model_params(model, coverage)
+  vdf = vcfio.load_variants_soa(vcf_fname, sample_name, bed_fname)
+  units = [(ps, w['region_idx'], w['region_cpy'], w['rng_seed'])
+           for ps, w in enumerate(get_data_for_workers(read_model, vdf, seed))]
+  weights = [vdf[ri]['region'][2] - vdf[ri]['region'][1] for _, ri, _, _ in units]
+  pieces = plan_pieces(weights, world, layout)
+  mine = [i for i, pc in enumerate(pieces) if pc[3] == rank]
+  my_units = sorted({pieces[i][0] for i in mine})
+  write2 = fastq2_fname is not None
+
+  if backend is None:
+    backend = DeviceBackend(int(os.environ.get('LOCAL_RANK', '0')))
+  if corrupt_seed is not None:
+    backend.set_corruption(model, corrupt_seed)
+  regions = sorted({units[u][1] for u in my_units})
+  if regions:
+    seqs = mfasta.read_fasta(fasta_fname, names={vdf[ri]['region'][0] for ri in regions})
+    for ri in regions:
+      chrom, s0, e = vdf[ri]['region']
+      backend.load_region(ri, vdf[ri]['region'], mfasta.fetch(seqs, chrom, s0, e))
+
+  # batches of this rank's units; in the sliced layout every rank holds every unit, so the batches (and the
+  # per-batch all-reduce of slice survivor counts) line up across ranks
+  sliced = any(pc[2] > 1 for pc in pieces)
+  batches, cur, draws = [], [], 0
+  for u in my_units:
+    ri = units[u][1]
+    cur.append(u)
+    draws += int(weights[u] * read_model['p'] * 1.2)
+    if draws >= max_batch_draws or u == my_units[-1]:
+      batches.append(cur)
+      cur, draws = [], 0
+
+  emitted = {}   # piece index -> (kept, range1, range2)
+  stats = {'units': len(units), 'pieces': len(mine), 'templates': 0, 'kept': 0}
+  soa_of = lambda r, c: vdf[r]['copies'][c]
+  for batch in batches:
+    ns = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
+                        read_model['cum_tlen'], rng)
+    k_of = {u: k for k, u in enumerate(batch)}
+    bases = {}
+    if sliced:
+      local = [0] * len(pieces)
+      for i in mine:
+        u, s, S, _ = pieces[i]
+        if u in k_of:
+          local[i] = backend.count_kept(k_of[u], *slice_range(ns[k_of[u]], s, S))
+      kept_all = allreduce_i64(local, group)
+      bases = dict(enumerate(exclusive_bases(pieces, kept_all)))
+    for i in mine:
+      u, s, S, _ = pieces[i]
+      if u not in k_of:
+        continue
+      ps, ri, cpy, useed = units[u]
+      k = k_of[u]
+      rng_range = slice_range(ns[k], s, S) if S > 1 else None
+      emitted[i] = backend.emit(k, '{}:{}:{}'.format(sample_name, 0, ps), vdf[ri]['region'][0], cpy, write2, useed,
+                                rng_range, bases.get(i, 0))
+      stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k]
+      stats['kept'] += emitted[i][0]
+
+  # file offsets of every piece, then positioned writes
+  sz = [0] * (2 * len(pieces))
+  for i, (_, r1, r2) in emitted.items():
+    sz[2 * i], sz[2 * i + 1] = r1[1], r2[1]
+  sz = allreduce_i64(sz + [stats['templates'], stats['kept']], group)
+  tot_templates, tot_kept = sz[-2], sz[-1]
+  off1, total1 = file_offsets(sz[0:2 * len(pieces):2])
+  off2, total2 = file_offsets(sz[1:2 * len(pieces):2])
+  fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
+  if rank == 0:
+    for fn, total in zip(fnames, (total1, total2)):
+      with open(fn, 'wb') as fp:
+        fp.truncate(total)
+  if world > 1:
+    dist.barrier(group)
+  fds = [os.open(fn, os.O_WRONLY) for fn in fnames]
+  try:
+    for i in sorted(emitted):
+      _, r1, r2 = emitted[i]
+      d1, d2 = backend.fetch(r1, r2 if write2 else (0, 0))
+      _pwrite_all(fds[0], d1, off1[i])
+      if write2:
+        _pwrite_all(fds[1], d2, off2[i])
+  finally:
+    for fd in fds:
+      os.close(fd)
+  if world > 1:
+    dist.barrier(group)
+  stats.update({'job_templates': tot_templates, 'job_kept': tot_kept, 'bytes1': total1,
+                'bytes2': total2 if write2 else 0, 'seconds': time.time() - t0, 'rank': rank, 'world': world})
+  return stats
+
+
+def _pwrite_all(fd, data, off):
+  mv = memoryview(data)
+  while len(mv):
+    n = os.pwrite(fd, mv, off)
+    mv, off = mv[n:], off + n

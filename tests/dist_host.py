@@ -1,0 +1,55 @@
+"""Host stand-in for DeviceBackend (test infrastructure): per-unit FASTQ from the CPU oracle, so the multi-rank
+orchestration of mitty_amd.distributed (plan, slice counts, cnt bases, file offsets, pwrite) runs with gloo on CPU.
+Every oracle record is a kept template, and the stand-in renumbers cnt from the base it is given, so a wrong
+cnt_base or offset shows up as a byte difference against the single-process output."""
+from oracle import oracle as O
+
+
+class OracleBackend:
+  def __init__(self):
+    self.regions = {}
+    self.arena = [bytearray(), bytearray()]
+
+  def set_corruption(self, model, seed):
+    raise NotImplementedError
+
+  def load_region(self, ri, region, seq):
+    self.regions[ri] = (region, seq)
+
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng):
+    self.recs = []
+    for ps, ri, cpy, seed in units:
+      (chrom, s0, _), seq = self.regions[ri]
+      _, b1, b2 = O.generate_unit_soa(seq, s0, soa_of(ri, cpy), p, rlen, cum_tlen, seed, 'X:0:0', chrom, cpy)
+      self.recs.append((_records(b1), _records(b2)))
+    return [len(r[0]) for r in self.recs]
+
+  def count_kept(self, k, t0, t1):
+    return t1 - t0
+
+  def emit(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+    r1, r2 = self.recs[k]
+    t0, t1 = t_range if t_range is not None else (0, len(r1))
+    out = []
+    for f, recs in enumerate((r1, r2)):
+      if f == 1 and not write2:
+        out.append((len(self.arena[1]), 0))
+        continue
+      data = b''.join(b'@' + stub.encode() + b':' + str(cnt_base + j + 1).encode() + b'|' + recs[t0 + j]
+                      for j in range(t1 - t0))
+      out.append((len(self.arena[f]), len(data)))
+      self.arena[f] += data
+    return t1 - t0, out[0], out[1]
+
+  def fetch(self, r1, r2):
+    return bytes(self.arena[0][r1[0]:r1[0] + r1[1]]), bytes(self.arena[1][r2[0]:r2[0] + r2[1]])
+
+  def close(self):
+    pass
+
+
+def _records(b):
+  """FASTQ bytes -> records with the '@{stub}:{cnt}|' head stripped."""
+  lines = b.split(b'\n')
+  return [lines[i].split(b'|', 1)[1] + b'\n' + b'\n'.join(lines[i + 1:i + 4]) + b'\n'
+          for i in range(0, len(lines) - 1, 4)]

@@ -362,3 +362,68 @@ def test_corruption_statistics(native, tmp_path):
     assert abs(err.mean() - exp) < 0.1 * exp + 1e-4
     changed = SC[err]
     assert not np.any(changed == SA[err])
+
+
+# ---- multi-GPU slices ---------------------------------------------------------------------------
+@pytest.mark.parametrize('corrupt', [False, True])
+def test_emit_slices_concatenate_to_unit(native, corrupt):
+  """mh_emit_reads_range over consecutive slices, each numbered from the kept count of the slices before it
+  (mh_count_kept), concatenates to the whole-unit emission byte for byte (corruption keyed by the unit index)."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  seq = synth.contig(2_500_000, 31)
+  copies = synth.copies_soa(synth.variants(seq, 32))
+  eng = Engine(0)
+  try:
+    if corrupt:
+      eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 5)
+    eng.load_region(0, ('1', 0, len(seq)), seq)
+    slot = eng.haplotype(0, 0, copies[0])[0]
+    n = int(eng.ctx.sample_units([0], [slot], [4242], p, 150, mdl['cum_tlen'])[0])
+    eng.ctx.use_templates(0)
+    kept, b1, b2 = eng.ctx.emit_reads(slot, 'S:0:1', '1', 0, True, 4242)
+    whole = eng.ctx.fetch_output()
+    eng.ctx.reset_output()
+    assert eng.ctx.count_kept(slot, 0, n) == kept
+    cuts = [0, 1, 1, 777, n // 3, n - 5, n]
+    base = 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+      k, _, _ = eng.ctx.emit_reads(slot, 'S:0:1', '1', 0, True, 4242, t_range=(a, b), cnt_base=base)
+      assert k == eng.ctx.count_kept(slot, a, b)
+      base += k
+    assert base == kept
+    assert eng.ctx.fetch_output() == whole
+  finally:
+    eng.close()
+
+
+def _gpu_rank(rank, world, port, layout, outdir):
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    from mitty_amd import distributed as D
+    from mitty_amd.readmodel import get_read_model
+    c = G.load_json('e2e_config.json')['1kg-pcr-free']
+    mod, mdl = get_read_model('1kg-pcr-free.pkl')
+    D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                 c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
+                                 seed=c['seed'], backend=D.DeviceBackend(0), layout=layout)
+  finally:
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('layout', ['lpt', 'slice'])
+def test_distributed_two_ranks_one_gpu(native, tmp_path, layout):
+  """Two ranks (gloo for the int64 exchanges, both on GPU 0) write the reference --threads 1 files."""
+  import socket
+  import torch.multiprocessing as mp
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  mp.start_processes(_gpu_rank, args=(2, port, layout, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+  assert open(tmp_path / 'r1.fq', 'rb').read() == G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz')
+  assert open(tmp_path / 'r2.fq', 'rb').read() == G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz')
