@@ -134,6 +134,28 @@ int32_t mh_read_batch(mh_ctx *ctx, int32_t slot, const int64_t *p, const int64_t
                       char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
                       char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used);
 
+/* ---- god-aligner: perfect-alignment BAM (god_aligner.py:19-183, cli.py:183-204) ------------------------------
+ * write_perfect_reads per template (god_aligner.py:153-183) on the device, then samtools sort's coordinate order
+ * (stable on (tid, pos+1, is_reverse)), BGZF and a BAI (pysam.sort / pysam.index, god_aligner.py:117-131).
+ *   mh_bam_set_refs     @SQ names (NUL-separated, n_refs of them) and lengths, from <fasta>.ann (parse_ann :31-40);
+ *                       clears the record store
+ *   mh_bam_add_fastq    host FASTQ bytes, file 2 optional (NULL = single-end): every complete template in the
+ *                       buffers (at most max_templates; -1 = all) becomes 1 or 2 records.  *used1 / *used2 = bytes
+ *                       consumed (whole records), so the caller carries the rest into the next call.  Read names
+ *                       longer than 254 characters, chroms missing from the header and unparseable qnames are
+ *                       MH_E_ARG (the reference raises in pysam / parse_qname)
+ *   mh_bam_add_output   the same from this context's FASTQ arenas (mh_emit_reads output, no host round trip)
+ *   mh_bam_write        sort, write `bam_path` (BGZF, deflate `level` 0..9 on `threads` host threads) with the
+ *                       header text, and the BAI at `bai_path` (NULL = none) */
+int32_t mh_bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);
+int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2,
+                         int64_t max_templates, int64_t *used1, int64_t *used2, int64_t *templates);
+int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates);
+int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes);
+int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
+                     int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
+int32_t mh_bam_reset(mh_ctx *ctx);
+
 /* ---- corruption (Philox mode) -------------------------------------------------------------------------- */
 /* Configure the empirical-BQ corruption (illumina.corrupt_template, illumina.py:113-162) that mh_emit_reads then
  * applies while it writes each record: per base bq = min(searchsorted(cum_bq[file][n], U1), 93), the base replaced

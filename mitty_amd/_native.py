@@ -20,7 +20,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
-           'mh_emit_reads_range', 'mh_count_kept']
+           'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
+           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset']
 
 
 class NativeError(RuntimeError):
@@ -73,6 +74,13 @@ def lib():
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
+  _sig(L, 'mh_bam_set_refs', [c_vp, c_i32, ctypes.c_char_p, c_vp])
+  _sig(L, 'mh_bam_add_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_bam_add_output', [c_vp, c_i64, P_i64])
+  _sig(L, 'mh_bam_records', [c_vp, P_i64, P_i64])
+  _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
+                           P_i64])
+  _sig(L, 'mh_bam_reset', [c_vp])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -295,6 +303,42 @@ class Context:
 
   def reset_output(self):
     self._chk(self._L.mh_output_reset(self._h))
+
+  # ---- god-aligner BAM ----
+  def bam_set_refs(self, names, lengths):
+    blob = b''.join(n.encode() + b'\0' for n in names)
+    ln = np.ascontiguousarray(lengths, dtype=np.int64)
+    self._chk(self._L.mh_bam_set_refs(self._h, len(names), blob, _ptr(ln) if len(names) else None))
+
+  def bam_add_fastq(self, fq1, fq2=None, max_templates=-1):
+    """Parse the complete templates of FASTQ byte buffers into BAM records.  Returns (used1, used2, templates)."""
+    u1, u2, t = c_i64(), c_i64(), c_i64()
+    a1 = np.frombuffer(fq1, np.uint8) if len(fq1) else np.zeros(1, np.uint8)
+    a2 = None if fq2 is None else (np.frombuffer(fq2, np.uint8) if len(fq2) else np.zeros(1, np.uint8))
+    self._chk(self._L.mh_bam_add_fastq(self._h, _ptr(a1), len(fq1), None if a2 is None else _ptr(a2),
+                                       0 if fq2 is None else len(fq2), int(max_templates), ctypes.byref(u1),
+                                       ctypes.byref(u2), ctypes.byref(t)))
+    return u1.value, u2.value, t.value
+
+  def bam_add_output(self, max_templates=-1):
+    t = c_i64()
+    self._chk(self._L.mh_bam_add_output(self._h, int(max_templates), ctypes.byref(t)))
+    return t.value
+
+  def bam_records(self):
+    n, b = c_i64(), c_i64()
+    self._chk(self._L.mh_bam_records(self._h, ctypes.byref(n), ctypes.byref(b)))
+    return n.value, b.value
+
+  def bam_write(self, bam_path, header_text, level=6, threads=4, bai_path=None):
+    n, b = c_i64(), c_i64()
+    h = header_text.encode()
+    self._chk(self._L.mh_bam_write(self._h, bam_path.encode(), h, len(h), int(level), int(threads),
+                                   None if bai_path is None else bai_path.encode(), ctypes.byref(n), ctypes.byref(b)))
+    return n.value, b.value
+
+  def bam_reset(self):
+    self._chk(self._L.mh_bam_reset(self._h))
 
   def read_batch(self, slot, p, l):
     p = np.ascontiguousarray(p, dtype=np.int64)

@@ -1,10 +1,10 @@
 """`mitty` command line (reference mitty/cli.py), MI355X build.
 
-Implemented: generate-reads (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
+Implemented: generate-reads (GPU), god-aligner (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
 --rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Multi-GPU: launch generate-reads under
 `python -m torch.distributed.run --nproc-per-node N -m mitty_amd.cli generate-reads ...` (one process per GPU,
 RCCL); the output files are identical to the one-GPU run.  Out of scope for this build (not on the
-generate-reads path): filter-variants, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
+generate-reads path): filter-variants, filter-bam, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
 """
 import logging
 import os
@@ -96,6 +96,24 @@ def generate_reads(fasta, vcf, sample_name, bed, modelfile, coverage, seed, fast
                                               fastq2, threads=threads, seed=seed, device=device, rng=rng,
                                               corrupt_seed=corrupt_seed)
   logging.info('generate-reads: {}'.format(stats))
+
+
+@cli.command('god-aligner', short_help='Create a perfect BAM from simulated FASTQs')
+@click.argument('fasta', type=click.Path(exists=True))
+@click.argument('fastq1', type=click.Path(exists=True))
+@click.argument('bam')
+@click.option('--fastq2', type=click.Path(exists=True), help='If a paired-end FASTQ, second file goes here')
+@click.option('--sample-name', help='If supplied, this is put into the BAM header')
+@click.option('--max-templates', type=int, help='For debugging: quits after processing these many templates')
+@click.option('--threads', default=2)
+@click.option('--device', default=0, help='HIP device ordinal')
+def god_aligner(fasta, bam, sample_name, fastq1, fastq2, max_templates, threads, device):
+  """Given a FASTA.ann file and FASTQ made of simulated reads,
+     construct a perfectly aligned BAM from them (reference cli.py:183-204).
+
+     Note: The program uses the fasta.ann file to construct the BAM header"""
+  from mitty_amd.benchmarking import god_aligner as god
+  god.process_multi_threaded(fasta, bam, fastq1, fastq2, threads, max_templates, sample_name, device=device)
 
 
 def main():

@@ -2,6 +2,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "mh_bgzf.h"
 #include "mh_internal.h"
 
 namespace mh {
@@ -153,6 +154,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2); release(ctx->emit_slots);
+  bam_release(ctx->bam);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return MH_OK;
@@ -516,6 +518,81 @@ int32_t mh_stage_times(mh_ctx *ctx, const char **names, double *ms, int32_t cap,
   }
   *n = k;
   if (names || ms) ctx->last_times.clear();   // a size query (both NULL) keeps them
+  return MH_OK;
+}
+
+// ---- god-aligner BAM (mh_bam.hip, mh_bgzf.cpp) ----------------------------------------------------------------
+int32_t mh_bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths) {
+  CTX_GUARD(ctx);
+  if (n_refs < 0 || (n_refs > 0 && (!names || !lengths))) return arg_fail(ctx, MH_E_ARG, "bad reference list");
+  bam_release(ctx->bam);
+  return bam_set_refs(ctx, n_refs, names, lengths);
+}
+
+static int32_t stage_in(mh_ctx *ctx, DevBuf &b, const char *src, int64_t len) {
+  MH_TRY(ensure(ctx, b, (size_t)len + 64));
+  if (len) HIPCHK(ctx, hipMemcpyAsync(b.p, src, len, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync((char *)b.p + len, 0, 64, ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2,
+                         int64_t max_templates, int64_t *used1, int64_t *used2, int64_t *templates) {
+  CTX_GUARD(ctx);
+  if (!fq1 || len1 < 0 || (fq2 && len2 < 0) || !used1 || !used2 || !templates)
+    return arg_fail(ctx, MH_E_ARG, "null argument");
+  MH_TRY(stage_in(ctx, ctx->bam.in1, fq1, len1));
+  if (fq2) MH_TRY(stage_in(ctx, ctx->bam.in2, fq2, len2));
+  return bam_add(ctx, (const uint8_t *)ctx->bam.in1.p, len1, fq2 ? (const uint8_t *)ctx->bam.in2.p : nullptr,
+                 fq2 ? len2 : 0, max_templates, used1, used2, templates);
+}
+
+int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates) {
+  CTX_GUARD(ctx);
+  if (!templates) return arg_fail(ctx, MH_E_ARG, "null argument");
+  int64_t u1 = 0, u2 = 0;
+  const bool two = ctx->used2 > 0;
+  return bam_add(ctx, (const uint8_t *)ctx->out1.p, ctx->used1, two ? (const uint8_t *)ctx->out2.p : nullptr,
+                 two ? ctx->used2 : 0, max_templates, &u1, &u2, templates);
+}
+
+int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes) {
+  if (!ctx) return MH_E_ARG;
+  if (n_records) *n_records = ctx->bam.n_rec;
+  if (bytes) *bytes = ctx->bam.bytes;
+  return MH_OK;
+}
+
+int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
+                     int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  if (level < 0 || level > 9) return arg_fail(ctx, MH_E_ARG, "compression level must be 0..9");
+  MH_TRY(bam_sort(ctx));
+  const int64_t n = B.n_rec;
+  std::vector<uint8_t> recs((size_t)B.bytes + 1);
+  std::vector<int64_t> soff((size_t)n + 1, 0);
+  std::vector<BaiRec> info((size_t)n + 1);
+  MH_TRY(bam_fetch_sorted(ctx, recs.data(), soff.data(), (int32_t *)info.data()));
+  const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
+                                           B.ref_names, B.ref_len);
+  std::vector<int64_t> coff;
+  std::string err;
+  if (!bgzf_write(bam_path, hdr, recs.data(), B.bytes, level, threads, coff, err))
+    return arg_fail(ctx, MH_E_ARG, err);
+  if (bai_path && !bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
+    return arg_fail(ctx, MH_E_ARG, err);
+  if (out_records) *out_records = n;
+  if (out_bytes) *out_bytes = B.bytes;
+  return MH_OK;
+}
+
+int32_t mh_bam_reset(mh_ctx *ctx) {
+  if (!ctx) return MH_E_ARG;
+  ctx->bam.n_rec = ctx->bam.bytes = 0;
+  ctx->bam.n_files = 0;
   return MH_OK;
 }
 

@@ -1,0 +1,549 @@
+// mh_bam.hip — the god-aligner's perfect-alignment BAM (reference mitty/benchmarking/god_aligner.py:19-183) on the
+// device: SURVEY.md §8(a) A16 / §8(f) rank 1.
+//
+//   FASTQ bytes (host chunks, or the context's own FASTQ arenas)
+//     -> newline positions           (SWAR '\n' count per 16-byte chunk, one device scan, positions stored)
+//     -> k_bam_parse                 (thread per template: parse_qname of file 1's name (readgenerate.py:259-291),
+//                                     the CIGAR, tid from the @SQ names, seq / qual spans; BAM record sizes)
+//     -> scan of record sizes        (appends to the resident record store)
+//     -> k_bam_write                 (wave per record: core fields, name, CIGAR, 4-bit seq (reverse-complemented
+//                                     for strand 1 with the ATCGN-only table), qual - 33 (reversed for strand 1))
+//   finish:
+//     -> stable radix sort of (tid, pos + 1, is_reverse)  (samtools sort's coordinate order, input order on ties)
+//     -> k_bam_gather                (records into sorted order + per-record index info)
+//     -> host: BGZF deflate on a thread pool, BAI from the virtual offsets (mh_bgzf.cpp)
+//
+// Record attributes follow write_perfect_reads (god_aligner.py:153-183): pos = qname pos - 1, CIGAR from the qname
+// ('>p:nI' -> 'nI'), MAPQ 60, flag = reverse | paired / proper / read1 / read2 for two files, mate = the other
+// read's tid / pos, TLEN 0, no tags, qname = file 1's read name.  bin = reg2bin(pos, bam_endpos) as htslib sets it.
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "mh_internal.h"
+#include "mh_scan.h"
+
+namespace mh {
+namespace {
+
+constexpr int BAM_MAX_READS = 2;
+
+struct BamRead {
+  int64_t seq_off, qual_off;   // into the file's buffer
+  int32_t tid, pos, end;       // end = bam_endpos (pos + reference span, at least 1)
+  int32_t l_seq, cig_off, cig_len;   // cig_* relative to the qname start
+  int32_t size;                // BAM record bytes including block_size
+  uint16_t flag, bin, n_cig;
+  uint16_t pad;
+};
+
+struct BamTpl {
+  int64_t qn_off;    // qname start in file 1 (after '@')
+  int32_t qn_len;
+  int32_t n_reads;
+  BamRead r[BAM_MAX_READS];
+};
+
+struct RInfo {       // per record, for the BAI
+  int32_t tid, beg, end;
+  uint32_t bin;
+};
+
+// ---- newline index ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t nl_mask4(uint32_t v) {   // 0x80 in every byte equal to '\n'
+  uint32_t x = v ^ 0x0a0a0a0au;
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+
+struct LoadNL {
+  const uint8_t *b;
+  int64_t len;
+  __device__ int64_t operator()(int64_t t) const {
+    const int64_t o = t * 16;
+    if (o >= len) return 0;
+    if (o + 16 <= len) {
+      uint4 v = *(const uint4 *)(b + o);
+      return __popc(nl_mask4(v.x)) + __popc(nl_mask4(v.y)) + __popc(nl_mask4(v.z)) + __popc(nl_mask4(v.w));
+    }
+    int64_t c = 0;
+    for (int64_t i = o; i < len; i++) c += b[i] == '\n';
+    return c;
+  }
+};
+
+struct StoreNL {
+  const uint8_t *b;
+  int64_t len;
+  int64_t *nl;
+  __device__ void operator()(int64_t t, int64_t, int64_t excl) const {
+    const int64_t o = t * 16;
+    if (o >= len) return;
+    if (o + 16 <= len) {
+      uint4 v = *(const uint4 *)(b + o);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t m = nl_mask4(w[k]);
+        while (m) {
+          int bit = __ffs(m) - 1;
+          nl[excl++] = o + 4 * k + (bit >> 3);
+          m &= m - 1;
+        }
+      }
+      return;
+    }
+    for (int64_t i = o; i < len; i++)
+      if (b[i] == '\n') nl[excl++] = i;
+  }
+};
+
+// ---- parsing ----------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int cigar_code(uint8_t c) {   // BAM_CIGAR_STR "MIDNSHP=X"
+  switch (c) {
+    case 'M': return 0; case 'I': return 1; case 'D': return 2; case 'N': return 3; case 'S': return 4;
+    case 'H': return 5; case 'P': return 6; case '=': return 7; case 'X': return 8;
+    default: return -1;
+  }
+}
+__device__ __forceinline__ bool cigar_consumes_ref(int op) { return op == 0 || op == 2 || op == 3 || op == 7 || op == 8; }
+
+// hts_reg2bin(beg, end, 14, 5)
+__device__ __forceinline__ uint32_t reg2bin(int64_t beg, int64_t end) {
+  --end;
+  if (beg >> 14 == end >> 14) return ((1 << 15) - 1) / 7 + (uint32_t)(beg >> 14);
+  if (beg >> 17 == end >> 17) return ((1 << 12) - 1) / 7 + (uint32_t)(beg >> 17);
+  if (beg >> 20 == end >> 20) return ((1 << 9) - 1) / 7 + (uint32_t)(beg >> 20);
+  if (beg >> 23 == end >> 23) return ((1 << 6) - 1) / 7 + (uint32_t)(beg >> 23);
+  if (beg >> 26 == end >> 26) return ((1 << 3) - 1) / 7 + (uint32_t)(beg >> 26);
+  return 0;
+}
+
+// int() of a decimal field; false if empty or not all digits (optional leading '-')
+__device__ __forceinline__ bool parse_int(const uint8_t *s, int32_t n, int64_t &v) {
+  if (n <= 0) return false;
+  int i = 0;
+  bool neg = false;
+  if (s[0] == '-' || s[0] == '+') { neg = s[0] == '-'; i = 1; }
+  if (i >= n) return false;
+  int64_t x = 0;
+  for (; i < n; i++) {
+    uint32_t d = (uint32_t)s[i] - '0';
+    if (d > 9) return false;
+    x = x * 10 + d;
+  }
+  v = neg ? -x : x;
+  return true;
+}
+
+enum { BE_QNAME = 1, BE_CHROM = 2, BE_FIELDS = 4, BE_CIGAR = 8, BE_QNAME_LEN = 16, BE_SEQ = 32 };
+
+struct ParseArgs {
+  const uint8_t *b[BAM_MAX_READS];
+  const int64_t *nl[BAM_MAX_READS];
+  int32_t n_files;
+  const char *names;          // @SQ names, concatenated
+  const int32_t *name_off;    // [n_refs + 1]
+  int32_t n_refs;
+};
+
+__device__ __forceinline__ int64_t line_start(const int64_t *nl, int64_t line) { return line == 0 ? 0 : nl[line - 1] + 1; }
+
+__global__ void __launch_bounds__(256) k_bam_parse(ParseArgs a, int64_t T, BamTpl *tpl, int32_t *err) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  BamTpl o;
+  const uint8_t *b0 = a.b[0];
+  const int64_t s0 = line_start(a.nl[0], 4 * t);
+  const int64_t e0 = a.nl[0][4 * t];
+  int32_t e = 0;
+  if (e0 <= s0 || b0[s0] != '@') e |= BE_QNAME;
+  int64_t q0 = s0 + 1, q1 = q0;
+  while (q1 < e0 && b0[q1] != ' ' && b0[q1] != '\t') q1++;   // FastxFile name: up to the first whitespace
+  o.qn_off = q0;
+  o.qn_len = (int32_t)(q1 - q0);
+  if (o.qn_len > 254) e |= BE_QNAME_LEN;
+  o.n_reads = a.n_files;
+  // split on '|': rid, chrom, cpy, then (strand, pos, rlen, cigar, v_list) per read
+  int32_t fs[3 + 5 * BAM_MAX_READS], fe[3 + 5 * BAM_MAX_READS];
+  int nf = 0;
+  {
+    int64_t st = q0;
+    for (int64_t i = q0; i <= q1 && nf < 3 + 5 * BAM_MAX_READS; i++) {
+      if (i == q1 || b0[i] == '|') {
+        fs[nf] = (int32_t)(st - q0);
+        fe[nf] = (int32_t)(i - q0);
+        nf++;
+        st = i + 1;
+      }
+    }
+  }
+  if (nf < 3 + 5 * a.n_files - 1) e |= BE_FIELDS;   // the last read's v_list may be the (empty) tail
+  const uint8_t *qn = b0 + q0;
+  // chrom -> tid
+  int32_t tid = -1;
+  if (!(e & BE_FIELDS)) {
+    const int32_t cl = fe[1] - fs[1];
+    for (int32_t r = 0; r < a.n_refs && tid < 0; r++) {
+      const int32_t no = a.name_off[r], nl = a.name_off[r + 1] - no;
+      if (nl != cl) continue;
+      bool eq = true;
+      for (int32_t k = 0; k < cl && eq; k++) eq = a.names[no + k] == (char)qn[fs[1] + k];
+      if (eq) tid = r;
+    }
+    if (tid < 0) e |= BE_CHROM;
+  }
+  for (int s = 0; s < a.n_files && !e; s++) {
+    BamRead &r = o.r[s];
+    const int f = 3 + 5 * s;
+    int64_t strand, pos;
+    if (!parse_int(qn + fs[f], fe[f] - fs[f], strand) || !parse_int(qn + fs[f + 1], fe[f + 1] - fs[f + 1], pos)) {
+      e |= BE_FIELDS;
+      break;
+    }
+    int32_t cs = fs[f + 3], ce = fe[f + 3];
+    if (ce > cs && qn[cs] == '>') {   // '>p:nI' -> 'nI' (parse_qname: split(':')[-1])
+      int32_t k = ce;
+      while (k > cs && qn[k - 1] != ':') k--;
+      cs = k;
+    }
+    int32_t n_cig = 0;
+    int64_t ref_span = 0, num = 0;
+    bool have = false;
+    for (int32_t k = cs; k < ce; k++) {
+      uint32_t d = (uint32_t)qn[k] - '0';
+      if (d <= 9) { num = num * 10 + d; have = true; continue; }
+      int op = cigar_code(qn[k]);
+      if (op < 0 || !have) { e |= BE_CIGAR; break; }
+      if (cigar_consumes_ref(op)) ref_span += num;
+      n_cig++;
+      num = 0;
+      have = false;
+    }
+    if (have) e |= BE_CIGAR;
+    const int64_t ls = line_start(a.nl[s], 4 * t + 1), le = a.nl[s][4 * t + 1];
+    const int64_t qs = line_start(a.nl[s], 4 * t + 3), qe = a.nl[s][4 * t + 3];
+    r.seq_off = ls;
+    r.qual_off = qs;
+    r.l_seq = (int32_t)(le - ls);
+    if (qe - qs != le - ls) e |= BE_SEQ;
+    r.tid = tid;
+    r.pos = (int32_t)(pos - 1);
+    r.end = (int32_t)(r.pos + (ref_span > 0 ? ref_span : 1));
+    r.bin = (uint16_t)reg2bin(r.pos, r.end);
+    r.cig_off = cs;
+    r.cig_len = ce - cs;
+    r.n_cig = (uint16_t)n_cig;
+    r.flag = strand ? 0x10 : 0;
+    if (a.n_files == 2) r.flag |= 0x1 | 0x2 | (s == 0 ? 0x40 : 0x80);
+    r.size = 4 + 32 + (o.qn_len + 1) + 4 * n_cig + (r.l_seq + 1) / 2 + r.l_seq;
+  }
+  tpl[t] = o;
+  if (e) atomicOr(err, e);
+}
+
+struct LoadSize {
+  const BamTpl *tpl;
+  int32_t nr;
+  int64_t n;   // records
+  __device__ int64_t operator()(int64_t i) const { return i < n ? tpl[i / nr].r[i % nr].size : 0; }
+};
+struct StoreOff64 {
+  int64_t *off;
+  int64_t base;
+  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { off[i] = base + excl; }
+};
+
+__device__ __forceinline__ uint8_t nt16(uint8_t c) {   // htslib seq_nt16_table
+  switch (c | 0x20) {
+    case 'a': return 1; case 'c': return 2; case 'm': return 3; case 'g': return 4; case 'r': return 5;
+    case 's': return 6; case 'v': return 7; case 't': case 'u': return 8; case 'w': return 9; case 'y': return 10;
+    case 'h': return 11; case 'k': return 12; case 'd': return 13; case 'b': return 14;
+    default: return c == '=' ? 0 : 15;
+  }
+}
+__device__ __forceinline__ uint8_t comp_atcgn(uint8_t c) {   // str.maketrans('ATCGN', 'TAGCN')
+  return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
+}
+
+// One wave per record.  Records are byte-packed (BAM has no padding), so stores are bytewise.
+__global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tpl, int64_t n_rec, int32_t nr,
+                                                   const int64_t *off, int64_t off_base, uint8_t *out, uint64_t *key,
+                                                   uint32_t *val, RInfo *info, int64_t rec_base) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n_rec) return;
+  const int64_t t = i / nr;
+  const int s = (int)(i % nr);
+  const BamTpl &T = tpl[t];
+  const BamRead &r = T.r[s];
+  const BamRead &m = T.r[nr == 2 ? 1 - s : s];
+  uint8_t *d = out + (off[i] - off_base);
+  const uint8_t *qn = a.b[0] + T.qn_off;
+  const int32_t lq = T.qn_len + 1;
+  const int32_t hdr = 36;
+  if (lane < 9) {
+    int32_t w;
+    switch (lane) {
+      case 0: w = r.size - 4; break;
+      case 1: w = r.tid; break;
+      case 2: w = r.pos; break;
+      case 3: w = (int32_t)((uint32_t)r.bin << 16 | 60u << 8 | (uint32_t)lq); break;
+      case 4: w = (int32_t)((uint32_t)r.flag << 16 | r.n_cig); break;
+      case 5: w = r.l_seq; break;
+      case 6: w = nr == 2 ? m.tid : -1; break;
+      case 7: w = nr == 2 ? m.pos : -1; break;
+      default: w = 0; break;   // TLEN
+    }
+    uint8_t *p = d + 4 * lane;
+    p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
+  }
+  for (int32_t k = lane; k < lq; k += 64) d[hdr + k] = k < T.qn_len ? qn[k] : 0;
+  // CIGAR: lane 0 walks the text (short), writes packed ops
+  uint8_t *dc = d + hdr + lq;
+  if (lane == 0) {
+    uint32_t num = 0;
+    int j = 0;
+    for (int32_t k = r.cig_off; k < r.cig_off + r.cig_len; k++) {
+      uint32_t dd = (uint32_t)qn[k] - '0';
+      if (dd <= 9) { num = num * 10 + dd; continue; }
+      uint32_t w = num << 4 | (uint32_t)cigar_code(qn[k]);
+      dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
+      dc[4 * j + 3] = (uint8_t)(w >> 24);
+      j++;
+      num = 0;
+    }
+  }
+  const uint8_t *sq = a.b[s] + r.seq_off, *ql = a.b[s] + r.qual_off;
+  const int32_t L = r.l_seq;
+  const bool rev = r.flag & 0x10;
+  uint8_t *ds = dc + 4 * r.n_cig;
+  for (int32_t k = lane; k < (L + 1) / 2; k += 64) {
+    const int32_t i0 = 2 * k, i1 = 2 * k + 1;
+    uint8_t c0 = rev ? comp_atcgn(sq[L - 1 - i0]) : sq[i0];
+    uint8_t hi = nt16(c0), lo = 0;
+    if (i1 < L) lo = nt16(rev ? comp_atcgn(sq[L - 1 - i1]) : sq[i1]);
+    ds[k] = (uint8_t)(hi << 4 | lo);
+  }
+  uint8_t *dq = ds + (L + 1) / 2;
+  for (int32_t k = lane; k < L; k += 64) dq[k] = (uint8_t)((rev ? ql[L - 1 - k] : ql[k]) - 33);
+  if (lane == 0) {
+    key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
+    val[i] = (uint32_t)(rec_base + i);
+    info[i] = RInfo{r.tid, r.pos, r.end, r.bin};
+  }
+}
+
+// sorted position k <- record val[k]
+struct LoadSortedSize {
+  const uint32_t *val;
+  const int64_t *roff;   // [n + 1] unsorted offsets (roff[n] = total)
+  int64_t n;
+  __device__ int64_t operator()(int64_t k) const {
+    if (k >= n) return 0;
+    const uint32_t r = val[k];
+    return roff[r + 1] - roff[r];
+  }
+};
+
+__global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const int64_t *roff, const uint32_t *val,
+                                                    const int64_t *soff, int64_t n, uint8_t *dst, const RInfo *info,
+                                                    RInfo *sinfo) {
+  const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (k >= n) return;
+  const uint32_t r = val[k];
+  const int64_t a = roff[r], len = roff[r + 1] - a;
+  const uint8_t *s = src + a;
+  uint8_t *d = dst + soff[k];
+  for (int64_t j = lane; j < len; j += 64) d[j] = s[j];
+  if (lane == 0) sinfo[k] = info[r];
+}
+
+}  // namespace
+
+int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths) {
+  BamStore &B = ctx->bam;
+  B.ref_names.clear();
+  B.ref_len.assign(lengths, lengths + n_refs);
+  std::vector<int32_t> off(1, 0);
+  std::string cat;
+  const char *p = names;
+  for (int32_t i = 0; i < n_refs; i++) {
+    std::string nm(p);
+    p += nm.size() + 1;
+    B.ref_names.push_back(nm);
+    cat += nm;
+    off.push_back((int32_t)cat.size());
+  }
+  MH_TRY(ensure(ctx, B.names, cat.size() + 16));
+  MH_TRY(ensure(ctx, B.name_off, sizeof(int32_t) * off.size()));
+  if (!cat.empty()) HIPCHK(ctx, hipMemcpyAsync(B.names.p, cat.data(), cat.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(B.name_off.p, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice,
+                             ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  B.n_rec = 0;
+  B.bytes = 0;
+  B.n_files = 0;
+  B.refs_set = true;
+  return MH_OK;
+}
+
+// Newline index of a device buffer into `nl` (grown as needed); returns the count.
+static int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count) {
+  hipStream_t st = ctx->stream;
+  const int64_t chunks = (len + 15) / 16;
+  *count = 0;
+  if (len == 0) return MH_OK;
+  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(chunks) + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int64_t *tot = (int64_t *)ctx->d_small.p;
+  HIPCHK(ctx, device_reduce<int64_t>(st, chunks, LoadNL{b, len}, OpSum{}, (int64_t)0,
+                                     (int64_t *)ctx->scan_partials.p, tot));
+  int64_t n = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&n, tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  MH_TRY(ensure(ctx, nl, sizeof(int64_t) * (n + 1)));
+  HIPCHK(ctx, device_scan<int64_t>(st, chunks, LoadNL{b, len}, StoreNL{b, len, (int64_t *)nl.p}, OpSum{}, (int64_t)0,
+                                   (int64_t *)ctx->scan_partials.p, tot));
+  *count = n;
+  return MH_OK;
+}
+
+int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2, int64_t len2, int64_t max_templates,
+                int64_t *used1, int64_t *used2, int64_t *templates) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  *used1 = *used2 = *templates = 0;
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  const int32_t nf = d2 ? 2 : 1;
+  if (B.n_files && B.n_files != nf) return arg_fail(ctx, MH_E_ARG, "single-end and paired input mixed in one BAM");
+  int64_t nnl1 = 0, nnl2 = 0;
+  stage_begin(ctx, "bam_index");
+  MH_TRY(newline_index(ctx, d1, len1, B.nl1, &nnl1));
+  if (d2) MH_TRY(newline_index(ctx, d2, len2, B.nl2, &nnl2));
+  stage_end(ctx);
+  int64_t T = nnl1 / 4;
+  if (d2 && nnl2 / 4 < T) T = nnl2 / 4;
+  if (max_templates >= 0 && T > max_templates) T = max_templates;
+  if (T == 0) return MH_OK;
+  B.n_files = nf;
+
+  MH_TRY(ensure(ctx, B.tpl, sizeof(BamTpl) * T));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int32_t *err = (int32_t *)((char *)ctx->d_small.p + 64);
+  HIPCHK(ctx, hipMemsetAsync(err, 0, 4, st));
+  ParseArgs a{{d1, d2}, {(const int64_t *)B.nl1.p, d2 ? (const int64_t *)B.nl2.p : nullptr}, nf,
+              (const char *)B.names.p, (const int32_t *)B.name_off.p, (int32_t)B.ref_names.size()};
+  stage_begin(ctx, "bam_parse");
+  hipLaunchKernelGGL(k_bam_parse, dim3(grid_for(T, 256, INT32_MAX)), dim3(256), 0, st, a, T, (BamTpl *)B.tpl.p, err);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  int32_t herr = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (herr) {
+    std::string m = "god-aligner input:";
+    if (herr & BE_QNAME) m += " malformed FASTQ record;";
+    if (herr & BE_QNAME_LEN) m += " read name longer than 254 characters (BAM limit);";
+    if (herr & BE_CHROM) m += " qname chrom not among the @SQ names (.ann);";
+    if (herr & BE_FIELDS) m += " qname does not parse (readgenerate.parse_qname);";
+    if (herr & BE_CIGAR) m += " invalid CIGAR in qname;";
+    if (herr & BE_SEQ) m += " sequence and quality lengths differ;";
+    return arg_fail(ctx, MH_E_ARG, m);
+  }
+  // record offsets (appended to the store)
+  const int64_t n_rec = T * nf;
+  MH_TRY(ensure_keep(ctx, B.roff, sizeof(int64_t) * (B.n_rec + n_rec + 1), sizeof(int64_t) * (B.n_rec + 1)));
+  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(n_rec + 1) + 64));
+  int64_t *roff = (int64_t *)B.roff.p + B.n_rec;
+  int64_t *tot = (int64_t *)ctx->d_small.p;
+  HIPCHK(ctx, device_scan<int64_t>(st, n_rec + 1, LoadSize{(const BamTpl *)B.tpl.p, nf, n_rec},
+                                   StoreOff64{roff, B.bytes}, OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p,
+                                   tot));
+  int64_t add_bytes = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  MH_TRY(ensure_keep(ctx, B.recs, B.bytes + add_bytes + 64, B.bytes));
+  MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n_rec), sizeof(uint64_t) * B.n_rec));
+  MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n_rec), sizeof(uint32_t) * B.n_rec));
+  MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n_rec), sizeof(RInfo) * B.n_rec));
+  stage_begin(ctx, "bam_write");
+  hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n_rec * 64, 256, INT32_MAX)), dim3(256), 0, st, a,
+                     (const BamTpl *)B.tpl.p, n_rec, nf, (const int64_t *)roff, (int64_t)0, (uint8_t *)B.recs.p,
+                     (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
+                     B.n_rec);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  B.n_rec += n_rec;
+  B.bytes += add_bytes;
+  int64_t last1 = 0, last2 = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
+  if (d2) HIPCHK(ctx, hipMemcpyAsync(&last2, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *used1 = last1 + 1;
+  *used2 = d2 ? last2 + 1 : 0;
+  *templates = T;
+  return MH_OK;
+}
+
+int32_t bam_sort(mh_ctx *ctx) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  const int64_t n = B.n_rec;
+  if (n == 0) return MH_OK;
+  if (n >= (int64_t)UINT32_MAX) return arg_fail(ctx, MH_E_CAPACITY, "more than 2^32 records in one BAM");
+  int tid_bits = 1;
+  while ((1ull << tid_bits) < (uint64_t)B.ref_names.size() + 1) tid_bits++;
+  const unsigned end_bit = 33 + tid_bits;
+  MH_TRY(ensure(ctx, B.key2, sizeof(uint64_t) * n));
+  MH_TRY(ensure(ctx, B.val2, sizeof(uint32_t) * n));
+  size_t tmp = 0;
+  stage_begin(ctx, "bam_sort");
+  HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, (uint64_t *)B.key.p, (uint64_t *)B.key2.p, (uint32_t *)B.val.p,
+                                        (uint32_t *)B.val2.p, (size_t)n, 0u, end_bit, st));
+  MH_TRY(ensure(ctx, B.sort_tmp, tmp + 256));
+  HIPCHK(ctx, rocprim::radix_sort_pairs(B.sort_tmp.p, tmp, (uint64_t *)B.key.p, (uint64_t *)B.key2.p,
+                                        (uint32_t *)B.val.p, (uint32_t *)B.val2.p, (size_t)n, 0u, end_bit, st));
+  stage_end(ctx);
+  // sorted offsets, then the gather
+  MH_TRY(ensure(ctx, B.soff, sizeof(int64_t) * (n + 1)));
+  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(n + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  HIPCHK(ctx, device_scan<int64_t>(st, n + 1, LoadSortedSize{(const uint32_t *)B.val2.p, (const int64_t *)B.roff.p, n},
+                                   StoreOff64{(int64_t *)B.soff.p, 0}, OpSum{}, (int64_t)0,
+                                   (int64_t *)ctx->scan_partials.p, (int64_t *)ctx->d_small.p));
+  MH_TRY(ensure(ctx, B.srecs, B.bytes + 64));
+  MH_TRY(ensure(ctx, B.sinfo, sizeof(RInfo) * n));
+  stage_begin(ctx, "bam_gather");
+  hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st,
+                     (const uint8_t *)B.recs.p, (const int64_t *)B.roff.p, (const uint32_t *)B.val2.p,
+                     (const int64_t *)B.soff.p, n, (uint8_t *)B.srecs.p, (const RInfo *)B.info.p,
+                     (RInfo *)B.sinfo.p);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return MH_OK;
+}
+
+int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  const int64_t n = B.n_rec;
+  if (n == 0) return MH_OK;
+  static_assert(sizeof(RInfo) == 16, "RInfo layout");
+  if (recs) HIPCHK(ctx, hipMemcpyAsync(recs, B.srecs.p, B.bytes, hipMemcpyDeviceToHost, st));
+  if (soff) HIPCHK(ctx, hipMemcpyAsync(soff, B.soff.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
+  if (info) HIPCHK(ctx, hipMemcpyAsync(info, B.sinfo.p, sizeof(RInfo) * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  return MH_OK;
+}
+
+void bam_release(BamStore &B) {
+  for (DevBuf *b : {&B.names, &B.name_off, &B.nl1, &B.nl2, &B.tpl, &B.roff, &B.recs, &B.key, &B.val, &B.info,
+                    &B.key2, &B.val2, &B.sort_tmp, &B.soff, &B.srecs, &B.sinfo, &B.in1, &B.in2})
+    release(*b);
+  B.n_rec = B.bytes = 0;
+  B.n_files = 0;
+  B.refs_set = false;
+}
+
+}  // namespace mh

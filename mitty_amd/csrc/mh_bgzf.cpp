@@ -1,0 +1,201 @@
+// mh_bgzf.cpp — BGZF framing + BAI (see mh_bgzf.h).
+#include "mh_bgzf.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <thread>
+
+namespace mh {
+
+namespace {
+
+void put32(std::string &s, uint32_t v) {
+  char b[4] = {(char)v, (char)(v >> 8), (char)(v >> 16), (char)(v >> 24)};
+  s.append(b, 4);
+}
+void put64(std::string &s, uint64_t v) {
+  put32(s, (uint32_t)v);
+  put32(s, (uint32_t)(v >> 32));
+}
+
+// One BGZF block (RFC 1952 member with the 'BC' extra field) for n <= BGZF_BLOCK input bytes.
+bool bgzf_block(const uint8_t *in, int64_t n, int level, std::string &out) {
+  const size_t cap = compressBound((uLong)n) + 64;
+  std::string buf(18 + cap + 8, '\0');
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  zs.next_in = (Bytef *)in;
+  zs.avail_in = (uInt)n;
+  zs.next_out = (Bytef *)&buf[18];
+  zs.avail_out = (uInt)cap;
+  int rc = deflate(&zs, Z_FINISH);
+  const size_t clen = zs.total_out;
+  deflateEnd(&zs);
+  if (rc != Z_STREAM_END) return false;
+  const size_t bsize = 18 + clen + 8;
+  if (bsize > 65536) return false;
+  static const uint8_t hdr[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
+  memcpy(&buf[0], hdr, 16);
+  buf[16] = (char)((bsize - 1) & 0xff);
+  buf[17] = (char)((bsize - 1) >> 8);
+  const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), in, (uInt)n);
+  std::string tail;
+  put32(tail, crc);
+  put32(tail, (uint32_t)n);
+  memcpy(&buf[18 + clen], tail.data(), 8);
+  buf.resize(bsize);
+  out.swap(buf);
+  return true;
+}
+
+const uint8_t BGZF_EOF[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0,
+                              0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+}  // namespace
+
+std::string bam_header_bytes(const std::string &text, const std::vector<std::string> &names,
+                             const std::vector<int64_t> &lens) {
+  std::string s("BAM\1", 4);
+  put32(s, (uint32_t)text.size());
+  s += text;
+  put32(s, (uint32_t)names.size());
+  for (size_t i = 0; i < names.size(); i++) {
+    put32(s, (uint32_t)(names[i].size() + 1));
+    s += names[i];
+    s.push_back('\0');
+    put32(s, (uint32_t)lens[i]);
+  }
+  return s;
+}
+
+bool bgzf_write(const char *path, const std::string &header, const uint8_t *data, int64_t n, int level, int threads,
+                std::vector<int64_t> &coff, std::string &err) {
+  FILE *fp = fopen(path, "wb");
+  if (!fp) {
+    err = std::string("cannot open ") + path;
+    return false;
+  }
+  int64_t pos = 0;
+  bool ok = true;
+  std::string blk;
+  for (size_t h = 0; h < header.size() && ok; h += BGZF_BLOCK) {
+    const int64_t m = std::min<int64_t>(BGZF_BLOCK, (int64_t)(header.size() - h));
+    ok = bgzf_block((const uint8_t *)header.data() + h, m, level, blk) && fwrite(blk.data(), 1, blk.size(), fp) ==
+         blk.size();
+    pos += (int64_t)blk.size();
+  }
+  const int64_t nblk = (n + BGZF_BLOCK - 1) / BGZF_BLOCK;
+  coff.assign(nblk + 1, 0);
+  if (threads < 1) threads = 1;
+  const int64_t round = (int64_t)threads * 64;
+  std::vector<std::string> out(round);
+  for (int64_t b0 = 0; b0 < nblk && ok; b0 += round) {
+    const int64_t b1 = std::min(nblk, b0 + round);
+    std::vector<std::thread> pool;
+    std::vector<char> good(threads, 1);
+    for (int w = 0; w < threads; w++) {
+      pool.emplace_back([&, w]() {
+        for (int64_t b = b0 + w; b < b1; b += threads) {
+          const int64_t m = std::min<int64_t>(BGZF_BLOCK, n - b * BGZF_BLOCK);
+          if (!bgzf_block(data + b * BGZF_BLOCK, m, level, out[b - b0])) good[w] = 0;
+        }
+      });
+    }
+    for (auto &t : pool) t.join();
+    for (int w = 0; w < threads; w++) ok = ok && good[w];
+    for (int64_t b = b0; b < b1 && ok; b++) {
+      coff[b] = pos;
+      ok = fwrite(out[b - b0].data(), 1, out[b - b0].size(), fp) == out[b - b0].size();
+      pos += (int64_t)out[b - b0].size();
+    }
+  }
+  coff[nblk] = pos;
+  ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
+  ok = (fclose(fp) == 0) && ok;
+  if (!ok) err = std::string("BGZF write failed: ") + path;
+  return ok;
+}
+
+bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
+               const std::vector<int64_t> &coff, std::string &err) {
+  std::string s("BAI\1", 4);
+  put32(s, (uint32_t)n_refs);
+  int64_t i = 0;
+  for (int32_t tid = 0; tid < n_refs; tid++) {
+    if (i < n && recs[i].tid < tid) {
+      err = "BAI: records not coordinate-sorted";
+      return false;
+    }
+    int64_t j = i;
+    while (j < n && recs[j].tid == tid) j++;
+    if (j == i) {   // no records on this reference
+      put32(s, 0);
+      put32(s, 0);
+      continue;
+    }
+    // bins: runs of consecutive records with the same bin form one chunk; adjacent chunks of a bin merge
+    std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+    std::vector<uint64_t> lin;
+    for (int64_t k = i; k < j; k++) {
+      const uint64_t vb = voffset(coff, soff[k]), ve = voffset(coff, soff[k + 1]);
+      auto &ch = bins[recs[k].bin];
+      if (!ch.empty() && ch.back().second == vb)
+        ch.back().second = ve;
+      else
+        ch.emplace_back(vb, ve);
+      const int64_t w0 = recs[k].beg >> 14, w1 = (recs[k].end - 1) >> 14;
+      if ((int64_t)lin.size() <= w1) lin.resize(w1 + 1, UINT64_MAX);
+      for (int64_t w = w0; w <= w1; w++)
+        if (lin[w] == UINT64_MAX) lin[w] = vb;
+    }
+    put32(s, (uint32_t)(bins.size() + 1));
+    for (auto &kv : bins) {
+      put32(s, kv.first);
+      put32(s, (uint32_t)kv.second.size());
+      for (auto &c : kv.second) {
+        put64(s, c.first);
+        put64(s, c.second);
+      }
+    }
+    // pseudo-bin 37450: (first record, end of last record), (mapped, unmapped)
+    put32(s, 37450);
+    put32(s, 2);
+    put64(s, voffset(coff, soff[i]));
+    put64(s, voffset(coff, soff[j]));
+    put64(s, (uint64_t)(j - i));
+    put64(s, 0);
+    // linear index: windows with no overlapping record take the next window's offset (the last one set so far
+    // going backwards), i.e. the first record that can overlap anything at or after them
+    uint64_t next = voffset(coff, soff[j]);
+    for (int64_t w = (int64_t)lin.size() - 1; w >= 0; w--) {
+      if (lin[w] == UINT64_MAX)
+        lin[w] = next;
+      else
+        next = lin[w];
+    }
+    put32(s, (uint32_t)lin.size());
+    for (uint64_t v : lin) put64(s, v);
+    i = j;
+  }
+  if (i != n) {
+    err = "BAI: record tid outside the header's references";
+    return false;
+  }
+  put64(s, 0);   // n_no_coor
+  FILE *fp = fopen(path, "wb");
+  if (!fp) {
+    err = std::string("cannot open ") + path;
+    return false;
+  }
+  bool ok = fwrite(s.data(), 1, s.size(), fp) == s.size();
+  ok = (fclose(fp) == 0) && ok;
+  if (!ok) err = std::string("BAI write failed: ") + path;
+  return ok;
+}
+
+}  // namespace mh

@@ -1,0 +1,39 @@
+// mh_bgzf.h — host side of the BAM writer: BGZF framing on a deflate thread pool and the BAI index (SAM/BAM
+// specification §4.1 / §5.2; the reference produces these through htslib via pysam.sort / pysam.index,
+// god_aligner.py:117-131).  Plain C++ (no HIP); compiled with g++ and linked against zlib.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mh {
+
+constexpr int64_t BGZF_BLOCK = 0xff00;   // uncompressed bytes per block (htslib BGZF_BLOCK_SIZE)
+
+struct BaiRec {   // one record, coordinate-sorted
+  int32_t tid, beg, end;
+  uint32_t bin;
+};
+
+// BAM header bytes: magic, l_text, text, n_ref, (l_name, name\0, l_ref) per reference.
+std::string bam_header_bytes(const std::string &text, const std::vector<std::string> &names,
+                             const std::vector<int64_t> &lens);
+
+// Writes a BGZF file: `header` (own block(s), as htslib flushes after the header), then `data` cut into
+// BGZF_BLOCK-byte blocks, then the EOF marker.  rec_block_coff[b] = file offset of data block b
+// (b = 0..nblocks; the last entry is the offset of the EOF block).  Returns false and sets err on failure.
+bool bgzf_write(const char *path, const std::string &header, const uint8_t *data, int64_t n, int level, int threads,
+                std::vector<int64_t> &rec_block_coff, std::string &err);
+
+// BAI for n sorted records whose data offsets are soff[0..n] (soff[n] = end), given the block map from bgzf_write.
+bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
+               const std::vector<int64_t> &rec_block_coff, std::string &err);
+
+// virtual offset of data offset u
+inline uint64_t voffset(const std::vector<int64_t> &coff, int64_t u) {
+  const int64_t b = u / BGZF_BLOCK;
+  return (uint64_t)coff[b] << 16 | (uint64_t)(u - b * BGZF_BLOCK);
+}
+
+}  // namespace mh

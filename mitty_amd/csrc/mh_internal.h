@@ -53,6 +53,22 @@ struct Contig {
   int64_t len = 0;
 };
 
+// God-aligner record store (mh_bam.hip): parsed FASTQ -> BAM records, resident until mh_bam_write.
+struct BamStore {
+  bool refs_set = false;
+  std::vector<std::string> ref_names;
+  std::vector<int64_t> ref_len;
+  DevBuf names, name_off;      // @SQ names on the device (concatenated + offsets)
+  DevBuf in1, in2;             // staged host FASTQ chunks
+  DevBuf nl1, nl2;             // newline positions of the current input
+  DevBuf tpl;                  // per-template parse results
+  DevBuf roff, recs;           // record offsets [n_rec + 1] / bytes (input order)
+  DevBuf key, val, info;       // sort key, record index, BAI info per record
+  DevBuf key2, val2, sort_tmp, soff, srecs, sinfo;   // sorted
+  int64_t n_rec = 0, bytes = 0;
+  int32_t n_files = 0;
+};
+
 struct StageTime {
   const char *name;
   hipEvent_t a, b;
@@ -103,6 +119,9 @@ struct mh_ctx {
   std::vector<mh::StageTime> stages;    // open (begun, not ended)
   std::vector<mh::StageTime> pending;   // ended, not yet resolved
   std::vector<std::pair<const char *, double>> last_times;
+
+  // god-aligner BAM records
+  mh::BamStore bam;
 };
 
 namespace mh {
@@ -148,6 +167,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                    int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept);
+
+int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);
+int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2, int64_t len2, int64_t max_templates,
+                int64_t *used1, int64_t *used2, int64_t *templates);
+int32_t bam_sort(mh_ctx *ctx);
+int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
+void bam_release(BamStore &B);
 
 int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l, int64_t n, int64_t *out_pos,
                    int64_t *out_n0, int64_t *out_n1, char *cigar, int64_t cigar_cap, int64_t *cigar_off,

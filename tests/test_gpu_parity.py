@@ -427,3 +427,133 @@ def test_distributed_two_ranks_one_gpu(native, tmp_path, layout):
   mp.start_processes(_gpu_rank, args=(2, port, layout, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
   assert open(tmp_path / 'r1.fq', 'rb').read() == G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz')
   assert open(tmp_path / 'r2.fq', 'rb').read() == G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz')
+
+
+# ---- god-aligner BAM -------------------------------------------------------------------------
+def _god_setup(tmp_path):
+  fa = tmp_path / 'ref.fa'
+  fa.write_text('')
+  (tmp_path / 'ref.fa.ann').write_text('1 1 11\n0 1 (null)\n0 50000 0\n0 2 (null)\n0 20000 0\n0 3 (null)\n0 8000 0\n')
+  return str(fa)
+
+
+def _god_check(bam, fq1, fq2, max_templates=None, sample='Seven'):
+  """The BAM file against the oracle: header bytes, sorted record stream, BAI over the file's own offsets."""
+  from oracle import god
+  from mitty_amd.benchmarking import god_aligner as ga
+  data = open(bam, 'rb').read()
+  header, recs, vo, vend = god.record_voffsets(data)
+  sq = G.load_json('god_header.json')
+  import base64
+  import sys
+  text = ga.header_text({'HD': {'VN': '1.0'},
+                         'PG': [{'CL': ' '.join(sys.argv), 'ID': 'mitty-god-aligner', 'PN': 'god-aligner',
+                                 'VN': ga.__version__}],
+                         'RG': [{'ID': base64.b64encode(' '.join(sys.argv).encode('ascii')), 'SM': sample}],
+                         'SQ': sq})
+  assert header == god.header_bytes(text, sq)
+  want = god.sorted_stream(god.god_records(fq1, fq2, {'1': 0, '2': 1, '3': 2}, max_templates))
+  assert len(recs) == len(want)
+  assert recs == [god.encode(r) for r in want]
+  dec = [god.decode(r) for r in recs]
+  assert open(bam + '.bai', 'rb').read() == god.bai(len(sq), dec, vo, vend)
+  return dec
+
+
+@pytest.mark.parametrize('model', G.MODELS)
+def test_god_aligner_bam_vs_oracle(native, model, tmp_path):
+  from mitty_amd.benchmarking import god_aligner as ga
+  fa = _god_setup(tmp_path)
+  fq1, fq2 = G.path('e2e_{}.r1.fq.gz'.format(model)), G.path('e2e_{}.r2.fq.gz'.format(model))
+  bam = str(tmp_path / 'g.bam')
+  st = ga.process_multi_threaded(fa, bam, fq1, fq2, threads=3)
+  b1, b2 = G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+  dec = _god_check(bam, b1, b2)
+  assert st['records'] == 2 * (b1.count(b'\n') // 4)
+  # every record of god.json (captured from the reference's write_perfect_reads) is in the BAM
+  have = {(d['qname'], d['is_read1']): d for d in dec}
+  for qn, recs in G.load_json('god.json'):
+    for r in recs:
+      if (qn, r['is_read1']) in have:
+        got = have[(qn, r['is_read1'])]
+        assert {k: got[k] for k in r} == r
+  # small input chunks (records carried across calls), level 0 and 9, give the same records
+  for chunk, level in ((7001, 0), (65536, 9)):
+    bam2 = str(tmp_path / 'g{}.bam'.format(chunk))
+    ga.process_multi_threaded(fa, bam2, fq1, fq2, threads=2, chunk_bytes=chunk, level=level)
+    _god_check(bam2, b1, b2)
+
+
+def test_god_aligner_single_end_and_max_templates(native, tmp_path):
+  from mitty_amd.benchmarking import god_aligner as ga
+  fa = _god_setup(tmp_path)
+  fq1 = G.path('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
+  b1 = G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
+  bam = str(tmp_path / 's.bam')
+  ga.process_multi_threaded(fa, bam, fq1, None, sample_name='S1')
+  dec = _god_check(bam, b1, None, sample='S1')
+  assert all(d['flag'] & 0x1 == 0 for d in dec)
+  bam = str(tmp_path / 'm.bam')
+  st = ga.process_multi_threaded(fa, bam, fq1, G.path('e2e_hiseq-X-v2.5-Garvan.r2.fq.gz'), max_templates=9)
+  assert st['templates'] == 10   # the reference stops after template index max_templates
+  _god_check(bam, b1, G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r2.fq.gz'), max_templates=10)
+
+
+def test_god_aligner_errors(native, tmp_path):
+  ctx = native.Context(0)
+  try:
+    ctx.bam_set_refs(['1', '2'], [50000, 20000])
+    rec = b'@S:0:0:1|3|0|0|10|4|4=||1|20|4|4=|\nACGT\n+\n~~~~\n'
+    with pytest.raises(ValueError, match='chrom'):
+      ctx.bam_add_fastq(rec, rec)
+    long_q = b'@S:0:0:1|1|0|0|10|4|4=|' + b'1,' * 200 + b'1|1|20|4|4=|\nACGT\n+\n~~~~\n'
+    with pytest.raises(ValueError, match='254'):
+      ctx.bam_add_fastq(long_q, long_q)
+    bad = b'@S:0:0:1|1|0|0|10|4|4Q||1|20|4|4=|\nACGT\n+\n~~~~\n'
+    with pytest.raises(ValueError, match='CIGAR'):
+      ctx.bam_add_fastq(bad, bad)
+    # an incomplete trailing record is left for the next call
+    ok = b'@S:0:0:1|1|0|0|10|4|4=||1|20|4|4=|\nACGT\n+\n~~~~\n'
+    u1, u2, t = ctx.bam_add_fastq(ok + ok[:20], ok + ok[:30])
+    assert (u1, u2, t) == (len(ok), len(ok), 1)
+  finally:
+    ctx.close()
+
+
+def test_god_aligner_from_device_arenas(native, tmp_path):
+  """generate-reads output fed to the BAM builder on the device (no FASTQ round trip) = the file-based BAM."""
+  from mitty_amd.benchmarking import god_aligner as ga
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  c = G.load_json('e2e_config.json')['hiseq-X-v2.5-Garvan']
+  mod, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  f1, f2 = str(tmp_path / 'r1.fq'), str(tmp_path / 'r2.fq')
+  readgenerate.process_multi_threaded(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], f1, f2, seed=c['seed'])
+  fa = _god_setup(tmp_path)
+  bam_a = str(tmp_path / 'a.bam')
+  ga.process_multi_threaded(fa, bam_a, f1, f2)
+  from mitty_amd.engine import Engine
+  from mitty_amd.lib import fasta as mfasta, vcfio
+  rm = mod.read_model_params(mdl, c['coverage'])
+  vdf = vcfio.load_variants_soa(G.path(c['vcf']), c['sample'], G.path(c['bed']))
+  seqs = mfasta.read_fasta(G.path(c['fasta']))
+  units = [(ps, w['region_idx'], w['region_cpy'], w['rng_seed'])
+           for ps, w in enumerate(readgenerate.get_data_for_workers(rm, vdf, c['seed']))]
+  eng = Engine(0)
+  try:
+    for ri, reg in enumerate(vdf):
+      eng.load_region(ri, reg['region'], mfasta.fetch(seqs, *reg['region']))
+    eng.run_units(units, lambda r, cp: vdf[r]['copies'][cp], rm['p'], rm['rlen'], rm['cum_tlen'], c['sample'])
+    eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
+    assert eng.ctx.bam_add_output() == open(f1, 'rb').read().count(b'\n') // 4
+    text = open(bam_a, 'rb').read()
+    from oracle import god
+    header, recs_a, _, _ = god.record_voffsets(text)
+    l_text = int.from_bytes(header[4:8], 'little')
+    bam_b = str(tmp_path / 'b.bam')
+    eng.ctx.bam_write(bam_b, header[8:8 + l_text].decode(), bai_path=bam_b + '.bai')
+  finally:
+    eng.close()
+  _, recs_b, _, _ = god.record_voffsets(open(bam_b, 'rb').read())
+  assert recs_a == recs_b

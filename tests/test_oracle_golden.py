@@ -98,3 +98,51 @@ def test_corruption_exact(model):
   b1, b2 = O.corrupt_fastq(G.model(model), [r[0] for r in r1], [r[1] for r in r1], [r[1] for r in r2], seed=7)
   assert b1 == G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model))
   assert b2 == G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model))
+
+
+# ---- god-aligner (oracle/god.py) ------------------------------------------------------------------------------
+def test_god_records_match_reference():
+  """write_perfect_reads attributes (tests/golden/god.json, captured from the reference) from the e2e FASTQs."""
+  from oracle import god
+  want = {}
+  for qn, recs in G.load_json('god.json'):
+    want.setdefault(qn, []).append(recs)
+  ref_dict = {'1': 0, '2': 1, '3': 2}
+  hit = 0
+  for m in G.MODELS:
+    l1 = G.fastq_bytes('e2e_{}.r1.fq.gz'.format(m)).decode().split('\n')
+    l2 = G.fastq_bytes('e2e_{}.r2.fq.gz'.format(m)).decode().split('\n')
+    for i in range(len(l1) // 4):
+      qn = l1[4 * i][1:]
+      if qn not in want:
+        continue
+      got = god.perfect_reads(qn, ref_dict, [(l1[4 * i + 1], l1[4 * i + 3]), (l2[4 * i + 1], l2[4 * i + 3])])
+      assert got in want[qn]
+      hit += 1
+  assert hit >= len(G.load_json('god.json'))
+
+
+def test_god_encode_decode_roundtrip():
+  from oracle import god
+  for qn, recs in G.load_json('god.json')[:60]:
+    for r in recs:
+      d = god.decode(god.encode(r))
+      assert {k: d[k] for k in r} == r
+      assert d['bin'] == god.reg2bin(r['pos'], god.end_pos(r))
+
+
+def test_god_header_text():
+  from mitty_amd.benchmarking import god_aligner as ga
+  hdr = {'HD': {'VN': '1.0'}, 'PG': [{'CL': 'mitty god-aligner x', 'ID': 'mitty-god-aligner', 'PN': 'god-aligner',
+                                      'VN': '2.7.3.dev0'}],
+         'RG': [{'ID': b'bWl0dHk=', 'SM': None}], 'SQ': G.load_json('god_header.json')}
+  assert ga.header_text(hdr) == ('@HD\tVN:1.0\tSO:coordinate\n@SQ\tSN:1\tLN:50000\n@SQ\tSN:2\tLN:20000\n'
+                                 '@SQ\tSN:3\tLN:8000\n@RG\tID:b\'bWl0dHk=\'\tSM:None\n'
+                                 '@PG\tPN:god-aligner\tID:mitty-god-aligner\tVN:2.7.3.dev0\tCL:mitty god-aligner x\n')
+
+
+def test_god_parse_ann(tmp_path):
+  from mitty_amd.benchmarking import god_aligner as ga
+  ann = tmp_path / 'x.ann'
+  ann.write_text('1 1 11\n0 1 (null)\n0 50000 0\n0 2 (null)\n0 20000 0\n0 3 (null)\n0 8000 0\n')
+  assert ga.parse_ann(str(ann)) == G.load_json('god_header.json')
