@@ -156,6 +156,14 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);
 
+/* ---- corrupt-reads over existing FASTQ (readcorrupt.multi_process, readcorrupt.py:18-118; cli.py:144-157) -----
+ * The complete templates of the host buffers (file 2 optional) are corrupted with the model set by
+ * mh_set_corruption (must be enabled) and appended to the FASTQ arenas as '@{file-1 name}\n{seq}\n+\n{bq}\n' per
+ * file (readcorrupt.py:112-114).  t_base = index of the buffers' first template in the whole input (the Philox
+ * counter), *used1 / *used2 = bytes consumed, *templates = templates done. */
+int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
+                         int64_t *used1, int64_t *used2, int64_t *templates);
+
 /* ---- corruption (Philox mode) -------------------------------------------------------------------------- */
 /* Configure the empirical-BQ corruption (illumina.corrupt_template, illumina.py:113-162) that mh_emit_reads then
  * applies while it writes each record: per base bq = min(searchsorted(cum_bq[file][n], U1), 93), the base replaced

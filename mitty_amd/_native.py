@@ -21,7 +21,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset']
+           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq']
 
 
 class NativeError(RuntimeError):
@@ -81,6 +81,7 @@ def lib():
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
   _sig(L, 'mh_bam_reset', [c_vp])
+  _sig(L, 'mh_corrupt_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -339,6 +340,16 @@ class Context:
 
   def bam_reset(self):
     self._chk(self._L.mh_bam_reset(self._h))
+
+  def corrupt_fastq(self, fq1, fq2=None, t_base=0):
+    """Corrupt the complete templates of FASTQ byte buffers into the arenas.  Returns (used1, used2, templates)."""
+    u1, u2, t = c_i64(), c_i64(), c_i64()
+    a1 = np.frombuffer(fq1, np.uint8) if len(fq1) else np.zeros(1, np.uint8)
+    a2 = None if fq2 is None else (np.frombuffer(fq2, np.uint8) if len(fq2) else np.zeros(1, np.uint8))
+    self._chk(self._L.mh_corrupt_fastq(self._h, _ptr(a1), len(fq1), None if a2 is None else _ptr(a2),
+                                       0 if fq2 is None else len(fq2), int(t_base), ctypes.byref(u1),
+                                       ctypes.byref(u2), ctypes.byref(t)))
+    return u1.value, u2.value, t.value
 
   def read_batch(self, slot, p, l):
     p = np.ascontiguousarray(p, dtype=np.int64)

@@ -14,13 +14,13 @@ pysam's order; values through str(), so the base64 RG ID keeps its b'...' form a
 depends on the samtools version bundled with pysam).
 """
 import base64
-import gzip
 import logging
 import os
 import sys
 import time
 
 from mitty_amd import _native
+from mitty_amd.lib.fastq_stream import stream_templates
 
 logger = logging.getLogger(__name__)
 
@@ -81,56 +81,6 @@ def header_text(hdr, sorted_by='coordinate'):
   return '\n'.join(lines) + '\n'
 
 
-def _reader(fname, chunk):
-  with open(fname, 'rb') as fp:
-    gz = fp.read(2) == b'\x1f\x8b'
-  fp = gzip.open(fname, 'rb') if gz else open(fname, 'rb')
-  try:
-    while True:
-      b = fp.read(chunk)
-      if not b:
-        return
-      yield b
-  finally:
-    fp.close()
-
-
-def _feed(ctx, fastq1, fastq2, limit, chunk):
-  """Stream both files through the device parser in chunks; returns the templates consumed."""
-  r1 = _reader(fastq1, chunk)
-  r2 = _reader(fastq2, chunk) if fastq2 else None
-  buf1, buf2 = b'', (b'' if fastq2 else None)
-  eof1 = eof2 = False
-  total, stalled = 0, False
-  while True:
-    if not eof1 and (len(buf1) < chunk or stalled):
-      nxt = next(r1, None)
-      eof1 = nxt is None
-      buf1 += nxt or b''
-    if r2 is not None and not eof2 and (len(buf2) < chunk or stalled):
-      nxt = next(r2, None)
-      eof2 = nxt is None
-      buf2 += nxt or b''
-    done = eof1 and (r2 is None or eof2)
-    if done:   # a last record without its final newline
-      if buf1 and not buf1.endswith(b'\n'):
-        buf1 += b'\n'
-      if buf2 and not buf2.endswith(b'\n'):
-        buf2 += b'\n'
-    want = -1 if limit is None else limit - total
-    if want == 0:
-      break
-    u1, u2, t = ctx.bam_add_fastq(buf1, buf2, want)
-    total += t
-    stalled = t == 0
-    buf1 = buf1[u1:]
-    if buf2 is not None:
-      buf2 = buf2[u2:]
-    if done and t == 0:
-      break
-  return total
-
-
 def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max_templates=None,
                            sample_name='Seven', device=0, level=6, chunk_bytes=1 << 30):
   """god_aligner.process_multi_threaded (:44-131): `bam_fname` (coordinate-sorted BAM) + `bam_fname.bai`.
@@ -145,7 +95,8 @@ def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max
   try:
     ctx.bam_set_refs([s['SN'] for s in hdr['SQ']], [s['LN'] for s in hdr['SQ']])
     limit = None if max_templates is None else max_templates + 1
-    n_t = _feed(ctx, fastq1, fastq2, limit, chunk_bytes)
+    n_t = stream_templates(fastq1, fastq2, lambda b1, b2, want, done: ctx.bam_add_fastq(b1, b2, want),
+                           chunk_bytes, limit)
     n_rec, n_bytes = ctx.bam_write(bam_fname, header_text(hdr), level=level, threads=max(threads, 1),
                                    bai_path=bam_fname + '.bai')
   finally:

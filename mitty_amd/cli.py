@@ -1,6 +1,6 @@
 """`mitty` command line (reference mitty/cli.py), MI355X build.
 
-Implemented: generate-reads (GPU), god-aligner (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
+Implemented: generate-reads (GPU), corrupt-reads (GPU), god-aligner (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
 --rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Multi-GPU: launch generate-reads under
 `python -m torch.distributed.run --nproc-per-node N -m mitty_amd.cli generate-reads ...` (one process per GPU,
 RCCL); the output files are identical to the one-GPU run.  Out of scope for this build (not on the
@@ -96,6 +96,24 @@ def generate_reads(fasta, vcf, sample_name, bed, modelfile, coverage, seed, fast
                                               fastq2, threads=threads, seed=seed, device=device, rng=rng,
                                               corrupt_seed=corrupt_seed)
   logging.info('generate-reads: {}'.format(stats))
+
+
+@cli.command('corrupt-reads', short_help='Apply corruption model to FASTQ file of reads')
+@click.argument('modelfile')
+@click.argument('fastq1_in', type=click.Path(exists=True))
+@click.argument('fastq1_out', type=click.Path())
+@click.argument('seed', type=int)
+@click.option('--fastq2-in', type=click.Path(exists=True))
+@click.option('--fastq2-out', type=click.Path())
+@click.option('--threads', default=2)
+@click.option('--device', default=0, help='HIP device ordinal')
+def read_corruption(modelfile, fastq1_in, fastq1_out, seed, fastq2_in, fastq2_out, threads, device):
+  """Apply corruption model to FASTQ file of reads (reference cli.py:144-157)"""
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readcorrupt as rc
+  read_module, read_model = get_read_model(modelfile)
+  rc.multi_process(read_module, read_model, fastq1_in, fastq1_out, fastq2_in, fastq2_out, processes=threads, seed=seed,
+                   device=device)
 
 
 @cli.command('god-aligner', short_help='Create a perfect BAM from simulated FASTQs')

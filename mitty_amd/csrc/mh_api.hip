@@ -589,6 +589,17 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
   return MH_OK;
 }
 
+int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
+                         int64_t *used1, int64_t *used2, int64_t *templates) {
+  CTX_GUARD(ctx);
+  if (!fq1 || len1 < 0 || (fq2 && len2 < 0) || t_base < 0 || !used1 || !used2 || !templates)
+    return arg_fail(ctx, MH_E_ARG, "null argument");
+  MH_TRY(stage_in(ctx, ctx->bam.in1, fq1, len1));
+  if (fq2) MH_TRY(stage_in(ctx, ctx->bam.in2, fq2, len2));
+  return corrupt_fastq(ctx, (const uint8_t *)ctx->bam.in1.p, len1, fq2 ? (const uint8_t *)ctx->bam.in2.p : nullptr,
+                       fq2 ? len2 : 0, t_base, used1, used2, templates);
+}
+
 int32_t mh_bam_reset(mh_ctx *ctx) {
   if (!ctx) return MH_E_ARG;
   ctx->bam.n_rec = ctx->bam.bytes = 0;

@@ -387,7 +387,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
 }
 
 // Newline index of a device buffer into `nl` (grown as needed); returns the count.
-static int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count) {
+int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count) {
   hipStream_t st = ctx->stream;
   const int64_t chunks = (len + 15) / 16;
   *count = 0;

@@ -24,6 +24,7 @@
 //                         the workgroup's output range; neighbouring workgroups own disjoint byte ranges).
 // The sequence of a read is hap[p - p_min, min(p + l, hap_end) - p_min): non-'D' nodes tile sample coordinates
 // contiguously, so the reference's per-node slice concatenation (rpc.py:146) is one contiguous range.
+#include "mh_corrupt.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -360,49 +361,6 @@ struct TplMeta {
 __device__ __forceinline__ uint8_t comp(uint8_t c) {
   // str.maketrans('ATCGN', 'TAGCN'): everything else passes through
   return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
-}
-
-struct CorruptCfg {
-  int32_t enable;
-  const float *cum;      // [2][max_bp][n_bq] cumulative BQ tables (f32)
-  const double *phred;   // [100]
-  int32_t max_bp, n_bq;
-  uint32_t k0, k1, c3;   // Philox key and the constant counter word
-  int64_t t_base;        // index of the launch's first template inside its unit (slices: mh_emit_reads_range)
-};
-
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
-#pragma unroll
-  for (int r = 0; r < 10; r++) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-    k.x += 0x9E3779B9u;
-    k.y += 0xBB67AE85u;
-  }
-  return c;
-}
-
-// illumina.corrupt_single_read for one base (illumina.py:155-160), Philox-driven.
-__device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, int f, int n, uint8_t &b, uint8_t &q) {
-  t += cc.t_base;
-  uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ((uint32_t)f << 16) | (uint32_t)n, cc.c3),
-                          make_uint2(cc.k0, cc.k1));
-  const float u1 = (float)(r.x >> 8) * (1.0f / 16777216.0f);
-  const float *row = cc.cum + ((int64_t)f * cc.max_bp + n) * cc.n_bq;
-  int lo = 0, hi = cc.n_bq;                 // np.searchsorted(bq_mat[n, :], U1) (side='left')
-  while (lo < hi) {
-    int mid = (lo + hi) >> 1;
-    if (row[mid] < u1) lo = mid + 1; else hi = mid;
-  }
-  const int bq = lo < 93 ? lo : 93;
-  const double u2 = (double)r.y * (1.0 / 4294967296.0);
-  if (u2 < cc.phred[bq]) {
-    const uint32_t ch = __umulhi(r.z, 3u);  // randint(0, 3)
-    const char *rot = b == 'A' ? "CTG" : b == 'C' ? "ATG" : b == 'T' ? "ACG" : b == 'G' ? "ACT" : "NNN";
-    b = (uint8_t)rot[ch];
-  }
-  q = (uint8_t)(bq + 33);
 }
 
 // LDS: meta[EW_T] | windows[EW_T][2][win_stride] | image 0 [cap+16] | image 1 [cap+16]

@@ -1,0 +1,57 @@
+"""corrupt-reads over existing FASTQ (reference mitty/simulation/readcorrupt.py:18-118, CLI cli.py:144-157),
+MI355X build.
+
+The reference reads template after template (file 1's name + each file's sequence, readcorrupt.py:50-54), corrupts
+them in `processes` workers seeded from RandomState(seed) (:31-37) with illumina.corrupt_template and writes
+'@{name}\n{seq}\n+\n{bq}\n' per file (:112-114), in whatever order the workers finish.  Here the FASTQ goes to the
+GPU in large chunks and every base is corrupted in parallel with the same model and rule (mh_corrupt.hip), its
+uniforms drawn from Philox4x32-10 keyed by `seed` and counted by (template, file, base): output order = input
+order, and the result does not depend on chunking or GPU count.  The reference's own output is only defined up to
+its worker scheduling, so parity is statistical (BQ distribution per position, substitution rate, substitutions
+to other bases); the bit-exact single-stream restatement (processes=1) is the CPU oracle's, for fixtures.
+"""
+import logging
+import time
+
+import numpy as np
+
+from mitty_amd import _native
+from mitty_amd.lib.fastq_stream import stream_templates
+
+logger = logging.getLogger(__name__)
+
+SEED_MAX = (1 << 32) - 1
+
+
+def multi_process(read_module, read_model, fastq1_in, fastq1_out, fastq2_in=None, fastq2_out=None, processes=2,
+                  seed=7, device=0, chunk_bytes=1 << 30, flush_bytes=1 << 30):
+  """readcorrupt.multi_process; `processes` is accepted for compatibility.  Returns a stats dict."""
+  t0 = time.time()
+  ctx = _native.Context(device)
+  fps = [open(fastq1_out, 'wb')] + ([open(fastq2_out, 'wb')] if fastq2_in is not None and fastq2_out else [])
+  try:
+    ctx.set_corruption(True, read_model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), seed)
+
+    def consume(b1, b2, want, done):
+      r = ctx.corrupt_fastq(b1, b2, done)
+      u1, u2 = ctx.output_size()
+      if u1 + u2 >= flush_bytes:
+        flush()
+      return r
+
+    def flush():
+      d1, d2 = ctx.fetch_output()
+      fps[0].write(d1)
+      if len(fps) > 1:
+        fps[1].write(d2)
+      ctx.reset_output()
+
+    n = stream_templates(fastq1_in, fastq2_in, consume, chunk_bytes)
+    flush()
+  finally:
+    for fp in fps:
+      fp.close()
+    ctx.close()
+  dt = time.time() - t0
+  logger.debug('Processed {} templates in {:0.2f}s ({:0.2f} t/s)'.format(n, dt, n / max(dt, 1e-9)))
+  return {'templates': n, 'seconds': dt}

@@ -557,3 +557,68 @@ def test_god_aligner_from_device_arenas(native, tmp_path):
     eng.close()
   _, recs_b, _, _ = god.record_voffsets(open(bam_b, 'rb').read())
   assert recs_a == recs_b
+
+
+# ---- standalone corrupt-reads --------------------------------------------------------------
+@pytest.mark.parametrize('model', G.MODELS)
+def test_corrupt_reads_over_fastq(native, model, tmp_path):
+  """corrupt-reads on the e2e FASTQ pair: names (file 1's) and lengths kept, substitutions only to other bases,
+  BQ per position distributed as the model says, substitution rate = mean phred error; chunking does not change
+  the output; the CLI gives the same files."""
+  from click.testing import CliRunner
+  from mitty_amd.cli import cli
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readcorrupt
+  mod, mdl = get_read_model(model + '.pkl')
+  i1, i2 = G.path('e2e_{}.r1.fq.gz'.format(model)), G.path('e2e_{}.r2.fq.gz'.format(model))
+  o1, o2 = str(tmp_path / 'c1.fq'), str(tmp_path / 'c2.fq')
+  st = readcorrupt.multi_process(mod, mdl, i1, o1, i2, o2, seed=11)
+  a1, a2 = G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+  assert st['templates'] == a1.count(b'\n') // 4
+  names = [ln.split(b' ')[0] for ln in a1.split(b'\n')[0::4][:-1]]
+  rlen = int(mdl['mean_rlen'])
+  for mate, (a, cfile) in enumerate(((a1, o1), (a2, o2))):
+    c = open(cfile, 'rb').read()
+    la, lc = a.split(b'\n'), c.split(b'\n')
+    assert len(la) == len(lc)
+    assert lc[0::4][:-1] == names and set(lc[2::4][:-1]) == {b'+'}
+    sa, sc, q = la[1::4][:-1], lc[1::4][:-1], lc[3::4][:-1]
+    assert [len(x) for x in sa] == [len(x) for x in sc] == [len(x) for x in q]
+    full = [i for i, x in enumerate(sa) if len(x) == rlen]
+    SA = np.frombuffer(b''.join(sa[i] for i in full), np.uint8).reshape(-1, rlen)
+    SC = np.frombuffer(b''.join(sc[i] for i in full), np.uint8).reshape(-1, rlen)
+    Q = np.frombuffer(b''.join(q[i] for i in full), np.uint8).reshape(-1, rlen).astype(np.int64) - 33
+    n = len(full)
+    for pos in (0, rlen // 2, rlen - 1):
+      pmf = np.diff(np.concatenate([[0.0], mdl['cum_bq_mat'][mate, pos, :]]))
+      h = np.bincount(Q[:, pos], minlength=94)[:94] / n
+      assert np.abs(h - pmf).max() < 4.5 / np.sqrt(n) + 0.005, (mate, pos)
+    err = SA != SC
+    exp = (10 ** (-Q / 10.0)).mean()
+    assert abs(err.mean() - exp) < 0.15 * exp + 5e-4
+    assert not np.any(SC[err] == SA[err])
+  # chunk size does not change the output
+  o1b, o2b = str(tmp_path / 'd1.fq'), str(tmp_path / 'd2.fq')
+  readcorrupt.multi_process(mod, mdl, i1, o1b, i2, o2b, seed=11, chunk_bytes=5003, flush_bytes=20000)
+  assert open(o1b, 'rb').read() == open(o1, 'rb').read() and open(o2b, 'rb').read() == open(o2, 'rb').read()
+  # CLI
+  e1, e2 = str(tmp_path / 'e1.fq'), str(tmp_path / 'e2.fq')
+  res = CliRunner().invoke(cli, ['corrupt-reads', model + '.pkl', i1, e1, '11', '--fastq2-in', i2, '--fastq2-out', e2])
+  assert res.exit_code == 0, res.output + repr(res.exception)
+  assert open(e1, 'rb').read() == open(o1, 'rb').read() and open(e2, 'rb').read() == open(o2, 'rb').read()
+
+
+def test_corrupt_reads_single_end_and_errors(native, tmp_path):
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readcorrupt
+  mod, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  i1 = G.path('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
+  o1 = str(tmp_path / 's.fq')
+  readcorrupt.multi_process(mod, mdl, i1, o1, seed=3)
+  c = open(o1, 'rb').read()
+  assert c.count(b'\n') == G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz').count(b'\n')
+  long_read = tmp_path / 'long.fq'
+  L = mdl['cum_bq_mat'].shape[1] + 1
+  long_read.write_bytes(b'@r1\n' + b'A' * L + b'\n+\n' + b'~' * L + b'\n')
+  with pytest.raises(ValueError, match='BQ model'):
+    readcorrupt.multi_process(mod, mdl, str(long_read), str(tmp_path / 'x.fq'), seed=3)
