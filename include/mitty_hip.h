@@ -156,6 +156,13 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);
 
+/* ---- compressed FASTQ sink: host-side BGZF (gzip-compatible members of <= 65280 input
+ * bytes, deflated on `threads` threads).  MH_E_CAPACITY if `cap` is short (*used = bytes needed).  mh_bgzf_eof
+ * writes the 28-byte end-of-file marker block.  No context or device needed. */
+int32_t mh_bgzf_compress(const char *in, int64_t len, int32_t level, int32_t threads, char *out, int64_t cap,
+                         int64_t *used);
+int32_t mh_bgzf_eof(char *out28);
+
 /* ---- corrupt-reads over existing FASTQ (readcorrupt.multi_process, readcorrupt.py:18-118; cli.py:144-157) -----
  * The complete templates of the host buffers (file 2 optional) are corrupted with the model set by
  * mh_set_corruption (must be enabled) and appended to the FASTQ arenas as '@{file-1 name}\n{seq}\n+\n{bq}\n' per

@@ -21,7 +21,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq']
+           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof']
 
 
 class NativeError(RuntimeError):
@@ -82,6 +82,8 @@ def lib():
                            P_i64])
   _sig(L, 'mh_bam_reset', [c_vp])
   _sig(L, 'mh_corrupt_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_bgzf_compress', [c_vp, c_i64, c_i32, c_i32, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_bgzf_eof', [c_vp])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -108,6 +110,28 @@ def mt_window_at(seed, offset):
   if rc:
     _raise(rc, 'mh_mt_window_at failed')
   return out
+
+
+def bgzf_compress(data, level=6, threads=8):
+  """BGZF members for `data` (host-side deflate pool; no device needed).  Append bgzf_eof() at the end of a file."""
+  n = len(data)
+  src = np.frombuffer(data, np.uint8) if n else np.zeros(1, np.uint8)
+  cap = n + (n // 0xff00 + 1) * 64 + 64
+  out = np.empty(cap, np.uint8)
+  used = c_i64()
+  rc = lib().mh_bgzf_compress(_ptr(src), n, int(level), int(threads), _ptr(out), cap, ctypes.byref(used))
+  if rc == MH_E_CAPACITY:
+    out = np.empty(used.value, np.uint8)
+    rc = lib().mh_bgzf_compress(_ptr(src), n, int(level), int(threads), _ptr(out), used.value, ctypes.byref(used))
+  if rc:
+    _raise(rc, 'mh_bgzf_compress failed')
+  return out[:used.value].tobytes()
+
+
+def bgzf_eof():
+  out = np.empty(28, np.uint8)
+  lib().mh_bgzf_eof(_ptr(out))
+  return out.tobytes()
 
 
 def device_count():

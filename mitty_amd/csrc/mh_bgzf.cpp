@@ -1,6 +1,8 @@
 // mh_bgzf.cpp — BGZF framing + BAI (see mh_bgzf.h).
 #include "mh_bgzf.h"
 
+#include "../../include/mitty_hip.h"
+
 #include <zlib.h>
 
 #include <algorithm>
@@ -53,10 +55,10 @@ bool bgzf_block(const uint8_t *in, int64_t n, int level, std::string &out) {
   return true;
 }
 
+}  // namespace
+
 const uint8_t BGZF_EOF[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0,
                               0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-
-}  // namespace
 
 std::string bam_header_bytes(const std::string &text, const std::vector<std::string> &names,
                              const std::vector<int64_t> &lens) {
@@ -71,6 +73,34 @@ std::string bam_header_bytes(const std::string &text, const std::vector<std::str
     put32(s, (uint32_t)lens[i]);
   }
   return s;
+}
+
+// Deflate data in BGZF_BLOCK pieces on `threads` host threads, handing the blocks to `sink` in order.
+template <typename Sink>
+static bool compress_blocks(const uint8_t *data, int64_t n, int level, int threads, Sink sink) {
+  const int64_t nblk = (n + BGZF_BLOCK - 1) / BGZF_BLOCK;
+  if (threads < 1) threads = 1;
+  const int64_t round = (int64_t)threads * 64;
+  std::vector<std::string> out(std::min<int64_t>(round, std::max<int64_t>(nblk, 1)));
+  for (int64_t b0 = 0; b0 < nblk; b0 += round) {
+    const int64_t b1 = std::min(nblk, b0 + round);
+    std::vector<std::thread> pool;
+    std::vector<char> good(threads, 1);
+    for (int w = 0; w < threads; w++) {
+      pool.emplace_back([&, w]() {
+        for (int64_t b = b0 + w; b < b1; b += threads) {
+          const int64_t m = std::min<int64_t>(BGZF_BLOCK, n - b * BGZF_BLOCK);
+          if (!bgzf_block(data + b * BGZF_BLOCK, m, level, out[b - b0])) good[w] = 0;
+        }
+      });
+    }
+    for (auto &t : pool) t.join();
+    for (int w = 0; w < threads; w++)
+      if (!good[w]) return false;
+    for (int64_t b = b0; b < b1; b++)
+      if (!sink(b, out[b - b0])) return false;
+  }
+  return true;
 }
 
 bool bgzf_write(const char *path, const std::string &header, const uint8_t *data, int64_t n, int level, int threads,
@@ -91,29 +121,11 @@ bool bgzf_write(const char *path, const std::string &header, const uint8_t *data
   }
   const int64_t nblk = (n + BGZF_BLOCK - 1) / BGZF_BLOCK;
   coff.assign(nblk + 1, 0);
-  if (threads < 1) threads = 1;
-  const int64_t round = (int64_t)threads * 64;
-  std::vector<std::string> out(round);
-  for (int64_t b0 = 0; b0 < nblk && ok; b0 += round) {
-    const int64_t b1 = std::min(nblk, b0 + round);
-    std::vector<std::thread> pool;
-    std::vector<char> good(threads, 1);
-    for (int w = 0; w < threads; w++) {
-      pool.emplace_back([&, w]() {
-        for (int64_t b = b0 + w; b < b1; b += threads) {
-          const int64_t m = std::min<int64_t>(BGZF_BLOCK, n - b * BGZF_BLOCK);
-          if (!bgzf_block(data + b * BGZF_BLOCK, m, level, out[b - b0])) good[w] = 0;
-        }
-      });
-    }
-    for (auto &t : pool) t.join();
-    for (int w = 0; w < threads; w++) ok = ok && good[w];
-    for (int64_t b = b0; b < b1 && ok; b++) {
-      coff[b] = pos;
-      ok = fwrite(out[b - b0].data(), 1, out[b - b0].size(), fp) == out[b - b0].size();
-      pos += (int64_t)out[b - b0].size();
-    }
-  }
+  ok = ok && compress_blocks(data, n, level, threads, [&](int64_t b, const std::string &z) {
+    coff[b] = pos;
+    pos += (int64_t)z.size();
+    return fwrite(z.data(), 1, z.size(), fp) == z.size();
+  });
   coff[nblk] = pos;
   ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
   ok = (fclose(fp) == 0) && ok;
@@ -199,3 +211,28 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
 }
 
 }  // namespace mh
+
+// ---- C ABI: BGZF for the compressed FASTQ sink ------------------------------------------
+extern "C" int32_t mh_bgzf_compress(const char *in, int64_t len, int32_t level, int32_t threads, char *out,
+                                    int64_t cap, int64_t *used) {
+  if ((!in && len > 0) || len < 0 || !used || level < 0 || level > 9) return MH_E_ARG;
+  int64_t w = 0;
+  bool fits = true;
+  bool ok = mh::compress_blocks((const uint8_t *)in, len, level, threads, [&](int64_t, const std::string &z) {
+    if (fits && out && w + (int64_t)z.size() <= cap)
+      memcpy(out + w, z.data(), z.size());
+    else
+      fits = false;
+    w += (int64_t)z.size();
+    return true;
+  });
+  *used = w;
+  if (!ok) return MH_E_ARG;
+  return fits ? MH_OK : MH_E_CAPACITY;
+}
+
+extern "C" int32_t mh_bgzf_eof(char *out28) {
+  if (!out28) return MH_E_ARG;
+  memcpy(out28, mh::BGZF_EOF, 28);
+  return MH_OK;
+}

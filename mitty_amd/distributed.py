@@ -195,26 +195,43 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k]
       stats['kept'] += emitted[i][0]
 
-  # file offsets of every piece, then positioned writes
+  # file offsets of every piece, then positioned writes.  '.gz' outputs: each piece becomes BGZF members first
+  # (decompressed content identical to the one-GPU file; rank 0 adds the EOF marker)
+  gz = fastq1_fname.endswith('.gz')
+  payload = {}
+  if gz:
+    from mitty_amd import _native
+    for i in sorted(emitted):
+      _, r1, r2 = emitted[i]
+      d1, d2 = backend.fetch(r1, r2 if write2 else (0, 0))
+      payload[i] = (_native.bgzf_compress(d1), _native.bgzf_compress(d2) if write2 else b'')
   sz = [0] * (2 * len(pieces))
   for i, (_, r1, r2) in emitted.items():
-    sz[2 * i], sz[2 * i + 1] = r1[1], r2[1]
+    if gz:
+      sz[2 * i], sz[2 * i + 1] = len(payload[i][0]), len(payload[i][1])
+    else:
+      sz[2 * i], sz[2 * i + 1] = r1[1], r2[1]
   sz = allreduce_i64(sz + [stats['templates'], stats['kept']], group)
   tot_templates, tot_kept = sz[-2], sz[-1]
   off1, total1 = file_offsets(sz[0:2 * len(pieces):2])
   off2, total2 = file_offsets(sz[1:2 * len(pieces):2])
   fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
+  totals = (total1, total2)
   if rank == 0:
-    for fn, total in zip(fnames, (total1, total2)):
+    for fn, total in zip(fnames, totals):
       with open(fn, 'wb') as fp:
         fp.truncate(total)
+        if gz:
+          from mitty_amd import _native
+          fp.seek(total)
+          fp.write(_native.bgzf_eof())
   if world > 1:
     dist.barrier(group)
   fds = [os.open(fn, os.O_WRONLY) for fn in fnames]
   try:
     for i in sorted(emitted):
       _, r1, r2 = emitted[i]
-      d1, d2 = backend.fetch(r1, r2 if write2 else (0, 0))
+      d1, d2 = payload.pop(i) if gz else backend.fetch(r1, r2 if write2 else (0, 0))
       _pwrite_all(fds[0], d1, off1[i])
       if write2:
         _pwrite_all(fds[1], d2, off2[i])

@@ -55,3 +55,33 @@ def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None):
     if done and t == 0:
       break
   return total
+
+
+class FastqSink:
+  """Sequential FASTQ output (works with FIFOs / process substitution, examples/reads/run.sh:13-16).  A name ending
+  in '.gz' gets BGZF (gzip-compatible) output, deflated on a host thread pool."""
+
+  def __init__(self, fname, level=6, threads=8, compress=None):
+    self.fp = open(fname, 'wb')
+    self.gz = fname.endswith('.gz') if compress is None else compress
+    self.level, self.threads = level, threads
+    self.raw = 0
+
+  def write(self, data):
+    self.raw += len(data)
+    if self.gz:
+      from mitty_amd import _native
+      data = _native.bgzf_compress(data, self.level, self.threads)
+    mv = memoryview(data)
+    while len(mv):
+      n = self.fp.write(mv)
+      mv = mv[n:]
+
+  def close(self):
+    if self.fp is None:
+      return
+    if self.gz:
+      from mitty_amd import _native
+      self.fp.write(_native.bgzf_eof())
+    self.fp.close()
+    self.fp = None

@@ -16,7 +16,7 @@ import time
 import numpy as np
 
 from mitty_amd import _native
-from mitty_amd.lib.fastq_stream import stream_templates
+from mitty_amd.lib.fastq_stream import FastqSink, stream_templates
 
 logger = logging.getLogger(__name__)
 
@@ -28,7 +28,7 @@ def multi_process(read_module, read_model, fastq1_in, fastq1_out, fastq2_in=None
   """readcorrupt.multi_process; `processes` is accepted for compatibility.  Returns a stats dict."""
   t0 = time.time()
   ctx = _native.Context(device)
-  fps = [open(fastq1_out, 'wb')] + ([open(fastq2_out, 'wb')] if fastq2_in is not None and fastq2_out else [])
+  fps = [FastqSink(fastq1_out)] + ([FastqSink(fastq2_out)] if fastq2_in is not None and fastq2_out else [])
   try:
     ctx.set_corruption(True, read_model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), seed)
 

@@ -16,6 +16,7 @@ from mitty_amd import _native
 from mitty_amd.engine import Engine
 from mitty_amd.lib import fasta as mfasta
 from mitty_amd.lib import vcfio
+from mitty_amd.lib.fastq_stream import FastqSink
 
 logger = logging.getLogger(__name__)
 
@@ -65,13 +66,6 @@ def get_data_for_workers(model, vcf, seed):
     yield {'region_idx': r, 'region_cpy': c, 'rng_seed': s}
 
 
-def _write_all(fp, data):
-  mv = memoryview(data)
-  while len(mv):
-    n = fp.write(mv)
-    mv = mv[n:]
-
-
 def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                            fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
                            flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000):
@@ -94,8 +88,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     eng.load_region(ri, reg['region'], mfasta.fetch(seqs, chrom, s0, e))
   stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0}
   write2 = fastq2_fname is not None
-  fp1 = open(fastq1_fname, 'wb')
-  fp2 = open(fastq2_fname, 'wb') if write2 else None
+  fp1 = FastqSink(fastq1_fname)   # '.gz' names get BGZF output
+  fp2 = FastqSink(fastq2_fname) if write2 else None
 
   def flush(ps, n, kept, b1, b2):
     stats['templates'] += n
@@ -105,9 +99,9 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     u1, u2 = eng.ctx.output_size()
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
       d1, d2 = eng.ctx.fetch_output()
-      _write_all(fp1, d1)
+      fp1.write(d1)
       if write2:
-        _write_all(fp2, d2)
+        fp2.write(d2)
       eng.ctx.reset_output()
 
   try:

@@ -59,3 +59,35 @@ def test_distributed_output_identical_to_single_process(tmp_path, world, layout)
                      start_method='spawn')
   assert open(tmp_path / 'r1.fq', 'rb').read() == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
   assert open(tmp_path / 'r2.fq', 'rb').read() == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+
+
+def test_distributed_gz_output(tmp_path):
+  """'.gz' outputs: BGZF pieces at all-reduced offsets + EOF marker; decompresses to the single-process bytes."""
+  import gzip
+  import socket
+  import torch.multiprocessing as mp
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  mp.start_processes(_rank_gz, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+  model = 'hiseq-X-v2.5-Garvan'
+  assert gzip.open(str(tmp_path / 'r1.fq.gz')).read() == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
+  assert gzip.open(str(tmp_path / 'r2.fq.gz')).read() == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+
+
+def _rank_gz(rank, world, port, outdir):
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    from mitty_amd.readmodel import get_read_model
+    from tests.dist_host import OracleBackend
+    model_name = 'hiseq-X-v2.5-Garvan'
+    c = G.load_json('e2e_config.json')[model_name]
+    mod, mdl = get_read_model(model_name + '.pkl')
+    D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                 c['coverage'], os.path.join(outdir, 'r1.fq.gz'), os.path.join(outdir, 'r2.fq.gz'),
+                                 seed=c['seed'], backend=OracleBackend(), layout='slice')
+  finally:
+    dist.destroy_process_group()

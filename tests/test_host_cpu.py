@@ -161,3 +161,31 @@ def test_mt19937_jump_ahead_host(seed):
     w = _native.mt_window_at(seed, J)
     assert (int(w[0]) >> 31) == (xs[J] >> 31)
     assert [int(v) for v in w[1:]] == xs[J + 1:J + 624], J
+
+
+# ---- compressed FASTQ sink (host BGZF, no device) -------------------------------------------------------------------
+@pytest.mark.parametrize('n', [0, 1, 65279, 65280, 65281, 1_000_003])
+def test_bgzf_compress_roundtrip(n):
+  import gzip
+  import os
+  data = (os.urandom(n // 3) + b'ACGTN\n+\n~~~' * (n // 10 + 1))[:n]
+  z = _native.bgzf_compress(data, level=6, threads=3) + _native.bgzf_eof()
+  assert gzip.decompress(z) == data
+  from oracle import god
+  blocks = god.bgzf_blocks(z)          # framing + CRC of every block
+  assert all(len(raw) <= 0xff00 for _, raw in blocks) and blocks[-1][1] == b''
+
+
+def test_fastq_sink_gz(tmp_path):
+  import gzip
+  from mitty_amd.lib.fastq_stream import FastqSink
+  s = FastqSink(str(tmp_path / 'a.fq.gz'), threads=2)
+  parts = [b'@r%d\nACGT\n+\n~~~~\n' % i * 5000 for i in range(3)]
+  for p in parts:
+    s.write(p)
+  s.close()
+  assert gzip.open(str(tmp_path / 'a.fq.gz')).read() == b''.join(parts)
+  s = FastqSink(str(tmp_path / 'b.fq'))
+  s.write(parts[0])
+  s.close()
+  assert open(str(tmp_path / 'b.fq'), 'rb').read() == parts[0]
