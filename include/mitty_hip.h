@@ -156,6 +156,21 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);
 
+/* ---- VCF ingest (vcfio.load_variant_file / split_copies / parse, vcfio.py:51-126) ------
+ * Host-only (no device): mh_vcf_open parses a plain or bgzipped VCF for one sample; mh_vcf_region runs the BED
+ * region query (htslib overlap: pos0 < end and pos0 + rlen > start0) and splits the records per copy, returning
+ * ploidy and per-copy counts (n_var[c], alt_bytes[c] for c < cap); mh_vcf_copy copies one copy's SoA out
+ * (the layout mh_build_haplotype takes).  Complex variants -> MH_E_COMPLEX_VARIANT, an unknown sample -> MH_E_ARG
+ * (the reference raises ValueError for both); mh_vcf_error has the message. */
+typedef struct mh_vcf mh_vcf;
+int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out);
+const char *mh_vcf_error(const mh_vcf *v);
+int32_t mh_vcf_close(mh_vcf *v);
+int32_t mh_vcf_region(mh_vcf *v, const char *chrom, int64_t start0, int64_t end, int32_t *ploidy, int64_t *n_var,
+                      int64_t *alt_bytes, int32_t cap);
+int32_t mh_vcf_copy(mh_vcf *v, int32_t cpy, int64_t *pos, uint8_t *op, int64_t *oplen, int64_t *alt_off,
+                    int64_t *alt_len, char *alt_pool);
+
 /* ---- compressed FASTQ sink: host-side BGZF (gzip-compatible members of <= 65280 input
  * bytes, deflated on `threads` threads).  MH_E_CAPACITY if `cap` is short (*used = bytes needed).  mh_bgzf_eof
  * writes the 28-byte end-of-file marker block.  No context or device needed. */

@@ -21,7 +21,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof']
+           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
+           'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy']
 
 
 class NativeError(RuntimeError):
@@ -84,6 +85,11 @@ def lib():
   _sig(L, 'mh_corrupt_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_bgzf_compress', [c_vp, c_i64, c_i32, c_i32, c_vp, c_i64, P_i64])
   _sig(L, 'mh_bgzf_eof', [c_vp])
+  _sig(L, 'mh_vcf_open', [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(c_vp)])
+  _sig(L, 'mh_vcf_error', [c_vp], ctypes.c_char_p)
+  _sig(L, 'mh_vcf_close', [c_vp])
+  _sig(L, 'mh_vcf_region', [c_vp, ctypes.c_char_p, c_i64, c_i64, ctypes.POINTER(c_i32), c_vp, c_vp, c_i32])
+  _sig(L, 'mh_vcf_copy', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -126,6 +132,52 @@ def bgzf_compress(data, level=6, threads=8):
   if rc:
     _raise(rc, 'mh_bgzf_compress failed')
   return out[:used.value].tobytes()
+
+
+class VcfFile:
+  """Host VCF reader (mh_vcf.cpp) for one sample: region(chrom, start0, end) -> (ploidy, [SoA per copy])."""
+
+  def __init__(self, path, sample):
+    L = lib()
+    self._L = L
+    self._h = c_vp()
+    rc = L.mh_vcf_open(path.encode(), sample.encode(), ctypes.byref(self._h))
+    if rc:
+      msg = L.mh_vcf_error(self._h).decode() if self._h else 'mh_vcf_open failed'
+      self.close()
+      _raise(rc, msg)
+
+  def close(self):
+    if getattr(self, '_h', None):
+      self._L.mh_vcf_close(self._h)
+      self._h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass
+
+  def region(self, chrom, start0, end):
+    pl = c_i32()
+    nv = np.zeros(64, np.int64)
+    ab = np.zeros(64, np.int64)
+    rc = self._L.mh_vcf_region(self._h, chrom.encode(), int(start0), int(end), ctypes.byref(pl), _ptr(nv), _ptr(ab),
+                               64)
+    if rc:
+      _raise(rc, self._L.mh_vcf_error(self._h).decode())
+    copies = []
+    for c in range(pl.value):
+      n, nb = int(nv[c]), int(ab[c])
+      pos, oplen, aoff, alen = (np.empty(n, np.int64) for _ in range(4))
+      op = np.empty(n, np.uint8)
+      pool = np.empty(max(nb, 1), np.uint8)
+      rc = self._L.mh_vcf_copy(self._h, c, _ptr(pos), _ptr(op), _ptr(oplen), _ptr(aoff), _ptr(alen), _ptr(pool))
+      if rc:
+        _raise(rc, self._L.mh_vcf_error(self._h).decode())
+      copies.append({'pos': pos, 'op': op, 'oplen': oplen, 'alt_off': aoff, 'alt_len': alen,
+                     'alt_pool': pool[:nb].tobytes()})
+    return pl.value, copies
 
 
 def bgzf_eof():

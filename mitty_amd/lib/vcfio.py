@@ -137,7 +137,24 @@ def _split_soa(region, recs):
 
 
 def load_variants_soa(fname, sample, bed_fname):
-  """[{'region': (chrom, s0, e), 'ploidy': k, 'copies': [soa, ...]}] in BED order."""
+  """[{'region': (chrom, s0, e), 'ploidy': k, 'copies': [soa, ...]}] in BED order, parsed by the native reader
+  (mitty_amd/csrc/mh_vcf.cpp; same semantics as the restatement below, which serves load_variant_file)."""
+  from mitty_amd import _native
+  vf = _native.VcfFile(fname, sample)
+  try:
+    out = []
+    for region in read_bed(bed_fname):
+      ploidy, copies = vf.region(*region)
+      if not any(len(c['pos']) for c in copies) and ploidy == 2:
+        logger.debug('Region {} has no variants for this sample'.format(region))
+      out.append({'region': region, 'ploidy': ploidy, 'copies': copies})
+    return out
+  finally:
+    vf.close()
+
+
+def _load_records_soa(fname, sample, bed_fname):
+  """Python restatement of the region query + split (kept for load_variant_file's Variant objects)."""
   recs = _Records(fname, sample)
   out = []
   for region in read_bed(bed_fname):
@@ -150,7 +167,7 @@ def load_variants_soa(fname, sample, bed_fname):
 def load_variant_file(fname, sample, bed_fname):
   """Reference-compatible form: [{'region': region, 'v': [[Variant, ...] per copy]}] (vcfio.py:51-64)."""
   out = []
-  for reg in load_variants_soa(fname, sample, bed_fname):
+  for reg in _load_records_soa(fname, sample, bed_fname):
     recs = reg['_recs']
     v = []
     for cpy in range(reg['ploidy']):

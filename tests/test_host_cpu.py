@@ -189,3 +189,34 @@ def test_fastq_sink_gz(tmp_path):
   s.write(parts[0])
   s.close()
   assert open(str(tmp_path / 'b.fq'), 'rb').read() == parts[0]
+
+
+# ---- native VCF reader (mh_vcf.cpp) vs the Python restatement --------------------------------------------------------
+@pytest.mark.parametrize('vcf,sample,bed', [('data/syn.vcf', 'S1', 'data/syn.bed'), ('data/syn.vcf.gz', 'S1', 'data/syn.bed'),
+                                            ('data/syn.vcf', 'S0', 'data/syn.bed'),
+                                            ('data/tiny.vcf', 'g0_s0', 'data/tiny.whole.bed'),
+                                            ('data/tiny.vcf', 'g0_s0', 'data/tiny.8-14.bed')])
+def test_native_vcf_matches_restatement(vcf, sample, bed):
+  a = vcfio.load_variants_soa(G.path(vcf), sample, G.path(bed))
+  b = vcfio._load_records_soa(G.path(vcf), sample, G.path(bed))
+  assert len(a) == len(b)
+  for ra, rb in zip(a, b):
+    assert ra['region'] == rb['region'] and ra['ploidy'] == rb['ploidy']
+    for ca, cb in zip(ra['copies'], rb['copies']):
+      for k in ('pos', 'op', 'oplen', 'alt_off', 'alt_len'):
+        assert np.array_equal(ca[k], cb[k]), k
+      assert ca['alt_pool'] == cb['alt_pool']
+
+
+def test_native_vcf_errors(tmp_path):
+  with pytest.raises(ValueError, match='sample'):
+    vcfio.load_variants_soa(G.path('data/syn.vcf'), 'nobody', G.path('data/syn.bed'))
+  with pytest.raises(ValueError, match='Complex'):
+    vcfio.load_variants_soa(G.path('data/flawed-tiny.vcf'), 'g0_s0', G.path('data/tiny.whole.bed'))
+  v = tmp_path / 'end.vcf'   # INFO END= widens the overlap span (htslib rlen)
+  v.write_text('##fileformat=VCFv4.1\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS\n'
+               '1\t5\t.\tA\tG\t.\t.\tEND=20\tGT\t1|0\n1\t30\t.\tC\tT\t.\t.\t.\tGT\t0|1\n')
+  b = tmp_path / 'r.bed'
+  b.write_text('1\t15\t40\n')
+  r = vcfio.load_variants_soa(str(v), 'S', str(b))[0]
+  assert r['ploidy'] == 2 and list(r['copies'][0]['pos']) == [5] and list(r['copies'][1]['pos']) == [30]
