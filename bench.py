@@ -11,7 +11,8 @@ Inputs (contig bytes) are resident before timing; variant arrays are re-uploaded
 Multi-GPU (torchrun, one process per GPU): every rank simulates its own chr1-shaped chromosome (weak scaling, no
 data-path collective); an RCCL all-reduce of the per-rank template counts closes each step.
 
-Prints one JSON line (rank 0).  `roofline` is for the emission kernel (k_emit_write): algorithmic bytes per launch =
+Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_assemble; k_emit_write with
+--emit-mode 1): algorithmic bytes per launch =
 sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ bytes written (both files), divided by the
 launch's HIP-event duration; `stage_ms` gives every stage per step so the dominant kernel is visible.
 """
@@ -44,6 +45,7 @@ def parse():
                   help='bounded CPU-oracle sample: one unit on the first N Mbp of the contig (0 = skip)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
+  ap.add_argument('--emit-mode', type=int, default=0, help='0: pull-model assembler, 1: LDS-image writer')
   return ap.parse_args()
 
 
@@ -79,6 +81,8 @@ def main():
   if a.corrupt:
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), a.seed)
   eng.load_region(0, ('1', 0, a.length), seq)
+  eng.ctx.set_emit_mode(a.emit_mode)
+  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_assemble'
 
   def step():
     eng.drop_haplotypes()
@@ -131,7 +135,7 @@ def main():
   alg_bytes = 2 * rlen * kept + b1 + b2                       # this rank's algorithmic bytes over the timed steps
   achieved = alg_bytes / (ew_ms * 1e-3) / 1e9 if ew_ms > 0 else None
   traffic = None
-  pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_emit_write_*.json')))
+  pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_{}_*.json'.format(kernel))))
   if pmc:
     try:
       with open(pmc[-1]) as fp:
@@ -166,7 +170,7 @@ def main():
                                                                          ', +BQ corruption' if a.corrupt else ''),
                  'model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units_per_gpu': len(units),
                  'templates_per_step': kept_all // a.steps, 'parallelism': 'unit-shard x{}'.format(world)},
-      'roofline': {'kernel': 'k_emit_write', 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS,
+      'roofline': {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS,
                    'unit': 'GB/s', 'frac': (achieved / PEAK_HBM_GBS) if achieved else None,
                    'traffic': traffic,
                    'algorithmic_bytes_per_launch': alg_bytes / max(ew_n, 1),
