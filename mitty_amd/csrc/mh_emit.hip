@@ -548,6 +548,31 @@ struct Emit16 {
   }
 };
 
+// 16 bytes from an arbitrary LDS address: five aligned dword reads + v_alignbyte.
+__device__ __forceinline__ uint4 lds_load16(const uint8_t *p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  if (sh == 0) return make_uint4(w0, w1, w2, w3);
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+// 0xff in every byte of x equal to the byte replicated in c
+__device__ __forceinline__ uint32_t byte_eq(uint32_t x, uint32_t c) {
+  const uint32_t y = x ^ c;
+  const uint32_t t = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+  return (t >> 7) * 0xffu;
+}
+
+// str.maketrans('ATCGN', 'TAGCN') on four bytes at once ('A'^'T' = 0x15, 'C'^'G' = 0x04; others unchanged)
+__device__ __forceinline__ uint32_t comp4(uint32_t x) {
+  const uint32_t at = byte_eq(x, 0x41414141u) | byte_eq(x, 0x54545454u);
+  const uint32_t cg = byte_eq(x, 0x43434343u) | byte_eq(x, 0x47474747u);
+  return x ^ (at & 0x15151515u) ^ (cg & 0x04040404u);
+}
+
 __global__ void __launch_bounds__(EA_THREADS) k_emit_assemble(HapView h, int64_t m, const int64_t *pos0,
                                                               const int64_t *pos1, const int8_t *fo0, int64_t rlen,
                                                               QFixed q, const Rec *recs, const E3 *off,
@@ -663,6 +688,31 @@ __global__ void __launch_bounds__(EA_THREADS) k_emit_assemble(HapView h, int64_t
       int r = g - meta[j].start[f];
       Emit16 e{0, 0};
       int b = 0;
+      if (nb == 16 && !cc.enable) {
+        // fast paths: a chunk entirely inside the bases or the '~' qualities of one record (most of the bytes)
+        while (r >= meta[j].len[f]) { j++; r = 0; }
+        const AMeta &mt = meta[j];
+        const int S = mt.S[f];
+        const int e3 = mt.e3, e5 = e3 + 1 + S, e6 = e5 + 3, e7 = e6 + (int)rlen;
+        if (r >= e6 && r + 16 <= e7) {
+          e.lo = e.hi = 0x7e7e7e7e7e7e7e7eull;
+          b = 16;
+        } else if (r > e3 && r + 16 <= e5) {
+          const int k0 = r - e3 - 1;
+          const uint8_t *w = wins + mt.win[f];
+          uint4 v;
+          if ((mt.rc >> f) & 1) {   // mate 1: reversed, complemented
+            const uint4 u = lds_load16(w + S - 16 - k0);
+            v = make_uint4(comp4(__builtin_bswap32(u.w)), comp4(__builtin_bswap32(u.z)),
+                           comp4(__builtin_bswap32(u.y)), comp4(__builtin_bswap32(u.x)));
+          } else {
+            v = lds_load16(w + k0);
+          }
+          e.lo = (uint64_t)v.x | (uint64_t)v.y << 32;
+          e.hi = (uint64_t)v.z | (uint64_t)v.w << 32;
+          b = 16;
+        }
+      }
       while (b < nb) {
         while (r >= meta[j].len[f]) { j++; r = 0; }
         const AMeta &mt = meta[j];
