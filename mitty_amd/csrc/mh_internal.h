@@ -93,6 +93,8 @@ struct mh_ctx {
   mh::DevBuf jump_polys;
   int64_t jump_k = 0;
   int64_t fixups = 0;   // units redone on the exact fallback path
+  mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
+  int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)
 
   // scratch (grow-only), reused by all stages
   mh::DevBuf s[16];

@@ -254,6 +254,153 @@ __global__ void __launch_bounds__(DC_THREADS) k_shuffle_decode2(const DecJob *jo
   if (t == 0) *job.status = i0 < 1 ? 0 : i0;
 }
 
+// ---- chunk-parallel decode ---------------------------------------------------------------------------------------
+// Every DC_CHUNK-word chunk of every unit's shuffle stream is decoded by its own workgroup, given the draw index i0
+// the sequential decode would have at the chunk's first word (start[c]).  Those starts are a prefix sum of the
+// chunks' accept counts, which depend on the starts only through words whose masked value lies between a guessed
+// and the true i0, so the host iterates count passes (changed chunks only) from an expectation-based guess to the
+// fixed point, where every start equals the sequential one; one write pass then emits all swap indices.
+struct ChunkJob {
+  const uint32_t *words;   // the unit's shuffle stream
+  int64_t n_words;
+  int64_t base;            // first word of the chunk
+  uint32_t *j;             // the unit's swap-index array
+};
+
+constexpr int32_t DC_BIG = 1 << 30;
+
+// Per chunk: the accept count and the margin [dlo, dhi]: for every start shift d in it, no accept decision and no
+// interval mask of the chunk changes (all i shift by d), so the count stays valid.  dhi = 0 once i reached 0.
+template <bool WRITE>
+__global__ void __launch_bounds__(DC_THREADS) k_decode_chunks(const ChunkJob *jobs, const int32_t *todo,
+                                                              const int64_t *start, int32_t *count,
+                                                              int32_t *margin) {
+  __shared__ int32_t wsum[DC_WAVES];
+  __shared__ int32_t wlo[DC_WAVES], whi[DC_WAVES];
+  __shared__ int32_t s_tot;
+  const int32_t c = todo ? todo[blockIdx.x] : (int32_t)blockIdx.x;
+  const ChunkJob job = jobs[c];
+  const int64_t i0 = start[c];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (i0 < 1) {
+    if (t == 0) {
+      count[c] = 0;
+      margin[2 * c] = -DC_BIG;
+      margin[2 * c + 1] = 0;
+    }
+    return;
+  }
+  const int64_t base = job.base;
+  uint32_t w[DC_PER];
+  bool valid[DC_PER];
+  if (base + DC_PER * t + 3 < job.n_words) {
+    const uint4 q = *(const uint4 *)(job.words + base + DC_PER * t);
+    w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < DC_PER; e++) w[e] = base + DC_PER * t + e < job.n_words ? job.words[base + DC_PER * t + e] : 0u;
+  }
+#pragma unroll
+  for (int e = 0; e < DC_PER; e++) valid[e] = base + DC_PER * t + e < job.n_words;
+  // first guess of the accepts before this thread's words: the acceptance rate at i0
+  const uint32_t m0 = interval_mask((uint32_t)i0);
+  int32_t A = (int32_t)((float)(i0 + 1) / ((float)m0 + 1.0f) * (float)(DC_PER * t));
+  int32_t cnt = 0;
+  uint32_t v[DC_PER];
+  bool acc[DC_PER];
+  bool converged = false;
+  for (int it = 0; it < 24; it++) {
+    cnt = 0;
+#pragma unroll
+    for (int e = 0; e < DC_PER; e++) {
+      const int64_t i = i0 - A - cnt;
+      v[e] = (i >= 1) ? (w[e] & interval_mask((uint32_t)i)) : 0u;
+      acc[e] = valid[e] && i >= 1 && v[e] <= (uint32_t)i;
+      cnt += acc[e];
+    }
+    int32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      int32_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < DC_WAVES; q++) {
+      const int32_t s = wsum[q];
+      pre += q < wave ? s : 0;
+      tot += s;
+    }
+    const int32_t A2 = pre + incl - cnt;
+    const int same = __syncthreads_and(A2 == A);
+    A = A2;
+    if (t == 0) s_tot = tot;
+    if (same) {
+      converged = true;
+      break;
+    }
+  }
+  if (!converged) {   // exact sequential decode of the chunk (i0 comparable to the chunk size)
+    __syncthreads();
+    if (t == 0) {
+      int64_t ii = i0;
+      int64_t lo = -DC_BIG, hi = DC_BIG;
+      for (int64_t k = 0; k < DC_CHUNK && base + k < job.n_words; k++) {
+        if (ii < 1) { hi = 0; break; }
+        const uint32_t m = interval_mask((uint32_t)ii);
+        const uint32_t vv = job.words[base + k] & m;
+        lo = max(lo, (int64_t)(m >> 1) + 1 - ii);
+        hi = min(hi, (int64_t)m - ii);
+        if (vv <= (uint32_t)ii) {
+          lo = max(lo, (int64_t)vv - ii);
+          if (WRITE) job.j[ii] = vv;
+          ii--;
+        } else {
+          hi = min(hi, (int64_t)vv - ii - 1);
+        }
+      }
+      count[c] = (int32_t)(i0 - ii);
+      margin[2 * c] = (int32_t)lo;
+      margin[2 * c + 1] = (int32_t)hi;
+    }
+    return;
+  }
+  // margins of this thread's words, then block min / max
+  int64_t lo = -DC_BIG, hi = DC_BIG;
+  {
+    int32_t a = 0;
+#pragma unroll
+    for (int e = 0; e < DC_PER; e++) {
+      if (!valid[e]) continue;
+      const int64_t i = i0 - A - a;
+      if (i < 1) { hi = 0; continue; }
+      const uint32_t m = interval_mask((uint32_t)i);
+      lo = max(lo, (int64_t)(m >> 1) + 1 - i);
+      hi = min(hi, (int64_t)m - i);
+      if (acc[e]) lo = max(lo, (int64_t)v[e] - i); else hi = min(hi, (int64_t)v[e] - i - 1);
+      if (WRITE && acc[e]) job.j[i] = v[e];
+      a += acc[e];
+    }
+  }
+  int32_t l32 = (int32_t)max(lo, (int64_t)-DC_BIG), h32 = (int32_t)min(hi, (int64_t)DC_BIG);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    l32 = max(l32, __shfl_xor(l32, d, 64));
+    h32 = min(h32, __shfl_xor(h32, d, 64));
+  }
+  if (lane == 0) { wlo[wave] = l32; whi[wave] = h32; }
+  __syncthreads();
+  if (t == 0) {
+    int32_t L = -DC_BIG, H = DC_BIG;
+    for (int q = 0; q < DC_WAVES; q++) { L = max(L, wlo[q]); H = min(H, whi[q]); }
+    count[c] = s_tot;
+    margin[2 * c] = L;
+    margin[2 * c + 1] = H;
+  }
+}
+
 // Sequential-stream variant (exact fallback): MT19937 in LDS fused with the decode, one 640-thread workgroup.
 constexpr int SD_THREADS = 640;
 constexpr int SD_WAVES = SD_THREADS / 64;
@@ -554,6 +701,110 @@ struct UnitPlan {
   TplSet *out;
 };
 
+// Chunk-parallel Fisher-Yates decode of every unit in `dec` (see k_decode_chunks).  On success the swap indices are
+// written and d_status[u] = draws left undecoded (0 unless the unit ran out of pre-generated words); *done = false
+// when the starts did not reach their fixed point within the pass budget (the caller then runs k_shuffle_decode2).
+int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_status, bool *done) {
+  hipStream_t st = ctx->stream;
+  *done = false;
+  std::vector<ChunkJob> cj;
+  std::vector<int32_t> first(dec.size() + 1, 0);
+  for (size_t u = 0; u < dec.size(); u++) {
+    first[u] = (int32_t)cj.size();
+    for (int64_t b = 0; b < dec[u].n_words; b += DC_CHUNK) cj.push_back(ChunkJob{dec[u].words, dec[u].n_words, b, dec[u].j});
+  }
+  first[dec.size()] = (int32_t)cj.size();
+  const int64_t C = (int64_t)cj.size();
+  if (C == 0) {
+    *done = true;
+    return MH_OK;
+  }
+  // starts: the exact one for each unit's first chunk, then the expected accepts (rate (i+1)/(mask+1))
+  std::vector<int64_t> s0(C), s1(C);
+  std::vector<int32_t> cnt(C), todo;
+  for (size_t u = 0; u < dec.size(); u++) {
+    double i = (double)(dec[u].n - 1);
+    for (int32_t c = first[u]; c < first[u + 1]; c++) {
+      s0[c] = i >= 1.0 ? (int64_t)llround(i) : 0;
+      if (c == first[u]) s0[c] = dec[u].n - 1;
+      double rem = DC_CHUNK;
+      while (rem > 0 && i >= 1.0) {   // integrate the acceptance rate piecewise over mask epochs
+        uint32_t ii = (uint32_t)i, m = ii;
+        m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+        const double rate = (i + 1.0) / ((double)m + 1.0);
+        const double lo = (double)((m >> 1) + 1);              // i stays in this epoch while i >= lo
+        const double need = (i - lo + 1.0) / rate;             // words to leave the epoch
+        if (need >= rem) { i -= rem * rate; rem = 0; }
+        else { i = lo - 1.0; rem -= need; }
+      }
+    }
+  }
+  const size_t bytes = sizeof(ChunkJob) * C + 8 * C + 4 * C + 4 * C + 8 * C + 256;
+  MH_TRY(ensure(ctx, ctx->dec_buf, bytes));
+  char *p = (char *)ctx->dec_buf.p;
+  ChunkJob *d_jobs = (ChunkJob *)p;
+  int64_t *d_start = (int64_t *)(p + ((sizeof(ChunkJob) * C + 15) / 16) * 16);
+  int32_t *d_count = (int32_t *)(d_start + C);
+  int32_t *d_todo = d_count + C;
+  int32_t *d_margin = d_todo + C;
+  std::vector<int32_t> marg(2 * C);
+  HIPCHK(ctx, hipMemcpyAsync(d_jobs, cj.data(), sizeof(ChunkJob) * C, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_start, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
+  int64_t n_todo = C;
+  bool conv = false;
+  int passes = 0;
+  for (; passes < 64; passes++) {
+    hipLaunchKernelGGL(k_decode_chunks<false>, dim3((unsigned)n_todo), dim3(DC_THREADS), 0, st,
+                       (const ChunkJob *)d_jobs, passes ? (const int32_t *)d_todo : nullptr, (const int64_t *)d_start,
+                       d_count, d_margin);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(cnt.data(), d_count, 4 * C, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(marg.data(), d_margin, 8 * C, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    // the starts the counts imply; a chunk whose count was taken at a start outside its margin is redone there
+    todo.clear();
+    for (size_t u = 0; u < dec.size(); u++) {
+      int64_t s = dec[u].n - 1;
+      for (int32_t c = first[u]; c < first[u + 1]; c++) {
+        s1[c] = s > 0 ? s : 0;
+        const int64_t d = s1[c] - s0[c];
+        if (d < marg[2 * c] || d > marg[2 * c + 1]) todo.push_back(c);
+        s -= cnt[c];
+      }
+    }
+    if (todo.empty()) {
+      conv = true;
+      break;
+    }
+    for (int32_t c : todo) s0[c] = s1[c];
+    n_todo = (int64_t)todo.size();
+    HIPCHK(ctx, hipMemcpyAsync(d_start, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_todo, todo.data(), 4 * n_todo, hipMemcpyHostToDevice, st));
+  }
+  ctx->dec_passes = passes + 1;
+  if (!conv) return MH_OK;
+  // every start exact now: the write pass
+  HIPCHK(ctx, hipMemcpyAsync(d_start, s1.data(), 8 * C, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_decode_chunks<true>, dim3((unsigned)C), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
+                     (const int32_t *)nullptr, (const int64_t *)d_start, d_count, d_margin);
+  HIPCHK(ctx, hipGetLastError());
+  std::vector<int64_t> rem(dec.size());
+  for (size_t u = 0; u < dec.size(); u++) {
+    int64_t s = dec[u].n - 1;
+    for (int32_t c = first[u]; c < first[u + 1]; c++) s -= cnt[c];
+    rem[u] = s < 1 ? 0 : s;
+    if (dec[u].n > 0) {
+      HIPCHK(ctx, hipMemcpyAsync(d_status + (dec[u].status - d_status), &rem[u], 8, hipMemcpyHostToDevice, st));
+    }
+  }
+  // j[0] = 0 (the shuffle's unused slot), as k_shuffle_decode2 sets it
+  for (size_t u = 0; u < dec.size(); u++)
+    if (dec[u].n > 0) HIPCHK(ctx, hipMemsetAsync(dec[u].j, 0, 4, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *done = true;
+  return MH_OK;
+}
+
 // Everything after the word streams for one unit: ts (geometric scan), shuffle, tlen + keep + compaction into
 // `out`, file order.  `exact`: materialise the draws and recompute flagged ones on the host (rare path).
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
@@ -743,9 +994,13 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       HIPCHK(ctx, hipGetLastError());
       stage_end(ctx);
       stage_begin(ctx, "sample_shuffle_decode");
-      hipLaunchKernelGGL(k_shuffle_decode2, dim3((unsigned)dec.size()), dim3(DC_THREADS), 0, st,
-                         (const DecJob *)d_dec);
-      HIPCHK(ctx, hipGetLastError());
+      bool done = false;
+      MH_TRY(decode_parallel(ctx, dec, d_status, &done));
+      if (!done) {   // no fixed point within the pass budget: the block-sequential decode
+        hipLaunchKernelGGL(k_shuffle_decode2, dim3((unsigned)dec.size()), dim3(DC_THREADS), 0, st,
+                           (const DecJob *)d_dec);
+        HIPCHK(ctx, hipGetLastError());
+      }
       stage_end(ctx);
       // keep the job tables alive until the kernels ran
       HIPCHK(ctx, hipStreamSynchronize(st));
