@@ -11,8 +11,8 @@ Inputs (contig bytes) are resident before timing; variant arrays are re-uploaded
 Multi-GPU (torchrun, one process per GPU): every rank simulates its own chr1-shaped chromosome (weak scaling, no
 data-path collective); an RCCL all-reduce of the per-rank template counts closes each step.
 
-Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_assemble; k_emit_write with
---emit-mode 1): algorithmic bytes per launch =
+Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_direct; k_emit_write with
+--emit-mode 1 or --corrupt): algorithmic bytes per launch =
 sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ bytes written (both files), divided by the
 launch's HIP-event duration; `stage_ms` gives every stage per step so the dominant kernel is visible.
 """
@@ -45,7 +45,7 @@ def parse():
                   help='bounded CPU-oracle sample: one unit on the first N Mbp of the contig (0 = skip)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
-  ap.add_argument('--emit-mode', type=int, default=0, help='0: pull-model assembler, 1: LDS-image writer')
+  ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
   return ap.parse_args()
 
 
@@ -82,7 +82,7 @@ def main():
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), a.seed)
   eng.load_region(0, ('1', 0, a.length), seq)
   eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_assemble'
+  kernel = 'k_emit_write' if (a.emit_mode or a.corrupt) else 'k_emit_direct'
 
   def step():
     eng.drop_haplotypes()

@@ -206,9 +206,12 @@ int32_t mh_enable_timing(mh_ctx *ctx, int32_t on);
 /* Host computation of the MT19937 window (x_J .. x_{J+623}, untempered) of the stream seeded with `seed`, via the
  * jump polynomial x^J mod P — the same math the device segments use (tests compare it with the plain recurrence). */
 int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624);
-/* Emission kernel choice: 0 = pull-model assembler (default; falls back to 1 for a unit whose qname reads part
- * exceeds 256 bytes), 1 = LDS-image writer always. */
+/* Emission kernel choice: 0 = direct writer (default; falls back to 1 for a unit whose qname reads part exceeds
+ * 256 bytes, with fused corruption, or for sample names too long for its LDS layout), 1 = LDS-image writer always. */
 int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode);
+/* Fisher-Yates swap-index decode: 0 = chunk-parallel (default; falls back to 1 when the chunk starts do not reach
+ * their fixed point), 1 = block-sequential always. */
+int32_t mh_set_decode_mode(mh_ctx *ctx, int32_t mode);
 /* Units the context redid on the exact sequential fallback path (decode out of words / near-integer quotient). */
 int32_t mh_fixup_count(mh_ctx *ctx, int64_t *n);
 

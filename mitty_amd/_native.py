@@ -19,7 +19,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
-           'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode',
+           'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy']
@@ -105,6 +105,7 @@ def lib():
   _sig(L, 'mh_mt_window_at', [ctypes.c_uint32, c_u64, c_vp])
   _sig(L, 'mh_fixup_count', [c_vp, P_i64])
   _sig(L, 'mh_set_emit_mode', [c_vp, c_i32])
+  _sig(L, 'mh_set_decode_mode', [c_vp, c_i32])
   _lib = L
   return L
 
@@ -320,8 +321,12 @@ class Context:
     self._chk(self._L.mh_release_templates(self._h, int(tpl_id)))
 
   def set_emit_mode(self, mode):
-    """0: pull-model assembler (default), 1: LDS-image writer."""
+    """0: direct writer (default), 1: LDS-image writer."""
     self._chk(self._L.mh_set_emit_mode(self._h, int(mode)))
+
+  def set_decode_mode(self, mode):
+    """0: chunk-parallel shuffle decode (default), 1: block-sequential decode."""
+    self._chk(self._L.mh_set_decode_mode(self._h, int(mode)))
 
   def fixup_count(self):
     n = c_i64()

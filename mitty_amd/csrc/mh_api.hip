@@ -489,6 +489,12 @@ int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode) {
   return MH_OK;
 }
 
+int32_t mh_set_decode_mode(mh_ctx *ctx, int32_t mode) {
+  if (!ctx || mode < 0 || mode > 1) return MH_E_ARG;
+  ctx->decode_sequential = mode == 1;
+  return MH_OK;
+}
+
 int32_t mh_fixup_count(mh_ctx *ctx, int64_t *n) {
   if (!ctx || !n) return MH_E_ARG;
   *n = ctx->fixups;

@@ -446,7 +446,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
     if (herr & BE_CHROM) m += " qname chrom not among the @SQ names (.ann);";
     if (herr & BE_FIELDS) m += " qname does not parse (readgenerate.parse_qname);";
     if (herr & BE_CIGAR) m += " invalid CIGAR in qname;";
-    if (herr & BE_SEQ) m += " sequence and quality lengths differ;";
+    if (herr & BE_SEQ) m += " quality and sequence mismatch (sequence and quality lengths differ);";
     return arg_fail(ctx, MH_E_ARG, m);
   }
   // record offsets (appended to the store)

@@ -522,41 +522,46 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
   }
 }
 
-// ---- pull-model assembler ------------------------------------------------------------------------------------
-// Every thread builds whole 16-byte output chunks in registers: it finds the record holding the chunk's first byte
-// and walks the record's fields ('@stub:' | cnt | '|chrom|cpy' | reads part of the qname (slot) | '\n' | bases |
-// '\n+\n' | qualities | '\n'), pulling bytes from LDS (haplotype windows, qname slots) or constants; full chunks
-// leave as one 16-byte aligned store, the two ragged ends of the workgroup's range as byte stores.
-constexpr int EA_T = 32;
-constexpr int EA_THREADS = 256;
+// ---- direct writer -------------------------------------------------------------------------------------------
+// The default emission kernel.  k_emit_measure has already formatted the reads part of every kept template's qname
+// into a 256-byte slot; here, per 32-template tile:
+//   P0/P1 (one phase, no barrier between): owner threads write the qname head ('@stub:' cnt '|chrom|cpy') right-
+//          aligned before the slot area of the template's qname buffer in LDS, and every thread issues the 16-byte
+//          gathers of both mates' haplotype windows and of the slots (straight into the qname buffers), so the qname
+//          is one contiguous LDS string;
+//   P2     one wave per (template, file) record writes the record straight to the FASTQ arena as aligned dwords:
+//          each lane builds the dword at its global address from up to three byte ranges (qname, bases — reversed
+//          and complemented for mate 1 — and the '\n' '+' '\n' / '~' / '\n' constants) with unaligned LDS reads
+//          (v_alignbyte) and byte masks; the '~' run is a second, constant sweep; the partial dwords at the two ends
+//          of a record are byte stores (the neighbouring record owns the other bytes).
+// No LDS image and no copy-out pass: one barrier per tile, ~23 KB of LDS, six workgroups per CU.
+constexpr int ED_T = 32;
+constexpr int ED_THREADS = 256;
+constexpr int ED_WAVES = ED_THREADS / 64;
 
-struct AMeta {
-  int32_t start[2], len[2];   // record start (workgroup-relative) and length per file; len 0 = dropped
-  int32_t e1, e3;             // end of the cnt digits / of the reads part (record-relative)
-  int32_t S[2], win[2];       // per file: bases, LDS window offset of the read's first base
-  int32_t rc;                 // bit f: file f holds mate 1 (reverse complement)
-  int32_t nd;                 // cnt digits
-  uint32_t bcd_lo, bcd_hi;    // cnt digits, 4 bits each, least significant first
-  int32_t rest_off;           // LDS offset of the slot copy
+struct DMeta {
+  int32_t rel[2];    // record start relative to the tile's first byte, per file
+  int32_t len[2];    // record length per file (0: template dropped by the N filter)
+  int32_t qoff;      // LDS offset of the qname's first byte ('@')
+  int32_t ql;        // qname length (no '\n')
+  int32_t S[2];      // bases per file
+  int32_t win[2];    // LDS offset of the file's read's first base inside its window
+  int32_t rc;        // bit f: file f holds mate 1 (reverse complement)
   int32_t pad;
 };
 
-struct Emit16 {
-  uint64_t lo, hi;
-  __device__ __forceinline__ void put(int b, uint8_t c) {
-    if (b < 8) lo |= (uint64_t)c << (8 * b); else hi |= (uint64_t)c << (8 * (b - 8));
-  }
-};
-
-// 16 bytes from an arbitrary LDS address: five aligned dword reads + v_alignbyte.
-__device__ __forceinline__ uint4 lds_load16(const uint8_t *p) {
+// 4 bytes from an arbitrary LDS address (two aligned dword reads + v_alignbyte)
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {
   const uintptr_t a = (uintptr_t)p;
   const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
-  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-  if (sh == 0) return make_uint4(w0, w1, w2, w3);
-  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// bytes i (0..3) of a dword whose byte i sits at record offset x0 + i, with x0 + i < n
+__device__ __forceinline__ uint32_t lt_mask(int32_t x0, int32_t n) {
+  int32_t k = n - x0;
+  k = k < 0 ? 0 : (k > 4 ? 4 : k);
+  return (uint32_t)((1ull << (8 * k)) - 1ull);
 }
 
 // 0xff in every byte of x equal to the byte replicated in c
@@ -573,59 +578,51 @@ __device__ __forceinline__ uint32_t comp4(uint32_t x) {
   return x ^ (at & 0x15151515u) ^ (cg & 0x04040404u);
 }
 
-__global__ void __launch_bounds__(EA_THREADS) k_emit_assemble(HapView h, int64_t m, const int64_t *pos0,
-                                                              const int64_t *pos1, const int8_t *fo0, int64_t rlen,
-                                                              QFixed q, const Rec *recs, const E3 *off,
-                                                              const uint8_t *slots, char *out1, char *out2,
-                                                              int write2, int32_t win_stride, CorruptCfg cc) {
+__global__ void __launch_bounds__(ED_THREADS) k_emit_direct(HapView h, int64_t m, const int64_t *pos0,
+                                                            const int64_t *pos1, const int8_t *fo0, int64_t rlen,
+                                                            QFixed q, const Rec *recs, const E3 *off,
+                                                            const uint8_t *slots, char *out1, char *out2,
+                                                            int write2, int32_t win_stride, int32_t head,
+                                                            int32_t qstride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  AMeta *meta = (AMeta *)smem;
-  uint8_t *wins = (uint8_t *)smem + ((sizeof(AMeta) * EA_T + 15) / 16) * 16;
-  uint8_t *rests = wins + (size_t)EA_T * 2 * win_stride;
-  char *fixed = (char *)(rests + (size_t)EA_T * SLOT);   // prefix | mid
-  __shared__ int64_t s_g0[2], s_g1[2];
+  DMeta *meta = (DMeta *)smem;
+  uint8_t *wins = (uint8_t *)smem + ((sizeof(DMeta) * ED_T + 15) / 16) * 16;
+  uint8_t *qbuf = wins + (size_t)ED_T * 2 * win_stride;
 
-  const int64_t t0 = (int64_t)blockIdx.x * EA_T;
-  const int64_t t1 = t0 + EA_T < m ? t0 + EA_T : m;
+  const int64_t t0 = (int64_t)blockIdx.x * ED_T;
+  const int64_t t1 = t0 + ED_T < m ? t0 + ED_T : m;
   const int nt = (int)(t1 - t0);
-  const int nfile = write2 ? 2 : 1;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Lp = q.prefix_len, Lm = q.mid_len;
+  const E3 base = off[t0];
 
-  for (int i = tid; i < Lp + Lm; i += EA_THREADS) fixed[i] = i < Lp ? q.prefix[i] : q.mid[i - Lp];
-  if (tid == 0) {
-    const E3 a = off[t0], b = off[t1];
-    s_g0[0] = a.b1; s_g0[1] = a.b2;
-    s_g1[0] = b.b1; s_g1[1] = b.b2;
-  }
-  // ---- per-template metadata ----------------------------------------------------------------------------------
+  // ---- P0: per-template metadata and the qname head -----------------------------------------------------------
   if (tid < nt) {
     const int64_t t = t0 + tid;
     const Rec rc = recs[t];
-    const E3 o = off[t];
-    const E3 base = off[t0];
-    AMeta mt;
-    mt.start[0] = (int32_t)(o.b1 - base.b1);
-    mt.start[1] = (int32_t)(o.b2 - base.b2);
-    mt.len[0] = rc.keep ? rc.len1 : 0;
-    mt.len[1] = rc.keep ? rc.len2 : 0;
-    mt.rest_off = tid * SLOT;
+    DMeta mt;
+    mt.len[0] = mt.len[1] = 0;
+    mt.rc = 0;
     if (rc.keep) {
-      const int64_t cnt = o.kept + 1;
-      uint64_t bcd = 0;
-      int nd = 0;
-      uint64_t x = (uint64_t)cnt;
-      do { bcd |= (uint64_t)(x % 10u) << (4 * nd); x /= 10u; nd++; } while (x && nd < 16);
-      mt.nd = nd;
-      mt.bcd_lo = (uint32_t)bcd;
-      mt.bcd_hi = (uint32_t)(bcd >> 32);
-      mt.e1 = Lp + nd;
-      mt.e3 = mt.e1 + Lm + rc.rest;
+      const E3 o = off[t];
+      mt.rel[0] = (int32_t)(o.b1 - base.b1);
+      mt.rel[1] = (int32_t)(o.b2 - base.b2);
+      uint64_t x = (uint64_t)(o.kept + 1);   // cnt: 1-based among kept templates (readgenerate.py:209-210)
+      const int nd = ndig_u(x);
+      uint32_t x32 = (uint32_t)x;            // the host caps templates per launch below 2^32
+      const int lh = Lp + nd + Lm;
+      mt.qoff = tid * qstride + head - lh;
+      mt.ql = lh + rc.rest;
+      mt.len[0] = rc.len1 + nd;              // Rec lengths exclude the cnt digits
+      mt.len[1] = rc.len2 + nd;
+      uint8_t *d = qbuf + mt.qoff;
+      for (int i = 0; i < Lp; i++) d[i] = (uint8_t)q.prefix[i];
+      for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (uint8_t)('0' + x32 % 10u); x32 /= 10u; }
+      for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (uint8_t)q.mid[i];
       const int f0 = fo0[t];
       const int64_t p[2] = {pos0[t], pos1[t]};
-      mt.rc = 0;
       for (int f = 0; f < 2; f++) {
-        const int s = f == f0 ? 0 : 1;
+        const int s = f == f0 ? 0 : 1;       // file f holds mate s (reads[fo] = mate, readgenerate.py:207)
         int64_t a = p[s] - h.p_min, e = p[s] + rlen - h.p_min;
         if (e > h.hap_len) e = h.hap_len;
         if (a > h.hap_len) a = h.hap_len;
@@ -633,157 +630,90 @@ __global__ void __launch_bounds__(EA_THREADS) k_emit_assemble(HapView h, int64_t
         mt.win[f] = (tid * 2 + s) * win_stride + (int)(a & 15);
         mt.rc |= s << f;
       }
-    } else {
-      mt.nd = 0; mt.bcd_lo = mt.bcd_hi = 0; mt.e1 = mt.e3 = 0; mt.S[0] = mt.S[1] = 0; mt.win[0] = mt.win[1] = 0;
-      mt.rc = 0;
     }
     meta[tid] = mt;
   }
-  __syncthreads();
-  // ---- gathers: both mates' haplotype windows and the qname slots (all loads in flight) ------------------------
+  // ---- P1: haplotype windows and qname slots into LDS (all loads of the tile in flight) -----------------------
   const int chunks = win_stride / 16;
-  for (int it = tid; it < nt * 2 * chunks; it += EA_THREADS) {
+  for (int it = tid; it < nt * 2 * chunks; it += ED_THREADS) {
     const int j = it / (2 * chunks), rem = it - j * 2 * chunks, s = rem / chunks, c = rem - s * chunks;
-    if (meta[j].len[0] == 0) continue;
     const int64_t t = t0 + j;
     int64_t a = (s ? pos1[t] : pos0[t]) - h.p_min;
     if (a > h.hap_len) a = h.hap_len;
     const int64_t a16 = a & ~(int64_t)15;
-    if (a16 + 16 * c < a + rlen)
+    if (a16 + 16 * c < a + rlen && recs[t].keep)
       *(uint4 *)(wins + (size_t)(j * 2 + s) * win_stride + 16 * c) = *(const uint4 *)(h.hap + a16 + 16 * c);
   }
-  for (int it = tid; it < nt * (SLOT / 16); it += EA_THREADS) {
+  for (int it = tid; it < nt * (SLOT / 16); it += ED_THREADS) {
     const int j = it / (SLOT / 16), c = it - j * (SLOT / 16);
-    const AMeta &mt = meta[j];
-    if (mt.len[0] == 0 || 16 * c >= mt.e3 - mt.e1 - Lm) continue;
-    *(uint4 *)(rests + mt.rest_off + 16 * c) = *(const uint4 *)(slots + (t0 + j) * SLOT + 16 * c);
+    const Rec &rc = recs[t0 + j];
+    if (!rc.keep || 16 * c >= rc.rest) continue;
+    *(uint4 *)(qbuf + (size_t)j * qstride + head + 16 * c) = *(const uint4 *)(slots + (t0 + j) * SLOT + 16 * c);
   }
   __syncthreads();
 
-  // ---- assemble ------------------------------------------------------------------------------------------------
-  for (int f = 0; f < nfile; f++) {
-    const int64_t G0 = s_g0[f], G1 = s_g1[f];
-    if (G1 <= G0) continue;
+  // ---- P2: records straight to the arenas ----------------------------------------------------------------------
+  const int nfile = write2 ? 2 : 1;
+  const int32_t Q = (int32_t)rlen;   // perfect reads: rlen '~' (readgenerate.py:229)
+  for (int pr = wave; pr < nt * nfile; pr += ED_WAVES) {
+    const int j = pr / nfile, f = pr - j * nfile;
+    const DMeta &mt = meta[j];
+    const int32_t L = mt.len[f];
+    if (L == 0) continue;
+    const int64_t G0 = f ? base.b2 : base.b1;
     char *out = f ? out2 : out1;
-    int64_t A0 = (G0 + 15) & ~(int64_t)15, A1 = G1 & ~(int64_t)15;
-    if (A0 > G1) A0 = G1;
-    if (A1 < A0) A1 = A0;
-    const int64_t nvec = (A1 - A0) >> 4;
-    // work items: 0 = head [G0, A0), 1 = tail [A1, G1), 2.. = full chunks
-    for (int64_t w = tid; w < nvec + 2; w += EA_THREADS) {
-      int64_t gs, ge;
-      if (w == 0) { gs = G0; ge = A0; }
-      else if (w == 1) { gs = A1; ge = G1; }
-      else { gs = A0 + ((w - 2) << 4); ge = gs + 16; }
-      if (ge <= gs) continue;
-      const int nb = (int)(ge - gs);
-      const int32_t g = (int32_t)(gs - G0);
-      // record holding byte g: the last record whose start <= g (dropped records have length 0)
-      int lo = 0, hi = nt;
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (meta[mid].start[f] <= g) lo = mid + 1; else hi = mid;
-      }
-      int j = lo - 1;
-      int r = g - meta[j].start[f];
-      Emit16 e{0, 0};
-      int b = 0;
-      if (nb == 16 && !cc.enable) {
-        // fast paths: a chunk entirely inside the bases or the '~' qualities of one record (most of the bytes)
-        while (r >= meta[j].len[f]) { j++; r = 0; }
-        const AMeta &mt = meta[j];
-        const int S = mt.S[f];
-        const int e3 = mt.e3, e5 = e3 + 1 + S, e6 = e5 + 3, e7 = e6 + (int)rlen;
-        if (r >= e6 && r + 16 <= e7) {
-          e.lo = e.hi = 0x7e7e7e7e7e7e7e7eull;
-          b = 16;
-        } else if (r > e3 && r + 16 <= e5) {
-          const int k0 = r - e3 - 1;
-          const uint8_t *w = wins + mt.win[f];
-          uint4 v;
-          if ((mt.rc >> f) & 1) {   // mate 1: reversed, complemented
-            const uint4 u = lds_load16(w + S - 16 - k0);
-            v = make_uint4(comp4(__builtin_bswap32(u.w)), comp4(__builtin_bswap32(u.z)),
-                           comp4(__builtin_bswap32(u.y)), comp4(__builtin_bswap32(u.x)));
-          } else {
-            v = lds_load16(w + k0);
-          }
-          e.lo = (uint64_t)v.x | (uint64_t)v.y << 32;
-          e.hi = (uint64_t)v.z | (uint64_t)v.w << 32;
-          b = 16;
-        }
-      }
-      while (b < nb) {
-        while (r >= meta[j].len[f]) { j++; r = 0; }
-        const AMeta &mt = meta[j];
-        const int S = mt.S[f];
-        const int Q = cc.enable ? S : (int)rlen;
-        const int e3 = mt.e3, e5 = e3 + 1 + S, e6 = e5 + 3, e7 = e6 + Q;
-        int n;
-        if (r < Lp) {
-          n = min(nb - b, Lp - r);
-          for (int k = 0; k < n; k++) e.put(b + k, (uint8_t)fixed[r + k]);
-        } else if (r < mt.e1) {
-          n = min(nb - b, mt.e1 - r);
-          const uint64_t bcd = ((uint64_t)mt.bcd_hi << 32) | mt.bcd_lo;
-          for (int k = 0; k < n; k++) {
-            const int di = mt.nd - 1 - (r + k - Lp);
-            e.put(b + k, (uint8_t)('0' + ((bcd >> (4 * di)) & 15)));
-          }
-        } else if (r < mt.e1 + Lm) {
-          n = min(nb - b, mt.e1 + Lm - r);
-          for (int k = 0; k < n; k++) e.put(b + k, (uint8_t)fixed[Lp + r + k - mt.e1]);
-        } else if (r < e3) {
-          n = min(nb - b, e3 - r);
-          const uint8_t *src = rests + mt.rest_off + (r - mt.e1 - Lm);
-          for (int k = 0; k < n; k++) e.put(b + k, src[k]);
-        } else if (r == e3 || r == e5 || r == e5 + 2 || r == e7) {
-          n = 1;
-          e.put(b, '\n');
-        } else if (r == e5 + 1) {
-          n = 1;
-          e.put(b, '+');
-        } else if (r < e5) {
-          const int k0 = r - e3 - 1;
-          n = min(nb - b, e5 - r);
-          const uint8_t *w = wins + mt.win[f];
-          const bool rcf = (mt.rc >> f) & 1;
-          for (int k = 0; k < n; k++) {
-            const int kk = k0 + k;
-            uint8_t c = rcf ? comp(w[S - 1 - kk]) : w[kk];
-            if (cc.enable) {
-              uint8_t qq;
-              corrupt_base(cc, t0 + j, f, kk, c, qq);
-            }
-            e.put(b + k, c);
-          }
-        } else {   // qualities
-          const int k0 = r - e6;
-          n = min(nb - b, e7 - r);
-          if (!cc.enable) {
-            for (int k = 0; k < n; k++) e.put(b + k, '~');
-          } else {
-            const uint8_t *w = wins + mt.win[f];
-            const bool rcf = (mt.rc >> f) & 1;
-            for (int k = 0; k < n; k++) {
-              const int kk = k0 + k;
-              uint8_t c = rcf ? comp(w[S - 1 - kk]) : w[kk], qq;
-              corrupt_base(cc, t0 + j, f, kk, c, qq);
-              e.put(b + k, qq);
-            }
-          }
-        }
-        b += n;
-        r += n;
-      }
-      if (nb == 16 && (gs & 15) == 0) {
-        *(uint4 *)(out + gs) = make_uint4((uint32_t)e.lo, (uint32_t)(e.lo >> 32), (uint32_t)e.hi,
-                                          (uint32_t)(e.hi >> 32));
+    const uintptr_t ga = (uintptr_t)(out + G0 + mt.rel[f]);   // global address of the record's first byte
+    const int32_t ql = mt.ql, S = mt.S[f];
+    const int32_t sb = ql + 1;            // first base
+    const int32_t tl = sb + S;            // '\n' '+' '\n' then Q '~' then '\n'
+    const int32_t qa = tl + 3, qe = qa + Q;
+    const uint8_t *qn = qbuf + mt.qoff;
+    const uint8_t *w = wins + mt.win[f];
+    const bool rcf = (mt.rc >> f) & 1;
+    // dword range of the record, and the constant '~' dwords inside it
+    const uintptr_t d0 = ga >> 2, d1 = (ga + L + 3) >> 2;
+    uintptr_t c0 = (ga + qa + 3) >> 2, c1 = (ga + qe) >> 2;
+    if (c1 < c0) c1 = c0;
+    const int32_t n1 = (int32_t)(c0 - d0), nA = n1 + (int32_t)(d1 - c1);
+    // sweep A: everything except the '~' dwords
+    for (int32_t k = lane; k < nA; k += 64) {
+      const uintptr_t d = k < n1 ? d0 + k : c1 + (k - n1);
+      const int32_t x0 = (int32_t)((intptr_t)(d << 2) - (intptr_t)ga);   // record offset of the dword's byte 0
+      // qname bytes
+      const int32_t xq = x0 < ql ? x0 : ql;
+      const uint32_t vq = lds_u32(qn + xq);
+      // bases
+      int32_t y = x0 - sb;
+      y = y < -3 ? -3 : (y > S ? S : y);
+      uint32_t vs;
+      if (rcf) {
+        const uint32_t u = lds_u32(w + (S - 4 - y));
+        vs = comp4(__builtin_bswap32(u));
       } else {
-        for (int k = 0; k < nb; k++)
-          out[gs + k] = (char)(k < 8 ? (e.lo >> (8 * k)) : (e.hi >> (8 * (k - 8))));
+        vs = lds_u32(w + y);
+      }
+      // constants: '\n' after the qname, '\n+\n', '~', final '\n'
+      uint32_t vc = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int32_t x = x0 + i;
+        const uint32_t c = (x == ql || x == tl || x == tl + 2 || x == qe) ? 0x0au : (x == tl + 1 ? 0x2bu : 0x7eu);
+        vc |= c << (8 * i);
+      }
+      const uint32_t mq = lt_mask(x0, ql);
+      const uint32_t ms = lt_mask(x0, tl) & ~lt_mask(x0, sb);
+      const uint32_t v = (vq & mq) | (vs & ms) | (vc & ~(mq | ms));
+      char *g = (char *)(d << 2);
+      if (x0 >= 0 && x0 + 4 <= L) {
+        *(uint32_t *)g = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (x0 + i >= 0 && x0 + i < L) g[i] = (char)(v >> (8 * i));
       }
     }
+    // sweep B: the '~' dwords
+    for (uintptr_t d = c0 + lane; d < c1; d += 64) *(uint32_t *)(d << 2) = 0x7e7e7e7eu;
   }
 }
 
@@ -889,13 +819,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   Rec *recs = (Rec *)ctx->s[14].p;
   E3 *off = (E3 *)ctx->s[15].p;
 
-  const bool assemble = !ctx->emit_lds_only;
+  const bool direct = !ctx->emit_lds_only && !ctx->corrupt_on;   // fused corruption uses the LDS-image writer
   int32_t *overflow = (int32_t *)(small + 40);
-  if (assemble) MH_TRY(ensure(ctx, ctx->emit_slots, (size_t)SLOT * (m + 1)));
+  if (direct) MH_TRY(ensure(ctx, ctx->emit_slots, (size_t)SLOT * (m + 1)));
   stage_begin(ctx, "emit_measure");
   hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
                      rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                     assemble ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow);
+                     direct ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");
@@ -937,22 +867,24 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
   }
   int32_t hover = 0;
-  if (assemble) {
+  if (direct) {
     HIPCHK(ctx, hipMemcpyAsync(&hover, overflow, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
   }
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   stage_begin(ctx, "emit_write");
-  if (assemble && !hover) {
-    // pull-model assembler (qname reads part formatted by k_emit_measure into 256-byte slots)
-    const size_t lds_a = ((sizeof(AMeta) * EA_T + 15) / 16) * 16 + (size_t)EA_T * 2 * win_stride +
-                         (size_t)EA_T * SLOT + 4160;
-    const int64_t nblk_a = (m + EA_T - 1) / EA_T;
-    hipLaunchKernelGGL(k_emit_assemble, dim3((unsigned)nblk_a), dim3(EA_THREADS), lds_a, st, hv, m,
+  const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 24) + 15) / 16 * 16);
+  const int32_t qstride = head + SLOT + 16;
+  const size_t lds_d = ((sizeof(DMeta) * ED_T + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride +
+                       (size_t)ED_T * qstride;
+  if (direct && !hover && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
+    // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots)
+    const int64_t nblk_d = (m + ED_T - 1) / ED_T;
+    hipLaunchKernelGGL(k_emit_direct, dim3((unsigned)nblk_d), dim3(ED_THREADS), lds_d, st, hv, m,
                        pos0, pos1, fo0, rlen, q,
                        (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p, o1, o2, write_fastq2,
-                       win_stride, cc);
+                       win_stride, head, qstride);
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot
     const int64_t nblk = (m + EW_T - 1) / EW_T;

@@ -111,6 +111,7 @@ struct mh_ctx {
   // emission: per-template qname slots; emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   mh::DevBuf emit_slots;
   bool emit_lds_only = false;
+  bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas
   mh::DevBuf out1, out2;

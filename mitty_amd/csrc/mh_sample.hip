@@ -995,7 +995,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       stage_end(ctx);
       stage_begin(ctx, "sample_shuffle_decode");
       bool done = false;
-      MH_TRY(decode_parallel(ctx, dec, d_status, &done));
+      if (!ctx->decode_sequential) MH_TRY(decode_parallel(ctx, dec, d_status, &done));
       if (!done) {   // no fixed point within the pass budget: the block-sequential decode
         hipLaunchKernelGGL(k_shuffle_decode2, dim3((unsigned)dec.size()), dim3(DC_THREADS), 0, st,
                            (const DecJob *)d_dec);

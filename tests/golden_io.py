@@ -41,3 +41,16 @@ def parse_fastq(b):
   for i in range(0, len(lines) - 3, 4):
     recs.append((lines[i][1:].decode(), lines[i + 1].decode(), lines[i + 3].decode()))
   return recs
+
+
+def check_same(got, want, what='output'):
+  """Byte-exact comparison that reports the first differing line (pytest's own diff of multi-MB bytes takes
+  minutes)."""
+  if got == want:
+    return
+  lg, lw = got.split(b'\n'), want.split(b'\n')
+  for i, (x, y) in enumerate(zip(lg, lw)):
+    if x != y:
+      raise AssertionError('{} differs at line {}: got {!r} want {!r}'.format(what, i, x[:300], y[:300]))
+  raise AssertionError('{} differs in length: {} vs {} lines ({} vs {} bytes)'.format(what, len(lg), len(lw),
+                                                                                       len(got), len(want)))

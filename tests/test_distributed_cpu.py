@@ -57,8 +57,8 @@ def test_distributed_output_identical_to_single_process(tmp_path, world, layout)
   model = 'hiseq-X-v2.5-Garvan'
   mp.start_processes(_rank, args=(world, port, layout, model, str(tmp_path)), nprocs=world, join=True,
                      start_method='spawn')
-  assert open(tmp_path / 'r1.fq', 'rb').read() == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
-  assert open(tmp_path / 'r2.fq', 'rb').read() == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+  G.check_same(open(tmp_path / 'r1.fq', 'rb').read(), G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
+  G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
 
 
 def test_distributed_gz_output(tmp_path):
@@ -71,8 +71,8 @@ def test_distributed_gz_output(tmp_path):
     port = s.getsockname()[1]
   mp.start_processes(_rank_gz, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
   model = 'hiseq-X-v2.5-Garvan'
-  assert gzip.open(str(tmp_path / 'r1.fq.gz')).read() == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
-  assert gzip.open(str(tmp_path / 'r2.fq.gz')).read() == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+  G.check_same(gzip.open(str(tmp_path / 'r1.fq.gz')).read(), G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
+  G.check_same(gzip.open(str(tmp_path / 'r2.fq.gz')).read(), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
 
 
 def _rank_gz(rank, world, port, outdir):

@@ -87,8 +87,8 @@ def test_e2e_fastq_byte_identical(model):
   mdl = G.model(model)
   b1, b2, n = O.generate_reads_fastq(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mdl,
                                      c['coverage'], c['seed'])
-  assert b1 == G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model))
-  assert b2 == G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
+  G.check_same(b1, G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
+  G.check_same(b2, G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
 
 
 @pytest.mark.parametrize('model', G.MODELS)
@@ -96,8 +96,8 @@ def test_corruption_exact(model):
   r1 = G.parse_fastq(G.fastq_bytes('corrupt_in_{}.r1.fq.gz'.format(model)))
   r2 = G.parse_fastq(G.fastq_bytes('corrupt_in_{}.r2.fq.gz'.format(model)))
   b1, b2 = O.corrupt_fastq(G.model(model), [r[0] for r in r1], [r[1] for r in r1], [r[1] for r in r2], seed=7)
-  assert b1 == G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model))
-  assert b2 == G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model))
+  G.check_same(b1, G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model)))
+  G.check_same(b2, G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model)))
 
 
 # ---- god-aligner (oracle/god.py) ------------------------------------------------------------------------------
