@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       out.rest = ql - q.prefix_len - q.mid_len;
       local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
       if (slots != nullptr) {
-        if (out.rest > SLOT) {
+        if (out.rest + 1 > SLOT) {   // the slot holds the reads part and the qname's '\n'
           atomicOr(overflow, 1);
         } else {   // the reads part of the qname, in file order (readgenerate.py:223-225)
           ByteWriter bw{(uint32_t *)(slots + t * SLOT), 0u, 0};
@@ -304,6 +304,7 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
               first = false;
             }
           }
+          bw.put('\n');
           bw.flush();
         }
       }
@@ -523,41 +524,42 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 }
 
 // ---- direct writer -------------------------------------------------------------------------------------------
-// The default emission kernel.  k_emit_measure has already formatted the reads part of every kept template's qname
-// into a 256-byte slot; here, per 32-template tile:
-//   P0/P1 (one phase, no barrier between): owner threads write the qname head ('@stub:' cnt '|chrom|cpy') right-
-//          aligned before the slot area of the template's qname buffer in LDS, and every thread issues the 16-byte
-//          gathers of both mates' haplotype windows and of the slots (straight into the qname buffers), so the qname
-//          is one contiguous LDS string;
-//   P2     one wave per (template, file) record writes the record straight to the FASTQ arena as aligned dwords:
-//          each lane builds the dword at its global address from up to three byte ranges (qname, bases — reversed
-//          and complemented for mate 1 — and the '\n' '+' '\n' / '~' / '\n' constants) with unaligned LDS reads
-//          (v_alignbyte) and byte masks; the '~' run is a second, constant sweep; the partial dwords at the two ends
-//          of a record are byte stores (the neighbouring record owns the other bytes).
-// No LDS image and no copy-out pass: one barrier per tile, ~23 KB of LDS, six workgroups per CU.
+// The default emission kernel (no fused corruption).  Every FASTQ record is three byte strings held in LDS:
+//   Q  the qname line: head ('@stub:' cnt '|chrom|cpy', written by the owner thread) + the reads part and '\n'
+//      that k_emit_measure formatted into the template's 256-byte slot (gathered in 16-byte chunks);
+//   B  the bases: the haplotype window of the file's mate, gathered in 16-byte chunks; mate 1's chunks are
+//      reversed and complemented in registers on the way in and stored mirrored, so B is forward in both cases;
+//   T  '\n+\n' + rlen '~' + '\n', one copy per workgroup (identical for every perfect read).
+// P0/P1 (one phase): metadata, Q heads, T, and all gathers of the 32-template tile in flight; one barrier; then
+// P2 writes the tile's output bytes as aligned 16-byte stores straight to the arenas, in two sweeps:
+//   pure  chunks inside one string of one record: one unaligned 16-byte LDS read (v_alignbyte) and one store;
+//   seam  the (at most four) chunks per record that straddle strings or records — record start (previous record's
+//         T end + Q), Q|B, B|T, and the tile's ragged end — merged per dword with byte masks (v_bfi); the tile's
+//         first and last chunks are byte stores of the tile's own bytes (the neighbouring tiles own the rest).
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
-constexpr int ED_WAVES = ED_THREADS / 64;
+constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
 
 struct DMeta {
   int32_t rel[2];    // record start relative to the tile's first byte, per file
   int32_t len[2];    // record length per file (0: template dropped by the N filter)
-  int32_t qoff;      // LDS offset of the qname's first byte ('@')
-  int32_t ql;        // qname length (no '\n')
+  int32_t qb;        // LDS offset of Q (qname '@' ... '\n')
+  int32_t sb;        // Q length = offset of the first base
+  int32_t bb[2];     // LDS offset of B per file (forward order)
   int32_t S[2];      // bases per file
-  int32_t win[2];    // LDS offset of the file's read's first base inside its window
-  int32_t rc;        // bit f: file f holds mate 1 (reverse complement)
-  int32_t pad;
 };
 
-// 4 bytes from an arbitrary LDS address (two aligned dword reads + v_alignbyte)
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t *p) {
+// 16 bytes from an arbitrary LDS address: five aligned dword reads + v_alignbyte.
+__device__ __forceinline__ uint4 lds_load16(const uint8_t *p) {
   const uintptr_t a = (uintptr_t)p;
   const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
-  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
 }
 
-// bytes i (0..3) of a dword whose byte i sits at record offset x0 + i, with x0 + i < n
+// bytes i (0..3) of a dword whose byte i sits at offset x0 + i, with x0 + i < n
 __device__ __forceinline__ uint32_t lt_mask(int32_t x0, int32_t n) {
   int32_t k = n - x0;
   k = k < 0 ? 0 : (k > 4 ? 4 : k);
@@ -578,46 +580,53 @@ __device__ __forceinline__ uint32_t comp4(uint32_t x) {
   return x ^ (at & 0x15151515u) ^ (cg & 0x04040404u);
 }
 
+__device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
 __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(HapView h, int64_t m, const int64_t *pos0,
                                                             const int64_t *pos1, const int8_t *fo0, int64_t rlen,
                                                             QFixed q, const Rec *recs, const E3 *off,
                                                             const uint8_t *slots, char *out1, char *out2,
                                                             int write2, int32_t win_stride, int32_t head,
-                                                            int32_t qstride) {
+                                                            int32_t qstride, int32_t nchunk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   DMeta *meta = (DMeta *)smem;
-  uint8_t *wins = (uint8_t *)smem + ((sizeof(DMeta) * ED_T + 15) / 16) * 16;
-  uint8_t *qbuf = wins + (size_t)ED_T * 2 * win_stride;
+  uint8_t *wins = (uint8_t *)smem + ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16;
+  uint8_t *qbuf = wins + (size_t)ED_T * 2 * win_stride + ED_PAD;
+  uint8_t *tstr = qbuf + (size_t)ED_T * qstride + ED_PAD;
+  const int32_t Q = (int32_t)rlen;   // perfect reads: rlen '~' (readgenerate.py:229)
+  const int32_t TL = Q + 4;          // T = '\n+\n' + Q '~' + '\n'
 
   const int64_t t0 = (int64_t)blockIdx.x * ED_T;
   const int64_t t1 = t0 + ED_T < m ? t0 + ED_T : m;
   const int nt = (int)(t1 - t0);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   const int Lp = q.prefix_len, Lm = q.mid_len;
-  const E3 base = off[t0];
+  const int nfile = write2 ? 2 : 1;
+  const E3 base = off[t0], endo = off[t1];
+  const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
 
-  // ---- P0: per-template metadata and the qname head -----------------------------------------------------------
+  // ---- P0: per-template metadata, the qname heads, T -------------------------------------------------------
+  for (int i = tid; i < TL; i += ED_THREADS) tstr[i] = (uint8_t)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
   if (tid < nt) {
     const int64_t t = t0 + tid;
     const Rec rc = recs[t];
     DMeta mt;
     mt.len[0] = mt.len[1] = 0;
-    mt.rc = 0;
+    mt.rel[0] = mt.rel[1] = 0;
     if (rc.keep) {
       const E3 o = off[t];
       mt.rel[0] = (int32_t)(o.b1 - base.b1);
       mt.rel[1] = (int32_t)(o.b2 - base.b2);
-      uint64_t x = (uint64_t)(o.kept + 1);   // cnt: 1-based among kept templates (readgenerate.py:209-210)
+      uint32_t x = (uint32_t)(o.kept + 1);   // cnt: 1-based among kept templates (readgenerate.py:209-210)
       const int nd = ndig_u(x);
-      uint32_t x32 = (uint32_t)x;            // the host caps templates per launch below 2^32
       const int lh = Lp + nd + Lm;
-      mt.qoff = tid * qstride + head - lh;
-      mt.ql = lh + rc.rest;
+      mt.qb = tid * qstride + head - lh;
+      mt.sb = lh + rc.rest + 1;
       mt.len[0] = rc.len1 + nd;              // Rec lengths exclude the cnt digits
       mt.len[1] = rc.len2 + nd;
-      uint8_t *d = qbuf + mt.qoff;
+      uint8_t *d = qbuf + mt.qb;
       for (int i = 0; i < Lp; i++) d[i] = (uint8_t)q.prefix[i];
-      for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (uint8_t)('0' + x32 % 10u); x32 /= 10u; }
+      for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (uint8_t)('0' + x % 10u); x /= 10u; }
       for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (uint8_t)q.mid[i];
       const int f0 = fo0[t];
       const int64_t p[2] = {pos0[t], pos1[t]};
@@ -626,94 +635,109 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(HapView h, int64_t m
         int64_t a = p[s] - h.p_min, e = p[s] + rlen - h.p_min;
         if (e > h.hap_len) e = h.hap_len;
         if (a > h.hap_len) a = h.hap_len;
-        mt.S[f] = (int32_t)(e > a ? e - a : 0);
-        mt.win[f] = (tid * 2 + s) * win_stride + (int)(a & 15);
-        mt.rc |= s << f;
+        const int32_t S = (int32_t)(e > a ? e - a : 0);
+        mt.S[f] = S;
+        const int32_t slot = (tid * 2 + s) * win_stride;
+        mt.bb[f] = s ? slot + win_stride - (int32_t)(a & 15) - S : slot + (int32_t)(a & 15);
       }
     }
     meta[tid] = mt;
   }
-  // ---- P1: haplotype windows and qname slots into LDS (all loads of the tile in flight) -----------------------
+  // ---- P1: windows (mate 1 reverse-complemented and mirrored) and qname slots --------------------------------
   const int chunks = win_stride / 16;
-  for (int it = tid; it < nt * 2 * chunks; it += ED_THREADS) {
-    const int j = it / (2 * chunks), rem = it - j * 2 * chunks, s = rem / chunks, c = rem - s * chunks;
+  for (int it = tid; it < 2 * nt * chunks; it += ED_THREADS) {
+    const int s = it >= nt * chunks;           // mate 0 items first: the mate 1 work is wave-uniform
+    const int r = it - s * nt * chunks, j = r / chunks, c = r - j * chunks;
     const int64_t t = t0 + j;
     int64_t a = (s ? pos1[t] : pos0[t]) - h.p_min;
     if (a > h.hap_len) a = h.hap_len;
     const int64_t a16 = a & ~(int64_t)15;
-    if (a16 + 16 * c < a + rlen && recs[t].keep)
-      *(uint4 *)(wins + (size_t)(j * 2 + s) * win_stride + 16 * c) = *(const uint4 *)(h.hap + a16 + 16 * c);
+    if (a16 + 16 * c >= a + rlen || !recs[t].keep) continue;
+    const uint4 v = *(const uint4 *)(h.hap + a16 + 16 * c);
+    uint8_t *slot = wins + (size_t)(j * 2 + s) * win_stride;
+    if (s) {
+      *(uint4 *)(slot + win_stride - 16 - 16 * c) = make_uint4(comp4(__builtin_bswap32(v.w)),
+                                                                comp4(__builtin_bswap32(v.z)),
+                                                                comp4(__builtin_bswap32(v.y)),
+                                                                comp4(__builtin_bswap32(v.x)));
+    } else {
+      *(uint4 *)(slot + 16 * c) = v;
+    }
   }
   for (int it = tid; it < nt * (SLOT / 16); it += ED_THREADS) {
     const int j = it / (SLOT / 16), c = it - j * (SLOT / 16);
     const Rec &rc = recs[t0 + j];
-    if (!rc.keep || 16 * c >= rc.rest) continue;
+    if (!rc.keep || 16 * c > rc.rest) continue;   // the slot holds rest bytes + '\n'
     *(uint4 *)(qbuf + (size_t)j * qstride + head + 16 * c) = *(const uint4 *)(slots + (t0 + j) * SLOT + 16 * c);
   }
   __syncthreads();
 
-  // ---- P2: records straight to the arenas ----------------------------------------------------------------------
-  const int nfile = write2 ? 2 : 1;
-  const int32_t Q = (int32_t)rlen;   // perfect reads: rlen '~' (readgenerate.py:229)
-  for (int pr = wave; pr < nt * nfile; pr += ED_WAVES) {
+  // ---- P2a: pure chunks ------------------------------------------------------------------------------------------
+  for (int it = tid; it < nt * nfile * nchunk; it += ED_THREADS) {
+    const int pr = it / nchunk, c = it - pr * nchunk;
     const int j = pr / nfile, f = pr - j * nfile;
     const DMeta &mt = meta[j];
     const int32_t L = mt.len[f];
     if (L == 0) continue;
-    const int64_t G0 = f ? base.b2 : base.b1;
     char *out = f ? out2 : out1;
-    const uintptr_t ga = (uintptr_t)(out + G0 + mt.rel[f]);   // global address of the record's first byte
-    const int32_t ql = mt.ql, S = mt.S[f];
-    const int32_t sb = ql + 1;            // first base
-    const int32_t tl = sb + S;            // '\n' '+' '\n' then Q '~' then '\n'
-    const int32_t qa = tl + 3, qe = qa + Q;
-    const uint8_t *qn = qbuf + mt.qoff;
-    const uint8_t *w = wins + mt.win[f];
-    const bool rcf = (mt.rc >> f) & 1;
-    // dword range of the record, and the constant '~' dwords inside it
-    const uintptr_t d0 = ga >> 2, d1 = (ga + L + 3) >> 2;
-    uintptr_t c0 = (ga + qa + 3) >> 2, c1 = (ga + qe) >> 2;
-    if (c1 < c0) c1 = c0;
-    const int32_t n1 = (int32_t)(c0 - d0), nA = n1 + (int32_t)(d1 - c1);
-    // sweep A: everything except the '~' dwords
-    for (int32_t k = lane; k < nA; k += 64) {
-      const uintptr_t d = k < n1 ? d0 + k : c1 + (k - n1);
-      const int32_t x0 = (int32_t)((intptr_t)(d << 2) - (intptr_t)ga);   // record offset of the dword's byte 0
-      // qname bytes
-      const int32_t xq = x0 < ql ? x0 : ql;
-      const uint32_t vq = lds_u32(qn + xq);
-      // bases
-      int32_t y = x0 - sb;
-      y = y < -3 ? -3 : (y > S ? S : y);
-      uint32_t vs;
-      if (rcf) {
-        const uint32_t u = lds_u32(w + (S - 4 - y));
-        vs = comp4(__builtin_bswap32(u));
-      } else {
-        vs = lds_u32(w + y);
-      }
-      // constants: '\n' after the qname, '\n+\n', '~', final '\n'
-      uint32_t vc = 0;
+    const uintptr_t ga = (uintptr_t)(out + (f ? base.b2 : base.b1) + mt.rel[f]);
+    const uintptr_t cs = ga >> 4;
+    const uintptr_t cg = cs + c;                              // this item's chunk
+    const int32_t x0 = (int32_t)((intptr_t)(cg << 4) - (intptr_t)ga);
+    const int32_t sb = mt.sb, tl = sb + mt.S[f];
+    if (x0 < 0 || x0 + 16 > L) continue;                      // seam or beyond the record
+    if ((x0 < sb && x0 + 16 > sb) || (x0 < tl && x0 + 16 > tl)) continue;   // straddles Q|B or B|T
+    const uint8_t *src = x0 + 16 <= sb ? qbuf + mt.qb + x0 : (x0 + 16 <= tl ? wins + mt.bb[f] + (x0 - sb)
+                                                                             : tstr + (x0 - tl));
+    *(uint4 *)(cg << 4) = lds_load16(src);
+  }
+  // ---- P2b: seams -------------------------------------------------------------------------------------------------
+  for (int it = tid; it < nt * nfile * 4; it += ED_THREADS) {
+    const int pr = it >> 2, b = it & 3;
+    const int j = pr / nfile, f = pr - j * nfile;
+    const DMeta &mt = meta[j];
+    const int32_t L = mt.len[f];
+    if (L == 0) continue;
+    char *out = f ? out2 : out1;
+    const uintptr_t ga = (uintptr_t)(out + (f ? base.b2 : base.b1) + mt.rel[f]);
+    const int32_t sb = mt.sb, tl = sb + mt.S[f];
+    const bool tile_end = mt.rel[f] + L == span[f];
+    // seams (record-relative): 0 = record start (previous record's T end | Q), sb = Q|B, tl = B|T, L = the tile's
+    // ragged end (a record end inside the tile is the next record's start seam)
+    const int32_t sp[4] = {0, sb, tl, L};
+    if (b == 3 && !tile_end) continue;
+    if (((ga + sp[b]) & 15) == 0) continue;                   // aligned: both sides are pure chunks
+    const uintptr_t cg = (ga + sp[b]) >> 4;
+    bool dup = false;                                         // a chunk holding several seams: the first one writes
+    for (int e = 0; e < b; e++) dup |= ((ga + sp[e]) & 15) != 0 && ((ga + sp[e]) >> 4) == cg;
+    if (dup) continue;
+    const int32_t x0 = (int32_t)((intptr_t)(cg << 4) - (intptr_t)ga);
+    // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
+    const uint4 vp = lds_load16(tstr + TL + (x0 < 0 ? x0 : -16));
+    const uint4 vq = lds_load16(qbuf + mt.qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0)));
+    int32_t yb = x0 - sb;
+    yb = yb < -16 ? -16 : (yb > mt.S[f] ? mt.S[f] : yb);
+    const uint4 vb = lds_load16(wins + mt.bb[f] + yb);
+    int32_t yt = x0 - tl;
+    yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
+    const uint4 vt = lds_load16(tstr + yt);
+    uint32_t w[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int32_t x = x0 + i;
-        const uint32_t c = (x == ql || x == tl || x == tl + 2 || x == qe) ? 0x0au : (x == tl + 1 ? 0x2bu : 0x7eu);
-        vc |= c << (8 * i);
-      }
-      const uint32_t mq = lt_mask(x0, ql);
-      const uint32_t ms = lt_mask(x0, tl) & ~lt_mask(x0, sb);
-      const uint32_t v = (vq & mq) | (vs & ms) | (vc & ~(mq | ms));
-      char *g = (char *)(d << 2);
-      if (x0 >= 0 && x0 + 4 <= L) {
-        *(uint32_t *)g = v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (x0 + i >= 0 && x0 + i < L) g[i] = (char)(v >> (8 * i));
-      }
+    for (int k = 0; k < 4; k++) {
+      const int32_t x = x0 + 4 * k;
+      const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
+      uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
+      v = (u4get(vq, k) & mq) | (v & ~mq);
+      w[k] = (u4get(vp, k) & mp) | (v & ~mp);
     }
-    // sweep B: the '~' dwords
-    for (uintptr_t d = c0 + lane; d < c1; d += 64) *(uint32_t *)(d << 2) = 0x7e7e7e7eu;
+    char *g = (char *)(cg << 4);
+    const int32_t lo = (mt.rel[f] == 0 && x0 < 0) ? -x0 : 0;   // tile start: the previous tile owns the rest
+    const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
+    if (lo == 0 && hi == 16) {
+      *(uint4 *)g = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+    }
   }
 }
 
@@ -874,17 +898,18 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   stage_begin(ctx, "emit_write");
-  const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 24) + 15) / 16 * 16);
-  const int32_t qstride = head + SLOT + 16;
-  const size_t lds_d = ((sizeof(DMeta) * ED_T + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride +
-                       (size_t)ED_T * qstride;
+  const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
+  const int32_t qstride = head + SLOT + 32;
+  const int32_t nchunk = (hmax + 15) / 16 + 1;
+  const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
+                       (size_t)ED_T * qstride + ED_PAD + (size_t)(rlen + 4) + 2 * ED_PAD;
   if (direct && !hover && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
     // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots)
     const int64_t nblk_d = (m + ED_T - 1) / ED_T;
     hipLaunchKernelGGL(k_emit_direct, dim3((unsigned)nblk_d), dim3(ED_THREADS), lds_d, st, hv, m,
                        pos0, pos1, fo0, rlen, q,
                        (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p, o1, o2, write_fastq2,
-                       win_stride, head, qstride);
+                       win_stride, head, qstride, nchunk);
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot
     const int64_t nblk = (m + EW_T - 1) / EW_T;
