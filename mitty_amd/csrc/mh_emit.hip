@@ -24,6 +24,9 @@
 //                         the workgroup's output range; neighbouring workgroups own disjoint byte ranges).
 // The sequence of a read is hap[p - p_min, min(p + l, hap_end) - p_min): non-'D' nodes tile sample coordinates
 // contiguously, so the reference's per-node slice concatenation (rpc.py:146) is one contiguous range.
+#include <cstdlib>
+#include <cstring>
+
 #include "mh_corrupt.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
@@ -37,6 +40,7 @@ struct HapView {
   const uint8_t *op;
   int64_t n_nodes;
   const uint8_t *hap;
+  const uint8_t *rc;    // reverse complement of hap (str.maketrans('ATCGN', 'TAGCN') + [::-1]), same length
   int64_t p_min, hap_len;
   const int64_t *nrs, *nre;
   int64_t n_runs;
@@ -538,7 +542,8 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 //         first and last chunks are byte stores of the tile's own bytes (the neighbouring tiles own the rest).
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
-constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
+constexpr int ED_PAD = 32;
+constexpr int ED_WMAX = 5;   // window chunks per thread (4 threads per mate): win_stride <= 320, rlen <= 289   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
 
 struct DMeta {
   int32_t rel[2];    // record start relative to the tile's first byte, per file
@@ -549,11 +554,11 @@ struct DMeta {
   int32_t S[2];      // bases per file
 };
 
-// 16 bytes from an arbitrary LDS address: five aligned dword reads + v_alignbyte.
-__device__ __forceinline__ uint4 lds_load16(const uint8_t *p) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t *q = (const uint32_t *)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
+// 16 bytes at an arbitrary byte offset of the dynamic LDS block: five aligned dword reads + v_alignbyte.  (Offsets,
+// not pointers: an integer round trip of an LDS pointer turns its reads into flat loads.)
+__device__ __forceinline__ uint4 lds_load16(const char *lds, uint32_t off) {
+  const uint32_t *q = (const uint32_t *)(lds + (off & ~3u));
+  const uint32_t sh = off & 3u;
   const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
@@ -582,161 +587,220 @@ __device__ __forceinline__ uint32_t comp4(uint32_t x) {
 
 __device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-__global__ void __launch_bounds__(ED_THREADS) k_emit_direct(HapView h, int64_t m, const int64_t *pos0,
-                                                            const int64_t *pos1, const int8_t *fo0, int64_t rlen,
-                                                            QFixed q, const Rec *recs, const E3 *off,
-                                                            const uint8_t *slots, char *out1, char *out2,
-                                                            int write2, int32_t win_stride, int32_t head,
-                                                            int32_t qstride, int32_t nchunk) {
+// qname head constants by value (kernel arguments: uniform indexing reads them through the scalar cache)
+struct QHead {
+  uint32_t w[24];    // prefix ('@stub:') then mid ('|chrom|cpy'), packed little-endian
+  int32_t lp, lm;
+  __device__ __forceinline__ uint8_t at(int i) const { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
+};
+
+// Per-tile registers: round 1 (records, positions; the owner lanes' metadata) and round 2 (the gathers).
+struct EdOwner {     // owner lanes (one per template)
+  int32_t keep, len1, len2, rest;
+  int64_t kept, b1, b2;
+  int64_t p0, p1;
+  int32_t fo, pad;
+};
+
+struct EdArgs {
+  HapView h;
+  int64_t m;
+  const int64_t *pos0, *pos1;
+  const int8_t *fo0;
+  const Rec *recs;
+  const E3 *off;
+  const uint8_t *slots;
+  char *arena[2];
+  int64_t used[2];
+  int32_t rlen, win_stride, head, qstride;
+  int32_t dbg;
+};
+
+template <int NF>
+__global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
+  // pad | T | pad | seam chunks [NF][ED_T][4] x 16 B | dump (16 B)
   DMeta *meta = (DMeta *)smem;
-  uint8_t *wins = (uint8_t *)smem + ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16;
-  uint8_t *qbuf = wins + (size_t)ED_T * 2 * win_stride + ED_PAD;
-  uint8_t *tstr = qbuf + (size_t)ED_T * qstride + ED_PAD;
-  const int32_t Q = (int32_t)rlen;   // perfect reads: rlen '~' (readgenerate.py:229)
-  const int32_t TL = Q + 4;          // T = '\n+\n' + Q '~' + '\n'
+  const HapView &h = A.h;
+  const int32_t win_stride = A.win_stride, qstride = A.qstride, head = A.head;
+  const int32_t o_win = (int32_t)(((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16);
+  const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
+  const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
+  const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
+  const int32_t o_dump = o_s + NF * ED_T * 4 * 16;            // 16-byte sink for unused gathers
+  const int32_t TL = A.rlen + 4;     // T = '\n+\n' + rlen '~' + '\n' (perfect reads, readgenerate.py:229)
+  const int tid = threadIdx.x;
+  const int Lp = qh.lp, Lm = qh.lm;
 
   const int64_t t0 = (int64_t)blockIdx.x * ED_T;
-  const int64_t t1 = t0 + ED_T < m ? t0 + ED_T : m;
-  const int nt = (int)(t1 - t0);
-  const int tid = threadIdx.x;
-  const int Lp = q.prefix_len, Lm = q.mid_len;
-  const int nfile = write2 ? 2 : 1;
-  const E3 base = off[t0], endo = off[t1];
-  const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
+  const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
 
-  // ---- P0: per-template metadata, the qname heads, T -------------------------------------------------------
-  for (int i = tid; i < TL; i += ED_THREADS) tstr[i] = (uint8_t)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
+  // ---- round 1: records and positions (thread -> template jw = tid / 8, mate sw = (tid / 4) & 1), and the owner
+  // lanes' metadata (wave 0, lane j < nt owns template j) ------------------------------------------------------
+  const int jw = tid >> 3, sw = (tid >> 2) & 1, qw = tid & 3, qs = tid & 7;
+  EdOwner ow{};
+  if (tid < 64) {   // wave-uniform
+    const int64_t tm = t0 + (tid < nt ? tid : 0);
+    const int4 rc = *(const int4 *)(A.recs + tm);
+    const E3 o = A.off[tm];
+    ow = EdOwner{rc.x, rc.y, rc.z, rc.w, o.kept, o.b1, o.b2, A.pos0[tm], A.pos1[tm], A.fo0[tm], 0};
+  }
+  const int64_t tw = t0 + (jw < nt ? jw : 0);
+  const int4 rc4 = *(const int4 *)(A.recs + tw);              // keep, len1, len2, rest
+  const int64_t pw = sw ? A.pos1[tw] : A.pos0[tw];
+  const E3 base = A.off[t0], endo = A.off[t0 + nt];
+  const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
+  // arena offsets of the tile's first byte per file; the arenas are 256-byte aligned, so offset & 15 is the
+  // address alignment
+  const int64_t gbase[2] = {A.used[0] + base.b1, A.used[1] + base.b2};
+
+  // ---- owner lanes: metadata and the qname head ('@stub:' cnt '|chrom|cpy', right-aligned before the slot
+  // area of the template's qname buffer); T ------------------------------------------------------------------------
+  for (int i = tid; i < TL; i += ED_THREADS)
+    smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
   if (tid < nt) {
-    const int64_t t = t0 + tid;
-    const Rec rc = recs[t];
     DMeta mt;
     mt.len[0] = mt.len[1] = 0;
     mt.rel[0] = mt.rel[1] = 0;
-    if (rc.keep) {
-      const E3 o = off[t];
-      mt.rel[0] = (int32_t)(o.b1 - base.b1);
-      mt.rel[1] = (int32_t)(o.b2 - base.b2);
-      uint32_t x = (uint32_t)(o.kept + 1);   // cnt: 1-based among kept templates (readgenerate.py:209-210)
+    if (ow.keep) {
+      const int64_t p[2] = {ow.p0, ow.p1};
+      mt.rel[0] = (int32_t)(ow.b1 - base.b1);
+      mt.rel[1] = (int32_t)(ow.b2 - base.b2);
+      uint32_t x = (uint32_t)(ow.kept + 1);      // cnt: 1-based among kept templates (readgenerate.py:209-210)
       const int nd = ndig_u(x);
       const int lh = Lp + nd + Lm;
-      mt.qb = tid * qstride + head - lh;
-      mt.sb = lh + rc.rest + 1;
-      mt.len[0] = rc.len1 + nd;              // Rec lengths exclude the cnt digits
-      mt.len[1] = rc.len2 + nd;
-      uint8_t *d = qbuf + mt.qb;
-      for (int i = 0; i < Lp; i++) d[i] = (uint8_t)q.prefix[i];
-      for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (uint8_t)('0' + x % 10u); x /= 10u; }
-      for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (uint8_t)q.mid[i];
-      const int f0 = fo0[t];
-      const int64_t p[2] = {pos0[t], pos1[t]};
+      mt.qb = o_q + tid * qstride + head - lh;
+      mt.sb = lh + ow.rest + 1;
+      mt.len[0] = ow.len1 + nd;                  // Rec lengths exclude the cnt digits
+      mt.len[1] = ow.len2 + nd;
+      char *d = smem + mt.qb;
+      if (!(A.dbg & 8)) {
+        for (int i = 0; i < Lp; i++) d[i] = (char)qh.at(i);
+        for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
+        for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
+      }
       for (int f = 0; f < 2; f++) {
-        const int s = f == f0 ? 0 : 1;       // file f holds mate s (reads[fo] = mate, readgenerate.py:207)
-        int64_t a = p[s] - h.p_min, e = p[s] + rlen - h.p_min;
+        const int s = f == ow.fo ? 0 : 1;        // file f holds mate s (reads[fo] = mate, readgenerate.py:207)
+        int64_t a = p[s] - h.p_min, e = p[s] + A.rlen - h.p_min;
         if (e > h.hap_len) e = h.hap_len;
         if (a > h.hap_len) a = h.hap_len;
         const int32_t S = (int32_t)(e > a ? e - a : 0);
         mt.S[f] = S;
-        const int32_t slot = (tid * 2 + s) * win_stride;
-        mt.bb[f] = s ? slot + win_stride - (int32_t)(a & 15) - S : slot + (int32_t)(a & 15);
+        // mate 0 reads hap[a, a + S); mate 1 its reverse complement = rc[hap_len - a - S, hap_len - a)
+        const int64_t a2 = s ? h.hap_len - a - S : a;
+        mt.bb[f] = o_win + (tid * 2 + s) * win_stride + (int32_t)(a2 & 15);
       }
     }
     meta[tid] = mt;
   }
-  // ---- P1: windows (mate 1 reverse-complemented and mirrored) and qname slots --------------------------------
+
+  // ---- round 2: the gathers, all in flight together (unconditional: an unused chunk re-reads the first one) -----
   const int chunks = win_stride / 16;
-  for (int it = tid; it < 2 * nt * chunks; it += ED_THREADS) {
-    const int s = it >= nt * chunks;           // mate 0 items first: the mate 1 work is wave-uniform
-    const int r = it - s * nt * chunks, j = r / chunks, c = r - j * chunks;
-    const int64_t t = t0 + j;
-    int64_t a = (s ? pos1[t] : pos0[t]) - h.p_min;
-    if (a > h.hap_len) a = h.hap_len;
-    const int64_t a16 = a & ~(int64_t)15;
-    if (a16 + 16 * c >= a + rlen || !recs[t].keep) continue;
-    const uint4 v = *(const uint4 *)(h.hap + a16 + 16 * c);
-    uint8_t *slot = wins + (size_t)(j * 2 + s) * win_stride;
-    if (s) {
-      *(uint4 *)(slot + win_stride - 16 - 16 * c) = make_uint4(comp4(__builtin_bswap32(v.w)),
-                                                                comp4(__builtin_bswap32(v.z)),
-                                                                comp4(__builtin_bswap32(v.y)),
-                                                                comp4(__builtin_bswap32(v.x)));
-    } else {
-      *(uint4 *)(slot + 16 * c) = v;
-    }
+  const bool kept = jw < nt && rc4.x;
+  int64_t aw = pw - h.p_min, ew = pw + A.rlen - h.p_min;
+  if (ew > h.hap_len) ew = h.hap_len;
+  if (aw > h.hap_len) aw = h.hap_len;
+  const int64_t sw_len = ew > aw ? ew - aw : 0;
+  const int64_t a2w = sw ? h.hap_len - aw - sw_len : aw;     // mate 1: the reverse-complement haplotype
+  const int64_t a16 = a2w & ~(int64_t)15;
+  const uint8_t *hsrc = (A.dbg & 1) ? A.slots : (sw ? h.rc : h.hap) + a16;   // dbg 1: no haplotype gathers
+  uint4 wv[ED_WMAX], sv[2];
+  uint32_t use = 0;
+#pragma unroll
+  for (int k = 0; k < ED_WMAX; k++) {
+    const int c = qw + 4 * k;
+    const bool u = kept && c < chunks && a16 + 16 * c < a2w + sw_len;
+    use |= (uint32_t)u << k;
+    wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
   }
-  for (int it = tid; it < nt * (SLOT / 16); it += ED_THREADS) {
-    const int j = it / (SLOT / 16), c = it - j * (SLOT / 16);
-    const Rec &rc = recs[t0 + j];
-    if (!rc.keep || 16 * c > rc.rest) continue;   // the slot holds rest bytes + '\n'
-    *(uint4 *)(qbuf + (size_t)j * qstride + head + 16 * c) = *(const uint4 *)(slots + (t0 + j) * SLOT + 16 * c);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int c = qs + 8 * k;
+    const bool u = kept && 16 * c <= rc4.w;   // the slot holds rest bytes + '\n'
+    use |= (uint32_t)u << (ED_WMAX + k);
+    sv[k] = *(const uint4 *)(A.slots + tw * SLOT + (u ? 16 * c : 0));
+  }
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int c = qs + 8 * k;
+    *(uint4 *)(smem + (((use >> (ED_WMAX + k)) & 1) ? o_q + jw * qstride + head + 16 * c : o_dump)) = sv[k];
+  }
+  {
+    const int32_t slot = o_win + (jw * 2 + sw) * win_stride;
+#pragma unroll
+    for (int k = 0; k < ED_WMAX; k++)
+      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (qw + 4 * k) : o_dump)) = wv[k];
   }
   __syncthreads();
+  if (A.dbg & 2) return;
 
-  // ---- P2a: pure chunks ------------------------------------------------------------------------------------------
-  for (int it = tid; it < nt * nfile * nchunk; it += ED_THREADS) {
-    const int pr = it / nchunk, c = it - pr * nchunk;
-    const int j = pr / nfile, f = pr - j * nfile;
-    const DMeta &mt = meta[j];
-    const int32_t L = mt.len[f];
-    if (L == 0) continue;
-    char *out = f ? out2 : out1;
-    const uintptr_t ga = (uintptr_t)(out + (f ? base.b2 : base.b1) + mt.rel[f]);
-    const uintptr_t cs = ga >> 4;
-    const uintptr_t cg = cs + c;                              // this item's chunk
-    const int32_t x0 = (int32_t)((intptr_t)(cg << 4) - (intptr_t)ga);
-    const int32_t sb = mt.sb, tl = sb + mt.S[f];
-    if (x0 < 0 || x0 + 16 > L) continue;                      // seam or beyond the record
-    if ((x0 < sb && x0 + 16 > sb) || (x0 < tl && x0 + 16 > tl)) continue;   // straddles Q|B or B|T
-    const uint8_t *src = x0 + 16 <= sb ? qbuf + mt.qb + x0 : (x0 + 16 <= tl ? wins + mt.bb[f] + (x0 - sb)
-                                                                             : tstr + (x0 - tl));
-    *(uint4 *)(cg << 4) = lds_load16(src);
-  }
-  // ---- P2b: seams -------------------------------------------------------------------------------------------------
-  for (int it = tid; it < nt * nfile * 4; it += ED_THREADS) {
-    const int pr = it >> 2, b = it & 3;
-    const int j = pr / nfile, f = pr - j * nfile;
-    const DMeta &mt = meta[j];
-    const int32_t L = mt.len[f];
-    if (L == 0) continue;
-    char *out = f ? out2 : out1;
-    const uintptr_t ga = (uintptr_t)(out + (f ? base.b2 : base.b1) + mt.rel[f]);
-    const int32_t sb = mt.sb, tl = sb + mt.S[f];
-    const bool tile_end = mt.rel[f] + L == span[f];
-    // seams (record-relative): 0 = record start (previous record's T end | Q), sb = Q|B, tl = B|T, L = the tile's
-    // ragged end (a record end inside the tile is the next record's start seam)
-    const int32_t sp[4] = {0, sb, tl, L};
-    if (b == 3 && !tile_end) continue;
-    if (((ga + sp[b]) & 15) == 0) continue;                   // aligned: both sides are pure chunks
-    const uintptr_t cg = (ga + sp[b]) >> 4;
-    bool dup = false;                                         // a chunk holding several seams: the first one writes
-    for (int e = 0; e < b; e++) dup |= ((ga + sp[e]) & 15) != 0 && ((ga + sp[e]) >> 4) == cg;
-    if (dup) continue;
-    const int32_t x0 = (int32_t)((intptr_t)(cg << 4) - (intptr_t)ga);
-    // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
-    const uint4 vp = lds_load16(tstr + TL + (x0 < 0 ? x0 : -16));
-    const uint4 vq = lds_load16(qbuf + mt.qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0)));
-    int32_t yb = x0 - sb;
-    yb = yb < -16 ? -16 : (yb > mt.S[f] ? mt.S[f] : yb);
-    const uint4 vb = lds_load16(wins + mt.bb[f] + yb);
-    int32_t yt = x0 - tl;
-    yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
-    const uint4 vt = lds_load16(tstr + yt);
-    uint32_t w[4];
+  // ---- output: LPR lanes per record (record r = file f, template j) -------------------------------------------
+  constexpr int LPR = NF == 2 ? 4 : 8;
+  const int r = tid / LPR, q = tid % LPR;
+  const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
+  const bool live = j < nt;
+  const DMeta &M = meta[live ? j : 0];                        // LDS reads of the file's fields (no local copy)
+  const int32_t L = live ? M.len[f] : 0;
+  const int32_t rel = M.rel[f];
+  const int64_t ga = gbase[f] + rel;                          // arena offset of the record's first byte
+  const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f];
+  char *const arena = A.arena[f];
+  // seams (record-relative): 0 = record start (previous record's T end | Q), sb = Q|B, tl = B|T, L = the tile's
+  // ragged end (a record end inside the tile is the next record's start seam); a chunk holding several seams
+  // belongs to the first of them.  Lane q < 4 computes seam q into LDS (the tile's ragged edges straight out).
+  if (L > 0 && q < 4) {
+    const int b = q;
+    const bool tile_end = rel + L == span[f];
+    const int32_t spb = b == 0 ? 0 : b == 1 ? sb : b == 2 ? tl : L;
+    const int64_t cg = (ga + spb) >> 4;
+    bool skip = (b == 3 && !tile_end) || ((ga + spb) & 15) == 0;   // aligned: both sides are pure chunks
+    skip |= b > 0 && (ga & 15) != 0 && (ga >> 4) == cg;
+    skip |= b > 1 && ((ga + sb) & 15) != 0 && ((ga + sb) >> 4) == cg;
+    skip |= b > 2 && ((ga + tl) & 15) != 0 && ((ga + tl) >> 4) == cg;
+    if (!skip) {
+      const int32_t x0 = (int32_t)((cg << 4) - ga);
+      // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
+      const uint4 vp = lds_load16(smem, (uint32_t)(o_t + TL + (x0 < 0 ? x0 : -16)));
+      const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
+      int32_t yb = x0 - sb;
+      yb = yb < -16 ? -16 : (yb > S ? S : yb);
+      const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
+      int32_t yt = x0 - tl;
+      yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
+      const uint4 vt = lds_load16(smem, (uint32_t)(o_t + yt));
+      uint32_t w[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int32_t x = x0 + 4 * k;
-      const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
-      uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
-      v = (u4get(vq, k) & mq) | (v & ~mq);
-      w[k] = (u4get(vp, k) & mp) | (v & ~mp);
+      for (int k = 0; k < 4; k++) {
+        const int32_t x = x0 + 4 * k;
+        const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
+        uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
+        v = (u4get(vq, k) & mq) | (v & ~mq);
+        w[k] = (u4get(vp, k) & mp) | (v & ~mp);
+      }
+      const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;   // tile start: the previous tile owns the rest
+      const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
+      if (lo == 0 && hi == 16) {
+        *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        char *g = arena + (cg << 4);
+        for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+      }
     }
-    char *g = (char *)(cg << 4);
-    const int32_t lo = (mt.rel[f] == 0 && x0 < 0) ? -x0 : 0;   // tile start: the previous tile owns the rest
-    const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
-    if (lo == 0 && hi == 16) {
-      *(uint4 *)g = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
+  }
+  __syncthreads();
+  // every full chunk of the record: one unaligned LDS read (or a seam) and one aligned 16-byte store
+  {
+    const int64_t c0 = ga >> 4;
+    int32_t x0 = (int32_t)((c0 << 4) - ga) + 16 * q;
+    const bool first_rec = rel == 0;
+    for (int64_t cg = c0 + q; x0 + 16 <= L; cg += LPR, x0 += 16 * LPR) {
+      const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
+      if (b == 0 && first_rec) continue;                        // ragged tile start, already written
+      const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
+                                 : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : o_t + (x0 - tl)));
+      const uint4 v = (A.dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
+      *(uint4 *)(arena + (cg << 4)) = v;
     }
   }
 }
@@ -775,7 +839,8 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
-                 (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p, h.p_min,
+                 (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
+                 (const uint8_t *)h.rc.p, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 
@@ -900,16 +965,28 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   stage_begin(ctx, "emit_write");
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
   const int32_t qstride = head + SLOT + 32;
-  const int32_t nchunk = (hmax + 15) / 16 + 1;
   const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
-                       (size_t)ED_T * qstride + ED_PAD + (size_t)(rlen + 4) + 2 * ED_PAD;
-  if (direct && !hover && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
+                       (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
+                       (size_t)2 * ED_T * 4 * 16 + 16;
+  QHead qh{};
+  const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
+  if (head_fits) {
+    std::string pm = prefix + mid;
+    std::memcpy(qh.w, pm.data(), pm.size());
+    qh.lp = (int32_t)prefix.size();
+    qh.lm = (int32_t)mid.size();
+  }
+  if (direct && !hover && head_fits && win_stride <= 16 * 4 * ED_WMAX && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
     // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots)
-    const int64_t nblk_d = (m + ED_T - 1) / ED_T;
-    hipLaunchKernelGGL(k_emit_direct, dim3((unsigned)nblk_d), dim3(ED_THREADS), lds_d, st, hv, m,
-                       pos0, pos1, fo0, rlen, q,
-                       (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p, o1, o2, write_fastq2,
-                       win_stride, head, qstride, nchunk);
+    const int64_t ntiles = (m + ED_T - 1) / ED_T;
+    const char *dbg_env = getenv("MH_EMIT_DBG");   // timing experiments only: skip parts of the kernel
+    EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p,
+             {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
+             qstride, dbg_env ? atoi(dbg_env) : 0};
+    if (write_fastq2)
+      hipLaunchKernelGGL(k_emit_direct<2>, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
+    else
+      hipLaunchKernelGGL(k_emit_direct<1>, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot
     const int64_t nblk = (m + EW_T - 1) / EW_T;

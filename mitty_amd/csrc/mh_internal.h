@@ -36,7 +36,7 @@ struct DevBuf {
 // Sample coordinates are the reference's 1-based `ps`; hap[k] is the base at sample position p_min + k.
 struct Hap {
   bool valid = false;
-  DevBuf hap, keys, ps, pr, op, oplen, nrun_s, nrun_e;
+  DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
 };
 

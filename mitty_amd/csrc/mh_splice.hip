@@ -208,6 +208,25 @@ struct StoreRuns {
   }
 };
 
+// Reverse complement of the haplotype (readgenerate.py:56,205-206: str.maketrans('ATCGN', 'TAGCN') then [::-1]):
+// rc[i] = comp(hap[hap_len - 1 - i]); mate-1 reads are then forward ranges of rc.  16 output bytes per thread.
+__global__ void __launch_bounds__(256) k_hap_rc(const uint8_t *hap, int64_t hap_len, uint8_t *rc) {
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (i0 >= hap_len) return;
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int64_t i = i0 + k;
+    uint8_t c = 0;
+    if (i < hap_len) {
+      c = hap[hap_len - 1 - i];
+      c = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
+    }
+    w[k >> 2] |= (uint32_t)c << (8 * (k & 3));
+  }
+  *(uint4 *)(rc + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 }  // namespace
 
 int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int64_t *v_pos, const uint8_t *v_op,
@@ -328,6 +347,15 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
     int64_t threads = pieces * 64;
     hipLaunchKernelGGL(k_hap_copy, dim3(grid_for(threads, 256, INT32_MAX)), dim3(256), 0, st, pieces, n_nodes, poff,
                        ps, nl, nsrc, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p, p_min);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+  }
+  // --- reverse complement (mate-1 reads) --------------------------------------------------------------------
+  MH_TRY(ensure(ctx, h.rc, hap_len + 1024));
+  if (hap_len > 0) {
+    stage_begin(ctx, "splice_hap_rc");
+    hipLaunchKernelGGL(k_hap_rc, dim3(grid_for((hap_len + 15) / 16, 256, INT32_MAX)), dim3(256), 0, st,
+                       (const uint8_t *)h.hap.p, hap_len, (uint8_t *)h.rc.p);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   }
