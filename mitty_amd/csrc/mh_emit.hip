@@ -616,7 +616,7 @@ struct EdArgs {
   int32_t dbg;
 };
 
-template <int NF>
+template <int NF, int LPR>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
@@ -735,21 +735,22 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   __syncthreads();
   if (A.dbg & 2) return;
 
-  // ---- output: LPR lanes per record (record r = file f, template j) -------------------------------------------
-  constexpr int LPR = NF == 2 ? 4 : 8;
-  const int r = tid / LPR, q = tid % LPR;
-  const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
-  const bool live = j < nt;
-  const DMeta &M = meta[live ? j : 0];                        // LDS reads of the file's fields (no local copy)
-  const int32_t L = live ? M.len[f] : 0;
-  const int32_t rel = M.rel[f];
-  const int64_t ga = gbase[f] + rel;                          // arena offset of the record's first byte
-  const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f];
-  char *const arena = A.arena[f];
+  // ---- output: LPR lanes per record (record r = file f, template j); passes over the tile's NF * ED_T records ----
+  constexpr int RPP = ED_THREADS / LPR;                        // records per pass
+  const int q = tid % LPR;
   // seams (record-relative): 0 = record start (previous record's T end | Q), sb = Q|B, tl = B|T, L = the tile's
   // ragged end (a record end inside the tile is the next record's start seam); a chunk holding several seams
-  // belongs to the first of them.  Lane q < 4 computes seam q into LDS (the tile's ragged edges straight out).
-  if (L > 0 && q < 4) {
+  // belongs to the first of them.  Lane q < 4 of a record computes seam q into LDS (the tile's ragged edges go
+  // straight out as byte stores).
+  for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
+    const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
+    if (j >= nt || q >= 4) continue;
+    const DMeta &M = meta[j];
+    const int32_t L = M.len[f];
+    if (L == 0) continue;
+    const int32_t rel = M.rel[f];
+    const int64_t ga = gbase[f] + rel;                        // arena offset of the record's first byte
+    const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f];
     const int b = q;
     const bool tile_end = rel + L == span[f];
     const int32_t spb = b == 0 ? 0 : b == 1 ? sb : b == 2 ? tl : L;
@@ -758,45 +759,51 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     skip |= b > 0 && (ga & 15) != 0 && (ga >> 4) == cg;
     skip |= b > 1 && ((ga + sb) & 15) != 0 && ((ga + sb) >> 4) == cg;
     skip |= b > 2 && ((ga + tl) & 15) != 0 && ((ga + tl) >> 4) == cg;
-    if (!skip) {
-      const int32_t x0 = (int32_t)((cg << 4) - ga);
-      // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
-      const uint4 vp = lds_load16(smem, (uint32_t)(o_t + TL + (x0 < 0 ? x0 : -16)));
-      const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
-      int32_t yb = x0 - sb;
-      yb = yb < -16 ? -16 : (yb > S ? S : yb);
-      const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
-      int32_t yt = x0 - tl;
-      yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
-      const uint4 vt = lds_load16(smem, (uint32_t)(o_t + yt));
-      uint32_t w[4];
+    if (skip) continue;
+    const int32_t x0 = (int32_t)((cg << 4) - ga);
+    // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
+    const uint4 vp = lds_load16(smem, (uint32_t)(o_t + TL + (x0 < 0 ? x0 : -16)));
+    const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
+    int32_t yb = x0 - sb;
+    yb = yb < -16 ? -16 : (yb > S ? S : yb);
+    const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
+    int32_t yt = x0 - tl;
+    yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
+    const uint4 vt = lds_load16(smem, (uint32_t)(o_t + yt));
+    uint32_t w[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int32_t x = x0 + 4 * k;
-        const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
-        uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
-        v = (u4get(vq, k) & mq) | (v & ~mq);
-        w[k] = (u4get(vp, k) & mp) | (v & ~mp);
-      }
-      const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;   // tile start: the previous tile owns the rest
-      const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
-      if (lo == 0 && hi == 16) {
-        *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-      } else {
-        char *g = arena + (cg << 4);
-        for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
-      }
+    for (int k = 0; k < 4; k++) {
+      const int32_t x = x0 + 4 * k;
+      const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
+      uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
+      v = (u4get(vq, k) & mq) | (v & ~mq);
+      w[k] = (u4get(vp, k) & mp) | (v & ~mp);
+    }
+    const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;        // tile start: the previous tile owns the rest
+    const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
+    if (lo == 0 && hi == 16) {
+      *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      char *g = A.arena[f] + (cg << 4);
+      for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
   __syncthreads();
-  // every full chunk of the record: one unaligned LDS read (or a seam) and one aligned 16-byte store
-  {
+  // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
+  for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
+    const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
+    if (j >= nt) continue;
+    const DMeta &M = meta[j];
+    const int32_t L = M.len[f];
+    const int32_t rel = M.rel[f];
+    const int64_t ga = gbase[f] + rel;
+    const int32_t sb = M.sb, tl = sb + M.S[f], qb = M.qb, bb = M.bb[f];
+    char *const arena = A.arena[f];
     const int64_t c0 = ga >> 4;
     int32_t x0 = (int32_t)((c0 << 4) - ga) + 16 * q;
-    const bool first_rec = rel == 0;
     for (int64_t cg = c0 + q; x0 + 16 <= L; cg += LPR, x0 += 16 * LPR) {
       const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
-      if (b == 0 && first_rec) continue;                        // ragged tile start, already written
+      if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
                                  : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : o_t + (x0 - tl)));
       const uint4 v = (A.dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
@@ -983,10 +990,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p,
              {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
              qstride, dbg_env ? atoi(dbg_env) : 0};
-    if (write_fastq2)
-      hipLaunchKernelGGL(k_emit_direct<2>, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
-    else
-      hipLaunchKernelGGL(k_emit_direct<1>, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
+    const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
+    auto kfn = write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16> : lpr == 8 ? k_emit_direct<2, 8> : k_emit_direct<2, 4>)
+                            : (lpr == 16 ? k_emit_direct<1, 16> : k_emit_direct<1, 8>);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot
     const int64_t nblk = (m + EW_T - 1) / EW_T;
