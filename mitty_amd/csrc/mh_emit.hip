@@ -41,6 +41,8 @@ struct HapView {
   int64_t n_nodes;
   const uint8_t *hap;
   const uint8_t *rc;    // reverse complement of hap (str.maketrans('ATCGN', 'TAGCN') + [::-1]), same length
+  const int32_t *bkt;   // node-search buckets (Hap::bkt)
+  int64_t n_bkt;
   int64_t p_min, hap_len;
   const int64_t *nrs, *nre;
   int64_t n_runs;
@@ -51,6 +53,20 @@ __device__ __forceinline__ int64_t upper_bound(const int64_t *a, int64_t n, int6
   while (lo < hi) {
     int64_t mid = (lo + hi) >> 1;
     if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// searchsorted(keys, x, 'right') (rpc.py:127-130) through the bucket table: the answer lies in
+// [bkt[k], bkt[k+1]] for x's bucket k, a few keys at most.
+__device__ __forceinline__ int64_t node_upper(const HapView &h, int64_t x) {
+  int64_t k = (x - h.p_min) >> NODE_BKT_SHIFT;
+  if (k < 0) return upper_bound(h.keys, h.n_nodes, x);
+  if (k >= h.n_bkt) k = h.n_bkt - 1;
+  int64_t lo = h.bkt[k], hi = k + 1 < h.n_bkt ? h.bkt[k + 1] : h.n_nodes;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (h.keys[mid] <= x) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
@@ -126,8 +142,8 @@ __device__ __forceinline__ void read_place(const HapView &h, int64_t p, int64_t 
 
 // rpc.get_begin_end_nodes + the lengths of rpc.generate_read's outputs.  Requires p >= p_min (n0 >= 0).
 __device__ void read_info(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
-  r.n0 = upper_bound(h.keys, h.n_nodes, p) - 1;
-  r.n1 = upper_bound(h.keys, h.n_nodes, p + l - 1) - 1;
+  r.n0 = node_upper(h, p) - 1;
+  r.n1 = node_upper(h, p + l - 1) - 1;
   int32_t cl = 0, vl = 0;
   bool first = true;
   for (int64_t k = r.n0; k <= r.n1; k++) {
@@ -186,21 +202,28 @@ struct Rec {
   int32_t n0[2], n1[2];             // start / end node per mate (pass 2 skips the searches)
 };
 
-// Packs bytes into dwords and stores each completed dword (one thread writing its own slot).
+// Packs bytes into dwords and stores each completed dword while `cap` dwords remain (one thread writing its own
+// slot; p == nullptr counts only); n counts every byte.
 struct ByteWriter {
   uint32_t *p;
   uint32_t acc;
   int nb;
+  int32_t n;
+  int32_t cap;
   __device__ __forceinline__ void put(uint8_t c) {
     acc |= (uint32_t)c << (8 * nb);
+    n++;
     if (++nb == 4) {
-      *p++ = acc;
+      if (p != nullptr && cap > 0) {
+        *p++ = acc;
+        cap--;
+      }
       acc = 0;
       nb = 0;
     }
   }
   __device__ __forceinline__ void flush() {
-    if (nb) *p = acc;
+    if (nb && p != nullptr && cap > 0) *p = acc;
   }
   // decimal, most significant digit first: digits packed 4 bits each (LSB-first) then emitted from the top
   __device__ __forceinline__ void put_u(uint64_t v) {
@@ -263,55 +286,57 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   if (t < m) {
     ReadInfo r[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
-    read_info(h, p[0], rlen, r[0]);
-    read_info(h, p[1], rlen, r[1]);
-    int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
-               count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
+#pragma unroll
+    for (int s = 0; s < 2; s++) {   // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range
+      r[s].n0 = node_upper(h, p[s]) - 1;
+      r[s].n1 = node_upper(h, p[s] + rlen - 1) - 1;
+      read_place(h, p[s], rlen, r[s]);
+    }
+    const int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+                     count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
-      int32_t ql = qname_len_wo_cnt(q, r, rlen);
-      int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-      int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
-      int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
-      int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
+      // the reads part of the qname, in file order (readgenerate.py:223-225), and the qname's '\n': formatted into
+      // the slot while it fits, counted either way (its length sizes the records)
+      ByteWriter bw{slots ? (uint32_t *)(slots + t * SLOT) : nullptr, 0u, 0, 0, SLOT / 4};
+      for (int fr = 0; fr < 2; fr++) {
+        const int s = fr == f0 ? 0 : 1;
+        const ReadInfo &ri = r[s];
+        bw.put('|'); bw.put((uint8_t)('0' + s));
+        bw.put('|'); bw.put_s(ri.pos);
+        bw.put('|'); bw.put_s(rlen);
+        bw.put('|');
+        if (ri.special) {
+          bw.put('>'); bw.put_s(p[s] - h.ps[ri.n0]); bw.put(':'); bw.put_s(rlen); bw.put('I');
+        } else {
+          for (int64_t k = ri.n0; k <= ri.n1; k++) {
+            bw.put_s(node_count(h, k, p[s], rlen));
+            bw.put(h.op[k]);
+          }
+        }
+        bw.put('|');
+        bool first = true;
+        for (int64_t k = ri.n0; k <= ri.n1; k++) {
+          if (h.op[k] == '=') continue;
+          if (!first) bw.put(',');
+          bw.put_s(node_v(h, k));
+          first = false;
+        }
+      }
+      bw.put('\n');
+      bw.flush();
+      if (slots != nullptr && bw.n > SLOT) atomicOr(overflow, 1);   // the unit falls back to the LDS-image writer
+      const int32_t rest = bw.n - 1;
+      const int32_t ql = q.prefix_len + q.mid_len + rest;          // qname length without the cnt digits
+      const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
+      const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
+      const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
       out.keep = 1;
       out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
       out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
-      out.rest = ql - q.prefix_len - q.mid_len;
+      out.rest = rest;
       local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
-      if (slots != nullptr) {
-        if (out.rest + 1 > SLOT) {   // the slot holds the reads part and the qname's '\n'
-          atomicOr(overflow, 1);
-        } else {   // the reads part of the qname, in file order (readgenerate.py:223-225)
-          ByteWriter bw{(uint32_t *)(slots + t * SLOT), 0u, 0};
-          for (int fr = 0; fr < 2; fr++) {
-            const int s = fr == f0 ? 0 : 1;
-            const ReadInfo &ri = r[s];
-            bw.put('|'); bw.put((uint8_t)('0' + s));
-            bw.put('|'); bw.put_s(ri.pos);
-            bw.put('|'); bw.put_s(rlen);
-            bw.put('|');
-            if (ri.special) {
-              bw.put('>'); bw.put_s(p[s] - h.ps[ri.n0]); bw.put(':'); bw.put_s(rlen); bw.put('I');
-            } else {
-              for (int64_t k = ri.n0; k <= ri.n1; k++) {
-                bw.put_s(node_count(h, k, p[s], rlen));
-                bw.put(h.op[k]);
-              }
-            }
-            bw.put('|');
-            bool first = true;
-            for (int64_t k = ri.n0; k <= ri.n1; k++) {
-              if (h.op[k] == '=') continue;
-              if (!first) bw.put(',');
-              bw.put_s(node_v(h, k));
-              first = false;
-            }
-          }
-          bw.put('\n');
-          bw.flush();
-        }
-      }
     }
     recs[t] = out;
   }
@@ -847,7 +872,7 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
                  (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
-                 (const uint8_t *)h.rc.p, h.p_min,
+                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, h.n_bkt, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 

@@ -34,9 +34,13 @@ struct DevBuf {
 
 // Haplotype (one chromosome copy of one BED region) resident on the device.  SURVEY.md §8(a) A9.
 // Sample coordinates are the reference's 1-based `ps`; hap[k] is the base at sample position p_min + k.
+constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
+
 struct Hap {
   bool valid = false;
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
+  DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
+  int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
 };
 

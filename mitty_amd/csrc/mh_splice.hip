@@ -227,6 +227,21 @@ __global__ void __launch_bounds__(256) k_hap_rc(const uint8_t *hap, int64_t hap_
   *(uint4 *)(rc + i0) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Node-search buckets: bkt[k] = first node whose key is >= p_min + (k << NODE_BKT_SHIFT) (lower_bound), so the
+// searchsorted of rpc.get_begin_end_nodes (rpc.py:127-130) only scans the few keys of one bucket.
+__global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64_t n, int64_t p_min, int64_t n_bkt,
+                                                      int32_t *bkt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n_bkt) return;
+  const int64_t x = p_min + (k << NODE_BKT_SHIFT);
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  bkt[k] = (int32_t)lo;
+}
+
 }  // namespace
 
 int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int64_t *v_pos, const uint8_t *v_op,
@@ -349,6 +364,15 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
                        ps, nl, nsrc, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p, p_min);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
+  }
+  // --- node-search buckets ------------------------------------------------------------------------------------
+  {
+    const int64_t n_bkt = ((hap_len + 2048) >> NODE_BKT_SHIFT) + 1;   // keys reach at most p_min + hap_len + 1
+    MH_TRY(ensure(ctx, h.bkt, 4 * (n_bkt + 2)));
+    hipLaunchKernelGGL(k_node_buckets, dim3(grid_for(n_bkt + 1, 256, INT32_MAX)), dim3(256), 0, st,
+                       (const int64_t *)h.keys.p, n_nodes, p_min, n_bkt, (int32_t *)h.bkt.p);
+    HIPCHK(ctx, hipGetLastError());
+    h.n_bkt = n_bkt;
   }
   // --- reverse complement (mate-1 reads) --------------------------------------------------------------------
   MH_TRY(ensure(ctx, h.rc, hap_len + 1024));
