@@ -143,7 +143,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &kv : ctx->contigs) release(kv.second.seq);
   for (auto &kv : ctx->haps) {
     Hap &h = kv.second;
-    release(h.hap); release(h.rc); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
+    release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
     release(h.nrun_s); release(h.nrun_e);
   }
   for (auto &kv : ctx->tsets) {
@@ -271,7 +271,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  release(h.hap); release(h.rc); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
+  release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
   release(h.nrun_s); release(h.nrun_e);
   ctx->haps.erase(it);
   return MH_OK;

@@ -42,6 +42,7 @@ struct HapView {
   const uint8_t *hap;
   const uint8_t *rc;    // reverse complement of hap (str.maketrans('ATCGN', 'TAGCN') + [::-1]), same length
   const int32_t *bkt;   // node-search buckets (Hap::bkt)
+  const Node32 *nd;     // AoS node copy (Hap::nd)
   int64_t n_bkt;
   int64_t p_min, hap_len;
   const int64_t *nrs, *nre;
@@ -66,7 +67,7 @@ __device__ __forceinline__ int64_t node_upper(const HapView &h, int64_t x) {
   int64_t lo = h.bkt[k], hi = k + 1 < h.n_bkt ? h.bkt[k + 1] : h.n_nodes;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (h.keys[mid] <= x) lo = mid + 1; else hi = mid;
+    if (h.nd[mid].key <= x) lo = mid + 1; else hi = mid;
   }
   return lo;
 }
@@ -108,31 +109,33 @@ struct ReadInfo {
   bool special;
 };
 
-__device__ __forceinline__ int64_t node_count(const HapView &h, int64_t k, int64_t p, int64_t l) {
-  int64_t ps = h.ps[k], ol = h.oplen[k];
-  if (h.op[k] == 'D') return ol;
-  int64_t hi = p + l - ps < ol ? p + l - ps : ol;
-  int64_t lo = p - ps > 0 ? p - ps : 0;
+__device__ __forceinline__ int64_t node_count(const Node32 &n, int64_t p, int64_t l) {
+  if (n.op == 'D') return n.oplen;
+  int64_t hi = p + l - n.ps < n.oplen ? p + l - n.ps : n.oplen;
+  int64_t lo = p - n.ps > 0 ? p - n.ps : 0;
   return hi - lo;
 }
-__device__ __forceinline__ int64_t node_v(const HapView &h, int64_t k) {
-  uint8_t o = h.op[k];
-  return o == 'X' ? 0 : (o == 'I' ? h.oplen[k] : -h.oplen[k]);
+__device__ __forceinline__ int64_t node_count(const HapView &h, int64_t k, int64_t p, int64_t l) {
+  return node_count(h.nd[k], p, l);
 }
+__device__ __forceinline__ int64_t node_v(const Node32 &n) {
+  return n.op == 'X' ? 0 : (n.op == 'I' ? n.oplen : -n.oplen);
+}
+__device__ __forceinline__ int64_t node_v(const HapView &h, int64_t k) { return node_v(h.nd[k]); }
 
 // POS / special-CIGAR / sequence range of a read whose start and end nodes are known (rpc.py:144-160).
 __device__ __forceinline__ void read_place(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
   r.special = false;
-  const uint8_t o0 = h.op[r.n0];
-  if (o0 == 'I') {
+  const Node32 n0 = h.nd[r.n0];
+  if (n0.op == 'I') {
     if (r.n0 == r.n1) {
       r.special = true;
-      r.pos = h.pr[r.n0] - 1;
+      r.pos = n0.pr - 1;
     } else {
-      r.pos = h.pr[r.n0];
+      r.pos = n0.pr;
     }
   } else {
-    r.pos = p - h.ps[r.n0] + h.pr[r.n0];
+    r.pos = p - n0.ps + n0.pr;
   }
   int64_t a = p - h.p_min, b = p + l - h.p_min;
   if (b > h.hap_len) b = h.hap_len;
@@ -276,13 +279,66 @@ __device__ __forceinline__ int32_t qname_len_wo_cnt(const QFixed &q, const ReadI
 }
 
 constexpr int SLOT = 256;   // bytes per template for the reads part of the qname ("|s|pos|rlen|cigar|v,..|...")
+constexpr int MS_STG = 112;   // of which the first MS_STG bytes are staged in LDS by k_emit_measure
+
+// ByteWriter for k_emit_measure: dword k goes to LDS while k < MS_STG / 4, else to the global slot (k < SLOT / 4)
+struct SplitWriter {
+  uint32_t *lds;
+  uint32_t *g;
+  uint32_t acc;
+  int nb;
+  int32_t n;
+  __device__ __forceinline__ void store(uint32_t v) {
+    const int k = (n - 1) >> 2;
+    if (k < MS_STG / 4) lds[k] = v;
+    else if (g != nullptr && k < SLOT / 4) g[k] = v;
+  }
+  __device__ __forceinline__ void put(uint8_t c) {
+    acc |= (uint32_t)c << (8 * nb);
+    n++;
+    if (++nb == 4) {
+      store(acc);
+      acc = 0;
+      nb = 0;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    if (nb) store(acc);
+  }
+  __device__ __forceinline__ void put_u(uint64_t v) {
+    if (v <= 0xffffffffull) {
+      uint32_t x = (uint32_t)v;
+      uint64_t bcd = 0;
+      int nd = 0;
+      do {
+        bcd |= (uint64_t)(x % 10u) << (4 * nd);
+        x /= 10u;
+        nd++;
+      } while (x);
+      for (int i = nd - 1; i >= 0; i--) put((uint8_t)('0' + ((bcd >> (4 * i)) & 15)));
+    } else {
+      char tmp[24];
+      int nd = 0;
+      do { tmp[nd++] = (char)('0' + v % 10u); v /= 10u; } while (v);
+      for (int i = nd - 1; i >= 0; i--) put((uint8_t)tmp[i]);
+    }
+  }
+  __device__ __forceinline__ void put_s(int64_t v) {
+    if (v < 0) { put('-'); put_u((uint64_t)(-v)); } else put_u((uint64_t)v);
+  }
+};
 
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
                                                       Rec *recs, int32_t *max_rec, uint8_t *slots,
-                                                      int32_t *overflow) {
+                                                      int32_t *overflow, int32_t dbg) {
+  // the reads part is formatted into LDS (bytes past MS_STG straight to the slot) and leaves in coalesced 16-byte
+  // chunks after the barrier
+  __shared__ uint32_t stg[256][MS_STG / 4];
+  __shared__ int32_t s_n[256];
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int32_t local_max = 0;
+  int32_t nbytes = 0;
   if (t < m) {
     ReadInfo r[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
@@ -299,8 +355,8 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     if (keep) {
       // the reads part of the qname, in file order (readgenerate.py:223-225), and the qname's '\n': formatted into
       // the slot while it fits, counted either way (its length sizes the records)
-      ByteWriter bw{slots ? (uint32_t *)(slots + t * SLOT) : nullptr, 0u, 0, 0, SLOT / 4};
-      for (int fr = 0; fr < 2; fr++) {
+      SplitWriter bw{stg[threadIdx.x], slots && !(dbg & 1) ? (uint32_t *)(slots + t * SLOT) : nullptr, 0u, 0, 0};
+      for (int fr = 0; fr < 2 && !(dbg & 2); fr++) {
         const int s = fr == f0 ? 0 : 1;
         const ReadInfo &ri = r[s];
         bw.put('|'); bw.put((uint8_t)('0' + s));
@@ -308,25 +364,28 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
         bw.put('|'); bw.put_s(rlen);
         bw.put('|');
         if (ri.special) {
-          bw.put('>'); bw.put_s(p[s] - h.ps[ri.n0]); bw.put(':'); bw.put_s(rlen); bw.put('I');
+          bw.put('>'); bw.put_s(p[s] - h.nd[ri.n0].ps); bw.put(':'); bw.put_s(rlen); bw.put('I');
         } else {
           for (int64_t k = ri.n0; k <= ri.n1; k++) {
-            bw.put_s(node_count(h, k, p[s], rlen));
-            bw.put(h.op[k]);
+            const Node32 n = h.nd[k];
+            bw.put_s(node_count(n, p[s], rlen));
+            bw.put(n.op);
           }
         }
         bw.put('|');
         bool first = true;
         for (int64_t k = ri.n0; k <= ri.n1; k++) {
-          if (h.op[k] == '=') continue;
+          const Node32 n = h.nd[k];
+          if (n.op == '=') continue;
           if (!first) bw.put(',');
-          bw.put_s(node_v(h, k));
+          bw.put_s(node_v(n));
           first = false;
         }
       }
       bw.put('\n');
       bw.flush();
       if (slots != nullptr && bw.n > SLOT) atomicOr(overflow, 1);   // the unit falls back to the LDS-image writer
+      nbytes = slots != nullptr && !(dbg & 1) && bw.n <= SLOT ? bw.n : 0;
       const int32_t rest = bw.n - 1;
       const int32_t ql = q.prefix_len + q.mid_len + rest;          // qname length without the cnt digits
       const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
@@ -345,6 +404,16 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     local_max = o > local_max ? o : local_max;
   }
   if ((threadIdx.x & 63) == 0 && local_max > 0) atomicMax(max_rec, local_max);
+  s_n[threadIdx.x] = nbytes;
+  __syncthreads();
+  if (slots == nullptr) return;
+  const int64_t tb = (int64_t)blockIdx.x * blockDim.x;
+  constexpr int CH = MS_STG / 16;
+  for (int it = threadIdx.x; it < 256 * CH; it += 256) {
+    const int j = it / CH, c = it - j * CH;
+    if (16 * c >= s_n[j]) continue;
+    *(uint4 *)(slots + (tb + j) * SLOT + 16 * c) = *(const uint4 *)&stg[j][4 * c];
+  }
 }
 
 struct LoadRec {
@@ -872,7 +941,7 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
                  (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
-                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, h.n_bkt, h.p_min,
+                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, (const Node32 *)h.nd.p, h.n_bkt, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 
@@ -946,7 +1015,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   stage_begin(ctx, "emit_measure");
   hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
                      rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                     direct ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow);
+                     direct ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow,
+                     getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");

@@ -34,11 +34,19 @@ struct DevBuf {
 
 // Haplotype (one chromosome copy of one BED region) resident on the device.  SURVEY.md §8(a) A9.
 // Sample coordinates are the reference's 1-based `ps`; hap[k] is the base at sample position p_min + k.
+// One node in 32 bytes (emission's random node lookups touch one sector instead of five SoA arrays).
+struct Node32 {
+  int64_t key, ps, pr;   // search key (ps + 1 for 'D'), sample / reference positions (rpc.py:5-20)
+  int32_t oplen;
+  uint8_t op, pad[3];
+};
+
 constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
 
 struct Hap {
   bool valid = false;
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
+  DevBuf nd;    // Node32 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;

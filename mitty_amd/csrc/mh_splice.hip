@@ -227,6 +227,15 @@ __global__ void __launch_bounds__(256) k_hap_rc(const uint8_t *hap, int64_t hap_
   *(uint4 *)(rc + i0) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// AoS copy of the node arrays for the emission kernels' random lookups.
+__global__ void __launch_bounds__(256) k_node_pack(int64_t n, const int64_t *keys, const int64_t *ps,
+                                                   const int64_t *pr, const int64_t *oplen, const uint8_t *op,
+                                                   Node32 *nd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  nd[i] = Node32{keys[i], ps[i], pr[i], (int32_t)oplen[i], op[i], {0, 0, 0}};
+}
+
 // Node-search buckets: bkt[k] = first node whose key is >= p_min + (k << NODE_BKT_SHIFT) (lower_bound), so the
 // searchsorted of rpc.get_begin_end_nodes (rpc.py:127-130) only scans the few keys of one bucket.
 __global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64_t n, int64_t p_min, int64_t n_bkt,
@@ -365,8 +374,13 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   }
-  // --- node-search buckets ------------------------------------------------------------------------------------
+  // --- node-search buckets and the AoS node copy ---------------------------------------------------------------
   {
+    MH_TRY(ensure(ctx, h.nd, sizeof(Node32) * (n_nodes + 1)));
+    hipLaunchKernelGGL(k_node_pack, dim3(grid_for(n_nodes, 256, INT32_MAX)), dim3(256), 0, st, n_nodes,
+                       (const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
+                       (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, (Node32 *)h.nd.p);
+    HIPCHK(ctx, hipGetLastError());
     const int64_t n_bkt = ((hap_len + 2048) >> NODE_BKT_SHIFT) + 1;   // keys reach at most p_min + hap_len + 1
     MH_TRY(ensure(ctx, h.bkt, 4 * (n_bkt + 2)));
     hipLaunchKernelGGL(k_node_buckets, dim3(grid_for(n_bkt + 1, 256, INT32_MAX)), dim3(256), 0, st,
