@@ -399,11 +399,19 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     }
     recs[t] = out;
   }
+  int32_t local_slot = nbytes;
   for (int d = 32; d >= 1; d >>= 1) {   // one atomic per wave
     int32_t o = __shfl_xor(local_max, d, 64);
     local_max = o > local_max ? o : local_max;
+    o = __shfl_xor(local_slot, d, 64);
+    local_slot = o > local_slot ? o : local_slot;
   }
-  if ((threadIdx.x & 63) == 0 && local_max > 0) atomicMax(max_rec, local_max);
+  // one lane per wave, and only when the (possibly stale) current maximum is lower: same-address atomics from every
+  // wave of the launch serialize at the memory side
+  if ((threadIdx.x & 63) == 0) {
+    if (local_max > 0 && local_max > __builtin_nontemporal_load(max_rec)) atomicMax(max_rec, local_max);
+    if (local_slot > 0 && local_slot > __builtin_nontemporal_load(max_rec + 3)) atomicMax(max_rec + 3, local_slot);
+  }
   s_n[threadIdx.x] = nbytes;
   __syncthreads();
   if (slots == nullptr) return;
@@ -722,7 +730,8 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
   const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
-  const int32_t o_dump = o_s + NF * ED_T * 4 * 16;            // 16-byte sink for unused gathers
+  const bool staged = !(A.dbg & 128);                          // seam chunks via LDS (dbg 128: direct stores)
+  const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;     // T = '\n+\n' + rlen '~' + '\n' (perfect reads, readgenerate.py:229)
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
@@ -876,13 +885,14 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;        // tile start: the previous tile owns the rest
     const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
     if (lo == 0 && hi == 16) {
-      *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (staged) *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      else *(uint4 *)(A.arena[f] + (cg << 4)) = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
       char *g = A.arena[f] + (cg << 4);
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
-  __syncthreads();
+  if (staged) __syncthreads();
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
     const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
@@ -898,6 +908,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     for (int64_t cg = c0 + q; x0 + 16 <= L; cg += LPR, x0 += 16 * LPR) {
       const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
+      if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
                                  : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : o_t + (x0 - tl)));
       const uint4 v = (A.dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
@@ -1024,10 +1035,11 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
                               (E3 *)ctx->scan_partials.p, tot));
   stage_end(ctx);
   E3 ht;
-  int32_t hmax = 0;
+  int32_t hm4[4] = {0, 0, 0, 0};   // max record length + 20, err, overflow, max slot bytes
   HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(&hmax, max_rec, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  const int32_t hmax = hm4[0], hslot = hm4[3];
   ht.kept -= cnt_base;
 
   // arenas: append after what is already there
@@ -1066,10 +1078,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   stage_begin(ctx, "emit_write");
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
-  const int32_t qstride = head + SLOT + 32;
+  const char *dbg_env = getenv("MH_EMIT_DBG");   // timing experiments only: skip parts of the kernel
+  const int32_t edbg = dbg_env ? atoi(dbg_env) : 0;
+  const bool staged = !(edbg & 128);              // seam chunks staged in LDS (dbg 128: stored directly, experiment)
+  const int32_t qstride = head + ((edbg & 256) ? SLOT : (hslot > 16 ? (hslot + 15) / 16 * 16 : 16)) + 32;
   const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
                        (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-                       (size_t)2 * ED_T * 4 * 16 + 16;
+                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16;
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -1081,10 +1096,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   if (direct && !hover && head_fits && win_stride <= 16 * 4 * ED_WMAX && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
     // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots)
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
-    const char *dbg_env = getenv("MH_EMIT_DBG");   // timing experiments only: skip parts of the kernel
     EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p,
              {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
-             qstride, dbg_env ? atoi(dbg_env) : 0};
+             qstride, edbg};
     const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
     auto kfn = write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16> : lpr == 8 ? k_emit_direct<2, 8> : k_emit_direct<2, 4>)
                             : (lpr == 16 ? k_emit_direct<1, 16> : k_emit_direct<1, 8>);

@@ -20,7 +20,9 @@
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
 // fallback for a unit whose decode ran out of pre-generated words.
 #include <cmath>
+#include <cstdlib>
 
+#include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -57,7 +59,7 @@ __device__ void mt_seed_lds(uint32_t *st, uint32_t seed) {
       st[i] = v;
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // One twist: o (old state) -> nw (new state), calling emit(k, tempered word) for k = 0..623.
@@ -70,14 +72,14 @@ __device__ __forceinline__ void mt_twist_block(const uint32_t *o, uint32_t *nw, 
     nw[t] = v;
     emit(t, mt_temper(v));
   }
-  __syncthreads();
+  lds_barrier();
   if (t < 227) {
     int i = 227 + t;
     uint32_t v = nw[i - 227] ^ mt_mix(o[i], o[i + 1]);
     nw[i] = v;
     emit(i, mt_temper(v));
   }
-  __syncthreads();
+  lds_barrier();
   if (t < 170) {
     int i = 454 + t;
     uint32_t nxt = (i < 623) ? o[i + 1] : nw[0];
@@ -85,7 +87,7 @@ __device__ __forceinline__ void mt_twist_block(const uint32_t *o, uint32_t *nw, 
     nw[i] = v;
     emit(i, mt_temper(v));
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // ---- jump-ahead segments ---------------------------------------------------------------------------------------
@@ -97,49 +99,87 @@ struct SegJob {
   int32_t k;          // segment index: start = k * SEG_WORDS, jump polynomial polys[k]
 };
 
-__global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys) {
-  __shared__ uint32_t x[EXT_WORDS];
+constexpr int CB_WORDS = 2048;   // circular window of the extended sequence x_i (jump), then the two twist states
+constexpr int CB_MASK = CB_WORDS - 1;
+
+// The jump W_J[w] = XOR over set bits k of g of x_{k+w} walks the polynomial's bits in increasing k, so x is
+// generated 624 words at a time into a 2048-word circular window just ahead of the bits that need it (10.5 KB of
+// LDS instead of 82 KB: eight workgroups per CU instead of one).
+__global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys, int dbg) {
+  __shared__ uint32_t cb[CB_WORDS];
+  __shared__ uint32_t gp[624];
   const SegJob job = jobs[blockIdx.x];
   const int t = threadIdx.x;
-  mt_seed_lds(x, job.seed);
-  if (job.k > 0) {
-    // x_624 .. x_20591 in place: x[i] = x[i-227] ^ mix(x[i-624], x[i-623])
-    for (int b = 624; b < EXT_WORDS; b += 624) {
-      if (t < 227) { int i = b + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
-      __syncthreads();
-      if (t < 227) { int i = b + 227 + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
-      __syncthreads();
-      if (t < 170) { int i = b + 454 + t; x[i] = x[i - 227] ^ mt_mix(x[i - 624], x[i - 623]); }
-      __syncthreads();
-    }
-    // W_J[w] = XOR over set bits k of g of x[k + w]
+  mt_seed_lds(cb, job.seed);   // x_0 .. x_623
+  if (job.k > 0 && !(dbg & 1)) {
     const uint32_t *g = polys + (int64_t)job.k * 624;
+    for (int i = t; i < 624; i += 256) gp[i] = g[i];
+    lds_barrier();
     const int w0 = t, w1 = t + 256, w2 = t + 512;
     const bool h2 = w2 < 624;
     uint32_t a0 = 0, a1 = 0, a2 = 0;
+    int32_t G = 624;   // x_0 .. x_{G-1} exist (the last CB_WORDS of them in the window)
     for (int pw = 0; pw < 624; pw++) {
-      uint32_t m = g[pw];
       const int kb = pw * 32;
-      while (m) {
-        const int k = kb + __builtin_ctz(m);
-        m &= m - 1;
-        a0 ^= x[k + w0];
-        a1 ^= x[k + w1];
-        if (h2) a2 ^= x[k + w2];
+      // bits kb .. kb+31 read x up to x_{kb+31+623}.  Overwritten slots hold x_{G-2048} .. x_{G-1425}, older than
+      // any x still needed (>= x_{kb} >= x_{G-654}) by this or a lagging wave (>= x_{G-1278}).
+      while (G <= kb + 31 + 623) {   // G and kb are uniform: every wave takes the same barriers
+        if (t < 227) {
+          const int i = G + t;
+          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
+        }
+        lds_barrier();
+        if (t < 227) {
+          const int i = G + 227 + t;
+          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
+        }
+        lds_barrier();
+        if (t < 170) {
+          const int i = G + 454 + t;
+          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
+        }
+        lds_barrier();
+        G += 624;
+      }
+      uint32_t m = gp[pw];
+      while (m) {   // eight set bits per step: 24 independent LDS reads in flight
+        int kk[8];
+        uint32_t v0[8], v1[8], v2[8];
+        int nb = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          kk[u] = kb + (m ? __builtin_ctz(m) : 0);
+          nb += m != 0;
+          m &= m - 1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          v0[u] = cb[(kk[u] + w0) & CB_MASK];
+          v1[u] = cb[(kk[u] + w1) & CB_MASK];
+          v2[u] = h2 ? cb[(kk[u] + w2) & CB_MASK] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          if (u < nb) {
+            a0 ^= v0[u];
+            a1 ^= v1[u];
+            a2 ^= v2[u];
+          }
+        }
       }
     }
-    __syncthreads();
-    x[w0] = a0;
-    x[w1] = a1;
-    if (h2) x[w2] = a2;
-    __syncthreads();
+    lds_barrier();
+    cb[w0] = a0;
+    cb[w1] = a1;
+    if (h2) cb[w2] = a2;
+    lds_barrier();
   }
-  uint32_t *st0 = x, *st1 = x + 624;
+  uint32_t *st0 = cb, *st1 = cb + 624;
   uint32_t *out = job.out + job.start;
-  const int64_t cnt = job.count;
+  const int64_t cnt = (dbg & 2) ? 0 : job.count;
   for (int64_t base = 0; base < cnt; base += 624) {
     mt_twist_block(st0, st1, [&](int k, uint32_t w) {
-      if (base + k < cnt) out[base + k] = w;
+      if (base + k < cnt && !(dbg & 4)) out[base + k] = w;
     });
     uint32_t *tmp = st0; st0 = st1; st1 = tmp;
   }
@@ -990,7 +1030,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       HIPCHK(ctx, hipMemcpyAsync(d_dec, dec.data(), sizeof(DecJob) * dec.size(), hipMemcpyHostToDevice, st));
       stage_begin(ctx, "sample_mt_segments");
       hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)d_jobs,
-                         (const uint32_t *)ctx->jump_polys.p);
+                         (const uint32_t *)ctx->jump_polys.p, getenv("MH_MT_DBG") ? atoi(getenv("MH_MT_DBG")) : 0);
       HIPCHK(ctx, hipGetLastError());
       stage_end(ctx);
       stage_begin(ctx, "sample_shuffle_decode");
