@@ -20,6 +20,7 @@
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
 // fallback for a unit whose decode ran out of pre-generated words.
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 
 #include "mh_device.h"
@@ -199,7 +200,7 @@ struct DecJob {
   int64_t *status;         // remaining i0 (0 = complete)
 };
 
-constexpr int DC_THREADS = 1024;
+constexpr int DC_THREADS = 256;
 constexpr int DC_WAVES = DC_THREADS / 64;
 constexpr int DC_PER = 4;
 constexpr int DC_CHUNK = DC_THREADS * DC_PER;
@@ -312,13 +313,8 @@ constexpr int32_t DC_BIG = 1 << 30;
 // Per chunk: the accept count and the margin [dlo, dhi]: for every start shift d in it, no accept decision and no
 // interval mask of the chunk changes (all i shift by d), so the count stays valid.  dhi = 0 once i reached 0.
 template <bool WRITE>
-__global__ void __launch_bounds__(DC_THREADS) k_decode_chunks(const ChunkJob *jobs, const int32_t *todo,
-                                                              const int64_t *start, int32_t *count,
-                                                              int32_t *margin) {
-  __shared__ int32_t wsum[DC_WAVES];
-  __shared__ int32_t wlo[DC_WAVES], whi[DC_WAVES];
-  __shared__ int32_t s_tot;
-  const int32_t c = todo ? todo[blockIdx.x] : (int32_t)blockIdx.x;
+__device__ void decode_chunk(const ChunkJob *jobs, int32_t c, const int64_t *start, int32_t *count, int32_t *margin,
+                             int32_t *wsum, int32_t *wlo, int32_t *whi, int32_t &s_tot) {
   const ChunkJob job = jobs[c];
   const int64_t i0 = start[c];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -438,6 +434,108 @@ __global__ void __launch_bounds__(DC_THREADS) k_decode_chunks(const ChunkJob *jo
     count[c] = s_tot;
     margin[2 * c] = L;
     margin[2 * c + 1] = H;
+  }
+}
+
+// Chunks todo[0 .. *n_todo) (all chunks when todo == nullptr), strided over the grid; the list and its length are
+// device-resident, written by k_decode_resolve, so passes chain on the stream without host round trips.
+template <bool WRITE>
+__global__ void __launch_bounds__(DC_THREADS) k_decode_chunks(const ChunkJob *jobs, const int32_t *todo,
+                                                              const int32_t *n_todo, int32_t n_all,
+                                                              const int64_t *start, int32_t *count,
+                                                              int32_t *margin) {
+  __shared__ int32_t wsum[DC_WAVES];
+  __shared__ int32_t wlo[DC_WAVES], whi[DC_WAVES];
+  __shared__ int32_t s_tot;
+  const int32_t n = todo ? *n_todo : n_all;
+  for (int32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    decode_chunk<WRITE>(jobs, todo ? todo[i] : i, start, count, margin, wsum, wlo, whi, s_tot);
+    __syncthreads();
+  }
+}
+
+// After a count pass: per unit, the starts the counts imply (s = n - 1 - accepts before the chunk), and the chunks
+// whose count was taken at a start outside their margin, which are queued for the next pass at the implied start.
+// Tiles of up to DR_TILE chunks never cross a unit: k_decode_tile_sums sums each tile's counts, then
+// k_decode_resolve (one workgroup per tile) adds the unit's earlier tiles as its carry.
+constexpr int DR_THREADS = 1024, DR_PER = 8, DR_TILE = DR_THREADS * DR_PER;
+struct DecTile {
+  int32_t unit, begin, end, first_tile;   // chunks [begin, end); first_tile = the unit's first tile index
+};
+
+__device__ __forceinline__ int64_t block_sum_1024(int64_t v, int64_t *wsum) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if (lane == 0) wsum[wave] = v;
+  __syncthreads();
+  int64_t tot = 0;
+#pragma unroll
+  for (int q = 0; q < DR_THREADS / 64; q++) tot += wsum[q];
+  return tot;
+}
+
+__global__ void __launch_bounds__(DR_THREADS) k_decode_tile_sums(const DecTile *tiles, const int32_t *count,
+                                                                 int64_t *tile_sum, int32_t *n_todo) {
+  __shared__ int64_t wsum[DR_THREADS / 64];
+  const DecTile tl = tiles[blockIdx.x];
+  const int32_t c0 = tl.begin + threadIdx.x * DR_PER;
+  int64_t loc = 0;
+#pragma unroll
+  for (int k = 0; k < DR_PER; k++) loc += c0 + k < tl.end ? count[c0 + k] : 0;
+  const int64_t tot = block_sum_1024(loc, wsum);
+  if (threadIdx.x == 0) {
+    tile_sum[blockIdx.x] = tot;
+    if (blockIdx.x == 0) *n_todo = 0;   // k_decode_resolve (next on the stream) appends to the queue
+  }
+}
+
+__global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *tiles, const int64_t *n_draws,
+                                                               const int64_t *tile_sum, const int32_t *count,
+                                                               const int32_t *margin, int64_t *s0, int64_t *s1,
+                                                               int32_t *todo, int32_t *n_todo, int64_t *rem) {
+  __shared__ int64_t wsum[DR_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const DecTile tl = tiles[blockIdx.x];
+  int64_t carry = n_draws[tl.unit] - 1;
+  for (int32_t k = tl.first_tile; k < (int32_t)blockIdx.x; k++) carry -= tile_sum[k];
+  const int32_t c0 = tl.begin + t * DR_PER;
+  int32_t cv[DR_PER];
+  int64_t loc = 0;
+#pragma unroll
+  for (int k = 0; k < DR_PER; k++) {
+    cv[k] = c0 + k < tl.end ? count[c0 + k] : 0;
+    loc += cv[k];
+  }
+  int64_t incl = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int64_t pre = 0;
+#pragma unroll
+  for (int q = 0; q < DR_THREADS / 64; q++) pre += q < wave ? wsum[q] : 0;
+  int64_t s = carry - (pre + incl - loc);
+#pragma unroll
+  for (int k = 0; k < DR_PER; k++) {
+    const int32_t c = c0 + k;
+    if (c >= tl.end) break;
+    const int64_t sv = s > 0 ? s : 0;
+    s1[c] = sv;
+    const int64_t d = sv - s0[c];
+    if (d < margin[2 * c] || d > margin[2 * c + 1]) {
+      s0[c] = sv;
+      todo[atomicAdd(n_todo, 1)] = c;
+    }
+    s -= cv[k];
+  }
+  // the unit's last tile: draws left after its last chunk
+  if (t == DR_THREADS - 1 && (blockIdx.x + 1 == gridDim.x || tiles[blockIdx.x + 1].unit != tl.unit)) {
+    const int64_t left = carry - (pre + incl);
+    rem[tl.unit] = left < 1 ? 0 : left;
   }
 }
 
@@ -760,8 +858,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     return MH_OK;
   }
   // starts: the exact one for each unit's first chunk, then the expected accepts (rate (i+1)/(mask+1))
-  std::vector<int64_t> s0(C), s1(C);
-  std::vector<int32_t> cnt(C), todo;
+  std::vector<int64_t> s0(C);
   for (size_t u = 0; u < dec.size(); u++) {
     double i = (double)(dec[u].n - 1);
     for (int32_t c = first[u]; c < first[u + 1]; c++) {
@@ -779,64 +876,75 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
       }
     }
   }
-  const size_t bytes = sizeof(ChunkJob) * C + 8 * C + 4 * C + 4 * C + 8 * C + 256;
+  const int32_t U = (int32_t)dec.size();
+  std::vector<DecTile> tiles;
+  for (int32_t u = 0; u < U; u++) {
+    const int32_t ft = (int32_t)tiles.size();
+    for (int32_t b = first[u]; b < first[u + 1]; b += DR_TILE)
+      tiles.push_back(DecTile{u, b, std::min(b + DR_TILE, first[u + 1]), ft});
+  }
+  const int32_t T = (int32_t)tiles.size();
+  const size_t bytes = ((sizeof(ChunkJob) * C + 15) / 16) * 16 + 8 * C * 2 + 8 * U * 2 + 8 * (T + 1) +
+                       sizeof(DecTile) * (T + 1) + 4 * C * 2 + 8 * C + 256;
   MH_TRY(ensure(ctx, ctx->dec_buf, bytes));
   char *p = (char *)ctx->dec_buf.p;
   ChunkJob *d_jobs = (ChunkJob *)p;
-  int64_t *d_start = (int64_t *)(p + ((sizeof(ChunkJob) * C + 15) / 16) * 16);
-  int32_t *d_count = (int32_t *)(d_start + C);
+  int64_t *d_s0 = (int64_t *)(p + ((sizeof(ChunkJob) * C + 15) / 16) * 16);
+  int64_t *d_s1 = d_s0 + C;
+  int64_t *d_ndraw = d_s1 + C;
+  int64_t *d_rem = d_ndraw + U;
+  int64_t *d_tsum = d_rem + U;
+  DecTile *d_tiles = (DecTile *)(d_tsum + T + 1);
+  int32_t *d_count = (int32_t *)(d_tiles + T + 1);
   int32_t *d_todo = d_count + C;
   int32_t *d_margin = d_todo + C;
-  std::vector<int32_t> marg(2 * C);
+  int32_t *d_ntodo = d_margin + 2 * C;
+  std::vector<int64_t> ndraw(U);
+  for (int32_t u = 0; u < U; u++) ndraw[u] = dec[u].n;
   HIPCHK(ctx, hipMemcpyAsync(d_jobs, cj.data(), sizeof(ChunkJob) * C, hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipMemcpyAsync(d_start, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
-  int64_t n_todo = C;
+  HIPCHK(ctx, hipMemcpyAsync(d_s0, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_tiles, tiles.data(), sizeof(DecTile) * T, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_ndraw, ndraw.data(), 8 * U, hipMemcpyHostToDevice, st));
+  const unsigned grid = (unsigned)std::min<int64_t>(C, 4096);
+  // pass 1 over every chunk, then passes over the queued chunks, PASS_BATCH per host check
+  constexpr int PASS_BATCH = 8, MAX_PASSES = 64;
+  hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
+                     (const int32_t *)nullptr, (const int32_t *)nullptr, (int32_t)C, (const int64_t *)d_s0, d_count,
+                     d_margin);
+  HIPCHK(ctx, hipGetLastError());
   bool conv = false;
-  int passes = 0;
-  for (; passes < 64; passes++) {
-    hipLaunchKernelGGL(k_decode_chunks<false>, dim3((unsigned)n_todo), dim3(DC_THREADS), 0, st,
-                       (const ChunkJob *)d_jobs, passes ? (const int32_t *)d_todo : nullptr, (const int64_t *)d_start,
-                       d_count, d_margin);
-    HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipMemcpyAsync(cnt.data(), d_count, 4 * C, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(marg.data(), d_margin, 8 * C, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    // the starts the counts imply; a chunk whose count was taken at a start outside its margin is redone there
-    todo.clear();
-    for (size_t u = 0; u < dec.size(); u++) {
-      int64_t s = dec[u].n - 1;
-      for (int32_t c = first[u]; c < first[u + 1]; c++) {
-        s1[c] = s > 0 ? s : 0;
-        const int64_t d = s1[c] - s0[c];
-        if (d < marg[2 * c] || d > marg[2 * c + 1]) todo.push_back(c);
-        s -= cnt[c];
-      }
+  int passes = 1;
+  while (passes < MAX_PASSES) {
+    for (int k = 0; k < PASS_BATCH; k++, passes++) {
+      hipLaunchKernelGGL(k_decode_tile_sums, dim3(T), dim3(DR_THREADS), 0, st, (const DecTile *)d_tiles,
+                         (const int32_t *)d_count, d_tsum, d_ntodo);
+      hipLaunchKernelGGL(k_decode_resolve, dim3(T), dim3(DR_THREADS), 0, st, (const DecTile *)d_tiles,
+                         (const int64_t *)d_ndraw, (const int64_t *)d_tsum, (const int32_t *)d_count,
+                         (const int32_t *)d_margin, d_s0, d_s1, d_todo, d_ntodo, d_rem);
+      hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
+                         (const int32_t *)d_todo, (const int32_t *)d_ntodo, (int32_t)C, (const int64_t *)d_s0,
+                         d_count, d_margin);
     }
-    if (todo.empty()) {
+    HIPCHK(ctx, hipGetLastError());
+    int32_t h_ntodo = -1;
+    HIPCHK(ctx, hipMemcpyAsync(&h_ntodo, d_ntodo, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
+                                          h_ntodo, (long long)C);
+    if (h_ntodo == 0) {   // the last pass counted nothing: the starts in s1 are the sequential ones
       conv = true;
       break;
     }
-    for (int32_t c : todo) s0[c] = s1[c];
-    n_todo = (int64_t)todo.size();
-    HIPCHK(ctx, hipMemcpyAsync(d_start, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_todo, todo.data(), 4 * n_todo, hipMemcpyHostToDevice, st));
   }
-  ctx->dec_passes = passes + 1;
+  ctx->dec_passes = passes;
   if (!conv) return MH_OK;
-  // every start exact now: the write pass
-  HIPCHK(ctx, hipMemcpyAsync(d_start, s1.data(), 8 * C, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_decode_chunks<true>, dim3((unsigned)C), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
-                     (const int32_t *)nullptr, (const int64_t *)d_start, d_count, d_margin);
+  // every start exact now: the write pass, and draws left per unit (0 unless a unit ran out of words)
+  hipLaunchKernelGGL(k_decode_chunks<true>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
+                     (const int32_t *)nullptr, (const int32_t *)nullptr, (int32_t)C, (const int64_t *)d_s1, d_count,
+                     d_margin);
   HIPCHK(ctx, hipGetLastError());
-  std::vector<int64_t> rem(dec.size());
-  for (size_t u = 0; u < dec.size(); u++) {
-    int64_t s = dec[u].n - 1;
-    for (int32_t c = first[u]; c < first[u + 1]; c++) s -= cnt[c];
-    rem[u] = s < 1 ? 0 : s;
-    if (dec[u].n > 0) {
-      HIPCHK(ctx, hipMemcpyAsync(d_status + (dec[u].status - d_status), &rem[u], 8, hipMemcpyHostToDevice, st));
-    }
-  }
+  for (int32_t u = 0; u < U; u++)
+    if (dec[u].n > 0) HIPCHK(ctx, hipMemcpyAsync(dec[u].status, d_rem + u, 8, hipMemcpyDeviceToDevice, st));
   // j[0] = 0 (the shuffle's unused slot), as k_shuffle_decode2 sets it
   for (size_t u = 0; u < dec.size(); u++)
     if (dec[u].n > 0) HIPCHK(ctx, hipMemsetAsync(dec[u].j, 0, 4, st));
