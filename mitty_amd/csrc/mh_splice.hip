@@ -154,6 +154,48 @@ __global__ void __launch_bounds__(256) k_hap_copy(int64_t total_pieces, int64_t 
   for (int64_t b = b0 + lane; b < b1; b += 64) dp[b] = sp[b];
 }
 
+// Haplotype bytes by output position: thread i writes hap[16i, 16i+16).  The node holding sample position x is the
+// last node whose key is <= x (the bucket table narrows the search, as in emission); 'D' nodes hold no bytes
+// (their key equals the next node's).  Bytes no node covers (possible only before the first node's bytes) are 0.
+__global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min, int64_t n_nodes, const int64_t *keys,
+                                                  const int64_t *ps, const uint8_t *nop, const int64_t *nl,
+                                                  const int64_t *src, const int32_t *bkt, int64_t n_bkt,
+                                                  const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap) {
+  const int64_t o0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (o0 >= hap_len) return;
+  const int64_t x0 = p_min + o0;
+  int64_t kb = (x0 - p_min) >> NODE_BKT_SHIFT;
+  if (kb >= n_bkt) kb = n_bkt - 1;
+  int64_t lo = bkt[kb], hi = kb + 1 < n_bkt ? bkt[kb + 1] : n_nodes;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] <= x0) lo = mid + 1; else hi = mid;
+  }
+  int64_t k = lo - 1;
+  uint32_t w[4] = {0, 0, 0, 0};
+  int64_t nk = k >= 0 ? ps[k] : 0, ne = k >= 0 ? nk + (nop[k] == 'D' ? 0 : nl[k]) : 0;
+  const uint8_t *sp = nullptr;
+  if (k >= 0) {
+    const int64_t s = src[k];
+    sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
+  }
+#pragma unroll
+  for (int b = 0; b < 16; b++) {
+    const int64_t x = x0 + b;
+    if (o0 + b >= hap_len) break;
+    while (k + 1 < n_nodes && keys[k + 1] <= x) {
+      k++;
+      nk = ps[k];
+      ne = nk + (nop[k] == 'D' ? 0 : nl[k]);
+      const int64_t s = src[k];
+      sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
+    }
+    const uint32_t c = (k >= 0 && x >= nk && x < ne) ? sp[x - nk] : 0u;
+    w[b >> 2] |= c << (8 * (b & 3));
+  }
+  *(uint4 *)(hap + o0) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // ---- N runs ---------------------------------------------------------------------------------------------------
 constexpr int64_t NCHUNK = 16;
 
@@ -366,15 +408,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
   }
   int64_t p_min = ps0;
   MH_TRY(ensure(ctx, h.hap, hap_len + 1024));   // emission gathers whole 16-byte chunks past the last base
-  if (pieces > 0) {
-    stage_begin(ctx, "splice_hap_copy");
-    int64_t threads = pieces * 64;
-    hipLaunchKernelGGL(k_hap_copy, dim3(grid_for(threads, 256, INT32_MAX)), dim3(256), 0, st, pieces, n_nodes, poff,
-                       ps, nl, nsrc, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p, p_min);
-    HIPCHK(ctx, hipGetLastError());
-    stage_end(ctx);
-  }
-  // --- node-search buckets and the AoS node copy ---------------------------------------------------------------
+  // --- node-search buckets and the AoS node copy (the byte fill below and emission search through them) --------
   {
     MH_TRY(ensure(ctx, h.nd, sizeof(Node32) * (n_nodes + 1)));
     hipLaunchKernelGGL(k_node_pack, dim3(grid_for(n_nodes, 256, INT32_MAX)), dim3(256), 0, st, n_nodes,
@@ -387,6 +421,15 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int
                        (const int64_t *)h.keys.p, n_nodes, p_min, n_bkt, (int32_t *)h.bkt.p);
     HIPCHK(ctx, hipGetLastError());
     h.n_bkt = n_bkt;
+  }
+  if (pieces > 0 && hap_len > 0) {
+    stage_begin(ctx, "splice_hap_copy");
+    hipLaunchKernelGGL(k_hap_fill, dim3(grid_for((hap_len + 15) / 16, 256, INT32_MAX)), dim3(256), 0, st, hap_len,
+                       p_min, n_nodes, (const int64_t *)keys, (const int64_t *)ps, (const uint8_t *)nop,
+                       (const int64_t *)nl, (const int64_t *)nsrc, (const int32_t *)h.bkt.p, h.n_bkt,
+                       (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
   }
   // --- reverse complement (mate-1 reads) --------------------------------------------------------------------
   MH_TRY(ensure(ctx, h.rc, hap_len + 1024));
