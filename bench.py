@@ -81,6 +81,8 @@ def main():
   if a.corrupt:
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), a.seed)
   eng.load_region(0, ('1', 0, a.length), seq)
+  for cpy in range(len(copies)):   # inputs resident in HBM before timing: contig and both copies' variants
+    eng.upload_variants(0, cpy, copies[cpy])
   eng.ctx.set_emit_mode(a.emit_mode)
   kernel = 'k_emit_write' if (a.emit_mode or a.corrupt) else 'k_emit_direct'
 

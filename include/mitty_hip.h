@@ -9,6 +9,7 @@
  *   mh_upload_contig      pysam.FastaFile.fetch of a BED region          mitty/simulation/readgenerate.py:181,186
  *   mh_build_haplotype    rpc.create_node_list (+ rpc.Node)              mitty/simulation/rpc.py:5-116
  *                         fed by vcfio.split_copies/parse per copy       mitty/lib/vcfio.py:67-126
+ *   mh_upload_variants    (the same copy's variant list, kept resident; mh_build_haplotype_vset splices from it)
  *   mh_sample_templates   illumina.generate_reads                        mitty/simulation/illumina.py:43-110
  *   mh_sample_units       (the same for many units: the worker pool of readgenerate.py:102-115)
  *   mh_set_templates      (the template arrays a read module returns)   mitty/simulation/illumina.py:238-269
@@ -75,6 +76,14 @@ int32_t mh_build_haplotype(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t
                            const int64_t *v_alt_off, const int64_t *v_alt_len, const char *alt_pool,
                            int64_t alt_pool_len, int64_t n_var,
                            int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max);
+/* Resident variant sets: upload one copy's variants once (same arrays and checks as mh_build_haplotype), then
+ * splice from the device copy as often as needed — the input stays in HBM across jobs. */
+int32_t mh_upload_variants(mh_ctx *ctx, int32_t vset, const int64_t *v_pos, const uint8_t *v_op,
+                           const int64_t *v_oplen, const int64_t *v_alt_off, const int64_t *v_alt_len,
+                           const char *alt_pool, int64_t alt_pool_len, int64_t n_var);
+int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, int32_t vset,
+                                int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max);
+int32_t mh_release_variants(mh_ctx *ctx, int32_t vset);
 /* Copy a slot's node list back (arrays sized n_nodes; seq bytes of node k = hap[ps[k]-p_min .. +oplen) for
  * non-'D' nodes).  Any pointer may be NULL. */
 int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_t *op, int64_t *oplen,

@@ -15,7 +15,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
-           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_get_nodes',
+           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
@@ -63,6 +63,9 @@ def lib():
   _sig(L, 'mh_read_model_params', [c_i64, c_dbl, ctypes.POINTER(c_dbl), P_i64])
   _sig(L, 'mh_work_units', [c_u64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, P_i64])
   _sig(L, 'mh_upload_contig', [c_vp, c_i32, c_vp, c_i64])
+  _sig(L, 'mh_upload_variants', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64])
+  _sig(L, 'mh_build_haplotype_vset', [c_vp, c_i32, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_release_variants', [c_vp, c_i32])
   _sig(L, 'mh_build_haplotype', [c_vp, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                  P_i64, P_i64, P_i64])
   _sig(L, 'mh_get_nodes', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
@@ -272,6 +275,24 @@ class Context:
                                          _ptr(pool_arr), len(pool), n, ctypes.byref(nn), ctypes.byref(pmin),
                                          ctypes.byref(pmax)))
     return nn.value, pmin.value, pmax.value
+
+  def upload_variants(self, vset, vsoa):
+    """Keep one copy's variants resident on the device (same layout and checks as build_haplotype)."""
+    n = len(vsoa['pos'])
+    pool = vsoa['alt_pool']
+    pool_arr = np.frombuffer(pool, dtype=np.uint8) if len(pool) else np.zeros(1, np.uint8)
+    arrs = [np.ascontiguousarray(vsoa[k], dtype=dt) for k, dt in
+            (('pos', np.int64), ('op', np.uint8), ('oplen', np.int64), ('alt_off', np.int64), ('alt_len', np.int64))]
+    self._chk(self._L.mh_upload_variants(self._h, int(vset), *[_ptr(a) for a in arrs], _ptr(pool_arr), len(pool), n))
+
+  def build_haplotype_vset(self, slot, contig_id, ref_start_pos, vset):
+    nn, pmin, pmax = c_i64(), c_i64(), c_i64()
+    self._chk(self._L.mh_build_haplotype_vset(self._h, slot, contig_id, int(ref_start_pos), int(vset),
+                                              ctypes.byref(nn), ctypes.byref(pmin), ctypes.byref(pmax)))
+    return nn.value, pmin.value, pmax.value
+
+  def release_variants(self, vset):
+    self._chk(self._L.mh_release_variants(self._h, int(vset)))
 
   def get_nodes(self, slot, n_nodes, with_hap=True):
     ps, pr, ol = (np.empty(max(n_nodes, 1), np.int64) for _ in range(3))

@@ -60,6 +60,11 @@ void release(DevBuf &b) {
   b.cap = 0;
 }
 
+void release_hap(Hap &h) {
+  release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr);
+  release(h.op); release(h.oplen); release(h.nrun_s); release(h.nrun_e);
+}
+
 void stage_begin(mh_ctx *ctx, const char *name) {
   if (!ctx->timing) return;
   StageTime s{name, nullptr, nullptr};
@@ -141,15 +146,13 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   for (auto &kv : ctx->contigs) release(kv.second.seq);
-  for (auto &kv : ctx->haps) {
-    Hap &h = kv.second;
-    release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
-    release(h.nrun_s); release(h.nrun_e);
-  }
+  for (auto &kv : ctx->haps) release_hap(kv.second);
+  for (auto &h : ctx->hap_spare) release_hap(h);
+  for (auto &kv : ctx->vsets) release_vars(kv.second);
   for (auto &kv : ctx->tsets) {
     release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1);
   }
-  release(ctx->jump_polys);
+  release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->s) release(b);
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
@@ -222,22 +225,71 @@ int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_
   return MH_OK;
 }
 
+static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, const VarSet &v,
+                          int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
+  auto it = ctx->contigs.find(contig_id);
+  if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+  if (!ctx->haps.count(slot) && !ctx->hap_spare.empty()) {   // reuse a released haplotype's buffers
+    Hap r{};
+    const Hap &s = ctx->hap_spare.back();
+    r.hap = s.hap; r.rc = s.rc; r.keys = s.keys; r.ps = s.ps; r.pr = s.pr; r.op = s.op; r.oplen = s.oplen;
+    r.nrun_s = s.nrun_s; r.nrun_e = s.nrun_e; r.nd = s.nd; r.bkt = s.bkt;
+    ctx->hap_spare.pop_back();
+    ctx->haps[slot] = r;
+  }
+  Hap &h = ctx->haps[slot];
+  h.valid = false;
+  MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v));
+  if (out_n_nodes) *out_n_nodes = h.n_nodes;
+  if (out_p_min) *out_p_min = h.p_min;
+  if (out_p_max) *out_p_max = h.p_max;
+  return MH_OK;
+}
+
 int32_t mh_build_haplotype(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, const int64_t *v_pos,
                            const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
                            const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var,
                            int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
   CTX_GUARD(ctx);
-  auto it = ctx->contigs.find(contig_id);
-  if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+  if (!ctx->contigs.count(contig_id)) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
   if (n_var < 0 || (n_var > 0 && (!v_pos || !v_op || !v_oplen || !v_alt_off || !v_alt_len)))
     return arg_fail(ctx, MH_E_ARG, "bad variant arrays");
-  Hap &h = ctx->haps[slot];
-  h.valid = false;
-  MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v_pos, v_op, v_oplen, v_alt_off, v_alt_len, alt_pool,
-                      alt_pool_len, n_var));
-  if (out_n_nodes) *out_n_nodes = h.n_nodes;
-  if (out_p_min) *out_p_min = h.p_min;
-  if (out_p_max) *out_p_max = h.p_max;
+  VarSet &v = ctx->vsets[-1];   // scratch set, replaced by every call
+  MH_TRY(var_upload(ctx, v, v_pos, v_op, v_oplen, v_alt_off, v_alt_len, alt_pool, alt_pool_len, n_var));
+  return build_from(ctx, slot, contig_id, ref_start_pos, v, out_n_nodes, out_p_min, out_p_max);
+}
+
+int32_t mh_upload_variants(mh_ctx *ctx, int32_t vset, const int64_t *v_pos, const uint8_t *v_op,
+                           const int64_t *v_oplen, const int64_t *v_alt_off, const int64_t *v_alt_len,
+                           const char *alt_pool, int64_t alt_pool_len, int64_t n_var) {
+  CTX_GUARD(ctx);
+  if (vset < 0) return arg_fail(ctx, MH_E_ARG, "variant set ids are >= 0");
+  if (n_var < 0 || (n_var > 0 && (!v_pos || !v_op || !v_oplen || !v_alt_off || !v_alt_len)))
+    return arg_fail(ctx, MH_E_ARG, "bad variant arrays");
+  const int32_t rc = var_upload(ctx, ctx->vsets[vset], v_pos, v_op, v_oplen, v_alt_off, v_alt_len, alt_pool,
+                                alt_pool_len, n_var);
+  if (rc != MH_OK) {
+    release_vars(ctx->vsets[vset]);
+    ctx->vsets.erase(vset);
+  }
+  return rc;
+}
+
+int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, int32_t vset,
+                                int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
+  CTX_GUARD(ctx);
+  auto it = ctx->vsets.find(vset);
+  if (vset < 0 || it == ctx->vsets.end()) return arg_fail(ctx, MH_E_STATE, "unknown variant set id");
+  return build_from(ctx, slot, contig_id, ref_start_pos, it->second, out_n_nodes, out_p_min, out_p_max);
+}
+
+int32_t mh_release_variants(mh_ctx *ctx, int32_t vset) {
+  CTX_GUARD(ctx);
+  auto it = ctx->vsets.find(vset);
+  if (it == ctx->vsets.end()) return MH_OK;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  release_vars(it->second);
+  ctx->vsets.erase(it);
   return MH_OK;
 }
 
@@ -270,9 +322,15 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr); release(h.op); release(h.oplen);
-  release(h.nrun_s); release(h.nrun_e);
+  // keep the buffers for the next build (stream order protects them: every later user is on ctx->stream)
+  constexpr size_t SPARE_MAX = 4;
+  if (ctx->hap_spare.size() < SPARE_MAX) {
+    h.valid = false;
+    ctx->hap_spare.push_back(h);
+  } else {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    release_hap(h);
+  }
   ctx->haps.erase(it);
   return MH_OK;
 }

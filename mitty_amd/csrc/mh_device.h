@@ -10,4 +10,28 @@ namespace mh {
 // memory round trip on every barrier of a kernel that streams results out between barriers.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// 0xff in every byte of x equal to the byte replicated in c
+__device__ __forceinline__ uint32_t byte_eq(uint32_t x, uint32_t c) {
+  const uint32_t y = x ^ c;
+  const uint32_t t = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+  return (t >> 7) * 0xffu;
+}
+
+// str.maketrans('ATCGN', 'TAGCN') on four bytes at once ('A'^'T' = 0x15, 'C'^'G' = 0x04; others unchanged)
+__device__ __forceinline__ uint32_t comp4(uint32_t x) {
+  const uint32_t at = byte_eq(x, 0x41414141u) | byte_eq(x, 0x54545454u);
+  const uint32_t cg = byte_eq(x, 0x43434343u) | byte_eq(x, 0x47474747u);
+  return x ^ (at & 0x15151515u) ^ (cg & 0x04040404u);
+}
+
+// 16 bytes from an arbitrarily aligned global address: five dword loads from the dword below it + v_alignbyte.
+// Reads up to 3 bytes before and 4 bytes after the range (callers' buffers are padded).
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t *a) {
+  const uint32_t *q = (const uint32_t *)((uintptr_t)a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)((uintptr_t)a & 3u);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
 }  // namespace mh

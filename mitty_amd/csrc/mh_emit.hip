@@ -673,20 +673,6 @@ __device__ __forceinline__ uint32_t lt_mask(int32_t x0, int32_t n) {
   return (uint32_t)((1ull << (8 * k)) - 1ull);
 }
 
-// 0xff in every byte of x equal to the byte replicated in c
-__device__ __forceinline__ uint32_t byte_eq(uint32_t x, uint32_t c) {
-  const uint32_t y = x ^ c;
-  const uint32_t t = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
-  return (t >> 7) * 0xffu;
-}
-
-// str.maketrans('ATCGN', 'TAGCN') on four bytes at once ('A'^'T' = 0x15, 'C'^'G' = 0x04; others unchanged)
-__device__ __forceinline__ uint32_t comp4(uint32_t x) {
-  const uint32_t at = byte_eq(x, 0x41414141u) | byte_eq(x, 0x54545454u);
-  const uint32_t cg = byte_eq(x, 0x43434343u) | byte_eq(x, 0x47474747u);
-  return x ^ (at & 0x15151515u) ^ (cg & 0x04040404u);
-}
-
 __device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // qname head constants by value (kernel arguments: uniform indexing reads them through the scalar cache)

@@ -65,6 +65,13 @@ struct Contig {
   int64_t len = 0;
 };
 
+// One chromosome copy's variants, device-resident (the splice's input): 1-based pos, op 'X'/'I'/'D', oplen, alt
+// bytes pool[aoff .. +alen).
+struct VarSet {
+  DevBuf pos, op, oplen, aoff, alen, pool;
+  int64_t n = 0, pool_len = 0;
+};
+
 // God-aligner record store (mh_bam.hip): parsed FASTQ -> BAM records, resident until mh_bam_write.
 struct BamStore {
   bool refs_set = false;
@@ -105,6 +112,9 @@ struct mh_ctx {
   mh::DevBuf jump_polys;
   int64_t jump_k = 0;
   int64_t fixups = 0;   // units redone on the exact fallback path
+  std::map<int32_t, mh::VarSet> vsets;   // resident variant sets (mh_upload_variants); id -1: mh_build_haplotype's
+  std::vector<mh::Hap> hap_spare;   // released haplotypes' buffers, reused by the next build (no hipMalloc/hipFree)
+  mh::DevBuf perm_tmp;  // radix sort scratch of the permutation
   mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
   int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)
 
@@ -155,6 +165,7 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);
 // Grow preserving the first `keep` bytes (stream-ordered copy).
 int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep);
 void release(DevBuf &b);
+void release_hap(Hap &h);
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);
@@ -170,9 +181,11 @@ inline unsigned grid_for(int64_t n, int threads, int64_t cap = 1 << 20) {
 }
 
 // ---- subsystem entry points (host side, called from mh_api.cpp) -----------------------------------------------
-int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const int64_t *v_pos,
-                     const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
-                     const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var);
+int32_t var_upload(mh_ctx *ctx, VarSet &v, const int64_t *v_pos, const uint8_t *v_op, const int64_t *v_oplen,
+                   const int64_t *v_alt_off, const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len,
+                   int64_t n_var);
+void release_vars(VarSet &v);
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const VarSet &v);
 
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,

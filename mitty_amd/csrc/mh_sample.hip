@@ -14,7 +14,8 @@
 //   scan(geometric)   ts = cumsum(ceil(log1p(-U)/log(1-p))) + p_min + 1 (numpy legacy inversion, pinned against
 //                     numpy), computed inside the scan's Load; quotients within 1e-12 of an integer are flagged
 //                     and the unit is redone with those draws recomputed by the host libm
-//   k_perm_*          the permutation the swaps produce, without replaying them (see k_perm_gather)
+//   k_perm_*          the permutation the swaps produce, without replaying them: steps radix-sorted by target,
+//                     then a chase per step (see k_perm_heads)
 //   k_tlen + scan     tl = searchsorted(cum_tlen (LDS), U) clipped to rlen; keep te < p_max; compaction
 //   k_file_order      fo0[k] = byte (k & 3) of word k >> 2, & 1 (randint(2, dtype=int8) buffering)
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
@@ -22,6 +23,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "mh_device.h"
 #include "mh_internal.h"
@@ -601,57 +605,33 @@ __global__ void __launch_bounds__(SD_THREADS) k_shuffle_decode(uint32_t seed, in
 }
 
 // ---- permutation from swap indices -------------------------------------------------------------------------
-__global__ void k_perm_hist(int64_t n, const uint32_t *j, int32_t *cnt) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  atomicAdd(&cnt[s == 0 ? 0 : j[s]], 1);
-}
-struct LoadCnt {
-  const int32_t *cnt;
-  __device__ int64_t operator()(int64_t i) const { return cnt[i]; }
-};
-struct StoreStart {
-  int32_t *start;
-  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { start[i] = (int32_t)excl; }
-};
-__global__ void k_perm_scatter(int64_t n, const uint32_t *j, const int32_t *start, int32_t *fill, int32_t *entries) {
-  int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  uint32_t b = s == 0 ? 0 : j[s];
-  int32_t slot = atomicAdd(&fill[b], 1);
-  entries[start[b] + slot] = (int32_t)s;
+// Fisher-Yates (for i = n-1..1: swap(x[i], x[j_i]), j_i <= i) composes to a_final[p] = x[sigma(p)], sigma =
+// tau_{n-1} o ... o tau_1 with tau_i = (i j_i).  Following p through tau_1, tau_2, ...: nothing moves it before
+// step p; step p sends it to slot j_p; afterwards it moves only when a later step i targets its current slot c,
+// landing on slot i.  With the steps sorted by (target, step) — one radix sort of j with the step index as value —
+// the first move after step p is the next entry of p's bucket, and every move after that is
+// next(c) = the smallest step > c targeting c = the head of bucket c (or the one after it when step c targeted
+// itself).  So sigma(p) = the end of the chain first(p), next(.), next(.), ... or j_p when p's bucket has no later
+// step.  (j_0 = 0: step 0 is a self-swap, which the sort places first in bucket 0.)
+__global__ void __launch_bounds__(256) k_perm_heads(int64_t n, const uint32_t *K, const uint32_t *V, int32_t *nxt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t b = K[k];
+  if (k > 0 && K[k - 1] == b) return;
+  int32_t s = (int32_t)V[k];
+  if ((uint32_t)s == b) s = (k + 1 < n && K[k + 1] == b) ? (int32_t)V[k + 1] : -1;   // step b: not later than b
+  nxt[b] = s;   // buckets without a head keep the -1 of the memset
 }
 
-// Smallest step s' > after in bucket b, or -1.
-__device__ __forceinline__ int64_t bucket_next(const int32_t *start, const int32_t *entries, int64_t b,
-                                               int64_t after) {
-  int64_t best = -1;
-  for (int32_t e = start[b]; e < start[b + 1]; e++) {
-    int64_t s = entries[e];
-    if (s > after && (best < 0 || s < best)) best = s;
-  }
-  return best;
-}
-
-// Fisher-Yates (for i = n-1..1: swap(x[i], x[j_i])) composes to a_final[p] = x[tau_{n-1}(...tau_1(p))] with
-// tau_i = (i j_i).  Following p through tau_1, tau_2, ...: nothing moves it before step p; step p sends it to
-// j_p; afterwards it moves only when a later step i targets its current slot q (j_i == q), landing on q = i.
-// So q = j_p, then repeatedly the smallest later step whose target is the current slot.
-__global__ void k_perm_gather(int64_t n, const uint32_t *j, const int32_t *start, const int32_t *entries,
-                              const int64_t *ts, int64_t *out) {
-  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  int64_t jp = p == 0 ? 0 : j[p];
-  int64_t c = bucket_next(start, entries, jp, p);   // smallest step > p that targets j_p
-  int64_t q;
-  if (c < 0) {
-    q = jp;
-  } else {
-    for (;;) {
-      int64_t c2 = bucket_next(start, entries, c, c);
-      if (c2 < 0) break;
-      c = c2;
-    }
+__global__ void __launch_bounds__(256) k_perm_chase(int64_t n, const uint32_t *K, const uint32_t *V,
+                                                    const int32_t *nxt, const int64_t *ts, int64_t *out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t b = K[k], p = V[k];
+  int64_t q = b;
+  if (k + 1 < n && K[k + 1] == b) {
+    int32_t c = (int32_t)V[k + 1], d;
+    while ((d = nxt[c]) >= 0) c = d;
     q = c;
   }
   out[p] = ts[q];
@@ -963,7 +943,6 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
   int64_t *ts = (int64_t *)ctx->s[4].p, *ts_shuf = (int64_t *)ctx->s[5].p, *te = (int64_t *)ctx->s[6].p;
   uint8_t *keep = (uint8_t *)ctx->s[7].p;
-  int32_t *cnt = (int32_t *)ctx->s[8].p, *start = (int32_t *)ctx->s[9].p, *entries = (int32_t *)ctx->s[10].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
   int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128);
   const double log_q = std::log(1.0 - p);
@@ -999,15 +978,21 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   const int64_t *ts_use = ts;
   if (rng_mode == MH_RNG_MITTY && n > 1) {
     stage_begin(ctx, "sample_permutation");
-    HIPCHK(ctx, hipMemsetAsync(cnt, 0, 4 * (n + 1), st));
-    hipLaunchKernelGGL(k_perm_hist, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, jarr, cnt);
-    HIPCHK(ctx, device_scan<int64_t>(st, n + 1, LoadCnt{cnt}, StoreStart{start}, OpSum{}, (int64_t)0,
-                                     (int64_t *)ctx->scan_partials.p, tot + 1));
-    HIPCHK(ctx, hipMemsetAsync(cnt, 0, 4 * (n + 1), st));
-    hipLaunchKernelGGL(k_perm_scatter, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, jarr, start, cnt,
-                       entries);
-    hipLaunchKernelGGL(k_perm_gather, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, jarr, start, entries,
-                       ts, ts_shuf);
+    // steps sorted by (target, step): keys j, values the step index (stable LSD radix sort over the target's bits)
+    uint32_t *sk = (uint32_t *)ctx->s[8].p, *sv = (uint32_t *)ctx->s[9].p;
+    int32_t *nxt = (int32_t *)ctx->s[10].p;
+    unsigned end_bit = 1;
+    while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
+    size_t tmp = 0;
+    const rocprim::counting_iterator<uint32_t> iota(0u);
+    HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+    MH_TRY(ensure(ctx, ctx->perm_tmp, tmp + 256));
+    HIPCHK(ctx, rocprim::radix_sort_pairs(ctx->perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+    HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
+    hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
+                       (const uint32_t *)sv, nxt);
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
+                       (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)ts, ts_shuf);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     ts_use = ts_shuf;

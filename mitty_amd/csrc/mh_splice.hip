@@ -10,6 +10,7 @@
 //                                   resident contig / alt pool, 4 KiB pieces, one wave each;
 //   6. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
 // Node arrays are SoA in HBM: keys (search key, ps+1 for 'D' as rpc.py:127), ps, pr, op, oplen.
+#include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -179,6 +180,12 @@ __global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min
     const int64_t s = src[k];
     sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
   }
+  // the usual case: all 16 bytes inside one node's bytes (no later node starts within them)
+  const int64_t kn = k + 1 < n_nodes ? keys[k + 1] : INT64_MAX;
+  if (k >= 0 && o0 + 16 <= hap_len && kn > x0 + 15 && x0 >= nk && x0 + 16 <= ne) {
+    *(uint4 *)(hap + o0) = load16_unaligned(sp + (x0 - nk));
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 16; b++) {
     const int64_t x = x0 + b;
@@ -255,18 +262,16 @@ struct StoreRuns {
 __global__ void __launch_bounds__(256) k_hap_rc(const uint8_t *hap, int64_t hap_len, uint8_t *rc) {
   const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
   if (i0 >= hap_len) return;
-  uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int64_t i = i0 + k;
-    uint8_t c = 0;
-    if (i < hap_len) {
-      c = hap[hap_len - 1 - i];
-      c = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
-    }
-    w[k >> 2] |= (uint32_t)c << (8 * (k & 3));
+  if (i0 + 16 <= hap_len) {   // rc[i0, i0 + 16) = complement of hap[hap_len - 16 - i0, hap_len - i0), reversed
+    const uint4 v = load16_unaligned(hap + (hap_len - 16 - i0));
+    *(uint4 *)(rc + i0) = make_uint4(comp4(__builtin_bswap32(v.w)), comp4(__builtin_bswap32(v.z)),
+                                     comp4(__builtin_bswap32(v.y)), comp4(__builtin_bswap32(v.x)));
+    return;
   }
-  *(uint4 *)(rc + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int k = 0; k < 16 && i0 + k < hap_len; k++)
+    w[k >> 2] |= (uint32_t)hap[hap_len - 1 - (i0 + k)] << (8 * (k & 3));
+  *(uint4 *)(rc + i0) = make_uint4(comp4(w[0]), comp4(w[1]), comp4(w[2]), comp4(w[3]));
 }
 
 // AoS copy of the node arrays for the emission kernels' random lookups.
@@ -295,38 +300,53 @@ __global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64
 
 }  // namespace
 
-int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const int64_t *v_pos, const uint8_t *v_op,
-                     const int64_t *v_oplen, const int64_t *v_alt_off, const int64_t *v_alt_len,
-                     const char *alt_pool, int64_t alt_pool_len, int64_t n_var) {
-  hipStream_t st = ctx->stream;
+int32_t var_upload(mh_ctx *ctx, VarSet &v, const int64_t *v_pos, const uint8_t *v_op, const int64_t *v_oplen,
+                   const int64_t *v_alt_off, const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len,
+                   int64_t n_var) {
   for (int64_t i = 0; i < n_var; i++)
     if (v_op[i] != 'X' && v_op[i] != 'I' && v_op[i] != 'D')
       return arg_fail(ctx, MH_E_COMPLEX_VARIANT, "Complex variants present in VCF. Please filter or refactor these.");
   for (int64_t i = 0; i < n_var; i++)
     if (v_alt_off[i] < 0 || v_alt_len[i] < 0 || v_alt_off[i] + v_alt_len[i] > alt_pool_len)
       return arg_fail(ctx, MH_E_ARG, "variant alt bytes outside alt_pool");
+  hipStream_t st = ctx->stream;
+  const int64_t nv = n_var > 0 ? n_var : 1;
+  MH_TRY(ensure(ctx, v.pos, 8 * nv));
+  MH_TRY(ensure(ctx, v.op, nv));
+  MH_TRY(ensure(ctx, v.oplen, 8 * nv));
+  MH_TRY(ensure(ctx, v.aoff, 8 * nv));
+  MH_TRY(ensure(ctx, v.alen, 8 * nv));
+  MH_TRY(ensure(ctx, v.pool, alt_pool_len > 0 ? alt_pool_len : 1));
+  if (n_var > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(v.pos.p, v_pos, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(v.op.p, v_op, n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(v.oplen.p, v_oplen, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(v.aoff.p, v_alt_off, 8 * n_var, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(v.alen.p, v_alt_len, 8 * n_var, hipMemcpyHostToDevice, st));
+  }
+  if (alt_pool_len > 0) HIPCHK(ctx, hipMemcpyAsync(v.pool.p, alt_pool, alt_pool_len, hipMemcpyHostToDevice, st));
+  // pageable sources: the copies have read them once the stream reaches here
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  v.n = n_var;
+  v.pool_len = alt_pool_len;
+  return MH_OK;
+}
+
+void release_vars(VarSet &v) {
+  release(v.pos); release(v.op); release(v.oplen); release(v.aoff); release(v.alen); release(v.pool);
+  v.n = v.pool_len = 0;
+}
+
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const VarSet &v) {
+  hipStream_t st = ctx->stream;
+  const int64_t n_var = v.n;
   const int64_t nv = n_var > 0 ? n_var : 1;
   const int64_t node_cap = 2 * n_var + 1;
 
   stage_begin(ctx, "splice");
-  // --- inputs to the device (scratch 0..5) -----------------------------------------------------------------
-  MH_TRY(ensure(ctx, ctx->s[0], 8 * nv));
-  MH_TRY(ensure(ctx, ctx->s[1], nv));
-  MH_TRY(ensure(ctx, ctx->s[2], 8 * nv));
-  MH_TRY(ensure(ctx, ctx->s[3], 8 * nv));
-  MH_TRY(ensure(ctx, ctx->s[4], 8 * nv));
-  MH_TRY(ensure(ctx, ctx->s[5], alt_pool_len > 0 ? alt_pool_len : 1));
-  int64_t *d_pos = (int64_t *)ctx->s[0].p, *d_oplen = (int64_t *)ctx->s[2].p;
-  int64_t *d_aoff = (int64_t *)ctx->s[3].p, *d_alen = (int64_t *)ctx->s[4].p;
-  uint8_t *d_op = (uint8_t *)ctx->s[1].p, *d_pool = (uint8_t *)ctx->s[5].p;
-  if (n_var > 0) {
-    HIPCHK(ctx, hipMemcpyAsync(d_pos, v_pos, 8 * n_var, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_op, v_op, n_var, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_oplen, v_oplen, 8 * n_var, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_aoff, v_alt_off, 8 * n_var, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_alen, v_alt_len, 8 * n_var, hipMemcpyHostToDevice, st));
-  }
-  if (alt_pool_len > 0) HIPCHK(ctx, hipMemcpyAsync(d_pool, alt_pool, alt_pool_len, hipMemcpyHostToDevice, st));
+  const int64_t *d_pos = (const int64_t *)v.pos.p, *d_oplen = (const int64_t *)v.oplen.p;
+  const int64_t *d_aoff = (const int64_t *)v.aoff.p, *d_alen = (const int64_t *)v.alen.p;
+  const uint8_t *d_op = (const uint8_t *)v.op.p, *d_pool = (const uint8_t *)v.pool.p;
 
   // --- scratch: anchor(6) accepted(7) ref_before(8) node src(9) piece_off(10) small(d_small) -----------------
   MH_TRY(ensure(ctx, ctx->s[6], nv));

@@ -22,6 +22,7 @@ class Engine:
     self.device = device
     self._regions = {}   # ri -> region tuple (contig uploaded)
     self._haps = {}      # (ri, cpy) -> (slot, n_nodes, p_min, p_max)
+    self._vsets = {}     # (ri, cpy) -> resident variant set id (upload_variants)
 
   def close(self):
     self.ctx.close()
@@ -30,14 +31,28 @@ class Engine:
     self.ctx.upload_contig(ri, ref_seq)
     self._regions[ri] = region
 
+  def upload_variants(self, ri, cpy, soa):
+    """Keep (ri, cpy)'s variants in HBM: later haplotype builds of that copy splice from the device copy."""
+    vset = ri * self.SLOTS_PER_REGION + cpy
+    self.ctx.upload_variants(vset, soa)
+    self._vsets[(ri, cpy)] = vset
+
   def haplotype(self, ri, cpy, soa):
     key = (ri, cpy)
     if key not in self._haps:
       region = self._regions[ri]
       slot = ri * self.SLOTS_PER_REGION + cpy
-      n_nodes, p_min, p_max = self.ctx.build_haplotype(slot, ri, region[1] + 1, soa)
+      if key in self._vsets:
+        n_nodes, p_min, p_max = self.ctx.build_haplotype_vset(slot, ri, region[1] + 1, self._vsets[key])
+      else:
+        n_nodes, p_min, p_max = self.ctx.build_haplotype(slot, ri, region[1] + 1, soa)
       self._haps[key] = (slot, n_nodes, p_min, p_max)
     return self._haps[key]
+
+  def drop_variants(self):
+    for vset in self._vsets.values():
+      self.ctx.release_variants(vset)
+    self._vsets.clear()
 
   def drop_haplotypes(self):
     for slot, *_ in self._haps.values():

@@ -281,6 +281,57 @@ def test_batched_units_vs_oracle(native):
   assert fix <= 1
 
 
+def test_resident_variants_and_buffer_reuse(native):
+  """Haplotypes spliced from resident variant sets (mh_upload_variants) equal the host-array path, and rebuilding
+  after a drop (the released buffers are reused, holding another copy's bytes) gives the same nodes, bytes and
+  FASTQ."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  L = 12_000_000
+  seq = synth.contig(L, 11)
+  copies = synth.copies_soa(synth.variants(seq, 12))
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('1', 0, L), seq)
+
+    def run(order):
+      out = {}
+      for cpy in order:
+        n, kept, b1, b2 = eng.run_unit(0, 0, cpy, 777 + cpy, copies[cpy], p, 150, mdl['cum_tlen'], 'SYN')
+        slot, n_nodes, _, _ = eng.haplotype(0, cpy, copies[cpy])
+        out[cpy] = (eng.ctx.get_nodes(slot, n_nodes), eng.ctx.fetch_output(0, b1, 0, b2))
+        eng.ctx.reset_output()
+      eng.drop_haplotypes()
+      return out
+
+    host = run([0, 1])
+    for cpy in (0, 1):
+      eng.upload_variants(0, cpy, copies[cpy])
+    dev = run([1, 0])
+    dev2 = run([0, 1])
+    with pytest.raises(_native.NativeError, match='unknown variant set'):
+      eng.ctx.build_haplotype_vset(5, 0, 1, 99)
+    bad = dict(copies[0])
+    bad['op'] = bad['op'].copy()
+    bad['op'][0] = ord('Q')
+    with pytest.raises(ValueError, match='Complex variants'):
+      eng.ctx.upload_variants(98, bad)
+    eng.drop_variants()
+  finally:
+    eng.close()
+  for cpy in (0, 1):
+    (ps, pr, op, ol, hap), (d1, d2) = host[cpy]
+    for other in (dev[cpy], dev2[cpy]):
+      (ps2, pr2, op2, ol2, hap2), (e1, e2) = other
+      assert np.array_equal(ps, ps2) and np.array_equal(pr, pr2) and np.array_equal(op, op2)
+      assert np.array_equal(ol, ol2)
+      G.check_same(hap, hap2, 'hap copy {}'.format(cpy))
+      G.check_same(d1, e1, 'fastq1 copy {}'.format(cpy))
+      G.check_same(d2, e2, 'fastq2 copy {}'.format(cpy))
+
+
 # ---- size-independent properties at full chromosome scale -------------------------------------------------------
 def test_chr1_scale_properties(native):
   """One chr1-sized unit (249 Mbp): every record parses, POS/CIGAR are consistent with the sequence length, every
