@@ -990,7 +990,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   stage_begin(ctx, "emit");
   MH_TRY(ensure(ctx, ctx->s[14], sizeof(Rec) * m));
   MH_TRY(ensure(ctx, ctx->s[15], sizeof(E3) * (m + 1)));
-  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(E3) * scan_partials_count(m + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   char *small = (char *)ctx->d_small.p;
   E3 *tot = (E3 *)small;                 // [0, 24)
@@ -1017,8 +1017,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");
-  HIPCHK(ctx, device_scan<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, OpSum{}, E3{0, 0, 0},
-                              (E3 *)ctx->scan_partials.p, tot));
+  HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, ctx->scan_partials.p, tot));
   stage_end(ctx);
   E3 ht;
   int32_t hm4[4] = {0, 0, 0, 0};   // max record length + 20, err, overflow, max slot bytes

@@ -110,7 +110,7 @@ struct mh_ctx {
 
   // MT19937 jump polynomials on the device (x^(k * SEG_WORDS) mod P, k < jump_k)
   mh::DevBuf jump_polys;
-  int64_t jump_k = 0;
+  int64_t jump_k = 0, jump_seg = 0;
   int64_t fixups = 0;   // units redone on the exact fallback path
   std::map<int32_t, mh::VarSet> vsets;   // resident variant sets (mh_upload_variants); id -1: mh_build_haplotype's
   std::vector<mh::Hap> hap_spare;   // released haplotypes' buffers, reused by the next build (no hipMalloc/hipFree)

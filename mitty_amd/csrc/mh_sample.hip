@@ -40,7 +40,12 @@ void jump_poly_words(uint64_t L, int64_t k, uint32_t *out624);
 namespace {
 
 constexpr uint32_t MT_UP = 0x80000000u, MT_LO = 0x7fffffffu, MT_A = 0x9908b0dfu;
-constexpr int64_t SEG_WORDS = 624 * 320;     // outputs per segment
+constexpr int64_t SEG_WORDS_DEFAULT = 624 * 640;   // outputs per segment (fewer, longer segments: the jump is the cost)
+// MH_SEG_TWISTS (experiments): segment length in 624-word twists
+static int64_t seg_words() {
+  static const int64_t w = getenv("MH_SEG_TWISTS") ? 624 * std::max(1, atoi(getenv("MH_SEG_TWISTS"))) : SEG_WORDS_DEFAULT;
+  return w;
+}
 constexpr int EXT_WORDS = 624 * 33;          // x_0 .. x_20591 >= 19936 + 623
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -106,22 +111,29 @@ struct SegJob {
 
 constexpr int CB_WORDS = 2048;   // circular window of the extended sequence x_i (jump), then the two twist states
 constexpr int CB_MASK = CB_WORDS - 1;
+constexpr int JW = 208;          // jump lanes: lane w accumulates state words w, w + 208, w + 416
+constexpr int CB_ZERO = 2 * CB_WORDS;   // 624 zero words: the target of a batch's unused bit slots
 
 // The jump W_J[w] = XOR over set bits k of g of x_{k+w} walks the polynomial's bits in increasing k, so x is
-// generated 624 words at a time into a 2048-word circular window just ahead of the bits that need it (10.5 KB of
-// LDS instead of 82 KB: eight workgroups per CU instead of one).
+// generated 624 words at a time into a 2048-word circular window just ahead of the bits that need it.  The window
+// is stored twice (slot s and s + 2048), so x_{k+w}, x_{k+w+208}, x_{k+w+416} sit at (k mod 2048) + w + {0, 208,
+// 416} with no wrap: one address add per set bit (the three reads use immediate offsets), and a batch's unused
+// bit slots read a zero block instead of being masked out.  26 KB of LDS.
 __global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys, int dbg) {
-  __shared__ uint32_t cb[CB_WORDS];
+  __shared__ uint32_t cb[2 * CB_WORDS + 624];
   __shared__ uint32_t gp[624];
   const SegJob job = jobs[blockIdx.x];
   const int t = threadIdx.x;
   mt_seed_lds(cb, job.seed);   // x_0 .. x_623
   if (job.k > 0 && !(dbg & 1)) {
     const uint32_t *g = polys + (int64_t)job.k * 624;
-    for (int i = t; i < 624; i += 256) gp[i] = g[i];
+    for (int i = t; i < 624; i += 256) {
+      gp[i] = g[i];
+      cb[CB_WORDS + i] = cb[i];   // mirror of x_0 .. x_623
+      cb[CB_ZERO + i] = 0u;
+    }
     lds_barrier();
-    const int w0 = t, w1 = t + 256, w2 = t + 512;
-    const bool h2 = w2 < 624;
+    const int w = t < JW ? t : 0;   // lanes >= 208 compute lane 0's words and discard them
     uint32_t a0 = 0, a1 = 0, a2 = 0;
     int32_t G = 624;   // x_0 .. x_{G-1} exist (the last CB_WORDS of them in the window)
     for (int pw = 0; pw < 624; pw++) {
@@ -129,54 +141,49 @@ __global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const u
       // bits kb .. kb+31 read x up to x_{kb+31+623}.  Overwritten slots hold x_{G-2048} .. x_{G-1425}, older than
       // any x still needed (>= x_{kb} >= x_{G-654}) by this or a lagging wave (>= x_{G-1278}).
       while (G <= kb + 31 + 623) {   // G and kb are uniform: every wave takes the same barriers
-        if (t < 227) {
-          const int i = G + t;
-          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
+#pragma unroll
+        for (int ph = 0; ph < 3; ph++) {
+          if (t < (ph < 2 ? 227 : 170)) {
+            const int i = G + 227 * ph + t;
+            const uint32_t v = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
+            cb[i & CB_MASK] = v;
+            cb[(i & CB_MASK) + CB_WORDS] = v;
+          }
+          lds_barrier();
         }
-        lds_barrier();
-        if (t < 227) {
-          const int i = G + 227 + t;
-          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
-        }
-        lds_barrier();
-        if (t < 170) {
-          const int i = G + 454 + t;
-          cb[i & CB_MASK] = cb[(i - 227) & CB_MASK] ^ mt_mix(cb[(i - 624) & CB_MASK], cb[(i - 623) & CB_MASK]);
-        }
-        lds_barrier();
         G += 624;
       }
       uint32_t m = gp[pw];
-      while (m) {   // eight set bits per step: 24 independent LDS reads in flight
-        int kk[8];
-        uint32_t v0[8], v1[8], v2[8];
-        int nb = 0;
+      const int base = kb & CB_MASK;
+      while (m) {   // eight set bits per batch: 24 independent LDS reads in flight
+        int off[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          kk[u] = kb + (m ? __builtin_ctz(m) : 0);
-          nb += m != 0;
+          off[u] = m ? base + __builtin_ctz(m) : CB_ZERO;
           m &= m - 1;
         }
+        uint32_t v0[8], v1[8], v2[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          v0[u] = cb[(kk[u] + w0) & CB_MASK];
-          v1[u] = cb[(kk[u] + w1) & CB_MASK];
-          v2[u] = h2 ? cb[(kk[u] + w2) & CB_MASK] : 0u;
+          const uint32_t *q = cb + off[u] + w;
+          v0[u] = q[0];
+          v1[u] = q[JW];
+          v2[u] = q[2 * JW];
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          if (u < nb) {
-            a0 ^= v0[u];
-            a1 ^= v1[u];
-            a2 ^= v2[u];
-          }
+          a0 ^= v0[u];
+          a1 ^= v1[u];
+          a2 ^= v2[u];
         }
       }
     }
     lds_barrier();
-    cb[w0] = a0;
-    cb[w1] = a1;
-    if (h2) cb[w2] = a2;
+    if (t < JW) {
+      cb[t] = a0;
+      cb[t + JW] = a1;
+      cb[t + 2 * JW] = a2;
+    }
     lds_barrier();
   }
   uint32_t *st0 = cb, *st1 = cb + 624;
@@ -887,7 +894,8 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   HIPCHK(ctx, hipMemcpyAsync(d_ndraw, ndraw.data(), 8 * U, hipMemcpyHostToDevice, st));
   const unsigned grid = (unsigned)std::min<int64_t>(C, 4096);
   // pass 1 over every chunk, then passes over the queued chunks, PASS_BATCH per host check
-  constexpr int PASS_BATCH = 8, MAX_PASSES = 64;
+  constexpr int MAX_PASSES = 64;
+  const int PASS_BATCH = getenv("MH_DEC_BATCH") ? std::max(1, atoi(getenv("MH_DEC_BATCH"))) : 8;   // diagnostics
   hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
                      (const int32_t *)nullptr, (const int32_t *)nullptr, (int32_t)C, (const int64_t *)d_s0, d_count,
                      d_margin);
@@ -950,8 +958,8 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
 
   stage_begin(ctx, "sample_geometric_scan");
   if (!exact) {
-    HIPCHK(ctx, device_scan<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1}, OpSum{},
-                                     (int64_t)0, (int64_t *)ctx->scan_partials.p, tot));
+    HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1},
+                                         ctx->scan_partials.p, tot));
   } else {
     int64_t *g = (int64_t *)ctx->s[12].p;
     uint32_t nflag = 0;
@@ -1002,10 +1010,10 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   hipLaunchKernelGGL(k_tlen, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 8 * n_tlen, st, n, w_tlen, d_cum, n_tlen,
                      (int64_t)rlen, u.p_max, ts_use, te, keep);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, device_scan<int64_t>(st, n, LoadKeep{keep},
-                                   StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p, (int64_t *)u.out->pos1.p,
-                                                (int64_t)rlen},
-                                   OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p, d_m));
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
+                                       StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p,
+                                                    (int64_t *)u.out->pos1.p, (int64_t)rlen},
+                                       ctx->scan_partials.p, d_m));
   hipLaunchKernelGGL(k_file_order, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const int64_t *)d_m,
                      w_fo, (int8_t *)u.out->fo0.p);
   HIPCHK(ctx, hipGetLastError());
@@ -1075,7 +1083,8 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 64));
   MH_TRY(ensure(ctx, ctx->s[1], 64 * (size_t)n_units + 64));          // per-unit m, flags, decode status
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
-  MH_TRY(ensure(ctx, ctx->scan_partials, 16 * scan_partials_count(nn + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->scan_partials, std::max<size_t>(16 * scan_partials_count(nn + 1) + 64,
+                                                           scan_lb_scratch_bytes<int64_t>(nn + 1))));
   uint32_t *words = (uint32_t *)ctx->s[0].p, *jall = (uint32_t *)ctx->s[3].p;
   double *d_cum = (double *)ctx->s[13].p;
   int64_t *d_m = (int64_t *)ctx->s[1].p;                                // [n_units]
@@ -1090,6 +1099,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     std::vector<SegJob> jobs;
     std::vector<DecJob> dec;
     int64_t kmax = 0;
+    const int64_t SEG_WORDS = seg_words();
     auto add_stream = [&](uint32_t *out, int64_t count, uint32_t seed) {
       for (int64_t k = 0; k * SEG_WORDS < count; k++) {
         int64_t s0 = k * SEG_WORDS;
@@ -1108,13 +1118,14 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     }
     if (!jobs.empty()) {
       // jump polynomials x^(k * SEG_WORDS) mod P, k = 0..kmax (cached on host and device)
-      if (ctx->jump_k < kmax + 1) {
+      if (ctx->jump_k < kmax + 1 || ctx->jump_seg != SEG_WORDS) {
         std::vector<uint32_t> polys((size_t)(kmax + 1) * 624);
         for (int64_t k = 0; k <= kmax; k++) jump::jump_poly_words((uint64_t)SEG_WORDS, k, polys.data() + k * 624);
         MH_TRY(ensure(ctx, ctx->jump_polys, 4 * polys.size()));
         HIPCHK(ctx, hipMemcpyAsync(ctx->jump_polys.p, polys.data(), 4 * polys.size(), hipMemcpyHostToDevice, st));
         HIPCHK(ctx, hipStreamSynchronize(st));
         ctx->jump_k = kmax + 1;
+        ctx->jump_seg = SEG_WORDS;
       }
       MH_TRY(ensure(ctx, ctx->s[2], sizeof(SegJob) * jobs.size() + sizeof(DecJob) * dec.size() + 64));
       SegJob *d_jobs = (SegJob *)ctx->s[2].p;

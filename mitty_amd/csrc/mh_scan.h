@@ -144,6 +144,176 @@ inline hipError_t device_reduce(hipStream_t st, int64_t n, Load load, Op op, T i
   return hipGetLastError();
 }
 
+// ---- single-pass scan (decoupled look-back) for sums of non-negative int64 fields ------------------------------
+// One kernel reads every element once: tiles are taken in launch order from an atomic ticket (so every tile a tile
+// waits for is already running), each publishes its aggregate, then its inclusive prefix once the look-back over
+// its predecessors (one wave, 64 tiles per step) finds an inclusive one.  Status words pack the value with a
+// 2-bit flag (1 = aggregate, 2 = inclusive) and travel as 64-bit agent-scope atomics, so no fences are needed.
+// T must be a struct of int64 fields, each summed, each in [0, 2^61).
+constexpr int LB_ITEMS = 8;
+constexpr int LB_TILE = SCAN_THREADS * LB_ITEMS;
+
+template <typename T>
+struct LbFields {
+  static constexpr int K = sizeof(T) / 8;
+  static_assert(sizeof(T) % 8 == 0, "look-back scan element must be int64 fields");
+  __device__ static int64_t get(const T &v, int k) { return reinterpret_cast<const int64_t *>(&v)[k]; }
+  __device__ static void set(T &v, int k, int64_t x) { reinterpret_cast<int64_t *>(&v)[k] = x; }
+};
+
+template <typename T>
+__device__ __forceinline__ T shfl_xor_t(const T &v, int d) {
+  union U {
+    T t;
+    int i[sizeof(T) / 4];
+    __device__ U() {}
+  } a, b;
+  a.t = v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) b.i[k] = __shfl_xor(a.i[k], d, 64);
+  return b.t;
+}
+
+template <typename T>
+__device__ __forceinline__ T shfl_idx_t(const T &v, int src) {
+  union U {
+    T t;
+    int i[sizeof(T) / 4];
+    __device__ U() {}
+  } a, b;
+  a.t = v;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) b.i[k] = __shfl(a.i[k], src, 64);
+  return b.t;
+}
+
+__device__ __forceinline__ void lb_put(uint64_t *w, int64_t v, uint64_t flag) {
+  __hip_atomic_store(w, ((uint64_t)v << 2) | flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_get(const uint64_t *w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// scratch: [ticket (64 B)] [aggregate words K x nt] [inclusive words K x nt], zeroed before the launch
+template <typename T, typename Load, typename Store>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, Store store, uint64_t *scratch,
+                                                         int64_t nt, T *total) {
+  using F = LbFields<T>;
+  constexpr int K = F::K;
+  __shared__ T lds_w[SCAN_THREADS / 64];
+  __shared__ T s_prefix;
+  __shared__ int64_t s_tile;
+  uint32_t *ticket = (uint32_t *)scratch;
+  uint64_t *agg = scratch + 8, *inc = agg + (size_t)K * nt;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  // wave w owns elements [tile * LB_TILE + w * 64 * LB_ITEMS, +64 * LB_ITEMS): item k of lane l is element
+  // w * 64 * LB_ITEMS + 64 k + l (coalesced loads and stores), scanned with one wave scan per item
+  const int64_t base = tile * LB_TILE + (int64_t)wave * 64 * LB_ITEMS + lane;
+  T v[LB_ITEMS];
+  T carry{};
+#pragma unroll
+  for (int k = 0; k < LB_ITEMS; k++) {
+    const int64_t i = base + 64 * k;
+    T x = i < n ? load(i) : T{};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const T o = shfl_up_t(x, d);
+      if (lane >= d) x = o + x;
+    }
+    v[k] = carry + x;                // inclusive prefix within the wave's segment
+    carry = shfl_idx_t(v[k], 63);    // running total of the segment
+  }
+  if (lane == 0) lds_w[wave] = carry;      // the wave segment's total
+  __syncthreads();
+  T pre{}, tot{};
+#pragma unroll
+  for (int w = 0; w < SCAN_THREADS / 64; w++) {
+    if (w < wave) pre = pre + lds_w[w];
+    tot = tot + lds_w[w];
+  }
+  // publish and look back (wave 0)
+  if (wave == 0) {
+    T prefix{};
+    if (tile == 0) {
+      if (lane < K) lb_put(inc + (size_t)lane * nt, F::get(tot, lane), 2u);
+    } else {
+      if (lane < K) lb_put(agg + (size_t)lane * nt + tile, F::get(tot, lane), 1u);
+      for (int64_t j = tile - 1;; j -= 64) {
+        const int64_t jj = j - lane;   // lane l looks at tile j - l (jj < 0: past tile 0, never needed)
+        bool is_inc = jj < 0, ok = jj < 0;
+        T val{};
+        while (!ok) {
+          bool all_inc = true, all_agg = true;
+          int64_t xi[K], xa[K];
+#pragma unroll
+          for (int k = 0; k < K; k++) {
+            const uint64_t wi = lb_get(inc + (size_t)k * nt + jj);
+            const uint64_t wa = lb_get(agg + (size_t)k * nt + jj);
+            all_inc &= (wi & 3u) == 2u;
+            all_agg &= (wa & 3u) == 1u;
+            xi[k] = (int64_t)(wi >> 2);
+            xa[k] = (int64_t)(wa >> 2);
+          }
+          if (all_inc || all_agg) {
+            ok = true;
+            is_inc = all_inc;
+#pragma unroll
+            for (int k = 0; k < K; k++) F::set(val, k, all_inc ? xi[k] : xa[k]);
+          } else {
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const uint64_t bal = __ballot(is_inc);
+        const int first = bal ? __builtin_ctzll(bal) : 64;   // nearest tile with an inclusive prefix
+        if (lane > first || jj < 0) val = T{};
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) val = val + shfl_xor_t(val, d);
+        prefix = prefix + val;
+        if (first < 64) break;
+      }
+      const T mine = prefix + tot;
+      if (lane < K) lb_put(inc + (size_t)lane * nt + tile, F::get(mine, lane), 2u);
+    }
+    if (lane == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  const T off = s_prefix + pre;
+  // element exclusive prefix = the previous lane's inclusive one (lane 0: the previous item's last lane)
+  T prev = off;
+#pragma unroll
+  for (int k = 0; k < LB_ITEMS; k++) {
+    const int64_t i = base + 64 * k;
+    const T incl = off + v[k];
+    T ex = shfl_up_t(incl, 1);
+    if (lane == 0) ex = prev;
+    prev = shfl_idx_t(incl, 63);
+    if (i < n) store(i, incl, ex);
+  }
+  if (tile == nt - 1 && tid == SCAN_THREADS - 1) *total = off + v[LB_ITEMS - 1];
+}
+
+template <typename T>
+inline size_t scan_lb_scratch_bytes(int64_t n) {
+  const int64_t nt = (n + LB_TILE - 1) / LB_TILE;
+  return 64 + 2 * sizeof(T) * (size_t)(nt < 1 ? 1 : nt) + 64;
+}
+
+// Host launcher: exclusive/inclusive sums through Store, grand total to *total.  `scratch` holds
+// scan_lb_scratch_bytes<T>(n) bytes of device memory.
+template <typename T, typename Load, typename Store>
+inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store store, void *scratch, T *total) {
+  int64_t nt = (n + LB_TILE - 1) / LB_TILE;
+  if (nt < 1) nt = 1;
+  hipError_t e = hipMemsetAsync(scratch, 0, scan_lb_scratch_bytes<T>(n), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_scan_lb<T, Load, Store>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, st, n, load, store,
+                     (uint64_t *)scratch, nt, total);
+  return hipGetLastError();
+}
+
 inline int64_t scan_partials_count(int64_t n) {
   int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   return nb < 1 ? 1 : nb;

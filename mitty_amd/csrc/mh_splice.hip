@@ -464,7 +464,8 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   int64_t nchunks = (hap_len + 1 + NCHUNK - 1) / NCHUNK;
   RunCnt *rtot = (RunCnt *)(small + 128);
   // count first (sizes the run arrays), then the same scan again to write them
-  MH_TRY(ensure(ctx, ctx->scan_partials, 16 * scan_partials_count(nchunks) + 64));
+  MH_TRY(ensure(ctx, ctx->scan_partials, std::max<size_t>(16 * scan_partials_count(nchunks) + 64,
+                                                           scan_lb_scratch_bytes<RunCnt>(nchunks))));
   HIPCHK(ctx, device_reduce<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len}, OpSum{}, RunCnt{0, 0},
                                     (RunCnt *)ctx->scan_partials.p, rtot));
   RunCnt hr;
@@ -474,10 +475,10 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   MH_TRY(ensure(ctx, h.nrun_s, 8 * (hr.starts + 1)));
   MH_TRY(ensure(ctx, h.nrun_e, 8 * (hr.ends + 1)));
   if (hr.starts > 0) {
-    HIPCHK(ctx, device_scan<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len},
-                                    StoreRuns{(const uint8_t *)h.hap.p, hap_len, (int64_t *)h.nrun_s.p,
-                                              (int64_t *)h.nrun_e.p},
-                                    OpSum{}, RunCnt{0, 0}, (RunCnt *)ctx->scan_partials.p, rtot));
+    HIPCHK(ctx, device_scan_sum<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len},
+                                        StoreRuns{(const uint8_t *)h.hap.p, hap_len, (int64_t *)h.nrun_s.p,
+                                                  (int64_t *)h.nrun_e.p},
+                                        ctx->scan_partials.p, rtot));
   }
   stage_end(ctx);
 
