@@ -42,7 +42,7 @@ struct HapView {
   const uint8_t *hap;
   const uint8_t *rc;    // reverse complement of hap (str.maketrans('ATCGN', 'TAGCN') + [::-1]), same length
   const int32_t *bkt;   // node-search buckets (Hap::bkt)
-  const Node32 *nd;     // AoS node copy (Hap::nd)
+  const Node16 *nd;     // packed node copy (Hap::nd)
   int64_t n_bkt;
   int64_t p_min, hap_len;
   const int64_t *nrs, *nre;
@@ -67,9 +67,17 @@ __device__ __forceinline__ int64_t node_upper(const HapView &h, int64_t x) {
   int64_t lo = h.bkt[k], hi = k + 1 < h.n_bkt ? h.bkt[k + 1] : h.n_nodes;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (h.nd[mid].key <= x) lo = mid + 1; else hi = mid;
+    if (h.nd[mid].key() <= x) lo = mid + 1; else hi = mid;
   }
   return lo;
+}
+
+// searchsorted(keys, x, 'right') - 1 from a node k0 whose key is <= x: nodes average ~770 bp, so the end node of a
+// read is usually k0 or the next one (adjacent 32-byte records) — no second bucket search.
+__device__ __forceinline__ int64_t node_walk(const HapView &h, int64_t k0, int64_t x) {
+  int64_t k = k0;
+  while (k + 1 < h.n_nodes && h.nd[k + 1].key() <= x) k++;
+  return k;
 }
 
 __device__ __forceinline__ int ndig_u(uint64_t v) {
@@ -109,33 +117,35 @@ struct ReadInfo {
   bool special;
 };
 
-__device__ __forceinline__ int64_t node_count(const Node32 &n, int64_t p, int64_t l) {
-  if (n.op == 'D') return n.oplen;
-  int64_t hi = p + l - n.ps < n.oplen ? p + l - n.ps : n.oplen;
-  int64_t lo = p - n.ps > 0 ? p - n.ps : 0;
+__device__ __forceinline__ int64_t node_count(const Node16 &n, int64_t p, int64_t l) {
+  const int64_t ol = n.oplen(), ps = n.ps();
+  if (n.code() == 3) return ol;
+  int64_t hi = p + l - ps < ol ? p + l - ps : ol;
+  int64_t lo = p - ps > 0 ? p - ps : 0;
   return hi - lo;
 }
 __device__ __forceinline__ int64_t node_count(const HapView &h, int64_t k, int64_t p, int64_t l) {
   return node_count(h.nd[k], p, l);
 }
-__device__ __forceinline__ int64_t node_v(const Node32 &n) {
-  return n.op == 'X' ? 0 : (n.op == 'I' ? n.oplen : -n.oplen);
+__device__ __forceinline__ int64_t node_v(const Node16 &n) {
+  const int c = n.code();
+  return c == 1 ? 0 : (c == 2 ? n.oplen() : -n.oplen());
 }
 __device__ __forceinline__ int64_t node_v(const HapView &h, int64_t k) { return node_v(h.nd[k]); }
 
-// POS / special-CIGAR / sequence range of a read whose start and end nodes are known (rpc.py:144-160).
-__device__ __forceinline__ void read_place(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
+// POS / special-CIGAR / sequence range of a read whose start and end nodes are known (rpc.py:144-160); n0 is
+// node r.n0.
+__device__ __forceinline__ void read_place(const HapView &h, const Node16 &n0, int64_t p, int64_t l, ReadInfo &r) {
   r.special = false;
-  const Node32 n0 = h.nd[r.n0];
-  if (n0.op == 'I') {
+  if (n0.code() == 2) {   // 'I'
     if (r.n0 == r.n1) {
       r.special = true;
-      r.pos = n0.pr - 1;
+      r.pos = n0.pr() - 1;
     } else {
-      r.pos = n0.pr;
+      r.pos = n0.pr();
     }
   } else {
-    r.pos = p - n0.ps + n0.pr;
+    r.pos = p - n0.ps() + n0.pr();
   }
   int64_t a = p - h.p_min, b = p + l - h.p_min;
   if (b > h.hap_len) b = h.hap_len;
@@ -156,7 +166,7 @@ __device__ void read_info(const HapView &h, int64_t p, int64_t l, ReadInfo &r) {
       first = false;
     }
   }
-  read_place(h, p, l, r);
+  read_place(h, h.nd[r.n0], p, l, r);
   if (r.special) cl = 1 + ndig_s(p - h.ps[r.n0]) + 1 + ndig_s(l) + 1;
   r.cigar_len = cl;
   r.vlist_len = vl;
@@ -186,6 +196,22 @@ __device__ char *write_vlist(char *d, const HapView &h, const ReadInfo &r) {
     first = false;
   }
   return d;
+}
+
+// Number of 'N' in hap[a, b) from n sorted runs [rs[r], re[r]) (e.g. staged in LDS), capped at 3.
+__device__ __forceinline__ int count_N_runs(const int64_t *rs, const int64_t *re, int64_t n, int64_t a, int64_t b) {
+  if (n == 0 || b <= a) return 0;
+  int64_t lo = 0, hi = n;   // first run with end > a
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (re[mid] <= a) lo = mid + 1; else hi = mid;
+  }
+  int64_t c = 0;
+  for (int64_t r = lo; r < n && rs[r] < b && c <= 2; r++) {
+    const int64_t s = rs[r] > a ? rs[r] : a, e = re[r] < b ? re[r] : b;
+    if (e > s) c += e - s;
+  }
+  return (int)(c > 3 ? 3 : c);
 }
 
 // Number of 'N' in hap[a, b), capped at 3 (the filter only needs > 2).
@@ -279,43 +305,64 @@ __device__ __forceinline__ int32_t qname_len_wo_cnt(const QFixed &q, const ReadI
 }
 
 constexpr int SLOT = 256;   // bytes per template for the reads part of the qname ("|s|pos|rlen|cigar|v,..|...")
-constexpr int MS_STG = 112;   // of which the first MS_STG bytes are staged in LDS by k_emit_measure
+constexpr int MS_STG = 64;    // of which the first MS_STG bytes are staged in LDS by k_emit_measure
+constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
-// ByteWriter for k_emit_measure: dword k goes to LDS while k < MS_STG / 4, else to the global slot (k < SLOT / 4)
+// Four ASCII digits of w < 10000, first digit in the low byte.
+__device__ __forceinline__ uint32_t ascii4(uint32_t w) {
+  const uint32_t c = (w * 5243u) >> 19, d = w - 100u * c;   // w / 100, w % 100
+  const uint32_t ct = (c * 103u) >> 10, dt = (d * 103u) >> 10;   // tens of each pair
+  return 0x30303030u | ct | ((c - 10u * ct) << 8) | (dt << 16) | ((d - 10u * dt) << 24);
+}
+
+// ByteWriter for k_emit_measure: dword k goes to LDS while k < MS_STG / 4, else to the global slot (k < SLOT / 4).
+// Bytes gather in a 64-bit accumulator and leave a dword at a time; numbers are appended up to four digits per step.
 struct SplitWriter {
   uint32_t *lds;
   uint32_t *g;
-  uint32_t acc;
+  uint64_t acc;   // nb pending bytes (< 4)
   int nb;
-  int32_t n;
+  int32_t n;      // bytes appended
+  int dw;         // dwords stored
   __device__ __forceinline__ void store(uint32_t v) {
-    const int k = (n - 1) >> 2;
+    const int k = dw++;
     if (k < MS_STG / 4) lds[k] = v;
     else if (g != nullptr && k < SLOT / 4) g[k] = v;
   }
-  __device__ __forceinline__ void put(uint8_t c) {
-    acc |= (uint32_t)c << (8 * nb);
-    n++;
-    if (++nb == 4) {
-      store(acc);
-      acc = 0;
-      nb = 0;
+  // append the low k (1..4) bytes of v
+  __device__ __forceinline__ void putk(uint32_t v, int k) {
+    acc |= (uint64_t)v << (8 * nb);
+    nb += k;
+    n += k;
+    if (nb >= 4) {
+      store((uint32_t)acc);
+      acc >>= 32;
+      nb -= 4;
     }
   }
+  __device__ __forceinline__ void put(uint8_t c) { putk(c, 1); }
   __device__ __forceinline__ void flush() {
-    if (nb) store(acc);
+    if (nb) store((uint32_t)acc);
   }
   __device__ __forceinline__ void put_u(uint64_t v) {
     if (v <= 0xffffffffull) {
-      uint32_t x = (uint32_t)v;
-      uint64_t bcd = 0;
-      int nd = 0;
-      do {
-        bcd |= (uint64_t)(x % 10u) << (4 * nd);
-        x /= 10u;
-        nd++;
-      } while (x);
-      for (int i = nd - 1; i >= 0; i--) put((uint8_t)('0' + ((bcd >> (4 * i)) & 15)));
+      const uint32_t x = (uint32_t)v;
+      const int nd = ndig_u(x);
+      const uint32_t hi = x / 100000000u, lo = x - hi * 100000000u;
+      const uint32_t a = (uint32_t)(((uint64_t)lo * 109951163ull) >> 40);   // lo / 10000
+      const uint32_t L0 = ascii4(a), L1 = ascii4(lo - 10000u * a);          // the 8 low digits
+      if (nd > 8) {
+        if (hi >= 10u) putk(0x3030u | (hi / 10u) | ((hi % 10u) << 8), 2);
+        else putk(0x30u | hi, 1);
+        putk(L0, 4);
+        putk(L1, 4);
+      } else if (nd > 4) {
+        const int s = 8 - nd;   // leading zeros of the 8-digit string
+        putk(L0 >> (8 * s), 4 - s);
+        putk(L1, 4);
+      } else {
+        putk(L1 >> (8 * (4 - nd)), nd);
+      }
     } else {
       char tmp[24];
       int nd = 0;
@@ -334,28 +381,44 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
                                                       int32_t *overflow, int32_t dbg) {
   // the reads part is formatted into LDS (bytes past MS_STG straight to the slot) and leaves in coalesced 16-byte
   // chunks after the barrier
-  __shared__ uint32_t stg[256][MS_STG / 4];
+  __shared__ uint32_t stg[256][MS_STG / 4 + 1];   // odd row stride: the per-thread rows spread over all banks
   __shared__ int32_t s_n[256];
+  __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
+  const bool runs_lds = h.n_runs <= MS_RUNS;
+  if (runs_lds)
+    for (int i = threadIdx.x; i < h.n_runs; i += 256) {
+      s_rs[i] = h.nrs[i];
+      s_re[i] = h.nre[i];
+    }
+  __syncthreads();
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int32_t local_max = 0;
   int32_t nbytes = 0;
   if (t < m) {
     ReadInfo r[2];
+    Node16 nn0[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
 #pragma unroll
     for (int s = 0; s < 2; s++) {   // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range
       r[s].n0 = node_upper(h, p[s]) - 1;
-      r[s].n1 = node_upper(h, p[s] + rlen - 1) - 1;
-      read_place(h, p[s], rlen, r[s]);
+      r[s].n1 = node_walk(h, r[s].n0, p[s] + rlen - 1);
+      nn0[s] = h.nd[r[s].n0];
+      read_place(h, nn0[s], p[s], rlen, r[s]);
     }
-    const int keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
-                     count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    int keep;
+    if (runs_lds) {
+      keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+             count_N_runs(s_rs, s_re, h.n_runs, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    } else {
+      keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+             count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
       // the reads part of the qname, in file order (readgenerate.py:223-225), and the qname's '\n': formatted into
       // the slot while it fits, counted either way (its length sizes the records)
-      SplitWriter bw{stg[threadIdx.x], slots && !(dbg & 1) ? (uint32_t *)(slots + t * SLOT) : nullptr, 0u, 0, 0};
+      SplitWriter bw{stg[threadIdx.x], slots && !(dbg & 1) ? (uint32_t *)(slots + t * SLOT) : nullptr, 0ull, 0, 0, 0};
       for (int fr = 0; fr < 2 && !(dbg & 2); fr++) {
         const int s = fr == f0 ? 0 : 1;
         const ReadInfo &ri = r[s];
@@ -364,19 +427,19 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
         bw.put('|'); bw.put_s(rlen);
         bw.put('|');
         if (ri.special) {
-          bw.put('>'); bw.put_s(p[s] - h.nd[ri.n0].ps); bw.put(':'); bw.put_s(rlen); bw.put('I');
+          bw.put('>'); bw.put_s(p[s] - nn0[s].ps()); bw.put(':'); bw.put_s(rlen); bw.put('I');
         } else {
           for (int64_t k = ri.n0; k <= ri.n1; k++) {
-            const Node32 n = h.nd[k];
+            const Node16 n = k == ri.n0 ? nn0[s] : h.nd[k];
             bw.put_s(node_count(n, p[s], rlen));
-            bw.put(n.op);
+            bw.put(n.op());
           }
         }
         bw.put('|');
         bool first = true;
         for (int64_t k = ri.n0; k <= ri.n1; k++) {
-          const Node32 n = h.nd[k];
-          if (n.op == '=') continue;
+          const Node16 n = k == ri.n0 ? nn0[s] : h.nd[k];
+          if (n.code() == 0) continue;
           if (!first) bw.put(',');
           bw.put_s(node_v(n));
           first = false;
@@ -420,7 +483,8 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   for (int it = threadIdx.x; it < 256 * CH; it += 256) {
     const int j = it / CH, c = it - j * CH;
     if (16 * c >= s_n[j]) continue;
-    *(uint4 *)(slots + (tb + j) * SLOT + 16 * c) = *(const uint4 *)&stg[j][4 * c];
+    const uint32_t *s = &stg[j][4 * c];
+    *(uint4 *)(slots + (tb + j) * SLOT + 16 * c) = make_uint4(s[0], s[1], s[2], s[3]);
   }
 }
 
@@ -540,7 +604,7 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
         for (int s = 0; s < 2; s++) {
           r[s].n0 = rc.n0[s];
           r[s].n1 = rc.n1[s];
-          read_place(h, p[s], rlen, r[s]);
+          read_place(h, h.nd[r[s].n0], p[s], rlen, r[s]);
           mt.seq_len[s] = r[s].seq_len;
           mt.win[s] = (threadIdx.x * 2 + s) * win_stride + (int)(r[s].hap_a & 15);
         }
@@ -938,7 +1002,7 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
                  (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
-                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, (const Node32 *)h.nd.p, h.n_bkt, h.p_min,
+                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, (const Node16 *)h.nd.p, h.n_bkt, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 

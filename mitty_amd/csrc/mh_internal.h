@@ -34,11 +34,17 @@ struct DevBuf {
 
 // Haplotype (one chromosome copy of one BED region) resident on the device.  SURVEY.md §8(a) A9.
 // Sample coordinates are the reference's 1-based `ps`; hap[k] is the base at sample position p_min + k.
-// One node in 32 bytes (emission's random node lookups touch one sector instead of five SoA arrays).
-struct Node32 {
-  int64_t key, ps, pr;   // search key (ps + 1 for 'D'), sample / reference positions (rpc.py:5-20)
-  int32_t oplen;
-  uint8_t op, pad[3];
+// One node in 16 bytes (emission's random node lookups are one 16-byte load instead of five SoA arrays):
+//   a = ps | op code << 40 | (oplen mod 2^22) << 42,   b = pr | (oplen >> 22) << 40
+// op codes 0 '=', 1 'X', 2 'I', 3 'D'; positions < 2^40, oplen < 2^46 (k_node_pack flags anything larger).
+struct Node16 {
+  uint64_t a, b;
+  __host__ __device__ int64_t ps() const { return (int64_t)(a & 0xffffffffffull); }
+  __host__ __device__ int64_t pr() const { return (int64_t)(b & 0xffffffffffull); }
+  __host__ __device__ int code() const { return (int)((a >> 40) & 3u); }
+  __host__ __device__ uint8_t op() const { return (uint8_t)(0x4449583Du >> (8 * code())); }   // '=' 'X' 'I' 'D'
+  __host__ __device__ int64_t oplen() const { return (int64_t)((a >> 42) | ((b >> 40) << 22)); }
+  __host__ __device__ int64_t key() const { return ps() + (code() == 3); }   // 'D': ps + 1 (rpc.py:41-45)
 };
 
 constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
@@ -46,7 +52,7 @@ constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes
 struct Hap {
   bool valid = false;
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
-  DevBuf nd;    // Node32 copy of the node arrays
+  DevBuf nd;    // Node16 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;

@@ -864,15 +864,16 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     }
   }
   const int32_t U = (int32_t)dec.size();
+  const int32_t tile_sz = DR_TILE;
   std::vector<DecTile> tiles;
   for (int32_t u = 0; u < U; u++) {
     const int32_t ft = (int32_t)tiles.size();
-    for (int32_t b = first[u]; b < first[u + 1]; b += DR_TILE)
-      tiles.push_back(DecTile{u, b, std::min(b + DR_TILE, first[u + 1]), ft});
+    for (int32_t b = first[u]; b < first[u + 1]; b += tile_sz)
+      tiles.push_back(DecTile{u, b, std::min(b + tile_sz, first[u + 1]), ft});
   }
   const int32_t T = (int32_t)tiles.size();
   const size_t bytes = ((sizeof(ChunkJob) * C + 15) / 16) * 16 + 8 * C * 2 + 8 * U * 2 + 8 * (T + 1) +
-                       sizeof(DecTile) * (T + 1) + 4 * C * 2 + 8 * C + 256;
+                       sizeof(DecTile) * (T + 1) + 4 * C * 2 + 8 * C + 512;
   MH_TRY(ensure(ctx, ctx->dec_buf, bytes));
   char *p = (char *)ctx->dec_buf.p;
   ChunkJob *d_jobs = (ChunkJob *)p;
@@ -919,6 +920,23 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     HIPCHK(ctx, hipStreamSynchronize(st));
     if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
                                           h_ntodo, (long long)C);
+    if (getenv("MH_DEC_VERBOSE") && atoi(getenv("MH_DEC_VERBOSE")) >= 2 && h_ntodo > 0) {   // where they are
+      std::vector<int32_t> q(h_ntodo);
+      std::vector<int64_t> hs(C);
+      HIPCHK(ctx, hipMemcpy(q.data(), d_todo, 4 * (size_t)h_ntodo, hipMemcpyDeviceToHost));
+      HIPCHK(ctx, hipMemcpy(hs.data(), d_s0, 8 * (size_t)C, hipMemcpyDeviceToHost));
+      int hist[40] = {0};
+      for (int32_t c : q) {
+        int64_t s = hs[c];
+        int b2 = 0;
+        while (s > 1 && b2 < 39) { s >>= 1; b2++; }
+        hist[b2]++;
+      }
+      fprintf(stderr, "  queued by log2(start):");
+      for (int b2 = 0; b2 < 40; b2++)
+        if (hist[b2]) fprintf(stderr, " %d:%d", b2, hist[b2]);
+      fprintf(stderr, "\n");
+    }
     if (h_ntodo == 0) {   // the last pass counted nothing: the starts in s1 are the sequential ones
       conv = true;
       break;

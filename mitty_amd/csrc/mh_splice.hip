@@ -158,49 +158,117 @@ __global__ void __launch_bounds__(256) k_hap_copy(int64_t total_pieces, int64_t 
 // Haplotype bytes by output position: thread i writes hap[16i, 16i+16).  The node holding sample position x is the
 // last node whose key is <= x (the bucket table narrows the search, as in emission); 'D' nodes hold no bytes
 // (their key equals the next node's).  Bytes no node covers (possible only before the first node's bytes) are 0.
-__global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min, int64_t n_nodes, const int64_t *keys,
-                                                  const int64_t *ps, const uint8_t *nop, const int64_t *nl,
-                                                  const int64_t *src, const int32_t *bkt, int64_t n_bkt,
-                                                  const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap) {
-  const int64_t o0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-  if (o0 >= hap_len) return;
+constexpr int FILL_NODES = 512;   // nodes of one workgroup's span staged in LDS (more: searched in global memory)
+constexpr int FILL_Q = 4;         // 16-byte chunks per thread (lane-strided: stores stay coalesced)
+constexpr int64_t FILL_SPAN = 256 * 16 * FILL_Q;
+
+// One 16-byte chunk of the haplotype at output offset o0 (sample position x0): node search, then the bytes.
+__device__ __forceinline__ void hap_fill_chunk(int64_t o0, int64_t hap_len, int64_t p_min, int64_t n_nodes,
+                                               const Node16 *nd, const int64_t *src, const int32_t *bkt,
+                                               int64_t n_bkt, const uint8_t *contig, const uint8_t *alt_pool,
+                                               uint8_t *hap, bool staged, int64_t lo, int64_t cnt,
+                                               const Node16 *s_nd, const int64_t *s_src) {
   const int64_t x0 = p_min + o0;
-  int64_t kb = (x0 - p_min) >> NODE_BKT_SHIFT;
-  if (kb >= n_bkt) kb = n_bkt - 1;
-  int64_t lo = bkt[kb], hi = kb + 1 < n_bkt ? bkt[kb + 1] : n_nodes;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (keys[mid] <= x0) lo = mid + 1; else hi = mid;
+  int64_t k;   // the last node whose key is <= x0 (-1: none)
+  bool global = !staged;
+  if (staged) {
+    int64_t a = 0, b = cnt;
+    while (a < b) {
+      const int64_t mid = (a + b) >> 1;
+      if (s_nd[mid].key() <= x0) a = mid + 1; else b = mid;
+    }
+    k = lo + a - 1;
+    global = a == 0 && lo > 0;   // below the staged range (not expected): search globally
   }
-  int64_t k = lo - 1;
-  uint32_t w[4] = {0, 0, 0, 0};
-  int64_t nk = k >= 0 ? ps[k] : 0, ne = k >= 0 ? nk + (nop[k] == 'D' ? 0 : nl[k]) : 0;
+  if (global) {
+    int64_t kb = (x0 - p_min) >> NODE_BKT_SHIFT;
+    if (kb >= n_bkt) kb = n_bkt - 1;
+    int64_t l2 = bkt[kb], h2 = kb + 1 < n_bkt ? bkt[kb + 1] : n_nodes;
+    while (l2 < h2) {
+      const int64_t mid = (l2 + h2) >> 1;
+      if (nd[mid].key() <= x0) l2 = mid + 1; else h2 = mid;
+    }
+    k = l2 - 1;
+  }
+  auto node_at = [&](int64_t q) -> Node16 { return staged && q >= lo && q < lo + cnt ? s_nd[q - lo] : nd[q]; };
+  auto src_at = [&](int64_t q) -> int64_t { return staged && q >= lo && q < lo + cnt ? s_src[q - lo] : src[q]; };
+  int64_t nk = 0, ne = 0;
   const uint8_t *sp = nullptr;
   if (k >= 0) {
-    const int64_t s = src[k];
+    const Node16 n = node_at(k);
+    nk = n.ps();
+    ne = nk + (n.code() == 3 ? 0 : n.oplen());
+    const int64_t s = src_at(k);
     sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
   }
   // the usual case: all 16 bytes inside one node's bytes (no later node starts within them)
-  const int64_t kn = k + 1 < n_nodes ? keys[k + 1] : INT64_MAX;
+  const int64_t kn = k + 1 < n_nodes ? node_at(k + 1).key() : INT64_MAX;
   if (k >= 0 && o0 + 16 <= hap_len && kn > x0 + 15 && x0 >= nk && x0 + 16 <= ne) {
     *(uint4 *)(hap + o0) = load16_unaligned(sp + (x0 - nk));
     return;
   }
-#pragma unroll
-  for (int b = 0; b < 16; b++) {
-    const int64_t x = x0 + b;
-    if (o0 + b >= hap_len) break;
-    while (k + 1 < n_nodes && keys[k + 1] <= x) {
-      k++;
-      nk = ps[k];
-      ne = nk + (nop[k] == 'D' ? 0 : nl[k]);
-      const int64_t s = src[k];
-      sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
+  // a chunk meeting several nodes: each node's bytes in it from one 16-byte load, shifted into place
+  typedef unsigned __int128 u128;
+  const int64_t xe = x0 + (o0 + 16 <= hap_len ? 16 : hap_len - o0);   // end of the chunk's positions
+  u128 acc = 0;
+  for (int guard = 0; guard < 40; guard++) {   // at most 16 byte-holding nodes (+ 'D' nodes) meet 16 positions
+    if (k >= 0) {
+      const int64_t a = x0 > nk ? x0 : nk, e = xe < ne ? xe : ne;
+      if (e > a) {
+        const uint4 v = load16_unaligned(sp + (a - nk));
+        u128 V = ((u128)(((uint64_t)v.w << 32) | v.z) << 64) | (((uint64_t)v.y << 32) | v.x);
+        const int off = (int)(a - x0), len = (int)(e - a);   // 0 <= off, off + len <= 16
+        const u128 m = len >= 16 ? ~(u128)0 : (((u128)1 << (8 * len)) - 1);
+        acc |= (V & m) << (8 * off);
+      }
     }
-    const uint32_t c = (k >= 0 && x >= nk && x < ne) ? sp[x - nk] : 0u;
-    w[b >> 2] |= c << (8 * (b & 3));
+    const int64_t kn2 = k + 1 < n_nodes ? node_at(k + 1).key() : INT64_MAX;
+    if (kn2 >= xe) break;
+    k++;
+    const Node16 n = node_at(k);
+    nk = n.ps();
+    ne = nk + (n.code() == 3 ? 0 : n.oplen());
+    const int64_t s = src_at(k);
+    sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
   }
-  *(uint4 *)(hap + o0) = make_uint4(w[0], w[1], w[2], w[3]);
+  const uint64_t lo64 = (uint64_t)acc, hi64 = (uint64_t)(acc >> 64);
+  *(uint4 *)(hap + o0) = make_uint4((uint32_t)lo64, (uint32_t)(lo64 >> 32), (uint32_t)hi64, (uint32_t)(hi64 >> 32));
+}
+
+// A workgroup fills FILL_SPAN bytes; its nodes (from the last one keyed below its first bucket to the first one
+// past its last bucket) are staged in LDS first, so every chunk's search is an LDS binary search.
+__global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min, int64_t n_nodes, const Node16 *nd,
+                                                  const int64_t *src, const int32_t *bkt, int64_t n_bkt,
+                                                  const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap) {
+  __shared__ Node16 s_nd[FILL_NODES];
+  __shared__ int64_t s_src[FILL_NODES];
+  __shared__ int64_t s_lo, s_hi;
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * FILL_SPAN;
+  if (tid == 0) {
+    int64_t kb0 = b0 >> NODE_BKT_SHIFT, kb1 = ((b0 + FILL_SPAN - 1) >> NODE_BKT_SHIFT) + 1;
+    if (kb0 >= n_bkt) kb0 = n_bkt - 1;
+    const int64_t lo = bkt[kb0] - 1, hi = kb1 < n_bkt ? (int64_t)bkt[kb1] + 1 : n_nodes;
+    s_lo = lo < 0 ? 0 : lo;
+    s_hi = hi > n_nodes ? n_nodes : hi;
+  }
+  __syncthreads();
+  const int64_t lo = s_lo, cnt = s_hi - s_lo;
+  const bool staged = cnt <= FILL_NODES;   // workgroup-uniform
+  if (staged) {
+    for (int i = tid; i < cnt; i += 256) {
+      s_nd[i] = nd[lo + i];
+      s_src[i] = src[lo + i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < FILL_Q; q++) {
+    const int64_t o0 = b0 + (int64_t)(q * 256 + tid) * 16;
+    if (o0 < hap_len)
+      hap_fill_chunk(o0, hap_len, p_min, n_nodes, nd, src, bkt, n_bkt, contig, alt_pool, hap, staged, lo, cnt, s_nd,
+                     s_src);
+  }
 }
 
 // ---- N runs ---------------------------------------------------------------------------------------------------
@@ -274,13 +342,15 @@ __global__ void __launch_bounds__(256) k_hap_rc(const uint8_t *hap, int64_t hap_
   *(uint4 *)(rc + i0) = make_uint4(comp4(w[0]), comp4(w[1]), comp4(w[2]), comp4(w[3]));
 }
 
-// AoS copy of the node arrays for the emission kernels' random lookups.
-__global__ void __launch_bounds__(256) k_node_pack(int64_t n, const int64_t *keys, const int64_t *ps,
-                                                   const int64_t *pr, const int64_t *oplen, const uint8_t *op,
-                                                   Node32 *nd) {
+// AoS copy of the node arrays for the emission kernels' random lookups (field ranges checked on the host).
+__global__ void __launch_bounds__(256) k_node_pack(int64_t n, const int64_t *ps, const int64_t *pr,
+                                                   const int64_t *oplen, const uint8_t *op, Node16 *nd) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  nd[i] = Node32{keys[i], ps[i], pr[i], (int32_t)oplen[i], op[i], {0, 0, 0}};
+  const uint8_t o = op[i];
+  const uint64_t code = o == 'X' ? 1u : o == 'I' ? 2u : o == 'D' ? 3u : 0u;
+  const uint64_t a = (uint64_t)ps[i], b = (uint64_t)pr[i], l = (uint64_t)oplen[i];
+  nd[i] = Node16{(a & 0xffffffffffull) | code << 40 | (l & 0x3fffffull) << 42, (b & 0xffffffffffull) | (l >> 22) << 40};
 }
 
 // Node-search buckets: bkt[k] = first node whose key is >= p_min + (k << NODE_BKT_SHIFT) (lower_bound), so the
@@ -430,10 +500,15 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   MH_TRY(ensure(ctx, h.hap, hap_len + 1024));   // emission gathers whole 16-byte chunks past the last base
   // --- node-search buckets and the AoS node copy (the byte fill below and emission search through them) --------
   {
-    MH_TRY(ensure(ctx, h.nd, sizeof(Node32) * (n_nodes + 1)));
+    // Node16 holds positions below 2^40 and lengths below 2^46: ps <= rs + hap_len, pr <= rs + contig length
+    if (rs < 0 || rs + hap_len + c.len >= ((int64_t)1 << 40)) {
+      stage_end(ctx);
+      return arg_fail(ctx, MH_E_ARG, "region coordinates beyond 2^40");
+    }
+    MH_TRY(ensure(ctx, h.nd, sizeof(Node16) * (n_nodes + 1)));
     hipLaunchKernelGGL(k_node_pack, dim3(grid_for(n_nodes, 256, INT32_MAX)), dim3(256), 0, st, n_nodes,
-                       (const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
-                       (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, (Node32 *)h.nd.p);
+                       (const int64_t *)h.ps.p, (const int64_t *)h.pr.p, (const int64_t *)h.oplen.p,
+                       (const uint8_t *)h.op.p, (Node16 *)h.nd.p);
     HIPCHK(ctx, hipGetLastError());
     const int64_t n_bkt = ((hap_len + 2048) >> NODE_BKT_SHIFT) + 1;   // keys reach at most p_min + hap_len + 1
     MH_TRY(ensure(ctx, h.bkt, 4 * (n_bkt + 2)));
@@ -444,10 +519,9 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   }
   if (pieces > 0 && hap_len > 0) {
     stage_begin(ctx, "splice_hap_copy");
-    hipLaunchKernelGGL(k_hap_fill, dim3(grid_for((hap_len + 15) / 16, 256, INT32_MAX)), dim3(256), 0, st, hap_len,
-                       p_min, n_nodes, (const int64_t *)keys, (const int64_t *)ps, (const uint8_t *)nop,
-                       (const int64_t *)nl, (const int64_t *)nsrc, (const int32_t *)h.bkt.p, h.n_bkt,
-                       (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p);
+    hipLaunchKernelGGL(k_hap_fill, dim3((unsigned)((hap_len + FILL_SPAN - 1) / FILL_SPAN)), dim3(256), 0, st, hap_len,
+                       p_min, n_nodes, (const Node16 *)h.nd.p, (const int64_t *)nsrc, (const int32_t *)h.bkt.p,
+                       h.n_bkt, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   }
