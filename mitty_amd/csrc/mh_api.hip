@@ -152,7 +152,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &kv : ctx->tsets) {
     release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1);
   }
-  release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->dec_buf);
+  release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->s) release(b);
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);

@@ -120,7 +120,8 @@ struct mh_ctx {
   int64_t fixups = 0;   // units redone on the exact fallback path
   std::map<int32_t, mh::VarSet> vsets;   // resident variant sets (mh_upload_variants); id -1: mh_build_haplotype's
   std::vector<mh::Hap> hap_spare;   // released haplotypes' buffers, reused by the next build (no hipMalloc/hipFree)
-  mh::DevBuf perm_tmp;  // radix sort scratch of the permutation
+  mh::DevBuf perm_tmp;  // radix sort scratch (permutation, N runs)
+  mh::DevBuf nrun_tmp;  // unsorted N-run boundaries
   mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
   int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)
 

@@ -6,10 +6,13 @@
 //   2. k_resolve                 -> one thread per anchor walks its (short) run of non-anchors sequentially;
 //   3. max-scan of accepted ends -> ref cursor before each variant (accepted ends are strictly increasing);
 //   4. sum-scan of (nodes, sample length) -> every node's index and ps, written straight from the scan's Store;
-//   5. piece copy                -> haplotype bytes (hap[k] = base at sample position p_min + k) gathered from the
-//                                   resident contig / alt pool, 4 KiB pieces, one wave each;
-//   6. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
+//   5. packed nodes + buckets    -> Node16 copy and the node-search bucket table;
+//   6. k_hap_fill                -> haplotype bytes (hap[k] = base at sample position p_min + k) by output position
+//                                   from the resident contig / alt pool; k_hap_rc the reverse complement;
+//   7. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
 // Node arrays are SoA in HBM: keys (search key, ps+1 for 'D' as rpc.py:127), ps, pr, op, oplen.
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
@@ -18,7 +21,6 @@ namespace mh {
 
 namespace {
 
-constexpr int64_t PIECE = 4096;
 constexpr int64_t ALT_FLAG = (int64_t)1 << 62;
 
 __device__ __forceinline__ int64_t var_end(int64_t pos, uint8_t op, int64_t oplen) {
@@ -118,41 +120,6 @@ struct StoreNodes {
 __global__ void k_trailing(int64_t k, int64_t sp, int64_t rp, int64_t rs, int64_t len, int64_t *keys, int64_t *ps,
                            int64_t *pr, int64_t *nl, int64_t *src, uint8_t *nop) {
   keys[k] = sp; ps[k] = sp; pr[k] = rp; nop[k] = '='; nl[k] = len; src[k] = rp - rs;
-}
-
-struct LoadPieces {
-  const uint8_t *nop; const int64_t *nl;
-  __device__ int64_t operator()(int64_t i) const { return nop[i] == 'D' ? 0 : (nl[i] + PIECE - 1) / PIECE; }
-};
-struct StorePieceOff {
-  int64_t *off;
-  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { off[i] = excl; }
-};
-
-__device__ __forceinline__ int64_t upper_bound_i64(const int64_t *a, int64_t n, int64_t x) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-__global__ void __launch_bounds__(256) k_hap_copy(int64_t total_pieces, int64_t n_nodes, const int64_t *piece_off,
-                                                  const int64_t *ps, const int64_t *nl, const int64_t *src,
-                                                  const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap,
-                                                  int64_t p_min) {
-  int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  int lane = threadIdx.x & 63;
-  if (w >= total_pieces) return;
-  int64_t node = upper_bound_i64(piece_off, n_nodes, w) - 1;
-  int64_t q = w - piece_off[node];
-  int64_t b0 = q * PIECE, b1 = b0 + PIECE;
-  if (b1 > nl[node]) b1 = nl[node];
-  int64_t s = src[node];
-  const uint8_t *sp = (s & ALT_FLAG) ? alt_pool + (s & ~ALT_FLAG) : contig + s;
-  uint8_t *dp = hap + (ps[node] - p_min);
-  for (int64_t b = b0 + lane; b < b1; b += 64) dp[b] = sp[b];
 }
 
 // Haplotype bytes by output position: thread i writes hap[16i, 16i+16).  The node holding sample position x is the
@@ -272,58 +239,46 @@ __global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min
 }
 
 // ---- N runs ---------------------------------------------------------------------------------------------------
-constexpr int64_t NCHUNK = 16;
-
-struct RunCnt {
-  int64_t starts, ends;
-  __device__ RunCnt operator+(const RunCnt &o) const { return RunCnt{starts + o.starts, ends + o.ends}; }
-};
-
-// Element c covers byte positions k in [c*16, c*16+16) ∩ [0, len]; a run starts at k if hap[k]=='N' and
-// hap[k-1] != 'N', and ends (exclusive) at k if hap[k-1]=='N' and (k == len or hap[k] != 'N').
-// 16 bytes per element as one aligned 16-byte load (the haplotype buffer is padded), 'N' found with SWAR.
+// A run starts at position k if hap[k]=='N' and hap[k-1] != 'N', and ends (exclusive) at k if hap[k-1]=='N' and
+// (k == len or hap[k] != 'N').  'N' found with SWAR over aligned 16-byte loads (the haplotype buffer is padded).
 __device__ __forceinline__ uint32_t n_bits4(uint32_t w) {
   const uint32_t t = w ^ 0x4E4E4E4Eu;                                    // zero byte where 'N'
   const uint32_t nz = ((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t;             // bit 7 of each byte: byte != 0
   const uint32_t z = ~nz & 0x80808080u;
   return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
 }
-// masks over the 16 positions of element c: starts, ends
-__device__ __forceinline__ void run_masks(const uint8_t *hap, int64_t len, int64_t c, uint32_t &st, uint32_t &en) {
-  const int64_t k0 = c * NCHUNK;
-  uint32_t nm = 0;
-  if (k0 < len) {
-    const uint4 v = *(const uint4 *)(hap + k0);
-    nm = n_bits4(v.x) | (n_bits4(v.y) << 4) | (n_bits4(v.z) << 8) | (n_bits4(v.w) << 12);
-    const int64_t valid = len - k0;                                      // positions >= len are not 'N'
-    if (valid < 16) nm &= (1u << valid) - 1u;
+// One pass over the haplotype for the run boundaries, 64 positions per thread: boundaries are rare, so each is
+// appended to an unsorted list through an atomic counter (cap entries kept, all counted); sorted afterwards.
+__global__ void __launch_bounds__(256) k_nrun_find(const uint8_t *hap, int64_t len, int64_t cap, int64_t *rs,
+                                                   int64_t *re, unsigned long long *cnt) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k0 = c * 64;
+  if (k0 > len) return;
+  uint64_t nm = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = *(const uint4 *)(hap + k0 + 16 * q);   // the buffer is padded past len
+    const uint64_t m = n_bits4(v.x) | (n_bits4(v.y) << 4) | (n_bits4(v.z) << 8) | (n_bits4(v.w) << 12);
+    nm |= m << (16 * q);
   }
-  const uint32_t prev = (k0 > 0 && k0 - 1 < len && hap[k0 - 1] == 'N') ? 1u : 0u;
-  const uint32_t sh = ((nm << 1) | prev) & 0xFFFFu;                      // bit i: hap[k0 + i - 1] == 'N'
-  uint32_t pos_mask = 0xFFFFu;                                           // positions k0 + i <= len
-  if (len - k0 < 15) pos_mask = (len - k0 < 0) ? 0u : ((1u << (len - k0 + 1)) - 1u);
-  st = nm & ~sh & pos_mask;
-  en = sh & ~nm & pos_mask;
+  const int64_t valid = len - k0;                            // positions >= len are not 'N'
+  if (valid < 64) nm &= (1ull << valid) - 1ull;
+  const uint64_t prev = (k0 > 0 && hap[k0 - 1] == 'N') ? 1ull : 0ull;
+  const uint64_t sh = (nm << 1) | prev;                       // bit i: hap[k0 + i - 1] == 'N'
+  uint64_t pos = ~0ull;                                       // positions k0 + i <= len
+  if (valid < 63) pos = (1ull << (valid + 1)) - 1ull;
+  uint64_t st = nm & ~sh & pos, en = sh & ~nm & pos;
+  while (st) {
+    const unsigned long long i = atomicAdd(cnt, 1ull);
+    if ((int64_t)i < cap) rs[i] = k0 + __builtin_ctzll(st);
+    st &= st - 1;
+  }
+  while (en) {
+    const unsigned long long i = atomicAdd(cnt + 1, 1ull);
+    if ((int64_t)i < cap) re[i] = k0 + __builtin_ctzll(en);
+    en &= en - 1;
+  }
 }
-
-struct LoadRuns {
-  const uint8_t *hap; int64_t len;
-  __device__ RunCnt operator()(int64_t c) const {
-    uint32_t st, en;
-    run_masks(hap, len, c, st, en);
-    return RunCnt{__popc(st), __popc(en)};
-  }
-};
-struct StoreRuns {
-  const uint8_t *hap; int64_t len; int64_t *rs_out; int64_t *re_out;
-  __device__ void operator()(int64_t c, RunCnt, RunCnt excl) const {
-    uint32_t st, en;
-    run_masks(hap, len, c, st, en);
-    int64_t a = excl.starts, b = excl.ends;
-    while (st) { rs_out[a++] = c * NCHUNK + __ffs(st) - 1; st &= st - 1; }
-    while (en) { re_out[b++] = c * NCHUNK + __ffs(en) - 1; en &= en - 1; }
-  }
-};
 
 // Reverse complement of the haplotype (readgenerate.py:56,205-206: str.maketrans('ATCGN', 'TAGCN') then [::-1]):
 // rc[i] = comp(hap[hap_len - 1 - i]); mate-1 reads are then forward ranges of rc.  16 output bytes per thread.
@@ -418,21 +373,19 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   const int64_t *d_aoff = (const int64_t *)v.aoff.p, *d_alen = (const int64_t *)v.alen.p;
   const uint8_t *d_op = (const uint8_t *)v.op.p, *d_pool = (const uint8_t *)v.pool.p;
 
-  // --- scratch: anchor(6) accepted(7) ref_before(8) node src(9) piece_off(10) small(d_small) -----------------
+  // --- scratch: anchor(6) accepted(7) ref_before(8) node src(9) small(d_small) -----------------------------
   MH_TRY(ensure(ctx, ctx->s[6], nv));
   MH_TRY(ensure(ctx, ctx->s[7], nv));
   MH_TRY(ensure(ctx, ctx->s[8], 8 * nv));
   MH_TRY(ensure(ctx, ctx->s[9], 8 * node_cap));
-  MH_TRY(ensure(ctx, ctx->s[10], 8 * node_cap));
   MH_TRY(ensure(ctx, ctx->d_small, 256));
   MH_TRY(ensure(ctx, ctx->scan_partials, 32 * scan_partials_count(node_cap > nv ? node_cap : nv) + 64));
   uint8_t *anchor = (uint8_t *)ctx->s[6].p, *accepted = (uint8_t *)ctx->s[7].p;
-  int64_t *ref_before = (int64_t *)ctx->s[8].p, *nsrc = (int64_t *)ctx->s[9].p, *poff = (int64_t *)ctx->s[10].p;
+  int64_t *ref_before = (int64_t *)ctx->s[8].p, *nsrc = (int64_t *)ctx->s[9].p;
   char *small = (char *)ctx->d_small.p;
   int64_t *tot_i64 = (int64_t *)small;           // [0]
   NS *tot_ns = (NS *)(small + 16);                // [16..32)
   int32_t *err = (int32_t *)(small + 64);
-  int64_t *tot_pieces = (int64_t *)(small + 80);
   HIPCHK(ctx, hipMemsetAsync(small, 0, 256, st));
 
   MH_TRY(ensure(ctx, h.keys, 8 * node_cap));
@@ -484,11 +437,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   HIPCHK(ctx, hipMemcpyAsync(&nll, nl + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
 
   // --- haplotype bytes ---------------------------------------------------------------------------------------
-  HIPCHK(ctx, device_scan<int64_t>(st, n_nodes, LoadPieces{nop, nl}, StorePieceOff{poff}, OpSum{}, (int64_t)0,
-                                   (int64_t *)ctx->scan_partials.p, tot_pieces));
-  int64_t pieces = 0;
   int32_t herr = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&pieces, tot_pieces, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
   if (herr) {
@@ -517,7 +466,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     HIPCHK(ctx, hipGetLastError());
     h.n_bkt = n_bkt;
   }
-  if (pieces > 0 && hap_len > 0) {
+  if (hap_len > 0) {
     stage_begin(ctx, "splice_hap_copy");
     hipLaunchKernelGGL(k_hap_fill, dim3((unsigned)((hap_len + FILL_SPAN - 1) / FILL_SPAN)), dim3(256), 0, st, hap_len,
                        p_min, n_nodes, (const Node16 *)h.nd.p, (const int64_t *)nsrc, (const int32_t *)h.bkt.p,
@@ -534,25 +483,45 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   }
-  // --- N runs -----------------------------------------------------------------------------------------------
-  int64_t nchunks = (hap_len + 1 + NCHUNK - 1) / NCHUNK;
-  RunCnt *rtot = (RunCnt *)(small + 128);
-  // count first (sizes the run arrays), then the same scan again to write them
-  MH_TRY(ensure(ctx, ctx->scan_partials, std::max<size_t>(16 * scan_partials_count(nchunks) + 64,
-                                                           scan_lb_scratch_bytes<RunCnt>(nchunks))));
-  HIPCHK(ctx, device_reduce<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len}, OpSum{}, RunCnt{0, 0},
-                                    (RunCnt *)ctx->scan_partials.p, rtot));
-  RunCnt hr;
-  HIPCHK(ctx, hipMemcpyAsync(&hr, rtot, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
-  h.n_runs = hr.starts;
-  MH_TRY(ensure(ctx, h.nrun_s, 8 * (hr.starts + 1)));
-  MH_TRY(ensure(ctx, h.nrun_e, 8 * (hr.ends + 1)));
-  if (hr.starts > 0) {
-    HIPCHK(ctx, device_scan_sum<RunCnt>(st, nchunks, LoadRuns{(const uint8_t *)h.hap.p, hap_len},
-                                        StoreRuns{(const uint8_t *)h.hap.p, hap_len, (int64_t *)h.nrun_s.p,
-                                                  (int64_t *)h.nrun_e.p},
-                                        ctx->scan_partials.p, rtot));
+  // --- N runs: boundaries appended by k_nrun_find, then sorted ----------------------------------------------
+  {
+    unsigned long long *cnt = (unsigned long long *)(small + 128);
+    int64_t cap = std::max<int64_t>(4096, (int64_t)(h.nrun_s.cap / 8) - 1);
+    unsigned long long hc[2] = {0, 0};
+    for (int attempt = 0; attempt < 2; attempt++) {
+      MH_TRY(ensure(ctx, ctx->nrun_tmp, 16 * (size_t)cap + 64));
+      int64_t *us = (int64_t *)ctx->nrun_tmp.p, *ue = us + cap;
+      HIPCHK(ctx, hipMemsetAsync(cnt, 0, 16, st));
+      const int64_t nel = hap_len / 64 + 1;
+      hipLaunchKernelGGL(k_nrun_find, dim3(grid_for(nel, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)h.hap.p,
+                         hap_len, cap, us, ue, cnt);
+      HIPCHK(ctx, hipGetLastError());
+      HIPCHK(ctx, hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if ((int64_t)hc[0] <= cap && (int64_t)hc[1] <= cap) break;
+      cap = (int64_t)std::max(hc[0], hc[1]);   // more boundaries than room: once more with room for all
+    }
+    const int64_t nr = (int64_t)hc[0];
+    if ((int64_t)hc[1] != nr) {
+      stage_end(ctx);
+      return arg_fail(ctx, MH_E_STATE, "N-run starts and ends do not pair");
+    }
+    h.n_runs = nr;
+    MH_TRY(ensure(ctx, h.nrun_s, 8 * (nr + 1)));
+    MH_TRY(ensure(ctx, h.nrun_e, 8 * (nr + 1)));
+    if (nr > 0) {
+      unsigned bits = 1;
+      while (bits < 63 && ((int64_t)1 << bits) <= hap_len) bits++;
+      int64_t *us = (int64_t *)ctx->nrun_tmp.p, *ue = us + cap;
+      size_t tmp = 0;
+      HIPCHK(ctx, rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p, (size_t)nr, 0u,
+                                           bits, st));
+      MH_TRY(ensure(ctx, ctx->perm_tmp, tmp + 256));
+      HIPCHK(ctx, rocprim::radix_sort_keys(ctx->perm_tmp.p, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p,
+                                           (size_t)nr, 0u, bits, st));
+      HIPCHK(ctx, rocprim::radix_sort_keys(ctx->perm_tmp.p, tmp, (const uint64_t *)ue, (uint64_t *)h.nrun_e.p,
+                                           (size_t)nr, 0u, bits, st));
+    }
   }
   stage_end(ctx);
 
