@@ -27,6 +27,7 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return MH_OK;
   if (b.p) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // a queued FASTQ writer may still read or write it
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipFree(b.p));
     b.p = nullptr;
@@ -47,6 +48,7 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
   if (b.cap >= bytes) return MH_OK;
   DevBuf nb;
   MH_TRY(ensure(ctx, nb, bytes + bytes / 2));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   if (b.p) HIPCHK(ctx, hipFree(b.p));
@@ -65,12 +67,19 @@ void release_hap(Hap &h) {
   release(h.op); release(h.oplen); release(h.nrun_s); release(h.nrun_e);
 }
 
+int32_t join_writer(mh_ctx *ctx) {
+  if (!ctx->writer_pending) return MH_OK;
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_writer, 0));
+  ctx->writer_pending = false;
+  return MH_OK;
+}
+
 void stage_begin(mh_ctx *ctx, const char *name) {
   if (!ctx->timing) return;
   StageTime s{name, nullptr, nullptr};
   (void)hipEventCreate(&s.a);
   (void)hipEventCreate(&s.b);
-  (void)hipEventRecord(s.a, ctx->stream);
+  (void)hipEventRecord(s.a, ctx->stage_stream ? ctx->stage_stream : ctx->stream);
   ctx->stages.push_back(s);
 }
 
@@ -78,7 +87,7 @@ void stage_end(mh_ctx *ctx) {
   if (!ctx->timing || ctx->stages.empty()) return;
   StageTime s = ctx->stages.back();
   ctx->stages.pop_back();
-  (void)hipEventRecord(s.b, ctx->stream);   // resolved later by stages_collect: no host sync here
+  (void)hipEventRecord(s.b, ctx->stage_stream ? ctx->stage_stream : ctx->stream);   // resolved by stages_collect
   ctx->pending.push_back(s);
 }
 
@@ -98,11 +107,17 @@ void stages_collect(mh_ctx *ctx) {
 
 using namespace mh;
 
-#define CTX_GUARD(ctx)                                                     \
+#define CTX_GUARD_NOJOIN(ctx)                                              \
   do {                                                                     \
     if (!(ctx)) return MH_E_ARG;                                           \
     hipError_t _e = hipSetDevice((ctx)->device);                           \
     if (_e != hipSuccess) return hip_fail((ctx), _e, "hipSetDevice", __FILE__, __LINE__); \
+  } while (0)
+// every entry point but the emission ones: the main stream first waits for the last queued FASTQ writer
+#define CTX_GUARD(ctx)                                                     \
+  do {                                                                     \
+    CTX_GUARD_NOJOIN(ctx);                                                 \
+    MH_TRY(join_writer(ctx));                                              \
   } while (0)
 
 extern "C" {
@@ -131,7 +146,12 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   if (device < 0 || device >= n) return MH_E_ARG;
   mh_ctx *ctx = new mh_ctx();
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->wstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->eset[0].done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->eset[1].done, hipEventDisableTiming) != hipSuccess) {
     delete ctx;
     return MH_E_HIP;
   }
@@ -144,6 +164,7 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
 int32_t mh_destroy(mh_ctx *ctx) {
   if (!ctx) return MH_OK;
   (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->wstream);
   (void)hipStreamSynchronize(ctx->stream);
   for (auto &kv : ctx->contigs) release(kv.second.seq);
   for (auto &kv : ctx->haps) release_hap(kv.second);
@@ -156,7 +177,14 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &b : ctx->s) release(b);
   release(ctx->scan_partials); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
-  release(ctx->out1); release(ctx->out2); release(ctx->emit_slots);
+  release(ctx->out1); release(ctx->out2);
+  for (auto &e : ctx->eset) {
+    release(e.recs); release(e.off); release(e.slots);
+    (void)hipEventDestroy(e.done);
+  }
+  (void)hipEventDestroy(ctx->ev_ready);
+  (void)hipEventDestroy(ctx->ev_writer);
+  (void)hipStreamDestroy(ctx->wstream);
   bam_release(ctx->bam);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -442,7 +470,7 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
 
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
@@ -453,7 +481,7 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");

@@ -1052,8 +1052,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   if (m == 0) return MH_OK;
 
   stage_begin(ctx, "emit");
-  MH_TRY(ensure(ctx, ctx->s[14], sizeof(Rec) * m));
-  MH_TRY(ensure(ctx, ctx->s[15], sizeof(E3) * (m + 1)));
+  // this unit's buffer set; the writer that last read it (two calls ago) must be done before the measure refills it
+  EmitSet &es = ctx->eset[ctx->eset_i];
+  ctx->eset_i ^= 1;
+  if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
+  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
+  MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
   MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   char *small = (char *)ctx->d_small.p;
@@ -1067,16 +1071,16 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
   QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
-  Rec *recs = (Rec *)ctx->s[14].p;
-  E3 *off = (E3 *)ctx->s[15].p;
+  Rec *recs = (Rec *)es.recs.p;
+  E3 *off = (E3 *)es.off.p;
 
   const bool direct = !ctx->emit_lds_only && !ctx->corrupt_on;   // fused corruption uses the LDS-image writer
   int32_t *overflow = (int32_t *)(small + 40);
-  if (direct) MH_TRY(ensure(ctx, ctx->emit_slots, (size_t)SLOT * (m + 1)));
+  if (direct) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
   stage_begin(ctx, "emit_measure");
   hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
                      rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                     direct ? (uint8_t *)ctx->emit_slots.p : nullptr, overflow,
+                     direct ? (uint8_t *)es.slots.p : nullptr, overflow,
                      getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
@@ -1125,7 +1129,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   }
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
-  stage_begin(ctx, "emit_write");
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
   const char *dbg_env = getenv("MH_EMIT_DBG");   // timing experiments only: skip parts of the kernel
   const int32_t edbg = dbg_env ? atoi(dbg_env) : 0;
@@ -1143,29 +1146,43 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     qh.lm = (int32_t)mid.size();
   }
   if (direct && !hover && head_fits && win_stride <= 16 * 4 * ED_WMAX && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
-    // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots)
+    // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots), queued on the writer
+    // stream: the call returns while it runs, so the next unit's measure pass overlaps it
+    HIPCHK(ctx, hipEventRecord(ctx->ev_ready, st));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_ready, 0));
+    ctx->stage_stream = ctx->wstream;
+    stage_begin(ctx, "emit_write");
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
-    EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)ctx->emit_slots.p,
+    EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)es.slots.p,
              {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
              qstride, edbg};
     const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
     auto kfn = write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16> : lpr == 8 ? k_emit_direct<2, 8> : k_emit_direct<2, 4>)
                             : (lpr == 16 ? k_emit_direct<1, 16> : k_emit_direct<1, 8>);
-    hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, st, A, qh);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    stage_end(ctx);   // "emit"
+    ctx->stage_stream = nullptr;
+    HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ctx->wstream));
+    es.busy = true;
+    ctx->writer_pending = true;
   } else {
-    // LDS-image writer: fallback when a qname's reads part exceeds its slot
+    // LDS-image writer: fallback when a qname's reads part exceeds its slot (synchronous, main stream)
+    stage_begin(ctx, "emit_write");
     const int64_t nblk = (m + EW_T - 1) / EW_T;
     hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
                        pos0, pos1, fo0, rlen, q,
                        (const Rec *)recs, (const E3 *)off, o1, o2, write_fastq2, cap, win_stride, cc, err);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    int32_t herr = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    stage_end(ctx);
+    if (herr) return arg_fail(ctx, MH_E_CAPACITY, "FASTQ record larger than the LDS staging image");
   }
-  HIPCHK(ctx, hipGetLastError());
-  stage_end(ctx);
-  int32_t herr = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
-  stage_end(ctx);
-  if (herr) return arg_fail(ctx, MH_E_CAPACITY, "FASTQ record larger than the LDS staging image");
   ctx->used1 += ht.b1;
   if (write_fastq2) ctx->used2 += ht.b2;
   *out_kept = ht.kept;

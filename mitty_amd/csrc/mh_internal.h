@@ -101,9 +101,27 @@ struct StageTime {
 
 }  // namespace mh
 
+namespace mh {
+// One set of emission buffers (records, offsets, qname reads-part slots).  Two sets alternate so the FASTQ writer of
+// one unit (on the writer stream) overlaps the measure pass of the next (on the main stream).
+struct EmitSet {
+  DevBuf recs, off, slots;
+  hipEvent_t done = nullptr;   // the last writer that read this set
+  bool busy = false;
+};
+}  // namespace mh
+
 struct mh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // FASTQ writer stream: mh_emit_reads returns once its writer is queued here; every other entry point first makes
+  // the main stream wait for the last queued writer (ev_writer)
+  hipStream_t wstream = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
+  bool writer_pending = false;
+  mh::EmitSet eset[2];
+  int eset_i = 0;
+  hipStream_t stage_stream = nullptr;   // stream the stage timing events go to (nullptr: stream)
   std::string err;
   int32_t max_cu = 256;
 
@@ -137,8 +155,7 @@ struct mh_ctx {
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
   uint64_t corrupt_seed = 0;
 
-  // emission: per-template qname slots; emit_lds_only forces the LDS-image writer (A/B and fallback testing)
-  mh::DevBuf emit_slots;
+  // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
@@ -173,6 +190,7 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);
 int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep);
 void release(DevBuf &b);
 void release_hap(Hap &h);
+int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);
