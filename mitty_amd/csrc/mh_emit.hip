@@ -1122,11 +1122,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     stage_end(ctx);
     return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
   }
-  int32_t hover = 0;
-  if (direct) {
-    HIPCHK(ctx, hipMemcpyAsync(&hover, overflow, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-  }
+  const int32_t hover = direct ? hm4[2] : 0;   // a reads part overflowed its slot (read back with the maxima)
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
