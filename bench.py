@@ -87,11 +87,12 @@ def main():
   kernel = 'k_emit_write' if (a.emit_mode or a.corrupt) else 'k_emit_direct'
 
   def step():
+    # one chr1 job; consecutive jobs pipeline on the device (this job's splice and sampling run while the previous
+    # job's last FASTQ writers drain); the timed region ends with a full synchronisation
     eng.drop_haplotypes()
     eng.ctx.reset_output()
     res = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p, rlen,
                         model['cum_tlen'], 'SYN', 0, True, a.rng)
-    eng.ctx.sync()
     return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
 
   def barrier():

@@ -119,6 +119,11 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_bytes1,
                       int64_t *out_bytes2);
+/* The first half of mh_emit_reads for the current template set: the measure pass and record offsets, with the same
+ * outputs.  The next mh_emit_reads of the same unit (same slot and names) only queues the writer, so a caller that
+ * prepares a batch of units first (at most 4 at a time) queues their writers back to back and moves on. */
+int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 /* A slice of a unit for multi-GPU sharding: emit only templates [t_begin, t_end) of the current
  * set, numbering the kept ones from cnt_base + 1 (cnt_base = templates kept before t_begin, e.g. from an all-gather
  * of mh_count_kept over the ranks' slices).  Concatenating the slices in order reproduces mh_emit_reads byte for

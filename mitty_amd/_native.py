@@ -17,7 +17,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_emit_reads', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
+           'mh_get_templates', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
@@ -75,6 +75,7 @@ def lib():
   _sig(L, 'mh_set_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32])
   _sig(L, 'mh_get_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_emit_prepare', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
@@ -369,6 +370,15 @@ class Context:
     return fo0[:m], p0[:m], p1[:m]
 
   # ---- emission ----------------------------------------------------------------------------------------
+  def emit_prepare(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+    """The measure pass and record offsets of the current templates (the next emit_reads of the same unit only
+    queues the writer).  Returns (kept, bytes1, bytes2)."""
+    k, b1, b2 = c_i64(), c_i64(), c_i64()
+    self._chk(self._L.mh_emit_prepare(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                      1 if write_fastq2 else 0, int(unit_key), ctypes.byref(k), ctypes.byref(b1),
+                                      ctypes.byref(b2)))
+    return k.value, b1.value, b2.value
+
   def emit_reads(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, t_range=None, cnt_base=0):
     """Emit the current templates (or the slice t_range = (t_begin, t_end), kept ones numbered from cnt_base + 1).
     Returns (kept, bytes1, bytes2)."""

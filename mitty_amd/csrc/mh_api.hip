@@ -3,6 +3,8 @@
 #include <cstring>
 
 #include "mh_bgzf.h"
+#include <vector>
+
 #include "mh_internal.h"
 
 namespace mh {
@@ -65,6 +67,21 @@ void release(DevBuf &b) {
 void release_hap(Hap &h) {
   release(h.hap); release(h.rc); release(h.nd); release(h.bkt); release(h.keys); release(h.ps); release(h.pr);
   release(h.op); release(h.oplen); release(h.nrun_s); release(h.nrun_e);
+  if (h.used) (void)hipEventDestroy(h.used);
+  h.used = nullptr;
+  h.used_set = false;
+}
+
+int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set) {
+  if (!ev) HIPCHK(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIPCHK(ctx, hipEventRecord(ev, ctx->wstream));
+  set = true;
+  return MH_OK;
+}
+
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set) {
+  if (set) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
+  return MH_OK;
 }
 
 int32_t join_writer(mh_ctx *ctx) {
@@ -135,6 +152,21 @@ int32_t mh_device_count(int32_t *out) {
   return MH_OK;
 }
 
+// The writer stream may be limited to a share of the CUs (MH_WRITER_CUS = eighths of each XCD's CUs, experiments):
+// the bandwidth-bound writers then leave whole CUs to the next job's latency-bound sampling kernels.
+static hipError_t create_writer_stream(mh_ctx *ctx, int device, int prio) {
+  const char *e = getenv("MH_WRITER_CUS");
+  const int eighths = e ? atoi(e) : 8;
+  hipDeviceProp_t prop;
+  if (eighths >= 8 || eighths <= 0 || hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return hipStreamCreateWithPriority(&ctx->wstream, hipStreamNonBlocking, prio);
+  const int n = prop.multiProcessorCount;
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int cu = 0; cu < n; cu++)
+    if ((cu % 8) < eighths) mask[cu / 32] |= 1u << (cu % 32);
+  return hipExtStreamCreateWithCUMask(&ctx->wstream, (uint32_t)mask.size(), mask.data());
+}
+
 int32_t mh_create(int32_t device, mh_ctx **out) {
   if (!out) return MH_E_ARG;
   *out = nullptr;
@@ -146,12 +178,22 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   if (device < 0 || device >= n) return MH_E_ARG;
   mh_ctx *ctx = new mh_ctx();
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->wstream, hipStreamNonBlocking) != hipSuccess ||
+  // the FASTQ writers (bandwidth-bound, long) yield to the main stream's latency-bound sampling kernels
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipSetDevice(device);
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const char *pe = getenv("MH_STREAM_PRIO");   // experiments: 0 disables the priorities
+  if (pe && atoi(pe) == 0) prio_lo = prio_hi = 0;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      create_writer_stream(ctx, device, prio_lo) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->eset[0].done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->eset[1].done, hipEventDisableTiming) != hipSuccess) {
+      [&] {
+        for (auto &e : ctx->eset)
+          if (hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) return true;
+        return false;
+      }()) {
     delete ctx;
     return MH_E_HIP;
   }
@@ -172,6 +214,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &kv : ctx->vsets) release_vars(kv.second);
   for (auto &kv : ctx->tsets) {
     release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1);
+    if (kv.second.used) (void)hipEventDestroy(kv.second.used);
   }
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->s) release(b);
@@ -257,15 +300,21 @@ static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t 
                           int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
   auto it = ctx->contigs.find(contig_id);
   if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
-  if (!ctx->haps.count(slot) && !ctx->hap_spare.empty()) {   // reuse a released haplotype's buffers
+  // reuse the oldest released haplotype's buffers unless a queued writer still reads them (then allocate: the pool
+  // grows to the two generations a pipelined job needs)
+  const bool spare_ready = !ctx->hap_spare.empty() &&
+                           (!ctx->hap_spare.front().used_set || hipEventQuery(ctx->hap_spare.front().used) == hipSuccess);
+  if (!ctx->haps.count(slot) && spare_ready) {
     Hap r{};
-    const Hap &s = ctx->hap_spare.back();
+    const Hap &s = ctx->hap_spare.front();
     r.hap = s.hap; r.rc = s.rc; r.keys = s.keys; r.ps = s.ps; r.pr = s.pr; r.op = s.op; r.oplen = s.oplen;
     r.nrun_s = s.nrun_s; r.nrun_e = s.nrun_e; r.nd = s.nd; r.bkt = s.bkt;
-    ctx->hap_spare.pop_back();
+    r.used = s.used; r.used_set = s.used_set;
+    ctx->hap_spare.erase(ctx->hap_spare.begin());
     ctx->haps[slot] = r;
   }
   Hap &h = ctx->haps[slot];
+  MH_TRY(wait_unused(ctx, h.used, h.used_set));   // a queued writer may still read the old bytes
   h.valid = false;
   MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v));
   if (out_n_nodes) *out_n_nodes = h.n_nodes;
@@ -278,7 +327,7 @@ int32_t mh_build_haplotype(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t
                            const uint8_t *v_op, const int64_t *v_oplen, const int64_t *v_alt_off,
                            const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len, int64_t n_var,
                            int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   if (!ctx->contigs.count(contig_id)) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
   if (n_var < 0 || (n_var > 0 && (!v_pos || !v_op || !v_oplen || !v_alt_off || !v_alt_len)))
     return arg_fail(ctx, MH_E_ARG, "bad variant arrays");
@@ -305,7 +354,7 @@ int32_t mh_upload_variants(mh_ctx *ctx, int32_t vset, const int64_t *v_pos, cons
 
 int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, int32_t vset,
                                 int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   auto it = ctx->vsets.find(vset);
   if (vset < 0 || it == ctx->vsets.end()) return arg_fail(ctx, MH_E_STATE, "unknown variant set id");
   return build_from(ctx, slot, contig_id, ref_start_pos, it->second, out_n_nodes, out_p_min, out_p_max);
@@ -346,7 +395,7 @@ int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_
 }
 
 int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
@@ -356,6 +405,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
     h.valid = false;
     ctx->hap_spare.push_back(h);
   } else {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     release_hap(h);
   }
@@ -365,7 +415,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
 
 int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                             uint64_t seed, int32_t rng_mode, int64_t *out_n) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0)) return arg_fail(ctx, MH_E_ARG, "bad arguments");
@@ -379,7 +429,7 @@ int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, c
 int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, double p, int32_t rlen,
                                  const double *cum_tlen, int32_t n_tlen, uint64_t seed, int32_t rng_mode,
                                  int64_t *out_n) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0) || p_max < p_min)
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
   const int32_t id = -1;
@@ -391,7 +441,7 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
 int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
                         const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                         int32_t rng_mode, int64_t *out_n) {
-  CTX_GUARD(ctx);
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   if (n_units < 0 || (n_units > 0 && (!tpl_ids || !slots || !seeds)) || !cum_tlen || rlen <= 0 ||
       !(p > 0.0 && p <= 1.0))
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
@@ -423,6 +473,7 @@ int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id) {
   if (it == ctx->tsets.end()) return MH_OK;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   release(it->second.fo0); release(it->second.pos0); release(it->second.pos1);
+  if (it->second.used) (void)hipEventDestroy(it->second.used);
   ctx->tsets.erase(it);
   if (ctx->cur_tpl == tpl_id) ctx->cur_tpl = -1;
   return MH_OK;
@@ -474,8 +525,18 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
-  return emit_reads(ctx, it->second, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, out_kept, out_b1,
-                    out_b2);
+  return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, false, out_kept,
+                    out_b1, out_b2);
+}
+
+int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+  CTX_GUARD_NOJOIN(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
+  return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, true, out_kept,
+                    out_b1, out_b2);
 }
 
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
@@ -486,8 +547,8 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (t_begin < 0 || t_end < t_begin || cnt_base < 0) return arg_fail(ctx, MH_E_ARG, "bad template range");
-  return emit_reads(ctx, it->second, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,
-                    out_kept, out_b1, out_b2);
+  return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,
+                    false, out_kept, out_b1, out_b2);
 }
 
 int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end, int64_t *out_kept) {

@@ -1029,9 +1029,9 @@ int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, in
   return MH_OK;
 }
 
-int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
-                   int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+                   bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   auto tit = ctx->tsets.find(ctx->cur_tpl);
   if (tit == ctx->tsets.end() || !tit->second.valid)
     return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
@@ -1050,51 +1050,96 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   *out_b1 = 0;
   *out_b2 = 0;
   if (m == 0) return MH_OK;
-
-  stage_begin(ctx, "emit");
-  // this unit's buffer set; the writer that last read it (two calls ago) must be done before the measure refills it
-  EmitSet &es = ctx->eset[ctx->eset_i];
-  ctx->eset_i ^= 1;
-  if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
-  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
-  MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
-  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   char *small = (char *)ctx->d_small.p;
-  E3 *tot = (E3 *)small;                 // [0, 24)
-  int32_t *max_rec = (int32_t *)(small + 32);
   int32_t *err = (int32_t *)(small + 36);
   char *d_prefix = small + 256;
   char *d_mid = small + 256 + 4096;
-  HIPCHK(ctx, hipMemsetAsync(small, 0, 64, st));
-  HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
   QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
-  Rec *recs = (Rec *)es.recs.p;
-  E3 *off = (E3 *)es.off.p;
-
   const bool direct = !ctx->emit_lds_only && !ctx->corrupt_on;   // fused corruption uses the LDS-image writer
-  int32_t *overflow = (int32_t *)(small + 40);
-  if (direct) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
-  stage_begin(ctx, "emit_measure");
-  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
-                     rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                     direct ? (uint8_t *)es.slots.p : nullptr, overflow,
-                     getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
-  HIPCHK(ctx, hipGetLastError());
-  stage_end(ctx);
-  stage_begin(ctx, "emit_scan");
-  HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, ctx->scan_partials.p, tot));
-  stage_end(ctx);
+
+  // ---- measure + record offsets (skipped when mh_emit_prepare already ran them for this unit) ----------------------
+  EmitPrep &pp = tp.prep;
+  const bool have_prep = !prepare_only && pp.valid && pp.slot == slot && pp.t_begin == t_begin && pp.t_end == t_end &&
+                         pp.cnt_base == cnt_base && pp.prefix == prefix && pp.mid == mid && pp.direct == direct;
+  if (pp.valid && !have_prep) {   // a stale preparation: its buffer set is free again
+    ctx->eset[pp.set].prepared = false;
+    pp.valid = false;
+  }
+  int32_t set;
   E3 ht;
   int32_t hm4[4] = {0, 0, 0, 0};   // max record length + 20, err, overflow, max slot bytes
-  HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  stage_begin(ctx, "emit");
+  if (have_prep) {
+    set = pp.set;
+    ht = E3{pp.ht.kept, pp.ht.b1, pp.ht.b2};
+    std::memcpy(hm4, pp.hm4, sizeof(hm4));
+    pp.valid = false;
+  } else {
+    // this unit's buffer set; the writer that last read it (N_ESET units ago) must be done before the measure
+    // refills it
+    set = ctx->eset_i;
+    EmitSet &es = ctx->eset[set];
+    if (es.prepared) {
+      stage_end(ctx);
+      return arg_fail(ctx, MH_E_STATE, "more units prepared than emission buffer sets (emit the prepared units first)");
+    }
+    ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
+    if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
+    MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
+    MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
+    E3 *tot = (E3 *)small;                 // [0, 24)
+    int32_t *max_rec = (int32_t *)(small + 32);
+    HIPCHK(ctx, hipMemsetAsync(small, 0, 64, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
+    Rec *recs = (Rec *)es.recs.p;
+    E3 *off = (E3 *)es.off.p;
+    int32_t *overflow = (int32_t *)(small + 40);
+    if (direct) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
+    stage_begin(ctx, "emit_measure");
+    hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
+                       rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
+                       direct ? (uint8_t *)es.slots.p : nullptr, overflow,
+                       getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    stage_begin(ctx, "emit_scan");
+    HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, ctx->scan_partials.p, tot));
+    stage_end(ctx);
+    HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    ht.kept -= cnt_base;
+    if (prepare_only) {
+      stage_end(ctx);
+      pp.valid = true;
+      pp.set = set;
+      pp.slot = slot;
+      pp.t_begin = t_begin;
+      pp.t_end = t_end;
+      pp.cnt_base = cnt_base;
+      pp.prefix = prefix;
+      pp.mid = mid;
+      pp.direct = direct;
+      pp.ht = E3h{ht.kept, ht.b1, ht.b2};
+      std::memcpy(pp.hm4, hm4, sizeof(hm4));
+      es.prepared = true;
+      *out_kept = ht.kept;
+      *out_b1 = ht.b1;
+      *out_b2 = write_fastq2 ? ht.b2 : 0;
+      return MH_OK;
+    }
+  }
+  EmitSet &es = ctx->eset[set];
+  es.prepared = false;
+  const Rec *recs = (const Rec *)es.recs.p;
+  const E3 *off = (const E3 *)es.off.p;
   const int32_t hmax = hm4[0], hslot = hm4[3];
-  ht.kept -= cnt_base;
 
+  // ---- the writer ------------------------------------------------------------------------------------------------
   // arenas: append after what is already there
   const int64_t need1 = ctx->used1 + ht.b1, need2 = ctx->used2 + (write_fastq2 ? ht.b2 : 0);
   MH_TRY(ensure_keep(ctx, ctx->out1, need1 + 64, ctx->used1));
@@ -1143,14 +1188,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
   }
   if (direct && !hover && head_fits && win_stride <= 16 * 4 * ED_WMAX && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
     // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots), queued on the writer
-    // stream: the call returns while it runs, so the next unit's measure pass overlaps it
+    // stream: the call returns while it runs, so the next unit's measure pass and the next job's sampling overlap it
     HIPCHK(ctx, hipEventRecord(ctx->ev_ready, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_ready, 0));
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
-    EdArgs A{hv, m, pos0, pos1, fo0, (const Rec *)recs, (const E3 *)off, (const uint8_t *)es.slots.p,
-             {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
+    EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
              qstride, edbg};
     const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
     auto kfn = write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16> : lpr == 8 ? k_emit_direct<2, 8> : k_emit_direct<2, 4>)
@@ -1162,15 +1206,19 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const cha
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
     HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ctx->wstream));
+    MH_TRY(mark_used(ctx, h.used, h.used_set));     // the haplotype and the templates stay live until then
+    MH_TRY(mark_used(ctx, tp.used, tp.used_set));
     es.busy = true;
     ctx->writer_pending = true;
   } else {
     // LDS-image writer: fallback when a qname's reads part exceeds its slot (synchronous, main stream)
+    HIPCHK(ctx, hipMemsetAsync(small + 32, 0, 16, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
     stage_begin(ctx, "emit_write");
     const int64_t nblk = (m + EW_T - 1) / EW_T;
     hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
-                       pos0, pos1, fo0, rlen, q,
-                       (const Rec *)recs, (const E3 *)off, o1, o2, write_fastq2, cap, win_stride, cc, err);
+                       pos0, pos1, fo0, rlen, q, recs, off, o1, o2, write_fastq2, cap, win_stride, cc, err);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     int32_t herr = 0;

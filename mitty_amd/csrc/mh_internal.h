@@ -51,6 +51,8 @@ constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes
 
 struct Hap {
   bool valid = false;
+  mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
+  mutable bool used_set = false;
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
   DevBuf nd;    // Node16 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
@@ -59,8 +61,25 @@ struct Hap {
 };
 
 // One work unit's templates (illumina.generate_reads output), device-resident.
+// mh_emit_prepare's results for a template set: the measure pass and record offsets already in buffer set `set`
+struct E3h {
+  int64_t kept, b1, b2;
+};
+struct EmitPrep {
+  bool valid = false;
+  int32_t set = -1, slot = -1;
+  int64_t t_begin = 0, t_end = 0, cnt_base = 0;
+  std::string prefix, mid;
+  bool direct = true;
+  E3h ht{0, 0, 0};
+  int32_t hm4[4] = {0, 0, 0, 0};
+};
+
 struct TplSet {
   DevBuf fo0, pos0, pos1;
+  mutable EmitPrep prep;
+  mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
+  mutable bool used_set = false;
   int64_t n = 0;
   int32_t rlen = 0;
   bool valid = false;
@@ -102,12 +121,13 @@ struct StageTime {
 }  // namespace mh
 
 namespace mh {
-// One set of emission buffers (records, offsets, qname reads-part slots).  Two sets alternate so the FASTQ writer of
-// one unit (on the writer stream) overlaps the measure pass of the next (on the main stream).
+// One set of emission buffers (records, offsets, qname reads-part slots).  Sets rotate so the FASTQ writers of earlier
+// units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
   DevBuf recs, off, slots;
   hipEvent_t done = nullptr;   // the last writer that read this set
   bool busy = false;
+  bool prepared = false;       // holds a prepared unit whose writer is not queued yet
 };
 }  // namespace mh
 
@@ -119,7 +139,8 @@ struct mh_ctx {
   hipStream_t wstream = nullptr;
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
-  mh::EmitSet eset[2];
+  static constexpr int N_ESET = 4;   // emission buffer sets in flight (a job's units; the next job's sampling overlaps)
+  mh::EmitSet eset[N_ESET];
   int eset_i = 0;
   hipStream_t stage_stream = nullptr;   // stream the stage timing events go to (nullptr: stream)
   std::string err;
@@ -191,6 +212,9 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep);
 void release(DevBuf &b);
 void release_hap(Hap &h);
 int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer
+// a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
+int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set);
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set);
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);
@@ -216,9 +240,11 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                      int32_t rng_mode, int64_t *out_n);
 
-int32_t emit_reads(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+// FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
+// record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)
+int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
-                   int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
+                   bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept);
 
 int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);

@@ -113,6 +113,7 @@ constexpr int CB_WORDS = 2048;   // circular window of the extended sequence x_i
 constexpr int CB_MASK = CB_WORDS - 1;
 constexpr int JW = 208;          // jump lanes: lane w accumulates state words w, w + 208, w + 416
 constexpr int CB_ZERO = 2 * CB_WORDS;   // 624 zero words: the target of a batch's unused bit slots
+constexpr int JB = 16;                  // set bits per batch of the jump
 
 // The jump W_J[w] = XOR over set bits k of g of x_{k+w} walks the polynomial's bits in increasing k, so x is
 // generated 624 words at a time into a 2048-word circular window just ahead of the bits that need it.  The window
@@ -153,25 +154,25 @@ __global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const u
         }
         G += 624;
       }
-      uint32_t m = gp[pw];
+      uint32_t m = __builtin_amdgcn_readfirstlane(gp[pw]);   // uniform: the bit walk stays in scalar registers
       const int base = kb & CB_MASK;
-      while (m) {   // eight set bits per batch: 24 independent LDS reads in flight
-        int off[8];
+      for (int nleft = __builtin_popcount(m); nleft > 0; nleft -= JB) {   // JB set bits per batch: 3 * JB LDS reads
+        int off[JB];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          off[u] = m ? base + __builtin_ctz(m) : CB_ZERO;
-          m &= m - 1;
+        for (int u = 0; u < JB; u++) {
+          off[u] = u < nleft ? base + __builtin_ctz(m) : CB_ZERO;
+          m &= m - 1u;
         }
-        uint32_t v0[8], v1[8], v2[8];
+        uint32_t v0[JB], v1[JB], v2[JB];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < JB; u++) {
           const uint32_t *q = cb + off[u] + w;
           v0[u] = q[0];
           v1[u] = q[JW];
           v2[u] = q[2 * JW];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < JB; u++) {
           a0 ^= v0[u];
           a1 ^= v1[u];
           a2 ^= v2[u];
@@ -690,24 +691,28 @@ struct StoreTs {
 };
 
 // ---- template length, compaction, file order ----------------------------------------------------------------
+constexpr int TLEN_PER = 8;
 __global__ void __launch_bounds__(256) k_tlen(int64_t n, const uint32_t *w, const double *cum_tlen, int32_t n_tlen,
                                               int64_t rlen, int64_t p_max, const int64_t *ts, int64_t *te,
                                               uint8_t *keep) {
   extern __shared__ __attribute__((aligned(16))) double s_cum[];
   for (int i = threadIdx.x; i < n_tlen; i += blockDim.x) s_cum[i] = cum_tlen[i];
   __syncthreads();
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  double u = mt_double(w, k);
-  int32_t lo = 0, hi = n_tlen;                        // searchsorted(side='left')
-  while (lo < hi) {
-    int32_t mid = (lo + hi) >> 1;
-    if (s_cum[mid] < u) lo = mid + 1; else hi = mid;
+  // TLEN_PER draws per thread (lane-strided): the table is staged once per TLEN_PER * 256 draws
+  for (int q = 0; q < TLEN_PER; q++) {
+    const int64_t k = ((int64_t)blockIdx.x * TLEN_PER + q) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double u = mt_double(w, k);
+    int32_t lo = 0, hi = n_tlen;                        // searchsorted(side='left')
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (s_cum[mid] < u) lo = mid + 1; else hi = mid;
+    }
+    const int64_t tl = lo < rlen ? rlen : lo;           // tl.clip(rlen)
+    const int64_t e = ts[k] + tl;
+    te[k] = e;
+    keep[k] = e < p_max;
   }
-  int64_t tl = lo < rlen ? rlen : lo;                 // tl.clip(rlen)
-  int64_t e = ts[k] + tl;
-  te[k] = e;
-  keep[k] = e < p_max;
 }
 struct LoadKeep {
   const uint8_t *keep;
@@ -1025,7 +1030,8 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   }
 
   stage_begin(ctx, "sample_tlen_compact");
-  hipLaunchKernelGGL(k_tlen, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 8 * n_tlen, st, n, w_tlen, d_cum, n_tlen,
+  hipLaunchKernelGGL(k_tlen, dim3(grid_for((n + TLEN_PER - 1) / TLEN_PER, 256, INT32_MAX)), dim3(256), 8 * n_tlen, st,
+                     n, w_tlen, d_cum, n_tlen,
                      (int64_t)rlen, u.p_max, ts_use, te, keep);
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
@@ -1081,6 +1087,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     q.j_off = j_total; j_total += q.n + 4;
     n_max = std::max(n_max, q.n);
     TplSet &ts = ctx->tsets[tpl_ids[u]];
+    MH_TRY(wait_unused(ctx, ts.used, ts.used_set));   // a queued FASTQ writer may still read the old templates
     MH_TRY(ensure(ctx, ts.fo0, q.n + 16));
     MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
     MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));

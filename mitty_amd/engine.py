@@ -16,6 +16,8 @@ RNG_MODES = {'mitty': _native.MH_RNG_MITTY, 'philox': _native.MH_RNG_PHILOX}
 
 class Engine:
   SLOTS_PER_REGION = 64
+  EMIT_SETS = 4         # units prepared ahead of their writers (the library's emission buffer sets)
+  TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
 
   def __init__(self, device=0):
     self.ctx = _native.Context(device)
@@ -23,6 +25,7 @@ class Engine:
     self._regions = {}   # ri -> region tuple (contig uploaded)
     self._haps = {}      # (ri, cpy) -> (slot, n_nodes, p_min, p_max)
     self._vsets = {}     # (ri, cpy) -> resident variant set id (upload_variants)
+    self._tpl_base = 0
 
   def close(self):
     self.ctx.close()
@@ -67,16 +70,28 @@ class Engine:
     unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
     """
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-    ns = self.ctx.sample_units(list(range(len(units))), slots, [u[3] for u in units], p, rlen, cum_tlen,
+    # template ids alternate between two ranges per batch, so this batch's sampling never waits for the previous
+    # batch's FASTQ writers (still queued on their own stream) to finish reading theirs
+    base = self._tpl_base
+    self._tpl_base = self.TPL_BATCH - base
+    ns = self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
                                RNG_MODES[rng])
     out = []
-    for k, (ps, ri, cpy, seed) in enumerate(units):
-      self.ctx.use_templates(k)
-      kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
-                                         self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
-      out.append((int(ns[k]), kept, b1, b2))
-      if on_unit is not None:
-        on_unit(ps, int(ns[k]), kept, b1, b2)
+    # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
+    # stream): the writers drain while the caller moves on to the next batch
+    for c0 in range(0, len(units), self.EMIT_SETS):
+      chunk = list(enumerate(units))[c0:c0 + self.EMIT_SETS]
+      for k, (ps, ri, cpy, seed) in chunk:
+        self.ctx.use_templates(base + k)
+        self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
+                              write_fastq2, unit_key=seed)
+      for k, (ps, ri, cpy, seed) in chunk:
+        self.ctx.use_templates(base + k)
+        kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
+                                           self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
+        out.append((int(ns[k]), kept, b1, b2))
+        if on_unit is not None:
+          on_unit(ps, int(ns[k]), kept, b1, b2)
     return out
 
   def run_unit(self, ps, ri, cpy, rng_seed, soa, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
