@@ -318,6 +318,7 @@ struct ChunkJob {
   int64_t n_words;
   int64_t base;            // first word of the chunk
   uint32_t *j;             // the unit's swap-index array
+  int64_t tail;            // 1: part of the unit's tail (k_decode_tail decodes it; count passes skip it)
 };
 
 constexpr int32_t DC_BIG = 1 << 30;
@@ -330,6 +331,14 @@ __device__ void decode_chunk(const ChunkJob *jobs, int32_t c, const int64_t *sta
   const ChunkJob job = jobs[c];
   const int64_t i0 = start[c];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (job.tail) {   // never queued; its count is not needed (the tail follows every bulk chunk of the unit)
+    if (!WRITE && t == 0) {
+      count[c] = 0;
+      margin[2 * c] = -DC_BIG;
+      margin[2 * c + 1] = DC_BIG;
+    }
+    return;
+  }
   if (i0 < 1) {
     if (t == 0) {
       count[c] = 0;
@@ -468,14 +477,14 @@ __global__ void __launch_bounds__(DC_THREADS) k_decode_chunks(const ChunkJob *jo
 
 // After a count pass: per unit, the starts the counts imply (s = n - 1 - accepts before the chunk), and the chunks
 // whose count was taken at a start outside their margin, which are queued for the next pass at the implied start.
-// Tiles of up to DR_TILE chunks never cross a unit: k_decode_tile_sums sums each tile's counts, then
-// k_decode_resolve (one workgroup per tile) adds the unit's earlier tiles as its carry.
-constexpr int DR_THREADS = 1024, DR_PER = 8, DR_TILE = DR_THREADS * DR_PER;
+// Tiles of up to DR_TILE chunks never cross a unit; k_decode_resolve (one workgroup per tile) adds the unit's earlier
+// tiles as its carry.
+constexpr int DR_THREADS = 256, DR_PER = 8, DR_TILE = DR_THREADS * DR_PER;
 struct DecTile {
   int32_t unit, begin, end, first_tile;   // chunks [begin, end); first_tile = the unit's first tile index
 };
 
-__device__ __forceinline__ int64_t block_sum_1024(int64_t v, int64_t *wsum) {
+__device__ __forceinline__ int64_t block_sum_dr(int64_t v, int64_t *wsum) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -487,30 +496,23 @@ __device__ __forceinline__ int64_t block_sum_1024(int64_t v, int64_t *wsum) {
   return tot;
 }
 
-__global__ void __launch_bounds__(DR_THREADS) k_decode_tile_sums(const DecTile *tiles, const int32_t *count,
-                                                                 int64_t *tile_sum, int32_t *n_todo) {
-  __shared__ int64_t wsum[DR_THREADS / 64];
-  const DecTile tl = tiles[blockIdx.x];
-  const int32_t c0 = tl.begin + threadIdx.x * DR_PER;
-  int64_t loc = 0;
-#pragma unroll
-  for (int k = 0; k < DR_PER; k++) loc += c0 + k < tl.end ? count[c0 + k] : 0;
-  const int64_t tot = block_sum_1024(loc, wsum);
-  if (threadIdx.x == 0) {
-    tile_sum[blockIdx.x] = tot;
-    if (blockIdx.x == 0) *n_todo = 0;   // k_decode_resolve (next on the stream) appends to the queue
-  }
-}
-
+// One launch per pass: every tile sums its unit's earlier tiles itself (a unit spans a few tiles), appends the chunks
+// to requeue to *n_todo, and zeroes *n_next, the counter the next pass appends to (the two alternate by pass).
 __global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *tiles, const int64_t *n_draws,
-                                                               const int64_t *tile_sum, const int32_t *count,
-                                                               const int32_t *margin, int64_t *s0, int64_t *s1,
-                                                               int32_t *todo, int32_t *n_todo, int64_t *rem) {
+                                                               const int32_t *count, const int32_t *margin,
+                                                               int64_t *s0, int64_t *s1, int32_t *todo,
+                                                               int32_t *n_todo, int32_t *n_next, int64_t *rem) {
   __shared__ int64_t wsum[DR_THREADS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const DecTile tl = tiles[blockIdx.x];
-  int64_t carry = n_draws[tl.unit] - 1;
-  for (int32_t k = tl.first_tile; k < (int32_t)blockIdx.x; k++) carry -= tile_sum[k];
+  if (blockIdx.x == 0 && t == 0) *n_next = 0;
+  int64_t before = 0;
+  for (int32_t k = tl.first_tile; k < (int32_t)blockIdx.x; k++) {
+    const DecTile e = tiles[k];
+    for (int32_t c = e.begin + t; c < e.end; c += DR_THREADS) before += count[c];
+  }
+  const int64_t carry = n_draws[tl.unit] - 1 - block_sum_dr(before, wsum);
+  __syncthreads();   // wsum is reused by the scan below
   const int32_t c0 = tl.begin + t * DR_PER;
   int32_t cv[DR_PER];
   int64_t loc = 0;
@@ -534,13 +536,23 @@ __global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *ti
 #pragma unroll
   for (int k = 0; k < DR_PER; k++) {
     const int32_t c = c0 + k;
-    if (c >= tl.end) break;
-    const int64_t sv = s > 0 ? s : 0;
-    s1[c] = sv;
-    const int64_t d = sv - s0[c];
-    if (d < margin[2 * c] || d > margin[2 * c + 1]) {
-      s0[c] = sv;
-      todo[atomicAdd(n_todo, 1)] = c;
+    bool requeue = false;
+    if (c < tl.end) {
+      const int64_t sv = s > 0 ? s : 0;
+      s1[c] = sv;
+      const int64_t d = sv - s0[c];
+      if (d < margin[2 * c] || d > margin[2 * c + 1]) {
+        s0[c] = sv;
+        requeue = true;
+      }
+    }
+    // one queue append per wave
+    const uint64_t bal = __ballot(requeue);
+    if (bal) {
+      int32_t q0 = 0;
+      if (lane == 0) q0 = atomicAdd(n_todo, (int32_t)__popcll(bal));
+      q0 = __shfl(q0, 0, 64);
+      if (requeue) todo[q0 + (int32_t)__popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull))] = c;
     }
     s -= cv[k];
   }
@@ -549,6 +561,89 @@ __global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *ti
     const int64_t left = carry - (pre + incl);
     rem[tl.unit] = left < 1 ? 0 : left;
   }
+}
+
+// ---- the tail: a unit's last draws (small i) ----------------------------------------------------------------------
+// Below a few ten thousand draws a chunk's margin is a handful of draws, so every correction upstream requeues it and
+// the count passes would keep running for the tail alone.  Instead the tail is excluded from the passes and decoded
+// here once the bulk has converged: one wave per unit walks the words 256 at a time (4 per lane) from the exact start.
+// Within a step, lane k's words start at draw index i - A_k with A_k = accepts of lanes < k; A is iterated to its fixed
+// point, which is the sequential solution (lane k is exact after k + 1 iterations, so at most 65 iterations).
+struct TailJob {
+  const uint32_t *words;
+  int64_t n_words;
+  int64_t base;           // first word of the tail
+  const int64_t *start;   // exact draw index at `base` (s1 of the unit's first tail chunk)
+  uint32_t *j;
+  int64_t *status;        // draws left undecoded (0 = complete)
+};
+
+constexpr int DT_PER = 4;                 // words per lane per step
+constexpr int DT_STEP = 64 * DT_PER;
+
+__device__ __forceinline__ void tail_load(const TailJob &job, int64_t at, uint32_t (&w)[DT_PER]) {
+  if (at + DT_PER <= job.n_words) {
+    const uint4 q = *(const uint4 *)(job.words + at);   // stream and tail bases are 16-byte aligned
+    w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < DT_PER; e++) w[e] = at + e < job.n_words ? job.words[at + e] : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_decode_tail(const TailJob *jobs) {
+  const TailJob job = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  int64_t i = *job.start;
+  int64_t pos = job.base;
+  uint32_t w[DT_PER], wn[DT_PER];
+  tail_load(job, pos + DT_PER * lane, w);
+  while (i >= 1 && pos < job.n_words) {
+    const int64_t at = pos + DT_PER * lane;
+    tail_load(job, at + DT_STEP, wn);   // next step's words, loaded early
+    const uint32_t m0 = interval_mask((uint32_t)min(i, (int64_t)0xFFFFFFFF));
+    int32_t A = (int32_t)((float)(i + 1) / ((float)m0 + 1.0f) * (float)(DT_PER * lane));
+    uint32_t v[DT_PER];
+    bool acc[DT_PER];
+    int32_t cnt = 0, tot = 0;
+    bool conv = false;
+    for (int it = 0; it < 66; it++) {
+      cnt = 0;
+#pragma unroll
+      for (int e = 0; e < DT_PER; e++) {
+        const int64_t ii = i - A - cnt;
+        v[e] = ii >= 1 ? (w[e] & interval_mask((uint32_t)ii)) : 0u;
+        acc[e] = at + e < job.n_words && ii >= 1 && v[e] <= (uint32_t)ii;
+        cnt += acc[e];
+      }
+      int32_t incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
+      }
+      tot = __shfl(incl, 63, 64);
+      const int32_t A2 = incl - cnt;
+      const bool moved = A2 != A;
+      A = A2;
+      if (__ballot(moved) == 0) {
+        conv = true;
+        break;
+      }
+    }
+    if (!conv) break;   // cannot happen (see above); status != 0 sends the unit to the exact sequential decode
+    int32_t a = 0;
+#pragma unroll
+    for (int e = 0; e < DT_PER; e++) {
+      if (acc[e]) job.j[i - A - a] = v[e];
+      a += acc[e];
+    }
+    i -= tot;
+    pos += DT_STEP;
+#pragma unroll
+    for (int e = 0; e < DT_PER; e++) w[e] = wn[e];
+  }
+  if (lane == 0) *job.status = i < 1 ? 0 : i;
 }
 
 // Sequential-stream variant (exact fallback): MT19937 in LDS fused with the decode, one 640-thread workgroup.
@@ -841,7 +936,8 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   std::vector<int32_t> first(dec.size() + 1, 0);
   for (size_t u = 0; u < dec.size(); u++) {
     first[u] = (int32_t)cj.size();
-    for (int64_t b = 0; b < dec[u].n_words; b += DC_CHUNK) cj.push_back(ChunkJob{dec[u].words, dec[u].n_words, b, dec[u].j});
+    for (int64_t b = 0; b < dec[u].n_words; b += DC_CHUNK)
+      cj.push_back(ChunkJob{dec[u].words, dec[u].n_words, b, dec[u].j, 0});
   }
   first[dec.size()] = (int32_t)cj.size();
   const int64_t C = (int64_t)cj.size();
@@ -869,6 +965,16 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     }
   }
   const int32_t U = (int32_t)dec.size();
+  // the tail of each unit: its chunks from the first one expected to start below MH_DEC_TAIL draws
+  const int64_t tail_at = getenv("MH_DEC_TAIL") ? atoll(getenv("MH_DEC_TAIL")) : (int64_t)1 << 15;
+  std::vector<int32_t> tail_c(U, -1);
+  for (int32_t u = 0; u < U; u++)
+    for (int32_t c = first[u]; c < first[u + 1] && tail_at > 0; c++)
+      if (s0[c] < tail_at) {
+        tail_c[u] = c;
+        for (int32_t k = c; k < first[u + 1]; k++) cj[k].tail = 1;
+        break;
+      }
   const int32_t tile_sz = DR_TILE;
   std::vector<DecTile> tiles;
   for (int32_t u = 0; u < U; u++) {
@@ -877,7 +983,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
       tiles.push_back(DecTile{u, b, std::min(b + tile_sz, first[u + 1]), ft});
   }
   const int32_t T = (int32_t)tiles.size();
-  const size_t bytes = ((sizeof(ChunkJob) * C + 15) / 16) * 16 + 8 * C * 2 + 8 * U * 2 + 8 * (T + 1) +
+  const size_t bytes = ((sizeof(ChunkJob) * C + 15) / 16) * 16 + 8 * C * 2 + 8 * U * 2 + sizeof(TailJob) * U +
                        sizeof(DecTile) * (T + 1) + 4 * C * 2 + 8 * C + 512;
   MH_TRY(ensure(ctx, ctx->dec_buf, bytes));
   char *p = (char *)ctx->dec_buf.p;
@@ -886,20 +992,26 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   int64_t *d_s1 = d_s0 + C;
   int64_t *d_ndraw = d_s1 + C;
   int64_t *d_rem = d_ndraw + U;
-  int64_t *d_tsum = d_rem + U;
-  DecTile *d_tiles = (DecTile *)(d_tsum + T + 1);
+  TailJob *d_tail = (TailJob *)(d_rem + U);
+  DecTile *d_tiles = (DecTile *)(d_tail + U);
   int32_t *d_count = (int32_t *)(d_tiles + T + 1);
   int32_t *d_todo = d_count + C;
   int32_t *d_margin = d_todo + C;
-  int32_t *d_ntodo = d_margin + 2 * C;
+  int32_t *d_ntodo = d_margin + 2 * C;   // two queue counters, alternating by pass
   std::vector<int64_t> ndraw(U);
   for (int32_t u = 0; u < U; u++) ndraw[u] = dec[u].n;
+  std::vector<TailJob> tj;
+  for (int32_t u = 0; u < U; u++)
+    if (tail_c[u] >= 0 && dec[u].n > 0)
+      tj.push_back(TailJob{dec[u].words, dec[u].n_words, cj[tail_c[u]].base, d_s1 + tail_c[u], dec[u].j, dec[u].status});
   HIPCHK(ctx, hipMemcpyAsync(d_jobs, cj.data(), sizeof(ChunkJob) * C, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(d_s0, s0.data(), 8 * C, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(d_tiles, tiles.data(), sizeof(DecTile) * T, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(d_ndraw, ndraw.data(), 8 * U, hipMemcpyHostToDevice, st));
+  if (!tj.empty()) HIPCHK(ctx, hipMemcpyAsync(d_tail, tj.data(), sizeof(TailJob) * tj.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemsetAsync(d_ntodo, 0, 8, st));
   const unsigned grid = (unsigned)std::min<int64_t>(C, 4096);
-  // pass 1 over every chunk, then passes over the queued chunks, PASS_BATCH per host check
+  // pass 1 over every chunk, then passes over the queued chunks (resolve + recount), PASS_BATCH per host check
   constexpr int MAX_PASSES = 64;
   const int PASS_BATCH = getenv("MH_DEC_BATCH") ? std::max(1, atoi(getenv("MH_DEC_BATCH"))) : 8;   // diagnostics
   hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
@@ -909,19 +1021,22 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   bool conv = false;
   int passes = 1;
   while (passes < MAX_PASSES) {
+    int32_t *cur = d_ntodo;
     for (int k = 0; k < PASS_BATCH; k++, passes++) {
-      hipLaunchKernelGGL(k_decode_tile_sums, dim3(T), dim3(DR_THREADS), 0, st, (const DecTile *)d_tiles,
-                         (const int32_t *)d_count, d_tsum, d_ntodo);
+      cur = d_ntodo + (passes & 1);
+      int32_t *nxt = d_ntodo + ((passes + 1) & 1);
+      // the queue shrinks fast: a smaller grid once the first passes are done
+      const unsigned g = passes < 4 ? grid : std::min(grid, 1024u);
       hipLaunchKernelGGL(k_decode_resolve, dim3(T), dim3(DR_THREADS), 0, st, (const DecTile *)d_tiles,
-                         (const int64_t *)d_ndraw, (const int64_t *)d_tsum, (const int32_t *)d_count,
-                         (const int32_t *)d_margin, d_s0, d_s1, d_todo, d_ntodo, d_rem);
-      hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
-                         (const int32_t *)d_todo, (const int32_t *)d_ntodo, (int32_t)C, (const int64_t *)d_s0,
-                         d_count, d_margin);
+                         (const int64_t *)d_ndraw, (const int32_t *)d_count, (const int32_t *)d_margin, d_s0, d_s1,
+                         d_todo, cur, nxt, d_rem);
+      hipLaunchKernelGGL(k_decode_chunks<false>, dim3(g), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
+                         (const int32_t *)d_todo, (const int32_t *)cur, (int32_t)C, (const int64_t *)d_s0, d_count,
+                         d_margin);
     }
     HIPCHK(ctx, hipGetLastError());
     int32_t h_ntodo = -1;
-    HIPCHK(ctx, hipMemcpyAsync(&h_ntodo, d_ntodo, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&h_ntodo, cur, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
                                           h_ntodo, (long long)C);
@@ -949,13 +1064,18 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   }
   ctx->dec_passes = passes;
   if (!conv) return MH_OK;
-  // every start exact now: the write pass, and draws left per unit (0 unless a unit ran out of words)
+  // every bulk start exact now: the write pass, the tails from their exact starts, and draws left per unit (0 unless
+  // a unit ran out of words; a unit with a tail gets it from k_decode_tail)
   hipLaunchKernelGGL(k_decode_chunks<true>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
                      (const int32_t *)nullptr, (const int32_t *)nullptr, (int32_t)C, (const int64_t *)d_s1, d_count,
                      d_margin);
   HIPCHK(ctx, hipGetLastError());
   for (int32_t u = 0; u < U; u++)
-    if (dec[u].n > 0) HIPCHK(ctx, hipMemcpyAsync(dec[u].status, d_rem + u, 8, hipMemcpyDeviceToDevice, st));
+    if (dec[u].n > 0 && tail_c[u] < 0) HIPCHK(ctx, hipMemcpyAsync(dec[u].status, d_rem + u, 8, hipMemcpyDeviceToDevice, st));
+  if (!tj.empty()) {
+    hipLaunchKernelGGL(k_decode_tail, dim3((unsigned)tj.size()), dim3(64), 0, st, (const TailJob *)d_tail);
+    HIPCHK(ctx, hipGetLastError());
+  }
   // j[0] = 0 (the shuffle's unused slot), as k_shuffle_decode2 sets it
   for (size_t u = 0; u < dec.size(); u++)
     if (dec[u].n > 0) HIPCHK(ctx, hipMemsetAsync(dec[u].j, 0, 4, st));

@@ -61,6 +61,21 @@ def test_templates_vs_oracle(native, model, span, seed):
   assert np.array_equal(r[1]['pos'], p1)
 
 
+@pytest.mark.parametrize('tail', ['0', '4096', '300000', '100000000'])
+def test_templates_decode_tail_vs_oracle(native, monkeypatch, tail):
+  """The shuffle decode's tail cutoff (MH_DEC_TAIL: draws below it are decoded by k_decode_tail after the count
+  passes; 0 = no tail, 1e8 = the whole unit) never changes the templates."""
+  from mitty_amd.simulation import illumina
+  from oracle import oracle as O
+  monkeypatch.setenv('MH_DEC_TAIL', tail)
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  rm = illumina.read_model_params(mdl, 30.0)
+  r = illumina.generate_reads(rm, 500, 500 + 12_000_000, 2024)
+  fo, p0, p1 = O.generate_templates(rm['p'], int(rm['rlen']), mdl['cum_tlen'], 500, 500 + 12_000_000, 2024)
+  assert np.array_equal(r[0]['pos'], p0) and np.array_equal(r[1]['pos'], p1)
+  assert np.array_equal(r[0]['file_order'], fo)
+
+
 def test_templates_high_coverage_vs_oracle(native):
   """p close to 0.1 (coverage 60, 2x150 -> passes 4, p = 0.025 ... use a direct p) and tiny rlen."""
   from mitty_amd.simulation import illumina
