@@ -507,9 +507,13 @@ __global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *ti
   const DecTile tl = tiles[blockIdx.x];
   if (blockIdx.x == 0 && t == 0) *n_next = 0;
   int64_t before = 0;
-  for (int32_t k = tl.first_tile; k < (int32_t)blockIdx.x; k++) {
-    const DecTile e = tiles[k];
-    for (int32_t c = e.begin + t; c < e.end; c += DR_THREADS) before += count[c];
+  for (int32_t k = tl.first_tile; k < (int32_t)blockIdx.x; k++) {   // every load of a tile issued back to back
+    const int32_t b = tiles[k].begin + t * DR_PER, e = tiles[k].end;
+    int32_t cb[DR_PER];
+#pragma unroll
+    for (int q = 0; q < DR_PER; q++) cb[q] = b + q < e ? count[b + q] : 0;
+#pragma unroll
+    for (int q = 0; q < DR_PER; q++) before += cb[q];
   }
   const int64_t carry = n_draws[tl.unit] - 1 - block_sum_dr(before, wsum);
   __syncthreads();   // wsum is reused by the scan below
@@ -591,58 +595,64 @@ __device__ __forceinline__ void tail_load(const TailJob &job, int64_t at, uint32
   }
 }
 
+// One 256-word step from draw index i at word pos; false if the fixed point was not reached (cannot happen).
+// Lane counts are 0..4, so their exclusive prefix is three ballots' bit-plane popcounts.
+__device__ __forceinline__ bool tail_step(const TailJob &job, int64_t &i, int64_t pos, const uint32_t (&w)[DT_PER],
+                                          int lane, uint64_t below) {
+  const int64_t at = pos + DT_PER * lane;
+  const uint32_t m0 = interval_mask((uint32_t)min(i, (int64_t)0xFFFFFFFF));
+  int32_t A = (int32_t)((float)(i + 1) / ((float)m0 + 1.0f) * (float)(DT_PER * lane));
+  uint32_t v[DT_PER];
+  bool acc[DT_PER];
+  for (int it = 0; it < 66; it++) {
+    int32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < DT_PER; e++) {
+      const int64_t ii = i - A - cnt;
+      v[e] = ii >= 1 ? (w[e] & interval_mask((uint32_t)ii)) : 0u;
+      acc[e] = at + e < job.n_words && ii >= 1 && v[e] <= (uint32_t)ii;
+      cnt += acc[e];
+    }
+    const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+    const int32_t A2 = (int32_t)(__popcll(b0 & below) + 2 * __popcll(b1 & below) + 4 * __popcll(b2 & below));
+    if (__ballot(A2 != A) == 0) {
+      int32_t a = 0;
+#pragma unroll
+      for (int e = 0; e < DT_PER; e++) {
+        if (acc[e]) job.j[i - A - a] = v[e];
+        a += acc[e];
+      }
+      i -= (int64_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+      return true;
+    }
+    A = A2;
+  }
+  return false;
+}
+
+// Words are prefetched DT_RING steps ahead (a register ring, unrolled so every index is static).
+constexpr int DT_RING = 4;
+
 __global__ void __launch_bounds__(64) k_decode_tail(const TailJob *jobs) {
   const TailJob job = jobs[blockIdx.x];
   const int lane = threadIdx.x;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   int64_t i = *job.start;
   int64_t pos = job.base;
-  uint32_t w[DT_PER], wn[DT_PER];
-  tail_load(job, pos + DT_PER * lane, w);
-  while (i >= 1 && pos < job.n_words) {
-    const int64_t at = pos + DT_PER * lane;
-    tail_load(job, at + DT_STEP, wn);   // next step's words, loaded early
-    const uint32_t m0 = interval_mask((uint32_t)min(i, (int64_t)0xFFFFFFFF));
-    int32_t A = (int32_t)((float)(i + 1) / ((float)m0 + 1.0f) * (float)(DT_PER * lane));
-    uint32_t v[DT_PER];
-    bool acc[DT_PER];
-    int32_t cnt = 0, tot = 0;
-    bool conv = false;
-    for (int it = 0; it < 66; it++) {
-      cnt = 0;
+  uint32_t w[DT_RING][DT_PER];
 #pragma unroll
-      for (int e = 0; e < DT_PER; e++) {
-        const int64_t ii = i - A - cnt;
-        v[e] = ii >= 1 ? (w[e] & interval_mask((uint32_t)ii)) : 0u;
-        acc[e] = at + e < job.n_words && ii >= 1 && v[e] <= (uint32_t)ii;
-        cnt += acc[e];
-      }
-      int32_t incl = cnt;
+  for (int r = 0; r < DT_RING; r++) tail_load(job, pos + (int64_t)r * DT_STEP + DT_PER * lane, w[r]);
+  bool ok = true;
+  while (ok && i >= 1 && pos < job.n_words) {
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t o = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += o;
-      }
-      tot = __shfl(incl, 63, 64);
-      const int32_t A2 = incl - cnt;
-      const bool moved = A2 != A;
-      A = A2;
-      if (__ballot(moved) == 0) {
-        conv = true;
-        break;
-      }
+    for (int r = 0; r < DT_RING; r++) {
+      if (!(ok && i >= 1 && pos < job.n_words)) break;
+      ok = tail_step(job, i, pos, w[r], lane, below);
+      tail_load(job, pos + (int64_t)DT_RING * DT_STEP + DT_PER * lane, w[r]);
+      pos += DT_STEP;
     }
-    if (!conv) break;   // cannot happen (see above); status != 0 sends the unit to the exact sequential decode
-    int32_t a = 0;
-#pragma unroll
-    for (int e = 0; e < DT_PER; e++) {
-      if (acc[e]) job.j[i - A - a] = v[e];
-      a += acc[e];
-    }
-    i -= tot;
-    pos += DT_STEP;
-#pragma unroll
-    for (int e = 0; e < DT_PER; e++) w[e] = wn[e];
   }
+  // !ok cannot happen; i != 0 then sends the unit to the exact sequential decode
   if (lane == 0) *job.status = i < 1 ? 0 : i;
 }
 
