@@ -186,6 +186,9 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   if (pe && atoi(pe) == 0) prio_lo = prio_hi = 0;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
       create_writer_stream(ctx, device, prio_lo) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
@@ -208,6 +211,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->wstream);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   for (auto &kv : ctx->contigs) release(kv.second.seq);
   for (auto &kv : ctx->haps) release_hap(kv.second);
   for (auto &h : ctx->hap_spare) release_hap(h);
@@ -218,7 +222,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   }
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->s) release(b);
-  release(ctx->scan_partials); release(ctx->d_small);
+  for (auto &b : ctx->lane2) release(b);
+  release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
   for (auto &e : ctx->eset) {
@@ -229,6 +234,9 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipEventDestroy(ctx->ev_writer);
   (void)hipStreamDestroy(ctx->wstream);
   bam_release(ctx->bam);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return MH_OK;

@@ -134,6 +134,8 @@ struct EmitSet {
 struct mh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // second sampling lane: per-unit finish stages of odd units run here
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // FASTQ writer stream: mh_emit_reads returns once its writer is queued here; every other entry point first makes
   // the main stream wait for the last queued writer (ev_writer)
   hipStream_t wstream = nullptr;
@@ -167,6 +169,8 @@ struct mh_ctx {
   // scratch (grow-only), reused by all stages
   mh::DevBuf s[16];
   mh::DevBuf scan_partials;
+  mh::DevBuf lane2[8];   // the second lane's copies of s[4..10] and its radix-sort scratch (index 7)
+  mh::DevBuf scan_partials2;
   mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
   mh::DevBuf d_small;        // device small scalars
 

@@ -1096,23 +1096,33 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 
 // Everything after the word streams for one unit: ts (geometric scan), shuffle, tlen + keep + compaction into
 // `out`, file order.  `exact`: materialise the draws and recompute flagged ones on the host (rare path).
+// `lane` 1 runs on the second sampling stream with its own scratch (the units' stages are latency-bound, so two
+// units side by side fill the chip better than one after the other).
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
                     const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
-                    uint32_t *d_flag) {
-  hipStream_t st = ctx->stream;
+                    uint32_t *d_flag, int lane = 0) {
+  hipStream_t st = lane ? ctx->stream2 : ctx->stream;
+  ctx->stage_stream = lane ? ctx->stream2 : nullptr;
+  struct Restore {
+    mh_ctx *c;
+    ~Restore() { c->stage_stream = nullptr; }
+  } restore{ctx};
+  mh::DevBuf *S4 = lane ? ctx->lane2 : ctx->s + 4;   // the lane's s[4..10]
+  mh::DevBuf &perm_tmp = lane ? ctx->lane2[7] : ctx->perm_tmp;
+  void *scan_partials = lane ? ctx->scan_partials2.p : ctx->scan_partials.p;
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
-  int64_t *ts = (int64_t *)ctx->s[4].p, *ts_shuf = (int64_t *)ctx->s[5].p, *te = (int64_t *)ctx->s[6].p;
-  uint8_t *keep = (uint8_t *)ctx->s[7].p;
+  int64_t *ts = (int64_t *)S4[0].p, *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
+  uint8_t *keep = (uint8_t *)S4[3].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
-  int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128);
+  int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128 + 64 * lane);
   const double log_q = std::log(1.0 - p);
   GeoFlags fl{flag_idx, d_flag, 1024};
 
   stage_begin(ctx, "sample_geometric_scan");
   if (!exact) {
     HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1},
-                                         ctx->scan_partials.p, tot));
+                                         scan_partials, tot));
   } else {
     int64_t *g = (int64_t *)ctx->s[12].p;
     uint32_t nflag = 0;
@@ -1132,7 +1142,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
     }
     HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
     HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
-                                     (int64_t *)ctx->scan_partials.p, tot));
+                                     (int64_t *)scan_partials, tot));
   }
   stage_end(ctx);
 
@@ -1140,15 +1150,15 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   if (rng_mode == MH_RNG_MITTY && n > 1) {
     stage_begin(ctx, "sample_permutation");
     // steps sorted by (target, step): keys j, values the step index (stable LSD radix sort over the target's bits)
-    uint32_t *sk = (uint32_t *)ctx->s[8].p, *sv = (uint32_t *)ctx->s[9].p;
-    int32_t *nxt = (int32_t *)ctx->s[10].p;
+    uint32_t *sk = (uint32_t *)S4[4].p, *sv = (uint32_t *)S4[5].p;
+    int32_t *nxt = (int32_t *)S4[6].p;
     unsigned end_bit = 1;
     while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
     size_t tmp = 0;
     const rocprim::counting_iterator<uint32_t> iota(0u);
     HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
-    MH_TRY(ensure(ctx, ctx->perm_tmp, tmp + 256));
-    HIPCHK(ctx, rocprim::radix_sort_pairs(ctx->perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+    MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
+    HIPCHK(ctx, rocprim::radix_sort_pairs(perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
     HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                        (const uint32_t *)sv, nxt);
@@ -1167,7 +1177,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
                                        StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p,
                                                     (int64_t *)u.out->pos1.p, (int64_t)rlen},
-                                       ctx->scan_partials.p, d_m));
+                                       scan_partials, d_m));
   hipLaunchKernelGGL(k_file_order, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const int64_t *)d_m,
                      w_fo, (int8_t *)u.out->fo0.p);
   HIPCHK(ctx, hipGetLastError());
@@ -1235,6 +1245,18 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
   MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
   MH_TRY(ensure(ctx, ctx->s[11], 8 * 1024));
+  const bool two_lanes = n_units > 1 && !getenv("MH_ONE_LANE");   // MH_ONE_LANE: experiments
+  if (two_lanes) {
+    MH_TRY(ensure(ctx, ctx->lane2[0], 8 * nn));
+    MH_TRY(ensure(ctx, ctx->lane2[1], 8 * nn));
+    MH_TRY(ensure(ctx, ctx->lane2[2], 8 * nn));
+    MH_TRY(ensure(ctx, ctx->lane2[3], nn));
+    MH_TRY(ensure(ctx, ctx->lane2[4], 4 * (nn + 1)));
+    MH_TRY(ensure(ctx, ctx->lane2[5], 4 * (nn + 1)));
+    MH_TRY(ensure(ctx, ctx->lane2[6], 4 * nn));
+    MH_TRY(ensure(ctx, ctx->scan_partials2, std::max<size_t>(16 * scan_partials_count(nn + 1) + 64,
+                                                              scan_lb_scratch_bytes<int64_t>(nn + 1))));
+  }
   MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 64));
   MH_TRY(ensure(ctx, ctx->s[1], 64 * (size_t)n_units + 64));          // per-unit m, flags, decode status
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
@@ -1320,10 +1342,19 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   }
 
   // ---- per-unit parallel stages (stream-ordered, shared scratch) ------------------------------------------------
-  for (int32_t u = 0; u < n_units; u++) {
+  // units alternate between the two lanes; the second lane forks after the word streams and joins before readback
+  if (two_lanes) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+  }
+  for (int32_t u = 0, k = 0; u < n_units; u++) {
     if (plan[u].n == 0) continue;
     MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                       d_flags + u));
+                       d_flags + u, two_lanes ? (k++ & 1) : 0));
+  }
+  if (two_lanes) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+    HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
   }
   std::vector<int64_t> hm(n_units), hstat(n_units);
   std::vector<uint32_t> hflag(n_units);
