@@ -537,28 +537,46 @@ __global__ void __launch_bounds__(DR_THREADS) k_decode_resolve(const DecTile *ti
 #pragma unroll
   for (int q = 0; q < DR_THREADS / 64; q++) pre += q < wave ? wsum[q] : 0;
   int64_t s = carry - (pre + incl - loc);
+  // every load first, then one queue append per wave (an atomic round trip per chunk would serialise the kernel)
+  int64_t o0[DR_PER];
+  int32_t mlo[DR_PER], mhi[DR_PER];
+#pragma unroll
+  for (int k = 0; k < DR_PER; k++) {
+    const int32_t c = c0 + k < tl.end ? c0 + k : tl.begin;
+    o0[k] = s0[c];
+    mlo[k] = margin[2 * c];
+    mhi[k] = margin[2 * c + 1];
+  }
+  uint32_t rq = 0;
 #pragma unroll
   for (int k = 0; k < DR_PER; k++) {
     const int32_t c = c0 + k;
-    bool requeue = false;
     if (c < tl.end) {
       const int64_t sv = s > 0 ? s : 0;
       s1[c] = sv;
-      const int64_t d = sv - s0[c];
-      if (d < margin[2 * c] || d > margin[2 * c + 1]) {
+      const int64_t d = sv - o0[k];
+      if (d < mlo[k] || d > mhi[k]) {
         s0[c] = sv;
-        requeue = true;
+        rq |= 1u << k;
       }
     }
-    // one queue append per wave
-    const uint64_t bal = __ballot(requeue);
-    if (bal) {
-      int32_t q0 = 0;
-      if (lane == 0) q0 = atomicAdd(n_todo, (int32_t)__popcll(bal));
-      q0 = __shfl(q0, 0, 64);
-      if (requeue) todo[q0 + (int32_t)__popcll(bal & (lane ? (~0ull >> (64 - lane)) : 0ull))] = c;
-    }
     s -= cv[k];
+  }
+  const int32_t nrq = __popc(rq);
+  int32_t rincl = nrq;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t o = __shfl_up(rincl, d, 64);
+    if (lane >= d) rincl += o;
+  }
+  const int32_t wtot = __shfl(rincl, 63, 64);
+  if (wtot > 0) {
+    int32_t q0 = 0;
+    if (lane == 63) q0 = atomicAdd(n_todo, wtot);
+    q0 = __shfl(q0, 63, 64) + rincl - nrq;
+#pragma unroll
+    for (int k = 0; k < DR_PER; k++)
+      if (rq & (1u << k)) todo[q0++] = c0 + k;
   }
   // the unit's last tile: draws left after its last chunk
   if (t == DR_THREADS - 1 && (blockIdx.x + 1 == gridDim.x || tiles[blockIdx.x + 1].unit != tl.unit)) {
