@@ -33,8 +33,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
-  ap.add_argument('--steps', type=int, default=3)
-  ap.add_argument('--warmup', type=int, default=1)
+  ap.add_argument('--steps', type=int, default=10)
+  ap.add_argument('--warmup', type=int, default=2)
   ap.add_argument('--model', default='hiseq-X-v2.5-Garvan')
   ap.add_argument('--coverage', type=float, default=30.0)
   ap.add_argument('--length', type=int, default=CHR1)
