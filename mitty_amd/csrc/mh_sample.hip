@@ -318,7 +318,8 @@ struct ChunkJob {
   int64_t n_words;
   int64_t base;            // first word of the chunk
   uint32_t *j;             // the unit's swap-index array
-  int64_t tail;            // 1: part of the unit's tail (k_decode_tail decodes it; count passes skip it)
+  int32_t tail;            // 1: part of the unit's tail (k_decode_tail decodes it; count passes skip it)
+  int32_t size;            // words in the chunk (a multiple of 64, at most DC_CHUNK)
 };
 
 constexpr int32_t DC_BIG = 1 << 30;
@@ -358,7 +359,7 @@ __device__ void decode_chunk(const ChunkJob *jobs, int32_t c, const int64_t *sta
     for (int e = 0; e < DC_PER; e++) w[e] = base + DC_PER * t + e < job.n_words ? job.words[base + DC_PER * t + e] : 0u;
   }
 #pragma unroll
-  for (int e = 0; e < DC_PER; e++) valid[e] = base + DC_PER * t + e < job.n_words;
+  for (int e = 0; e < DC_PER; e++) valid[e] = DC_PER * t + e < job.size && base + DC_PER * t + e < job.n_words;
   // first guess of the accepts before this thread's words: the acceptance rate at i0
   const uint32_t m0 = interval_mask((uint32_t)i0);
   int32_t A = (int32_t)((float)(i0 + 1) / ((float)m0 + 1.0f) * (float)(DC_PER * t));
@@ -404,7 +405,7 @@ __device__ void decode_chunk(const ChunkJob *jobs, int32_t c, const int64_t *sta
     if (t == 0) {
       int64_t ii = i0;
       int64_t lo = -DC_BIG, hi = DC_BIG;
-      for (int64_t k = 0; k < DC_CHUNK && base + k < job.n_words; k++) {
+      for (int64_t k = 0; k < job.size && base + k < job.n_words; k++) {
         if (ii < 1) { hi = 0; break; }
         const uint32_t m = interval_mask((uint32_t)ii);
         const uint32_t vv = job.words[base + k] & m;
@@ -960,27 +961,24 @@ struct UnitPlan {
 int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_status, bool *done) {
   hipStream_t st = ctx->stream;
   *done = false;
+  // Chunks shrink with the draw index: a chunk's margin (in draws) is about mask(i) / its words, so sizing chunks as
+  // i / MH_DEC_DIV words (a power of two, MH_DEC_MINW .. DC_CHUNK) keeps margins from collapsing as i falls.
+  // Starts: the exact one for each unit's first chunk, then the expected accepts (rate (i+1)/(mask+1)).
+  const int64_t div = getenv("MH_DEC_DIV") ? std::max(1LL, atoll(getenv("MH_DEC_DIV"))) : 128;
+  const int64_t minw = getenv("MH_DEC_MINW") ? std::min<int64_t>(DC_CHUNK, std::max(64LL, atoll(getenv("MH_DEC_MINW"))))
+                                             : 64;
   std::vector<ChunkJob> cj;
+  std::vector<int64_t> s0;
   std::vector<int32_t> first(dec.size() + 1, 0);
   for (size_t u = 0; u < dec.size(); u++) {
     first[u] = (int32_t)cj.size();
-    for (int64_t b = 0; b < dec[u].n_words; b += DC_CHUNK)
-      cj.push_back(ChunkJob{dec[u].words, dec[u].n_words, b, dec[u].j, 0});
-  }
-  first[dec.size()] = (int32_t)cj.size();
-  const int64_t C = (int64_t)cj.size();
-  if (C == 0) {
-    *done = true;
-    return MH_OK;
-  }
-  // starts: the exact one for each unit's first chunk, then the expected accepts (rate (i+1)/(mask+1))
-  std::vector<int64_t> s0(C);
-  for (size_t u = 0; u < dec.size(); u++) {
     double i = (double)(dec[u].n - 1);
-    for (int32_t c = first[u]; c < first[u + 1]; c++) {
-      s0[c] = i >= 1.0 ? (int64_t)llround(i) : 0;
-      if (c == first[u]) s0[c] = dec[u].n - 1;
-      double rem = DC_CHUNK;
+    for (int64_t b = 0; b < dec[u].n_words;) {
+      int64_t size = DC_CHUNK;
+      while (size > minw && (double)size * (double)div > i) size >>= 1;
+      cj.push_back(ChunkJob{dec[u].words, dec[u].n_words, b, dec[u].j, 0, (int32_t)size});
+      s0.push_back(b == 0 ? dec[u].n - 1 : (i >= 1.0 ? (int64_t)llround(i) : 0));
+      double rem = (double)size;
       while (rem > 0 && i >= 1.0) {   // integrate the acceptance rate piecewise over mask epochs
         uint32_t ii = (uint32_t)i, m = ii;
         m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
@@ -990,11 +988,18 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
         if (need >= rem) { i -= rem * rate; rem = 0; }
         else { i = lo - 1.0; rem -= need; }
       }
+      b += size;
     }
+  }
+  first[dec.size()] = (int32_t)cj.size();
+  const int64_t C = (int64_t)cj.size();
+  if (C == 0) {
+    *done = true;
+    return MH_OK;
   }
   const int32_t U = (int32_t)dec.size();
   // the tail of each unit: its chunks from the first one expected to start below MH_DEC_TAIL draws
-  const int64_t tail_at = getenv("MH_DEC_TAIL") ? atoll(getenv("MH_DEC_TAIL")) : (int64_t)1 << 15;
+  const int64_t tail_at = getenv("MH_DEC_TAIL") ? atoll(getenv("MH_DEC_TAIL")) : (int64_t)1 << 15;   // TODO tune
   std::vector<int32_t> tail_c(U, -1);
   for (int32_t u = 0; u < U; u++)
     for (int32_t c = first[u]; c < first[u + 1] && tail_at > 0; c++)

@@ -218,8 +218,10 @@ def generate_unit(ref_seq, region_start0, vl, p, rlen, cum_tlen, rng_seed, seria
   return n, b1, b2
 
 
-def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, serial_stub, chrom, cpy):
-  """generate_unit for variants already in structure-of-arrays form (pos, op, oplen, alt_off, alt_len, alt_pool)."""
+def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, serial_stub, chrom, cpy,
+                      keep_output=True):
+  """generate_unit for variants already in structure-of-arrays form (pos, op, oplen, alt_off, alt_len, alt_pool).
+  keep_output=False frees the FASTQ bytes without copying them into Python (timing runs: no GIL-held copy)."""
   pos = np.ascontiguousarray(soa['pos'], dtype=np.int64)
   op = np.ascontiguousarray(soa['op'], dtype=np.uint8)
   oplen = np.ascontiguousarray(soa['oplen'], dtype=np.int64)
@@ -235,8 +237,8 @@ def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, 
                              pool, len(pos), p, rlen, _p(cum_tlen), len(cum_tlen), rng_seed, serial_stub.encode(),
                              chrom.encode(), cpy, ctypes.byref(o1), ctypes.byref(l1), ctypes.byref(o2),
                              ctypes.byref(l2))
-  b1 = ctypes.string_at(o1, l1.value) if l1.value else b''
-  b2 = ctypes.string_at(o2, l2.value) if l2.value else b''
+  b1 = ctypes.string_at(o1, l1.value) if l1.value and keep_output else b''
+  b2 = ctypes.string_at(o2, l2.value) if l2.value and keep_output else b''
   lib().mo_free(o1)
   lib().mo_free(o2)
   return n, b1, b2

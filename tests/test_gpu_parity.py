@@ -61,13 +61,16 @@ def test_templates_vs_oracle(native, model, span, seed):
   assert np.array_equal(r[1]['pos'], p1)
 
 
-@pytest.mark.parametrize('tail', ['0', '4096', '300000', '100000000'])
-def test_templates_decode_tail_vs_oracle(native, monkeypatch, tail):
+@pytest.mark.parametrize('tail,div', [('0', '1'), ('0', '128'), ('4096', '512'), ('300000', '128'),
+                                      ('100000000', '128')])
+def test_templates_decode_tail_vs_oracle(native, monkeypatch, tail, div):
   """The shuffle decode's tail cutoff (MH_DEC_TAIL: draws below it are decoded by k_decode_tail after the count
-  passes; 0 = no tail, 1e8 = the whole unit) never changes the templates."""
+  passes; 0 = no tail, 1e8 = the whole unit) and chunk sizing (MH_DEC_DIV: chunk words ~ i / div) never change the
+  templates."""
   from mitty_amd.simulation import illumina
   from oracle import oracle as O
   monkeypatch.setenv('MH_DEC_TAIL', tail)
+  monkeypatch.setenv('MH_DEC_DIV', div)
   mdl = G.model('hiseq-X-v2.5-Garvan')
   rm = illumina.read_model_params(mdl, 30.0)
   r = illumina.generate_reads(rm, 500, 500 + 12_000_000, 2024)
