@@ -121,7 +121,9 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
                       int64_t *out_bytes2);
 /* The first half of mh_emit_reads for the current template set: the measure pass and record offsets, with the same
  * outputs.  The next mh_emit_reads of the same unit (same slot and names) only queues the writer, so a caller that
- * prepares a batch of units first (at most 4 at a time) queues their writers back to back and moves on. */
+ * prepares a batch of units first (at most 4 at a time) queues their writers back to back and moves on.
+ * out_kept, out_b1 and out_b2 may all be NULL: the call then returns without waiting for the measure pass (no host
+ * round trip between a batch's passes); the totals are read back when the unit's mh_emit_reads queues its writer. */
 int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                         int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 /* A slice of a unit for multi-GPU sharding: emit only templates [t_begin, t_end) of the current

@@ -370,9 +370,14 @@ class Context:
     return fo0[:m], p0[:m], p1[:m]
 
   # ---- emission ----------------------------------------------------------------------------------------
-  def emit_prepare(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+  def emit_prepare(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, wait=True):
     """The measure pass and record offsets of the current templates (the next emit_reads of the same unit only
-    queues the writer).  Returns (kept, bytes1, bytes2)."""
+    queues the writer).  Returns (kept, bytes1, bytes2); with wait=False it returns None at once, without waiting
+    for the pass (emit_reads reads its totals)."""
+    if not wait:
+      self._chk(self._L.mh_emit_prepare(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                        1 if write_fastq2 else 0, int(unit_key), None, None, None))
+      return None
     k, b1, b2 = c_i64(), c_i64(), c_i64()
     self._chk(self._L.mh_emit_prepare(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
                                       1 if write_fastq2 else 0, int(unit_key), ctypes.byref(k), ctypes.byref(b1),

@@ -194,7 +194,10 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
       [&] {
         for (auto &e : ctx->eset)
-          if (hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) return true;
+          if (hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&e.rb, hipEventDisableTiming) != hipSuccess ||
+              hipHostMalloc((void **)&e.h_stat, 64 + 8192, hipHostMallocDefault) != hipSuccess)
+            return true;
         return false;
       }()) {
     delete ctx;
@@ -227,8 +230,10 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
   for (auto &e : ctx->eset) {
-    release(e.recs); release(e.off); release(e.slots);
+    release(e.recs); release(e.off); release(e.slots); release(e.stat);
     (void)hipEventDestroy(e.done);
+    if (e.rb) (void)hipEventDestroy(e.rb);
+    if (e.h_stat) (void)hipHostFree(e.h_stat);
   }
   (void)hipEventDestroy(ctx->ev_ready);
   (void)hipEventDestroy(ctx->ev_writer);
@@ -542,7 +547,8 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
   CTX_GUARD_NOJOIN(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
-  if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!serial_stub || !chrom || (!out_kept) != (!out_b1) || (!out_kept) != (!out_b2))
+    return arg_fail(ctx, MH_E_ARG, "null argument");
   return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, true, out_kept,
                     out_b1, out_b2);
 }

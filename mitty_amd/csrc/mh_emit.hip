@@ -1046,9 +1046,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   std::string prefix = std::string("@") + serial_stub + ":";
   std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
   if (prefix.size() + mid.size() > 4000) return arg_fail(ctx, MH_E_ARG, "sample/chrom names too long");
-  *out_kept = 0;
-  *out_b1 = 0;
-  *out_b2 = 0;
+  // prepare_only with null outputs: return without waiting for the measure pass (its totals are read back when the
+  // unit's writer is queued), so a batch's measure passes run back to back with no host round trip between them
+  const bool defer = prepare_only && !out_kept;
+  if (!defer) {
+    *out_kept = 0;
+    *out_b1 = 0;
+    *out_b2 = 0;
+  }
   if (m == 0) return MH_OK;
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   char *small = (char *)ctx->d_small.p;
@@ -1073,8 +1078,17 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   stage_begin(ctx, "emit");
   if (have_prep) {
     set = pp.set;
-    ht = E3{pp.ht.kept, pp.ht.b1, pp.ht.b2};
-    std::memcpy(hm4, pp.hm4, sizeof(hm4));
+    if (pp.deferred) {   // the measure pass's totals, copied to the set's pinned readback
+      const EmitSet &es = ctx->eset[set];
+      HIPCHK(ctx, hipEventSynchronize(es.rb));
+      std::memcpy(&ht, es.h_stat, sizeof(E3));
+      std::memcpy(hm4, (const char *)es.h_stat + 32, sizeof(hm4));
+      ht.kept -= pp.cnt_base;
+      pp.deferred = false;
+    } else {
+      ht = E3{pp.ht.kept, pp.ht.b1, pp.ht.b2};
+      std::memcpy(hm4, pp.hm4, sizeof(hm4));
+    }
     pp.valid = false;
   } else {
     // this unit's buffer set; the writer that last read it (N_ESET units ago) must be done before the measure
@@ -1090,14 +1104,20 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
     MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
     MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
-    E3 *tot = (E3 *)small;                 // [0, 24)
-    int32_t *max_rec = (int32_t *)(small + 32);
-    HIPCHK(ctx, hipMemsetAsync(small, 0, 64, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
+    MH_TRY(ensure(ctx, es.stat, 64));
+    char *stat = (char *)es.stat.p;        // per set: a deferred readback must not see the next unit's totals
+    E3 *tot = (E3 *)stat;                  // [0, 24)
+    int32_t *max_rec = (int32_t *)(stat + 32);
+    HIPCHK(ctx, hipMemsetAsync(stat, 0, 64, st));
+    // staged through the set's pinned block: the call may return before these copies ran (deferred prepare)
+    char *hp = (char *)es.h_stat + 64, *hmid = (char *)es.h_stat + 64 + 4096;
+    std::memcpy(hp, prefix.data(), prefix.size());
+    std::memcpy(hmid, mid.data(), mid.size());
+    HIPCHK(ctx, hipMemcpyAsync(d_prefix, hp, prefix.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_mid, hmid, mid.size(), hipMemcpyHostToDevice, st));
     Rec *recs = (Rec *)es.recs.p;
     E3 *off = (E3 *)es.off.p;
-    int32_t *overflow = (int32_t *)(small + 40);
+    int32_t *overflow = (int32_t *)(stat + 40);
     if (direct) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
     stage_begin(ctx, "emit_measure");
     hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
@@ -1109,10 +1129,16 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_begin(ctx, "emit_scan");
     HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, ctx->scan_partials.p, tot));
     stage_end(ctx);
-    HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    ht.kept -= cnt_base;
+    if (defer) {
+      HIPCHK(ctx, hipMemcpyAsync(es.h_stat, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync((char *)es.h_stat + 32, max_rec, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipEventRecord(es.rb, st));
+    } else {
+      HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      ht.kept -= cnt_base;
+    }
     if (prepare_only) {
       stage_end(ctx);
       pp.valid = true;
@@ -1124,12 +1150,15 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       pp.prefix = prefix;
       pp.mid = mid;
       pp.direct = direct;
-      pp.ht = E3h{ht.kept, ht.b1, ht.b2};
-      std::memcpy(pp.hm4, hm4, sizeof(hm4));
+      pp.deferred = defer;
       es.prepared = true;
-      *out_kept = ht.kept;
-      *out_b1 = ht.b1;
-      *out_b2 = write_fastq2 ? ht.b2 : 0;
+      if (!defer) {
+        pp.ht = E3h{ht.kept, ht.b1, ht.b2};
+        std::memcpy(pp.hm4, hm4, sizeof(hm4));
+        *out_kept = ht.kept;
+        *out_b1 = ht.b1;
+        *out_b2 = write_fastq2 ? ht.b2 : 0;
+      }
       return MH_OK;
     }
   }

@@ -73,6 +73,7 @@ struct EmitPrep {
   bool direct = true;
   E3h ht{0, 0, 0};
   int32_t hm4[4] = {0, 0, 0, 0};
+  bool deferred = false;       // ht / hm4 still in the set's pinned readback (wait on its rb event)
 };
 
 struct TplSet {
@@ -125,6 +126,9 @@ namespace mh {
 // units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
   DevBuf recs, off, slots;
+  DevBuf stat;                 // the measure pass's totals (E3 at 0) and maxima (int32[4] at 32)
+  int64_t *h_stat = nullptr;   // pinned: stat's readback (64 B), then the qname prefix (+64) and mid (+4160) staged
+  hipEvent_t rb = nullptr;     // after that copy
   hipEvent_t done = nullptr;   // the last writer that read this set
   bool busy = false;
   bool prepared = false;       // holds a prepared unit whose writer is not queued yet

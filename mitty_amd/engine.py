@@ -6,6 +6,7 @@ the haplotype is spliced on the device once and kept resident for all of that co
 segments — and then emitted one by one, in the reference's unit order, into the device FASTQ arenas.
 """
 import logging
+import os
 
 from mitty_amd import _native
 
@@ -84,7 +85,7 @@ class Engine:
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
-                              write_fastq2, unit_key=seed)
+                              write_fastq2, unit_key=seed, wait=bool(os.environ.get('MH_PREP_WAIT')))
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),

@@ -1,7 +1,7 @@
 # Interleaved A/B of env settings on the steady-state bench (VARS = space-separated KEY=VAL settings, X=0 = default)
 mkdir -p gpurun_out/ab
 cd "$GRAFT_REPO_ROOT"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in ${VARS}; do
     echo -n "$v: "
     env $v timeout -k 10 120 python bench.py --steps 6 --warmup 2 --no-cpu-baseline 2>/dev/null > gpurun_out/ab/o.log || exit 1

@@ -5,7 +5,7 @@ echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 tail -30 gpurun_out/pytest_gpu.log
 if [ "$rc" = 0 ] || [ "$rc" = 1 ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-  timeout -k 10 400 python bench.py --steps 2 --warmup 1 --cpu-baseline-mbp 20 > gpurun_out/bench.log 2>&1
+  timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1
   echo "smoke/bench rc=$?"
   tail -n 5 gpurun_out/smoke.log gpurun_out/bench.log
 fi
