@@ -7,7 +7,8 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libmitty_hip.so')
+LIB_PATH = (os.environ.get('MH_LIB') or   # MH_LIB: another build of the library (A/B experiments)
+            os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libmitty_hip.so'))
 
 MH_OK, MH_E_ARG, MH_E_HIP, MH_E_OOM, MH_E_CAPACITY, MH_E_COMPLEX_VARIANT, MH_E_SEED, MH_E_STATE, MH_E_NO_DEVICE = \
   0, -1, -2, -3, -4, -5, -6, -7, -8
