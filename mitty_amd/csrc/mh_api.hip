@@ -1,10 +1,12 @@
 // mh_api.hip — the C ABI (include/mitty_hip.h): context, buffers, argument checks, dispatch to the subsystems.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
 #include "mh_bgzf.h"
 #include <vector>
 
+#include "mh_corrupt.h"
 #include "mh_internal.h"
 
 namespace mh {
@@ -622,9 +624,22 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
   std::vector<float> f((size_t)2 * max_bp * n_bq);
   for (size_t i = 0; i < f.size(); i++) f[i] = (float)cum_bq[i];
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, 4 * f.size()));
+  // search guide per row: g[k] = entries < k / CG_BUCKETS (a lower bound for any draw in bucket k, g[k + 1] an upper
+  // one), so the device search covers [g[k], g[k + 1]] instead of the whole row
+  std::vector<uint16_t> guide((size_t)2 * max_bp * (mh::CG_BUCKETS + 1));
+  for (size_t r = 0; r < (size_t)2 * max_bp; r++) {
+    const float *row = f.data() + r * n_bq;
+    for (int k = 0; k <= mh::CG_BUCKETS; k++) {
+      const float thr = (float)k / (float)mh::CG_BUCKETS;   // exact (a power-of-two fraction)
+      guide[r * (mh::CG_BUCKETS + 1) + k] = (uint16_t)(std::lower_bound(row, row + n_bq, thr) - row);
+    }
+  }
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, 4 * f.size() + 2 * guide.size() + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_cum.p, f.data(), 4 * f.size(), hipMemcpyHostToDevice, ctx->stream));
+  ctx->corrupt_guide_off = ((4 * f.size() + 15) / 16) * 16;
+  HIPCHK(ctx, hipMemcpyAsync((char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off, guide.data(), 2 * guide.size(),
+                             hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;

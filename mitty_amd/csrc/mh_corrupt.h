@@ -9,6 +9,8 @@
 
 namespace mh {
 
+constexpr int CG_BUCKETS = 256;   // search-guide buckets per BQ row: bucket k = draws in [k / 256, (k + 1) / 256)
+
 struct CorruptCfg {
   int32_t enable;
   const float *cum;      // [2][max_bp][n_bq] cumulative BQ tables (f32)
@@ -16,6 +18,7 @@ struct CorruptCfg {
   int32_t max_bp, n_bq;
   uint32_t k0, k1, c3;   // Philox key and the constant counter word
   int64_t t_base;        // index of the launch's first template inside its unit (slices: mh_emit_reads_range)
+  const uint16_t *guide = nullptr;   // [2][max_bp][CG_BUCKETS + 1]: entries of the row below k / CG_BUCKETS
 };
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
@@ -36,8 +39,14 @@ __device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, in
   uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ((uint32_t)f << 16) | (uint32_t)n, cc.c3),
                           make_uint2(cc.k0, cc.k1));
   const float u1 = (float)(r.x >> 8) * (1.0f / 16777216.0f);
-  const float *row = cc.cum + ((int64_t)f * cc.max_bp + n) * cc.n_bq;
+  const int64_t ri = (int64_t)f * cc.max_bp + n;
+  const float *row = cc.cum + ri * cc.n_bq;
   int lo = 0, hi = cc.n_bq;                 // np.searchsorted(bq_mat[n, :], U1) (side='left')
+  if (cc.guide) {                           // the answer lies in [g[k], g[k + 1]] for u1's bucket k
+    const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (r.x >> 24);
+    lo = g[0];
+    hi = g[1];
+  }
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
     if (row[mid] < u1) lo = mid + 1; else hi = mid;

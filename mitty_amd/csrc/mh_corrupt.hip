@@ -149,6 +149,7 @@ int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_
   CorruptCfg cc{1, (const float *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
                 ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)key,
                 (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(key >> 32) ^ 0x636f7272u, t_base};
+  cc.guide = (const uint16_t *)((const char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off);
   stage_begin(ctx, "corrupt_write");
   hipLaunchKernelGGL(k_cr_write, dim3(grid_for(T * nf * 64, 256, INT32_MAX)), dim3(256), 0, st, d0, d1,
                      (const CrTpl *)tpl, T, nf, (const Off2 *)off, (char *)ctx->out1.p + ctx->used1,

@@ -182,6 +182,7 @@ struct mh_ctx {
   bool corrupt_on = false;
   mh::DevBuf corrupt_cum, corrupt_phred;
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
+  size_t corrupt_guide_off = 0;   // byte offset of the search guide inside corrupt_cum
   uint64_t corrupt_seed = 0;
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
