@@ -297,13 +297,6 @@ struct QFixed {
   int32_t prefix_len, mid_len;
 };
 
-__device__ __forceinline__ int32_t qname_len_wo_cnt(const QFixed &q, const ReadInfo *r, int64_t rlen) {
-  int32_t n = q.prefix_len + q.mid_len;
-  for (int s = 0; s < 2; s++)
-    n += 2 + 1 + ndig_s(r[s].pos) + 1 + ndig_s(rlen) + 1 + r[s].cigar_len + 1 + r[s].vlist_len;
-  return n;
-}
-
 constexpr int SLOT = 256;   // bytes per template for the reads part of the qname ("|s|pos|rlen|cigar|v,..|...")
 constexpr int MS_STG = 64;    // of which the first MS_STG bytes are staged in LDS by k_emit_measure
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)

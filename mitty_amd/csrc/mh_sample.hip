@@ -46,7 +46,6 @@ static int64_t seg_words() {
   static const int64_t w = getenv("MH_SEG_TWISTS") ? 624 * std::max(1, atoi(getenv("MH_SEG_TWISTS"))) : SEG_WORDS_DEFAULT;
   return w;
 }
-constexpr int EXT_WORDS = 624 * 33;          // x_0 .. x_20591 >= 19936 + 623
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
