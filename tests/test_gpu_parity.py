@@ -392,6 +392,49 @@ def test_pipelined_jobs_match_isolated_runs(native):
   G.check_same(b2, a2, 'fastq2')
 
 
+def test_deferred_prepare_matches_waiting_prepare(native, monkeypatch):
+  """mh_emit_prepare with null outputs (no host round trip; totals read back when the writer is queued) gives the
+  bytes and counts of the waiting form, and the waiting form's returned totals are the writer's."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  L = 3_000_000
+  seq = synth.contig(L, 41)
+  copies = synth.copies_soa(synth.variants(seq, 42))
+  units = [(0, 0, 0, 51), (1, 0, 1, 52), (2, 0, 0, 53), (3, 0, 1, 54)]
+
+  def run(wait):
+    if wait:
+      monkeypatch.setenv('MH_PREP_WAIT', '1')
+    else:
+      monkeypatch.delenv('MH_PREP_WAIT', raising=False)
+    eng = Engine(0)
+    try:
+      eng.load_region(0, ('1', 0, L), seq)
+      res = eng.run_units(units, lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'SYN')
+      return res, eng.ctx.fetch_output()
+    finally:
+      eng.close()
+
+  res_w, (w1, w2) = run(True)
+  res_d, (d1, d2) = run(False)
+  assert res_w == res_d and all(r[1] > 1000 for r in res_w)
+  G.check_same(d1, w1, 'fastq1')
+  G.check_same(d2, w2, 'fastq2')
+  # the waiting form's totals equal what the writer then reports
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('1', 0, L), seq)
+    slot = eng.haplotype(0, 0, copies[0])[0]
+    eng.ctx.sample_units([0], [slot], [51], p, 150, mdl['cum_tlen'])
+    eng.ctx.use_templates(0)
+    got = eng.ctx.emit_prepare(slot, 'SYN:0:0', '1', 0, True, unit_key=51)
+    assert got == eng.ctx.emit_reads(slot, 'SYN:0:0', '1', 0, True, unit_key=51)
+  finally:
+    eng.close()
+
+
 # ---- size-independent properties at full chromosome scale -------------------------------------------------------
 def test_chr1_scale_properties(native):
   """One chr1-sized unit (249 Mbp): every record parses, POS/CIGAR are consistent with the sequence length, every
