@@ -171,7 +171,7 @@ def main():
       'config': {'workload': 'generate-reads chr1 (249,250,621 bp) diploid, {} 2x{} PE, {}x, rng={}{}, '
                              'one chr1-sized chromosome per GPU'.format(a.model, rlen, a.coverage, a.rng,
                                                                          ', +BQ corruption' if a.corrupt else ''),
-                 'model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units_per_gpu': len(units),
+                 'read_model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units_per_gpu': len(units),
                  'templates_per_step': kept_all // a.steps, 'parallelism': 'unit-shard x{}'.format(world)},
       'roofline': {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS,
                    'unit': 'GB/s', 'frac': (achieved / PEAK_HBM_GBS) if achieved else None,
