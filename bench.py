@@ -84,7 +84,7 @@ def main():
   for cpy in range(len(copies)):   # inputs resident in HBM before timing: contig and both copies' variants
     eng.upload_variants(0, cpy, copies[cpy])
   eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if (a.emit_mode or a.corrupt) else 'k_emit_direct'
+  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_direct'
 
   def step():
     # one chr1 job; consecutive jobs pipeline on the device (this job's splice and sampling run while the previous

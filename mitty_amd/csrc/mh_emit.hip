@@ -711,6 +711,8 @@ struct DMeta {
   int32_t sb;        // Q length = offset of the first base
   int32_t bb[2];     // LDS offset of B per file (forward order)
   int32_t S[2];      // bases per file
+  int32_t tb[2];     // LDS offset of the record's T (the shared one, or its own with fused corruption)
+  int32_t tn[2];     // T length: rlen + 4, or S + 4 with corruption (qualities = len(seq))
 };
 
 // 16 bytes at an arbitrary byte offset of the dynamic LDS block: five aligned dword reads + v_alignbyte.  (Offsets,
@@ -759,9 +761,13 @@ struct EdArgs {
   int64_t used[2];
   int32_t rlen, win_stride, head, qstride;
   int32_t dbg;
+  CorruptCfg cc;     // fused BQ corruption (the CR instantiation)
 };
 
-template <int NF, int LPR>
+// CR: fused BQ corruption (illumina.corrupt_template, illumina.py:139-162): after the gathers, every base of B is
+// corrupted in place and the record's own T ('\n+\n' + qualities + '\n') is built in LDS; the output passes then read
+// the record's T instead of the shared one.  Same Philox counters as k_emit_write, so the bytes are identical.
+template <int NF, int LPR, bool CR>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
@@ -776,6 +782,8 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   const bool staged = !(A.dbg & 128);                          // seam chunks via LDS (dbg 128: direct stores)
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;     // T = '\n+\n' + rlen '~' + '\n' (perfect reads, readgenerate.py:229)
+  const int32_t t_stride = ((A.rlen + 4 + 15) / 16) * 16 + 32;   // per-record T with corruption (+ read slack)
+  const int32_t o_tr = ((o_dump + 16 + 15) / 16) * 16;          // CR: per-record T strings [ED_T][NF]
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
 
@@ -836,6 +844,8 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
         // mate 0 reads hap[a, a + S); mate 1 its reverse complement = rc[hap_len - a - S, hap_len - a)
         const int64_t a2 = s ? h.hap_len - a - S : a;
         mt.bb[f] = o_win + (tid * 2 + s) * win_stride + (int32_t)(a2 & 15);
+        mt.tb[f] = CR ? o_tr + (tid * NF + (NF == 2 ? f : 0)) * t_stride : o_t;
+        mt.tn[f] = CR ? S + 4 : TL;
       }
     }
     meta[tid] = mt;
@@ -880,6 +890,27 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   }
   __syncthreads();
   if (A.dbg & 2) return;
+  if constexpr (CR) {   // corrupt B in place, write the record's T
+    const int32_t rl = A.rlen;
+    for (int idx = tid; idx < nt * NF * (rl + 1); idx += ED_THREADS) {
+      const int rr = idx / (rl + 1), n = idx - rr * (rl + 1);
+      const int j = rr / NF, f = rr - j * NF;
+      const DMeta &M = meta[j];
+      if (M.len[f] == 0) continue;
+      const int32_t S = M.S[f];
+      char *T = smem + M.tb[f];
+      if (n == rl) {   // the separators
+        T[0] = '\n'; T[1] = '+'; T[2] = '\n'; T[3 + S] = '\n';
+        continue;
+      }
+      if (n >= S) continue;
+      uint8_t b = (uint8_t)smem[M.bb[f] + n], qq;
+      corrupt_base(A.cc, t0 + j, f, n, b, qq);
+      smem[M.bb[f] + n] = (char)b;
+      T[3 + n] = (char)qq;
+    }
+    __syncthreads();
+  }
 
   // ---- output: LPR lanes per record (record r = file f, template j); passes over the tile's NF * ED_T records ----
   constexpr int RPP = ED_THREADS / LPR;                        // records per pass
@@ -896,7 +927,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     if (L == 0) continue;
     const int32_t rel = M.rel[f];
     const int64_t ga = gbase[f] + rel;                        // arena offset of the record's first byte
-    const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f];
+    const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f], tb = M.tb[f], tn = M.tn[f];
     const int b = q;
     const bool tile_end = rel + L == span[f];
     const int32_t spb = b == 0 ? 0 : b == 1 ? sb : b == 2 ? tl : L;
@@ -908,14 +939,21 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     if (skip) continue;
     const int32_t x0 = (int32_t)((cg << 4) - ga);
     // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
-    const uint4 vp = lds_load16(smem, (uint32_t)(o_t + TL + (x0 < 0 ? x0 : -16)));
+    int32_t pte = o_t + TL;                                   // end of the previous record's T
+    if (CR && x0 < 0 && rel > 0)                              // the previous kept record of this file in the tile
+      for (int pj = j - 1; pj >= 0; pj--)
+        if (meta[pj].len[f] > 0) {
+          pte = meta[pj].tb[f] + meta[pj].tn[f];
+          break;
+        }
+    const uint4 vp = lds_load16(smem, (uint32_t)(pte + (x0 < 0 ? x0 : -16)));
     const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
     int32_t yb = x0 - sb;
     yb = yb < -16 ? -16 : (yb > S ? S : yb);
     const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
     int32_t yt = x0 - tl;
-    yt = yt < -16 ? -16 : (yt > TL ? TL : yt);
-    const uint4 vt = lds_load16(smem, (uint32_t)(o_t + yt));
+    yt = yt < -16 ? -16 : (yt > tn ? tn : yt);
+    const uint4 vt = lds_load16(smem, (uint32_t)(tb + yt));
     uint32_t w[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -944,7 +982,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     const int32_t L = M.len[f];
     const int32_t rel = M.rel[f];
     const int64_t ga = gbase[f] + rel;
-    const int32_t sb = M.sb, tl = sb + M.S[f], qb = M.qb, bb = M.bb[f];
+    const int32_t sb = M.sb, tl = sb + M.S[f], qb = M.qb, bb = M.bb[f], tb = M.tb[f];
     char *const arena = A.arena[f];
     const int64_t c0 = ga >> 4;
     int32_t x0 = (int32_t)((c0 << 4) - ga) + 16 * q;
@@ -953,7 +991,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
-                                 : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : o_t + (x0 - tl)));
+                                 : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : tb + (x0 - tl)));
       const uint4 v = (A.dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
       *(uint4 *)(arena + (cg << 4)) = v;
     }
@@ -1055,7 +1093,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *d_mid = small + 256 + 4096;
   QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
-  const bool direct = !ctx->emit_lds_only && !ctx->corrupt_on;   // fused corruption uses the LDS-image writer
+  // the direct writer (fused corruption too, unless MH_CORRUPT_LDS asks for the LDS-image writer: experiments)
+  const bool direct = !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS"));
 
   // ---- measure + record offsets (skipped when mh_emit_prepare already ran them for this unit) ----------------------
   EmitPrep &pp = tp.prep;
@@ -1200,7 +1239,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   const int32_t qstride = head + ((edbg & 256) ? SLOT : (hslot > 16 ? (hslot + 15) / 16 * 16 : 16)) + 32;
   const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
                        (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16;
+                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16 +
+                       (ctx->corrupt_on ? 16 + (size_t)ED_T * 2 * ((((int32_t)rlen + 4 + 15) / 16) * 16 + 32) : 0);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -1218,10 +1258,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_begin(ctx, "emit_write");
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
     EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
-             qstride, edbg};
+             qstride, edbg, cc};
     const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
-    auto kfn = write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16> : lpr == 8 ? k_emit_direct<2, 8> : k_emit_direct<2, 4>)
-                            : (lpr == 16 ? k_emit_direct<1, 16> : k_emit_direct<1, 8>);
+    auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true> : k_emit_direct<1, 8, true>)
+             : write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16, false>
+                                         : lpr == 8 ? k_emit_direct<2, 8, false> : k_emit_direct<2, 4, false>)
+                            : (lpr == 16 ? k_emit_direct<1, 16, false> : k_emit_direct<1, 8, false>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);

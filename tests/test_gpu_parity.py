@@ -518,6 +518,41 @@ def test_corruption_statistics(native, tmp_path):
     assert not np.any(changed == SA[err])
 
 
+@pytest.mark.parametrize('model', G.MODELS)
+def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model):
+  """Fused corruption in the direct writer (B corrupted in LDS, per-record quality strings) gives the bytes of the
+  LDS-image writer (same Philox counters), golden synthetic genome with lowercase / IUPAC / N bytes included."""
+  from mitty_amd import _native
+  from mitty_amd.engine import Engine
+  from mitty_amd.lib import fasta as mfasta, vcfio
+  mdl = G.model(model)
+  rlen = int(mdl['mean_rlen'])
+  p, _ = _native.read_model_params(rlen, 30.0)
+  vdf = vcfio.load_variants_soa(G.path('data/syn.vcf'), 'S1', G.path('data/syn.bed'))
+  seqs = mfasta.read_fasta(G.path('data/syn.fa'))
+  outs = []
+  for lds in (False, True):
+    if lds:
+      monkeypatch.setenv('MH_CORRUPT_LDS', '1')
+    else:
+      monkeypatch.delenv('MH_CORRUPT_LDS', raising=False)
+    eng = Engine(0)
+    try:
+      eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 9)
+      for ri in range(len(vdf)):
+        chrom, s0, e = vdf[ri]['region']
+        eng.load_region(ri, vdf[ri]['region'], mfasta.fetch(seqs, chrom, s0, e))
+        for cpy in range(len(vdf[ri]['copies'])):
+          eng.run_unit(ri, ri, cpy, 1000 + 10 * ri + cpy, vdf[ri]['copies'][cpy], p, rlen, mdl['cum_tlen'], 'S1')
+      outs.append(eng.ctx.fetch_output())
+    finally:
+      eng.close()
+  (d1, d2), (l1, l2) = outs
+  assert len(d1) > 10000
+  G.check_same(d1, l1, 'fastq1')
+  G.check_same(d2, l2, 'fastq2')
+
+
 # ---- multi-GPU slices (SURVEY.md §8(e)) ---------------------------------------------------------------------------
 @pytest.mark.parametrize('corrupt', [False, True])
 def test_emit_slices_concatenate_to_unit(native, corrupt):
