@@ -35,17 +35,16 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
-// illumina.corrupt_single_read for one base (illumina.py:155-160), Philox-driven.
-__device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, int f, int n, uint8_t &b, uint8_t &q) {
-  t += cc.t_base;
-  uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ((uint32_t)f << 16) | (uint32_t)n, cc.c3),
-                          make_uint2(cc.k0, cc.k1));
-  const float u1 = (float)(r.x >> 8) * (1.0f / 16777216.0f);
+// illumina.corrupt_single_read (illumina.py:155-160) for bases n0 and n0 + 1 (n0 even; cnt = 1 or 2 of them),
+// Philox-driven: one draw per pair, counter (t, f, n0 / 2): words x, y are base n0's U1 and U2, z, w base n0 + 1's;
+// a substituted base draws its replacement from a second counter (bit 15 of the position word set).
+__device__ __forceinline__ uint32_t corrupt_bq(const CorruptCfg &cc, int f, int n, uint32_t w) {
+  const float u1 = (float)(w >> 8) * (1.0f / 16777216.0f);
   const int64_t ri = (int64_t)f * cc.max_bp + n;
   const float *row = cc.cum + ri * cc.n_bq;
   int lo = 0, hi = cc.n_bq;                 // np.searchsorted(bq_mat[n, :], U1) (side='left')
   if (cc.guide) {                           // the answer lies in [g[k], g[k + 1]] for u1's bucket k
-    const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (r.x >> 24);
+    const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (w >> 24);
     lo = g[0];
     hi = g[1];
   }
@@ -53,14 +52,36 @@ __device__ __forceinline__ void corrupt_base(const CorruptCfg &cc, int64_t t, in
     int mid = (lo + hi) >> 1;
     if (row[mid] < u1) lo = mid + 1; else hi = mid;
   }
-  const int bq = lo < 93 ? lo : 93;
-  const double u2 = (double)r.y * (1.0 / 4294967296.0);
-  if (u2 < cc.phred[bq]) {
-    const uint32_t ch = __umulhi(r.z, 3u);  // randint(0, 3)
-    const char *rot = b == 'A' ? "CTG" : b == 'C' ? "ATG" : b == 'T' ? "ACG" : b == 'G' ? "ACT" : "NNN";
-    b = (uint8_t)rot[ch];
+  return lo < 93 ? lo : 93;
+}
+
+__device__ __forceinline__ void corrupt_pair(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
+                                             uint8_t *q) {
+  t += cc.t_base;
+  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 1);
+  const uint2 key = make_uint2(cc.k0, cc.k1);
+  const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
+  const uint32_t wu1[2] = {r.x, r.z}, wu2[2] = {r.y, r.w};
+  bool sub[2] = {false, false};
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    if (i >= cnt) break;
+    const uint32_t bq = corrupt_bq(cc, f, n0 + i, wu1[i]);
+    sub[i] = (double)wu2[i] * (1.0 / 4294967296.0) < cc.phred[bq];
+    q[i] = (uint8_t)(bq + 33);
   }
-  q = (uint8_t)(bq + 33);
+  if (sub[0] || sub[1]) {   // rare: the replacement bases (randint(0, 3))
+    const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
+    const uint32_t wc[2] = {c.x, c.y};
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      if (!sub[i]) continue;
+      const uint32_t ch = __umulhi(wc[i], 3u);
+      const uint8_t x = b[i];
+      const char *rot = x == 'A' ? "CTG" : x == 'C' ? "ATG" : x == 'T' ? "ACG" : x == 'G' ? "ACT" : "NNN";
+      b[i] = (uint8_t)rot[ch];
+    }
+  }
 }
 
 }  // namespace mh

@@ -7,7 +7,7 @@
 //
 // The reference sends (file 1's name, seq1[, seq2]) to corrupt_template (readcorrupt.py:53-54, illumina.py:113-127)
 // and writes '@{name}\n{seq}\n+\n{bq}\n' per mate (readcorrupt.py:112-114): both output files carry file 1's name,
-// the mate index selects the BQ table, the input qualities are dropped.  Each base goes through corrupt_base
+// the mate index selects the BQ table, the input qualities are dropped.  Each base pair goes through corrupt_pair
 // (mh_corrupt.h) counted by (template index in the whole input, file, base).
 #include "mh_corrupt.h"
 #include "mh_internal.h"
@@ -93,11 +93,16 @@ __global__ void __launch_bounds__(256) k_cr_write(const uint8_t *b0, const uint8
     ds[L] = '\n'; ds[L + 1] = '+'; ds[L + 2] = '\n';
     dq[L] = '\n';
   }
-  for (int32_t k = lane; k < L; k += 64) {
-    uint8_t b = sq[k], qq;
-    corrupt_base(cc, t, f, k, b, qq);
-    ds[k] = (char)b;
-    dq[k] = (char)qq;
+  for (int32_t k = 2 * lane; k < L; k += 128) {   // base pairs: one Philox draw each
+    const int cnt = L - k > 1 ? 2 : 1;
+    uint8_t b[2] = {sq[k], cnt > 1 ? sq[k + 1] : (uint8_t)0}, qq[2];
+    corrupt_pair(cc, t, f, k, cnt, b, qq);
+    ds[k] = (char)b[0];
+    dq[k] = (char)qq[0];
+    if (cnt > 1) {
+      ds[k + 1] = (char)b[1];
+      dq[k + 1] = (char)qq[1];
+    }
   }
 }
 

@@ -639,14 +639,21 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
       char *d = d0 + mt.qlen;                         // '\n' seq '\n+\n' qual '\n'
       const uint8_t *w = wins + mt.win[s];
       const int64_t t = sb + j;
-      for (int n = lane; n < S; n += 64) {
-        uint8_t b = s ? comp(w[S - 1 - n]) : w[n];
-        if (cc.enable) {
-          uint8_t qq;
-          corrupt_base(cc, t, f, n, b, qq);
-          d[4 + S + n] = (char)qq;
+      if (cc.enable) {
+        for (int n = 2 * lane; n < S; n += 128) {   // base pairs: one Philox draw each
+          const int cnt = S - n > 1 ? 2 : 1;
+          uint8_t b[2] = {s ? comp(w[S - 1 - n]) : w[n], 0}, qq[2];
+          if (cnt > 1) b[1] = s ? comp(w[S - 2 - n]) : w[n + 1];
+          corrupt_pair(cc, t, f, n, cnt, b, qq);
+          d[1 + n] = (char)b[0];
+          d[4 + S + n] = (char)qq[0];
+          if (cnt > 1) {
+            d[2 + n] = (char)b[1];
+            d[5 + S + n] = (char)qq[1];
+          }
         }
-        d[1 + n] = (char)b;
+      } else {
+        for (int n = lane; n < S; n += 64) d[1 + n] = (char)(s ? comp(w[S - 1 - n]) : w[n]);
       }
       if (!cc.enable)
         for (int n = lane; n < Q; n += 64) d[4 + S + n] = '~';
@@ -892,22 +899,30 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   if (A.dbg & 2) return;
   if constexpr (CR) {   // corrupt B in place, write the record's T
     const int32_t rl = A.rlen;
-    for (int idx = tid; idx < nt * NF * (rl + 1); idx += ED_THREADS) {
-      const int rr = idx / (rl + 1), n = idx - rr * (rl + 1);
+    const int rp = (rl + 1) / 2 + 1;   // base pairs per record, then the separators
+    for (int idx = tid; idx < nt * NF * rp; idx += ED_THREADS) {
+      const int rr = idx / rp, k = idx - rr * rp;
       const int j = rr / NF, f = rr - j * NF;
       const DMeta &M = meta[j];
       if (M.len[f] == 0) continue;
       const int32_t S = M.S[f];
       char *T = smem + M.tb[f];
-      if (n == rl) {   // the separators
+      if (k == rp - 1) {   // the separators
         T[0] = '\n'; T[1] = '+'; T[2] = '\n'; T[3 + S] = '\n';
         continue;
       }
+      const int n = 2 * k;
       if (n >= S) continue;
-      uint8_t b = (uint8_t)smem[M.bb[f] + n], qq;
-      corrupt_base(A.cc, t0 + j, f, n, b, qq);
-      smem[M.bb[f] + n] = (char)b;
-      T[3 + n] = (char)qq;
+      const int cnt = S - n > 1 ? 2 : 1;
+      char *B = smem + M.bb[f] + n;
+      uint8_t b[2] = {(uint8_t)B[0], cnt > 1 ? (uint8_t)B[1] : (uint8_t)0}, qq[2];
+      corrupt_pair(A.cc, t0 + j, f, n, cnt, b, qq);
+      B[0] = (char)b[0];
+      T[3 + n] = (char)qq[0];
+      if (cnt > 1) {
+        B[1] = (char)b[1];
+        T[4 + n] = (char)qq[1];
+      }
     }
     __syncthreads();
   }
