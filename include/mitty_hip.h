@@ -12,12 +12,13 @@
  *   mh_upload_variants    (the same copy's variant list, kept resident; mh_build_haplotype_vset splices from it)
  *   mh_sample_templates   illumina.generate_reads                        mitty/simulation/illumina.py:43-110
  *   mh_sample_units       (the same for many units: the worker pool of readgenerate.py:102-115)
- *   mh_set_templates      (the template arrays a read module returns)   mitty/simulation/illumina.py:238-269
+ *   mh_set_templates      (the template arrays a read module returns)   mitty/simulation/illumina.py:79-110
  *   mh_get_templates      (same arrays back to the host)
  *   mh_emit_reads         read_generating_worker loop + fastq_lines      mitty/simulation/readgenerate.py:184-230
  *   mh_read_batch         rpc.get_begin_end_nodes + rpc.generate_read    mitty/simulation/rpc.py:119-160
- *   mh_set_corruption     illumina.corrupt_template (Philox mode)        mitty/simulation/illumina.py:113-162
- *                         + readcorrupt.multi_process's worker loop        mitty/simulation/readcorrupt.py:73-93
+ *   mh_set_corruption     illumina.corrupt_template / corrupt_single_read mitty/simulation/illumina.py:113-162
+ *   mh_set_corruption_stream  corrupt_rng = RandomState(seed) of a worker  mitty/simulation/readcorrupt.py:84
+ *   mh_corrupt_fastq      readcorrupt.multi_process's reader/worker/writer  mitty/simulation/readcorrupt.py:18-118
  *   mh_work_units         readgenerate.get_data_for_workers              mitty/simulation/readgenerate.py:129-159
  *   mh_read_model_params  illumina.read_model_params                     mitty/simulation/illumina.py:12-40
  *
@@ -202,15 +203,27 @@ int32_t mh_bgzf_eof(char *out28);
 int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
                          int64_t *used1, int64_t *used2, int64_t *templates);
 
-/* ---- corruption (Philox mode) -------------------------------------------------------------------------- */
+/* ---- corruption -------------------------------------------------------------------------------------- */
 /* Configure the empirical-BQ corruption (illumina.corrupt_template, illumina.py:113-162) that mh_emit_reads then
- * applies while it writes each record: per base bq = min(searchsorted(cum_bq[file][n], U1), 93), the base replaced
- * by one of the other three ('NNN' for non-ACGT) when U2 < phred_p[bq], quality chr(bq + 33) instead of '~'.
- * U1/U2/choice come from Philox4x32-10 keyed by (seed, unit_key) and counted by (template, file, base), so the
- * output does not depend on GPU count or launch geometry.  cum_bq: f64[2][max_bp][n_bq]; phred_p: f64[100]
- * (pass the reference's own 10 ** (-arange(100) / 10)).  enable = 0 turns it off. */
+ * applies while it writes each record, and that mh_corrupt_fastq applies to existing FASTQ: per base
+ * bq = min(searchsorted(cum_bq[file][n], U1), 93) over the f64 table, the base replaced by one of the other three
+ * ('NNN' for non-ACGT) when U2 < phred_p[bq], quality chr(bq + 33) instead of '~'.  U1, U2 are 53-bit doubles
+ * built as numpy's rand() builds them.  Their words come from Philox4x32-10 keyed by (seed, unit_key) and counted
+ * by (template, file, base), so the output does not depend on GPU count or launch geometry.  cum_bq:
+ * f64[2][max_bp][n_bq]; phred_p: f64[100] (pass the reference's own 10 ** (-arange(100) / 10)).  enable = 0 turns
+ * it off. */
 int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int32_t max_bp, int32_t n_bq,
                           const double *phred_p, uint64_t seed);
+/* Word source of mh_corrupt_fastq (fused emission always uses Philox).  MH_RNG_PHILOX: as above (default).
+ * MH_RNG_MITTY: the reference's exact single-worker stream (readcorrupt.py:84 with processes=1) — one MT19937 stream
+ * consumed template by template, mate 0 then mate 1, per mate rand(n), rand(n), randint(0, 3, n)
+ * (illumina.py:151-153); key624 = NULL starts RandomState(seed) at its first word, otherwise the stream continues
+ * the explicit state (key624, pos) as numpy's RandomState.get_state() gives it.  Later mh_corrupt_fastq calls carry
+ * on from where the previous one stopped. */
+int32_t mh_set_corruption_stream(mh_ctx *ctx, int32_t rng_mode, uint64_t seed, const uint32_t *key624, int32_t pos);
+/* The exact stream's current state (key624 / pos may be NULL) and, for a seeded stream, the words consumed so far
+ * (-1 for an explicit-state stream): RandomState.set_state(('MT19937', key, pos, 0, 0.0)) continues it. */
+int32_t mh_get_corruption_stream(mh_ctx *ctx, uint32_t *key624, int32_t *pos, int64_t *words);
 
 /* ---- timing / profiling hooks ------------------------------------------------------------------------- */
 /* Per-stage device time of the most recent mh_emit_reads / mh_sample_templates / mh_build_haplotype calls,

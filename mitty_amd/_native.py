@@ -19,7 +19,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
-           'mh_read_batch', 'mh_set_corruption', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
+           'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
@@ -101,6 +101,8 @@ def lib():
   _sig(L, 'mh_read_batch', [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64])
   _sig(L, 'mh_set_corruption', [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_u64])
+  _sig(L, 'mh_set_corruption_stream', [c_vp, c_i32, c_u64, c_vp, c_i32])
+  _sig(L, 'mh_get_corruption_stream', [c_vp, c_vp, ctypes.POINTER(c_i32), P_i64])
   _sig(L, 'mh_stage_times', [c_vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_dbl), c_i32,
                              ctypes.POINTER(c_i32)])
   _sig(L, 'mh_enable_timing', [c_vp, c_i32])
@@ -498,6 +500,22 @@ class Context:
     cb = np.ascontiguousarray(cum_bq, dtype=np.float64)
     ph = np.ascontiguousarray(phred_p, dtype=np.float64)
     self._chk(self._L.mh_set_corruption(self._h, 1, _ptr(cb), cb.shape[1], cb.shape[2], _ptr(ph), int(seed)))
+
+  def set_corruption_stream(self, rng_mode, seed=0, key=None, pos=624):
+    """mh_corrupt_fastq's word source: MH_RNG_PHILOX, or MH_RNG_MITTY = the reference's exact MT19937 stream
+    (RandomState(seed) from its first word, or continuing an explicit numpy state (key uint32[624], pos))."""
+    k = None if key is None else np.ascontiguousarray(key, dtype=np.uint32)
+    if k is not None and k.shape != (624,):
+      raise ValueError('MT19937 key must hold 624 words')
+    self._chk(self._L.mh_set_corruption_stream(self._h, int(rng_mode), int(seed), None if k is None else _ptr(k),
+                                               int(pos)))
+
+  def get_corruption_stream(self):
+    """(key uint32[624], pos, words consumed or -1) of the exact corruption stream."""
+    key = np.empty(624, np.uint32)
+    pos, words = c_i32(), c_i64()
+    self._chk(self._L.mh_get_corruption_stream(self._h, _ptr(key), ctypes.byref(pos), ctypes.byref(words)))
+    return key, pos.value, words.value
 
   def enable_timing(self, on=True):
     self._chk(self._L.mh_enable_timing(self._h, 1 if on else 0))

@@ -1,7 +1,7 @@
 """`mitty` command line (reference mitty/cli.py), MI355X build.
 
 Implemented: generate-reads (GPU), corrupt-reads (GPU), god-aligner (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
---rng {mitty,philox}, --corrupt-seed (fused Philox corruption).  Multi-GPU: launch generate-reads under
+--rng {mitty,philox}, --corrupt-seed (fused Philox corruption); on corrupt-reads: --device, --rng {mitty,philox}.  Multi-GPU: launch generate-reads under
 `python -m torch.distributed.run --nproc-per-node N -m mitty_amd.cli generate-reads ...` (one process per GPU,
 RCCL); the output files are identical to the one-GPU run.  Out of scope for this build (not on the
 generate-reads path): filter-variants, filter-bam, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
@@ -107,13 +107,15 @@ def generate_reads(fasta, vcf, sample_name, bed, modelfile, coverage, seed, fast
 @click.option('--fastq2-out', type=click.Path())
 @click.option('--threads', default=2)
 @click.option('--device', default=0, help='HIP device ordinal')
-def read_corruption(modelfile, fastq1_in, fastq1_out, seed, fastq2_in, fastq2_out, threads, device):
+@click.option('--rng', type=click.Choice(['mitty', 'philox']), default='mitty',
+              help='mitty: the reference\'s --threads 1 MT19937 stream, byte for byte; philox: counter-based')
+def read_corruption(modelfile, fastq1_in, fastq1_out, seed, fastq2_in, fastq2_out, threads, device, rng):
   """Apply corruption model to FASTQ file of reads (reference cli.py:144-157)"""
   from mitty_amd.readmodel import get_read_model
   from mitty_amd.simulation import readcorrupt as rc
   read_module, read_model = get_read_model(modelfile)
   rc.multi_process(read_module, read_model, fastq1_in, fastq1_out, fastq2_in, fastq2_out, processes=threads, seed=seed,
-                   device=device)
+                   device=device, rng=rng)
 
 
 @cli.command('god-aligner', short_help='Create a perfect BAM from simulated FASTQs')

@@ -622,22 +622,22 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   if (!cum_bq || !phred_p || max_bp <= 0 || n_bq <= 0 || n_bq > 4096)
     return arg_fail(ctx, MH_E_ARG, "bad corruption model");
   if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
-  std::vector<float> f((size_t)2 * max_bp * n_bq);
-  for (size_t i = 0; i < f.size(); i++) f[i] = (float)cum_bq[i];
+  const size_t nt = (size_t)2 * max_bp * n_bq;
+  // (a NaN entry compares like numpy's searchsorted treats it, as larger than any draw, in both searches)
   // search guide per row: g[k] = entries < k / CG_BUCKETS (a lower bound for any draw in bucket k, g[k + 1] an upper
   // one), so the device search covers [g[k], g[k + 1]] instead of the whole row
   std::vector<uint16_t> guide((size_t)2 * max_bp * (mh::CG_BUCKETS + 1));
   for (size_t r = 0; r < (size_t)2 * max_bp; r++) {
-    const float *row = f.data() + r * n_bq;
+    const double *row = cum_bq + r * n_bq;
     for (int k = 0; k <= mh::CG_BUCKETS; k++) {
-      const float thr = (float)k / (float)mh::CG_BUCKETS;   // exact (a power-of-two fraction)
+      const double thr = (double)k / (double)mh::CG_BUCKETS;   // exact (a power-of-two fraction)
       guide[r * (mh::CG_BUCKETS + 1) + k] = (uint16_t)(std::lower_bound(row, row + n_bq, thr) - row);
     }
   }
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, 4 * f.size() + 2 * guide.size() + 64));
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, 8 * nt + 2 * guide.size() + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
-  HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_cum.p, f.data(), 4 * f.size(), hipMemcpyHostToDevice, ctx->stream));
-  ctx->corrupt_guide_off = ((4 * f.size() + 15) / 16) * 16;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_cum.p, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
+  ctx->corrupt_guide_off = ((8 * nt + 15) / 16) * 16;
   HIPCHK(ctx, hipMemcpyAsync((char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off, guide.data(), 2 * guide.size(),
                              hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
@@ -646,6 +646,54 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   ctx->corrupt_max_bp = max_bp;
   ctx->corrupt_n_bq = n_bq;
   ctx->corrupt_seed = seed;
+  return MH_OK;
+}
+
+int32_t mh_set_corruption_stream(mh_ctx *ctx, int32_t rng_mode, uint64_t seed, const uint32_t *key624, int32_t pos) {
+  CTX_GUARD(ctx);
+  if (rng_mode == MH_RNG_PHILOX) {
+    ctx->cx_mode = 0;
+    return MH_OK;
+  }
+  if (rng_mode != MH_RNG_MITTY) return arg_fail(ctx, MH_E_ARG, "unknown rng mode");
+  if (key624) {
+    if (pos < 0 || pos > 624) return arg_fail(ctx, MH_E_ARG, "MT19937 state position outside 0..624");
+    std::copy(key624, key624 + 624, ctx->cx_key);
+    ctx->cx_kpos = pos;
+    ctx->cx_mode = 2;
+    return MH_OK;
+  }
+  if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
+  ctx->cx_seed = (uint32_t)seed;
+  ctx->cx_pos = 0;
+  ctx->cx_mode = 1;
+  return MH_OK;
+}
+
+int32_t mh_get_corruption_stream(mh_ctx *ctx, uint32_t *key624, int32_t *pos, int64_t *words) {
+  CTX_GUARD(ctx);
+  if (ctx->cx_mode == 0) return arg_fail(ctx, MH_E_STATE, "corruption stream is Philox (no MT19937 state)");
+  if (words) *words = ctx->cx_mode == 1 ? ctx->cx_pos : -1;
+  if (!key624 && !pos) return MH_OK;
+  HostMT h;
+  if (ctx->cx_mode == 1) {   // RandomState(seed) advanced by the words consumed (twists only)
+    h.seed(ctx->cx_seed);
+    for (int64_t left = ctx->cx_pos; left > 0;) {
+      if (h.pos == 624) {
+        h.next();
+        left--;
+        continue;
+      }
+      const int64_t take = std::min<int64_t>(624 - h.pos, left);
+      h.pos += (int)take;
+      left -= take;
+    }
+  } else {
+    std::copy(ctx->cx_key, ctx->cx_key + 624, h.key);
+    h.pos = ctx->cx_kpos;
+  }
+  if (key624) std::copy(h.key, h.key + 624, key624);
+  if (pos) *pos = h.pos;
   return MH_OK;
 }
 

@@ -1,6 +1,12 @@
-// mh_corrupt.h — the empirical-BQ corruption of one base (illumina.corrupt_single_read, illumina.py:139-162) driven
-// by Philox4x32-10, shared by the fused emission (mh_emit.hip) and standalone corrupt-reads (mh_corrupt.hip).
-// Counter = (template index, file, base): output independent of launch geometry, GPU count and slicing.
+// mh_corrupt.h — the empirical-BQ corruption of one base (illumina.corrupt_single_read, illumina.py:140-162),
+// shared by the fused emission (mh_emit.hip) and standalone corrupt-reads (mh_corrupt.hip).
+//
+// Arithmetic is the reference's in both RNG modes: U1, U2 are 53-bit doubles built like numpy's rand()
+// ((a >> 5) * 2^26 + (b >> 6)) / 2^53 from two 32-bit words, bq = min(searchsorted(cum_bq[mate, n, :], U1,
+// side='left'), 93) over the f64 table, substitution when U2 < phred_p[bq] (f64).  Only the word source differs:
+//   Philox mode  words from Philox4x32-10 keyed by (seed, unit), counter (template, file, base): one draw per base;
+//                the replacement base from a second counter, umulhi(word, 3)
+//   exact mode   the reference's own MT19937 stream (mh_corrupt.hip: rand(n), rand(n), randint(0, 3, n) per mate)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -13,7 +19,7 @@ constexpr int CG_BUCKETS = 256;   // search-guide buckets per BQ row: bucket k =
 
 struct CorruptCfg {
   int32_t enable;
-  const float *cum;      // [2][max_bp][n_bq] cumulative BQ tables (f32)
+  const double *cum;     // [2][max_bp][n_bq] cumulative BQ tables (the model's f64 cum_bq_mat)
   const double *phred;   // [100]
   int32_t max_bp, n_bq;
   uint32_t k0, k1, c3;   // Philox key and the constant counter word
@@ -35,51 +41,53 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
-// illumina.corrupt_single_read (illumina.py:155-160) for bases n0 and n0 + 1 (n0 even; cnt = 1 or 2 of them),
-// Philox-driven: one draw per pair, counter (t, f, n0 / 2): words x, y are base n0's U1 and U2, z, w base n0 + 1's;
-// a substituted base draws its replacement from a second counter (bit 15 of the position word set).
-__device__ __forceinline__ uint32_t corrupt_bq(const CorruptCfg &cc, int f, int n, uint32_t w) {
-  const float u1 = (float)(w >> 8) * (1.0f / 16777216.0f);
-  const int64_t ri = (int64_t)f * cc.max_bp + n;
-  const float *row = cc.cum + ri * cc.n_bq;
-  int lo = 0, hi = cc.n_bq;                 // np.searchsorted(bq_mat[n, :], U1) (side='left')
-  if (cc.guide) {                           // the answer lies in [g[k], g[k + 1]] for u1's bucket k
-    const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (w >> 24);
+// numpy's legacy double from two consecutive 32-bit words (random_standard_uniform / rk_double)
+__device__ __forceinline__ double mt_double(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// np.searchsorted(cum_bq[f, n, :], u) (side='left'), clamped to 93 (illumina.py:156); the guide narrows the search
+// to [g[k], g[k + 1]] for u in bucket k (exact: g[k] counts the entries below k / CG_BUCKETS)
+__device__ __forceinline__ uint32_t bq_search(const double *cum, const uint16_t *guide, int32_t max_bp, int32_t n_bq,
+                                              int f, int n, double u) {
+  const int64_t ri = (int64_t)f * max_bp + n;
+  const double *row = cum + ri * n_bq;
+  int lo = 0, hi = n_bq;
+  if (guide) {
+    const uint16_t *g = guide + ri * (CG_BUCKETS + 1) + (int)(u * CG_BUCKETS);
     lo = g[0];
     hi = g[1];
   }
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
-    if (row[mid] < u1) lo = mid + 1; else hi = mid;
+    if (row[mid] < u) lo = mid + 1; else hi = mid;
   }
   return lo < 93 ? lo : 93;
 }
 
+// base_rot.get(b, 'NNN')[c] (illumina.py:131-136, 160)
+__device__ __forceinline__ uint8_t rot_base(uint8_t x, uint32_t c) {
+  const char *rot = x == 'A' ? "CTG" : x == 'C' ? "ATG" : x == 'T' ? "ACG" : x == 'G' ? "ACT" : "NNN";
+  return (uint8_t)rot[c];
+}
+
+// Philox mode: bases n0 and n0 + 1 (cnt = 1 or 2 of them) of file f of template t.  Base n draws counter
+// (t, f, n): words x, y make U1, words z, w make U2; a substituted base draws its replacement from a second counter
+// (bit 15 of the position word set).
 __device__ __forceinline__ void corrupt_pair(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
                                              uint8_t *q) {
   t += cc.t_base;
-  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 1);
   const uint2 key = make_uint2(cc.k0, cc.k1);
-  const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
-  const uint32_t wu1[2] = {r.x, r.z}, wu2[2] = {r.y, r.w};
-  bool sub[2] = {false, false};
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     if (i >= cnt) break;
-    const uint32_t bq = corrupt_bq(cc, f, n0 + i, wu1[i]);
-    sub[i] = (double)wu2[i] * (1.0 / 4294967296.0) < cc.phred[bq];
+    const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)(n0 + i);
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
+    const uint32_t bq = bq_search(cc.cum, cc.guide, cc.max_bp, cc.n_bq, f, n0 + i, mt_double(r.x, r.y));
     q[i] = (uint8_t)(bq + 33);
-  }
-  if (sub[0] || sub[1]) {   // rare: the replacement bases (randint(0, 3))
-    const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
-    const uint32_t wc[2] = {c.x, c.y};
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      if (!sub[i]) continue;
-      const uint32_t ch = __umulhi(wc[i], 3u);
-      const uint8_t x = b[i];
-      const char *rot = x == 'A' ? "CTG" : x == 'C' ? "ATG" : x == 'T' ? "ACG" : x == 'G' ? "ACT" : "NNN";
-      b[i] = (uint8_t)rot[ch];
+    if (mt_double(r.z, r.w) < cc.phred[bq]) {   // rare: the replacement base (randint(0, 3))
+      const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
+      b[i] = rot_base(b[i], __umulhi(c.x, 3u));
     }
   }
 }

@@ -1235,7 +1235,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       stage_end(ctx);
       return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
     }
-    cc = CorruptCfg{1, (const float *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
+    cc = CorruptCfg{1, (const double *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
                     ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
                     (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u, t_begin};
     cc.guide = (const uint16_t *)((const char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off);

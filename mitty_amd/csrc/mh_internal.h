@@ -184,6 +184,14 @@ struct mh_ctx {
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
   size_t corrupt_guide_off = 0;   // byte offset of the search guide inside corrupt_cum
   uint64_t corrupt_seed = 0;
+  // exact corruption stream of mh_corrupt_fastq (mh_corrupt_stream_seed / _state): 0 = Philox; 1 = the stream of
+  // RandomState(cx_seed) from output cx_pos on; 2 = continuing the explicit state (cx_key, cx_kpos)
+  int32_t cx_mode = 0;
+  uint32_t cx_seed = 0;
+  int64_t cx_pos = 0;
+  uint32_t cx_key[624] = {0};
+  int32_t cx_kpos = 624;
+  mh::DevBuf cx_words, cx_bits, cx_start, cx_aux;
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
@@ -271,6 +279,14 @@ int32_t read_batch(mh_ctx *ctx, const Hap &h, const int64_t *p, const int64_t *l
                    int64_t *cigar_used, char *vlist, int64_t vlist_cap, int64_t *vlist_off, int64_t *vlist_used,
                    char *seq, int64_t seq_cap, int64_t *seq_off, int64_t *seq_used);
 
+
+// MT19937 word streams for exact corruption (mh_sample.hip).  mt_stream_words: outputs [first, first + count) of
+// RandomState(seed) generated as whole jump-ahead segments into `out`; output `first` sits at out[*lead].
+// mt_state_words: `count` outputs continuing an explicit state (numpy get_state(): raw key, pos) into out[0..).
+int32_t mt_stream_words(mh_ctx *ctx, hipStream_t st, uint32_t seed, int64_t first, int64_t count, DevBuf &out,
+                        DevBuf &jobs_buf, int64_t *lead);
+int32_t mt_state_words(mh_ctx *ctx, hipStream_t st, const uint32_t *key624, int32_t pos, int64_t count, DevBuf &out,
+                       DevBuf &key_buf);
 
 // Host-side MT19937 (numpy RandomState seeding), used for seed derivation and the rare exact fix-ups.
 struct HostMT {

@@ -946,6 +946,71 @@ uint64_t HostMT::interval(uint64_t max) {
 
 namespace {
 
+// jump polynomials x^(k * seg) mod P, k = 0..kmax (cached on host and device)
+int32_t ensure_polys(mh_ctx *ctx, hipStream_t st, int64_t kmax, int64_t seg) {
+  if (ctx->jump_k >= kmax + 1 && ctx->jump_seg == seg) return MH_OK;
+  std::vector<uint32_t> polys((size_t)(kmax + 1) * 624);
+  for (int64_t k = 0; k <= kmax; k++) jump::jump_poly_words((uint64_t)seg, k, polys.data() + k * 624);
+  MH_TRY(ensure(ctx, ctx->jump_polys, 4 * polys.size()));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->jump_polys.p, polys.data(), 4 * polys.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  ctx->jump_k = kmax + 1;
+  ctx->jump_seg = seg;
+  return MH_OK;
+}
+
+// The stream continued from an explicit state (numpy's get_state(): raw key, pos): one workgroup, twist by twist.
+__global__ void __launch_bounds__(256) k_mt_state(const uint32_t *key, int32_t pos, int64_t count, uint32_t *out) {
+  __shared__ uint32_t st[2][624];
+  for (int i = threadIdx.x; i < 624; i += 256) st[0][i] = key[i];
+  lds_barrier();
+  const int64_t lead = 624 - pos;   // outputs left in the current state
+  for (int64_t i = threadIdx.x; i < lead && i < count; i += 256) out[i] = mt_temper(st[0][pos + i]);
+  uint32_t *o = st[0], *nw = st[1];
+  for (int64_t base = lead; base < count; base += 624) {
+    mt_twist_block(o, nw, [&](int k, uint32_t w) {
+      if (base + k < count) out[base + k] = w;
+    });
+    uint32_t *tmp = o; o = nw; nw = tmp;
+  }
+}
+
+}  // namespace
+
+int32_t mt_stream_words(mh_ctx *ctx, hipStream_t st, uint32_t seed, int64_t first, int64_t count, DevBuf &out,
+                        DevBuf &jobs_buf, int64_t *lead) {
+  const int64_t SEG = seg_words();
+  const int64_t k0 = first / SEG, k1 = (first + std::max<int64_t>(count, 1) - 1) / SEG;
+  *lead = first - k0 * SEG;
+  MH_TRY(ensure(ctx, out, 4 * (size_t)((k1 - k0 + 1) * SEG) + 64));
+  std::vector<SegJob> jobs;
+  for (int64_t k = k0; k <= k1; k++)
+    jobs.push_back(SegJob{(uint32_t *)out.p, (k - k0) * SEG, std::min(SEG, first + count - k * SEG), seed, (int32_t)k});
+  MH_TRY(ensure_polys(ctx, st, k1, SEG));
+  MH_TRY(ensure(ctx, jobs_buf, sizeof(SegJob) * jobs.size() + 64));
+  HIPCHK(ctx, hipMemcpyAsync(jobs_buf.p, jobs.data(), sizeof(SegJob) * jobs.size(), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)jobs_buf.p,
+                     (const uint32_t *)ctx->jump_polys.p, 0);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));   // the host job table goes out of scope
+  return MH_OK;
+}
+
+int32_t mt_state_words(mh_ctx *ctx, hipStream_t st, const uint32_t *key624, int32_t pos, int64_t count, DevBuf &out,
+                       DevBuf &key_buf) {
+  if (pos < 0 || pos > 624) return arg_fail(ctx, MH_E_ARG, "MT19937 state position outside 0..624");
+  MH_TRY(ensure(ctx, out, 4 * (size_t)count + 64));
+  MH_TRY(ensure(ctx, key_buf, 4 * 624));
+  HIPCHK(ctx, hipMemcpyAsync(key_buf.p, key624, 4 * 624, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_mt_state, dim3(1), dim3(256), 0, st, (const uint32_t *)key_buf.p, pos, count,
+                     (uint32_t *)out.p);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));   // key624 is the caller's host memory
+  return MH_OK;
+}
+
+namespace {
+
 struct UnitPlan {
   int64_t p_min, p_max, n, n_fo_words, n_shuf_words;
   uint32_t s_tloc, s_tlen, s_shuf, s_fo;
@@ -1316,16 +1381,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       dec.push_back(DecJob{words + q.w_shuf, q.n_shuf_words, q.n, jall + q.j_off, d_status + u});
     }
     if (!jobs.empty()) {
-      // jump polynomials x^(k * SEG_WORDS) mod P, k = 0..kmax (cached on host and device)
-      if (ctx->jump_k < kmax + 1 || ctx->jump_seg != SEG_WORDS) {
-        std::vector<uint32_t> polys((size_t)(kmax + 1) * 624);
-        for (int64_t k = 0; k <= kmax; k++) jump::jump_poly_words((uint64_t)SEG_WORDS, k, polys.data() + k * 624);
-        MH_TRY(ensure(ctx, ctx->jump_polys, 4 * polys.size()));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->jump_polys.p, polys.data(), 4 * polys.size(), hipMemcpyHostToDevice, st));
-        HIPCHK(ctx, hipStreamSynchronize(st));
-        ctx->jump_k = kmax + 1;
-        ctx->jump_seg = SEG_WORDS;
-      }
+      MH_TRY(ensure_polys(ctx, st, kmax, SEG_WORDS));
       MH_TRY(ensure(ctx, ctx->s[2], sizeof(SegJob) * jobs.size() + sizeof(DecJob) * dec.size() + 64));
       SegJob *d_jobs = (SegJob *)ctx->s[2].p;
       DecJob *d_dec = (DecJob *)((char *)ctx->s[2].p + ((sizeof(SegJob) * jobs.size() + 15) / 16) * 16);

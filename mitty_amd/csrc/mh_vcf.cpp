@@ -68,7 +68,7 @@ bool parse_i64(const char *s, size_t n, int64_t &v) {
   if (i == n) return false;
   for (; i < n; i++) {
     unsigned d = (unsigned)(s[i] - '0');
-    if (d > 9) return false;
+    if (d > 9 || x > (INT64_MAX - 9) / 10) return false;   // not a number, or beyond int64 (htslib rejects it too)
     x = x * 10 + d;
   }
   v = neg ? -x : x;

@@ -195,33 +195,33 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k]
       stats['kept'] += emitted[i][0]
 
-  # file offsets of every piece, then positioned writes.  '.gz' outputs: each piece becomes BGZF members first
-  # (decompressed content identical to the one-GPU file; rank 0 adds the EOF marker)
-  gz = fastq1_fname.endswith('.gz')
+  # file offsets of every piece, then positioned writes.  A '.gz' output (decided per file, as FastqSink does): each
+  # piece becomes BGZF members first (decompressed content identical to the one-GPU file; rank 0 adds the EOF marker)
+  fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
+  gz = [fn.endswith('.gz') for fn in fnames] + [False]
   payload = {}
-  if gz:
+  if any(gz):
     from mitty_amd import _native
     for i in sorted(emitted):
       _, r1, r2 = emitted[i]
       d1, d2 = backend.fetch(r1, r2 if write2 else (0, 0))
-      payload[i] = (_native.bgzf_compress(d1), _native.bgzf_compress(d2) if write2 else b'')
+      payload[i] = (_native.bgzf_compress(d1) if gz[0] else d1, _native.bgzf_compress(d2) if gz[1] else d2)
   sz = [0] * (2 * len(pieces))
   for i, (_, r1, r2) in emitted.items():
-    if gz:
-      sz[2 * i], sz[2 * i + 1] = len(payload[i][0]), len(payload[i][1])
+    if payload:
+      sz[2 * i], sz[2 * i + 1] = len(payload[i][0]), len(payload[i][1]) if write2 else 0
     else:
       sz[2 * i], sz[2 * i + 1] = r1[1], r2[1]
   sz = allreduce_i64(sz + [stats['templates'], stats['kept']], group)
   tot_templates, tot_kept = sz[-2], sz[-1]
   off1, total1 = file_offsets(sz[0:2 * len(pieces):2])
   off2, total2 = file_offsets(sz[1:2 * len(pieces):2])
-  fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
   totals = (total1, total2)
   if rank == 0:
-    for fn, total in zip(fnames, totals):
+    for fn, total, z in zip(fnames, totals, gz):
       with open(fn, 'wb') as fp:
         fp.truncate(total)
-        if gz:
+        if z:
           from mitty_amd import _native
           fp.seek(total)
           fp.write(_native.bgzf_eof())
@@ -231,7 +231,7 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
   try:
     for i in sorted(emitted):
       _, r1, r2 = emitted[i]
-      d1, d2 = payload.pop(i) if gz else backend.fetch(r1, r2 if write2 else (0, 0))
+      d1, d2 = payload.pop(i) if payload else backend.fetch(r1, r2 if write2 else (0, 0))
       _pwrite_all(fds[0], d1, off1[i])
       if write2:
         _pwrite_all(fds[1], d2, off2[i])

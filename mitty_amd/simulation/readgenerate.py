@@ -140,21 +140,20 @@ ri = namedtuple('ReadInfo', ['sample', 'rid', 'chrom', 'cpy', 'strand', 'pos', '
 
 
 def parse_qname(qname):
-  """readgenerate.parse_qname (readgenerate.py:259-291)."""
-  def _parse_(_cigar, _v_list):
-    if _cigar[0] == '>':
-      _special_cigar = _cigar
-      _cigar = _cigar.split(':')[-1]
-    else:
-      _special_cigar = None
-    return _cigar, _special_cigar, [int(v) for v in _v_list.split(',') if v != '']
+  """readgenerate.parse_qname (readgenerate.py:259-291): the qname's reads, in file order, as ReadInfo.
 
-  d = qname.split('|')
-  rid, chrom, cpy = d[:3]
-  sample, _ = rid.split(':', 1)
-  cpy = int(cpy)
-  return [ri(sample, rid, chrom, cpy, int(strand), int(pos), int(rlen), *_parse_(cigar, v_list))
-          for strand, pos, rlen, cigar, v_list in zip(d[3::5], d[4::5], d[5::5], d[6::5], d[7::5])]
+  A read from inside a long insertion carries the CIGAR '>p:nI'; it is reported as cigar 'nI' with the original in
+  special_cigar.  Fields of a trailing incomplete read are ignored, as the reference's zip() ignores them."""
+  fields = qname.split('|')
+  rid, chrom, cpy = fields[0], fields[1], int(fields[2])
+  sample = rid[:rid.index(':')]   # ValueError without a ':' (the reference's tuple unpacking raises too)
+  reads = []
+  for k in range(3, 3 + 5 * ((len(fields) - 3) // 5), 5):
+    strand, pos, rlen, cigar, vs = fields[k:k + 5]
+    special = cigar if cigar[:1] == '>' else None
+    reads.append(ri(sample, rid, chrom, cpy, int(strand), int(pos), int(rlen),
+                    cigar.rpartition(':')[2] if special else cigar, special, [int(x) for x in vs.split(',') if x]))
+  return reads
 
 
 cigar_parser = re.compile(r'(\d+)(\D)')

@@ -2,8 +2,9 @@
 
 `create_node_list` splices on the GPU (mh_build_haplotype) and returns a NodeList — a list of Node exactly as the
 reference builds it — that remembers its device slot, so `get_begin_end_nodes` and `generate_read` run on the
-device (mh_read_batch) against the same haplotype.  `snp` / `insertion` / `deletion` are the reference's
-per-variant expansion helpers, kept for API compatibility (the device splice does not call them).
+device (mh_read_batch) against the same haplotype.  The reference's per-variant helpers `create_nodes` / `snp` /
+`insertion` / `deletion` (rpc.py:66-116) are the inner steps of its create_node_list; the device splice replaces the
+whole walk, so they are not exported.
 """
 import itertools
 
@@ -111,45 +112,3 @@ def generate_read(p, l, n0, n1, nodes):
     raise ValueError('n0/n1 ({}, {}) are not the start/end nodes of read ({}, {}): expected ({}, {})'.format(
       n0, n1, p, l, int(a[0]), int(b[0])))
   return res[0]
-
-
-# ---- per-variant expansion helpers (reference rpc.py:66-116; API compatibility) ---------------------------------
-def create_nodes(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
-  if v.cigarop == 'X':
-    return snp(ref_seq, samp_pos, ref_pos, v, ref_start_pos)
-  elif v.cigarop == 'I':
-    return insertion(ref_seq, samp_pos, ref_pos, v, ref_start_pos)
-  return deletion(ref_seq, samp_pos, ref_pos, v, ref_start_pos)
-
-
-def snp(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
-  nodes = []
-  delta = v.pos - ref_pos
-  if delta > 0:
-    nodes.append(Node(samp_pos, ref_pos, '=', delta, ref_seq[ref_pos - ref_start_pos:v.pos - ref_start_pos]))
-    ref_pos = v.pos
-    samp_pos += delta
-  nodes.append(Node(samp_pos, ref_pos, 'X', 1, v.alt))
-  return nodes, samp_pos + 1, ref_pos + 1
-
-
-def insertion(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
-  nodes = []
-  delta = v.pos + 1 - ref_pos
-  if delta > 0:
-    nodes.append(Node(samp_pos, ref_pos, '=', delta, ref_seq[ref_pos - ref_start_pos:v.pos + 1 - ref_start_pos]))
-    samp_pos += delta
-  ref_pos = v.pos + 1
-  nodes.append(Node(samp_pos, ref_pos, 'I', v.oplen, v.alt[1:]))
-  return nodes, samp_pos + v.oplen, ref_pos
-
-
-def deletion(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
-  nodes = []
-  delta = v.pos + 1 - ref_pos
-  if delta > 0:
-    nodes.append(Node(samp_pos, ref_pos, '=', delta, ref_seq[ref_pos - ref_start_pos:v.pos + 1 - ref_start_pos]))
-    samp_pos += delta
-  ref_pos = v.pos + 1 + v.oplen
-  nodes.append(Node(samp_pos - 1, ref_pos, 'D', v.oplen, ''))
-  return nodes, samp_pos, ref_pos

@@ -63,6 +63,11 @@ def _p(a):
   return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _take(ptr, n):
+  """n bytes at ptr (ctypes.string_at takes a C int size: it fails past 2 GiB)."""
+  return bytes((ctypes.c_char * n).from_address(ptr.value)) if n else b''
+
+
 # ---- RNG / small primitives ------------------------------------------------------------------------------------
 def mt_words(seed, n):
   out = np.empty(n, dtype=np.uint32)
@@ -211,8 +216,8 @@ def generate_unit(ref_seq, region_start0, vl, p, rlen, cum_tlen, rng_seed, seria
                              pool, len(vl), p, rlen, _p(cum_tlen), len(cum_tlen), rng_seed, serial_stub.encode(),
                              chrom.encode(), cpy, ctypes.byref(o1), ctypes.byref(l1), ctypes.byref(o2),
                              ctypes.byref(l2))
-  b1 = ctypes.string_at(o1, l1.value) if l1.value else b''
-  b2 = ctypes.string_at(o2, l2.value) if l2.value else b''
+  b1 = _take(o1, l1.value)
+  b2 = _take(o2, l2.value)
   lib().mo_free(o1)
   lib().mo_free(o2)
   return n, b1, b2
@@ -237,8 +242,8 @@ def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, 
                              pool, len(pos), p, rlen, _p(cum_tlen), len(cum_tlen), rng_seed, serial_stub.encode(),
                              chrom.encode(), cpy, ctypes.byref(o1), ctypes.byref(l1), ctypes.byref(o2),
                              ctypes.byref(l2))
-  b1 = ctypes.string_at(o1, l1.value) if l1.value and keep_output else b''
-  b2 = ctypes.string_at(o2, l2.value) if l2.value and keep_output else b''
+  b1 = _take(o1, l1.value) if keep_output else b''
+  b2 = _take(o2, l2.value) if keep_output else b''
   lib().mo_free(o1)
   lib().mo_free(o2)
   return n, b1, b2
@@ -285,7 +290,7 @@ def corrupt_fastq(model, names, seq1, seq2, seed=7):
                              _p(ph), ctypes.byref(o1), ctypes.byref(ol1), ctypes.byref(o2), ctypes.byref(ol2))
   if r < 0:
     raise ValueError('read longer than the BQ model')
-  b1, b2 = ctypes.string_at(o1, ol1.value), ctypes.string_at(o2, ol2.value)
+  b1, b2 = _take(o1, ol1.value), _take(o2, ol2.value)
   lib().mo_free(o1)
   lib().mo_free(o2)
   return b1, b2

@@ -61,21 +61,29 @@ def test_distributed_output_identical_to_single_process(tmp_path, world, layout)
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
 
 
-def test_distributed_gz_output(tmp_path):
-  """'.gz' outputs: BGZF pieces at all-reduced offsets + EOF marker; decompresses to the single-process bytes."""
+@pytest.mark.parametrize('names', [('r1.fq.gz', 'r2.fq.gz'), ('r1.fq.gz', 'r2.fq'), ('r1.fq', 'r2.fq.gz')])
+def test_distributed_gz_output(tmp_path, names):
+  """'.gz' outputs (decided per file, as the single-GPU FastqSink decides): BGZF pieces at all-reduced offsets + EOF
+  marker; each file decompresses (or reads) to the single-process bytes."""
   import gzip
   import socket
   import torch.multiprocessing as mp
   with socket.socket() as s:
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
-  mp.start_processes(_rank_gz, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+  mp.start_processes(_rank_gz, args=(2, port, str(tmp_path), names), nprocs=2, join=True, start_method='spawn')
   model = 'hiseq-X-v2.5-Garvan'
-  G.check_same(gzip.open(str(tmp_path / 'r1.fq.gz')).read(), G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
-  G.check_same(gzip.open(str(tmp_path / 'r2.fq.gz')).read(), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
+  for k, fn in enumerate(names):
+    raw = open(str(tmp_path / fn), 'rb').read()
+    if fn.endswith('.gz'):
+      assert raw[-28:] == bytes.fromhex('1f8b08040000000000ff0600424302001b0003000000000000000000')
+      raw = gzip.decompress(raw)
+    else:
+      assert raw[:2] != b'\x1f\x8b'
+    G.check_same(raw, G.fastq_bytes('e2e_{}.r{}.fq.gz'.format(model, k + 1)))
 
 
-def _rank_gz(rank, world, port, outdir):
+def _rank_gz(rank, world, port, outdir, names):
   import torch.distributed as dist
   os.environ['MASTER_ADDR'] = '127.0.0.1'
   os.environ['MASTER_PORT'] = str(port)
@@ -87,7 +95,7 @@ def _rank_gz(rank, world, port, outdir):
     c = G.load_json('e2e_config.json')[model_name]
     mod, mdl = get_read_model(model_name + '.pkl')
     D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
-                                 c['coverage'], os.path.join(outdir, 'r1.fq.gz'), os.path.join(outdir, 'r2.fq.gz'),
+                                 c['coverage'], os.path.join(outdir, names[0]), os.path.join(outdir, names[1]),
                                  seed=c['seed'], backend=OracleBackend(), layout='slice')
   finally:
     dist.destroy_process_group()

@@ -5,6 +5,7 @@ Mbp, and size-independent properties at larger sizes.
 """
 import gzip
 import os
+import re
 
 import numpy as np
 import pytest
@@ -263,6 +264,13 @@ def test_unit_vs_oracle_no_variants(native):
   _unit_vs_oracle(600_000, 1, '1kg-pcr-free', n_seed=9, rate=0.0)
 
 
+@pytest.mark.parametrize('emit_mode', [0, 1])
+def test_unit_vs_oracle_nine_digit_positions(native, emit_mode):
+  """A 2 Mbp region starting at 150,000,000 of a 152 Mbp contig: every POS has 9 digits (both writers)."""
+  assert _unit_vs_oracle(152_000_000, 8, '1kg-pcr-free', n_seed=17, start0=150_000_000, cpys=(1,),
+                         emit_mode=emit_mode) > 10000
+
+
 def test_batched_units_vs_oracle(native):
   """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
   reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated."""
@@ -435,44 +443,144 @@ def test_deferred_prepare_matches_waiting_prepare(native, monkeypatch):
     eng.close()
 
 
-# ---- size-independent properties at full chromosome scale -------------------------------------------------------
-def test_chr1_scale_properties(native):
-  """One chr1-sized unit (249 Mbp): every record parses, POS/CIGAR are consistent with the sequence length, every
-  read sequence equals the haplotype slice its qname implies, cnt runs 1..kept."""
+# ---- the bench configuration (BASELINE configs[1]) at full size -----------------------------------------------------
+CHR1 = 249_250_621
+CHR1_SEED = 12345
+
+
+@pytest.fixture(scope='module')
+def chr1_unit(native):
+  """One chr1-sized work unit (249 Mbp, copy 1, ~7.48 M draws, ~5.9 M kept templates) of the bench workload, run once
+  on the GPU perfect and once with fused corruption: both FASTQ arenas, the node list and the haplotype."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
-  from mitty_amd.simulation.readgenerate import parse_qname
   mdl = G.model('hiseq-X-v2.5-Garvan')
   p, _ = _native.read_model_params(150, 30.0)
-  L = 249_250_621
-  seq = synth.contig(L, 1)
-  recs = synth.variants(seq, 2)
-  copies = synth.copies_soa(recs)
-  eng = Engine(0)
-  try:
-    eng.load_region(0, ('1', 0, L), seq)
-    n, kept, b1, b2 = eng.run_unit(0, 0, 1, 12345, copies[1], p, 150, mdl['cum_tlen'], 'SYN')
-    assert n > 6_000_000 and kept > 0.9 * n   # n = templates kept by te < p_max (draws ~7.48 M)
-    slot, n_nodes, p_min, p_max = eng.haplotype(0, 1, copies[1])
-    ps, pr, op, ol, hap = eng.ctx.get_nodes(slot, n_nodes)
-    # sample a slice of records from the arena
-    d1, d2 = eng.ctx.fetch_output(0, min(b1, 40_000_000), 0, min(b2, 40_000_000))
-  finally:
-    eng.close()
-  assert b1 == b2 or abs(b1 - b2) < b1 // 1000
+  seq = synth.contig(CHR1, 1)
+  copies = synth.copies_soa(synth.variants(seq, 2))
+  out = {'seq': seq, 'copies': copies, 'p': p, 'model': mdl}
+  for corrupt in (False, True):
+    eng = Engine(0)
+    try:
+      if corrupt:
+        eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 7)
+      eng.load_region(0, ('1', 0, CHR1), seq)
+      n, kept, b1, b2 = eng.run_unit(0, 0, 1, CHR1_SEED, copies[1], p, 150, mdl['cum_tlen'], 'SYN')
+      key = 'corrupt' if corrupt else 'perfect'
+      out[key] = eng.ctx.fetch_output()
+      out[key + '_counts'] = (n, kept, b1, b2)
+      if not corrupt:
+        slot, n_nodes, p_min, p_max = eng.haplotype(0, 1, copies[1])
+        out['nodes'] = eng.ctx.get_nodes(slot, n_nodes)
+        out['span'] = (p_min, p_max)
+    finally:
+      eng.close()
+  return out
+
+
+@pytest.fixture(scope='module')
+def chr1_oracle(chr1_unit):
+  """The same unit through the CPU oracle (~15-20 s on one core)."""
+  from oracle import oracle as O
+  u = chr1_unit
+  return O.generate_unit_soa(u['seq'], 0, u['copies'][1], u['p'], 150, u['model']['cum_tlen'], CHR1_SEED, 'SYN:0:0',
+                             '1', 1)
+
+
+def test_chr1_templates_vs_oracle(native, chr1_unit):
+  """The whole template arrays of a chr1-length unit (7.48 M geometric draws, the full Fisher-Yates decode and
+  permutation, k_decode_tail) equal the oracle's (illumina.py:66-76)."""
+  from mitty_amd.simulation import illumina
+  from oracle import oracle as O
+  mdl = chr1_unit['model']
+  p_min, p_max = chr1_unit['span']
+  rm = illumina.read_model_params(mdl, 30.0)
+  r = illumina.generate_reads(rm, p_min, p_max, CHR1_SEED)
+  fo, p0, p1 = O.generate_templates(rm['p'], 150, mdl['cum_tlen'], p_min, p_max, CHR1_SEED)
+  assert len(p0) > 6_000_000
+  assert np.array_equal(r[0]['file_order'], fo)
+  assert np.array_equal(r[0]['pos'], p0)
+  assert np.array_equal(r[1]['pos'], p1)
+
+
+def test_chr1_unit_fastq_vs_oracle(native, chr1_unit, chr1_oracle):
+  """Both FASTQ files of the full chr1 unit byte-identical to the oracle: 9-digit POS (SplitWriter::put_u's nd > 8
+  branch) and 7-digit cnt (digit_sum offsets past 999,999 kept templates) are exercised throughout."""
+  k, o1, o2 = chr1_oracle
+  n, kept, b1, b2 = chr1_unit['perfect_counts']
+  d1, d2 = chr1_unit['perfect']
+  assert kept == k and kept > 1_000_000
+  assert (len(d1), len(d2)) == (b1, b2)
+  G.check_same(d1, o1, 'chr1 file 1')
+  G.check_same(d2, o2, 'chr1 file 2')
+  last = d1[d1.rindex(b'\n@', 0, len(d1) - 1) + 2:].split(b'\n')[0].decode()
+  assert last.startswith('SYN:0:0:{}|'.format(kept)) and len(str(kept)) == 7
+  assert re.search(rb'\|[01]\|[1-9][0-9]{8}\|150\|', d1[-50_000_000:])   # 9-digit positions
+
+
+def _line_fields_equal(a, b, fields):
+  """FASTQ texts a, b: same line structure, and lines whose index mod 4 is in `fields` byte-equal."""
+  A, B = np.frombuffer(a, np.uint8), np.frombuffer(b, np.uint8)
+  assert len(A) == len(B)
+  nl = np.flatnonzero(A == 10)
+  assert np.array_equal(nl, np.flatnonzero(B == 10))
+  starts = np.concatenate([[0], nl[:-1] + 1])
+  for f in fields:
+    s, e = starts[f::4], nl[f::4]
+    for c in range(0, len(s), 1 << 20):
+      cs, ce = s[c:c + (1 << 20)], e[c:c + (1 << 20)]
+      ln = ce - cs
+      idx = np.repeat(cs - np.concatenate([[0], np.cumsum(ln)[:-1]]), ln) + np.arange(int(ln.sum()))
+      if not np.array_equal(A[idx], B[idx]):
+        bad = int(np.nonzero(A[idx] != B[idx])[0][0])
+        raise AssertionError('field {} differs near byte {}'.format(f, int(idx[bad])))
+
+
+def test_chr1_corrupted_qnames_vs_oracle(native, chr1_unit, chr1_oracle):
+  """BASELINE configs[2]: the chr1 unit with fused BQ corruption keeps every qname (and the '+' lines) byte-equal to
+  the CPU oracle's; sequences and qualities keep their lengths; qualities are no longer all '~'."""
+  _, o1, o2 = chr1_oracle
+  c1, c2 = chr1_unit['corrupt']
+  assert chr1_unit['corrupt_counts'] == chr1_unit['perfect_counts']
+  _line_fields_equal(c1, o1, (0, 2))
+  _line_fields_equal(c2, o2, (0, 2))
+  assert c1 != o1 and c2 != o2
+
+
+def test_chr1_scale_properties(native, chr1_unit):
+  """Size-independent checks over every record of the first 40 MB: qnames parse, cnt runs 1, 2, ..., the CIGAR
+  consumes the read length, qualities are '~', and each read equals the haplotype slice its qname implies (POS mapped
+  to a sample coordinate through the node list; mate on strand 1 reverse-complemented)."""
+  from mitty_amd.simulation.readgenerate import parse_qname
+  ps, pr, op, ol, hap = chr1_unit['nodes']
+  p_min = int(ps[0])
+  d1 = chr1_unit['perfect'][0][:40_000_000]
+  eq = (op == ord('=')) | (op == ord('X'))
+  eq_pr, eq_ps, eq_len = pr[eq], ps[eq], np.where(op[eq] == ord('X'), 1, ol[eq])
+  comp = bytes.maketrans(b'ATCGN', b'TAGCN')
   lines = d1.split(b'\n')
   n_rec = (len(lines) - 1) // 4
   assert n_rec > 50000
-  for i in range(0, n_rec - 1, 97):
+  checked = 0
+  for i in range(n_rec - 1):
     qn, s, q = lines[4 * i][1:].decode(), lines[4 * i + 1], lines[4 * i + 3]
-    ri = parse_qname(qn)
     assert int(qn.split('|')[0].split(':')[3]) == i + 1
     assert len(q) == 150 and set(q) == {ord('~')}
-    r = ri[0]
-    if r.special_cigar is None:
-      import re
-      consumed = sum(int(a) for a, o in re.findall(r'(\d+)([=XID])', r.cigar) if o in '=XI')
-      assert consumed == len(s) == 150
+    r = parse_qname(qn)[0]
+    if r.special_cigar is not None or len(s) != 150:
+      continue
+    consumed = sum(int(a) for a, o in re.findall(r'(\d+)([=XID])', r.cigar) if o in '=XI')
+    assert consumed == 150
+    if re.match(r'\d+([=XID])', r.cigar).group(1) not in '=X':   # a read starting inside an insertion
+      continue
+    k = int(np.searchsorted(eq_pr, r.pos, 'right')) - 1
+    assert eq_pr[k] <= r.pos < eq_pr[k] + eq_len[k]
+    samp = int(eq_ps[k]) + r.pos - int(eq_pr[k])
+    want = bytes(hap[samp - p_min:samp - p_min + 150])
+    got = s if r.strand == 0 else s.translate(comp)[::-1]
+    assert got == want, (i, qn)
+    checked += 1
+  assert checked > 0.9 * n_rec
 
 
 # ---- corruption (Philox mode) ----------------------------------------------------------------------------------
@@ -784,8 +892,9 @@ def test_god_aligner_from_device_arenas(native, tmp_path):
 
 
 # ---- standalone corrupt-reads --------------------------------------------------------------
+@pytest.mark.parametrize('rng', ['mitty', 'philox'])
 @pytest.mark.parametrize('model', G.MODELS)
-def test_corrupt_reads_over_fastq(native, model, tmp_path):
+def test_corrupt_reads_over_fastq(native, model, rng, tmp_path):
   """corrupt-reads on the e2e FASTQ pair: names (file 1's) and lengths kept, substitutions only to other bases,
   BQ per position distributed as the model says, substitution rate = mean phred error; chunking does not change
   the output; the CLI gives the same files."""
@@ -796,7 +905,7 @@ def test_corrupt_reads_over_fastq(native, model, tmp_path):
   mod, mdl = get_read_model(model + '.pkl')
   i1, i2 = G.path('e2e_{}.r1.fq.gz'.format(model)), G.path('e2e_{}.r2.fq.gz'.format(model))
   o1, o2 = str(tmp_path / 'c1.fq'), str(tmp_path / 'c2.fq')
-  st = readcorrupt.multi_process(mod, mdl, i1, o1, i2, o2, seed=11)
+  st = readcorrupt.multi_process(mod, mdl, i1, o1, i2, o2, seed=11, rng=rng)
   a1, a2 = G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model))
   assert st['templates'] == a1.count(b'\n') // 4
   names = [ln.split(b' ')[0] for ln in a1.split(b'\n')[0::4][:-1]]
@@ -823,11 +932,12 @@ def test_corrupt_reads_over_fastq(native, model, tmp_path):
     assert not np.any(SC[err] == SA[err])
   # chunk size does not change the output
   o1b, o2b = str(tmp_path / 'd1.fq'), str(tmp_path / 'd2.fq')
-  readcorrupt.multi_process(mod, mdl, i1, o1b, i2, o2b, seed=11, chunk_bytes=5003, flush_bytes=20000)
+  readcorrupt.multi_process(mod, mdl, i1, o1b, i2, o2b, seed=11, chunk_bytes=5003, flush_bytes=20000, rng=rng)
   assert open(o1b, 'rb').read() == open(o1, 'rb').read() and open(o2b, 'rb').read() == open(o2, 'rb').read()
   # CLI
   e1, e2 = str(tmp_path / 'e1.fq'), str(tmp_path / 'e2.fq')
-  res = CliRunner().invoke(cli, ['corrupt-reads', model + '.pkl', i1, e1, '11', '--fastq2-in', i2, '--fastq2-out', e2])
+  res = CliRunner().invoke(cli, ['corrupt-reads', model + '.pkl', i1, e1, '11', '--fastq2-in', i2, '--fastq2-out', e2,
+                                 '--rng', rng])
   assert res.exit_code == 0, res.output + repr(res.exception)
   assert open(e1, 'rb').read() == open(o1, 'rb').read() and open(e2, 'rb').read() == open(o2, 'rb').read()
 
@@ -846,3 +956,117 @@ def test_corrupt_reads_single_end_and_errors(native, tmp_path):
   long_read.write_bytes(b'@r1\n' + b'A' * L + b'\n+\n' + b'~' * L + b'\n')
   with pytest.raises(ValueError, match='BQ model'):
     readcorrupt.multi_process(mod, mdl, str(long_read), str(tmp_path / 'x.fq'), seed=3)
+
+
+# ---- exact corruption: the reference's single-worker MT19937 stream (readcorrupt.py:84, processes=1) ----------------
+@pytest.mark.parametrize('chunk', [None, 3001])
+@pytest.mark.parametrize('model', G.MODELS)
+def test_corrupt_reads_exact_byte_identical_to_reference(native, model, chunk, tmp_path):
+  """corrupt-reads --rng mitty on the reference's input pair reproduces the reference's processes=1 output
+  (tests/golden/corrupt_*.fq.gz) byte for byte; small chunks carry the stream across calls."""
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readcorrupt
+  mod, mdl = get_read_model(model + '.pkl')
+  i1, i2 = G.path('corrupt_in_{}.r1.fq.gz'.format(model)), G.path('corrupt_in_{}.r2.fq.gz'.format(model))
+  o1, o2 = str(tmp_path / 'c1.fq'), str(tmp_path / 'c2.fq')
+  readcorrupt.multi_process(mod, mdl, i1, o1, i2, o2, processes=1, seed=7, chunk_bytes=chunk)
+  G.check_same(open(o1, 'rb').read(), G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model)), 'corrupt file 1')
+  G.check_same(open(o2, 'rb').read(), G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model)), 'corrupt file 2')
+
+
+def test_corrupt_reads_exact_cli(native, tmp_path):
+  from click.testing import CliRunner
+  from mitty_amd.cli import cli
+  model = 'hiseq-X-v2.5-Garvan'
+  i1, i2 = G.path('corrupt_in_{}.r1.fq.gz'.format(model)), G.path('corrupt_in_{}.r2.fq.gz'.format(model))
+  e1, e2 = str(tmp_path / 'e1.fq'), str(tmp_path / 'e2.fq')
+  res = CliRunner().invoke(cli, ['corrupt-reads', model + '.pkl', i1, e1, '7', '--fastq2-in', i2, '--fastq2-out', e2,
+                                 '--threads', '1'])
+  assert res.exit_code == 0, res.output + repr(res.exception)
+  G.check_same(open(e1, 'rb').read(), G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model)))
+  G.check_same(open(e2, 'rb').read(), G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model)))
+
+
+@pytest.mark.parametrize('model', G.MODELS)
+def test_corrupt_template_plugin_api_vs_reference(native, model):
+  """The plugin functions illumina.corrupt_template / corrupt_single_read (illumina.py:113-162) on a caller's
+  RandomState: template by template they reproduce the reference's processes=1 output, and leave the RandomState
+  where rand(n), rand(n), randint(0, 3, n) per mate leave it."""
+  from mitty_amd.simulation import illumina
+  mdl = G.model(model)
+  r1 = G.parse_fastq(G.fastq_bytes('corrupt_in_{}.r1.fq.gz'.format(model)))
+  r2 = G.parse_fastq(G.fastq_bytes('corrupt_in_{}.r2.fq.gz'.format(model)))
+  want1 = G.parse_fastq(G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model)))
+  want2 = G.parse_fastq(G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model)))
+  seed = int(np.random.RandomState(7).randint((1 << 32) - 1))
+  rng, shadow = np.random.RandomState(seed), np.random.RandomState(seed)
+  for k, (a, b) in enumerate(zip(r1, r2)):
+    if k % 7 == 3:   # the single-read form, mate by mate
+      got = [(a[0],) + illumina.corrupt_single_read(s, mdl['cum_bq_mat'][m], rng) for m, s in ((0, a[1]), (1, b[1]))]
+    else:
+      got = illumina.corrupt_template(mdl, [a[0], a[1], b[1]], rng)
+    assert got == [want1[k], want2[k]], k
+    for s in (a[1], b[1]):
+      shadow.rand(len(s))
+      shadow.rand(len(s))
+      shadow.randint(0, 3, size=len(s))
+    st, sh = rng.get_state(), shadow.get_state()
+    assert np.array_equal(st[1], sh[1]) and st[2] == sh[2], k
+  with pytest.raises(IndexError):
+    illumina.corrupt_single_read('A' * 301, mdl['cum_bq_mat'][0], rng)
+
+
+# ---- counter-based sampling mode (--rng philox) ----------------------------------------------------------------------
+def test_philox_sampling_properties(native):
+  """--rng philox: deterministic per seed, positions and template lengths inside the reference's support
+  (ts > p_min, te < p_max, tlen = max(searchsorted(cum_tlen, U), rlen)), the tlen distribution follows the model's,
+  file-order bits are fair, the kept count matches the MT19937 mode's in expectation, and units sampled in one batch
+  equal the same units sampled alone."""
+  from mitty_amd.simulation import illumina
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  rm = illumina.read_model_params(mdl, 30.0)
+  rlen, p_min, p_max = 150, 1000, 1000 + 20_000_000
+  a = illumina.generate_reads(rm, p_min, p_max, 77, rng='philox')
+  b = illumina.generate_reads(rm, p_min, p_max, 77, rng='philox')
+  c = illumina.generate_reads(rm, p_min, p_max, 78, rng='philox')
+  for k in (0, 1):
+    assert np.array_equal(a[k]['pos'], b[k]['pos']) and np.array_equal(a[k]['file_order'], b[k]['file_order'])
+  assert not np.array_equal(a[0]['pos'][:1000], c[0]['pos'][:1000])
+  ts, te = a[0]['pos'], a[1]['pos'] + rlen
+  m = len(ts)
+  assert ts.min() > p_min and te.max() < p_max
+  tl = te - ts
+  assert tl.min() >= rlen and tl.max() <= len(mdl['cum_tlen'])
+  want = np.clip(np.searchsorted(mdl['cum_tlen'], (np.arange(100_000) + 0.5) / 100_000), rlen, None)
+  grid = np.arange(rlen, len(mdl['cum_tlen']) + 1)
+  cdf_got = np.searchsorted(np.sort(tl), grid, side='right') / m
+  cdf_want = np.searchsorted(np.sort(want), grid, side='right') / len(want)
+  assert np.abs(cdf_got - cdf_want).max() < 0.01
+  fo = a[0]['file_order']
+  assert set(np.unique(fo)) <= {0, 1} and abs(fo.mean() - 0.5) < 5 / np.sqrt(m)
+  assert np.array_equal(a[1]['file_order'], 1 - fo)
+  mt = illumina.generate_reads(rm, p_min, p_max, 77)
+  assert abs(m - len(mt[0]['pos'])) < 0.02 * m
+  assert len(np.unique(ts)) > 0.97 * m   # geometric gaps >= 1: the starts are distinct
+  # batched == alone
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  seq = synth.contig(3_000_000, 51)
+  copies = synth.copies_soa(synth.variants(seq, 52))
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('1', 0, len(seq)), seq)
+    slots = [eng.haplotype(0, cpy, copies[cpy])[0] for cpy in (0, 1)]
+    eng.ctx.sample_units([0, 1], slots, [901, 902], rm['p'], rlen, mdl['cum_tlen'], _native.MH_RNG_PHILOX)
+    batched = []
+    for k in (0, 1):
+      eng.ctx.use_templates(k)
+      batched.append(eng.ctx.get_templates())
+    for k in (0, 1):
+      eng.ctx.sample_units([5], [slots[k]], [901 + k], rm['p'], rlen, mdl['cum_tlen'], _native.MH_RNG_PHILOX)
+      eng.ctx.use_templates(5)
+      alone = eng.ctx.get_templates()
+      for x, y in zip(batched[k], alone):
+        assert np.array_equal(x, y)
+  finally:
+    eng.close()

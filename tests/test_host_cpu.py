@@ -220,3 +220,77 @@ def test_native_vcf_errors(tmp_path):
   b.write_text('1\t15\t40\n')
   r = vcfio.load_variants_soa(str(v), 'S', str(b))[0]
   assert r['ploidy'] == 2 and list(r['copies'][0]['pos']) == [5] and list(r['copies'][1]['pos']) == [30]
+
+
+def test_mitty_console_entry_point(tmp_path):
+  """setup.py declares the reference's console command (`mitty = ...cli:cli`, reference setup.py:12) and
+  `python -m mitty_amd` runs the same click group (the qname subcommand prints the reference's format text)."""
+  import subprocess
+  import sys
+  repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+  subprocess.check_call([sys.executable, 'setup.py', '-q', 'egg_info', '--egg-base', str(tmp_path)], cwd=repo,
+                        stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+  eps = open(os.path.join(str(tmp_path), 'mitty_mi355x.egg-info', 'entry_points.txt')).read()
+  assert 'mitty = mitty_amd.cli:cli' in eps
+  out = subprocess.check_output([sys.executable, '-m', 'mitty_amd', 'qname'], cwd=repo).decode()
+  from mitty_amd.simulation.readgenerate import __qname_format_details__
+  assert out.strip() == __qname_format_details__.strip()
+  out = subprocess.check_output([sys.executable, '-m', 'mitty_amd', 'generate-reads', '--help'], cwd=repo).decode()
+  assert '--fastq2' in out and '--threads' in out
+
+
+def test_host_cpp_under_asan_ubsan(tmp_path):
+  """the host C++ that parses untrusted VCF (mh_vcf.cpp) and writes into caller buffers and files
+  (mh_bgzf.cpp: BGZF, BAM framing, BAI) built with -fsanitize=address,undefined and driven over the golden VCFs,
+  mutated / truncated VCFs (plain and gzip), empty and exact-capacity compression buffers: no sanitizer report."""
+  import gzip
+  import shutil
+  import subprocess
+  if shutil.which('g++') is None:
+    pytest.skip('no g++')
+  exe = str(tmp_path / 'san_driver')
+  subprocess.check_call(['g++', '-std=c++17', '-O1', '-g', '-fno-omit-frame-pointer', '-fsanitize=address,undefined',
+                         '-fno-sanitize-recover=undefined', os.path.join(REPO, 'tests', 'sanitize', 'san_driver.cpp'),
+                         os.path.join(REPO, 'mitty_amd', 'csrc', 'mh_vcf.cpp'),
+                         os.path.join(REPO, 'mitty_amd', 'csrc', 'mh_bgzf.cpp'), '-lz', '-lpthread', '-o', exe])
+  src = open(G.path('data/syn.vcf'), 'rb').read()
+  rs = np.random.RandomState(5)
+  cmds = []
+  for k in range(40):
+    b = bytearray(src)
+    kind = k % 5
+    if kind == 0:     # truncated anywhere
+      b = b[:rs.randint(0, len(b))]
+    elif kind == 1:   # random byte flips
+      for _ in range(20):
+        b[rs.randint(len(b))] = rs.randint(256)
+    elif kind == 2:   # fields dropped from random lines
+      lines = bytes(b).split(b'\n')
+      for _ in range(10):
+        i = rs.randint(len(lines))
+        f = lines[i].split(b'\t')
+        lines[i] = b'\t'.join(f[:rs.randint(0, len(f) + 1)])
+      b = bytearray(b'\n'.join(lines))
+    elif kind == 3:   # absurd numbers / genotypes
+      b = bytearray(bytes(b).replace(b'\t0|1', b'\t0|99').replace(b'\t1|0', b'\t.|-3').replace(b'1\t1', b'1\t99999999999999999999', 3))
+    else:             # a gzip member cut short
+      b = bytearray(gzip.compress(bytes(b))[:rs.randint(10, 2000)])
+    fn = str(tmp_path / 'm{}.vcf'.format(k))
+    open(fn, 'wb').write(bytes(b))
+    for chrom, s0, e in (('1', 0, 60000), ('2', 100, 20000), ('3', 0, 10 ** 12)):
+      cmds.append('vcf {} S1 {} {} {}'.format(fn, chrom, s0, e))
+  for v, s, bed in (('syn.vcf', 'S1', 'syn.bed'), ('syn.vcf.gz', 'S1', 'syn.bed'), ('tiny.vcf', 'g0_s0', 'tiny.whole.bed'),
+                    ('flawed-tiny.vcf', 'g0_s0', 'tiny.whole.bed'), ('syn.vcf', 'NOPE', 'syn.bed')):
+    for line in open(G.path('data', bed)):
+      chrom, s0, e = line.split()[:3]
+      cmds.append('vcf {} {} {} {} {}'.format(G.path('data', v), s, chrom, s0, e))
+  cmds += ['bgzf {} {} {} {}'.format(n, lvl, th, n) for n, lvl, th in
+           ((0, 6, 1), (1, 0, 1), (65280, 1, 2), (65281, 9, 3), (300000, 6, 8))]
+  cmds += ['bam {} {} {}'.format(tmp_path / 'b{}.bam'.format(n), n, n) for n in (0, 1, 5000)]
+  env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:abort_on_error=0', UBSAN_OPTIONS='print_stacktrace=1')
+  env.pop('LD_PRELOAD', None)
+  r = subprocess.run([exe], input='\n'.join(cmds).encode(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
+                     timeout=600)
+  err = r.stderr.decode(errors='replace')
+  assert r.returncode == 0 and 'ERROR: AddressSanitizer' not in err and 'runtime error' not in err, err[-4000:]
+  assert r.stdout.count(b'\n') >= len(cmds)
