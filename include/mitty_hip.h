@@ -187,6 +187,16 @@ int32_t mh_vcf_region(mh_vcf *v, const char *chrom, int64_t start0, int64_t end,
                       int64_t *alt_bytes, int32_t cap);
 int32_t mh_vcf_copy(mh_vcf *v, int32_t cpy, int64_t *pos, uint8_t *op, int64_t *oplen, int64_t *alt_off,
                     int64_t *alt_len, char *alt_pool);
+/* filter-variants (vcfio.prepare_variant_file, vcfio.py:129-168; cli.py:20-35): for each of the n_regions BED
+ * regions in order (chroms NUL-separated, start0/end per region), the region's records (the mh_vcf_region overlap
+ * query; a record in two regions is written twice, as the reference writes it) except complex ones — rlen > 1 and
+ * one of the sample's genotype alleles longer than 1 and different from REF (vcfio.py:139-146) — written to
+ * out_path with the first 9 columns and the sample's column (BGZF-compressed on `threads` threads when bgzf != 0).
+ * Header: the input's meta lines and the #CHROM line cut to the sample.  A missing allele on a multi-base record is
+ * MH_E_ARG (the reference raises TypeError there).  err (err_cap bytes) receives the message on failure. */
+int32_t mh_vcf_filter(const char *in_path, const char *sample, int32_t n_regions, const char *chroms,
+                      const int64_t *start0, const int64_t *end, const char *out_path, int32_t bgzf, int32_t threads,
+                      int64_t *n_written, int64_t *n_filtered, char *err, int32_t err_cap);
 
 /* ---- compressed FASTQ sink: host-side BGZF (gzip-compatible members of <= 65280 input
  * bytes, deflated on `threads` threads).  MH_E_CAPACITY if `cap` is short (*used = bytes needed).  mh_bgzf_eof

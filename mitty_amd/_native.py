@@ -23,7 +23,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
-           'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy']
+           'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter']
 
 
 class NativeError(RuntimeError):
@@ -95,6 +95,8 @@ def lib():
   _sig(L, 'mh_vcf_close', [c_vp])
   _sig(L, 'mh_vcf_region', [c_vp, ctypes.c_char_p, c_i64, c_i64, ctypes.POINTER(c_i32), c_vp, c_vp, c_i32])
   _sig(L, 'mh_vcf_copy', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_vcf_filter', [ctypes.c_char_p, ctypes.c_char_p, c_i32, c_vp, c_vp, c_vp, ctypes.c_char_p, c_i32, c_i32,
+                            P_i64, P_i64, ctypes.c_char_p, c_i32])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
@@ -186,6 +188,22 @@ class VcfFile:
       copies.append({'pos': pos, 'op': op, 'oplen': oplen, 'alt_off': aoff, 'alt_len': alen,
                      'alt_pool': pool[:nb].tobytes()})
     return pl.value, copies
+
+
+def vcf_filter(path_in, sample, regions, path_out, bgzf=False, threads=8):
+  """filter-variants (mh_vcf_filter): regions [(chrom, start0, end)] in BED order.  Returns (written, filtered)."""
+  L = lib()
+  chroms = b''.join(c.encode() + b'\0' for c, _, _ in regions) or b'\0'
+  s0 = np.array([r[1] for r in regions] or [0], np.int64)
+  e = np.array([r[2] for r in regions] or [0], np.int64)
+  cbuf = ctypes.create_string_buffer(chroms, len(chroms))
+  w, f = c_i64(), c_i64()
+  err = ctypes.create_string_buffer(1024)
+  rc = L.mh_vcf_filter(path_in.encode(), sample.encode(), len(regions), ctypes.cast(cbuf, c_vp), _ptr(s0), _ptr(e),
+                       path_out.encode(), 1 if bgzf else 0, int(threads), ctypes.byref(w), ctypes.byref(f), err, 1024)
+  if rc:
+    _raise(rc, err.value.decode())
+  return w.value, f.value
 
 
 def bgzf_eof():

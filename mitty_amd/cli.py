@@ -1,10 +1,11 @@
 """`mitty` command line (reference mitty/cli.py), MI355X build.
 
-Implemented: generate-reads (GPU), corrupt-reads (GPU), god-aligner (GPU), qname, list-read-models.  Additive options on generate-reads: --device,
+Implemented: generate-reads (GPU), corrupt-reads (GPU), god-aligner (GPU), filter-variants (host C++), qname,
+list-read-models.  Additive options on generate-reads: --device,
 --rng {mitty,philox}, --corrupt-seed (fused Philox corruption); on corrupt-reads: --device, --rng {mitty,philox}.  Multi-GPU: launch generate-reads under
 `python -m torch.distributed.run --nproc-per-node N -m mitty_amd.cli generate-reads ...` (one process per GPU,
 RCCL); the output files are identical to the one-GPU run.  Out of scope for this build (not on the
-generate-reads path): filter-variants, filter-bam, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
+generate-reads path): filter-bam, gc-cov, bq, bam2illumina, describe-read-model, mq-plot, derr-plot.
 """
 import logging
 import os
@@ -18,6 +19,18 @@ import click
 def cli(verbose):
   """A genomic data simulator for testing and debugging bio-informatics tools"""
   logging.basicConfig(level=[logging.ERROR, logging.WARNING, logging.INFO, logging.DEBUG][min(verbose, 3)])
+
+
+@cli.command('filter-variants', short_help='Remove complex variants from VCF')
+@click.argument('vcfin', type=click.Path(exists=True))
+@click.argument('sample')
+@click.argument('bed')
+@click.argument('vcfout', type=click.Path())
+def filter_vcf(vcfin, sample, bed, vcfout):
+  """Subset VCF for given sample, apply BED file and filter out complex variants
+   making it suitable to use for read generation (reference cli.py:20-35)"""
+  from mitty_amd.lib import vcfio
+  vcfio.prepare_variant_file(vcfin, sample, bed, vcfout)
 
 
 @cli.command('list-read-models')

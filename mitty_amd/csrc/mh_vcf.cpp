@@ -9,9 +9,18 @@
 //  * per copy c: records with GT[c] != 0; alt = (REF, ALT...)[GT[c]]; X (ref 1, alt 1), I (ref 1, alt > 1,
 //    oplen = len(alt) - 1), D (ref > 1, alt 1, oplen = len(ref) - 1), anything else is a complex variant
 //    (vcfio.py:116-124).
+//
+// filter-variants (vcfio.prepare_variant_file, vcfio.py:129-168; cli.py:20-35): mh_vcf_filter writes, per BED region
+// in BED order, the region's records (the same overlap query; a record in two regions is written twice, as the
+// reference's loop writes it twice) except complex ones, keeping the first 9 columns and the sample's column.
+// Complex (vcfio.py:139-146): rlen > 1 and one of the sample's genotype alleles is longer than 1 and differs from
+// REF.  Header: the input's meta lines, the #CHROM line cut to the sample (htslib's header re-serialisation is not
+// reproduced: no htslib here).
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -26,7 +35,14 @@ struct mh_vcf {
     int64_t pos1, rlen;
     uint64_t ref_off, alt_off, gt_off;   // into `text`
     uint32_t ref_len, alt_len, gt_len;
+    uint64_t head_off = 0, smp_off = 0;  // filter-variants: the record's first 9 columns and the sample's column
+    uint32_t head_len = 0, smp_len = 0;
   };
+  bool keep_lines = false;
+  std::string meta;        // '##' lines (keep_lines)
+  std::string chrom_head;  // the #CHROM line's first 9 columns (keep_lines)
+  std::string sample;
+  std::vector<std::string> order;   // contigs in file order
   std::unordered_map<std::string, std::vector<Rec>> by_chrom;
   std::string text;   // REF / ALT / GT fields of every record
   // last region query
@@ -90,13 +106,7 @@ void gt_alleles(const char *s, size_t n, std::vector<int> &g) {
 
 }  // namespace
 
-extern "C" {
-
-int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out) {
-  if (!path || !sample || !out) return MH_E_ARG;
-  *out = nullptr;
-  mh_vcf *v = new mh_vcf();
-  *out = v;
+static int32_t vcf_load(const char *path, const char *sample, mh_vcf *v) {
   gzFile fp = gzopen(path, "rb");
   if (!fp) return fail(v, MH_E_ARG, std::string("cannot open ") + path);
   gzbuffer(fp, 1 << 20);
@@ -108,9 +118,13 @@ int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out) {
   int32_t rc = MH_OK;
   auto line_fn = [&](const char *s, size_t n) -> int32_t {
     if (n && s[n - 1] == '\r') n--;
-    if (n >= 2 && s[0] == '#' && s[1] == '#') return MH_OK;
+    if (n >= 2 && s[0] == '#' && s[1] == '#') {
+      if (v->keep_lines) v->meta.append(s, n).push_back('\n');
+      return MH_OK;
+    }
     if (n >= 6 && memcmp(s, "#CHROM", 6) == 0) {
       tabs(s, n, f, SIZE_MAX);
+      if (v->keep_lines && f.size() >= 9) v->chrom_head.assign(s, f[8].second);
       for (size_t i = 0; i < f.size(); i++)
         if (std::string(s + f[i].first, f[i].second - f[i].first) == smp) col = (long)i;
       if (col < 9) return fail(v, MH_E_ARG, "invalid sample name: " + smp);
@@ -176,7 +190,18 @@ int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out) {
     r.gt_off = v->text.size();
     r.gt_len = (uint32_t)gt.size();
     v->text += gt;
-    v->by_chrom[std::string(s + f[0].first, f[0].second - f[0].first)].push_back(r);
+    if (v->keep_lines) {
+      r.head_off = v->text.size();
+      r.head_len = (uint32_t)f[8].second;
+      v->text.append(s, f[8].second);
+      r.smp_off = v->text.size();
+      r.smp_len = (uint32_t)(f[col].second - f[col].first);
+      v->text.append(s + f[col].first, r.smp_len);
+    }
+    std::string chrom(s + f[0].first, f[0].second - f[0].first);
+    auto &lst = v->by_chrom[chrom];
+    if (lst.empty()) v->order.push_back(chrom);
+    lst.push_back(r);
     return MH_OK;
   };
   for (;;) {
@@ -208,6 +233,129 @@ int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out) {
   return rc;
 }
 
+// the records of `chrom` overlapping [start0, end) (htslib: pos0 < end and pos0 + rlen > start0), in file order
+static void region_records(const mh_vcf *v, const char *chrom, int64_t start0, int64_t end,
+                           std::vector<const mh_vcf::Rec *> &recs) {
+  recs.clear();
+  auto it = v->by_chrom.find(chrom);
+  if (it == v->by_chrom.end()) return;
+  for (const auto &r : it->second)
+    if (r.pos1 - 1 < end && r.pos1 - 1 + r.rlen > start0) recs.push_back(&r);
+}
+
+// ALT alleles of a record as [begin, end) offsets into its ALT field ('.' = none)
+static void alt_spans(const char *alt, uint32_t n, std::vector<std::pair<size_t, size_t>> &alts) {
+  alts.clear();
+  if (n == 1 && alt[0] == '.') return;
+  size_t a = 0;
+  for (size_t i = 0; i <= n; i++)
+    if (i == n || alt[i] == ',') {
+      alts.emplace_back(a, i);
+      a = i + 1;
+    }
+}
+
+extern "C" {
+
+int32_t mh_vcf_open(const char *path, const char *sample, mh_vcf **out) {
+  if (!path || !sample || !out) return MH_E_ARG;
+  *out = nullptr;
+  mh_vcf *v = new mh_vcf();
+  *out = v;
+  return vcf_load(path, sample, v);
+}
+
+int32_t mh_vcf_filter(const char *in_path, const char *sample, int32_t n_regions, const char *chroms,
+                      const int64_t *start0, const int64_t *end, const char *out_path, int32_t bgzf, int32_t threads,
+                      int64_t *n_written, int64_t *n_filtered, char *err, int32_t err_cap) {
+  auto set_err = [&](const std::string &m) {
+    if (err && err_cap > 0) {
+      const size_t k = std::min<size_t>(m.size(), (size_t)err_cap - 1);
+      memcpy(err, m.data(), k);
+      err[k] = 0;
+    }
+  };
+  if (!in_path || !sample || !out_path || n_regions < 0 || (n_regions > 0 && (!chroms || !start0 || !end))) {
+    set_err("bad arguments");
+    return MH_E_ARG;
+  }
+  mh_vcf v;
+  v.keep_lines = true;
+  int32_t rc = vcf_load(in_path, sample, &v);
+  if (rc != MH_OK) {
+    set_err(v.err);
+    return rc;
+  }
+  std::string out = v.meta + v.chrom_head + "\t" + sample + "\n";
+  int64_t written = 0, filtered = 0;
+  std::vector<const mh_vcf::Rec *> recs;
+  std::vector<std::pair<size_t, size_t>> alts;
+  std::vector<int> g;
+  const char *cp = chroms;
+  for (int32_t k = 0; k < n_regions; k++) {
+    region_records(&v, cp, start0[k], end[k], recs);
+    for (const mh_vcf::Rec *r : recs) {
+      const char *ref = v.text.data() + r->ref_off;
+      const char *alt = v.text.data() + r->alt_off;
+      alt_spans(alt, r->alt_len, alts);
+      gt_alleles(v.text.data() + r->gt_off, r->gt_len, g);
+      bool complex = false;
+      if (r->rlen > 1) {
+        for (int a : g) {
+          if (a < 0) {   // the reference takes len(None) here (TypeError)
+            set_err("missing genotype allele on a multi-base record at " + std::string(cp) + ":" +
+                    std::to_string(r->pos1));
+            return MH_E_ARG;
+          }
+          if ((size_t)a > alts.size()) {
+            set_err("GT allele index out of range at " + std::string(cp) + ":" + std::to_string(r->pos1));
+            return MH_E_ARG;
+          }
+          const char *as = a == 0 ? ref : alt + alts[a - 1].first;
+          const size_t al = a == 0 ? r->ref_len : alts[a - 1].second - alts[a - 1].first;
+          if (al > 1 && !(al == r->ref_len && memcmp(as, ref, al) == 0)) complex = true;
+        }
+      }
+      if (complex) {
+        filtered++;
+        continue;
+      }
+      out.append(v.text.data() + r->head_off, r->head_len).push_back('\t');
+      out.append(v.text.data() + r->smp_off, r->smp_len).push_back('\n');
+      written++;
+    }
+    cp += strlen(cp) + 1;
+  }
+  std::string data;
+  if (bgzf) {
+    int64_t need = 0;
+    mh_bgzf_compress(out.data(), (int64_t)out.size(), 6, threads, nullptr, 0, &need);
+    data.resize((size_t)need + 28);
+    int64_t used = 0;
+    rc = mh_bgzf_compress(out.data(), (int64_t)out.size(), 6, threads, &data[0], need, &used);
+    if (rc != MH_OK) {
+      set_err("BGZF compression failed");
+      return rc;
+    }
+    mh_bgzf_eof(&data[(size_t)used]);
+    data.resize((size_t)used + 28);
+  }
+  const std::string &bytes = bgzf ? data : out;
+  FILE *fp = fopen(out_path, "wb");
+  if (!fp) {
+    set_err(std::string("cannot open ") + out_path);
+    return MH_E_ARG;
+  }
+  const bool ok = fwrite(bytes.data(), 1, bytes.size(), fp) == bytes.size();
+  if (fclose(fp) != 0 || !ok) {
+    set_err(std::string("write failed: ") + out_path);
+    return MH_E_ARG;
+  }
+  if (n_written) *n_written = written;
+  if (n_filtered) *n_filtered = filtered;
+  return MH_OK;
+}
+
 const char *mh_vcf_error(const mh_vcf *v) { return v ? v->err.c_str() : "null handle"; }
 
 int32_t mh_vcf_close(mh_vcf *v) {
@@ -221,10 +369,7 @@ int32_t mh_vcf_region(mh_vcf *v, const char *chrom, int64_t start0, int64_t end,
   v->copies.clear();
   v->ploidy = 0;
   std::vector<const mh_vcf::Rec *> recs;
-  auto it = v->by_chrom.find(chrom);
-  if (it != v->by_chrom.end())
-    for (const auto &r : it->second)
-      if (r.pos1 - 1 < end && r.pos1 - 1 + r.rlen > start0) recs.push_back(&r);
+  region_records(v, chrom, start0, end, recs);
   std::vector<int> g;
   int32_t pl = 2;
   if (!recs.empty()) {
@@ -241,15 +386,7 @@ int32_t mh_vcf_region(mh_vcf *v, const char *chrom, int64_t start0, int64_t end,
                                    " has fewer GT entries than the region ploidy");
     const char *ref = v->text.data() + r->ref_off;
     const char *alt = v->text.data() + r->alt_off;
-    alts.clear();
-    if (!(r->alt_len == 1 && alt[0] == '.')) {
-      size_t a = 0;
-      for (size_t i = 0; i <= r->alt_len; i++)
-        if (i == r->alt_len || alt[i] == ',') {
-          alts.emplace_back(a, i);
-          a = i + 1;
-        }
-    }
+    alt_spans(alt, r->alt_len, alts);
     for (int32_t c = 0; c < pl; c++) {
       if (g[c] == 0) continue;
       if (g[c] < 0)

@@ -203,3 +203,19 @@ def soa_from_variants(vl):
           'op': np.frombuffer(''.join(v.cigarop for v in vl).encode(), dtype=np.uint8).copy(),
           'oplen': np.array([v.oplen for v in vl], dtype=np.int64), 'alt_off': alt_off, 'alt_len': alt_len,
           'alt_pool': b''.join(alts)}
+
+
+def prepare_variant_file(fname_in, sample, bed_fname, fname_out, write_mode='w'):
+  """vcfio.prepare_variant_file (vcfio.py:129-168): the sample's column only, restricted to the BED regions, complex
+  calls dropped — on the host VCF reader (mh_vcf_filter).  write_mode 'wz' (or an output name ending in .gz) writes
+  BGZF.  Returns (records written, records filtered)."""
+  import time
+  from mitty_amd import _native
+  t0 = time.time()
+  regions = read_bed(bed_fname)
+  written, filtered = _native.vcf_filter(fname_in, sample, regions, fname_out,
+                                         bgzf='z' in write_mode or fname_out.endswith('.gz'))
+  logger.debug('Wrote {} variants'.format(written))
+  logger.debug('Filtered out {} complex variants'.format(filtered))
+  logger.debug('Took {} s'.format(time.time() - t0))
+  return written, filtered

@@ -8,6 +8,10 @@ Semantics restated from htslib as the reference relies on them (SURVEY.md Append
   file order.
 * record.samples[0]['GT'] is a tuple of ints (None for '.'); record.samples[0].alleles maps each GT entry to its
   allele string ((REF,)+ALTS indexed by the GT value).
+* rlen = END - POS + 1 when INFO carries END=, else len(REF) (htslib).
+* VariantFile(fname, 'w', header=...): a writer that records each written record as its first 9 columns plus the
+  subset sample's column (what the retained-record fixture of filter-variants compares; htslib's own re-serialisation
+  of header and fields is not reproduced).
 """
 import gzip
 
@@ -57,21 +61,43 @@ class _Samples(list):
 
 
 class _Record:
-  __slots__ = ('contig', 'pos', 'ref', 'alts', 'rlen', 'samples')
+  __slots__ = ('contig', 'pos', 'ref', 'alts', 'rlen', 'samples', 'raw')
+
+
+class _Header:
+  def __init__(self, lines, samples):
+    self.lines, self.samples = lines, samples
 
 
 class VariantFile:
   def __init__(self, fname, mode='r', header=None):
-    self.records, self.sample_names, self._col = [], [], None
+    self.records, self.sample_names, self._col, self._meta = [], [], None, []
+    if mode.startswith('w'):
+      self._out = open(fname, 'w')
+      for line in header.lines:
+        self._out.write(line + '\n')
+      self._out.write('\t'.join(['#CHROM', 'POS', 'ID', 'REF', 'ALT', 'QUAL', 'FILTER', 'INFO', 'FORMAT'] +
+                                 header.samples) + '\n')
+      return
+    self._out = None
     with _open_text(fname) as fp:
       for line in fp:
         if line.startswith('##'):
+          self._meta.append(line.rstrip('\n'))
           continue
         f = line.rstrip('\n').split('\t')
         if line.startswith('#CHROM'):
           self.sample_names = f[9:]
           continue
         self.records.append(f)
+
+  @property
+  def header(self):
+    return _Header(self._meta, [self.sample_names[self._col - 9]] if self._col is not None else self.sample_names)
+
+  def write(self, rec):
+    self._out.write('\t'.join(rec.raw) + '\n')
+    self._out.flush()
 
   def subset_samples(self, samples):
     self._col = 9 + self.sample_names.index(samples[0])
@@ -81,7 +107,11 @@ class VariantFile:
     r.contig, r.pos, r.ref = f[0], int(f[1]), f[3]
     r.alts = tuple(f[4].split(',')) if f[4] != '.' else None
     r.rlen = len(r.ref)
+    for kv in f[7].split(';'):
+      if kv.startswith('END='):
+        r.rlen = int(kv[4:]) - r.pos + 1
     col = self._col if self._col is not None else 9
+    r.raw = f[:9] + [f[col]]
     fmt = f[8].split(':')
     gt_txt = f[col].split(':')[fmt.index('GT')]
     gt = tuple(None if g == '.' else int(g) for g in gt_txt.replace('/', '|').split('|'))
@@ -94,10 +124,10 @@ class VariantFile:
     for f in self.records:
       if f[0] != contig:
         continue
-      beg = int(f[1]) - 1
-      end = beg + len(f[3])
-      if beg < stop and end > start:
-        yield self._make(f)
+      r = self._make(f)
+      beg = r.pos - 1
+      if beg < stop and beg + r.rlen > start:
+        yield r
 
 
 class _FastxRecord:

@@ -1,7 +1,8 @@
 // Host-side sanitizer driver (TEST INFRASTRUCTURE): the host C++ that parses untrusted input (mh_vcf.cpp) and writes
 // into caller buffers / files (mh_bgzf.cpp), built with -fsanitize=address,undefined by tests/test_host_cpu.py.
 // Commands on stdin, one per line:
-//   vcf <path> <sample> <chrom> <start0> <end>   open, query one region, copy every copy out
+//   vcf <path> <sample> <chrom> <start0> <end>   open, query one region, copy every copy out; then filter-variants
+//                                                 of that region into <path>.filt.vcf(.gz)
 //   bgzf <nbytes> <level> <threads> <seed>       compress pseudo-random bytes (short and exact-capacity buffers too)
 //   bam <path> <n_records> <seed>                BGZF BAM + BAI of synthetic sorted records
 #include <cstdint>
@@ -22,6 +23,14 @@ static uint64_t rnd(uint64_t &s) {
 
 static int run_vcf(const std::string &path, const std::string &sample, const std::string &chrom, int64_t s0,
                    int64_t e) {
+  char err[256];
+  int64_t w = 0, fl = 0;
+  const std::string reg = chrom + std::string(1, '\0');
+  for (int z = 0; z < 2; z++) {
+    const int32_t frc = mh_vcf_filter(path.c_str(), sample.c_str(), 1, reg.c_str(), &s0, &e,
+                       (path + (z ? ".filt.vcf.gz" : ".filt.vcf")).c_str(), z, 2, &w, &fl, err, (int32_t)sizeof err);
+    std::printf("filter rc=%d written=%lld filtered=%lld\n", frc, (long long)w, (long long)fl);
+  }
   mh_vcf *v = nullptr;
   int32_t rc = mh_vcf_open(path.c_str(), sample.c_str(), &v);
   if (rc != MH_OK) {

@@ -281,9 +281,11 @@ def test_host_cpp_under_asan_ubsan(tmp_path):
       cmds.append('vcf {} S1 {} {} {}'.format(fn, chrom, s0, e))
   for v, s, bed in (('syn.vcf', 'S1', 'syn.bed'), ('syn.vcf.gz', 'S1', 'syn.bed'), ('tiny.vcf', 'g0_s0', 'tiny.whole.bed'),
                     ('flawed-tiny.vcf', 'g0_s0', 'tiny.whole.bed'), ('syn.vcf', 'NOPE', 'syn.bed')):
+    local = str(tmp_path / v)   # filter-variants writes <vcf>.filt.vcf next to its input
+    shutil.copy(G.path('data', v), local)
     for line in open(G.path('data', bed)):
       chrom, s0, e = line.split()[:3]
-      cmds.append('vcf {} {} {} {} {}'.format(G.path('data', v), s, chrom, s0, e))
+      cmds.append('vcf {} {} {} {} {}'.format(local, s, chrom, s0, e))
   cmds += ['bgzf {} {} {} {}'.format(n, lvl, th, n) for n, lvl, th in
            ((0, 6, 1), (1, 0, 1), (65280, 1, 2), (65281, 9, 3), (300000, 6, 8))]
   cmds += ['bam {} {} {}'.format(tmp_path / 'b{}.bam'.format(n), n, n) for n in (0, 1, 5000)]
@@ -294,3 +296,40 @@ def test_host_cpp_under_asan_ubsan(tmp_path):
   err = r.stderr.decode(errors='replace')
   assert r.returncode == 0 and 'ERROR: AddressSanitizer' not in err and 'runtime error' not in err, err[-4000:]
   assert r.stdout.count(b'\n') >= len(cmds)
+
+
+@pytest.mark.parametrize('out_name', ['out.vcf', 'out.vcf.gz'])
+def test_filter_variants_matches_reference(tmp_path, out_name):
+  """filter-variants (vcfio.prepare_variant_file, vcfio.py:129-168) keeps exactly the records the reference writes
+  (tests/golden/filter_variants.json, captured by make_golden_filter.py): BED order, records in two overlapping
+  regions written twice, complex calls of the sample's genotype dropped, INFO END spans, haploid / missing GTs on
+  single-base records.  Header text is parity-unpinned (htslib re-serialises it; no htslib here)."""
+  import gzip
+  from click.testing import CliRunner
+  from mitty_amd.cli import cli
+  want = G.load_json('filter_variants.json')
+  out = str(tmp_path / out_name)
+  res = CliRunner().invoke(cli, ['filter-variants', G.path('data/filt.vcf'), 'S1', G.path('data/filt.bed'), out])
+  assert res.exit_code == 0, res.output + repr(res.exception)
+  raw = open(out, 'rb').read()
+  text = (gzip.decompress(raw) if out_name.endswith('.gz') else raw).decode()
+  lines = text.rstrip('\n').split('\n')
+  head = [ln for ln in lines if ln.startswith('#')]
+  assert head[-1].split('\t')[9:] == ['S1'] and head[0] == '##fileformat=VCFv4.1'
+  recs = [ln.split('\t') for ln in lines if not ln.startswith('#')]
+  assert all(len(f) == 10 for f in recs)
+  assert [[f[0], int(f[1]), f[2], f[3], f[4], f[9]] for f in recs] == want['records']
+  w, f = vcfio.prepare_variant_file(G.path('data/filt.vcf'), 'S1', G.path('data/filt.bed'), str(tmp_path / 'b.vcf'))
+  assert w == len(want['records']) and f > 0
+
+
+def test_filter_variants_errors(tmp_path):
+  bad = tmp_path / 'bad.vcf'
+  bad.write_text('##fileformat=VCFv4.1\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1\n'
+                 '1\t5\t.\tAC\tA\t50\tPASS\t.\tGT\t.|1\n')
+  bed = tmp_path / 'b.bed'
+  bed.write_text('1\t0\t100\n')
+  with pytest.raises(ValueError, match='missing genotype'):
+    vcfio.prepare_variant_file(str(bad), 'S1', str(bed), str(tmp_path / 'o.vcf'))
+  with pytest.raises(ValueError, match='sample'):
+    vcfio.prepare_variant_file(str(bad), 'NOPE', str(bed), str(tmp_path / 'o.vcf'))
