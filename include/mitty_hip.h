@@ -112,6 +112,15 @@ int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id);
 int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, const int64_t *pos1, int64_t n,
                          int32_t rlen);
 int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1, int64_t cap, int64_t *n);
+/* Multi-GPU template sharing (a few-unit job samples each unit once, on one rank, and sends its
+ * arrays to the ranks that emit slices of it).  on_device != 0: the pointers are device buffers of this context's
+ * GPU (e.g. the buffers an RCCL broadcast fills); otherwise host memory.
+ *   mh_templates_export  template set tpl_id -> fo0[n], pos0[n], pos1[n] (*n = its size; MH_E_CAPACITY if cap < n)
+ *   mh_templates_import  template set tpl_id := the n templates in the buffers (rlen = read length) */
+int32_t mh_templates_export(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, int8_t *fo0, int64_t *pos0,
+                            int64_t *pos1, int64_t cap, int64_t *n);
+int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, const int8_t *fo0, const int64_t *pos0,
+                            const int64_t *pos1, int64_t n, int32_t rlen);
 
 /* ---- read emission ------------------------------------------------------------------------------------- */
 /* Turn the current templates into FASTQ text for both files, appended to the device arenas.

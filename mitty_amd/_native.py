@@ -18,7 +18,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
@@ -103,6 +103,8 @@ def lib():
   _sig(L, 'mh_read_batch', [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64])
   _sig(L, 'mh_set_corruption', [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_u64])
+  _sig(L, 'mh_templates_export', [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_templates_import', [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i64, c_i32])
   _sig(L, 'mh_set_corruption_stream', [c_vp, c_i32, c_u64, c_vp, c_i32])
   _sig(L, 'mh_get_corruption_stream', [c_vp, c_vp, ctypes.POINTER(c_i32), P_i64])
   _sig(L, 'mh_stage_times', [c_vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_dbl), c_i32,
@@ -518,6 +520,32 @@ class Context:
     cb = np.ascontiguousarray(cum_bq, dtype=np.float64)
     ph = np.ascontiguousarray(phred_p, dtype=np.float64)
     self._chk(self._L.mh_set_corruption(self._h, 1, _ptr(cb), cb.shape[1], cb.shape[2], _ptr(ph), int(seed)))
+
+  def templates_export(self, tpl_id, fo0=None, pos0=None, pos1=None, cap=None):
+    """Template set tpl_id's arrays.  With device pointers (ints) fo0/pos0/pos1 and cap: copied there on the device,
+    returns n; without: returns host arrays (fo0, pos0, pos1)."""
+    n = c_i64()
+    if fo0 is not None:
+      self._chk(self._L.mh_templates_export(self._h, int(tpl_id), 1, c_vp(fo0), c_vp(pos0), c_vp(pos1), int(cap),
+                                            ctypes.byref(n)))
+      return n.value
+    self._L.mh_templates_export(self._h, int(tpl_id), 0, None, None, None, 0, ctypes.byref(n))
+    m = n.value
+    a, b, c = np.empty(max(m, 1), np.int8), np.empty(max(m, 1), np.int64), np.empty(max(m, 1), np.int64)
+    self._chk(self._L.mh_templates_export(self._h, int(tpl_id), 0, _ptr(a), _ptr(b), _ptr(c), max(m, 1),
+                                          ctypes.byref(n)))
+    return a[:m], b[:m], c[:m]
+
+  def templates_import(self, tpl_id, n, rlen, fo0, pos0, pos1, on_device=False):
+    """Template set tpl_id := n templates from host arrays, or from device pointers (ints) with on_device."""
+    if on_device:
+      self._chk(self._L.mh_templates_import(self._h, int(tpl_id), 1, c_vp(fo0), c_vp(pos0), c_vp(pos1), int(n),
+                                            int(rlen)))
+      return
+    a = np.ascontiguousarray(fo0, dtype=np.int8)
+    b = np.ascontiguousarray(pos0, dtype=np.int64)
+    c = np.ascontiguousarray(pos1, dtype=np.int64)
+    self._chk(self._L.mh_templates_import(self._h, int(tpl_id), 0, _ptr(a), _ptr(b), _ptr(c), int(n), int(rlen)))
 
   def set_corruption_stream(self, rng_mode, seed=0, key=None, pos=624):
     """mh_corrupt_fastq's word source: MH_RNG_PHILOX, or MH_RNG_MITTY = the reference's exact MT19937 stream

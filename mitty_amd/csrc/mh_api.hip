@@ -534,6 +534,52 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
   return MH_OK;
 }
 
+int32_t mh_templates_export(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, int8_t *fo0, int64_t *pos0,
+                            int64_t *pos1, int64_t cap, int64_t *n) {
+  CTX_GUARD(ctx);
+  auto it = ctx->tsets.find(tpl_id);
+  if (it == ctx->tsets.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  const TplSet &ts = it->second;
+  if (n) *n = ts.n;
+  if (cap < ts.n) return arg_fail(ctx, MH_E_CAPACITY, "template buffers too small");
+  const size_t m = (size_t)ts.n;
+  const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (m) {
+    if (fo0) HIPCHK(ctx, hipMemcpyAsync(fo0, ts.fo0.p, m, k, ctx->stream));
+    if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ts.pos0.p, 8 * m, k, ctx->stream));
+    if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ts.pos1.p, 8 * m, k, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, const int8_t *fo0, const int64_t *pos0,
+                            const int64_t *pos1, int64_t n, int32_t rlen) {
+  CTX_GUARD(ctx);
+  if (n < 0 || rlen <= 0 || (n > 0 && (!fo0 || !pos0 || !pos1))) return arg_fail(ctx, MH_E_ARG, "bad templates");
+  if (!on_device)
+    for (int64_t i = 0; i < n; i++)
+      if (fo0[i] != 0 && fo0[i] != 1) return arg_fail(ctx, MH_E_ARG, "file_order must be 0/1");
+  TplSet &ts = ctx->tsets[tpl_id];
+  MH_TRY(wait_unused(ctx, ts.used, ts.used_set));   // a queued FASTQ writer may still read the old templates
+  ts.valid = false;
+  MH_TRY(ensure(ctx, ts.fo0, n + 16));
+  MH_TRY(ensure(ctx, ts.pos0, 8 * (n + 16)));
+  MH_TRY(ensure(ctx, ts.pos1, 8 * (n + 16)));
+  const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(ts.fo0.p, fo0, n, k, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ts.pos0.p, pos0, 8 * n, k, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ts.pos1.p, pos1, 8 * n, k, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ts.prep.valid = false;
+  ts.n = n;
+  ts.rlen = rlen;
+  ts.valid = true;
+  return MH_OK;
+}
+
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   CTX_GUARD_NOJOIN(ctx);

@@ -92,6 +92,15 @@ __device__ __forceinline__ int ndig_u(uint64_t v) {
 }
 __device__ __forceinline__ int ndig_s(int64_t v) { return v < 0 ? 1 + ndig_u((uint64_t)(-v)) : ndig_u((uint64_t)v); }
 
+// decimal digits of a value >= 2^32, most significant first, through put(c) (no digit array: a private array would
+// be placed in scratch memory); never on the hot path (positions and counts fit 32 bits)
+#define put_big(v)                                                          \
+  do {                                                                      \
+    uint64_t _d = 1;                                                        \
+    while ((v) / _d >= 10u) _d *= 10u;                                      \
+    for (; _d; _d /= 10u) put((uint8_t)('0' + ((v) / _d) % 10u));           \
+  } while (0)
+
 __device__ __forceinline__ char *put_u(char *d, uint64_t v) {
   int nd = ndig_u(v);
   if (v <= 0xffffffffull) {
@@ -267,10 +276,7 @@ struct ByteWriter {
       } while (x);
       for (int i = nd - 1; i >= 0; i--) put((uint8_t)('0' + ((bcd >> (4 * i)) & 15)));
     } else {
-      char tmp[24];
-      int nd = 0;
-      do { tmp[nd++] = (char)('0' + v % 10u); v /= 10u; } while (v);
-      for (int i = nd - 1; i >= 0; i--) put((uint8_t)tmp[i]);
+      put_big(v);
     }
   }
   __device__ __forceinline__ void put_s(int64_t v) {
@@ -357,10 +363,7 @@ struct SplitWriter {
         putk(L1 >> (8 * (4 - nd)), nd);
       }
     } else {
-      char tmp[24];
-      int nd = 0;
-      do { tmp[nd++] = (char)('0' + v % 10u); v /= 10u; } while (v);
-      for (int i = nd - 1; i >= 0; i--) put((uint8_t)tmp[i]);
+      put_big(v);
     }
   }
   __device__ __forceinline__ void put_s(int64_t v) {
@@ -368,14 +371,34 @@ struct SplitWriter {
   }
 };
 
+// Length of one read's part of the qname ('|' strand '|' pos '|' rlen '|' cigar '|' v1,v2,..; readgenerate.py:223-225)
+// for the read of length rlen at p whose start / end nodes are n0 (node nd0) .. n1.
+__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
+                                                 bool special, int64_t pos, int64_t p, int64_t rlen) {
+  int32_t L = 3 + ndig_s(pos) + 1 + ndig_s(rlen) + 1 + 1;
+  if (special) L += 1 + ndig_s(p - nd0.ps()) + 1 + ndig_s(rlen) + 1;
+  int32_t nv = 0;
+  for (int64_t k = n0; k <= n1; k++) {
+    const Node16 n = k == n0 ? nd0 : h.nd[k];
+    if (!special) L += ndig_s(node_count(n, p, rlen)) + 1;
+    if (n.code() != 0) {
+      L += ndig_s(node_v(n)) + (nv ? 1 : 0);
+      nv++;
+    }
+  }
+  return L;
+}
+
+// SLOTS: format the reads part into the 256-byte slots (MH_EMIT_SLOTS layout); otherwise record lengths only.
+template <bool SLOTS>
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
                                                       Rec *recs, int32_t *max_rec, uint8_t *slots,
                                                       int32_t *overflow, int32_t dbg) {
   // the reads part is formatted into LDS (bytes past MS_STG straight to the slot) and leaves in coalesced 16-byte
   // chunks after the barrier
-  __shared__ uint32_t stg[256][MS_STG / 4 + 1];   // odd row stride: the per-thread rows spread over all banks
-  __shared__ int32_t s_n[256];
+  __shared__ uint32_t stg[SLOTS ? 256 : 1][MS_STG / 4 + 1];   // odd row stride: rows spread over all banks
+  __shared__ int32_t s_n[SLOTS ? 256 : 1];
   __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
   const bool runs_lds = h.n_runs <= MS_RUNS;
   if (runs_lds)
@@ -408,7 +431,21 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
              count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
     }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
-    if (keep) {
+    if (!SLOTS && keep) {   // lengths only: the writer formats the reads part itself
+      const int32_t l0 = read_part_len(h, nn0[0], r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
+      const int32_t l1 = read_part_len(h, nn0[1], r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
+      const int32_t rest = l0 + l1;
+      const int32_t ql = q.prefix_len + q.mid_len + rest;
+      const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
+      const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
+      const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
+      out.keep = 1 | ((f0 == 0 ? l0 : l1) << 1);   // kept; the first read's part length (where the second starts)
+      out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
+      out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
+      out.rest = rest;
+      local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+      nbytes = rest + 1;
+    } else if (SLOTS && keep) {
       // the reads part of the qname, in file order (readgenerate.py:223-225), and the qname's '\n': formatted into
       // the slot while it fits, counted either way (its length sizes the records)
       SplitWriter bw{stg[threadIdx.x], slots && !(dbg & 1) ? (uint32_t *)(slots + t * SLOT) : nullptr, 0ull, 0, 0, 0};
@@ -468,9 +505,9 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     if (local_max > 0 && local_max > __builtin_nontemporal_load(max_rec)) atomicMax(max_rec, local_max);
     if (local_slot > 0 && local_slot > __builtin_nontemporal_load(max_rec + 3)) atomicMax(max_rec + 3, local_slot);
   }
+  if (!SLOTS || slots == nullptr) return;
   s_n[threadIdx.x] = nbytes;
   __syncthreads();
-  if (slots == nullptr) return;
   const int64_t tb = (int64_t)blockIdx.x * blockDim.x;
   constexpr int CH = MS_STG / 16;
   for (int it = threadIdx.x; it < 256 * CH; it += 256) {
@@ -709,6 +746,7 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
 constexpr int ED_PAD = 32;
+constexpr int ED_GMAX = 7;   // FMT layout: window chunks per thread (3 threads per mate): up to 21 chunks
 constexpr int ED_WMAX = 5;   // window chunks per thread (4 threads per mate): win_stride <= 320, rlen <= 289   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
 
 struct DMeta {
@@ -721,6 +759,29 @@ struct DMeta {
   int32_t tb[2];     // LDS offset of the record's T (the shared one, or its own with fused corruption)
   int32_t tn[2];     // T length: rlen + 4, or S + 4 with corruption (qualities = len(seq))
 };
+
+// decimal text of v at byte offset o of the dynamic LDS block; returns the offset after it
+__device__ __forceinline__ uint32_t lds_put_u(char *lds, uint32_t o, uint64_t v) {
+  if (v > 0xffffffffull) {
+    auto put = [&](uint8_t c) { lds[o++] = (char)c; };
+    put_big(v);
+    return o;
+  }
+  uint32_t x = (uint32_t)v;
+  const int nd = ndig_u(x);
+  for (int i = nd - 1; i >= 0; i--) {
+    lds[o + i] = (char)('0' + x % 10u);
+    x /= 10u;
+  }
+  return o + nd;
+}
+__device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) {
+  if (v < 0) {
+    lds[o] = '-';
+    return lds_put_u(lds, o + 1, (uint64_t)(-v));
+  }
+  return lds_put_u(lds, o, (uint64_t)v);
+}
 
 // 16 bytes at an arbitrary byte offset of the dynamic LDS block: five aligned dword reads + v_alignbyte.  (Offsets,
 // not pointers: an integer round trip of an LDS pointer turns its reads into flat loads.)
@@ -774,7 +835,9 @@ struct EdArgs {
 // CR: fused BQ corruption (illumina.corrupt_template, illumina.py:139-162): after the gathers, every base of B is
 // corrupted in place and the record's own T ('\n+\n' + qualities + '\n') is built in LDS; the output passes then read
 // the record's T instead of the shared one.  Same Philox counters as k_emit_write, so the bytes are identical.
-template <int NF, int LPR, bool CR>
+// FMT: the qname's reads part is formatted here, from the template's nodes (k_emit_measure measured its length
+// only), instead of gathered from the 256-byte slot k_emit_measure formatted it into (MH_EMIT_SLOTS=1).
+template <int NF, int LPR, bool CR, bool FMT>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
@@ -808,8 +871,12 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     ow = EdOwner{rc.x, rc.y, rc.z, rc.w, o.kept, o.b1, o.b2, A.pos0[tm], A.pos1[tm], A.fo0[tm], 0};
   }
   const int64_t tw = t0 + (jw < nt ? jw : 0);
-  const int4 rc4 = *(const int4 *)(A.recs + tw);              // keep, len1, len2, rest
-  const int64_t pw = sw ? A.pos1[tw] : A.pos0[tw];
+  int4 rc4 = make_int4(0, 0, 0, 0);                           // keep, len1, len2, rest
+  int64_t pw = 0;
+  if (!FMT) {
+    rc4 = *(const int4 *)(A.recs + tw);
+    pw = sw ? A.pos1[tw] : A.pos0[tw];
+  }
   const E3 base = A.off[t0], endo = A.off[t0 + nt];
   const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
   // arena offsets of the tile's first byte per file; the arenas are 256-byte aligned, so offset & 15 is the
@@ -860,36 +927,133 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
 
   // ---- round 2: the gathers, all in flight together (unconditional: an unused chunk re-reads the first one) -----
   const int chunks = win_stride / 16;
-  const bool kept = jw < nt && rc4.x;
-  int64_t aw = pw - h.p_min, ew = pw + A.rlen - h.p_min;
-  if (ew > h.hap_len) ew = h.hap_len;
-  if (aw > h.hap_len) aw = h.hap_len;
-  const int64_t sw_len = ew > aw ? ew - aw : 0;
-  const int64_t a2w = sw ? h.hap_len - aw - sw_len : aw;     // mate 1: the reverse-complement haplotype
-  const int64_t a16 = a2w & ~(int64_t)15;
-  const uint8_t *hsrc = (A.dbg & 1) ? A.slots : (sw ? h.rc : h.hap) + a16;   // dbg 1: no haplotype gathers
-  uint4 wv[ED_WMAX], sv[2];
-  uint32_t use = 0;
+  if constexpr (FMT) {
+    // waves 1-3 gather (three threads per mate window, chunks q3, q3 + 3, ...); wave 0 formats the reads part of
+    // the qnames meanwhile (lane l: template l / 2, mate l % 2)
+    if (tid >= 64) {
+      const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
+      const int jg = pr >> 1, sg = pr & 1;
+      const int64_t tg = t0 + (jg < nt ? jg : 0);
+      const bool kg = jg < nt && A.recs[tg].keep;
+      const int64_t pg = sg ? A.pos1[tg] : A.pos0[tg];
+      int64_t ag = pg - h.p_min, eg = pg + A.rlen - h.p_min;
+      if (eg > h.hap_len) eg = h.hap_len;
+      if (ag > h.hap_len) ag = h.hap_len;
+      const int64_t lg = eg > ag ? eg - ag : 0;
+      const int64_t a2g = sg ? h.hap_len - ag - lg : ag;    // mate 1: the reverse-complement haplotype
+      const int64_t a16 = a2g & ~(int64_t)15;
+      const uint8_t *hsrc = (A.dbg & 1) ? (const uint8_t *)A.pos0 : (sg ? h.rc : h.hap) + a16;   // dbg 1: no gathers
+      uint4 wv[ED_GMAX];
+      uint32_t use = 0;
 #pragma unroll
-  for (int k = 0; k < ED_WMAX; k++) {
-    const int c = qw + 4 * k;
-    const bool u = kept && c < chunks && a16 + 16 * c < a2w + sw_len;
-    use |= (uint32_t)u << k;
-    wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
-  }
+      for (int k = 0; k < ED_GMAX; k++) {
+        const int c = q3 + 3 * k;
+        const bool u = kg && c < chunks && a16 + 16 * c < a2g + lg;
+        use |= (uint32_t)u << k;
+        wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
+      }
+      const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int c = qs + 8 * k;
-    const bool u = kept && 16 * c <= rc4.w;   // the slot holds rest bytes + '\n'
-    use |= (uint32_t)u << (ED_WMAX + k);
-    sv[k] = *(const uint4 *)(A.slots + tw * SLOT + (u ? 16 * c : 0));
+      for (int k = 0; k < ED_GMAX; k++)
+        *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (q3 + 3 * k) : o_dump)) = wv[k];
+    } else if (!(A.dbg & 16)) {
+      // the reads part, in file order (readgenerate.py:223-225): mate s is read fr of the qname (reads[fo] = mate 0,
+      // readgenerate.py:207); read 1 ends at `rest`, where the qname's '\n' goes
+      const int jf = tid >> 1, s = tid & 1;
+      const int64_t tf = t0 + (jf < nt ? jf : 0);
+      const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
+      const int64_t p = s ? A.pos1[tf] : A.pos0[tf];
+      const int fo = A.fo0[tf];
+      if (jf < nt && r0.x) {
+        const int fr = s == 0 ? fo : 1 - fo;
+        const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
+        const int64_t rl = A.rlen;
+        // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
+        const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
+                     q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
+        // node k of the read (selects on the words: an indexed array of nodes would be placed in scratch)
+#define NODE_AT(k)                                                                                       \
+  Node16 n;                                                                                              \
+  {                                                                                                      \
+    const int64_t i_ = (k) - n0;                                                                         \
+    if (i_ > 3) {                                                                                        \
+      const uint64_t *g_ = (const uint64_t *)(h.nd + (k));                                               \
+      n.a = g_[0];                                                                                       \
+      n.b = g_[1];                                                                                       \
+    } else {                                                                                             \
+      n.a = i_ == 0 ? q0.a : i_ == 1 ? q1.a : i_ == 2 ? q2.a : q3.a;                                     \
+      n.b = i_ == 0 ? q0.b : i_ == 1 ? q1.b : i_ == 2 ? q2.b : q3.b;                                     \
+    }                                                                                                    \
   }
+        const Node16 nd0 = q0;
+        ReadInfo ri;
+        ri.n0 = n0;
+        ri.n1 = n1;
+        read_place(h, nd0, p, rl, ri);
+        uint32_t o = (uint32_t)(o_q + jf * qstride + head);
+        if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part (its length, from the measure pass)
+        smem[o] = '|';
+        smem[o + 1] = (char)('0' + s);
+        smem[o + 2] = '|';
+        o = lds_put_s(smem, o + 3, ri.pos);
+        smem[o] = '|';
+        o = lds_put_s(smem, o + 1, rl);
+        smem[o++] = '|';
+        if (ri.special) {
+          smem[o] = '>';
+          o = lds_put_s(smem, o + 1, p - nd0.ps());
+          smem[o] = ':';
+          o = lds_put_s(smem, o + 1, rl);
+          smem[o++] = 'I';
+        } else {
+          for (int64_t k = n0; k <= n1; k++) {
+            NODE_AT(k)
+            o = lds_put_s(smem, o, node_count(n, p, rl));
+            smem[o++] = (char)n.op();
+          }
+        }
+        smem[o++] = '|';
+        bool first = true;
+        for (int64_t k = n0; k <= n1; k++) {
+          NODE_AT(k)
+          if (n.code() == 0) continue;
+          if (!first) smem[o++] = ',';
+          o = lds_put_s(smem, o, node_v(n));
+          first = false;
+        }
+        if (fr == 1) smem[o] = '\n';
+      }
+    }
+  } else {
+    const bool kept = jw < nt && rc4.x;
+    int64_t aw = pw - h.p_min, ew = pw + A.rlen - h.p_min;
+    if (ew > h.hap_len) ew = h.hap_len;
+    if (aw > h.hap_len) aw = h.hap_len;
+    const int64_t sw_len = ew > aw ? ew - aw : 0;
+    const int64_t a2w = sw ? h.hap_len - aw - sw_len : aw;     // mate 1: the reverse-complement haplotype
+    const int64_t a16 = a2w & ~(int64_t)15;
+    const uint8_t *hsrc = (A.dbg & 1) ? (const uint8_t *)A.pos0 : (sw ? h.rc : h.hap) + a16;   // dbg 1: no gathers
+    uint4 wv[ED_WMAX], sv[2];
+    uint32_t use = 0;
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int c = qs + 8 * k;
-    *(uint4 *)(smem + (((use >> (ED_WMAX + k)) & 1) ? o_q + jw * qstride + head + 16 * c : o_dump)) = sv[k];
-  }
-  {
+    for (int k = 0; k < ED_WMAX; k++) {
+      const int c = qw + 4 * k;
+      const bool u = kept && c < chunks && a16 + 16 * c < a2w + sw_len;
+      use |= (uint32_t)u << k;
+      wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int c = qs + 8 * k;
+      const bool u = kept && 16 * c <= rc4.w;   // the slot holds rest bytes + '\n'
+      use |= (uint32_t)u << (ED_WMAX + k);
+      sv[k] = *(const uint4 *)(A.slots + tw * SLOT + (u ? 16 * c : 0));
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int c = qs + 8 * k;
+      *(uint4 *)(smem + (((use >> (ED_WMAX + k)) & 1) ? o_q + jw * qstride + head + 16 * c : o_dump)) = sv[k];
+    }
     const int32_t slot = o_win + (jw * 2 + sw) * win_stride;
 #pragma unroll
     for (int k = 0; k < ED_WMAX; k++)
@@ -1110,6 +1274,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   HapView hv = view_of(h);
   // the direct writer (fused corruption too, unless MH_CORRUPT_LDS asks for the LDS-image writer: experiments)
   const bool direct = !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS"));
+  // the direct writer formats the qname's reads part itself (measure records lengths only); MH_EMIT_SLOTS=1: the
+  // round-1 layout, measure formats it into 256-byte slots the writer gathers (A/B experiments)
+  static const bool use_slots = getenv("MH_EMIT_SLOTS") && atoi(getenv("MH_EMIT_SLOTS"));
 
   // ---- measure + record offsets (skipped when mh_emit_prepare already ran them for this unit) ----------------------
   EmitPrep &pp = tp.prep;
@@ -1165,11 +1332,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     Rec *recs = (Rec *)es.recs.p;
     E3 *off = (E3 *)es.off.p;
     int32_t *overflow = (int32_t *)(stat + 40);
-    if (direct) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
+    if (direct && use_slots) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
     stage_begin(ctx, "emit_measure");
-    hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
+    hipLaunchKernelGGL(direct && use_slots ? k_emit_measure<true> : k_emit_measure<false>,
+                       dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
                        rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                       direct ? (uint8_t *)es.slots.p : nullptr, overflow,
+                       direct && use_slots ? (uint8_t *)es.slots.p : nullptr, overflow,
                        getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -1244,7 +1412,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_end(ctx);
     return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
   }
-  const int32_t hover = direct ? hm4[2] : 0;   // a reads part overflowed its slot (read back with the maxima)
+  const int32_t hover = direct && use_slots ? hm4[2] : 0;   // a reads part overflowed its slot (slot layout)
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
@@ -1252,6 +1420,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   const int32_t edbg = dbg_env ? atoi(dbg_env) : 0;
   const bool staged = !(edbg & 128);              // seam chunks staged in LDS (dbg 128: stored directly, experiment)
   const int32_t qstride = head + ((edbg & 256) ? SLOT : (hslot > 16 ? (hslot + 15) / 16 * 16 : 16)) + 32;
+  // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
   const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
                        (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
                        (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16 +
@@ -1274,11 +1443,11 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
     EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
              qstride, edbg, cc};
-    const int lpr = A.dbg & 32 ? 16 : (A.dbg & 64 ? 8 : 4);   // lanes per output record (experiments)
-    auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true> : k_emit_direct<1, 8, true>)
-             : write_fastq2 ? (lpr == 16 ? k_emit_direct<2, 16, false>
-                                         : lpr == 8 ? k_emit_direct<2, 8, false> : k_emit_direct<2, 4, false>)
-                            : (lpr == 16 ? k_emit_direct<1, 16, false> : k_emit_direct<1, 8, false>);
+    auto kfn = use_slots
+                   ? (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, false> : k_emit_direct<1, 8, true, false>)
+                                      : (write_fastq2 ? k_emit_direct<2, 4, false, false> : k_emit_direct<1, 8, false, false>))
+                   : (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, true> : k_emit_direct<1, 8, true, true>)
+                                      : (write_fastq2 ? k_emit_direct<2, 4, false, true> : k_emit_direct<1, 8, false, true>));
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);

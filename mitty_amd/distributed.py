@@ -5,9 +5,11 @@ illumina.py:56-58), so the path shards without any data-path collective:
 
 * every rank builds the reference's unit list (A6) itself, so seeds and `ps` do not depend on the GPU count;
 * with at least 2 units per GPU the units are dealt out whole by LPT on region length;
-* with fewer (chr1 = 4 units on 8 GPUs) every rank samples every unit and emits only its slice
-  [m*r/W, m*(r+1)/W) of the unit's templates; the cnt of the slice's first kept template comes from one
-  all-reduce of the per-slice N-filter survivor counts (the only coupling between templates, an exclusive prefix);
+* with fewer (chr1 = 4 units on 8 GPUs) every rank emits only its slice [m*r/W, m*(r+1)/W) of every unit's
+  templates.  Each unit is sampled once, on rank u mod W, and its template arrays (17 B per template) are broadcast
+  to the other ranks (RCCL over xGMI on device buffers; gloo on host arrays for the CPU tests); the cnt of a slice's
+  first kept template comes from one all-reduce of the per-slice N-filter survivor counts (the only coupling between
+  templates, an exclusive prefix);
 * one more all-reduce of per-piece byte sizes gives every piece its file offset, and each rank pwrites its pieces
   there, so the files are byte-identical to the single-GPU run (= reference --threads 1) at any GPU count.
 
@@ -17,6 +19,8 @@ The collectives carry a few int64 per piece; no sequence data crosses xGMI.  Out
 import logging
 import os
 import time
+
+import numpy as np
 
 from mitty_amd.lib import fasta as mfasta
 from mitty_amd.lib import vcfio
@@ -95,12 +99,49 @@ class DeviceBackend:
   def load_region(self, ri, region, seq):
     self.eng.load_region(ri, region, seq)
 
-  def sample(self, units, soa_of, p, rlen, cum_tlen, rng):
-    """units: [(ps, ri, cpy, seed)] -> template counts; unit k's set becomes template id k."""
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None):
+    """units: [(ps, ri, cpy, seed)]; the units k in `which` (all by default) are sampled into template id k.  Every
+    unit's haplotype is built (its slices are emitted here).  Returns template counts (None where not sampled)."""
     from mitty_amd.engine import RNG_MODES
     self._slots = [self.eng.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-    return [int(x) for x in self.eng.ctx.sample_units(list(range(len(units))), self._slots, [u[3] for u in units],
-                                                      p, rlen, cum_tlen, RNG_MODES[rng])]
+    which = list(range(len(units))) if which is None else list(which)
+    out = [None] * len(units)
+    if which:
+      ns = self.eng.ctx.sample_units(which, [self._slots[k] for k in which], [units[k][3] for k in which], p, rlen,
+                                     cum_tlen, RNG_MODES[rng])
+      for k, n in zip(which, ns):
+        out[k] = int(n)
+    return out
+
+  def share(self, k, n, src, rlen, group=None):
+    """Template set k (n templates) from rank src to every rank: an RCCL broadcast of the device arrays under
+    'nccl' (pos0 | pos1 | fo0 packed in one buffer, device-to-device copies on either side), host arrays under gloo."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    ctx = self.eng.ctx
+    if dist.get_backend(group) == 'nccl':
+      buf = torch.empty(max(17 * n, 16), dtype=torch.uint8, device='cuda')
+      b = buf.data_ptr()
+      if rank == src:
+        ctx.templates_export(k, b + 16 * n, b, b + 8 * n, n)
+      dist.broadcast(buf, src, group=group)
+      torch.cuda.current_stream().synchronize()
+      if rank != src:
+        ctx.templates_import(k, n, rlen, b + 16 * n, b, b + 8 * n, on_device=True)
+      return
+    buf = torch.empty(max(17 * n, 16), dtype=torch.uint8)
+    if rank == src:
+      fo0, p0, p1 = ctx.templates_export(k)
+      a = buf.numpy()
+      a[:8 * n] = p0.view(np.uint8)
+      a[8 * n:16 * n] = p1.view(np.uint8)
+      a[16 * n:17 * n] = fo0.view(np.uint8)
+    dist.broadcast(buf, src, group=group)
+    if rank != src:
+      a = buf.numpy()
+      ctx.templates_import(k, n, rlen, a[16 * n:17 * n].view(np.int8), a[:8 * n].view(np.int64),
+                           a[8 * n:16 * n].view(np.int64))
 
   def count_kept(self, k, t0, t1):
     self.eng.ctx.use_templates(k)
@@ -171,8 +212,18 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
   stats = {'units': len(units), 'pieces': len(mine), 'templates': 0, 'kept': 0}
   soa_of = lambda r, c: vdf[r]['copies'][c]
   for batch in batches:
-    ns = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
-                        read_model['cum_tlen'], rng)
+    if sliced and world > 1:
+      # each unit sampled once, on rank u mod W; its template count all-reduced, its arrays broadcast
+      owner = [u % world for u in batch]
+      got = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
+                           read_model['cum_tlen'], rng, which=[k for k, o in enumerate(owner) if o == rank])
+      ns = allreduce_i64([got[k] if o == rank else 0 for k, o in enumerate(owner)], group)
+      for k, o in enumerate(owner):
+        backend.share(k, ns[k], o, read_model['rlen'], group)
+      stats['sampled'] = stats.get('sampled', 0) + sum(1 for o in owner if o == rank)
+    else:
+      ns = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
+                          read_model['cum_tlen'], rng)
     k_of = {u: k for k, u in enumerate(batch)}
     bases = {}
     if sliced:

@@ -16,13 +16,25 @@ class OracleBackend:
   def load_region(self, ri, region, seq):
     self.regions[ri] = (region, seq)
 
-  def sample(self, units, soa_of, p, rlen, cum_tlen, rng):
-    self.recs = []
-    for ps, ri, cpy, seed in units:
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None):
+    self.recs = [None] * len(units)
+    self.sampled = []
+    for k, (ps, ri, cpy, seed) in enumerate(units):
+      if which is not None and k not in which:
+        continue
       (chrom, s0, _), seq = self.regions[ri]
       _, b1, b2 = O.generate_unit_soa(seq, s0, soa_of(ri, cpy), p, rlen, cum_tlen, seed, 'X:0:0', chrom, cpy)
-      self.recs.append((_records(b1), _records(b2)))
-    return [len(r[0]) for r in self.recs]
+      self.recs[k] = (_records(b1), _records(b2))
+      self.sampled.append(k)
+    return [None if r is None else len(r[0]) for r in self.recs]
+
+  def share(self, k, n, src, rlen, group=None):
+    """The unit's records (the stand-in's 'templates') from rank src, as DeviceBackend.share sends arrays."""
+    import torch.distributed as dist
+    obj = [self.recs[k] if dist.get_rank(group) == src else None]
+    dist.broadcast_object_list(obj, src, group=group)
+    assert obj[0] is not None and len(obj[0][0]) == n
+    self.recs[k] = obj[0]
 
   def count_kept(self, k, t0, t1):
     return t1 - t0

@@ -43,6 +43,11 @@ def _rank(rank, world, port, layout, model_name, outdir):
                                       c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
                                       seed=c['seed'], backend=OracleBackend(), layout=layout)
     assert st['world'] == world
+    if layout == 'slice':   # every unit sampled exactly once over the ranks, then broadcast
+      import torch
+      t = torch.tensor([st.get('sampled', 0)], dtype=torch.int64)
+      dist.all_reduce(t)
+      assert int(t.item()) == st['units'], (int(t.item()), st['units'])
   finally:
     dist.destroy_process_group()
 
