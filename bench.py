@@ -1,26 +1,32 @@
 #!/usr/bin/env python3
-"""Benchmark: paired 2x150 bp templates/s for `generate-reads` on chr1 (249 Mbp) diploid at 30x, MI355X.
+"""Benchmark: paired 2x150 bp templates/s for `generate-reads` at 30x on MI355X.
 
-Workload (BASELINE.json configs[1], per GPU): a synthetic chr1-shaped contig (249,250,621 bp, N caps + centromere
-gap) with ~1.3 variants/kbp (SNV/INS/DEL, long insertions, deliberate overlaps), phased diploid, read model
-hiseq-X-v2.5-Garvan (the built-in 2x150 model; SURVEY.md Finding 3), coverage 30, seed 7, perfect reads.
-One step = the whole job for that chromosome: splice both haplotypes on the GPU, then the reference's 4 work units
-(2 copies x 2 passes) — MT19937-exact template sampling + read emission — with the FASTQ output left in HBM.
-Inputs (contig bytes) are resident before timing; variant arrays are re-uploaded inside the step (13 MB).
+N = 1 (BASELINE.json configs[1]): a synthetic chr1-shaped contig (249,250,621 bp, N caps + centromere gap) with
+~1.3 variants/kbp (SNV/INS/DEL, long insertions, deliberate overlaps), phased diploid, read model
+hiseq-X-v2.5-Garvan (the built-in 2x150 model; SURVEY.md Finding 3), coverage 30, seed 7, perfect reads.  One step =
+the whole job for that chromosome: splice both haplotypes on the GPU, then the reference's 4 work units (2 copies x
+2 passes) — MT19937-exact template sampling + read emission — with the FASTQ output left in HBM.  Inputs (contig
+bytes and both copies' variant arrays) are resident before timing.
 
-Multi-GPU (torchrun, one process per GPU): every rank simulates its own chr1-shaped chromosome (weak scaling, no
-data-path collective); an RCCL all-reduce of the per-rank template counts closes each step.
+N > 1 (configs[3], torchrun, one process per GPU): the whole synthetic GRCh37 (24 contigs + MT, one BED interval per
+contig, ~100 work units) under mitty_amd.distributed's plan — work units dealt to ranks by LPT on region length,
+every unit sampled and emitted by its owner, no data-path collective — output in HBM; an RCCL all-reduce of the
+per-rank template and byte counts closes each step (the counts the file writer turns into offsets).  Total work is
+fixed as N grows (strong scaling).
 
 Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_direct; k_emit_write with
---emit-mode 1 or --corrupt): algorithmic bytes per launch =
-sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ bytes written (both files), divided by the
-launch's HIP-event duration; `stage_ms` gives every stage per step so the dominant kernel is visible.
+--emit-mode 1): algorithmic bytes per launch = sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ
+bytes written (both files), divided by the launch's HIP-event duration on the writer's stream; `stage_ms` gives
+every stage per step.  At N = 1 the line also carries `cpu_baseline` (the CPU oracle on the host cores) and
+`end_to_end` (FASTA + VCF files parsed on the host, GPU job, FASTQ copied to page-locked memory and written to
+/dev/null: the whole `generate-reads` command).
 """
 import argparse
 import glob
 import json
 import os
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -28,6 +34,7 @@ sys.path.insert(0, REPO)
 
 CHR1 = 249_250_621
 PEAK_HBM_GBS = 8000.0
+METRIC = 'paired 2x150bp reads/sec at 30x WGS, 1/2/4/8 MI355X; qname POS/CIGAR bit-exact'
 
 
 def parse():
@@ -42,11 +49,68 @@ def parse():
   ap.add_argument('--rng', default='mitty', choices=['mitty', 'philox'])
   ap.add_argument('--corrupt', action='store_true', help='fused BQ corruption (BASELINE configs[2])')
   ap.add_argument('--cpu-baseline-mbp', type=float, default=100.0,
-                  help='bounded CPU-oracle sample: one unit on the first N Mbp of the contig (0 = skip)')
+                  help='bounded CPU-oracle sample: the job\'s units on the first N Mbp of the contig (0 = skip)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
+  ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end (files in, /dev/null out) leg')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
   ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
+  ap.add_argument('--genome-scale', type=float, default=1.0,
+                  help='N > 1: contig lengths scaled by this (rehearsals of the plan on one GPU; 1 = GRCh37)')
   return ap.parse_args()
+
+
+def roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=True):
+  agg = {}
+  for name, ms in stages:
+    agg.setdefault(name, [0.0, 0])
+    agg[name][0] += ms
+    agg[name][1] += 1
+  ew_ms, ew_n = agg.get('emit_write', [0.0, 0])
+  alg_bytes = 2 * rlen * kept + b1 + b2                       # this rank's algorithmic bytes over the timed steps
+  achieved = alg_bytes / (ew_ms * 1e-3) / 1e9 if ew_ms > 0 else None
+  traffic = None   # measured in separate rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE), see profiles/pmc_*.json
+  pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_{}_*.json'.format(kernel))))
+  traffic_src = None
+  if pmc and pmc_config:
+    try:
+      with open(pmc[-1]) as fp:
+        d = json.load(fp)
+      if d.get('rlen') == rlen and d.get('length') == CHR1:
+        traffic = d.get('hbm_bytes_per_launch')
+        traffic_src = os.path.relpath(pmc[-1], REPO)
+    except Exception:
+      traffic = None
+  stage_ms = {k: round(v[0] / steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])}
+  return {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+          'frac': (achieved / PEAK_HBM_GBS) if achieved else None, 'traffic': traffic,
+          'traffic_source': ('PMC passes of the same config, ' + traffic_src) if traffic_src else None,
+          'algorithmic_bytes_per_launch': alg_bytes / max(ew_n, 1),
+          'avg_launch_ms': ew_ms / max(ew_n, 1)}, stage_ms
+
+
+def timed(step, steps, warmup, eng, dist):
+  def barrier():
+    if dist is not None:
+      dist.barrier()
+
+  for _ in range(warmup):
+    step()
+  eng.ctx.enable_timing(True)
+  barrier()
+  eng.ctx.sync()
+  t0 = time.perf_counter()
+  kept = b1 = b2 = 0
+  for _ in range(steps):
+    k, x1, x2 = step()
+    kept += k
+    b1 += x1
+    b2 += x2
+  eng.ctx.sync()
+  barrier()
+  dt = time.perf_counter() - t0
+  stages = eng.ctx.stage_times()
+  eng.ctx.enable_timing(False)
+  return dt, kept, b1, b2, stages
 
 
 def main():
@@ -58,10 +122,18 @@ def main():
   if world > 1:
     import torch
     import torch.distributed as tdist
+    local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks on one GPU
     torch.cuda.set_device(local)
-    tdist.init_process_group('nccl')
+    # MH_DIST_BACKEND=gloo: rehearsal of the multi-rank plan with several ranks on one GPU (RCCL needs one per GPU)
+    tdist.init_process_group(os.environ.get('MH_DIST_BACKEND', 'nccl'))
     dist = tdist
+    run_genome(a, rank, world, local, dist)
+    dist.destroy_process_group()
+    return
+  run_chr1(a)
 
+
+def run_chr1(a):
   import numpy as np
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
@@ -70,14 +142,12 @@ def main():
   _, model = get_read_model(a.model + '.pkl')
   rlen = int(model['mean_rlen'])
   p, passes = _native.read_model_params(rlen, a.coverage)
-  t_in = time.time()
-  seq = synth.contig(a.length, 1000 + rank)
-  recs = synth.variants(seq, 2000 + rank)
+  seq = synth.contig(a.length, 1000)
+  recs = synth.variants(seq, 2000)
   copies = synth.copies_soa(recs)
-  units = _native.work_units(a.seed + rank, [2], passes)
-  t_in = time.time() - t_in
+  units = _native.work_units(a.seed, [2], passes)
 
-  eng = Engine(local)
+  eng = Engine(0)
   if a.corrupt:
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), a.seed)
   eng.load_region(0, ('1', 0, a.length), seq)
@@ -95,97 +165,172 @@ def main():
                         model['cum_tlen'], 'SYN', 0, True, a.rng)
     return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
 
-  def barrier():
-    if dist is not None:
-      dist.barrier()
+  dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
+  eng.close()
+  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps)
+  if a.stages:
+    print(json.dumps(stage_ms), file=sys.stderr)
 
-  for _ in range(a.warmup):
-    step()
-  eng.ctx.enable_timing(True)
-  barrier()
-  eng.ctx.sync()
-  t0 = time.perf_counter()
-  kept = b1 = b2 = 0
-  for _ in range(a.steps):
-    k, x1, x2 = step()
-    kept += k
-    b1 += x1
-    b2 += x2
-  eng.ctx.sync()
-  barrier()
-  dt = time.perf_counter() - t0
-  stages = eng.ctx.stage_times()
-  eng.ctx.enable_timing(False)
-
-  if dist is not None:
-    import torch
-    t = torch.tensor([dt], dtype=torch.float64, device='cuda')
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    c = torch.tensor([kept, b1, b2], dtype=torch.int64, device='cuda')
-    dist.all_reduce(c)    # RCCL reduce of read counts over xGMI
-    kept_all, b1_all, b2_all = (int(x) for x in c.tolist())
-  else:
-    kept_all, b1_all, b2_all = kept, b1, b2
-
-  # per-stage totals (this rank) and the emission roofline
-  agg = {}
-  for name, ms in stages:
-    agg.setdefault(name, [0.0, 0])
-    agg[name][0] += ms
-    agg[name][1] += 1
-  ew_ms, ew_n = agg.get('emit_write', [0.0, 0])
-  alg_bytes = 2 * rlen * kept + b1 + b2                       # this rank's algorithmic bytes over the timed steps
-  achieved = alg_bytes / (ew_ms * 1e-3) / 1e9 if ew_ms > 0 else None
-  traffic = None
-  pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_{}_*.json'.format(kernel))))
-  if pmc:
-    try:
-      with open(pmc[-1]) as fp:
-        d = json.load(fp)
-      if d.get('rlen') == rlen and d.get('length') == a.length:
-        traffic = d.get('hbm_bytes_per_launch')
-    except Exception:
-      traffic = None
-
+  e2e = None
+  if not a.no_e2e and not a.corrupt and a.rng == 'mitty':
+    e2e = end_to_end(a, seq, recs, model, kept // a.steps)
   cpu = None
-  if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_baseline_mbp > 0:
+  if not a.no_cpu_baseline and a.cpu_baseline_mbp > 0:
     cpu = cpu_baseline(a, seq, recs, p, rlen, model, units)
 
+  ms_per_step = dt / a.steps * 1e3
+  out = {
+    'metric': METRIC,
+    'value': kept / dt,
+    'unit': 'templates/s',
+    'n_gpus': 1,
+    'steps': a.steps,
+    'warmup': a.warmup,
+    'ms_per_step': ms_per_step,
+    'higher_is_better': True,
+    'scaling': 'weak',
+    'vs_baseline': None,
+    'dtype': 'int64+u8',
+    'data': 'synthetic chr1-shaped contig + ~1.3/kbp phased diploid variants (mitty_amd.synth), seed-fixed',
+    'config': {'workload': 'generate-reads chr1 (249,250,621 bp) diploid, {} 2x{} PE, {}x, rng={}{} '
+                           '(BASELINE configs[{}])'.format(a.model, rlen, a.coverage, a.rng,
+                                                           ', +BQ corruption' if a.corrupt else '',
+                                                           2 if a.corrupt else 1),
+               'read_model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units': len(units),
+               'templates_per_step': kept // a.steps, 'parallelism': 'single GPU'},
+    'roofline': roof,
+    'cpu_baseline': cpu,
+    'end_to_end': e2e,
+    'stage_ms': stage_ms,
+    'fastq_bytes_per_template': (b1 + b2) / max(kept, 1),
+    'host_cpus': os.cpu_count(),
+  }
+  print(json.dumps(out), flush=True)
+
+
+def end_to_end(a, seq, recs, model, kept_per_job):
+  """The whole generate-reads command on chr1: FASTA and VCF parsed by the host readers, the GPU job, FASTQ pulled to
+  page-locked memory and written to /dev/null (readgenerate.process_multi_threaded).  Input files are written first
+  (untimed) to a temp directory."""
+  from mitty_amd import synth
+  from mitty_amd.lib import fasta as mfasta
+  from mitty_amd.lib import vcfio
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  d = tempfile.mkdtemp(prefix='mh_e2e_', dir='/tmp')
+  try:
+    fa, vcf, bed = os.path.join(d, 'chr1.fa'), os.path.join(d, 'chr1.vcf'), os.path.join(d, 'chr1.bed')
+    synth.write_fasta(fa, [('1', seq)])
+    synth.write_vcf(vcf, [('1', seq)], {'1': recs}, sample='SYN')
+    with open(bed, 'w') as fp:
+      fp.write('1\t0\t{}\n'.format(len(seq)))
+    mod, mdl = get_read_model(a.model + '.pkl')
+    t0 = time.perf_counter()
+    mfasta.read_fasta(fa)
+    t1 = time.perf_counter()
+    vcfio.load_variants_soa(vcf, 'SYN', bed)
+    t2 = time.perf_counter()
+    st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
+                                             seed=a.seed)
+    t3 = time.perf_counter()
+    return {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
+            'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
+            'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
+                    'page-locked memory, written to /dev/null; seconds = the whole command'}
+  finally:
+    for f in glob.glob(os.path.join(d, '*')):
+      os.remove(f)
+    os.rmdir(d)
+
+
+def run_genome(a, rank, world, local, dist):
+  """configs[3]: whole synthetic GRCh37 over `world` GPUs, the distributed plan's LPT unit deal, output in HBM."""
+  import torch
+  from mitty_amd import _native, synth
+  from mitty_amd import distributed as D
+  from mitty_amd.engine import Engine
+  from mitty_amd.readmodel import get_read_model
+
+  _, model = get_read_model(a.model + '.pkl')
+  rlen = int(model['mean_rlen'])
+  p, passes = _native.read_model_params(rlen, a.coverage)
+  contigs = [(n, max(20000, int(L * a.genome_scale))) for n, L in synth.GRCH37]
+  units = _native.work_units(a.seed, [2] * len(contigs), passes)     # (region, copy, seed), reference order
+  weights = [contigs[ri][1] for ri, _, _ in units]
+  pieces = D.plan_pieces(weights, world)                              # ~100 units >= 2 per rank: LPT, whole units
+  mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == rank]
+  regions = sorted({ri for _, ri, _, _ in mine})
+
+  eng = Engine(local)
+  copies = {}
+  for ri in regions:
+    name, length = contigs[ri]
+    seq = synth.contig(length, 1000 + ri)
+    copies[ri] = synth.copies_soa(synth.variants(seq, 2000 + ri))
+    eng.load_region(ri, (name, 0, length), seq)
+    for cpy in (0, 1):
+      eng.upload_variants(ri, cpy, copies[ri][cpy])
+    del seq
+  eng.ctx.set_emit_mode(a.emit_mode)
+  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_direct'
+  dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+  counts = torch.zeros(3, dtype=torch.int64, device=dev)
+
+  def step():
+    eng.drop_haplotypes()
+    eng.ctx.reset_output()
+    kept = b1 = b2 = 0
+    batch, draws = [], 0
+    for k, u in enumerate(mine):   # batches of ~200 M draws, as process_multi_threaded samples them
+      batch.append(u)
+      draws += int(contigs[u[1]][1] * p * 1.2)
+      if draws >= 200_000_000 or k == len(mine) - 1:
+        for _, kp, x1, x2 in eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0,
+                                           True, a.rng):
+          kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
+        batch, draws = [], 0
+    counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
+    dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)
+    return kept, b1, b2
+
+  steps, warmup = a.steps, a.warmup
+  dt, kept, b1, b2, stages = timed(step, steps, warmup, eng, dist)
+  eng.close()
+  t = torch.tensor([dt], dtype=torch.float64, device=dev)
+  dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  dt = float(t.item())
+  c = torch.tensor([kept, b1, b2, len(mine)], dtype=torch.int64, device=dev)
+  dist.all_reduce(c)
+  kept_all, b1_all, b2_all, n_units = (int(x) for x in c.tolist())
+  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=False)
   if rank == 0:
-    ms_per_step = dt / a.steps * 1e3
-    stage_ms = {k: round(v[0] / a.steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])}
     out = {
-      'metric': 'paired 2x150bp reads/sec at 30x WGS, 1/2/4/8 MI355X; qname POS/CIGAR bit-exact',
-      'value': kept_all / a.steps / (dt / a.steps),
+      'metric': METRIC,
+      'value': kept_all / dt,
       'unit': 'templates/s',
       'n_gpus': world,
-      'steps': a.steps,
-      'warmup': a.warmup,
-      'ms_per_step': ms_per_step,
+      'steps': steps,
+      'warmup': warmup,
+      'ms_per_step': dt / steps * 1e3,
       'higher_is_better': True,
-      'scaling': 'weak',
+      'scaling': 'strong',
       'vs_baseline': None,
       'dtype': 'int64+u8',
-      'data': 'synthetic chr1-shaped contig + ~1.3/kbp phased diploid variants (mitty_amd.synth), seed-fixed',
-      'config': {'workload': 'generate-reads chr1 (249,250,621 bp) diploid, {} 2x{} PE, {}x, rng={}{}, '
-                             'one chr1-sized chromosome per GPU'.format(a.model, rlen, a.coverage, a.rng,
-                                                                         ', +BQ corruption' if a.corrupt else ''),
-                 'read_model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units_per_gpu': len(units),
-                 'templates_per_step': kept_all // a.steps, 'parallelism': 'unit-shard x{}'.format(world)},
-      'roofline': {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS,
-                   'unit': 'GB/s', 'frac': (achieved / PEAK_HBM_GBS) if achieved else None,
-                   'traffic': traffic,
-                   'algorithmic_bytes_per_launch': alg_bytes / max(ew_n, 1),
-                   'avg_launch_ms': ew_ms / max(ew_n, 1)},
-      'cpu_baseline': cpu,
+      'data': 'synthetic GRCh37-shaped genome (24 contigs + MT) + ~1.3/kbp phased diploid variants (mitty_amd.synth)',
+      'config': {'workload': 'generate-reads whole GRCh37{} diploid, {} 2x{} PE, {}x, rng={}, one BED interval per '
+                             'contig, units dealt by LPT over {} GPUs (BASELINE configs[3])'.format(
+                               '' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
+                               a.model, rlen, a.coverage, a.rng, world),
+                 'genome_bp': sum(L for _, L in contigs),
+                 'read_model': a.model, 'coverage': a.coverage, 'units': n_units,
+                 'templates_per_step': kept_all // steps, 'parallelism': 'unit-shard (LPT) x{}'.format(world)},
+      'roofline': roof,
+      'roofline_rank': 0,
+      'cpu_baseline': None,
       'stage_ms': stage_ms,
       'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
     }
     print(json.dumps(out), flush=True)
-  eng.close()
-  if dist is not None:
-    dist.destroy_process_group()
 
 
 def _cpu_unit(args):
@@ -214,9 +359,12 @@ def cpu_baseline(a, seq, recs, p, rlen, model, units):
     res = pool.map(_cpu_unit, jobs)
   n = sum(r[0] for r in res)
   dt = max(r[2] for r in res) - min(r[1] for r in res)
+  per_core = [r[0] / (r[2] - r[1]) for r in res]
   return {'value': n / dt, 'unit': 'templates/s', 'cores': len(jobs), 'kind': 'port',
-          'sample': '{} work units (2 copies x {} passes, one worker process each) on chr1[0:{:.0f} Mbp), {} templates '
-                    'in {:.2f} s'.format(len(jobs), len(jobs) // 2, a.cpu_baseline_mbp, n, dt)}
+          'per_core': sum(per_core) / len(per_core), 'host_cpus': os.cpu_count(),
+          'sample': '{} work units (2 copies x {} passes, one worker process each, {} host CPUs) on chr1[0:{:.0f} Mbp), '
+                    '{} templates in {:.2f} s'.format(len(jobs), len(jobs) // 2, os.cpu_count(), a.cpu_baseline_mbp,
+                                                     n, dt)}
 
 
 if __name__ == '__main__':

@@ -150,6 +150,9 @@ int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t offset1, char *fq1, int64_t len1, int64_t offset2, char *fq2,
                         int64_t len2);
 int32_t mh_output_reset(mh_ctx *ctx);
+/* Page-locked host memory for mh_output_fetch destinations (D2H at full link rate; the FASTQ sink writes from it). */
+int32_t mh_host_alloc(int64_t bytes, void **out);
+int32_t mh_host_free(void *p);
 
 /* rpc.generate_read for a batch of (p, l) on haplotype `slot`: positions, start/end nodes and the text fields.
  * Text outputs are concatenated; *_off arrays (n+1 entries) index them.  MH_E_CAPACITY if a text buffer is short
@@ -206,6 +209,17 @@ int32_t mh_vcf_copy(mh_vcf *v, int32_t cpy, int64_t *pos, uint8_t *op, int64_t *
 int32_t mh_vcf_filter(const char *in_path, const char *sample, int32_t n_regions, const char *chroms,
                       const int64_t *start0, const int64_t *end, const char *out_path, int32_t bgzf, int32_t threads,
                       int64_t *n_written, int64_t *n_filtered, char *err, int32_t err_cap);
+
+/* ---- FASTA reader (pysam.FastaFile for the generate-reads front end, readgenerate.py:181,186) -------------------
+ * Host-only: plain or gzip/bgzip FASTA; contig name = the header's first word; bytes as stored.  names: contigs to
+ * keep, NUL-separated and ended by an empty name (NULL = all).  mh_fasta_contig's pointers stay valid until
+ * mh_fasta_close. */
+typedef struct mh_fasta mh_fasta;
+int32_t mh_fasta_open(const char *path, const char *names, mh_fasta **out);
+const char *mh_fasta_error(const mh_fasta *f);
+int32_t mh_fasta_count(const mh_fasta *f, int32_t *n);
+int32_t mh_fasta_contig(const mh_fasta *f, int32_t i, const char **name, const char **seq, int64_t *len);
+int32_t mh_fasta_close(mh_fasta *f);
 
 /* ---- compressed FASTQ sink: host-side BGZF (gzip-compatible members of <= 65280 input
  * bytes, deflated on `threads` threads).  MH_E_CAPACITY if `cap` is short (*used = bytes needed).  mh_bgzf_eof

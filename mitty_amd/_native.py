@@ -18,12 +18,13 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
-           'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter']
+           'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
+           'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
 
 
 class NativeError(RuntimeError):
@@ -97,9 +98,16 @@ def lib():
   _sig(L, 'mh_vcf_copy', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
   _sig(L, 'mh_vcf_filter', [ctypes.c_char_p, ctypes.c_char_p, c_i32, c_vp, c_vp, c_vp, ctypes.c_char_p, c_i32, c_i32,
                             P_i64, P_i64, ctypes.c_char_p, c_i32])
+  _sig(L, 'mh_fasta_open', [ctypes.c_char_p, c_vp, ctypes.POINTER(c_vp)])
+  _sig(L, 'mh_fasta_error', [c_vp], ctypes.c_char_p)
+  _sig(L, 'mh_fasta_count', [c_vp, ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_fasta_contig', [c_vp, c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_vp), P_i64])
+  _sig(L, 'mh_fasta_close', [c_vp])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
   _sig(L, 'mh_output_reset', [c_vp])
+  _sig(L, 'mh_host_alloc', [c_i64, ctypes.POINTER(c_vp)])
+  _sig(L, 'mh_host_free', [c_vp])
   _sig(L, 'mh_read_batch', [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64])
   _sig(L, 'mh_set_corruption', [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_u64])
@@ -206,6 +214,62 @@ def vcf_filter(path_in, sample, regions, path_out, bgzf=False, threads=8):
   if rc:
     _raise(rc, err.value.decode())
   return w.value, f.value
+
+
+class PinnedBuffer:
+  """Page-locked host staging (mh_host_alloc), grown on demand."""
+
+  def __init__(self):
+    self.ptr, self.cap = None, 0
+
+  def reserve(self, n):
+    if n > self.cap:
+      self.free()
+      p = c_vp()
+      rc = lib().mh_host_alloc(int(n), ctypes.byref(p))
+      if rc:
+        _raise(rc, 'mh_host_alloc failed')
+      self.ptr, self.cap = p.value, int(n)
+
+  def view(self, n):
+    if n == 0:
+      return memoryview(b'')
+    return memoryview((ctypes.c_uint8 * n).from_address(self.ptr)).cast('B')
+
+  def free(self):
+    if self.ptr:
+      lib().mh_host_free(c_vp(self.ptr))
+    self.ptr, self.cap = None, 0
+
+  def __del__(self):
+    try:
+      self.free()
+    except Exception:
+      pass
+
+
+def read_fasta(path, names=None):
+  """Host FASTA reader (mh_fasta.cpp): {contig name: bytes}, only `names` when given."""
+  L = lib()
+  h = c_vp()
+  sel = None
+  if names is not None:
+    sel = ctypes.create_string_buffer(b''.join(n.encode() + b'\0' for n in names) + b'\0')
+  rc = L.mh_fasta_open(path.encode(), ctypes.cast(sel, c_vp) if sel is not None else None, ctypes.byref(h))
+  try:
+    if rc:
+      _raise(rc, L.mh_fasta_error(h).decode() if h else 'mh_fasta_open failed')
+    n = c_i32()
+    L.mh_fasta_count(h, ctypes.byref(n))
+    out = {}
+    for i in range(n.value):
+      nm, sq, ln = ctypes.c_char_p(), c_vp(), c_i64()
+      L.mh_fasta_contig(h, i, ctypes.byref(nm), ctypes.byref(sq), ctypes.byref(ln))
+      out[nm.value.decode()] = bytes((ctypes.c_char * ln.value).from_address(sq.value)) if ln.value else b''
+    return out
+  finally:
+    if h:
+      L.mh_fasta_close(h)
 
 
 def bgzf_eof():
@@ -441,6 +505,32 @@ class Context:
     b2 = np.empty(max(len2, 1), np.uint8)
     self._chk(self._L.mh_output_fetch(self._h, off1, _ptr(b1), len1, off2, _ptr(b2) if len2 > 0 else None, len2))
     return b1[:len1].tobytes(), b2[:len2].tobytes()
+
+  def stream_output(self, sinks, pin, chunk=256 << 20):
+    """Both arenas to the sinks (file-like objects; None skips a file) through one page-locked staging buffer,
+    `chunk` bytes per copy."""
+    u = self.output_size()
+    pin.reserve(min(chunk, max(u)) if max(u) else 1)
+    for f in (0, 1):
+      if sinks[f] is None:
+        continue
+      for off in range(0, u[f], chunk):
+        n = min(chunk, u[f] - off)
+        if f == 0:
+          self._chk(self._L.mh_output_fetch(self._h, off, c_vp(pin.ptr), n, 0, None, 0))
+        else:
+          self._chk(self._L.mh_output_fetch(self._h, 0, None, 0, off, c_vp(pin.ptr), n))
+        sinks[f].write(pin.view(n))
+
+  def fetch_output_pinned(self, pins):
+    """The whole arenas into page-locked staging (pins: [PinnedBuffer, PinnedBuffer], grown as needed); returns
+    memoryviews of the bytes (valid until the next fetch)."""
+    u1, u2 = self.output_size()
+    pins[0].reserve(u1)
+    pins[1].reserve(u2)
+    self._chk(self._L.mh_output_fetch(self._h, 0, c_vp(pins[0].ptr), u1, 0, c_vp(pins[1].ptr) if u2 > 0 else None,
+                                      u2))
+    return pins[0].view(u1), pins[1].view(u2)
 
   def reset_output(self):
     self._chk(self._L.mh_output_reset(self._h))

@@ -139,6 +139,19 @@ using namespace mh;
     MH_TRY(join_writer(ctx));                                              \
   } while (0)
 
+namespace mh {
+CorruptCfg corrupt_cfg(const mh_ctx *ctx, uint64_t unit_key, int64_t t_base) {
+  CorruptCfg cc{1, (const double *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
+                ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
+                (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u, t_base};
+  const char *base = (const char *)ctx->corrupt_cum.p;
+  cc.guide = (const uint16_t *)(base + ctx->corrupt_guide_off);
+  cc.F = (const uint32_t *)(base + ctx->corrupt_F_off);
+  cc.Fp = (const uint32_t *)(base + ctx->corrupt_Fp_off);
+  return cc;
+}
+}  // namespace mh
+
 extern "C" {
 
 int32_t mh_version(void) { return 1; }
@@ -668,24 +681,40 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   if (!cum_bq || !phred_p || max_bp <= 0 || n_bq <= 0 || n_bq > 4096)
     return arg_fail(ctx, MH_E_ARG, "bad corruption model");
   if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
+  if (max_bp > 16384) return arg_fail(ctx, MH_E_ARG, "BQ model longer than 16384 positions");
   const size_t nt = (size_t)2 * max_bp * n_bq;
-  // (a NaN entry compares like numpy's searchsorted treats it, as larger than any draw, in both searches)
-  // search guide per row: g[k] = entries < k / CG_BUCKETS (a lower bound for any draw in bucket k, g[k + 1] an upper
-  // one), so the device search covers [g[k], g[k + 1]] instead of the whole row
+  // u32 tables of the Philox mode: F = min(floor(x * 2^32), 2^32 - 1) (exact: x * 2^32 is exact in f64); a NaN entry
+  // counts as larger than any draw, as numpy's searchsorted orders it
+  auto fix32 = [](double x) -> uint32_t {
+    if (!(x > 0.0)) return x != x ? 0xffffffffu : 0u;
+    const double y = std::floor(x * 4294967296.0);
+    return y >= 4294967295.0 ? 0xffffffffu : (uint32_t)y;
+  };
+  std::vector<uint32_t> F(nt), Fp(100);
+  for (size_t i = 0; i < nt; i++) F[i] = fix32(cum_bq[i]);
+  for (int i = 0; i < 100; i++) Fp[i] = fix32(phred_p[i]);
+  // search guide per row: g[k] = entries with F < k * 2^24, i.e. below k / CG_BUCKETS (a lower bound for any draw in
+  // bucket k, g[k + 1] an upper one), so both searches (u32 and f64) cover [g[k], g[k + 1]] instead of the whole row
   std::vector<uint16_t> guide((size_t)2 * max_bp * (mh::CG_BUCKETS + 1));
   for (size_t r = 0; r < (size_t)2 * max_bp; r++) {
-    const double *row = cum_bq + r * n_bq;
+    const uint32_t *row = F.data() + r * n_bq;
     for (int k = 0; k <= mh::CG_BUCKETS; k++) {
-      const double thr = (double)k / (double)mh::CG_BUCKETS;   // exact (a power-of-two fraction)
-      guide[r * (mh::CG_BUCKETS + 1) + k] = (uint16_t)(std::lower_bound(row, row + n_bq, thr) - row);
+      int64_t c = 0;
+      while (c < n_bq && (uint64_t)row[c] < ((uint64_t)k << 24)) c++;
+      guide[r * (mh::CG_BUCKETS + 1) + k] = (uint16_t)c;
     }
   }
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, 8 * nt + 2 * guide.size() + 64));
-  MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
-  HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_cum.p, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
   ctx->corrupt_guide_off = ((8 * nt + 15) / 16) * 16;
-  HIPCHK(ctx, hipMemcpyAsync((char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off, guide.data(), 2 * guide.size(),
-                             hipMemcpyHostToDevice, ctx->stream));
+  ctx->corrupt_F_off = ((ctx->corrupt_guide_off + 2 * guide.size() + 15) / 16) * 16;
+  ctx->corrupt_Fp_off = ((ctx->corrupt_F_off + 4 * nt + 15) / 16) * 16;
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_Fp_off + 4 * 100 + 64));
+  MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
+  char *base = (char *)ctx->corrupt_cum.p;
+  HIPCHK(ctx, hipMemcpyAsync(base, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_guide_off, guide.data(), 2 * guide.size(), hipMemcpyHostToDevice,
+                             ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_F_off, F.data(), 4 * nt, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp_off, Fp.data(), 4 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;
@@ -740,6 +769,18 @@ int32_t mh_get_corruption_stream(mh_ctx *ctx, uint32_t *key624, int32_t *pos, in
   }
   if (key624) std::copy(h.key, h.key + 624, key624);
   if (pos) *pos = h.pos;
+  return MH_OK;
+}
+
+int32_t mh_host_alloc(int64_t bytes, void **out) {
+  if (!out || bytes < 0) return MH_E_ARG;
+  *out = nullptr;
+  if (hipHostMalloc(out, (size_t)(bytes > 0 ? bytes : 1), hipHostMallocDefault) != hipSuccess) return MH_E_OOM;
+  return MH_OK;
+}
+
+int32_t mh_host_free(void *p) {
+  if (p && hipHostFree(p) != hipSuccess) return MH_E_HIP;
   return MH_OK;
 }
 

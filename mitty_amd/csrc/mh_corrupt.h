@@ -1,12 +1,16 @@
 // mh_corrupt.h — the empirical-BQ corruption of one base (illumina.corrupt_single_read, illumina.py:140-162),
 // shared by the fused emission (mh_emit.hip) and standalone corrupt-reads (mh_corrupt.hip).
 //
-// Arithmetic is the reference's in both RNG modes: U1, U2 are 53-bit doubles built like numpy's rand()
-// ((a >> 5) * 2^26 + (b >> 6)) / 2^53 from two 32-bit words, bq = min(searchsorted(cum_bq[mate, n, :], U1,
-// side='left'), 93) over the f64 table, substitution when U2 < phred_p[bq] (f64).  Only the word source differs:
-//   Philox mode  words from Philox4x32-10 keyed by (seed, unit), counter (template, file, base): one draw per base;
-//                the replacement base from a second counter, umulhi(word, 3)
-//   exact mode   the reference's own MT19937 stream (mh_corrupt.hip: rand(n), rand(n), randint(0, 3, n) per mate)
+// Arithmetic: U1, U2 are 53-bit uniforms and the decisions are the reference's f64 ones, bq =
+// min(searchsorted(cum_bq[mate, n, :], U1, side='left'), 93) and substitution when U2 < phred_p[bq].  Word sources:
+//   exact mode   the reference's own MT19937 stream (mh_corrupt.hip: rand(n), rand(n), randint(0, 3, n) per mate),
+//                U = numpy's ((a >> 5) * 2^26 + (b >> 6)) / 2^53, compared in f64
+//   Philox mode  Philox4x32-10 keyed by (seed, unit), one draw per base pair, counter (template, file, pair): each
+//                base gets the high 32 bits h of U1 and of U2 (U = (h * 2^21 + l) / 2^53).  The decisions are taken
+//                on h against u32 tables F = floor(threshold * 2^32): F < h decides "below", F > h "not below";
+//                only F == h needs the low 21 bits, which then come from a second draw (flag 0x4000) and the f64
+//                comparison runs — the same outcome as comparing the full 53-bit U in f64, at 32-bit cost.
+//                The replacement base comes from a third counter (flag 0x8000), umulhi(word, 3).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -25,6 +29,8 @@ struct CorruptCfg {
   uint32_t k0, k1, c3;   // Philox key and the constant counter word
   int64_t t_base;        // index of the launch's first template inside its unit (slices: mh_emit_reads_range)
   const uint16_t *guide = nullptr;   // [2][max_bp][CG_BUCKETS + 1]: entries of the row below k / CG_BUCKETS
+  const uint32_t *F = nullptr;       // [2][max_bp][n_bq]: min(floor(cum * 2^32), 2^32 - 1)
+  const uint32_t *Fp = nullptr;      // [100]: min(floor(phred_p * 2^32), 2^32 - 1)
 };
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
@@ -71,24 +77,62 @@ __device__ __forceinline__ uint8_t rot_base(uint8_t x, uint32_t c) {
   return (uint8_t)rot[c];
 }
 
-// Philox mode: bases n0 and n0 + 1 (cnt = 1 or 2 of them) of file f of template t.  Base n draws counter
-// (t, f, n): words x, y make U1, words z, w make U2; a substituted base draws its replacement from a second counter
-// (bit 15 of the position word set).
+// Philox mode, one base: h1 / h2 the high words of U1 / U2; returns bq and sets *sub.  `ex` supplies the low words
+// (second draw) when h lands exactly on a table value.
+template <typename Ex>
+__device__ __forceinline__ uint32_t corrupt_base32(const CorruptCfg &cc, int f, int n, uint32_t h1, uint32_t h2,
+                                                   bool *sub, Ex ex) {
+  const int64_t ri = (int64_t)f * cc.max_bp + n;
+  const uint32_t *F = cc.F + ri * cc.n_bq;
+  const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (h1 >> 24);
+  int lo = g[0];
+  const int hb = g[1];
+  int hi = hb;
+  while (lo < hi) {   // first entry with F >= h1 (entries below k * 2^24 are below every h1 of bucket k)
+    const int mid = (lo + hi) >> 1;
+    if (F[mid] < h1) lo = mid + 1; else hi = mid;
+  }
+  uint32_t bq;
+  if (lo < hb && F[lo] == h1) {   // a threshold inside [h1, h1 + 1) / 2^32: the full 53 bits decide
+    const uint2 l = ex();
+    bq = bq_search(cc.cum, cc.guide, cc.max_bp, cc.n_bq, f, n,
+                   ((double)h1 * 2097152.0 + (double)(l.x >> 11)) * (1.0 / 9007199254740992.0));
+    *sub = ((double)h2 * 2097152.0 + (double)(l.y >> 11)) * (1.0 / 9007199254740992.0) < cc.phred[bq];
+    return bq;
+  }
+  bq = lo < 93 ? lo : 93;
+  const uint32_t fp = cc.Fp[bq];
+  if (h2 == fp) {
+    const uint2 l = ex();
+    *sub = ((double)h2 * 2097152.0 + (double)(l.y >> 11)) * (1.0 / 9007199254740992.0) < cc.phred[bq];
+  } else {
+    *sub = h2 < fp;
+  }
+  return bq;
+}
+
+// Philox mode: bases n0 and n0 + 1 (n0 even; cnt = 1 or 2 of them) of file f of template t (corruption in place,
+// qualities to q).  Draw (t, f, n0 / 2): words x, y are base n0's h1, h2; z, w base n0 + 1's.
 __device__ __forceinline__ void corrupt_pair(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
                                              uint8_t *q) {
   t += cc.t_base;
   const uint2 key = make_uint2(cc.k0, cc.k1);
+  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 1);
+  const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
+  bool sub[2] = {false, false};
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     if (i >= cnt) break;
-    const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)(n0 + i);
-    const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
-    const uint32_t bq = bq_search(cc.cum, cc.guide, cc.max_bp, cc.n_bq, f, n0 + i, mt_double(r.x, r.y));
+    const uint32_t bq = corrupt_base32(cc, f, n0 + i, i ? r.z : r.x, i ? r.w : r.y, &sub[i], [&]() {
+      const uint4 l = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x4000u, cc.c3), key);
+      return i ? make_uint2(l.z, l.w) : make_uint2(l.x, l.y);
+    });
     q[i] = (uint8_t)(bq + 33);
-    if (mt_double(r.z, r.w) < cc.phred[bq]) {   // rare: the replacement base (randint(0, 3))
-      const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
-      b[i] = rot_base(b[i], __umulhi(c.x, 3u));
-    }
+  }
+  if (sub[0] || sub[1]) {   // rare: the replacement bases (randint(0, 3))
+    const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
+    if (sub[0]) b[0] = rot_base(b[0], __umulhi(c.x, 3u));
+    if (sub[1]) b[1] = rot_base(b[1], __umulhi(c.y, 3u));
   }
 }
 

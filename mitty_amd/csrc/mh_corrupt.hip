@@ -314,10 +314,7 @@ int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_
   MH_TRY(ensure_keep(ctx, ctx->out1, ctx->used1 + tot.a + 64, ctx->used1));
   if (d1) MH_TRY(ensure_keep(ctx, ctx->out2, ctx->used2 + tot.b + 64, ctx->used2));
   const uint64_t key = 0x636f7272757074ull;   // fixed unit key of the standalone tool
-  CorruptCfg cc{1, (const double *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
-                ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)key,
-                (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(key >> 32) ^ 0x636f7272u, t_base};
-  cc.guide = (const uint16_t *)((const char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off);
+  const CorruptCfg cc = corrupt_cfg(ctx, key, t_base);
   CxArgs xa{nullptr, nullptr, 0, cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq};
   char *o0 = (char *)ctx->out1.p + ctx->used1, *o1 = d1 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const unsigned grid = grid_for(T * nf * 64, 256, INT32_MAX);

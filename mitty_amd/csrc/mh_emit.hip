@@ -1062,30 +1062,88 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   __syncthreads();
   if (A.dbg & 2) return;
   if constexpr (CR) {   // corrupt B in place, write the record's T
+    // one item per base pair (corrupt_pair's draw) or per record's separators; four items per thread and step,
+    // each phase for all four before the next, so their table loads are in flight together
     const int32_t rl = A.rlen;
-    const int rp = (rl + 1) / 2 + 1;   // base pairs per record, then the separators
-    for (int idx = tid; idx < nt * NF * rp; idx += ED_THREADS) {
-      const int rr = idx / rp, k = idx - rr * rp;
-      const int j = rr / NF, f = rr - j * NF;
-      const DMeta &M = meta[j];
-      if (M.len[f] == 0) continue;
-      const int32_t S = M.S[f];
-      char *T = smem + M.tb[f];
-      if (k == rp - 1) {   // the separators
-        T[0] = '\n'; T[1] = '+'; T[2] = '\n'; T[3 + S] = '\n';
-        continue;
+    const int rp = (rl + 1) / 2 + 1;
+    const int total = nt * NF * rp;
+    const CorruptCfg &cc = A.cc;
+    const uint2 key = make_uint2(cc.k0, cc.k1);
+    for (int i0 = tid; i0 < total; i0 += 4 * ED_THREADS) {
+      int32_t bo[4], to[4], nn[4], ff[4], cnt[4];   // LDS offsets of the pair's bases and the record's T; n0; file
+      int64_t tt[4];
+      int kind[4];                                   // 0: nothing, 1: a base pair, 2: the separators
+      uint4 r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int idx = i0 + u * ED_THREADS;
+        kind[u] = 0;
+        bo[u] = to[u] = nn[u] = ff[u] = cnt[u] = 0;
+        tt[u] = 0;
+        r[u] = make_uint4(0, 0, 0, 0);
+        if (idx >= total) continue;
+        const int rr = idx / rp, k = idx - rr * rp;
+        const int j = rr / NF, f = rr - j * NF;
+        const DMeta &M = meta[j];
+        if (M.len[f] == 0) continue;
+        const int32_t S = M.S[f];
+        to[u] = M.tb[f];
+        if (k == rp - 1) {
+          kind[u] = 2;
+          nn[u] = S;
+          continue;
+        }
+        const int n = 2 * k;
+        if (n >= S) continue;
+        kind[u] = 1;
+        bo[u] = M.bb[f] + n;
+        nn[u] = n;
+        ff[u] = f;
+        cnt[u] = S - n > 1 ? 2 : 1;
+        tt[u] = t0 + j + cc.t_base;
+        if (A.dbg & 1024)   // timing experiment: no Philox
+          r[u] = make_uint4((uint32_t)tt[u] * 2654435761u, (uint32_t)n * 40503u, (uint32_t)tt[u] ^ n, 77u);
+        else
+          r[u] = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32),
+                                          ((uint32_t)f << 16) | ((uint32_t)n >> 1), cc.c3), key);
       }
-      const int n = 2 * k;
-      if (n >= S) continue;
-      const int cnt = S - n > 1 ? 2 : 1;
-      char *B = smem + M.bb[f] + n;
-      uint8_t b[2] = {(uint8_t)B[0], cnt > 1 ? (uint8_t)B[1] : (uint8_t)0}, qq[2];
-      corrupt_pair(A.cc, t0 + j, f, n, cnt, b, qq);
-      B[0] = (char)b[0];
-      T[3 + n] = (char)qq[0];
-      if (cnt > 1) {
-        B[1] = (char)b[1];
-        T[4 + n] = (char)qq[1];
+      uint32_t bq[4][2];
+      bool sub[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          bq[u][i] = 0;
+          sub[u][i] = false;
+          if (kind[u] != 1 || i >= cnt[u]) continue;
+          if (A.dbg & 512) {   // timing experiment: no table lookups
+            bq[u][i] = (i ? r[u].z : r[u].x) % 41u;
+            continue;
+          }
+          bq[u][i] = corrupt_base32(cc, ff[u], nn[u] + i, i ? r[u].z : r[u].x, i ? r[u].w : r[u].y, &sub[u][i], [&]() {
+            const uint32_t cw = ((uint32_t)ff[u] << 16) | ((uint32_t)nn[u] >> 1) | 0x4000u;
+            const uint4 l = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32), cw, cc.c3), key);
+            return i ? make_uint2(l.z, l.w) : make_uint2(l.x, l.y);
+          });
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (kind[u] == 0) continue;
+        char *T = smem + to[u];
+        if (kind[u] == 2) {   // the separators
+          const int32_t S = nn[u];
+          T[0] = '\n'; T[1] = '+'; T[2] = '\n'; T[3 + S] = '\n';
+          continue;
+        }
+        T[3 + nn[u]] = (char)(bq[u][0] + 33);
+        if (cnt[u] > 1) T[4 + nn[u]] = (char)(bq[u][1] + 33);
+        if (sub[u][0] || sub[u][1]) {   // rare: the replacement bases (randint(0, 3))
+          const uint32_t cw = ((uint32_t)ff[u] << 16) | ((uint32_t)nn[u] >> 1) | 0x8000u;
+          const uint4 c = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32), cw, cc.c3), key);
+          if (sub[u][0]) smem[bo[u]] = (char)rot_base((uint8_t)smem[bo[u]], __umulhi(c.x, 3u));
+          if (sub[u][1]) smem[bo[u] + 1] = (char)rot_base((uint8_t)smem[bo[u] + 1], __umulhi(c.y, 3u));
+        }
       }
     }
     __syncthreads();
@@ -1403,10 +1461,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       stage_end(ctx);
       return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
     }
-    cc = CorruptCfg{1, (const double *)ctx->corrupt_cum.p, (const double *)ctx->corrupt_phred.p, ctx->corrupt_max_bp,
-                    ctx->corrupt_n_bq, (uint32_t)ctx->corrupt_seed, (uint32_t)unit_key,
-                    (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u, t_begin};
-    cc.guide = (const uint16_t *)((const char *)ctx->corrupt_cum.p + ctx->corrupt_guide_off);
+    cc = corrupt_cfg(ctx, unit_key, t_begin);
   }
   if (lds > 160 * 1024) {
     stage_end(ctx);

@@ -182,7 +182,8 @@ struct mh_ctx {
   bool corrupt_on = false;
   mh::DevBuf corrupt_cum, corrupt_phred;
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
-  size_t corrupt_guide_off = 0;   // byte offset of the search guide inside corrupt_cum
+  size_t corrupt_guide_off = 0;   // byte offsets inside corrupt_cum: the search guide, the u32 tables F and Fp
+  size_t corrupt_F_off = 0, corrupt_Fp_off = 0;
   uint64_t corrupt_seed = 0;
   // exact corruption stream of mh_corrupt_fastq (mh_corrupt_stream_seed / _state): 0 = Philox; 1 = the stream of
   // RandomState(cx_seed) from output cx_pos on; 2 = continuing the explicit state (cx_key, cx_kpos)
@@ -287,6 +288,10 @@ int32_t mt_stream_words(mh_ctx *ctx, hipStream_t st, uint32_t seed, int64_t firs
                         DevBuf &jobs_buf, int64_t *lead);
 int32_t mt_state_words(mh_ctx *ctx, hipStream_t st, const uint32_t *key624, int32_t pos, int64_t count, DevBuf &out,
                        DevBuf &key_buf);
+
+// The corruption configuration of a launch (mh_set_corruption's tables; Philox key from the unit).
+struct CorruptCfg;
+CorruptCfg corrupt_cfg(const mh_ctx *ctx, uint64_t unit_key, int64_t t_base);
 
 // Host-side MT19937 (numpy RandomState seeding), used for seed derivation and the rare exact fix-ups.
 struct HostMT {

@@ -3,7 +3,14 @@ import gzip
 
 
 def read_fasta(fname, names=None):
-  """{contig name (first word of the header): bytes}.  If `names` is given, other contigs are skipped."""
+  """{contig name (first word of the header): bytes}.  If `names` is given, other contigs are skipped.  Parsed by the
+  host C++ reader (mh_fasta.cpp)."""
+  from mitty_amd import _native
+  return _native.read_fasta(fname, names)
+
+
+def read_fasta_py(fname, names=None):
+  """The same in Python (kept for the host-reader test)."""
   with open(fname, 'rb') as fp:
     gz = fp.read(2) == b'\x1f\x8b'
   seqs, name, chunks, keep = {}, None, [], True

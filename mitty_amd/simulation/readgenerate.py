@@ -91,6 +91,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   fp1 = FastqSink(fastq1_fname)   # '.gz' names get BGZF output
   fp2 = FastqSink(fastq2_fname) if write2 else None
 
+  pins = [_native.PinnedBuffer()]   # page-locked D2H staging for the sinks
+
   def flush(ps, n, kept, b1, b2):
     stats['templates'] += n
     stats['kept'] += kept
@@ -98,10 +100,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     stats['bytes2'] += b2
     u1, u2 = eng.ctx.output_size()
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
-      d1, d2 = eng.ctx.fetch_output()
-      fp1.write(d1)
-      if write2:
-        fp2.write(d2)
+      eng.ctx.stream_output([fp1, fp2 if write2 else None], pins[0])
       eng.ctx.reset_output()
 
   try:
@@ -123,6 +122,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     if fp2:
       fp2.close()
     eng.close()
+    for b in pins:
+      b.free()
   stats['seconds'] = time.time() - t0
   return stats
 

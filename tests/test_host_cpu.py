@@ -333,3 +333,50 @@ def test_filter_variants_errors(tmp_path):
     vcfio.prepare_variant_file(str(bad), 'S1', str(bed), str(tmp_path / 'o.vcf'))
   with pytest.raises(ValueError, match='sample'):
     vcfio.prepare_variant_file(str(bad), 'NOPE', str(bed), str(tmp_path / 'o.vcf'))
+
+
+def test_native_fasta_reader(tmp_path):
+  """mh_fasta.cpp (pysam.FastaFile's role, readgenerate.py:181,186) = the plain Python parse: plain and gzip input,
+  CRLF line ends, header descriptions, empty contigs, lowercase / IUPAC bytes, a names filter."""
+  import gzip
+  from mitty_amd.lib import fasta
+  txt = (b'>c1 some description\r\nACGTN\r\nacgtRYK\r\n>empty\n>c3\tx\n' + b'ACGT' * 5000 + b'\n' + b'GGN' * 33 +
+         b'\n>last\nTTTT')
+  plain, gz = tmp_path / 'a.fa', tmp_path / 'a.fa.gz'
+  plain.write_bytes(txt)
+  gz.write_bytes(gzip.compress(txt))
+  for f in (str(plain), str(gz), G.path('data/syn.fa'), G.path('data/tiny.fasta')):
+    assert fasta.read_fasta(f) == fasta.read_fasta_py(f), f
+  assert fasta.read_fasta(str(plain))['c1'] == b'ACGTNacgtRYK'
+  assert fasta.read_fasta(str(plain))['empty'] == b''
+  assert set(fasta.read_fasta(str(gz), names={'c3', 'nope'})) == {'c3'}
+  with pytest.raises(ValueError):
+    fasta.read_fasta(str(tmp_path / 'missing.fa'))
+
+
+def test_philox_u32_decision_rule_equals_f64():
+  """The Philox-mode corruption decides on the high 32 bits h of a 53-bit uniform U = (h * 2^21 + l) / 2^53 against
+  F = min(floor(x * 2^32), 2^32 - 1) (mh_corrupt.h corrupt_base32): F < h -> x < U, F > h -> not, F == h -> the f64
+  comparison with the low bits.  The rule must equal searchsorted(row, U, 'left') and U < phred in f64 for every
+  U, including h landing exactly on a table value."""
+  rs = np.random.RandomState(3)
+  for m in G.MODELS:
+    cum = G.model(m)['cum_bq_mat']
+    phred = 10 ** (-np.arange(100) / 10)
+    F = np.minimum(np.floor(np.clip(cum, 0, None) * 2.0 ** 32), 2 ** 32 - 1).astype(np.uint64)
+    Fp = np.minimum(np.floor(phred * 2.0 ** 32), 2 ** 32 - 1).astype(np.uint64)
+    for _ in range(200):
+      f, n = rs.randint(2), rs.randint(int(G.model(m)['max_rlen']))
+      row, Frow = cum[f, n], F[f, n]
+      hs = np.concatenate([rs.randint(0, 2 ** 32, 64, dtype=np.uint64), Frow[rs.randint(0, len(Frow), 16)]])
+      for h in hs:
+        for l in (0, 1, rs.randint(0, 2 ** 21), 2 ** 21 - 1):
+          U = (float(h) * 2.0 ** 21 + l) / 2.0 ** 53
+          want = min(int(np.searchsorted(row, U, side='left')), 93)
+          lo = int(np.searchsorted(Frow, h, side='left'))
+          got = min(int(np.searchsorted(row, U, side='left')), 93) if lo < len(Frow) and Frow[lo] == h else min(lo, 93)
+          assert got == want, (m, f, n, h, l)
+          U2 = U
+          sub_want = U2 < phred[want]
+          sub_got = (U2 < phred[want]) if h == Fp[want] else bool(h < Fp[want])
+          assert sub_got == sub_want
