@@ -146,8 +146,9 @@ CorruptCfg corrupt_cfg(const mh_ctx *ctx, uint64_t unit_key, int64_t t_base) {
                 (uint32_t)(ctx->corrupt_seed >> 32) ^ (uint32_t)(unit_key >> 32) ^ 0x636f7272u, t_base};
   const char *base = (const char *)ctx->corrupt_cum.p;
   cc.guide = (const uint16_t *)(base + ctx->corrupt_guide_off);
-  cc.F = (const uint32_t *)(base + ctx->corrupt_F_off);
-  cc.Fp = (const uint32_t *)(base + ctx->corrupt_Fp_off);
+  cc.bk = (const uint8_t *)(base + ctx->corrupt_bk_off);
+  cc.T16 = (const uint16_t *)(base + ctx->corrupt_T16_off);
+  cc.Fp16 = (const uint16_t *)(base + ctx->corrupt_Fp16_off);
   return cc;
 }
 }  // namespace mh
@@ -683,38 +684,49 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   if (seed > 0xffffffffull) return arg_fail(ctx, MH_E_SEED, "Seed value out of range 0 - 4294967295");
   if (max_bp > 16384) return arg_fail(ctx, MH_E_ARG, "BQ model longer than 16384 positions");
   const size_t nt = (size_t)2 * max_bp * n_bq;
-  // u32 tables of the Philox mode: F = min(floor(x * 2^32), 2^32 - 1) (exact: x * 2^32 is exact in f64); a NaN entry
+  // u16 tables of the Philox mode: T = min(floor(x * 2^16), 65535) (exact: x * 2^16 is exact in f64); a NaN entry
   // counts as larger than any draw, as numpy's searchsorted orders it
-  auto fix32 = [](double x) -> uint32_t {
-    if (!(x > 0.0)) return x != x ? 0xffffffffu : 0u;
-    const double y = std::floor(x * 4294967296.0);
-    return y >= 4294967295.0 ? 0xffffffffu : (uint32_t)y;
+  auto fix16 = [](double x) -> uint16_t {
+    if (!(x > 0.0)) return x != x ? 0xffff : 0;
+    const double y = std::floor(x * 65536.0);
+    return y >= 65535.0 ? 0xffff : (uint16_t)y;
   };
-  std::vector<uint32_t> F(nt), Fp(100);
-  for (size_t i = 0; i < nt; i++) F[i] = fix32(cum_bq[i]);
-  for (int i = 0; i < 100; i++) Fp[i] = fix32(phred_p[i]);
-  // search guide per row: g[k] = entries with F < k * 2^24, i.e. below k / CG_BUCKETS (a lower bound for any draw in
-  // bucket k, g[k + 1] an upper one), so both searches (u32 and f64) cover [g[k], g[k + 1]] instead of the whole row
+  std::vector<uint16_t> T16(nt), Fp16(100);
+  for (size_t i = 0; i < nt; i++) T16[i] = fix16(cum_bq[i]);
+  for (int i = 0; i < 100; i++) Fp16[i] = fix16(phred_p[i]);
+  // per row: the f64 search guide g[k] = entries below k / CG_BUCKETS (a lower bound for any draw in bucket k,
+  // g[k + 1] an upper one), and the Philox-mode bucket table bk[k] = min(g[k], 93) | 0x80 when an entry lies in
+  // [k, k + 1) / 256 and g[k] < 93 (CB_ROW = CG_BUCKETS buckets of the 16-bit draw)
+  static_assert(mh::CB_ROW == mh::CG_BUCKETS, "bucket table and guide share their buckets");
   std::vector<uint16_t> guide((size_t)2 * max_bp * (mh::CG_BUCKETS + 1));
+  std::vector<uint8_t> bk((size_t)2 * max_bp * mh::CB_ROW);
   for (size_t r = 0; r < (size_t)2 * max_bp; r++) {
-    const uint32_t *row = F.data() + r * n_bq;
+    const uint16_t *row = T16.data() + r * n_bq;
+    uint16_t *g = guide.data() + r * (mh::CG_BUCKETS + 1);
+    int64_t c = 0;
     for (int k = 0; k <= mh::CG_BUCKETS; k++) {
-      int64_t c = 0;
-      while (c < n_bq && (uint64_t)row[c] < ((uint64_t)k << 24)) c++;
-      guide[r * (mh::CG_BUCKETS + 1) + k] = (uint16_t)c;
+      while (c < n_bq && (uint32_t)row[c] < ((uint32_t)k << 8)) c++;
+      g[k] = (uint16_t)c;
+    }
+    for (int k = 0; k < mh::CB_ROW; k++) {
+      const int lo = g[k];
+      bk[r * mh::CB_ROW + k] = (uint8_t)((lo < 93 ? lo : 93) | (lo < 93 && g[k + 1] > lo ? 0x80 : 0));
     }
   }
-  ctx->corrupt_guide_off = ((8 * nt + 15) / 16) * 16;
-  ctx->corrupt_F_off = ((ctx->corrupt_guide_off + 2 * guide.size() + 15) / 16) * 16;
-  ctx->corrupt_Fp_off = ((ctx->corrupt_F_off + 4 * nt + 15) / 16) * 16;
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_Fp_off + 4 * 100 + 64));
+  auto al16 = [](size_t x) { return ((x + 15) / 16) * 16; };
+  ctx->corrupt_guide_off = al16(8 * nt);
+  ctx->corrupt_bk_off = al16(ctx->corrupt_guide_off + 2 * guide.size());
+  ctx->corrupt_T16_off = al16(ctx->corrupt_bk_off + bk.size());
+  ctx->corrupt_Fp16_off = al16(ctx->corrupt_T16_off + 2 * nt);
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_Fp16_off + 2 * 100 + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
   char *base = (char *)ctx->corrupt_cum.p;
   HIPCHK(ctx, hipMemcpyAsync(base, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_guide_off, guide.data(), 2 * guide.size(), hipMemcpyHostToDevice,
                              ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_F_off, F.data(), 4 * nt, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp_off, Fp.data(), 4 * 100, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_bk_off, bk.data(), bk.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_T16_off, T16.data(), 2 * nt, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp16_off, Fp16.data(), 2 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;

@@ -5,12 +5,15 @@
 // min(searchsorted(cum_bq[mate, n, :], U1, side='left'), 93) and substitution when U2 < phred_p[bq].  Word sources:
 //   exact mode   the reference's own MT19937 stream (mh_corrupt.hip: rand(n), rand(n), randint(0, 3, n) per mate),
 //                U = numpy's ((a >> 5) * 2^26 + (b >> 6)) / 2^53, compared in f64
-//   Philox mode  Philox4x32-10 keyed by (seed, unit), one draw per base pair, counter (template, file, pair): each
-//                base gets the high 32 bits h of U1 and of U2 (U = (h * 2^21 + l) / 2^53).  The decisions are taken
-//                on h against u32 tables F = floor(threshold * 2^32): F < h decides "below", F > h "not below";
-//                only F == h needs the low 21 bits, which then come from a second draw (flag 0x4000) and the f64
-//                comparison runs — the same outcome as comparing the full 53-bit U in f64, at 32-bit cost.
-//                The replacement base comes from a third counter (flag 0x8000), umulhi(word, 3).
+//   Philox mode  Philox4x32-10 keyed by (seed, unit), one draw per four bases, counter (template, file, quad):
+//                base i of the quad takes word i, h1 = its high 16 bits (the top of U1), h2 = its low 16 bits (the
+//                top of U2), U = (h * 2^37 + l) / 2^53.  Decisions are taken on h against u16 tables T = floor(x * 2^16)
+//                (clamped to 65535): T < h decides "below", T > h "not below"; only T == h needs the low 37 bits,
+//                which then come from a per-base draw (flag 0x4000) and the f64 comparison runs — the outcome of
+//                comparing the full 53-bit U in f64.  The BQ search is one byte per draw: bk[row][h1 >> 8] holds the
+//                entries below the bucket (capped at 93) and a flag when a threshold falls inside it (then the
+//                row's T entries from there are walked).  The replacement bases come from a per-quad counter with
+//                flag 0x8000, umulhi(word i, 3).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -20,6 +23,7 @@
 namespace mh {
 
 constexpr int CG_BUCKETS = 256;   // search-guide buckets per BQ row: bucket k = draws in [k / 256, (k + 1) / 256)
+constexpr int CB_ROW = 256;       // Philox mode: bucket-table bytes per BQ row (h1 >> 8)
 
 struct CorruptCfg {
   int32_t enable;
@@ -29,8 +33,9 @@ struct CorruptCfg {
   uint32_t k0, k1, c3;   // Philox key and the constant counter word
   int64_t t_base;        // index of the launch's first template inside its unit (slices: mh_emit_reads_range)
   const uint16_t *guide = nullptr;   // [2][max_bp][CG_BUCKETS + 1]: entries of the row below k / CG_BUCKETS
-  const uint32_t *F = nullptr;       // [2][max_bp][n_bq]: min(floor(cum * 2^32), 2^32 - 1)
-  const uint32_t *Fp = nullptr;      // [100]: min(floor(phred_p * 2^32), 2^32 - 1)
+  const uint8_t *bk = nullptr;       // [2][max_bp][CB_ROW]: min(entries below k / 256, 93) | 0x80 (one inside)
+  const uint16_t *T16 = nullptr;     // [2][max_bp][n_bq]: min(floor(cum * 2^16), 65535)
+  const uint16_t *Fp16 = nullptr;    // [100]: min(floor(phred_p * 2^16), 65535)
 };
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
@@ -77,63 +82,112 @@ __device__ __forceinline__ uint8_t rot_base(uint8_t x, uint32_t c) {
   return (uint8_t)rot[c];
 }
 
-// Philox mode, one base: h1 / h2 the high words of U1 / U2; returns bq and sets *sub.  `ex` supplies the low words
-// (second draw) when h lands exactly on a table value.
-template <typename Ex>
-__device__ __forceinline__ uint32_t corrupt_base32(const CorruptCfg &cc, int f, int n, uint32_t h1, uint32_t h2,
-                                                   bool *sub, Ex ex) {
-  const int64_t ri = (int64_t)f * cc.max_bp + n;
-  const uint32_t *F = cc.F + ri * cc.n_bq;
-  const uint16_t *g = cc.guide + ri * (CG_BUCKETS + 1) + (h1 >> 24);
-  int lo = g[0];
-  const int hb = g[1];
-  int hi = hb;
-  while (lo < hi) {   // first entry with F >= h1 (entries below k * 2^24 are below every h1 of bucket k)
-    const int mid = (lo + hi) >> 1;
-    if (F[mid] < h1) lo = mid + 1; else hi = mid;
-  }
-  uint32_t bq;
-  if (lo < hb && F[lo] == h1) {   // a threshold inside [h1, h1 + 1) / 2^32: the full 53 bits decide
-    const uint2 l = ex();
-    bq = bq_search(cc.cum, cc.guide, cc.max_bp, cc.n_bq, f, n,
-                   ((double)h1 * 2097152.0 + (double)(l.x >> 11)) * (1.0 / 9007199254740992.0));
-    *sub = ((double)h2 * 2097152.0 + (double)(l.y >> 11)) * (1.0 / 9007199254740992.0) < cc.phred[bq];
-    return bq;
-  }
-  bq = lo < 93 ? lo : 93;
-  const uint32_t fp = cc.Fp[bq];
-  if (h2 == fp) {
-    const uint2 l = ex();
-    *sub = ((double)h2 * 2097152.0 + (double)(l.y >> 11)) * (1.0 / 9007199254740992.0) < cc.phred[bq];
-  } else {
-    *sub = h2 < fp;
+// Philox mode, the BQ step from global memory: entries of row (f, n) below h1 (capped at 93) and whether one equals
+// h1 (then the low bits decide), from the bucket entry e = bk[f][n][h1 >> 8] and, for a flagged bucket, a walk over
+// the row's T16 from the bucket's first entry.
+__device__ __forceinline__ uint32_t bq_walk_g(const CorruptCfg &cc, int f, int n, uint32_t h1, bool *amb) {
+  const uint32_t e = cc.bk[((int64_t)f * cc.max_bp + n) * CB_ROW + (h1 >> 8)];
+  uint32_t bq = e & 0x7fu;
+  *amb = false;
+  if (e & 0x80u) {
+    const uint16_t *T = cc.T16 + ((int64_t)f * cc.max_bp + n) * cc.n_bq;
+    const uint32_t lim = cc.n_bq < 93 ? (uint32_t)cc.n_bq : 93u;
+    uint32_t v = bq < lim ? T[bq] : 0xffffffffu;
+    while (v < h1) {
+      bq++;
+      v = bq < lim ? T[bq] : 0xffffffffu;
+    }
+    *amb = v == h1;
   }
   return bq;
 }
 
-// Philox mode: bases n0 and n0 + 1 (n0 even; cnt = 1 or 2 of them) of file f of template t (corruption in place,
-// qualities to q).  Draw (t, f, n0 / 2): words x, y are base n0's h1, h2; z, w base n0 + 1's.
-__device__ __forceinline__ void corrupt_pair(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
-                                             uint8_t *q) {
-  t += cc.t_base;
-  const uint2 key = make_uint2(cc.k0, cc.k1);
-  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 1);
-  const uint4 r = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw, cc.c3), key);
-  bool sub[2] = {false, false};
+// Philox mode, the rare tails out of line (the hot loop stays small): the f64 decisions with the base's low bits
+// (draw (t, f | 0x4000, n)) when h1 lands on a BQ threshold (amb) or h2 on Fp16[bq]; returns bq | sub << 8.
+__device__ __forceinline__ uint32_t cq_exact_body(const double *cum, const double *phred, const uint16_t *guide,
+                                                  int32_t max_bp, int32_t n_bq, uint32_t k0, uint32_t k1, uint32_t c3,
+                                                  uint32_t tl, uint32_t th, int f, int n, uint32_t w, uint32_t bq,
+                                                  uint32_t amb) {
+  const uint4 l = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x4000u | (uint32_t)n, c3), make_uint2(k0, k1));
+  if (amb) {
+    const double u1 = ((double)(w >> 16) * 137438953472.0 + (double)(((uint64_t)l.x << 5) | (l.y >> 27))) *
+                      (1.0 / 9007199254740992.0);
+    bq = bq_search(cum, guide, max_bp, n_bq, f, n, u1);
+  }
+  const double u2 = ((double)(w & 0xffffu) * 137438953472.0 + (double)(((uint64_t)l.z << 5) | (l.w >> 27))) *
+                    (1.0 / 9007199254740992.0);
+  return bq | (u2 < phred[bq] ? 0x100u : 0u);
+}
+static __device__ __noinline__ uint32_t cq_exact(const double *cum, const double *phred, const uint16_t *guide,
+                                                 int32_t max_bp, int32_t n_bq, uint32_t k0, uint32_t k1, uint32_t c3,
+                                                 uint32_t tl, uint32_t th, int f, int n, uint32_t w, uint32_t bq,
+                                                 uint32_t amb) {
+  return cq_exact_body(cum, phred, guide, max_bp, n_bq, k0, k1, c3, tl, th, f, n, w, bq, amb);
+}
+
+// the replacement bases (randint(0, 3)) of the quad's substituted bases (mask subm), packed four to a word
+static __device__ __noinline__ uint32_t cq_subst(uint32_t k0, uint32_t k1, uint32_t c3, uint32_t tl, uint32_t th, uint32_t cw,
+                                          uint32_t subm, uint32_t bases) {
+  const uint4 c = philox4x32_10(make_uint4(tl, th, cw | 0x8000u, c3), make_uint2(k0, k1));
 #pragma unroll
-  for (int i = 0; i < 2; i++) {
-    if (i >= cnt) break;
-    const uint32_t bq = corrupt_base32(cc, f, n0 + i, i ? r.z : r.x, i ? r.w : r.y, &sub[i], [&]() {
-      const uint4 l = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x4000u, cc.c3), key);
-      return i ? make_uint2(l.z, l.w) : make_uint2(l.x, l.y);
-    });
-    q[i] = (uint8_t)(bq + 33);
+  for (int i = 0; i < 4; i++)
+    if ((subm >> i) & 1) {
+      const uint32_t w = i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w;
+      const uint32_t nb = rot_base((uint8_t)(bases >> (8 * i)), __umulhi(w, 3u));
+      bases = (bases & ~(0xffu << (8 * i))) | (nb << (8 * i));
+    }
+  return bases;
+}
+
+// Philox mode: bases n0 .. n0 + cnt - 1 (n0 = 4 * quad, cnt <= 4) of file f of template t (t without t_base): b[]
+// corrupted in place, qualities (bq + 33) to q[].  walk(n, h1, &amb) -> the BQ step (entries below h1, capped at
+// 93; amb when one equals h1), fp(bq) -> Fp16[bq].
+template <typename BK, typename FP>
+__device__ __forceinline__ void corrupt_quad(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
+                                             uint8_t *q, BK walk, FP fp) {
+  t += cc.t_base;
+  const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
+  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 2);
+  const uint4 r = philox4x32_10(make_uint4(tl, th, cw, cc.c3), make_uint2(cc.k0, cc.k1));
+  uint32_t subm = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {   // (selects, not an indexed array: that would be placed in scratch)
+    if (i < cnt) {
+      const int n = n0 + i;
+      const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
+      bool amb;
+      uint32_t bq = walk(n, w >> 16, &amb);
+      const uint32_t p = fp(bq);
+      bool s;
+      if (amb || (w & 0xffffu) == p) {   // U1 or U2 within 2^-16 of a threshold: the full 53 bits decide
+        const uint32_t x = cq_exact(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
+                                    w, bq, amb);
+        bq = x & 0xffu;
+        s = x >> 8;
+      } else {
+        s = (w & 0xffffu) < p;
+      }
+      q[i] = (uint8_t)(bq + 33);
+      subm |= (uint32_t)s << i;
+    }
   }
-  if (sub[0] || sub[1]) {   // rare: the replacement bases (randint(0, 3))
-    const uint4 c = philox4x32_10(make_uint4((uint32_t)t, (uint32_t)(t >> 32), cw | 0x8000u, cc.c3), key);
-    if (sub[0]) b[0] = rot_base(b[0], __umulhi(c.x, 3u));
-    if (sub[1]) b[1] = rot_base(b[1], __umulhi(c.y, 3u));
+  if (subm) {   // rare: the replacement bases
+    const uint32_t nb = cq_subst(cc.k0, cc.k1, cc.c3, tl, th, cw, subm,
+                                 (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
+    b[0] = (uint8_t)nb;
+    b[1] = (uint8_t)(nb >> 8);
+    b[2] = (uint8_t)(nb >> 16);
+    b[3] = (uint8_t)(nb >> 24);
   }
+}
+
+// corrupt_quad with the tables read from global memory
+__device__ __forceinline__ void corrupt_quad_g(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
+                                               uint8_t *q) {
+  corrupt_quad(
+      cc, t, f, n0, cnt, b, q,
+      [&](int n, uint32_t h1, bool *amb) -> uint32_t { return bq_walk_g(cc, f, n, h1, amb); },
+      [&](uint32_t bq) -> uint32_t { return cc.Fp16[bq]; });
 }
 
 }  // namespace mh

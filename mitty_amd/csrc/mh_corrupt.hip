@@ -256,16 +256,18 @@ __global__ void __launch_bounds__(256) k_cr_write(const uint8_t *b0, const uint8
     }
     return;
   }
-  for (int32_t k = 2 * lane; k < L; k += 128) {   // base pairs
-    const int cnt = L - k > 1 ? 2 : 1;
-    uint8_t b[2] = {sq[k], cnt > 1 ? sq[k + 1] : (uint8_t)0}, qq[2];
-    corrupt_pair(cc, t, f, k, cnt, b, qq);
-    ds[k] = (char)b[0];
-    dq[k] = (char)qq[0];
-    if (cnt > 1) {
-      ds[k + 1] = (char)b[1];
-      dq[k + 1] = (char)qq[1];
-    }
+  for (int32_t k = 4 * lane; k < L; k += 256) {   // base quads (one Philox draw each)
+    const int cnt = L - k < 4 ? L - k : 4;
+    uint8_t b[4], qq[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b[i] = i < cnt ? sq[k + i] : (uint8_t)0;
+    corrupt_quad_g(cc, t, f, k, cnt, b, qq);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i < cnt) {
+        ds[k + i] = (char)b[i];
+        dq[k + i] = (char)qq[i];
+      }
   }
 }
 

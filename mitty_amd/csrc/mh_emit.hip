@@ -18,8 +18,8 @@
 //                         LDS window buffer — all gathers of the tile in flight at once;
 //                     A   one owner thread per template formats the qname into the file-1 LDS image;
 //                     B1  one wave per (template, file) copies the qname into the file-2 image and writes
-//                         '\n' seq '\n+\n' qual '\n' from the LDS windows (reverse complement for mate 1, fused
-//                         BQ corruption when enabled);
+//                         '\n' seq '\n+\n' qual '\n' from the LDS windows (reverse complement for mate 1; with
+//                         corruption len(seq) placeholder qualities, k_cr_inplace corrupts the record afterwards);
 //                     C   both images leave LDS as 16-byte aligned stores (byte stores only at the ragged edges of
 //                         the workgroup's output range; neighbouring workgroups own disjoint byte ranges).
 // The sequence of a read is hap[p - p_min, min(p + l, hap_end) - p_min): non-'D' nodes tile sample coordinates
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
                                                            const int64_t *pos1, const int8_t *fo0, int64_t rlen,
                                                            QFixed q, const Rec *recs, const E3 *off, char *out1,
                                                            char *out2, int write2, int32_t cap, int32_t win_stride,
-                                                           CorruptCfg cc, int32_t *err) {
+                                                           int32_t corrupt, int32_t *err) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   TplMeta *meta = (TplMeta *)smem;
   uint8_t *wins = (uint8_t *)smem + ((sizeof(TplMeta) * EW_T + 15) / 16) * 16;
@@ -669,31 +669,14 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
       const int f0 = mt.keep >> 1;
       const int s = f == f0 ? 0 : 1;                  // mate held by file f
       const int S = mt.seq_len[s];
-      const int Q = cc.enable ? S : (int)rlen;        // corrupt_single_read emits len(seq) qualities
+      const int Q = corrupt ? S : (int)rlen;          // corrupt_single_read emits len(seq) qualities
       char *d0 = img[f] + mt.loc[f];
       if (f == 1)
         for (int i = lane; i < mt.qlen; i += 64) d0[i] = img[0][mt.loc[0] + i];
       char *d = d0 + mt.qlen;                         // '\n' seq '\n+\n' qual '\n'
       const uint8_t *w = wins + mt.win[s];
-      const int64_t t = sb + j;
-      if (cc.enable) {
-        for (int n = 2 * lane; n < S; n += 128) {   // base pairs: one Philox draw each
-          const int cnt = S - n > 1 ? 2 : 1;
-          uint8_t b[2] = {s ? comp(w[S - 1 - n]) : w[n], 0}, qq[2];
-          if (cnt > 1) b[1] = s ? comp(w[S - 2 - n]) : w[n + 1];
-          corrupt_pair(cc, t, f, n, cnt, b, qq);
-          d[1 + n] = (char)b[0];
-          d[4 + S + n] = (char)qq[0];
-          if (cnt > 1) {
-            d[2 + n] = (char)b[1];
-            d[5 + S + n] = (char)qq[1];
-          }
-        }
-      } else {
-        for (int n = lane; n < S; n += 64) d[1 + n] = (char)(s ? comp(w[S - 1 - n]) : w[n]);
-      }
-      if (!cc.enable)
-        for (int n = lane; n < Q; n += 64) d[4 + S + n] = '~';
+      for (int n = lane; n < S; n += 64) d[1 + n] = (char)(s ? comp(w[S - 1 - n]) : w[n]);
+      for (int n = lane; n < Q; n += 64) d[4 + S + n] = '~';
       if (lane == 0) {
         d[0] = '\n';
         d[1 + S] = '\n';
@@ -756,7 +739,7 @@ struct DMeta {
   int32_t sb;        // Q length = offset of the first base
   int32_t bb[2];     // LDS offset of B per file (forward order)
   int32_t S[2];      // bases per file
-  int32_t tb[2];     // LDS offset of the record's T (the shared one, or its own with fused corruption)
+  int32_t tb[2];     // LDS offset of the record's T (the shared one)
   int32_t tn[2];     // T length: rlen + 4, or S + 4 with corruption (qualities = len(seq))
 };
 
@@ -829,12 +812,11 @@ struct EdArgs {
   int64_t used[2];
   int32_t rlen, win_stride, head, qstride;
   int32_t dbg;
-  CorruptCfg cc;     // fused BQ corruption (the CR instantiation)
 };
 
-// CR: fused BQ corruption (illumina.corrupt_template, illumina.py:139-162): after the gathers, every base of B is
-// corrupted in place and the record's own T ('\n+\n' + qualities + '\n') is built in LDS; the output passes then read
-// the record's T instead of the shared one.  Same Philox counters as k_emit_write, so the bytes are identical.
+// CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
+// read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
+// placeholders into qualities) when it corrupts the record.
 // FMT: the qname's reads part is formatted here, from the template's nodes (k_emit_measure measured its length
 // only), instead of gathered from the 256-byte slot k_emit_measure formatted it into (MH_EMIT_SLOTS=1).
 template <int NF, int LPR, bool CR, bool FMT>
@@ -852,8 +834,6 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   const bool staged = !(A.dbg & 128);                          // seam chunks via LDS (dbg 128: direct stores)
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;     // T = '\n+\n' + rlen '~' + '\n' (perfect reads, readgenerate.py:229)
-  const int32_t t_stride = ((A.rlen + 4 + 15) / 16) * 16 + 32;   // per-record T with corruption (+ read slack)
-  const int32_t o_tr = ((o_dump + 16 + 15) / 16) * 16;          // CR: per-record T strings [ED_T][NF]
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
 
@@ -918,7 +898,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
         // mate 0 reads hap[a, a + S); mate 1 its reverse complement = rc[hap_len - a - S, hap_len - a)
         const int64_t a2 = s ? h.hap_len - a - S : a;
         mt.bb[f] = o_win + (tid * 2 + s) * win_stride + (int32_t)(a2 & 15);
-        mt.tb[f] = CR ? o_tr + (tid * NF + (NF == 2 ? f : 0)) * t_stride : o_t;
+        mt.tb[f] = o_t;
         mt.tn[f] = CR ? S + 4 : TL;
       }
     }
@@ -1061,94 +1041,6 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   }
   __syncthreads();
   if (A.dbg & 2) return;
-  if constexpr (CR) {   // corrupt B in place, write the record's T
-    // one item per base pair (corrupt_pair's draw) or per record's separators; four items per thread and step,
-    // each phase for all four before the next, so their table loads are in flight together
-    const int32_t rl = A.rlen;
-    const int rp = (rl + 1) / 2 + 1;
-    const int total = nt * NF * rp;
-    const CorruptCfg &cc = A.cc;
-    const uint2 key = make_uint2(cc.k0, cc.k1);
-    for (int i0 = tid; i0 < total; i0 += 4 * ED_THREADS) {
-      int32_t bo[4], to[4], nn[4], ff[4], cnt[4];   // LDS offsets of the pair's bases and the record's T; n0; file
-      int64_t tt[4];
-      int kind[4];                                   // 0: nothing, 1: a base pair, 2: the separators
-      uint4 r[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int idx = i0 + u * ED_THREADS;
-        kind[u] = 0;
-        bo[u] = to[u] = nn[u] = ff[u] = cnt[u] = 0;
-        tt[u] = 0;
-        r[u] = make_uint4(0, 0, 0, 0);
-        if (idx >= total) continue;
-        const int rr = idx / rp, k = idx - rr * rp;
-        const int j = rr / NF, f = rr - j * NF;
-        const DMeta &M = meta[j];
-        if (M.len[f] == 0) continue;
-        const int32_t S = M.S[f];
-        to[u] = M.tb[f];
-        if (k == rp - 1) {
-          kind[u] = 2;
-          nn[u] = S;
-          continue;
-        }
-        const int n = 2 * k;
-        if (n >= S) continue;
-        kind[u] = 1;
-        bo[u] = M.bb[f] + n;
-        nn[u] = n;
-        ff[u] = f;
-        cnt[u] = S - n > 1 ? 2 : 1;
-        tt[u] = t0 + j + cc.t_base;
-        if (A.dbg & 1024)   // timing experiment: no Philox
-          r[u] = make_uint4((uint32_t)tt[u] * 2654435761u, (uint32_t)n * 40503u, (uint32_t)tt[u] ^ n, 77u);
-        else
-          r[u] = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32),
-                                          ((uint32_t)f << 16) | ((uint32_t)n >> 1), cc.c3), key);
-      }
-      uint32_t bq[4][2];
-      bool sub[4][2];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-          bq[u][i] = 0;
-          sub[u][i] = false;
-          if (kind[u] != 1 || i >= cnt[u]) continue;
-          if (A.dbg & 512) {   // timing experiment: no table lookups
-            bq[u][i] = (i ? r[u].z : r[u].x) % 41u;
-            continue;
-          }
-          bq[u][i] = corrupt_base32(cc, ff[u], nn[u] + i, i ? r[u].z : r[u].x, i ? r[u].w : r[u].y, &sub[u][i], [&]() {
-            const uint32_t cw = ((uint32_t)ff[u] << 16) | ((uint32_t)nn[u] >> 1) | 0x4000u;
-            const uint4 l = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32), cw, cc.c3), key);
-            return i ? make_uint2(l.z, l.w) : make_uint2(l.x, l.y);
-          });
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        if (kind[u] == 0) continue;
-        char *T = smem + to[u];
-        if (kind[u] == 2) {   // the separators
-          const int32_t S = nn[u];
-          T[0] = '\n'; T[1] = '+'; T[2] = '\n'; T[3 + S] = '\n';
-          continue;
-        }
-        T[3 + nn[u]] = (char)(bq[u][0] + 33);
-        if (cnt[u] > 1) T[4 + nn[u]] = (char)(bq[u][1] + 33);
-        if (sub[u][0] || sub[u][1]) {   // rare: the replacement bases (randint(0, 3))
-          const uint32_t cw = ((uint32_t)ff[u] << 16) | ((uint32_t)nn[u] >> 1) | 0x8000u;
-          const uint4 c = philox4x32_10(make_uint4((uint32_t)tt[u], (uint32_t)(tt[u] >> 32), cw, cc.c3), key);
-          if (sub[u][0]) smem[bo[u]] = (char)rot_base((uint8_t)smem[bo[u]], __umulhi(c.x, 3u));
-          if (sub[u][1]) smem[bo[u] + 1] = (char)rot_base((uint8_t)smem[bo[u] + 1], __umulhi(c.y, 3u));
-        }
-      }
-    }
-    __syncthreads();
-  }
-
   // ---- output: LPR lanes per record (record r = file f, template j); passes over the tile's NF * ED_T records ----
   constexpr int RPP = ED_THREADS / LPR;                        // records per pass
   const int q = tid % LPR;
@@ -1233,6 +1125,294 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
       *(uint4 *)(arena + (cg << 4)) = v;
     }
   }
+}
+
+// ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
+// After the writer (same stream), over the records it laid out with len(seq) placeholder qualities:
+//   k_cr_recs     one thread per template: each record's first-base offset in its arena and S (0: dropped), packed
+//                 in 8 bytes (offset low word | offset high bits << 16 | S);
+//   k_cr_inplace  one item per base quad of every record (one Philox draw, the fast path below); qualities
+//                 stored, the record's last byte set to '\n', substituted bases written back.  Persistent
+//                 workgroups stage the bucket-table rows of the read positions and the low threshold bytes in LDS
+//                 once, so a base's BQ is one LDS byte read (plus a short walk in a flagged bucket).  A wave takes
+//                 CI_U chunks of 64 consecutive items per step, software-pipelined: the record words of step s+2
+//                 and the bases of step s+1 are in flight while step s computes.
+constexpr int CI_THREADS = 1024;
+constexpr int CI_U = 4;   // wave-chunks per step
+
+struct CiArgs {
+  int64_t p_min, hap_len;
+  int64_t m;
+  const int64_t *pos0, *pos1;
+  const int8_t *fo0;
+  const Rec *recs;
+  const E3 *off;
+  char *arena[2];         // the emission's first byte per file
+  const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
+  int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
+  CorruptCfg cc;
+};
+
+__global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= A.m) return;
+  const int4 rc = *(const int4 *)(A.recs + t);   // keep, len1, len2, rest
+  const int fo = A.fo0[t];
+  const E3 o = A.off[t];
+  for (int f = 0; f < A.nf; f++) {
+    const int64_t p = f == fo ? A.pos0[t] : A.pos1[t];   // file f holds mate f == fo ? 0 : 1
+    int64_t a = p - A.p_min, e = p + A.rlen - A.p_min;
+    if (e > A.hap_len) e = A.hap_len;
+    if (a > A.hap_len) a = A.hap_len;
+    const uint32_t S = rc.x && e > a ? (uint32_t)(e - a) : 0u;
+    // '@stub:' cnt '|chrom|cpy' reads-part '\n' | bases | '\n+\n' | qualities | '\n'
+    const uint64_t so = (uint64_t)((f ? o.b2 : o.b1) + A.lh0 + ndig_u((uint64_t)(o.kept + 1)) + rc.w + 1);
+    crec[t * A.nf + f] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | S);
+  }
+}
+
+// a[u] for a lane-varying u < CI_U, as masks and ors: an indexed register array (or a select chain the compiler
+// folds into one) would be placed in scratch
+template <typename T>
+__device__ __forceinline__ T ci_pick(T a0, T a1, T a2, T a3, int u) {
+  const T m0 = (T)0 - (T)(u == 0), m1 = (T)0 - (T)(u == 1), m2 = (T)0 - (T)(u == 2), m3 = (T)0 - (T)(u == 3);
+  return (a0 & m0) | (a1 & m1) | (a2 & m2) | (a3 & m3);
+}
+static_assert(CI_U == 4, "ci_sel picks over four chunks");
+#define ci_sel(a, u) ci_pick((a)[0], (a)[1], (a)[2], (a)[3], (u))
+
+template <bool LDS_TAB>
+__global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
+  // LDS: bucket entries [2][rlen][CB_ROW] | Fp16[100] | low threshold bytes T16 & 0xff [2][rlen][n_bq]
+  extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
+  const CorruptCfg &cc = A.cc;
+  const int rlen = A.rlen, n_bq = cc.n_bq;
+  const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
+  const int32_t row_bytes = rlen * CB_ROW;   // per file
+  const uint16_t *fp16 = (const uint16_t *)(ctab + 2 * row_bytes);
+  const int32_t o_t8 = 2 * row_bytes + 256;
+  if (LDS_TAB) {
+    for (int f = 0; f < 2; f++) {
+      const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
+      uint4 *dst = (uint4 *)(ctab + f * row_bytes);
+      for (int i = threadIdx.x; i < row_bytes / 16; i += CI_THREADS) dst[i] = src[i];
+      const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
+      for (int i = threadIdx.x; i < rlen * n_bq; i += CI_THREADS) ctab[o_t8 + f * rlen * n_bq + i] = (uint8_t)t16[i];
+    }
+    for (int i = threadIdx.x; i < 100; i += CI_THREADS) ((uint16_t *)fp16)[i] = cc.Fp16[i];
+    __syncthreads();
+  }
+  // the BQ step of base n of file f for the draw's high 16 bits: entries below h1 (capped at 93), amb when one
+  // equals h1.  LDS: the bucket entry; a flagged bucket walks the row's low threshold bytes up to the next bucket's
+  // count.  Global: bq_walk_g.
+  auto walk = [&](int f, int n, uint32_t h1, bool *amb) -> uint32_t {
+    if (!LDS_TAB) return bq_walk_g(cc, f, n, h1, amb);
+    const int row = f * rlen + n;
+    const int kb = (int)(h1 >> 8);
+    const uint32_t e = ctab[row * CB_ROW + kb];
+    uint32_t bq = e & 0x7fu;
+    *amb = false;
+    if (e & 0x80u) {
+      const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
+      const uint8_t *t8 = ctab + o_t8 + row * n_bq;
+      const uint32_t lo = h1 & 0xffu;
+      uint32_t v = bq < lim ? t8[bq] : 0x100u;
+      while (v < lo) {
+        bq++;
+        v = bq < lim ? t8[bq] : 0x100u;
+      }
+      *amb = v == lo;
+    }
+    return bq;
+  };
+  auto fp = [&](uint32_t bq) -> uint32_t { return LDS_TAB ? fp16[bq] : cc.Fp16[bq]; };
+  const uint2 key = make_uint2(cc.k0, cc.k1);
+  const int QPR = (rlen + 3) >> 2;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t n_rec = A.m * A.nf;
+  const int64_t items = n_rec * QPR;
+  const int64_t nchunks = (items + 63) >> 6;
+  // chunk c covers items [64c, 64c + 64); a wave's chunks are c_first + j * wstride, j = 0, 1, ...  The position of
+  // the chunk's first item (record rr_w, quad k_w) advances by a fixed (dq, dr) per chunk instead of a division.
+  const int64_t wstride = (int64_t)gridDim.x * (CI_THREADS / 64);
+  const int64_t c_first = (int64_t)blockIdx.x * (CI_THREADS / 64) + wave;
+  const int64_t nj = c_first < nchunks ? (nchunks - c_first + wstride - 1) / wstride : 0;   // the wave's chunks
+  int64_t rr_w = (c_first << 6) / QPR;
+  int k_w = (int)((c_first << 6) - rr_w * QPR);
+  const int64_t dq = (wstride << 6) / QPR;
+  const int dr = (int)((wstride << 6) - dq * QPR);
+  // the lane's item of the chunk at the current position: record rr (< n_rec when valid), quad k
+  auto item = [&]() -> longlong2 {   // (rr, k); advances the position to the wave's next chunk
+    int k = k_w + lane;
+    int64_t rr = rr_w;
+    while (k >= QPR) {
+      k -= QPR;
+      rr++;
+    }
+    k_w += dr;
+    rr_w += dq;
+    if (k_w >= QPR) {
+      k_w -= QPR;
+      rr_w++;
+    }
+    return make_longlong2(rr, k);
+  };
+  auto rec_load = [&](int64_t rr) -> uint2 { return A.crec[rr < n_rec ? rr : 0]; };
+  // stages: A = step being computed, B = next (record words and bases loaded), C = after next (record words)
+  int64_t rA[CI_U], rB[CI_U], rC[CI_U];
+  int kA[CI_U], kB[CI_U], kC[CI_U];
+  uint2 RA[CI_U], RB[CI_U], RC[CI_U];
+  uint32_t bA[CI_U], bB[CI_U];
+  auto bases = [&](int64_t rr, int k, uint2 R) -> uint32_t {   // the quad's bases, packed
+    const uint32_t S = R.y & 0xffffu;
+    const int n0 = 4 * k;
+    uint32_t w = 0;
+    if (rr < n_rec && (uint32_t)n0 < S) {
+      const char *sq = (A.nf == 2 && (rr & 1) ? A.arena[1] : A.arena[0]) + (((uint64_t)(R.y >> 16) << 32) | R.x) + n0;
+      const int cnt = S - n0 < 4 ? (int)S - n0 : 4;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < cnt) w |= (uint32_t)(uint8_t)sq[i] << (8 * i);
+    }
+    return w;
+  };
+  int64_t j0 = 0;
+  // prologue: steps 0 (records and bases) and 1 (records)
+#pragma unroll
+  for (int u = 0; u < CI_U; u++) {
+    const longlong2 it = item();
+    rA[u] = it.x;
+    kA[u] = (int)it.y;
+    if (j0 + u >= nj) rA[u] = n_rec;
+    RA[u] = rec_load(rA[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < CI_U; u++) {
+    const longlong2 it = item();
+    rB[u] = it.x;
+    kB[u] = (int)it.y;
+    if (j0 + CI_U + u >= nj) rB[u] = n_rec;
+    RB[u] = rec_load(rB[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < CI_U; u++) bA[u] = bases(rA[u], kA[u], RA[u]);
+  for (; j0 < nj; j0 += CI_U) {
+#pragma unroll
+    for (int u = 0; u < CI_U; u++) {   // step + 2: record words
+      const longlong2 it = item();
+    rC[u] = it.x;
+    kC[u] = (int)it.y;
+      if (j0 + 2 * CI_U + u >= nj) rC[u] = n_rec;
+      RC[u] = rec_load(rC[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < CI_U; u++) bB[u] = bases(rB[u], kB[u], RB[u]);   // step + 1: bases
+    // step: one draw per quad, per base the BQ step and the 16-bit decisions; qualities stored.  Bases whose draw
+    // lands on a threshold (px) and substituted bases (ps) are marked, bit 4u + i, for the loops below.
+    uint32_t px = 0, ps = 0;
+#pragma unroll
+    for (int u = 0; u < CI_U; u++) {
+      const uint32_t S = RA[u].y & 0xffffu;
+      const int n0 = 4 * kA[u];
+      if (rA[u] >= n_rec || (uint32_t)n0 >= S) continue;
+      const int cnt = S - n0 < 4 ? (int)S - n0 : 4;
+      const int f = A.nf == 2 ? (int)(rA[u] & 1) : 0;
+      const int64_t tt = (A.nf == 2 ? rA[u] >> 1 : rA[u]) + cc.t_base;
+      const uint4 r = philox4x32_10(
+          make_uint4((uint32_t)tt, (uint32_t)(tt >> 32), ((uint32_t)f << 16) | ((uint32_t)n0 >> 2), cc.c3), key);
+      char *qual = (f ? A.arena[1] : A.arena[0]) + (((uint64_t)(RA[u].y >> 16) << 32) | RA[u].x) + S + 3;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (i < cnt) {
+          const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
+          bool amb;
+          const uint32_t bq = walk(f, n0 + i, w >> 16, &amb);
+          const uint32_t pth = fp(bq), h2 = w & 0xffffu;
+          px |= (uint32_t)(amb || h2 == pth) << (4 * u + i);
+          ps |= (uint32_t)(!amb && h2 < pth) << (4 * u + i);
+          qual[n0 + i] = (char)(bq + 33);
+        }
+      }
+      if (n0 + cnt == (int)S) qual[S] = '\n';
+    }
+    // rare: the full 53-bit decisions (one copy of the code for every base of the step)
+    while (px) {
+      const int j = __builtin_ctz(px);
+      px &= px - 1;
+      const int u = j >> 2, i = j & 3;
+      const int64_t rr = ci_sel(rA, u);
+      uint2 R;
+      R.x = ci_pick(RA[0].x, RA[1].x, RA[2].x, RA[3].x, u);
+      R.y = ci_pick(RA[0].y, RA[1].y, RA[2].y, RA[3].y, u);
+      const int f = A.nf == 2 ? (int)(rr & 1) : 0, n = 4 * ci_sel(kA, u) + i;
+      const int64_t tt = (A.nf == 2 ? rr >> 1 : rr) + cc.t_base;
+      const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
+      const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n >> 2), cc.c3), key);
+      const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
+      bool amb;
+      const uint32_t bq = walk(f, n, w >> 16, &amb);
+      const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f,
+                                       n, w, bq, amb);
+      (f ? A.arena[1] : A.arena[0])[(((uint64_t)(R.y >> 16) << 32) | R.x) + (R.y & 0xffffu) + 3 + n] = (char)((x & 0xffu) + 33);
+      ps |= (x >> 8) << j;
+    }
+    // the substituted bases: base_rot[b][randint(0, 3)], the draw (t, f | 0x8000, quad)
+    while (ps) {
+      const int j = __builtin_ctz(ps);
+      ps &= ps - 1;
+      const int u = j >> 2, i = j & 3;
+      const int64_t rr = ci_sel(rA, u);
+      uint2 R;
+      R.x = ci_pick(RA[0].x, RA[1].x, RA[2].x, RA[3].x, u);
+      R.y = ci_pick(RA[0].y, RA[1].y, RA[2].y, RA[3].y, u);
+      const int f = A.nf == 2 ? (int)(rr & 1) : 0, n = 4 * ci_sel(kA, u) + i;
+      const int64_t tt = (A.nf == 2 ? rr >> 1 : rr) + cc.t_base;
+      const uint4 c = philox4x32_10(
+          make_uint4((uint32_t)tt, (uint32_t)(tt >> 32), ((uint32_t)f << 16) | 0x8000u | ((uint32_t)n >> 2), cc.c3),
+          key);
+      const uint32_t w = i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w;
+      (f ? A.arena[1] : A.arena[0])[(((uint64_t)(R.y >> 16) << 32) | R.x) + n] =
+          (char)rot_base((uint8_t)(ci_sel(bA, u) >> (8 * i)), __umulhi(w, 3u));
+    }
+#pragma unroll
+    for (int u = 0; u < CI_U; u++) {   // rotate the stages
+      rA[u] = rB[u];
+      kA[u] = kB[u];
+      RA[u] = RB[u];
+      bA[u] = bB[u];
+      rB[u] = rC[u];
+      kB[u] = kC[u];
+      RB[u] = RC[u];
+    }
+  }
+}
+
+// the corruption pass over one emission's records (on stream `st`, after its writer)
+int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_t m, const int64_t *pos0,
+                          const int64_t *pos1, const int8_t *fo0, const Rec *recs, const E3 *off, uint2 *crec,
+                          char *o1, char *o2, int32_t nf, int32_t lh0, int32_t rlen, const CorruptCfg &cc) {
+  if (m <= 0) return MH_OK;
+  int ncu = 0;
+  HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  if (ncu <= 0) ncu = 256;
+  const size_t lds = (size_t)2 * rlen * (CB_ROW + cc.n_bq) + 256;
+  const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
+  const int64_t QPR = (rlen + 3) / 4;
+  const int64_t nchunks = (m * nf * QPR + 63) / 64;
+  const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
+  int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (nchunks + CI_THREADS / 64 - 1) / (CI_THREADS / 64));
+  if (grid < 1) grid = 1;
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, cc};
+  stage_begin(ctx, "emit_corrupt");
+  hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
+  HIPCHK(ctx, hipGetLastError());
+  if (lds_tab)
+    hipLaunchKernelGGL(k_cr_inplace<true>, dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
+  else
+    hipLaunchKernelGGL(k_cr_inplace<false>, dim3((unsigned)grid), dim3(CI_THREADS), 0, st, A);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  return MH_OK;
 }
 
 // ---- rpc.generate_read facade: per-read text into host-visible buffers ------------------------------------
@@ -1375,6 +1555,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
     MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+    if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));   // k_cr_recs: 8 bytes per record
     MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
     MH_TRY(ensure(ctx, es.stat, 64));
     char *stat = (char *)es.stat.p;        // per set: a deferred readback must not see the next unit's totals
@@ -1456,6 +1637,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
   size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + (size_t)EW_T * 2 * win_stride + 2 * (size_t)(cap + 16);
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
+  if (ctx->corrupt_on && es.crrec.cap < 16 * (size_t)m + 64) {   // corruption switched on after this unit's measure
+    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+    MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
+  }
   if (ctx->corrupt_on) {
     if (rlen > ctx->corrupt_max_bp) {
       stage_end(ctx);
@@ -1478,8 +1663,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
   const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
                        (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16 +
-                       (ctx->corrupt_on ? 16 + (size_t)ED_T * 2 * ((((int32_t)rlen + 4 + 15) / 16) * 16 + 32) : 0);
+                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16;
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -1497,7 +1681,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_begin(ctx, "emit_write");
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
     EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
-             qstride, edbg, cc};
+             qstride, edbg};
     auto kfn = use_slots
                    ? (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, false> : k_emit_direct<1, 8, true, false>)
                                       : (write_fastq2 ? k_emit_direct<2, 4, false, false> : k_emit_direct<1, 8, false, false>))
@@ -1506,6 +1690,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
+    if (ctx->corrupt_on)
+      MH_TRY(launch_cr_inplace(ctx, ctx->wstream, hv, m, pos0, pos1, fo0, recs, off, (uint2 *)es.crrec.p, o1, o2,
+                               write_fastq2 ? 2 : 1,
+                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc));
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
@@ -1522,9 +1710,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_begin(ctx, "emit_write");
     const int64_t nblk = (m + EW_T - 1) / EW_T;
     hipLaunchKernelGGL(k_emit_write, dim3((unsigned)nblk), dim3(EW_THREADS), lds, st, hv, m,
-                       pos0, pos1, fo0, rlen, q, recs, off, o1, o2, write_fastq2, cap, win_stride, cc, err);
+                       pos0, pos1, fo0, rlen, q, recs, off, o1, o2, write_fastq2, cap, win_stride,
+                       (int32_t)ctx->corrupt_on, err);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
+    if (ctx->corrupt_on)
+      MH_TRY(launch_cr_inplace(ctx, st, hv, m, pos0, pos1, fo0, recs, off, (uint2 *)es.crrec.p, o1, o2,
+                               write_fastq2 ? 2 : 1,
+                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc));
     int32_t herr = 0;
     HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));

@@ -126,6 +126,7 @@ namespace mh {
 // units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
   DevBuf recs, off, slots;
+  DevBuf crrec;                // corruption: per record the first base's offset and S (k_cr_recs)
   DevBuf stat;                 // the measure pass's totals (E3 at 0) and maxima (int32[4] at 32)
   int64_t *h_stat = nullptr;   // pinned: stat's readback (64 B), then the qname prefix (+64) and mid (+4160) staged
   hipEvent_t rb = nullptr;     // after that copy
@@ -182,8 +183,8 @@ struct mh_ctx {
   bool corrupt_on = false;
   mh::DevBuf corrupt_cum, corrupt_phred;
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
-  size_t corrupt_guide_off = 0;   // byte offsets inside corrupt_cum: the search guide, the u32 tables F and Fp
-  size_t corrupt_F_off = 0, corrupt_Fp_off = 0;
+  size_t corrupt_guide_off = 0;   // byte offsets inside corrupt_cum: the search guide, the Philox-mode bucket table
+  size_t corrupt_bk_off = 0, corrupt_T16_off = 0, corrupt_Fp16_off = 0;   // and the u16 tables T16, Fp16
   uint64_t corrupt_seed = 0;
   // exact corruption stream of mh_corrupt_fastq (mh_corrupt_stream_seed / _state): 0 = Philox; 1 = the stream of
   // RandomState(cx_seed) from output cx_pos on; 2 = continuing the explicit state (cx_key, cx_kpos)

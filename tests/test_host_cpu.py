@@ -354,29 +354,65 @@ def test_native_fasta_reader(tmp_path):
     fasta.read_fasta(str(tmp_path / 'missing.fa'))
 
 
-def test_philox_u32_decision_rule_equals_f64():
-  """The Philox-mode corruption decides on the high 32 bits h of a 53-bit uniform U = (h * 2^21 + l) / 2^53 against
-  F = min(floor(x * 2^32), 2^32 - 1) (mh_corrupt.h corrupt_base32): F < h -> x < U, F > h -> not, F == h -> the f64
-  comparison with the low bits.  The rule must equal searchsorted(row, U, 'left') and U < phred in f64 for every
-  U, including h landing exactly on a table value."""
+def _bucket_tables(cum):
+  """The Philox-mode tables of mh_set_corruption: T = min(floor(x * 2^16), 65535) and per row bk[k] = min(entries
+  below k / 256, 93) | 0x80 when an entry lies in bucket k (and fewer than 93 are below it)."""
+  T = np.minimum(np.floor(np.clip(cum, 0, None) * 65536.0), 65535).astype(np.int64)
+  below = np.stack([(T < (k << 8)).sum(-1) for k in range(257)], -1)
+  bk = np.minimum(below[..., :256], 93) | np.where((below[..., :256] < 93) & (below[..., 1:] > below[..., :256]),
+                                                   0x80, 0)
+  return T, bk
+
+
+def _decide16(Trow, bkrow, n_bq, h1):
+  """corrupt_base16's BQ step: (count below h1 capped at 93, ambiguous) from the bucket entry and the row walk."""
+  e = int(bkrow[h1 >> 8])
+  bq = e & 0x7f
+  if not e & 0x80:
+    return bq, False
+  lim = min(n_bq, 93)
+  v = int(Trow[bq]) if bq < lim else 1 << 32
+  while v < h1:
+    bq += 1
+    v = int(Trow[bq]) if bq < lim else 1 << 32
+  return bq, v == h1
+
+
+def test_philox_u16_decision_rule_equals_f64():
+  """The Philox-mode corruption decides on the high 16 bits h of a 53-bit uniform U = (h * 2^37 + l) / 2^53 against
+  T = min(floor(x * 2^16), 65535), through a per-row bucket table (mh_corrupt.h corrupt_base16): T < h -> x < U,
+  T > h -> not, T == h -> the f64 comparison with the low bits.  The rule must equal min(searchsorted(row, U,
+  'left'), 93) and U < phred in f64 for every U, including h landing exactly on a table value."""
   rs = np.random.RandomState(3)
+  phred = 10 ** (-np.arange(100) / 10)
+  Fp = np.minimum(np.floor(phred * 65536.0), 65535).astype(np.int64)
   for m in G.MODELS:
     cum = G.model(m)['cum_bq_mat']
-    phred = 10 ** (-np.arange(100) / 10)
-    F = np.minimum(np.floor(np.clip(cum, 0, None) * 2.0 ** 32), 2 ** 32 - 1).astype(np.uint64)
-    Fp = np.minimum(np.floor(phred * 2.0 ** 32), 2 ** 32 - 1).astype(np.uint64)
+    T, bk = _bucket_tables(cum)
+    n_bq = cum.shape[-1]
     for _ in range(200):
       f, n = rs.randint(2), rs.randint(int(G.model(m)['max_rlen']))
-      row, Frow = cum[f, n], F[f, n]
-      hs = np.concatenate([rs.randint(0, 2 ** 32, 64, dtype=np.uint64), Frow[rs.randint(0, len(Frow), 16)]])
+      row, Trow, bkrow = cum[f, n], T[f, n], bk[f, n]
+      hs = np.concatenate([rs.randint(0, 2 ** 16, 64), Trow[rs.randint(0, n_bq, 16)], [0, 65535]])
       for h in hs:
-        for l in (0, 1, rs.randint(0, 2 ** 21), 2 ** 21 - 1):
-          U = (float(h) * 2.0 ** 21 + l) / 2.0 ** 53
+        h = int(h)
+        for l in (0, 1, rs.randint(0, 2 ** 37, dtype=np.int64), 2 ** 37 - 1):
+          U = (float(h) * 2.0 ** 37 + float(l)) / 2.0 ** 53
           want = min(int(np.searchsorted(row, U, side='left')), 93)
-          lo = int(np.searchsorted(Frow, h, side='left'))
-          got = min(int(np.searchsorted(row, U, side='left')), 93) if lo < len(Frow) and Frow[lo] == h else min(lo, 93)
+          bq, amb = _decide16(Trow, bkrow, n_bq, h)
+          got = want if amb else bq
           assert got == want, (m, f, n, h, l)
-          U2 = U
-          sub_want = U2 < phred[want]
-          sub_got = (U2 < phred[want]) if h == Fp[want] else bool(h < Fp[want])
+          sub_want = U < phred[want]
+          sub_got = (U < phred[want]) if (amb or h == Fp[want]) else bool(h < Fp[want])
           assert sub_got == sub_want
+
+
+def test_philox_restatement_known_answers():
+  """tests/philox_ref.py (the Philox-mode parity restatement) against Random123's Philox4x32-10 known-answer
+  vectors (ctr = key = 0; ctr = key = all ones)."""
+  from tests import philox_ref as P
+  assert [int(x[0]) for x in P.philox4x32_10([0], [0], [0], [0], 0, 0)] == \
+      [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+  m = 0xffffffff
+  assert [int(x[0]) for x in P.philox4x32_10([m], [m], [m], [m], m, m)] == \
+      [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
