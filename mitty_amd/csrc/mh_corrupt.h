@@ -5,15 +5,16 @@
 // min(searchsorted(cum_bq[mate, n, :], U1, side='left'), 93) and substitution when U2 < phred_p[bq].  Word sources:
 //   exact mode   the reference's own MT19937 stream (mh_corrupt.hip: rand(n), rand(n), randint(0, 3, n) per mate),
 //                U = numpy's ((a >> 5) * 2^26 + (b >> 6)) / 2^53, compared in f64
-//   Philox mode  Philox4x32-10 keyed by (seed, unit), one draw per four bases, counter (template, file, quad):
-//                base i of the quad takes word i, h1 = its high 16 bits (the top of U1), h2 = its low 16 bits (the
-//                top of U2), U = (h * 2^37 + l) / 2^53.  Decisions are taken on h against u16 tables T = floor(x * 2^16)
-//                (clamped to 65535): T < h decides "below", T > h "not below"; only T == h needs the low 37 bits,
-//                which then come from a per-base draw (flag 0x4000) and the f64 comparison runs — the outcome of
-//                comparing the full 53-bit U in f64.  The BQ search is one byte per draw: bk[row][h1 >> 8] holds the
-//                entries below the bucket (capped at 93) and a flag when a threshold falls inside it (then the
-//                row's T entries from there are walked).  The replacement bases come from a per-quad counter with
-//                flag 0x8000, umulhi(word i, 3).
+//   Philox mode  Philox4x32-10 keyed by (seed, unit), one draw per three bases, counter (template, file, triple):
+//                base k of the triple takes word k (x, y, z): h1 = its high 16 bits (the top of U1), h2 = its low
+//                16 bits (the top of U2), U = (h * 2^37 + l) / 2^53; word w holds the three bases' replacement
+//                choices, 10 bits each (c < 1023: randint(0, 3) = c % 3, exact since 1023 = 3 * 341; c = 1023: the
+//                base's own draw (t, f | 0x8000, n), umulhi(x, 3)).  Decisions are taken on h against u16 tables
+//                T = floor(x * 2^16) (clamped to 65535): T < h decides "below", T > h "not below"; only T == h needs
+//                the low 37 bits, which then come from a per-base draw (flag 0x4000) and the f64 comparison runs —
+//                the outcome of comparing the full 53-bit U in f64.  The BQ search is one byte per draw:
+//                bk[row][h1 >> 8] holds the entries below the bucket (capped at 93) and a flag when a threshold
+//                falls inside it (then the row's T entries from there are walked).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -78,8 +79,10 @@ __device__ __forceinline__ uint32_t bq_search(const double *cum, const uint16_t 
 
 // base_rot.get(b, 'NNN')[c] (illumina.py:131-136, 160)
 __device__ __forceinline__ uint8_t rot_base(uint8_t x, uint32_t c) {
-  const char *rot = x == 'A' ? "CTG" : x == 'C' ? "ATG" : x == 'T' ? "ACG" : x == 'G' ? "ACT" : "NNN";
-  return (uint8_t)rot[c];
+  // the three replacements packed little-endian in a word (no table load): "CTG", "ATG", "ACG", "ACT", "NNN"
+  const uint32_t rot = x == 'A' ? 0x475443u : x == 'C' ? 0x475441u : x == 'T' ? 0x474341u : x == 'G' ? 0x544341u
+                                                                                                    : 0x4e4e4eu;
+  return (uint8_t)(rot >> (8 * c));
 }
 
 // Philox mode, the BQ step from global memory: entries of row (f, n) below h1 (capped at 93) and whether one equals
@@ -125,36 +128,21 @@ static __device__ __noinline__ uint32_t cq_exact(const double *cum, const double
   return cq_exact_body(cum, phred, guide, max_bp, n_bq, k0, k1, c3, tl, th, f, n, w, bq, amb);
 }
 
-// the replacement bases (randint(0, 3)) of the quad's substituted bases (mask subm), packed four to a word
-static __device__ __noinline__ uint32_t cq_subst(uint32_t k0, uint32_t k1, uint32_t c3, uint32_t tl, uint32_t th, uint32_t cw,
-                                          uint32_t subm, uint32_t bases) {
-  const uint4 c = philox4x32_10(make_uint4(tl, th, cw | 0x8000u, c3), make_uint2(k0, k1));
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-    if ((subm >> i) & 1) {
-      const uint32_t w = i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w;
-      const uint32_t nb = rot_base((uint8_t)(bases >> (8 * i)), __umulhi(w, 3u));
-      bases = (bases & ~(0xffu << (8 * i))) | (nb << (8 * i));
-    }
-  return bases;
-}
-
-// Philox mode: bases n0 .. n0 + cnt - 1 (n0 = 4 * quad, cnt <= 4) of file f of template t (t without t_base): b[]
-// corrupted in place, qualities (bq + 33) to q[].  walk(n, h1, &amb) -> the BQ step (entries below h1, capped at
-// 93; amb when one equals h1), fp(bq) -> Fp16[bq].
+// Philox mode: bases n0 .. n0 + cnt - 1 (n0 = 3 * triple, cnt <= 3) of file f of template t (t without t_base):
+// b[] corrupted in place, qualities (bq + 33) to q[].  walk(n, h1, &amb) -> the BQ step (entries below h1, capped
+// at 93; amb when one equals h1), fp(bq) -> Fp16[bq].
 template <typename BK, typename FP>
-__device__ __forceinline__ void corrupt_quad(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
-                                             uint8_t *q, BK walk, FP fp) {
+__device__ __forceinline__ void corrupt_triple(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
+                                               uint8_t *q, BK walk, FP fp) {
   t += cc.t_base;
   const uint32_t tl = (uint32_t)t, th = (uint32_t)(t >> 32);
-  const uint32_t cw = ((uint32_t)f << 16) | ((uint32_t)n0 >> 2);
-  const uint4 r = philox4x32_10(make_uint4(tl, th, cw, cc.c3), make_uint2(cc.k0, cc.k1));
-  uint32_t subm = 0;
+  const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u), cc.c3),
+                                make_uint2(cc.k0, cc.k1));
 #pragma unroll
-  for (int i = 0; i < 4; i++) {   // (selects, not an indexed array: that would be placed in scratch)
-    if (i < cnt) {
-      const int n = n0 + i;
-      const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
+  for (int k = 0; k < 3; k++) {   // (selects, not an indexed array: that would be placed in scratch)
+    if (k < cnt) {
+      const int n = n0 + k;
+      const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
       bool amb;
       uint32_t bq = walk(n, w >> 16, &amb);
       const uint32_t p = fp(bq);
@@ -167,24 +155,22 @@ __device__ __forceinline__ void corrupt_quad(const CorruptCfg &cc, int64_t t, in
       } else {
         s = (w & 0xffffu) < p;
       }
-      q[i] = (uint8_t)(bq + 33);
-      subm |= (uint32_t)s << i;
+      q[k] = (uint8_t)(bq + 33);
+      if (s) {   // randint(0, 3): the triple's 10 choice bits, or (rejected) the base's own draw
+        uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+        if (c10 == 1023u)
+          c10 = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)n, cc.c3),
+                                       make_uint2(cc.k0, cc.k1)).x, 3u);
+        b[k] = rot_base(b[k], c10 % 3u);
+      }
     }
-  }
-  if (subm) {   // rare: the replacement bases
-    const uint32_t nb = cq_subst(cc.k0, cc.k1, cc.c3, tl, th, cw, subm,
-                                 (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24));
-    b[0] = (uint8_t)nb;
-    b[1] = (uint8_t)(nb >> 8);
-    b[2] = (uint8_t)(nb >> 16);
-    b[3] = (uint8_t)(nb >> 24);
   }
 }
 
-// corrupt_quad with the tables read from global memory
-__device__ __forceinline__ void corrupt_quad_g(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
-                                               uint8_t *q) {
-  corrupt_quad(
+// corrupt_triple with the tables read from global memory
+__device__ __forceinline__ void corrupt_triple_g(const CorruptCfg &cc, int64_t t, int f, int n0, int cnt, uint8_t *b,
+                                                 uint8_t *q) {
+  corrupt_triple(
       cc, t, f, n0, cnt, b, q,
       [&](int n, uint32_t h1, bool *amb) -> uint32_t { return bq_walk_g(cc, f, n, h1, amb); },
       [&](uint32_t bq) -> uint32_t { return cc.Fp16[bq]; });

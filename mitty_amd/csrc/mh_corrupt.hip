@@ -256,14 +256,14 @@ __global__ void __launch_bounds__(256) k_cr_write(const uint8_t *b0, const uint8
     }
     return;
   }
-  for (int32_t k = 4 * lane; k < L; k += 256) {   // base quads (one Philox draw each)
-    const int cnt = L - k < 4 ? L - k : 4;
-    uint8_t b[4], qq[4];
+  for (int32_t k = 3 * lane; k < L; k += 192) {   // base triples (one Philox draw each)
+    const int cnt = L - k < 3 ? L - k : 3;
+    uint8_t b[3], qq[3];
 #pragma unroll
-    for (int i = 0; i < 4; i++) b[i] = i < cnt ? sq[k + i] : (uint8_t)0;
-    corrupt_quad_g(cc, t, f, k, cnt, b, qq);
+    for (int i = 0; i < 3; i++) b[i] = i < cnt ? sq[k + i] : (uint8_t)0;
+    corrupt_triple_g(cc, t, f, k, cnt, b, qq);
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < 3; i++)
       if (i < cnt) {
         ds[k + i] = (char)b[i];
         dq[k + i] = (char)qq[i];

@@ -1131,14 +1131,13 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
 // After the writer (same stream), over the records it laid out with len(seq) placeholder qualities:
 //   k_cr_recs     one thread per template: each record's first-base offset in its arena and S (0: dropped), packed
 //                 in 8 bytes (offset low word | offset high bits << 16 | S);
-//   k_cr_inplace  one item per base quad of every record (one Philox draw, the fast path below); qualities
-//                 stored, the record's last byte set to '\n', substituted bases written back.  Persistent
-//                 workgroups stage the bucket-table rows of the read positions and the low threshold bytes in LDS
-//                 once, so a base's BQ is one LDS byte read (plus a short walk in a flagged bucket).  A wave takes
-//                 CI_U chunks of 64 consecutive items per step, software-pipelined: the record words of step s+2
-//                 and the bases of step s+1 are in flight while step s computes.
+//   k_cr_inplace  one item per 15-base block of every record (five Philox triple draws); qualities stored, the
+//                 record's last byte set to '\n', substituted bases replaced from the block's prefetched bases;
+//                 the rare bases whose draw lands on a threshold (full 53-bit decisions) in a loop after the block.  Persistent workgroups stage the bucket-table rows of the read positions and the low
+//                 threshold bytes in LDS once, so a base's BQ is one LDS byte read (plus a short walk in a flagged
+//                 bucket); the next item's record word is loaded while the current one computes.
 constexpr int CI_THREADS = 1024;
-constexpr int CI_U = 4;   // wave-chunks per step
+constexpr int CI_BLK = 15;   // bases per item: five triple draws
 
 struct CiArgs {
   int64_t p_min, hap_len;
@@ -1150,6 +1149,7 @@ struct CiArgs {
   char *arena[2];         // the emission's first byte per file
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
+  int32_t dbg;            // timing experiments (MH_CR_DBG): 1 no exact loop, 2 no substitution loop, 4 no walk
   CorruptCfg cc;
 };
 
@@ -1170,16 +1170,6 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
     crec[t * A.nf + f] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | S);
   }
 }
-
-// a[u] for a lane-varying u < CI_U, as masks and ors: an indexed register array (or a select chain the compiler
-// folds into one) would be placed in scratch
-template <typename T>
-__device__ __forceinline__ T ci_pick(T a0, T a1, T a2, T a3, int u) {
-  const T m0 = (T)0 - (T)(u == 0), m1 = (T)0 - (T)(u == 1), m2 = (T)0 - (T)(u == 2), m3 = (T)0 - (T)(u == 3);
-  return (a0 & m0) | (a1 & m1) | (a2 & m2) | (a3 & m3);
-}
-static_assert(CI_U == 4, "ci_sel picks over four chunks");
-#define ci_sel(a, u) ci_pick((a)[0], (a)[1], (a)[2], (a)[3], (u))
 
 template <bool LDS_TAB>
 __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
@@ -1210,180 +1200,146 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
     const int row = f * rlen + n;
     const int kb = (int)(h1 >> 8);
     const uint32_t e = ctab[row * CB_ROW + kb];
-    uint32_t bq = e & 0x7fu;
-    *amb = false;
-    if (e & 0x80u) {
-      const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
-      const uint8_t *t8 = ctab + o_t8 + row * n_bq;
-      const uint32_t lo = h1 & 0xffu;
-      uint32_t v = bq < lim ? t8[bq] : 0x100u;
-      while (v < lo) {
-        bq++;
-        v = bq < lim ? t8[bq] : 0x100u;
-      }
-      *amb = v == lo;
+    const uint32_t c = e & 0x7fu;
+    // the bucket's first two low bytes, read for every lane (no branch; past the row's end they are masked by lim)
+    const uint8_t *t8 = ctab + o_t8 + row * n_bq;
+    const uint32_t v0 = t8[c], v1 = t8[c + 1];
+    const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
+    const uint32_t lo = h1 & 0xffu;
+    if (!(e & 0x80u) || (A.dbg & 4)) {
+      *amb = false;
+      return c;
     }
+    // flagged: c < lim
+    const bool b0 = v0 < lo, b1 = b0 && c + 1 < lim && v1 < lo;
+    if (!b1) {
+      *amb = b0 ? (c + 1 < lim && v1 == lo) : v0 == lo;
+      return c + (uint32_t)b0;
+    }
+    uint32_t bq = c + 2;   // rare: two or more entries of the bucket below h1
+    uint32_t v = bq < lim ? t8[bq] : 0x100u;
+    while (v < lo) {
+      bq++;
+      v = bq < lim ? t8[bq] : 0x100u;
+    }
+    *amb = v == lo;
     return bq;
   };
   auto fp = [&](uint32_t bq) -> uint32_t { return LDS_TAB ? fp16[bq] : cc.Fp16[bq]; };
   const uint2 key = make_uint2(cc.k0, cc.k1);
-  const int QPR = (rlen + 3) >> 2;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int64_t n_rec = A.m * A.nf;
-  const int64_t items = n_rec * QPR;
-  const int64_t nchunks = (items + 63) >> 6;
-  // chunk c covers items [64c, 64c + 64); a wave's chunks are c_first + j * wstride, j = 0, 1, ...  The position of
-  // the chunk's first item (record rr_w, quad k_w) advances by a fixed (dq, dr) per chunk instead of a division.
-  const int64_t wstride = (int64_t)gridDim.x * (CI_THREADS / 64);
-  const int64_t c_first = (int64_t)blockIdx.x * (CI_THREADS / 64) + wave;
-  const int64_t nj = c_first < nchunks ? (nchunks - c_first + wstride - 1) / wstride : 0;   // the wave's chunks
-  int64_t rr_w = (c_first << 6) / QPR;
-  int k_w = (int)((c_first << 6) - rr_w * QPR);
-  const int64_t dq = (wstride << 6) / QPR;
-  const int dr = (int)((wstride << 6) - dq * QPR);
-  // the lane's item of the chunk at the current position: record rr (< n_rec when valid), quad k
-  auto item = [&]() -> longlong2 {   // (rr, k); advances the position to the wave's next chunk
-    int k = k_w + lane;
-    int64_t rr = rr_w;
-    while (k >= QPR) {
-      k -= QPR;
-      rr++;
-    }
-    k_w += dr;
-    rr_w += dq;
-    if (k_w >= QPR) {
-      k_w -= QPR;
-      rr_w++;
-    }
-    return make_longlong2(rr, k);
+  // items: 15-base blocks of the records, NB per record (block b = bases 15b .. 15b + 14: five triple draws)
+  const uint32_t NB = (uint32_t)(rlen + CI_BLK - 1) / CI_BLK;
+  const uint32_t n_items = (uint32_t)(A.m * A.nf) * NB;
+  const uint32_t stride = gridDim.x * CI_THREADS;
+  const uint32_t nb_magic = 0xffffffffu / NB + 1u;   // umulhi(i, nb_magic) is i / NB or one more
+  auto rec_of = [&](uint32_t i) -> uint32_t {
+    i = i < n_items ? i : 0u;
+    const uint32_t q = __umulhi(i, nb_magic);
+    return q * NB > i ? q - 1 : q;
   };
-  auto rec_load = [&](int64_t rr) -> uint2 { return A.crec[rr < n_rec ? rr : 0]; };
-  // stages: A = step being computed, B = next (record words and bases loaded), C = after next (record words)
-  int64_t rA[CI_U], rB[CI_U], rC[CI_U];
-  int kA[CI_U], kB[CI_U], kC[CI_U];
-  uint2 RA[CI_U], RB[CI_U], RC[CI_U];
-  uint32_t bA[CI_U], bB[CI_U];
-  auto bases = [&](int64_t rr, int k, uint2 R) -> uint32_t {   // the quad's bases, packed
+  uint32_t i = blockIdx.x * CI_THREADS + threadIdx.x;
+  uint2 R = A.crec[rec_of(i)];                         // this item's record word; the next one is in flight below
+  for (; i < n_items; i += stride) {
+    const uint32_t rr = rec_of(i);
+    const uint2 Rn = A.crec[rec_of(i + stride)];     // prefetch
     const uint32_t S = R.y & 0xffffu;
-    const int n0 = 4 * k;
-    uint32_t w = 0;
-    if (rr < n_rec && (uint32_t)n0 < S) {
-      const char *sq = (A.nf == 2 && (rr & 1) ? A.arena[1] : A.arena[0]) + (((uint64_t)(R.y >> 16) << 32) | R.x) + n0;
-      const int cnt = S - n0 < 4 ? (int)S - n0 : 4;
+    const int n0 = CI_BLK * (int)(i - rr * NB);
+    if ((uint32_t)n0 < S) {
+      const int cnt = S - n0 < CI_BLK ? (int)S - n0 : CI_BLK;
+      const int f = A.nf == 2 ? (int)(rr & 1) : 0;
+      const int64_t tt = (int64_t)(A.nf == 2 ? rr >> 1 : rr) + cc.t_base;
+      const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
+      char *const seq = (f ? A.arena[1] : A.arena[0]) + (((uint64_t)(R.y >> 16) << 32) | R.x);
+      char *const qual = seq + S + 3;
+      // the block's bases: the two aligned 16-byte chunks holding them, shifted into bw[0..3] (base j = byte j)
+      const uint64_t sa = (uint64_t)(seq + n0);
+      const uint4 *sp = (const uint4 *)(sa & ~(uint64_t)15);
+      const uint4 g0 = sp[0], g1 = sp[1];
+      uint32_t qd[4] = {0, 0, 0, 0};   // the block's qualities, packed
+      uint32_t px = 0, pc = 0, ps = 0;   // bases needing the f64 decisions / a fallback choice draw; substituted
+      uint32_t ch = 0;                   // choices of the substituted bases (2 bits each)
 #pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (i < cnt) w |= (uint32_t)(uint8_t)sq[i] << (8 * i);
-    }
-    return w;
-  };
-  int64_t j0 = 0;
-  // prologue: steps 0 (records and bases) and 1 (records)
+      for (int g = 0; g < CI_BLK / 3; g++) {
+        if (3 * g < cnt) {
+          const uint4 r = philox4x32_10(
+              make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
 #pragma unroll
-  for (int u = 0; u < CI_U; u++) {
-    const longlong2 it = item();
-    rA[u] = it.x;
-    kA[u] = (int)it.y;
-    if (j0 + u >= nj) rA[u] = n_rec;
-    RA[u] = rec_load(rA[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < CI_U; u++) {
-    const longlong2 it = item();
-    rB[u] = it.x;
-    kB[u] = (int)it.y;
-    if (j0 + CI_U + u >= nj) rB[u] = n_rec;
-    RB[u] = rec_load(rB[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < CI_U; u++) bA[u] = bases(rA[u], kA[u], RA[u]);
-  for (; j0 < nj; j0 += CI_U) {
-#pragma unroll
-    for (int u = 0; u < CI_U; u++) {   // step + 2: record words
-      const longlong2 it = item();
-    rC[u] = it.x;
-    kC[u] = (int)it.y;
-      if (j0 + 2 * CI_U + u >= nj) rC[u] = n_rec;
-      RC[u] = rec_load(rC[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < CI_U; u++) bB[u] = bases(rB[u], kB[u], RB[u]);   // step + 1: bases
-    // step: one draw per quad, per base the BQ step and the 16-bit decisions; qualities stored.  Bases whose draw
-    // lands on a threshold (px) and substituted bases (ps) are marked, bit 4u + i, for the loops below.
-    uint32_t px = 0, ps = 0;
-#pragma unroll
-    for (int u = 0; u < CI_U; u++) {
-      const uint32_t S = RA[u].y & 0xffffu;
-      const int n0 = 4 * kA[u];
-      if (rA[u] >= n_rec || (uint32_t)n0 >= S) continue;
-      const int cnt = S - n0 < 4 ? (int)S - n0 : 4;
-      const int f = A.nf == 2 ? (int)(rA[u] & 1) : 0;
-      const int64_t tt = (A.nf == 2 ? rA[u] >> 1 : rA[u]) + cc.t_base;
-      const uint4 r = philox4x32_10(
-          make_uint4((uint32_t)tt, (uint32_t)(tt >> 32), ((uint32_t)f << 16) | ((uint32_t)n0 >> 2), cc.c3), key);
-      char *qual = (f ? A.arena[1] : A.arena[0]) + (((uint64_t)(RA[u].y >> 16) << 32) | RA[u].x) + S + 3;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        if (i < cnt) {
-          const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
-          bool amb;
-          const uint32_t bq = walk(f, n0 + i, w >> 16, &amb);
-          const uint32_t pth = fp(bq), h2 = w & 0xffffu;
-          px |= (uint32_t)(amb || h2 == pth) << (4 * u + i);
-          ps |= (uint32_t)(!amb && h2 < pth) << (4 * u + i);
-          qual[n0 + i] = (char)(bq + 33);
+          for (int k = 0; k < 3; k++) {
+            const int j = 3 * g + k;
+            if (j < cnt) {
+              const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+              bool amb;
+              const uint32_t bq = walk(f, n0 + j, w >> 16, &amb);
+              const uint32_t pth = fp(bq), h2 = w & 0xffffu;
+              const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+              const bool sub = !amb && h2 < pth;
+              px |= (uint32_t)(amb || h2 == pth) << j;
+              ps |= (uint32_t)sub << j;
+              pc |= (uint32_t)(sub && c10 == 1023u) << j;
+              ch |= (c10 % 3u) << (2 * j);
+              qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
+            }
+          }
         }
       }
-      if (n0 + cnt == (int)S) qual[S] = '\n';
-    }
-    // rare: the full 53-bit decisions (one copy of the code for every base of the step)
-    while (px) {
-      const int j = __builtin_ctz(px);
-      px &= px - 1;
-      const int u = j >> 2, i = j & 3;
-      const int64_t rr = ci_sel(rA, u);
-      uint2 R;
-      R.x = ci_pick(RA[0].x, RA[1].x, RA[2].x, RA[3].x, u);
-      R.y = ci_pick(RA[0].y, RA[1].y, RA[2].y, RA[3].y, u);
-      const int f = A.nf == 2 ? (int)(rr & 1) : 0, n = 4 * ci_sel(kA, u) + i;
-      const int64_t tt = (A.nf == 2 ? rr >> 1 : rr) + cc.t_base;
-      const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
-      const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n >> 2), cc.c3), key);
-      const uint32_t w = i == 0 ? r.x : i == 1 ? r.y : i == 2 ? r.z : r.w;
-      bool amb;
-      const uint32_t bq = walk(f, n, w >> 16, &amb);
-      const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f,
-                                       n, w, bq, amb);
-      (f ? A.arena[1] : A.arena[0])[(((uint64_t)(R.y >> 16) << 32) | R.x) + (R.y & 0xffffu) + 3 + n] = (char)((x & 0xffu) + 33);
-      ps |= (x >> 8) << j;
-    }
-    // the substituted bases: base_rot[b][randint(0, 3)], the draw (t, f | 0x8000, quad)
-    while (ps) {
-      const int j = __builtin_ctz(ps);
-      ps &= ps - 1;
-      const int u = j >> 2, i = j & 3;
-      const int64_t rr = ci_sel(rA, u);
-      uint2 R;
-      R.x = ci_pick(RA[0].x, RA[1].x, RA[2].x, RA[3].x, u);
-      R.y = ci_pick(RA[0].y, RA[1].y, RA[2].y, RA[3].y, u);
-      const int f = A.nf == 2 ? (int)(rr & 1) : 0, n = 4 * ci_sel(kA, u) + i;
-      const int64_t tt = (A.nf == 2 ? rr >> 1 : rr) + cc.t_base;
-      const uint4 c = philox4x32_10(
-          make_uint4((uint32_t)tt, (uint32_t)(tt >> 32), ((uint32_t)f << 16) | 0x8000u | ((uint32_t)n >> 2), cc.c3),
-          key);
-      const uint32_t w = i == 0 ? c.x : i == 1 ? c.y : i == 2 ? c.z : c.w;
-      (f ? A.arena[1] : A.arena[0])[(((uint64_t)(R.y >> 16) << 32) | R.x) + n] =
-          (char)rot_base((uint8_t)(ci_sel(bA, u) >> (8 * i)), __umulhi(w, 3u));
-    }
+      char *const qb = qual + n0;
+      if (cnt == CI_BLK) {
 #pragma unroll
-    for (int u = 0; u < CI_U; u++) {   // rotate the stages
-      rA[u] = rB[u];
-      kA[u] = kB[u];
-      RA[u] = RB[u];
-      bA[u] = bB[u];
-      rB[u] = rC[u];
-      kB[u] = kC[u];
-      RB[u] = RC[u];
+        for (int j = 0; j < CI_BLK; j++) qb[j] = (char)(qd[j >> 2] >> (8 * (j & 3)));
+      } else {
+#pragma unroll
+        for (int j = 0; j < CI_BLK; j++)
+          if (j < cnt) qb[j] = (char)(qd[j >> 2] >> (8 * (j & 3)));
+      }
+      if (n0 + cnt == (int)S) qual[S] = '\n';
+      if (A.dbg & 1) px = 0;
+      if (A.dbg & 2) ps = pc = 0;
+      // rare: the full 53-bit decisions (the choice bits come from the same triple draw)
+      while (px) {
+        const int j = __builtin_ctz(px);
+        px &= px - 1;
+        const int n = n0 + j;
+        const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+        const int k = n % 3;
+        const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+        bool amb;
+        const uint32_t bq = walk(f, n, w >> 16, &amb);
+        const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f,
+                                         n, w, bq, amb);
+        qual[n] = (char)((x & 0xffu) + 33);
+        const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+        ps |= (x >> 8) << j;
+        pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
+      }
+      // rare: a substituted base whose 10 choice bits are 1023 (rejected): its own draw (t, f | 0x8000, n)
+      while (pc) {
+        const int j = __builtin_ctz(pc);
+        pc &= pc - 1;
+        const uint4 c = philox4x32_10(
+            make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
+        ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
+      }
+      // the substituted bases: base_rot[b][choice]
+      if (ps) {
+        const uint32_t sh = (uint32_t)(sa & 15);
+        const uint32_t o = sh >> 2, bsh = 8 * (sh & 3);
+        // dwords o .. o + 4 of the 32 loaded bytes, then byte-aligned
+        const uint32_t d0 = o == 0 ? g0.x : o == 1 ? g0.y : o == 2 ? g0.z : g0.w;
+        const uint32_t d1 = o == 0 ? g0.y : o == 1 ? g0.z : o == 2 ? g0.w : g1.x;
+        const uint32_t d2 = o == 0 ? g0.z : o == 1 ? g0.w : o == 2 ? g1.x : g1.y;
+        const uint32_t d3 = o == 0 ? g0.w : o == 1 ? g1.x : o == 2 ? g1.y : g1.z;
+        const uint32_t d4 = o == 0 ? g1.x : o == 1 ? g1.y : o == 2 ? g1.z : g1.w;
+        const uint32_t bw0 = (uint32_t)(((uint64_t)d1 << 32 | d0) >> bsh), bw1 = (uint32_t)(((uint64_t)d2 << 32 | d1) >> bsh),
+                       bw2 = (uint32_t)(((uint64_t)d3 << 32 | d2) >> bsh), bw3 = (uint32_t)(((uint64_t)d4 << 32 | d3) >> bsh);
+        do {   // one iteration per substituted base of the lane (about 0.7 of 15 at a 4.7 % error rate)
+          const int j = __builtin_ctz(ps);
+          ps &= ps - 1;
+          const uint32_t bw = j < 4 ? bw0 : j < 8 ? bw1 : j < 12 ? bw2 : bw3;
+          seq[n0 + j] = (char)rot_base((uint8_t)(bw >> (8 * (j & 3))), (ch >> (2 * j)) & 3u);
+        } while (ps);
+      }
     }
+    R = Rn;
   }
 }
 
@@ -1395,14 +1351,15 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (ncu <= 0) ncu = 256;
-  const size_t lds = (size_t)2 * rlen * (CB_ROW + cc.n_bq) + 256;
+  const size_t lds = (size_t)2 * rlen * (CB_ROW + cc.n_bq) + 256 + 16;   // (+16: the walk's speculative reads)
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
-  const int64_t QPR = (rlen + 3) / 4;
-  const int64_t nchunks = (m * nf * QPR + 63) / 64;
+  const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
+  if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
   const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
-  int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (nchunks + CI_THREADS / 64 - 1) / (CI_THREADS / 64));
+  int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
   if (grid < 1) grid = 1;
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, cc};
+  static const int32_t dbg = getenv("MH_CR_DBG") ? atoi(getenv("MH_CR_DBG")) : 0;
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, dbg, cc};
   stage_begin(ctx, "emit_corrupt");
   hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
   HIPCHK(ctx, hipGetLastError());

@@ -1,11 +1,12 @@
-"""numpy restatement of the Philox-mode BQ corruption (test infrastructure; mh_corrupt.h corrupt_quad).
+"""numpy restatement of the Philox-mode BQ corruption (test infrastructure; mh_corrupt.h corrupt_triple).
 
 The Philox mode is this framework's counter-based stream, so its specification lives here rather than in the
-reference: for base n of file f of template t (t counted inside the unit), the draw (t, f, n // 4) of Philox4x32-10
-gives word w = draw[n % 4]; U1 = ((w >> 16) * 2^37 + l1) / 2^53 and U2 = ((w & 0xffff) * 2^37 + l2) / 2^53, where l1, l2
+reference: for base n of file f of template t (t counted inside the unit), the draw (t, f, n // 3) of Philox4x32-10
+gives word w = draw[n % 3]; U1 = ((w >> 16) * 2^37 + l1) / 2^53 and U2 = ((w & 0xffff) * 2^37 + l2) / 2^53, where l1, l2
 are the 37-bit values (x << 5 | y >> 27), (z << 5 | w >> 27) of the base's own draw (t, f | 0x4000 flag, n).  Then the
 reference's decisions in f64 (illumina.py:156-160): bq = min(searchsorted(cum_bq[f, n], U1, 'left'), 93), substitution
-when U2 < phred_p[bq], by base_rot[b][umulhi(c, 3)] with c = word n % 4 of the draw (t, f | 0x8000 flag, n // 4).
+when U2 < phred_p[bq], by base_rot[b][c], c = c10 % 3 with c10 = bits 10 (n % 3) .. + 9 of the triple draw's fourth
+word, or, when c10 = 1023, umulhi(x, 3) of the base's draw (t, f | 0x8000 flag, n).
 The device decides on the 16 high bits through its u16 tables and only draws the low bits when they matter; this
 restatement always uses the full 53 bits, so agreement pins the table shortcut too."""
 import numpy as np
@@ -41,8 +42,9 @@ def corrupt_reads(seqs, ts, f, cum_bq, phred, seed, unit_key):
   N = np.concatenate([np.arange(l) for l in lens]).astype(np.uint64)
   th, tl = T >> np.uint64(32), T & MASK
   fw = np.uint64(f << 16)
-  r = philox4x32_10(tl, th, fw | (N >> np.uint64(2)), np.full_like(T, c3), k0, k1)
-  w = np.choose((N & np.uint64(3)).astype(np.int64), r)
+  r = philox4x32_10(tl, th, fw | (N // np.uint64(3)), np.full_like(T, c3), k0, k1)
+  k = (N % np.uint64(3)).astype(np.int64)
+  w = np.choose(k, r[:3])
   lo = philox4x32_10(tl, th, fw | np.uint64(0x4000) | N, np.full_like(T, c3), k0, k1)
   l1 = ((lo[0] << np.uint64(5)) | (lo[1] >> np.uint64(27))).astype(np.float64)
   l2 = ((lo[2] << np.uint64(5)) | (lo[3] >> np.uint64(27))).astype(np.float64)
@@ -54,8 +56,12 @@ def corrupt_reads(seqs, ts, f, cum_bq, phred, seed, unit_key):
     sel = Ni == n
     bq[sel] = np.minimum(np.searchsorted(cum_bq[f, n], u1[sel], side='left'), 93)
   sub = u2 < np.asarray(phred)[bq]
-  c = philox4x32_10(tl, th, fw | np.uint64(0x8000) | (N >> np.uint64(2)), np.full_like(T, c3), k0, k1)
-  ch = ((np.choose((N & np.uint64(3)).astype(np.int64), c) * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
+  c10 = ((r[3] >> (np.uint64(10) * k.astype(np.uint64))) & np.uint64(1023)).astype(np.int64)
+  ch = c10 % 3
+  rej = np.nonzero(sub & (c10 == 1023))[0]
+  if len(rej):
+    c = philox4x32_10(tl[rej], th[rej], fw | np.uint64(0x8000) | N[rej], np.full(len(rej), c3, np.uint64), k0, k1)
+    ch[rej] = ((c[0] * np.uint64(3)) >> np.uint64(32)).astype(np.int64)
   base = np.frombuffer(b''.join(seqs), np.uint8).copy()
   for i in np.nonzero(sub)[0]:
     base[i] = ROT.get(int(base[i]), b'NNN')[ch[i]]
