@@ -1149,7 +1149,6 @@ struct CiArgs {
   char *arena[2];         // the emission's first byte per file
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
-  int32_t dbg;            // timing experiments (MH_CR_DBG): 1 no exact loop, 2 no substitution loop, 4 no walk
   CorruptCfg cc;
 };
 
@@ -1173,7 +1172,7 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
 
 template <bool LDS_TAB>
 __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
-  // LDS: bucket entries [2][rlen][CB_ROW] | Fp16[100] | low threshold bytes T16 & 0xff [2][rlen][n_bq]
+  // LDS: bucket entries [2][rlen][CB_ROW] | Fp16[100] | low-byte pairs of the thresholds [2][rlen][n_bq] (u16)
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
   const CorruptCfg &cc = A.cc;
   const int rlen = A.rlen, n_bq = cc.n_bq;
@@ -1186,8 +1185,13 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
       const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
       uint4 *dst = (uint4 *)(ctab + f * row_bytes);
       for (int i = threadIdx.x; i < row_bytes / 16; i += CI_THREADS) dst[i] = src[i];
+      // per entry j: its low byte | (entry j + 1's low byte when j + 1 < min(n_bq, 93) lies in j's bucket, else 0xff) << 8
       const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
-      for (int i = threadIdx.x; i < rlen * n_bq; i += CI_THREADS) ctab[o_t8 + f * rlen * n_bq + i] = (uint8_t)t16[i];
+      for (int i = threadIdx.x; i < rlen * n_bq; i += CI_THREADS) {
+        const int j = i % n_bq;
+        const uint32_t a = t16[i], b = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
+        ((uint16_t *)(ctab + o_t8))[f * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
+      }
     }
     for (int i = threadIdx.x; i < 100; i += CI_THREADS) ((uint16_t *)fp16)[i] = cc.Fp16[i];
     __syncthreads();
@@ -1195,32 +1199,35 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
   // the BQ step of base n of file f for the draw's high 16 bits: entries below h1 (capped at 93), amb when one
   // equals h1.  LDS: the bucket entry; a flagged bucket walks the row's low threshold bytes up to the next bucket's
   // count.  Global: bq_walk_g.
+  const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
   auto walk = [&](int f, int n, uint32_t h1, bool *amb) -> uint32_t {
     if (!LDS_TAB) return bq_walk_g(cc, f, n, h1, amb);
     const int row = f * rlen + n;
     const int kb = (int)(h1 >> 8);
     const uint32_t e = ctab[row * CB_ROW + kb];
     const uint32_t c = e & 0x7fu;
-    // the bucket's first two low bytes, read for every lane (no branch; past the row's end they are masked by lim)
-    const uint8_t *t8 = ctab + o_t8 + row * n_bq;
-    const uint32_t v0 = t8[c], v1 = t8[c + 1];
-    const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
+    // the low bytes of entry c and, when it lies in the same bucket, of entry c + 1 (else 0xff), one LDS read
+    const uint32_t pr = t8p[row * n_bq + c];
     const uint32_t lo = h1 & 0xffu;
-    if (!(e & 0x80u) || (A.dbg & 4)) {
+    if (!(e & 0x80u)) {
       *amb = false;
       return c;
     }
-    // flagged: c < lim
-    const bool b0 = v0 < lo, b1 = b0 && c + 1 < lim && v1 < lo;
+    // flagged: entry c lies in the bucket.  A 0xff stand-in for entry c + 1 never counts as below, and makes amb
+    // conservative when lo = 255 (the exact path then decides, with the same result).
+    const uint32_t v0 = pr & 0xffu, v1 = pr >> 8;
+    const bool b0 = v0 < lo, b1 = b0 && v1 < lo;
     if (!b1) {
-      *amb = b0 ? (c + 1 < lim && v1 == lo) : v0 == lo;
+      *amb = b0 ? v1 == lo : v0 == lo;
       return c + (uint32_t)b0;
     }
-    uint32_t bq = c + 2;   // rare: two or more entries of the bucket below h1
-    uint32_t v = bq < lim ? t8[bq] : 0x100u;
+    // rare: two or more entries of the bucket below h1
+    const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
+    uint32_t bq = c + 2;
+    uint32_t v = bq < lim ? (t8p[row * n_bq + bq] & 0xffu) : 0x100u;
     while (v < lo) {
       bq++;
-      v = bq < lim ? t8[bq] : 0x100u;
+      v = bq < lim ? (t8p[row * n_bq + bq] & 0xffu) : 0x100u;
     }
     *amb = v == lo;
     return bq;
@@ -1292,8 +1299,6 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
           if (j < cnt) qb[j] = (char)(qd[j >> 2] >> (8 * (j & 3)));
       }
       if (n0 + cnt == (int)S) qual[S] = '\n';
-      if (A.dbg & 1) px = 0;
-      if (A.dbg & 2) ps = pc = 0;
       // rare: the full 53-bit decisions (the choice bits come from the same triple draw)
       while (px) {
         const int j = __builtin_ctz(px);
@@ -1351,15 +1356,14 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (ncu <= 0) ncu = 256;
-  const size_t lds = (size_t)2 * rlen * (CB_ROW + cc.n_bq) + 256 + 16;   // (+16: the walk's speculative reads)
+  const size_t lds = (size_t)2 * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads entry c <= n_bq)
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
   const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
   if (grid < 1) grid = 1;
-  static const int32_t dbg = getenv("MH_CR_DBG") ? atoi(getenv("MH_CR_DBG")) : 0;
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, dbg, cc};
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
   hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
   HIPCHK(ctx, hipGetLastError());
