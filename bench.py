@@ -88,6 +88,22 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=True):
           'avg_launch_ms': ew_ms / max(ew_n, 1)}, stage_ms
 
 
+def corrupt_roofline(stages, kept, b1, b2, rlen):
+  """The corruption pass (k_cr_recs + k_cr_inplace, stage 'emit_corrupt' timed by HIP events on the writer stream).
+  Algorithmic bytes: per base one read (the block's bases) and one quality written, the substituted bases written
+  back (4.7 % of the bases under hiseq-X-v2.5-Garvan), 8 bytes of record word read and one '\n' per record; it is
+  bound by VALU issue (Philox rounds and the table walk: profiles/pmc_k_cr_inplace_r02.json), not by HBM."""
+  ms = sum(v for k, v in stages if k == 'emit_corrupt')
+  n = sum(1 for k, _ in stages if k == 'emit_corrupt')
+  bases = 2 * rlen * kept   # (upper bound: reads cut by the haplotype end are shorter)
+  alg = bases * (2 + 0.047) + 2 * kept * 9
+  gbs = alg / (ms * 1e-3) / 1e9 if ms > 0 else None
+  return {'kernel': 'k_cr_inplace', 'bound': 'valu', 'avg_launch_ms': ms / max(n, 1),
+          'algorithmic_bytes_per_launch': alg / max(n, 1), 'achieved_gbs': gbs,
+          'hbm_frac': gbs / PEAK_HBM_GBS if gbs else None,
+          'bases_per_s': bases / (ms * 1e-3) if ms > 0 else None}
+
+
 def timed(step, steps, warmup, eng, dist):
   def barrier():
     if dist is not None:
@@ -170,6 +186,9 @@ def run_chr1(a):
   roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps)
   if a.stages:
     print(json.dumps(stage_ms), file=sys.stderr)
+  corrupt_pass = None
+  if a.corrupt:
+    corrupt_pass = corrupt_roofline(stages, kept, b1, b2, rlen)
 
   e2e = None
   if not a.no_e2e and not a.corrupt and a.rng == 'mitty':
@@ -199,6 +218,7 @@ def run_chr1(a):
                'read_model': a.model, 'coverage': a.coverage, 'contig_bp': a.length, 'units': len(units),
                'templates_per_step': kept // a.steps, 'parallelism': 'single GPU'},
     'roofline': roof,
+    'corrupt_pass': corrupt_pass,
     'cpu_baseline': cpu,
     'end_to_end': e2e,
     'stage_ms': stage_ms,
