@@ -54,6 +54,9 @@ def parse():
   ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end (files in, /dev/null out) leg')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
   ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
+  ap.add_argument('--sync-emit', action='store_true',
+                  help='chr1: the synchronous emission path (measure on the main stream, host readback) instead of '
+                       'the pipelined one (mh_emit_async)')
   ap.add_argument('--genome-scale', type=float, default=1.0,
                   help='N > 1: contig lengths scaled by this (rehearsals of the plan on one GPU; 1 = GRCh37)')
   return ap.parse_args()
@@ -110,20 +113,21 @@ def timed(step, steps, warmup, eng, dist):
       dist.barrier()
 
   for _ in range(warmup):
-    step()
+    step()()
   eng.ctx.enable_timing(True)
   barrier()
   eng.ctx.sync()
   t0 = time.perf_counter()
-  kept = b1 = b2 = 0
-  for _ in range(steps):
-    k, x1, x2 = step()
-    kept += k
-    b1 += x1
-    b2 += x2
+  done = [step() for _ in range(steps)]   # each step's counts: read once its units have landed
   eng.ctx.sync()
   barrier()
   dt = time.perf_counter() - t0
+  kept = b1 = b2 = 0
+  for get in done:
+    k, x1, x2 = get()
+    kept += k
+    b1 += x1
+    b2 += x2
   stages = eng.ctx.stage_times()
   eng.ctx.enable_timing(False)
   return dt, kept, b1, b2, stages
@@ -177,9 +181,13 @@ def run_chr1(a):
     # job's last FASTQ writers drain); the timed region ends with a full synchronisation
     eng.drop_haplotypes()
     eng.ctx.reset_output()
-    res = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p, rlen,
-                        model['cum_tlen'], 'SYN', 0, True, a.rng)
-    return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
+    pend = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
+                         rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=not a.sync_emit)
+
+    def get():
+      res = pend.resolve() if hasattr(pend, 'resolve') else pend
+      return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
+    return get
 
   dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
   eng.close()
@@ -311,7 +319,7 @@ def run_genome(a, rank, world, local, dist):
         batch, draws = [], 0
     counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
     dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)
-    return kept, b1, b2
+    return lambda: (kept, b1, b2)
 
   steps, warmup = a.steps, a.warmup
   dt, kept, b1, b2, stages = timed(step, steps, warmup, eng, dist)

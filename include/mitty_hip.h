@@ -84,6 +84,11 @@ int32_t mh_upload_variants(mh_ctx *ctx, int32_t vset, const int64_t *v_pos, cons
                            const char *alt_pool, int64_t alt_pool_len, int64_t n_var);
 int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, int32_t vset,
                                 int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max);
+/* Several mh_build_haplotype_vset calls at once: slots[i] from contig contig_ids[i] at ref_starts[i] with resident
+ * variant set vsets[i]; two copies are spliced side by side (second stream, second host thread).  Outputs per slot. */
+int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
+                                 const int64_t *ref_starts, const int32_t *vsets, int64_t *out_n_nodes,
+                                 int64_t *out_p_min, int64_t *out_p_max);
 int32_t mh_release_variants(mh_ctx *ctx, int32_t vset);
 /* Copy a slot's node list back (arrays sized n_nodes; seq bytes of node k = hap[ps[k]-p_min .. +oplen) for
  * non-'D' nodes).  Any pointer may be NULL. */
@@ -143,6 +148,18 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2);
+/* mh_emit_reads without a host round trip (the engine's pipelined path; same bytes, readgenerate.py:184-230): the
+ * unit's measure pass, record offsets, writer and corruption are queued on the writer stream and the call returns a
+ * ticket at once.  The unit lands in the arenas after the units queued before it (its base offsets come from the
+ * device); room is reserved from mh_haplotype_read_bound.  mh_emit_result waits for the ticket's unit and returns its
+ * kept count, bytes and base offsets per file (256 tickets in flight; read a ticket before it comes round again). */
+int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                      int32_t write_fastq2, uint64_t unit_key, int32_t *out_ticket);
+int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2,
+                       int64_t *out_base1, int64_t *out_base2);
+/* An upper bound on the qname part of one read of length rlen from the haplotype in `slot` ('|' strand '|' POS '|'
+ * rlen '|' CIGAR '|' v-list, readgenerate.py:223-225): the priciest window of nodes a read can span (rpc.py:119-160). */
+int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t *out_bytes);
 /* Templates in [t_begin, t_end) of the current set that survive the N filter (readgenerate.py:201-204). */
 int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end, int64_t *out_kept);
 int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);

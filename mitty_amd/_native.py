@@ -16,9 +16,9 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
-           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_release_variants', 'mh_get_nodes',
+           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
@@ -78,6 +78,10 @@ def lib():
   _sig(L, 'mh_get_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_emit_prepare', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_build_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_emit_async', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_emit_result', [c_vp, c_i32, P_i64, P_i64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_haplotype_read_bound', [c_vp, c_i32, c_i32, ctypes.POINTER(c_i32)])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
@@ -379,6 +383,16 @@ class Context:
                                               ctypes.byref(nn), ctypes.byref(pmin), ctypes.byref(pmax)))
     return nn.value, pmin.value, pmax.value
 
+  def build_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+    """Several resident-variant haplotypes at once (two side by side); [(n_nodes, p_min, p_max)] per slot."""
+    n = len(slots)
+    a = lambda xs, t: np.ascontiguousarray(np.asarray(xs, dtype=t))
+    s, c, r, v = a(slots, np.int32), a(contig_ids, np.int32), a(ref_starts, np.int64), a(vsets, np.int32)
+    nn, pmin, pmax = (np.zeros(max(n, 1), np.int64) for _ in range(3))
+    self._chk(self._L.mh_build_haplotypes_vset(self._h, n, _ptr(s), _ptr(c), _ptr(r), _ptr(v), _ptr(nn), _ptr(pmin),
+                                               _ptr(pmax)))
+    return [(int(nn[i]), int(pmin[i]), int(pmax[i])) for i in range(n)]
+
   def release_variants(self, vset):
     self._chk(self._L.mh_release_variants(self._h, int(vset)))
 
@@ -457,6 +471,25 @@ class Context:
     return fo0[:m], p0[:m], p1[:m]
 
   # ---- emission ----------------------------------------------------------------------------------------
+  def emit_async(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+    """Queue one unit's emission (measure, offsets, writer, corruption) on the writer stream; returns a ticket for
+    emit_result."""
+    t = c_i32()
+    self._chk(self._L.mh_emit_async(self._h, int(slot), serial_stub.encode(), chrom.encode(), int(cpy),
+                                    1 if write_fastq2 else 0, int(unit_key), ctypes.byref(t)))
+    return t.value
+
+  def emit_result(self, ticket):
+    """(kept, bytes1, bytes2, base1, base2) of an emit_async ticket (waits for its unit)."""
+    r = [c_i64() for _ in range(5)]
+    self._chk(self._L.mh_emit_result(self._h, int(ticket), *[ctypes.byref(x) for x in r]))
+    return tuple(x.value for x in r)
+
+  def read_bound(self, slot, rlen):
+    out = c_i32()
+    self._chk(self._L.mh_haplotype_read_bound(self._h, int(slot), int(rlen), ctypes.byref(out)))
+    return out.value
+
   def emit_prepare(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, wait=True):
     """The measure pass and record offsets of the current templates (the next emit_reads of the same unit only
     queues the writer).  Returns (kept, bytes1, bytes2); with wait=False it returns None at once, without waiting

@@ -2,6 +2,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
+#include <thread>
 
 #include "mh_bgzf.h"
 #include <vector>
@@ -14,8 +16,11 @@ namespace jump {
 void window_at(uint32_t seed, uint64_t J, uint32_t *out624);
 }
 
+static std::mutex g_err_mu;   // the splice's second lane (a host thread) may report an error beside the first
+
 int32_t hip_fail(mh_ctx *ctx, hipError_t e, const char *what, const char *file, int line) {
   if (ctx) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
     ctx->err = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") in " + what + " at " +
                file + ":" + std::to_string(line);
   }
@@ -23,7 +28,10 @@ int32_t hip_fail(mh_ctx *ctx, hipError_t e, const char *what, const char *file, 
 }
 
 int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg) {
-  if (ctx) ctx->err = msg;
+  if (ctx) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    ctx->err = msg;
+  }
   return code;
 }
 
@@ -84,6 +92,12 @@ int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set) {
 int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set) {
   if (set) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
   return MH_OK;
+}
+
+int64_t *pinned_small(mh_ctx *ctx) {
+  if (!ctx->h_small && hipHostMalloc((void **)&ctx->h_small, 4096, hipHostMallocDefault) != hipSuccess)
+    ctx->h_small = nullptr;
+  return ctx->h_small;
 }
 
 int32_t join_writer(mh_ctx *ctx) {
@@ -245,8 +259,14 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
+  release(ctx->d_used); release(ctx->scan_partials_w); release(ctx->rb_tmp);
+  for (auto &b : ctx->sl2) release(b);
+  for (auto &e : ctx->res_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+  if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   for (auto &e : ctx->eset) {
-    release(e.recs); release(e.off); release(e.slots); release(e.stat);
+    release(e.recs); release(e.off); release(e.slots); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
     if (e.rb) (void)hipEventDestroy(e.rb);
     if (e.h_stat) (void)hipHostFree(e.h_stat);
@@ -325,12 +345,10 @@ int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_
   return MH_OK;
 }
 
-static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, const VarSet &v,
-                          int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
-  auto it = ctx->contigs.find(contig_id);
-  if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
-  // reuse the oldest released haplotype's buffers unless a queued writer still reads them (then allocate: the pool
-  // grows to the two generations a pipelined job needs)
+// the slot's Hap for a (re)build: the oldest released haplotype's buffers unless a queued writer still reads them
+// (then fresh ones: the pool grows to the generations a pipelined job needs); the main stream waits for the slot's
+// last writer
+static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, Hap **out) {
   const bool spare_ready = !ctx->hap_spare.empty() &&
                            (!ctx->hap_spare.front().used_set || hipEventQuery(ctx->hap_spare.front().used) == hipSuccess);
   if (!ctx->haps.count(slot) && spare_ready) {
@@ -345,6 +363,18 @@ static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t 
   Hap &h = ctx->haps[slot];
   MH_TRY(wait_unused(ctx, h.used, h.used_set));   // a queued writer may still read the old bytes
   h.valid = false;
+  h.rb_rlen = h.rb_bytes = 0;
+  *out = &h;
+  return MH_OK;
+}
+
+static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t ref_start_pos, const VarSet &v,
+                          int64_t *out_n_nodes, int64_t *out_p_min, int64_t *out_p_max) {
+  auto it = ctx->contigs.find(contig_id);
+  if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+  Hap *hp = nullptr;
+  MH_TRY(hap_for_build(ctx, slot, &hp));
+  Hap &h = *hp;
   MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v));
   if (out_n_nodes) *out_n_nodes = h.n_nodes;
   if (out_p_min) *out_p_min = h.p_min;
@@ -389,6 +419,54 @@ int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, in
   return build_from(ctx, slot, contig_id, ref_start_pos, it->second, out_n_nodes, out_p_min, out_p_max);
 }
 
+int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
+                                 const int64_t *ref_starts, const int32_t *vsets, int64_t *out_n_nodes,
+                                 int64_t *out_p_min, int64_t *out_p_max) {
+  CTX_GUARD_NOJOIN(ctx);
+  if (n < 0 || (n > 0 && (!slots || !contig_ids || !ref_starts || !vsets))) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  for (int32_t i = 0; i < n; i++) {
+    if (!ctx->contigs.count(contig_ids[i])) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+    if (vsets[i] < 0 || !ctx->vsets.count(vsets[i])) return arg_fail(ctx, MH_E_STATE, "unknown variant set id");
+    for (int32_t j = 0; j < i; j++)
+      if (slots[j] == slots[i]) return arg_fail(ctx, MH_E_ARG, "a slot appears twice");
+  }
+  if (!pinned_small(ctx)) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  for (int32_t i0 = 0; i0 < n; i0 += 2) {   // two copies at a time: the second on its own stream and host thread
+    const int32_t k = n - i0 < 2 ? n - i0 : 2;
+    Hap *hp[2] = {nullptr, nullptr};
+    for (int32_t j = 0; j < k; j++) MH_TRY(hap_for_build(ctx, slots[i0 + j], &hp[j]));
+    if (k == 1) {
+      MH_TRY(splice_build(ctx, *hp[0], ctx->contigs[contig_ids[i0]], ref_starts[i0], ctx->vsets[vsets[i0]]));
+    } else {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));   // lane 1 after everything the main stream waits for
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+      const Contig &c1 = ctx->contigs[contig_ids[i0 + 1]];
+      const VarSet &v1 = ctx->vsets[vsets[i0 + 1]];
+      int32_t rc1 = MH_OK;
+      std::thread t1([&]() {
+        if (hipSetDevice(ctx->device) != hipSuccess) {
+          rc1 = MH_E_HIP;
+          return;
+        }
+        rc1 = splice_build(ctx, *hp[1], c1, ref_starts[i0 + 1], v1, 1);
+      });
+      const int32_t rc0 = splice_build(ctx, *hp[0], ctx->contigs[contig_ids[i0]], ref_starts[i0],
+                                       ctx->vsets[vsets[i0]]);
+      t1.join();
+      HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+      if (rc0 != MH_OK) return rc0;
+      if (rc1 != MH_OK) return rc1;
+    }
+    for (int32_t j = 0; j < k; j++) {
+      if (out_n_nodes) out_n_nodes[i0 + j] = hp[j]->n_nodes;
+      if (out_p_min) out_p_min[i0 + j] = hp[j]->p_min;
+      if (out_p_max) out_p_max[i0 + j] = hp[j]->p_max;
+    }
+  }
+  return MH_OK;
+}
+
 int32_t mh_release_variants(mh_ctx *ctx, int32_t vset) {
   CTX_GUARD(ctx);
   auto it = ctx->vsets.find(vset);
@@ -429,7 +507,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
   // keep the buffers for the next build (stream order protects them: every later user is on ctx->stream)
-  constexpr size_t SPARE_MAX = 4;
+  constexpr size_t SPARE_MAX = 8;   // three generations of a pipelined job's haplotypes (asynchronous emission)
   if (ctx->hap_spare.size() < SPARE_MAX) {
     h.valid = false;
     ctx->hap_spare.push_back(h);
@@ -637,7 +715,8 @@ int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end,
 }
 
 int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
-  if (!ctx) return MH_E_ARG;
+  CTX_GUARD_NOJOIN(ctx);
+  MH_TRY(sync_async_fill(ctx));
   if (b1) *b1 = ctx->used1;
   if (b2) *b2 = ctx->used2;
   return MH_OK;
@@ -645,6 +724,7 @@ int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
 
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2, int64_t len2) {
   CTX_GUARD(ctx);
+  MH_TRY(sync_async_fill(ctx));
   if ((fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
@@ -655,8 +735,37 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
 }
 
 int32_t mh_output_reset(mh_ctx *ctx) {
-  if (!ctx) return MH_E_ARG;
-  ctx->used1 = ctx->used2 = 0;
+  CTX_GUARD_NOJOIN(ctx);
+  return output_reset(ctx);
+}
+
+int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t *out_bytes) {
+  CTX_GUARD_NOJOIN(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (rlen <= 0 || !out_bytes) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return read_part_bound(ctx, it->second, rlen, out_bytes);
+}
+
+int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                      int32_t write_fastq2, uint64_t unit_key, int32_t *ticket) {
+  CTX_GUARD_NOJOIN(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!serial_stub || !chrom || !ticket) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return emit_async(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, ticket);
+}
+
+int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2,
+                       int64_t *out_base1, int64_t *out_base2) {
+  CTX_GUARD_NOJOIN(ctx);
+  int64_t r[5];
+  MH_TRY(emit_result(ctx, ticket, r));
+  if (out_kept) *out_kept = r[0];
+  if (out_b1) *out_b1 = r[1];
+  if (out_b2) *out_b2 = r[2];
+  if (out_base1) *out_base1 = r[3];
+  if (out_base2) *out_base2 = r[4];
   return MH_OK;
 }
 
@@ -878,6 +987,7 @@ int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char 
 
 int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates) {
   CTX_GUARD(ctx);
+  MH_TRY(sync_async_fill(ctx));
   if (!templates) return arg_fail(ctx, MH_E_ARG, "null argument");
   int64_t u1 = 0, u2 = 0;
   const bool two = ctx->used2 > 0;
@@ -921,6 +1031,7 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
 int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
                          int64_t *used1, int64_t *used2, int64_t *templates) {
   CTX_GUARD(ctx);
+  MH_TRY(sync_async_fill(ctx));
   if (!fq1 || len1 < 0 || (fq2 && len2 < 0) || t_base < 0 || !used1 || !used2 || !templates)
     return arg_fail(ctx, MH_E_ARG, "null argument");
   MH_TRY(stage_in(ctx, ctx->bam.in1, fq1, len1));

@@ -810,6 +810,7 @@ struct EdArgs {
   const uint8_t *slots;
   char *arena[2];
   int64_t used[2];
+  const int64_t *d_base;   // asynchronous emission: the arena offsets from the device (else used[])
   int32_t rlen, win_stride, head, qstride;
   int32_t dbg;
 };
@@ -861,7 +862,8 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
   const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
   // arena offsets of the tile's first byte per file; the arenas are 256-byte aligned, so offset & 15 is the
   // address alignment
-  const int64_t gbase[2] = {A.used[0] + base.b1, A.used[1] + base.b2};
+  const int64_t gbase[2] = {(A.d_base ? A.d_base[0] : A.used[0]) + base.b1,
+                            (A.d_base ? A.d_base[1] : A.used[1]) + base.b2};
 
   // ---- owner lanes: metadata and the qname head ('@stub:' cnt '|chrom|cpy', right-aligned before the slot
   // area of the template's qname buffer); T ------------------------------------------------------------------------
@@ -1146,7 +1148,8 @@ struct CiArgs {
   const int8_t *fo0;
   const Rec *recs;
   const E3 *off;
-  char *arena[2];         // the emission's first byte per file
+  char *arena[2];         // the emission's first byte per file (asynchronous: the arena start, plus d_base)
+  const int64_t *d_base;  // asynchronous emission: the emission's arena offsets from the device (else null)
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
   CorruptCfg cc;
@@ -1165,7 +1168,8 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
     if (a > A.hap_len) a = A.hap_len;
     const uint32_t S = rc.x && e > a ? (uint32_t)(e - a) : 0u;
     // '@stub:' cnt '|chrom|cpy' reads-part '\n' | bases | '\n+\n' | qualities | '\n'
-    const uint64_t so = (uint64_t)((f ? o.b2 : o.b1) + A.lh0 + ndig_u((uint64_t)(o.kept + 1)) + rc.w + 1);
+    const uint64_t so = (uint64_t)((A.d_base ? A.d_base[f] : 0) + (f ? o.b2 : o.b1) + A.lh0 +
+                                   ndig_u((uint64_t)(o.kept + 1)) + rc.w + 1);
     crec[t * A.nf + f] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | S);
   }
 }
@@ -1351,7 +1355,8 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
 // the corruption pass over one emission's records (on stream `st`, after its writer)
 int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_t m, const int64_t *pos0,
                           const int64_t *pos1, const int8_t *fo0, const Rec *recs, const E3 *off, uint2 *crec,
-                          char *o1, char *o2, int32_t nf, int32_t lh0, int32_t rlen, const CorruptCfg &cc) {
+                          char *o1, char *o2, int32_t nf, int32_t lh0, int32_t rlen, const CorruptCfg &cc,
+                          const int64_t *d_base = nullptr) {
   if (m <= 0) return MH_OK;
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1363,7 +1368,7 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
   if (grid < 1) grid = 1;
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, cc};
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
   hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
   HIPCHK(ctx, hipGetLastError());
@@ -1446,6 +1451,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
   const TplSet &tp = tit->second;
   hipStream_t st = ctx->stream;
+  if (!prepare_only) MH_TRY(sync_async_fill(ctx));   // the arena fill of queued asynchronous units
   if (t_end < 0 || t_end > tp.n) t_end = tp.n;
   if (t_begin > t_end) t_begin = t_end;
   const int64_t m = t_end - t_begin;
@@ -1641,7 +1647,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
     const int64_t ntiles = (m + ED_T - 1) / ED_T;
-    EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, (int32_t)rlen, win_stride, head,
+    EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, nullptr, (int32_t)rlen, win_stride, head,
              qstride, edbg};
     auto kfn = use_slots
                    ? (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, false> : k_emit_direct<1, 8, true, false>)
@@ -1690,6 +1696,298 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   *out_kept = ht.kept;
   *out_b1 = ht.b1;
   *out_b2 = write_fastq2 ? ht.b2 : 0;
+  return MH_OK;
+}
+
+// ---- asynchronous emission ------------------------------------------------------------------------------------
+// mh_emit_async queues a unit's measure pass, record offsets, writer (and corruption) on the writer stream and
+// returns at once: no host round trip separates sampling, measuring and writing.  Two things the synchronous path
+// reads back before queuing the writer come from elsewhere:
+//   * where the unit lands in the arenas: k_emit_advance takes the device-side fill (d_used) as the unit's base and
+//     adds the unit's totals, in stream order; the writer and the corruption pass read the base from the device;
+//   * how much room to reserve and the writer's per-template qname buffer: read_part_bound, an upper bound on one
+//     read's qname part (the longest window of the haplotype's nodes that a read can span, priced at its CIGAR and
+//     v-list digits), so a unit needs at most m * (head + cnt digits + 2 * bound + 1 + 2 * rlen + 5) bytes per file.
+// Results (kept, bytes, bases) come back through a pinned slot per ticket (mh_emit_result).
+static int ndig_host(int64_t v) {
+  int d = 1;
+  for (; v >= 10; v /= 10) d++;
+  return d;
+}
+
+struct LoadNodeCost {   // CIGAR entry (count <= max(oplen, rlen), op) + v-list entry (value, comma) of node k
+  const Node16 *nd;
+  int64_t rlen;
+  __device__ int64_t operator()(int64_t k) const {
+    const Node16 n = nd[k];
+    const int64_t ol = n.oplen();
+    int64_t c = ndig_u((uint64_t)(ol > rlen ? ol : rlen)) + 1;
+    if (n.code() != 0) c += ndig_s(node_v(n)) + 1;
+    return c;
+  }
+};
+struct StoreIncl {
+  int64_t *pre;
+  __device__ void operator()(int64_t k, int64_t incl, int64_t) const { pre[k] = incl; }
+};
+// the priciest window of nodes whose ps lie in [ps_k, ps_k + rlen - 1] (a read's nodes after its first one), and the
+// priciest single node (its first)
+__global__ void __launch_bounds__(256) k_window_cost(int64_t n, const Node16 *nd, const int64_t *pre, int64_t rlen,
+                                                     unsigned long long *mx) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int64_t lim = nd[k].ps() + rlen - 1;
+  int64_t lo = k, hi = n - 1;
+  while (lo < hi) {   // last node with ps <= lim (ps is non-decreasing)
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (nd[mid].ps() <= lim) lo = mid; else hi = mid - 1;
+  }
+  const int64_t before = k ? pre[k - 1] : 0;
+  atomicMax(mx, (unsigned long long)(pre[lo] - before));
+  atomicMax(mx + 1, (unsigned long long)(pre[k] - before));
+}
+
+int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out) {
+  if (h.rb_rlen == rlen && h.rb_bytes > 0) {
+    *out = h.rb_bytes;
+    return MH_OK;
+  }
+  hipStream_t st = ctx->stream;
+  int64_t nodes = 0;
+  unsigned long long mx[2] = {0, 0};
+  if (h.n_nodes > 0) {
+    MH_TRY(ensure(ctx, ctx->rb_tmp, 8 * (size_t)h.n_nodes + 64));
+    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(h.n_nodes)));
+    MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+    unsigned long long *dmx = (unsigned long long *)((char *)ctx->d_small.p + 96);
+    int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 112);
+    HIPCHK(ctx, hipMemsetAsync(dmx, 0, 16, st));
+    HIPCHK(ctx, device_scan_sum<int64_t>(st, h.n_nodes, LoadNodeCost{(const Node16 *)h.nd.p, rlen},
+                                         StoreIncl{(int64_t *)ctx->rb_tmp.p}, ctx->scan_partials.p, tot));
+    hipLaunchKernelGGL(k_window_cost, dim3(grid_for(h.n_nodes, 256, INT32_MAX)), dim3(256), 0, st, h.n_nodes,
+                       (const Node16 *)h.nd.p, (const int64_t *)ctx->rb_tmp.p, (int64_t)rlen, dmx);
+    HIPCHK(ctx, hipGetLastError());
+    int64_t *hs = pinned_small(ctx);
+    if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+    HIPCHK(ctx, hipMemcpyAsync(hs + 16, dmx, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    mx[0] = (unsigned long long)hs[16];
+    mx[1] = (unsigned long long)hs[17];
+    nodes = (int64_t)(mx[0] + mx[1]);
+  }
+  // '|' strand '|' POS (< 2^40: 13 digits) '|' rlen '|' ... '|' + the special CIGAR ('>' offset ':' rlen 'I')
+  const int64_t b = 8 + 20 + 2 * (int64_t)ndig_host(rlen) + 24 + nodes;
+  if (b > (1 << 20)) return arg_fail(ctx, MH_E_CAPACITY, "qname bound too large");
+  h.rb_rlen = rlen;
+  h.rb_bytes = (int32_t)b;
+  *out = (int32_t)b;
+  return MH_OK;
+}
+
+// the unit's base offsets and the device fill after it; its totals (off[m]: cnt digits included) copied to the result
+// words beside the bases
+__global__ void k_emit_advance(const E3 *off_m, int64_t *d_used, int64_t *stat, int32_t write2) {
+  const E3 t = *off_m;
+  stat[0] = t.kept;
+  stat[1] = t.b1;
+  stat[2] = write2 ? t.b2 : 0;
+  stat[6] = d_used[0];
+  stat[7] = d_used[1];
+  d_used[0] += t.b1;
+  if (write2) d_used[1] += t.b2;
+}
+__global__ void k_set_used(int64_t *d_used, int64_t u1, int64_t u2) {
+  d_used[0] = u1;
+  d_used[1] = u2;
+}
+
+int32_t sync_async_fill(mh_ctx *ctx) {
+  if (!ctx->async_pending) return MH_OK;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+  int64_t u[2] = {0, 0};
+  HIPCHK(ctx, hipMemcpy(u, ctx->d_used.p, 16, hipMemcpyDeviceToHost));
+  ctx->used1 = u[0];
+  ctx->used2 = u[1];
+  ctx->async_pending = false;
+  ctx->res1 = ctx->res2 = 0;
+  return MH_OK;
+}
+
+// mh_output_reset: the arenas empty again; with asynchronous units queued, the device fill restarts from zero in
+// stream order (after their writers)
+int32_t output_reset(mh_ctx *ctx) {
+  ctx->used1 = ctx->used2 = 0;
+  ctx->res1 = ctx->res2 = 0;
+  if (ctx->async_pending) {
+    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, (int64_t)0,
+                       (int64_t)0);
+    HIPCHK(ctx, hipGetLastError());
+  }
+  return MH_OK;
+}
+
+int32_t emit_result(mh_ctx *ctx, int32_t t, int64_t *out) {
+  if (t < 0 || t >= mh_ctx::RES_N || ctx->res_state[t] == 0) return arg_fail(ctx, MH_E_ARG, "unknown emission ticket");
+  if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
+  const int64_t *r = ctx->h_res + 8 * t;
+  out[0] = r[0];
+  out[1] = r[1];
+  out[2] = r[2];
+  out[3] = r[6];
+  out[4] = r[7];
+  return MH_OK;
+}
+
+int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                   int32_t write_fastq2, uint64_t unit_key, int32_t *ticket) {
+  *ticket = -1;
+  auto tit = ctx->tsets.find(ctx->cur_tpl);
+  if (tit == ctx->tsets.end() || !tit->second.valid)
+    return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
+  const TplSet &tp = tit->second;
+  for (auto &e : ctx->eset)
+    if (e.prepared) return arg_fail(ctx, MH_E_STATE, "emit the prepared units before asynchronous emission");
+  if (!ctx->h_res) {
+    HIPCHK(ctx, hipHostMalloc((void **)&ctx->h_res, 64 * (size_t)mh_ctx::RES_N, hipHostMallocDefault));
+    for (auto &e : ctx->res_ev) HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const int32_t t = ctx->res_next;
+  if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
+  ctx->res_next = (t + 1) % mh_ctx::RES_N;
+  int64_t *res = ctx->h_res + 8 * t;
+  const int64_t m = tp.n, rlen = tp.rlen;
+  std::string prefix = std::string("@") + serial_stub + ":";
+  std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
+  QHead qh{};
+  const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
+  const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
+  const int32_t head = (int32_t)(((prefix.size() + mid.size() + 10 + 16) + 15) / 16 * 16);
+  int32_t rb = 0;
+  bool direct = head_fits && !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS")) &&
+                win_stride <= 16 * 4 * ED_WMAX && m < (int64_t)UINT32_MAX && m > 0 && !getenv("MH_EMIT_SYNC") &&
+                !(getenv("MH_EMIT_SLOTS") && atoi(getenv("MH_EMIT_SLOTS")));
+  if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
+  const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
+  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32;
+  const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
+                       (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
+                       (size_t)2 * ED_T * 4 * 16 + 16;
+  if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
+    return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
+  if (!direct || lds_d > 64 * 1024) {
+    // the synchronous path (its base is the host fill once the queued units are accounted for)
+    MH_TRY(sync_async_fill(ctx));
+    const int64_t b1 = ctx->used1, b2 = ctx->used2;
+    int64_t k = 0, x1 = 0, x2 = 0;
+    MH_TRY(emit_reads(ctx, h, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, false, &k, &x1, &x2));
+    res[0] = k;
+    res[1] = x1;
+    res[2] = x2;
+    res[6] = b1;
+    res[7] = b2;
+    ctx->res_state[t] = 2;
+    *ticket = t;
+    return MH_OK;
+  }
+  std::string pm = prefix + mid;
+  std::memcpy(qh.w, pm.data(), pm.size());
+  qh.lp = (int32_t)prefix.size();
+  qh.lm = (int32_t)mid.size();
+
+  // room: an upper bound per file (qname line + bases + '\n+\n' + qualities + '\n')
+  const int64_t per_file = (int64_t)(prefix.size() + mid.size()) + ndig_host(m) + hslot_b + 2 * rlen + 5;
+  const int64_t U = m * per_file;
+  MH_TRY(ensure(ctx, ctx->d_used, 64));
+  if (!ctx->async_pending) {
+    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, ctx->used1,
+                       ctx->used2);
+    HIPCHK(ctx, hipGetLastError());
+    ctx->res1 = ctx->used1;
+    ctx->res2 = ctx->used2;
+    ctx->async_pending = true;
+  }
+  if ((int64_t)ctx->out1.cap < ctx->res1 + U + 64 || (write_fastq2 && (int64_t)ctx->out2.cap < ctx->res2 + U + 64)) {
+    // grow the arenas: everything queued lands first (a rare full synchronisation), then the fill restarts from the
+    // host's exact numbers.  The new size covers the reservations that were queued (a quarter more), so the next job
+    // of the same shape fits without another synchronisation.
+    const int64_t want1 = (ctx->res1 + U + 64) * 5 / 4, want2 = (ctx->res2 + U + 64) * 5 / 4;
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    MH_TRY(sync_async_fill(ctx));
+    MH_TRY(ensure_keep(ctx, ctx->out1, std::max(want1, ctx->used1 + U + 64), ctx->used1));
+    if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, std::max(want2, ctx->used2 + U + 64), ctx->used2));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, ctx->used1,
+                       ctx->used2);
+    HIPCHK(ctx, hipGetLastError());
+    ctx->res1 = ctx->used1;
+    ctx->res2 = ctx->used2;
+    ctx->async_pending = true;
+  }
+  ctx->res1 += U;
+  if (write_fastq2) ctx->res2 += U;
+
+  const int32_t set = ctx->eset_i;
+  ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
+  EmitSet &es = ctx->eset[set];
+  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
+  MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+  MH_TRY(ensure(ctx, es.stat, 64));
+  if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
+  MH_TRY(ensure(ctx, ctx->scan_partials_w, scan_lb_scratch_bytes<E3>(m + 1)));
+  char *stat = (char *)es.stat.p;
+  Rec *recs = (Rec *)es.recs.p;
+  E3 *off = (E3 *)es.off.p;
+  int64_t *d_base = (int64_t *)(stat + 48);
+  const int64_t *pos0 = (const int64_t *)tp.pos0.p, *pos1 = (const int64_t *)tp.pos1.p;
+  const int8_t *fo0 = (const int8_t *)tp.fo0.p;
+  HapView hv = view_of(h);
+  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
+  if (ctx->corrupt_on) cc = corrupt_cfg(ctx, unit_key, 0);
+
+  hipStream_t ws = ctx->wstream;
+  HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));   // the unit's templates (main stream) are ready
+  HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
+  ctx->stage_stream = ws;
+  stage_begin(ctx, "emit");
+  HIPCHK(ctx, hipMemsetAsync(stat, 0, 48, ws));
+  stage_begin(ctx, "emit_measure");
+  QFixed q{nullptr, nullptr, (int32_t)prefix.size(), (int32_t)mid.size()};
+  hipLaunchKernelGGL(k_emit_measure<false>, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, ws, hv, m, pos0, pos1,
+                     fo0, rlen, q, (int32_t)ctx->corrupt_on, recs, (int32_t *)(stat + 32), (uint8_t *)nullptr,
+                     (int32_t *)(stat + 40), 0);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  stage_begin(ctx, "emit_scan");
+  HIPCHK(ctx, device_scan_sum<E3>(ws, m + 1, LoadRec{recs, m}, StoreOff{off, 0}, ctx->scan_partials_w.p, (E3 *)stat));
+  hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (const E3 *)(off + m), (int64_t *)ctx->d_used.p,
+                     (int64_t *)stat, write_fastq2);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  stage_begin(ctx, "emit_write");
+  const int64_t ntiles = (m + ED_T - 1) / ED_T;
+  EdArgs A{hv, m, pos0, pos1, fo0, recs, off, nullptr, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0}, d_base,
+           (int32_t)rlen, win_stride, head, qstride, 0};
+  auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, true> : k_emit_direct<1, 8, true, true>)
+                             : (write_fastq2 ? k_emit_direct<2, 4, false, true> : k_emit_direct<1, 8, false, true>);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  if (ctx->corrupt_on)
+    MH_TRY(launch_cr_inplace(ctx, ws, hv, m, pos0, pos1, fo0, recs, off, (uint2 *)es.crrec.p, (char *)ctx->out1.p,
+                             (char *)ctx->out2.p, write_fastq2 ? 2 : 1, (int32_t)(prefix.size() + mid.size()),
+                             (int32_t)rlen, cc, d_base));
+  stage_end(ctx);   // "emit"
+  ctx->stage_stream = nullptr;
+  HIPCHK(ctx, hipMemcpyAsync(res, stat, 64, hipMemcpyDeviceToHost, ws));
+  HIPCHK(ctx, hipEventRecord(ctx->res_ev[t], ws));
+  ctx->res_state[t] = 1;
+  HIPCHK(ctx, hipEventRecord(es.done, ws));
+  HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ws));
+  MH_TRY(mark_used(ctx, h.used, h.used_set));
+  MH_TRY(mark_used(ctx, tp.used, tp.used_set));
+  es.busy = true;
+  ctx->writer_pending = true;
+  *ticket = t;
   return MH_OK;
 }
 

@@ -58,6 +58,7 @@ struct Hap {
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
+  int32_t rb_rlen = 0, rb_bytes = 0;   // read_part_bound's cache: the longest qname reads part of one read of rb_rlen
 };
 
 // One work unit's templates (illumina.generate_reads output), device-resident.
@@ -176,6 +177,7 @@ struct mh_ctx {
   mh::DevBuf scan_partials;
   mh::DevBuf lane2[8];   // the second lane's copies of s[4..10] and its radix-sort scratch (index 7)
   mh::DevBuf scan_partials2;
+  mh::DevBuf sl2[8];   // the splice's second lane: anchor, accepted, ref_before, node src, small, partials, N runs, sort
   mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
   mh::DevBuf d_small;        // device small scalars
 
@@ -202,6 +204,19 @@ struct mh_ctx {
   // FASTQ arenas
   mh::DevBuf out1, out2;
   int64_t used1 = 0, used2 = 0;
+  // asynchronous emission (mh_emit_async): measure, offsets, writer and corruption queued on the writer stream; the
+  // arena fill lives on the device (d_used) until a call needs it on the host (sync_async_fill)
+  mh::DevBuf d_used;                     // int64[2]
+  mh::DevBuf scan_partials_w;            // look-back scratch of the writer stream's scans
+  mh::DevBuf rb_tmp;                     // read_part_bound's prefix sums
+  bool async_pending = false;            // units queued asynchronously whose fill is not in used1 / used2 yet
+  int64_t res1 = 0, res2 = 0;            // arena bytes reserved by queued asynchronous units (upper bounds)
+  static constexpr int RES_N = 256;      // result slots (tickets) in flight
+  int64_t *h_res = nullptr;              // pinned [RES_N][8]: E3 totals, bases (words 6, 7)
+  hipEvent_t res_ev[RES_N] = {};
+  int8_t res_state[RES_N] = {};          // 0 free, 1 queued (event), 2 filled by the host (synchronous fallback)
+  int32_t res_next = 0;
+  int64_t *h_small = nullptr;            // pinned 4 KiB for small readbacks (no staged copy per value)
 
   // timing
   bool timing = false;
@@ -253,7 +268,8 @@ int32_t var_upload(mh_ctx *ctx, VarSet &v, const int64_t *v_pos, const uint8_t *
                    const int64_t *v_alt_off, const int64_t *v_alt_len, const char *alt_pool, int64_t alt_pool_len,
                    int64_t n_var);
 void release_vars(VarSet &v);
-int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const VarSet &v);
+// lane 0: ctx->stream and the shared scratch; lane 1: ctx->stream2 and sl2 (a second host thread)
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const VarSet &v, int lane = 0);
 
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
@@ -261,6 +277,13 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
 
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)
+int32_t sync_async_fill(mh_ctx *ctx);
+int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
+int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);
+int32_t output_reset(mh_ctx *ctx);
+int32_t emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out);   // kept, bytes1, bytes2, base1, base2
+int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                   int32_t write_fastq2, uint64_t unit_key, int32_t *ticket);
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                    bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);

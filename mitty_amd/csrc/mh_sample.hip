@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -1132,9 +1133,11 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
                          d_margin);
     }
     HIPCHK(ctx, hipGetLastError());
-    int32_t h_ntodo = -1;
-    HIPCHK(ctx, hipMemcpyAsync(&h_ntodo, cur, 4, hipMemcpyDeviceToHost, st));
+    int64_t *hs = pinned_small(ctx);
+    if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+    HIPCHK(ctx, hipMemcpyAsync(hs + 32, cur, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
+    const int32_t h_ntodo = (int32_t)(hs[32] & 0xffffffff);
     if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
                                           h_ntodo, (long long)C);
     if (getenv("MH_DEC_VERBOSE") && atoi(getenv("MH_DEC_VERBOSE")) >= 2 && h_ntodo > 0) {   // where they are
@@ -1436,10 +1439,21 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   }
   std::vector<int64_t> hm(n_units), hstat(n_units);
   std::vector<uint32_t> hflag(n_units);
-  HIPCHK(ctx, hipMemcpyAsync(hm.data(), d_m, 8 * n_units, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hstat.data(), d_status, 8 * n_units, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hflag.data(), d_flags, 4 * n_units, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  // d_m, d_status, d_flags are consecutive in s[1] (20 bytes per unit): one readback into pinned memory
+  int64_t *hs = pinned_small(ctx);
+  const size_t rb_bytes = 20 * (size_t)n_units;
+  if (hs && rb_bytes <= 3072) {
+    HIPCHK(ctx, hipMemcpyAsync(hs + 64, d_m, rb_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    std::memcpy(hm.data(), hs + 64, 8 * n_units);
+    std::memcpy(hstat.data(), hs + 64 + n_units, 8 * n_units);
+    std::memcpy(hflag.data(), hs + 64 + 2 * n_units, 4 * n_units);
+  } else {
+    HIPCHK(ctx, hipMemcpyAsync(hm.data(), d_m, 8 * n_units, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hstat.data(), d_status, 8 * n_units, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hflag.data(), d_flags, 4 * n_units, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+  }
 
   // ---- rare exact fix-ups: decode out of words (sequential stream), near-integer geometric quotients ------------
   for (int32_t u = 0; u < n_units; u++) {

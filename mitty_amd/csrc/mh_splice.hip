@@ -362,8 +362,24 @@ void release_vars(VarSet &v) {
   v.n = v.pool_len = 0;
 }
 
-int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const VarSet &v) {
-  hipStream_t st = ctx->stream;
+int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const VarSet &v, int lane) {
+  // lane 1 (mh_build_haplotypes_vset's second copy, on a host thread of its own): the second stream and its own
+  // scratch, no stage timing
+  const bool l1 = lane != 0;
+  hipStream_t st = l1 ? ctx->stream2 : ctx->stream;
+  DevBuf &b_anchor = l1 ? ctx->sl2[0] : ctx->s[6], &b_acc = l1 ? ctx->sl2[1] : ctx->s[7];
+  DevBuf &b_refb = l1 ? ctx->sl2[2] : ctx->s[8], &b_nsrc = l1 ? ctx->sl2[3] : ctx->s[9];
+  DevBuf &b_small = l1 ? ctx->sl2[4] : ctx->d_small, &b_part = l1 ? ctx->sl2[5] : ctx->scan_partials;
+  DevBuf &b_nrun = l1 ? ctx->sl2[6] : ctx->nrun_tmp, &b_perm = l1 ? ctx->sl2[7] : ctx->perm_tmp;
+  auto stage_begin = [&](mh_ctx *cx, const char *name) {
+    if (!l1) ::mh::stage_begin(cx, name);
+  };
+  auto stage_end = [&](mh_ctx *cx) {
+    if (!l1) ::mh::stage_end(cx);
+  };
+  int64_t *hs_base = pinned_small(ctx);
+  if (!hs_base) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  int64_t *const hs_lane = hs_base + (l1 ? 256 : 0);
   const int64_t n_var = v.n;
   const int64_t nv = n_var > 0 ? n_var : 1;
   const int64_t node_cap = 2 * n_var + 1;
@@ -374,15 +390,15 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   const uint8_t *d_op = (const uint8_t *)v.op.p, *d_pool = (const uint8_t *)v.pool.p;
 
   // --- scratch: anchor(6) accepted(7) ref_before(8) node src(9) small(d_small) -----------------------------
-  MH_TRY(ensure(ctx, ctx->s[6], nv));
-  MH_TRY(ensure(ctx, ctx->s[7], nv));
-  MH_TRY(ensure(ctx, ctx->s[8], 8 * nv));
-  MH_TRY(ensure(ctx, ctx->s[9], 8 * node_cap));
-  MH_TRY(ensure(ctx, ctx->d_small, 256));
-  MH_TRY(ensure(ctx, ctx->scan_partials, 32 * scan_partials_count(node_cap > nv ? node_cap : nv) + 64));
-  uint8_t *anchor = (uint8_t *)ctx->s[6].p, *accepted = (uint8_t *)ctx->s[7].p;
-  int64_t *ref_before = (int64_t *)ctx->s[8].p, *nsrc = (int64_t *)ctx->s[9].p;
-  char *small = (char *)ctx->d_small.p;
+  MH_TRY(ensure(ctx, b_anchor, nv));
+  MH_TRY(ensure(ctx, b_acc, nv));
+  MH_TRY(ensure(ctx, b_refb, 8 * nv));
+  MH_TRY(ensure(ctx, b_nsrc, 8 * node_cap));
+  MH_TRY(ensure(ctx, b_small, 256));
+  MH_TRY(ensure(ctx, b_part, 32 * scan_partials_count(node_cap > nv ? node_cap : nv) + 64));
+  uint8_t *anchor = (uint8_t *)b_anchor.p, *accepted = (uint8_t *)b_acc.p;
+  int64_t *ref_before = (int64_t *)b_refb.p, *nsrc = (int64_t *)b_nsrc.p;
+  char *small = (char *)b_small.p;
   int64_t *tot_i64 = (int64_t *)small;           // [0]
   NS *tot_ns = (NS *)(small + 16);                // [16..32)
   int32_t *err = (int32_t *)(small + 64);
@@ -401,24 +417,25 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   NS tot{0, 0};
   if (n_var > 0) {
     HIPCHK(ctx, device_scan<int64_t>(st, n_var, LoadEnd{d_pos, d_op, d_oplen}, StoreAnchor{d_pos, anchor, rs}, OpMax{},
-                                     INT64_MIN, (int64_t *)ctx->scan_partials.p, tot_i64));
+                                     INT64_MIN, (int64_t *)b_part.p, tot_i64));
     HIPCHK(ctx, hipMemsetAsync(accepted, 0, n_var, st));
     hipLaunchKernelGGL(k_resolve, dim3(grid_for(n_var, 256)), dim3(256), 0, st, n_var, d_pos, d_op, d_oplen, anchor,
                        accepted, rs);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, device_scan<int64_t>(st, n_var, LoadAccEnd{d_pos, d_op, d_oplen, accepted, rs},
                                      StoreRefBefore{ref_before, rs}, OpMax{}, INT64_MIN,
-                                     (int64_t *)ctx->scan_partials.p, tot_i64));
+                                     (int64_t *)b_part.p, tot_i64));
     HIPCHK(ctx, device_scan<NS>(st, n_var, LoadNS{d_pos, d_op, d_oplen, accepted, ref_before},
                                 StoreNodes{d_pos, d_op, d_oplen, accepted, ref_before, d_aoff, d_alen, keys, ps, pr, nl,
                                            nsrc, nop, rs, c.len, err},
-                                OpSum{}, NS{0, 0}, (NS *)ctx->scan_partials.p, tot_ns));
-    int64_t hb[2];
-    HIPCHK(ctx, hipMemcpyAsync(&final_ref, tot_i64, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(hb, tot_ns, 16, hipMemcpyDeviceToHost, st));
+                                OpSum{}, NS{0, 0}, (NS *)b_part.p, tot_ns));
+    // one readback into pinned memory: tot_i64 at small + 0, tot_ns at small + 16
+    int64_t *hs = hs_lane;
+    HIPCHK(ctx, hipMemcpyAsync(hs, small, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
+    final_ref = hs[0];
     if (final_ref < rs) final_ref = rs;
-    tot = NS{hb[0], hb[1]};
+    tot = NS{hs[2], hs[3]};
   }
   int64_t n_nodes = tot.nodes, samp_end = rs + tot.samp, hap_len = tot.samp;
   int64_t offset = final_ref - rs;
@@ -431,15 +448,16 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     hap_len += len;
   }
   // p_min / p_max (readgenerate.py:192): ps of the first node; ps + oplen of the last
-  int64_t ps0, psl, nll;
-  HIPCHK(ctx, hipMemcpyAsync(&ps0, ps, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(&psl, ps + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(&nll, nl + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
+  int64_t *hs = hs_lane;
+  HIPCHK(ctx, hipMemcpyAsync(hs + 8, ps, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 9, ps + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 10, nl + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
 
   // --- haplotype bytes ---------------------------------------------------------------------------------------
-  int32_t herr = 0;
-  HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 11, err, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  const int64_t ps0 = hs[8], psl = hs[9], nll = hs[10];
+  const int32_t herr = (int32_t)(hs[11] & 0xffffffff);
   if (herr) {
     stage_end(ctx);
     return arg_fail(ctx, MH_E_ARG, herr & 1 ? "variant beyond the end of the fetched reference region"
@@ -486,18 +504,20 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   // --- N runs: boundaries appended by k_nrun_find, then sorted ----------------------------------------------
   {
     unsigned long long *cnt = (unsigned long long *)(small + 128);
-    int64_t cap = std::max<int64_t>(4096, (int64_t)(h.nrun_s.cap / 8) - 1);
+    int64_t cap = std::max<int64_t>(4096, (int64_t)(h.nrun_s.cap / 8) - 1);   // (nrun scratch: b_nrun)
     unsigned long long hc[2] = {0, 0};
     for (int attempt = 0; attempt < 2; attempt++) {
-      MH_TRY(ensure(ctx, ctx->nrun_tmp, 16 * (size_t)cap + 64));
-      int64_t *us = (int64_t *)ctx->nrun_tmp.p, *ue = us + cap;
+      MH_TRY(ensure(ctx, b_nrun, 16 * (size_t)cap + 64));
+      int64_t *us = (int64_t *)b_nrun.p, *ue = us + cap;
       HIPCHK(ctx, hipMemsetAsync(cnt, 0, 16, st));
       const int64_t nel = hap_len / 64 + 1;
       hipLaunchKernelGGL(k_nrun_find, dim3(grid_for(nel, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)h.hap.p,
                          hap_len, cap, us, ue, cnt);
       HIPCHK(ctx, hipGetLastError());
-      HIPCHK(ctx, hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs + 12, cnt, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
+      hc[0] = (unsigned long long)hs[12];
+      hc[1] = (unsigned long long)hs[13];
       if ((int64_t)hc[0] <= cap && (int64_t)hc[1] <= cap) break;
       cap = (int64_t)std::max(hc[0], hc[1]);   // more boundaries than room: once more with room for all
     }
@@ -512,14 +532,14 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     if (nr > 0) {
       unsigned bits = 1;
       while (bits < 63 && ((int64_t)1 << bits) <= hap_len) bits++;
-      int64_t *us = (int64_t *)ctx->nrun_tmp.p, *ue = us + cap;
+      int64_t *us = (int64_t *)b_nrun.p, *ue = us + cap;
       size_t tmp = 0;
       HIPCHK(ctx, rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p, (size_t)nr, 0u,
                                            bits, st));
-      MH_TRY(ensure(ctx, ctx->perm_tmp, tmp + 256));
-      HIPCHK(ctx, rocprim::radix_sort_keys(ctx->perm_tmp.p, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p,
+      MH_TRY(ensure(ctx, b_perm, tmp + 256));
+      HIPCHK(ctx, rocprim::radix_sort_keys(b_perm.p, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p,
                                            (size_t)nr, 0u, bits, st));
-      HIPCHK(ctx, rocprim::radix_sort_keys(ctx->perm_tmp.p, tmp, (const uint64_t *)ue, (uint64_t *)h.nrun_e.p,
+      HIPCHK(ctx, rocprim::radix_sort_keys(b_perm.p, tmp, (const uint64_t *)ue, (uint64_t *)h.nrun_e.p,
                                            (size_t)nr, 0u, bits, st));
     }
   }

@@ -53,6 +53,18 @@ class Engine:
       self._haps[key] = (slot, n_nodes, p_min, p_max)
     return self._haps[key]
 
+  def haplotypes(self, keys):
+    """Build the haplotypes of several (ri, cpy) keys whose variants are resident (upload_variants), two copies at a
+    time side by side (mh_build_haplotypes_vset); keys already built are kept."""
+    todo = [k for k in dict.fromkeys(keys) if k not in self._haps and k in self._vsets]
+    if todo:
+      slots = [ri * self.SLOTS_PER_REGION + cpy for ri, cpy in todo]
+      res = self.ctx.build_haplotypes_vset(slots, [ri for ri, _ in todo],
+                                           [self._regions[ri][1] + 1 for ri, _ in todo],
+                                           [self._vsets[k] for k in todo])
+      for k, slot, r in zip(todo, slots, res):
+        self._haps[k] = (slot,) + tuple(r)
+
   def drop_variants(self):
     for vset in self._vsets.values():
       self.ctx.release_variants(vset)
@@ -64,19 +76,34 @@ class Engine:
     self._haps.clear()
 
   def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None):
+                on_unit=None, lazy=False):
     """Sample a batch of work units together, then emit them in order.
 
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
     unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
+    lazy: the pipelined path — every unit's emission is queued on the writer stream (mh_emit_async: no host round trip
+    between sampling, measuring and writing) and a PendingUnits comes back at once; its resolve() gives the list
+    (the units' bytes land in the arenas in unit order, as on the synchronous path).
     """
+    if not os.environ.get('MH_SPLICE_ONE_LANE'):
+      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    if lazy:
+      for s in set(slots):   # the qname bound for the writer's room, while the splice's results are fresh
+        self.ctx.read_bound(s, rlen)
     # template ids alternate between two ranges per batch, so this batch's sampling never waits for the previous
     # batch's FASTQ writers (still queued on their own stream) to finish reading theirs
     base = self._tpl_base
     self._tpl_base = self.TPL_BATCH - base
     ns = self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
                                RNG_MODES[rng])
+    if lazy and on_unit is None:
+      tickets = []
+      for k, (ps, ri, cpy, seed) in enumerate(units):
+        self.ctx.use_templates(base + k)
+        tickets.append(self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
+                                           self._regions[ri][0], cpy, write_fastq2, unit_key=seed))
+      return PendingUnits(self.ctx, [int(x) for x in ns], tickets)
     out = []
     # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
     # stream): the writers drain while the caller moves on to the next batch
@@ -100,3 +127,19 @@ class Engine:
     """One work unit: sample templates, emit FASTQ.  Returns (n_templates, kept, bytes1, bytes2)."""
     return self.run_units([(ps, ri, cpy, rng_seed)], lambda a, b: soa, p, rlen, cum_tlen, sample_name, worker_id,
                           write_fastq2, rng)[0]
+
+
+class PendingUnits:
+  """Emissions queued by Engine.run_units(lazy=True): resolve() waits for them and returns [(n, kept, b1, b2)]
+  (and keeps each unit's arena bases in .bases)."""
+
+  def __init__(self, ctx, ns, tickets):
+    self.ctx, self.ns, self.tickets = ctx, ns, tickets
+    self.result, self.bases = None, None
+
+  def resolve(self):
+    if self.result is None:
+      rs = [self.ctx.emit_result(t) for t in self.tickets]
+      self.result = [(n, r[0], r[1], r[2]) for n, r in zip(self.ns, rs)]
+      self.bases = [(r[3], r[4]) for r in rs]
+    return self.result

@@ -358,6 +358,49 @@ def test_resident_variants_and_buffer_reuse(native):
       G.check_same(d2, e2, 'fastq2 copy {}'.format(cpy))
 
 
+def test_two_lane_splice_matches_one_lane(native, monkeypatch):
+  """Both copies spliced side by side (mh_build_haplotypes_vset: second stream, second host thread, its own scratch)
+  give the nodes, haplotype bytes and FASTQ of one-at-a-time builds, over two contigs and a rebuild after a drop."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  seqs = [synth.contig(3_000_000, 51), synth.contig(2_000_000, 52)]
+  copies = [synth.copies_soa(synth.variants(sq, 53 + i)) for i, sq in enumerate(seqs)]
+  units = [(0, 0, 0, 61), (1, 0, 1, 62), (2, 1, 0, 63), (3, 1, 1, 64)]
+
+  def run(one_lane):
+    if one_lane:
+      monkeypatch.setenv('MH_SPLICE_ONE_LANE', '1')
+    else:
+      monkeypatch.delenv('MH_SPLICE_ONE_LANE', raising=False)
+    eng = Engine(0)
+    try:
+      for ri, sq in enumerate(seqs):
+        eng.load_region(ri, (str(ri + 1), 0, len(sq)), sq)
+        for cpy in (0, 1):
+          eng.upload_variants(ri, cpy, copies[ri][cpy])
+      out = []
+      for _ in range(2):
+        eng.drop_haplotypes()
+        eng.ctx.reset_output()
+        res = eng.run_units(units, lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'SYN')
+        nodes = [eng.ctx.get_nodes(*eng.haplotype(ri, cpy, None)[:2]) for ri in (0, 1) for cpy in (0, 1)]
+        out.append((res, nodes, eng.ctx.fetch_output()))
+      return out
+    finally:
+      eng.close()
+
+  a, b = run(True), run(False)
+  for (ra, na, (a1, a2)), (rb, nb, (b1, b2)) in zip(a, b):
+    assert ra == rb
+    for x, y in zip(na, nb):
+      for u, v in zip(x, y):
+        assert np.array_equal(np.asarray(u), np.asarray(v)) if not isinstance(u, bytes) else u == v
+    G.check_same(a1, b1, 'fastq1')
+    G.check_same(a2, b2, 'fastq2')
+
+
 def test_pipelined_jobs_match_isolated_runs(native):
   """Jobs queued back to back (the next job's haplotype rebuild and sampling run while the previous job's FASTQ
   writers are still queued, reusing released haplotype buffers) give the same bytes as each job run alone."""
@@ -702,6 +745,48 @@ def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, wri
     assert lc[3::4][:len(ts)] == want_q
     n_sub += sum(x != y for x, y in zip(la[1::4], want_s))
   assert n_sub > 100
+
+
+@pytest.mark.parametrize('corrupt,write2', [(False, True), (True, True), (False, False)])
+def test_async_emission_matches_sync(native, corrupt, write2):
+  """The pipelined path (Engine.run_units(lazy=True): mh_emit_async — measure, offsets, writer and corruption on the
+  writer stream, arena bases from the device) writes the synchronous path's bytes, over two consecutive jobs of three
+  units (two contigs with N runs, both copies), with the arena reset between them as the bench does, and reports the
+  same counts; a synchronous job afterwards appends where the asynchronous fill ended."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  seqs = [synth.contig(1_500_000, 41), synth.contig(900_000, 42)]
+  copies = [synth.copies_soa(synth.variants(sq, 43 + i)) for i, sq in enumerate(seqs)]
+  units = [(0, 0, 0, 501), (1, 0, 1, 502), (2, 1, 0, 503)]
+  outs = []
+  for lazy in (False, True):
+    eng = Engine(0)
+    try:
+      if corrupt:
+        eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 11)
+      for ri, sq in enumerate(seqs):
+        eng.load_region(ri, (str(ri + 1), 0, len(sq)), sq)
+      got = []
+      for job in range(2):
+        eng.drop_haplotypes()
+        eng.ctx.reset_output()
+        r = eng.run_units(units, lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'S', 0, write2, lazy=lazy)
+        r = r.resolve() if lazy else r
+        got.append((r, eng.ctx.fetch_output()))
+      # a synchronous job after the asynchronous ones appends at the device fill
+      r3 = eng.run_units(units[:1], lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'S', 0, write2)
+      got.append((r3, eng.ctx.fetch_output()))
+      outs.append(got)
+    finally:
+      eng.close()
+  for (rs, (a1, a2)), (ra, (b1, b2)) in zip(outs[0], outs[1]):
+    assert rs == ra
+    assert sum(x[1] for x in rs) > 10000
+    G.check_same(a1, b1, 'fastq1')
+    G.check_same(a2, b2, 'fastq2')
+  assert outs[0][0][1][0] == outs[0][1][1][0]   # the two jobs write the same bytes after the reset
 
 
 # ---- multi-GPU slices (SURVEY.md §8(e)) ---------------------------------------------------------------------------
