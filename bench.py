@@ -54,9 +54,10 @@ def parse():
   ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end (files in, /dev/null out) leg')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
   ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
-  ap.add_argument('--sync-emit', action='store_true',
-                  help='chr1: the synchronous emission path (measure on the main stream, host readback) instead of '
-                       'the pipelined one (mh_emit_async)')
+  ap.add_argument('--async-emit', action='store_true',
+                  help='chr1: the pipelined emission path (mh_emit_async: measure, offsets and writer on the writer '
+                       'stream, no host readback) instead of the default (measure on the main stream); the same step '
+                       'time on the pool, with the writer sharing the chip with more of the sampling')
   ap.add_argument('--genome-scale', type=float, default=1.0,
                   help='N > 1: contig lengths scaled by this (rehearsals of the plan on one GPU; 1 = GRCh37)')
   return ap.parse_args()
@@ -182,7 +183,7 @@ def run_chr1(a):
     eng.drop_haplotypes()
     eng.ctx.reset_output()
     pend = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
-                         rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=not a.sync_emit)
+                         rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=a.async_emit)
 
     def get():
       res = pend.resolve() if hasattr(pend, 'resolve') else pend

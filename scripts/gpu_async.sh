@@ -8,7 +8,7 @@ grep -E 'PASSED|FAILED|ERROR' gpurun_out/pytest_$TAG.log | tail -20; tail -30 gp
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-e2e > gpurun_out/b_$TAG.log 2>&1 || exit $?
 tail -1 gpurun_out/b_$TAG.log | cut -c1-330
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-e2e --sync-emit > gpurun_out/bs_$TAG.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-e2e --async-emit > gpurun_out/bs_$TAG.log 2>&1 || exit $?
 tail -1 gpurun_out/bs_$TAG.log | cut -c1-330
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-e2e --corrupt > gpurun_out/bc_$TAG.log 2>&1 || exit $?
 tail -1 gpurun_out/bc_$TAG.log | cut -c1-330
