@@ -14,7 +14,7 @@ every unit sampled and emitted by its owner, no data-path collective — output 
 per-rank template and byte counts closes each step (the counts the file writer turns into offsets).  Total work is
 fixed as N grows (strong scaling).
 
-Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_direct; k_emit_write with
+Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_tiles; k_emit_write with
 --emit-mode 1): algorithmic bytes per launch = sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ
 bytes written (both files), divided by the launch's HIP-event duration on the writer's stream; `stage_ms` gives
 every stage per step.  At N = 1 the line also carries `cpu_baseline` (the CPU oracle on the host cores) and
@@ -175,7 +175,7 @@ def run_chr1(a):
   for cpy in range(len(copies)):   # inputs resident in HBM before timing: contig and both copies' variants
     eng.upload_variants(0, cpy, copies[cpy])
   eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_direct'
+  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
 
   def step():
     # one chr1 job; consecutive jobs pipeline on the device (this job's splice and sampling run while the previous
@@ -301,7 +301,7 @@ def run_genome(a, rank, world, local, dist):
       eng.upload_variants(ri, cpy, copies[ri][cpy])
     del seq
   eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_direct'
+  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
   dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
   counts = torch.zeros(3, dtype=torch.int64, device=dev)
 

@@ -266,7 +266,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   for (auto &e : ctx->eset) {
-    release(e.recs); release(e.off); release(e.slots); release(e.stat); release(e.crrec);
+    release(e.recs); release(e.off); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
     if (e.rb) (void)hipEventDestroy(e.rb);
     if (e.h_stat) (void)hipHostFree(e.h_stat);

@@ -240,49 +240,6 @@ struct Rec {
   int32_t n0[2], n1[2];             // start / end node per mate (pass 2 skips the searches)
 };
 
-// Packs bytes into dwords and stores each completed dword while `cap` dwords remain (one thread writing its own
-// slot; p == nullptr counts only); n counts every byte.
-struct ByteWriter {
-  uint32_t *p;
-  uint32_t acc;
-  int nb;
-  int32_t n;
-  int32_t cap;
-  __device__ __forceinline__ void put(uint8_t c) {
-    acc |= (uint32_t)c << (8 * nb);
-    n++;
-    if (++nb == 4) {
-      if (p != nullptr && cap > 0) {
-        *p++ = acc;
-        cap--;
-      }
-      acc = 0;
-      nb = 0;
-    }
-  }
-  __device__ __forceinline__ void flush() {
-    if (nb && p != nullptr && cap > 0) *p = acc;
-  }
-  // decimal, most significant digit first: digits packed 4 bits each (LSB-first) then emitted from the top
-  __device__ __forceinline__ void put_u(uint64_t v) {
-    if (v <= 0xffffffffull) {
-      uint32_t x = (uint32_t)v;
-      uint64_t bcd = 0;
-      int nd = 0;
-      do {
-        bcd |= (uint64_t)(x % 10u) << (4 * nd);
-        x /= 10u;
-        nd++;
-      } while (x);
-      for (int i = nd - 1; i >= 0; i--) put((uint8_t)('0' + ((bcd >> (4 * i)) & 15)));
-    } else {
-      put_big(v);
-    }
-  }
-  __device__ __forceinline__ void put_s(int64_t v) {
-    if (v < 0) { put('-'); put_u((uint64_t)(-v)); } else put_u((uint64_t)v);
-  }
-};
 struct E3 {
   int64_t kept, b1, b2;
   __device__ E3 operator+(const E3 &o) const { return E3{kept + o.kept, b1 + o.b1, b2 + o.b2}; }
@@ -303,73 +260,7 @@ struct QFixed {
   int32_t prefix_len, mid_len;
 };
 
-constexpr int SLOT = 256;   // bytes per template for the reads part of the qname ("|s|pos|rlen|cigar|v,..|...")
-constexpr int MS_STG = 64;    // of which the first MS_STG bytes are staged in LDS by k_emit_measure
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
-
-// Four ASCII digits of w < 10000, first digit in the low byte.
-__device__ __forceinline__ uint32_t ascii4(uint32_t w) {
-  const uint32_t c = (w * 5243u) >> 19, d = w - 100u * c;   // w / 100, w % 100
-  const uint32_t ct = (c * 103u) >> 10, dt = (d * 103u) >> 10;   // tens of each pair
-  return 0x30303030u | ct | ((c - 10u * ct) << 8) | (dt << 16) | ((d - 10u * dt) << 24);
-}
-
-// ByteWriter for k_emit_measure: dword k goes to LDS while k < MS_STG / 4, else to the global slot (k < SLOT / 4).
-// Bytes gather in a 64-bit accumulator and leave a dword at a time; numbers are appended up to four digits per step.
-struct SplitWriter {
-  uint32_t *lds;
-  uint32_t *g;
-  uint64_t acc;   // nb pending bytes (< 4)
-  int nb;
-  int32_t n;      // bytes appended
-  int dw;         // dwords stored
-  __device__ __forceinline__ void store(uint32_t v) {
-    const int k = dw++;
-    if (k < MS_STG / 4) lds[k] = v;
-    else if (g != nullptr && k < SLOT / 4) g[k] = v;
-  }
-  // append the low k (1..4) bytes of v
-  __device__ __forceinline__ void putk(uint32_t v, int k) {
-    acc |= (uint64_t)v << (8 * nb);
-    nb += k;
-    n += k;
-    if (nb >= 4) {
-      store((uint32_t)acc);
-      acc >>= 32;
-      nb -= 4;
-    }
-  }
-  __device__ __forceinline__ void put(uint8_t c) { putk(c, 1); }
-  __device__ __forceinline__ void flush() {
-    if (nb) store((uint32_t)acc);
-  }
-  __device__ __forceinline__ void put_u(uint64_t v) {
-    if (v <= 0xffffffffull) {
-      const uint32_t x = (uint32_t)v;
-      const int nd = ndig_u(x);
-      const uint32_t hi = x / 100000000u, lo = x - hi * 100000000u;
-      const uint32_t a = (uint32_t)(((uint64_t)lo * 109951163ull) >> 40);   // lo / 10000
-      const uint32_t L0 = ascii4(a), L1 = ascii4(lo - 10000u * a);          // the 8 low digits
-      if (nd > 8) {
-        if (hi >= 10u) putk(0x3030u | (hi / 10u) | ((hi % 10u) << 8), 2);
-        else putk(0x30u | hi, 1);
-        putk(L0, 4);
-        putk(L1, 4);
-      } else if (nd > 4) {
-        const int s = 8 - nd;   // leading zeros of the 8-digit string
-        putk(L0 >> (8 * s), 4 - s);
-        putk(L1, 4);
-      } else {
-        putk(L1 >> (8 * (4 - nd)), nd);
-      }
-    } else {
-      put_big(v);
-    }
-  }
-  __device__ __forceinline__ void put_s(int64_t v) {
-    if (v < 0) { put('-'); put_u((uint64_t)(-v)); } else put_u((uint64_t)v);
-  }
-};
 
 // Length of one read's part of the qname ('|' strand '|' pos '|' rlen '|' cigar '|' v1,v2,..; readgenerate.py:223-225)
 // for the read of length rlen at p whose start / end nodes are n0 (node nd0) .. n1.
@@ -389,16 +280,13 @@ __device__ __forceinline__ int32_t read_part_len(const HapView &h, const Node16 
   return L;
 }
 
-// SLOTS: format the reads part into the 256-byte slots (MH_EMIT_SLOTS layout); otherwise record lengths only.
-template <bool SLOTS>
+// One thread per template: start/end node of both mates, POS, the N filter (readgenerate.py:201-204), the qname
+// reads part's length (not its text: the writer formats it) and the record lengths without the cnt digits, into
+// Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the longest record
+// (+20) and the longest reads part + '\n' as maxima (one atomic per wave).
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
-                                                      Rec *recs, int32_t *max_rec, uint8_t *slots,
-                                                      int32_t *overflow, int32_t dbg) {
-  // the reads part is formatted into LDS (bytes past MS_STG straight to the slot) and leaves in coalesced 16-byte
-  // chunks after the barrier
-  __shared__ uint32_t stg[SLOTS ? 256 : 1][MS_STG / 4 + 1];   // odd row stride: rows spread over all banks
-  __shared__ int32_t s_n[SLOTS ? 256 : 1];
+                                                      Rec *recs, int4 *tsum, int32_t *max_rec) {
   __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
   const bool runs_lds = h.n_runs <= MS_RUNS;
   if (runs_lds)
@@ -410,6 +298,7 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int32_t local_max = 0;
   int32_t nbytes = 0;
+  int32_t sk = 0, s1 = 0, s2 = 0;   // this template's share of the tile sums
   if (t < m) {
     ReadInfo r[2];
     Node16 nn0[2];
@@ -431,7 +320,7 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
              count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
     }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
-    if (!SLOTS && keep) {   // lengths only: the writer formats the reads part itself
+    if (keep) {
       const int32_t l0 = read_part_len(h, nn0[0], r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
       const int32_t l1 = read_part_len(h, nn0[1], r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
       const int32_t rest = l0 + l1;
@@ -445,52 +334,20 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       out.rest = rest;
       local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
       nbytes = rest + 1;
-    } else if (SLOTS && keep) {
-      // the reads part of the qname, in file order (readgenerate.py:223-225), and the qname's '\n': formatted into
-      // the slot while it fits, counted either way (its length sizes the records)
-      SplitWriter bw{stg[threadIdx.x], slots && !(dbg & 1) ? (uint32_t *)(slots + t * SLOT) : nullptr, 0ull, 0, 0, 0};
-      for (int fr = 0; fr < 2 && !(dbg & 2); fr++) {
-        const int s = fr == f0 ? 0 : 1;
-        const ReadInfo &ri = r[s];
-        bw.put('|'); bw.put((uint8_t)('0' + s));
-        bw.put('|'); bw.put_s(ri.pos);
-        bw.put('|'); bw.put_s(rlen);
-        bw.put('|');
-        if (ri.special) {
-          bw.put('>'); bw.put_s(p[s] - nn0[s].ps()); bw.put(':'); bw.put_s(rlen); bw.put('I');
-        } else {
-          for (int64_t k = ri.n0; k <= ri.n1; k++) {
-            const Node16 n = k == ri.n0 ? nn0[s] : h.nd[k];
-            bw.put_s(node_count(n, p[s], rlen));
-            bw.put(n.op());
-          }
-        }
-        bw.put('|');
-        bool first = true;
-        for (int64_t k = ri.n0; k <= ri.n1; k++) {
-          const Node16 n = k == ri.n0 ? nn0[s] : h.nd[k];
-          if (n.code() == 0) continue;
-          if (!first) bw.put(',');
-          bw.put_s(node_v(n));
-          first = false;
-        }
-      }
-      bw.put('\n');
-      bw.flush();
-      if (slots != nullptr && bw.n > SLOT) atomicOr(overflow, 1);   // the unit falls back to the LDS-image writer
-      nbytes = slots != nullptr && !(dbg & 1) && bw.n <= SLOT ? bw.n : 0;
-      const int32_t rest = bw.n - 1;
-      const int32_t ql = q.prefix_len + q.mid_len + rest;          // qname length without the cnt digits
-      const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
-      const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
-      const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
-      out.keep = 1;
-      out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
-      out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
-      out.rest = rest;
-      local_max = (out.len1 > out.len2 ? out.len1 : out.len2) + 20;
+      sk = 1;
+      s1 = out.len1;
+      s2 = out.len2;
     }
     recs[t] = out;
+  }
+  if (tsum != nullptr) {   // the tile = the 32 lanes of a wave half
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) {
+      sk += __shfl_xor(sk, d, 64);
+      s1 += __shfl_xor(s1, d, 64);
+      s2 += __shfl_xor(s2, d, 64);
+    }
+    if ((threadIdx.x & 31) == 0 && t < m) tsum[t >> 5] = make_int4(sk, s1, s2, 0);
   }
   int32_t local_slot = nbytes;
   for (int d = 32; d >= 1; d >>= 1) {   // one atomic per wave
@@ -504,17 +361,6 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   if ((threadIdx.x & 63) == 0) {
     if (local_max > 0 && local_max > __builtin_nontemporal_load(max_rec)) atomicMax(max_rec, local_max);
     if (local_slot > 0 && local_slot > __builtin_nontemporal_load(max_rec + 3)) atomicMax(max_rec + 3, local_slot);
-  }
-  if (!SLOTS || slots == nullptr) return;
-  s_n[threadIdx.x] = nbytes;
-  __syncthreads();
-  const int64_t tb = (int64_t)blockIdx.x * blockDim.x;
-  constexpr int CH = MS_STG / 16;
-  for (int it = threadIdx.x; it < 256 * CH; it += 256) {
-    const int j = it / CH, c = it - j * CH;
-    if (16 * c >= s_n[j]) continue;
-    const uint32_t *s = &stg[j][4 * c];
-    *(uint4 *)(slots + (tb + j) * SLOT + 16 * c) = make_uint4(s[0], s[1], s[2], s[3]);
   }
 }
 
@@ -714,23 +560,28 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 }
 
 // ---- direct writer -------------------------------------------------------------------------------------------
-// The default emission kernel (no fused corruption).  Every FASTQ record is three byte strings held in LDS:
-//   Q  the qname line: head ('@stub:' cnt '|chrom|cpy', written by the owner thread) + the reads part and '\n'
-//      that k_emit_measure formatted into the template's 256-byte slot (gathered in 16-byte chunks);
-//   B  the bases: the haplotype window of the file's mate, gathered in 16-byte chunks; mate 1's chunks are
-//      reversed and complemented in registers on the way in and stored mirrored, so B is forward in both cases;
+// The default emission kernel.  k_emit_measure has recorded per template its start/end nodes, keep flag and record
+// lengths (without the cnt digits) and per 32-template tile the sums (kept, bytes per file); a small scan over the
+// tiles gives each tile's prefix (k_tile_scan).  Per tile, every FASTQ record is three byte strings held in LDS:
+//   Q  the qname line: head ('@stub:' cnt '|chrom|cpy') + the reads part ('|strand|POS|rlen|CIGAR|v,..' per read,
+//      formatted here from the template's nodes) and '\n';
+//   B  the bases: the haplotype window of the file's mate, gathered in 16-byte chunks (mate 1 from the reverse-
+//      complement haplotype, so B reads forward in both cases);
 //   T  '\n+\n' + rlen '~' + '\n', one copy per workgroup (identical for every perfect read).
-// P0/P1 (one phase): metadata, Q heads, T, and all gathers of the 32-template tile in flight; one barrier; then
-// P2 writes the tile's output bytes as aligned 16-byte stores straight to the arenas, in two sweeps:
+// Phase 1: waves 1-3 issue all gathers of the tile; wave 0 (lane = read) formats the qname parts, scans the tile's
+// record lengths, numbers the kept templates (cnt = cnt_base + kept before + 1, readgenerate.py:209) and adds the cnt
+// digits in closed form (digit_sum); owner lanes write the metadata and the qname heads.  One barrier.  Phase 2
+// writes the tile's bytes as aligned 16-byte stores straight to the arenas, in two sweeps:
 //   pure  chunks inside one string of one record: one unaligned 16-byte LDS read (v_alignbyte) and one store;
 //   seam  the (at most four) chunks per record that straddle strings or records — record start (previous record's
 //         T end + Q), Q|B, B|T, and the tile's ragged end — merged per dword with byte masks (v_bfi); the tile's
 //         first and last chunks are byte stores of the tile's own bytes (the neighbouring tiles own the rest).
+// With corruption the records carry len(seq) placeholder qualities and the writer also leaves each record's
+// first-base offset for k_cr_inplace.
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
-constexpr int ED_PAD = 32;
-constexpr int ED_GMAX = 7;   // FMT layout: window chunks per thread (3 threads per mate): up to 21 chunks
-constexpr int ED_WMAX = 5;   // window chunks per thread (4 threads per mate): win_stride <= 320, rlen <= 289   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
+constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
+constexpr int ED_GMAX = 7;   // window chunks per gather thread (3 threads per mate): up to 21 chunks, rlen <= 321
 
 struct DMeta {
   int32_t rel[2];    // record start relative to the tile's first byte, per file
@@ -792,258 +643,15 @@ struct QHead {
   __device__ __forceinline__ uint8_t at(int i) const { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
 };
 
-// Per-tile registers: round 1 (records, positions; the owner lanes' metadata) and round 2 (the gathers).
-struct EdOwner {     // owner lanes (one per template)
-  int32_t keep, len1, len2, rest;
-  int64_t kept, b1, b2;
-  int64_t p0, p1;
-  int32_t fo, pad;
-};
-
-struct EdArgs {
-  HapView h;
-  int64_t m;
-  const int64_t *pos0, *pos1;
-  const int8_t *fo0;
-  const Rec *recs;
-  const E3 *off;
-  const uint8_t *slots;
-  char *arena[2];
-  int64_t used[2];
-  const int64_t *d_base;   // asynchronous emission: the arena offsets from the device (else used[])
-  int32_t rlen, win_stride, head, qstride;
-  int32_t dbg;
-};
-
-// CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
-// read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
-// placeholders into qualities) when it corrupts the record.
-// FMT: the qname's reads part is formatted here, from the template's nodes (k_emit_measure measured its length
-// only), instead of gathered from the 256-byte slot k_emit_measure formatted it into (MH_EMIT_SLOTS=1).
-template <int NF, int LPR, bool CR, bool FMT>
-__global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) {
+// The output sweeps of a 32-template tile whose strings and metadata are in LDS: LPR lanes per record (record
+// r = file f, template j), passes over the tile's NF * ED_T records.  gbase: arena offset of the tile's first byte per
+// file; span: the tile's bytes per file.
+template <int NF, int LPR, bool CR>
+__device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64_t gbase[2], const int32_t span[2],
+                                          int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena,
+                                          int32_t dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
-  // pad | T | pad | seam chunks [NF][ED_T][4] x 16 B | dump (16 B)
-  DMeta *meta = (DMeta *)smem;
-  const HapView &h = A.h;
-  const int32_t win_stride = A.win_stride, qstride = A.qstride, head = A.head;
-  const int32_t o_win = (int32_t)(((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16);
-  const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
-  const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
-  const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
-  const bool staged = !(A.dbg & 128);                          // seam chunks via LDS (dbg 128: direct stores)
-  const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
-  const int32_t TL = A.rlen + 4;     // T = '\n+\n' + rlen '~' + '\n' (perfect reads, readgenerate.py:229)
   const int tid = threadIdx.x;
-  const int Lp = qh.lp, Lm = qh.lm;
-
-  const int64_t t0 = (int64_t)blockIdx.x * ED_T;
-  const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
-
-  // ---- round 1: records and positions (thread -> template jw = tid / 8, mate sw = (tid / 4) & 1), and the owner
-  // lanes' metadata (wave 0, lane j < nt owns template j) ------------------------------------------------------
-  const int jw = tid >> 3, sw = (tid >> 2) & 1, qw = tid & 3, qs = tid & 7;
-  EdOwner ow{};
-  if (tid < 64) {   // wave-uniform
-    const int64_t tm = t0 + (tid < nt ? tid : 0);
-    const int4 rc = *(const int4 *)(A.recs + tm);
-    const E3 o = A.off[tm];
-    ow = EdOwner{rc.x, rc.y, rc.z, rc.w, o.kept, o.b1, o.b2, A.pos0[tm], A.pos1[tm], A.fo0[tm], 0};
-  }
-  const int64_t tw = t0 + (jw < nt ? jw : 0);
-  int4 rc4 = make_int4(0, 0, 0, 0);                           // keep, len1, len2, rest
-  int64_t pw = 0;
-  if (!FMT) {
-    rc4 = *(const int4 *)(A.recs + tw);
-    pw = sw ? A.pos1[tw] : A.pos0[tw];
-  }
-  const E3 base = A.off[t0], endo = A.off[t0 + nt];
-  const int32_t span[2] = {(int32_t)(endo.b1 - base.b1), (int32_t)(endo.b2 - base.b2)};
-  // arena offsets of the tile's first byte per file; the arenas are 256-byte aligned, so offset & 15 is the
-  // address alignment
-  const int64_t gbase[2] = {(A.d_base ? A.d_base[0] : A.used[0]) + base.b1,
-                            (A.d_base ? A.d_base[1] : A.used[1]) + base.b2};
-
-  // ---- owner lanes: metadata and the qname head ('@stub:' cnt '|chrom|cpy', right-aligned before the slot
-  // area of the template's qname buffer); T ------------------------------------------------------------------------
-  for (int i = tid; i < TL; i += ED_THREADS)
-    smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
-  if (tid < nt) {
-    DMeta mt;
-    mt.len[0] = mt.len[1] = 0;
-    mt.rel[0] = mt.rel[1] = 0;
-    if (ow.keep) {
-      const int64_t p[2] = {ow.p0, ow.p1};
-      mt.rel[0] = (int32_t)(ow.b1 - base.b1);
-      mt.rel[1] = (int32_t)(ow.b2 - base.b2);
-      uint32_t x = (uint32_t)(ow.kept + 1);      // cnt: 1-based among kept templates (readgenerate.py:209-210)
-      const int nd = ndig_u(x);
-      const int lh = Lp + nd + Lm;
-      mt.qb = o_q + tid * qstride + head - lh;
-      mt.sb = lh + ow.rest + 1;
-      mt.len[0] = ow.len1 + nd;                  // Rec lengths exclude the cnt digits
-      mt.len[1] = ow.len2 + nd;
-      char *d = smem + mt.qb;
-      if (!(A.dbg & 8)) {
-        for (int i = 0; i < Lp; i++) d[i] = (char)qh.at(i);
-        for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
-        for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
-      }
-      for (int f = 0; f < 2; f++) {
-        const int s = f == ow.fo ? 0 : 1;        // file f holds mate s (reads[fo] = mate, readgenerate.py:207)
-        int64_t a = p[s] - h.p_min, e = p[s] + A.rlen - h.p_min;
-        if (e > h.hap_len) e = h.hap_len;
-        if (a > h.hap_len) a = h.hap_len;
-        const int32_t S = (int32_t)(e > a ? e - a : 0);
-        mt.S[f] = S;
-        // mate 0 reads hap[a, a + S); mate 1 its reverse complement = rc[hap_len - a - S, hap_len - a)
-        const int64_t a2 = s ? h.hap_len - a - S : a;
-        mt.bb[f] = o_win + (tid * 2 + s) * win_stride + (int32_t)(a2 & 15);
-        mt.tb[f] = o_t;
-        mt.tn[f] = CR ? S + 4 : TL;
-      }
-    }
-    meta[tid] = mt;
-  }
-
-  // ---- round 2: the gathers, all in flight together (unconditional: an unused chunk re-reads the first one) -----
-  const int chunks = win_stride / 16;
-  if constexpr (FMT) {
-    // waves 1-3 gather (three threads per mate window, chunks q3, q3 + 3, ...); wave 0 formats the reads part of
-    // the qnames meanwhile (lane l: template l / 2, mate l % 2)
-    if (tid >= 64) {
-      const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
-      const int jg = pr >> 1, sg = pr & 1;
-      const int64_t tg = t0 + (jg < nt ? jg : 0);
-      const bool kg = jg < nt && A.recs[tg].keep;
-      const int64_t pg = sg ? A.pos1[tg] : A.pos0[tg];
-      int64_t ag = pg - h.p_min, eg = pg + A.rlen - h.p_min;
-      if (eg > h.hap_len) eg = h.hap_len;
-      if (ag > h.hap_len) ag = h.hap_len;
-      const int64_t lg = eg > ag ? eg - ag : 0;
-      const int64_t a2g = sg ? h.hap_len - ag - lg : ag;    // mate 1: the reverse-complement haplotype
-      const int64_t a16 = a2g & ~(int64_t)15;
-      const uint8_t *hsrc = (A.dbg & 1) ? (const uint8_t *)A.pos0 : (sg ? h.rc : h.hap) + a16;   // dbg 1: no gathers
-      uint4 wv[ED_GMAX];
-      uint32_t use = 0;
-#pragma unroll
-      for (int k = 0; k < ED_GMAX; k++) {
-        const int c = q3 + 3 * k;
-        const bool u = kg && c < chunks && a16 + 16 * c < a2g + lg;
-        use |= (uint32_t)u << k;
-        wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
-      }
-      const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
-#pragma unroll
-      for (int k = 0; k < ED_GMAX; k++)
-        *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (q3 + 3 * k) : o_dump)) = wv[k];
-    } else if (!(A.dbg & 16)) {
-      // the reads part, in file order (readgenerate.py:223-225): mate s is read fr of the qname (reads[fo] = mate 0,
-      // readgenerate.py:207); read 1 ends at `rest`, where the qname's '\n' goes
-      const int jf = tid >> 1, s = tid & 1;
-      const int64_t tf = t0 + (jf < nt ? jf : 0);
-      const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
-      const int64_t p = s ? A.pos1[tf] : A.pos0[tf];
-      const int fo = A.fo0[tf];
-      if (jf < nt && r0.x) {
-        const int fr = s == 0 ? fo : 1 - fo;
-        const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
-        const int64_t rl = A.rlen;
-        // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
-        const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
-                     q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
-        // node k of the read (selects on the words: an indexed array of nodes would be placed in scratch)
-#define NODE_AT(k)                                                                                       \
-  Node16 n;                                                                                              \
-  {                                                                                                      \
-    const int64_t i_ = (k) - n0;                                                                         \
-    if (i_ > 3) {                                                                                        \
-      const uint64_t *g_ = (const uint64_t *)(h.nd + (k));                                               \
-      n.a = g_[0];                                                                                       \
-      n.b = g_[1];                                                                                       \
-    } else {                                                                                             \
-      n.a = i_ == 0 ? q0.a : i_ == 1 ? q1.a : i_ == 2 ? q2.a : q3.a;                                     \
-      n.b = i_ == 0 ? q0.b : i_ == 1 ? q1.b : i_ == 2 ? q2.b : q3.b;                                     \
-    }                                                                                                    \
-  }
-        const Node16 nd0 = q0;
-        ReadInfo ri;
-        ri.n0 = n0;
-        ri.n1 = n1;
-        read_place(h, nd0, p, rl, ri);
-        uint32_t o = (uint32_t)(o_q + jf * qstride + head);
-        if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part (its length, from the measure pass)
-        smem[o] = '|';
-        smem[o + 1] = (char)('0' + s);
-        smem[o + 2] = '|';
-        o = lds_put_s(smem, o + 3, ri.pos);
-        smem[o] = '|';
-        o = lds_put_s(smem, o + 1, rl);
-        smem[o++] = '|';
-        if (ri.special) {
-          smem[o] = '>';
-          o = lds_put_s(smem, o + 1, p - nd0.ps());
-          smem[o] = ':';
-          o = lds_put_s(smem, o + 1, rl);
-          smem[o++] = 'I';
-        } else {
-          for (int64_t k = n0; k <= n1; k++) {
-            NODE_AT(k)
-            o = lds_put_s(smem, o, node_count(n, p, rl));
-            smem[o++] = (char)n.op();
-          }
-        }
-        smem[o++] = '|';
-        bool first = true;
-        for (int64_t k = n0; k <= n1; k++) {
-          NODE_AT(k)
-          if (n.code() == 0) continue;
-          if (!first) smem[o++] = ',';
-          o = lds_put_s(smem, o, node_v(n));
-          first = false;
-        }
-        if (fr == 1) smem[o] = '\n';
-      }
-    }
-  } else {
-    const bool kept = jw < nt && rc4.x;
-    int64_t aw = pw - h.p_min, ew = pw + A.rlen - h.p_min;
-    if (ew > h.hap_len) ew = h.hap_len;
-    if (aw > h.hap_len) aw = h.hap_len;
-    const int64_t sw_len = ew > aw ? ew - aw : 0;
-    const int64_t a2w = sw ? h.hap_len - aw - sw_len : aw;     // mate 1: the reverse-complement haplotype
-    const int64_t a16 = a2w & ~(int64_t)15;
-    const uint8_t *hsrc = (A.dbg & 1) ? (const uint8_t *)A.pos0 : (sw ? h.rc : h.hap) + a16;   // dbg 1: no gathers
-    uint4 wv[ED_WMAX], sv[2];
-    uint32_t use = 0;
-#pragma unroll
-    for (int k = 0; k < ED_WMAX; k++) {
-      const int c = qw + 4 * k;
-      const bool u = kept && c < chunks && a16 + 16 * c < a2w + sw_len;
-      use |= (uint32_t)u << k;
-      wv[k] = *(const uint4 *)(hsrc + (u && !(A.dbg & 1) ? 16 * c : 0));
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int c = qs + 8 * k;
-      const bool u = kept && 16 * c <= rc4.w;   // the slot holds rest bytes + '\n'
-      use |= (uint32_t)u << (ED_WMAX + k);
-      sv[k] = *(const uint4 *)(A.slots + tw * SLOT + (u ? 16 * c : 0));
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int c = qs + 8 * k;
-      *(uint4 *)(smem + (((use >> (ED_WMAX + k)) & 1) ? o_q + jw * qstride + head + 16 * c : o_dump)) = sv[k];
-    }
-    const int32_t slot = o_win + (jw * 2 + sw) * win_stride;
-#pragma unroll
-    for (int k = 0; k < ED_WMAX; k++)
-      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (qw + 4 * k) : o_dump)) = wv[k];
-  }
-  __syncthreads();
-  if (A.dbg & 2) return;
-  // ---- output: LPR lanes per record (record r = file f, template j); passes over the tile's NF * ED_T records ----
   constexpr int RPP = ED_THREADS / LPR;                        // records per pass
   const int q = tid % LPR;
   // seams (record-relative): 0 = record start (previous record's T end | Q), sb = Q|B, tl = B|T, L = the tile's
@@ -1098,9 +706,9 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
     if (lo == 0 && hi == 16) {
       if (staged) *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-      else *(uint4 *)(A.arena[f] + (cg << 4)) = make_uint4(w[0], w[1], w[2], w[3]);
+      else *(uint4 *)(arena[f] + (cg << 4)) = make_uint4(w[0], w[1], w[2], w[3]);
     } else {
-      char *g = A.arena[f] + (cg << 4);
+      char *g = arena[f] + (cg << 4);
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
@@ -1114,7 +722,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
     const int32_t rel = M.rel[f];
     const int64_t ga = gbase[f] + rel;
     const int32_t sb = M.sb, tl = sb + M.S[f], qb = M.qb, bb = M.bb[f], tb = M.tb[f];
-    char *const arena = A.arena[f];
+    char *const out = arena[f];
     const int64_t c0 = ga >> 4;
     int32_t x0 = (int32_t)((c0 << 4) - ga) + 16 * q;
     for (int64_t cg = c0 + q; x0 + 16 <= L; cg += LPR, x0 += 16 * LPR) {
@@ -1123,10 +731,239 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_direct(EdArgs A, QHead qh) 
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
                                  : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : tb + (x0 - tl)));
-      const uint4 v = (A.dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
-      *(uint4 *)(arena + (cg << 4)) = v;
+      const uint4 v = (dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
+      *(uint4 *)(out + (cg << 4)) = v;
     }
   }
+}
+
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// tile sums of k_emit_measure -> tile prefixes (kept, bytes per file without the cnt digits)
+struct LoadTile {
+  const int4 *ts; int64_t n;
+  __device__ E3 operator()(int64_t i) const {
+    if (i >= n) return E3{0, 0, 0};
+    const int4 v = ts[i];
+    return E3{v.x, v.y, v.z};
+  }
+};
+struct StoreTile {
+  E3 *pre;
+  __device__ void operator()(int64_t i, E3, E3 excl) const { pre[i] = excl; }
+};
+
+struct TArgs {
+  HapView h;
+  int64_t m;
+  const int64_t *pos0, *pos1;
+  const int8_t *fo0;
+  const Rec *recs;          // k_emit_measure's records
+  const E3 *tpre;           // per tile: kept templates and record bytes (no cnt digits) before it
+  char *arena[2];
+  int64_t used[2];          // arena offset of the emission's first byte per file (synchronous path)
+  const int64_t *d_base;    // asynchronous path: the same offsets from the device (the fill before the unit)
+  int64_t cnt_base;         // templates kept before the emission's first one (cnt numbering)
+  uint2 *crec;              // corruption: per record the first base's arena offset and S (k_cr_inplace's words)
+  int32_t rlen, win_stride, head, qstride;
+};
+
+// node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
+// array of nodes would be placed in scratch)
+#define NODE_AT(k)                                                                                       \
+  Node16 n;                                                                                              \
+  {                                                                                                      \
+    const int64_t i_ = (k) - n0;                                                                         \
+    if (i_ > 3) {                                                                                        \
+      const uint64_t *g_ = (const uint64_t *)(h.nd + (k));                                               \
+      n.a = g_[0];                                                                                       \
+      n.b = g_[1];                                                                                       \
+    } else {                                                                                             \
+      n.a = i_ == 0 ? q0.a : i_ == 1 ? q1.a : i_ == 2 ? q2.a : q3.a;                                     \
+      n.b = i_ == 0 ? q0.b : i_ == 1 ? q1.b : i_ == 2 ? q2.b : q3.b;                                     \
+    }                                                                                                    \
+  }
+
+// CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
+// read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
+// placeholders into qualities) when it corrupts the record.
+template <int NF, int LPR, bool CR>
+__global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
+  __shared__ int32_t s_span[2];   // the tile's bytes per file
+  // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
+  // pad | T | pad | seam chunks [NF][ED_T][4] x 16 B | dump (16 B)
+  DMeta *meta = (DMeta *)smem;
+  const HapView &h = A.h;
+  const int32_t win_stride = A.win_stride, qstride = A.qstride, head = A.head;
+  const int32_t o_win = (int32_t)(((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16);
+  const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
+  const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
+  const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
+  const int32_t o_dump = o_s + NF * ED_T * 4 * 16;   // 16-byte sink for unused gathers
+  const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
+  const int tid = threadIdx.x;
+  const int Lp = qh.lp, Lm = qh.lm;
+  const int64_t tile = blockIdx.x;
+  const int64_t t0 = tile * ED_T;
+  const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
+  const int chunks = win_stride / 16;
+  for (int i = tid; i < TL; i += ED_THREADS)
+    smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
+  if (tid >= 64) {
+    // waves 1-3: the gathers (three threads per mate window), all in flight together; an unused chunk re-reads the
+    // first one
+    const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
+    const int jg = pr >> 1, sg = pr & 1;
+    const int64_t tg = t0 + (jg < nt ? jg : 0);
+    const bool kg = jg < nt;
+    const int64_t pg = sg ? A.pos1[tg] : A.pos0[tg];
+    int64_t ag = pg - h.p_min, eg = pg + A.rlen - h.p_min;
+    if (eg > h.hap_len) eg = h.hap_len;
+    if (ag > h.hap_len) ag = h.hap_len;
+    const int64_t lg = eg > ag ? eg - ag : 0;
+    const int64_t a2g = sg ? h.hap_len - ag - lg : ag;    // mate 1: the reverse-complement haplotype
+    const int64_t a16 = a2g & ~(int64_t)15;
+    const uint8_t *hsrc = (sg ? h.rc : h.hap) + a16;
+    uint4 wv[ED_GMAX];
+    uint32_t use = 0;
+#pragma unroll
+    for (int k = 0; k < ED_GMAX; k++) {
+      const int c = q3 + 3 * k;
+      const bool u = kg && c < chunks && a16 + 16 * c < a2g + lg;
+      use |= (uint32_t)u << k;
+      wv[k] = *(const uint4 *)(hsrc + (u ? 16 * c : 0));
+    }
+    const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
+#pragma unroll
+    for (int k = 0; k < ED_GMAX; k++)
+      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (q3 + 3 * k) : o_dump)) = wv[k];
+  } else {
+    // wave 0: lane = read (template jf, mate s)
+    const int jf = tid >> 1, s = tid & 1;
+    const bool valid = jf < nt;
+    const int64_t tf = t0 + (valid ? jf : 0);
+    const int64_t p = s ? A.pos1[tf] : A.pos0[tf];
+    const int fo = A.fo0[tf];
+    const int fr = s == 0 ? fo : 1 - fo;   // the read's place in the qname = its file (reads[fo] = mate 0, :207)
+    const int64_t rl = A.rlen;
+    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length, nodes
+    const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
+    const E3 P = A.tpre[tile];
+    const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
+    const bool keep = valid && (r0.x & 1);
+    const int32_t rest = r0.w;
+    // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
+    const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
+                 q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
+    int64_t a = p - h.p_min, e = p + rl - h.p_min;   // the read's bases: hap[a, a + S)
+    if (e > h.hap_len) e = h.hap_len;
+    if (a > h.hap_len) a = h.hap_len;
+    const int32_t S = (int32_t)(e > a ? e - a : 0);
+    if (keep) {
+      ReadInfo ri;
+      ri.n0 = n0;
+      ri.n1 = n1;
+      read_place(h, q0, p, rl, ri);
+      // the read's part of the qname at its place (readgenerate.py:223-225); read 1 ends at `rest`, where the '\n' goes
+      uint32_t o = (uint32_t)(o_q + jf * qstride + head);
+      if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part
+      smem[o] = '|';
+      smem[o + 1] = (char)('0' + s);
+      smem[o + 2] = '|';
+      o = lds_put_s(smem, o + 3, ri.pos);
+      smem[o] = '|';
+      o = lds_put_s(smem, o + 1, rl);
+      smem[o++] = '|';
+      if (ri.special) {
+        smem[o] = '>';
+        o = lds_put_s(smem, o + 1, p - q0.ps());
+        smem[o] = ':';
+        o = lds_put_s(smem, o + 1, rl);
+        smem[o++] = 'I';
+      } else {
+        for (int64_t k = n0; k <= n1; k++) {
+          NODE_AT(k)
+          o = lds_put_s(smem, o, node_count(n, p, rl));
+          smem[o++] = (char)n.op();
+        }
+      }
+      smem[o++] = '|';
+      bool first = true;
+      for (int64_t k = n0; k <= n1; k++) {
+        NODE_AT(k)
+        if (n.code() == 0) continue;
+        if (!first) smem[o++] = ',';
+        o = lds_put_s(smem, o, node_v(n));
+        first = false;
+      }
+      if (fr == 1) smem[o] = '\n';
+    }
+    // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
+    const int32_t lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
+    const int32_t ik = wave_incl_scan(keep && fr == 0 ? 1 : 0);
+    const int32_t i0 = wave_incl_scan(fr == 0 ? lw : 0);
+    const int32_t i1 = wave_incl_scan(fr == 1 ? lw : 0);
+    // sums over the tile's templates before this one (the inclusive value of lane 2 jf - 1) and the tile's totals
+    const int src = jf ? 2 * jf - 1 : 0;
+    int32_t xk = __shfl(ik, src, 64), x0 = __shfl(i0, src, 64), x1 = __shfl(i1, src, 64);
+    if (jf == 0) xk = x0 = x1 = 0;
+    const int32_t tk = __shfl(ik, 63, 64), tb0 = __shfl(i0, 63, 64), tb1 = __shfl(i1, 63, 64);
+    const int64_t K0 = A.cnt_base + P.kept;                          // templates kept before the tile
+    const int64_t ds0 = digit_sum(K0) - digit_sum(A.cnt_base);       // cnt digits of the emission's records before it
+    const int64_t g0 = (A.d_base ? A.d_base[0] : A.used[0]) + P.b1 + ds0;
+    const int64_t g1 = (A.d_base ? A.d_base[1] : A.used[1]) + P.b2 + ds0;
+    if (tid == 0) {
+      const int64_t dst = digit_sum(K0 + tk) - digit_sum(K0);        // ... of the tile's records
+      s_g[0] = g0;
+      s_g[1] = g1;
+      s_span[0] = (int32_t)(tb0 + dst);
+      s_span[1] = (int32_t)(tb1 + dst);
+    }
+    if (valid) {
+      DMeta &mt = meta[jf];
+      const int64_t cnt = K0 + xk + 1;                               // 1-based among kept templates (:209-210)
+      const int nd = ndig_u((uint64_t)cnt);
+      const int32_t rel = (int32_t)((fr == 0 ? x0 : x1) + digit_sum(K0 + xk) - digit_sum(K0));
+      mt.len[fr] = keep ? lw + nd : 0;
+      mt.rel[fr] = rel;
+      const int32_t lh = Lp + nd + Lm;
+      const int32_t qb = o_q + jf * qstride + head - lh, sb = lh + rest + 1;
+      if (keep) {
+        const int64_t a2 = s ? h.hap_len - a - S : a;              // mate 1 reads the reverse complement forward
+        mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + (int32_t)(a2 & 15);
+        mt.S[fr] = S;
+        mt.tb[fr] = o_t;
+        mt.tn[fr] = CR ? S + 4 : TL;
+        if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
+          mt.qb = qb;
+          mt.sb = sb;
+          char *d = smem + qb;
+          for (int i = 0; i < Lp; i++) d[i] = (char)qh.at(i);
+          uint32_t x = (uint32_t)cnt;
+          for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
+          for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
+        }
+      }
+      if (CR && (NF == 2 || fr == 0)) {   // the record's first base, for the corruption pass (S = 0: dropped)
+        const uint64_t so = (uint64_t)((fr ? g1 : g0) + rel + sb);
+        A.crec[tf * NF + fr] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | (uint32_t)(keep ? S : 0));
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t gbase[2] = {s_g[0], s_g[1]};
+  const int32_t span[2] = {s_span[0], s_span[1]};
+  ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, true, A.arena, 0);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -1356,7 +1193,7 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
 int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_t m, const int64_t *pos0,
                           const int64_t *pos1, const int8_t *fo0, const Rec *recs, const E3 *off, uint2 *crec,
                           char *o1, char *o2, int32_t nf, int32_t lh0, int32_t rlen, const CorruptCfg &cc,
-                          const int64_t *d_base = nullptr) {
+                          const int64_t *d_base = nullptr, bool crec_ready = false) {
   if (m <= 0) return MH_OK;
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1370,8 +1207,10 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   if (grid < 1) grid = 1;
   CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
-  hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
-  HIPCHK(ctx, hipGetLastError());
+  if (!crec_ready) {   // (the fused writer wrote the record words itself)
+    hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
+    HIPCHK(ctx, hipGetLastError());
+  }
   if (lds_tab)
     hipLaunchKernelGGL(k_cr_inplace<true>, dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else
@@ -1443,6 +1282,23 @@ int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, in
   return MH_OK;
 }
 
+// Sum of digits(c) for c = 1..K (host side of digit_sum)
+static int64_t digit_sum_host(int64_t K) {
+  if (K <= 0) return 0;
+  int nd = 1;
+  for (int64_t v = K; v >= 10; v /= 10) nd++;
+  int64_t rep = 0;
+  for (int i = 0; i < nd; i++) rep = rep * 10 + 1;
+  return (K + 1) * nd - rep;
+}
+
+// dynamic LDS of k_emit_tiles: metadata, windows, qname buffers, T, seam chunks, dump
+static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf) {
+  return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
+         (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
+         (size_t)nf * ED_T * 4 * 16 + 16;
+}
+
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                    bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
@@ -1477,13 +1333,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *d_mid = small + 256 + 4096;
   QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
-  // the direct writer (fused corruption too, unless MH_CORRUPT_LDS asks for the LDS-image writer: experiments)
+  // the direct writer (corruption too, unless MH_CORRUPT_LDS asks for the LDS-image writer: experiments): record
+  // offsets from per-tile prefixes; the LDS-image writer reads per-template offsets
   const bool direct = !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS"));
-  // the direct writer formats the qname's reads part itself (measure records lengths only); MH_EMIT_SLOTS=1: the
-  // round-1 layout, measure formats it into 256-byte slots the writer gathers (A/B experiments)
-  static const bool use_slots = getenv("MH_EMIT_SLOTS") && atoi(getenv("MH_EMIT_SLOTS"));
+  const int64_t ntiles = (m + ED_T - 1) / ED_T;
 
-  // ---- measure + record offsets (skipped when mh_emit_prepare already ran them for this unit) ----------------------
+  // ---- measure + tile prefixes (skipped when mh_emit_prepare already ran them for this unit) ------------------------
   EmitPrep &pp = tp.prep;
   const bool have_prep = !prepare_only && pp.valid && pp.slot == slot && pp.t_begin == t_begin && pp.t_end == t_end &&
                          pp.cnt_base == cnt_base && pp.prefix == prefix && pp.mid == mid && pp.direct == direct;
@@ -1493,7 +1348,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   }
   int32_t set;
   E3 ht;
-  int32_t hm4[4] = {0, 0, 0, 0};   // max record length + 20, err, overflow, max slot bytes
+  int32_t hm4[4] = {0, 0, 0, 0};   // max record length + 20, -, -, longest reads part + '\n'
+  // the scans' totals (kept, bytes without the cnt digits) -> the emission's totals
+  auto totals = [&](const E3 &t) {
+    const int64_t ds = digit_sum_host(cnt_base + t.kept) - digit_sum_host(cnt_base);
+    return E3{t.kept, t.b1 + ds, t.b2 + ds};
+  };
   stage_begin(ctx, "emit");
   if (have_prep) {
     set = pp.set;
@@ -1502,7 +1362,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       HIPCHK(ctx, hipEventSynchronize(es.rb));
       std::memcpy(&ht, es.h_stat, sizeof(E3));
       std::memcpy(hm4, (const char *)es.h_stat + 32, sizeof(hm4));
-      ht.kept -= pp.cnt_base;
+      ht = totals(ht);
       pp.deferred = false;
     } else {
       ht = E3{pp.ht.kept, pp.ht.b1, pp.ht.b2};
@@ -1521,44 +1381,43 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
     if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
-    MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
-    if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));   // k_cr_recs: 8 bytes per record
-    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
+    MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)ntiles));
+    MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)ntiles));
+    if (!direct) MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+    if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));   // 8 bytes per record
+    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(direct ? ntiles : m + 1)));
     MH_TRY(ensure(ctx, es.stat, 64));
     char *stat = (char *)es.stat.p;        // per set: a deferred readback must not see the next unit's totals
     E3 *tot = (E3 *)stat;                  // [0, 24)
     int32_t *max_rec = (int32_t *)(stat + 32);
     HIPCHK(ctx, hipMemsetAsync(stat, 0, 64, st));
-    // staged through the set's pinned block: the call may return before these copies ran (deferred prepare)
-    char *hp = (char *)es.h_stat + 64, *hmid = (char *)es.h_stat + 64 + 4096;
-    std::memcpy(hp, prefix.data(), prefix.size());
-    std::memcpy(hmid, mid.data(), mid.size());
-    HIPCHK(ctx, hipMemcpyAsync(d_prefix, hp, prefix.size(), hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(d_mid, hmid, mid.size(), hipMemcpyHostToDevice, st));
     Rec *recs = (Rec *)es.recs.p;
-    E3 *off = (E3 *)es.off.p;
-    int32_t *overflow = (int32_t *)(stat + 40);
-    if (direct && use_slots) MH_TRY(ensure(ctx, es.slots, (size_t)SLOT * (m + 1)));
     stage_begin(ctx, "emit_measure");
-    hipLaunchKernelGGL(direct && use_slots ? k_emit_measure<true> : k_emit_measure<false>,
-                       dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
-                       rlen, q, (int32_t)ctx->corrupt_on, recs, max_rec,
-                       direct && use_slots ? (uint8_t *)es.slots.p : nullptr, overflow,
-                       getenv("MH_MEASURE_DBG") ? atoi(getenv("MH_MEASURE_DBG")) : 0);
+    hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
+                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     stage_begin(ctx, "emit_scan");
-    HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{off, cnt_base}, ctx->scan_partials.p, tot));
+    if (direct)
+      HIPCHK(ctx, device_scan_sum<E3>(st, ntiles, LoadTile{(const int4 *)es.tsum.p, ntiles},
+                                      StoreTile{(E3 *)es.tpre.p}, ctx->scan_partials.p, tot));
+    else
+      HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{(E3 *)es.off.p, cnt_base},
+                                      ctx->scan_partials.p, tot));
     stage_end(ctx);
     if (defer) {
-      HIPCHK(ctx, hipMemcpyAsync(es.h_stat, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(es.h_stat, tot, sizeof(E3), hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipMemcpyAsync((char *)es.h_stat + 32, max_rec, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipEventRecord(es.rb, st));
     } else {
-      HIPCHK(ctx, hipMemcpyAsync(&ht, &off[m], sizeof(E3), hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(hm4, max_rec, 16, hipMemcpyDeviceToHost, st));
+      int64_t *hs = pinned_small(ctx);
+      if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+      HIPCHK(ctx, hipMemcpyAsync(hs, tot, sizeof(E3), hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs + 4, max_rec, 16, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
-      ht.kept -= cnt_base;
+      std::memcpy(&ht, hs, sizeof(E3));
+      std::memcpy(hm4, hs + 4, sizeof(hm4));
+      ht = totals(ht);
     }
     if (prepare_only) {
       stage_end(ctx);
@@ -1586,7 +1445,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   EmitSet &es = ctx->eset[set];
   es.prepared = false;
   const Rec *recs = (const Rec *)es.recs.p;
-  const E3 *off = (const E3 *)es.off.p;
   const int32_t hmax = hm4[0], hslot = hm4[3];
 
   // ---- the writer ------------------------------------------------------------------------------------------------
@@ -1619,18 +1477,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_end(ctx);
     return arg_fail(ctx, MH_E_CAPACITY, "read length too large for the LDS staging layout");
   }
-  const int32_t hover = direct && use_slots ? hm4[2] : 0;   // a reads part overflowed its slot (slot layout)
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
-  const char *dbg_env = getenv("MH_EMIT_DBG");   // timing experiments only: skip parts of the kernel
-  const int32_t edbg = dbg_env ? atoi(dbg_env) : 0;
-  const bool staged = !(edbg & 128);              // seam chunks staged in LDS (dbg 128: stored directly, experiment)
-  const int32_t qstride = head + ((edbg & 256) ? SLOT : (hslot > 16 ? (hslot + 15) / 16 * 16 : 16)) + 32;
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
-  const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
-                       (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-                       (staged ? (size_t)2 * ED_T * 4 * 16 : 0) + 16;
+  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32;
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -1639,28 +1491,26 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     qh.lp = (int32_t)prefix.size();
     qh.lm = (int32_t)mid.size();
   }
-  if (direct && !hover && head_fits && win_stride <= 16 * 4 * ED_WMAX && lds_d <= 64 * 1024 && cnt_base + m < (int64_t)UINT32_MAX) {
-    // direct writer (qname reads part formatted by k_emit_measure into 256-byte slots), queued on the writer
-    // stream: the call returns while it runs, so the next unit's measure pass and the next job's sampling overlap it
+  if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
+      cnt_base + m < (int64_t)UINT32_MAX) {
+    // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
+    // and the next job's sampling overlap it
     HIPCHK(ctx, hipEventRecord(ctx->ev_ready, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_ready, 0));
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
-    const int64_t ntiles = (m + ED_T - 1) / ED_T;
-    EdArgs A{hv, m, pos0, pos1, fo0, recs, off, (const uint8_t *)es.slots.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {ctx->used1, ctx->used2}, nullptr, (int32_t)rlen, win_stride, head,
-             qstride, edbg};
-    auto kfn = use_slots
-                   ? (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, false> : k_emit_direct<1, 8, true, false>)
-                                      : (write_fastq2 ? k_emit_direct<2, 4, false, false> : k_emit_direct<1, 8, false, false>))
-                   : (ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, true> : k_emit_direct<1, 8, true, true>)
-                                      : (write_fastq2 ? k_emit_direct<2, 4, false, true> : k_emit_direct<1, 8, false, true>));
+    TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
+            {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
+            qstride};
+    auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
+                               : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     if (ctx->corrupt_on)
-      MH_TRY(launch_cr_inplace(ctx, ctx->wstream, hv, m, pos0, pos1, fo0, recs, off, (uint2 *)es.crrec.p, o1, o2,
-                               write_fastq2 ? 2 : 1,
-                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc));
+      MH_TRY(launch_cr_inplace(ctx, ctx->wstream, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p,
+                               (char *)ctx->out1.p, (char *)ctx->out2.p, write_fastq2 ? 2 : 1,
+                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc, nullptr, true));
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
@@ -1670,7 +1520,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     es.busy = true;
     ctx->writer_pending = true;
   } else {
-    // LDS-image writer: fallback when a qname's reads part exceeds its slot (synchronous, main stream)
+    // LDS-image writer: the fallback (very long qnames or names; synchronous, main stream); per-template offsets
+    if (direct) {
+      MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+      MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(m + 1)));
+      HIPCHK(ctx, device_scan_sum<E3>(st, m + 1, LoadRec{recs, m}, StoreOff{(E3 *)es.off.p, cnt_base},
+                                      ctx->scan_partials.p, (E3 *)((char *)ctx->d_small.p + 128)));
+    }
+    const E3 *off = (const E3 *)es.off.p;
     HIPCHK(ctx, hipMemsetAsync(small + 32, 0, 16, st));
     HIPCHK(ctx, hipMemcpyAsync(d_prefix, prefix.data(), prefix.size(), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemcpyAsync(d_mid, mid.data(), mid.size(), hipMemcpyHostToDevice, st));
@@ -1784,17 +1641,16 @@ int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out) {
   return MH_OK;
 }
 
-// the unit's base offsets and the device fill after it; its totals (off[m]: cnt digits included) copied to the result
-// words beside the bases
-__global__ void k_emit_advance(const E3 *off_m, int64_t *d_used, int64_t *stat, int32_t write2) {
-  const E3 t = *off_m;
-  stat[0] = t.kept;
-  stat[1] = t.b1;
-  stat[2] = write2 ? t.b2 : 0;
+// the unit's totals (stat[0..2]: the tile scan's kept and bytes without the cnt digits; the cnt digits of cnt = 1..kept
+// added), its base offsets (stat[6..7]: the device fill before it) and the device fill after it
+__global__ void k_emit_advance(int64_t *d_used, int64_t *stat, int32_t write2) {
+  const int64_t ds = digit_sum(stat[0]);
+  stat[1] += ds;
+  stat[2] = write2 ? stat[2] + ds : 0;
   stat[6] = d_used[0];
   stat[7] = d_used[1];
-  d_used[0] += t.b1;
-  if (write2) d_used[1] += t.b2;
+  d_used[0] += stat[1];
+  d_used[1] += stat[2];
 }
 __global__ void k_set_used(int64_t *d_used, int64_t u1, int64_t u2) {
   d_used[0] = u1;
@@ -1864,14 +1720,11 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   const int32_t head = (int32_t)(((prefix.size() + mid.size() + 10 + 16) + 15) / 16 * 16);
   int32_t rb = 0;
   bool direct = head_fits && !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS")) &&
-                win_stride <= 16 * 4 * ED_WMAX && m < (int64_t)UINT32_MAX && m > 0 && !getenv("MH_EMIT_SYNC") &&
-                !(getenv("MH_EMIT_SLOTS") && atoi(getenv("MH_EMIT_SLOTS")));
+                win_stride <= 16 * 3 * ED_GMAX && m < (int64_t)UINT32_MAX && m > 0 && !getenv("MH_EMIT_SYNC");
   if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
   const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32;
-  const size_t lds_d = ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
-                       (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-                       (size_t)2 * ED_T * 4 * 16 + 16;
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
   if (!direct || lds_d > 64 * 1024) {
@@ -1929,15 +1782,15 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   const int32_t set = ctx->eset_i;
   ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
   EmitSet &es = ctx->eset[set];
+  const int64_t ntiles = (m + ED_T - 1) / ED_T;
   MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
-  MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
+  MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)ntiles));
+  MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)ntiles));
+  MH_TRY(ensure(ctx, ctx->scan_partials_w, scan_lb_scratch_bytes<E3>(ntiles)));
   MH_TRY(ensure(ctx, es.stat, 64));
   if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
-  MH_TRY(ensure(ctx, ctx->scan_partials_w, scan_lb_scratch_bytes<E3>(m + 1)));
   char *stat = (char *)es.stat.p;
   Rec *recs = (Rec *)es.recs.p;
-  E3 *off = (E3 *)es.off.p;
-  int64_t *d_base = (int64_t *)(stat + 48);
   const int64_t *pos0 = (const int64_t *)tp.pos0.p, *pos1 = (const int64_t *)tp.pos1.p;
   const int8_t *fo0 = (const int8_t *)tp.fo0.p;
   HapView hv = view_of(h);
@@ -1952,30 +1805,29 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   HIPCHK(ctx, hipMemsetAsync(stat, 0, 48, ws));
   stage_begin(ctx, "emit_measure");
   QFixed q{nullptr, nullptr, (int32_t)prefix.size(), (int32_t)mid.size()};
-  hipLaunchKernelGGL(k_emit_measure<false>, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, ws, hv, m, pos0, pos1,
-                     fo0, rlen, q, (int32_t)ctx->corrupt_on, recs, (int32_t *)(stat + 32), (uint8_t *)nullptr,
-                     (int32_t *)(stat + 40), 0);
+  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, ws, hv, m, pos0, pos1, fo0, rlen,
+                     q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, (int32_t *)(stat + 32));
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   stage_begin(ctx, "emit_scan");
-  HIPCHK(ctx, device_scan_sum<E3>(ws, m + 1, LoadRec{recs, m}, StoreOff{off, 0}, ctx->scan_partials_w.p, (E3 *)stat));
-  hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (const E3 *)(off + m), (int64_t *)ctx->d_used.p,
-                     (int64_t *)stat, write_fastq2);
-  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, device_scan_sum<E3>(ws, ntiles, LoadTile{(const int4 *)es.tsum.p, ntiles}, StoreTile{(E3 *)es.tpre.p},
+                                  ctx->scan_partials_w.p, (E3 *)stat));
   stage_end(ctx);
   stage_begin(ctx, "emit_write");
-  const int64_t ntiles = (m + ED_T - 1) / ED_T;
-  EdArgs A{hv, m, pos0, pos1, fo0, recs, off, nullptr, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0}, d_base,
-           (int32_t)rlen, win_stride, head, qstride, 0};
-  auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_direct<2, 4, true, true> : k_emit_direct<1, 8, true, true>)
-                             : (write_fastq2 ? k_emit_direct<2, 4, false, true> : k_emit_direct<1, 8, false, true>);
+  TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
+          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride};
+  auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
+                             : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
+  // the unit's totals (cnt digits added), its base (the fill before it) and the fill after it
+  hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (int64_t *)ctx->d_used.p, (int64_t *)stat, write_fastq2);
+  HIPCHK(ctx, hipGetLastError());
   if (ctx->corrupt_on)
-    MH_TRY(launch_cr_inplace(ctx, ws, hv, m, pos0, pos1, fo0, recs, off, (uint2 *)es.crrec.p, (char *)ctx->out1.p,
+    MH_TRY(launch_cr_inplace(ctx, ws, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p, (char *)ctx->out1.p,
                              (char *)ctx->out2.p, write_fastq2 ? 2 : 1, (int32_t)(prefix.size() + mid.size()),
-                             (int32_t)rlen, cc, d_base));
+                             (int32_t)rlen, cc, nullptr, true));
   stage_end(ctx);   // "emit"
   ctx->stage_stream = nullptr;
   HIPCHK(ctx, hipMemcpyAsync(res, stat, 64, hipMemcpyDeviceToHost, ws));

@@ -123,10 +123,11 @@ struct StageTime {
 }  // namespace mh
 
 namespace mh {
-// One set of emission buffers (records, offsets, qname reads-part slots).  Sets rotate so the FASTQ writers of earlier
+// One set of emission buffers (records, tile sums and prefixes, offsets).  Sets rotate so the FASTQ writers of earlier
 // units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
-  DevBuf recs, off, slots;
+  DevBuf recs, off;            // per template: k_emit_measure's records; offsets (LDS-image writer only)
+  DevBuf tsum, tpre;           // per 32-template tile: sums (kept, bytes per file) and their exclusive prefixes
   DevBuf crrec;                // corruption: per record the first base's offset and S (k_cr_recs)
   DevBuf stat;                 // the measure pass's totals (E3 at 0) and maxima (int32[4] at 32)
   int64_t *h_stat = nullptr;   // pinned: stat's readback (64 B), then the qname prefix (+64) and mid (+4160) staged

@@ -2,7 +2,7 @@
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-bytes}
-KRE=${2:-k_emit_direct}
+KRE=${2:-k_emit_tiles}
 i=2
 for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))

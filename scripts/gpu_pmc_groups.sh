@@ -3,7 +3,7 @@
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-grp}
-KRE=${2:-k_emit_direct}
+KRE=${2:-k_emit_tiles}
 i=0
 IFS=';' read -ra GS <<< "$PMC_GROUPS"
 for grp in "${GS[@]}"; do
