@@ -1038,40 +1038,26 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
     __syncthreads();
   }
   // the BQ step of base n of file f for the draw's high 16 bits: entries below h1 (capped at 93), amb when one
-  // equals h1.  LDS: the bucket entry; a flagged bucket walks the row's low threshold bytes up to the next bucket's
-  // count.  Global: bq_walk_g.
+  // equals h1 — or when three or more of the bucket's entries lie below h1 (rare): amb sends the base to the exact
+  // path, whose f64 search gives the same step.  LDS: the bucket entry, then for a flagged bucket the low bytes of
+  // its first three entries from two pair reads, without branches.  Global: bq_walk_g.
   const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
   auto walk = [&](int f, int n, uint32_t h1, bool *amb) -> uint32_t {
     if (!LDS_TAB) return bq_walk_g(cc, f, n, h1, amb);
     const int row = f * rlen + n;
-    const int kb = (int)(h1 >> 8);
-    const uint32_t e = ctab[row * CB_ROW + kb];
+    const uint32_t e = ctab[row * CB_ROW + (int)(h1 >> 8)];
     const uint32_t c = e & 0x7fu;
-    // the low bytes of entry c and, when it lies in the same bucket, of entry c + 1 (else 0xff), one LDS read
-    const uint32_t pr = t8p[row * n_bq + c];
+    // entry c's low byte | entry c + 1's (0xff when outside the bucket) << 8; the same pair of entry c + 1.  A 0xff
+    // stand-in never counts as below, and makes amb conservative when lo = 255 (the exact path decides the same).
+    const uint32_t pa = t8p[row * n_bq + c], pb = t8p[row * n_bq + c + 1];
     const uint32_t lo = h1 & 0xffu;
-    if (!(e & 0x80u)) {
-      *amb = false;
-      return c;
-    }
-    // flagged: entry c lies in the bucket.  A 0xff stand-in for entry c + 1 never counts as below, and makes amb
-    // conservative when lo = 255 (the exact path then decides, with the same result).
-    const uint32_t v0 = pr & 0xffu, v1 = pr >> 8;
-    const bool b0 = v0 < lo, b1 = b0 && v1 < lo;
-    if (!b1) {
-      *amb = b0 ? v1 == lo : v0 == lo;
-      return c + (uint32_t)b0;
-    }
-    // rare: two or more entries of the bucket below h1
-    const uint32_t lim = kb < CB_ROW - 1 ? ctab[row * CB_ROW + kb + 1] & 0x7fu : lim_all;
-    uint32_t bq = c + 2;
-    uint32_t v = bq < lim ? (t8p[row * n_bq + bq] & 0xffu) : 0x100u;
-    while (v < lo) {
-      bq++;
-      v = bq < lim ? (t8p[row * n_bq + bq] & 0xffu) : 0x100u;
-    }
-    *amb = v == lo;
-    return bq;
+    const uint32_t fl = e >> 7;
+    const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = pb >> 8;
+    // (bitwise, not short-circuit: no branches)
+    const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
+    const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);   // the first entry not below h1 so far
+    *amb = (b2 | (fl & (uint32_t)(vn == lo))) != 0u;
+    return c + b0 + b1;
   };
   auto fp = [&](uint32_t bq) -> uint32_t { return LDS_TAB ? fp16[bq] : cc.Fp16[bq]; };
   const uint2 key = make_uint2(cc.k0, cc.k1);
@@ -1198,7 +1184,7 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (ncu <= 0) ncu = 256;
-  const size_t lds = (size_t)2 * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads entry c <= n_bq)
+  const size_t lds = (size_t)2 * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads pairs c + 1 <= n_bq + 1)
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
@@ -1355,10 +1341,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     return E3{t.kept, t.b1 + ds, t.b2 + ds};
   };
   stage_begin(ctx, "emit");
+  // what the writer waits for on the main stream: everything queued there so far, or (a deferred preparation) only
+  // this unit's measure pass and tile scan — not the measure passes of the units prepared after it
+  hipEvent_t writer_dep = nullptr;
   if (have_prep) {
     set = pp.set;
     if (pp.deferred) {   // the measure pass's totals, copied to the set's pinned readback
       const EmitSet &es = ctx->eset[set];
+      writer_dep = es.rb;
       HIPCHK(ctx, hipEventSynchronize(es.rb));
       std::memcpy(&ht, es.h_stat, sizeof(E3));
       std::memcpy(hm4, (const char *)es.h_stat + 32, sizeof(hm4));
@@ -1495,8 +1485,11 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       cnt_base + m < (int64_t)UINT32_MAX) {
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
     // and the next job's sampling overlap it
-    HIPCHK(ctx, hipEventRecord(ctx->ev_ready, st));
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_ready, 0));
+    if (!writer_dep) {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_ready, st));
+      writer_dep = ctx->ev_ready;
+    }
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, writer_dep, 0));
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},

@@ -1423,7 +1423,13 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   }
 
   // ---- per-unit parallel stages (stream-ordered, shared scratch) ------------------------------------------------
-  // units alternate between the two lanes; the second lane forks after the word streams and joins before readback
+  // units alternate between the two lanes; the second lane forks after the word streams and joins before readback.
+  // MH_STAGE_WAIT=1 (experiments): they start only once the FASTQ writers queued earlier (the previous job's) have
+  // drained.  The radix sorts and look-back scans of these stages run several times slower beside a bandwidth-bound
+  // writer than alone, but waiting leaves the writer stream idle instead: the same step time on the pool (14.8 ms
+  // either way), so by default they overlap.
+  static const bool stage_wait = getenv("MH_STAGE_WAIT") && atoi(getenv("MH_STAGE_WAIT"));
+  if (stage_wait && ctx->writer_pending) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_writer, 0));
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
