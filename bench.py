@@ -58,6 +58,11 @@ def parse():
                   help='chr1: the pipelined emission path (mh_emit_async: measure, offsets and writer on the writer '
                        'stream, no host readback) instead of the default (measure on the main stream); the same step '
                        'time on the pool, with the writer sharing the chip with more of the sampling')
+  ap.add_argument('--tumor-normal', action='store_true',
+                  help='BASELINE configs[4] on one GPU: tumor 60x + normal 30x, 2x250 model (1kg-pcr-free), mixed '
+                       'into one FASTQ pair, + the god-aligner BAM records built and coordinate-sorted in HBM')
+  ap.add_argument('--tn-length', type=int, default=50_000_000,
+                  help='--tumor-normal: contig length (a chr1 job at 90x of 2x250 does not fit one GPU with its BAM)')
   ap.add_argument('--genome-scale', type=float, default=1.0,
                   help='N > 1: contig lengths scaled by this (rehearsals of the plan on one GPU; 1 = GRCh37)')
   return ap.parse_args()
@@ -151,6 +156,9 @@ def main():
     run_genome(a, rank, world, local, dist)
     dist.destroy_process_group()
     return
+  if a.tumor_normal:
+    run_tumor_normal(a)
+    return
   run_chr1(a)
 
 
@@ -235,6 +243,71 @@ def run_chr1(a):
     'host_cpus': os.cpu_count(),
   }
   print(json.dumps(out), flush=True)
+
+
+def run_tumor_normal(a):
+  """BASELINE configs[4] (one GPU, a contig of --tn-length): per step, the normal sample at 30x and the tumor sample
+  at 60x (2x250, 1kg-pcr-free) generated into the same FASTQ arenas — the mix — then the god-aligner's perfect BAM
+  from the arenas: every record parsed and encoded (write_perfect_reads, god_aligner.py:153-183) and coordinate-sorted
+  (samtools sort's order) in HBM.  The BAM file itself (host BGZF + BAI) is written once after the timed steps."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from mitty_amd.readmodel import get_read_model
+
+  _, model = get_read_model('1kg-pcr-free.pkl')
+  rlen = int(model['mean_rlen'])
+  L = a.tn_length
+  seq = synth.contig(L, 1000)
+  eng = Engine(0)
+  jobs = []
+  # the tumor's variants: an independent synthetic set of the same density (its own haplotypes)
+  for k, (name, cov, vseed) in enumerate((('NORMAL', 30.0, 2000), ('TUMOR', 60.0, 2001))):
+    copies = synth.copies_soa(synth.variants(seq, vseed))
+    eng.load_region(k, ('1', 0, L), seq)
+    for cpy in range(2):
+      eng.upload_variants(k, cpy, copies[cpy])
+    p, passes = _native.read_model_params(rlen, cov)
+    jobs.append((name, k, copies, p, _native.work_units(a.seed + k, [2], passes)))
+
+  def step():
+    eng.drop_haplotypes()
+    eng.ctx.reset_output()
+    tot = [0, 0, 0]
+    for name, k, copies, p, units in jobs:
+      res = eng.run_units([(ps, k, cpy, s) for ps, (_, cpy, s) in enumerate(units)],
+                          lambda r, c, cp=copies: cp[c], p, rlen, model['cum_tlen'], name, 0, True, 'mitty')
+      for r in res:
+        tot[0] += r[1]
+        tot[1] += r[2]
+        tot[2] += r[3]
+    eng.ctx.bam_set_refs(['1'], [L])
+    eng.ctx.bam_add_output()
+    eng.ctx.bam_sort()
+    return lambda: tuple(tot)
+
+  dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
+  n_rec, bam_bytes = eng.ctx.bam_records()
+  threads = min(16, os.cpu_count() or 1)
+  t0 = time.perf_counter()
+  eng.ctx.bam_write('/dev/null', '@HD\tVN:1.0\tSO:coordinate\n', level=1, threads=threads)
+  bam_file_s = time.perf_counter() - t0
+  eng.close()
+  agg = {}
+  for name, ms in stages:
+    agg[name] = agg.get(name, 0.0) + ms
+  ms_per_step = dt / a.steps * 1e3
+  print(json.dumps({
+    'metric': 'paired 2x250 templates/s, tumor 60x + normal 30x mixed, + god-aligner BAM records sorted in HBM',
+    'value': kept / dt, 'unit': 'templates/s', 'n_gpus': 1, 'steps': a.steps, 'warmup': a.warmup,
+    'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+    'dtype': 'int64+u8', 'data': 'synthetic contig + two independent synthetic variant sets (mitty_amd.synth)',
+    'config': {'workload': 'generate-reads tumor/normal mix (BASELINE configs[4], one GPU, {} bp contig)'.format(L),
+               'read_model': '1kg-pcr-free', 'coverage': {'TUMOR': 60, 'NORMAL': 30},
+               'templates_per_step': kept // a.steps, 'bam_records_per_step': n_rec},
+    'bam_bytes_per_step': bam_bytes, 'fastq_bytes_per_step': (b1 + b2) // a.steps,
+    'bam_file_after_timing': {'seconds': bam_file_s, 'level': 1, 'threads': threads, 'sink': '/dev/null'},
+    'stage_ms': {k: round(v / a.steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])},
+    'host_cpus': os.cpu_count()}), flush=True)
 
 
 def end_to_end(a, seq, recs, model, kept_per_job):

@@ -191,13 +191,16 @@ int32_t mh_read_batch(mh_ctx *ctx, int32_t slot, const int64_t *p, const int64_t
  *                       longer than 254 characters, chroms missing from the header and unparseable qnames are
  *                       MH_E_ARG (the reference raises in pysam / parse_qname)
  *   mh_bam_add_output   the same from this context's FASTQ arenas (mh_emit_reads output, no host round trip)
- *   mh_bam_write        sort, write `bam_path` (BGZF, deflate `level` 0..9 on `threads` host threads) with the
+ *   mh_bam_sort         the coordinate sort alone, in HBM (samtools sort's order, god_aligner.py:117-127); done once
+ *                       per store (mh_bam_write reuses it), undone by the next mh_bam_add_*
+ *   mh_bam_write        sort (unless sorted), write `bam_path` (BGZF, deflate `level` 0..9 on `threads` host threads) with the
  *                       header text, and the BAI at `bai_path` (NULL = none) */
 int32_t mh_bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);
 int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2,
                          int64_t max_templates, int64_t *used1, int64_t *used2, int64_t *templates);
 int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates);
 int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes);
+int32_t mh_bam_sort(mh_ctx *ctx);
 int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);

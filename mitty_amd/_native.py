@@ -22,7 +22,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
+           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
 
@@ -92,6 +92,7 @@ def lib():
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
   _sig(L, 'mh_bam_reset', [c_vp])
+  _sig(L, 'mh_bam_sort', [c_vp])
   _sig(L, 'mh_corrupt_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_bgzf_compress', [c_vp, c_i64, c_i32, c_i32, c_vp, c_i64, P_i64])
   _sig(L, 'mh_bgzf_eof', [c_vp])
@@ -603,6 +604,10 @@ class Context:
 
   def bam_reset(self):
     self._chk(self._L.mh_bam_reset(self._h))
+
+  def bam_sort(self):
+    """Coordinate-sort the record store in HBM (mh_bam_write reuses the result)."""
+    self._chk(self._L.mh_bam_sort(self._h))
 
   def corrupt_fastq(self, fq1, fq2=None, t_base=0):
     """Corrupt the complete templates of FASTQ byte buffers into the arenas.  Returns (used1, used2, templates)."""

@@ -1040,10 +1040,17 @@ int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char 
                        fq2 ? len2 : 0, t_base, used1, used2, templates);
 }
 
+int32_t mh_bam_sort(mh_ctx *ctx) {
+  CTX_GUARD(ctx);
+  if (!ctx->bam.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  return bam_sort(ctx);
+}
+
 int32_t mh_bam_reset(mh_ctx *ctx) {
   if (!ctx) return MH_E_ARG;
   ctx->bam.n_rec = ctx->bam.bytes = 0;
   ctx->bam.n_files = 0;
+  ctx->bam.sorted = false;
   return MH_OK;
 }
 

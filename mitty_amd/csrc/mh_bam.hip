@@ -2,7 +2,7 @@
 // device: SURVEY.md §8(a) A16 / §8(f) rank 1.
 //
 //   FASTQ bytes (host chunks, or the context's own FASTQ arenas)
-//     -> newline positions           (SWAR '\n' count per 16-byte chunk, one device scan, positions stored)
+//     -> newline positions           (SWAR '\n' count per 64-byte chunk, a look-back scan, positions stored)
 //     -> k_bam_parse                 (thread per template: parse_qname of file 1's name (readgenerate.py:259-291),
 //                                     the CIGAR, tid from the @SQ names, seq / qual spans; BAM record sizes)
 //     -> scan of record sizes        (appends to the resident record store)
@@ -53,15 +53,22 @@ __device__ __forceinline__ uint32_t nl_mask4(uint32_t v) {   // 0x80 in every by
   return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
 }
 
+// element t = the 64 bytes [64 t, 64 t + 64) of the buffer
+constexpr int NL_CH = 64;
 struct LoadNL {
   const uint8_t *b;
   int64_t len;
   __device__ int64_t operator()(int64_t t) const {
-    const int64_t o = t * 16;
+    const int64_t o = t * NL_CH;
     if (o >= len) return 0;
-    if (o + 16 <= len) {
-      uint4 v = *(const uint4 *)(b + o);
-      return __popc(nl_mask4(v.x)) + __popc(nl_mask4(v.y)) + __popc(nl_mask4(v.z)) + __popc(nl_mask4(v.w));
+    if (o + NL_CH <= len) {
+      int64_t c = 0;
+#pragma unroll
+      for (int q = 0; q < NL_CH / 16; q++) {
+        const uint4 v = *(const uint4 *)(b + o + 16 * q);
+        c += __popc(nl_mask4(v.x)) + __popc(nl_mask4(v.y)) + __popc(nl_mask4(v.z)) + __popc(nl_mask4(v.w));
+      }
+      return c;
     }
     int64_t c = 0;
     for (int64_t i = o; i < len; i++) c += b[i] == '\n';
@@ -74,18 +81,21 @@ struct StoreNL {
   int64_t len;
   int64_t *nl;
   __device__ void operator()(int64_t t, int64_t, int64_t excl) const {
-    const int64_t o = t * 16;
+    const int64_t o = t * NL_CH;
     if (o >= len) return;
-    if (o + 16 <= len) {
-      uint4 v = *(const uint4 *)(b + o);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (o + NL_CH <= len) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint32_t m = nl_mask4(w[k]);
-        while (m) {
-          int bit = __ffs(m) - 1;
-          nl[excl++] = o + 4 * k + (bit >> 3);
-          m &= m - 1;
+      for (int q = 0; q < NL_CH / 16; q++) {
+        const uint4 v = *(const uint4 *)(b + o + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint32_t m = nl_mask4(w[k]);
+          while (m) {
+            const int bit = __ffs(m) - 1;
+            nl[excl++] = o + 16 * q + 4 * k + (bit >> 3);
+            m &= m - 1;
+          }
         }
       }
       return;
@@ -142,21 +152,47 @@ struct ParseArgs {
   const char *names;          // @SQ names, concatenated
   const int32_t *name_off;    // [n_refs + 1]
   int32_t n_refs;
+  int64_t len0;               // bytes of file 1's buffer
 };
 
 __device__ __forceinline__ int64_t line_start(const int64_t *nl, int64_t line) { return line == 0 ? 0 : nl[line - 1] + 1; }
 
+// The name lines of a workgroup's 256 templates are first staged in LDS (a wave copies its 64 lines with one 16-byte
+// load per lane per line, all in flight together), so the per-template parse below reads LDS, not a chain of
+// dependent global byte loads.  A line longer than its LDS row is read from memory.
+constexpr int BP_ROW = 192;
+
 __global__ void __launch_bounds__(256) k_bam_parse(ParseArgs a, int64_t T, BamTpl *tpl, int32_t *err) {
+  __shared__ __attribute__((aligned(16))) uint8_t rows[256 * BP_ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t tw = (int64_t)blockIdx.x * 256 + 64 * wave;   // the wave's first template
+  {
+    const int64_t tl = tw + lane;
+    const int64_t ls0 = tl < T ? line_start(a.nl[0], 4 * tl) : 0, le0 = tl < T ? a.nl[0][4 * tl] : 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+      const int64_t s0 = __shfl(ls0, j, 64), e0 = __shfl(le0, j, 64);
+      const int64_t c0 = s0 & ~(int64_t)15;
+      const int nch = (int)((e0 - c0 + 15) >> 4);
+      if (tw + j < T && nch * 16 <= BP_ROW && c0 + 16 * nch <= a.len0 && lane < nch)
+        *(uint4 *)(rows + (64 * wave + j) * BP_ROW + 16 * lane) = *(const uint4 *)(a.b[0] + c0 + 16 * lane);
+    }
+  }
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
   BamTpl o;
-  const uint8_t *b0 = a.b[0];
   const int64_t s0 = line_start(a.nl[0], 4 * t);
   const int64_t e0 = a.nl[0][4 * t];
+  const int64_t c0 = s0 & ~(int64_t)15;
+  const int nch = (int)((e0 - c0 + 15) >> 4);
+  const bool staged = nch * 16 <= BP_ROW && c0 + 16 * nch <= a.len0;
+  // lp: the line's first byte (LDS row or the buffer itself); lp[x - s0] = file byte x
+  const uint8_t *lp = staged ? rows + threadIdx.x * BP_ROW + (s0 - c0) : a.b[0] + s0;
   int32_t e = 0;
-  if (e0 <= s0 || b0[s0] != '@') e |= BE_QNAME;
+  if (e0 <= s0 || lp[0] != '@') e |= BE_QNAME;
   int64_t q0 = s0 + 1, q1 = q0;
-  while (q1 < e0 && b0[q1] != ' ' && b0[q1] != '\t') q1++;   // FastxFile name: up to the first whitespace
+  while (q1 < e0 && lp[q1 - s0] != ' ' && lp[q1 - s0] != '\t') q1++;   // FastxFile name: up to the first whitespace
   o.qn_off = q0;
   o.qn_len = (int32_t)(q1 - q0);
   if (o.qn_len > 254) e |= BE_QNAME_LEN;
@@ -167,7 +203,7 @@ __global__ void __launch_bounds__(256) k_bam_parse(ParseArgs a, int64_t T, BamTp
   {
     int64_t st = q0;
     for (int64_t i = q0; i <= q1 && nf < 3 + 5 * BAM_MAX_READS; i++) {
-      if (i == q1 || b0[i] == '|') {
+      if (i == q1 || lp[i - s0] == '|') {
         fs[nf] = (int32_t)(st - q0);
         fe[nf] = (int32_t)(i - q0);
         nf++;
@@ -176,7 +212,7 @@ __global__ void __launch_bounds__(256) k_bam_parse(ParseArgs a, int64_t T, BamTp
     }
   }
   if (nf < 3 + 5 * a.n_files - 1) e |= BE_FIELDS;   // the last read's v_list may be the (empty) tail
-  const uint8_t *qn = b0 + q0;
+  const uint8_t *qn = lp + (q0 - s0);
   // chrom -> tid
   int32_t tid = -1;
   if (!(e & BE_FIELDS)) {
@@ -251,22 +287,23 @@ struct StoreOff64 {
   __device__ void operator()(int64_t i, int64_t, int64_t excl) const { off[i] = base + excl; }
 };
 
-__device__ __forceinline__ uint8_t nt16(uint8_t c) {   // htslib seq_nt16_table
-  switch (c | 0x20) {
-    case 'a': return 1; case 'c': return 2; case 'm': return 3; case 'g': return 4; case 'r': return 5;
-    case 's': return 6; case 'v': return 7; case 't': case 'u': return 8; case 'w': return 9; case 'y': return 10;
-    case 'h': return 11; case 'k': return 12; case 'd': return 13; case 'b': return 14;
-    default: return c == '=' ? 0 : 15;
-  }
+__device__ __forceinline__ uint8_t nt16(uint8_t c) {   // htslib seq_nt16_table: letters a..z (either case) from
+  // two nibble tables (selects, no branches or table loads), '=' 0, anything else 15
+  const uint32_t x = (uint32_t)(c | 0x20) - 'a';
+  const uint64_t lo = 0xfff3fcffb4ffd2e1ull, hi = 0xfaf978865full;
+  const uint32_t v = (uint32_t)((x < 16 ? lo >> ((4 * x) & 63) : hi >> ((4 * (x - 16)) & 63)) & 15u);
+  return (uint8_t)(x < 26 ? v : c == '=' ? 0u : 15u);
 }
 __device__ __forceinline__ uint8_t comp_atcgn(uint8_t c) {   // str.maketrans('ATCGN', 'TAGCN')
   return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'C' ? 'G' : c == 'G' ? 'C' : c;
 }
 
-// One wave per record.  Records are byte-packed (BAM has no padding), so stores are bytewise.
+// One wave per record.  Records are byte-packed (BAM has no padding), so stores are bytewise; every input byte the
+// wave needs is loaded by the lanes together (restrict pointers let the loads of an unrolled loop issue ahead of the
+// stores), and the CIGAR text is walked from registers (shuffles), not from memory.
 __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tpl, int64_t n_rec, int32_t nr,
-                                                   const int64_t *off, int64_t off_base, uint8_t *out, uint64_t *key,
-                                                   uint32_t *val, RInfo *info, int64_t rec_base) {
+                                                   const int64_t *off, uint8_t *out, uint64_t *key, uint32_t *val,
+                                                   RInfo *info, int64_t rec_base) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (i >= n_rec) return;
@@ -275,8 +312,8 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   const BamTpl &T = tpl[t];
   const BamRead &r = T.r[s];
   const BamRead &m = T.r[nr == 2 ? 1 - s : s];
-  uint8_t *d = out + (off[i] - off_base);
-  const uint8_t *qn = a.b[0] + T.qn_off;
+  uint8_t *__restrict__ d = out + off[i];
+  const uint8_t *__restrict__ qn = a.b[0] + T.qn_off;
   const int32_t lq = T.qn_len + 1;
   const int32_t hdr = 36;
   if (lane < 9) {
@@ -295,35 +332,61 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
     uint8_t *p = d + 4 * lane;
     p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
   }
-  for (int32_t k = lane; k < lq; k += 64) d[hdr + k] = k < T.qn_len ? qn[k] : 0;
-  // CIGAR: lane 0 walks the text (short), writes packed ops
-  uint8_t *dc = d + hdr + lq;
-  if (lane == 0) {
-    uint32_t num = 0;
-    int j = 0;
-    for (int32_t k = r.cig_off; k < r.cig_off + r.cig_len; k++) {
-      uint32_t dd = (uint32_t)qn[k] - '0';
-      if (dd <= 9) { num = num * 10 + dd; continue; }
-      uint32_t w = num << 4 | (uint32_t)cigar_code(qn[k]);
-      dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
-      dc[4 * j + 3] = (uint8_t)(w >> 24);
-      j++;
-      num = 0;
-    }
-  }
-  const uint8_t *sq = a.b[s] + r.seq_off, *ql = a.b[s] + r.qual_off;
+  const uint8_t *__restrict__ sq = a.b[s] + r.seq_off, *__restrict__ ql = a.b[s] + r.qual_off;
   const int32_t L = r.l_seq;
   const bool rev = r.flag & 0x10;
-  uint8_t *ds = dc + 4 * r.n_cig;
-  for (int32_t k = lane; k < (L + 1) / 2; k += 64) {
-    const int32_t i0 = 2 * k, i1 = 2 * k + 1;
-    uint8_t c0 = rev ? comp_atcgn(sq[L - 1 - i0]) : sq[i0];
-    uint8_t hi = nt16(c0), lo = 0;
-    if (i1 < L) lo = nt16(rev ? comp_atcgn(sq[L - 1 - i1]) : sq[i1]);
-    ds[k] = (uint8_t)(hi << 4 | lo);
+  // every load first: qname, CIGAR text, bases, qualities (up to 4 x 64 bytes each per pass)
+  uint8_t qb[4], cb, sb0[4], sb1[4], qv[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int32_t k = lane + 64 * u;
+    qb[u] = k < T.qn_len ? qn[k] : 0;
   }
+  cb = lane < r.cig_len ? qn[r.cig_off + lane] : 0;
+  uint8_t *dc = d + hdr + lq;
+  uint8_t *ds = dc + 4 * r.n_cig;
   uint8_t *dq = ds + (L + 1) / 2;
-  for (int32_t k = lane; k < L; k += 64) dq[k] = (uint8_t)((rev ? ql[L - 1 - k] : ql[k]) - 33);
+  for (int32_t k0 = 0; k0 < L; k0 += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t k = k0 + lane + 64 * u;          // quality k
+      const int32_t j = k0 / 2 + lane + 64 * u;      // seq byte j: bases 2j, 2j + 1
+      qv[u] = k < L ? (rev ? ql[L - 1 - k] : ql[k]) : 0;
+      sb0[u] = 2 * j < L ? (rev ? sq[L - 1 - 2 * j] : sq[2 * j]) : 0;
+      sb1[u] = 2 * j + 1 < L ? (rev ? sq[L - 2 - 2 * j] : sq[2 * j + 1]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t k = k0 + lane + 64 * u, j = k0 / 2 + lane + 64 * u;
+      if (k < L) dq[k] = (uint8_t)(qv[u] - 33);
+      if (j < (L + 1) / 2 && j < k0 / 2 + 128) {
+        const uint8_t c0 = rev ? comp_atcgn(sb0[u]) : sb0[u];
+        const uint8_t lo = 2 * j + 1 < L ? nt16(rev ? comp_atcgn(sb1[u]) : sb1[u]) : 0;
+        ds[j] = (uint8_t)(nt16(c0) << 4 | lo);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int32_t k = lane + 64 * u;
+    if (k < lq) d[hdr + k] = qb[u];
+  }
+  for (int32_t k = lane + 256; k < lq; k += 64) d[hdr + k] = k < T.qn_len ? qn[k] : 0;   // names > 256 bytes
+  // CIGAR: ops packed from the text in registers (lane 0 writes; a text longer than 64 bytes continues from memory)
+  uint32_t num = 0;
+  int j = 0;
+  for (int32_t k = 0; k < r.cig_len; k++) {
+    const uint8_t c = k < 64 ? (uint8_t)__shfl((int)cb, k, 64) : qn[r.cig_off + k];
+    const uint32_t dd = (uint32_t)c - '0';
+    if (dd <= 9) { num = num * 10 + dd; continue; }
+    if (lane == 0) {
+      const uint32_t w = num << 4 | (uint32_t)cigar_code(c);
+      dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
+      dc[4 * j + 3] = (uint8_t)(w >> 24);
+    }
+    j++;
+    num = 0;
+  }
   if (lane == 0) {
     key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
     val[i] = (uint32_t)(rec_base + i);
@@ -351,9 +414,21 @@ __global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const in
   if (k >= n) return;
   const uint32_t r = val[k];
   const int64_t a = roff[r], len = roff[r + 1] - a;
-  const uint8_t *s = src + a;
-  uint8_t *d = dst + soff[k];
-  for (int64_t j = lane; j < len; j += 64) d[j] = s[j];
+  const uint8_t *__restrict__ s = src + a;
+  uint8_t *__restrict__ d = dst + soff[k];
+  for (int64_t j0 = 0; j0 < len; j0 += 512) {   // eight loads in flight per lane, then the stores
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t j = j0 + lane + 64 * u;
+      v[u] = j < len ? s[j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t j = j0 + lane + 64 * u;
+      if (j < len) d[j] = v[u];
+    }
+  }
   if (lane == 0) sinfo[k] = info[r];
 }
 
@@ -382,6 +457,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
   B.n_rec = 0;
   B.bytes = 0;
   B.n_files = 0;
+  B.sorted = false;
   B.refs_set = true;
   return MH_OK;
 }
@@ -389,10 +465,11 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
 // Newline index of a device buffer into `nl` (grown as needed); returns the count.
 int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count) {
   hipStream_t st = ctx->stream;
-  const int64_t chunks = (len + 15) / 16;
+  const int64_t chunks = (len + NL_CH - 1) / NL_CH;
   *count = 0;
   if (len == 0) return MH_OK;
-  MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(chunks) + 64));
+  MH_TRY(ensure(ctx, ctx->scan_partials, std::max<size_t>(sizeof(int64_t) * scan_partials_count(chunks) + 64,
+                                                          scan_lb_scratch_bytes<int64_t>(chunks))));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   int64_t *tot = (int64_t *)ctx->d_small.p;
   HIPCHK(ctx, device_reduce<int64_t>(st, chunks, LoadNL{b, len}, OpSum{}, (int64_t)0,
@@ -401,8 +478,9 @@ int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, in
   HIPCHK(ctx, hipMemcpyAsync(&n, tot, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
   MH_TRY(ensure(ctx, nl, sizeof(int64_t) * (n + 1)));
-  HIPCHK(ctx, device_scan<int64_t>(st, chunks, LoadNL{b, len}, StoreNL{b, len, (int64_t *)nl.p}, OpSum{}, (int64_t)0,
-                                   (int64_t *)ctx->scan_partials.p, tot));
+  // single pass (decoupled look-back): each element's bytes are re-read by the thread that counted them
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, chunks, LoadNL{b, len}, StoreNL{b, len, (int64_t *)nl.p},
+                                       ctx->scan_partials.p, tot + 1));
   *count = n;
   return MH_OK;
 }
@@ -431,7 +509,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int32_t *err = (int32_t *)((char *)ctx->d_small.p + 64);
   HIPCHK(ctx, hipMemsetAsync(err, 0, 4, st));
   ParseArgs a{{d1, d2}, {(const int64_t *)B.nl1.p, d2 ? (const int64_t *)B.nl2.p : nullptr}, nf,
-              (const char *)B.names.p, (const int32_t *)B.name_off.p, (int32_t)B.ref_names.size()};
+              (const char *)B.names.p, (const int32_t *)B.name_off.p, (int32_t)B.ref_names.size(), len1};
   stage_begin(ctx, "bam_parse");
   hipLaunchKernelGGL(k_bam_parse, dim3(grid_for(T, 256, INT32_MAX)), dim3(256), 0, st, a, T, (BamTpl *)B.tpl.p, err);
   HIPCHK(ctx, hipGetLastError());
@@ -467,7 +545,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n_rec), sizeof(RInfo) * B.n_rec));
   stage_begin(ctx, "bam_write");
   hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n_rec * 64, 256, INT32_MAX)), dim3(256), 0, st, a,
-                     (const BamTpl *)B.tpl.p, n_rec, nf, (const int64_t *)roff, (int64_t)0, (uint8_t *)B.recs.p,
+                     (const BamTpl *)B.tpl.p, n_rec, nf, (const int64_t *)roff, (uint8_t *)B.recs.p,
                      (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
                      B.n_rec);
   HIPCHK(ctx, hipGetLastError());
@@ -475,6 +553,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   HIPCHK(ctx, hipStreamSynchronize(st));
   B.n_rec += n_rec;
   B.bytes += add_bytes;
+  B.sorted = false;
   int64_t last1 = 0, last2 = 0;
   HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
   if (d2) HIPCHK(ctx, hipMemcpyAsync(&last2, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
@@ -489,7 +568,7 @@ int32_t bam_sort(mh_ctx *ctx) {
   BamStore &B = ctx->bam;
   hipStream_t st = ctx->stream;
   const int64_t n = B.n_rec;
-  if (n == 0) return MH_OK;
+  if (n == 0 || B.sorted) return MH_OK;
   if (n >= (int64_t)UINT32_MAX) return arg_fail(ctx, MH_E_CAPACITY, "more than 2^32 records in one BAM");
   int tid_bits = 1;
   while ((1ull << tid_bits) < (uint64_t)B.ref_names.size() + 1) tid_bits++;
@@ -521,6 +600,7 @@ int32_t bam_sort(mh_ctx *ctx) {
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   HIPCHK(ctx, hipStreamSynchronize(st));
+  B.sorted = true;
   return MH_OK;
 }
 
@@ -544,6 +624,7 @@ void bam_release(BamStore &B) {
   B.n_rec = B.bytes = 0;
   B.n_files = 0;
   B.refs_set = false;
+  B.sorted = false;
 }
 
 }  // namespace mh

@@ -113,6 +113,7 @@ struct BamStore {
   DevBuf key2, val2, sort_tmp, soff, srecs, sinfo;   // sorted
   int64_t n_rec = 0, bytes = 0;
   int32_t n_files = 0;
+  bool sorted = false;         // srecs/soff/sinfo hold the current store in coordinate order
 };
 
 struct StageTime {

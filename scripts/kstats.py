@@ -12,4 +12,4 @@ for x in rows[:top]:
     n = re.sub(r'rocprim::ROCPRIM_\w+::', 'rp::', n)
     n = re.sub(r'rp::detail::trampoline_kernel<.*?(onesweep_\w+|transform|histogram)\w*.*', r'rocprim \1', n)
     print(f"{float(x['TotalDurationNs']) / 1e6 / steps:8.3f} ms/step  calls {int(x['Calls']) / steps:5.1f}  "
-          f"avg {float(x['AverageNs']) / 1e3:8.1f} us  {n[:80]}")
+          f"avg {float(x['AverageNs']) / 1e3:8.1f} us  min {float(x['MinNs']) / 1e3:8.1f} us  {n[:70]}")

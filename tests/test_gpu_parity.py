@@ -1019,6 +1019,55 @@ def test_god_aligner_from_device_arenas(native, tmp_path):
   assert recs_a == recs_b
 
 
+def test_tumor_normal_mix_god_aligner(native, tmp_path):
+  """BASELINE configs[4] in small: a normal (sample S0, 6x) and a tumor (S1, 12x, the VCF's other sample) run of the
+  2x250 model into the same device arenas — the mix is the two runs' FASTQ one after the other, each sample named in
+  its qnames (Readme.md:14-16) — then the perfect BAM built from the arenas (parse, encode, coordinate sort in HBM).
+  The FASTQ equals the oracle's two runs concatenated; the BAM records equal the oracle god-aligner's over it."""
+  from mitty_amd.engine import Engine
+  from mitty_amd.lib import fasta as mfasta, vcfio
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  from oracle import god
+  from oracle import oracle as O
+  c = G.load_json('e2e_config.json')['1kg-pcr-free']
+  mod, mdl = get_read_model('1kg-pcr-free.pkl')
+  seqs = mfasta.read_fasta(G.path(c['fasta']))
+  runs = (('S0', 6.0, 11), ('S1', 12.0, 12))
+  want1, want2 = b'', b''
+  eng = Engine(0)
+  try:
+    ri0 = 0
+    for sample, cov, seed in runs:
+      rm = mod.read_model_params(mdl, cov)
+      vdf = vcfio.load_variants_soa(G.path(c['vcf']), sample, G.path(c['bed']))
+      for k, reg in enumerate(vdf):   # each sample's regions in their own slots (own haplotypes)
+        eng.load_region(ri0 + k, reg['region'], mfasta.fetch(seqs, *reg['region']))
+      units = [(ps, ri0 + w['region_idx'], w['region_cpy'], w['rng_seed'])
+               for ps, w in enumerate(readgenerate.get_data_for_workers(rm, vdf, seed))]
+      eng.run_units(units, lambda r, cp, v=vdf, o=ri0: v[r - o]['copies'][cp], rm['p'], rm['rlen'], rm['cum_tlen'],
+                    sample)
+      o1, o2, _ = O.generate_reads_fastq(G.path(c['fasta']), G.path(c['vcf']), sample, G.path(c['bed']),
+                                         G.model('1kg-pcr-free'), cov, seed)
+      want1 += o1
+      want2 += o2
+      ri0 += len(vdf)
+    d1, d2 = eng.ctx.fetch_output()
+    G.check_same(d1, want1)
+    G.check_same(d2, want2)
+    assert b'@S0:' in d1 and b'@S1:' in d1
+    eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
+    assert eng.ctx.bam_add_output() == want1.count(b'\n') // 4
+    eng.ctx.bam_sort()
+    bam = str(tmp_path / 'tn.bam')
+    eng.ctx.bam_write(bam, '@HD\tVN:1.0\n', bai_path=bam + '.bai')   # the sort above is reused
+  finally:
+    eng.close()
+  _, recs, _, _ = god.record_voffsets(open(bam, 'rb').read())
+  want = god.sorted_stream(god.god_records(want1, want2, {'1': 0, '2': 1, '3': 2}))
+  assert recs == [god.encode(r) for r in want]
+
+
 # ---- standalone corrupt-reads (SURVEY.md §8(f) rank 2) --------------------------------------------------------------
 @pytest.mark.parametrize('rng', ['mitty', 'philox'])
 @pytest.mark.parametrize('model', G.MODELS)
