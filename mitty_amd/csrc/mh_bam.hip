@@ -279,7 +279,9 @@ struct LoadSize {
   const BamTpl *tpl;
   int32_t nr;
   int64_t n;   // records
-  __device__ int64_t operator()(int64_t i) const { return i < n ? tpl[i / nr].r[i % nr].size : 0; }
+  __device__ int64_t operator()(int64_t i) const {   // nr is 1 or 2: shifts, not 64-bit divisions
+    return i < n ? (nr == 2 ? tpl[i >> 1].r[i & 1] : tpl[i].r[0]).size : 0;
+  }
 };
 struct StoreOff64 {
   int64_t *off;
@@ -307,8 +309,8 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (i >= n_rec) return;
-  const int64_t t = i / nr;
-  const int s = (int)(i % nr);
+  const int64_t t = nr == 2 ? i >> 1 : i;   // nr is 1 or 2
+  const int s = nr == 2 ? (int)(i & 1) : 0;
   const BamTpl &T = tpl[t];
   const BamRead &r = T.r[s];
   const BamRead &m = T.r[nr == 2 ? 1 - s : s];
@@ -346,20 +348,26 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   uint8_t *dc = d + hdr + lq;
   uint8_t *ds = dc + 4 * r.n_cig;
   uint8_t *dq = ds + (L + 1) / 2;
+  // loads in ascending address order across the lanes for both strands (a strand-1 read is reversed by where each
+  // lane stores, not by which byte it loads: descending lane addresses do not coalesce)
+  const int32_t J = (L + 1) / 2;   // sequence bytes
   for (int32_t k0 = 0; k0 < L; k0 += 256) {
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int32_t k = k0 + lane + 64 * u;          // quality k
-      const int32_t j = k0 / 2 + lane + 64 * u;      // seq byte j: bases 2j, 2j + 1
-      qv[u] = k < L ? (rev ? ql[L - 1 - k] : ql[k]) : 0;
-      sb0[u] = 2 * j < L ? (rev ? sq[L - 1 - 2 * j] : sq[2 * j]) : 0;
-      sb1[u] = 2 * j + 1 < L ? (rev ? sq[L - 2 - 2 * j] : sq[2 * j + 1]) : 0;
+      const int32_t y = k0 + lane + 64 * u;            // quality byte loaded
+      const int32_t jx = k0 / 2 + lane + 64 * u;       // sequence byte, in load order
+      const int32_t j = rev ? J - 1 - jx : jx;         // ... its output index: bases 2j, 2j + 1
+      const bool jv = jx < J && jx < k0 / 2 + 128;
+      qv[u] = y < L ? ql[y] : 0;
+      sb0[u] = jv ? sq[rev ? L - 1 - 2 * j : 2 * j] : 0;
+      sb1[u] = jv && 2 * j + 1 < L ? sq[rev ? L - 2 - 2 * j : 2 * j + 1] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int32_t k = k0 + lane + 64 * u, j = k0 / 2 + lane + 64 * u;
-      if (k < L) dq[k] = (uint8_t)(qv[u] - 33);
-      if (j < (L + 1) / 2 && j < k0 / 2 + 128) {
+      const int32_t y = k0 + lane + 64 * u, jx = k0 / 2 + lane + 64 * u;
+      if (y < L) dq[rev ? L - 1 - y : y] = (uint8_t)(qv[u] - 33);
+      if (jx < J && jx < k0 / 2 + 128) {
+        const int32_t j = rev ? J - 1 - jx : jx;
         const uint8_t c0 = rev ? comp_atcgn(sb0[u]) : sb0[u];
         const uint8_t lo = 2 * j + 1 < L ? nt16(rev ? comp_atcgn(sb1[u]) : sb1[u]) : 0;
         ds[j] = (uint8_t)(nt16(c0) << 4 | lo);
@@ -372,20 +380,42 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
     if (k < lq) d[hdr + k] = qb[u];
   }
   for (int32_t k = lane + 256; k < lq; k += 64) d[hdr + k] = k < T.qn_len ? qn[k] : 0;   // names > 256 bytes
-  // CIGAR: ops packed from the text in registers (lane 0 writes; a text longer than 64 bytes continues from memory)
-  uint32_t num = 0;
-  int j = 0;
-  for (int32_t k = 0; k < r.cig_len; k++) {
-    const uint8_t c = k < 64 ? (uint8_t)__shfl((int)cb, k, 64) : qn[r.cig_off + k];
-    const uint32_t dd = (uint32_t)c - '0';
-    if (dd <= 9) { num = num * 10 + dd; continue; }
-    if (lane == 0) {
-      const uint32_t w = num << 4 | (uint32_t)cigar_code(c);
+  // CIGAR: lane k holds text byte k; every op lane packs its own op from the digits since the previous op (ballot +
+  // shuffles, no serial walk).  A text longer than 64 bytes is walked serially from memory.
+  if (r.cig_len <= 64) {
+    const bool is_op = lane < r.cig_len && (uint32_t)cb - '0' > 9;
+    const uint64_t ops = __ballot(is_op);
+    const uint64_t below = lane ? ops & ((~0ull) >> (64 - lane)) : 0ull;
+    const int prev = below ? 63 - __builtin_clzll(below) : -1;   // the previous op's lane
+    uint32_t num = 0;
+    const int nd = is_op ? lane - prev - 1 : 0;
+    const int ndmax = __reduce_max_sync(~0ull, nd);
+    for (int q = 0; q < ndmax; q++) {   // the digits prev + 1 .. lane - 1, most significant first
+      const int src = prev + 1 + q;
+      const uint32_t dgt = (uint32_t)__shfl((int)cb, src < 64 ? (src > 0 ? src : 0) : 63, 64) - '0';
+      if (q < nd) num = num * 10 + dgt;
+    }
+    if (is_op) {
+      const int j = __popcll(below);
+      const uint32_t w = num << 4 | (uint32_t)cigar_code(cb);
       dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
       dc[4 * j + 3] = (uint8_t)(w >> 24);
     }
-    j++;
-    num = 0;
+  } else {
+    uint32_t num = 0;
+    int j = 0;
+    for (int32_t k = 0; k < r.cig_len; k++) {
+      const uint8_t c = qn[r.cig_off + k];
+      const uint32_t dd = (uint32_t)c - '0';
+      if (dd <= 9) { num = num * 10 + dd; continue; }
+      if (lane == 0) {
+        const uint32_t w = num << 4 | (uint32_t)cigar_code(c);
+        dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
+        dc[4 * j + 3] = (uint8_t)(w >> 24);
+      }
+      j++;
+      num = 0;
+    }
   }
   if (lane == 0) {
     key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
