@@ -18,3 +18,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
   python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
 echo prof ok
+timeout -k 10 400 python -u bench.py --tumor-normal --steps 3 --warmup 1 > gpurun_out/benchtn_$TAG.log 2>&1 || exit $?
+tail -1 gpurun_out/benchtn_$TAG.log | cut -c1-300
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_proftn -o run -- \
+  python3 bench.py --tumor-normal --steps 2 --warmup 1 > gpurun_out/${TAG}_proftn.log 2>&1 || exit $?
+echo proftn ok
