@@ -1369,7 +1369,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       return arg_fail(ctx, MH_E_STATE, "more units prepared than emission buffer sets (emit the prepared units first)");
     }
     ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
-    if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
+    if (es.busy) {
+      gate_open_for(ctx, es.done_gate);
+      HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
+    }
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
     MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)ntiles));
     MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)ntiles));
@@ -1453,6 +1456,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + (size_t)EW_T * 2 * win_stride + 2 * (size_t)(cap + 16);
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on && es.crrec.cap < 16 * (size_t)m + 64) {   // corruption switched on after this unit's measure
+    gate_open(ctx);
     HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
     MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
   }
@@ -1490,6 +1494,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       writer_dep = ctx->ev_ready;
     }
     HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, writer_dep, 0));
+    // the writer gate: this job's writers from the gate_at-th on wait for the next job's sorts (mh_internal.h)
+    if (ctx->gate && ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at && ctx->job > 0) {
+      if (gate_debug()) fprintf(stderr, "mh gate: writer %d of job %u waits for %u\n", ctx->writers_in_job, ctx->job,
+                                ctx->job + 1);
+      HIPCHK(ctx, hipStreamWaitValue32(ctx->wstream, ctx->gate, ctx->job + 1, hipStreamWaitValueGte, 0xffffffffu));
+      if (ctx->job + 1 > ctx->gate_waited) ctx->gate_waited = ctx->job + 1;
+    }
+    ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
@@ -1507,9 +1519,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
+    es.done_gate = ctx->gate_waited;
     HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ctx->wstream));
-    MH_TRY(mark_used(ctx, h.used, h.used_set));     // the haplotype and the templates stay live until then
-    MH_TRY(mark_used(ctx, tp.used, tp.used_set));
+    MH_TRY(mark_used(ctx, h.used, h.used_set, h.used_gate));     // the haplotype and the templates stay live until then
+    MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
     es.busy = true;
     ctx->writer_pending = true;
   } else {
@@ -1652,6 +1665,7 @@ __global__ void k_set_used(int64_t *d_used, int64_t u1, int64_t u2) {
 
 int32_t sync_async_fill(mh_ctx *ctx) {
   if (!ctx->async_pending) return MH_OK;
+  gate_open(ctx);
   HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
   int64_t u[2] = {0, 0};
   HIPCHK(ctx, hipMemcpy(u, ctx->d_used.p, 16, hipMemcpyDeviceToHost));
@@ -1677,6 +1691,7 @@ int32_t output_reset(mh_ctx *ctx) {
 
 int32_t emit_result(mh_ctx *ctx, int32_t t, int64_t *out) {
   if (t < 0 || t >= mh_ctx::RES_N || ctx->res_state[t] == 0) return arg_fail(ctx, MH_E_ARG, "unknown emission ticket");
+  gate_open(ctx);
   if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
   const int64_t *r = ctx->h_res + 8 * t;
   out[0] = r[0];
@@ -1701,6 +1716,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
     for (auto &e : ctx->res_ev) HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   const int32_t t = ctx->res_next;
+  gate_open(ctx);
   if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
   ctx->res_next = (t + 1) % mh_ctx::RES_N;
   int64_t *res = ctx->h_res + 8 * t;
@@ -1827,9 +1843,10 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   HIPCHK(ctx, hipEventRecord(ctx->res_ev[t], ws));
   ctx->res_state[t] = 1;
   HIPCHK(ctx, hipEventRecord(es.done, ws));
+  es.done_gate = ctx->gate_waited;
   HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ws));
-  MH_TRY(mark_used(ctx, h.used, h.used_set));
-  MH_TRY(mark_used(ctx, tp.used, tp.used_set));
+  MH_TRY(mark_used(ctx, h.used, h.used_set, h.used_gate));
+  MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
   es.busy = true;
   ctx->writer_pending = true;
   *ticket = t;

@@ -53,6 +53,7 @@ struct Hap {
   bool valid = false;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
+  mutable uint32_t used_gate = 0;      // the gate value that writer needs
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
   DevBuf nd;    // Node16 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
@@ -82,6 +83,7 @@ struct TplSet {
   mutable EmitPrep prep;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
+  mutable uint32_t used_gate = 0;      // the gate value that writer needs
   int64_t n = 0;
   int32_t rlen = 0;
   bool valid = false;
@@ -134,6 +136,7 @@ struct EmitSet {
   int64_t *h_stat = nullptr;   // pinned: stat's readback (64 B), then the qname prefix (+64) and mid (+4160) staged
   hipEvent_t rb = nullptr;     // after that copy
   hipEvent_t done = nullptr;   // the last writer that read this set
+  uint32_t done_gate = 0;      // ... and the gate value it needs
   bool busy = false;
   bool prepared = false;       // holds a prepared unit whose writer is not queued yet
 };
@@ -149,6 +152,21 @@ struct mh_ctx {
   hipStream_t wstream = nullptr;
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
+  // Writer gate.  The permutation's radix sort cannot run beside a FASTQ writer (its workgroups need a whole CU and
+  // wait until the writers drain), so the writers from a job's `gate_at`-th on wait on the device (hipStreamWaitValue32
+  // on `gate`) until the NEXT job's sampling has sorted (it writes its job number there): the sorts run alone in a short
+  // gap instead of after all the writers.  Any host wait for a writer first opens the gate (gate_open), so a job with
+  // no successor never waits.  Opt-in: MH_WRITER_GATE=k gates from a job's k-th writer (off by default).
+  hipStream_t gstream = nullptr;   // gate writes from the host side (never blocked)
+  hipEvent_t ev_sorted = nullptr;  // the first lane's last sort, for the gate write on the other lane
+  uint32_t *gate = nullptr;        // signal memory
+  uint32_t job = 0;                // sample_units calls so far (the current job's number)
+  uint32_t gate_waited = 0;        // the largest value a queued writer waits for
+  uint32_t gate_written = 0;       // the largest value a queued gate write stores
+  int32_t gate_at = -1;
+  int32_t writers_in_job = 0;
+  static constexpr int N_USORT = 4;   // units of a batch sorted before any is chased (per unit: ts, keys, values, heads)
+  mh::DevBuf usort[N_USORT][4];
   static constexpr int N_ESET = 4;   // emission buffer sets in flight (a job's units; the next job's sampling overlaps)
   mh::EmitSet eset[N_ESET];
   int eset_i = 0;
@@ -249,8 +267,12 @@ void release(DevBuf &b);
 void release_hap(Hap &h);
 int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer
 // a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
-int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set);
-int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set);
+int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set, uint32_t &gate);
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, uint32_t gate);
+bool gate_debug();                                  // MH_GATE_DEBUG: trace gate waits and writes
+void gate_open(mh_ctx *ctx);                        // release every writer waiting on the gate
+void gate_open_for(mh_ctx *ctx, uint32_t need);     // ... if a wait is about to depend on a writer needing `need`
+int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value);   // stream-ordered gate write (sampling)
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);

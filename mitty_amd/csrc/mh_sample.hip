@@ -1188,9 +1188,13 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // `out`, file order.  `exact`: materialise the draws and recompute flagged ones on the host (rare path).
 // `lane` 1 runs on the second sampling stream with its own scratch (the units' stages are latency-bound, so two
 // units side by side fill the chip better than one after the other).
+// gate_role (the writer gate, mh_internal.h), right after the permutation's sort: 1 = record ev_sorted (the other
+// lane's last unit writes the gate), 2 = wait for ev_sorted then write the gate, 3 = write the gate.
+// phase: 0 = everything; 1 = the geometric scan and the sort (up to the gate); 2 = the rest.  `ub` (phases 1/2): the
+// unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
                     const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
-                    uint32_t *d_flag, int lane = 0) {
+                    uint32_t *d_flag, int lane = 0, int gate_role = 0, int phase = 0, mh::DevBuf *ub = nullptr) {
   hipStream_t st = lane ? ctx->stream2 : ctx->stream;
   ctx->stage_stream = lane ? ctx->stream2 : nullptr;
   struct Restore {
@@ -1202,56 +1206,69 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   void *scan_partials = lane ? ctx->scan_partials2.p : ctx->scan_partials.p;
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
-  int64_t *ts = (int64_t *)S4[0].p, *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
+  int64_t *ts = (int64_t *)(ub ? ub[0] : S4[0]).p, *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
+  uint32_t *sk = (uint32_t *)(ub ? ub[1] : S4[4]).p, *sv = (uint32_t *)(ub ? ub[2] : S4[5]).p;
+  int32_t *nxt = (int32_t *)(ub ? ub[3] : S4[6]).p;
+  const bool permute = rng_mode == MH_RNG_MITTY && n > 1;
   uint8_t *keep = (uint8_t *)S4[3].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
   int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128 + 64 * lane);
   const double log_q = std::log(1.0 - p);
   GeoFlags fl{flag_idx, d_flag, 1024};
 
-  stage_begin(ctx, "sample_geometric_scan");
-  if (!exact) {
-    HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1},
-                                         scan_partials, tot));
-  } else {
-    int64_t *g = (int64_t *)ctx->s[12].p;
-    uint32_t nflag = 0;
-    HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
-    hipLaunchKernelGGL(k_geo_array, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, w_tloc, p, log_q, fl, g);
-    HIPCHK(ctx, hipMemcpyAsync(&nflag, d_flag, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
-    std::vector<int64_t> idx(nflag);
-    if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
-    for (int64_t k : idx) {
-      uint32_t ww[2];
-      HIPCHK(ctx, hipMemcpy(ww, w_tloc + 2 * k, 8, hipMemcpyDeviceToHost));
-      double U = (((int32_t)(ww[0] >> 5)) * 67108864.0 + ((int32_t)(ww[1] >> 6))) / 9007199254740992.0;
-      int64_t gv = (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));   // the reference's libm
-      HIPCHK(ctx, hipMemcpy(g + k, &gv, 8, hipMemcpyHostToDevice));
+  if (phase != 2) {
+    stage_begin(ctx, "sample_geometric_scan");
+    if (!exact) {
+      HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1},
+                                           scan_partials, tot));
+    } else {
+      int64_t *g = (int64_t *)ctx->s[12].p;
+      uint32_t nflag = 0;
+      HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
+      hipLaunchKernelGGL(k_geo_array, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, w_tloc, p, log_q, fl, g);
+      HIPCHK(ctx, hipMemcpyAsync(&nflag, d_flag, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
+      std::vector<int64_t> idx(nflag);
+      if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
+      for (int64_t k : idx) {
+        uint32_t ww[2];
+        HIPCHK(ctx, hipMemcpy(ww, w_tloc + 2 * k, 8, hipMemcpyDeviceToHost));
+        double U = (((int32_t)(ww[0] >> 5)) * 67108864.0 + ((int32_t)(ww[1] >> 6))) / 9007199254740992.0;
+        int64_t gv = (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));   // the reference's libm
+        HIPCHK(ctx, hipMemcpy(g + k, &gv, 8, hipMemcpyHostToDevice));
+      }
+      HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
+      HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
+                                       (int64_t *)scan_partials, tot));
     }
-    HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
-    HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
-                                     (int64_t *)scan_partials, tot));
+    stage_end(ctx);
+
+    if (permute) {
+      stage_begin(ctx, "sample_permutation");
+      // steps sorted by (target, step): keys j, values the step index (stable LSD radix sort over the target's bits)
+      unsigned end_bit = 1;
+      while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
+      size_t tmp = 0;
+      const rocprim::counting_iterator<uint32_t> iota(0u);
+      HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+      MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
+      HIPCHK(ctx, rocprim::radix_sort_pairs(perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+      HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
+      hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
+                         (const uint32_t *)sv, nxt);
+      if (ctx->gate && gate_role == 1) HIPCHK(ctx, hipEventRecord(ctx->ev_sorted, st));
+      if (ctx->gate && gate_role == 2) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_sorted, 0));
+      if (gate_role >= 2) MH_TRY(gate_release(ctx, st, ctx->job));
+      HIPCHK(ctx, hipGetLastError());
+      stage_end(ctx);
+    }
   }
-  stage_end(ctx);
+  if (phase == 1) return MH_OK;
 
   const int64_t *ts_use = ts;
-  if (rng_mode == MH_RNG_MITTY && n > 1) {
+  if (permute) {
     stage_begin(ctx, "sample_permutation");
-    // steps sorted by (target, step): keys j, values the step index (stable LSD radix sort over the target's bits)
-    uint32_t *sk = (uint32_t *)S4[4].p, *sv = (uint32_t *)S4[5].p;
-    int32_t *nxt = (int32_t *)S4[6].p;
-    unsigned end_bit = 1;
-    while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
-    size_t tmp = 0;
-    const rocprim::counting_iterator<uint32_t> iota(0u);
-    HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
-    MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
-    HIPCHK(ctx, rocprim::radix_sort_pairs(perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
-    HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
-    hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
-                       (const uint32_t *)sv, nxt);
     hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                        (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)ts, ts_shuf);
     HIPCHK(ctx, hipGetLastError());
@@ -1285,6 +1302,8 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seeds[u]) + " is out of range 0 - 4294967295");
   if (n_tlen <= 0 || n_tlen > 8192) return arg_fail(ctx, MH_E_ARG, "cum_tlen must have 1..8192 entries");
   if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
+  ctx->job++;   // a new job: its writers count from 0 for the gate, and it opens the previous job's gate
+  ctx->writers_in_job = 0;
   hipStream_t st = ctx->stream;
 
   // ---- plan ---------------------------------------------------------------------------------------------------
@@ -1317,7 +1336,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     q.j_off = j_total; j_total += q.n + 4;
     n_max = std::max(n_max, q.n);
     TplSet &ts = ctx->tsets[tpl_ids[u]];
-    MH_TRY(wait_unused(ctx, ts.used, ts.used_set));   // a queued FASTQ writer may still read the old templates
+    MH_TRY(wait_unused(ctx, ts.used, ts.used_set, ts.used_gate));   // a queued FASTQ writer may still read the old templates
     MH_TRY(ensure(ctx, ts.fo0, q.n + 16));
     MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
     MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));
@@ -1434,15 +1453,34 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
   }
-  for (int32_t u = 0, k = 0; u < n_units; u++) {
-    if (plan[u].n == 0) continue;
-    MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                       d_flags + u, two_lanes ? (k++ & 1) : 0));
-  }
+  // the writer gate opens after the last unit's sort on each lane (the lane whose last unit is queued last writes it)
+  int32_t last[2] = {-1, -1};
+  for (int32_t u = 0, k = 0; u < n_units; u++)
+    if (plan[u].n > 0) last[two_lanes ? (k++ & 1) : 0] = u;
+  // Up to four units (two per lane): every unit's sort first, then the rest, each unit with its own sort buffers, so
+  // the gate opens after the sorts alone.  More units: unit after unit.
+  const bool split = ctx->gate && n_units <= mh_ctx::N_USORT;
+  if (split)
+    for (int32_t u = 0; u < n_units; u++) {
+      const int64_t nu = plan[u].n + 1;
+      MH_TRY(ensure(ctx, ctx->usort[u][0], 8 * (size_t)nu));
+      for (int b = 1; b < 4; b++) MH_TRY(ensure(ctx, ctx->usort[u][b], 4 * (size_t)nu + 16));
+    }
+  for (int ph = split ? 1 : 0; ph <= (split ? 2 : 0); ph++)
+    for (int32_t u = 0, k = 0; u < n_units; u++) {
+      if (plan[u].n == 0) continue;
+      const int lane = two_lanes ? (k++ & 1) : 0;
+      const int other = last[1 - lane];
+      int role = 0;
+      if (u == last[lane] && ph != 2) role = other < 0 ? 3 : other < u ? 2 : 1;
+      MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
+                         d_flags + u, lane, role, ph, split ? ctx->usort[u] : nullptr));
+    }
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
     HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
   }
+  MH_TRY(gate_release(ctx, st, ctx->job));   // (no permutation: Philox mode, single-template units)
   std::vector<int64_t> hm(n_units), hstat(n_units);
   std::vector<uint32_t> hflag(n_units);
   // d_m, d_status, d_flags are consecutive in s[1] (20 bytes per unit): one readback into pinned memory

@@ -1247,3 +1247,42 @@ def test_philox_sampling_properties(native):
         assert np.array_equal(x, y)
   finally:
     eng.close()
+
+
+def test_writer_gate_pipelined_jobs(native, monkeypatch):
+  """The opt-in writer gate (MH_WRITER_GATE=2: a job's writers from the third on wait on the device until the next
+  job has sorted; each batch's units sorted before any is chased): three 4-unit jobs queued back to back, the arenas
+  read only at the end, equal three times the oracle's job (reference unit order, qname serials 0..3)."""
+  monkeypatch.setenv('MH_WRITER_GATE', '2')
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  rlen = int(mdl['mean_rlen'])
+  p, passes = _native.read_model_params(rlen, 30.0)
+  length = 1_500_000
+  seq = synth.contig(length, 3)
+  copies = synth.copies_soa(synth.variants(seq, 4))
+  units = _native.work_units(7, [2], passes)
+  assert len(units) == 4
+  want1, want2 = b'', b''
+  for ps, (ri, cpy, s) in enumerate(units):
+    _, o1, o2 = O.generate_unit_soa(seq, 0, copies[cpy], p, rlen, mdl['cum_tlen'], s, 'SYN:0:{}'.format(ps), '7', cpy)
+    want1 += o1
+    want2 += o2
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('7', 0, length), seq)
+    for cpy in range(2):
+      eng.upload_variants(0, cpy, copies[cpy])
+    job = [(ps, 0, cpy, s) for ps, (ri, cpy, s) in enumerate(units)]
+    for rnd in range(2):   # the first round grows every buffer (growth opens the gate); the second is checked
+      eng.ctx.reset_output()
+      for _ in range(3):
+        eng.drop_haplotypes()
+        eng.run_units(job, lambda r, c: copies[c], p, rlen, mdl['cum_tlen'], 'SYN')
+    d1, d2 = eng.ctx.fetch_output()
+  finally:
+    eng.close()
+  G.check_same(d1, want1 * 3, 'file 1 differs')
+  G.check_same(d2, want2 * 3, 'file 2 differs')
