@@ -251,6 +251,13 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
       hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
+      [&] {
+        for (int l = 0; l < 2; l++)
+          if (hipStreamCreateWithPriority(&ctx->xstream[l], hipStreamNonBlocking, prio_hi) != hipSuccess ||
+              hipEventCreateWithFlags(&ctx->ev_xjoin[l], hipEventDisableTiming) != hipSuccess)
+            return true;
+        return false;
+      }() ||
       create_writer_stream(ctx, device, prio_lo) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
@@ -300,6 +307,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipStreamSynchronize(ctx->wstream);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  for (auto x : ctx->xstream)
+    if (x) (void)hipStreamSynchronize(x);
   for (auto &kv : ctx->contigs) release(kv.second.seq);
   for (auto &kv : ctx->haps) release_hap(kv.second);
   for (auto &h : ctx->hap_spare) release_hap(h);
@@ -311,6 +320,9 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->s) release(b);
   for (auto &b : ctx->lane2) release(b);
+  for (auto &l : ctx->xlane)
+    for (auto &b : l) release(b);
+  for (auto &b : ctx->xscan) release(b);
   for (auto &u : ctx->usort)
     for (auto &b : u) release(b);
   release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
@@ -339,6 +351,10 @@ int32_t mh_destroy(mh_ctx *ctx) {
   if (ctx->ev_sorted) (void)hipEventDestroy(ctx->ev_sorted);
   if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  for (int l = 0; l < 2; l++) {
+    if (ctx->xstream[l]) (void)hipStreamDestroy(ctx->xstream[l]);
+    if (ctx->ev_xjoin[l]) (void)hipEventDestroy(ctx->ev_xjoin[l]);
+  }
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return MH_OK;

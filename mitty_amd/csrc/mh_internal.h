@@ -197,6 +197,11 @@ struct mh_ctx {
   mh::DevBuf scan_partials;
   mh::DevBuf lane2[8];   // the second lane's copies of s[4..10] and its radix-sort scratch (index 7)
   mh::DevBuf scan_partials2;
+  // lanes 2 and 3 (a four-unit job's units each on a lane of their own): streams, scratch, join events
+  hipStream_t xstream[2] = {nullptr, nullptr};
+  mh::DevBuf xlane[2][8];
+  mh::DevBuf xscan[2];
+  hipEvent_t ev_xjoin[2] = {nullptr, nullptr};
   mh::DevBuf sl2[8];   // the splice's second lane: anchor, accepted, ref_before, node src, small, partials, N runs, sort
   mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
   mh::DevBuf d_small;        // device small scalars

@@ -1195,15 +1195,15 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
                     const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
                     uint32_t *d_flag, int lane = 0, int gate_role = 0, int phase = 0, mh::DevBuf *ub = nullptr) {
-  hipStream_t st = lane ? ctx->stream2 : ctx->stream;
-  ctx->stage_stream = lane ? ctx->stream2 : nullptr;
+  hipStream_t st = lane == 0 ? ctx->stream : lane == 1 ? ctx->stream2 : ctx->xstream[lane - 2];
+  ctx->stage_stream = lane ? st : nullptr;
   struct Restore {
     mh_ctx *c;
     ~Restore() { c->stage_stream = nullptr; }
   } restore{ctx};
-  mh::DevBuf *S4 = lane ? ctx->lane2 : ctx->s + 4;   // the lane's s[4..10]
-  mh::DevBuf &perm_tmp = lane ? ctx->lane2[7] : ctx->perm_tmp;
-  void *scan_partials = lane ? ctx->scan_partials2.p : ctx->scan_partials.p;
+  mh::DevBuf *S4 = lane == 0 ? ctx->s + 4 : lane == 1 ? ctx->lane2 : ctx->xlane[lane - 2];   // the lane's s[4..10]
+  mh::DevBuf &perm_tmp = lane == 0 ? ctx->perm_tmp : S4[7];
+  void *scan_partials = lane == 0 ? ctx->scan_partials.p : lane == 1 ? ctx->scan_partials2.p : ctx->xscan[lane - 2].p;
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
   int64_t *ts = (int64_t *)(ub ? ub[0] : S4[0]).p, *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
@@ -1354,17 +1354,21 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
   MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
   MH_TRY(ensure(ctx, ctx->s[11], 8 * 1024));
-  const bool two_lanes = n_units > 1 && !getenv("MH_ONE_LANE");   // MH_ONE_LANE: experiments
-  if (two_lanes) {
-    MH_TRY(ensure(ctx, ctx->lane2[0], 8 * nn));
-    MH_TRY(ensure(ctx, ctx->lane2[1], 8 * nn));
-    MH_TRY(ensure(ctx, ctx->lane2[2], 8 * nn));
-    MH_TRY(ensure(ctx, ctx->lane2[3], nn));
-    MH_TRY(ensure(ctx, ctx->lane2[4], 4 * (nn + 1)));
-    MH_TRY(ensure(ctx, ctx->lane2[5], 4 * (nn + 1)));
-    MH_TRY(ensure(ctx, ctx->lane2[6], 4 * nn));
-    MH_TRY(ensure(ctx, ctx->scan_partials2, std::max<size_t>(16 * scan_partials_count(nn + 1) + 64,
-                                                              scan_lb_scratch_bytes<int64_t>(nn + 1))));
+  // sampling lanes for the per-unit stages: up to MH_LANES (default 4; the writer gate uses 2), at most one per unit
+  static const int lanes_env = getenv("MH_LANES") ? atoi(getenv("MH_LANES")) : 4;
+  int n_lanes = getenv("MH_ONE_LANE") ? 1 : std::max(1, std::min({lanes_env, (int)n_units, ctx->gate ? 2 : 4}));
+  const bool two_lanes = n_lanes > 1;
+  for (int l = 1; l < n_lanes; l++) {
+    mh::DevBuf *L = l == 1 ? ctx->lane2 : ctx->xlane[l - 2];
+    MH_TRY(ensure(ctx, L[0], 8 * nn));
+    MH_TRY(ensure(ctx, L[1], 8 * nn));
+    MH_TRY(ensure(ctx, L[2], 8 * nn));
+    MH_TRY(ensure(ctx, L[3], nn));
+    MH_TRY(ensure(ctx, L[4], 4 * (nn + 1)));
+    MH_TRY(ensure(ctx, L[5], 4 * (nn + 1)));
+    MH_TRY(ensure(ctx, L[6], 4 * nn));
+    MH_TRY(ensure(ctx, l == 1 ? ctx->scan_partials2 : ctx->xscan[l - 2],
+                  std::max<size_t>(16 * scan_partials_count(nn + 1) + 64, scan_lb_scratch_bytes<int64_t>(nn + 1))));
   }
   MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 64));
   MH_TRY(ensure(ctx, ctx->s[1], 64 * (size_t)n_units + 64));          // per-unit m, flags, decode status
@@ -1452,11 +1456,12 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+    for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
   }
   // the writer gate opens after the last unit's sort on each lane (the lane whose last unit is queued last writes it)
-  int32_t last[2] = {-1, -1};
+  int32_t last[4] = {-1, -1, -1, -1};
   for (int32_t u = 0, k = 0; u < n_units; u++)
-    if (plan[u].n > 0) last[two_lanes ? (k++ & 1) : 0] = u;
+    if (plan[u].n > 0) last[k++ % n_lanes] = u;
   // Up to four units (two per lane): every unit's sort first, then the rest, each unit with its own sort buffers, so
   // the gate opens after the sorts alone.  More units: unit after unit.
   const bool split = ctx->gate && n_units <= mh_ctx::N_USORT;
@@ -1469,16 +1474,22 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   for (int ph = split ? 1 : 0; ph <= (split ? 2 : 0); ph++)
     for (int32_t u = 0, k = 0; u < n_units; u++) {
       if (plan[u].n == 0) continue;
-      const int lane = two_lanes ? (k++ & 1) : 0;
-      const int other = last[1 - lane];
+      const int lane = k++ % n_lanes;
       int role = 0;
-      if (u == last[lane] && ph != 2) role = other < 0 ? 3 : other < u ? 2 : 1;
+      if (ctx->gate && u == last[lane] && ph != 2) {   // (at most two lanes with the gate)
+        const int other = n_lanes > 1 ? last[1 - lane] : -1;
+        role = other < 0 ? 3 : other < u ? 2 : 1;
+      }
       MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
                          d_flags + u, lane, role, ph, split ? ctx->usort[u] : nullptr));
     }
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
     HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
+    for (int l = 2; l < n_lanes; l++) {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_xjoin[l - 2], ctx->xstream[l - 2]));
+      HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_xjoin[l - 2], 0));
+    }
   }
   MH_TRY(gate_release(ctx, st, ctx->job));   // (no permutation: Philox mode, single-template units)
   std::vector<int64_t> hm(n_units), hstat(n_units);
