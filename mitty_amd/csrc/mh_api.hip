@@ -1070,7 +1070,7 @@ int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates
   int64_t u1 = 0, u2 = 0;
   const bool two = ctx->used2 > 0;
   return bam_add(ctx, (const uint8_t *)ctx->out1.p, ctx->used1, two ? (const uint8_t *)ctx->out2.p : nullptr,
-                 two ? ctx->used2 : 0, max_templates, &u1, &u2, templates);
+                 two ? ctx->used2 : 0, max_templates, &u1, &u2, templates, true);
 }
 
 int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes) {
@@ -1129,6 +1129,7 @@ int32_t mh_bam_reset(mh_ctx *ctx) {
   ctx->bam.n_rec = ctx->bam.bytes = 0;
   ctx->bam.n_files = 0;
   ctx->bam.sorted = false;
+  ctx->bam.direct = false;
   return MH_OK;
 }
 

@@ -303,18 +303,22 @@ __device__ __forceinline__ uint8_t comp_atcgn(uint8_t c) {   // str.maketrans('A
 // One wave per record.  Records are byte-packed (BAM has no padding), so stores are bytewise; every input byte the
 // wave needs is loaded by the lanes together (restrict pointers let the loads of an unrolled loop issue ahead of the
 // stores), and the CIGAR text is walked from registers (shuffles), not from memory.
+// slot (direct sorted write, bam_add_output into an empty store): record i goes to sorted place slot[i] — at
+// off[slot[i]], its BAI info at info[slot[i]], no sort key (records are read in input order, so the FASTQ reads
+// stream); otherwise record i at off[i] with its key.
 __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tpl, int64_t n_rec, int32_t nr,
-                                                   const int64_t *off, uint8_t *out, uint64_t *key, uint32_t *val,
-                                                   RInfo *info, int64_t rec_base) {
+                                                   const uint32_t *slot, const int64_t *off, uint8_t *out,
+                                                   uint64_t *key, uint32_t *val, RInfo *info, int64_t rec_base) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (i >= n_rec) return;
+  const int64_t w = slot ? (int64_t)slot[i] : i;
   const int64_t t = nr == 2 ? i >> 1 : i;   // nr is 1 or 2
   const int s = nr == 2 ? (int)(i & 1) : 0;
   const BamTpl &T = tpl[t];
   const BamRead &r = T.r[s];
   const BamRead &m = T.r[nr == 2 ? 1 - s : s];
-  uint8_t *__restrict__ d = out + off[i];
+  uint8_t *__restrict__ d = out + off[w];
   const uint8_t *__restrict__ qn = a.b[0] + T.qn_off;
   const int32_t lq = T.qn_len + 1;
   const int32_t hdr = 36;
@@ -418,10 +422,27 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
     }
   }
   if (lane == 0) {
-    key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
-    val[i] = (uint32_t)(rec_base + i);
-    info[i] = RInfo{r.tid, r.pos, r.end, r.bin};
+    if (key) {
+      key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
+      val[i] = (uint32_t)(rec_base + i);
+    }
+    info[w] = RInfo{r.tid, r.pos, r.end, r.bin};
   }
+}
+
+// record -> its sorted place
+__global__ void k_bam_slots(const uint32_t *val2, int64_t n, uint32_t *slot) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) slot[val2[k]] = (uint32_t)k;
+}
+
+// samtools sort's key of every record (the direct sorted write sorts before it writes)
+__global__ void k_bam_keys(const BamTpl *tpl, int64_t n_rec, int32_t nr, uint64_t *key, uint32_t *val) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rec) return;
+  const BamRead &r = tpl[nr == 2 ? i >> 1 : i].r[nr == 2 ? (int)(i & 1) : 0];
+  key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | ((r.flag & 0x10) ? 1u : 0u);
+  val[i] = (uint32_t)i;
 }
 
 // sorted position k <- record val[k]
@@ -488,6 +509,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
   B.bytes = 0;
   B.n_files = 0;
   B.sorted = false;
+  B.direct = false;
   B.refs_set = true;
   return MH_OK;
 }
@@ -516,8 +538,9 @@ int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, in
 }
 
 int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2, int64_t len2, int64_t max_templates,
-                int64_t *used1, int64_t *used2, int64_t *templates) {
+                int64_t *used1, int64_t *used2, int64_t *templates, bool sorted_direct) {
   BamStore &B = ctx->bam;
+  if (B.direct) MH_TRY(bam_undirect(ctx));   // more records after a direct sorted write: back to input order
   hipStream_t st = ctx->stream;
   *used1 = *used2 = *templates = 0;
   if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
@@ -569,13 +592,36 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int64_t add_bytes = 0;
   HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
+  if (sorted_direct && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
+    // the whole input is here (the context's own arenas) and the store is empty: sort first, then every record is
+    // written once, straight to its coordinate-sorted place (no input-order copy, no gather)
+    MH_TRY(ensure(ctx, B.key, sizeof(uint64_t) * n_rec));
+    MH_TRY(ensure(ctx, B.val, sizeof(uint32_t) * n_rec));
+    hipLaunchKernelGGL(k_bam_keys, dim3(grid_for(n_rec, 256, INT32_MAX)), dim3(256), 0, st, (const BamTpl *)B.tpl.p,
+                       n_rec, nf, (uint64_t *)B.key.p, (uint32_t *)B.val.p);
+    HIPCHK(ctx, hipGetLastError());
+    B.n_rec = n_rec;
+    B.bytes = add_bytes;
+    B.sorted = false;
+    MH_TRY(bam_sort(ctx, &a));   // sorted keys, order and offsets; the records written by k_bam_write
+    B.direct = true;
+    int64_t last1 = 0, last2 = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
+    if (d2) HIPCHK(ctx, hipMemcpyAsync(&last2, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    *used1 = last1 + 1;
+    *used2 = d2 ? last2 + 1 : 0;
+    *templates = T;
+    return MH_OK;
+  }
   MH_TRY(ensure_keep(ctx, B.recs, B.bytes + add_bytes + 64, B.bytes));
   MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n_rec), sizeof(uint64_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n_rec), sizeof(uint32_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n_rec), sizeof(RInfo) * B.n_rec));
   stage_begin(ctx, "bam_write");
   hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n_rec * 64, 256, INT32_MAX)), dim3(256), 0, st, a,
-                     (const BamTpl *)B.tpl.p, n_rec, nf, (const int64_t *)roff, (uint8_t *)B.recs.p,
+                     (const BamTpl *)B.tpl.p, n_rec, nf, (const uint32_t *)nullptr, (const int64_t *)roff,
+                     (uint8_t *)B.recs.p,
                      (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
                      B.n_rec);
   HIPCHK(ctx, hipGetLastError());
@@ -594,7 +640,9 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   return MH_OK;
 }
 
-int32_t bam_sort(mh_ctx *ctx) {
+// pa: the direct sorted write's parse (records not written yet: k_bam_write places them in sorted order);
+// null: the records are in recs (input order) and are gathered
+int32_t bam_sort(mh_ctx *ctx, const void *pa) {
   BamStore &B = ctx->bam;
   hipStream_t st = ctx->stream;
   const int64_t n = B.n_rec;
@@ -622,15 +670,54 @@ int32_t bam_sort(mh_ctx *ctx) {
                                    (int64_t *)ctx->scan_partials.p, (int64_t *)ctx->d_small.p));
   MH_TRY(ensure(ctx, B.srecs, B.bytes + 64));
   MH_TRY(ensure(ctx, B.sinfo, sizeof(RInfo) * n));
-  stage_begin(ctx, "bam_gather");
-  hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st,
-                     (const uint8_t *)B.recs.p, (const int64_t *)B.roff.p, (const uint32_t *)B.val2.p,
-                     (const int64_t *)B.soff.p, n, (uint8_t *)B.srecs.p, (const RInfo *)B.info.p,
-                     (RInfo *)B.sinfo.p);
-  HIPCHK(ctx, hipGetLastError());
-  stage_end(ctx);
+  if (pa) {
+    stage_begin(ctx, "bam_write");
+    hipLaunchKernelGGL(k_bam_slots, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint32_t *)B.val2.p, n,
+                       (uint32_t *)B.val.p);   // (the sort's input values are no longer needed)
+    hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st, *(const ParseArgs *)pa,
+                       (const BamTpl *)B.tpl.p, n, B.n_files, (const uint32_t *)B.val.p, (const int64_t *)B.soff.p,
+                       (uint8_t *)B.srecs.p, (uint64_t *)nullptr, (uint32_t *)nullptr, (RInfo *)B.sinfo.p, (int64_t)0);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+  } else {
+    stage_begin(ctx, "bam_gather");
+    hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st,
+                       (const uint8_t *)B.recs.p, (const int64_t *)B.roff.p, (const uint32_t *)B.val2.p,
+                       (const int64_t *)B.soff.p, n, (uint8_t *)B.srecs.p, (const RInfo *)B.info.p,
+                       (RInfo *)B.sinfo.p);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+  }
   HIPCHK(ctx, hipStreamSynchronize(st));
   B.sorted = true;
+  return MH_OK;
+}
+
+// after a direct sorted write, more records: the sorted block becomes the store's input-order prefix (a stable sort
+// keeps its order on ties, which is the order it had as input)
+__global__ void k_iota(uint32_t *v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+int32_t bam_undirect(mh_ctx *ctx) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  const int64_t n = B.n_rec;
+  MH_TRY(ensure(ctx, B.recs, B.bytes + 64));
+  MH_TRY(ensure(ctx, B.roff, sizeof(int64_t) * (n + 1)));
+  MH_TRY(ensure(ctx, B.key, sizeof(uint64_t) * n + 8));
+  MH_TRY(ensure(ctx, B.val, sizeof(uint32_t) * n + 8));
+  MH_TRY(ensure(ctx, B.info, sizeof(RInfo) * n + 16));
+  HIPCHK(ctx, hipMemcpyAsync(B.recs.p, B.srecs.p, B.bytes, hipMemcpyDeviceToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(B.roff.p, B.soff.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(B.key.p, B.key2.p, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(B.info.p, B.sinfo.p, sizeof(RInfo) * n, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (uint32_t *)B.val.p, n);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  B.direct = false;
+  B.sorted = false;
   return MH_OK;
 }
 
@@ -655,6 +742,7 @@ void bam_release(BamStore &B) {
   B.n_files = 0;
   B.refs_set = false;
   B.sorted = false;
+  B.direct = false;
 }
 
 }  // namespace mh

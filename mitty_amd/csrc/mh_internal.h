@@ -116,6 +116,7 @@ struct BamStore {
   int64_t n_rec = 0, bytes = 0;
   int32_t n_files = 0;
   bool sorted = false;         // srecs/soff/sinfo hold the current store in coordinate order
+  bool direct = false;         // ... written there straight from the parse (no input-order copy in recs yet)
 };
 
 struct StageTime {
@@ -320,8 +321,9 @@ int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, in
 
 int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);
 int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2, int64_t len2, int64_t max_templates,
-                int64_t *used1, int64_t *used2, int64_t *templates);
-int32_t bam_sort(mh_ctx *ctx);
+                int64_t *used1, int64_t *used2, int64_t *templates, bool sorted_direct = false);
+int32_t bam_sort(mh_ctx *ctx, const void *pa = nullptr);
+int32_t bam_undirect(mh_ctx *ctx);
 int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
 void bam_release(BamStore &B);
 int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count);

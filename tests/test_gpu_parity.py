@@ -1061,11 +1061,17 @@ def test_tumor_normal_mix_god_aligner(native, tmp_path):
     eng.ctx.bam_sort()
     bam = str(tmp_path / 'tn.bam')
     eng.ctx.bam_write(bam, '@HD\tVN:1.0\n', bai_path=bam + '.bai')   # the sort above is reused
+    # more records after the direct sorted write (the sorted block becomes the input-order prefix)
+    eng.ctx.bam_add_fastq(want1, want2)
+    bam2 = str(tmp_path / 'tn2.bam')
+    eng.ctx.bam_write(bam2, '@HD\tVN:1.0\n')
   finally:
     eng.close()
+  refs = {'1': 0, '2': 1, '3': 2}
   _, recs, _, _ = god.record_voffsets(open(bam, 'rb').read())
-  want = god.sorted_stream(god.god_records(want1, want2, {'1': 0, '2': 1, '3': 2}))
-  assert recs == [god.encode(r) for r in want]
+  assert recs == [god.encode(r) for r in god.sorted_stream(god.god_records(want1, want2, refs))]
+  _, recs2, _, _ = god.record_voffsets(open(bam2, 'rb').read())
+  assert recs2 == [god.encode(r) for r in god.sorted_stream(god.god_records(want1 + want1, want2 + want2, refs))]
 
 
 # ---- standalone corrupt-reads --------------------------------------------------------------
