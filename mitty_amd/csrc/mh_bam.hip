@@ -6,7 +6,7 @@
 //     -> k_bam_parse                 (thread per template: parse_qname of file 1's name (readgenerate.py:259-291),
 //                                     the CIGAR, tid from the @SQ names, seq / qual spans; BAM record sizes)
 //     -> scan of record sizes        (appends to the resident record store)
-//     -> k_bam_write                 (wave per record: core fields, name, CIGAR, 4-bit seq (reverse-complemented
+//     -> k_bam_write                 (32 lanes per record: core fields, name, CIGAR, 4-bit seq (reverse-complemented
 //                                     for strand 1 with the ATCGN-only table), qual - 33 (reversed for strand 1))
 //   finish:
 //     -> stable radix sort of (tid, pos + 1, is_reverse)  (samtools sort's coordinate order, input order on ties)
@@ -306,12 +306,16 @@ __device__ __forceinline__ uint8_t comp_atcgn(uint8_t c) {   // str.maketrans('A
 // slot (direct sorted write, bam_add_output into an empty store): record i goes to sorted place slot[i] — at
 // off[slot[i]], its BAI info at info[slot[i]], no sort key (records are read in input order, so the FASTQ reads
 // stream); otherwise record i at off[i] with its key.
+// G lanes per record (64: a wave; 32: two records per wave side by side, so twice the records in flight per resident
+// wave — the kernel is bound by each record's chain of dependent loads, not by bandwidth)
+template <int G>
 __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tpl, int64_t n_rec, int32_t nr,
                                                    const uint32_t *slot, const int64_t *off, uint8_t *out,
                                                    uint64_t *key, uint32_t *val, RInfo *info, int64_t rec_base) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (i >= n_rec) return;
+  const int gl = lane & (G - 1), gb = lane & ~(G - 1);   // lane within the record's group, the group's first lane
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  if (i >= n_rec) return;   // (a whole group)
   const int64_t w = slot ? (int64_t)slot[i] : i;
   const int64_t t = nr == 2 ? i >> 1 : i;   // nr is 1 or 2
   const int s = nr == 2 ? (int)(i & 1) : 0;
@@ -322,55 +326,55 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   const uint8_t *__restrict__ qn = a.b[0] + T.qn_off;
   const int32_t lq = T.qn_len + 1;
   const int32_t hdr = 36;
-  if (lane < 9) {
-    int32_t w;
-    switch (lane) {
-      case 0: w = r.size - 4; break;
-      case 1: w = r.tid; break;
-      case 2: w = r.pos; break;
-      case 3: w = (int32_t)((uint32_t)r.bin << 16 | 60u << 8 | (uint32_t)lq); break;
-      case 4: w = (int32_t)((uint32_t)r.flag << 16 | r.n_cig); break;
-      case 5: w = r.l_seq; break;
-      case 6: w = nr == 2 ? m.tid : -1; break;
-      case 7: w = nr == 2 ? m.pos : -1; break;
-      default: w = 0; break;   // TLEN
+  if (gl < 9) {
+    int32_t x;
+    switch (gl) {
+      case 0: x = r.size - 4; break;
+      case 1: x = r.tid; break;
+      case 2: x = r.pos; break;
+      case 3: x = (int32_t)((uint32_t)r.bin << 16 | 60u << 8 | (uint32_t)lq); break;
+      case 4: x = (int32_t)((uint32_t)r.flag << 16 | r.n_cig); break;
+      case 5: x = r.l_seq; break;
+      case 6: x = nr == 2 ? m.tid : -1; break;
+      case 7: x = nr == 2 ? m.pos : -1; break;
+      default: x = 0; break;   // TLEN
     }
-    uint8_t *p = d + 4 * lane;
-    p[0] = (uint8_t)w; p[1] = (uint8_t)(w >> 8); p[2] = (uint8_t)(w >> 16); p[3] = (uint8_t)(w >> 24);
+    uint8_t *p = d + 4 * gl;
+    p[0] = (uint8_t)x; p[1] = (uint8_t)(x >> 8); p[2] = (uint8_t)(x >> 16); p[3] = (uint8_t)(x >> 24);
   }
   const uint8_t *__restrict__ sq = a.b[s] + r.seq_off, *__restrict__ ql = a.b[s] + r.qual_off;
   const int32_t L = r.l_seq;
   const bool rev = r.flag & 0x10;
-  // every load first: qname, CIGAR text, bases, qualities (up to 4 x 64 bytes each per pass)
+  // every load first: qname, CIGAR text, bases, qualities (4 x G bytes each per pass)
   uint8_t qb[4], cb, sb0[4], sb1[4], qv[4];
 #pragma unroll
   for (int u = 0; u < 4; u++) {
-    const int32_t k = lane + 64 * u;
+    const int32_t k = gl + G * u;
     qb[u] = k < T.qn_len ? qn[k] : 0;
   }
-  cb = lane < r.cig_len ? qn[r.cig_off + lane] : 0;
+  cb = gl < r.cig_len ? qn[r.cig_off + gl] : 0;
   uint8_t *dc = d + hdr + lq;
   uint8_t *ds = dc + 4 * r.n_cig;
   uint8_t *dq = ds + (L + 1) / 2;
   // loads in ascending address order across the lanes for both strands (a strand-1 read is reversed by where each
   // lane stores, not by which byte it loads: descending lane addresses do not coalesce)
   const int32_t J = (L + 1) / 2;   // sequence bytes
-  for (int32_t k0 = 0; k0 < L; k0 += 256) {
+  for (int32_t k0 = 0; k0 < L; k0 += 4 * G) {
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int32_t y = k0 + lane + 64 * u;            // quality byte loaded
-      const int32_t jx = k0 / 2 + lane + 64 * u;       // sequence byte, in load order
+      const int32_t y = k0 + gl + G * u;               // quality byte loaded
+      const int32_t jx = k0 / 2 + gl + G * u;          // sequence byte, in load order
       const int32_t j = rev ? J - 1 - jx : jx;         // ... its output index: bases 2j, 2j + 1
-      const bool jv = jx < J && jx < k0 / 2 + 128;
+      const bool jv = jx < J && jx < k0 / 2 + 2 * G;
       qv[u] = y < L ? ql[y] : 0;
       sb0[u] = jv ? sq[rev ? L - 1 - 2 * j : 2 * j] : 0;
       sb1[u] = jv && 2 * j + 1 < L ? sq[rev ? L - 2 - 2 * j : 2 * j + 1] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int32_t y = k0 + lane + 64 * u, jx = k0 / 2 + lane + 64 * u;
+      const int32_t y = k0 + gl + G * u, jx = k0 / 2 + gl + G * u;
       if (y < L) dq[rev ? L - 1 - y : y] = (uint8_t)(qv[u] - 33);
-      if (jx < J && jx < k0 / 2 + 128) {
+      if (jx < J && jx < k0 / 2 + 2 * G) {
         const int32_t j = rev ? J - 1 - jx : jx;
         const uint8_t c0 = rev ? comp_atcgn(sb0[u]) : sb0[u];
         const uint8_t lo = 2 * j + 1 < L ? nt16(rev ? comp_atcgn(sb1[u]) : sb1[u]) : 0;
@@ -380,30 +384,32 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   }
 #pragma unroll
   for (int u = 0; u < 4; u++) {
-    const int32_t k = lane + 64 * u;
+    const int32_t k = gl + G * u;
     if (k < lq) d[hdr + k] = qb[u];
   }
-  for (int32_t k = lane + 256; k < lq; k += 64) d[hdr + k] = k < T.qn_len ? qn[k] : 0;   // names > 256 bytes
-  // CIGAR: lane k holds text byte k; every op lane packs its own op from the digits since the previous op (ballot +
-  // shuffles, no serial walk).  A text longer than 64 bytes is walked serially from memory.
-  if (r.cig_len <= 64) {
-    const bool is_op = lane < r.cig_len && (uint32_t)cb - '0' > 9;
-    const uint64_t ops = __ballot(is_op);
-    const uint64_t below = lane ? ops & ((~0ull) >> (64 - lane)) : 0ull;
-    const int prev = below ? 63 - __builtin_clzll(below) : -1;   // the previous op's lane
+  for (int32_t k = gl + 4 * G; k < lq; k += G) d[hdr + k] = k < T.qn_len ? qn[k] : 0;   // longer names
+  // CIGAR: lane k of the group holds text byte k; every op lane packs its own op from the digits since the previous
+  // op (ballot + shuffles, no serial walk).  A text longer than G bytes is walked serially from memory.
+  if (r.cig_len <= G) {
+    const bool is_op = gl < r.cig_len && (uint32_t)cb - '0' > 9;
+    const uint64_t ops = (__ballot(is_op) >> gb) & (G == 64 ? ~0ull : 0xffffffffull);
+    const uint64_t below = gl ? ops & ((~0ull) >> (64 - gl)) : 0ull;
+    const int prev = below ? 63 - __builtin_clzll(below) : -1;   // the previous op's lane in the group
     uint32_t num = 0;
-    const int nd = is_op ? lane - prev - 1 : 0;
-    const int ndmax = __reduce_max_sync(~0ull, nd);
-    for (int q = 0; q < ndmax; q++) {   // the digits prev + 1 .. lane - 1, most significant first
+    const int nd = is_op ? gl - prev - 1 : 0;
+    int ndmax = nd;
+#pragma unroll
+    for (int o = 1; o < G; o <<= 1) ndmax = max(ndmax, __shfl_xor(ndmax, o, 64));
+    for (int q = 0; q < ndmax; q++) {   // the digits prev + 1 .. gl - 1, most significant first
       const int src = prev + 1 + q;
-      const uint32_t dgt = (uint32_t)__shfl((int)cb, src < 64 ? (src > 0 ? src : 0) : 63, 64) - '0';
+      const uint32_t dgt = (uint32_t)__shfl((int)cb, gb + (src < G ? (src > 0 ? src : 0) : G - 1), 64) - '0';
       if (q < nd) num = num * 10 + dgt;
     }
     if (is_op) {
       const int j = __popcll(below);
-      const uint32_t w = num << 4 | (uint32_t)cigar_code(cb);
-      dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
-      dc[4 * j + 3] = (uint8_t)(w >> 24);
+      const uint32_t x = num << 4 | (uint32_t)cigar_code(cb);
+      dc[4 * j] = (uint8_t)x; dc[4 * j + 1] = (uint8_t)(x >> 8); dc[4 * j + 2] = (uint8_t)(x >> 16);
+      dc[4 * j + 3] = (uint8_t)(x >> 24);
     }
   } else {
     uint32_t num = 0;
@@ -412,16 +418,16 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
       const uint8_t c = qn[r.cig_off + k];
       const uint32_t dd = (uint32_t)c - '0';
       if (dd <= 9) { num = num * 10 + dd; continue; }
-      if (lane == 0) {
-        const uint32_t w = num << 4 | (uint32_t)cigar_code(c);
-        dc[4 * j] = (uint8_t)w; dc[4 * j + 1] = (uint8_t)(w >> 8); dc[4 * j + 2] = (uint8_t)(w >> 16);
-        dc[4 * j + 3] = (uint8_t)(w >> 24);
+      if (gl == 0) {
+        const uint32_t x = num << 4 | (uint32_t)cigar_code(c);
+        dc[4 * j] = (uint8_t)x; dc[4 * j + 1] = (uint8_t)(x >> 8); dc[4 * j + 2] = (uint8_t)(x >> 16);
+        dc[4 * j + 3] = (uint8_t)(x >> 24);
       }
       j++;
       num = 0;
     }
   }
-  if (lane == 0) {
+  if (gl == 0) {
     if (key) {
       key[i] = (uint64_t)(uint32_t)r.tid << 33 | (uint64_t)(uint32_t)(r.pos + 1) << 1 | (rev ? 1u : 0u);
       val[i] = (uint32_t)(rec_base + i);
@@ -429,6 +435,7 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
     info[w] = RInfo{r.tid, r.pos, r.end, r.bin};
   }
 }
+constexpr int BW_G = 32;   // lanes per record (16: the same time)
 
 // record -> its sorted place
 __global__ void k_bam_slots(const uint32_t *val2, int64_t n, uint32_t *slot) {
@@ -619,7 +626,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n_rec), sizeof(uint32_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n_rec), sizeof(RInfo) * B.n_rec));
   stage_begin(ctx, "bam_write");
-  hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n_rec * 64, 256, INT32_MAX)), dim3(256), 0, st, a,
+  hipLaunchKernelGGL(k_bam_write<BW_G>, dim3(grid_for(n_rec * BW_G, 256, INT32_MAX)), dim3(256), 0, st, a,
                      (const BamTpl *)B.tpl.p, n_rec, nf, (const uint32_t *)nullptr, (const int64_t *)roff,
                      (uint8_t *)B.recs.p,
                      (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
@@ -674,8 +681,8 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
     stage_begin(ctx, "bam_write");
     hipLaunchKernelGGL(k_bam_slots, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint32_t *)B.val2.p, n,
                        (uint32_t *)B.val.p);   // (the sort's input values are no longer needed)
-    hipLaunchKernelGGL(k_bam_write, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st, *(const ParseArgs *)pa,
-                       (const BamTpl *)B.tpl.p, n, B.n_files, (const uint32_t *)B.val.p, (const int64_t *)B.soff.p,
+    hipLaunchKernelGGL(k_bam_write<BW_G>, dim3(grid_for(n * BW_G, 256, INT32_MAX)), dim3(256), 0, st,
+                       *(const ParseArgs *)pa, (const BamTpl *)B.tpl.p, n, B.n_files, (const uint32_t *)B.val.p, (const int64_t *)B.soff.p,
                        (uint8_t *)B.srecs.p, (uint64_t *)nullptr, (uint32_t *)nullptr, (RInfo *)B.sinfo.p, (int64_t)0);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
