@@ -251,13 +251,6 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
       hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
-      [&] {
-        for (int l = 0; l < 2; l++)
-          if (hipStreamCreateWithPriority(&ctx->xstream[l], hipStreamNonBlocking, prio_hi) != hipSuccess ||
-              hipEventCreateWithFlags(&ctx->ev_xjoin[l], hipEventDisableTiming) != hipSuccess)
-            return true;
-        return false;
-      }() ||
       create_writer_stream(ctx, device, prio_lo) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||

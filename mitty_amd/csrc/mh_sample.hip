@@ -1359,6 +1359,16 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   static const int lanes_env = getenv("MH_LANES") ? atoi(getenv("MH_LANES")) : 2;
   int n_lanes = getenv("MH_ONE_LANE") ? 1 : std::max(1, std::min({lanes_env, (int)n_units, ctx->gate ? 2 : 4}));
   const bool two_lanes = n_lanes > 1;
+  // lanes 2 and 3 get their streams on first use only: the box runs with 4 hardware queues per process
+  // (GPU_MAX_HW_QUEUES), and streams beyond that share queues — a sampling lane sharing the writer's queue would
+  // serialize behind it
+  for (int l = 2; l < n_lanes; l++)
+    if (!ctx->xstream[l - 2]) {
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      HIPCHK(ctx, hipStreamCreateWithPriority(&ctx->xstream[l - 2], hipStreamNonBlocking, hi));
+      HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_xjoin[l - 2], hipEventDisableTiming));
+    }
   for (int l = 1; l < n_lanes; l++) {
     mh::DevBuf *L = l == 1 ? ctx->lane2 : ctx->xlane[l - 2];
     MH_TRY(ensure(ctx, L[0], 8 * nn));
