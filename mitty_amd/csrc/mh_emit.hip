@@ -1011,27 +1011,33 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
   }
 }
 
-template <bool LDS_TAB>
-__global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
-  // LDS: bucket entries [2][rlen][CB_ROW] | Fp16[100] | low-byte pairs of the thresholds [2][rlen][n_bq] (u16)
+// PF (two files): a workgroup corrupts one file's records only (file = blockIdx.x & 1), so it stages that file's tables
+// alone — half the LDS, two workgroups (8 waves per SIMD) per CU instead of one.
+template <bool LDS_TAB, bool PF>
+__global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A) {   // (PF: 8 waves per SIMD)
+  // LDS: bucket entries [NT][rlen][CB_ROW] | Fp16[100] | low-byte pairs of the thresholds [NT][rlen][n_bq] (u16);
+  // NT = 2 files, or 1 with PF
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
+  constexpr int NT = PF ? 1 : 2;
+  const int f_pf = PF ? (int)(blockIdx.x & 1u) : 0;
   const CorruptCfg &cc = A.cc;
   const int rlen = A.rlen, n_bq = cc.n_bq;
   const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
   const int32_t row_bytes = rlen * CB_ROW;   // per file
-  const uint16_t *fp16 = (const uint16_t *)(ctab + 2 * row_bytes);
-  const int32_t o_t8 = 2 * row_bytes + 256;
+  const uint16_t *fp16 = (const uint16_t *)(ctab + NT * row_bytes);
+  const int32_t o_t8 = NT * row_bytes + 256;
   if (LDS_TAB) {
-    for (int f = 0; f < 2; f++) {
+    for (int ft = 0; ft < NT; ft++) {
+      const int f = PF ? f_pf : ft;
       const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
-      uint4 *dst = (uint4 *)(ctab + f * row_bytes);
+      uint4 *dst = (uint4 *)(ctab + ft * row_bytes);
       for (int i = threadIdx.x; i < row_bytes / 16; i += CI_THREADS) dst[i] = src[i];
       // per entry j: its low byte | (entry j + 1's low byte when j + 1 < min(n_bq, 93) lies in j's bucket, else 0xff) << 8
       const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
       for (int i = threadIdx.x; i < rlen * n_bq; i += CI_THREADS) {
         const int j = i % n_bq;
         const uint32_t a = t16[i], b = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
-        ((uint16_t *)(ctab + o_t8))[f * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
+        ((uint16_t *)(ctab + o_t8))[ft * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
       }
     }
     for (int i = threadIdx.x; i < 100; i += CI_THREADS) ((uint16_t *)fp16)[i] = cc.Fp16[i];
@@ -1044,7 +1050,7 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
   const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
   auto walk = [&](int f, int n, uint32_t h1, bool *amb) -> uint32_t {
     if (!LDS_TAB) return bq_walk_g(cc, f, n, h1, amb);
-    const int row = f * rlen + n;
+    const int row = (PF ? 0 : f * rlen) + n;
     const uint32_t e = ctab[row * CB_ROW + (int)(h1 >> 8)];
     const uint32_t c = e & 0x7fu;
     // entry c's low byte | entry c + 1's (0xff when outside the bucket) << 8; the same pair of entry c + 1.  A 0xff
@@ -1062,22 +1068,25 @@ __global__ void __launch_bounds__(CI_THREADS) k_cr_inplace(CiArgs A) {
   auto fp = [&](uint32_t bq) -> uint32_t { return LDS_TAB ? fp16[bq] : cc.Fp16[bq]; };
   const uint2 key = make_uint2(cc.k0, cc.k1);
   // items: 15-base blocks of the records, NB per record (block b = bases 15b .. 15b + 14: five triple draws)
+  // (PF: items of this workgroup's file only; an item's unit q is then the template, its record 2 q + file)
   const uint32_t NB = (uint32_t)(rlen + CI_BLK - 1) / CI_BLK;
-  const uint32_t n_items = (uint32_t)(A.m * A.nf) * NB;
-  const uint32_t stride = gridDim.x * CI_THREADS;
+  const uint32_t n_items = (uint32_t)(A.m * (PF ? 1 : A.nf)) * NB;
+  const uint32_t stride = (PF ? gridDim.x >> 1 : gridDim.x) * CI_THREADS;
   const uint32_t nb_magic = 0xffffffffu / NB + 1u;   // umulhi(i, nb_magic) is i / NB or one more
-  auto rec_of = [&](uint32_t i) -> uint32_t {
+  auto unit_of = [&](uint32_t i) -> uint32_t {
     i = i < n_items ? i : 0u;
     const uint32_t q = __umulhi(i, nb_magic);
     return q * NB > i ? q - 1 : q;
   };
-  uint32_t i = blockIdx.x * CI_THREADS + threadIdx.x;
+  auto rec_of = [&](uint32_t i) -> uint32_t { return PF ? 2u * unit_of(i) + (uint32_t)f_pf : unit_of(i); };
+  uint32_t i = (PF ? blockIdx.x >> 1 : blockIdx.x) * CI_THREADS + threadIdx.x;
   uint2 R = A.crec[rec_of(i)];                         // this item's record word; the next one is in flight below
   for (; i < n_items; i += stride) {
-    const uint32_t rr = rec_of(i);
+    const uint32_t uq = unit_of(i);
+    const uint32_t rr = PF ? 2u * uq + (uint32_t)f_pf : uq;
     const uint2 Rn = A.crec[rec_of(i + stride)];     // prefetch
     const uint32_t S = R.y & 0xffffu;
-    const int n0 = CI_BLK * (int)(i - rr * NB);
+    const int n0 = CI_BLK * (int)(i - uq * NB);
     if ((uint32_t)n0 < S) {
       const int cnt = S - n0 < CI_BLK ? (int)S - n0 : CI_BLK;
       const int f = A.nf == 2 ? (int)(rr & 1) : 0;
@@ -1184,23 +1193,29 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (ncu <= 0) ncu = 256;
-  const size_t lds = (size_t)2 * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads pairs c + 1 <= n_bq + 1)
+  // per-file workgroups (two files): each stages one file's tables (MH_CR_PERFILE=0, experiments: both)
+  static const bool pf_env = !(getenv("MH_CR_PERFILE") && atoi(getenv("MH_CR_PERFILE")) == 0);
+  const bool pf = pf_env && nf == 2;
+  const size_t lds = (size_t)(pf ? 1 : 2) * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads pairs c + 1 <= n_bq + 1)
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
   const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
   if (grid < 1) grid = 1;
+  if (pf) grid = (grid + 1) & ~(int64_t)1;   // even: workgroup pairs (file 0, file 1)
   CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
   if (!crec_ready) {   // (the fused writer wrote the record words itself)
     hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
     HIPCHK(ctx, hipGetLastError());
   }
-  if (lds_tab)
-    hipLaunchKernelGGL(k_cr_inplace<true>, dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
+  if (lds_tab && pf)
+    hipLaunchKernelGGL((k_cr_inplace<true, true>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
+  else if (lds_tab)
+    hipLaunchKernelGGL((k_cr_inplace<true, false>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else
-    hipLaunchKernelGGL(k_cr_inplace<false>, dim3((unsigned)grid), dim3(CI_THREADS), 0, st, A);
+    hipLaunchKernelGGL((k_cr_inplace<false, false>), dim3((unsigned)grid), dim3(CI_THREADS), 0, st, A);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   return MH_OK;
