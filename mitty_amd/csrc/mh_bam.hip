@@ -464,30 +464,32 @@ struct LoadSortedSize {
   }
 };
 
+// 32 lanes per record, two records per wave (as k_bam_write: each record is a short chain of dependent loads)
 __global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const int64_t *roff, const uint32_t *val,
                                                     const int64_t *soff, int64_t n, uint8_t *dst, const RInfo *info,
                                                     RInfo *sinfo) {
-  const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (k >= n) return;
+  constexpr int G = 32;
+  const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int gl = threadIdx.x & (G - 1);
+  if (k >= n) return;   // (a whole group)
   const uint32_t r = val[k];
   const int64_t a = roff[r], len = roff[r + 1] - a;
   const uint8_t *__restrict__ s = src + a;
   uint8_t *__restrict__ d = dst + soff[k];
-  for (int64_t j0 = 0; j0 < len; j0 += 512) {   // eight loads in flight per lane, then the stores
+  for (int64_t j0 = 0; j0 < len; j0 += 8 * G) {   // eight loads in flight per lane, then the stores
     uint8_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int64_t j = j0 + lane + 64 * u;
+      const int64_t j = j0 + gl + G * u;
       v[u] = j < len ? s[j] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int64_t j = j0 + lane + 64 * u;
+      const int64_t j = j0 + gl + G * u;
       if (j < len) d[j] = v[u];
     }
   }
-  if (lane == 0) sinfo[k] = info[r];
+  if (gl == 0) sinfo[k] = info[r];
 }
 
 }  // namespace
@@ -599,7 +601,8 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int64_t add_bytes = 0;
   HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
-  if (sorted_direct && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
+  static const bool direct_off = getenv("MH_BAM_DIRECT") && atoi(getenv("MH_BAM_DIRECT")) == 0;   // experiments
+  if (sorted_direct && !direct_off && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
     // the whole input is here (the context's own arenas) and the store is empty: sort first, then every record is
     // written once, straight to its coordinate-sorted place (no input-order copy, no gather)
     MH_TRY(ensure(ctx, B.key, sizeof(uint64_t) * n_rec));
@@ -688,7 +691,7 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
     stage_end(ctx);
   } else {
     stage_begin(ctx, "bam_gather");
-    hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 64, 256, INT32_MAX)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 32, 256, INT32_MAX)), dim3(256), 0, st,
                        (const uint8_t *)B.recs.p, (const int64_t *)B.roff.p, (const uint32_t *)B.val2.p,
                        (const int64_t *)B.soff.p, n, (uint8_t *)B.srecs.p, (const RInfo *)B.info.p,
                        (RInfo *)B.sinfo.p);
