@@ -1,25 +1,29 @@
 #!/usr/bin/env python3
-"""Benchmark: paired 2x150 bp templates/s for `generate-reads` at 30x on MI355X.
+"""Benchmark: paired 2x150 bp templates/s for `generate-reads` at 30x WGS on 1/2/4/8 MI355X.
 
-N = 1 (BASELINE.json configs[1]): a synthetic chr1-shaped contig (249,250,621 bp, N caps + centromere gap) with
-~1.3 variants/kbp (SNV/INS/DEL, long insertions, deliberate overlaps), phased diploid, read model
-hiseq-X-v2.5-Garvan (the built-in 2x150 model; SURVEY.md Finding 3), coverage 30, seed 7, perfect reads.  One step =
-the whole job for that chromosome: splice both haplotypes on the GPU, then the reference's 4 work units (2 copies x
-2 passes) — MT19937-exact template sampling + read emission — with the FASTQ output left in HBM.  Inputs (contig
-bytes and both copies' variant arrays) are resident before timing.
+Default workload (`--workload wgs`, BASELINE.json metric, configs[3]'s genome at every N): the whole synthetic GRCh37
+(24 contigs + MT at their real lengths, one BED interval per contig, i.i.d. ACGT with N caps and a centromere gap,
+~1.3 variants/kbp: SNV/INS/DEL, long insertions, deliberate overlaps, phased diploid), read model hiseq-X-v2.5-Garvan
+(the built-in 2x150 model; SURVEY.md Finding 3), coverage 30, seed 7, perfect reads, rng=mitty (MT19937-exact).  The
+reference's work-unit list (readgenerate.py:129-159: 25 regions x 2 copies x 2 passes = 100 units) is dealt to the
+ranks by mitty_amd.distributed's LPT plan.  One step = the whole genome's job: every haplotype spliced on the device,
+every unit sampled and emitted into the device FASTQ arenas, which are recycled per batch of units (the bytes of a
+batch are complete in HBM before the next batch overwrites them; at N = 1 a whole genome's 229 GB of FASTQ would not
+fit one GPU beside its inputs).  The same workload runs at every N (strong scaling: total work fixed), and at N > 1 an
+RCCL all-reduce of the per-rank template and byte counts closes each step (the counts the file writer turns into
+file offsets).  Inputs (contigs and variant arrays) are resident in HBM before timing.
 
-N > 1 (configs[3], torchrun, one process per GPU): the whole synthetic GRCh37 (24 contigs + MT, one BED interval per
-contig, ~100 work units) under mitty_amd.distributed's plan — work units dealt to ranks by LPT on region length,
-every unit sampled and emitted by its owner, no data-path collective — output in HBM; an RCCL all-reduce of the
-per-rank template and byte counts closes each step (the counts the file writer turns into offsets).  Total work is
-fixed as N grows (strong scaling).
+`--workload chr1`: BASELINE configs[1] (one chr1-shaped contig, 4 units per step; N = 1 only).
+`--tumor-normal`: BASELINE configs[4] on one GPU.
 
-Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_tiles; k_emit_write with
---emit-mode 1): algorithmic bytes per launch = sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ
-bytes written (both files), divided by the launch's HIP-event duration on the writer's stream; `stage_ms` gives
-every stage per step.  At N = 1 the line also carries `cpu_baseline` (the CPU oracle on the host cores) and
-`end_to_end` (FASTA + VCF files parsed on the host, GPU job, FASTQ copied to page-locked memory and written to
-/dev/null: the whole `generate-reads` command).
+N ranks: `python bench.py --gpus N` starts N rank processes itself (before any GPU call); under torchrun WORLD_SIZE
+must equal --gpus.  `MH_DIST_BACKEND=gloo` rehearses the plan with several ranks on one GPU.
+
+Prints one JSON line (rank 0).  `roofline` is for the emission writer (k_emit_tiles): algorithmic bytes per launch =
+sum over kept templates of 2*rlen (haplotype bases gathered) + FASTQ bytes written (both files), divided by the
+launch's HIP-event duration on the writer's stream; `stage_ms` gives every stage per step.  At N = 1 the line also
+carries `cpu_baseline` (the CPU oracle on the host cores, and the configs[0] CPU config beside it) and `end_to_end`
+(the whole `generate-reads` command on chr1: files in, FASTQ to /dev/null).
 """
 import argparse
 import glob
@@ -63,12 +67,21 @@ def parse():
                        'into one FASTQ pair, + the god-aligner BAM records built and coordinate-sorted in HBM')
   ap.add_argument('--tn-length', type=int, default=50_000_000,
                   help='--tumor-normal: contig length (a chr1 job at 90x of 2x250 does not fit one GPU with its BAM)')
+  ap.add_argument('--workload', default='wgs', choices=['wgs', 'chr1'],
+                  help='wgs: whole synthetic GRCh37 at every N (the metric; configs[3]); chr1: configs[1], N = 1')
   ap.add_argument('--genome-scale', type=float, default=1.0,
-                  help='N > 1: contig lengths scaled by this (rehearsals of the plan on one GPU; 1 = GRCh37)')
+                  help='wgs: contig lengths scaled by this (rehearsals of the plan; 1 = GRCh37)')
+  ap.add_argument('--batch-draws', type=float, default=32e6,
+                  help='wgs: units are sampled in batches of about this many template draws (a chr1 job is 30 M); '
+                       'the FASTQ arenas are recycled per batch')
+  ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
+  ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
+                  help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
+                       '--threads 2)')
   return ap.parse_args()
 
 
-def roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=True):
+def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
   agg = {}
   for name, ms in stages:
     agg.setdefault(name, [0.0, 0])
@@ -80,11 +93,11 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=True):
   traffic = None   # measured in separate rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE), see profiles/pmc_*.json
   pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_{}_*.json'.format(kernel))))
   traffic_src = None
-  if pmc and pmc_config:
+  if pmc and workload:
     try:
       with open(pmc[-1]) as fp:
         d = json.load(fp)
-      if d.get('rlen') == rlen and d.get('length') == CHR1:
+      if d.get('rlen') == rlen and d.get('workload', 'chr1' if d.get('length') == CHR1 else None) == workload:
         traffic = d.get('hbm_bytes_per_launch')
         traffic_src = os.path.relpath(pmc[-1], REPO)
     except Exception:
@@ -139,27 +152,56 @@ def timed(step, steps, warmup, eng, dist):
   return dt, kept, b1, b2, stages
 
 
+def launch_ranks(n):
+  """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+  MASTER_* as torchrun sets them) and exit with the worst exit status.  Nothing here touches the GPU (the ranks are
+  children, not an exec)."""
+  import signal
+  import socket
+  import subprocess
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  procs = []
+  for r in range(n):
+    env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+  rc = 0
+  try:
+    while procs:
+      for p in list(procs):
+        code = p.poll()
+        if code is None:
+          continue
+        procs.remove(p)
+        if code != 0:
+          rc = rc or code
+          for q in procs:   # one rank failed: the others would wait in a collective forever
+            q.send_signal(signal.SIGTERM)
+      time.sleep(0.05)
+  finally:
+    for q in procs:
+      q.kill()
+  return 1 if rc < 0 else rc
+
+
 def main():
   a = parse()
+  ws = os.environ.get('WORLD_SIZE')
+  if ws is None and a.gpus > 1:
+    sys.exit(launch_ranks(a.gpus))
+  world = int(ws or '1')
+  if world != a.gpus:
+    sys.exit('bench.py: --gpus {} but WORLD_SIZE={}: the launcher and the flag disagree'.format(a.gpus, world))
   rank = int(os.environ.get('RANK', '0'))
-  world = int(os.environ.get('WORLD_SIZE', '1'))
   local = int(os.environ.get('LOCAL_RANK', '0'))
-  dist = None
-  if world > 1:
-    import torch
-    import torch.distributed as tdist
-    local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks on one GPU
-    torch.cuda.set_device(local)
-    # MH_DIST_BACKEND=gloo: rehearsal of the multi-rank plan with several ranks on one GPU (RCCL needs one per GPU)
-    tdist.init_process_group(os.environ.get('MH_DIST_BACKEND', 'nccl'))
-    dist = tdist
-    run_genome(a, rank, world, local, dist)
-    dist.destroy_process_group()
+  if a.tumor_normal or a.workload == 'chr1':
+    if world != 1:
+      sys.exit('bench.py: --tumor-normal and --workload chr1 are one-GPU configs')
+    run_tumor_normal(a) if a.tumor_normal else run_chr1(a)
     return
-  if a.tumor_normal:
-    run_tumor_normal(a)
-    return
-  run_chr1(a)
+  run_genome(a, rank, world, local)
 
 
 def run_chr1(a):
@@ -345,94 +387,139 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     os.rmdir(d)
 
 
-def run_genome(a, rank, world, local, dist):
-  """configs[3]: whole synthetic GRCh37 over `world` GPUs, the distributed plan's LPT unit deal, output in HBM."""
-  import torch
+def run_genome(a, rank, world, local):
+  """The metric's workload at any N: whole synthetic GRCh37, the reference's unit list dealt to the ranks by LPT
+  (mitty_amd.distributed.plan_pieces), every unit sampled and emitted by its owner, output in HBM (arenas recycled
+  per batch), an all-reduce of the counts closing each step."""
   from mitty_amd import _native, synth
   from mitty_amd import distributed as D
-  from mitty_amd.engine import Engine
   from mitty_amd.readmodel import get_read_model
 
   _, model = get_read_model(a.model + '.pkl')
   rlen = int(model['mean_rlen'])
   p, passes = _native.read_model_params(rlen, a.coverage)
-  contigs = [(n, max(20000, int(L * a.genome_scale))) for n, L in synth.GRCH37]
+  contigs = synth.genome_contigs(a.genome_scale)
   units = _native.work_units(a.seed, [2] * len(contigs), passes)     # (region, copy, seed), reference order
   weights = [contigs[ri][1] for ri, _, _ in units]
-  pieces = D.plan_pieces(weights, world)                              # ~100 units >= 2 per rank: LPT, whole units
+  pieces = D.plan_pieces(weights, world, 'lpt')                       # 100 units: whole units by LPT at any N
   mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == rank]
   regions = sorted({ri for _, ri, _, _ in mine})
+  t_synth = time.perf_counter()
+  data = synth.genome_regions(contigs, regions, workers=max(1, a.synth_workers // world))
+  t_synth = time.perf_counter() - t_synth
 
+  dist = None
+  if world > 1:
+    import torch
+    import torch.distributed as tdist
+    local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks on one GPU
+    torch.cuda.set_device(local)
+    # MH_DIST_BACKEND=gloo: rehearsal of the multi-rank plan with several ranks on one GPU (RCCL needs one per GPU)
+    tdist.init_process_group(os.environ.get('MH_DIST_BACKEND', 'nccl'))
+    dist = tdist
+    if dist.get_world_size() != world:
+      sys.exit('bench.py: the process group has {} ranks, WORLD_SIZE={}'.format(dist.get_world_size(), world))
+  from mitty_amd.engine import Engine
   eng = Engine(local)
   copies = {}
   for ri in regions:
     name, length = contigs[ri]
-    seq = synth.contig(length, 1000 + ri)
-    copies[ri] = synth.copies_soa(synth.variants(seq, 2000 + ri))
+    seq, _, copies[ri] = data[ri]
     eng.load_region(ri, (name, 0, length), seq)
     for cpy in (0, 1):
       eng.upload_variants(ri, cpy, copies[ri][cpy])
-    del seq
   eng.ctx.set_emit_mode(a.emit_mode)
   kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
-  dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
-  counts = torch.zeros(3, dtype=torch.int64, device=dev)
+  batches, cur, draws = [], [], 0
+  for u in mine:   # batches of about --batch-draws template draws, in unit (ps) order
+    cur.append(u)
+    draws += int(contigs[u[1]][1] * p * 1.2)
+    if draws >= a.batch_draws:
+      batches.append(cur)
+      cur, draws = [], 0
+  if cur:
+    batches.append(cur)
+  if dist is not None:
+    import torch
+    dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
 
   def step():
     eng.drop_haplotypes()
-    eng.ctx.reset_output()
     kept = b1 = b2 = 0
-    batch, draws = [], 0
-    for k, u in enumerate(mine):   # batches of ~200 M draws, as process_multi_threaded samples them
-      batch.append(u)
-      draws += int(contigs[u[1]][1] * p * 1.2)
-      if draws >= 200_000_000 or k == len(mine) - 1:
-        for _, kp, x1, x2 in eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0,
-                                           True, a.rng):
-          kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
-        batch, draws = [], 0
-    counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
-    dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)
+    for batch in batches:
+      # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
+      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it
+      eng.ctx.reset_output()
+      for _, kp, x1, x2 in eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0,
+                                         True, a.rng):
+        kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
+    if dist is not None:
+      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
+      dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)
     return lambda: (kept, b1, b2)
 
   steps, warmup = a.steps, a.warmup
   dt, kept, b1, b2, stages = timed(step, steps, warmup, eng, dist)
   eng.close()
-  t = torch.tensor([dt], dtype=torch.float64, device=dev)
-  dist.all_reduce(t, op=dist.ReduceOp.MAX)
-  dt = float(t.item())
-  c = torch.tensor([kept, b1, b2, len(mine)], dtype=torch.int64, device=dev)
-  dist.all_reduce(c)
-  kept_all, b1_all, b2_all, n_units = (int(x) for x in c.tolist())
-  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, pmc_config=False)
-  if rank == 0:
-    out = {
-      'metric': METRIC,
-      'value': kept_all / dt,
-      'unit': 'templates/s',
-      'n_gpus': world,
-      'steps': steps,
-      'warmup': warmup,
-      'ms_per_step': dt / steps * 1e3,
-      'higher_is_better': True,
-      'scaling': 'strong',
-      'vs_baseline': None,
-      'dtype': 'int64+u8',
-      'data': 'synthetic GRCh37-shaped genome (24 contigs + MT) + ~1.3/kbp phased diploid variants (mitty_amd.synth)',
-      'config': {'workload': 'generate-reads whole GRCh37{} diploid, {} 2x{} PE, {}x, rng={}, one BED interval per '
-                             'contig, units dealt by LPT over {} GPUs (BASELINE configs[3])'.format(
-                               '' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
-                               a.model, rlen, a.coverage, a.rng, world),
-                 'genome_bp': sum(L for _, L in contigs),
-                 'read_model': a.model, 'coverage': a.coverage, 'units': n_units,
-                 'templates_per_step': kept_all // steps, 'parallelism': 'unit-shard (LPT) x{}'.format(world)},
-      'roofline': roof,
-      'roofline_rank': 0,
-      'cpu_baseline': None,
-      'stage_ms': stage_ms,
-      'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
-    }
-    print(json.dumps(out), flush=True)
+  kept_all, b1_all, b2_all, n_units = kept, b1, b2, len(mine)
+  backend, seen = None, 1
+  if dist is not None:
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    c = torch.tensor([kept, b1, b2, len(mine)], dtype=torch.int64, device=dev)
+    dist.all_reduce(c)
+    kept_all, b1_all, b2_all, n_units = (int(x) for x in c.tolist())
+    backend, seen = dist.get_backend(), dist.get_world_size()
+  workload = 'wgs' if a.genome_scale == 1 else None
+  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload)
+  cpu = e2e = None
+  if world == 1:
+    seq1, recs1, _ = data[0]
+    if not a.no_e2e and a.genome_scale == 1 and a.rng == 'mitty':
+      e2e = end_to_end(a, seq1, recs1, model, None)
+    if not a.no_cpu_baseline and a.cpu_baseline_mbp > 0:
+      cpu = cpu_baseline(a, seq1, recs1, p, rlen, model, _native.work_units(a.seed, [2], passes))
+      if a.cpu_config0:
+        cpu['configs0'] = cpu_baseline_config0(a, data)
+  if dist is not None:
+    dist.destroy_process_group()
+  if rank != 0:
+    return
+  ms_per_step = dt / steps * 1e3
+  out = {
+    'metric': METRIC,
+    'value': kept_all / dt,
+    'unit': 'templates/s',
+    'n_gpus': world,
+    'steps': steps,
+    'warmup': warmup,
+    'ms_per_step': ms_per_step,
+    'higher_is_better': True,
+    'scaling': 'strong',
+    'vs_baseline': None,
+    'dtype': 'int64+u8',
+    'data': 'synthetic GRCh37-shaped genome (24 contigs + MT) + ~1.3/kbp phased diploid variants (mitty_amd.synth), '
+            'seed-fixed',
+    'config': {'workload': 'generate-reads 30x WGS: whole GRCh37{} diploid, {} 2x{} PE, {}x, rng={}, one BED '
+                           'interval per contig, the 100 work units dealt by LPT over {} GPU(s) (BASELINE configs[3] '
+                           'genome)'.format('' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
+                                            a.model, rlen, a.coverage, a.rng, world),
+               'genome_bp': sum(L for _, L in contigs), 'read_model': a.model, 'coverage': a.coverage,
+               'units': n_units, 'batches_rank0': len(batches), 'templates_per_step': kept_all // steps,
+               'parallelism': 'unit-shard (LPT) x{}'.format(world) if world > 1 else 'single GPU',
+               'world_size_seen': seen, 'collective_backend': backend},
+    'roofline': roof,
+    'roofline_rank': 0,
+    'cpu_baseline': cpu,
+    'end_to_end': e2e,
+    'stage_ms': stage_ms,
+    'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
+    'setup_s': {'synth_inputs': round(t_synth, 2)},
+    'host_cpus': os.cpu_count(),
+  }
+  print(json.dumps(out), flush=True)
 
 
 def _cpu_unit(args):
@@ -467,6 +554,47 @@ def cpu_baseline(a, seq, recs, p, rlen, model, units):
           'sample': '{} work units (2 copies x {} passes, one worker process each, {} host CPUs) on chr1[0:{:.0f} Mbp), '
                     '{} templates in {:.2f} s'.format(len(jobs), len(jobs) // 2, os.cpu_count(), a.cpu_baseline_mbp,
                                                      n, dt)}
+
+
+HG001_BED = [('1', 20000, 1020000), ('10', 60000, 1060000)]   # reference examples/reads/hg001.bed
+
+
+def _cpu_unit_region(args):
+  """One configs[0] work unit through the CPU oracle (a worker of the 2-process pool)."""
+  ref, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy = args
+  sys.path.insert(0, REPO)
+  from oracle import oracle as O
+  return O.generate_unit_soa(ref, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy, keep_output=False)[0]
+
+
+def cpu_baseline_config0(a, data):
+  """BASELINE configs[0] as stated: `mitty generate-reads` on hg001.bed (2 regions x 1 Mbp) with the 1kg-pcr-free
+  model (2x250), 30x, seed 7, --threads 2 — here the CPU oracle in 2 worker processes that take the 8 work units in
+  the reference's unit order (readgenerate.py:102-115), on the synthetic contigs 1 and 10."""
+  import multiprocessing as mp
+  from mitty_amd import _native, synth
+  from mitty_amd.readmodel import get_read_model
+  _, model = get_read_model('1kg-pcr-free.pkl')
+  rlen = int(model['mean_rlen'])
+  p, passes = _native.read_model_params(rlen, a.coverage)
+  idx = {name: ri for ri, (name, _) in enumerate(synth.GRCH37)}
+  units = _native.work_units(a.seed, [2] * len(HG001_BED), passes)
+  jobs = []
+  for ps, (ri, cpy, seed) in enumerate(units):
+    chrom, s0, e = HG001_BED[ri]
+    seq, recs, _ = data[idx[chrom]]
+    soa = synth.copies_soa(recs, s0, e)[cpy]
+    jobs.append((seq[s0:e], s0, soa, p, rlen, model['cum_tlen'], seed, 'SYN:{}:{}'.format(ps % 2, ps // 2), chrom,
+                 cpy))
+  with mp.get_context('spawn').Pool(2) as pool:
+    pool.map(_cpu_unit_region, jobs[:2])   # workers warm (imports) before timing
+    t0 = time.perf_counter()
+    n = sum(pool.map(_cpu_unit_region, jobs, chunksize=1))
+    dt = time.perf_counter() - t0
+  return {'value': n / dt, 'unit': 'templates/s', 'cores': 2, 'kind': 'port',
+          'sample': 'BASELINE configs[0]: hg001.bed (1:20000-1020000, 10:60000-1060000) on the synthetic contigs, '
+                    '1kg-pcr-free 2x{}, {}x, seed {}, 2 worker processes over the {} work units: {} templates in '
+                    '{:.2f} s'.format(rlen, a.coverage, a.seed, len(jobs), n, dt)}
 
 
 if __name__ == '__main__':

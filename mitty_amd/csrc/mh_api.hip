@@ -736,6 +736,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
     HIPCHK(ctx, hipMemcpyAsync(ts.pos1.p, pos1, 8 * n, k, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (ts.prep.valid) ctx->eset[ts.prep.set].prepared = false;   // the buffer set of a measure pass made for the old set
   ts.prep.valid = false;
   ts.n = n;
   ts.rlen = rlen;

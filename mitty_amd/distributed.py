@@ -113,35 +113,47 @@ class DeviceBackend:
         out[k] = int(n)
     return out
 
+  # the broadcast buffer of a template set of n templates: pos0 at 0, pos1 at 8n, fo0 at 16n (17 B per template)
+  def pack_device(self, k, n, ptr):
+    """Template set k into the device buffer at ptr (>= 17 n bytes); returns n."""
+    return self.eng.ctx.templates_export(k, ptr + 16 * n, ptr, ptr + 8 * n, n)
+
+  def unpack_device(self, k, n, rlen, ptr):
+    self.eng.ctx.templates_import(k, n, rlen, ptr + 16 * n, ptr, ptr + 8 * n, on_device=True)
+
+  def pack_host(self, k, n, a):
+    """Template set k into the uint8 host array a (>= 17 n bytes)."""
+    fo0, p0, p1 = self.eng.ctx.templates_export(k)
+    assert len(fo0) == n
+    a[:8 * n] = p0.view(np.uint8)
+    a[8 * n:16 * n] = p1.view(np.uint8)
+    a[16 * n:17 * n] = fo0.view(np.uint8)
+
+  def unpack_host(self, k, n, rlen, a):
+    self.eng.ctx.templates_import(k, n, rlen, a[16 * n:17 * n].view(np.int8), a[:8 * n].view(np.int64),
+                                  a[8 * n:16 * n].view(np.int64))
+
   def share(self, k, n, src, rlen, group=None):
     """Template set k (n templates) from rank src to every rank: an RCCL broadcast of the device arrays under
     'nccl' (pos0 | pos1 | fo0 packed in one buffer, device-to-device copies on either side), host arrays under gloo."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
-    ctx = self.eng.ctx
     if dist.get_backend(group) == 'nccl':
       buf = torch.empty(max(17 * n, 16), dtype=torch.uint8, device='cuda')
-      b = buf.data_ptr()
       if rank == src:
-        ctx.templates_export(k, b + 16 * n, b, b + 8 * n, n)
+        self.pack_device(k, n, buf.data_ptr())   # (synchronous: the copies are done before the broadcast reads)
       dist.broadcast(buf, src, group=group)
       torch.cuda.current_stream().synchronize()
       if rank != src:
-        ctx.templates_import(k, n, rlen, b + 16 * n, b, b + 8 * n, on_device=True)
+        self.unpack_device(k, n, rlen, buf.data_ptr())
       return
     buf = torch.empty(max(17 * n, 16), dtype=torch.uint8)
     if rank == src:
-      fo0, p0, p1 = ctx.templates_export(k)
-      a = buf.numpy()
-      a[:8 * n] = p0.view(np.uint8)
-      a[8 * n:16 * n] = p1.view(np.uint8)
-      a[16 * n:17 * n] = fo0.view(np.uint8)
+      self.pack_host(k, n, buf.numpy())
     dist.broadcast(buf, src, group=group)
     if rank != src:
-      a = buf.numpy()
-      ctx.templates_import(k, n, rlen, a[16 * n:17 * n].view(np.int8), a[:8 * n].view(np.int64),
-                           a[8 * n:16 * n].view(np.int64))
+      self.unpack_host(k, n, rlen, buf.numpy())
 
   def count_kept(self, k, t0, t1):
     self.eng.ctx.use_templates(k)

@@ -1,5 +1,4 @@
 """FASTA access for read generation (replaces pysam.FastaFile.fetch, reference readgenerate.py:181,186)."""
-import gzip
 
 
 def read_fasta(fname, names=None):
@@ -11,10 +10,9 @@ def read_fasta(fname, names=None):
 
 def read_fasta_py(fname, names=None):
   """The same in Python (kept for the host-reader test)."""
-  with open(fname, 'rb') as fp:
-    gz = fp.read(2) == b'\x1f\x8b'
+  from mitty_amd.lib.openfile import open_input
   seqs, name, chunks, keep = {}, None, [], True
-  with (gzip.open(fname, 'rb') if gz else open(fname, 'rb')) as fp:
+  with open_input(fname) as fp:   # one open: FIFOs and process substitution lose no bytes
     for line in fp:
       if line.startswith(b'>'):
         if name is not None and keep:

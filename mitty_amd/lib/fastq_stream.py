@@ -4,39 +4,97 @@ The host reads large chunks (gzip handled as pysam.FastxFile does); the device f
 reports how many bytes of each buffer it consumed (whole templates only, the same number from both files); the
 rest is carried into the next call.
 """
-import gzip
+from mitty_amd.lib.openfile import open_input
 
 
-def _reader(fname, chunk):
-  with open(fname, 'rb') as fp:
-    gz = fp.read(2) == b'\x1f\x8b'
-  fp = gzip.open(fname, 'rb') if gz else open(fname, 'rb')
-  try:
-    while True:
-      b = fp.read(chunk)
-      if not b:
-        return
-      yield b
-  finally:
-    fp.close()
+class _Prefetch:
+  """One input file read on its own thread into a queue of pieces (at most `max_bytes` not yet taken), so that a
+  producer writing the two files of a pair (a FIFO or `<(...)` each, examples/reads/run.sh:13-16) never blocks on one
+  pipe while we wait on the other: both pipes are drained as data arrives, whatever order the producer writes in
+  (record by record like the reference's writer, readgenerate.py:233-253, or file by file in pieces up to
+  `max_bytes`)."""
+
+  def __init__(self, fname, piece, max_bytes):
+    import collections
+    import threading
+    self._pieces = collections.deque()
+    self._cv = threading.Condition()
+    self._held = 0             # bytes read and not yet taken
+    self._eof = False
+    self._err = None
+    self._piece, self._max = piece, max_bytes
+    self._t = threading.Thread(target=self._run, args=(fname,), daemon=True)
+    self._t.start()
+
+  def _run(self, fname):
+    try:
+      with open_input(fname) as fp:   # one open: FIFOs and process substitution lose no bytes
+        read = getattr(fp, 'read1', fp.read)
+        while True:
+          with self._cv:
+            while self._held >= self._max:
+              self._cv.wait()
+          b = read(self._piece)   # what the pipe holds, or a whole piece of a file
+          if not b:
+            break
+          with self._cv:
+            self._pieces.append(b)
+            self._held += len(b)
+            self._cv.notify_all()
+    except BaseException as e:   # re-raised in the consumer
+      self._err = e
+    finally:
+      with self._cv:
+        self._eof = True
+        self._cv.notify_all()
+
+  def take(self, want):
+    """Up to about `want` bytes: blocks until some are there, then takes what is queued.  b'' at end of file."""
+    with self._cv:
+      while not self._pieces and not self._eof:
+        self._cv.wait()
+      out, n = [], 0
+      while self._pieces and n < want:
+        b = self._pieces.popleft()
+        out.append(b)
+        n += len(b)
+      self._held -= n
+      self._cv.notify_all()
+      if not out and self._err is not None:
+        raise self._err
+    return b''.join(out)
 
 
-def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None):
-  """consume(buf1, buf2_or_None, max_templates, t_done) -> (used1, used2, templates).  Returns the templates done."""
-  r1 = _reader(fastq1, chunk)
-  r2 = _reader(fastq2, chunk) if fastq2 else None
+def _fill(r, buf, chunk, stalled):
+  """buf topped up to `chunk` bytes (blocking until there or EOF), or by one more take when the consumer stalled."""
+  parts, n = [buf], len(buf)
+  while n < chunk or stalled:
+    nxt = r.take(max(chunk - n, 1))
+    if not nxt:
+      return b''.join(parts), True
+    parts.append(nxt)
+    n += len(nxt)
+    if stalled:
+      break
+  return b''.join(parts), False
+
+
+def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None, max_ahead=None):
+  """consume(buf1, buf2_or_None, max_templates, t_done) -> (used1, used2, templates).  Returns the templates done.
+  Each file is prefetched on its own thread, up to `max_ahead` bytes (default: 2 chunks, at least 1 GiB) beyond what
+  the device has taken."""
+  ahead = max_ahead or max(2 * chunk, 1 << 30)
+  piece = min(chunk, 16 << 20)
+  r1 = _Prefetch(fastq1, piece, ahead)
+  r2 = _Prefetch(fastq2, piece, ahead) if fastq2 else None
   buf1, buf2 = b'', (b'' if fastq2 else None)
   eof1 = eof2 = False
   total, stalled = 0, False
   while True:
-    if not eof1 and (len(buf1) < chunk or stalled):
-      nxt = next(r1, None)
-      eof1 = nxt is None
-      buf1 += nxt or b''
-    if r2 is not None and not eof2 and (len(buf2) < chunk or stalled):
-      nxt = next(r2, None)
-      eof2 = nxt is None
-      buf2 += nxt or b''
+    if not eof1:
+      buf1, eof1 = _fill(r1, buf1, chunk, stalled)
+    if r2 is not None and not eof2:
+      buf2, eof2 = _fill(r2, buf2, chunk, stalled)
     done = eof1 and (r2 is None or eof2)
     if done:   # a last record without its final newline
       if buf1 and not buf1.endswith(b'\n'):
@@ -55,6 +113,32 @@ def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None):
     if done and t == 0:
       break
   return total
+
+
+def write_pair(sinks, datas):
+  """Write datas[f] to sinks[f] (None: skipped), each file on its own thread, so a reader that takes the two files in
+  lockstep (pysam FastxFile pairs, `corrupt-reads` on FIFOs) never leaves us blocked on one pipe while it waits on
+  the other."""
+  jobs = [(s, d) for s, d in zip(sinks, datas) if s is not None]
+  if len(jobs) <= 1:
+    for s, d in jobs:
+      s.write(d)
+    return
+  import threading
+  errs = []
+
+  def run(s, d):
+    try:
+      s.write(d)
+    except BaseException as e:
+      errs.append(e)
+  ts = [threading.Thread(target=run, args=j) for j in jobs]
+  for t in ts:
+    t.start()
+  for t in ts:
+    t.join()
+  if errs:
+    raise errs[0]
 
 
 class FastqSink:

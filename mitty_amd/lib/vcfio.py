@@ -11,10 +11,11 @@ Semantics follow the reference + htslib exactly:
 The engine consumes the structure-of-arrays form (`load_variants_soa`); `load_variant_file` returns the reference's
 list-of-Variant form for API compatibility.
 """
-import gzip
 import logging
 
 import numpy as np
+
+from mitty_amd.lib.openfile import open_input
 
 logger = logging.getLogger(__name__)
 
@@ -42,9 +43,7 @@ def read_bed(bed_fname):
 
 
 def _open(fname):
-  with open(fname, 'rb') as fp:
-    gz = fp.read(2) == b'\x1f\x8b'
-  return gzip.open(fname, 'rb') if gz else open(fname, 'rb')
+  return open_input(fname)   # one open: FIFOs and process substitution lose no bytes
 
 
 class _Records:

@@ -18,7 +18,7 @@ import time
 import numpy as np
 
 from mitty_amd import _native
-from mitty_amd.lib.fastq_stream import FastqSink, stream_templates
+from mitty_amd.lib.fastq_stream import FastqSink, stream_templates, write_pair
 
 logger = logging.getLogger(__name__)
 
@@ -51,9 +51,7 @@ def multi_process(read_module, read_model, fastq1_in, fastq1_out, fastq2_in=None
 
     def flush():
       d1, d2 = ctx.fetch_output()
-      fps[0].write(d1)
-      if len(fps) > 1:
-        fps[1].write(d2)
+      write_pair(fps + [None] * (2 - len(fps)), [d1, d2])   # each file on its own thread (FIFO outputs)
       ctx.reset_output()
 
     n = stream_templates(fastq1_in, fastq2_in, consume, chunk_bytes)

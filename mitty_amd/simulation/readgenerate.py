@@ -16,7 +16,7 @@ from mitty_amd import _native
 from mitty_amd.engine import Engine
 from mitty_amd.lib import fasta as mfasta
 from mitty_amd.lib import vcfio
-from mitty_amd.lib.fastq_stream import FastqSink
+from mitty_amd.lib.fastq_stream import FastqSink, write_pair
 
 logger = logging.getLogger(__name__)
 
@@ -91,7 +91,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   fp1 = FastqSink(fastq1_fname)   # '.gz' names get BGZF output
   fp2 = FastqSink(fastq2_fname) if write2 else None
 
-  pins = [_native.PinnedBuffer()]   # page-locked D2H staging for the sinks
+  pins = [_native.PinnedBuffer(), _native.PinnedBuffer()]   # page-locked D2H staging, one per file
 
   def flush(ps, n, kept, b1, b2):
     stats['templates'] += n
@@ -100,7 +100,10 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     stats['bytes2'] += b2
     u1, u2 = eng.ctx.output_size()
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
-      eng.ctx.stream_output([fp1, fp2 if write2 else None], pins[0])
+      # both arenas to page-locked memory, then each file written on its own thread: a FIFO reader that takes the
+      # two files in lockstep (examples/reads/run.sh:13-16) is never starved of one while we block on the other
+      d1, d2 = eng.ctx.fetch_output_pinned(pins)
+      write_pair([fp1, fp2 if write2 else None], [d1, d2])
       eng.ctx.reset_output()
 
   try:

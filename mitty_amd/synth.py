@@ -101,6 +101,38 @@ def copies_soa(recs, start0=0, end=None):
   return out
 
 
+def genome_contigs(scale=1.0, min_len=20000):
+  """GRCh37's contigs, lengths scaled by `scale` (rehearsals on small genomes; 1 = the real lengths)."""
+  if scale == 1.0:
+    return list(GRCH37)
+  return [(n, max(min_len, int(L * scale))) for n, L in GRCH37]
+
+
+def _region_job(args):
+  length, cseed, vseed = args
+  seq = contig(length, cseed)
+  recs = variants(seq, vseed)
+  return seq, recs, copies_soa(recs)
+
+
+def genome_regions(contigs, indices, workers=8):
+  """Synthetic inputs of the whole-genome workload for the regions `indices` of `contigs`: region ri gets contig seed
+  1000 + ri and variant seed 2000 + ri.  Returns {ri: (seq, records, per-copy SoA)}.  Built in `workers` spawned
+  processes (fresh interpreters: safe whether or not the caller has touched the GPU)."""
+  jobs = [(contigs[ri][1], 1000 + ri, 2000 + ri) for ri in indices]
+  if workers <= 1 or len(jobs) <= 1:
+    res = [_region_job(j) for j in jobs]
+  else:
+    import multiprocessing as mp
+    order = sorted(range(len(jobs)), key=lambda k: -jobs[k][0])   # longest first
+    with mp.get_context('spawn').Pool(min(workers, len(jobs))) as pool:
+      got = pool.map(_region_job, [jobs[k] for k in order], chunksize=1)
+    res = [None] * len(jobs)
+    for k, r in zip(order, got):
+      res[k] = r
+  return dict(zip(indices, res))
+
+
 def write_fasta(path, contigs, width=60):
   with open(path, 'wb') as fp:
     for name, s in contigs:

@@ -294,3 +294,34 @@ def corrupt_fastq(model, names, seq1, seq2, seed=7):
   lib().mo_free(o1)
   lib().mo_free(o2)
   return b1, b2
+
+
+def _unit_digest(args):
+  """One work unit in a worker process: (templates, len1, sha256 of file 1's bytes, len2, sha256 of file 2's)."""
+  import hashlib
+  ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy = args
+  n, b1, b2 = generate_unit_soa(ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy)
+  return n, len(b1), hashlib.sha256(b1).hexdigest(), len(b2), hashlib.sha256(b2).hexdigest()
+
+
+def unit_digests(seqs, vdf, sample, model, coverage, seed, workers=8):
+  """readgenerate.process_multi_threaded(..., threads=1) unit by unit: per unit in the reference's order (ps), the
+  byte length and sha256 of its piece of each FASTQ file (the files are the pieces concatenated in ps order).  Units
+  run in `workers` spawned processes.  Returns [(ps, region_idx, cpy, templates, len1, sha1, len2, sha2)]."""
+  import multiprocessing as mp
+  p, passes = read_model_params(model['mean_rlen'], coverage)
+  units = work_units(seed, [len(r['v']) for r in vdf], passes)
+  jobs = []
+  for ps, (ri, cpy, s) in enumerate(units):
+    chrom, s0, e = vdf[ri]['region']
+    pos, op, oplen, aoff, alen, pool = _variant_soa(vdf[ri]['v'][cpy])
+    soa = {'pos': pos, 'op': op, 'oplen': oplen, 'alt_off': aoff, 'alt_len': alen, 'alt_pool': pool}
+    jobs.append((seqs[chrom][s0:e], s0, soa, p, int(model['mean_rlen']), model['cum_tlen'], s,
+                 '{}:{}:{}'.format(sample, 0, ps), chrom, cpy))
+  order = sorted(range(len(jobs)), key=lambda k: -len(jobs[k][0]))   # longest first
+  with mp.get_context('spawn').Pool(max(1, min(workers, len(jobs)))) as pool:
+    got = pool.map(_unit_digest, [jobs[k] for k in order], chunksize=1)
+  res = [None] * len(jobs)
+  for k, r in zip(order, got):
+    res[k] = r
+  return [(ps, units[ps][0], units[ps][1]) + tuple(res[ps]) for ps in range(len(jobs))]

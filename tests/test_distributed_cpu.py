@@ -104,3 +104,53 @@ def _rank_gz(rank, world, port, outdir, names):
                                  seed=c['seed'], backend=OracleBackend(), layout='slice')
   finally:
     dist.destroy_process_group()
+
+
+def _rank_wgs(rank, world, port, g, outdir):
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    from mitty_amd.readmodel import get_read_model
+    from tests.dist_host import OracleBackend
+    mod, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+    st = D.generate_reads_distributed(g['fa'], g['vcf'], 'SYN', g['bed'], mod, mdl, 30.0,
+                                      os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'), seed=7,
+                                      backend=OracleBackend(), max_batch_draws=100_000)
+    assert st['units'] == 100 and st['pieces'] >= 20   # LPT: whole units, every rank has a share
+  finally:
+    dist.destroy_process_group()
+
+
+def test_wgs_plan_four_ranks(tmp_path):
+  """The whole-genome plan (GRCh37's 25 contigs, one BED interval each, 100 units dealt by LPT; the bench's and
+  configs[3]'s shape) over 4 gloo ranks, at lengths x0.0005: the files equal the oracle's units in unit order."""
+  import hashlib
+  import socket
+  import torch.multiprocessing as mp
+  from mitty_amd import synth
+  from mitty_amd.readmodel import get_read_model
+  from oracle import oracle as O
+  contigs = synth.genome_contigs(0.0005)
+  data = synth.genome_regions(contigs, list(range(len(contigs))), workers=1)
+  seqs = [(n, data[ri][0]) for ri, (n, _) in enumerate(contigs)]
+  g = {'fa': str(tmp_path / 'g.fa'), 'vcf': str(tmp_path / 'g.vcf.gz'), 'bed': str(tmp_path / 'g.bed')}
+  synth.write_fasta(g['fa'], seqs)
+  synth.write_vcf(g['vcf'], seqs, {n: data[ri][1] for ri, (n, _) in enumerate(contigs)})
+  with open(g['bed'], 'w') as fp:
+    fp.write(''.join('{}\t0\t{}\n'.format(n, L) for n, L in contigs))
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  mp.start_processes(_rank_wgs, args=(4, port, g, str(tmp_path)), nprocs=4, join=True, start_method='spawn')
+  _, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  units = O.unit_digests(dict(seqs), O.load_variant_file(g['vcf'], 'SYN', g['bed']), 'SYN', mdl, 30.0, 7, workers=4)
+  assert len(units) == 100 and len({u[1] for u in units}) == 25
+  for f, (li, hi) in (('r1.fq', (4, 5)), ('r2.fq', (6, 7))):
+    b = open(str(tmp_path / f), 'rb').read()
+    assert len(b) == sum(u[li] for u in units)
+    off = 0
+    for u in units:
+      assert hashlib.sha256(b[off:off + u[li]]).hexdigest() == u[hi], (f, u[:3])
+      off += u[li]

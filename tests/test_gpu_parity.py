@@ -215,6 +215,88 @@ def test_e2e_single_file_and_cli(native, tmp_path):
   G.check_same(open(f1, 'rb').read(), G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz'))
 
 
+def _lockstep_reader(f1, f2):
+  """A consumer of a FIFO pair that alternates record by record (pysam.FastxFile zip, readcorrupt.py:49-53)."""
+  import threading
+  got = ([], [])
+
+  def run():
+    with open(f1, 'rb') as a, open(f2, 'rb') as b:
+      while True:
+        x = b''.join(a.readline() for _ in range(4))
+        y = b''.join(b.readline() for _ in range(4))
+        if not x and not y:
+          return
+        got[0].append(x)
+        got[1].append(y)
+  t = threading.Thread(target=run, daemon=True)
+  t.start()
+  return t, got
+
+
+def _fifo_producer(path, data):
+  import threading
+  def run():
+    with open(path, 'wb') as fp:   # one open, as `tee > tf1` does
+      fp.write(data[:1])
+      fp.flush()
+      fp.write(data[1:])
+  t = threading.Thread(target=run, daemon=True)
+  t.start()
+  return t
+
+
+@pytest.mark.timeout(120)
+def test_generate_reads_into_fifos_and_gz(native, tmp_path):
+  """generate-reads writing both files into FIFOs read in lockstep (examples/reads/run.sh:13-16), with small flushes
+  so several pieces cross the pipes; then '.gz' names: BGZF files that decompress to the golden bytes."""
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  model = '1kg-pcr-free'
+  c = G.load_json('e2e_config.json')[model]
+  mod, mdl = get_read_model(model + '.pkl')
+  f1, f2 = str(tmp_path / 'tf1'), str(tmp_path / 'tf2')
+  os.mkfifo(f1)
+  os.mkfifo(f2)
+  t, got = _lockstep_reader(f1, f2)
+  readgenerate.process_multi_threaded(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], f1, f2, seed=c['seed'], flush_bytes=50_000)
+  t.join(60)
+  G.check_same(b''.join(got[0]), G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
+  G.check_same(b''.join(got[1]), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
+  z1, z2 = str(tmp_path / 'r1.fq.gz'), str(tmp_path / 'r2.fq.gz')
+  readgenerate.process_multi_threaded(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], z1, z2, seed=c['seed'], flush_bytes=50_000)
+  for z, k in ((z1, 1), (z2, 2)):
+    raw = open(z, 'rb').read()
+    assert raw[:4] == b'\x1f\x8b\x08\x04' and raw[-28:] == bytes.fromhex(
+      '1f8b08040000000000ff0600424302001b0003000000000000000000')   # BGZF blocks + EOF marker
+    G.check_same(gzip.decompress(raw), G.fastq_bytes('e2e_{}.r{}.fq.gz'.format(model, k)))
+
+
+@pytest.mark.timeout(120)
+def test_corrupt_reads_fifo_in_fifo_out(native, tmp_path):
+  """corrupt-reads --rng mitty with both inputs on single-open FIFO producers (gzip bytes, like `<(cat < tf1)` of a
+  gzip stream) and both outputs on FIFOs read in lockstep: byte-identical to the reference's processes=1 output."""
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readcorrupt
+  model = 'hiseq-X-v2.5-Garvan'
+  mod, mdl = get_read_model(model + '.pkl')
+  fi1, fi2, fo1, fo2 = (str(tmp_path / n) for n in ('i1', 'i2', 'o1', 'o2'))
+  for f in (fi1, fi2, fo1, fo2):
+    os.mkfifo(f)
+  p1 = _fifo_producer(fi1, open(G.path('corrupt_in_{}.r1.fq.gz'.format(model)), 'rb').read())
+  p2 = _fifo_producer(fi2, open(G.path('corrupt_in_{}.r2.fq.gz'.format(model)), 'rb').read())
+  t, got = _lockstep_reader(fo1, fo2)
+  readcorrupt.multi_process(mod, mdl, fi1, fo1, fi2, fo2, processes=1, seed=7, chunk_bytes=3001,
+                            flush_bytes=20_000)
+  p1.join(30)
+  p2.join(30)
+  t.join(60)
+  G.check_same(b''.join(got[0]), G.fastq_bytes('corrupt_{}.r1.fq.gz'.format(model)), 'corrupt file 1')
+  G.check_same(b''.join(got[1]), G.fastq_bytes('corrupt_{}.r2.fq.gz'.format(model)), 'corrupt file 2')
+
+
 def _unit_vs_oracle(length, seed, model, n_seed=1, rate=1.3e-3, start0=0, cpys=(0, 1), emit_mode=0):
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
@@ -839,6 +921,54 @@ def _gpu_rank(rank, world, port, layout, outdir):
                                  seed=c['seed'], backend=D.DeviceBackend(0), layout=layout)
   finally:
     dist.destroy_process_group()
+
+
+def test_template_broadcast_packing_round_trip(native):
+  """The sliced multi-GPU layout's broadcast unit (DeviceBackend.share): a sampled unit's templates packed into one
+  device buffer (pos0 | pos1 | fo0 at 0 / 8n / 16n, the RCCL payload) and into a host buffer (the gloo payload),
+  imported into another template set, emit the same FASTQ bytes as the sampled set; share() itself under a one-rank
+  gloo group."""
+  import socket
+  import torch
+  import torch.distributed as dist
+  from mitty_amd import distributed as D, synth
+  from mitty_amd.readmodel import get_read_model
+  _, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  p, _ = native.read_model_params(150, 30.0)
+  seq = synth.contig(400_000, 31)
+  soa = synth.copies_soa(synth.variants(seq, 32))
+  be = D.DeviceBackend(0)
+  try:
+    be.load_region(0, ('4', 0, len(seq)), seq)
+    unit = (0, 0, 1, 123456)
+    ns = be.sample([unit, unit], lambda r, c: soa[c], p, 150, mdl['cum_tlen'], 'mitty', which=[0])
+    n = ns[0]
+    assert n > 10000 and ns[1] is None
+
+    def emitted(k):
+      _, r1, r2 = be.emit(k, 'S:0:0', '4', 1, True, unit[3], None, 0)
+      return be.fetch(r1, r2)
+    want = emitted(0)
+    buf = torch.empty(17 * n, dtype=torch.uint8, device='cuda')
+    assert be.pack_device(0, n, buf.data_ptr()) == n
+    be.unpack_device(1, n, 150, buf.data_ptr())
+    assert emitted(1) == want
+    host = np.zeros(17 * n, np.uint8)
+    be.pack_host(0, n, host)
+    assert np.array_equal(host, buf.cpu().numpy())
+    be.unpack_host(1, n, 150, host)
+    assert emitted(1) == want
+    with socket.socket() as s:
+      s.bind(('127.0.0.1', 0))
+      port = s.getsockname()[1]
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port), rank=0, world_size=1)
+    try:
+      be.share(0, n, 0, 150)
+    finally:
+      dist.destroy_process_group()
+    assert emitted(0) == want
+  finally:
+    be.close()
 
 
 @pytest.mark.parametrize('layout', ['lpt', 'slice'])
