@@ -391,6 +391,10 @@ def run_genome(a, rank, world, local):
   """The metric's workload at any N: whole synthetic GRCh37, the reference's unit list dealt to the ranks by LPT
   (mitty_amd.distributed.plan_pieces), every unit sampled and emitted by its owner, output in HBM (arenas recycled
   per batch), an all-reduce of the counts closing each step."""
+  if world > 1:
+    # torch before libmitty_hip: a process holds ONE HIP runtime, and whichever library loads first provides it
+    # (ours needs libamdhip64.so.7, which torch's copy satisfies; torch's own libamdhip64.so would not reuse ours)
+    import torch  # noqa: F401
   from mitty_amd import _native, synth
   from mitty_amd import distributed as D
   from mitty_amd.readmodel import get_read_model

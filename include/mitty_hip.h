@@ -16,6 +16,7 @@
  *   mh_get_templates      (same arrays back to the host)
  *   mh_emit_reads         read_generating_worker loop + fastq_lines      mitty/simulation/readgenerate.py:184-230
  *   mh_read_batch         rpc.get_begin_end_nodes + rpc.generate_read    mitty/simulation/rpc.py:119-160
+ *   mh_expand_variant     rpc.create_nodes / snp / insertion / deletion  mitty/simulation/rpc.py:66-116
  *   mh_set_corruption     illumina.corrupt_template / corrupt_single_read mitty/simulation/illumina.py:113-162
  *   mh_set_corruption_stream  corrupt_rng = RandomState(seed) of a worker  mitty/simulation/readcorrupt.py:84
  *   mh_corrupt_fastq      readcorrupt.multi_process's reader/worker/writer  mitty/simulation/readcorrupt.py:18-118
@@ -95,6 +96,14 @@ int32_t mh_release_variants(mh_ctx *ctx, int32_t vset);
 int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_t *op, int64_t *oplen,
                      char *hap, int64_t hap_cap, int64_t *hap_len);
 int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot);
+/* The nodes ONE variant adds at cursors (samp_pos, ref_pos) of a region starting at ref_start_pos — the node rules
+ * of the device splice (the same function runs inside it), exposed for the reference's per-variant helpers
+ * rpc.snp / insertion / deletion (op 'X' / 'I' / 'D' selects the rule, as the helper name does).  Host-only, no
+ * context.  out: up to 2 nodes x {ps, pr, op, oplen, src} (src: offset of an '=' node's bytes in the region's
+ * reference, of an 'X' / 'I' node's bytes in the variant's alt allele, -1 for 'D'); *n_nodes = 1 or 2;
+ * *samp_next / *ref_next: the cursors after the variant. */
+int32_t mh_expand_variant(int64_t samp_pos, int64_t ref_pos, int64_t ref_start_pos, int64_t v_pos, int32_t op,
+                          int64_t oplen, int64_t *out, int32_t *n_nodes, int64_t *samp_next, int64_t *ref_next);
 
 /* ---- templates ----------------------------------------------------------------------------------------- */
 /* illumina.generate_reads for haplotype `slot` (p_min/p_max from the slot).  rng_mode MH_RNG_MITTY reproduces
@@ -152,7 +161,8 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
  * unit's measure pass, record offsets, writer and corruption are queued on the writer stream and the call returns a
  * ticket at once.  The unit lands in the arenas after the units queued before it (its base offsets come from the
  * device); room is reserved from mh_haplotype_read_bound.  mh_emit_result waits for the ticket's unit and returns its
- * kept count, bytes and base offsets per file (256 tickets in flight; read a ticket before it comes round again). */
+ * kept count, bytes and base offsets per file (256 result slots: a ticket not read before its slot is handed out
+ * again, 256 emissions later, is rejected as stale with MH_E_STATE). */
 int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int32_t *out_ticket);
 int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2,
@@ -261,8 +271,14 @@ int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char 
  * applies while it writes each record, and that mh_corrupt_fastq applies to existing FASTQ: per base
  * bq = min(searchsorted(cum_bq[file][n], U1), 93) over the f64 table, the base replaced by one of the other three
  * ('NNN' for non-ACGT) when U2 < phred_p[bq], quality chr(bq + 33) instead of '~'.  U1, U2 are 53-bit doubles
- * built as numpy's rand() builds them.  Their words come from Philox4x32-10 keyed by (seed, unit_key) and counted
- * by (template, file, base), so the output does not depend on GPU count or launch geometry.  cum_bq:
+ * built as numpy's rand() builds them.  Their words come from Philox4x32-10 keyed by (seed, unit_key): ONE draw per
+ * three bases, counter (template, file << 16 | base / 3).  Base base % 3 = k of the triple takes word k — its high
+ * 16 bits are the top of U1, its low 16 bits the top of U2 — and the fourth word holds the three bases' replacement
+ * choices (bits 10k .. 10k + 9: c % 3; c = 1023 is redrawn from the base's own draw (template, file << 16 | 0x8000 |
+ * base)).  The low 37 bits of U1 and U2 come from the base's draw (template, file << 16 | 0x4000 | base), which the
+ * device takes only when the 16-bit prefix ties a table threshold's prefix (the f64 comparison then decides).
+ * tests/philox_ref.py restates this stream in numpy.  The output does not depend on GPU count or launch geometry.
+ * cum_bq:
  * f64[2][max_bp][n_bq]; phred_p: f64[100] (pass the reference's own 10 ** (-arange(100) / 10)).  enable = 0 turns
  * it off. */
 int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int32_t max_bp, int32_t n_bq,

@@ -4,6 +4,7 @@ There is no CPU fallback: if the library is missing or no HIP device is present,
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -17,7 +18,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
-           'mh_release_haplotype', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
+           'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
@@ -55,6 +56,11 @@ def lib():
   if not os.path.exists(LIB_PATH):
     raise NativeUnavailable('libmitty_hip.so not built ({}); run __graft_entry__.build() or make -C '
                             'mitty_amd/csrc'.format(LIB_PATH))
+  if 'torch' not in sys.modules and int(os.environ.get('WORLD_SIZE', '1')) > 1:
+    # a torch.distributed run: torch's HIP runtime must be the process's only one, so torch loads first (our
+    # libamdhip64.so.7 dependency then binds to torch's copy; loaded the other way round, torch would bring a second
+    # runtime, and whichever initialises second sees no GPU)
+    import torch  # noqa: F401
   L = ctypes.CDLL(LIB_PATH)
   _sig(L, 'mh_version', [])
   _sig(L, 'mh_device_count', [ctypes.POINTER(c_i32)])
@@ -72,6 +78,7 @@ def lib():
                                  P_i64, P_i64, P_i64])
   _sig(L, 'mh_get_nodes', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_release_haplotype', [c_vp, c_i32])
+  _sig(L, 'mh_expand_variant', [c_i64, c_i64, c_i64, c_i64, c_i32, c_i64, P_i64, ctypes.POINTER(c_i32), P_i64, P_i64])
   _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_set_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32])
@@ -704,3 +711,15 @@ class Context:
 
   def sync(self):
     self._chk(self._L.mh_sync(self._h))
+
+
+def expand_variant(samp_pos, ref_pos, ref_start_pos, v_pos, op, oplen):
+  """mh_expand_variant: ([(ps, pr, op, oplen, src)], samp_next, ref_next) for one variant at the given cursors."""
+  out = (c_i64 * 10)()
+  n, sn, rn = c_i32(), c_i64(), c_i64()
+  rc = lib().mh_expand_variant(int(samp_pos), int(ref_pos), int(ref_start_pos), int(v_pos), ord(op), int(oplen), out,
+                               ctypes.byref(n), ctypes.byref(sn), ctypes.byref(rn))
+  if rc:
+    _raise(rc, 'mh_expand_variant: bad variant (op {!r}, oplen {})'.format(op, oplen))
+  return [(out[5 * j], out[5 * j + 1], chr(out[5 * j + 2]), out[5 * j + 3], out[5 * j + 4])
+          for j in range(n.value)], sn.value, rn.value

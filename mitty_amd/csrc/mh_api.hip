@@ -105,8 +105,12 @@ bool gate_debug() {
   return d;
 }
 
+static std::mutex g_gate_mu;   // gate_written is read-modify-written by both splice lanes (ensure -> gate_open)
+
 void gate_open(mh_ctx *ctx) {
-  if (!ctx->gate || ctx->gate_waited <= ctx->gate_written) return;
+  if (!ctx->gate) return;
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  if (ctx->gate_waited <= ctx->gate_written) return;
   if (gate_debug()) fprintf(stderr, "mh gate: open %u\n", ctx->gate_waited);
   (void)hipStreamWriteValue32(ctx->gstream, ctx->gate, ctx->gate_waited, 0);
   ctx->gate_written = ctx->gate_waited;
@@ -117,7 +121,9 @@ void gate_open_for(mh_ctx *ctx, uint32_t need) {
 }
 
 int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
-  if (!ctx->gate || value <= ctx->gate_written) return MH_OK;
+  if (!ctx->gate) return MH_OK;
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  if (value <= ctx->gate_written) return MH_OK;
   if (gate_debug()) fprintf(stderr, "mh gate: release %u\n", value);
   HIPCHK(ctx, hipStreamWriteValue32(st, ctx->gate, value, 0));
   ctx->gate_written = value;
@@ -513,12 +519,21 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
       const Contig &c1 = ctx->contigs[contig_ids[i0 + 1]];
       const VarSet &v1 = ctx->vsets[vsets[i0 + 1]];
       int32_t rc1 = MH_OK;
-      std::thread t1([&]() {
-        if (hipSetDevice(ctx->device) != hipSuccess) {
-          rc1 = MH_E_HIP;
-          return;
+      std::thread t1([&]() {   // nothing may escape the lane's thread (std::terminate): errors become codes
+        try {
+          const hipError_t e = hipSetDevice(ctx->device);
+          if (e != hipSuccess) {
+            rc1 = hip_fail(ctx, e, "hipSetDevice (splice lane 1)", __FILE__, __LINE__);
+            return;
+          }
+          rc1 = splice_build(ctx, *hp[1], c1, ref_starts[i0 + 1], v1, 1);
+        } catch (const std::bad_alloc &) {
+          rc1 = arg_fail(ctx, MH_E_OOM, "host memory (splice lane 1)");
+        } catch (const std::exception &x) {
+          rc1 = arg_fail(ctx, MH_E_STATE, std::string("splice lane 1: ") + x.what());
+        } catch (...) {
+          rc1 = arg_fail(ctx, MH_E_STATE, "splice lane 1: unknown exception");
         }
-        rc1 = splice_build(ctx, *hp[1], c1, ref_starts[i0 + 1], v1, 1);
       });
       const int32_t rc0 = splice_build(ctx, *hp[0], ctx->contigs[contig_ids[i0]], ref_starts[i0],
                                        ctx->vsets[vsets[i0]]);
@@ -694,6 +709,23 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
     if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ts.pos1.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_expand_variant(int64_t samp_pos, int64_t ref_pos, int64_t ref_start_pos, int64_t v_pos, int32_t op,
+                          int64_t oplen, int64_t *out, int32_t *n_nodes, int64_t *samp_next, int64_t *ref_next) {
+  if (!out || !n_nodes || !samp_next || !ref_next || (op != 'X' && op != 'I' && op != 'D') || oplen < 0)
+    return MH_E_ARG;
+  VarNode v[2];
+  const int n = expand_variant((uint8_t)op, v_pos, oplen, ref_pos, samp_pos, ref_start_pos, v, samp_next, ref_next);
+  for (int j = 0; j < n; j++) {
+    out[5 * j] = v[j].ps;
+    out[5 * j + 1] = v[j].pr;
+    out[5 * j + 2] = v[j].op;
+    out[5 * j + 3] = v[j].oplen;
+    out[5 * j + 4] = v[j].src;
+  }
+  *n_nodes = n;
   return MH_OK;
 }
 

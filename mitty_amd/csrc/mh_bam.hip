@@ -311,7 +311,8 @@ __device__ __forceinline__ uint8_t comp_atcgn(uint8_t c) {   // str.maketrans('A
 template <int G>
 __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tpl, int64_t n_rec, int32_t nr,
                                                    const uint32_t *slot, const int64_t *off, uint8_t *out,
-                                                   uint64_t *key, uint32_t *val, RInfo *info, int64_t rec_base) {
+                                                   uint64_t *key, uint32_t *val, RInfo *info, int64_t rec_base,
+                                                   int64_t out_cap, int32_t *bad) {
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1), gb = lane & ~(G - 1);   // lane within the record's group, the group's first lane
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
@@ -322,6 +323,12 @@ __global__ void __launch_bounds__(256) k_bam_write(ParseArgs a, const BamTpl *tp
   const BamTpl &T = tpl[t];
   const BamRead &r = T.r[s];
   const BamRead &m = T.r[nr == 2 ? 1 - s : s];
+  // bounds: the record's place (a sorted slot from the sort's values) and its bytes inside the store; a violation is
+  // reported (mh_bam_*: MH_E_STATE), never written
+  if (w < 0 || w >= n_rec || off[w] < 0 || off[w] + r.size > out_cap) {
+    if (gl == 0) atomicOr(bad, 1);
+    return;
+  }
   uint8_t *__restrict__ d = out + off[w];
   const uint8_t *__restrict__ qn = a.b[0] + T.qn_off;
   const int32_t lq = T.qn_len + 1;
@@ -467,13 +474,23 @@ struct LoadSortedSize {
 // 32 lanes per record, two records per wave (as k_bam_write: each record is a short chain of dependent loads)
 __global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const int64_t *roff, const uint32_t *val,
                                                     const int64_t *soff, int64_t n, uint8_t *dst, const RInfo *info,
-                                                    RInfo *sinfo) {
+                                                    RInfo *sinfo, int64_t src_bytes, int64_t dst_cap, int32_t *bad) {
   constexpr int G = 32;
   const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
   const int gl = threadIdx.x & (G - 1);
   if (k >= n) return;   // (a whole group)
   const uint32_t r = val[k];
+  // bounds: r must be a record of the store (the sort's values are a permutation of [0, n)), its bytes inside the
+  // input-order store and its sorted place inside the output; a violation is reported, never followed
+  if (r >= (uint64_t)n) {
+    if (gl == 0) atomicOr(bad, 2);
+    return;
+  }
   const int64_t a = roff[r], len = roff[r + 1] - a;
+  if (a < 0 || len < 0 || a + len > src_bytes || soff[k] < 0 || soff[k] + len > dst_cap) {
+    if (gl == 0) atomicOr(bad, 4);
+    return;
+  }
   const uint8_t *__restrict__ s = src + a;
   uint8_t *__restrict__ d = dst + soff[k];
   for (int64_t j0 = 0; j0 < len; j0 += 8 * G) {   // eight loads in flight per lane, then the stores
@@ -493,6 +510,18 @@ __global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const in
 }
 
 }  // namespace
+
+// the record kernels' bounds flag (1: k_bam_write place / bytes, 2: a sort value outside [0, n), 4: k_bam_gather bytes)
+static int32_t bam_check_bounds(mh_ctx *ctx, const int32_t *bad, const char *who) {
+  int64_t *hs = pinned_small(ctx);
+  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  HIPCHK(ctx, hipMemcpyAsync(hs + 26, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const int32_t f = (int32_t)(hs[26] & 0xffffffff);
+  if (f) return arg_fail(ctx, MH_E_STATE, std::string("BAM store: ") + who + " index or bytes out of bounds (flag " +
+                                            std::to_string(f) + ", internal)");
+  return MH_OK;
+}
 
 int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths) {
   BamStore &B = ctx->bam;
@@ -569,7 +598,8 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   MH_TRY(ensure(ctx, B.tpl, sizeof(BamTpl) * T));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   int32_t *err = (int32_t *)((char *)ctx->d_small.p + 64);
-  HIPCHK(ctx, hipMemsetAsync(err, 0, 4, st));
+  int32_t *bad = err + 1;   // the record kernels' bounds flag
+  HIPCHK(ctx, hipMemsetAsync(err, 0, 8, st));
   ParseArgs a{{d1, d2}, {(const int64_t *)B.nl1.p, d2 ? (const int64_t *)B.nl2.p : nullptr}, nf,
               (const char *)B.names.p, (const int32_t *)B.name_off.p, (int32_t)B.ref_names.size(), len1};
   stage_begin(ctx, "bam_parse");
@@ -633,10 +663,10 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
                      (const BamTpl *)B.tpl.p, n_rec, nf, (const uint32_t *)nullptr, (const int64_t *)roff,
                      (uint8_t *)B.recs.p,
                      (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
-                     B.n_rec);
+                     B.n_rec, B.bytes + add_bytes, bad);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  MH_TRY(bam_check_bounds(ctx, bad, "k_bam_write"));
   B.n_rec += n_rec;
   B.bytes += add_bytes;
   B.sorted = false;
@@ -680,13 +710,25 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
                                    (int64_t *)ctx->scan_partials.p, (int64_t *)ctx->d_small.p));
   MH_TRY(ensure(ctx, B.srecs, B.bytes + 64));
   MH_TRY(ensure(ctx, B.sinfo, sizeof(RInfo) * n));
+  int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 68);
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  {   // the offsets must close on the store's byte count (a record-size mismatch would send the copies astray)
+    int64_t *hs = pinned_small(ctx);
+    if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+    HIPCHK(ctx, hipMemcpyAsync(hs + 24, (const int64_t *)B.soff.p + n, 8, hipMemcpyDeviceToHost, st));
+    if (!pa) HIPCHK(ctx, hipMemcpyAsync(hs + 25, (const int64_t *)B.roff.p + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (hs[24] != B.bytes || (!pa && hs[25] != B.bytes))
+      return arg_fail(ctx, MH_E_STATE, "BAM store: record offsets do not add up to the store's size (internal)");
+  }
   if (pa) {
     stage_begin(ctx, "bam_write");
     hipLaunchKernelGGL(k_bam_slots, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint32_t *)B.val2.p, n,
                        (uint32_t *)B.val.p);   // (the sort's input values are no longer needed)
     hipLaunchKernelGGL(k_bam_write<BW_G>, dim3(grid_for(n * BW_G, 256, INT32_MAX)), dim3(256), 0, st,
-                       *(const ParseArgs *)pa, (const BamTpl *)B.tpl.p, n, B.n_files, (const uint32_t *)B.val.p, (const int64_t *)B.soff.p,
-                       (uint8_t *)B.srecs.p, (uint64_t *)nullptr, (uint32_t *)nullptr, (RInfo *)B.sinfo.p, (int64_t)0);
+                       *(const ParseArgs *)pa, (const BamTpl *)B.tpl.p, n, B.n_files, (const uint32_t *)B.val.p,
+                       (const int64_t *)B.soff.p, (uint8_t *)B.srecs.p, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                       (RInfo *)B.sinfo.p, (int64_t)0, B.bytes, bad);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   } else {
@@ -694,11 +736,11 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
     hipLaunchKernelGGL(k_bam_gather, dim3(grid_for(n * 32, 256, INT32_MAX)), dim3(256), 0, st,
                        (const uint8_t *)B.recs.p, (const int64_t *)B.roff.p, (const uint32_t *)B.val2.p,
                        (const int64_t *)B.soff.p, n, (uint8_t *)B.srecs.p, (const RInfo *)B.info.p,
-                       (RInfo *)B.sinfo.p);
+                       (RInfo *)B.sinfo.p, B.bytes, B.bytes, bad);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
   }
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  MH_TRY(bam_check_bounds(ctx, bad, pa ? "k_bam_write (sorted places)" : "k_bam_gather"));
   B.sorted = true;
   return MH_OK;
 }

@@ -1704,8 +1704,13 @@ int32_t output_reset(mh_ctx *ctx) {
   return MH_OK;
 }
 
-int32_t emit_result(mh_ctx *ctx, int32_t t, int64_t *out) {
-  if (t < 0 || t >= mh_ctx::RES_N || ctx->res_state[t] == 0) return arg_fail(ctx, MH_E_ARG, "unknown emission ticket");
+// a ticket = result slot | the slot's generation << 8: a slot handed out again (a ticket nobody read, 256 emissions
+// later) invalidates the old ticket instead of answering it with another unit's results
+int32_t emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out) {
+  const int32_t t = ticket & (mh_ctx::RES_N - 1);
+  if (ticket < 0 || ctx->res_state[t] == 0) return arg_fail(ctx, MH_E_ARG, "unknown emission ticket");
+  if ((uint32_t)ticket >> 8 != ctx->res_gen[t])
+    return arg_fail(ctx, MH_E_STATE, "stale emission ticket (its result slot was reused by a later emission)");
   gate_open(ctx);
   if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
   const int64_t *r = ctx->h_res + 8 * t;
@@ -1734,6 +1739,9 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   gate_open(ctx);
   if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
   ctx->res_next = (t + 1) % mh_ctx::RES_N;
+  ctx->res_state[t] = 0;
+  ctx->res_gen[t] = (ctx->res_gen[t] + 1) & 0x7fffff;
+  const int32_t tk = (int32_t)(ctx->res_gen[t] << 8) | t;
   int64_t *res = ctx->h_res + 8 * t;
   const int64_t m = tp.n, rlen = tp.rlen;
   std::string prefix = std::string("@") + serial_stub + ":";
@@ -1763,7 +1771,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
     res[6] = b1;
     res[7] = b2;
     ctx->res_state[t] = 2;
-    *ticket = t;
+    *ticket = tk;
     return MH_OK;
   }
   std::string pm = prefix + mid;
@@ -1864,7 +1872,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
   es.busy = true;
   ctx->writer_pending = true;
-  *ticket = t;
+  *ticket = tk;
   return MH_OK;
 }
 

@@ -47,6 +47,15 @@ struct Node16 {
   __host__ __device__ int64_t key() const { return ps() + (code() == 3); }   // 'D': ps + 1 (rpc.py:41-45)
 };
 
+// One node produced by a variant (expand_variant, mh_splice.hip): src = offset into the region's reference bytes
+// ('='), into the variant's alt bytes ('X' / 'I'), or -1 ('D').
+struct VarNode {
+  int64_t ps, pr, oplen, src;
+  uint8_t op;
+};
+__host__ __device__ int expand_variant(uint8_t o, int64_t vp, int64_t oplen, int64_t rb, int64_t sp, int64_t rs,
+                                       VarNode out[2], int64_t *sp_next, int64_t *rp_next);
+
 constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
 
 struct Hap {
@@ -240,6 +249,7 @@ struct mh_ctx {
   static constexpr int RES_N = 256;      // result slots (tickets) in flight
   int64_t *h_res = nullptr;              // pinned [RES_N][8]: E3 totals, bases (words 6, 7)
   hipEvent_t res_ev[RES_N] = {};
+  uint32_t res_gen[RES_N] = {};          // generation of each slot (the ticket's high bits)
   int8_t res_state[RES_N] = {};          // 0 free, 1 queued (event), 2 filled by the host (synchronous fallback)
   int32_t res_next = 0;
   int64_t *h_small = nullptr;            // pinned 4 KiB for small readbacks (no staged copy per value)

@@ -88,6 +88,41 @@ struct LoadNS {
   }
 };
 
+}  // namespace
+
+// The nodes one variant adds from the two cursors (rb = ref_pos, sp = samp_pos; rs = ref_start_pos): rpc.py:66-116's
+// snp / insertion / deletion (op selects the rule).  An optional '=' node up to the variant (through its first base
+// for 'I' / 'D'), then the variant's node.  src: the '=' node's offset into the region's reference bytes, the
+// 'X' / 'I' node's offset into the variant's alt bytes, -1 for 'D'.  Shared by the device splice (StoreNodes) and
+// the host entry mh_expand_variant (the plugin API's per-variant helpers).
+__host__ __device__ int expand_variant(uint8_t o, int64_t vp, int64_t oplen, int64_t rb, int64_t sp, int64_t rs,
+                                       VarNode out[2], int64_t *sp_next, int64_t *rp_next) {
+  int n = 0;
+  const int64_t delta = (o == 'X') ? vp - rb : vp + 1 - rb;
+  int64_t pr_x = rb;
+  if (delta > 0) {
+    out[n++] = VarNode{sp, rb, delta, rb - rs, (uint8_t)'='};
+    sp += delta;
+    pr_x = vp;
+  }
+  if (o == 'X') {
+    out[n++] = VarNode{sp, pr_x, 1, 0, (uint8_t)'X'};
+    *rp_next = pr_x + 1;
+    *sp_next = sp + 1;
+  } else if (o == 'I') {
+    out[n++] = VarNode{sp, vp + 1, oplen, 1, (uint8_t)'I'};
+    *rp_next = vp + 1;
+    *sp_next = sp + oplen;
+  } else {
+    out[n++] = VarNode{sp - 1, vp + 1 + oplen, oplen, -1, (uint8_t)'D'};
+    *rp_next = vp + 1 + oplen;
+    *sp_next = sp;
+  }
+  return n;
+}
+
+namespace {
+
 struct StoreNodes {
   const int64_t *pos; const uint8_t *op; const int64_t *oplen; const uint8_t *accepted; const int64_t *ref_before;
   const int64_t *alt_off; const int64_t *alt_len;
@@ -95,24 +130,23 @@ struct StoreNodes {
   int64_t rs, ref_len; int32_t *err;
   __device__ void operator()(int64_t i, NS, NS excl) const {
     if (!accepted[i]) return;
-    uint8_t o = op[i];
-    int64_t vp = pos[i], rb = ref_before[i];
-    int64_t sp = rs + excl.samp, k = excl.nodes;
-    int64_t delta = (o == 'X') ? vp - rb : vp + 1 - rb;
-    if (delta > 0) {                                  // '=' node (rpc.py:78-81, 93-96, 108-111)
-      keys[k] = sp; ps[k] = sp; pr[k] = rb; nop[k] = '='; nl[k] = delta; src[k] = rb - rs;
-      if (rb - rs + delta > ref_len) atomicOr(err, 1);
-      k++;
-      sp += delta;
-    }
-    if (o == 'X') {                                   // rpc.py:84
-      keys[k] = sp; ps[k] = sp; pr[k] = vp; nop[k] = 'X'; nl[k] = 1; src[k] = ALT_FLAG | alt_off[i];
-      if (alt_len[i] != 1) atomicOr(err, 2);
-    } else if (o == 'I') {                            // rpc.py:98-100
-      keys[k] = sp; ps[k] = sp; pr[k] = vp + 1; nop[k] = 'I'; nl[k] = oplen[i]; src[k] = ALT_FLAG | (alt_off[i] + 1);
-      if (alt_len[i] - 1 != oplen[i]) atomicOr(err, 2);
-    } else {                                          // rpc.py:113-115
-      keys[k] = sp; ps[k] = sp - 1; pr[k] = vp + 1 + oplen[i]; nop[k] = 'D'; nl[k] = oplen[i]; src[k] = -1;
+    const uint8_t o = op[i];
+    VarNode v[2];
+    int64_t sn, rn;
+    const int nn = expand_variant(o, pos[i], oplen[i], ref_before[i], rs + excl.samp, rs, v, &sn, &rn);
+    for (int j = 0; j < nn; j++) {
+      const int64_t k = excl.nodes + j;
+      keys[k] = v[j].op == 'D' ? v[j].ps + 1 : v[j].ps;   // the search key (rpc.py:127)
+      ps[k] = v[j].ps; pr[k] = v[j].pr; nop[k] = v[j].op; nl[k] = v[j].oplen;
+      if (v[j].op == '=') {
+        src[k] = v[j].src;
+        if (v[j].src + v[j].oplen > ref_len) atomicOr(err, 1);
+      } else if (v[j].op == 'D') {
+        src[k] = -1;
+      } else {
+        src[k] = ALT_FLAG | (alt_off[i] + v[j].src);
+        if (alt_len[i] - v[j].src != (v[j].op == 'X' ? 1 : oplen[i])) atomicOr(err, 2);
+      }
     }
   }
 };

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mitty_hip.h"
@@ -43,6 +44,7 @@ struct mh_vcf {
   std::string chrom_head;  // the #CHROM line's first 9 columns (keep_lines)
   std::string sample;
   std::vector<std::string> order;   // contigs in file order
+  std::unordered_set<std::string> header_contigs;   // ##contig=<ID=...> names
   std::unordered_map<std::string, std::vector<Rec>> by_chrom;
   std::string text;   // REF / ALT / GT fields of every record
   // last region query
@@ -120,6 +122,12 @@ static int32_t vcf_load(const char *path, const char *sample, mh_vcf *v) {
     if (n && s[n - 1] == '\r') n--;
     if (n >= 2 && s[0] == '#' && s[1] == '#') {
       if (v->keep_lines) v->meta.append(s, n).push_back('\n');
+      static const char kc[] = "##contig=<ID=";
+      if (n > sizeof(kc) - 1 && memcmp(s, kc, sizeof(kc) - 1) == 0) {
+        size_t e = sizeof(kc) - 1;
+        while (e < n && s[e] != ',' && s[e] != '>') e++;
+        v->header_contigs.emplace(s + sizeof(kc) - 1, e - (sizeof(kc) - 1));
+      }
       return MH_OK;
     }
     if (n >= 6 && memcmp(s, "#CHROM", 6) == 0) {
@@ -293,6 +301,10 @@ int32_t mh_vcf_filter(const char *in_path, const char *sample, int32_t n_regions
   std::vector<int> g;
   const char *cp = chroms;
   for (int32_t k = 0; k < n_regions; k++) {
+    if (!v.by_chrom.count(cp) && !v.header_contigs.count(cp)) {   // pysam's fetch: ValueError('invalid contig')
+      set_err("invalid contig `" + std::string(cp) + "`");
+      return MH_E_ARG;
+    }
     region_records(&v, cp, start0[k], end[k], recs);
     for (const mh_vcf::Rec *r : recs) {
       const char *ref = v.text.data() + r->ref_off;

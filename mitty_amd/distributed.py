@@ -15,6 +15,9 @@ illumina.py:56-58), so the path shards without any data-path collective:
 
 The collectives carry a few int64 per piece; no sequence data crosses xGMI.  Outputs must be regular files
 (ranks write at offsets); FIFOs / process substitution need the single-GPU path.
+
+A process holds one HIP runtime: torch must load before libmitty_hip.so (mitty_amd._native does that itself when
+WORLD_SIZE > 1), otherwise torch brings its own runtime and whichever of the two initialises second sees no GPU.
 """
 import logging
 import os

@@ -10,7 +10,8 @@ GPU in large chunks and every base is corrupted in parallel with the same model 
                RandomState(RandomState(seed).randint(SEED_MAX)) consumed template by template — byte-identical to
                the reference's `--threads 1` output (with more workers the reference's own output depends on which
                worker dequeues which template, so `processes` only selects this one deterministic realisation)
-  rng='philox' counter-based: each base's words counted by (template, file, base), no sequential chain at all
+  rng='philox' counter-based: one Philox4x32-10 draw per three bases, counted by (template, file, triple)
+               (include/mitty_hip.h, mh_set_corruption), no sequential chain at all
 """
 import logging
 import time

@@ -3,8 +3,8 @@
 `create_node_list` splices on the GPU (mh_build_haplotype) and returns a NodeList — a list of Node exactly as the
 reference builds it — that remembers its device slot, so `get_begin_end_nodes` and `generate_read` run on the
 device (mh_read_batch) against the same haplotype.  The reference's per-variant helpers `create_nodes` / `snp` /
-`insertion` / `deletion` (rpc.py:66-116) are the inner steps of its create_node_list; the device splice replaces the
-whole walk, so they are not exported.
+`insertion` / `deletion` (rpc.py:66-116) are exposed over mh_expand_variant: the node rules the device splice applies
+to each accepted variant (one function, compiled for the kernel and the host), given the caller's cursors.
 """
 import itertools
 
@@ -75,6 +75,36 @@ def create_node_list(ref_seq, ref_start_pos, vl):
     seq = '' if o == 'D' else hap[ps[k] - p_min: ps[k] - p_min + ol[k]]
     nodes.append(Node(int(ps[k]), int(pr[k]), o, int(ol[k]), seq))
   return NodeList(nodes, ctx, slot, slot)
+
+
+def _expand(op, ref_seq, samp_pos, ref_pos, v, ref_start_pos):
+  from mitty_amd import _native
+  raw, samp_next, ref_next = _native.expand_variant(samp_pos, ref_pos, ref_start_pos, v.pos, op, v.oplen)
+  nodes = []
+  for ps, pr, o, ol, src in raw:
+    seq = ref_seq[src:src + ol] if o == '=' else ('' if o == 'D' else v.alt[src:])
+    nodes.append(Node(ps, pr, o, ol, seq))
+  return nodes, samp_next, ref_next
+
+
+def snp(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
+  """rpc.snp (rpc.py:75-87): ([optional '=' node, 'X' node], samp_pos, ref_pos) after the variant."""
+  return _expand('X', ref_seq, samp_pos, ref_pos, v, ref_start_pos)
+
+
+def insertion(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
+  """rpc.insertion (rpc.py:90-101)."""
+  return _expand('I', ref_seq, samp_pos, ref_pos, v, ref_start_pos)
+
+
+def deletion(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
+  """rpc.deletion (rpc.py:104-116)."""
+  return _expand('D', ref_seq, samp_pos, ref_pos, v, ref_start_pos)
+
+
+def create_nodes(ref_seq, samp_pos, ref_pos, v, ref_start_pos):
+  """rpc.create_nodes (rpc.py:66-72): the helper v.cigarop selects ('X', 'I', anything else 'D')."""
+  return _expand(v.cigarop if v.cigarop in ('X', 'I') else 'D', ref_seq, samp_pos, ref_pos, v, ref_start_pos)
 
 
 def _device_nodes(nodes):

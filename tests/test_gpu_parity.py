@@ -923,15 +923,11 @@ def _gpu_rank(rank, world, port, layout, outdir):
     dist.destroy_process_group()
 
 
-def test_template_broadcast_packing_round_trip(native):
-  """The sliced multi-GPU layout's broadcast unit (DeviceBackend.share): a sampled unit's templates packed into one
-  device buffer (pos0 | pos1 | fo0 at 0 / 8n / 16n, the RCCL payload) and into a host buffer (the gloo payload),
-  imported into another template set, emit the same FASTQ bytes as the sampled set; share() itself under a one-rank
-  gloo group."""
-  import socket
+def _packing_worker(_rank, port):
+  """(a fresh process: torch's HIP runtime first, as in every torch.distributed rank)"""
   import torch
   import torch.distributed as dist
-  from mitty_amd import distributed as D, synth
+  from mitty_amd import _native as native, distributed as D, synth
   from mitty_amd.readmodel import get_read_model
   _, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
   p, _ = native.read_model_params(150, 30.0)
@@ -958,9 +954,6 @@ def test_template_broadcast_packing_round_trip(native):
     assert np.array_equal(host, buf.cpu().numpy())
     be.unpack_host(1, n, 150, host)
     assert emitted(1) == want
-    with socket.socket() as s:
-      s.bind(('127.0.0.1', 0))
-      port = s.getsockname()[1]
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port), rank=0, world_size=1)
     try:
       be.share(0, n, 0, 150)
@@ -969,6 +962,19 @@ def test_template_broadcast_packing_round_trip(native):
     assert emitted(0) == want
   finally:
     be.close()
+
+
+def test_template_broadcast_packing_round_trip(native):
+  """The sliced multi-GPU layout's broadcast unit (DeviceBackend.share): a sampled unit's templates packed into one
+  device buffer (pos0 | pos1 | fo0 at 0 / 8n / 16n, the RCCL payload) and into a host buffer (the gloo payload),
+  imported into another template set, emit the same FASTQ bytes as the sampled set; share() itself under a one-rank
+  gloo group.  Runs in a spawned process (torch and libmitty_hip in one process need torch loaded first)."""
+  import socket
+  import torch.multiprocessing as mp
+  with socket.socket() as s:
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+  mp.start_processes(_packing_worker, args=(port,), nprocs=1, join=True, start_method='spawn')
 
 
 @pytest.mark.parametrize('layout', ['lpt', 'slice'])

@@ -333,6 +333,16 @@ def test_filter_variants_errors(tmp_path):
     vcfio.prepare_variant_file(str(bad), 'S1', str(bed), str(tmp_path / 'o.vcf'))
   with pytest.raises(ValueError, match='sample'):
     vcfio.prepare_variant_file(str(bad), 'NOPE', str(bed), str(tmp_path / 'o.vcf'))
+  # a BED contig the VCF knows neither from ##contig nor from records: pysam's fetch raises ValueError('invalid
+  # contig'); a declared contig without records is an empty region
+  ok = tmp_path / 'ok.vcf'
+  ok.write_text('##fileformat=VCFv4.1\n##contig=<ID=2,length=100>\n'
+                '#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1\n1\t5\t.\tA\tC\t50\tPASS\t.\tGT\t0|1\n')
+  (tmp_path / 'c3.bed').write_text('1\t0\t100\n3\t0\t100\n')
+  with pytest.raises(ValueError, match='invalid contig `3`'):
+    vcfio.prepare_variant_file(str(ok), 'S1', str(tmp_path / 'c3.bed'), str(tmp_path / 'o.vcf'))
+  (tmp_path / 'c2.bed').write_text('1\t0\t100\n2\t0\t100\n')
+  assert vcfio.prepare_variant_file(str(ok), 'S1', str(tmp_path / 'c2.bed'), str(tmp_path / 'o.vcf'))[0] == 1
 
 
 def test_native_fasta_reader(tmp_path):
@@ -416,3 +426,61 @@ def test_philox_restatement_known_answers():
   m = 0xffffffff
   assert [int(x[0]) for x in P.philox4x32_10([m], [m], [m], [m], m, m)] == \
       [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+
+
+# ---- rpc's per-variant helpers over mh_expand_variant (reference test_rpc.py:24-108, restated) ----------------------
+def _tiny_rpc():
+  from mitty_amd.lib import vcfio
+  ref_seq = open(G.path('data/tiny.fasta')).readlines()[1]
+  vcf = vcfio.load_variant_file(G.path('data/tiny.vcf'), 'g0_s0', G.path('data/tiny.whole.bed'))
+  return ref_seq, vcf
+
+
+def test_rpc_variant_helpers_reference_cases():
+  """The six expansion cases of the reference's test_rpc.py (:24-108): SNP / INS / DEL with and without an '=' node,
+  node tuples and the cursors after the variant."""
+  from mitty_amd.simulation import rpc
+  ref_seq, vcf = _tiny_rpc()
+  snp_v, ins_v, del_v = vcf[0]['v'][1][0], vcf[0]['v'][1][1], vcf[0]['v'][1][2]
+  nodes, sp, rp = rpc.snp(ref_seq, 1, 5, snp_v, 1)                       # test_snp_expansion2
+  assert [n.tuple() for n in nodes] == [(1, 5, 'X', 1, 'T', 0)] and (sp, rp) == (2, 6)
+  nodes, sp, rp = rpc.snp(ref_seq, 1, 1, snp_v, 1)                       # test_snp_expansion3
+  assert [n.tuple() for n in nodes] == [(1, 1, '=', 4, 'ATGA', None), (5, 5, 'X', 1, 'T', 0)]
+  nodes, sp, rp = rpc.insertion(ref_seq, 9, 9, ins_v, 1)                 # test_ins_expansion2
+  assert [n.tuple() for n in nodes] == [(9, 9, 'I', 3, 'TTT', 3)] and (sp, rp) == (12, 9)
+  nodes, sp, rp = rpc.insertion(ref_seq, 6, 6, ins_v, 1)                 # test_ins_expansion3
+  assert [n.tuple() for n in nodes] == [(6, 6, '=', 3, 'GTA', None), (9, 9, 'I', 3, 'TTT', 3)]
+  nodes, sp, rp = rpc.deletion(ref_seq, 12, 12, del_v, 1)                # test_del_expansion2
+  assert [n.tuple() for n in nodes] == [(11, 14, 'D', 2, '', -2)] and (sp, rp) == (12, 14)
+  nodes, sp, rp = rpc.deletion(ref_seq, 12, 9, del_v, 1)                 # test_del_expansion3
+  assert [n.tuple() for n in nodes] == [(12, 9, '=', 3, 'TCC', None), (14, 14, 'D', 2, '', -2)]
+  assert rpc.create_nodes(ref_seq, 12, 9, del_v, 1)[0] == nodes
+
+
+def test_rpc_variant_helpers_chain_equals_node_list_oracle():
+  """Walking the helpers the way create_node_list does (skip pos < ref cursor, trailing '=' node) gives the oracle's
+  node lists for both tiny copies and the SURVEY App. B edge cases."""
+  from mitty_amd.simulation import rpc
+  from oracle import oracle as O
+  ref_seq, vcf = _tiny_rpc()
+  cases = [(ref_seq, 1, vcf[0]['v'][c]) for c in range(2)]
+  V = O.Variant
+  cases.append(('ACGTACGTAC' * 3, 1, [V(27, 'CGTACG', 'C', 'D', 5)]))                                     # B1
+  cases.append(('ACGTACGTAC' * 3, 1, [V(5, 'A', 'A' + 'T' * 20, 'I', 20)]))                               # B2
+  cases.append(('ACGTACGTAC' * 3, 1, [V(5, 'ACGT', 'A', 'D', 3), V(6, 'C', 'T', 'X', 0), V(9, 'A', 'T', 'X', 0),
+                                      V(9, 'A', 'AGG', 'I', 2)]))                                        # B3
+  cases.append(('ACGTACGTAC' * 3, 1, [V(1, 'A', 'T', 'X', 0)]))                                           # B5
+  cases.append(('ACGTACGTAC' * 3, 1, [V(1, 'A', 'AT', 'I', 1)]))
+  for seq, rs, vl in cases:
+    samp_pos = ref_pos = rs
+    got = []
+    for v in vl:
+      if v.pos < ref_pos:
+        continue
+      nn, samp_pos, ref_pos = rpc.create_nodes(seq, samp_pos, ref_pos, v, rs)
+      got += [n.tuple() for n in nn]
+    off = ref_pos - rs
+    if off <= len(seq):
+      got.append((samp_pos, ref_pos, '=', len(seq) - off, seq[off:], None))
+    want = [tuple(n) for n in O.create_node_list(seq.encode(), rs, vl)]
+    assert got == want, (vl, got, want)
