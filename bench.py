@@ -56,6 +56,8 @@ def parse():
                   help='bounded CPU-oracle sample: the job\'s units on the first N Mbp of the contig (0 = skip)')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end (files in, /dev/null out) leg')
+  ap.add_argument('--e2e-gz', action=argparse.BooleanOptionalAction, default=True,
+                  help='end-to-end leg: also with BGZF-compressed output (host deflate, level 1)')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
   ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
   ap.add_argument('--async-emit', action='store_true',
@@ -75,6 +77,12 @@ def parse():
                   help='wgs: units are sampled in batches of about this many template draws (a chr1 job is 30 M); '
                        'the FASTQ arenas are recycled per batch')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
+  ap.add_argument('--pipeline', default='batch', choices=['batch', 'phased', 'phased-sync'],
+                  help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
+                       'writers of batch k); phased = sample every unit of the step, then emit every unit '
+                       '(phased-sync: and the step starts after the previous step\'s writers)')
+  ap.add_argument('--emit-chunk-bytes', type=float, default=24e9,
+                  help='wgs phased: FASTQ arenas recycled after about this many bytes')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
                   help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
                        '--threads 2)')
@@ -377,10 +385,20 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
                                              seed=a.seed)
     t3 = time.perf_counter()
-    return {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
-            'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
-            'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
-                    'page-locked memory, written to /dev/null; seconds = the whole command'}
+    out = {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
+           'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
+           'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
+                   'page-locked memory, written to /dev/null; seconds = the whole command'}
+    if a.e2e_gz:   # the same with both files BGZF-compressed on the host (what `.gz` output names cost)
+      threads = min(16, os.cpu_count() or 1)
+      t4 = time.perf_counter()
+      st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
+                                               seed=a.seed, compress=True, gz_level=1, gz_threads=threads)
+      t5 = time.perf_counter()
+      out['gz'] = {'seconds': t5 - t4, 'value': st['kept'] / (t5 - t4), 'unit': 'templates/s', 'level': 1,
+                   'gz_bytes': st['written1'] + st['written2'],
+                   'threads': threads, 'note': 'the same command with BGZF output (host deflate pool)'}
+    return out
   finally:
     for f in glob.glob(os.path.join(d, '*')):
       os.remove(f)
@@ -448,7 +466,40 @@ def run_genome(a, rank, world, local):
     dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
 
+  tpl_flip = [0]
+  soa_of = lambda r, c: copies[r][c]
+
+  def step_phased():
+    if a.pipeline == 'phased-sync':
+      eng.ctx.sync()   # the previous step's writers drain before this step's sampling starts
+    eng.drop_haplotypes()
+    base = tpl_flip[0] = (1 << 20) - tpl_flip[0]   # template ids alternate per step (a step's writers may still run)
+    ids, k = [], 0
+    for batch in batches:   # every unit sampled first ...
+      eng.sample_only(batch, soa_of, p, rlen, model['cum_tlen'], base + k, a.rng)
+      ids.append(list(range(base + k, base + k + len(batch))))
+      k += len(batch)
+    kept = b1 = b2 = 0
+    units_all = [u for b in batches for u in b]
+    ids_all = [i for x in ids for i in x]
+    est = 0
+    c0 = 0
+    eng.ctx.reset_output()
+    for j, u in enumerate(units_all):   # ... then emitted in order, the arenas recycled every --emit-chunk-bytes
+      est += int(contigs[u[1]][1] * p * 740)   # ~L p templates of ~740 FASTQ bytes
+      if est >= a.emit_chunk_bytes or j == len(units_all) - 1:
+        for kp, x1, x2 in eng.emit_only(units_all[c0:j + 1], ids_all[c0:j + 1], soa_of, 'SYN', 0, True):
+          kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
+        eng.ctx.reset_output()
+        c0, est = j + 1, 0
+    if dist is not None:
+      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
+      dist.all_reduce(counts)
+    return lambda: (kept, b1, b2)
+
   def step():
+    if a.pipeline != 'batch':
+      return step_phased()
     eng.drop_haplotypes()
     kept = b1 = b2 = 0
     for batch in batches:
@@ -511,7 +562,8 @@ def run_genome(a, rank, world, local):
                            'genome)'.format('' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
                                             a.model, rlen, a.coverage, a.rng, world),
                'genome_bp': sum(L for _, L in contigs), 'read_model': a.model, 'coverage': a.coverage,
-               'units': n_units, 'batches_rank0': len(batches), 'templates_per_step': kept_all // steps,
+               'units': n_units, 'batches_rank0': len(batches), 'pipeline': a.pipeline,
+               'templates_per_step': kept_all // steps,
                'parallelism': 'unit-shard (LPT) x{}'.format(world) if world > 1 else 'single GPU',
                'world_size_seen': seen, 'collective_backend': backend},
     'roofline': roof,

@@ -10,6 +10,7 @@
 
 #include "mh_corrupt.h"
 #include "mh_internal.h"
+#include "mh_scan.h"
 
 namespace mh {
 namespace jump {
@@ -42,6 +43,7 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
     gate_open(ctx);
     HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // a queued FASTQ writer may still read or write it
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    lb_forget(b.p);
     HIPCHK(ctx, hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
@@ -65,12 +67,14 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
   HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  lb_forget(b.p);
   if (b.p) HIPCHK(ctx, hipFree(b.p));
   b = nb;
   return MH_OK;
 }
 
 void release(DevBuf &b) {
+  lb_forget(b.p);
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.cap = 0;
@@ -317,6 +321,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
     if (kv.second.used) (void)hipEventDestroy(kv.second.used);
   }
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
+  for (auto &b : ctx->pb) release(b);
+  release(ctx->pb_tmp);
   for (auto &b : ctx->s) release(b);
   for (auto &b : ctx->lane2) release(b);
   for (auto &l : ctx->xlane)

@@ -28,6 +28,7 @@
 #include <cstring>
 
 #include "mh_corrupt.h"
+#include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -660,7 +661,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
   // straight out as byte stores).
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
     const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
-    if (j >= nt || q >= 4) continue;
+    if (j >= nt || q >= 4 || (dbg & 2)) continue;
     const DMeta &M = meta[j];
     const int32_t L = M.len[f];
     if (L == 0) continue;
@@ -712,7 +713,11 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
-  if (staged) __syncthreads();
+  // (LDS hand-off only: the ragged-edge byte stores above need not land before the chunk sweep; dbg 64: the full
+  // barrier, for A/B)
+  if (staged) {
+    if (dbg & 64) __syncthreads(); else lds_barrier();
+  }
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
     const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
@@ -729,9 +734,14 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
-      const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
-                                 : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : tb + (x0 - tl)));
-      const uint4 v = (dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
+      uint4 v;
+      if (b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
+        v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);   // inside T's '~' run: no LDS read
+      } else {
+        const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
+                                   : (x0 + 16 <= sb ? qb + x0 : (x0 + 16 <= tl ? bb + (x0 - sb) : tb + (x0 - tl)));
+        v = (dbg & 4) ? make_uint4(src, x0, 0, b) : lds_load16(smem, (uint32_t)src);
+      }
       *(uint4 *)(out + (cg << 4)) = v;
     }
   }
@@ -774,6 +784,9 @@ struct TArgs {
   int64_t cnt_base;         // templates kept before the emission's first one (cnt numbering)
   uint2 *crec;              // corruption: per record the first base's arena offset and S (k_cr_inplace's words)
   int32_t rlen, win_stride, head, qstride;
+  int32_t dbg;              // experiments (MH_EW_DBG): 1 skip the output sweeps, 2 skip the seam sweep, 8 skip the
+                            // qname formatting, 16 skip the gathers, 32 return at once — timing only, the bytes are
+                            // then wrong; 64 full barriers (s_waitcnt vmcnt(0)) instead of LDS-only ones (A/B)
 };
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
@@ -796,7 +809,7 @@ struct TArgs {
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
 template <int NF, int LPR, bool CR>
-__global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
+__device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
   __shared__ int32_t s_span[2];   // the tile's bytes per file
@@ -813,13 +826,12 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
-  const int64_t tile = blockIdx.x;
   const int64_t t0 = tile * ED_T;
   const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
   const int chunks = win_stride / 16;
   for (int i = tid; i < TL; i += ED_THREADS)
     smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
-  if (tid >= 64) {
+  if (tid >= 64 && !(A.dbg & 16)) {
     // waves 1-3: the gathers (three threads per mate window), all in flight together; an unused chunk re-reads the
     // first one
     const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
@@ -847,7 +859,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
 #pragma unroll
     for (int k = 0; k < ED_GMAX; k++)
       *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (q3 + 3 * k) : o_dump)) = wv[k];
-  } else {
+  } else if (tid < 64) {
     // wave 0: lane = read (template jf, mate s)
     const int jf = tid >> 1, s = tid & 1;
     const bool valid = jf < nt;
@@ -869,7 +881,7 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
-    if (keep) {
+    if (keep && !(A.dbg & 8)) {
       ReadInfo ri;
       ri.n0 = n0;
       ri.n1 = n1;
@@ -960,10 +972,19 @@ __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
       }
     }
   }
-  __syncthreads();
+  if (A.dbg & 64) __syncthreads(); else lds_barrier();   // LDS hand-off (each LDS write waited for its load data)
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
-  ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, true, A.arena, 0);
+  if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, true, A.arena, A.dbg);
+}
+
+// One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
+// waves per SIMD instead of eight — and the launch of 184 k workgroups costs only ~0.35 ms of a 2.6 ms chr1-unit
+// writer (MH_EW_DBG=32), so there is no persistent variant.)
+template <int NF, int LPR, bool CR>
+__global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
+  if (A.dbg & 32) return;   // (experiments: the launch alone)
+  emit_tile<NF, LPR, CR>(A, qh, blockIdx.x);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -1519,9 +1540,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
+    static const int ew_dbg = getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0;
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
-            qstride};
+            qstride, ew_dbg};
     auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
                                : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);

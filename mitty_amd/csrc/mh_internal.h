@@ -198,6 +198,8 @@ struct mh_ctx {
   std::map<int32_t, mh::VarSet> vsets;   // resident variant sets (mh_upload_variants); id -1: mh_build_haplotype's
   std::vector<mh::Hap> hap_spare;   // released haplotypes' buffers, reused by the next build (no hipMalloc/hipFree)
   mh::DevBuf perm_tmp;  // radix sort scratch (permutation, N runs)
+  mh::DevBuf pb[6];     // batch-wide permutation: ts, shuffled ts, global keys, sorted keys, sorted steps, heads
+  mh::DevBuf pb_tmp;    // its radix sort scratch
   mh::DevBuf nrun_tmp;  // unsorted N-run boundaries
   mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
   int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)

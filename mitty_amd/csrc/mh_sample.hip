@@ -769,6 +769,33 @@ __global__ void __launch_bounds__(256) k_perm_chase(int64_t n, const uint32_t *K
   out[p] = ts[q];
 }
 
+// The batch-wide permutation: every unit of a batch in one sort.  Unit u's step k sits at global index
+// j_off(u) + k and targets j_off(u) + j_k, so the units' buckets stay apart and one sort, one heads pass and one
+// chase serve them all (per-unit sorts of a whole-genome job were ~100 small sorts, each a handful of launches).
+// Padding entries between units target themselves (an empty chain).  Also sets every head to -1 (k_perm_heads
+// then writes the buckets that have one).
+constexpr int PK_UNITS = 512;   // units per batch staged in LDS
+__global__ void __launch_bounds__(256) k_perm_keys(int64_t total, const uint32_t *jall, const int64_t *u_off,
+                                                   const int64_t *u_n, int32_t n_units, uint32_t *keys,
+                                                   int32_t *nxt) {
+  __shared__ int64_t s_off[PK_UNITS], s_n[PK_UNITS];
+  for (int i = threadIdx.x; i < n_units; i += 256) {
+    s_off[i] = u_off[i];
+    s_n[i] = u_n[i];
+  }
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  int lo = 0, hi = n_units - 1;   // the last unit whose offset is <= g
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_off[mid] <= g) lo = mid; else hi = mid - 1;
+  }
+  const int64_t k = g - s_off[lo];
+  keys[g] = k < s_n[lo] ? (uint32_t)(s_off[lo] + jall[g]) : (uint32_t)g;
+  nxt[g] = -1;
+}
+
 // ---- geometric + cumsum ------------------------------------------------------------------------------------
 __device__ __forceinline__ double mt_double(const uint32_t *w, int64_t k) {
   int32_t a = (int32_t)(w[2 * k] >> 5), b = (int32_t)(w[2 * k + 1] >> 6);
@@ -1192,9 +1219,16 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // lane's last unit writes the gate), 2 = wait for ev_sorted then write the gate, 3 = write the gate.
 // phase: 0 = everything; 1 = the geometric scan and the sort (up to the gate); 2 = the rest.  `ub` (phases 1/2): the
 // unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
+// bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
+// from bp_tsh + j_off; the unit's own sort and chase are skipped
+struct BatchPerm {
+  int64_t *ts, *tsh;
+};
+
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
                     const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
-                    uint32_t *d_flag, int lane = 0, int gate_role = 0, int phase = 0, mh::DevBuf *ub = nullptr) {
+                    uint32_t *d_flag, int lane = 0, int gate_role = 0, int phase = 0, mh::DevBuf *ub = nullptr,
+                    const BatchPerm *bp = nullptr) {
   hipStream_t st = lane == 0 ? ctx->stream : lane == 1 ? ctx->stream2 : ctx->xstream[lane - 2];
   ctx->stage_stream = lane ? st : nullptr;
   struct Restore {
@@ -1206,10 +1240,11 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   void *scan_partials = lane == 0 ? ctx->scan_partials.p : lane == 1 ? ctx->scan_partials2.p : ctx->xscan[lane - 2].p;
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
-  int64_t *ts = (int64_t *)(ub ? ub[0] : S4[0]).p, *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
+  int64_t *ts = bp ? bp->ts + u.j_off : (int64_t *)(ub ? ub[0] : S4[0]).p;
+  int64_t *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
   uint32_t *sk = (uint32_t *)(ub ? ub[1] : S4[4]).p, *sv = (uint32_t *)(ub ? ub[2] : S4[5]).p;
   int32_t *nxt = (int32_t *)(ub ? ub[3] : S4[6]).p;
-  const bool permute = rng_mode == MH_RNG_MITTY && n > 1;
+  const bool permute = rng_mode == MH_RNG_MITTY && n > 1 && !bp;
   uint8_t *keep = (uint8_t *)S4[3].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
   int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128 + 64 * lane);
@@ -1266,7 +1301,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   }
   if (phase == 1) return MH_OK;
 
-  const int64_t *ts_use = ts;
+  const int64_t *ts_use = bp && rng_mode == MH_RNG_MITTY && n > 1 ? bp->tsh + u.j_off : ts;
   if (permute) {
     stage_begin(ctx, "sample_permutation");
     hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
@@ -1482,6 +1517,72 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       MH_TRY(ensure(ctx, ctx->usort[u][0], 8 * (size_t)nu));
       for (int b = 1; b < 4; b++) MH_TRY(ensure(ctx, ctx->usort[u][b], 4 * (size_t)nu + 16));
     }
+  // the batch-wide permutation (default; MH_PERM_UNIT=1 or the writer gate: one sort per unit)
+  static const bool perm_unit = getenv("MH_PERM_UNIT") && atoi(getenv("MH_PERM_UNIT"));
+  const bool batch = !ctx->gate && !perm_unit && rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) &&
+                     n_units <= PK_UNITS;
+  if (batch) {
+    MH_TRY(ensure(ctx, ctx->pb[0], 8 * (size_t)j_total + 64));
+    MH_TRY(ensure(ctx, ctx->pb[1], 8 * (size_t)j_total + 64));
+    for (int b = 2; b < 6; b++) MH_TRY(ensure(ctx, ctx->pb[b], 4 * (size_t)j_total + 64));
+    BatchPerm bp{(int64_t *)ctx->pb[0].p, (int64_t *)ctx->pb[1].p};
+    // 1. every unit's geometric cumsum into the batch ts (lanes)
+    for (int32_t u = 0, k = 0; u < n_units; u++) {
+      if (plan[u].n == 0) continue;
+      MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
+                         d_flags + u, k++ % n_lanes, 0, 1, nullptr, &bp));
+    }
+    if (two_lanes) {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+      HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
+      for (int l = 2; l < n_lanes; l++) {
+        HIPCHK(ctx, hipEventRecord(ctx->ev_xjoin[l - 2], ctx->xstream[l - 2]));
+        HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_xjoin[l - 2], 0));
+      }
+    }
+    // 2. one sort of every unit's (target, step), heads, chase (main stream)
+    stage_begin(ctx, "sample_permutation");
+    std::vector<int64_t> uo(n_units), un(n_units);
+    for (int32_t u = 0; u < n_units; u++) {
+      uo[u] = plan[u].j_off;
+      un[u] = plan[u].n;
+    }
+    int64_t *d_uo = (int64_t *)ctx->s[12].p;
+    MH_TRY(ensure(ctx, ctx->s[12], 16 * (size_t)n_units + 64));
+    d_uo = (int64_t *)ctx->s[12].p;
+    HIPCHK(ctx, hipMemcpyAsync(d_uo, uo.data(), 8 * n_units, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(d_uo + n_units, un.data(), 8 * n_units, hipMemcpyHostToDevice, st));
+    uint32_t *gk = (uint32_t *)ctx->pb[2].p, *sk = (uint32_t *)ctx->pb[3].p, *sv = (uint32_t *)ctx->pb[4].p;
+    int32_t *nxt = (int32_t *)ctx->pb[5].p;
+    hipLaunchKernelGGL(k_perm_keys, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
+                       (const uint32_t *)jall, (const int64_t *)d_uo, (const int64_t *)(d_uo + n_units), n_units, gk,
+                       nxt);
+    HIPCHK(ctx, hipGetLastError());
+    unsigned end_bit = 1;
+    while (end_bit < 32 && ((int64_t)1 << end_bit) < j_total) end_bit++;
+    size_t tmp = 0;
+    const rocprim::counting_iterator<uint32_t> iota(0u);
+    HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, gk, sk, iota, sv, (size_t)j_total, 0u, end_bit, st));
+    MH_TRY(ensure(ctx, ctx->pb_tmp, tmp + 256));
+    HIPCHK(ctx, rocprim::radix_sort_pairs(ctx->pb_tmp.p, tmp, gk, sk, iota, sv, (size_t)j_total, 0u, end_bit, st));
+    hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
+                       (const uint32_t *)sk, (const uint32_t *)sv, nxt);
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
+                       (const uint32_t *)sk, (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)bp.ts, bp.tsh);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    // 3. every unit's template lengths, compaction and file order (lanes)
+    if (two_lanes) {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+      for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
+    }
+    for (int32_t u = 0, k = 0; u < n_units; u++) {
+      if (plan[u].n == 0) continue;
+      MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
+                         d_flags + u, k++ % n_lanes, 0, 2, nullptr, &bp));
+    }
+  } else
   for (int ph = split ? 1 : 0; ph <= (split ? 2 : 0); ph++)
     for (int32_t u = 0, k = 0; u < n_units; u++) {
       if (plan[u].n == 0) continue;

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
+#include <unordered_map>
 
 namespace mh {
 
@@ -117,10 +119,33 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(int64_t n, Load load
   }
 }
 
+// Host state of every look-back scratch buffer: the bytes zeroed, the ticket counter's value after the launches
+// queued so far, the last epoch.  A buffer is used by one stream at a time (launches on it are stream-ordered).
+struct LbScratchState {
+  size_t zeroed = 0;
+  uint32_t ticket = 0;
+  uint32_t epoch = 0;
+};
+inline std::mutex &lb_mu() {
+  static std::mutex m;
+  return m;
+}
+inline std::unordered_map<const void *, LbScratchState> &lb_states() {
+  static std::unordered_map<const void *, LbScratchState> m;
+  return m;
+}
+// a device buffer about to be freed (or reallocated): whatever lands at its address later starts unzeroed
+inline void lb_forget(const void *p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(lb_mu());
+  lb_states().erase(p);
+}
+
 // Host launcher.  `partials` must hold ceil(n / SCAN_TILE) elements, `total` one element (device memory).
 template <typename T, typename Op, typename Load, typename Store>
 inline hipError_t device_scan(hipStream_t st, int64_t n, Load load, Store store, Op op, T identity, T *partials,
                               T *total) {
+  lb_forget(partials);   // (a buffer shared with look-back scans: their next use starts from zeroed scratch)
   int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL((k_scan_reduce<T, Op, Load>), dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, n, load, op,
@@ -135,6 +160,7 @@ inline hipError_t device_scan(hipStream_t st, int64_t n, Load load, Store store,
 // Reduction only (phases 1-2): grand total to *total.
 template <typename T, typename Op, typename Load>
 inline hipError_t device_reduce(hipStream_t st, int64_t n, Load load, Op op, T identity, T *partials, T *total) {
+  lb_forget(partials);
   int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL((k_scan_reduce<T, Op, Load>), dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, n, load, op,
@@ -147,9 +173,12 @@ inline hipError_t device_reduce(hipStream_t st, int64_t n, Load load, Op op, T i
 // ---- single-pass scan (decoupled look-back) for sums of non-negative int64 fields ------------------------------
 // One kernel reads every element once: tiles are taken in launch order from an atomic ticket (so every tile a tile
 // waits for is already running), each publishes its aggregate, then its inclusive prefix once the look-back over
-// its predecessors (one wave, 64 tiles per step) finds an inclusive one.  Status words pack the value with a
-// 2-bit flag (1 = aggregate, 2 = inclusive) and travel as 64-bit agent-scope atomics, so no fences are needed.
-// T must be a struct of int64 fields, each summed, each in [0, 2^61).
+// its predecessors (one wave, 64 tiles per step) finds an inclusive one.  Status words pack the value with a 16-bit
+// launch epoch and a 2-bit flag (1 = aggregate, 2 = inclusive) and travel as 64-bit agent-scope atomics, so no
+// fences are needed; the epoch makes the previous launches' words stale, so the scratch is zeroed only when it is
+// new (not before every launch: a memset per scan was ~6 us of GPU time each, hundreds per whole-genome step), and
+// the ticket counter runs on from launch to launch (each launch subtracts its base).
+// T must be a struct of int64 fields, each summed, each in [0, 2^46).
 constexpr int LB_ITEMS = 8;
 constexpr int LB_TILE = SCAN_THREADS * LB_ITEMS;
 
@@ -187,17 +216,26 @@ __device__ __forceinline__ T shfl_idx_t(const T &v, int src) {
   return b.t;
 }
 
-__device__ __forceinline__ void lb_put(uint64_t *w, int64_t v, uint64_t flag) {
-  __hip_atomic_store(w, ((uint64_t)v << 2) | flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+constexpr int LB_EPOCH_BITS = 16;
+constexpr int LB_VAL_SHIFT = 2 + LB_EPOCH_BITS;
+
+__device__ __forceinline__ void lb_put(uint64_t *w, int64_t v, uint64_t flag, uint32_t epoch) {
+  __hip_atomic_store(w, ((uint64_t)v << LB_VAL_SHIFT) | ((uint64_t)epoch << 2) | flag, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// the word's flag if it belongs to this launch (epoch), else 0
+__device__ __forceinline__ uint32_t lb_flag(uint64_t w, uint32_t epoch) {
+  return (uint32_t)((w >> 2) & ((1u << LB_EPOCH_BITS) - 1)) == epoch ? (uint32_t)(w & 3u) : 0u;
 }
 __device__ __forceinline__ uint64_t lb_get(const uint64_t *w) {
   return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// scratch: [ticket (64 B)] [aggregate words K x nt] [inclusive words K x nt], zeroed before the launch
+// scratch: [ticket (64 B)] [aggregate words K x nt] [inclusive words K x nt], zeroed when new; ticket_base: the
+// ticket counter's value when this launch starts; epoch: this launch's tag (1 .. 2^16 - 1)
 template <typename T, typename Load, typename Store>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, Store store, uint64_t *scratch,
-                                                         int64_t nt, T *total) {
+                                                         int64_t nt, T *total, uint32_t ticket_base, uint32_t epoch) {
   using F = LbFields<T>;
   constexpr int K = F::K;
   __shared__ T lds_w[SCAN_THREADS / 64];
@@ -206,7 +244,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
   uint32_t *ticket = (uint32_t *)scratch;
   uint64_t *agg = scratch + 8, *inc = agg + (size_t)K * nt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+  if (tid == 0) s_tile = (int64_t)(uint32_t)(atomicAdd(ticket, 1u) - ticket_base);
   __syncthreads();
   const int64_t tile = s_tile;
   // wave w owns elements [tile * LB_TILE + w * 64 * LB_ITEMS, +64 * LB_ITEMS): item k of lane l is element
@@ -238,13 +276,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
   if (wave == 0) {
     T prefix{};
     if (tile == 0) {
-      if (lane < K) lb_put(inc + (size_t)lane * nt, F::get(tot, lane), 2u);
+      if (lane < K) lb_put(inc + (size_t)lane * nt, F::get(tot, lane), 2u, epoch);
     } else {
-      if (lane < K) lb_put(agg + (size_t)lane * nt + tile, F::get(tot, lane), 1u);
+      if (lane < K) lb_put(agg + (size_t)lane * nt + tile, F::get(tot, lane), 1u, epoch);
       for (int64_t j = tile - 1;; j -= 64) {
         const int64_t jj = j - lane;   // lane l looks at tile j - l (jj < 0: past tile 0, never needed)
         bool is_inc = jj < 0, ok = jj < 0;
         T val{};
+        uint32_t spins = 0;   // a bound on the wait: a broken ticket or scratch gives wrong sums, never a hung GPU
         while (!ok) {
           bool all_inc = true, all_agg = true;
           int64_t xi[K], xa[K];
@@ -252,16 +291,18 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
           for (int k = 0; k < K; k++) {
             const uint64_t wi = lb_get(inc + (size_t)k * nt + jj);
             const uint64_t wa = lb_get(agg + (size_t)k * nt + jj);
-            all_inc &= (wi & 3u) == 2u;
-            all_agg &= (wa & 3u) == 1u;
-            xi[k] = (int64_t)(wi >> 2);
-            xa[k] = (int64_t)(wa >> 2);
+            all_inc &= lb_flag(wi, epoch) == 2u;
+            all_agg &= lb_flag(wa, epoch) == 1u;
+            xi[k] = (int64_t)(wi >> LB_VAL_SHIFT);
+            xa[k] = (int64_t)(wa >> LB_VAL_SHIFT);
           }
           if (all_inc || all_agg) {
             ok = true;
             is_inc = all_inc;
 #pragma unroll
             for (int k = 0; k < K; k++) F::set(val, k, all_inc ? xi[k] : xa[k]);
+          } else if (++spins > (1u << 24)) {
+            ok = is_inc = true;
           } else {
             __builtin_amdgcn_s_sleep(1);
           }
@@ -275,7 +316,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
         if (first < 64) break;
       }
       const T mine = prefix + tot;
-      if (lane < K) lb_put(inc + (size_t)lane * nt + tile, F::get(mine, lane), 2u);
+      if (lane < K) lb_put(inc + (size_t)lane * nt + tile, F::get(mine, lane), 2u, epoch);
     }
     if (lane == 0) s_prefix = prefix;
   }
@@ -307,10 +348,24 @@ template <typename T, typename Load, typename Store>
 inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store store, void *scratch, T *total) {
   int64_t nt = (n + LB_TILE - 1) / LB_TILE;
   if (nt < 1) nt = 1;
-  hipError_t e = hipMemsetAsync(scratch, 0, scan_lb_scratch_bytes<T>(n), st);
-  if (e != hipSuccess) return e;
+  const size_t need = scan_lb_scratch_bytes<T>(n);
+  uint32_t base, epoch;
+  {
+    std::lock_guard<std::mutex> lk(lb_mu());
+    LbScratchState &S = lb_states()[scratch];
+    if (S.zeroed < need || S.epoch >= (1u << LB_EPOCH_BITS) - 1) {   // new (or grown) scratch, or epochs used up
+      hipError_t e = hipMemsetAsync(scratch, 0, need, st);
+      if (e != hipSuccess) return e;
+      S.zeroed = need;
+      S.ticket = 0;
+      S.epoch = 0;
+    }
+    base = S.ticket;
+    epoch = ++S.epoch;
+    S.ticket += (uint32_t)nt;
+  }
   hipLaunchKernelGGL((k_scan_lb<T, Load, Store>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, st, n, load, store,
-                     (uint64_t *)scratch, nt, total);
+                     (uint64_t *)scratch, nt, total, base, epoch);
   return hipGetLastError();
 }
 

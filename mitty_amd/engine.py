@@ -122,6 +122,35 @@ class Engine:
           on_unit(ps, int(ns[k]), kept, b1, b2)
     return out
 
+  def sample_only(self, units, soa_of, p, rlen, cum_tlen, tpl_base, rng='mitty'):
+    """The sampling half of run_units: units [(ps, ri, cpy, rng_seed)] sampled together into template sets
+    tpl_base + k.  Returns the template counts (emit_only emits them later)."""
+    if not os.environ.get('MH_SPLICE_ONE_LANE'):
+      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
+    slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    return [int(x) for x in self.ctx.sample_units([tpl_base + k for k in range(len(units))], slots,
+                                                  [u[3] for u in units], p, rlen, cum_tlen, RNG_MODES[rng])]
+
+  def emit_only(self, units, tpl_ids, soa_of, sample_name, worker_id=0, write_fastq2=True):
+    """The emission half: units [(ps, ri, cpy, rng_seed)] whose templates are in sets tpl_ids, measured and written
+    in order (measure passes of up to EMIT_SETS units, then their writers queued back to back).  Returns
+    [(kept, b1, b2)] per unit."""
+    slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    out = []
+    for c0 in range(0, len(units), self.EMIT_SETS):
+      chunk = list(range(c0, min(c0 + self.EMIT_SETS, len(units))))
+      for k in chunk:
+        ps, ri, cpy, seed = units[k]
+        self.ctx.use_templates(tpl_ids[k])
+        self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
+                              write_fastq2, unit_key=seed, wait=False)
+      for k in chunk:
+        ps, ri, cpy, seed = units[k]
+        self.ctx.use_templates(tpl_ids[k])
+        out.append(self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
+                                       self._regions[ri][0], cpy, write_fastq2, unit_key=seed))
+    return out
+
   def run_unit(self, ps, ri, cpy, rng_seed, soa, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
                rng='mitty'):
     """One work unit: sample templates, emit FASTQ.  Returns (n_templates, kept, bytes1, bytes2)."""

@@ -149,13 +149,15 @@ class FastqSink:
     self.fp = open(fname, 'wb')
     self.gz = fname.endswith('.gz') if compress is None else compress
     self.level, self.threads = level, threads
-    self.raw = 0
+    self.raw = 0       # bytes handed in
+    self.written = 0   # bytes written (compressed when gz)
 
   def write(self, data):
     self.raw += len(data)
     if self.gz:
       from mitty_amd import _native
       data = _native.bgzf_compress(data, self.level, self.threads)
+    self.written += len(data)
     mv = memoryview(data)
     while len(mv):
       n = self.fp.write(mv)

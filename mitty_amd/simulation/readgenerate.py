@@ -68,10 +68,12 @@ def get_data_for_workers(model, vcf, seed):
 
 def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                            fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
-                           flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000):
+                           flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000, compress=None,
+                           gz_level=6, gz_threads=8):
   """Generate reads for every (region, copy, pass) unit and write FASTQ (reference readgenerate.py:76-126).
 
-  Returns a stats dict (templates sampled, kept, bytes, seconds).
+  compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it (level gz_level on
+  gz_threads host threads).  Returns a stats dict (templates sampled, kept, bytes, seconds).
   """
   t0 = time.time()
   read_model = read_module.read_model_params(model, coverage)
@@ -88,8 +90,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     eng.load_region(ri, reg['region'], mfasta.fetch(seqs, chrom, s0, e))
   stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0}
   write2 = fastq2_fname is not None
-  fp1 = FastqSink(fastq1_fname)   # '.gz' names get BGZF output
-  fp2 = FastqSink(fastq2_fname) if write2 else None
+  fp1 = FastqSink(fastq1_fname, gz_level, gz_threads, compress)   # '.gz' names get BGZF output
+  fp2 = FastqSink(fastq2_fname, gz_level, gz_threads, compress) if write2 else None
 
   pins = [_native.PinnedBuffer(), _native.PinnedBuffer()]   # page-locked D2H staging, one per file
 
@@ -127,6 +129,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     eng.close()
     for b in pins:
       b.free()
+  stats['written1'], stats['written2'] = fp1.written, fp2.written if fp2 else 0
   stats['seconds'] = time.time() - t0
   return stats
 
