@@ -257,6 +257,15 @@ int32_t mh_fasta_close(mh_fasta *f);
 int32_t mh_bgzf_compress(const char *in, int64_t len, int32_t level, int32_t threads, char *out, int64_t cap,
                          int64_t *used);
 int32_t mh_bgzf_eof(char *out28);
+/* The same BGZF framing deflated on the GPU (mh_deflate.hip: a workgroup per block, greedy LZ77 + dynamic Huffman
+ * per eighth of a block).  Output decompresses to the input (the bytes differ from zlib's).  No EOF marker.
+ *   mh_bgzf_compress_device  device buffer -> device buffer (cap bytes; MH_E_CAPACITY when short)
+ *   mh_bgzf_compress_gpu     host buffer -> host buffer through the context's staging
+ *   mh_output_bgzf           FASTQ arena `file` (0, 1) -> host buffer (out NULL: *used = the size only) */
+int32_t mh_bgzf_compress_device(mh_ctx *ctx, const void *d_in, int64_t len, void *d_out, int64_t cap,
+                                int64_t *used);
+int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out, int64_t cap, int64_t *used);
+int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used);
 
 /* ---- corrupt-reads over existing FASTQ (readcorrupt.multi_process, readcorrupt.py:18-118; cli.py:144-157) -----
  * The complete templates of the host buffers (file 2 optional) are corrupted with the model set by

@@ -23,7 +23,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof',
+           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
 
@@ -78,6 +78,9 @@ def lib():
                                  P_i64, P_i64, P_i64])
   _sig(L, 'mh_get_nodes', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_release_haplotype', [c_vp, c_i32])
+  _sig(L, 'mh_bgzf_compress_device', [c_vp, c_vp, c_i64, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_bgzf_compress_gpu', [c_vp, c_vp, c_i64, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_output_bgzf', [c_vp, c_i32, c_vp, c_i64, P_i64])
   _sig(L, 'mh_expand_variant', [c_i64, c_i64, c_i64, c_i64, c_i32, c_i64, P_i64, ctypes.POINTER(c_i32), P_i64, P_i64])
   _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
@@ -575,6 +578,29 @@ class Context:
 
   def reset_output(self):
     self._chk(self._L.mh_output_reset(self._h))
+
+  def bgzf_compress(self, data):
+    """BGZF members of `data` deflated on the GPU (no EOF marker; mh_bgzf_compress_gpu)."""
+    n = len(data)
+    if n == 0:
+      return b''
+    src = np.frombuffer(data, np.uint8)
+    out = np.empty(n + (n // 0xff00 + 2) * 40 + 64, np.uint8)
+    used = c_i64()
+    self._chk(self._L.mh_bgzf_compress_gpu(self._h, _ptr(src), n, _ptr(out), len(out), ctypes.byref(used)))
+    return out[:used.value].tobytes()
+
+  def output_bgzf_pinned(self, pins):
+    """Both arenas BGZF-compressed on the GPU into page-locked staging (pins: [PinnedBuffer, PinnedBuffer]);
+    returns memoryviews of the compressed bytes (no EOF marker)."""
+    out = []
+    for f, u in enumerate(self.output_size()):
+      cap = u + (u // 0xff00 + 2) * 40 + 64   # every block stored, at worst
+      pins[f].reserve(cap)
+      used = c_i64()
+      self._chk(self._L.mh_output_bgzf(self._h, f, c_vp(pins[f].ptr), cap, ctypes.byref(used)))
+      out.append(pins[f].view(used.value))
+    return out
 
   # ---- god-aligner BAM ----
   def bam_set_refs(self, names, lengths):

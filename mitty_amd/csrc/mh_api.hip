@@ -323,6 +323,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->pb) release(b);
   release(ctx->pb_tmp);
+  release(ctx->gz_slots); release(ctx->gz_info); release(ctx->gz_off); release(ctx->gz_scan); release(ctx->gz_out);
+  release(ctx->gz_in);
   for (auto &b : ctx->s) release(b);
   for (auto &b : ctx->lane2) release(b);
   for (auto &l : ctx->xlane)
@@ -1166,3 +1168,52 @@ int32_t mh_bam_reset(mh_ctx *ctx) {
 }
 
 }  // extern "C"
+
+// ---- device BGZF (mh_deflate.hip) ----
+int32_t mh_bgzf_compress_device(mh_ctx *ctx, const void *d_in, int64_t len, void *d_out, int64_t cap,
+                                int64_t *used) {
+  CTX_GUARD(ctx);
+  if ((!d_in && len > 0) || len < 0 || !d_out || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  return bgzf_device(ctx, ctx->stream, (const uint8_t *)d_in, len, (uint8_t *)d_out, cap, used);
+}
+
+int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out, int64_t cap, int64_t *used) {
+  CTX_GUARD(ctx);
+  if ((!in && len > 0) || len < 0 || !out || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  *used = 0;
+  if (len == 0) return MH_OK;
+  MH_TRY(ensure(ctx, ctx->gz_in, (size_t)len + 64));
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(len)));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->gz_in.p, in, len, hipMemcpyHostToDevice, ctx->stream));
+  int64_t u = 0;
+  MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)ctx->gz_in.p, len, (uint8_t *)ctx->gz_out.p,
+                     (int64_t)ctx->gz_out.cap, &u));
+  if (u > cap) {
+    *used = u;
+    return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
+  }
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  *used = u;
+  return MH_OK;
+}
+
+int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used) {
+  CTX_GUARD(ctx);
+  if ((file != 0 && file != 1) || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  MH_TRY(sync_async_fill(ctx));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the writers of the arena's last units
+  const int64_t n = file ? ctx->used2 : ctx->used1;
+  const uint8_t *src = (const uint8_t *)(file ? ctx->out2.p : ctx->out1.p);
+  *used = 0;
+  if (n == 0) return MH_OK;
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(n)));
+  int64_t u = 0;
+  MH_TRY(bgzf_device(ctx, ctx->stream, src, n, (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &u));
+  *used = u;
+  if (!out) return MH_OK;   // (the size only)
+  if (u > cap) return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}

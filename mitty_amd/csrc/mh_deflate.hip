@@ -1,0 +1,495 @@
+// mh_deflate.hip — BGZF compression of device buffers on the GPU (`.gz` FASTQ output;
+// reference readgenerate.py:233-253 writes through pysam / htslib, whose BGZF is zlib deflate in 0xff00-byte
+// blocks).  The host deflate pool (mh_bgzf.cpp) does ~1.5 GB/s on 16 cores; a chr1 job is 17.4 GB of FASTQ.
+//
+// One 512-thread workgroup per BGZF block (up to 0xff00 input bytes, staged in LDS).  Its eight waves each compress
+// one eighth of the block as a deflate block of their own (dynamic Huffman codes from that slice's symbols,
+// matches inside the slice): wave w < 7 ends its block with an empty stored block (a sync flush, 5 bytes) so the
+// next slice's bits start on a byte boundary, and the slices' bytes simply concatenate; wave 7's block is final.
+//   parse   greedy LZ77 over the slice, 64 positions per step: every lane looks up its position (a 2^11-entry hash of
+//           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1); the
+//           first lane with a four-byte match ends the step's literals, its match is extended by the whole wave
+//           (up to 258 bytes), then the positions passed are hashed in;
+//   pass 1  the parse, counting symbol frequencies;
+//   codes   lane 0: length-limited Huffman lengths (15 bits; 7 for the code-length code), canonical codes, the
+//           dynamic header (mh_deflate.h, host-testable);
+//   pass 2  the same parse again, each step's codes placed by a wave prefix sum of their bit lengths into an LDS
+//           staging strip, whole words flushed to the slice's region of the block's slot;
+//   CRC-32  every thread a 128-byte segment, combined over a tree (x^(8n) operators).
+// A block whose compressed size would not fit a BGZF block is stored instead.  k_bgzf_pack then writes the
+// blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets from a scan of their sizes.
+#include "mh_deflate.h"
+#include "mh_internal.h"
+#include "mh_scan.h"
+
+namespace mh {
+
+namespace {
+
+using namespace df;
+
+constexpr int DF_WAVES = 8;
+constexpr int DF_THREADS = 64 * DF_WAVES;
+constexpr int SLICE = (BLOCK + DF_WAVES - 1) / DF_WAVES;   // 8160 input bytes per wave
+constexpr int HBITS = 11;
+constexpr int REGION = 9216;                // a slice's output bytes in the slot (more: the block is stored)
+constexpr int SLOT = DF_WAVES * REGION;
+constexpr int STAGE = 112;                  // staging words: 64 codes of <= 48 bits, a carried word, slack
+
+struct CodeScratch {                        // while the codes are built (the hash table is idle then)
+  uint32_t keys[512], A[NLIT];
+  HeaderScratch H;
+};
+struct WaveLds {
+  union {
+    uint32_t ht[1 << HBITS];                // hash: position + 1 of the latest earlier position (atomicMax)
+    CodeScratch cs;
+  };
+  uint32_t lf[NLIT], dfq[NDIST];
+  uint8_t llen[NLIT], dlen[NDIST];
+  uint16_t lcode[NLIT], dcode[NDIST];
+  uint32_t stage[STAGE];
+  uint32_t hw[96];                          // the dynamic header's bits, as words
+};
+static_assert(sizeof(CodeScratch) <= sizeof(uint32_t) * (1 << HBITS), "code scratch inside the hash table");
+
+struct BlockLds {
+  uint8_t in[BLOCK + 64];                   // the block's input, zero-padded
+  uint32_t crc_tab[256];
+  uint32_t crc[DF_THREADS];
+  int32_t stored;
+  WaveLds w[DF_WAVES];
+};
+
+struct DfBlockInfo {
+  int32_t n;           // input bytes
+  int32_t stored;      // 1: stored block (the slices' regions unused)
+  uint32_t crc;
+  int32_t len[DF_WAVES];   // bytes of each slice's deflate data
+};
+
+__device__ __forceinline__ uint32_t load4(const uint8_t *b, int x) {   // bytes x .. x+3 of an LDS array
+  const uint32_t *q = (const uint32_t *)(b + (x & ~3));
+  return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(x & 3));
+}
+__device__ __forceinline__ uint32_t hash4(uint32_t w) { return (w * 2654435761u) >> (32 - HBITS); }
+
+// Wave-wide ascending sort of n <= 320 keys in LDS (bitonic over the next power of two, padded with ~0u).
+__device__ void wave_sort(uint32_t *k, int n, int lane) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = n + lane; i < P; i += 64) k[i] = 0xffffffffu;
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // (lgkmcnt(0)) the padding is in place
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < P / 2; i += 64) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint32_t a = k[lo], b = k[hi];
+        if ((a > b) == up) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Code lengths of one alphabet from the wave's frequencies (keys sorted by the whole wave, the rest on lane 0).
+__device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, uint16_t *code, uint32_t *keys,
+                             uint32_t *A, int lane) {
+  // keys of the used symbols, compacted in symbol order by a wave prefix count
+  int base = 0;
+  for (int s0 = 0; s0 < n; s0 += 64) {
+    const int s = s0 + lane;
+    const bool used = s < n && f[s] != 0;
+    const uint64_t bal = __ballot(used);
+    if (used) keys[base + __popcll(bal & ((1ull << lane) - 1))] = (f[s] << 9) | (uint32_t)s;
+    if (s < n) len[s] = 0;
+    base += __popcll(bal);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  wave_sort(keys, base, lane);
+  if (lane == 0) {
+    huffman_from_sorted(keys, base, limit, len, A);
+    canonical_codes(len, n, code);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One step of the parse at `cur` (wave-uniform): returns the next position; sets the number of literals `nlit`
+// (positions cur .. cur + nlit - 1) and, when has_match, the match (mlen, mdist) at cur + nlit.
+struct Step {
+  int next, nlit, mlen, mdist;
+  bool has_match;
+};
+
+__device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane) {
+  const int p = cur + lane;
+  int cand = -1;
+  if (p + MIN_MATCH <= S) {
+    const uint32_t w = load4(s, p);
+    if (p >= 1 && load4(s, p - 1) == w) {
+      cand = p - 1;                                  // a run: distance 1
+    } else {
+      const int j = (int)ht[hash4(w)] - 1;           // a position of an earlier step (< cur <= p)
+      if (j >= 0 && load4(s, j) == w) cand = j;
+    }
+  }
+  const uint64_t bal = __ballot(cand >= 0);
+  Step st;
+  const int lim = S - cur < 64 ? S - cur : 64;
+  if (bal == 0) {
+    st.nlit = lim;
+    st.has_match = false;
+    st.mlen = st.mdist = 0;
+    st.next = cur + lim;
+    return st;
+  }
+  const int f = __builtin_ctzll(bal);
+  const int q = cur + f;
+  const int j = __shfl(cand, f, 64);
+  const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
+  int len = MIN_MATCH;
+  for (;;) {   // the whole wave extends the match, 64 bytes per round
+    const int k = len + lane;
+    const bool eq = k < cap && s[q + k] == s[j + k];
+    const uint64_t ne = ~__ballot(eq);
+    const int run = ne ? __builtin_ctzll(ne) : 64;
+    len += run;
+    if (run < 64 || len >= cap) break;
+  }
+  if (len > cap) len = cap;
+  st.nlit = f;
+  st.has_match = true;
+  st.mlen = len;
+  st.mdist = q - j;
+  st.next = q + len;
+  return st;
+}
+
+// positions a .. b-1 into the hash table; lanes colliding on one entry keep the latest position (atomicMax), so
+// both passes see the same table
+__device__ __forceinline__ void hash_in(const uint8_t *s, int S, int a, int b, uint32_t *ht, int lane) {
+  for (int k = a + lane; k < b; k += 64)
+    if (k + MIN_MATCH <= S) atomicMax(&ht[hash4(load4(s, k))], (uint32_t)(k + 1));
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// the symbols of one step, pass 1: literal frequencies (a ballot loop over the distinct bytes) and the match's
+__device__ __forceinline__ void count_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, int lane) {
+  const bool lit = lane < st.nlit;
+  const uint32_t c = lit ? s[cur + lane] : 0u;
+  uint64_t todo = __ballot(lit);
+  while (todo) {
+    const int l0 = __builtin_ctzll(todo);
+    const uint32_t c0 = __shfl(c, l0, 64);
+    const uint64_t same = __ballot(lit && c == c0);
+    if (lane == l0) W.lf[c0] += (uint32_t)__popcll(same);
+    todo &= ~same;
+  }
+  if (st.has_match && lane == 0) {
+    W.lf[257 + len_code(st.mlen)]++;
+    W.dfq[dist_code(st.mdist)]++;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The wave's bit writer over its region (words): the staging strip holds the words from `wbase` on; stage[0] is
+// partial (the bits below bitpos % 32).
+struct BitWave {
+  uint32_t *region;    // the slice's output region (global)
+  int64_t bitpos;      // bits written
+  bool overflow;
+};
+
+// put each lane's (v, n) (n <= 57 bits: v < 2^n) in lane order after bitpos
+__device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t v, int n, int lane) {
+  int off = n;   // inclusive prefix of the bit lengths across the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(off, d, 64);
+    if (lane >= d) off += o;
+  }
+  const int total = __shfl(off, 63, 64);
+  const int excl = off - n;
+  const int r = (int)(bw.bitpos & 31) + excl;   // bit offset inside the staging strip
+  if (n) {
+    const int wi = r >> 5, sh = r & 31;
+    atomicOr(&stage[wi], (uint32_t)(v << sh));
+    const uint64_t hi = sh ? v >> (32 - sh) : v >> 32;
+    if (hi) atomicOr(&stage[wi + 1], (uint32_t)hi);
+    const uint64_t hi2 = sh ? (v >> (64 - sh)) : 0;
+    if (sh && (sh + n) > 64 && hi2) atomicOr(&stage[wi + 2], (uint32_t)hi2);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int64_t end = bw.bitpos + total;
+  const int full = (int)((end >> 5) - (bw.bitpos >> 5));   // words completed by this step
+  const int64_t w0 = bw.bitpos >> 5;
+  if ((end >> 3) + 8 > REGION) bw.overflow = true;
+  if (!bw.overflow)
+    for (int k = lane; k < full; k += 64) bw.region[w0 + k] = stage[k];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t carry = stage[full];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  for (int k = lane; k < STAGE; k += 64) stage[k] = k == 0 ? carry : 0u;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  bw.bitpos = end;
+}
+
+// the codes of one step, pass 2
+__device__ __forceinline__ void encode_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, BitWave &bw,
+                                            int lane) {
+  uint64_t v = 0;
+  int n = 0;
+  if (lane < st.nlit) {
+    const uint32_t c = s[cur + lane];
+    v = W.lcode[c];
+    n = W.llen[c];
+  }
+  put_bits(bw, W.stage, v, n, lane);
+  if (st.has_match) {
+    v = 0;
+    n = 0;
+    if (lane == 0) {
+      const int lc = len_code(st.mlen), dc = dist_code(st.mdist);
+      const int le = len_extra(lc), de = dist_extra(dc);
+      v = W.lcode[257 + lc];
+      n = W.llen[257 + lc];
+      v |= (uint64_t)(st.mlen - len_base(lc)) << n;
+      n += le;
+      v |= (uint64_t)W.dcode[dc] << n;
+      n += W.dlen[dc];
+      v |= (uint64_t)(st.mdist - dist_base(dc)) << n;
+      n += de;
+    }
+    put_bits(bw, W.stage, v, n, lane);
+  }
+}
+
+__global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, int64_t n_in, int64_t b0, int64_t nb,
+                                                            uint8_t *slots, DfBlockInfo *info) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  BlockLds &L = *(BlockLds *)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = b0 + blockIdx.x;
+  if (blockIdx.x >= nb) return;
+  const int64_t start = b * BLOCK;
+  const int n = (int)(n_in - start < BLOCK ? n_in - start : BLOCK);
+  // stage the block (16-byte loads where aligned, bytes otherwise) and the CRC table
+  for (int i = tid; i < BLOCK + 64; i += DF_THREADS) L.in[i] = i < n ? in[start + i] : 0;
+  for (int i = tid; i < 256; i += DF_THREADS) {
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ CRC_POLY : c >> 1;
+    L.crc_tab[i] = c;
+  }
+  if (tid == 0) L.stored = 0;
+  __syncthreads();
+  // CRC-32 of the block: 128-byte segments, then a tree of combinations
+  {
+    const int a = tid * 128, e = a + 128 < n ? a + 128 : n;
+    uint32_t c = 0xffffffffu;
+    for (int i = a; i < e; i++) c = L.crc_tab[(c ^ L.in[i]) & 0xffu] ^ (c >> 8);
+    L.crc[tid] = a < e ? ~c : 0u;
+    __syncthreads();
+    for (int h = 1; h < DF_THREADS; h <<= 1) {   // segment pairs (tid, tid + h) at tid % 2h == 0
+      if ((tid & (2 * h - 1)) == 0 && tid + h < DF_THREADS) {
+        const int ra = (tid + h) * 128;
+        const int rl = ra >= n ? 0 : (n - ra < 128 * h ? n - ra : 128 * h);   // bytes of the right part
+        if (rl > 0) L.crc[tid] = crc_combine(L.crc[tid], L.crc[tid + h], (uint64_t)rl);
+      }
+      __syncthreads();
+    }
+  }
+  // the wave's slice
+  WaveLds &W = L.w[wave];
+  const int s0 = wave * SLICE;
+  const int S = s0 >= n ? 0 : (n - s0 < SLICE ? n - s0 : SLICE);
+  const uint8_t *s = L.in + s0;
+  const bool last = s0 + SLICE >= n;   // the final deflate block (later waves have empty slices)
+  uint32_t *region = (uint32_t *)(slots + (size_t)blockIdx.x * SLOT + (size_t)wave * REGION);
+  int32_t out_len = 0;
+  if (S > 0) {
+    // pass 1: frequencies
+    for (int i = lane; i < (1 << HBITS); i += 64) W.ht[i] = 0;
+    for (int i = lane; i < NLIT; i += 64) W.lf[i] = 0;
+    for (int i = lane; i < NDIST; i += 64) W.dfq[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (int cur = 0; cur < S;) {
+      const Step st = parse_step(s, S, cur, W.ht, lane);
+      count_step(s, cur, st, W, lane);
+      hash_in(s, S, cur, st.next, W.ht, lane);
+      cur = st.next;
+    }
+    if (lane == 0) W.lf[256] = 1;   // end of block (a slice without matches: HDIST 1, one unused distance code)
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    // codes
+    wave_huffman(W.lf, NLIT, 15, W.llen, W.lcode, W.cs.keys, W.cs.A, lane);
+    wave_huffman(W.dfq, NDIST, 15, W.dlen, W.dcode, W.cs.keys, W.cs.A, lane);
+    // the header bits into hw (lane 0)
+    int hbits = 0;
+    if (lane == 0) {
+      BitSink bs{(uint8_t *)W.hw, 0, 0, 0};
+      bs.put(last ? 1u : 0u, 1);
+      bs.put(2u, 2);
+      write_dynamic_header(bs, W.llen, W.dlen, W.cs.H);
+      hbits = (int)(bs.pos * 8 + bs.nacc);
+      if (bs.nacc) ((uint8_t *)W.hw)[bs.pos] = (uint8_t)bs.acc;   // the last partial byte
+      for (int k = (int)bs.pos + (bs.nacc ? 1 : 0); k < (int)bs.pos + 8; k++) ((uint8_t *)W.hw)[k] = 0;
+    }
+    hbits = __shfl(hbits, 0, 64);
+    for (int k = lane; k < STAGE; k += 64) W.stage[k] = 0;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    BitWave bw{region, 0, false};
+    {   // the header's whole words straight to the region, its partial word into the strip
+      const int full = hbits >> 5;
+      for (int k = lane; k < full; k += 64) region[k] = W.hw[k];
+      if (lane == 0) W.stage[0] = (hbits & 31) ? W.hw[full] & ((1u << (hbits & 31)) - 1u) : 0u;
+      bw.bitpos = hbits;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    // pass 2: the same parse, encoded
+    for (int i = lane; i < (1 << HBITS); i += 64) W.ht[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (int cur = 0; cur < S;) {
+      const Step st = parse_step(s, S, cur, W.ht, lane);
+      encode_step(s, cur, st, W, bw, lane);
+      hash_in(s, S, cur, st.next, W.ht, lane);
+      cur = st.next;
+    }
+    // end of block; then either the final padding or a sync flush (empty stored block) to a byte boundary
+    put_bits(bw, W.stage, lane == 0 ? (uint64_t)W.lcode[256] : 0ull, lane == 0 ? W.llen[256] : 0, lane);
+    if (!last) {
+      put_bits(bw, W.stage, 0ull, lane == 0 ? 3 : 0, lane);               // BFINAL 0, BTYPE 00
+      const int pad = (int)((8 - (bw.bitpos & 7)) & 7);
+      put_bits(bw, W.stage, 0ull, lane == 0 ? pad : 0, lane);
+      put_bits(bw, W.stage, lane == 0 ? 0xffff0000ull : 0ull, lane == 0 ? 32 : 0, lane);   // LEN 0, NLEN ~0
+    }
+    const int pad = (int)((8 - (bw.bitpos & 7)) & 7);
+    put_bits(bw, W.stage, 0ull, lane == 0 ? pad : 0, lane);
+    // the partial last word
+    if (lane == 0 && !bw.overflow && (bw.bitpos & 31)) bw.region[bw.bitpos >> 5] = W.stage[0];
+    out_len = (int32_t)(bw.bitpos >> 3);
+    if (bw.overflow) out_len = -1;
+  }
+  if (lane == 0 && out_len < 0) atomicOr(&L.stored, 1);
+  __syncthreads();
+  if (lane == 0) info[blockIdx.x].len[wave] = out_len < 0 ? 0 : out_len;
+  __syncthreads();
+  if (tid == 0) {
+    DfBlockInfo &I = info[blockIdx.x];
+    I.n = n;
+    I.crc = L.crc[0];
+    int64_t tot = 0;
+    for (int w = 0; w < DF_WAVES; w++) tot += I.len[w];
+    I.stored = (L.stored || HDR + tot + TRL > MAX_BSIZE) ? 1 : 0;
+  }
+}
+
+__device__ __forceinline__ int64_t block_bytes(const DfBlockInfo &I) {
+  if (I.stored) return HDR + 5 + I.n + TRL;
+  int64_t t = HDR + TRL;
+  for (int w = 0; w < DF_WAVES; w++) t += I.len[w];
+  return t;
+}
+struct LoadBlk {
+  const DfBlockInfo *info;
+  int64_t nb;
+  __device__ int64_t operator()(int64_t i) const { return i < nb ? block_bytes(info[i]) : 0; }
+};
+struct StoreBlk {
+  int64_t *off;
+  __device__ void operator()(int64_t i, int64_t, int64_t excl) const { off[i] = excl; }
+};
+
+// one workgroup per block: gzip header, the slices (or the stored input), CRC32 and ISIZE at its offset
+__global__ void __launch_bounds__(256) k_bgzf_pack(const uint8_t *in, int64_t b0, const uint8_t *slots,
+                                                   const DfBlockInfo *info, const int64_t *off, uint8_t *out) {
+  const DfBlockInfo &I = info[blockIdx.x];
+  uint8_t *d = out + off[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int64_t bs = block_bytes(I);
+  if (tid < HDR) {
+    static constexpr uint8_t H0[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
+    d[tid] = tid < 16 ? H0[tid] : (uint8_t)((bs - 1) >> (8 * (tid - 16)));
+  }
+  int64_t o = HDR;
+  if (I.stored) {
+    if (tid == 0) {
+      d[o] = 1;   // BFINAL 1, BTYPE 00
+      d[o + 1] = (uint8_t)I.n;
+      d[o + 2] = (uint8_t)(I.n >> 8);
+      d[o + 3] = (uint8_t)~I.n;
+      d[o + 4] = (uint8_t)(~I.n >> 8);
+    }
+    const uint8_t *src = in + (b0 + blockIdx.x) * (int64_t)BLOCK;
+    for (int i = tid; i < I.n; i += 256) d[o + 5 + i] = src[i];
+    o += 5 + I.n;
+  } else {
+    for (int w = 0; w < DF_WAVES; w++) {
+      const uint8_t *src = slots + (size_t)blockIdx.x * SLOT + (size_t)w * REGION;
+      for (int i = tid; i < I.len[w]; i += 256) d[o + i] = src[i];
+      o += I.len[w];
+    }
+  }
+  if (tid < 8) d[o + tid] = (uint8_t)((tid < 4 ? I.crc : (uint32_t)I.n) >> (8 * (tid & 3)));
+}
+
+}  // namespace
+
+int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
+                    int64_t *used) {
+  *used = 0;
+  const int64_t nb_all = (n + BLOCK - 1) / BLOCK;
+  const int64_t CH = 8192;   // blocks per launch (slots: CH x 72 KiB)
+  MH_TRY(ensure(ctx, ctx->gz_slots, (size_t)CH * SLOT + 64));
+  MH_TRY(ensure(ctx, ctx->gz_info, sizeof(DfBlockInfo) * (size_t)CH + 64));
+  MH_TRY(ensure(ctx, ctx->gz_off, sizeof(int64_t) * (size_t)(CH + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->gz_scan, scan_lb_scratch_bytes<int64_t>(CH + 1)));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 3072);
+  int64_t *hs = pinned_small(ctx);
+  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  const size_t lds = sizeof(BlockLds);
+  int64_t w = 0;
+  for (int64_t b0 = 0; b0 < nb_all; b0 += CH) {
+    const int64_t nb = nb_all - b0 < CH ? nb_all - b0 : CH;
+    hipLaunchKernelGGL(k_bgzf_blocks, dim3((unsigned)nb), dim3(DF_THREADS), lds, st, d_in, n, b0, nb,
+                       (uint8_t *)ctx->gz_slots.p, (DfBlockInfo *)ctx->gz_info.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, device_scan_sum<int64_t>(st, nb, LoadBlk{(const DfBlockInfo *)ctx->gz_info.p, nb},
+                                         StoreBlk{(int64_t *)ctx->gz_off.p}, ctx->gz_scan.p, tot));
+    HIPCHK(ctx, hipMemcpyAsync(hs + 32, tot, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    const int64_t bytes = hs[32];
+    if (w + bytes > cap) return arg_fail(ctx, MH_E_CAPACITY, "BGZF output buffer too small");
+    hipLaunchKernelGGL(k_bgzf_pack, dim3((unsigned)nb), dim3(256), 0, st, d_in, b0,
+                       (const uint8_t *)ctx->gz_slots.p, (const DfBlockInfo *)ctx->gz_info.p,
+                       (const int64_t *)ctx->gz_off.p, d_out + w);
+    HIPCHK(ctx, hipGetLastError());
+    w += bytes;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *used = w;
+  return MH_OK;
+}
+
+// worst-case output bytes for n input bytes (every block stored)
+int64_t bgzf_device_bound(int64_t n) { return n + ((n + BLOCK - 1) / BLOCK + 1) * (HDR + 5 + TRL) + 64; }
+
+}  // namespace mh
+

@@ -618,14 +618,13 @@ __device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) 
   return lds_put_u(lds, o, (uint64_t)v);
 }
 
-// 16 bytes at an arbitrary byte offset of the dynamic LDS block: five aligned dword reads + v_alignbyte.  (Offsets,
-// not pointers: an integer round trip of an LDS pointer turns its reads into flat loads.)
+// 16 bytes at an arbitrary byte offset of the dynamic LDS block: one ds_read_b128 (gfx950 reads LDS unaligned; was
+// five aligned dword reads + v_alignbyte).  (Offsets, not pointers: an integer round trip of an LDS pointer turns
+// its reads into flat loads.)
 __device__ __forceinline__ uint4 lds_load16(const char *lds, uint32_t off) {
-  const uint32_t *q = (const uint32_t *)(lds + (off & ~3u));
-  const uint32_t sh = off & 3u;
-  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
-  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+  uint4 v;
+  __builtin_memcpy(&v, lds + off, 16);
+  return v;
 }
 
 // bytes i (0..3) of a dword whose byte i sits at offset x0 + i, with x0 + i < n
@@ -713,10 +712,10 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
-  // (LDS hand-off only: the ragged-edge byte stores above need not land before the chunk sweep; dbg 64: the full
-  // barrier, for A/B)
+  // (dbg 64: an LDS-only barrier — the ragged-edge byte stores above need not land before the chunk sweep — measured
+  // no faster than the full one)
   if (staged) {
-    if (dbg & 64) __syncthreads(); else lds_barrier();
+    if (dbg & 64) lds_barrier(); else __syncthreads();
   }
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
@@ -786,7 +785,7 @@ struct TArgs {
   int32_t rlen, win_stride, head, qstride;
   int32_t dbg;              // experiments (MH_EW_DBG): 1 skip the output sweeps, 2 skip the seam sweep, 8 skip the
                             // qname formatting, 16 skip the gathers, 32 return at once — timing only, the bytes are
-                            // then wrong; 64 full barriers (s_waitcnt vmcnt(0)) instead of LDS-only ones (A/B)
+                            // then wrong; 64 LDS-only barriers instead of full ones (A/B)
 };
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
@@ -972,7 +971,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
     }
   }
-  if (A.dbg & 64) __syncthreads(); else lds_barrier();   // LDS hand-off (each LDS write waited for its load data)
+  if (A.dbg & 64) lds_barrier(); else __syncthreads();   // (dbg 64: LDS-only barriers, measured no faster)
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
   if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, true, A.arena, A.dbg);

@@ -200,6 +200,7 @@ struct mh_ctx {
   mh::DevBuf perm_tmp;  // radix sort scratch (permutation, N runs)
   mh::DevBuf pb[6];     // batch-wide permutation: ts, shuffled ts, global keys, sorted keys, sorted steps, heads
   mh::DevBuf pb_tmp;    // its radix sort scratch
+  mh::DevBuf gz_slots, gz_info, gz_off, gz_scan, gz_out, gz_in;   // device BGZF (mh_deflate.hip)
   mh::DevBuf nrun_tmp;  // unsorted N-run boundaries
   mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
   int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)
@@ -320,6 +321,9 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)
 int32_t sync_async_fill(mh_ctx *ctx);
+int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
+                    int64_t *used);            // BGZF blocks of a device buffer (no EOF marker), mh_deflate.hip
+int64_t bgzf_device_bound(int64_t n);
 int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
 int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);
 int32_t output_reset(mh_ctx *ctx);

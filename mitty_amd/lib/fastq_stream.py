@@ -115,21 +115,28 @@ def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None, max_ahe
   return total
 
 
-def write_pair(sinks, datas):
+def write_pair(sinks, datas, raw_lens=None):
   """Write datas[f] to sinks[f] (None: skipped), each file on its own thread, so a reader that takes the two files in
   lockstep (pysam FastxFile pairs, `corrupt-reads` on FIFOs) never leaves us blocked on one pipe while it waits on
   the other."""
-  jobs = [(s, d) for s, d in zip(sinks, datas) if s is not None]
-  if len(jobs) <= 1:
-    for s, d in jobs:
+  raw_lens = raw_lens or [None] * len(sinks)
+  jobs = [(s, d, r) for s, d, r in zip(sinks, datas, raw_lens) if s is not None]
+
+  def put(s, d, r):   # r: BGZF bytes for r raw bytes (compressed on the GPU), else raw bytes
+    if r is None:
       s.write(d)
+    else:
+      s.write_bgzf(d, r)
+  if len(jobs) <= 1:
+    for j in jobs:
+      put(*j)
     return
   import threading
   errs = []
 
-  def run(s, d):
+  def run(s, d, r):
     try:
-      s.write(d)
+      put(s, d, r)
     except BaseException as e:
       errs.append(e)
   ts = [threading.Thread(target=run, args=j) for j in jobs]
@@ -157,6 +164,16 @@ class FastqSink:
     if self.gz:
       from mitty_amd import _native
       data = _native.bgzf_compress(data, self.level, self.threads)
+    self.written += len(data)
+    mv = memoryview(data)
+    while len(mv):
+      n = self.fp.write(mv)
+      mv = mv[n:]
+
+  def write_bgzf(self, data, raw_len):
+    """BGZF members compressed elsewhere (the GPU: mh_output_bgzf) for `raw_len` bytes of FASTQ."""
+    assert self.gz, 'BGZF members into an uncompressed sink'
+    self.raw += raw_len
     self.written += len(data)
     mv = memoryview(data)
     while len(mv):

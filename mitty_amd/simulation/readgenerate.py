@@ -69,11 +69,12 @@ def get_data_for_workers(model, vcf, seed):
 def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                            fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
                            flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000, compress=None,
-                           gz_level=6, gz_threads=8):
+                           gz_level=6, gz_threads=8, gz_device=True):
   """Generate reads for every (region, copy, pass) unit and write FASTQ (reference readgenerate.py:76-126).
 
-  compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it (level gz_level on
-  gz_threads host threads).  Returns a stats dict (templates sampled, kept, bytes, seconds).
+  compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it; gz_device: deflated on
+  the GPU (mh_output_bgzf) straight from the arenas, else on gz_threads host threads at gz_level.  Returns a stats
+  dict (templates sampled, kept, bytes, seconds).
   """
   t0 = time.time()
   read_model = read_module.read_model_params(model, coverage)
@@ -104,8 +105,14 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
       # both arenas to page-locked memory, then each file written on its own thread: a FIFO reader that takes the
       # two files in lockstep (examples/reads/run.sh:13-16) is never starved of one while we block on the other
-      d1, d2 = eng.ctx.fetch_output_pinned(pins)
-      write_pair([fp1, fp2 if write2 else None], [d1, d2])
+      sinks = [fp1, fp2 if write2 else None]
+      if gz_device and all(s is None or s.gz for s in sinks):
+        raw = eng.ctx.output_size()
+        z1, z2 = eng.ctx.output_bgzf_pinned(pins)
+        write_pair(sinks, [z1, z2], list(raw))
+      else:
+        d1, d2 = eng.ctx.fetch_output_pinned(pins)
+        write_pair(sinks, [d1, d2])
       eng.ctx.reset_output()
 
   try:

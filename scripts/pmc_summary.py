@@ -2,8 +2,10 @@
 """Summarise a gpu_pmc.sh run into profiles/pmc_<kernel>_<round>.json (read by bench.py for roofline.traffic).
 
 HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md § HBM: FETCH_SIZE and WRITE_SIZE are in KiB, from
-separate passes; on gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) streaming reads, so it is doubled
-(the kernel's haplotype / slot / metadata gathers are 16-byte loads).  WRITE_SIZE is exact for 16-byte stores.
+separate passes; on gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) streaming reads, so it is doubled.
+The doubling is calibrated for the writer's own pattern too — 16-byte gathers of 150-byte windows at random
+offsets read 1.97 x FETCH_SIZE bytes of distinct 128-byte lines (profiles/calib_fetch_size_r03.json,
+scripts/calib_fetch.hip).  WRITE_SIZE is exact for 16-byte stores.
 usage: pmc_summary.py <pmc dir> <tag> <kernel> <round> <rlen> <length> [algorithmic bytes per launch]
 """
 import csv

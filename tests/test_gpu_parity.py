@@ -1428,3 +1428,41 @@ def test_writer_gate_pipelined_jobs(native, monkeypatch):
     eng.close()
   G.check_same(d1, want1 * 3, 'file 1 differs')
   G.check_same(d2, want2 * 3, 'file 2 differs')
+
+
+# ---- device BGZF (mh_deflate.hip) ----------------------------------------------------------
+def _bgzf_members(z):
+  """The BGZF members of z: (BSIZE, ISIZE) each, checking the gzip header and the BC extra field."""
+  out, o = [], 0
+  while o < len(z):
+    assert z[o:o + 4] == b'\x1f\x8b\x08\x04' and z[o + 12:o + 16] == b'BC\x02\x00', o
+    bsize = int.from_bytes(z[o + 16:o + 18], 'little') + 1
+    isize = int.from_bytes(z[o + bsize - 4:o + bsize], 'little')
+    assert isize <= 0xff00
+    out.append((bsize, isize))
+    o += bsize
+  assert o == len(z)
+  return out
+
+
+@pytest.mark.parametrize('name', ['fastq', 'random', 'zeros', 'one', 'block', 'block1', 'large', 'mixed'])
+def test_device_bgzf_round_trip(ctx, name):
+  """GPU deflate (a workgroup per BGZF block, eight dynamic-Huffman slices): every member a valid BGZF block, the
+  whole inflating (zlib) to the input; incompressible blocks stored; FASTQ about as small as gzip -1."""
+  import os as _os
+  fq = G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
+  data = {'fastq': fq, 'random': _os.urandom(300_001), 'zeros': b'\0' * 1_000_000, 'one': b'@',
+          'block': fq[:0xff00], 'block1': fq[:0xff01], 'large': (fq * 40)[:25_000_003],
+          'mixed': fq[:100_000] + _os.urandom(70_000) + b'~' * 90_000 + fq[:50_000]}[name]
+  z = ctx.bgzf_compress(data)
+  members = _bgzf_members(z)
+  assert sum(m[1] for m in members) == len(data)
+  assert len(members) == (len(data) + 0xff00 - 1) // 0xff00
+  from mitty_amd import _native
+  assert gzip.decompress(z + _native.bgzf_eof()) == data
+  if name in ('fastq', 'large'):
+    assert len(z) < 1.1 * len(gzip.compress(data[:5_000_000], 1)) * max(1, len(data) / 5_000_000)
+
+
+def test_device_bgzf_empty(ctx):
+  assert ctx.bgzf_compress(b'') == b''
