@@ -387,17 +387,23 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     t3 = time.perf_counter()
     out = {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
            'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
+           'split_s': {k: round(st[k], 3) for k in ('setup_s', 'fetch_s', 'write_s')},
            'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
                    'page-locked memory, written to /dev/null; seconds = the whole command'}
-    if a.e2e_gz:   # the same with both files BGZF-compressed on the host (what `.gz` output names cost)
+    if a.e2e_gz:   # the same with both files BGZF-compressed (what `.gz` output names cost): on the GPU, then on host
       threads = min(16, os.cpu_count() or 1)
-      t4 = time.perf_counter()
-      st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
-                                               seed=a.seed, compress=True, gz_level=1, gz_threads=threads)
-      t5 = time.perf_counter()
-      out['gz'] = {'seconds': t5 - t4, 'value': st['kept'] / (t5 - t4), 'unit': 'templates/s', 'level': 1,
-                   'gz_bytes': st['written1'] + st['written2'],
-                   'threads': threads, 'note': 'the same command with BGZF output (host deflate pool)'}
+      for key, dev in (('gz', True), ('gz_host', False)):
+        t4 = time.perf_counter()
+        st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
+                                                 seed=a.seed, compress=True, gz_level=1, gz_threads=threads,
+                                                 gz_device=dev)
+        t5 = time.perf_counter()
+        out[key] = {'seconds': t5 - t4, 'value': st['kept'] / (t5 - t4), 'unit': 'templates/s',
+                    'gz_bytes': st['written1'] + st['written2'],
+                    'split_s': {k: round(st[k], 3) for k in ('setup_s', 'fetch_s', 'write_s')},
+                    'note': 'the same command with BGZF output, deflated ' +
+                            ('on the GPU from the arenas (mh_output_bgzf), then D2H of the compressed bytes' if dev else
+                             'by the host pool (level 1, {} threads) after D2H'.format(threads))}
     return out
   finally:
     for f in glob.glob(os.path.join(d, '*')):

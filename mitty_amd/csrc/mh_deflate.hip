@@ -16,8 +16,9 @@
 //   pass 2  the same parse again, each step's codes placed by a wave prefix sum of their bit lengths into an LDS
 //           staging strip, whole words flushed to the slice's region of the block's slot;
 //   CRC-32  every thread a 128-byte segment, combined over a tree (x^(8n) operators).
-// A block whose compressed size would not fit a BGZF block is stored instead.  k_bgzf_pack then writes the
-// blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets from a scan of their sizes.
+// A block whose codes would not fit a BGZF block, or not be smaller than its bytes, is stored instead.
+// k_bgzf_pack then writes the blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets
+// from a scan of their sizes.
 #include "mh_deflate.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
@@ -396,7 +397,8 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     I.crc = L.crc[0];
     int64_t tot = 0;
     for (int w = 0; w < DF_WAVES; w++) tot += I.len[w];
-    I.stored = (L.stored || HDR + tot + TRL > MAX_BSIZE) ? 1 : 0;
+    // stored also when the codes would not be smaller (random bytes): the output never exceeds bgzf_device_bound
+    I.stored = (L.stored || HDR + tot + TRL > MAX_BSIZE || tot >= 5 + (int64_t)n) ? 1 : 0;
   }
 }
 

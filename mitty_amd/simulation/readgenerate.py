@@ -74,7 +74,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
 
   compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it; gz_device: deflated on
   the GPU (mh_output_bgzf) straight from the arenas, else on gz_threads host threads at gz_level.  Returns a stats
-  dict (templates sampled, kept, bytes, seconds).
+  dict (templates sampled, kept, bytes, seconds; setup_s = inputs parsed and loaded, fetch_s = waiting for the GPU
+  and its D2H (deflate included), write_s = file writes).
   """
   t0 = time.time()
   read_model = read_module.read_model_params(model, coverage)
@@ -89,7 +90,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   for ri, reg in enumerate(vdf):
     chrom, s0, e = reg['region']
     eng.load_region(ri, reg['region'], mfasta.fetch(seqs, chrom, s0, e))
-  stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0}
+  stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0, 'setup_s': time.time() - t0,
+           'fetch_s': 0.0, 'write_s': 0.0}
   write2 = fastq2_fname is not None
   fp1 = FastqSink(fastq1_fname, gz_level, gz_threads, compress)   # '.gz' names get BGZF output
   fp2 = FastqSink(fastq2_fname, gz_level, gz_threads, compress) if write2 else None
@@ -106,13 +108,18 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
       # both arenas to page-locked memory, then each file written on its own thread: a FIFO reader that takes the
       # two files in lockstep (examples/reads/run.sh:13-16) is never starved of one while we block on the other
       sinks = [fp1, fp2 if write2 else None]
+      tf = time.time()
       if gz_device and all(s is None or s.gz for s in sinks):
         raw = eng.ctx.output_size()
         z1, z2 = eng.ctx.output_bgzf_pinned(pins)
+        tw = time.time()
         write_pair(sinks, [z1, z2], list(raw))
       else:
         d1, d2 = eng.ctx.fetch_output_pinned(pins)
+        tw = time.time()
         write_pair(sinks, [d1, d2])
+      stats['fetch_s'] += tw - tf
+      stats['write_s'] += time.time() - tw
       eng.ctx.reset_output()
 
   try:

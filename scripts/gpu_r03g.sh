@@ -19,3 +19,6 @@ C1="python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline"
 run chr1 $C1 || exit $?
 run chr1_b64 MH_EW_DBG=64 $C1 --no-e2e || exit $?
 run wgs python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --batch-draws 64e6 || exit $?
+run chr1_d128 MH_EW_DBG=128 $C1 --no-e2e || exit $?
+run chr1_d4 MH_EW_DBG=4 $C1 --no-e2e || exit $?
+run chr1_d1 MH_EW_DBG=1 $C1 --no-e2e || exit $?
