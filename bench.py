@@ -76,6 +76,9 @@ def parse():
   ap.add_argument('--batch-draws', type=float, default=32e6,
                   help='wgs: units are sampled in batches of about this many template draws (a chr1 job is 30 M); '
                        'the FASTQ arenas are recycled per batch')
+  ap.add_argument('--batch-ramp', type=int, default=0,
+                  help='wgs: the first K batches of a step are 2^-K, 2^-(K-1), .. of --batch-draws (the first writer '
+                       'starts after a small batch is sampled, not a full one)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
   ap.add_argument('--pipeline', default='batch', choices=['batch', 'phased', 'phased-sync'],
                   help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
@@ -459,10 +462,10 @@ def run_genome(a, rank, world, local):
   eng.ctx.set_emit_mode(a.emit_mode)
   kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
   batches, cur, draws = [], [], 0
-  for u in mine:   # batches of about --batch-draws template draws, in unit (ps) order
+  for u in mine:   # batches of about --batch-draws template draws (the first --batch-ramp ones smaller), in ps order
     cur.append(u)
     draws += int(contigs[u[1]][1] * p * 1.2)
-    if draws >= a.batch_draws:
+    if draws >= a.batch_draws / 2 ** max(0, a.batch_ramp - len(batches)):
       batches.append(cur)
       cur, draws = [], 0
   if cur:
@@ -568,7 +571,8 @@ def run_genome(a, rank, world, local):
                            'genome)'.format('' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
                                             a.model, rlen, a.coverage, a.rng, world),
                'genome_bp': sum(L for _, L in contigs), 'read_model': a.model, 'coverage': a.coverage,
-               'units': n_units, 'batches_rank0': len(batches), 'pipeline': a.pipeline,
+               'units': n_units, 'batches_rank0': len(batches), 'batch_draws': a.batch_draws,
+               'batch_ramp': a.batch_ramp, 'pipeline': a.pipeline,
                'templates_per_step': kept_all // steps,
                'parallelism': 'unit-shard (LPT) x{}'.format(world) if world > 1 else 'single GPU',
                'world_size_seen': seen, 'collective_backend': backend},

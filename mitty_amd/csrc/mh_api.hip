@@ -429,20 +429,29 @@ int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_
   return MH_OK;
 }
 
-// the slot's Hap for a (re)build: the oldest released haplotype's buffers unless a queued writer still reads them
-// (then fresh ones: the pool grows to the generations a pipelined job needs); the main stream waits for the slot's
-// last writer
-static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, Hap **out) {
-  const bool spare_ready = !ctx->hap_spare.empty() &&
-                           (!ctx->hap_spare.front().used_set || hipEventQuery(ctx->hap_spare.front().used) == hipSuccess);
-  if (!ctx->haps.count(slot) && spare_ready) {
-    Hap r{};
-    const Hap &s = ctx->hap_spare.front();
-    r.hap = s.hap; r.rc = s.rc; r.keys = s.keys; r.ps = s.ps; r.pr = s.pr; r.op = s.op; r.oplen = s.oplen;
-    r.nrun_s = s.nrun_s; r.nrun_e = s.nrun_e; r.nd = s.nd; r.bkt = s.bkt;
-    r.used = s.used; r.used_set = s.used_set; r.used_gate = s.used_gate;
-    ctx->hap_spare.erase(ctx->hap_spare.begin());
-    ctx->haps[slot] = r;
+// the slot's Hap for a (re)build: released haplotypes' buffers when one is free (no queued writer still reads it) —
+// the smallest whose haplotype buffer holds `need` bytes, else the largest (grown by the build) — else fresh ones
+// (the pool grows to the generations a pipelined job needs); the main stream waits for the slot's last writer.  Best
+// fit keeps a whole genome's haplotypes (50 of very different lengths) rebuilding without a hipMalloc / hipFree.
+static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, int64_t need, Hap **out) {
+  if (!ctx->haps.count(slot)) {
+    int best = -1, big = -1;
+    for (int i = 0; i < (int)ctx->hap_spare.size(); i++) {
+      const Hap &s = ctx->hap_spare[i];
+      if (s.used_set && hipEventQuery(s.used) != hipSuccess) continue;   // a queued writer still reads it
+      if (s.hap.cap >= (size_t)need && (best < 0 || s.hap.cap < ctx->hap_spare[best].hap.cap)) best = i;
+      if (big < 0 || s.hap.cap > ctx->hap_spare[big].hap.cap) big = i;
+    }
+    if (best < 0) best = big;
+    if (best >= 0) {
+      Hap r{};
+      const Hap &s = ctx->hap_spare[best];
+      r.hap = s.hap; r.rc = s.rc; r.keys = s.keys; r.ps = s.ps; r.pr = s.pr; r.op = s.op; r.oplen = s.oplen;
+      r.nrun_s = s.nrun_s; r.nrun_e = s.nrun_e; r.nd = s.nd; r.bkt = s.bkt;
+      r.used = s.used; r.used_set = s.used_set; r.used_gate = s.used_gate;
+      ctx->hap_spare.erase(ctx->hap_spare.begin() + best);
+      ctx->haps[slot] = r;
+    }
   }
   Hap &h = ctx->haps[slot];
   MH_TRY(wait_unused(ctx, h.used, h.used_set, h.used_gate));   // a queued writer may still read the old bytes
@@ -457,7 +466,7 @@ static int32_t build_from(mh_ctx *ctx, int32_t slot, int32_t contig_id, int64_t 
   auto it = ctx->contigs.find(contig_id);
   if (it == ctx->contigs.end()) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
   Hap *hp = nullptr;
-  MH_TRY(hap_for_build(ctx, slot, &hp));
+  MH_TRY(hap_for_build(ctx, slot, it->second.len + (it->second.len >> 6) + (1 << 20), &hp));
   Hap &h = *hp;
   MH_TRY(splice_build(ctx, h, it->second, ref_start_pos, v));
   if (out_n_nodes) *out_n_nodes = h.n_nodes;
@@ -518,7 +527,10 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
   for (int32_t i0 = 0; i0 < n; i0 += 2) {   // two copies at a time: the second on its own stream and host thread
     const int32_t k = n - i0 < 2 ? n - i0 : 2;
     Hap *hp[2] = {nullptr, nullptr};
-    for (int32_t j = 0; j < k; j++) MH_TRY(hap_for_build(ctx, slots[i0 + j], &hp[j]));
+    for (int32_t j = 0; j < k; j++) {
+      const int64_t L = ctx->contigs[contig_ids[i0 + j]].len;
+      MH_TRY(hap_for_build(ctx, slots[i0 + j], L + (L >> 6) + (1 << 20), &hp[j]));
+    }
     if (k == 1) {
       MH_TRY(splice_build(ctx, *hp[0], ctx->contigs[contig_ids[i0]], ref_starts[i0], ctx->vsets[vsets[i0]]));
     } else {
@@ -600,7 +612,8 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
   // keep the buffers for the next build (stream order protects them: every later user is on ctx->stream)
-  constexpr size_t SPARE_MAX = 8;   // three generations of a pipelined job's haplotypes (asynchronous emission)
+  // a whole genome's haplotypes (25 regions x 2 copies) plus pipelined generations (asynchronous emission)
+  constexpr size_t SPARE_MAX = 128;
   if (ctx->hap_spare.size() < SPARE_MAX) {
     h.valid = false;
     ctx->hap_spare.push_back(h);

@@ -799,7 +799,8 @@ struct TArgs {
   int32_t dbg;              // experiments (MH_EW_DBG): 1 skip the output sweeps, 2 skip the seam sweep, 4 no LDS
                             // reads in the chunk sweep, 8 skip the qname formatting, 16 skip the gathers, 32 return
                             // at once — timing only, the bytes are then wrong; 64 LDS-only barriers instead of full
-                            // ones, 128 chunk reads by aligned ds_read_b64 (A/B)
+                            // ones, 128 chunk reads by aligned ds_read_b64, 256 seam chunks stored by the seam
+                            // pass (4 KB less LDS per workgroup) (A/B)
 };
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
@@ -835,7 +836,8 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
   const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
-  const int32_t o_dump = o_s + NF * ED_T * 4 * 16;   // 16-byte sink for unused gathers
+  const bool staged = !(A.dbg & 256);                // seam chunks through LDS (in order with the others)
+  const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
@@ -988,7 +990,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   if (A.dbg & 64) lds_barrier(); else __syncthreads();   // (dbg 64: LDS-only barriers, measured no faster)
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
-  if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, true, A.arena, A.dbg);
+  if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena, A.dbg);
 }
 
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
@@ -1328,10 +1330,16 @@ static int64_t digit_sum_host(int64_t K) {
 }
 
 // dynamic LDS of k_emit_tiles: metadata, windows, qname buffers, T, seam chunks, dump
+// MH_EW_DBG (experiments, k_emit_tiles' TArgs.dbg)
+static int ew_dbg_env() {
+  static const int v = getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0;
+  return v;
+}
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf) {
+  const bool staged = !(ew_dbg_env() & 256);   // (256: seam chunks stored by the seam pass, no LDS for them)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-         (size_t)nf * ED_T * 4 * 16 + 16;
+         (staged ? (size_t)nf * ED_T * 4 * 16 : 0) + 16;
 }
 
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
@@ -1553,7 +1561,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
     stage_begin(ctx, "emit_write");
-    static const int ew_dbg = getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0;
+    const int ew_dbg = ew_dbg_env();
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
             qstride, ew_dbg};
@@ -1882,7 +1890,8 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   stage_end(ctx);
   stage_begin(ctx, "emit_write");
   TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
-          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride};
+          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride,
+          ew_dbg_env()};
   auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
                              : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
