@@ -15,7 +15,10 @@ constexpr int BLOCK = 0xff00;         // input bytes per BGZF block (htslib's BG
 constexpr int MAX_BSIZE = 65536;      // a BGZF block, header and trailer included
 constexpr int HDR = 18, TRL = 8;      // gzip member header with the BC extra field; CRC32 + ISIZE
 constexpr int NLIT = 286, NDIST = 30, NCL = 19;
-constexpr int MIN_MATCH = 4, MAX_MATCH = 258, MAX_DIST = 32768;
+// MIN_MATCH: the shortest match taken.  Inside FASTQ bases (random ACGT) a 4-6-byte match costs more bits than its
+// literals (~2 bits each) and cuts the parse into short steps: from 4 to 7 the golden FASTQ deflates to 4.50x instead
+// of 4.30x (gzip -1: 4.39x) in 6.8x fewer parse steps.  Positions are hashed on their first HASH_BYTES bytes.
+constexpr int MIN_MATCH = 7, HASH_BYTES = 4, MAX_MATCH = 258, MAX_DIST = 32768;
 
 __host__ __device__ inline int len_code(int len) {   // 3..258 -> 0..28 (symbol 257 + code)
   if (len <= 10) return len - 3;

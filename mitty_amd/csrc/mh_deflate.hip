@@ -8,7 +8,7 @@
 // next slice's bits start on a byte boundary, and the slices' bytes simply concatenate; wave 7's block is final.
 //   parse   greedy LZ77 over the slice, 64 positions per step: every lane looks up its position (a 2^11-entry hash of
 //           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1); the
-//           first lane with a four-byte match ends the step's literals, its match is extended by the whole wave
+//           first lane with a MIN_MATCH-byte match ends the step's literals, its match is extended by the whole wave
 //           (up to 258 bytes), then the positions passed are hashed in;
 //   pass 1  the parse, counting symbol frequencies;
 //   codes   lane 0: length-limited Huffman lengths (15 bits; 7 for the code-length code), canonical codes, the
@@ -20,6 +20,7 @@
 // k_bgzf_pack then writes the blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets
 // from a scan of their sizes.
 #include "mh_deflate.h"
+#include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -74,6 +75,11 @@ __device__ __forceinline__ uint32_t load4(const uint8_t *b, int x) {   // bytes 
   return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(x & 3));
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t w) { return (w * 2654435761u) >> (32 - HBITS); }
+// bytes p .. p+6 equal bytes c .. c+6 (MIN_MATCH = 7: two overlapping 4-byte words)
+__device__ __forceinline__ bool match7(const uint8_t *s, int p, uint32_t wp, int c) {
+  return load4(s, c) == wp && load4(s, c + 3) == load4(s, p + 3);
+}
+static_assert(MIN_MATCH == 7, "match7");
 
 // Wave-wide ascending sort of n <= 320 keys in LDS (bitonic over the next power of two, padded with ~0u).
 __device__ void wave_sort(uint32_t *k, int n, int lane) {
@@ -133,11 +139,11 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
   int cand = -1;
   if (p + MIN_MATCH <= S) {
     const uint32_t w = load4(s, p);
-    if (p >= 1 && load4(s, p - 1) == w) {
+    if (p >= 1 && match7(s, p, w, p - 1)) {
       cand = p - 1;                                  // a run: distance 1
     } else {
       const int j = (int)ht[hash4(w)] - 1;           // a position of an earlier step (< cur <= p)
-      if (j >= 0 && load4(s, j) == w) cand = j;
+      if (j >= 0 && match7(s, p, w, j)) cand = j;
     }
   }
   const uint64_t bal = __ballot(cand >= 0);
@@ -176,23 +182,14 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
 // both passes see the same table
 __device__ __forceinline__ void hash_in(const uint8_t *s, int S, int a, int b, uint32_t *ht, int lane) {
   for (int k = a + lane; k < b; k += 64)
-    if (k + MIN_MATCH <= S) atomicMax(&ht[hash4(load4(s, k))], (uint32_t)(k + 1));
+    if (k + HASH_BYTES <= S) atomicMax(&ht[hash4(load4(s, k))], (uint32_t)(k + 1));
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 }
 
-// the symbols of one step, pass 1: literal frequencies (a ballot loop over the distinct bytes) and the match's
+// the symbols of one step, pass 1: literal frequencies (LDS atomics, one per literal lane) and the match's
 __device__ __forceinline__ void count_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, int lane) {
-  const bool lit = lane < st.nlit;
-  const uint32_t c = lit ? s[cur + lane] : 0u;
-  uint64_t todo = __ballot(lit);
-  while (todo) {
-    const int l0 = __builtin_ctzll(todo);
-    const uint32_t c0 = __shfl(c, l0, 64);
-    const uint64_t same = __ballot(lit && c == c0);
-    if (lane == l0) W.lf[c0] += (uint32_t)__popcll(same);
-    todo &= ~same;
-  }
+  if (lane < st.nlit) atomicAdd(&W.lf[s[cur + lane]], 1u);
   if (st.has_match && lane == 0) {
     W.lf[257 + len_code(st.mlen)]++;
     W.dfq[dist_code(st.mdist)]++;
@@ -211,14 +208,8 @@ struct BitWave {
 
 // put each lane's (v, n) (n <= 57 bits: v < 2^n) in lane order after bitpos
 __device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t v, int n, int lane) {
-  int off = n;   // inclusive prefix of the bit lengths across the wave
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int o = __shfl_up(off, d, 64);
-    if (lane >= d) off += o;
-  }
-  const int total = __shfl(off, 63, 64);
-  const int excl = off - n;
+  int total;
+  const int excl = wave_sum_incl(n, total) - n;   // the bits before this lane's
   const int r = (int)(bw.bitpos & 31) + excl;   // bit offset inside the staging strip
   if (n) {
     const int wi = r >> 5, sh = r & 31;
@@ -286,8 +277,23 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   if (blockIdx.x >= nb) return;
   const int64_t start = b * BLOCK;
   const int n = (int)(n_in - start < BLOCK ? n_in - start : BLOCK);
-  // stage the block (16-byte loads where aligned, bytes otherwise) and the CRC table
-  for (int i = tid; i < BLOCK + 64; i += DF_THREADS) L.in[i] = i < n ? in[start + i] : 0;
+  // stage the block (16-byte loads when the block starts 16-byte aligned, bytes otherwise) and the CRC table
+  const uint8_t *src = in + start;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    for (int i = tid; i < (BLOCK + 64) / 16; i += DF_THREADS) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (16 * i + 16 <= n) {
+        v = reinterpret_cast<const uint4 *>(src)[i];
+      } else if (16 * i < n) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int k = 0; 16 * i + k < n; k++) w[k >> 2] |= (uint32_t)src[16 * i + k] << (8 * (k & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      reinterpret_cast<uint4 *>(L.in)[i] = v;
+    }
+  } else {
+    for (int i = tid; i < BLOCK + 64; i += DF_THREADS) L.in[i] = i < n ? src[i] : 0;
+  }
   for (int i = tid; i < 256; i += DF_THREADS) {
     uint32_t c = (uint32_t)i;
     for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ CRC_POLY : c >> 1;

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <rocprim/warp/warp_scan.hpp>
+
 namespace mh {
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations, not for its global
@@ -32,6 +34,16 @@ __device__ __forceinline__ uint4 load16_unaligned(const uint8_t *a) {
   const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
+
+// Inclusive sum across the 64 lanes of a wave (DPP row shifts and broadcasts: rocprim's cross-lane warp scan; the
+// __shfl_up loop it replaces is six ds_bpermute round trips); `total` = the wave's sum, in every lane.
+__device__ __forceinline__ int wave_sum_incl(int v, int &total) {
+  using WS = rocprim::warp_scan<int, 64>;
+  typename WS::storage_type none;
+  int out;
+  WS().inclusive_scan(v, out, total, none);
+  return out;
 }
 
 }  // namespace mh

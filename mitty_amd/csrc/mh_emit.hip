@@ -760,13 +760,8 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
 }
 
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
-  return v;
+  int total;
+  return wave_sum_incl(v, total);
 }
 
 // tile sums of k_emit_measure -> tile prefixes (kept, bytes per file without the cnt digits)

@@ -1221,6 +1221,17 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
+// The permutation's (target, step) sort: rocprim's LSD onesweep radix sort.  (Its gfx950 tuning runs 1024-thread
+// sort workgroups, which find no room on a CU beside the FASTQ writers and wait for them to drain; 256-thread onesweep
+// workgroups that do fit beside them made the steps slower — WGS 1.18 vs 1.37 G/s, chr1 1.30 vs 1.50 — so the
+// default tuning stays.)
+template <class KIn>
+static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
+                            size_t n, unsigned end_bit, hipStream_t st) {
+  const rocprim::counting_iterator<uint32_t> iota(0u);
+  return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
+}
+
 struct BatchPerm {
   int64_t *ts, *tsh;
 };
@@ -1285,10 +1296,9 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       unsigned end_bit = 1;
       while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
       size_t tmp = 0;
-      const rocprim::counting_iterator<uint32_t> iota(0u);
-      HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+      HIPCHK(ctx, perm_sort(nullptr, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
-      HIPCHK(ctx, rocprim::radix_sort_pairs(perm_tmp.p, tmp, jarr, sk, iota, sv, (size_t)n, 0u, end_bit, st));
+      HIPCHK(ctx, perm_sort(perm_tmp.p, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
       hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                          (const uint32_t *)sv, nxt);
@@ -1561,10 +1571,9 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     unsigned end_bit = 1;
     while (end_bit < 32 && ((int64_t)1 << end_bit) < j_total) end_bit++;
     size_t tmp = 0;
-    const rocprim::counting_iterator<uint32_t> iota(0u);
-    HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, gk, sk, iota, sv, (size_t)j_total, 0u, end_bit, st));
+    HIPCHK(ctx, perm_sort(nullptr, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     MH_TRY(ensure(ctx, ctx->pb_tmp, tmp + 256));
-    HIPCHK(ctx, rocprim::radix_sort_pairs(ctx->pb_tmp.p, tmp, gk, sk, iota, sv, (size_t)j_total, 0u, end_bit, st));
+    HIPCHK(ctx, perm_sort(ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
     hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,

@@ -1,7 +1,7 @@
 // Host check of the single-thread parts of the device BGZF compressor (mitty_amd/csrc/mh_deflate.h: Huffman code
 // lengths, canonical codes, the dynamic block header, CRC-32 combination).  Test infrastructure: compresses a file
 // into BGZF with a sequential restatement of mh_deflate.hip's parse (64-position steps, hash of earlier steps, run
-// candidate, eight slices per block with sync flushes) and the shared header code; tests/test_deflate_cpu.py then
+// candidate, MIN_MATCH-byte matches, eight slices per block with sync flushes) and the shared header code; tests/test_deflate_cpu.py then
 // inflates the output with Python's zlib.  usage: deflate_host IN OUT
 #include <cstdio>
 #include <cstring>
@@ -34,12 +34,13 @@ std::vector<Tok> parse(const uint8_t *s, int S) {
       const int p = cur + l;
       if (p + MIN_MATCH > S) continue;
       const uint32_t w = load4(s, p);
-      if (p >= 1 && load4(s, p - 1) == w) {
+      auto match = [&](int c) { return std::memcmp(s + p, s + c, MIN_MATCH) == 0; };
+      if (p >= 1 && match(p - 1)) {
         f = l;
         j = p - 1;
       } else {
         const int c = (int)ht[hash4(w)] - 1;
-        if (c >= 0 && load4(s, c) == w) {
+        if (c >= 0 && match(c)) {
           f = l;
           j = c;
         }
@@ -59,7 +60,7 @@ std::vector<Tok> parse(const uint8_t *s, int S) {
       next = q + len;
     }
     for (int k = cur; k < next; k++)
-      if (k + MIN_MATCH <= S) {
+      if (k + HASH_BYTES <= S) {
         uint32_t &e = ht[hash4(load4(s, k))];
         if ((uint32_t)(k + 1) > e) e = (uint32_t)(k + 1);
       }
