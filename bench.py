@@ -73,7 +73,7 @@ def parse():
                   help='wgs: whole synthetic GRCh37 at every N (the metric; configs[3]); chr1: configs[1], N = 1')
   ap.add_argument('--genome-scale', type=float, default=1.0,
                   help='wgs: contig lengths scaled by this (rehearsals of the plan; 1 = GRCh37)')
-  ap.add_argument('--batch-draws', type=float, default=32e6,
+  ap.add_argument('--batch-draws', type=float, default=64e6,
                   help='wgs: units are sampled in batches of about this many template draws (a chr1 job is 30 M); '
                        'the FASTQ arenas are recycled per batch')
   ap.add_argument('--batch-ramp', type=int, default=0,
@@ -510,14 +510,17 @@ def run_genome(a, rank, world, local):
     if a.pipeline != 'batch':
       return step_phased()
     eng.drop_haplotypes()
-    kept = b1 = b2 = 0
+    res = []
     for batch in batches:
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
-      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it
+      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it.  --async-emit: the batch's
+      # measure passes and writers are queued without a host round trip per unit (mh_emit_async), so the host moves
+      # on to the next batch's splice and sampling while they run
       eng.ctx.reset_output()
-      for _, kp, x1, x2 in eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0,
-                                         True, a.rng):
-        kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
+      res.append(eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
+                               lazy=a.async_emit))
+    res = [u for r in res for u in (r.resolve() if hasattr(r, 'resolve') else r)]
+    kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
     if dist is not None:
       counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
       dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)

@@ -261,11 +261,16 @@ int32_t mh_bgzf_eof(char *out28);
  * per eighth of a block).  Output decompresses to the input (the bytes differ from zlib's).  No EOF marker.
  *   mh_bgzf_compress_device  device buffer -> device buffer (cap bytes; MH_E_CAPACITY when short)
  *   mh_bgzf_compress_gpu     host buffer -> host buffer through the context's staging
- *   mh_output_bgzf           FASTQ arena `file` (0, 1) -> host buffer (out NULL: *used = the size only) */
+ *   mh_output_bgzf           FASTQ arena `file` (0, 1) -> host buffer (out NULL: *used = the size only)
+ *   mh_output_bgzf_range     bytes [offset, offset + len) of arena `file` -> host buffer: chunked D2H through small
+ *                            page-locked buffers; offsets at multiples of 0xff00 give the members one call over the
+ *                            whole arena gives */
 int32_t mh_bgzf_compress_device(mh_ctx *ctx, const void *d_in, int64_t len, void *d_out, int64_t cap,
                                 int64_t *used);
 int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out, int64_t cap, int64_t *used);
 int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used);
+int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t len, char *out, int64_t cap,
+                             int64_t *used);
 
 /* ---- corrupt-reads over existing FASTQ (readcorrupt.multi_process, readcorrupt.py:18-118; cli.py:144-157) -----
  * The complete templates of the host buffers (file 2 optional) are corrupted with the model set by

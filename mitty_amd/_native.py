@@ -24,6 +24,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
+           'mh_output_bgzf_range',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
 
@@ -81,6 +82,7 @@ def lib():
   _sig(L, 'mh_bgzf_compress_device', [c_vp, c_vp, c_i64, c_vp, c_i64, P_i64])
   _sig(L, 'mh_bgzf_compress_gpu', [c_vp, c_vp, c_i64, c_vp, c_i64, P_i64])
   _sig(L, 'mh_output_bgzf', [c_vp, c_i32, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_output_bgzf_range', [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, P_i64])
   _sig(L, 'mh_expand_variant', [c_i64, c_i64, c_i64, c_i64, c_i32, c_i64, P_i64, ctypes.POINTER(c_i32), P_i64, P_i64])
   _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
@@ -568,6 +570,15 @@ class Context:
           self._chk(self._L.mh_output_fetch(self._h, 0, None, 0, off, c_vp(pin.ptr), n))
         sinks[f].write(pin.view(n))
 
+  def fetch_range_pinned(self, pins, off1, n1, off2, n2):
+    """Arena bytes [off1, off1 + n1) of file 1 and [off2, off2 + n2) of file 2 into page-locked staging (pins:
+    [PinnedBuffer, PinnedBuffer], grown as needed); returns memoryviews of them (valid until the next fetch)."""
+    pins[0].reserve(max(n1, 1))
+    pins[1].reserve(max(n2, 1))
+    self._chk(self._L.mh_output_fetch(self._h, off1, c_vp(pins[0].ptr) if n1 > 0 else None, n1, off2,
+                                      c_vp(pins[1].ptr) if n2 > 0 else None, n2))
+    return pins[0].view(n1), pins[1].view(n2)
+
   def fetch_output_pinned(self, pins):
     """The whole arenas into page-locked staging (pins: [PinnedBuffer, PinnedBuffer], grown as needed); returns
     memoryviews of the bytes (valid until the next fetch)."""
@@ -591,6 +602,21 @@ class Context:
     used = c_i64()
     self._chk(self._L.mh_bgzf_compress_gpu(self._h, _ptr(src), n, _ptr(out), len(out), ctypes.byref(used)))
     return out[:used.value].tobytes()
+
+  def output_bgzf_range_pinned(self, pins, off, n1, n2):
+    """Arena bytes [off, off + n_f) of each file BGZF-compressed on the GPU into page-locked staging (pins:
+    [PinnedBuffer, PinnedBuffer]); returns memoryviews of the compressed bytes (no EOF marker)."""
+    out = []
+    for f, n in enumerate((n1, n2)):
+      if n <= 0:
+        out.append(memoryview(b''))
+        continue
+      cap = n + (n // 0xff00 + 2) * 40 + 64   # every block stored, at worst
+      pins[f].reserve(cap)
+      used = c_i64()
+      self._chk(self._L.mh_output_bgzf_range(self._h, f, off, n, c_vp(pins[f].ptr), cap, ctypes.byref(used)))
+      out.append(pins[f].view(used.value))
+    return out
 
   def output_bgzf_pinned(self, pins):
     """Both arenas BGZF-compressed on the GPU into page-locked staging (pins: [PinnedBuffer, PinnedBuffer]);

@@ -1211,22 +1211,31 @@ int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out
   return MH_OK;
 }
 
-int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used) {
+int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t len, char *out, int64_t cap,
+                             int64_t *used) {
   CTX_GUARD(ctx);
-  if ((file != 0 && file != 1) || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  if ((file != 0 && file != 1) || !used || offset < 0 || len < 0) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   MH_TRY(sync_async_fill(ctx));
   HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the writers of the arena's last units
   const int64_t n = file ? ctx->used2 : ctx->used1;
-  const uint8_t *src = (const uint8_t *)(file ? ctx->out2.p : ctx->out1.p);
+  if (offset > n || len > n - offset) return arg_fail(ctx, MH_E_ARG, "range outside the arena");
+  const uint8_t *src = (const uint8_t *)(file ? ctx->out2.p : ctx->out1.p) + offset;
   *used = 0;
-  if (n == 0) return MH_OK;
-  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(n)));
+  if (len == 0) return MH_OK;
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(len)));
   int64_t u = 0;
-  MH_TRY(bgzf_device(ctx, ctx->stream, src, n, (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &u));
+  MH_TRY(bgzf_device(ctx, ctx->stream, src, len, (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &u));
   *used = u;
   if (!out) return MH_OK;   // (the size only)
   if (u > cap) return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
+}
+
+int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used) {
+  CTX_GUARD(ctx);
+  if ((file != 0 && file != 1) || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  MH_TRY(sync_async_fill(ctx));
+  return mh_output_bgzf_range(ctx, file, 0, file ? ctx->used2 : ctx->used1, out, cap, used);
 }

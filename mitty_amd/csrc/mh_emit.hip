@@ -1425,9 +1425,11 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       gate_open_for(ctx, es.done_gate);
       HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
     }
-    MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
-    MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)ntiles));
-    MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)ntiles));
+    if (m > ctx->eset_max_m) ctx->eset_max_m = m;
+    const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
+    MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
+    MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
+    MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
     if (!direct) MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
     if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));   // 8 bytes per record
     MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(direct ? ntiles : m + 1)));
@@ -1853,9 +1855,11 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
   EmitSet &es = ctx->eset[set];
   const int64_t ntiles = (m + ED_T - 1) / ED_T;
-  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * m));
-  MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)ntiles));
-  MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)ntiles));
+  if (m > ctx->eset_max_m) ctx->eset_max_m = m;
+  const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
+  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
+  MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
+  MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
   MH_TRY(ensure(ctx, ctx->scan_partials_w, scan_lb_scratch_bytes<E3>(ntiles)));
   MH_TRY(ensure(ctx, es.stat, 64));
   if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));

@@ -177,8 +177,12 @@ struct mh_ctx {
   int32_t writers_in_job = 0;
   static constexpr int N_USORT = 4;   // units of a batch sorted before any is chased (per unit: ts, keys, values, heads)
   mh::DevBuf usort[N_USORT][4];
-  static constexpr int N_ESET = 4;   // emission buffer sets in flight (a job's units; the next job's sampling overlaps)
+  // emission buffer sets in flight: a unit's measure pass refills the set the writer N_ESET units back read, so with
+  // fewer sets than a batch's units the host (waiting for each unit's measure totals) is held until the batch's
+  // writers are nearly done and the next batch's sampling cannot start beside them
+  static constexpr int N_ESET = 16;
   mh::EmitSet eset[N_ESET];
+  int64_t eset_max_m = 0;   // the most templates a unit had: every set is sized for it (no growth, no drain, later)
   int eset_i = 0;
   hipStream_t stage_stream = nullptr;   // stream the stage timing events go to (nullptr: stream)
   std::string err;

@@ -1518,19 +1518,19 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
   int32_t last[4] = {-1, -1, -1, -1};
   for (int32_t u = 0, k = 0; u < n_units; u++)
     if (plan[u].n > 0) last[k++ % n_lanes] = u;
+  // the batch-wide permutation (default; MH_PERM_UNIT=1: one sort per unit).  With the writer gate the batch's one
+  // sort releases the previous job's gated writers (they wait until it has run alone on the chip)
+  static const bool perm_unit = getenv("MH_PERM_UNIT") && atoi(getenv("MH_PERM_UNIT"));
+  const bool batch = !perm_unit && rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) && n_units <= PK_UNITS;
   // Up to four units (two per lane): every unit's sort first, then the rest, each unit with its own sort buffers, so
   // the gate opens after the sorts alone.  More units: unit after unit.
-  const bool split = ctx->gate && n_units <= mh_ctx::N_USORT;
+  const bool split = ctx->gate && !batch && n_units <= mh_ctx::N_USORT;
   if (split)
     for (int32_t u = 0; u < n_units; u++) {
       const int64_t nu = plan[u].n + 1;
       MH_TRY(ensure(ctx, ctx->usort[u][0], 8 * (size_t)nu));
       for (int b = 1; b < 4; b++) MH_TRY(ensure(ctx, ctx->usort[u][b], 4 * (size_t)nu + 16));
     }
-  // the batch-wide permutation (default; MH_PERM_UNIT=1 or the writer gate: one sort per unit)
-  static const bool perm_unit = getenv("MH_PERM_UNIT") && atoi(getenv("MH_PERM_UNIT"));
-  const bool batch = !ctx->gate && !perm_unit && rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) &&
-                     n_units <= PK_UNITS;
   if (batch) {
     MH_TRY(ensure(ctx, ctx->pb[0], 8 * (size_t)j_total + 64));
     MH_TRY(ensure(ctx, ctx->pb[1], 8 * (size_t)j_total + 64));
@@ -1576,6 +1576,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     HIPCHK(ctx, perm_sort(ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
+    MH_TRY(gate_release(ctx, st, ctx->job));   // the previous job's gated writers may go
     hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)bp.ts, bp.tsh);
     HIPCHK(ctx, hipGetLastError());

@@ -148,6 +148,67 @@ def write_pair(sinks, datas, raw_lens=None):
     raise errs[0]
 
 
+class PairWriter:
+  """Queued writes to the FASTQ sinks, one thread per file (a reader taking the two files in lockstep never leaves
+  us blocked on one pipe while it waits on the other).  submit(slot, datas) returns at once; wait(slot) blocks until
+  every write handed in with that staging slot is done, so its page-locked buffers can be refilled; close() drains.
+  A write error is raised by the next wait() or close()."""
+
+  def __init__(self, sinks):
+    import queue
+    import threading
+    self.sinks = sinks
+    self.q = [queue.Queue() if s is not None else None for s in sinks]
+    self.errs = []
+    self.pending = {}
+    self.ts = [threading.Thread(target=self._run, args=(f,), daemon=True) for f in range(len(sinks))
+               if sinks[f] is not None]
+    for t in self.ts:
+      t.start()
+
+  def _run(self, f):
+    while True:
+      item = self.q[f].get()
+      if item is None:
+        return
+      data, raw, ev = item
+      try:
+        if raw is None:
+          self.sinks[f].write(data)
+        else:
+          self.sinks[f].write_bgzf(data, raw)
+      except BaseException as e:   # (reported by the caller's next wait / close)
+        self.errs.append(e)
+      finally:
+        ev.set()
+
+  def submit(self, slot, datas, raw_lens=None):
+    import threading
+    raw_lens = raw_lens or [None] * len(datas)
+    for f, (s, d, r) in enumerate(zip(self.sinks, datas, raw_lens)):
+      if s is None or d is None:
+        continue
+      ev = threading.Event()
+      self.pending.setdefault(slot, []).append(ev)
+      self.q[f].put((d, r, ev))
+
+  def wait(self, slot):
+    for ev in self.pending.pop(slot, []):
+      ev.wait()
+    if self.errs:
+      raise self.errs[0]
+
+  def close(self):
+    for q in self.q:
+      if q is not None:
+        q.put(None)
+    for t in self.ts:
+      t.join()
+    self.pending.clear()
+    if self.errs:
+      raise self.errs[0]
+
+
 class FastqSink:
   """Sequential FASTQ output (works with FIFOs / process substitution, examples/reads/run.sh:13-16).  A name ending
   in '.gz' gets BGZF (gzip-compatible) output, deflated on a host thread pool."""

@@ -16,7 +16,7 @@ from mitty_amd import _native
 from mitty_amd.engine import Engine
 from mitty_amd.lib import fasta as mfasta
 from mitty_amd.lib import vcfio
-from mitty_amd.lib.fastq_stream import FastqSink, write_pair
+from mitty_amd.lib.fastq_stream import FastqSink, PairWriter
 
 logger = logging.getLogger(__name__)
 
@@ -75,7 +75,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it; gz_device: deflated on
   the GPU (mh_output_bgzf) straight from the arenas, else on gz_threads host threads at gz_level.  Returns a stats
   dict (templates sampled, kept, bytes, seconds; setup_s = inputs parsed and loaded, fetch_s = waiting for the GPU
-  and its D2H (deflate included), write_s = file writes).
+  and its D2H (deflate included), write_s = waiting for the file writes to free a staging slot).
   """
   t0 = time.time()
   read_model = read_module.read_model_params(model, coverage)
@@ -96,7 +96,15 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   fp1 = FastqSink(fastq1_fname, gz_level, gz_threads, compress)   # '.gz' names get BGZF output
   fp2 = FastqSink(fastq2_fname, gz_level, gz_threads, compress) if write2 else None
 
-  pins = [_native.PinnedBuffer(), _native.PinnedBuffer()]   # page-locked D2H staging, one per file
+  # page-locked D2H staging: two slots (double buffering) of one buffer per file; each file is written on its own
+  # thread (PairWriter), so a FIFO reader that takes the two files in lockstep (examples/reads/run.sh:13-16) is never
+  # starved of one while we block on the other, and the next chunk's D2H overlaps the writes of this one
+  sinks = [fp1, fp2 if write2 else None]
+  pw = PairWriter(sinks)
+  pins = [[_native.PinnedBuffer(), _native.PinnedBuffer()] for _ in range(2)]
+  nslot = [0]
+  CHUNK = 256 << 20
+  GZ_CHUNK = 4096 * 0xff00   # whole BGZF blocks: the members equal one compression of the whole arena
 
   def flush(ps, n, kept, b1, b2):
     stats['templates'] += n
@@ -105,21 +113,32 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     stats['bytes2'] += b2
     u1, u2 = eng.ctx.output_size()
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
-      # both arenas to page-locked memory, then each file written on its own thread: a FIFO reader that takes the
-      # two files in lockstep (examples/reads/run.sh:13-16) is never starved of one while we block on the other
-      sinks = [fp1, fp2 if write2 else None]
-      tf = time.time()
       if gz_device and all(s is None or s.gz for s in sinks):
-        raw = eng.ctx.output_size()
-        z1, z2 = eng.ctx.output_bgzf_pinned(pins)
-        tw = time.time()
-        write_pair(sinks, [z1, z2], list(raw))
+        # BGZF members deflated on the GPU from the arenas (chunks of whole 0xff00-byte blocks), then D2H of the
+        # compressed bytes only
+        for off in range(0, max(u1, u2), GZ_CHUNK):
+          slot = nslot[0] % 2
+          nslot[0] += 1
+          tw = time.time()
+          pw.wait(slot)
+          tf = time.time()
+          n1, n2 = max(0, min(GZ_CHUNK, u1 - off)), max(0, min(GZ_CHUNK, u2 - off))
+          z1, z2 = eng.ctx.output_bgzf_range_pinned(pins[slot], off, n1, n2)
+          stats['write_s'] += tf - tw
+          stats['fetch_s'] += time.time() - tf
+          pw.submit(slot, [z1 if n1 else None, z2 if n2 else None], [n1, n2])
       else:
-        d1, d2 = eng.ctx.fetch_output_pinned(pins)
-        tw = time.time()
-        write_pair(sinks, [d1, d2])
-      stats['fetch_s'] += tw - tf
-      stats['write_s'] += time.time() - tw
+        for off in range(0, max(u1, u2), CHUNK):
+          slot = nslot[0] % 2
+          nslot[0] += 1
+          tw = time.time()
+          pw.wait(slot)   # the writes of this slot's previous chunk
+          tf = time.time()
+          n1, n2 = max(0, min(CHUNK, u1 - off)), max(0, min(CHUNK, u2 - off))
+          d1, d2 = eng.ctx.fetch_range_pinned(pins[slot], off, n1, off, n2)
+          stats['write_s'] += tf - tw
+          stats['fetch_s'] += time.time() - tf
+          pw.submit(slot, [d1 if n1 else None, d2 if n2 else None])
       eng.ctx.reset_output()
 
   try:
@@ -137,12 +156,18 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
         logger.debug('Units {}..{}: {:0.3f}s'.format(batch[0][0], batch[-1][0], time.time() - t1))
         batch, batch_draws = [], 0
   finally:
-    fp1.close()
-    if fp2:
-      fp2.close()
-    eng.close()
-    for b in pins:
-      b.free()
+    try:
+      tw = time.time()
+      pw.close()
+      stats['write_s'] += time.time() - tw
+    finally:
+      fp1.close()
+      if fp2:
+        fp2.close()
+      eng.close()
+      for slot in pins:
+        for b in slot:
+          b.free()
   stats['written1'], stats['written2'] = fp1.written, fp2.written if fp2 else 0
   stats['seconds'] = time.time() - t0
   return stats

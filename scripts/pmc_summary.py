@@ -6,7 +6,8 @@ separate passes; on gfx950 FETCH_SIZE counts half the bytes of wide (16 B/lane) 
 The doubling is calibrated for the writer's own pattern too — 16-byte gathers of 150-byte windows at random
 offsets read 1.97 x FETCH_SIZE bytes of distinct 128-byte lines (profiles/calib_fetch_size_r03.json,
 scripts/calib_fetch.hip).  WRITE_SIZE is exact for 16-byte stores.
-usage: pmc_summary.py <pmc dir> <tag> <kernel> <round> <rlen> <length> [algorithmic bytes per launch]
+usage: pmc_summary.py <pmc dir> <tag> <kernel> <round> <rlen> <length> [algorithmic bytes per launch] [workload]
+(workload: the bench workload the passes ran, 'chr1' or 'wgs'; bench.py takes traffic only from a matching file)
 """
 import csv
 import json
@@ -24,8 +25,10 @@ def per_dispatch(path, name):
 
 def main():
   d, tag, kernel, rnd, rlen, length = sys.argv[1:7]
-  alg = float(sys.argv[7]) if len(sys.argv) > 7 else None
+  alg = float(sys.argv[7]) if len(sys.argv) > 7 and sys.argv[7] != '-' else None
   out = {'kernel': kernel, 'rlen': int(rlen), 'length': int(length)}
+  if len(sys.argv) > 8:
+    out['workload'] = sys.argv[8]
   counters = {}
   for i in range(1, 6):
     p = os.path.join(d, '{}_{}'.format(tag, i), 'run_counter_collection.csv')

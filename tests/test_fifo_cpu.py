@@ -182,3 +182,54 @@ def test_write_pair_to_lockstep_fifo_reader(tmp_path):
   s2.close()
   t.join()
   assert b''.join(got[0]) == d1 and b''.join(got[1]) == d2
+
+
+def test_pair_writer_chunks_in_order_to_lockstep_fifo_reader(tmp_path):
+  """generate-reads' output side: chunks of both files handed to a PairWriter through two alternating staging slots
+  (the slot is waited on before it is refilled, as readgenerate.process_multi_threaded does around its D2H copies),
+  each FIFO drained by its own reader; file 2 shorter (fewer chunks)."""
+  r1, r2 = _records(120000, b'/1'), _records(90000, b'/2')
+  d1, d2 = b''.join(r1), b''.join(r2)
+  f1, f2 = str(tmp_path / 'o1'), str(tmp_path / 'o2')
+  os.mkfifo(f1)
+  os.mkfifo(f2)
+  got = ([], [])
+
+  def reader(path, out):
+    with open(path, 'rb') as a:
+      out.append(a.read())
+  ts = [threading.Thread(target=reader, args=(f, g), daemon=True) for f, g in zip((f1, f2), got)]
+  for t in ts:
+    t.start()
+  s1, s2 = FS.FastqSink(f1), FS.FastqSink(f2)
+  pw = FS.PairWriter([s1, s2])
+  bufs = [[None, None], [None, None]]
+  CH = 1 << 20
+  for k, off in enumerate(range(0, max(len(d1), len(d2)), CH)):
+    slot = k % 2
+    pw.wait(slot)
+    bufs[slot] = [bytearray(d1[off:off + CH]), bytearray(d2[off:off + CH])]   # a refilled staging slot
+    pw.submit(slot, [bytes(b) if b else None for b in bufs[slot]])
+  pw.close()
+  s1.close()
+  s2.close()
+  for t in ts:
+    t.join()
+  assert got[0][0] == d1 and got[1][0] == d2
+
+
+def test_pair_writer_reports_a_write_error(tmp_path):
+  class Broken:
+    gz = False
+
+    def write(self, data):
+      raise BrokenPipeError('reader went away')
+  ok = FS.FastqSink(str(tmp_path / 'ok'))
+  pw = FS.PairWriter([ok, Broken()])
+  pw.submit(0, [b'@r\nA\n+\n~\n', b'@r\nC\n+\n~\n'])
+  with pytest.raises(BrokenPipeError):
+    pw.wait(0)
+  with pytest.raises(BrokenPipeError):
+    pw.close()
+  ok.close()
+  assert open(str(tmp_path / 'ok'), 'rb').read() == b'@r\nA\n+\n~\n'

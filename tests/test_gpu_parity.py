@@ -1466,3 +1466,37 @@ def test_device_bgzf_round_trip(ctx, name):
 
 def test_device_bgzf_empty(ctx):
   assert ctx.bgzf_compress(b'') == b''
+
+
+def test_device_bgzf_arena_ranges_equal_whole_arena(native):
+  """generate-reads' chunked '.gz' path: ranges of the FASTQ arenas at multiples of 0xff00 deflated on the GPU
+  (mh_output_bgzf_range) concatenate to the members of one call over the whole arena (mh_output_bgzf), which inflate
+  to the arena's FASTQ."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(mdl['mean_rlen'], 30.0)
+  seq = synth.contig(3_000_000, 5)
+  copies = synth.copies_soa(synth.variants(seq, 6), 0, len(seq))
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('7', 0, len(seq)), seq)
+    eng.ctx.reset_output()
+    eng.run_unit(0, 0, 0, 99, copies[0], p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')
+    d1, d2 = eng.ctx.fetch_output()
+    u1, u2 = eng.ctx.output_size()
+    whole = [_native.PinnedBuffer(), _native.PinnedBuffer()]
+    w1, w2 = (bytes(v) for v in eng.ctx.output_bgzf_pinned(whole))
+    part = [_native.PinnedBuffer(), _native.PinnedBuffer()]
+    CH = 7 * 0xff00
+    z1, z2 = b'', b''
+    for off in range(0, max(u1, u2), CH):
+      a, b = eng.ctx.output_bgzf_range_pinned(part, off, max(0, min(CH, u1 - off)), max(0, min(CH, u2 - off)))
+      z1, z2 = z1 + bytes(a), z2 + bytes(b)
+    assert z1 == w1 and z2 == w2
+    eof = _native.bgzf_eof()
+    assert gzip.decompress(z1 + eof) == d1 and gzip.decompress(z2 + eof) == d2
+    with pytest.raises(ValueError):
+      eng.ctx.output_bgzf_range_pinned(part, u1 - 10, 20, 0)   # past the arena
+  finally:
+    eng.close()
