@@ -79,6 +79,12 @@ def parse():
   ap.add_argument('--batch-ramp', type=int, default=0,
                   help='wgs: the first K batches of a step are 2^-K, 2^-(K-1), .. of --batch-draws (the first writer '
                        'starts after a small batch is sampled, not a full one)')
+  ap.add_argument('--min-batches', type=int, default=4,
+                  help='wgs: at least this many batches per rank and step (a rank\'s share at N = 8 is ~1/8 of the '
+                       'genome: smaller batches keep its sampling beside its writers)')
+  ap.add_argument('--plan-share', default=None, metavar='R/N',
+                  help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
+                       'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
   ap.add_argument('--pipeline', default='batch', choices=['batch', 'phased', 'phased-sync'],
                   help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
@@ -104,15 +110,16 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
   traffic = None   # measured in separate rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE), see profiles/pmc_*.json
   pmc = sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_{}_*.json'.format(kernel))))
   traffic_src = None
-  if pmc and workload:
+  for path in reversed(pmc if workload else []):   # the latest summary of this workload
     try:
-      with open(pmc[-1]) as fp:
+      with open(path) as fp:
         d = json.load(fp)
-      if d.get('rlen') == rlen and d.get('workload', 'chr1' if d.get('length') == CHR1 else None) == workload:
-        traffic = d.get('hbm_bytes_per_launch')
-        traffic_src = os.path.relpath(pmc[-1], REPO)
     except Exception:
-      traffic = None
+      continue
+    if d.get('rlen') == rlen and d.get('workload', 'chr1' if d.get('length') == CHR1 else None) == workload:
+      traffic = d.get('hbm_bytes_per_launch')
+      traffic_src = os.path.relpath(path, REPO)
+      break
   stage_ms = {k: round(v[0] / steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])}
   return {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
           'frac': (achieved / PEAK_HBM_GBS) if achieved else None, 'traffic': traffic,
@@ -432,8 +439,13 @@ def run_genome(a, rank, world, local):
   contigs = synth.genome_contigs(a.genome_scale)
   units = _native.work_units(a.seed, [2] * len(contigs), passes)     # (region, copy, seed), reference order
   weights = [contigs[ri][1] for ri, _, _ in units]
-  pieces = D.plan_pieces(weights, world, 'lpt')                       # 100 units: whole units by LPT at any N
-  mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == rank]
+  plan_world, plan_rank = world, rank
+  if a.plan_share:   # projection: one rank's share of an N-rank plan, timed alone on this GPU
+    plan_rank, plan_world = (int(x) for x in a.plan_share.split('/'))
+    if world != 1 or not 0 <= plan_rank < plan_world:
+      sys.exit('bench.py: --plan-share R/N runs in one process (0 <= R < N)')
+  pieces = D.plan_pieces(weights, plan_world, 'lpt')                  # 100 units: whole units by LPT at any N
+  mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == plan_rank]
   regions = sorted({ri for _, ri, _, _ in mine})
   t_synth = time.perf_counter()
   data = synth.genome_regions(contigs, regions, workers=max(1, a.synth_workers // world))
@@ -462,10 +474,14 @@ def run_genome(a, rank, world, local):
   eng.ctx.set_emit_mode(a.emit_mode)
   kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
   batches, cur, draws = [], [], 0
-  for u in mine:   # batches of about --batch-draws template draws (the first --batch-ramp ones smaller), in ps order
+  # batches of about --batch-draws template draws (the first --batch-ramp ones smaller), in ps order; at least
+  # --min-batches per rank, so a rank's sampling of one batch runs beside its writers of the previous one
+  mine_draws = sum(int(contigs[u[1]][1] * p * 1.2) for u in mine)
+  batch_draws = min(a.batch_draws, mine_draws / max(1, a.min_batches))
+  for u in mine:
     cur.append(u)
     draws += int(contigs[u[1]][1] * p * 1.2)
-    if draws >= a.batch_draws / 2 ** max(0, a.batch_ramp - len(batches)):
+    if draws >= batch_draws / 2 ** max(0, a.batch_ramp - len(batches)):
       batches.append(cur)
       cur, draws = [], 0
   if cur:
@@ -542,7 +558,7 @@ def run_genome(a, rank, world, local):
   workload = 'wgs' if a.genome_scale == 1 else None
   roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload)
   cpu = e2e = None
-  if world == 1:
+  if world == 1 and not a.plan_share:
     seq1, recs1, _ = data[0]
     if not a.no_e2e and a.genome_scale == 1 and a.rng == 'mitty':
       e2e = end_to_end(a, seq1, recs1, model, None)
@@ -574,7 +590,7 @@ def run_genome(a, rank, world, local):
                            'genome)'.format('' if a.genome_scale == 1 else ' (lengths x{})'.format(a.genome_scale),
                                             a.model, rlen, a.coverage, a.rng, world),
                'genome_bp': sum(L for _, L in contigs), 'read_model': a.model, 'coverage': a.coverage,
-               'units': n_units, 'batches_rank0': len(batches), 'batch_draws': a.batch_draws,
+               'units': n_units, 'batches_rank0': len(batches), 'batch_draws': batch_draws,
                'batch_ramp': a.batch_ramp, 'pipeline': a.pipeline,
                'templates_per_step': kept_all // steps,
                'parallelism': 'unit-shard (LPT) x{}'.format(world) if world > 1 else 'single GPU',
@@ -588,6 +604,10 @@ def run_genome(a, rank, world, local):
     'setup_s': {'synth_inputs': round(t_synth, 2)},
     'host_cpus': os.cpu_count(),
   }
+  if a.plan_share:   # not the metric line: one rank's share of an N-rank plan, timed alone
+    out['metric'] = 'projection: one rank of an N-GPU run of [' + METRIC + ']'
+    out['projection'] = {'plan_rank': plan_rank, 'plan_world': plan_world, 'units': len(mine),
+                         'draws': mine_draws}
   print(json.dumps(out), flush=True)
 
 

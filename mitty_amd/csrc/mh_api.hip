@@ -41,7 +41,7 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
   if (b.cap >= bytes) return MH_OK;
   if (b.p) {
     gate_open(ctx);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // a queued FASTQ writer may still read or write it
+    MH_TRY(sync_writers(ctx));   // a queued FASTQ writer (or corruption pass) may still read or write it
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     lb_forget(b.p);
     HIPCHK(ctx, hipFree(b.p));
@@ -64,7 +64,7 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
   DevBuf nb;
   MH_TRY(ensure(ctx, nb, bytes + bytes / 2));
   gate_open(ctx);
-  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the old buffer's queued writers finish first
+  MH_TRY(sync_writers(ctx));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   lb_forget(b.p);
@@ -131,6 +131,14 @@ int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
   if (gate_debug()) fprintf(stderr, "mh gate: release %u\n", value);
   HIPCHK(ctx, hipStreamWriteValue32(st, ctx->gate, value, 0));
   ctx->gate_written = value;
+  return MH_OK;
+}
+
+int32_t sync_writers(mh_ctx *ctx) {
+  gate_open(ctx);
+  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+  if (ctx->crstream) HIPCHK(ctx, hipStreamSynchronize(ctx->crstream));
+  ctx->cr_pending = false;
   return MH_OK;
 }
 
@@ -308,6 +316,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   gate_open(ctx);
   (void)hipStreamSynchronize(ctx->wstream);
+  if (ctx->crstream) (void)hipStreamSynchronize(ctx->crstream);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   for (auto x : ctx->xstream)
@@ -350,6 +359,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipEventDestroy(ctx->ev_ready);
   (void)hipEventDestroy(ctx->ev_writer);
   (void)hipStreamDestroy(ctx->wstream);
+  if (ctx->crstream) (void)hipStreamDestroy(ctx->crstream);
+  if (ctx->ev_crw) (void)hipEventDestroy(ctx->ev_crw);
   bam_release(ctx->bam);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -619,7 +630,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
     ctx->hap_spare.push_back(h);
   } else {
     gate_open(ctx);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+    MH_TRY(sync_writers(ctx));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     release_hap(h);
   }
@@ -1216,7 +1227,7 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
   CTX_GUARD(ctx);
   if ((file != 0 && file != 1) || !used || offset < 0 || len < 0) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   MH_TRY(sync_async_fill(ctx));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));   // the writers of the arena's last units
+  MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
   const int64_t n = file ? ctx->used2 : ctx->used1;
   if (offset > n || len > n - offset) return arg_fail(ctx, MH_E_ARG, "range outside the arena");
   const uint8_t *src = (const uint8_t *)(file ? ctx->out2.p : ctx->out1.p) + offset;

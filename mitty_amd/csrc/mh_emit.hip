@@ -1215,6 +1215,13 @@ __global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A)
   }
 }
 
+// MH_CR_OVERLAP=1: the direct writer's corruption passes run on their own stream beside the next units' writers
+// (one 1024-thread workgroup per CU, so the writers' workgroups fit beside it) instead of after every writer
+static bool cr_overlap() {
+  static const bool v = getenv("MH_CR_OVERLAP") && atoi(getenv("MH_CR_OVERLAP"));
+  return v;
+}
+
 // the corruption pass over one emission's records (on stream `st`, after its writer)
 int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_t m, const int64_t *pos0,
                           const int64_t *pos1, const int8_t *fo0, const Rec *recs, const E3 *off, uint2 *crec,
@@ -1231,7 +1238,9 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
-  const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
+  int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
+  if (cr_overlap()) per_cu = 1;                           // room for the writers beside it
+  if (getenv("MH_CR_PER_CU")) per_cu = std::max(1, atoi(getenv("MH_CR_PER_CU")));
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
   if (grid < 1) grid = 1;
   if (pf) grid = (grid + 1) & ~(int64_t)1;   // even: workgroup pairs (file 0, file 1)
@@ -1510,8 +1519,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   size_t lds = ((sizeof(TplMeta) * EW_T + 15) / 16) * 16 + (size_t)EW_T * 2 * win_stride + 2 * (size_t)(cap + 16);
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on && es.crrec.cap < 16 * (size_t)m + 64) {   // corruption switched on after this unit's measure
-    gate_open(ctx);
-    HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+    MH_TRY(sync_writers(ctx));
     MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
   }
   if (ctx->corrupt_on) {
@@ -1567,15 +1575,29 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
-    if (ctx->corrupt_on)
-      MH_TRY(launch_cr_inplace(ctx, ctx->wstream, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p,
+    hipStream_t tail = ctx->wstream;   // the stream whose last work is this unit's last
+    if (ctx->corrupt_on) {
+      if (cr_overlap()) {   // the corruption pass on its own stream, beside the next units' writers
+        if (!ctx->crstream) {
+          HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->crstream, hipStreamNonBlocking));
+          HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_crw, hipEventDisableTiming));
+        }
+        HIPCHK(ctx, hipEventRecord(ctx->ev_crw, ctx->wstream));
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->crstream, ctx->ev_crw, 0));
+        tail = ctx->crstream;
+        ctx->stage_stream = tail;
+        ctx->cr_pending = true;
+      }
+      MH_TRY(launch_cr_inplace(ctx, tail, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p,
                                (char *)ctx->out1.p, (char *)ctx->out2.p, write_fastq2 ? 2 : 1,
                                (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc, nullptr, true));
+      ctx->stage_stream = ctx->wstream;
+    }
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
-    HIPCHK(ctx, hipEventRecord(es.done, ctx->wstream));
+    HIPCHK(ctx, hipEventRecord(es.done, tail));
     es.done_gate = ctx->gate_waited;
-    HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ctx->wstream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev_writer, tail));
     MH_TRY(mark_used(ctx, h.used, h.used_set, h.used_gate));     // the haplotype and the templates stay live until then
     MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
     es.busy = true;
@@ -1736,6 +1758,10 @@ int32_t sync_async_fill(mh_ctx *ctx) {
 int32_t output_reset(mh_ctx *ctx) {
   ctx->used1 = ctx->used2 = 0;
   ctx->res1 = ctx->res2 = 0;
+  if (ctx->cr_pending) {   // the next writers overwrite the arenas: after the queued corruption passes
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_writer, 0));
+    ctx->cr_pending = false;
+  }
   if (ctx->async_pending) {
     hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, (int64_t)0,
                        (int64_t)0);

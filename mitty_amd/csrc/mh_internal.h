@@ -160,6 +160,11 @@ struct mh_ctx {
   // FASTQ writer stream: mh_emit_reads returns once its writer is queued here; every other entry point first makes
   // the main stream wait for the last queued writer (ev_writer)
   hipStream_t wstream = nullptr;
+  // corruption stream (MH_CR_OVERLAP): each unit's k_cr_inplace waits for its writer (ev_crw) and runs beside the next
+  // units' writers; ev_writer is then recorded after the corruption pass, and writers into a reset arena wait for it
+  hipStream_t crstream = nullptr;
+  hipEvent_t ev_crw = nullptr;
+  bool cr_pending = false;
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
   // Writer gate.  The permutation's radix sort cannot run beside a FASTQ writer (its workgroups need a whole CU and
@@ -325,6 +330,7 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)
 int32_t sync_async_fill(mh_ctx *ctx);
+int32_t sync_writers(mh_ctx *ctx);   // the writer stream and the corruption stream drained (host wait)
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
                     int64_t *used);            // BGZF blocks of a device buffer (no EOF marker), mh_deflate.hip
 int64_t bgzf_device_bound(int64_t n);

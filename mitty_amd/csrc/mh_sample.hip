@@ -1550,7 +1550,11 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_xjoin[l - 2], 0));
       }
     }
-    // 2. one sort of every unit's (target, step), heads, chase (main stream)
+    // 2. one sort of every unit's (target, step), heads, chase (main stream).  MH_SORT_WAIT=1 (A/B): the sort starts
+    // only once the FASTQ writers queued so far have drained (its 1024-thread workgroups otherwise start one by one
+    // between writer workgroups, and the early ones hold their CUs spinning on the look-back)
+    static const bool sort_wait = getenv("MH_SORT_WAIT") && atoi(getenv("MH_SORT_WAIT"));
+    if (sort_wait && ctx->writer_pending) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_writer, 0));
     stage_begin(ctx, "sample_permutation");
     std::vector<int64_t> uo(n_units), un(n_units);
     for (int32_t u = 0; u < n_units; u++) {
