@@ -1339,6 +1339,12 @@ static int ew_dbg_env() {
   static const int v = getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0;
   return v;
 }
+// qname rows: a multiple of 16 bytes plus 4 (an odd number of dwords), so wave 0's lanes (one qname row per template)
+// writing the same column land on 32 different LDS banks instead of 8 (MH_EW_QPAD: A/B, 0 = the old multiple of 16)
+static int32_t ed_qpad() {
+  static const int v = getenv("MH_EW_QPAD") ? atoi(getenv("MH_EW_QPAD")) : 4;
+  return v;
+}
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf) {
   const bool staged = !(ew_dbg_env() & 256);   // (256: seam chunks stored by the seam pass, no LDS for them)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
@@ -1537,7 +1543,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
-  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32;
+  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ed_qpad();
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
@@ -1821,7 +1827,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
                 win_stride <= 16 * 3 * ED_GMAX && m < (int64_t)UINT32_MAX && m > 0 && !getenv("MH_EMIT_SYNC");
   if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
-  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32;
+  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ed_qpad();
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");

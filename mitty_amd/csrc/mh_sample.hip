@@ -1224,12 +1224,35 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // The permutation's (target, step) sort: rocprim's LSD onesweep radix sort.  (Its gfx950 tuning runs 1024-thread
 // sort workgroups, which find no room on a CU beside the FASTQ writers and wait for them to drain; 256-thread onesweep
 // workgroups that do fit beside them made the steps slower — WGS 1.18 vs 1.37 G/s, chr1 1.30 vs 1.50 — so the
-// default tuning stays.)
+// default tuning stays.)  9 key bits per onesweep pass instead of the tuning's 8, the same workgroups: a 64 M-draw
+// batch's 27-bit keys in 3 passes instead of 4 (WGS 1.591 vs 1.576 G/s, two alternations; 10 bits 1.577, 11 bits
+// 1.569).  MH_SORT_BITS = 8 / 10 / 11: A/B.
+template <unsigned B>
+using SortBitsCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, B,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+static int sort_bits() {
+  static const int v = getenv("MH_SORT_BITS") ? atoi(getenv("MH_SORT_BITS")) : 9;
+  return v;
+}
 template <class KIn>
 static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
                             size_t n, unsigned end_bit, hipStream_t st) {
   const rocprim::counting_iterator<uint32_t> iota(0u);
-  return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
+  switch (sort_bits()) {
+    case 9:
+      return rocprim::radix_sort_pairs<SortBitsCfg<9>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
+                                                       end_bit, st);
+    case 10:
+      return rocprim::radix_sort_pairs<SortBitsCfg<10>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
+                                                        end_bit, st);
+    case 11:
+      return rocprim::radix_sort_pairs<SortBitsCfg<11>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
+                                                        end_bit, st);
+    default:
+      return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
+  }
 }
 
 struct BatchPerm {
