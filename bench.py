@@ -421,6 +421,25 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     os.rmdir(d)
 
 
+def plan_batches(mine, draws_of_region, target, min_batches=1, ramp=0):
+  """A rank's units [(ps, ri, cpy, seed)] in batches of about `target` template draws (draws_of_region[ri] per
+  unit), in ps order; at least `min_batches` batches when the rank has that many units (so its sampling of one batch
+  runs beside its writers of the previous one); the first `ramp` batches 2^-ramp, 2^-(ramp-1), .. of the size.
+  Returns (batches, the batch size used, the rank's draws)."""
+  total = sum(int(draws_of_region[u[1]]) for u in mine)
+  size = min(target, total / max(1, min_batches))
+  batches, cur, draws = [], [], 0
+  for u in mine:
+    cur.append(u)
+    draws += int(draws_of_region[u[1]])
+    if draws >= size / 2 ** max(0, ramp - len(batches)):
+      batches.append(cur)
+      cur, draws = [], 0
+  if cur:
+    batches.append(cur)
+  return batches, size, total
+
+
 def run_genome(a, rank, world, local):
   """The metric's workload at any N: whole synthetic GRCh37, the reference's unit list dealt to the ranks by LPT
   (mitty_amd.distributed.plan_pieces), every unit sampled and emitted by its owner, output in HBM (arenas recycled
@@ -473,19 +492,8 @@ def run_genome(a, rank, world, local):
       eng.upload_variants(ri, cpy, copies[ri][cpy])
   eng.ctx.set_emit_mode(a.emit_mode)
   kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
-  batches, cur, draws = [], [], 0
-  # batches of about --batch-draws template draws (the first --batch-ramp ones smaller), in ps order; at least
-  # --min-batches per rank, so a rank's sampling of one batch runs beside its writers of the previous one
-  mine_draws = sum(int(contigs[u[1]][1] * p * 1.2) for u in mine)
-  batch_draws = min(a.batch_draws, mine_draws / max(1, a.min_batches))
-  for u in mine:
-    cur.append(u)
-    draws += int(contigs[u[1]][1] * p * 1.2)
-    if draws >= batch_draws / 2 ** max(0, a.batch_ramp - len(batches)):
-      batches.append(cur)
-      cur, draws = [], 0
-  if cur:
-    batches.append(cur)
+  batches, batch_draws, mine_draws = plan_batches(mine, [L * p * 1.2 for _, L in contigs], a.batch_draws,
+                                                  a.min_batches, a.batch_ramp)
   if dist is not None:
     import torch
     dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'

@@ -154,3 +154,21 @@ def test_wgs_plan_four_ranks(tmp_path):
     for u in units:
       assert hashlib.sha256(b[off:off + u[li]]).hexdigest() == u[hi], (f, u[:3])
       off += u[li]
+
+
+def test_bench_batch_plan():
+  """bench.py's WGS batches: every unit once, in ps order; about the target size; at least min_batches per rank
+  (a rank's share at N = 8 is ~1/8 of the genome); a ramp makes the first batches smaller."""
+  import bench
+  units = [(ps, ps % 5, ps % 2, 100 + ps) for ps in range(40)]
+  draws = [10.0, 20.0, 30.0, 40.0, 50.0]
+  for target, mb, ramp in ((100.0, 1, 0), (1e9, 4, 0), (100.0, 4, 2), (25.0, 1, 0)):
+    b, size, total = bench.plan_batches(units, draws, target, mb, ramp)
+    assert [u for x in b for u in x] == units
+    assert total == sum(draws[u[1]] for u in units)
+    assert size == min(target, total / mb)
+    assert len(b) >= min(mb, len(units))
+    for x in b[:-1]:   # every batch but the last reaches its size (the ramp's first ones a fraction of it)
+      assert sum(draws[u[1]] for u in x) >= size / 2 ** ramp
+  b, _, _ = bench.plan_batches(units, draws, 100.0, 1, 2)
+  assert sum(draws[u[1]] for u in b[0]) < sum(draws[u[1]] for u in b[2])
