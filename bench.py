@@ -86,10 +86,12 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
-  ap.add_argument('--pipeline', default='batch', choices=['batch', 'phased', 'phased-sync'],
+  ap.add_argument('--pipeline', default='batch', choices=['batch', 'lookahead', 'phased', 'phased-sync'],
                   help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
-                       'writers of batch k); phased = sample every unit of the step, then emit every unit '
-                       '(phased-sync: and the step starts after the previous step\'s writers)')
+                       'writers of batch k); lookahead = batch k+1\'s sampling up to its permutation sort queued '
+                       'before batch k\'s writers, which wait for that sort (MH_WRITER_GATE=0); phased = sample every '
+                       'unit of the step, then emit every unit (phased-sync: and the step starts after the previous '
+                       'step\'s writers)')
   ap.add_argument('--emit-chunk-bytes', type=float, default=24e9,
                   help='wgs phased: FASTQ arenas recycled after about this many bytes')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
@@ -482,6 +484,8 @@ def run_genome(a, rank, world, local):
     if dist.get_world_size() != world:
       sys.exit('bench.py: the process group has {} ranks, WORLD_SIZE={}'.format(dist.get_world_size(), world))
   from mitty_amd.engine import Engine
+  if a.pipeline == 'lookahead':
+    os.environ.setdefault('MH_WRITER_GATE', '0')   # read when the library context is created
   eng = Engine(local)
   copies = {}
   for ri in regions:
@@ -530,7 +534,19 @@ def run_genome(a, rank, world, local):
       dist.all_reduce(counts)
     return lambda: (kept, b1, b2)
 
+  def step_lookahead():
+    eng.drop_haplotypes()
+    res = eng.run_batches_lookahead(batches, soa_of, p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
+                                    on_batch=lambda k: eng.ctx.reset_output())
+    kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
+    if dist is not None:
+      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
+      dist.all_reduce(counts)
+    return lambda: (kept, b1, b2)
+
   def step():
+    if a.pipeline == 'lookahead':
+      return step_lookahead()
     if a.pipeline != 'batch':
       return step_phased()
     eng.drop_haplotypes()

@@ -120,6 +120,15 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
 int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
                         const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                         int32_t rng_mode, int64_t *out_n);
+/* The batched form in two halves, so the next batch's permutation sort can be queued ahead of this batch's FASTQ
+ * writers (the lookahead pipeline; readgenerate.py:102-115 runs units in worker processes instead): _begin queues
+ * the word streams, the decode, the geometric scans and the sort; _end queues the rest and returns out_n as
+ * mh_sample_units does.  One batch may be begun at a time; emissions may be queued in between (with the writer gate
+ * on, their writers then wait for the begun batch's sort). */
+int32_t mh_sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                              int32_t rng_mode);
+int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
 /* Make template set `tpl_id` the current one (used by mh_emit_reads / mh_get_templates). */
 int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id);
 int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id);

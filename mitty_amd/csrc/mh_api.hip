@@ -663,14 +663,14 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
   return MH_OK;
 }
 
-int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
-                        const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                        int32_t rng_mode, int64_t *out_n) {
-  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
+static int32_t unit_spans(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                          const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                          std::vector<int64_t> &pmin, std::vector<int64_t> &pmax) {
   if (n_units < 0 || (n_units > 0 && (!tpl_ids || !slots || !seeds)) || !cum_tlen || rlen <= 0 ||
       !(p > 0.0 && p <= 1.0))
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  std::vector<int64_t> pmin(n_units), pmax(n_units);
+  pmin.resize(n_units);
+  pmax.resize(n_units);
   for (int32_t u = 0; u < n_units; u++) {
     if (tpl_ids[u] < 0) return arg_fail(ctx, MH_E_ARG, "template set ids must be >= 0");
     for (int32_t v = 0; v < u; v++)
@@ -680,8 +680,32 @@ int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, co
     pmin[u] = it->second.p_min;
     pmax[u] = it->second.p_max;
   }
+  return MH_OK;
+}
+
+int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                        const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                        int32_t rng_mode, int64_t *out_n) {
+  CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
+  std::vector<int64_t> pmin, pmax;
+  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
   return sample_units(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen, rng_mode,
                       out_n);
+}
+
+int32_t mh_sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                              int32_t rng_mode) {
+  CTX_GUARD_NOJOIN(ctx);
+  std::vector<int64_t> pmin, pmax;
+  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
+  return sample_units_begin(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen,
+                            rng_mode);
+}
+
+int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n) {
+  CTX_GUARD_NOJOIN(ctx);
+  return sample_units_end(ctx, n_units, out_n);
 }
 
 int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id) {

@@ -1562,12 +1562,15 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       writer_dep = ctx->ev_ready;
     }
     HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, writer_dep, 0));
-    // the writer gate: this job's writers from the gate_at-th on wait for the next job's sorts (mh_internal.h)
+    // the writer gate: this job's writers from the gate_at-th on wait for the next job's sorts (mh_internal.h); with
+    // a batch begun ahead (mh_sample_units_begin: the lookahead pipeline) that batch is the next job and its sort is
+    // already queued, so they wait for gate >= job
     if (ctx->gate && ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at && ctx->job > 0) {
+      const uint32_t want = ctx->sample_state ? ctx->job : ctx->job + 1;
       if (gate_debug()) fprintf(stderr, "mh gate: writer %d of job %u waits for %u\n", ctx->writers_in_job, ctx->job,
-                                ctx->job + 1);
-      HIPCHK(ctx, hipStreamWaitValue32(ctx->wstream, ctx->gate, ctx->job + 1, hipStreamWaitValueGte, 0xffffffffu));
-      if (ctx->job + 1 > ctx->gate_waited) ctx->gate_waited = ctx->job + 1;
+                                want);
+      HIPCHK(ctx, hipStreamWaitValue32(ctx->wstream, ctx->gate, want, hipStreamWaitValueGte, 0xffffffffu));
+      if (want > ctx->gate_waited) ctx->gate_waited = want;
     }
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;

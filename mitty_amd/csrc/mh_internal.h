@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -165,6 +166,9 @@ struct mh_ctx {
   hipStream_t crstream = nullptr;
   hipEvent_t ev_crw = nullptr;
   bool cr_pending = false;
+  // a batch between mh_sample_units_begin and _end (mh_sample.hip SampleState); writers queued meanwhile wait, with
+  // the gate on, for the begun batch's sort (gate >= job) instead of the next one's (gate >= job + 1)
+  std::shared_ptr<void> sample_state;
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
   // Writer gate.  The permutation's radix sort cannot run beside a FASTQ writer (its workgroups need a whole CU and
@@ -326,6 +330,10 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                      int32_t rng_mode, int64_t *out_n);
+int32_t sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
+                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                           int32_t n_tlen, int32_t rng_mode);
+int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
 
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)

@@ -1362,9 +1362,26 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
 
 }  // namespace
 
-int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
-                     const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                     int32_t rng_mode, int64_t *out_n) {
+// A batch's sampling state between its two halves (sample_units_begin / _end): the plan, the batch buffers and the
+// lanes.  The batch buffers are shared by every batch, so one batch is begun at a time.
+struct SampleState {
+  std::vector<UnitPlan> plan;
+  int32_t n_units = 0, rng_mode = 0, rlen = 0, n_tlen = 0, n_lanes = 1;
+  bool two_lanes = false, batch = false;
+  double p = 0;
+  int64_t j_total = 0, nn = 0;
+  uint32_t *words = nullptr, *jall = nullptr;
+  double *d_cum = nullptr;
+  int64_t *d_m = nullptr, *d_status = nullptr;
+  uint32_t *d_flags = nullptr;
+  BatchPerm bp{nullptr, nullptr};
+};
+
+// First half: plan, word streams, shuffle decode, geometric scans and — batch path — the permutation's sort and
+// heads (the writer gate opens there); the per-unit path runs its units whole here.
+static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
+                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                           int32_t n_tlen, int32_t rng_mode) {
   for (int32_t u = 0; u < n_units; u++)
     if (seeds[u] > 0xffffffffull)
       return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seeds[u]) + " is out of range 0 - 4294967295");
@@ -1604,21 +1621,9 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
     MH_TRY(gate_release(ctx, st, ctx->job));   // the previous job's gated writers may go
-    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
-                       (const uint32_t *)sk, (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)bp.ts, bp.tsh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
-    // 3. every unit's template lengths, compaction and file order (lanes)
-    if (two_lanes) {
-      HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
-      HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
-      for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
-    }
-    for (int32_t u = 0, k = 0; u < n_units; u++) {
-      if (plan[u].n == 0) continue;
-      MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                         d_flags + u, k++ % n_lanes, 0, 2, nullptr, &bp));
-    }
+    S.bp = bp;
   } else
   for (int ph = split ? 1 : 0; ph <= (split ? 2 : 0); ph++)
     for (int32_t u = 0, k = 0; u < n_units; u++) {
@@ -1632,6 +1637,60 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
       MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
                          d_flags + u, lane, role, ph, split ? ctx->usort[u] : nullptr));
     }
+  S.plan = std::move(plan);
+  S.n_units = n_units;
+  S.rng_mode = rng_mode;
+  S.rlen = rlen;
+  S.n_tlen = n_tlen;
+  S.n_lanes = n_lanes;
+  S.two_lanes = two_lanes;
+  S.batch = batch;
+  S.p = p;
+  S.j_total = j_total;
+  S.nn = nn;
+  S.words = words;
+  S.jall = jall;
+  S.d_cum = d_cum;
+  S.d_m = d_m;
+  S.d_status = d_status;
+  S.d_flags = d_flags;
+  return MH_OK;
+}
+
+// Second half: the batch path's chase and per-unit template lengths, compaction and file order; the lanes joined,
+// the counts read back, the rare exact fix-ups, the template sets marked valid.
+static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
+  hipStream_t st = ctx->stream;
+  std::vector<UnitPlan> &plan = S.plan;
+  const int32_t n_units = S.n_units, rng_mode = S.rng_mode, rlen = S.rlen, n_tlen = S.n_tlen, n_lanes = S.n_lanes;
+  const bool two_lanes = S.two_lanes;
+  const double p = S.p;
+  const int64_t j_total = S.j_total, nn = S.nn;
+  uint32_t *words = S.words, *jall = S.jall;
+  double *d_cum = S.d_cum;
+  int64_t *d_m = S.d_m, *d_status = S.d_status;
+  uint32_t *d_flags = S.d_flags;
+  if (S.batch) {
+    const BatchPerm &bp = S.bp;
+    const uint32_t *sk = (const uint32_t *)ctx->pb[3].p, *sv = (const uint32_t *)ctx->pb[4].p;
+    const int32_t *nxt = (const int32_t *)ctx->pb[5].p;
+    stage_begin(ctx, "sample_permutation");
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total, sk, sv, nxt,
+                       (const int64_t *)bp.ts, bp.tsh);
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    // 3. every unit's template lengths, compaction and file order (lanes)
+    if (two_lanes) {
+      HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+      for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
+    }
+    for (int32_t u = 0, k = 0; u < n_units; u++) {
+      if (plan[u].n == 0) continue;
+      MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
+                         d_flags + u, k++ % n_lanes, 0, 2, nullptr, &bp));
+    }
+  }
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
     HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_join, 0));
@@ -1684,6 +1743,35 @@ int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const
     if (out_n) out_n[u] = ts.n;
   }
   return MH_OK;
+}
+
+int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
+                     const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                     int32_t rng_mode, int64_t *out_n) {
+  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
+  SampleState S;
+  MH_TRY(sample_head(ctx, S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
+  return sample_tail(ctx, S, out_n);
+}
+
+// The two halves as separate calls, so a caller can queue the next batch's sort ahead of this batch's writers (the
+// lookahead pipeline): begin = sample_head, end = sample_tail.
+int32_t sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
+                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                           int32_t n_tlen, int32_t rng_mode) {
+  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
+  auto S = std::make_shared<SampleState>();
+  MH_TRY(sample_head(ctx, *S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
+  ctx->sample_state = S;
+  return MH_OK;
+}
+
+int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n) {
+  auto S = std::static_pointer_cast<SampleState>(ctx->sample_state);
+  if (!S) return arg_fail(ctx, MH_E_STATE, "no begun batch (mh_sample_units_begin)");
+  if (n_units != S->n_units) return arg_fail(ctx, MH_E_ARG, "unit count differs from the begun batch's");
+  ctx->sample_state.reset();
+  return sample_tail(ctx, *S, out_n);
 }
 
 }  // namespace mh

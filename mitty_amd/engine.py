@@ -122,6 +122,57 @@ class Engine:
           on_unit(ps, int(ns[k]), kept, b1, b2)
     return out
 
+  def run_batches_lookahead(self, batches, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
+                            rng='mitty', on_batch=None):
+    """Batches of units [(ps, ri, cpy, rng_seed)] emitted in order with the next batch's sampling queued ahead:
+    batch k + 1's first half (word streams, decode, geometric scans, permutation sort: mh_sample_units_begin) is
+    queued before batch k's writers, so with the writer gate on (MH_WRITER_GATE=0) the sort runs alone between two
+    batches' writers and the rest of the sampling runs beside the writers.  on_batch(k) runs before batch k is
+    emitted (e.g. to recycle the arenas).  Returns [(n, kept, b1, b2)] per unit, in order."""
+    B = len(batches)
+    ids = [None] * B
+
+    def begin(k):
+      units = batches[k]
+      if not os.environ.get('MH_SPLICE_ONE_LANE'):
+        self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
+      slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+      base = (k % 3) * self.TPL_BATCH + 3 * self.TPL_BATCH   # three generations in flight (writers, end, begin)
+      ids[k] = [base + i for i in range(len(units))]
+      self.ctx.sample_units_begin(ids[k], slots, [u[3] for u in units], p, rlen, cum_tlen, RNG_MODES[rng])
+
+    out = []
+    if B == 0:
+      return out
+    begin(0)
+    ns = [None] * B
+    ns[0] = self.ctx.sample_units_end(len(batches[0]))
+    if B > 1:
+      begin(1)
+    for k in range(B):
+      if on_batch is not None:
+        on_batch(k)
+      units = batches[k]
+      slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+      for c0 in range(0, len(units), self.EMIT_SETS):
+        chunk = list(range(c0, min(c0 + self.EMIT_SETS, len(units))))
+        for i in chunk:
+          ps, ri, cpy, seed = units[i]
+          self.ctx.use_templates(ids[k][i])
+          self.ctx.emit_prepare(slots[i], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
+                                write_fastq2, unit_key=seed, wait=False)
+        for i in chunk:
+          ps, ri, cpy, seed = units[i]
+          self.ctx.use_templates(ids[k][i])
+          kept, b1, b2 = self.ctx.emit_reads(slots[i], '{}:{}:{}'.format(sample_name, worker_id, ps),
+                                             self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
+          out.append((int(ns[k][i]), kept, b1, b2))
+      if k + 1 < B:
+        ns[k + 1] = self.ctx.sample_units_end(len(batches[k + 1]))
+      if k + 2 < B:
+        begin(k + 2)
+    return out
+
   def sample_only(self, units, soa_of, p, rlen, cum_tlen, tpl_base, rng='mitty'):
     """The sampling half of run_units: units [(ps, ri, cpy, rng_seed)] sampled together into template sets
     tpl_base + k.  Returns the template counts (emit_only emits them later)."""

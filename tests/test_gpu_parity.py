@@ -1500,3 +1500,43 @@ def test_device_bgzf_arena_ranges_equal_whole_arena(native):
       eng.ctx.output_bgzf_range_pinned(part, u1 - 10, 20, 0)   # past the arena
   finally:
     eng.close()
+
+
+@pytest.mark.parametrize('gate', [None, '0'])
+def test_lookahead_batches_match_run_units(native, monkeypatch, gate):
+  """The lookahead pipeline (batch k+1's sampling up to its sort queued before batch k's writers, the writers gated on
+  that sort: Engine.run_batches_lookahead over mh_sample_units_begin / _end) writes the same FASTQ, byte for byte,
+  as batch after batch through run_units — three regions, 12 units in batches of 4, 5 and 3."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(mdl['mean_rlen'], 30.0)
+  lens = [1_500_000, 800_000, 2_000_000]
+  seqs = [synth.contig(L, 40 + i) for i, L in enumerate(lens)]
+  copies = [synth.copies_soa(synth.variants(s, 50 + i), 0, len(s)) for i, s in enumerate(seqs)]
+  units = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(_native.work_units(9, [2] * len(lens), passes))]
+  batches = [units[:4], units[4:9], units[9:]]
+  soa_of = lambda r, c: copies[r][c]
+
+  def run(lookahead):
+    if lookahead and gate is not None:
+      monkeypatch.setenv('MH_WRITER_GATE', gate)
+    else:
+      monkeypatch.delenv('MH_WRITER_GATE', raising=False)
+    eng = Engine(0)
+    try:
+      for ri, s in enumerate(seqs):
+        eng.load_region(ri, (str(ri + 1), 0, len(s)), s)
+      eng.ctx.reset_output()
+      if lookahead:
+        res = eng.run_batches_lookahead(batches, soa_of, p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')
+      else:
+        res = [r for b in batches for r in eng.run_units(b, soa_of, p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')]
+      return res, eng.ctx.fetch_output()
+    finally:
+      eng.close()
+  r0, (a1, a2) = run(False)
+  r1, (b1, b2) = run(True)
+  assert r0 == r1
+  G.check_same(b1, a1, 'file 1 differs')
+  G.check_same(b2, a2, 'file 2 differs')
