@@ -39,6 +39,14 @@ struct CorruptCfg {
   const uint16_t *Fp16 = nullptr;    // [100]: min(floor(phred_p * 2^16), 65535)
 };
 
+// a ^ b ^ k in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96; the compiler emits two v_xor_b32 for
+// it).  k is wave-uniform (the Philox key schedule), so it is passed in an SGPR.
+__device__ __forceinline__ uint32_t xor3_vvs(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
+  return d;
+}
+
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll
   for (int r = 0; r < 10; r++) {
@@ -46,7 +54,7 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    c = make_uint4(xor3_vvs(hi1, c.y, k.x), lo1, xor3_vvs(hi0, c.w, k.y), lo0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;
   }

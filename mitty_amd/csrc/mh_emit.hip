@@ -1021,7 +1021,128 @@ struct CiArgs {
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
   CorruptCfg cc;
+  int32_t dbg;            // experiments (MH_CR_DBG): 1 full blocks through the guarded per-base path (A/B); timing
+                          // only (wrong bytes): 2 no stores in full blocks, 4 no base loads, 8 no Philox, 16 the item loop alone
 };
+
+// The LDS-table BQ step of one base (k_cr_inplace's walk): bk = the base's bucket row, tp = its threshold-pair row.
+// Entries below h1 = w >> 16 (capped at 93); *amb when one equals h1, or three or more of the bucket's lie below it.
+__device__ __forceinline__ uint32_t cr_lds_walk(const uint8_t *bk, const uint16_t *tp, uint32_t w, uint32_t *amb) {
+  const uint32_t e = bk[w >> 24];
+  const uint32_t c = e & 0x7fu, fl = e >> 7;
+  const uint32_t pa = tp[c], pb = tp[c + 1];
+  const uint32_t lo = (w >> 16) & 0xffu;
+  const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = pb >> 8;
+  const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
+  const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
+  *amb = b2 | (fl & (uint32_t)(vn == lo));
+  return c + b0 + b1;
+}
+
+// One full 15-base block of a record with the tables in LDS: five triple draws, per base a BQ step and the U2
+// decision, the qualities stored; then the rare bases (f64 decisions), then the substituted bases with their choices
+// (the triple's 10-bit field, or the base's own draw when it is 1023) — the same stream and decisions as the guarded
+// path in k_cr_inplace, with no per-base guards so the fifteen bases' LDS reads can be in flight together.
+// bk / tp: the bucket and threshold-pair rows of base n0 (row j of base n0 + j at bk + j * CB_ROW, tp + j * n_bq).
+__device__ __forceinline__ void cr_full_block(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
+                                              const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f,
+                                              int n0, char *seq, uint64_t sa, uint4 g0, uint4 g1, char *qual,
+                                              int32_t dbg) {
+  const int n_bq = cc.n_bq;
+  // in phases, so each phase's fifteen LDS reads are in flight together (the arrays are registers: constant indices)
+  uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], P[CI_BLK], V2[CI_BLK], F[CI_BLK], BQ[CI_BLK];
+  const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
+#pragma unroll
+  for (int g = 0; g < CI_BLK / 3; g++) {   // the five triple draws
+    const uint4 r = (dbg & 8) ? make_uint4(tl * 0x9E3779B9u + g, th ^ (cw * 0x85ebca6bu), cw * 0xc2b2ae35u + g, tl ^ g)
+                              : philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
+    W[3 * g] = r.x;
+    W[3 * g + 1] = r.y;
+    W[3 * g + 2] = r.z;
+    RW[g] = r.w;
+  }
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) E[j] = bk[j * CB_ROW + (W[j] >> 24)];   // bucket entries
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {   // threshold pairs of entries c, c + 1 (only a flagged bucket uses them)
+    const uint16_t *t = tp + j * n_bq + (E[j] & 0x7fu);
+    P[j] = t[0];
+    V2[j] = ((const uint8_t *)t)[3];
+  }
+  uint32_t ps = 0, px = 0;
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {   // BQ steps (as cr_lds_walk), then Fp16 of each
+    const uint32_t e = E[j], c = e & 0x7fu, fl = e >> 7, pa = P[j];
+    const uint32_t lo = (W[j] >> 16) & 0xffu;
+    const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = V2[j];
+    const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
+    const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
+    const uint32_t amb = b2 | (fl & (uint32_t)(vn == lo));
+    BQ[j] = c + b0 + b1;
+    px |= amb << j;
+    F[j] = fp[BQ[j]];
+  }
+  uint32_t qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0;
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {   // U2 decisions
+    const uint32_t amb = (px >> j) & 1u, pth = F[j], h2 = W[j] & 0xffffu;
+    ps |= (uint32_t)(!amb && h2 < pth) << j;
+    px |= (uint32_t)(h2 == pth) << j;
+    const uint32_t qv = (BQ[j] + 33u) << (8 * (j & 3));
+    if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
+  }
+  const uint32_t rw0 = RW[0], rw1 = RW[1], rw2 = RW[2], rw3 = RW[3], rw4 = RW[4];
+  if (dbg & 2) {   // (timing only: no stores)
+    if ((qd0 ^ qd1 ^ qd2 ^ qd3 ^ ps ^ px) == 0x12345678u) qual[n0] = 0;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {
+    const uint32_t q = j < 4 ? qd0 : j < 8 ? qd1 : j < 12 ? qd2 : qd3;
+    qual[n0 + j] = (char)(q >> (8 * (j & 3)));
+  }
+  // rare: the full 53-bit decisions (U1 or U2 within 2^-16 of a threshold)
+  while (px) {
+    const int j = __builtin_ctz(px);
+    px &= px - 1;
+    const int n = n0 + j;
+    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+    const int k = n % 3;
+    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+    uint32_t amb;
+    const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
+    const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
+                                     w, bq, amb);
+    qual[n] = (char)((x & 0xffu) + 33);
+    ps |= (x >> 8) << j;
+  }
+  if (!ps) return;
+  // the substituted bases (about 0.7 of 15 at a 4.7 % error rate): base_rot[b][choice]
+  const uint32_t sh = (uint32_t)(sa & 15);
+  const uint32_t o = sh >> 2, bsh = 8 * (sh & 3);
+  const uint32_t d0 = o == 0 ? g0.x : o == 1 ? g0.y : o == 2 ? g0.z : g0.w;
+  const uint32_t d1 = o == 0 ? g0.y : o == 1 ? g0.z : o == 2 ? g0.w : g1.x;
+  const uint32_t d2 = o == 0 ? g0.z : o == 1 ? g0.w : o == 2 ? g1.x : g1.y;
+  const uint32_t d3 = o == 0 ? g0.w : o == 1 ? g1.x : o == 2 ? g1.y : g1.z;
+  const uint32_t d4 = o == 0 ? g1.x : o == 1 ? g1.y : o == 2 ? g1.z : g1.w;
+  const uint32_t bw0 = (uint32_t)(((uint64_t)d1 << 32 | d0) >> bsh), bw1 = (uint32_t)(((uint64_t)d2 << 32 | d1) >> bsh),
+                 bw2 = (uint32_t)(((uint64_t)d3 << 32 | d2) >> bsh), bw3 = (uint32_t)(((uint64_t)d4 << 32 | d3) >> bsh);
+  do {
+    const int j = __builtin_ctz(ps);
+    ps &= ps - 1;
+    const int g = j / 3, k = j - 3 * g;
+    const uint32_t rw = g == 0 ? rw0 : g == 1 ? rw1 : g == 2 ? rw2 : g == 3 ? rw3 : rw4;
+    const uint32_t c10 = (rw >> (10 * k)) & 1023u;
+    uint32_t chv;
+    if (c10 == 1023u)   // rejected: the base's own draw (t, f | 0x8000, n)
+      chv = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3),
+                                   key).x, 3u);
+    else
+      chv = c10 % 3u;
+    const uint32_t bw = j < 4 ? bw0 : j < 8 ? bw1 : j < 12 ? bw2 : bw3;
+    seq[n0 + j] = (char)rot_base((uint8_t)(bw >> (8 * (j & 3))), chv);
+  } while (ps);
+}
 
 __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1044,8 +1165,8 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
 
 // PF (two files): a workgroup corrupts one file's records only (file = blockIdx.x & 1), so it stages that file's tables
 // alone — half the LDS, two workgroups (8 waves per SIMD) per CU instead of one.
-template <bool LDS_TAB, bool PF>
-__global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A) {   // (PF: 8 waves per SIMD)
+template <bool LDS_TAB, bool PF, int THR>
+__global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_inplace(CiArgs A) {   // (PF: two per CU)
   // LDS: bucket entries [NT][rlen][CB_ROW] | Fp16[100] | low-byte pairs of the thresholds [NT][rlen][n_bq] (u16);
   // NT = 2 files, or 1 with PF
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
@@ -1062,16 +1183,16 @@ __global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A)
       const int f = PF ? f_pf : ft;
       const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
       uint4 *dst = (uint4 *)(ctab + ft * row_bytes);
-      for (int i = threadIdx.x; i < row_bytes / 16; i += CI_THREADS) dst[i] = src[i];
+      for (int i = threadIdx.x; i < row_bytes / 16; i += THR) dst[i] = src[i];
       // per entry j: its low byte | (entry j + 1's low byte when j + 1 < min(n_bq, 93) lies in j's bucket, else 0xff) << 8
       const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
-      for (int i = threadIdx.x; i < rlen * n_bq; i += CI_THREADS) {
+      for (int i = threadIdx.x; i < rlen * n_bq; i += THR) {
         const int j = i % n_bq;
         const uint32_t a = t16[i], b = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
         ((uint16_t *)(ctab + o_t8))[ft * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
       }
     }
-    for (int i = threadIdx.x; i < 100; i += CI_THREADS) ((uint16_t *)fp16)[i] = cc.Fp16[i];
+    for (int i = threadIdx.x; i < 100; i += THR) ((uint16_t *)fp16)[i] = cc.Fp16[i];
     __syncthreads();
   }
   // the BQ step of base n of file f for the draw's high 16 bits: entries below h1 (capped at 93), amb when one
@@ -1102,7 +1223,7 @@ __global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A)
   // (PF: items of this workgroup's file only; an item's unit q is then the template, its record 2 q + file)
   const uint32_t NB = (uint32_t)(rlen + CI_BLK - 1) / CI_BLK;
   const uint32_t n_items = (uint32_t)(A.m * (PF ? 1 : A.nf)) * NB;
-  const uint32_t stride = (PF ? gridDim.x >> 1 : gridDim.x) * CI_THREADS;
+  const uint32_t stride = (PF ? gridDim.x >> 1 : gridDim.x) * THR;
   const uint32_t nb_magic = 0xffffffffu / NB + 1u;   // umulhi(i, nb_magic) is i / NB or one more
   auto unit_of = [&](uint32_t i) -> uint32_t {
     i = i < n_items ? i : 0u;
@@ -1110,12 +1231,17 @@ __global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A)
     return q * NB > i ? q - 1 : q;
   };
   auto rec_of = [&](uint32_t i) -> uint32_t { return PF ? 2u * unit_of(i) + (uint32_t)f_pf : unit_of(i); };
-  uint32_t i = (PF ? blockIdx.x >> 1 : blockIdx.x) * CI_THREADS + threadIdx.x;
+  uint32_t i = (PF ? blockIdx.x >> 1 : blockIdx.x) * THR + threadIdx.x;
   uint2 R = A.crec[rec_of(i)];                         // this item's record word; the next one is in flight below
   for (; i < n_items; i += stride) {
     const uint32_t uq = unit_of(i);
     const uint32_t rr = PF ? 2u * uq + (uint32_t)f_pf : uq;
     const uint2 Rn = A.crec[rec_of(i + stride)];     // prefetch
+    if (A.dbg & 16) {   // (timing only: the item loop and record words alone)
+      if (R.x == 0x12345678u && R.y == 0x9abcdef0u) A.arena[0][i] = 0;
+      R = Rn;
+      continue;
+    }
     const uint32_t S = R.y & 0xffffu;
     const int n0 = CI_BLK * (int)(i - uq * NB);
     if ((uint32_t)n0 < S) {
@@ -1128,10 +1254,20 @@ __global__ void __launch_bounds__(CI_THREADS, PF ? 8 : 1) k_cr_inplace(CiArgs A)
       // the block's bases: the two aligned 16-byte chunks holding them, shifted into bw[0..3] (base j = byte j)
       const uint64_t sa = (uint64_t)(seq + n0);
       const uint4 *sp = (const uint4 *)(sa & ~(uint64_t)15);
-      const uint4 g0 = sp[0], g1 = sp[1];
+      const uint4 g0 = (A.dbg & 4) ? make_uint4(R.x, R.y, 0, 0) : sp[0], g1 = (A.dbg & 4) ? make_uint4(0, R.x, 0, R.y) : sp[1];
       uint32_t qd[4] = {0, 0, 0, 0};   // the block's qualities, packed
       uint32_t px = 0, pc = 0, ps = 0;   // bases needing the f64 decisions / a fallback choice draw; substituted
       uint32_t ch = 0;                   // choices of the substituted bases (2 bits each)
+      if (LDS_TAB && cnt == CI_BLK && !(A.dbg & 1)) {
+        // A full block (every block of a 150-bp read): no per-base guards, so the bases' LDS reads interleave; the
+        // choices are derived for the substituted bases only (cr_full_block).
+        const int row0 = (PF ? 0 : f * rlen) + n0;
+        cr_full_block(ctab + row0 * CB_ROW, t8p + row0 * n_bq, fp16, cc, key, tl, th, f, n0, seq, sa, g0, g1, qual,
+                      A.dbg);
+        if (n0 + cnt == (int)S) qual[S] = '\n';
+        R = Rn;
+        continue;
+      }
 #pragma unroll
       for (int g = 0; g < CI_BLK / 3; g++) {
         if (3 * g < cnt) {
@@ -1241,21 +1377,28 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
   if (cr_overlap()) per_cu = 1;                           // room for the writers beside it
   if (getenv("MH_CR_PER_CU")) per_cu = std::max(1, atoi(getenv("MH_CR_PER_CU")));
-  int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + CI_THREADS - 1) / CI_THREADS);
+  // MH_CR_THR=512 (A/B): per-file workgroups of 512 threads (4 waves per SIMD, up to 128 VGPRs for the full-block
+  // path) instead of 1024 (8 waves per SIMD at 64 VGPRs): measured no faster
+  static const int cr_thr = getenv("MH_CR_THR") ? atoi(getenv("MH_CR_THR")) : CI_THREADS;
+  const int thr = lds_tab && pf && cr_thr == 512 ? 512 : CI_THREADS;
+  int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
   if (grid < 1) grid = 1;
   if (pf) grid = (grid + 1) & ~(int64_t)1;   // even: workgroup pairs (file 0, file 1)
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
+  static const int32_t cr_dbg = getenv("MH_CR_DBG") ? atoi(getenv("MH_CR_DBG")) : 0;
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc, cr_dbg};
   stage_begin(ctx, "emit_corrupt");
   if (!crec_ready) {   // (the fused writer wrote the record words itself)
     hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
     HIPCHK(ctx, hipGetLastError());
   }
-  if (lds_tab && pf)
-    hipLaunchKernelGGL((k_cr_inplace<true, true>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
+  if (lds_tab && pf && cr_thr == 512)
+    hipLaunchKernelGGL((k_cr_inplace<true, true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A);
+  else if (lds_tab && pf)
+    hipLaunchKernelGGL((k_cr_inplace<true, true, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else if (lds_tab)
-    hipLaunchKernelGGL((k_cr_inplace<true, false>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
+    hipLaunchKernelGGL((k_cr_inplace<true, false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else
-    hipLaunchKernelGGL((k_cr_inplace<false, false>), dim3((unsigned)grid), dim3(CI_THREADS), 0, st, A);
+    hipLaunchKernelGGL((k_cr_inplace<false, false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), 0, st, A);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   return MH_OK;
