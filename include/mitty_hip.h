@@ -223,6 +223,13 @@ int32_t mh_bam_sort(mh_ctx *ctx);
 int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);
+/* mh_bam_write_gpu: mh_bam_write with the record blocks deflated on the device (mh_deflate.hip: dynamic-Huffman BGZF
+ *   blocks of the sorted store in HBM, 0xff00 input bytes each, the header's block deflated on the host at level 6):
+ *   only the compressed bytes cross PCIe.  Replaces the same pysam.sort / pysam.index pair (god_aligner.py:117-131);
+ *   the file decompresses to the same BAM stream, the BAI indexes its own virtual offsets.  *out_file_bytes = the
+ *   BAM file's size. */
+int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
+                         const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes);
 
 /* ---- VCF ingest (vcfio.load_variant_file / split_copies / parse, vcfio.py:51-126) ------
  * Host-only (no device): mh_vcf_open parses a plain or bgzipped VCF for one sample; mh_vcf_region runs the BED

@@ -23,7 +23,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_begin', 'mh_sample_units_end',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
+           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
@@ -103,6 +103,7 @@ def lib():
   _sig(L, 'mh_bam_records', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
+  _sig(L, 'mh_bam_write_gpu', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, P_i64, P_i64, P_i64])
   _sig(L, 'mh_bam_reset', [c_vp])
   _sig(L, 'mh_bam_sort', [c_vp])
   _sig(L, 'mh_corrupt_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
@@ -680,6 +681,15 @@ class Context:
     self._chk(self._L.mh_bam_write(self._h, bam_path.encode(), h, len(h), int(level), int(threads),
                                    None if bai_path is None else bai_path.encode(), ctypes.byref(n), ctypes.byref(b)))
     return n.value, b.value
+
+  def bam_write_gpu(self, bam_path, header_text, bai_path=None):
+    """mh_bam_write with the record blocks deflated on the device.  Returns (records, record bytes, file bytes)."""
+    n, b, fb = c_i64(), c_i64(), c_i64()
+    h = header_text.encode()
+    self._chk(self._L.mh_bam_write_gpu(self._h, bam_path.encode(), h, len(h),
+                                       None if bai_path is None else bai_path.encode(), ctypes.byref(n),
+                                       ctypes.byref(b), ctypes.byref(fb)))
+    return n.value, b.value, fb.value
 
   def bam_reset(self):
     self._chk(self._L.mh_bam_reset(self._h))

@@ -82,11 +82,12 @@ def header_text(hdr, sorted_by='coordinate'):
 
 
 def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max_templates=None,
-                           sample_name='Seven', device=0, level=6, chunk_bytes=1 << 30):
+                           sample_name='Seven', device=0, level=6, chunk_bytes=1 << 30, gpu_bgzf=False):
   """god_aligner.process_multi_threaded (:44-131): `bam_fname` (coordinate-sorted BAM) + `bam_fname.bai`.
 
   As in the reference, max_templates stops after template index max_templates, i.e. max_templates + 1 templates.
-  `threads` sizes the BGZF deflate pool.
+  `threads` sizes the BGZF deflate pool; gpu_bgzf: the record blocks deflated on the device instead
+  (mh_bam_write_gpu: the same BAM stream, only the compressed bytes leave the GPU).
   """
   rg_id = base64.b64encode(' '.join(sys.argv).encode('ascii'))
   hdr = construct_header(fasta + '.ann', rg_id=rg_id, sample=sample_name)
@@ -97,8 +98,11 @@ def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max
     limit = None if max_templates is None else max_templates + 1
     n_t = stream_templates(fastq1, fastq2, lambda b1, b2, want, done: ctx.bam_add_fastq(b1, b2, want),
                            chunk_bytes, limit)
-    n_rec, n_bytes = ctx.bam_write(bam_fname, header_text(hdr), level=level, threads=max(threads, 1),
-                                   bai_path=bam_fname + '.bai')
+    if gpu_bgzf:
+      n_rec, n_bytes, _ = ctx.bam_write_gpu(bam_fname, header_text(hdr), bai_path=bam_fname + '.bai')
+    else:
+      n_rec, n_bytes = ctx.bam_write(bam_fname, header_text(hdr), level=level, threads=max(threads, 1),
+                                     bai_path=bam_fname + '.bai')
   finally:
     ctx.close()
   logger.debug('Processed {} templates ({} records) in {:0.2f}s'.format(n_t, n_rec, time.time() - t0))

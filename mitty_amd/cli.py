@@ -140,13 +140,15 @@ def read_corruption(modelfile, fastq1_in, fastq1_out, seed, fastq2_in, fastq2_ou
 @click.option('--max-templates', type=int, help='For debugging: quits after processing these many templates')
 @click.option('--threads', default=2)
 @click.option('--device', default=0, help='HIP device ordinal')
-def god_aligner(fasta, bam, sample_name, fastq1, fastq2, max_templates, threads, device):
+@click.option('--gpu-bgzf', is_flag=True, help='Deflate the BAM record blocks on the GPU (additive option)')
+def god_aligner(fasta, bam, sample_name, fastq1, fastq2, max_templates, threads, device, gpu_bgzf):
   """Given a FASTA.ann file and FASTQ made of simulated reads,
      construct a perfectly aligned BAM from them (reference cli.py:183-204).
 
      Note: The program uses the fasta.ann file to construct the BAM header"""
   from mitty_amd.benchmarking import god_aligner as god
-  god.process_multi_threaded(fasta, bam, fastq1, fastq2, threads, max_templates, sample_name, device=device)
+  god.process_multi_threaded(fasta, bam, fastq1, fastq2, threads, max_templates, sample_name, device=device,
+                             gpu_bgzf=gpu_bgzf)
 
 
 def main():

@@ -1188,6 +1188,42 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
   return MH_OK;
 }
 
+int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
+                         const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  MH_TRY(bam_sort(ctx));
+  const int64_t n = B.n_rec;
+  // the sorted records deflated on the device (k_bgzf_blocks), then only the compressed bytes cross PCIe
+  std::vector<int64_t> boff;
+  int64_t nz = 0;
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
+  MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
+                     (int64_t)ctx->gz_out.cap, &nz, &boff));
+  const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
+                                           B.ref_names, B.ref_len);
+  const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
+  auto fetch = [&](int64_t o, int64_t len, uint8_t *buf) -> bool {
+    return hipMemcpy(buf, z + o, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess;
+  };
+  std::vector<int64_t> coff;
+  std::string err;
+  if (!bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err)) return arg_fail(ctx, MH_E_ARG, err);
+  if (bai_path) {
+    std::vector<int64_t> soff((size_t)n + 1, 0);
+    std::vector<BaiRec> info((size_t)n + 1);
+    MH_TRY(bam_fetch_sorted(ctx, nullptr, soff.data(), (int32_t *)info.data()));
+    if (!bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
+      return arg_fail(ctx, MH_E_ARG, err);
+  }
+  if (out_records) *out_records = n;
+  if (out_bytes) *out_bytes = B.bytes;
+  if (out_file_bytes) *out_file_bytes = coff.empty() ? 0 : coff.back() + 28;
+  return MH_OK;
+}
+
 int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
                          int64_t *used1, int64_t *used2, int64_t *templates) {
   CTX_GUARD(ctx);

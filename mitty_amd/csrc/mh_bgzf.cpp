@@ -133,6 +133,39 @@ bool bgzf_write(const char *path, const std::string &header, const uint8_t *data
   return ok;
 }
 
+bool bgzf_write_blocks(const char *path, const std::string &header, int level, int64_t n_z,
+                       const std::vector<int64_t> &boff,
+                       const std::function<bool(int64_t, int64_t, uint8_t *)> &fetch, std::vector<int64_t> &coff,
+                       std::string &err) {
+  FILE *fp = fopen(path, "wb");
+  if (!fp) {
+    err = std::string("cannot open ") + path;
+    return false;
+  }
+  int64_t pos = 0;
+  bool ok = true;
+  std::string blk;
+  for (size_t h = 0; h < header.size() && ok; h += BGZF_BLOCK) {
+    const int64_t m = std::min<int64_t>(BGZF_BLOCK, (int64_t)(header.size() - h));
+    ok = bgzf_block((const uint8_t *)header.data() + h, m, level, blk) && fwrite(blk.data(), 1, blk.size(), fp) ==
+         blk.size();
+    pos += (int64_t)blk.size();
+  }
+  coff.resize(boff.size());
+  for (size_t b = 0; b < boff.size(); b++) coff[b] = pos + boff[b];
+  const int64_t piece = (int64_t)1 << 28;
+  std::vector<uint8_t> buf;
+  for (int64_t o = 0; o < n_z && ok; o += piece) {
+    const int64_t m = std::min(piece, n_z - o);
+    buf.resize((size_t)m);
+    ok = fetch(o, m, buf.data()) && fwrite(buf.data(), 1, (size_t)m, fp) == (size_t)m;
+  }
+  ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
+  ok = (fclose(fp) == 0) && ok;
+  if (!ok && err.empty()) err = std::string("BGZF write failed: ") + path;
+  return ok;
+}
+
 bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
                const std::vector<int64_t> &coff, std::string &err) {
   std::string s("BAI\1", 4);

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -25,6 +26,14 @@ std::string bam_header_bytes(const std::string &text, const std::vector<std::str
 // (b = 0..nblocks; the last entry is the offset of the EOF block).  Returns false and sets err on failure.
 bool bgzf_write(const char *path, const std::string &header, const uint8_t *data, int64_t n, int level, int threads,
                 std::vector<int64_t> &rec_block_coff, std::string &err);
+
+// The same file from data blocks deflated elsewhere (the device, mh_bam_write_gpu): `header` deflated here at `level`
+// in its own block(s), then n_z bytes of ready BGZF blocks fetched in pieces by fetch(offset, len, buf), then the EOF
+// marker.  boff[b] = offset of data block b inside those bytes (b = 0..nblocks); rec_block_coff as bgzf_write's.
+bool bgzf_write_blocks(const char *path, const std::string &header, int level, int64_t n_z,
+                       const std::vector<int64_t> &boff,
+                       const std::function<bool(int64_t, int64_t, uint8_t *)> &fetch,
+                       std::vector<int64_t> &rec_block_coff, std::string &err);
 
 // BAI for n sorted records whose data offsets are soff[0..n] (soff[n] = end), given the block map from bgzf_write.
 bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,

@@ -460,9 +460,10 @@ __global__ void __launch_bounds__(256) k_bgzf_pack(const uint8_t *in, int64_t b0
 }  // namespace
 
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
-                    int64_t *used) {
+                    int64_t *used, std::vector<int64_t> *boff) {
   *used = 0;
   const int64_t nb_all = (n + BLOCK - 1) / BLOCK;
+  if (boff) boff->assign((size_t)nb_all + 1, 0);
   const int64_t CH = 8192;   // blocks per launch (slots: CH x 72 KiB)
   MH_TRY(ensure(ctx, ctx->gz_slots, (size_t)CH * SLOT + 64));
   MH_TRY(ensure(ctx, ctx->gz_info, sizeof(DfBlockInfo) * (size_t)CH + 64));
@@ -482,8 +483,11 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
     HIPCHK(ctx, device_scan_sum<int64_t>(st, nb, LoadBlk{(const DfBlockInfo *)ctx->gz_info.p, nb},
                                          StoreBlk{(int64_t *)ctx->gz_off.p}, ctx->gz_scan.p, tot));
     HIPCHK(ctx, hipMemcpyAsync(hs + 32, tot, 8, hipMemcpyDeviceToHost, st));
+    if (boff) HIPCHK(ctx, hipMemcpyAsync(boff->data() + b0, ctx->gz_off.p, 8 * (size_t)nb, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     const int64_t bytes = hs[32];
+    if (boff)
+      for (int64_t i = 0; i < nb; i++) (*boff)[b0 + i] += w;
     if (w + bytes > cap) return arg_fail(ctx, MH_E_CAPACITY, "BGZF output buffer too small");
     hipLaunchKernelGGL(k_bgzf_pack, dim3((unsigned)nb), dim3(256), 0, st, d_in, b0,
                        (const uint8_t *)ctx->gz_slots.p, (const DfBlockInfo *)ctx->gz_info.p,
@@ -493,6 +497,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
   }
   HIPCHK(ctx, hipStreamSynchronize(st));
   *used = w;
+  if (boff) (*boff)[nb_all] = w;
   return MH_OK;
 }
 

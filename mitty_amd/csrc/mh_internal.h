@@ -340,7 +340,8 @@ int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
 int32_t sync_async_fill(mh_ctx *ctx);
 int32_t sync_writers(mh_ctx *ctx);   // the writer stream and the corruption stream drained (host wait)
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
-                    int64_t *used);            // BGZF blocks of a device buffer (no EOF marker), mh_deflate.hip
+                    int64_t *used, std::vector<int64_t> *boff = nullptr);   // BGZF blocks of a device buffer (no EOF
+                    // marker), mh_deflate.hip; boff: each block's offset in d_out (+ the end), for a BAI
 int64_t bgzf_device_bound(int64_t n);
 int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
 int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);

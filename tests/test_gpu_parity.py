@@ -1149,10 +1149,20 @@ def test_god_aligner_from_device_arenas(native, tmp_path):
     l_text = int.from_bytes(header[4:8], 'little')
     bam_b = str(tmp_path / 'b.bam')
     eng.ctx.bam_write(bam_b, header[8:8 + l_text].decode(), bai_path=bam_b + '.bai')
+    bam_c = str(tmp_path / 'c.bam')   # the record blocks deflated on the device (mh_bam_write_gpu)
+    n_c, _, fb = eng.ctx.bam_write_gpu(bam_c, header[8:8 + l_text].decode(), bai_path=bam_c + '.bai')
   finally:
     eng.close()
   _, recs_b, _, _ = god.record_voffsets(open(bam_b, 'rb').read())
   assert recs_a == recs_b
+  # the device-deflated file: the same header and records (zlib inflates every member), and its BAI indexes its own
+  # virtual offsets as the oracle computes them
+  data_c = open(bam_c, 'rb').read()
+  assert len(data_c) == fb and data_c[-28:] == open(bam_b, 'rb').read()[-28:]
+  header_c, recs_c, vo, vend = god.record_voffsets(data_c)
+  assert header_c == header and recs_c == recs_a and n_c == len(recs_a)
+  sq = [(b'1', 50000), (b'2', 20000), (b'3', 8000)]
+  assert open(bam_c + '.bai', 'rb').read() == god.bai(len(sq), [god.decode(r) for r in recs_c], vo, vend)
 
 
 def test_tumor_normal_mix_god_aligner(native, tmp_path):
