@@ -17,7 +17,8 @@
 //   k_perm_*          the permutation the swaps produce, without replaying them: steps radix-sorted by target,
 //                     then a chase per step (see k_perm_heads)
 //   k_tlen + scan     tl = searchsorted(cum_tlen (LDS), U) clipped to rlen; keep te < p_max; compaction
-//   k_file_order      fo0[k] = byte (k & 3) of word k >> 2, & 1 (randint(2, dtype=int8) buffering)
+//   file order        fo0[k] = byte (k & 3) of word k >> 2, & 1 (randint(2, dtype=int8) buffering), written
+//                     by the compaction's store
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
 // fallback for a unit whose decode ran out of pre-generated words.
 #include <cmath>
@@ -869,18 +870,18 @@ struct LoadKeep {
   const uint8_t *keep;
   __device__ int64_t operator()(int64_t k) const { return keep[k]; }
 };
+// the kept template's place excl: its positions, and its file-order bit (fo0[k] = byte (k & 3) of word k >> 2, & 1:
+// randint(2, dtype=int8) buffering, illumina.py:80 — the k-th kept template takes the k-th draw)
 struct StoreCompact {
   const uint8_t *keep; const int64_t *ts, *te; int64_t *pos0, *pos1; int64_t rlen;
+  const uint32_t *wfo; int8_t *fo0;
   __device__ void operator()(int64_t k, int64_t, int64_t excl) const {
     if (!keep[k]) return;
     pos0[excl] = ts[k];
     pos1[excl] = te[k] - rlen;
+    fo0[excl] = (int8_t)((wfo[excl >> 2] >> (8 * (excl & 3))) & 1u);
   }
 };
-__global__ void k_file_order(int64_t n, const int64_t *m_ptr, const uint32_t *w, int8_t *fo0) {
-  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n && k < *m_ptr) fo0[k] = (int8_t)((w[k >> 2] >> (8 * (k & 3))) & 1u);
-}
 
 // ---- Philox4x32-10 fast mode ------------------------------------------------------------------------------
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
@@ -1351,11 +1352,9 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
                                        StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p,
-                                                    (int64_t *)u.out->pos1.p, (int64_t)rlen},
+                                                    (int64_t *)u.out->pos1.p, (int64_t)rlen, w_fo,
+                                                    (int8_t *)u.out->fo0.p},
                                        scan_partials, d_m));
-  hipLaunchKernelGGL(k_file_order, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const int64_t *)d_m,
-                     w_fo, (int8_t *)u.out->fo0.p);
-  HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   return MH_OK;
 }

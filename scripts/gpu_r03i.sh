@@ -1,28 +1,15 @@
 #!/bin/bash
-# Write/read pattern calibration for a position-ordered writer; WGS A/B of the unstaged seams (4 KB less LDS).
+# File-order bits written by the compaction store (no k_file_order launch): sampling/FASTQ parity, WGS bench A/B-free
+# line (two repeats).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/calib2
+mkdir -p gpurun_out
 T=${TAG:-r03i}
-timeout -k 10 120 ./scripts/calib_scatter > gpurun_out/calib_scatter_times.json || exit $?
-cat gpurun_out/calib_scatter_times.json
-cd /tmp && export TMPDIR=/tmp
-cd "$GRAFT_REPO_ROOT"
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/calib2/f -o run -- ./scripts/calib_scatter > /dev/null || exit $?
-timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/calib2/w -o run -- ./scripts/calib_scatter > /dev/null || exit $?
-python3 - << 'PY'
-import csv, glob, collections
-for tag in ('f', 'w'):
-  fs = glob.glob('gpurun_out/calib2/%s/**/*counter_collection.csv' % tag, recursive=True)
-  if not fs:
-    print(tag, 'no counter csv'); continue
-  acc = collections.defaultdict(list)
-  for r in csv.DictReader(open(fs[0])):
-    acc[(r['Kernel_Name'][:40], r.get('Grid_Size', ''), r['Counter_Name'])].append(float(r['Counter_Value']))
-  for k, v in acc.items():
-    print(tag, k, ['%.3e' % x for x in v[-4:]])
-PY
-for d in 0 256; do
-  MH_EW_DBG=$d timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --batch-draws 64e6 > gpurun_out/bench_${T}_wgs_d$d.json 2>/dev/null || exit $?
-  python3 -c "import json; d=json.load(open('gpurun_out/bench_${T}_wgs_d$d.json')); print('wgs d$d', round(d['value']/1e9,3), round(d['ms_per_step'],2), 'writer', round(d['roofline']['avg_launch_ms'],3))"
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_wgs.py -m gpu -x -q --timeout 600 --timeout-method thread -k "templates or unit or e2e or wgs or batched or pipelined or lookahead or philox_sampling or chr1" > gpurun_out/pytest_${T}.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_${T}.log
+[ $rc = 0 ] || { grep -E "Error|assert|Fail" gpurun_out/pytest_${T}.log | head -20; exit $rc; }
+for rep in 1 2; do
+  timeout -k 10 300 python -u bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/bench_${T}_$rep.json 2>gpurun_out/bench_${T}_$rep.err || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_${T}_$rep.json')); print('wgs rep$rep', round(d['value']/1e9,3), round(d['ms_per_step'],2), 'writer', round(d['roofline']['avg_launch_ms'],3))"
 done
