@@ -1379,7 +1379,7 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   if (getenv("MH_CR_PER_CU")) per_cu = std::max(1, atoi(getenv("MH_CR_PER_CU")));
   // per-file workgroups of 512 threads (4 waves per SIMD, up to 128 VGPRs: the full-block path's phases keep their
   // fifteen LDS reads in flight); at 1024 threads (MH_CR_THR=1024, 64 VGPRs) that path spills and takes 8.3 instead
-  // of 5.6-5.8 ms per chr1 unit (profiles/r03/corrupt_experiments_r03.txt)
+  // of 5.6-5.8 ms per chr1 unit (profiles/r03/experiments_r03.txt)
   static const int cr_thr = getenv("MH_CR_THR") ? atoi(getenv("MH_CR_THR")) : 512;
   const int thr = lds_tab && pf && cr_thr == 512 ? 512 : CI_THREADS;
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
