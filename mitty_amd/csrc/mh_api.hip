@@ -1,5 +1,6 @@
 // mh_api.hip — the C ABI (include/mitty_hip.h): context, buffers, argument checks, dispatch to the subsystems.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -1194,29 +1195,49 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   BamStore &B = ctx->bam;
   if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  static const bool tdbg = getenv("MH_BAM_TIMING") != nullptr;   // phase times to stderr (experiments)
+  auto t_now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t_prev = t_now();
+  auto tick = [&](const char *what) {
+    if (!tdbg) return;
+    const double t = t_now();
+    fprintf(stderr, "mh_bam_write_gpu %s %.3f s\n", what, t - t_prev);
+    t_prev = t;
+  };
   MH_TRY(bam_sort(ctx));
+  tick("sort");
   const int64_t n = B.n_rec;
   // the sorted records deflated on the device (k_bgzf_blocks), then only the compressed bytes cross PCIe
   std::vector<int64_t> boff;
   int64_t nz = 0;
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
+  tick("alloc");
   MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
                      (int64_t)ctx->gz_out.cap, &nz, &boff));
+  tick("deflate");
   const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
                                            B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
-  auto fetch = [&](int64_t o, int64_t len, uint8_t *buf) -> bool {
-    return hipMemcpy(buf, z + o, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess;
+  // D2H through a page-locked 64 MiB piece (allocated once per call)
+  uint8_t *pin = nullptr;
+  HIPCHK(ctx, hipHostMalloc((void **)&pin, (size_t)1 << 26, hipHostMallocDefault));
+  auto fetch = [&](int64_t o, int64_t len) -> const uint8_t * {
+    return hipMemcpy(pin, z + o, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess ? pin : nullptr;
   };
   std::vector<int64_t> coff;
   std::string err;
-  if (!bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err)) return arg_fail(ctx, MH_E_ARG, err);
+  const bool wrote = bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err);
+  (void)hipHostFree(pin);
+  if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
+  tick("file");
   if (bai_path) {
     std::vector<int64_t> soff((size_t)n + 1, 0);
     std::vector<BaiRec> info((size_t)n + 1);
     MH_TRY(bam_fetch_sorted(ctx, nullptr, soff.data(), (int32_t *)info.data()));
+    tick("bai fetch");
     if (!bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
       return arg_fail(ctx, MH_E_ARG, err);
+    tick("bai");
   }
   if (out_records) *out_records = n;
   if (out_bytes) *out_bytes = B.bytes;

@@ -135,7 +135,7 @@ bool bgzf_write(const char *path, const std::string &header, const uint8_t *data
 
 bool bgzf_write_blocks(const char *path, const std::string &header, int level, int64_t n_z,
                        const std::vector<int64_t> &boff,
-                       const std::function<bool(int64_t, int64_t, uint8_t *)> &fetch, std::vector<int64_t> &coff,
+                       const std::function<const uint8_t *(int64_t, int64_t)> &fetch, std::vector<int64_t> &coff,
                        std::string &err) {
   FILE *fp = fopen(path, "wb");
   if (!fp) {
@@ -153,12 +153,11 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
   }
   coff.resize(boff.size());
   for (size_t b = 0; b < boff.size(); b++) coff[b] = pos + boff[b];
-  const int64_t piece = (int64_t)1 << 28;
-  std::vector<uint8_t> buf;
+  const int64_t piece = (int64_t)1 << 26;
   for (int64_t o = 0; o < n_z && ok; o += piece) {
     const int64_t m = std::min(piece, n_z - o);
-    buf.resize((size_t)m);
-    ok = fetch(o, m, buf.data()) && fwrite(buf.data(), 1, (size_t)m, fp) == (size_t)m;
+    const uint8_t *buf = fetch(o, m);
+    ok = buf && fwrite(buf, 1, (size_t)m, fp) == (size_t)m;
   }
   ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
   ok = (fclose(fp) == 0) && ok;
@@ -183,11 +182,16 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
       put32(s, 0);
       continue;
     }
-    // bins: runs of consecutive records with the same bin form one chunk; adjacent chunks of a bin merge
-    std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+    // bins: runs of consecutive records with the same bin form one chunk; adjacent chunks of a bin merge.  Indexed by
+    // bin number (at most 37449, SAM spec §5.3), written in ascending order (a std::map per record cost ~4x more)
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> bins(37450);
     std::vector<uint64_t> lin;
     for (int64_t k = i; k < j; k++) {
       const uint64_t vb = voffset(coff, soff[k]), ve = voffset(coff, soff[k + 1]);
+      if (recs[k].bin >= 37450u) {
+        err = "BAI: bin number out of range";
+        return false;
+      }
       auto &ch = bins[recs[k].bin];
       if (!ch.empty() && ch.back().second == vb)
         ch.back().second = ve;
@@ -198,11 +202,14 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
       for (int64_t w = w0; w <= w1; w++)
         if (lin[w] == UINT64_MAX) lin[w] = vb;
     }
-    put32(s, (uint32_t)(bins.size() + 1));
-    for (auto &kv : bins) {
-      put32(s, kv.first);
-      put32(s, (uint32_t)kv.second.size());
-      for (auto &c : kv.second) {
+    uint32_t n_bins = 0;
+    for (const auto &ch : bins) n_bins += ch.empty() ? 0u : 1u;
+    put32(s, n_bins + 1);
+    for (uint32_t b = 0; b < (uint32_t)bins.size(); b++) {
+      if (bins[b].empty()) continue;
+      put32(s, b);
+      put32(s, (uint32_t)bins[b].size());
+      for (auto &c : bins[b]) {
         put64(s, c.first);
         put64(s, c.second);
       }

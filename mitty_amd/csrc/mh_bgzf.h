@@ -28,11 +28,12 @@ bool bgzf_write(const char *path, const std::string &header, const uint8_t *data
                 std::vector<int64_t> &rec_block_coff, std::string &err);
 
 // The same file from data blocks deflated elsewhere (the device, mh_bam_write_gpu): `header` deflated here at `level`
-// in its own block(s), then n_z bytes of ready BGZF blocks fetched in pieces by fetch(offset, len, buf), then the EOF
+// in its own block(s), then n_z bytes of ready BGZF blocks fetched in pieces, then the EOF
 // marker.  boff[b] = offset of data block b inside those bytes (b = 0..nblocks); rec_block_coff as bgzf_write's.
+// fetch(offset, len) returns host bytes [offset, offset + len) (len <= 64 MiB), valid until the next call, or null.
 bool bgzf_write_blocks(const char *path, const std::string &header, int level, int64_t n_z,
                        const std::vector<int64_t> &boff,
-                       const std::function<bool(int64_t, int64_t, uint8_t *)> &fetch,
+                       const std::function<const uint8_t *(int64_t, int64_t)> &fetch,
                        std::vector<int64_t> &rec_block_coff, std::string &err);
 
 // BAI for n sorted records whose data offsets are soff[0..n] (soff[n] = end), given the block map from bgzf_write.
