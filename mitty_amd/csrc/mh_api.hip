@@ -1228,6 +1228,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   std::string err;
   const bool wrote = bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err);
   (void)hipHostFree(pin);
+  release(ctx->gz_out);   // (sized for the whole BAM: not kept beside the next job's buffers)
   if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
   tick("file");
   if (bai_path) {

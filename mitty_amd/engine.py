@@ -17,7 +17,8 @@ RNG_MODES = {'mitty': _native.MH_RNG_MITTY, 'philox': _native.MH_RNG_PHILOX}
 
 class Engine:
   SLOTS_PER_REGION = 64
-  EMIT_SETS = 4         # units prepared ahead of their writers (the library's emission buffer sets)
+  # units prepared ahead of their writers (of the library's 16 emission buffer sets); MH_EMIT_AHEAD: A/B
+  EMIT_SETS = max(1, min(16, int(os.environ.get('MH_EMIT_AHEAD', '4'))))
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
 
   def __init__(self, device=0):
