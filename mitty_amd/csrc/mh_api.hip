@@ -345,7 +345,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
-  release(ctx->d_used); release(ctx->scan_partials_w); release(ctx->rb_tmp);
+  release(ctx->d_used); for (int k = 0; k < 2; k++) { release(ctx->cr_rows[k]); release(ctx->cr_codes[k]); if (ctx->ev_rows[k]) (void)hipEventDestroy(ctx->ev_rows[k]); if (ctx->ev_rfree[k]) (void)hipEventDestroy(ctx->ev_rfree[k]); } release(ctx->scan_partials_w); release(ctx->rb_tmp);
   for (auto &b : ctx->sl2) release(b);
   for (auto &e : ctx->res_ev)
     if (e) (void)hipEventDestroy(e);

@@ -582,6 +582,7 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
 constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
+constexpr int ED_CRB = 15;   // bases per corruption block (CI_BLK)
 constexpr int ED_GMAX = 7;   // window chunks per gather thread (3 threads per mate): up to 21 chunks, rlen <= 321
 
 struct DMeta {
@@ -657,7 +658,7 @@ struct QHead {
 // The output sweeps of a 32-template tile whose strings and metadata are in LDS: LPR lanes per record (record
 // r = file f, template j), passes over the tile's NF * ED_T records.  gbase: arena offset of the tile's first byte per
 // file; span: the tile's bytes per file.
-template <int NF, int LPR, bool CR>
+template <int NF, int LPR, int CR>
 __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64_t gbase[2], const int32_t span[2],
                                           int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena,
                                           int32_t dbg) {
@@ -745,7 +746,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       uint4 v;
-      if (b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
+      if (CR != 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
         v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);   // inside T's '~' run: no LDS read
       } else {
         const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
@@ -796,6 +797,9 @@ struct TArgs {
                             // at once — timing only, the bytes are then wrong; 64 LDS-only barriers instead of full
                             // ones, 128 chunk reads by aligned ds_read_b64, 256 seam chunks stored by the seam
                             // pass (4 KB less LDS per workgroup) (A/B)
+  const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
+  const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * m + template) * nb + block
+  int32_t nb;               // blocks per record row
 };
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
@@ -817,7 +821,7 @@ struct TArgs {
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
-template <int NF, int LPR, bool CR>
+template <int NF, int LPR, int CR>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
@@ -834,11 +838,37 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const bool staged = !(A.dbg & 256);                // seam chunks through LDS (in order with the others)
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
+  // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
+  const int32_t TS = (A.rlen + 4 + 15) / 16 * 16 + 16;
+  const int32_t o_tr = o_dump + 16 + ED_PAD;
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
   const int64_t t0 = tile * ED_T;
   const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
   const int chunks = win_stride / 16;
+  // CR 2: the tile's row slots (file f, template j, block b: slot f * ED_T * nb + j * nb + b), the first RK per thread
+  // loaded before the gathers so they are in flight with them
+  constexpr int RK = 3;
+  const int32_t nb = CR == 2 ? A.nb : 1, nsl = NF * ED_T * nb;
+  auto slot_g = [&](int32_t sl, int *sf, int *sj, int *sb_) -> int64_t {
+    const int f = sl / (ED_T * nb), rem = sl - f * ED_T * nb, j = rem / nb;
+    *sf = f;
+    *sj = j;
+    *sb_ = rem - j * nb;
+    return j < nt ? ((int64_t)f * A.m + t0 + j) * nb + (rem - j * nb) : 0;
+  };
+  uint4 rq[RK];
+  uint32_t rcw[RK];
+  if (CR == 2) {
+#pragma unroll
+    for (int k = 0; k < RK; k++) {
+      int sf, sj, sbk;
+      const int32_t sl = tid + k * ED_THREADS;
+      const int64_t g = sl < nsl ? slot_g(sl, &sf, &sj, &sbk) : 0;
+      rq[k] = A.crow[g];
+      rcw[k] = A.ccode[g];
+    }
+  }
   for (int i = tid; i < TL; i += ED_THREADS)
     smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
   if (tid >= 64 && !(A.dbg & 16)) {
@@ -964,7 +994,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
         const int64_t a2 = s ? h.hap_len - a - S : a;              // mate 1 reads the reverse complement forward
         mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + (int32_t)(a2 & 15);
         mt.S[fr] = S;
-        mt.tb[fr] = o_t;
+        mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
         if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
           mt.qb = qb;
@@ -976,13 +1006,63 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
           for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
         }
       }
-      if (CR && (NF == 2 || fr == 0)) {   // the record's first base, for the corruption pass (S = 0: dropped)
+      if (CR == 1 && (NF == 2 || fr == 0)) {   // the record's first base, for the corruption pass (S = 0: dropped)
         const uint64_t so = (uint64_t)((fr ? g1 : g0) + rel + sb);
         A.crec[tf * NF + fr] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | (uint32_t)(keep ? S : 0));
       }
     }
   }
   if (A.dbg & 64) lds_barrier(); else __syncthreads();   // (dbg 64: LDS-only barriers, measured no faster)
+  if (CR == 2) {
+    // each row slot of a kept record: its qualities into the record's T, its substitutions into the window
+    // (base_rot[b][code - 1], illumina.py:131-136,159-160); block 0 also writes T's separators
+    auto lay = [&](int32_t sl, uint4 q, uint32_t code) {
+      int f, j, b;
+      (void)slot_g(sl, &f, &j, &b);
+      if (j >= nt) return;
+      const DMeta &M = meta[j];
+      if (M.len[f] == 0) return;
+      const int32_t S = M.S[f];
+      char *const T = smem + M.tb[f];
+      if (b == 0) {
+        T[0] = '\n';
+        T[1] = '+';
+        T[2] = '\n';
+        T[3 + S] = '\n';
+      }
+      const int n0 = ED_CRB * b;
+      if (n0 >= S) return;
+      char *const d = T + 3 + n0;
+      if (S - n0 >= ED_CRB) {
+        __builtin_memcpy(d, &q.x, 4);
+        __builtin_memcpy(d + 4, &q.y, 4);
+        __builtin_memcpy(d + 8, &q.z, 4);
+        const uint16_t w2 = (uint16_t)q.w;
+        __builtin_memcpy(d + 12, &w2, 2);
+        d[14] = (char)(q.w >> 16);
+      } else {
+        const int cnt = S - n0;
+        for (int k = 0; k < cnt; k++) d[k] = (char)(u4get(q, k >> 2) >> (8 * (k & 3)));
+        code &= (1u << (2 * cnt)) - 1u;
+      }
+      char *const bs = smem + M.bb[f] + n0;
+      while (code) {
+        const int k = __builtin_ctz(code) >> 1;
+        const uint32_t c = (code >> (2 * k)) & 3u;
+        code &= ~(3u << (2 * k));
+        bs[k] = (char)rot_base((uint8_t)bs[k], c - 1u);
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < RK; k++)
+      if (tid + k * ED_THREADS < nsl) lay(tid + k * ED_THREADS, rq[k], rcw[k]);
+    for (int32_t sl = tid + RK * ED_THREADS; sl < nsl; sl += ED_THREADS) {   // (records of more than 23 blocks)
+      int sf, sj, sbk;
+      const int64_t g = slot_g(sl, &sf, &sj, &sbk);
+      lay(sl, A.crow[g], A.ccode[g]);
+    }
+    __syncthreads();
+  }
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
   if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena, A.dbg);
@@ -991,7 +1071,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
 // waves per SIMD instead of eight — and the launch of 184 k workgroups costs only ~0.35 ms of a 2.6 ms chr1-unit
 // writer (MH_EW_DBG=32), so there is no persistent variant.)
-template <int NF, int LPR, bool CR>
+template <int NF, int LPR, int CR>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
   if (A.dbg & 32) return;   // (experiments: the launch alone)
   emit_tile<NF, LPR, CR>(A, qh, blockIdx.x);
@@ -1351,6 +1431,309 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_inplace(
   }
 }
 
+static_assert(ED_CRB == CI_BLK, "the writer's row blocks are the corruption blocks");
+
+// ---- corruption rows (MH_CR_ROWS=1): the BQ draws before the writer -------------------------------------------
+// k_cr_rows runs the items, stream and decisions of k_cr_inplace over every block of every record up to rlen (a
+// record of S < rlen bases uses the first S: the draws are counted by (template, file, triple), not by S) without
+// touching the arenas: per block one aligned 16-byte row slot (its qualities + 33) and one word of 2-bit
+// substitution codes (choice + 1; 0: the base stays), slot (file * m + template) * NB + block.  The writer
+// (k_emit_tiles<.., 2>) lays the qualities into per-record T strings in LDS and applies the codes to its windows, so
+// the corrupted records leave the writer in its aligned 16-byte stores (no partial-line rewrite afterwards).
+
+// One full block with the tables in LDS (cr_full_block's phases), into registers: qualities packed in qo (byte 15
+// zero), the codes of the substituted bases in *code.
+__device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
+                                              const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
+                                              uint4 *qo, uint32_t *code) {
+  const int n_bq = cc.n_bq;
+  uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], P[CI_BLK], V2[CI_BLK], F[CI_BLK], BQ[CI_BLK];
+  const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
+#pragma unroll
+  for (int g = 0; g < CI_BLK / 3; g++) {
+    const uint4 r = philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
+    W[3 * g] = r.x;
+    W[3 * g + 1] = r.y;
+    W[3 * g + 2] = r.z;
+    RW[g] = r.w;
+  }
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) E[j] = bk[j * CB_ROW + (W[j] >> 24)];
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {
+    const uint16_t *t = tp + j * n_bq + (E[j] & 0x7fu);
+    P[j] = t[0];
+    V2[j] = ((const uint8_t *)t)[3];
+  }
+  uint32_t ps = 0, px = 0;
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {
+    const uint32_t e = E[j], c = e & 0x7fu, fl = e >> 7, pa = P[j];
+    const uint32_t lo = (W[j] >> 16) & 0xffu;
+    const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = V2[j];
+    const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
+    const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
+    const uint32_t amb = b2 | (fl & (uint32_t)(vn == lo));
+    BQ[j] = c + b0 + b1;
+    px |= amb << j;
+    F[j] = fp[BQ[j]];
+  }
+  uint32_t qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0;
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) {
+    const uint32_t amb = (px >> j) & 1u, pth = F[j], h2 = W[j] & 0xffffu;
+    ps |= (uint32_t)(!amb && h2 < pth) << j;
+    px |= (uint32_t)(h2 == pth) << j;
+    const uint32_t qv = (BQ[j] + 33u) << (8 * (j & 3));
+    if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
+  }
+  while (px) {   // rare: the full 53-bit decisions
+    const int j = __builtin_ctz(px);
+    px &= px - 1;
+    const int n = n0 + j;
+    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+    const int k = n % 3;
+    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+    uint32_t amb;
+    const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
+    const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
+                                     w, bq, amb);
+    const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
+    if (j < 4) qd0 = (qd0 & mk) | qv; else if (j < 8) qd1 = (qd1 & mk) | qv; else if (j < 12) qd2 = (qd2 & mk) | qv;
+    else qd3 = (qd3 & mk) | qv;
+    ps |= (x >> 8) << j;
+  }
+  *qo = make_uint4(qd0, qd1, qd2, qd3);
+  uint32_t cd = 0;
+  while (ps) {
+    const int j = __builtin_ctz(ps);
+    ps &= ps - 1;
+    const int g = j / 3, k = j - 3 * g;
+    const uint32_t rw = g == 0 ? RW[0] : g == 1 ? RW[1] : g == 2 ? RW[2] : g == 3 ? RW[3] : RW[4];
+    const uint32_t c10 = (rw >> (10 * k)) & 1023u;
+    uint32_t chv;
+    if (c10 == 1023u)   // rejected: the base's own draw (t, f | 0x8000, n)
+      chv = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3),
+                                   key).x, 3u);
+    else
+      chv = c10 % 3u;
+    cd |= (chv + 1u) << (2 * j);
+  }
+  *code = cd;
+}
+
+template <bool PF, int THR>
+__global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_rows(CiArgs A, uint4 *rows, uint32_t *codes) {
+  // LDS as k_cr_inplace: bucket entries [NT][rlen][CB_ROW] | Fp16[100] | threshold low-byte pairs [NT][rlen][n_bq]
+  extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
+  constexpr int NT = PF ? 1 : 2;
+  const int f_pf = PF ? (int)(blockIdx.x & 1u) : 0;
+  const CorruptCfg &cc = A.cc;
+  const int rlen = A.rlen, n_bq = cc.n_bq;
+  const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
+  const int32_t row_bytes = rlen * CB_ROW;
+  const uint16_t *fp16 = (const uint16_t *)(ctab + NT * row_bytes);
+  const int32_t o_t8 = NT * row_bytes + 256;
+  for (int ft = 0; ft < NT; ft++) {
+    const int f = PF ? f_pf : ft;
+    const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
+    uint4 *dst = (uint4 *)(ctab + ft * row_bytes);
+    for (int i = threadIdx.x; i < row_bytes / 16; i += THR) dst[i] = src[i];
+    const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
+    for (int i = threadIdx.x; i < rlen * n_bq; i += THR) {
+      const int j = i % n_bq;
+      const uint32_t a = t16[i], b = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
+      ((uint16_t *)(ctab + o_t8))[ft * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
+    }
+  }
+  for (int i = threadIdx.x; i < 100; i += THR) ((uint16_t *)fp16)[i] = cc.Fp16[i];
+  __syncthreads();
+  const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
+  const uint2 key = make_uint2(cc.k0, cc.k1);
+  const uint32_t NB = (uint32_t)(rlen + CI_BLK - 1) / CI_BLK;
+  const uint32_t n_items = (uint32_t)(A.m * (PF ? 1 : A.nf)) * NB;
+  const uint32_t stride = (PF ? gridDim.x >> 1 : gridDim.x) * THR;
+  const uint32_t nb_magic = 0xffffffffu / NB + 1u;
+  for (uint32_t i = (PF ? blockIdx.x >> 1 : blockIdx.x) * THR + threadIdx.x; i < n_items; i += stride) {
+    uint32_t uq = __umulhi(i, nb_magic);
+    uq = uq * NB > i ? uq - 1 : uq;
+    const uint32_t rr = PF ? 2u * uq + (uint32_t)f_pf : uq;   // record: template * nf + file
+    const int b = (int)(i - uq * NB), n0 = CI_BLK * b;
+    const int f = A.nf == 2 ? (int)(rr & 1) : 0;
+    const int64_t t = (int64_t)(A.nf == 2 ? rr >> 1 : rr);
+    const int64_t tt = t + cc.t_base;
+    const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
+    const int row0 = (PF ? 0 : f * rlen) + n0;
+    const int cnt = rlen - n0 < CI_BLK ? rlen - n0 : CI_BLK;
+    uint4 qo;
+    uint32_t code;
+    if (cnt == CI_BLK) {
+      cr_block_rows(ctab + row0 * CB_ROW, t8p + row0 * n_bq, fp16, cc, key, tl, th, f, n0, &qo, &code);
+    } else {   // a short last block (rlen not a multiple of 15): the guarded per-base path
+      uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
+#pragma unroll
+      for (int g = 0; g < CI_BLK / 3; g++) {
+        if (3 * g < cnt) {
+          const uint4 r = philox4x32_10(
+              make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            const int j = 3 * g + k;
+            if (j < cnt) {
+              const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+              uint32_t amb;
+              const uint32_t bq = cr_lds_walk(ctab + (row0 + j) * CB_ROW, t8p + (row0 + j) * n_bq, w, &amb);
+              const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
+              const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+              const bool sub = !amb && h2 < pth;
+              px |= (uint32_t)(amb || h2 == pth) << j;
+              ps |= (uint32_t)sub << j;
+              pc |= (uint32_t)(sub && c10 == 1023u) << j;
+              ch |= (c10 % 3u) << (2 * j);
+              qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
+            }
+          }
+        }
+      }
+      while (px) {
+        const int j = __builtin_ctz(px);
+        px &= px - 1;
+        const int n = n0 + j;
+        const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+        const int k = n % 3;
+        const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+        uint32_t amb;
+        const uint32_t bq = cr_lds_walk(ctab + (row0 + j) * CB_ROW, t8p + (row0 + j) * n_bq, w, &amb);
+        const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
+                                         f, n, w, bq, amb);
+        const uint32_t sh = 8u * (uint32_t)(j & 3);
+        qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
+        const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+        ps |= (x >> 8) << j;
+        pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
+      }
+      while (pc) {
+        const int j = __builtin_ctz(pc);
+        pc &= pc - 1;
+        const uint4 c = philox4x32_10(
+            make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
+        ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
+      }
+      code = 0;
+      while (ps) {
+        const int j = __builtin_ctz(ps);
+        ps &= ps - 1;
+        code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
+      }
+      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+    }
+    const int64_t sl = ((int64_t)f * A.m + t) * NB + b;
+    rows[sl] = qo;
+    codes[sl] = code;
+  }
+}
+
+// MH_CR_ROWS=1 (A/B): the corruption rows before the writer instead of the in-place pass after it
+static bool cr_rows_env() {
+  static const bool v = getenv("MH_CR_ROWS") && atoi(getenv("MH_CR_ROWS"));
+  return v;
+}
+// the row pass's LDS (per-file tables, or both files' with one file), 0 when the tables do not fit
+static size_t cr_rows_lds(int32_t nf, int64_t rlen, int32_t n_bq) {
+  const size_t lds = (size_t)(nf == 2 ? 1 : 2) * rlen * (CB_ROW + 2 * n_bq) + 256 + 16;
+  return lds <= 150 * 1024 ? lds : 0;
+}
+
+// the corruption rows of one emission (m templates, nf files) on stream `st`, before its writer
+static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
+                              uint4 *rows, uint32_t *codes) {
+  if (m <= 0) return MH_OK;
+  int ncu = 0;
+  HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  if (ncu <= 0) ncu = 256;
+  const size_t lds = cr_rows_lds(nf, rlen, cc.n_bq);
+  const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
+  if (!lds || m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
+  const bool pf = nf == 2;
+  const int thr = pf ? 512 : CI_THREADS;
+  const int per_cu = pf ? 2 : (lds <= 78 * 1024 ? 2 : 1);
+  // MH_CR_ROWS_GRID: workgroups (A/B; fewer leave room on every CU for the writers beside the pass)
+  static const int64_t g_env = getenv("MH_CR_ROWS_GRID") ? atoll(getenv("MH_CR_ROWS_GRID")) : 0;
+  int64_t grid = std::min<int64_t>(g_env > 0 ? g_env : (int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
+  if (grid < 1) grid = 1;
+  if (pf) grid = (grid + 1) & ~(int64_t)1;
+  CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, nullptr, rlen, nf, 0, cc, 0};
+  stage_begin(ctx, "emit_corrupt_rows");
+  if (pf)
+    hipLaunchKernelGGL((k_cr_rows<true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A, rows, codes);
+  else
+    hipLaunchKernelGGL((k_cr_rows<false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A, rows, codes);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  return MH_OK;
+}
+
+
+// rows mode: the buffers for an emission of m templates (before any stream waits: a reallocation drains the writers)
+static int32_t cr_rows_alloc(mh_ctx *ctx, int64_t m, int32_t nf, int64_t rlen) {
+  const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
+  const int k = ctx->cr_ri;
+  MH_TRY(ensure(ctx, ctx->cr_rows[k], (size_t)(m * nf * NB) * 16 + 64));
+  MH_TRY(ensure(ctx, ctx->cr_codes[k], (size_t)(m * nf * NB) * 4 + 64));
+  return MH_OK;
+}
+// MH_CR_ROWS_SAME=1 (A/B): the row pass on the writer stream, right before its writer
+static bool cr_rows_same() {
+  static const bool v = getenv("MH_CR_ROWS_SAME") && atoi(getenv("MH_CR_ROWS_SAME"));
+  return v;
+}
+// rows mode for this emission: the row pass queued into the current set — on crstream, after the writer that last
+// read the set, so it runs beside the previous unit's writer (compute-bound beside memory-bound) — and the writer
+// stream `st` waiting for it; returns the set, which cr_rows_release marks free after the writer
+static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
+                               TArgs &A) {
+  const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
+  const int k = ctx->cr_ri;
+  if (ctx->cr_rows[k].cap < (size_t)(m * nf * NB) * 16 + 64 || ctx->cr_codes[k].cap < (size_t)(m * nf * NB) * 4 + 64)
+    return arg_fail(ctx, MH_E_STATE, "corruption rows not allocated");
+  uint4 *rows = (uint4 *)ctx->cr_rows[k].p;
+  uint32_t *codes = (uint32_t *)ctx->cr_codes[k].p;
+  if (cr_rows_same()) {
+    MH_TRY(launch_cr_rows(ctx, st, m, nf, rlen, cc, rows, codes));
+  } else {
+    if (!ctx->crstream) {
+      HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->crstream, hipStreamNonBlocking));
+      HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_crw, hipEventDisableTiming));
+    }
+    for (int i = 0; i < 2; i++) {
+      if (!ctx->ev_rows[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_rows[i], hipEventDisableTiming));
+      if (!ctx->ev_rfree[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_rfree[i], hipEventDisableTiming));
+    }
+    if (ctx->rfree_rec[k]) HIPCHK(ctx, hipStreamWaitEvent(ctx->crstream, ctx->ev_rfree[k], 0));
+    hipStream_t ss = ctx->stage_stream;
+    ctx->stage_stream = ctx->crstream;
+    MH_TRY(launch_cr_rows(ctx, ctx->crstream, m, nf, rlen, cc, rows, codes));
+    ctx->stage_stream = ss;
+    HIPCHK(ctx, hipEventRecord(ctx->ev_rows[k], ctx->crstream));
+    HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_rows[k], 0));
+  }
+  A.crow = rows;
+  A.ccode = codes;
+  A.nb = (int32_t)NB;
+  return MH_OK;
+}
+// after the writer that read the current set (queued on `st`): the set is free once it has run; the next unit takes
+// the other set
+static int32_t cr_rows_release(mh_ctx *ctx, hipStream_t st) {
+  const int k = ctx->cr_ri;
+  if (ctx->ev_rfree[k]) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev_rfree[k], st));
+    ctx->rfree_rec[k] = true;
+  }
+  ctx->cr_ri ^= 1;
+  return MH_OK;
+}
+
 // MH_CR_OVERLAP=1: the direct writer's corruption passes run on their own stream beside the next units' writers
 // (one 1024-thread workgroup per CU, so the writers' workgroups fit beside it) instead of after every writer
 static bool cr_overlap() {
@@ -1489,11 +1872,12 @@ static int32_t ed_qpad() {
   static const int v = getenv("MH_EW_QPAD") ? atoi(getenv("MH_EW_QPAD")) : 4;
   return v;
 }
-static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf) {
+static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows = false) {
   const bool staged = !(ew_dbg_env() & 256);   // (256: seam chunks stored by the seam pass, no LDS for them)
+  const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16 + 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
-         (staged ? (size_t)nf * ED_T * 4 * 16 : 0) + 16;
+         (staged ? (size_t)nf * ED_T * 4 * 16 : 0) + 16 + (rows ? ED_PAD + (size_t)nf * ED_T * TS + 16 : 0);
 }
 
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
@@ -1688,7 +2072,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
   const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ed_qpad();
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
+  const bool cr_rows = ctx->corrupt_on && cr_rows_env() && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -1699,6 +2084,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   }
   if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
       cnt_base + m < (int64_t)UINT32_MAX) {
+    if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
     // and the next job's sampling overlap it
     if (!writer_dep) {
@@ -1723,13 +2109,16 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
             qstride, ew_dbg};
-    auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
-                               : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
+    if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
+    auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
+               : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
+                                 : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
+    if (cr_rows) MH_TRY(cr_rows_release(ctx, ctx->wstream));
     stage_end(ctx);
     hipStream_t tail = ctx->wstream;   // the stream whose last work is this unit's last
-    if (ctx->corrupt_on) {
+    if (ctx->corrupt_on && !cr_rows) {
       if (cr_overlap()) {   // the corruption pass on its own stream, beside the next units' writers
         if (!ctx->crstream) {
           HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->crstream, hipStreamNonBlocking));
@@ -1975,7 +2364,8 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
   const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ed_qpad();
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1);
+  const bool cr_rows = ctx->corrupt_on && cr_rows_env() && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
   if (!direct || lds_d > 64 * 1024) {
@@ -2050,6 +2440,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on) cc = corrupt_cfg(ctx, unit_key, 0);
 
+  if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
   hipStream_t ws = ctx->wstream;
   HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));   // the unit's templates (main stream) are ready
   HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
@@ -2070,15 +2461,18 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
           (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride,
           ew_dbg_env()};
-  auto kfn = ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, true> : k_emit_tiles<1, 8, true>)
-                             : (write_fastq2 ? k_emit_tiles<2, 4, false> : k_emit_tiles<1, 8, false>);
+  if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
+  auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
+             : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
+                               : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
+  if (cr_rows) MH_TRY(cr_rows_release(ctx, ws));
   stage_end(ctx);
   // the unit's totals (cnt digits added), its base (the fill before it) and the fill after it
   hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (int64_t *)ctx->d_used.p, (int64_t *)stat, write_fastq2);
   HIPCHK(ctx, hipGetLastError());
-  if (ctx->corrupt_on)
+  if (ctx->corrupt_on && !cr_rows)
     MH_TRY(launch_cr_inplace(ctx, ws, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p, (char *)ctx->out1.p,
                              (char *)ctx->out2.p, write_fastq2 ? 2 : 1, (int32_t)(prefix.size() + mid.size()),
                              (int32_t)rlen, cc, nullptr, true));

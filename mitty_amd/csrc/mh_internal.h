@@ -258,6 +258,12 @@ struct mh_ctx {
   // asynchronous emission (mh_emit_async): measure, offsets, writer and corruption queued on the writer stream; the
   // arena fill lives on the device (d_used) until a call needs it on the host (sync_async_fill)
   mh::DevBuf d_used;                     // int64[2]
+  // corruption rows (MH_CR_ROWS): per block 15 qualities | 2-bit codes; two sets, each unit's row pass on crstream
+  // (after the writer two units back has released the set: ev_rfree) beside the previous unit's writer
+  mh::DevBuf cr_rows[2], cr_codes[2];
+  hipEvent_t ev_rows[2] = {nullptr, nullptr}, ev_rfree[2] = {nullptr, nullptr};
+  bool rfree_rec[2] = {false, false};
+  int cr_ri = 0;
   mh::DevBuf scan_partials_w;            // look-back scratch of the writer stream's scans
   mh::DevBuf rb_tmp;                     // read_part_bound's prefix sums
   bool async_pending = false;            // units queued asynchronously whose fill is not in used1 / used2 yet
