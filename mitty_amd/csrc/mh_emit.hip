@@ -798,7 +798,7 @@ struct TArgs {
                             // ones, 128 chunk reads by aligned ds_read_b64, 256 seam chunks stored by the seam
                             // pass (4 KB less LDS per workgroup) (A/B)
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
-  const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * m + template) * nb + block
+  const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
 };
 
@@ -835,11 +835,13 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_q = o_win + ED_T * 2 * win_stride + ED_PAD;
   const int32_t o_t = o_q + ED_T * qstride + ED_PAD;
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
-  const bool staged = !(A.dbg & 256);                // seam chunks through LDS (in order with the others)
+  // seam chunks through LDS (in order with the others); CR 2 stores them from the seam pass (4 KB less LDS: with the
+  // per-record T strings that is 5 instead of 4 workgroups per CU, 0.77 vs 0.73 G/s on the corrupt bench)
+  const bool staged = !(A.dbg & 256) && CR != 2;
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
-  const int32_t TS = (A.rlen + 4 + 15) / 16 * 16 + 16;
+  const int32_t TS = (A.rlen + 4 + 15) / 16 * 16;   // (a read 16 bytes past a T lands in the next one or the pad)
   const int32_t o_tr = o_dump + 16 + ED_PAD;
   const int tid = threadIdx.x;
   const int Lp = qh.lp, Lm = qh.lm;
@@ -855,7 +857,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     *sf = f;
     *sj = j;
     *sb_ = rem - j * nb;
-    return j < nt ? ((int64_t)f * A.m + t0 + j) * nb + (rem - j * nb) : 0;
+    return j < nt ? ((int64_t)f * nb + (rem - j * nb)) * A.m + t0 + j : 0;
   };
   uint4 rq[RK];
   uint32_t rcw[RK];
@@ -1437,7 +1439,8 @@ static_assert(ED_CRB == CI_BLK, "the writer's row blocks are the corruption bloc
 // k_cr_rows runs the items, stream and decisions of k_cr_inplace over every block of every record up to rlen (a
 // record of S < rlen bases uses the first S: the draws are counted by (template, file, triple), not by S) without
 // touching the arenas: per block one aligned 16-byte row slot (its qualities + 33) and one word of 2-bit
-// substitution codes (choice + 1; 0: the base stays), slot (file * m + template) * NB + block.  The writer
+// substitution codes (choice + 1; 0: the base stays), slot (file * NB + block) * m + template (column-major: a
+// tile's 32 slots of one block are contiguous, and k_cr_cols writes whole lines).  The writer
 // (k_emit_tiles<.., 2>) lays the qualities into per-record T strings in LDS and applies the codes to its windows, so
 // the corrupted records leave the writer in its aligned 16-byte stores (no partial-line rewrite afterwards).
 
@@ -1627,15 +1630,121 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_rows(CiA
       }
       qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
     }
-    const int64_t sl = ((int64_t)f * A.m + t) * NB + b;
+    const int64_t sl = ((int64_t)f * NB + b) * A.m + t;   // column-major: slot (file, block, template)
     rows[sl] = qo;
     codes[sl] = code;
   }
 }
 
-// MH_CR_ROWS=1 (A/B): the corruption rows before the writer instead of the in-place pass after it
+// Position-major row pass (default for MH_CR_ROWS): a workgroup per (block column, template chunk) stages only its
+// column's tables (bucket rows and threshold pairs of 15 positions of one file: 6.7 KB instead of 67 KB), so
+// occupancy is bound by registers, not LDS; its threads take consecutive templates, so the slots it writes are
+// contiguous.  Same draws and decisions as k_cr_rows.
+constexpr int CC_THREADS = 256;
+template <int MW>   // MW: waves per SIMD the register budget is sized for (1: the compiler's choice, 8: <= 64 VGPRs)
+__global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes, int32_t per_wg) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
+  const CorruptCfg &cc = A.cc;
+  const int rlen = A.rlen, n_bq = cc.n_bq;
+  const int NB = (rlen + CI_BLK - 1) / CI_BLK;
+  const int col = (int)blockIdx.y, f = col / NB, b = col - f * NB, n0 = CI_BLK * b;
+  const int cnt = rlen - n0 < CI_BLK ? rlen - n0 : CI_BLK;
+  const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
+  // LDS: bucket rows [15][CB_ROW] | Fp16[100] (256 B) | threshold low-byte pairs [15][n_bq] (+16)
+  const int32_t o_fp = CI_BLK * CB_ROW, o_t8 = o_fp + 256;
+  {
+    const uint4 *src = (const uint4 *)(cc.bk + ((int64_t)f * cc.max_bp + n0) * CB_ROW);
+    uint4 *dst = (uint4 *)ctab;
+    for (int i = threadIdx.x; i < cnt * CB_ROW / 16; i += CC_THREADS) dst[i] = src[i];
+    const uint16_t *t16 = cc.T16 + ((int64_t)f * cc.max_bp + n0) * n_bq;
+    for (int i = threadIdx.x; i < cnt * n_bq; i += CC_THREADS) {
+      const int j = i % n_bq;
+      const uint32_t a = t16[i], c = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
+      ((uint16_t *)(ctab + o_t8))[i] = (uint16_t)((a & 0xffu) | ((c >> 8) == (a >> 8) ? (c & 0xffu) << 8 : 0xff00u));
+    }
+    for (int i = threadIdx.x; i < 100; i += CC_THREADS) ((uint16_t *)(ctab + o_fp))[i] = cc.Fp16[i];
+  }
+  __syncthreads();
+  const uint8_t *bk = ctab;
+  const uint16_t *fp16 = (const uint16_t *)(ctab + o_fp);
+  const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
+  const uint2 key = make_uint2(cc.k0, cc.k1);
+  const int64_t tb = (int64_t)blockIdx.x * per_wg, te = tb + per_wg < A.m ? tb + per_wg : A.m;
+  uint4 *const orow = rows + (int64_t)col * A.m;
+  uint32_t *const ocode = codes + (int64_t)col * A.m;
+  for (int64_t t = tb + threadIdx.x; t < te; t += CC_THREADS) {
+    const int64_t tt = t + cc.t_base;
+    const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
+    uint4 qo;
+    uint32_t code;
+    if (cnt == CI_BLK) {
+      cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
+    } else {   // a short last block: the guarded per-base path (k_cr_rows')
+      uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
+#pragma unroll
+      for (int g = 0; g < CI_BLK / 3; g++) {
+        if (3 * g < cnt) {
+          const uint4 r = philox4x32_10(
+              make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            const int j = 3 * g + k;
+            if (j < cnt) {
+              const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+              uint32_t amb;
+              const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+              const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
+              const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+              const bool sub = !amb && h2 < pth;
+              px |= (uint32_t)(amb || h2 == pth) << j;
+              ps |= (uint32_t)sub << j;
+              pc |= (uint32_t)(sub && c10 == 1023u) << j;
+              ch |= (c10 % 3u) << (2 * j);
+              qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
+            }
+          }
+        }
+      }
+      while (px) {
+        const int j = __builtin_ctz(px);
+        px &= px - 1;
+        const int n = n0 + j;
+        const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+        const int k = n % 3;
+        const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+        uint32_t amb;
+        const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+        const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
+                                         f, n, w, bq, amb);
+        const uint32_t sh = 8u * (uint32_t)(j & 3);
+        qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
+        const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+        ps |= (x >> 8) << j;
+        pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
+      }
+      while (pc) {
+        const int j = __builtin_ctz(pc);
+        pc &= pc - 1;
+        const uint4 c = philox4x32_10(
+            make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
+        ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
+      }
+      code = 0;
+      while (ps) {
+        const int j = __builtin_ctz(ps);
+        ps &= ps - 1;
+        code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
+      }
+      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+    }
+    orow[t] = qo;
+    ocode[t] = code;
+  }
+}
+
+// the corruption rows before the writer (default) instead of the in-place pass after it (MH_CR_ROWS=0)
 static bool cr_rows_env() {
-  static const bool v = getenv("MH_CR_ROWS") && atoi(getenv("MH_CR_ROWS"));
+  static const bool v = !(getenv("MH_CR_ROWS") && atoi(getenv("MH_CR_ROWS")) == 0);
   return v;
 }
 // the row pass's LDS (per-file tables, or both files' with one file), 0 when the tables do not fit
@@ -1664,7 +1773,17 @@ static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf
   if (pf) grid = (grid + 1) & ~(int64_t)1;
   CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, nullptr, rlen, nf, 0, cc, 0};
   stage_begin(ctx, "emit_corrupt_rows");
-  if (pf)
+  // MH_CR_COLS=0 (A/B): the record-major k_cr_rows instead of the position-major k_cr_cols
+  static const bool cols = !(getenv("MH_CR_COLS") && atoi(getenv("MH_CR_COLS")) == 0);
+  static const int32_t per_wg = getenv("MH_CR_COLS_PER") ? atoi(getenv("MH_CR_COLS_PER")) : 16 * CC_THREADS;
+  if (cols) {
+    const size_t lds_c = (size_t)CI_BLK * CB_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
+    const int64_t gx = (m + per_wg - 1) / per_wg;
+    if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
+    static const int mw = getenv("MH_CR_COLS_MW") ? atoi(getenv("MH_CR_COLS_MW")) : 1;   // (A/B)
+    hipLaunchKernelGGL(mw == 8 ? k_cr_cols<8> : k_cr_cols<1>, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS),
+                       lds_c, st, A, rows, codes, per_wg);
+  } else if (pf)
     hipLaunchKernelGGL((k_cr_rows<true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A, rows, codes);
   else
     hipLaunchKernelGGL((k_cr_rows<false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A, rows, codes);
@@ -1682,9 +1801,10 @@ static int32_t cr_rows_alloc(mh_ctx *ctx, int64_t m, int32_t nf, int64_t rlen) {
   MH_TRY(ensure(ctx, ctx->cr_codes[k], (size_t)(m * nf * NB) * 4 + 64));
   return MH_OK;
 }
-// MH_CR_ROWS_SAME=1 (A/B): the row pass on the writer stream, right before its writer
+// the row pass on the writer stream, right before its writer (default), or on crstream beside the previous unit's
+// writer (MH_CR_ROWS_OVERLAP=1, A/B: within noise of the default)
 static bool cr_rows_same() {
-  static const bool v = getenv("MH_CR_ROWS_SAME") && atoi(getenv("MH_CR_ROWS_SAME"));
+  static const bool v = !(getenv("MH_CR_ROWS_OVERLAP") && atoi(getenv("MH_CR_ROWS_OVERLAP")));
   return v;
 }
 // rows mode for this emission: the row pass queued into the current set — on crstream, after the writer that last
@@ -1873,8 +1993,8 @@ static int32_t ed_qpad() {
   return v;
 }
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows = false) {
-  const bool staged = !(ew_dbg_env() & 256);   // (256: seam chunks stored by the seam pass, no LDS for them)
-  const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16 + 16);   // CR 2: a T per record (emit_tile)
+  const bool staged = !(ew_dbg_env() & 256) && !rows;   // (256: seam chunks stored by the seam pass, no LDS for them)
+  const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
          (staged ? (size_t)nf * ED_T * 4 * 16 : 0) + 16 + (rows ? ED_PAD + (size_t)nf * ED_T * TS + 16 : 0);

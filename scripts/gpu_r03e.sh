@@ -1,26 +1,28 @@
 #!/bin/bash
-# Epoch look-back scans + batch-wide permutation: the GPU suite, then the WGS bench (batch / phased-sync), the chr1
-# bench, and the writer's launch-only floor (MH_EW_DBG=32).
+# Corruption rows as the default (position-major row pass on the writer stream, seams stored by the seam pass):
+# GPU suite + smoke on the defaults, the in-place pass (MH_CR_ROWS=0) under the corrupt tests, chr1-corrupt A/B,
+# kernel stats, and a WGS check.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 T=${TAG:-r03e}
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_$T.log 2>&1
-rc=$?
-echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_$T.log
-[ $rc -eq 0 ] || exit $rc
-run() {   # name, env..., bench args after --
-  local n=$1; shift
-  timeout -k 10 300 env "$@" > gpurun_out/bench_${T}_$n.json 2> gpurun_out/bench_${T}_$n.err || return $?
-  python3 -c "import json; d=json.load(open('gpurun_out/bench_${T}_$n.json')); print('$n', round(d['value']/1e9,3), round(d['ms_per_step'],2), 'writer', round(d['roofline']['avg_launch_ms'],3), round(d['roofline']['frac'],3), {k: d['stage_ms'][k] for k in list(d['stage_ms'])[:8]})"
-}
-run wgs python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e || exit $?
-run wgs_phs python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --pipeline phased-sync || exit $?
-run chr1 python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
-run chr1_unitperm MH_PERM_UNIT=1 python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
-run d32 MH_STAGE_WAIT=1 MH_EW_DBG=32 python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
-for k in 4 6 8; do
-  run p$k MH_STAGE_WAIT=1 MH_EW_PERSIST=$k python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_${T}.log 2>&1 || { tail -40 gpurun_out/pytest_${T}.log; exit 1; }
+tail -2 gpurun_out/pytest_${T}.log
+MH_CR_ROWS=0 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "corrupt or Corrupt" --timeout 120 --timeout-method thread > gpurun_out/pytest_${T}_inplace.log 2>&1 || { tail -40 gpurun_out/pytest_${T}_inplace.log; exit 1; }
+tail -2 gpurun_out/pytest_${T}_inplace.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_${T}.log 2>&1 || { tail -20 gpurun_out/smoke_${T}.log; exit 1; }
+tail -1 gpurun_out/smoke_${T}.log
+for p in 1 0 ov 1 0 ov; do
+  case $p in 1) E="MH_CR_ROWS=1";; 0) E="MH_CR_ROWS=0";; ov) E="MH_CR_ROWS_OVERLAP=1";; esac
+  env $E timeout -k 10 200 python -u bench.py --workload chr1 --corrupt --steps 4 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/bench_${T}_$p.json 2>gpurun_out/bench_${T}_$p.err || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_${T}_$p.json')); print('chr1 corrupt $p', round(d['value']/1e9,3), round(d['ms_per_step'],2), 'writer', round(d['roofline']['avg_launch_ms'],3))"
 done
-run p0 MH_STAGE_WAIT=1 python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
-run b64 MH_STAGE_WAIT=1 MH_EW_DBG=64 python -u bench.py --workload chr1 --steps 6 --warmup 2 --no-cpu-baseline --no-e2e || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${T} -o run -- python3 bench.py --workload chr1 --corrupt --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/${T}_prof.json 2>gpurun_out/${T}_prof.err || exit $?
+python3 - gpurun_out/prof_${T}/run_kernel_stats.csv <<'PY'
+import csv,sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:5]:
+  print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e6,3))
+PY
+timeout -k 10 300 python -u bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-e2e > gpurun_out/bench_${T}_wgs.json 2>gpurun_out/bench_${T}_wgs.err || exit $?
+python3 -c "import json; d=json.load(open('gpurun_out/bench_${T}_wgs.json')); print('wgs', round(d['value']/1e9,3), round(d['ms_per_step'],2), 'writer', round(d['roofline']['avg_launch_ms'],3))"
