@@ -131,16 +131,20 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
 
 
 def corrupt_roofline(stages, kept, b1, b2, rlen):
-  """The corruption pass (k_cr_recs + k_cr_inplace, stage 'emit_corrupt' timed by HIP events on the writer stream).
-  Algorithmic bytes: per base one read (the block's bases) and one quality written, the substituted bases written
-  back (4.7 % of the bases under hiseq-X-v2.5-Garvan), 8 bytes of record word read and one '\n' per record; it is
-  bound by VALU issue (Philox rounds and the table walk: profiles/pmc_k_cr_inplace_r02.json), not by HBM."""
-  ms = sum(v for k, v in stages if k == 'emit_corrupt')
-  n = sum(1 for k, _ in stages if k == 'emit_corrupt')
+  """The corruption pass, timed by HIP events on the writer stream.  Default (corruption rows): k_cr_cols, stage
+  'emit_corrupt_rows', before each writer — per 15-base block one 16-byte row slot and one 4-byte code word written
+  (20 B per 15 bases); the writer (stage 'emit_write') lays them into the records.  MH_CR_ROWS=0: k_cr_recs +
+  k_cr_inplace, stage 'emit_corrupt', after each writer — per base one read (the block's bases) and one quality
+  written, the substituted bases written back (4.7 % under hiseq-X-v2.5-Garvan), 8 bytes of record word read and one
+  '\n' per record.  Either is bound by VALU issue (Philox rounds and the table walk), not by HBM."""
+  rows = any(k == 'emit_corrupt_rows' for k, _ in stages)
+  name = 'emit_corrupt_rows' if rows else 'emit_corrupt'
+  ms = sum(v for k, v in stages if k == name)
+  n = sum(1 for k, _ in stages if k == name)
   bases = 2 * rlen * kept   # (upper bound: reads cut by the haplotype end are shorter)
-  alg = bases * (2 + 0.047) + 2 * kept * 9
+  alg = bases * 20 / 15 if rows else bases * (2 + 0.047) + 2 * kept * 9
   gbs = alg / (ms * 1e-3) / 1e9 if ms > 0 else None
-  return {'kernel': 'k_cr_inplace', 'bound': 'valu', 'avg_launch_ms': ms / max(n, 1),
+  return {'kernel': 'k_cr_cols' if rows else 'k_cr_inplace', 'bound': 'valu', 'avg_launch_ms': ms / max(n, 1),
           'algorithmic_bytes_per_launch': alg / max(n, 1), 'achieved_gbs': gbs,
           'hbm_frac': gbs / PEAK_HBM_GBS if gbs else None,
           'bases_per_s': bases / (ms * 1e-3) if ms > 0 else None}

@@ -2224,12 +2224,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     }
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
-    stage_begin(ctx, "emit_write");
     const int ew_dbg = ew_dbg_env();
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
             qstride, ew_dbg};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
+    stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
     auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
                : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
                                  : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
@@ -2577,11 +2577,11 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   HIPCHK(ctx, device_scan_sum<E3>(ws, ntiles, LoadTile{(const int4 *)es.tsum.p, ntiles}, StoreTile{(E3 *)es.tpre.p},
                                   ctx->scan_partials_w.p, (E3 *)stat));
   stage_end(ctx);
-  stage_begin(ctx, "emit_write");
   TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
           (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride,
           ew_dbg_env()};
   if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
+  stage_begin(ctx, "emit_write");
   auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
              : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
                                : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);

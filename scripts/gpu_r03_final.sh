@@ -23,3 +23,7 @@ KT=$(find gpurun_out/final/prof_$T -name '*kernel_trace.csv' | head -1)
 python3 scripts/wgs_gaps.py "$KT" > gpurun_out/final/gaps_$T.txt 2>&1
 gzip -f "$KT"
 echo done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/final/prof_cr_$T -o run -- \
+  python3 bench.py --workload chr1 --corrupt --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/final/prof_cr_bench_$T.log 2>&1 || exit $?
+gzip -f gpurun_out/final/prof_cr_$T/run_kernel_trace.csv
+echo done corrupt stats
