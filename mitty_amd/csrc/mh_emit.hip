@@ -1525,6 +1525,80 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
   *code = cd;
 }
 
+// The same block one triple draw at a time (three bases per phase: fewer live registers, so more waves hide the
+// LDS latency instead of fifteen reads in flight per wave).  Same outputs as cr_block_rows.
+__device__ __forceinline__ void cr_block_rows3(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
+                                               const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
+                                               uint4 *qo, uint32_t *code) {
+  const int n_bq = cc.n_bq;
+  const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
+  uint32_t qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0, ps = 0, px = 0, rws[CI_BLK / 3];
+#pragma unroll
+  for (int g = 0; g < CI_BLK / 3; g++) {
+    const uint4 r = philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
+    rws[g] = r.w;
+    const uint32_t W[3] = {r.x, r.y, r.z};
+    uint32_t E[3], P[3], V2[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) E[k] = bk[(3 * g + k) * CB_ROW + (W[k] >> 24)];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint16_t *t = tp + (3 * g + k) * n_bq + (E[k] & 0x7fu);
+      P[k] = t[0];
+      V2[k] = ((const uint8_t *)t)[3];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int j = 3 * g + k;
+      const uint32_t e = E[k], c = e & 0x7fu, fl = e >> 7, pa = P[k];
+      const uint32_t lo = (W[k] >> 16) & 0xffu;
+      const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = V2[k];
+      const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
+      const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
+      const uint32_t amb = b2 | (fl & (uint32_t)(vn == lo));
+      const uint32_t bq = c + b0 + b1;
+      const uint32_t pth = fp[bq], h2 = W[k] & 0xffffu;
+      ps |= (uint32_t)(!amb && h2 < pth) << j;
+      px |= (amb | (uint32_t)(h2 == pth)) << j;
+      const uint32_t qv = (bq + 33u) << (8 * (j & 3));
+      if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
+    }
+  }
+  while (px) {   // rare: the full 53-bit decisions
+    const int j = __builtin_ctz(px);
+    px &= px - 1;
+    const int n = n0 + j;
+    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+    const int k = n % 3;
+    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+    uint32_t amb;
+    const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
+    const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
+                                     w, bq, amb);
+    const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
+    if (j < 4) qd0 = (qd0 & mk) | qv; else if (j < 8) qd1 = (qd1 & mk) | qv; else if (j < 12) qd2 = (qd2 & mk) | qv;
+    else qd3 = (qd3 & mk) | qv;
+    ps = (ps & ~(1u << j)) | ((x >> 8) << j);
+  }
+  *qo = make_uint4(qd0, qd1, qd2, qd3);
+  uint32_t cd = 0;
+  while (ps) {
+    const int j = __builtin_ctz(ps);
+    ps &= ps - 1;
+    const int g = j / 3, k = j - 3 * g;
+    const uint32_t rw = g == 0 ? rws[0] : g == 1 ? rws[1] : g == 2 ? rws[2] : g == 3 ? rws[3] : rws[4];
+    const uint32_t c10 = (rw >> (10 * k)) & 1023u;
+    uint32_t chv;
+    if (c10 == 1023u)
+      chv = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3),
+                                   key).x, 3u);
+    else
+      chv = c10 % 3u;
+    cd |= (chv + 1u) << (2 * j);
+  }
+  *code = cd;
+}
+
 template <bool PF, int THR>
 __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_rows(CiArgs A, uint4 *rows, uint32_t *codes) {
   // LDS as k_cr_inplace: bucket entries [NT][rlen][CB_ROW] | Fp16[100] | threshold low-byte pairs [NT][rlen][n_bq]
@@ -1641,7 +1715,8 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_rows(CiA
 // occupancy is bound by registers, not LDS; its threads take consecutive templates, so the slots it writes are
 // contiguous.  Same draws and decisions as k_cr_rows.
 constexpr int CC_THREADS = 256;
-template <int MW>   // MW: waves per SIMD the register budget is sized for (1: the compiler's choice, 8: <= 64 VGPRs)
+template <int MW, bool G3>   // MW: waves per SIMD the register budget is sized for (1: the compiler's choice, 8: <= 64
+                            // VGPRs); G3: cr_block_rows3 (a triple draw at a time)
 __global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes, int32_t per_wg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
   const CorruptCfg &cc = A.cc;
@@ -1678,7 +1753,8 @@ __global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *row
     uint4 qo;
     uint32_t code;
     if (cnt == CI_BLK) {
-      cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
+      if (G3) cr_block_rows3(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
+      else cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
     } else {   // a short last block: the guarded per-base path (k_cr_rows')
       uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
 #pragma unroll
@@ -1781,8 +1857,9 @@ static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf
     const int64_t gx = (m + per_wg - 1) / per_wg;
     if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
     static const int mw = getenv("MH_CR_COLS_MW") ? atoi(getenv("MH_CR_COLS_MW")) : 1;   // (A/B)
-    hipLaunchKernelGGL(mw == 8 ? k_cr_cols<8> : k_cr_cols<1>, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS),
-                       lds_c, st, A, rows, codes, per_wg);
+    static const int g3 = getenv("MH_CR_COLS_G3") ? atoi(getenv("MH_CR_COLS_G3")) : 0;   // (A/B)
+    auto kc = g3 ? (mw == 8 ? k_cr_cols<8, true> : k_cr_cols<1, true>) : (mw == 8 ? k_cr_cols<8, false> : k_cr_cols<1, false>);
+    hipLaunchKernelGGL(kc, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS), lds_c, st, A, rows, codes, per_wg);
   } else if (pf)
     hipLaunchKernelGGL((k_cr_rows<true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A, rows, codes);
   else
