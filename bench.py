@@ -266,7 +266,7 @@ def run_chr1(a):
 
   dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
   eng.close()
-  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps)
+  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps, 'chr1_corrupt' if a.corrupt else 'chr1')
   if a.stages:
     print(json.dumps(stage_ms), file=sys.stderr)
   corrupt_pass = None
