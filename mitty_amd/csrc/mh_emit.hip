@@ -1919,9 +1919,10 @@ static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t n
   A.nb = (int32_t)NB;
   return MH_OK;
 }
-// after the writer that read the current set (queued on `st`): the set is free once it has run; the next unit takes
-// the other set
+// after the writer that read the current set (queued on `st`): the set is free once it has run; with the row pass on
+// crstream the next unit takes the other set (on the writer stream one set serves every unit, in stream order)
 static int32_t cr_rows_release(mh_ctx *ctx, hipStream_t st) {
+  if (cr_rows_same()) return MH_OK;
   const int k = ctx->cr_ri;
   if (ctx->ev_rfree[k]) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_rfree[k], st));
