@@ -38,6 +38,12 @@ sys.path.insert(0, REPO)
 
 CHR1 = 249_250_621
 PEAK_HBM_GBS = 8000.0
+# stage timers that bracket other stages and cross streams (their intervals include queue waits behind earlier work):
+# reported apart from the per-stage times
+SPANS = ('emit', 'sample', 'splice')
+STAGE_NOTE = ('stage_ms: per step, each stage = HIP events recorded on its own stream around its kernels (kernel '
+              'time plus launch gaps; stages on different streams overlap, so they sum past ms_per_step); span_ms: '
+              'the outer spans, which start on one stream and end on another and include queue waits')
 METRIC = 'paired 2x150bp reads/sec at 30x WGS, 1/2/4/8 MI355X; qname POS/CIGAR bit-exact'
 
 
@@ -53,7 +59,16 @@ def parse():
   ap.add_argument('--rng', default='mitty', choices=['mitty', 'philox'])
   ap.add_argument('--corrupt', action='store_true', help='fused BQ corruption (BASELINE configs[2])')
   ap.add_argument('--cpu-baseline-mbp', type=float, default=100.0,
-                  help='bounded CPU-oracle sample: the job\'s units on the first N Mbp of the contig (0 = skip)')
+                  help='chr1 leg of the CPU baseline: the chr1 job\'s units on the first N Mbp of the contig (0 = skip)')
+  ap.add_argument('--cpu-baseline-frac', type=float, default=0.25,
+                  help='WGS leg of the CPU baseline: all 100 work units, each on the first FRAC of its region '
+                       '(0 = skip)')
+  ap.add_argument('--cpu-workers', type=int, default=16,
+                  help='CPU baseline worker processes (the reference\'s --threads; 16 = the GPU box\'s CPU share '
+                       'for one GPU)')
+  ap.add_argument('--verify', action='store_true',
+                  help='wgs, N = 1: after the timed steps, run one more step unit by unit and compare every unit\'s '
+                       'FASTQ bytes (sha256 of its arena range, both files) with the CPU oracle\'s digests')
   ap.add_argument('--no-cpu-baseline', action='store_true')
   ap.add_argument('--no-e2e', action='store_true', help='skip the end-to-end (files in, /dev/null out) leg')
   ap.add_argument('--e2e-gz', action=argparse.BooleanOptionalAction, default=True,
@@ -122,12 +137,20 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
       traffic = d.get('hbm_bytes_per_launch')
       traffic_src = os.path.relpath(path, REPO)
       break
-  stage_ms = {k: round(v[0] / steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])}
+  stage_ms = {k: round(v[0] / steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1][0])
+              if k not in SPANS}
+  span_ms = {k: round(v[0] / steps, 3) for k, v in agg.items() if k in SPANS}
+  hap_bytes = 2 * rlen * kept                                   # haplotype bases gathered (the read side alone)
+  read_gbs = hap_bytes / (ew_ms * 1e-3) / 1e9 if ew_ms > 0 else None
   return {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
           'frac': (achieved / PEAK_HBM_GBS) if achieved else None, 'traffic': traffic,
-          'traffic_source': ('PMC passes of the same config, ' + traffic_src) if traffic_src else None,
+          'traffic_source': ('PMC passes (FETCH_SIZE, WRITE_SIZE) of this workload, ' + traffic_src)
+                            if traffic_src else None,
           'algorithmic_bytes_per_launch': alg_bytes / max(ew_n, 1),
-          'avg_launch_ms': ew_ms / max(ew_n, 1)}, stage_ms
+          'avg_launch_ms': ew_ms / max(ew_n, 1),
+          'read_bytes_per_launch': hap_bytes / max(ew_n, 1),
+          'read_only_achieved': read_gbs,
+          'read_only_frac': read_gbs / PEAK_HBM_GBS if read_gbs else None}, stage_ms, span_ms
 
 
 def corrupt_roofline(stages, kept, b1, b2, rlen):
@@ -266,7 +289,8 @@ def run_chr1(a):
 
   dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
   eng.close()
-  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps, 'chr1_corrupt' if a.corrupt else 'chr1')
+  roof, stage_ms, span_ms = roofline(stages, kept, b1, b2, rlen, kernel, a.steps,
+                                     'chr1_corrupt' if a.corrupt else 'chr1')
   if a.stages:
     print(json.dumps(stage_ms), file=sys.stderr)
   corrupt_pass = None
@@ -305,6 +329,8 @@ def run_chr1(a):
     'cpu_baseline': cpu,
     'end_to_end': e2e,
     'stage_ms': stage_ms,
+    'span_ms': span_ms,
+    'stage_note': STAGE_NOTE,
     'fastq_bytes_per_template': (b1 + b2) / max(kept, 1),
     'host_cpus': os.cpu_count(),
   }
@@ -462,7 +488,9 @@ def run_genome(a, rank, world, local):
   """The metric's workload at any N: whole synthetic GRCh37, the reference's unit list dealt to the ranks by LPT
   (mitty_amd.distributed.plan_pieces), every unit sampled and emitted by its owner, output in HBM (arenas recycled
   per batch), an all-reduce of the counts closing each step."""
-  if world > 1:
+  # a process group at N > 1, and at N = 1 when MH_DIST_BACKEND names one (the RCCL path exercised on one GPU)
+  use_pg = world > 1 or bool(os.environ.get('MH_DIST_BACKEND'))
+  if use_pg:
     # torch before libmitty_hip: a process holds ONE HIP runtime, and whichever library loads first provides it
     # (ours needs libamdhip64.so.7, which torch's copy satisfies; torch's own libamdhip64.so would not reuse ours)
     import torch  # noqa: F401
@@ -489,9 +517,18 @@ def run_genome(a, rank, world, local):
   t_synth = time.perf_counter() - t_synth
 
   dist = None
-  if world > 1:
+  if use_pg:
     import torch
     import torch.distributed as tdist
+    if world == 1:   # no launcher: a one-rank group on this host
+      os.environ.setdefault('RANK', '0')
+      os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+      if 'MASTER_PORT' not in os.environ:
+        import socket
+        with socket.socket() as sk:
+          sk.bind(('127.0.0.1', 0))
+          os.environ['MASTER_PORT'] = str(sk.getsockname()[1])
+      os.environ['WORLD_SIZE'] = '1'
     local = local % max(1, torch.cuda.device_count())   # rehearsals: several ranks on one GPU
     torch.cuda.set_device(local)
     # MH_DIST_BACKEND=gloo: rehearsal of the multi-rank plan with several ranks on one GPU (RCCL needs one per GPU)
@@ -584,6 +621,11 @@ def run_genome(a, rank, world, local):
 
   steps, warmup = a.steps, a.warmup
   dt, kept, b1, b2, stages = timed(step, steps, warmup, eng, dist)
+  verify = None
+  if a.verify:
+    if world != 1 or a.plan_share or a.rng != 'mitty':
+      sys.exit('bench.py: --verify is the N = 1, rng=mitty WGS line')
+    verify = verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model)
   eng.close()
   kept_all, b1_all, b2_all, n_units = kept, b1, b2, len(mine)
   backend, seen = None, 1
@@ -596,16 +638,23 @@ def run_genome(a, rank, world, local):
     kept_all, b1_all, b2_all, n_units = (int(x) for x in c.tolist())
     backend, seen = dist.get_backend(), dist.get_world_size()
   workload = 'wgs' if a.genome_scale == 1 else None
-  roof, stage_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload)
+  roof, stage_ms, span_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload)
   cpu = e2e = None
   if world == 1 and not a.plan_share:
     seq1, recs1, _ = data[0]
     if not a.no_e2e and a.genome_scale == 1 and a.rng == 'mitty':
       e2e = end_to_end(a, seq1, recs1, model, None)
-    if not a.no_cpu_baseline and a.cpu_baseline_mbp > 0:
-      cpu = cpu_baseline(a, seq1, recs1, p, rlen, model, _native.work_units(a.seed, [2], passes))
+    if not a.no_cpu_baseline:
+      legs = {}
+      if a.cpu_baseline_frac > 0:
+        legs['wgs'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model)
+      if a.cpu_baseline_mbp > 0:
+        legs['chr1'] = cpu_baseline(a, seq1, recs1, p, rlen, model, _native.work_units(a.seed, [2], passes))
       if a.cpu_config0:
-        cpu['configs0'] = cpu_baseline_config0(a, data)
+        legs['configs0'] = cpu_baseline_config0(a, data)
+      cpu = legs.pop('wgs', None) or legs.pop('chr1', None)   # the metric's workload when it ran
+      if cpu is not None:
+        cpu.update(legs)
   if dist is not None:
     dist.destroy_process_group()
   if rank != 0:
@@ -637,9 +686,12 @@ def run_genome(a, rank, world, local):
                'world_size_seen': seen, 'collective_backend': backend},
     'roofline': roof,
     'roofline_rank': 0,
+    'verify': verify,
     'cpu_baseline': cpu,
     'end_to_end': e2e,
     'stage_ms': stage_ms,
+    'span_ms': span_ms,
+    'stage_note': STAGE_NOTE,
     'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
     'setup_s': {'synth_inputs': round(t_synth, 2)},
     'host_cpus': os.cpu_count(),
@@ -651,35 +703,167 @@ def run_genome(a, rank, world, local):
   print(json.dumps(out), flush=True)
 
 
-def _cpu_unit(args):
-  """One work unit through the CPU oracle in a worker process; returns (templates, start, end) wall-clock stamps."""
-  ref, soa, p, rlen, cum_tlen, seed, stub, cpy = args
+def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
+  """One more step of the bench's own plan (same batches, engine and arenas), unit by unit: every unit's two FASTQ
+  ranges fetched from the arenas before the next batch recycles them and hashed (sha256), against the CPU oracle's
+  digests of the same unit (readgenerate.py:129-159 unit list, seeds and order; the oracle computes them in
+  --cpu-workers processes while the GPU runs).  Untimed; fails the run on the first differing unit."""
+  import hashlib
+  import threading
+  from concurrent.futures import ThreadPoolExecutor
   sys.path.insert(0, REPO)
   from oracle import oracle as O
+  t0 = time.perf_counter()
+  workers = max(1, min(a.cpu_workers, os.cpu_count() or 1))
+  d = tempfile.mkdtemp(prefix='mh_verify_', dir='/dev/shm' if os.path.isdir('/dev/shm') else None)
+  img = os.path.join(d, 'ref.bin')
+  offs = {}
+  try:
+    with open(img, 'wb') as fp:
+      for ri in sorted({u[0] for u in units}):
+        offs[ri] = (fp.tell(), len(data[ri][0]))
+        fp.write(bytes(data[ri][0]))
+    jobs = [((img,) + offs[ri], copies[ri][cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(ps),
+             contigs[ri][0], cpy) for ps, (ri, cpy, s) in enumerate(units)]
+    ref = {}
+    th = threading.Thread(target=lambda: ref.update(enumerate(O.digest_jobs(jobs, workers))), daemon=True)
+    th.start()
+    got = {}
+    hpool = ThreadPoolExecutor(8)
+
+    def sha(x):
+      return hashlib.sha256(memoryview(x)).hexdigest()
+
+    eng.ctx.sync()
+    eng.drop_haplotypes()
+    for batch in batches:
+      eng.ctx.reset_output()
+      res = eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
+      eng.ctx.sync()
+      o1 = o2 = 0
+      for (ps, ri, cpy, _), (n, kept, x1, x2) in zip(batch, res):
+        arr1, arr2 = eng.ctx.fetch_output_arrays(o1, x1, o2, x2)
+        f1, f2 = hpool.submit(sha, arr1), hpool.submit(sha, arr2)
+        got[ps] = (n, x1, f1, x2, f2)
+        o1, o2 = o1 + x1, o2 + x2
+      for ps in [u[0] for u in batch]:   # hashed before the arenas are reused
+        n, x1, f1, x2, f2 = got[ps]
+        got[ps] = (n, x1, f1.result(), x2, f2.result())
+    hpool.shutdown()
+    t_gpu = time.perf_counter() - t0
+    th.join()
+  finally:
+    for f in glob.glob(os.path.join(d, '*')):
+      os.remove(f)
+    os.rmdir(d)
+  bad = [ps for ps in range(len(units)) if got.get(ps) != ref.get(ps)]
+  out = {'units': len(units), 'units_equal': len(units) - len(bad), 'templates': sum(v[0] for v in got.values()),
+         'fastq_bytes': sum(v[1] + v[3] for v in got.values()), 'oracle_workers': workers,
+         'gpu_fetch_hash_s': round(t_gpu, 1), 'seconds': round(time.perf_counter() - t0, 1),
+         'method': 'per unit: sha256 of both FASTQ ranges of the arenas (D2H after the unit\'s batch) vs the CPU '
+                   'oracle\'s sha256 of the same unit (oracle.digest_jobs)'}
+  if bad:
+    out['first_bad'] = {'ps': bad[0], 'gpu': list(got.get(bad[0], ())), 'oracle': list(ref.get(bad[0], ()))}
+    print(json.dumps({'verify': out}), file=sys.stderr, flush=True)
+    sys.exit('bench.py --verify: {} of {} units differ from the oracle'.format(len(bad), len(units)))
+  return out
+
+
+def _cpu_unit(args):
+  """One work unit through the CPU oracle in a worker process; returns (templates, start, end) wall-clock stamps.
+  The unit's reference bytes come from a file (a /dev/shm image the parent wrote before timing) when `ref` is
+  (path, offset, length)."""
+  ref, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy = args
+  sys.path.insert(0, REPO)
+  from oracle import oracle as O
+  if isinstance(ref, tuple):
+    path, off, n = ref
+    with open(path, 'rb') as fp:
+      fp.seek(off)
+      ref = fp.read(n)
   t0 = time.time()
-  n = O.generate_unit_soa(ref, 0, soa, p, rlen, cum_tlen, seed, stub, '1', cpy, keep_output=False)[0]
+  n = O.generate_unit_soa(ref, 0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy, keep_output=False)[0]
   return n, t0, time.time()
 
 
-def cpu_baseline(a, seq, recs, p, rlen, model, units):
-  """The CPU oracle (oracle/mitty_oracle.c, a scalar port of the reference path) laid out like the reference's
-  multiprocessing path (`readgenerate.process_multi_threaded`: one worker process per work unit, `--threads` <=
-  #units): the job's work units run side by side in spawned worker processes (no GPU state in them) on the first
-  `cpu_baseline_mbp` Mbp of the same contig.  Rate = templates / (last unit's end - first unit's start)."""
+def _cpu_warm(_):
+  sys.path.insert(0, REPO)
+  from oracle import oracle as O
+  O.lib()
+  return os.getpid()
+
+
+def _cpu_pool_run(jobs, workers):
+  """The jobs through `workers` spawned oracle processes (warmed first: imports and the oracle library loaded before
+  timing), longest first; returns (templates, seconds from the first unit's start to the last unit's end, per-core
+  rate)."""
   import multiprocessing as mp
-  from mitty_amd import synth
-  L = int(a.cpu_baseline_mbp * 1e6)
-  sub = synth.copies_soa(recs, 0, L)
-  ref = bytes(seq[:L])
-  jobs = [(ref, sub[cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(k), cpy)
-          for k, (ri, cpy, s) in enumerate(units)]
-  with mp.get_context('spawn').Pool(len(jobs)) as pool:
-    res = pool.map(_cpu_unit, jobs)
+  pool = mp.get_context('spawn').Pool(workers)
+  try:
+    pool.map(_cpu_warm, range(workers), chunksize=1)
+    res = pool.map(_cpu_unit, jobs, chunksize=1)
+  except BaseException:
+    pool.terminate()
+    raise
+  pool.close()
+  pool.join()
   n = sum(r[0] for r in res)
   dt = max(r[2] for r in res) - min(r[1] for r in res)
-  per_core = [r[0] / (r[2] - r[1]) for r in res]
+  busy = sum(r[2] - r[1] for r in res)
+  return n, dt, n / busy if busy > 0 else None
+
+
+def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model):
+  """The metric's workload on the CPU: the CPU oracle (oracle/mitty_oracle.c, a scalar port of the reference path)
+  laid out like the reference's multiprocessing path (`readgenerate.process_multi_threaded`: worker processes pulling
+  work units, readgenerate.py:76-126) over all 100 work units of the 30x WGS job, in --cpu-workers processes.  Bounded
+  sample: each unit runs on the first --cpu-baseline-frac of its region (same variants, same seeds), so the sample
+  has the full job's unit list and topology.  Rate = templates / (last unit's end - first unit's start)."""
+  frac = a.cpu_baseline_frac
+  workers = max(1, min(a.cpu_workers, os.cpu_count() or 1))
+  d = tempfile.mkdtemp(prefix='mh_cpu_', dir='/dev/shm' if os.path.isdir('/dev/shm') else None)
+  img = os.path.join(d, 'ref.bin')
+  try:
+    offs, sub = {}, {}
+    with open(img, 'wb') as fp:   # the regions' prefixes, written once before timing (workers read their own)
+      for ri in sorted({u[0] for u in units}):
+        seq, recs, _ = data[ri]
+        L = max(1, int(len(seq) * frac))
+        offs[ri] = (fp.tell(), L)
+        fp.write(bytes(seq[:L]))
+        sub[ri] = synth_copies(recs, L)
+    jobs = [((img,) + offs[ri], sub[ri][cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(ps), contigs[ri][0],
+             cpy) for ps, (ri, cpy, s) in enumerate(units)]
+    order = sorted(range(len(jobs)), key=lambda k: -offs[units[k][0]][1])   # longest first, as the GPU deal
+    n, dt, per_core = _cpu_pool_run([jobs[k] for k in order], workers)
+  finally:
+    for f in glob.glob(os.path.join(d, '*')):
+      os.remove(f)
+    os.rmdir(d)
+  return {'value': n / dt, 'unit': 'templates/s', 'cores': workers, 'kind': 'port', 'per_core': per_core,
+          'host_cpus': os.cpu_count(), 'workload': 'wgs',
+          'sample': 'the 30x WGS job\'s {} work units (25 regions x 2 copies x 2 passes, the reference\'s unit order '
+                    'and seeds), each on the first {:.0%} of its region, in {} oracle worker processes ({} host CPUs '
+                    'visible; {} = the box\'s CPU share for one GPU): {} templates in {:.2f} s'.format(
+                        len(jobs), frac, workers, os.cpu_count(), a.cpu_workers, n, dt)}
+
+
+def synth_copies(recs, L):
+  from mitty_amd import synth
+  return synth.copies_soa(recs, 0, L)
+
+
+def cpu_baseline(a, seq, recs, p, rlen, model, units):
+  """chr1 leg (BASELINE configs[1]'s job): the oracle laid out like the reference's multiprocessing path, the job's
+  4 work units side by side in 4 worker processes on the first `cpu_baseline_mbp` Mbp of the chr1 contig."""
+  L = int(a.cpu_baseline_mbp * 1e6)
+  sub = synth_copies(recs, L)
+  ref = bytes(seq[:L])
+  jobs = [(ref, sub[cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(k), '1', cpy)
+          for k, (ri, cpy, s) in enumerate(units)]
+  n, dt, per_core = _cpu_pool_run(jobs, len(jobs))
   return {'value': n / dt, 'unit': 'templates/s', 'cores': len(jobs), 'kind': 'port',
-          'per_core': sum(per_core) / len(per_core), 'host_cpus': os.cpu_count(),
+          'per_core': per_core, 'host_cpus': os.cpu_count(), 'workload': 'chr1',
           'sample': '{} work units (2 copies x {} passes, one worker process each, {} host CPUs) on chr1[0:{:.0f} Mbp), '
                     '{} templates in {:.2f} s'.format(len(jobs), len(jobs) // 2, os.cpu_count(), a.cpu_baseline_mbp,
                                                      n, dt)}
@@ -715,11 +899,17 @@ def cpu_baseline_config0(a, data):
     soa = synth.copies_soa(recs, s0, e)[cpy]
     jobs.append((seq[s0:e], s0, soa, p, rlen, model['cum_tlen'], seed, 'SYN:{}:{}'.format(ps % 2, ps // 2), chrom,
                  cpy))
-  with mp.get_context('spawn').Pool(2) as pool:
+  pool = mp.get_context('spawn').Pool(2)
+  try:
     pool.map(_cpu_unit_region, jobs[:2])   # workers warm (imports) before timing
     t0 = time.perf_counter()
     n = sum(pool.map(_cpu_unit_region, jobs, chunksize=1))
     dt = time.perf_counter() - t0
+  except BaseException:
+    pool.terminate()
+    raise
+  pool.close()
+  pool.join()
   return {'value': n / dt, 'unit': 'templates/s', 'cores': 2, 'kind': 'port',
           'sample': 'BASELINE configs[0]: hg001.bed (1:20000-1020000, 10:60000-1060000) on the synthetic contigs, '
                     '1kg-pcr-free 2x{}, {}x, seed {}, 2 worker processes over the {} work units: {} templates in '

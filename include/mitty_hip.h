@@ -61,6 +61,12 @@ const char *mh_last_error(const mh_ctx *ctx);
 /* Synchronise the context's stream. */
 int32_t mh_sync(mh_ctx *ctx);
 
+/* Self-test of the look-back scans' fault report (no reference counterpart: the device offsets the scans produce —
+ * FASTQ record offsets, BAM record and BGZF block offsets — must never be wrong silently).  Runs a scan whose tile 0
+ * never publishes; returns MH_E_STATE when the timed-out wait was reported (the expected result), then checks that a
+ * correct scan after it succeeds. */
+int32_t mh_selftest_scan_fault(mh_ctx *ctx);
+
 /* ---- host-side helpers that mirror the reference's scalar logic ---------------------------------------- */
 int32_t mh_read_model_params(int64_t mean_rlen, double coverage, double *p, int64_t *passes);
 /* Work units in the reference's shuffled order; arrays sized sum(ploidy) * passes. */

@@ -17,6 +17,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
+           'mh_selftest_scan_fault',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
@@ -69,6 +70,7 @@ def lib():
   _sig(L, 'mh_destroy', [c_vp])
   _sig(L, 'mh_last_error', [c_vp], ctypes.c_char_p)
   _sig(L, 'mh_sync', [c_vp])
+  _sig(L, 'mh_selftest_scan_fault', [c_vp])
   _sig(L, 'mh_read_model_params', [c_i64, c_dbl, ctypes.POINTER(c_dbl), P_i64])
   _sig(L, 'mh_work_units', [c_u64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, P_i64])
   _sig(L, 'mh_upload_contig', [c_vp, c_i32, c_vp, c_i64])
@@ -573,6 +575,13 @@ class Context:
     self._chk(self._L.mh_output_fetch(self._h, off1, _ptr(b1), len1, off2, _ptr(b2) if len2 > 0 else None, len2))
     return b1[:len1].tobytes(), b2[:len2].tobytes()
 
+  def fetch_output_arrays(self, off1, len1, off2, len2):
+    """The same ranges as uint8 arrays (no bytes copy)."""
+    b1 = np.empty(max(len1, 1), np.uint8)
+    b2 = np.empty(max(len2, 1), np.uint8)
+    self._chk(self._L.mh_output_fetch(self._h, off1, _ptr(b1), len1, off2, _ptr(b2) if len2 > 0 else None, len2))
+    return b1[:len1], b2[:len2]
+
   def stream_output(self, sinks, pin, chunk=256 << 20):
     """Both arenas to the sinks (file-like objects; None skips a file) through one page-locked staging buffer,
     `chunk` bytes per copy."""
@@ -793,6 +802,11 @@ class Context:
 
   def sync(self):
     self._chk(self._L.mh_sync(self._h))
+
+  def selftest_scan_fault(self):
+    """(return code, message) of mh_selftest_scan_fault: MH_E_STATE when a timed-out look-back scan is reported."""
+    rc = self._L.mh_selftest_scan_fault(self._h)
+    return rc, self._L.mh_last_error(self._h).decode(errors='replace')
 
 
 def expand_variant(samp_pos, ref_pos, ref_start_pos, v_pos, op, oplen):

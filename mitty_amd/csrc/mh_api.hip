@@ -37,13 +37,24 @@ int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg) {
   return code;
 }
 
+bool scan_fault_pending() {
+  const uint32_t *h = scan_fault_host();
+  return h && __atomic_load_n(h, __ATOMIC_ACQUIRE) != 0;
+}
+
+int32_t scan_fault_fail(mh_ctx *ctx) {
+  (void)scan_fault_take();
+  return arg_fail(ctx, MH_E_STATE, "a look-back scan's wait timed out (a broken ticket base or scratch): its offsets "
+                                   "are wrong");
+}
+
 int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return MH_OK;
   if (b.p) {
     gate_open(ctx);
     MH_TRY(sync_writers(ctx));   // a queued FASTQ writer (or corruption pass) may still read or write it
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     lb_forget(b.p);
     HIPCHK(ctx, hipFree(b.p));
     b.p = nullptr;
@@ -67,7 +78,7 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
   gate_open(ctx);
   MH_TRY(sync_writers(ctx));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   lb_forget(b.p);
   if (b.p) HIPCHK(ctx, hipFree(b.p));
   b = nb;
@@ -137,8 +148,8 @@ int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
 
 int32_t sync_writers(mh_ctx *ctx) {
   gate_open(ctx);
-  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
-  if (ctx->crstream) HIPCHK(ctx, hipStreamSynchronize(ctx->crstream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->wstream));
+  if (ctx->crstream) SYNCCHK(ctx, hipStreamSynchronize(ctx->crstream));
   ctx->cr_pending = false;
   return MH_OK;
 }
@@ -383,8 +394,49 @@ const char *mh_last_error(const mh_ctx *ctx) { return ctx ? ctx->err.c_str() : "
 
 int32_t mh_sync(mh_ctx *ctx) {
   CTX_GUARD(ctx);
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
+}
+
+namespace {
+struct LoadOne {
+  __device__ int64_t operator()(int64_t) const { return 1; }
+};
+struct StoreCheck {   // element i's exclusive prefix must be i
+  int32_t *bad;
+  __device__ void operator()(int64_t i, int64_t, int64_t ex) const {
+    if (ex != i) atomicOr(bad, 1);
+  }
+};
+}  // namespace
+
+// A look-back scan whose tile 0 never runs (device_scan_sum's skip_tile0): every waiting tile times out, the fault
+// word is set, and the synchronisation after it fails with MH_E_STATE — the expected result.  A correct scan after it
+// then succeeds (the word was cleared).
+int32_t mh_selftest_scan_fault(mh_ctx *ctx) {
+  CTX_GUARD(ctx);
+  hipStream_t st = ctx->stream;
+  const int64_t n = 2 * (int64_t)LB_TILE + 5;
+  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(n)));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 160);
+  int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 168);
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadOne{}, StoreCheck{bad}, ctx->scan_partials.p, tot, true));
+  const int32_t rc = [&]() -> int32_t {
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+    return MH_OK;
+  }();
+  if (rc != MH_E_STATE) return arg_fail(ctx, MH_E_HIP, "the timed-out scan was not reported");
+  const std::string msg = ctx->err;
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadOne{}, StoreCheck{bad}, ctx->scan_partials.p, tot));
+  int32_t hb = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&hb, bad, 4, hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  if (hb) return arg_fail(ctx, MH_E_HIP, "the scan after the fault is wrong");
+  arg_fail(ctx, MH_E_STATE, msg);
+  return MH_E_STATE;
 }
 
 // illumina.read_model_params (illumina.py:12-40)
@@ -436,7 +488,7 @@ int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_
   Contig &c = ctx->contigs[contig_id];
   MH_TRY(ensure(ctx, c.seq, len + 16));
   if (len) HIPCHK(ctx, hipMemcpyAsync(c.seq.p, seq, len, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   c.len = len;
   return MH_OK;
 }
@@ -588,7 +640,7 @@ int32_t mh_release_variants(mh_ctx *ctx, int32_t vset) {
   CTX_GUARD(ctx);
   auto it = ctx->vsets.find(vset);
   if (it == ctx->vsets.end()) return MH_OK;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   release_vars(it->second);
   ctx->vsets.erase(it);
   return MH_OK;
@@ -609,12 +661,12 @@ int32_t mh_get_nodes(mh_ctx *ctx, int32_t slot, int64_t *ps, int64_t *pr, uint8_
   if (hap_len) *hap_len = h.hap_len;
   if (hap) {
     if (hap_cap < h.hap_len) {
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
       return arg_fail(ctx, MH_E_CAPACITY, "haplotype buffer too small");
     }
     if (h.hap_len) HIPCHK(ctx, hipMemcpyAsync(hap, h.hap.p, h.hap_len, hipMemcpyDeviceToHost, st));
   }
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   return MH_OK;
 }
 
@@ -632,7 +684,7 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   } else {
     gate_open(ctx);
     MH_TRY(sync_writers(ctx));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     release_hap(h);
   }
   ctx->haps.erase(it);
@@ -721,7 +773,7 @@ int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id) {
   CTX_GUARD(ctx);
   auto it = ctx->tsets.find(tpl_id);
   if (it == ctx->tsets.end()) return MH_OK;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   release(it->second.fo0); release(it->second.pos0); release(it->second.pos1);
   if (it->second.used) (void)hipEventDestroy(it->second.used);
   ctx->tsets.erase(it);
@@ -744,7 +796,7 @@ int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, co
     HIPCHK(ctx, hipMemcpyAsync(ts.pos0.p, pos0, 8 * n, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ts.pos1.p, pos1, 8 * n, hipMemcpyHostToDevice, ctx->stream));
   }
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   ts.n = n;
   ts.rlen = rlen;
   ts.valid = true;
@@ -765,7 +817,7 @@ int32_t mh_get_templates(mh_ctx *ctx, int8_t *fo0, int64_t *pos0, int64_t *pos1,
     if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ts.pos0.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
     if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ts.pos1.p, 8 * m, hipMemcpyDeviceToHost, ctx->stream));
   }
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
 
@@ -801,7 +853,7 @@ int32_t mh_templates_export(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, int8
     if (pos0) HIPCHK(ctx, hipMemcpyAsync(pos0, ts.pos0.p, 8 * m, k, ctx->stream));
     if (pos1) HIPCHK(ctx, hipMemcpyAsync(pos1, ts.pos1.p, 8 * m, k, ctx->stream));
   }
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
 
@@ -824,7 +876,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
     HIPCHK(ctx, hipMemcpyAsync(ts.pos0.p, pos0, 8 * n, k, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ts.pos1.p, pos1, 8 * n, k, ctx->stream));
   }
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   if (ts.prep.valid) ctx->eset[ts.prep.set].prepared = false;   // the buffer set of a measure pass made for the old set
   ts.prep.valid = false;
   ts.n = n;
@@ -891,7 +943,7 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
   if (fq1 && len1) HIPCHK(ctx, hipMemcpyAsync(fq1, (char *)ctx->out1.p + off1, len1, hipMemcpyDeviceToHost, ctx->stream));
   if (fq2 && len2) HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
 
@@ -998,7 +1050,7 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_T16_off, T16.data(), 2 * nt, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp16_off, Fp16.data(), 2 * 100, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;
   ctx->corrupt_max_bp = max_bp;
   ctx->corrupt_n_bq = n_bq;
@@ -1299,7 +1351,7 @@ int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out
     return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
   }
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   *used = u;
   return MH_OK;
 }
@@ -1322,7 +1374,7 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
   if (!out) return MH_OK;   // (the size only)
   if (u > cap) return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
 

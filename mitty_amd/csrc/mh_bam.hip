@@ -516,7 +516,7 @@ static int32_t bam_check_bounds(mh_ctx *ctx, const int32_t *bad, const char *who
   int64_t *hs = pinned_small(ctx);
   if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
   HIPCHK(ctx, hipMemcpyAsync(hs + 26, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   const int32_t f = (int32_t)(hs[26] & 0xffffffff);
   if (f) return arg_fail(ctx, MH_E_STATE, std::string("BAM store: ") + who + " index or bytes out of bounds (flag " +
                                             std::to_string(f) + ", internal)");
@@ -542,7 +542,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
   if (!cat.empty()) HIPCHK(ctx, hipMemcpyAsync(B.names.p, cat.data(), cat.size(), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(B.name_off.p, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice,
                              ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   B.n_rec = 0;
   B.bytes = 0;
   B.n_files = 0;
@@ -566,7 +566,7 @@ int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, in
                                      (int64_t *)ctx->scan_partials.p, tot));
   int64_t n = 0;
   HIPCHK(ctx, hipMemcpyAsync(&n, tot, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   MH_TRY(ensure(ctx, nl, sizeof(int64_t) * (n + 1)));
   // single pass (decoupled look-back): each element's bytes are re-read by the thread that counted them
   HIPCHK(ctx, device_scan_sum<int64_t>(st, chunks, LoadNL{b, len}, StoreNL{b, len, (int64_t *)nl.p},
@@ -608,7 +608,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   stage_end(ctx);
   int32_t herr = 0;
   HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   if (herr) {
     std::string m = "god-aligner input:";
     if (herr & BE_QNAME) m += " malformed FASTQ record;";
@@ -630,7 +630,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
                                    tot));
   int64_t add_bytes = 0;
   HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   static const bool direct_off = getenv("MH_BAM_DIRECT") && atoi(getenv("MH_BAM_DIRECT")) == 0;   // experiments
   if (sorted_direct && !direct_off && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
     // the whole input is here (the context's own arenas) and the store is empty: sort first, then every record is
@@ -648,7 +648,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
     int64_t last1 = 0, last2 = 0;
     HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
     if (d2) HIPCHK(ctx, hipMemcpyAsync(&last2, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     *used1 = last1 + 1;
     *used2 = d2 ? last2 + 1 : 0;
     *templates = T;
@@ -673,7 +673,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int64_t last1 = 0, last2 = 0;
   HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
   if (d2) HIPCHK(ctx, hipMemcpyAsync(&last2, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   *used1 = last1 + 1;
   *used2 = d2 ? last2 + 1 : 0;
   *templates = T;
@@ -717,7 +717,7 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
     if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
     HIPCHK(ctx, hipMemcpyAsync(hs + 24, (const int64_t *)B.soff.p + n, 8, hipMemcpyDeviceToHost, st));
     if (!pa) HIPCHK(ctx, hipMemcpyAsync(hs + 25, (const int64_t *)B.roff.p + n, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     if (hs[24] != B.bytes || (!pa && hs[25] != B.bytes))
       return arg_fail(ctx, MH_E_STATE, "BAM store: record offsets do not add up to the store's size (internal)");
   }
@@ -767,7 +767,7 @@ int32_t bam_undirect(mh_ctx *ctx) {
   HIPCHK(ctx, hipMemcpyAsync(B.info.p, B.sinfo.p, sizeof(RInfo) * n, hipMemcpyDeviceToDevice, st));
   hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (uint32_t *)B.val.p, n);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   B.direct = false;
   B.sorted = false;
   return MH_OK;
@@ -782,7 +782,7 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
   if (recs) HIPCHK(ctx, hipMemcpyAsync(recs, B.srecs.p, B.bytes, hipMemcpyDeviceToHost, st));
   if (soff) HIPCHK(ctx, hipMemcpyAsync(soff, B.soff.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
   if (info) HIPCHK(ctx, hipMemcpyAsync(info, B.sinfo.p, sizeof(RInfo) * n, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   return MH_OK;
 }
 

@@ -310,7 +310,7 @@ int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_
   HIPCHK(ctx, hipMemcpyAsync(&tot, off + T, sizeof(Off3), hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipMemcpyAsync(&last0, (const int64_t *)B.nl1.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
   if (d1) HIPCHK(ctx, hipMemcpyAsync(&last1, (const int64_t *)B.nl2.p + 4 * T - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   if (herr & CE_LONG) return arg_fail(ctx, MH_E_ARG, "read longer than the BQ model (illumina.corrupt_single_read)");
   if (herr) return arg_fail(ctx, MH_E_ARG, "malformed FASTQ record");
   MH_TRY(ensure_keep(ctx, ctx->out1, ctx->used1 + tot.a + 64, ctx->used1));
@@ -357,7 +357,7 @@ int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_
       int32_t hovf = 0;
       HIPCHK(ctx, hipMemcpyAsync(&hovf, ovf, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipMemcpyAsync(&consumed, mstart + K, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
       if (hovf) {
         need *= 2;
         continue;
@@ -392,7 +392,7 @@ int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_
       ctx->cx_kpos = h.pos;
     }
   }
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   ctx->used1 += tot.a;
   if (d1) ctx->used2 += tot.b;
   *used0 = last0 + 1;

@@ -484,7 +484,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
                                          StoreBlk{(int64_t *)ctx->gz_off.p}, ctx->gz_scan.p, tot));
     HIPCHK(ctx, hipMemcpyAsync(hs + 32, tot, 8, hipMemcpyDeviceToHost, st));
     if (boff) HIPCHK(ctx, hipMemcpyAsync(boff->data() + b0, ctx->gz_off.p, 8 * (size_t)nb, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     const int64_t bytes = hs[32];
     if (boff)
       for (int64_t i = 0; i < nb; i++) (*boff)[b0 + i] += w;
@@ -495,7 +495,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
     HIPCHK(ctx, hipGetLastError());
     w += bytes;
   }
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   *used = w;
   if (boff) (*boff)[nb_all] = w;
   return MH_OK;

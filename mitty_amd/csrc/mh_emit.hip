@@ -2044,7 +2044,7 @@ int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, in
                                                      (const int64_t *)tp.pos1.p + t_begin, m, tp.rlen},
                                      OpSum{}, (int64_t)0, (int64_t *)ctx->scan_partials.p, tot));
   HIPCHK(ctx, hipMemcpyAsync(out_kept, tot, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   return MH_OK;
 }
 
@@ -2142,7 +2142,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     if (pp.deferred) {   // the measure pass's totals, copied to the set's pinned readback
       const EmitSet &es = ctx->eset[set];
       writer_dep = es.rb;
-      HIPCHK(ctx, hipEventSynchronize(es.rb));
+      SYNCCHK(ctx, hipEventSynchronize(es.rb));
       std::memcpy(&ht, es.h_stat, sizeof(E3));
       std::memcpy(hm4, (const char *)es.h_stat + 32, sizeof(hm4));
       ht = totals(ht);
@@ -2202,7 +2202,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
       HIPCHK(ctx, hipMemcpyAsync(hs, tot, sizeof(E3), hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipMemcpyAsync(hs + 4, max_rec, 16, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
       std::memcpy(&ht, hs, sizeof(E3));
       std::memcpy(hm4, hs + 4, sizeof(hm4));
       ht = totals(ht);
@@ -2367,7 +2367,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
                                (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc));
     int32_t herr = 0;
     HIPCHK(ctx, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     stage_end(ctx);
     if (herr) return arg_fail(ctx, MH_E_CAPACITY, "FASTQ record larger than the LDS staging image");
   }
@@ -2450,7 +2450,7 @@ int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out) {
     int64_t *hs = pinned_small(ctx);
     if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
     HIPCHK(ctx, hipMemcpyAsync(hs + 16, dmx, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     mx[0] = (unsigned long long)hs[16];
     mx[1] = (unsigned long long)hs[17];
     nodes = (int64_t)(mx[0] + mx[1]);
@@ -2483,7 +2483,7 @@ __global__ void k_set_used(int64_t *d_used, int64_t u1, int64_t u2) {
 int32_t sync_async_fill(mh_ctx *ctx) {
   if (!ctx->async_pending) return MH_OK;
   gate_open(ctx);
-  HIPCHK(ctx, hipStreamSynchronize(ctx->wstream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->wstream));
   int64_t u[2] = {0, 0};
   HIPCHK(ctx, hipMemcpy(u, ctx->d_used.p, 16, hipMemcpyDeviceToHost));
   ctx->used1 = u[0];
@@ -2518,7 +2518,7 @@ int32_t emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out) {
   if ((uint32_t)ticket >> 8 != ctx->res_gen[t])
     return arg_fail(ctx, MH_E_STATE, "stale emission ticket (its result slot was reused by a later emission)");
   gate_open(ctx);
-  if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
+  if (ctx->res_state[t] == 1) SYNCCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
   const int64_t *r = ctx->h_res + 8 * t;
   out[0] = r[0];
   out[1] = r[1];
@@ -2543,7 +2543,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   }
   const int32_t t = ctx->res_next;
   gate_open(ctx);
-  if (ctx->res_state[t] == 1) HIPCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
+  if (ctx->res_state[t] == 1) SYNCCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
   ctx->res_next = (t + 1) % mh_ctx::RES_N;
   ctx->res_state[t] = 0;
   ctx->res_gen[t] = (ctx->res_gen[t] + 1) & 0x7fffff;
@@ -2603,11 +2603,11 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
     // host's exact numbers.  The new size covers the reservations that were queued (a quarter more), so the next job
     // of the same shape fits without another synchronisation.
     const int64_t want1 = (ctx->res1 + U + 64) * 5 / 4, want2 = (ctx->res2 + U + 64) * 5 / 4;
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     MH_TRY(sync_async_fill(ctx));
     MH_TRY(ensure_keep(ctx, ctx->out1, std::max(want1, ctx->used1 + U + 64), ctx->used1));
     if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, std::max(want2, ctx->used2 + U + 64), ctx->used2));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, ctx->used1,
                        ctx->used2);
     HIPCHK(ctx, hipGetLastError());

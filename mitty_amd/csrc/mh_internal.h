@@ -297,6 +297,16 @@ int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg);
     if (_e != hipSuccess) return ::mh::hip_fail((ctx), _e, #call, __FILE__, __LINE__); \
   } while (0)
 
+// A host synchronisation, then the look-back scans' fault word (mh_scan.h): a scan that timed out since the last check
+// fails the call instead of its wrong offsets being used
+int32_t scan_fault_fail(mh_ctx *ctx);
+#define SYNCCHK(ctx, call)                                                    \
+  do {                                                                        \
+    HIPCHK(ctx, call);                                                        \
+    if (::mh::scan_fault_pending()) return ::mh::scan_fault_fail(ctx);        \
+  } while (0)
+bool scan_fault_pending();
+
 // Grow `b` to hold at least `bytes`; contents are NOT preserved.
 int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);
 // Grow preserving the first `keep` bytes (stream-ordered copy).

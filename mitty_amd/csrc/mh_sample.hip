@@ -982,7 +982,7 @@ int32_t ensure_polys(mh_ctx *ctx, hipStream_t st, int64_t kmax, int64_t seg) {
   for (int64_t k = 0; k <= kmax; k++) jump::jump_poly_words((uint64_t)seg, k, polys.data() + k * 624);
   MH_TRY(ensure(ctx, ctx->jump_polys, 4 * polys.size()));
   HIPCHK(ctx, hipMemcpyAsync(ctx->jump_polys.p, polys.data(), 4 * polys.size(), hipMemcpyHostToDevice, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   ctx->jump_k = kmax + 1;
   ctx->jump_seg = seg;
   return MH_OK;
@@ -1021,7 +1021,7 @@ int32_t mt_stream_words(mh_ctx *ctx, hipStream_t st, uint32_t seed, int64_t firs
   hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)jobs_buf.p,
                      (const uint32_t *)ctx->jump_polys.p, 0);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipStreamSynchronize(st));   // the host job table goes out of scope
+  SYNCCHK(ctx, hipStreamSynchronize(st));   // the host job table goes out of scope
   return MH_OK;
 }
 
@@ -1034,7 +1034,7 @@ int32_t mt_state_words(mh_ctx *ctx, hipStream_t st, const uint32_t *key624, int3
   hipLaunchKernelGGL(k_mt_state, dim3(1), dim3(256), 0, st, (const uint32_t *)key_buf.p, pos, count,
                      (uint32_t *)out.p);
   HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, hipStreamSynchronize(st));   // key624 is the caller's host memory
+  SYNCCHK(ctx, hipStreamSynchronize(st));   // key624 is the caller's host memory
   return MH_OK;
 }
 
@@ -1164,7 +1164,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     int64_t *hs = pinned_small(ctx);
     if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
     HIPCHK(ctx, hipMemcpyAsync(hs + 32, cur, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     const int32_t h_ntodo = (int32_t)(hs[32] & 0xffffffff);
     if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
                                           h_ntodo, (long long)C);
@@ -1207,7 +1207,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   // j[0] = 0 (the shuffle's unused slot), as k_shuffle_decode2 sets it
   for (size_t u = 0; u < dec.size(); u++)
     if (dec[u].n > 0) HIPCHK(ctx, hipMemsetAsync(dec[u].j, 0, 4, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   *done = true;
   return MH_OK;
 }
@@ -1297,7 +1297,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
       hipLaunchKernelGGL(k_geo_array, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, w_tloc, p, log_q, fl, g);
       HIPCHK(ctx, hipMemcpyAsync(&nflag, d_flag, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
       if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
       std::vector<int64_t> idx(nflag);
       if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
@@ -1523,7 +1523,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
       }
       stage_end(ctx);
       // keep the job tables alive until the kernels ran
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
     }
   } else {
     for (int32_t u = 0; u < n_units; u++) {
@@ -1706,7 +1706,7 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
   const size_t rb_bytes = 20 * (size_t)n_units;
   if (hs && rb_bytes <= 3072) {
     HIPCHK(ctx, hipMemcpyAsync(hs + 64, d_m, rb_bytes, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     std::memcpy(hm.data(), hs + 64, 8 * n_units);
     std::memcpy(hstat.data(), hs + 64 + n_units, 8 * n_units);
     std::memcpy(hflag.data(), hs + 64 + 2 * n_units, 4 * n_units);
@@ -1714,7 +1714,7 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
     HIPCHK(ctx, hipMemcpyAsync(hm.data(), d_m, 8 * n_units, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(hstat.data(), d_status, 8 * n_units, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(hflag.data(), d_flags, 4 * n_units, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
   }
 
   // ---- rare exact fix-ups: decode out of words (sequential stream), near-integer geometric quotients ------------
@@ -1730,7 +1730,7 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
     MH_TRY(finish_unit(ctx, q, words, jall + q.j_off, p, rlen, d_cum, n_tlen, rng_mode, hflag[u] != 0, d_m + u,
                        d_flags + u));
     HIPCHK(ctx, hipMemcpyAsync(&hm[u], d_m + u, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     ctx->fixups++;
   }
   stage_end(ctx);

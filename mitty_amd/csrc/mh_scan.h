@@ -233,9 +233,38 @@ __device__ __forceinline__ uint64_t lb_get(const uint64_t *w) {
 
 // scratch: [ticket (64 B)] [aggregate words K x nt] [inclusive words K x nt], zeroed when new; ticket_base: the
 // ticket counter's value when this launch starts; epoch: this launch's tag (1 .. 2^16 - 1)
+// A host-mapped word every look-back scan reports a timed-out wait to (a broken ticket base or scratch: the scan's
+// sums are then wrong).  The host reads it after a synchronisation (scan_fault_take) and fails the call with
+// MH_E_STATE instead of returning the wrong offsets as success.
+inline uint32_t *scan_fault_host() {
+  static uint32_t *w = [] {
+    uint32_t *p = nullptr;
+    if (hipHostMalloc((void **)&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (uint32_t *)nullptr;
+    p[0] = 0;
+    return p;
+  }();
+  return w;
+}
+inline uint32_t *scan_fault_device() {
+  static uint32_t *d = [] {
+    uint32_t *h = scan_fault_host(), *p = nullptr;
+    if (!h || hipHostGetDevicePointer((void **)&p, h, 0) != hipSuccess) return (uint32_t *)nullptr;
+    return p;
+  }();
+  return d;
+}
+// 1 when a look-back scan timed out since the last call (the word is cleared)
+inline uint32_t scan_fault_take() {
+  uint32_t *h = scan_fault_host();
+  if (!h) return 0;
+  const uint32_t v = __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL);
+  return v;
+}
+
 template <typename T, typename Load, typename Store>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, Store store, uint64_t *scratch,
-                                                         int64_t nt, T *total, uint32_t ticket_base, uint32_t epoch) {
+                                                         int64_t nt, T *total, uint32_t ticket_base, uint32_t epoch,
+                                                         uint32_t *fault) {
   using F = LbFields<T>;
   constexpr int K = F::K;
   __shared__ T lds_w[SCAN_THREADS / 64];
@@ -283,7 +312,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
         const int64_t jj = j - lane;   // lane l looks at tile j - l (jj < 0: past tile 0, never needed)
         bool is_inc = jj < 0, ok = jj < 0;
         T val{};
-        uint32_t spins = 0;   // a bound on the wait: a broken ticket or scratch gives wrong sums, never a hung GPU
+        uint32_t spins = 0;
         while (!ok) {
           bool all_inc = true, all_agg = true;
           int64_t xi[K], xa[K];
@@ -301,8 +330,9 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
             is_inc = all_inc;
 #pragma unroll
             for (int k = 0; k < K; k++) F::set(val, k, all_inc ? xi[k] : xa[k]);
-          } else if (++spins > (1u << 24)) {
+          } else if (++spins > (1u << 24)) {   // (a bound on the wait: reported, never a hung GPU)
             ok = is_inc = true;
+            if (fault) __hip_atomic_fetch_or(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           } else {
             __builtin_amdgcn_s_sleep(1);
           }
@@ -344,10 +374,14 @@ inline size_t scan_lb_scratch_bytes(int64_t n) {
 
 // Host launcher: exclusive/inclusive sums through Store, grand total to *total.  `scratch` holds
 // scan_lb_scratch_bytes<T>(n) bytes of device memory.
+// skip_tile0 (self-test only, mh_selftest_scan_fault): the ticket base one below the counter and one workgroup
+// fewer, so tile 0 never publishes and every other tile's look-back times out (all accesses stay in range)
 template <typename T, typename Load, typename Store>
-inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store store, void *scratch, T *total) {
+inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store store, void *scratch, T *total,
+                                  bool skip_tile0 = false) {
   int64_t nt = (n + LB_TILE - 1) / LB_TILE;
   if (nt < 1) nt = 1;
+  if (skip_tile0 && nt < 2) return hipErrorInvalidValue;
   const size_t need = scan_lb_scratch_bytes<T>(n);
   uint32_t base, epoch;
   {
@@ -360,12 +394,12 @@ inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store st
       S.ticket = 0;
       S.epoch = 0;
     }
-    base = S.ticket;
+    base = S.ticket - (skip_tile0 ? 1u : 0u);
     epoch = ++S.epoch;
-    S.ticket += (uint32_t)nt;
+    S.ticket += (uint32_t)(skip_tile0 ? nt - 1 : nt);
   }
-  hipLaunchKernelGGL((k_scan_lb<T, Load, Store>), dim3((unsigned)nt), dim3(SCAN_THREADS), 0, st, n, load, store,
-                     (uint64_t *)scratch, nt, total, base, epoch);
+  hipLaunchKernelGGL((k_scan_lb<T, Load, Store>), dim3((unsigned)(skip_tile0 ? nt - 1 : nt)), dim3(SCAN_THREADS), 0,
+                     st, n, load, store, (uint64_t *)scratch, nt, total, base, epoch, scan_fault_device());
   return hipGetLastError();
 }
 

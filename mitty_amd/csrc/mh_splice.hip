@@ -385,7 +385,7 @@ int32_t var_upload(mh_ctx *ctx, VarSet &v, const int64_t *v_pos, const uint8_t *
   }
   if (alt_pool_len > 0) HIPCHK(ctx, hipMemcpyAsync(v.pool.p, alt_pool, alt_pool_len, hipMemcpyHostToDevice, st));
   // pageable sources: the copies have read them once the stream reaches here
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   v.n = n_var;
   v.pool_len = alt_pool_len;
   return MH_OK;
@@ -466,7 +466,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     // one readback into pinned memory: tot_i64 at small + 0, tot_ns at small + 16
     int64_t *hs = hs_lane;
     HIPCHK(ctx, hipMemcpyAsync(hs, small, 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
     final_ref = hs[0];
     if (final_ref < rs) final_ref = rs;
     tot = NS{hs[2], hs[3]};
@@ -489,7 +489,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
 
   // --- haplotype bytes ---------------------------------------------------------------------------------------
   HIPCHK(ctx, hipMemcpyAsync(hs + 11, err, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
   const int64_t ps0 = hs[8], psl = hs[9], nll = hs[10];
   const int32_t herr = (int32_t)(hs[11] & 0xffffffff);
   if (herr) {
@@ -549,7 +549,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
                          hap_len, cap, us, ue, cnt);
       HIPCHK(ctx, hipGetLastError());
       HIPCHK(ctx, hipMemcpyAsync(hs + 12, cnt, 16, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
       hc[0] = (unsigned long long)hs[12];
       hc[1] = (unsigned long long)hs[13];
       if ((int64_t)hc[0] <= cap && (int64_t)hc[1] <= cap) break;

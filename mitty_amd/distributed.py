@@ -136,27 +136,30 @@ class DeviceBackend:
     self.eng.ctx.templates_import(k, n, rlen, a[16 * n:17 * n].view(np.int8), a[:8 * n].view(np.int64),
                                   a[8 * n:16 * n].view(np.int64))
 
-  def share(self, k, n, src, rlen, group=None):
+  def share(self, k, n, src, rlen, group=None, into=None):
     """Template set k (n templates) from rank src to every rank: an RCCL broadcast of the device arrays under
-    'nccl' (pos0 | pos1 | fo0 packed in one buffer, device-to-device copies on either side), host arrays under gloo."""
+    'nccl' (pos0 | pos1 | fo0 packed in one buffer, device-to-device copies on either side), host arrays under gloo.
+    The receivers unpack into set k; `into` names another set the source also unpacks its broadcast buffer into
+    (the whole round trip on one rank: the one-GPU test of the RCCL path)."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
+    dst = k if rank != src else into
     if dist.get_backend(group) == 'nccl':
       buf = torch.empty(max(17 * n, 16), dtype=torch.uint8, device='cuda')
       if rank == src:
         self.pack_device(k, n, buf.data_ptr())   # (synchronous: the copies are done before the broadcast reads)
       dist.broadcast(buf, src, group=group)
       torch.cuda.current_stream().synchronize()
-      if rank != src:
-        self.unpack_device(k, n, rlen, buf.data_ptr())
+      if dst is not None:
+        self.unpack_device(dst, n, rlen, buf.data_ptr())
       return
     buf = torch.empty(max(17 * n, 16), dtype=torch.uint8)
     if rank == src:
       self.pack_host(k, n, buf.numpy())
     dist.broadcast(buf, src, group=group)
-    if rank != src:
-      self.unpack_host(k, n, rlen, buf.numpy())
+    if dst is not None:
+      self.unpack_host(dst, n, rlen, buf.numpy())
 
   def count_kept(self, k, t0, t1):
     self.eng.ctx.use_templates(k)

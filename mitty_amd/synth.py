@@ -21,6 +21,21 @@ GRCH37 = [('1', 249250621), ('2', 243199373), ('3', 198022430), ('4', 191154276)
 _ACGT = np.frombuffer(b'ACGT', dtype=np.uint8)
 
 
+def spawn_map(fn, jobs, workers, chunksize=1):
+  """pool.map over fresh (spawned) interpreters, the pool closed and joined afterwards.  (`with Pool()` terminates
+  its workers with SIGTERM on exit, which a profiler's signal handler in each idle worker reports as an abort.)"""
+  import multiprocessing as mp
+  pool = mp.get_context('spawn').Pool(max(1, workers))
+  try:
+    out = pool.map(fn, jobs, chunksize=chunksize)
+  except BaseException:
+    pool.terminate()
+    raise
+  pool.close()
+  pool.join()
+  return out
+
+
 def contig(length, seed, n_gaps=True):
   rs = np.random.RandomState(seed)
   s = _ACGT[rs.randint(0, 4, size=length, dtype=np.uint8)]
@@ -123,10 +138,8 @@ def genome_regions(contigs, indices, workers=8):
   if workers <= 1 or len(jobs) <= 1:
     res = [_region_job(j) for j in jobs]
   else:
-    import multiprocessing as mp
     order = sorted(range(len(jobs)), key=lambda k: -jobs[k][0])   # longest first
-    with mp.get_context('spawn').Pool(min(workers, len(jobs))) as pool:
-      got = pool.map(_region_job, [jobs[k] for k in order], chunksize=1)
+    got = spawn_map(_region_job, [jobs[k] for k in order], min(workers, len(jobs)))
     res = [None] * len(jobs)
     for k, r in zip(order, got):
       res[k] = r

@@ -224,9 +224,11 @@ def generate_unit(ref_seq, region_start0, vl, p, rlen, cum_tlen, rng_seed, seria
 
 
 def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, serial_stub, chrom, cpy,
-                      keep_output=True):
+                      keep_output=True, digest=False):
   """generate_unit for variants already in structure-of-arrays form (pos, op, oplen, alt_off, alt_len, alt_pool).
-  keep_output=False frees the FASTQ bytes without copying them into Python (timing runs: no GIL-held copy)."""
+  keep_output=False frees the FASTQ bytes without copying them into Python (timing runs: no GIL-held copy);
+  digest=True returns (n, len1, sha256 hex 1, len2, sha256 hex 2), hashed in place (no copy)."""
+  import hashlib
   pos = np.ascontiguousarray(soa['pos'], dtype=np.int64)
   op = np.ascontiguousarray(soa['op'], dtype=np.uint8)
   oplen = np.ascontiguousarray(soa['oplen'], dtype=np.int64)
@@ -242,10 +244,20 @@ def generate_unit_soa(ref_seq, region_start0, soa, p, rlen, cum_tlen, rng_seed, 
                              pool, len(pos), p, rlen, _p(cum_tlen), len(cum_tlen), rng_seed, serial_stub.encode(),
                              chrom.encode(), cpy, ctypes.byref(o1), ctypes.byref(l1), ctypes.byref(o2),
                              ctypes.byref(l2))
-  b1 = _take(o1, l1.value) if keep_output else b''
-  b2 = _take(o2, l2.value) if keep_output else b''
-  lib().mo_free(o1)
-  lib().mo_free(o2)
+  try:
+    if digest:
+      hs = []
+      for o, ln in ((o1, l1.value), (o2, l2.value)):
+        h = hashlib.sha256()
+        if ln:
+          h.update(memoryview((ctypes.c_char * ln).from_address(o.value)).cast('B'))
+        hs.append(h.hexdigest())
+      return n, l1.value, hs[0], l2.value, hs[1]
+    b1 = _take(o1, l1.value) if keep_output else b''
+    b2 = _take(o2, l2.value) if keep_output else b''
+  finally:
+    lib().mo_free(o1)
+    lib().mo_free(o2)
   return n, b1, b2
 
 
@@ -297,18 +309,21 @@ def corrupt_fastq(model, names, seq1, seq2, seed=7):
 
 
 def _unit_digest(args):
-  """One work unit in a worker process: (templates, len1, sha256 of file 1's bytes, len2, sha256 of file 2's)."""
-  import hashlib
+  """One work unit in a worker process: (templates, len1, sha256 of file 1's bytes, len2, sha256 of file 2's).
+  ref_seq may be (path, offset, length): the unit's reference bytes read from a file the caller wrote."""
   ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy = args
-  n, b1, b2 = generate_unit_soa(ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy)
-  return n, len(b1), hashlib.sha256(b1).hexdigest(), len(b2), hashlib.sha256(b2).hexdigest()
+  if isinstance(ref_seq, tuple):
+    path, off, ln = ref_seq
+    with open(path, 'rb') as fp:
+      fp.seek(off)
+      ref_seq = fp.read(ln)
+  return generate_unit_soa(ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy, digest=True)
 
 
 def unit_digests(seqs, vdf, sample, model, coverage, seed, workers=8):
   """readgenerate.process_multi_threaded(..., threads=1) unit by unit: per unit in the reference's order (ps), the
   byte length and sha256 of its piece of each FASTQ file (the files are the pieces concatenated in ps order).  Units
   run in `workers` spawned processes.  Returns [(ps, region_idx, cpy, templates, len1, sha1, len2, sha2)]."""
-  import multiprocessing as mp
   p, passes = read_model_params(model['mean_rlen'], coverage)
   units = work_units(seed, [len(r['v']) for r in vdf], passes)
   jobs = []
@@ -318,10 +333,28 @@ def unit_digests(seqs, vdf, sample, model, coverage, seed, workers=8):
     soa = {'pos': pos, 'op': op, 'oplen': oplen, 'alt_off': aoff, 'alt_len': alen, 'alt_pool': pool}
     jobs.append((seqs[chrom][s0:e], s0, soa, p, int(model['mean_rlen']), model['cum_tlen'], s,
                  '{}:{}:{}'.format(sample, 0, ps), chrom, cpy))
-  order = sorted(range(len(jobs)), key=lambda k: -len(jobs[k][0]))   # longest first
-  with mp.get_context('spawn').Pool(max(1, min(workers, len(jobs)))) as pool:
+  res = digest_jobs(jobs, workers)
+  return [(ps, units[ps][0], units[ps][1]) + tuple(res[ps]) for ps in range(len(jobs))]
+
+
+def _ref_len(ref):
+  return ref[2] if isinstance(ref, tuple) else len(ref)
+
+
+def digest_jobs(jobs, workers=8):
+  """_unit_digest over jobs (ref_seq, s0, soa, p, rlen, cum_tlen, seed, stub, chrom, cpy) in `workers` spawned
+  processes, longest region first; results in job order.  The pool is closed and joined (not terminated)."""
+  import multiprocessing as mp
+  order = sorted(range(len(jobs)), key=lambda k: -_ref_len(jobs[k][0]))   # longest first
+  pool = mp.get_context('spawn').Pool(max(1, min(workers, len(jobs))))
+  try:
     got = pool.map(_unit_digest, [jobs[k] for k in order], chunksize=1)
+  except BaseException:
+    pool.terminate()
+    raise
+  pool.close()
+  pool.join()
   res = [None] * len(jobs)
   for k, r in zip(order, got):
     res[k] = r
-  return [(ps, units[ps][0], units[ps][1]) + tuple(res[ps]) for ps in range(len(jobs))]
+  return res

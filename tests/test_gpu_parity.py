@@ -1550,3 +1550,12 @@ def test_lookahead_batches_match_run_units(native, monkeypatch, gate):
   assert r0 == r1
   G.check_same(b1, a1, 'file 1 differs')
   G.check_same(b2, a2, 'file 2 differs')
+
+
+def test_scan_timeout_is_reported(ctx, native):
+  """A look-back scan whose tile 0 never runs: the timed-out waits are reported (MH_E_STATE) instead of a fabricated
+  zero prefix returned as success, and a correct scan after it succeeds (mh_scan.h's bounded wait)."""
+  rc, msg = ctx.selftest_scan_fault()
+  assert rc == native.MH_E_STATE, (rc, msg)
+  assert 'timed out' in msg
+  ctx.sync()   # the fault word was cleared by the report
