@@ -1262,6 +1262,15 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   // the sorted records deflated on the device (k_bgzf_blocks), then only the compressed bytes cross PCIe
   std::vector<int64_t> boff;
   int64_t nz = 0;
+  // gz_out is sized for the whole BAM (GBs): released on every exit, never kept beside the next job's buffers
+  struct GzRelease {
+    mh_ctx *c;
+    uint8_t *pin = nullptr;
+    ~GzRelease() {
+      if (pin) (void)hipHostFree(pin);
+      release(c->gz_out);
+    }
+  } gz_guard{ctx};
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
   tick("alloc");
   MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
@@ -1271,16 +1280,14 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
                                            B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
   // D2H through a page-locked 64 MiB piece (allocated once per call)
-  uint8_t *pin = nullptr;
-  HIPCHK(ctx, hipHostMalloc((void **)&pin, (size_t)1 << 26, hipHostMallocDefault));
+  HIPCHK(ctx, hipHostMalloc((void **)&gz_guard.pin, (size_t)1 << 26, hipHostMallocDefault));
+  uint8_t *const pin = gz_guard.pin;
   auto fetch = [&](int64_t o, int64_t len) -> const uint8_t * {
     return hipMemcpy(pin, z + o, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess ? pin : nullptr;
   };
   std::vector<int64_t> coff;
   std::string err;
   const bool wrote = bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err);
-  (void)hipHostFree(pin);
-  release(ctx->gz_out);   // (sized for the whole BAM: not kept beside the next job's buffers)
   if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
   tick("file");
   if (bai_path) {

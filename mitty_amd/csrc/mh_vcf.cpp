@@ -380,6 +380,9 @@ int32_t mh_vcf_region(mh_vcf *v, const char *chrom, int64_t start0, int64_t end,
   if (!v || !chrom || !ploidy) return MH_E_ARG;
   v->copies.clear();
   v->ploidy = 0;
+  // pysam's fetch (vcfio.py:62): a contig neither in the header nor among the records is ValueError('invalid contig')
+  if (!v->by_chrom.count(chrom) && !v->header_contigs.count(chrom))
+    return fail(v, MH_E_ARG, "invalid contig `" + std::string(chrom) + "`");
   std::vector<const mh_vcf::Rec *> recs;
   region_records(v, chrom, start0, end, recs);
   std::vector<int> g;

@@ -22,6 +22,7 @@ class _Prefetch:
     self._held = 0             # bytes read and not yet taken
     self._eof = False
     self._err = None
+    self._stop = False         # close(): the reader thread closes the input and ends
     self._piece, self._max = piece, max_bytes
     self._t = threading.Thread(target=self._run, args=(fname,), daemon=True)
     self._t.start()
@@ -32,12 +33,16 @@ class _Prefetch:
         read = getattr(fp, 'read1', fp.read)
         while True:
           with self._cv:
-            while self._held >= self._max:
+            while self._held >= self._max and not self._stop:
               self._cv.wait()
+            if self._stop:
+              break
           b = read(self._piece)   # what the pipe holds, or a whole piece of a file
           if not b:
             break
           with self._cv:
+            if self._stop:
+              break
             self._pieces.append(b)
             self._held += len(b)
             self._cv.notify_all()
@@ -47,6 +52,15 @@ class _Prefetch:
       with self._cv:
         self._eof = True
         self._cv.notify_all()
+
+  def close(self):
+    """Stop reading: the thread drops what it holds and closes the input (a FIFO producer then gets EPIPE instead of
+    blocking on a reader that is gone).  A read already waiting on the pipe ends when the producer writes."""
+    with self._cv:
+      self._stop = True
+      self._pieces.clear()
+      self._held = 0
+      self._cv.notify_all()
 
   def take(self, want):
     """Up to about `want` bytes: blocks until some are there, then takes what is queued.  b'' at end of file."""
@@ -87,7 +101,16 @@ def stream_templates(fastq1, fastq2, consume, chunk=1 << 30, limit=None, max_ahe
   piece = min(chunk, 16 << 20)
   r1 = _Prefetch(fastq1, piece, ahead)
   r2 = _Prefetch(fastq2, piece, ahead) if fastq2 else None
-  buf1, buf2 = b'', (b'' if fastq2 else None)
+  try:
+    return _stream(r1, r2, consume, chunk, limit)
+  finally:   # an early return (limit) or an error: the readers stop and close their inputs
+    r1.close()
+    if r2 is not None:
+      r2.close()
+
+
+def _stream(r1, r2, consume, chunk, limit):
+  buf1, buf2 = b'', (b'' if r2 is not None else None)
   eof1 = eof2 = False
   total, stalled = 0, False
   while True:

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04a
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_rccl.py tests/test_gpu_parity.py::test_scan_timeout_is_reported > $O/pytest.log 2>&1
+  tests/test_gpu_rccl.py tests/test_gpu_parity.py::test_scan_timeout_is_reported tests/test_gpu_parity.py::test_device_bgzf_round_trip > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
 python3 scripts/bsum.py $O/bench.json || true

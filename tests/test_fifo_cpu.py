@@ -155,6 +155,34 @@ def test_stream_templates_fifo_pair(tmp_path, style):
   assert b''.join(out[0]) == b''.join(r1) and b''.join(out[1]) == b''.join(r2)
 
 
+def test_stream_templates_limit_releases_fifo_producer(tmp_path):
+  """stream_templates returning early (limit, as god-aligner --max-templates): both readers stop and close their
+  FIFOs, so a producer still writing gets EPIPE instead of blocking forever."""
+  r1, r2 = _records(200000, b'/1'), _records(200000, b'/2')
+  f1, f2 = str(tmp_path / 'lf1'), str(tmp_path / 'lf2')
+  os.mkfifo(f1)
+  os.mkfifo(f2)
+  res = {}
+
+  def produce():
+    try:
+      with open(f1, 'wb') as a, open(f2, 'wb') as b:
+        for x, y in zip(r1, r2):
+          a.write(x)
+          b.write(y)
+      res['end'] = 'finished'
+    except BrokenPipeError:
+      res['end'] = 'epipe'
+  t = threading.Thread(target=produce, daemon=True)
+  t.start()
+  out = ([], [])
+  n = FS.stream_templates(f1, f2, _consume_into(out), chunk=1 << 20, limit=1000, max_ahead=4 << 20)
+  assert n == 1000
+  t.join(30)
+  assert not t.is_alive(), 'the FIFO producer is still blocked after the consumer stopped'
+  assert res['end'] == 'epipe'
+
+
 def test_write_pair_to_lockstep_fifo_reader(tmp_path):
   """Our producer side: 20 MB per file handed to write_pair, read by a consumer that alternates record by record
   between the two FIFOs (pysam.FastxFile zip, readcorrupt.py:49-53)."""

@@ -1455,15 +1455,22 @@ def _bgzf_members(z):
   return out
 
 
-@pytest.mark.parametrize('name', ['fastq', 'random', 'zeros', 'one', 'block', 'block1', 'large', 'mixed'])
+@pytest.mark.parametrize('name', ['fastq', 'random', 'zeros', 'one', 'block', 'block1', 'large', 'mixed', 'chunked'])
 def test_device_bgzf_round_trip(ctx, name):
   """GPU deflate (a workgroup per BGZF block, eight dynamic-Huffman slices): every member a valid BGZF block, the
-  whole inflating (zlib) to the input; incompressible blocks stored; FASTQ about as small as gzip -1."""
+  whole inflating (zlib) to the input; incompressible blocks stored; FASTQ about as small as gzip -1.  'chunked':
+  more than one launch's 8192 blocks (mh_deflate.hip bgzf_device: slots reused, output appended at the running
+  offset across the seam)."""
   import os as _os
   fq = G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz')
-  data = {'fastq': fq, 'random': _os.urandom(300_001), 'zeros': b'\0' * 1_000_000, 'one': b'@',
-          'block': fq[:0xff00], 'block1': fq[:0xff01], 'large': (fq * 40)[:25_000_003],
-          'mixed': fq[:100_000] + _os.urandom(70_000) + b'~' * 90_000 + fq[:50_000]}[name]
+  if name == 'chunked':
+    n = 8192 * 0xff00 + 3 * 0xff00 + 12345                 # two launches: 8192 + 4 blocks
+    noise = _os.urandom(1 << 20)
+    data = ((fq + noise) * (n // (len(fq) + len(noise)) + 1))[:n]
+  else:
+    data = {'fastq': fq, 'random': _os.urandom(300_001), 'zeros': b'\0' * 1_000_000, 'one': b'@',
+            'block': fq[:0xff00], 'block1': fq[:0xff01], 'large': (fq * 40)[:25_000_003],
+            'mixed': fq[:100_000] + _os.urandom(70_000) + b'~' * 90_000 + fq[:50_000]}[name]
   z = ctx.bgzf_compress(data)
   members = _bgzf_members(z)
   assert sum(m[1] for m in members) == len(data)

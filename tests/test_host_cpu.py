@@ -343,6 +343,12 @@ def test_filter_variants_errors(tmp_path):
     vcfio.prepare_variant_file(str(ok), 'S1', str(tmp_path / 'c3.bed'), str(tmp_path / 'o.vcf'))
   (tmp_path / 'c2.bed').write_text('1\t0\t100\n2\t0\t100\n')
   assert vcfio.prepare_variant_file(str(ok), 'S1', str(tmp_path / 'c2.bed'), str(tmp_path / 'o.vcf'))[0] == 1
+  # the generate-reads load path (load_variant_file, vcfio.py:62 — the same fetch) rejects the unknown contig too, and
+  # a declared contig without records is an empty diploid region
+  with pytest.raises(ValueError, match='invalid contig `3`'):
+    vcfio.load_variants_soa(str(ok), 'S1', str(tmp_path / 'c3.bed'))
+  r = vcfio.load_variants_soa(str(ok), 'S1', str(tmp_path / 'c2.bed'))
+  assert r[1]['ploidy'] == 2 and all(len(c['pos']) == 0 for c in r[1]['copies'])
 
 
 def test_native_fasta_reader(tmp_path):
