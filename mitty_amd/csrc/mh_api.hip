@@ -301,11 +301,15 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   // bench measured 2-3 % shorter steps with 2 or 3, with slower writers), off when the device cannot wait on memory
   const char *ge = getenv("MH_WRITER_GATE");
   ctx->gate_at = ge ? atoi(ge) : -1;
+  const char *hf = getenv("MH_HAP_FWD");
+  ctx->hap_fwd = hf && atoi(hf) != 0;
+  const char *gt = getenv("MH_WRITER_GATE_TAIL");
+  ctx->gate_tail = gt ? std::max(0, atoi(gt)) : 0;
   int can_wait = 0;
   if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess) can_wait = 0;
   (void)hipGetLastError();
   hipError_t ge1 = hipSuccess, ge2 = hipSuccess, ge3 = hipSuccess;
-  if (ctx->gate_at >= 0 && can_wait) {
+  if ((ctx->gate_at >= 0 || ctx->gate_tail > 0) && can_wait) {
     void *g = nullptr;
     if (hipStreamCreateWithFlags(&ctx->gstream, hipStreamNonBlocking) == hipSuccess &&
         hipEventCreateWithFlags(&ctx->ev_sorted, hipEventDisableTiming) == hipSuccess &&

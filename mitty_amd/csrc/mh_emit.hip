@@ -885,9 +885,13 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     if (eg > h.hap_len) eg = h.hap_len;
     if (ag > h.hap_len) ag = h.hap_len;
     const int64_t lg = eg > ag ? eg - ag : 0;
-    const int64_t a2g = sg ? h.hap_len - ag - lg : ag;    // mate 1: the reverse-complement haplotype
+    // mate 1: a forward range of the reverse-complement haplotype, or (forward-only haplotypes) the forward window
+    // reverse-complemented on its way into LDS: chunk c lands mirrored at 16 (cmax - c), bytes reversed
+    const bool rev = sg && h.rc == nullptr;
+    const int64_t a2g = sg && !rev ? h.hap_len - ag - lg : ag;
     const int64_t a16 = a2g & ~(int64_t)15;
-    const uint8_t *hsrc = (sg ? h.rc : h.hap) + a16;
+    const uint8_t *hsrc = (sg && !rev ? h.rc : h.hap) + a16;
+    const int32_t cmax = lg > 0 ? (int32_t)(((a2g + lg - 1) >> 4) - (a16 >> 4)) : 0;
     uint4 wv[ED_GMAX];
     uint32_t use = 0;
 #pragma unroll
@@ -899,8 +903,14 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     }
     const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
 #pragma unroll
-    for (int k = 0; k < ED_GMAX; k++)
-      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (q3 + 3 * k) : o_dump)) = wv[k];
+    for (int k = 0; k < ED_GMAX; k++) {
+      const int c = q3 + 3 * k;
+      uint4 v = wv[k];
+      if (rev)
+        v = make_uint4(comp4(__builtin_bswap32(v.w)), comp4(__builtin_bswap32(v.z)), comp4(__builtin_bswap32(v.y)),
+                       comp4(__builtin_bswap32(v.x)));
+      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (rev ? cmax - c : c) : o_dump)) = v;
+    }
   } else if (tid < 64) {
     // wave 0: lane = read (template jf, mate s)
     const int jf = tid >> 1, s = tid & 1;
@@ -993,8 +1003,10 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       const int32_t lh = Lp + nd + Lm;
       const int32_t qb = o_q + jf * qstride + head - lh, sb = lh + rest + 1;
       if (keep) {
-        const int64_t a2 = s ? h.hap_len - a - S : a;              // mate 1 reads the reverse complement forward
-        mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + (int32_t)(a2 & 15);
+        // mate 1 reads the reverse complement forward: from rc at hap_len - a - S, or from the mirrored LDS window
+        const int32_t lead = !s ? (int32_t)(a & 15)
+                                : h.rc ? (int32_t)((h.hap_len - a - S) & 15) : (int32_t)((-(a + S)) & 15);
+        mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + lead;
         mt.S[fr] = S;
         mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
@@ -2021,7 +2033,7 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
                  (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
-                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, (const Node16 *)h.nd.p, h.n_bkt, h.p_min,
+                 h.rc_valid ? (const uint8_t *)h.rc.p : nullptr, (const int32_t *)h.bkt.p, (const Node16 *)h.nd.p, h.n_bkt, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 
@@ -2293,7 +2305,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     // the writer gate: this job's writers from the gate_at-th on wait for the next job's sorts (mh_internal.h); with
     // a batch begun ahead (mh_sample_units_begin: the lookahead pipeline) that batch is the next job and its sort is
     // already queued, so they wait for gate >= job
-    if (ctx->gate && ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at && ctx->job > 0) {
+    const bool gate_here = ctx->gate_tail > 0 ? ctx->writers_in_job == std::max(0, ctx->job_units - ctx->gate_tail)
+                                              : ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at;
+    if (ctx->gate && gate_here && ctx->job > 0) {
       const uint32_t want = ctx->sample_state ? ctx->job : ctx->job + 1;
       if (gate_debug()) fprintf(stderr, "mh gate: writer %d of job %u waits for %u\n", ctx->writers_in_job, ctx->job,
                                 want);

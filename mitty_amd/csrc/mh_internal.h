@@ -65,6 +65,7 @@ struct Hap {
   mutable bool used_set = false;
   mutable uint32_t used_gate = 0;      // the gate value that writer needs
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
+  bool rc_valid = false;       // rc built for this haplotype (not in forward-only mode: mh_ctx::hap_fwd)
   DevBuf nd;    // Node16 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
@@ -183,6 +184,8 @@ struct mh_ctx {
   uint32_t gate_waited = 0;        // the largest value a queued writer waits for
   uint32_t gate_written = 0;       // the largest value a queued gate write stores
   int32_t gate_at = -1;
+  int32_t gate_tail = 0;           // MH_WRITER_GATE_TAIL=D: the gate holds a job's last D writers instead
+  int32_t job_units = 0;           // units of the current job (the writers it will queue)
   int32_t writers_in_job = 0;
   static constexpr int N_USORT = 4;   // units of a batch sorted before any is chased (per unit: ts, keys, values, heads)
   mh::DevBuf usort[N_USORT][4];
@@ -250,6 +253,9 @@ struct mh_ctx {
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
+  // forward-only haplotypes (MH_HAP_FWD=1, experiment): no reverse-complement copy; the writer reverse-complements
+  // mate-1 windows into LDS itself
+  bool hap_fwd = false;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas

@@ -1388,6 +1388,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
   ctx->job++;   // a new job: its writers count from 0 for the gate, and it opens the previous job's gate
   ctx->writers_in_job = 0;
+  ctx->job_units = n_units;
   hipStream_t st = ctx->stream;
 
   // ---- plan ---------------------------------------------------------------------------------------------------

@@ -20,4 +20,7 @@ for dbg in 1 8 16 9 17 24 25 32; do
   MH_EW_DBG=$dbg timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-e2e > $O/dbg_$dbg.json 2> $O/dbg_$dbg.err || exit $?
   python3 -c "import json; d=json.load(open('$O/dbg_$dbg.json')); r=d['roofline']; print('dbg $dbg', round(d['value']/1e9,3), round(d['ms_per_step'],1), 'writer ms', round(r['avg_launch_ms'],3))"
 done
+
+timeout -k 10 120 ./scripts/calib_writer > $O/calib_writer.json || exit $?
+cat $O/calib_writer.json
 echo done

@@ -353,6 +353,16 @@ def test_unit_vs_oracle_nine_digit_positions(native, emit_mode):
                          emit_mode=emit_mode) > 10000
 
 
+@pytest.mark.parametrize('model', G.MODELS)
+def test_unit_vs_oracle_forward_haplotype(native, monkeypatch, model):
+  """Forward-only haplotypes (MH_HAP_FWD=1: no reverse-complement copy; the writer reverse-complements mate-1
+  windows into LDS, chunks mirrored): byte-identical to the oracle, with an offset region (reads cut by the haplotype
+  end, ragged window starts)."""
+  monkeypatch.setenv('MH_HAP_FWD', '1')
+  assert _unit_vs_oracle(2_000_000, 17, model) > 10000
+  _unit_vs_oracle(1_200_000, 4000000001, model, n_seed=7, rate=8e-3, start0=98_765)
+
+
 def test_batched_units_vs_oracle(native):
   """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
   reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated."""
@@ -786,8 +796,9 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
   G.check_same(d2, l2, 'fastq2')
 
 
-@pytest.mark.parametrize('tables,write2', [('lds', True), ('global', True), ('lds', False)])
-def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2):
+@pytest.mark.parametrize('tables,write2,fwd', [('lds', True, 0), ('global', True, 0), ('lds', False, 0),
+                                               ('lds', True, 1)])
+def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2, fwd):
   """Philox-mode corruption (the writer's len(seq) layout + k_cr_inplace) byte for byte against the numpy
   restatement of the draw scheme with full 53-bit uniforms (tests/philox_ref.py) applied to the perfect reads of the
   same sampling.  No N in the genome, so every template is kept and cnt - 1 is the template index; the bucket table
@@ -797,6 +808,8 @@ def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, wri
   from tests import philox_ref
   if tables == 'global':
     monkeypatch.setenv('MH_CR_GLOBAL', '1')
+  if fwd:   # forward-only haplotypes: the corruption rows' substitutions land in the mirrored mate-1 windows
+    monkeypatch.setenv('MH_HAP_FWD', '1')
   mdl = G.model('hiseq-X-v2.5-Garvan')
   p, _ = _native.read_model_params(150, 30.0)
   seq = synth.contig(400_000, 5, n_gaps=False)
@@ -1401,11 +1414,14 @@ def test_philox_sampling_properties(native):
     eng.close()
 
 
-def test_writer_gate_pipelined_jobs(native, monkeypatch):
+@pytest.mark.parametrize('knob,value', [('MH_WRITER_GATE', '2'), ('MH_WRITER_GATE_TAIL', '1'),
+                                        ('MH_WRITER_GATE_TAIL', '3')])
+def test_writer_gate_pipelined_jobs(native, monkeypatch, knob, value):
   """The opt-in writer gate (MH_WRITER_GATE=2: a job's writers from the third on wait on the device until the next
-  job has sorted; each batch's units sorted before any is chased): three 4-unit jobs queued back to back, the arenas
-  read only at the end, equal three times the oracle's job (reference unit order, qname serials 0..3)."""
-  monkeypatch.setenv('MH_WRITER_GATE', '2')
+  job has sorted; each batch's units sorted before any is chased; MH_WRITER_GATE_TAIL=D: a job's last D writers wait):
+  three 4-unit jobs queued back to back, the arenas read only at the end, equal three times the oracle's job
+  (reference unit order, qname serials 0..3)."""
+  monkeypatch.setenv(knob, value)
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from oracle import oracle as O
