@@ -101,6 +101,10 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
+  ap.add_argument('--unit-order', default='ps', choices=['ps', 'copy'],
+                  help='wgs: the order a rank emits its units in: ps = the reference\'s unit order; copy = grouped by '
+                       '(region, copy), so both passes of a haplotype run back to back (the arena bytes per unit are '
+                       'the same; only their order in the step differs)')
   ap.add_argument('--pipeline', default='batch', choices=['batch', 'lookahead', 'phased', 'phased-sync'],
                   help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
                        'writers of batch k); lookahead = batch k+1\'s sampling up to its permutation sort queued '
@@ -511,6 +515,8 @@ def run_genome(a, rank, world, local):
       sys.exit('bench.py: --plan-share R/N runs in one process (0 <= R < N)')
   pieces = D.plan_pieces(weights, plan_world, 'lpt')                  # 100 units: whole units by LPT at any N
   mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == plan_rank]
+  if a.unit_order == 'copy':
+    mine.sort(key=lambda u: (u[1], u[2], u[0]))
   regions = sorted({ri for _, ri, _, _ in mine})
   t_synth = time.perf_counter()
   data = synth.genome_regions(contigs, regions, workers=max(1, a.synth_workers // world))
