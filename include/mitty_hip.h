@@ -172,6 +172,14 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2);
+/* The byte sizes a slice [t_begin, t_end) of the current template set will emit (t_end < 0: the whole set), without
+ * writing it: the measure pass and its totals only (kept templates, bytes per FASTQ file), no buffer set held.  The
+ * multi-GPU writer (mitty_amd/distributed.py) all-reduces these to place every piece in the files before any piece is
+ * written, so each piece is written as soon as it is emitted (readgenerate.py:233-253 streams its output).  The sizes
+ * equal the later mh_emit_reads_range's outputs for the same arguments. */
+int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
+                        int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 /* mh_emit_reads without a host round trip (the engine's pipelined path; same bytes, readgenerate.py:184-230): the
  * unit's measure pass, record offsets, writer and corruption are queued on the writer stream and the call returns a
  * ticket at once.  The unit lands in the arenas after the units queued before it (its base offsets come from the

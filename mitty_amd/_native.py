@@ -23,7 +23,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_begin', 'mh_sample_units_end',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
-           'mh_emit_reads_range', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
+           'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
@@ -99,6 +99,8 @@ def lib():
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
+  _sig(L, 'mh_emit_measure', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64, c_i64,
+                              P_i64, P_i64, P_i64])
   _sig(L, 'mh_bam_set_refs', [c_vp, c_i32, ctypes.c_char_p, c_vp])
   _sig(L, 'mh_bam_add_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_bam_add_output', [c_vp, c_i64, P_i64])
@@ -554,6 +556,26 @@ class Context:
                                             int(t_range[1]), int(cnt_base), ctypes.byref(k), ctypes.byref(b1),
                                             ctypes.byref(b2)))
     return k.value, b1.value, b2.value
+
+  def emit_measure(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, t_range=None, cnt_base=0):
+    """(kept, bytes1, bytes2) that emit_reads with the same arguments will produce, without writing anything."""
+    k, b1, b2 = c_i64(), c_i64(), c_i64()
+    t0, t1 = t_range if t_range is not None else (0, -1)
+    self._chk(self._L.mh_emit_measure(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                      1 if write_fastq2 else 0, int(unit_key), int(t0), int(t1), int(cnt_base),
+                                      ctypes.byref(k), ctypes.byref(b1), ctypes.byref(b2)))
+    return k.value, b1.value, (b2.value if write_fastq2 else 0)
+
+  def bgzf_range(self, f, off, n, pin):
+    """Arena bytes [off, off + n) of file f BGZF-compressed on the GPU (mh_output_bgzf_range) into the page-locked
+    buffer pin; returns the compressed bytes (no EOF marker)."""
+    if n <= 0:
+      return b''
+    cap = n + (n // 0xff00 + 2) * 40 + 64
+    pin.reserve(cap)
+    used = c_i64()
+    self._chk(self._L.mh_output_bgzf_range(self._h, int(f), int(off), int(n), c_vp(pin.ptr), cap, ctypes.byref(used)))
+    return bytes(pin.view(used.value))
 
   def count_kept(self, slot, t_begin, t_end):
     """Templates of the current set in [t_begin, t_end) that pass the N filter."""

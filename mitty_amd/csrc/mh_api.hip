@@ -922,6 +922,24 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
                     false, out_kept, out_b1, out_b2);
 }
 
+int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
+                        int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
+  CTX_GUARD_NOJOIN(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (t_begin < 0 || (t_end >= 0 && t_end < t_begin) || cnt_base < 0) return arg_fail(ctx, MH_E_ARG, "bad template range");
+  MH_TRY(emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,
+                    true, out_kept, out_b1, out_b2));
+  auto tit = ctx->tsets.find(ctx->cur_tpl);   // the preparation is dropped: its buffer set is free again
+  if (tit != ctx->tsets.end() && tit->second.prep.valid) {
+    ctx->eset[tit->second.prep.set].prepared = false;
+    tit->second.prep.valid = false;
+  }
+  return MH_OK;
+}
+
 int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end, int64_t *out_kept) {
   CTX_GUARD(ctx);
   auto it = ctx->haps.find(slot);

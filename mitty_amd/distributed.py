@@ -10,8 +10,12 @@ illumina.py:56-58), so the path shards without any data-path collective:
   to the other ranks (RCCL over xGMI on device buffers; gloo on host arrays for the CPU tests); the cnt of a slice's
   first kept template comes from one all-reduce of the per-slice N-filter survivor counts (the only coupling between
   templates, an exclusive prefix);
-* one more all-reduce of per-piece byte sizes gives every piece its file offset, and each rank pwrites its pieces
-  there, so the files are byte-identical to the single-GPU run (= reference --threads 1) at any GPU count.
+* the output streams: every piece is measured first (mh_emit_measure: the measure pass alone, its templates kept
+  resident under their own set id) and one all-reduce of the sizes places every piece in the files; then each piece
+  is emitted, fetched and pwritten at its offset, and the arenas are recycled after it (readgenerate.py:233-253
+  writes as it goes).  A '.gz' file's pieces are deflated on the device as they are emitted and held compressed
+  (~4.5x smaller) until an all-reduce of the compressed sizes places them.  The files are byte-identical to the
+  single-GPU run (= reference --threads 1) at any GPU count.
 
 The collectives carry a few int64 per piece; no sequence data crosses xGMI.  Outputs must be regular files
 (ranks write at offsets); FIFOs / process substitution need the single-GPU path.
@@ -92,8 +96,11 @@ class DeviceBackend:
   """The per-rank device side: one Engine (HIP context) on this rank's GPU."""
 
   def __init__(self, device):
+    from mitty_amd import _native
     from mitty_amd.engine import Engine
     self.eng = Engine(device)
+    self._slots = {}   # template set id -> haplotype slot
+    self._pin = _native.PinnedBuffer()
 
   def set_corruption(self, model, seed):
     import numpy as np
@@ -102,16 +109,19 @@ class DeviceBackend:
   def load_region(self, ri, region, seq):
     self.eng.load_region(ri, region, seq)
 
-  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None):
-    """units: [(ps, ri, cpy, seed)]; the units k in `which` (all by default) are sampled into template id k.  Every
-    unit's haplotype is built (its slices are emitted here).  Returns template counts (None where not sampled)."""
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None, ids=None):
+    """units: [(ps, ri, cpy, seed)]; the units k in `which` (all by default) are sampled into template set ids[k]
+    (k by default).  Every unit's haplotype is built (its slices are emitted here).  Returns template counts (None
+    where not sampled)."""
     from mitty_amd.engine import RNG_MODES
-    self._slots = [self.eng.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    ids = list(range(len(units))) if ids is None else list(ids)
+    for k, (_, ri, cpy, _) in enumerate(units):
+      self._slots[ids[k]] = self.eng.haplotype(ri, cpy, soa_of(ri, cpy))[0]
     which = list(range(len(units))) if which is None else list(which)
     out = [None] * len(units)
     if which:
-      ns = self.eng.ctx.sample_units(which, [self._slots[k] for k in which], [units[k][3] for k in which], p, rlen,
-                                     cum_tlen, RNG_MODES[rng])
+      ns = self.eng.ctx.sample_units([ids[k] for k in which], [self._slots[ids[k]] for k in which],
+                                     [units[k][3] for k in which], p, rlen, cum_tlen, RNG_MODES[rng])
       for k, n in zip(which, ns):
         out[k] = int(n)
     return out
@@ -165,6 +175,12 @@ class DeviceBackend:
     self.eng.ctx.use_templates(k)
     return self.eng.ctx.count_kept(self._slots[k], t0, t1)
 
+  def measure(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+    """-> (kept, bytes file 1, bytes file 2) that emit() with the same arguments writes (mh_emit_measure)."""
+    ctx = self.eng.ctx
+    ctx.use_templates(k)
+    return ctx.emit_measure(self._slots[k], stub, chrom, cpy, write2, unit_key, t_range, cnt_base)
+
   def emit(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
     """-> (kept, (arena offset, length) for file 1, same for file 2)"""
     ctx = self.eng.ctx
@@ -175,6 +191,13 @@ class DeviceBackend:
 
   def fetch(self, r1, r2):
     return self.eng.ctx.fetch_output(r1[0], r1[1], r2[0], r2[1])
+
+  def fetch_gz(self, f, r):
+    """Arena range r = (offset, length) of file f as BGZF members deflated on the device (mh_output_bgzf_range)."""
+    return self.eng.ctx.bgzf_range(f, r[0], r[1], self._pin)
+
+  def reset_output(self):
+    self.eng.ctx.reset_output()
 
   def close(self):
     self.eng.close()
@@ -226,22 +249,27 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       batches.append(cur)
       cur, draws = [], 0
 
-  emitted = {}   # piece index -> (kept, range1, range2)
+  # ---- phase A: every piece sampled (its templates resident under its own set id) and measured ----------------
   stats = {'units': len(units), 'pieces': len(mine), 'templates': 0, 'kept': 0}
   soa_of = lambda r, c: vdf[r]['copies'][c]
+  fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
+  gz = [fn.endswith('.gz') for fn in fnames] + [False]
+  plan = {}   # piece index -> (template set id, stub, chrom, cpy, unit seed, t_range, cnt base)
+  sizes = {}  # piece index -> (kept, bytes1, bytes2)
   for batch in batches:
+    ids = list(batch)   # the unit index is the template set id: every set stays resident until phase B
     if sliced and world > 1:
       # each unit sampled once, on rank u mod W; its template count all-reduced, its arrays broadcast
       owner = [u % world for u in batch]
       got = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
-                           read_model['cum_tlen'], rng, which=[k for k, o in enumerate(owner) if o == rank])
+                           read_model['cum_tlen'], rng, which=[k for k, o in enumerate(owner) if o == rank], ids=ids)
       ns = allreduce_i64([got[k] if o == rank else 0 for k, o in enumerate(owner)], group)
       for k, o in enumerate(owner):
-        backend.share(k, ns[k], o, read_model['rlen'], group)
+        backend.share(ids[k], ns[k], o, read_model['rlen'], group)
       stats['sampled'] = stats.get('sampled', 0) + sum(1 for o in owner if o == rank)
     else:
       ns = backend.sample([units[u] for u in batch], soa_of, read_model['p'], read_model['rlen'],
-                          read_model['cum_tlen'], rng)
+                          read_model['cum_tlen'], rng, ids=ids)
     k_of = {u: k for k, u in enumerate(batch)}
     bases = {}
     if sliced:
@@ -249,7 +277,7 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       for i in mine:
         u, s, S, _ = pieces[i]
         if u in k_of:
-          local[i] = backend.count_kept(k_of[u], *slice_range(ns[k_of[u]], s, S))
+          local[i] = backend.count_kept(u, *slice_range(ns[k_of[u]], s, S))
       kept_all = allreduce_i64(local, group)
       bases = dict(enumerate(exclusive_bases(pieces, kept_all)))
     for i in mine:
@@ -257,60 +285,88 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       if u not in k_of:
         continue
       ps, ri, cpy, useed = units[u]
-      k = k_of[u]
-      rng_range = slice_range(ns[k], s, S) if S > 1 else None
-      emitted[i] = backend.emit(k, '{}:{}:{}'.format(sample_name, 0, ps), vdf[ri]['region'][0], cpy, write2, useed,
-                                rng_range, bases.get(i, 0))
-      stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k]
-      stats['kept'] += emitted[i][0]
+      rng_range = slice_range(ns[k_of[u]], s, S) if S > 1 else None
+      plan[i] = (u, '{}:{}:{}'.format(sample_name, 0, ps), vdf[ri]['region'][0], cpy, useed, rng_range, bases.get(i, 0))
+      if not all(gz[:len(fnames)]):   # plain files are placed from these sizes before anything is written
+        sizes[i] = backend.measure(u, plan[i][1], plan[i][2], cpy, write2, useed, rng_range, bases.get(i, 0))
+      stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k_of[u]]
 
-  # file offsets of every piece, then positioned writes.  A '.gz' output (decided per file, as FastqSink does): each
-  # piece becomes BGZF members first (decompressed content identical to the one-GPU file; rank 0 adds the EOF marker)
-  fnames = [fastq1_fname] + ([fastq2_fname] if write2 else [])
-  gz = [fn.endswith('.gz') for fn in fnames] + [False]
-  payload = {}
-  if any(gz):
-    from mitty_amd import _native
-    for i in sorted(emitted):
-      _, r1, r2 = emitted[i]
-      d1, d2 = backend.fetch(r1, r2 if write2 else (0, 0))
-      payload[i] = (_native.bgzf_compress(d1) if gz[0] else d1, _native.bgzf_compress(d2) if gz[1] else d2)
-  sz = [0] * (2 * len(pieces))
-  for i, (_, r1, r2) in emitted.items():
-    if payload:
-      sz[2 * i], sz[2 * i + 1] = len(payload[i][0]), len(payload[i][1]) if write2 else 0
-    else:
-      sz[2 * i], sz[2 * i + 1] = r1[1], r2[1]
-  sz = allreduce_i64(sz + [stats['templates'], stats['kept']], group)
-  tot_templates, tot_kept = sz[-2], sz[-1]
-  off1, total1 = file_offsets(sz[0:2 * len(pieces):2])
-  off2, total2 = file_offsets(sz[1:2 * len(pieces):2])
-  totals = (total1, total2)
-  if rank == 0:
-    for fn, total, z in zip(fnames, totals, gz):
-      with open(fn, 'wb') as fp:
-        fp.truncate(total)
-        if z:
-          from mitty_amd import _native
-          fp.seek(total)
-          fp.write(_native.bgzf_eof())
-  if world > 1:
-    dist.barrier(group)
-  fds = [os.open(fn, os.O_WRONLY) for fn in fnames]
+  # plain files: every piece's offset from one all-reduce of the measured sizes; rank 0 sizes the files
+  off = [None, None]
+  if sizes:
+    sz = [0] * (2 * len(pieces))
+    for i, (_, b1, b2) in sizes.items():
+      sz[2 * i], sz[2 * i + 1] = b1, b2
+    sz = allreduce_i64(sz, group)
+    for f in range(len(fnames)):
+      if not gz[f]:
+        off[f], total = file_offsets(sz[f:2 * len(pieces):2])
+        if rank == 0:
+          with open(fnames[f], 'wb') as fp:
+            fp.truncate(total)
+    if world > 1:
+      dist.barrier(group)
+
+  # ---- phase B: each piece emitted, then written at its offset (plain) or deflated on the device and held (gz);
+  # the arenas are recycled after every piece -------------------------------------------------------------------
+  fds = [os.open(fn, os.O_WRONLY) if not gz[f] else None for f, fn in enumerate(fnames)]
+  held = {}   # piece index -> compressed bytes per gz file
+  raw = [0, 0]
   try:
-    for i in sorted(emitted):
-      _, r1, r2 = emitted[i]
-      d1, d2 = payload.pop(i) if payload else backend.fetch(r1, r2 if write2 else (0, 0))
-      _pwrite_all(fds[0], d1, off1[i])
-      if write2:
-        _pwrite_all(fds[1], d2, off2[i])
+    for i in sorted(plan):
+      k, stub, chrom, cpy, useed, rng_range, base = plan[i]
+      backend.reset_output()
+      kept, r1, r2 = backend.emit(k, stub, chrom, cpy, write2, useed, rng_range, base)
+      stats['kept'] += kept
+      raw[0] += r1[1]
+      raw[1] += r2[1] if write2 else 0
+      if i in sizes and (kept, r1[1], r2[1] if write2 else 0) != tuple(sizes[i]):
+        raise RuntimeError('piece {}: emitted {} differs from its measured sizes {}'.format(
+            i, (kept, r1[1], r2[1]), sizes[i]))
+      rs = (r1, r2)
+      plain = [f for f in range(len(fnames)) if not gz[f]]
+      if plain:
+        data = backend.fetch(r1 if 0 in plain else (0, 0), r2 if 1 in plain else (0, 0))
+        for f in plain:
+          _pwrite_all(fds[f], data[f], off[f][i])
+      held[i] = [backend.fetch_gz(f, rs[f]) if gz[f] else None for f in range(len(fnames))]
   finally:
     for fd in fds:
-      os.close(fd)
+      if fd is not None:
+        os.close(fd)
+
+  # gz files: offsets from the compressed sizes, then the held members written (rank 0 adds the EOF marker)
+  if any(gz[:len(fnames)]):
+    zs = [0] * (2 * len(pieces))
+    for i, h in held.items():
+      for f in range(len(fnames)):
+        if gz[f]:
+          zs[2 * i + f] = len(h[f])
+    zs = allreduce_i64(zs, group)
+    for f in range(len(fnames)):
+      if not gz[f]:
+        continue
+      zoff, ztotal = file_offsets(zs[f:2 * len(pieces):2])
+      if rank == 0:
+        from mitty_amd import _native
+        with open(fnames[f], 'wb') as fp:
+          fp.truncate(ztotal)
+          fp.seek(ztotal)
+          fp.write(_native.bgzf_eof())
+      if world > 1:
+        dist.barrier(group)
+      fd = os.open(fnames[f], os.O_WRONLY)
+      try:
+        for i, h in held.items():
+          _pwrite_all(fd, h[f], zoff[i])
+      finally:
+        os.close(fd)
+  held.clear()
+  tot = allreduce_i64([stats['templates'], stats['kept']] + raw, group)
   if world > 1:
     dist.barrier(group)
-  stats.update({'job_templates': tot_templates, 'job_kept': tot_kept, 'bytes1': total1,
-                'bytes2': total2 if write2 else 0, 'seconds': time.time() - t0, 'rank': rank, 'world': world})
+  stats.update({'job_templates': tot[0], 'job_kept': tot[1], 'bytes1': tot[2], 'bytes2': tot[3] if write2 else 0,
+                'seconds': time.time() - t0, 'rank': rank, 'world': world})
   return stats
 
 

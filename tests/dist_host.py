@@ -16,22 +16,28 @@ class OracleBackend:
   def load_region(self, ri, region, seq):
     self.regions[ri] = (region, seq)
 
-  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None):
-    self.recs = [None] * len(units)
+  def sample(self, units, soa_of, p, rlen, cum_tlen, rng, which=None, ids=None):
+    ids = list(range(len(units))) if ids is None else list(ids)
+    if not hasattr(self, 'recs'):
+      self.recs = {}
     self.sampled = []
+    out = []
     for k, (ps, ri, cpy, seed) in enumerate(units):
       if which is not None and k not in which:
+        self.recs.pop(ids[k], None)
+        out.append(None)
         continue
       (chrom, s0, _), seq = self.regions[ri]
       _, b1, b2 = O.generate_unit_soa(seq, s0, soa_of(ri, cpy), p, rlen, cum_tlen, seed, 'X:0:0', chrom, cpy)
-      self.recs[k] = (_records(b1), _records(b2))
+      self.recs[ids[k]] = (_records(b1), _records(b2))
       self.sampled.append(k)
-    return [None if r is None else len(r[0]) for r in self.recs]
+      out.append(len(self.recs[ids[k]][0]))
+    return out
 
-  def share(self, k, n, src, rlen, group=None):
+  def share(self, k, n, src, rlen, group=None, into=None):
     """The unit's records (the stand-in's 'templates') from rank src, as DeviceBackend.share sends arrays."""
     import torch.distributed as dist
-    obj = [self.recs[k] if dist.get_rank(group) == src else None]
+    obj = [self.recs.get(k) if dist.get_rank(group) == src else None]
     dist.broadcast_object_list(obj, src, group=group)
     assert obj[0] is not None and len(obj[0][0]) == n
     self.recs[k] = obj[0]
@@ -39,22 +45,39 @@ class OracleBackend:
   def count_kept(self, k, t0, t1):
     return t1 - t0
 
-  def emit(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+  def _data(self, k, stub, write2, t_range, cnt_base):
     r1, r2 = self.recs[k]
     t0, t1 = t_range if t_range is not None else (0, len(r1))
     out = []
     for f, recs in enumerate((r1, r2)):
       if f == 1 and not write2:
-        out.append((len(self.arena[1]), 0))
+        out.append(b'')
         continue
-      data = b''.join(b'@' + stub.encode() + b':' + str(cnt_base + j + 1).encode() + b'|' + recs[t0 + j]
-                      for j in range(t1 - t0))
+      out.append(b''.join(b'@' + stub.encode() + b':' + str(cnt_base + j + 1).encode() + b'|' + recs[t0 + j]
+                         for j in range(t1 - t0)))
+    return t1 - t0, out
+
+  def measure(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+    kept, (d1, d2) = self._data(k, stub, write2, t_range, cnt_base)
+    return kept, len(d1), len(d2)
+
+  def emit(self, k, stub, chrom, cpy, write2, unit_key, t_range, cnt_base):
+    kept, datas = self._data(k, stub, write2, t_range, cnt_base)
+    out = []
+    for f, data in enumerate(datas):
       out.append((len(self.arena[f]), len(data)))
       self.arena[f] += data
-    return t1 - t0, out[0], out[1]
+    return kept, out[0], out[1]
 
   def fetch(self, r1, r2):
     return bytes(self.arena[0][r1[0]:r1[0] + r1[1]]), bytes(self.arena[1][r2[0]:r2[0] + r2[1]])
+
+  def fetch_gz(self, f, r):
+    from mitty_amd import _native
+    return _native.bgzf_compress(bytes(self.arena[f][r[0]:r[0] + r[1]])) if r[1] else b''
+
+  def reset_output(self):
+    self.arena = [bytearray(), bytearray()]
 
   def close(self):
     pass

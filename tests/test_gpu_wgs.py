@@ -47,7 +47,7 @@ def oracle_units(genome):
   return O.unit_digests(genome['seqs'], vdf, SAMPLE, mdl, COVERAGE, SEED, workers=min(16, os.cpu_count() or 1))
 
 
-def _rank(rank, world, port, g, outdir):
+def _rank(rank, world, port, g, outdir, names=('r1.fq', 'r2.fq')):
   import torch.distributed as dist
   os.environ['MASTER_ADDR'] = '127.0.0.1'
   os.environ['MASTER_PORT'] = str(port)
@@ -57,21 +57,21 @@ def _rank(rank, world, port, g, outdir):
     from mitty_amd.readmodel import get_read_model
     mod, mdl = get_read_model(MODEL + '.pkl')
     st = D.generate_reads_distributed(g['fa'], g['vcf'], SAMPLE, g['bed'], mod, mdl, COVERAGE,
-                                      os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'), seed=SEED,
+                                      os.path.join(outdir, names[0]), os.path.join(outdir, names[1]), seed=SEED,
                                       backend=D.DeviceBackend(0), max_batch_draws=32_000_000)
     assert st['units'] == 100 and st['world'] == world
   finally:
     dist.destroy_process_group()
 
 
-def _run(world, g, outdir):
+def _run(world, g, outdir, names=('r1.fq', 'r2.fq')):
   import torch.multiprocessing as mp
   with socket.socket() as s:
     s.bind(('127.0.0.1', 0))
     port = s.getsockname()[1]
   os.makedirs(outdir, exist_ok=True)
   gg = {k: v for k, v in g.items() if k in ('fa', 'vcf', 'bed')}
-  mp.start_processes(_rank, args=(world, port, gg, outdir), nprocs=world, join=True, start_method='spawn')
+  mp.start_processes(_rank, args=(world, port, gg, outdir, names), nprocs=world, join=True, start_method='spawn')
 
 
 def _check_units(fname, units, which):
@@ -86,8 +86,9 @@ def _check_units(fname, units, which):
 
 
 def _file_digest(fname):
+  import gzip
   h = hashlib.sha256()
-  with open(fname, 'rb') as fp:
+  with (gzip.open if fname.endswith('.gz') else open)(fname, 'rb') as fp:
     for chunk in iter(lambda: fp.read(64 << 20), b''):
       h.update(chunk)
   return h.hexdigest()
@@ -111,3 +112,12 @@ def test_wgs_two_ranks_one_gpu_vs_oracle(genome, oracle_units):
   assert [_file_digest(os.path.join(out1, f)) for f in ('r1.fq', 'r2.fq')] == d2
   for f in ('r1.fq', 'r2.fq'):
     os.remove(os.path.join(out1, f))
+  # '.gz' outputs on 2 ranks: every piece deflated on its rank's device as it is emitted, placed by the all-reduced
+  # compressed sizes; a plain file beside a '.gz' one is written piece by piece at its measured offset
+  outz = str(genome['dir'] / 'wz')
+  _run(2, genome, outz, ('r1.fq.gz', 'r2.fq'))
+  assert [_file_digest(os.path.join(outz, f)) for f in ('r1.fq.gz', 'r2.fq')] == d2
+  with open(os.path.join(outz, 'r1.fq.gz'), 'rb') as fp:
+    assert fp.read(4) == b'\x1f\x8b\x08\x04'
+  for f in ('r1.fq.gz', 'r2.fq'):
+    os.remove(os.path.join(outz, f))
