@@ -116,10 +116,6 @@ int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, uint32_t gate) {
   return MH_OK;
 }
 
-bool gate_debug() {
-  static const bool d = getenv("MH_GATE_DEBUG") != nullptr;
-  return d;
-}
 
 static std::mutex g_gate_mu;   // gate_written is read-modify-written by both splice lanes (ensure -> gate_open)
 
@@ -127,7 +123,6 @@ void gate_open(mh_ctx *ctx) {
   if (!ctx->gate) return;
   std::lock_guard<std::mutex> lk(g_gate_mu);
   if (ctx->gate_waited <= ctx->gate_written) return;
-  if (gate_debug()) fprintf(stderr, "mh gate: open %u\n", ctx->gate_waited);
   (void)hipStreamWriteValue32(ctx->gstream, ctx->gate, ctx->gate_waited, 0);
   ctx->gate_written = ctx->gate_waited;
 }
@@ -140,7 +135,6 @@ int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
   if (!ctx->gate) return MH_OK;
   std::lock_guard<std::mutex> lk(g_gate_mu);
   if (value <= ctx->gate_written) return MH_OK;
-  if (gate_debug()) fprintf(stderr, "mh gate: release %u\n", value);
   HIPCHK(ctx, hipStreamWriteValue32(st, ctx->gate, value, 0));
   ctx->gate_written = value;
   return MH_OK;
@@ -149,8 +143,6 @@ int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
 int32_t sync_writers(mh_ctx *ctx) {
   gate_open(ctx);
   SYNCCHK(ctx, hipStreamSynchronize(ctx->wstream));
-  if (ctx->crstream) SYNCCHK(ctx, hipStreamSynchronize(ctx->crstream));
-  ctx->cr_pending = false;
   return MH_OK;
 }
 
@@ -244,21 +236,6 @@ int32_t mh_device_count(int32_t *out) {
   return MH_OK;
 }
 
-// The writer stream may be limited to a share of the CUs (MH_WRITER_CUS = eighths of each XCD's CUs, experiments):
-// the bandwidth-bound writers then leave whole CUs to the next job's latency-bound sampling kernels.
-static hipError_t create_writer_stream(mh_ctx *ctx, int device, int prio) {
-  const char *e = getenv("MH_WRITER_CUS");
-  const int eighths = e ? atoi(e) : 8;
-  hipDeviceProp_t prop;
-  if (eighths >= 8 || eighths <= 0 || hipGetDeviceProperties(&prop, device) != hipSuccess)
-    return hipStreamCreateWithPriority(&ctx->wstream, hipStreamNonBlocking, prio);
-  const int n = prop.multiProcessorCount;
-  std::vector<uint32_t> mask((n + 31) / 32, 0u);
-  for (int cu = 0; cu < n; cu++)
-    if ((cu % 8) < eighths) mask[cu / 32] |= 1u << (cu % 32);
-  return hipExtStreamCreateWithCUMask(&ctx->wstream, (uint32_t)mask.size(), mask.data());
-}
-
 int32_t mh_create(int32_t device, mh_ctx **out) {
   if (!out) return MH_E_ARG;
   *out = nullptr;
@@ -274,14 +251,12 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipSetDevice(device);
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const char *pe = getenv("MH_STREAM_PRIO");   // experiments: 0 disables the priorities
-  if (pe && atoi(pe) == 0) prio_lo = prio_hi = 0;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
-      create_writer_stream(ctx, device, prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->wstream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_writer, hipEventDisableTiming) != hipSuccess ||
       [&] {
@@ -308,21 +283,15 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   int can_wait = 0;
   if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess) can_wait = 0;
   (void)hipGetLastError();
-  hipError_t ge1 = hipSuccess, ge2 = hipSuccess, ge3 = hipSuccess;
   if ((ctx->gate_at >= 0 || ctx->gate_tail > 0) && can_wait) {
     void *g = nullptr;
     if (hipStreamCreateWithFlags(&ctx->gstream, hipStreamNonBlocking) == hipSuccess &&
         hipEventCreateWithFlags(&ctx->ev_sorted, hipEventDisableTiming) == hipSuccess &&
-        ((ge1 = hipExtMallocWithFlags(&g, 8, hipMallocSignalMemory)) == hipSuccess ||
-         (ge1 = hipMalloc(&g, 64)) == hipSuccess) &&
-        (ge2 = hipStreamWriteValue32(ctx->gstream, g, 0, 0)) == hipSuccess &&
-        (ge3 = hipStreamSynchronize(ctx->gstream)) == hipSuccess)
+        (hipExtMallocWithFlags(&g, 8, hipMallocSignalMemory) == hipSuccess || hipMalloc(&g, 64) == hipSuccess) &&
+        hipStreamWriteValue32(ctx->gstream, g, 0, 0) == hipSuccess && hipStreamSynchronize(ctx->gstream) == hipSuccess)
       ctx->gate = (uint32_t *)g;
     (void)hipGetLastError();
   }
-  if (getenv("MH_GATE_DEBUG"))
-    fprintf(stderr, "mh gate: at=%d can_wait=%d malloc=%d write=%d sync=%d gate=%p\n", ctx->gate_at, can_wait, (int)ge1,
-            (int)ge2, (int)ge3, (void *)ctx->gate);
   *out = ctx;
   return MH_OK;
 }
@@ -332,7 +301,6 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   gate_open(ctx);
   (void)hipStreamSynchronize(ctx->wstream);
-  if (ctx->crstream) (void)hipStreamSynchronize(ctx->crstream);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   for (auto x : ctx->xstream)
@@ -360,7 +328,11 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
-  release(ctx->d_used); for (int k = 0; k < 2; k++) { release(ctx->cr_rows[k]); release(ctx->cr_codes[k]); if (ctx->ev_rows[k]) (void)hipEventDestroy(ctx->ev_rows[k]); if (ctx->ev_rfree[k]) (void)hipEventDestroy(ctx->ev_rfree[k]); } release(ctx->scan_partials_w); release(ctx->rb_tmp);
+  release(ctx->d_used);
+  release(ctx->cr_rows);
+  release(ctx->cr_codes);
+  release(ctx->scan_partials_w);
+  release(ctx->rb_tmp);
   for (auto &b : ctx->sl2) release(b);
   for (auto &e : ctx->res_ev)
     if (e) (void)hipEventDestroy(e);
@@ -375,8 +347,6 @@ int32_t mh_destroy(mh_ctx *ctx) {
   (void)hipEventDestroy(ctx->ev_ready);
   (void)hipEventDestroy(ctx->ev_writer);
   (void)hipStreamDestroy(ctx->wstream);
-  if (ctx->crstream) (void)hipStreamDestroy(ctx->crstream);
-  if (ctx->ev_crw) (void)hipEventDestroy(ctx->ev_crw);
   bam_release(ctx->bam);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -1269,17 +1239,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   BamStore &B = ctx->bam;
   if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
-  static const bool tdbg = getenv("MH_BAM_TIMING") != nullptr;   // phase times to stderr (experiments)
-  auto t_now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  double t_prev = t_now();
-  auto tick = [&](const char *what) {
-    if (!tdbg) return;
-    const double t = t_now();
-    fprintf(stderr, "mh_bam_write_gpu %s %.3f s\n", what, t - t_prev);
-    t_prev = t;
-  };
   MH_TRY(bam_sort(ctx));
-  tick("sort");
   const int64_t n = B.n_rec;
   // the sorted records deflated on the device (k_bgzf_blocks), then only the compressed bytes cross PCIe
   std::vector<int64_t> boff;
@@ -1294,10 +1254,8 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     }
   } gz_guard{ctx};
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
-  tick("alloc");
   MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
                      (int64_t)ctx->gz_out.cap, &nz, &boff));
-  tick("deflate");
   const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
                                            B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
@@ -1311,15 +1269,12 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   std::string err;
   const bool wrote = bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err);
   if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
-  tick("file");
   if (bai_path) {
     std::vector<int64_t> soff((size_t)n + 1, 0);
     std::vector<BaiRec> info((size_t)n + 1);
     MH_TRY(bam_fetch_sorted(ctx, nullptr, soff.data(), (int32_t *)info.data()));
-    tick("bai fetch");
     if (!bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
       return arg_fail(ctx, MH_E_ARG, err);
-    tick("bai");
   }
   if (out_records) *out_records = n;
   if (out_bytes) *out_bytes = B.bytes;

@@ -631,8 +631,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int64_t add_bytes = 0;
   HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
   SYNCCHK(ctx, hipStreamSynchronize(st));
-  static const bool direct_off = getenv("MH_BAM_DIRECT") && atoi(getenv("MH_BAM_DIRECT")) == 0;   // experiments
-  if (sorted_direct && !direct_off && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
+  if (sorted_direct && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
     // the whole input is here (the context's own arenas) and the store is empty: sort first, then every record is
     // written once, straight to its coordinate-sorted place (no input-order copy, no gather)
     MH_TRY(ensure(ctx, B.key, sizeof(uint64_t) * n_rec));

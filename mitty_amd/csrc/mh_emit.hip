@@ -1115,8 +1115,6 @@ struct CiArgs {
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
   CorruptCfg cc;
-  int32_t dbg;            // experiments (MH_CR_DBG): 1 full blocks through the guarded per-base path (A/B); timing
-                          // only (wrong bytes): 2 no stores in full blocks, 4 no base loads, 8 no Philox, 16 the item loop alone
 };
 
 // The LDS-table BQ step of one base (k_cr_inplace's walk): bk = the base's bucket row, tp = its threshold-pair row.
@@ -1140,16 +1138,14 @@ __device__ __forceinline__ uint32_t cr_lds_walk(const uint8_t *bk, const uint16_
 // bk / tp: the bucket and threshold-pair rows of base n0 (row j of base n0 + j at bk + j * CB_ROW, tp + j * n_bq).
 __device__ __forceinline__ void cr_full_block(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
                                               const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f,
-                                              int n0, char *seq, uint64_t sa, uint4 g0, uint4 g1, char *qual,
-                                              int32_t dbg) {
+                                              int n0, char *seq, uint64_t sa, uint4 g0, uint4 g1, char *qual) {
   const int n_bq = cc.n_bq;
   // in phases, so each phase's fifteen LDS reads are in flight together (the arrays are registers: constant indices)
   uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], P[CI_BLK], V2[CI_BLK], F[CI_BLK], BQ[CI_BLK];
   const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
 #pragma unroll
   for (int g = 0; g < CI_BLK / 3; g++) {   // the five triple draws
-    const uint4 r = (dbg & 8) ? make_uint4(tl * 0x9E3779B9u + g, th ^ (cw * 0x85ebca6bu), cw * 0xc2b2ae35u + g, tl ^ g)
-                              : philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
+    const uint4 r = philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
     W[3 * g] = r.x;
     W[3 * g + 1] = r.y;
     W[3 * g + 2] = r.z;
@@ -1186,10 +1182,6 @@ __device__ __forceinline__ void cr_full_block(const uint8_t *bk, const uint16_t 
     if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
   }
   const uint32_t rw0 = RW[0], rw1 = RW[1], rw2 = RW[2], rw3 = RW[3], rw4 = RW[4];
-  if (dbg & 2) {   // (timing only: no stores)
-    if ((qd0 ^ qd1 ^ qd2 ^ qd3 ^ ps ^ px) == 0x12345678u) qual[n0] = 0;
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < CI_BLK; j++) {
     const uint32_t q = j < 4 ? qd0 : j < 8 ? qd1 : j < 12 ? qd2 : qd3;
@@ -1331,11 +1323,6 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_inplace(
     const uint32_t uq = unit_of(i);
     const uint32_t rr = PF ? 2u * uq + (uint32_t)f_pf : uq;
     const uint2 Rn = A.crec[rec_of(i + stride)];     // prefetch
-    if (A.dbg & 16) {   // (timing only: the item loop and record words alone)
-      if (R.x == 0x12345678u && R.y == 0x9abcdef0u) A.arena[0][i] = 0;
-      R = Rn;
-      continue;
-    }
     const uint32_t S = R.y & 0xffffu;
     const int n0 = CI_BLK * (int)(i - uq * NB);
     if ((uint32_t)n0 < S) {
@@ -1348,16 +1335,15 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_inplace(
       // the block's bases: the two aligned 16-byte chunks holding them, shifted into bw[0..3] (base j = byte j)
       const uint64_t sa = (uint64_t)(seq + n0);
       const uint4 *sp = (const uint4 *)(sa & ~(uint64_t)15);
-      const uint4 g0 = (A.dbg & 4) ? make_uint4(R.x, R.y, 0, 0) : sp[0], g1 = (A.dbg & 4) ? make_uint4(0, R.x, 0, R.y) : sp[1];
+      const uint4 g0 = sp[0], g1 = sp[1];
       uint32_t qd[4] = {0, 0, 0, 0};   // the block's qualities, packed
       uint32_t px = 0, pc = 0, ps = 0;   // bases needing the f64 decisions / a fallback choice draw; substituted
       uint32_t ch = 0;                   // choices of the substituted bases (2 bits each)
-      if (LDS_TAB && cnt == CI_BLK && !(A.dbg & 1)) {
+      if (LDS_TAB && cnt == CI_BLK) {
         // A full block (every block of a 150-bp read): no per-base guards, so the bases' LDS reads interleave; the
         // choices are derived for the substituted bases only (cr_full_block).
         const int row0 = (PF ? 0 : f * rlen) + n0;
-        cr_full_block(ctab + row0 * CB_ROW, t8p + row0 * n_bq, fp16, cc, key, tl, th, f, n0, seq, sa, g0, g1, qual,
-                      A.dbg);
+        cr_full_block(ctab + row0 * CB_ROW, t8p + row0 * n_bq, fp16, cc, key, tl, th, f, n0, seq, sa, g0, g1, qual);
         if (n0 + cnt == (int)S) qual[S] = '\n';
         R = Rn;
         continue;
@@ -1447,8 +1433,8 @@ __global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_inplace(
 
 static_assert(ED_CRB == CI_BLK, "the writer's row blocks are the corruption blocks");
 
-// ---- corruption rows (MH_CR_ROWS=1): the BQ draws before the writer -------------------------------------------
-// k_cr_rows runs the items, stream and decisions of k_cr_inplace over every block of every record up to rlen (a
+// ---- corruption rows (the direct writer's mode): the BQ draws before the writer -----------------------------------
+// k_cr_cols runs the items, stream and decisions of k_cr_inplace over every block of every record up to rlen (a
 // record of S < rlen bases uses the first S: the draws are counted by (template, file, triple), not by S) without
 // touching the arenas: per block one aligned 16-byte row slot (its qualities + 33) and one word of 2-bit
 // substitution codes (choice + 1; 0: the base stays), slot (file * NB + block) * m + template (column-major: a
@@ -1537,199 +1523,15 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
   *code = cd;
 }
 
-// The same block one triple draw at a time (three bases per phase: fewer live registers, so more waves hide the
-// LDS latency instead of fifteen reads in flight per wave).  Same outputs as cr_block_rows.
-__device__ __forceinline__ void cr_block_rows3(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
-                                               const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
-                                               uint4 *qo, uint32_t *code) {
-  const int n_bq = cc.n_bq;
-  const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
-  uint32_t qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0, ps = 0, px = 0, rws[CI_BLK / 3];
-#pragma unroll
-  for (int g = 0; g < CI_BLK / 3; g++) {
-    const uint4 r = philox4x32_10(make_uint4(tl, th, cw + (uint32_t)g, cc.c3), key);
-    rws[g] = r.w;
-    const uint32_t W[3] = {r.x, r.y, r.z};
-    uint32_t E[3], P[3], V2[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) E[k] = bk[(3 * g + k) * CB_ROW + (W[k] >> 24)];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const uint16_t *t = tp + (3 * g + k) * n_bq + (E[k] & 0x7fu);
-      P[k] = t[0];
-      V2[k] = ((const uint8_t *)t)[3];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int j = 3 * g + k;
-      const uint32_t e = E[k], c = e & 0x7fu, fl = e >> 7, pa = P[k];
-      const uint32_t lo = (W[k] >> 16) & 0xffu;
-      const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = V2[k];
-      const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
-      const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
-      const uint32_t amb = b2 | (fl & (uint32_t)(vn == lo));
-      const uint32_t bq = c + b0 + b1;
-      const uint32_t pth = fp[bq], h2 = W[k] & 0xffffu;
-      ps |= (uint32_t)(!amb && h2 < pth) << j;
-      px |= (amb | (uint32_t)(h2 == pth)) << j;
-      const uint32_t qv = (bq + 33u) << (8 * (j & 3));
-      if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
-    }
-  }
-  while (px) {   // rare: the full 53-bit decisions
-    const int j = __builtin_ctz(px);
-    px &= px - 1;
-    const int n = n0 + j;
-    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-    const int k = n % 3;
-    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-    uint32_t amb;
-    const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
-    const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
-                                     w, bq, amb);
-    const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
-    if (j < 4) qd0 = (qd0 & mk) | qv; else if (j < 8) qd1 = (qd1 & mk) | qv; else if (j < 12) qd2 = (qd2 & mk) | qv;
-    else qd3 = (qd3 & mk) | qv;
-    ps = (ps & ~(1u << j)) | ((x >> 8) << j);
-  }
-  *qo = make_uint4(qd0, qd1, qd2, qd3);
-  uint32_t cd = 0;
-  while (ps) {
-    const int j = __builtin_ctz(ps);
-    ps &= ps - 1;
-    const int g = j / 3, k = j - 3 * g;
-    const uint32_t rw = g == 0 ? rws[0] : g == 1 ? rws[1] : g == 2 ? rws[2] : g == 3 ? rws[3] : rws[4];
-    const uint32_t c10 = (rw >> (10 * k)) & 1023u;
-    uint32_t chv;
-    if (c10 == 1023u)
-      chv = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3),
-                                   key).x, 3u);
-    else
-      chv = c10 % 3u;
-    cd |= (chv + 1u) << (2 * j);
-  }
-  *code = cd;
-}
-
-template <bool PF, int THR>
-__global__ void __launch_bounds__(THR, PF ? THR / 128 : THR / 256) k_cr_rows(CiArgs A, uint4 *rows, uint32_t *codes) {
-  // LDS as k_cr_inplace: bucket entries [NT][rlen][CB_ROW] | Fp16[100] | threshold low-byte pairs [NT][rlen][n_bq]
-  extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
-  constexpr int NT = PF ? 1 : 2;
-  const int f_pf = PF ? (int)(blockIdx.x & 1u) : 0;
-  const CorruptCfg &cc = A.cc;
-  const int rlen = A.rlen, n_bq = cc.n_bq;
-  const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
-  const int32_t row_bytes = rlen * CB_ROW;
-  const uint16_t *fp16 = (const uint16_t *)(ctab + NT * row_bytes);
-  const int32_t o_t8 = NT * row_bytes + 256;
-  for (int ft = 0; ft < NT; ft++) {
-    const int f = PF ? f_pf : ft;
-    const uint4 *src = (const uint4 *)(cc.bk + (int64_t)f * cc.max_bp * CB_ROW);
-    uint4 *dst = (uint4 *)(ctab + ft * row_bytes);
-    for (int i = threadIdx.x; i < row_bytes / 16; i += THR) dst[i] = src[i];
-    const uint16_t *t16 = cc.T16 + (int64_t)f * cc.max_bp * n_bq;
-    for (int i = threadIdx.x; i < rlen * n_bq; i += THR) {
-      const int j = i % n_bq;
-      const uint32_t a = t16[i], b = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
-      ((uint16_t *)(ctab + o_t8))[ft * rlen * n_bq + i] = (uint16_t)((a & 0xffu) | ((b >> 8) == (a >> 8) ? (b & 0xffu) << 8 : 0xff00u));
-    }
-  }
-  for (int i = threadIdx.x; i < 100; i += THR) ((uint16_t *)fp16)[i] = cc.Fp16[i];
-  __syncthreads();
-  const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
-  const uint2 key = make_uint2(cc.k0, cc.k1);
-  const uint32_t NB = (uint32_t)(rlen + CI_BLK - 1) / CI_BLK;
-  const uint32_t n_items = (uint32_t)(A.m * (PF ? 1 : A.nf)) * NB;
-  const uint32_t stride = (PF ? gridDim.x >> 1 : gridDim.x) * THR;
-  const uint32_t nb_magic = 0xffffffffu / NB + 1u;
-  for (uint32_t i = (PF ? blockIdx.x >> 1 : blockIdx.x) * THR + threadIdx.x; i < n_items; i += stride) {
-    uint32_t uq = __umulhi(i, nb_magic);
-    uq = uq * NB > i ? uq - 1 : uq;
-    const uint32_t rr = PF ? 2u * uq + (uint32_t)f_pf : uq;   // record: template * nf + file
-    const int b = (int)(i - uq * NB), n0 = CI_BLK * b;
-    const int f = A.nf == 2 ? (int)(rr & 1) : 0;
-    const int64_t t = (int64_t)(A.nf == 2 ? rr >> 1 : rr);
-    const int64_t tt = t + cc.t_base;
-    const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
-    const int row0 = (PF ? 0 : f * rlen) + n0;
-    const int cnt = rlen - n0 < CI_BLK ? rlen - n0 : CI_BLK;
-    uint4 qo;
-    uint32_t code;
-    if (cnt == CI_BLK) {
-      cr_block_rows(ctab + row0 * CB_ROW, t8p + row0 * n_bq, fp16, cc, key, tl, th, f, n0, &qo, &code);
-    } else {   // a short last block (rlen not a multiple of 15): the guarded per-base path
-      uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
-#pragma unroll
-      for (int g = 0; g < CI_BLK / 3; g++) {
-        if (3 * g < cnt) {
-          const uint4 r = philox4x32_10(
-              make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            const int j = 3 * g + k;
-            if (j < cnt) {
-              const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-              uint32_t amb;
-              const uint32_t bq = cr_lds_walk(ctab + (row0 + j) * CB_ROW, t8p + (row0 + j) * n_bq, w, &amb);
-              const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
-              const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-              const bool sub = !amb && h2 < pth;
-              px |= (uint32_t)(amb || h2 == pth) << j;
-              ps |= (uint32_t)sub << j;
-              pc |= (uint32_t)(sub && c10 == 1023u) << j;
-              ch |= (c10 % 3u) << (2 * j);
-              qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
-            }
-          }
-        }
-      }
-      while (px) {
-        const int j = __builtin_ctz(px);
-        px &= px - 1;
-        const int n = n0 + j;
-        const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-        const int k = n % 3;
-        const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-        uint32_t amb;
-        const uint32_t bq = cr_lds_walk(ctab + (row0 + j) * CB_ROW, t8p + (row0 + j) * n_bq, w, &amb);
-        const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
-                                         f, n, w, bq, amb);
-        const uint32_t sh = 8u * (uint32_t)(j & 3);
-        qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
-        const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-        ps |= (x >> 8) << j;
-        pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
-      }
-      while (pc) {
-        const int j = __builtin_ctz(pc);
-        pc &= pc - 1;
-        const uint4 c = philox4x32_10(
-            make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
-        ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
-      }
-      code = 0;
-      while (ps) {
-        const int j = __builtin_ctz(ps);
-        ps &= ps - 1;
-        code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
-      }
-      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
-    }
-    const int64_t sl = ((int64_t)f * NB + b) * A.m + t;   // column-major: slot (file, block, template)
-    rows[sl] = qo;
-    codes[sl] = code;
-  }
-}
-
-// Position-major row pass (default for MH_CR_ROWS): a workgroup per (block column, template chunk) stages only its
-// column's tables (bucket rows and threshold pairs of 15 positions of one file: 6.7 KB instead of 67 KB), so
-// occupancy is bound by registers, not LDS; its threads take consecutive templates, so the slots it writes are
-// contiguous.  Same draws and decisions as k_cr_rows.
+// The corruption rows: a workgroup per (block column, template chunk) stages only its column's tables (bucket rows
+// and threshold pairs of 15 positions of one file: 6.7 KB; a record-major pass staging a whole file's 67 KB was
+// LDS-bound at 4.3 ms per chr1 unit, round 3), so occupancy is bound by registers, not LDS; its threads take
+// consecutive templates, so the slots it writes are contiguous.  The items, stream and decisions of k_cr_inplace,
+// over every block of every record up to rlen.
 constexpr int CC_THREADS = 256;
-template <int MW, bool G3>   // MW: waves per SIMD the register budget is sized for (1: the compiler's choice, 8: <= 64
-                            // VGPRs); G3: cr_block_rows3 (a triple draw at a time)
-__global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes, int32_t per_wg) {
+constexpr int CC_PER_WG = 16 * CC_THREADS;   // templates per workgroup (2048 or 8192: within noise)
+__global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes) {
+  const int32_t per_wg = CC_PER_WG;
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
   const CorruptCfg &cc = A.cc;
   const int rlen = A.rlen, n_bq = cc.n_bq;
@@ -1765,9 +1567,8 @@ __global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *row
     uint4 qo;
     uint32_t code;
     if (cnt == CI_BLK) {
-      if (G3) cr_block_rows3(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
-      else cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
-    } else {   // a short last block: the guarded per-base path (k_cr_rows')
+      cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
+    } else {   // a short last block: the guarded per-base path
       uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
 #pragma unroll
       for (int g = 0; g < CI_BLK / 3; g++) {
@@ -1830,11 +1631,6 @@ __global__ void __launch_bounds__(CC_THREADS, MW) k_cr_cols(CiArgs A, uint4 *row
   }
 }
 
-// the corruption rows before the writer (default) instead of the in-place pass after it (MH_CR_ROWS=0)
-static bool cr_rows_env() {
-  static const bool v = !(getenv("MH_CR_ROWS") && atoi(getenv("MH_CR_ROWS")) == 0);
-  return v;
-}
 // the row pass's LDS (per-file tables, or both files' with one file), 0 when the tables do not fit
 static size_t cr_rows_lds(int32_t nf, int64_t rlen, int32_t n_bq) {
   const size_t lds = (size_t)(nf == 2 ? 1 : 2) * rlen * (CB_ROW + 2 * n_bq) + 256 + 16;
@@ -1845,110 +1641,40 @@ static size_t cr_rows_lds(int32_t nf, int64_t rlen, int32_t n_bq) {
 static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
                               uint4 *rows, uint32_t *codes) {
   if (m <= 0) return MH_OK;
-  int ncu = 0;
-  HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  if (ncu <= 0) ncu = 256;
-  const size_t lds = cr_rows_lds(nf, rlen, cc.n_bq);
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
-  if (!lds || m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
-  const bool pf = nf == 2;
-  const int thr = pf ? 512 : CI_THREADS;
-  const int per_cu = pf ? 2 : (lds <= 78 * 1024 ? 2 : 1);
-  // MH_CR_ROWS_GRID: workgroups (A/B; fewer leave room on every CU for the writers beside the pass)
-  static const int64_t g_env = getenv("MH_CR_ROWS_GRID") ? atoll(getenv("MH_CR_ROWS_GRID")) : 0;
-  int64_t grid = std::min<int64_t>(g_env > 0 ? g_env : (int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
-  if (grid < 1) grid = 1;
-  if (pf) grid = (grid + 1) & ~(int64_t)1;
-  CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, nullptr, rlen, nf, 0, cc, 0};
+  if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
+  CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, nullptr, rlen, nf, 0, cc};
   stage_begin(ctx, "emit_corrupt_rows");
-  // MH_CR_COLS=0 (A/B): the record-major k_cr_rows instead of the position-major k_cr_cols
-  static const bool cols = !(getenv("MH_CR_COLS") && atoi(getenv("MH_CR_COLS")) == 0);
-  static const int32_t per_wg = getenv("MH_CR_COLS_PER") ? atoi(getenv("MH_CR_COLS_PER")) : 16 * CC_THREADS;
-  if (cols) {
-    const size_t lds_c = (size_t)CI_BLK * CB_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
-    const int64_t gx = (m + per_wg - 1) / per_wg;
-    if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
-    static const int mw = getenv("MH_CR_COLS_MW") ? atoi(getenv("MH_CR_COLS_MW")) : 1;   // (A/B)
-    static const int g3 = getenv("MH_CR_COLS_G3") ? atoi(getenv("MH_CR_COLS_G3")) : 0;   // (A/B)
-    auto kc = g3 ? (mw == 8 ? k_cr_cols<8, true> : k_cr_cols<1, true>) : (mw == 8 ? k_cr_cols<8, false> : k_cr_cols<1, false>);
-    hipLaunchKernelGGL(kc, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS), lds_c, st, A, rows, codes, per_wg);
-  } else if (pf)
-    hipLaunchKernelGGL((k_cr_rows<true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A, rows, codes);
-  else
-    hipLaunchKernelGGL((k_cr_rows<false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A, rows, codes);
+  const size_t lds_c = (size_t)CI_BLK * CB_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
+  const int64_t gx = (m + CC_PER_WG - 1) / CC_PER_WG;
+  if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
+  hipLaunchKernelGGL(k_cr_cols, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS), lds_c, st, A, rows, codes);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
   return MH_OK;
 }
 
-
 // rows mode: the buffers for an emission of m templates (before any stream waits: a reallocation drains the writers)
 static int32_t cr_rows_alloc(mh_ctx *ctx, int64_t m, int32_t nf, int64_t rlen) {
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
-  const int k = ctx->cr_ri;
-  MH_TRY(ensure(ctx, ctx->cr_rows[k], (size_t)(m * nf * NB) * 16 + 64));
-  MH_TRY(ensure(ctx, ctx->cr_codes[k], (size_t)(m * nf * NB) * 4 + 64));
+  MH_TRY(ensure(ctx, ctx->cr_rows, (size_t)(m * nf * NB) * 16 + 64));
+  MH_TRY(ensure(ctx, ctx->cr_codes, (size_t)(m * nf * NB) * 4 + 64));
   return MH_OK;
 }
-// the row pass on the writer stream, right before its writer (default), or on crstream beside the previous unit's
-// writer (MH_CR_ROWS_OVERLAP=1, A/B: within noise of the default)
-static bool cr_rows_same() {
-  static const bool v = !(getenv("MH_CR_ROWS_OVERLAP") && atoi(getenv("MH_CR_ROWS_OVERLAP")));
-  return v;
-}
-// rows mode for this emission: the row pass queued into the current set — on crstream, after the writer that last
-// read the set, so it runs beside the previous unit's writer (compute-bound beside memory-bound) — and the writer
-// stream `st` waiting for it; returns the set, which cr_rows_release marks free after the writer
+// rows mode for this emission: the row pass queued on the writer stream `st`, right before its writer (one row set
+// serves every unit, in stream order; the pass on a stream of its own beside the previous writer was within noise)
 static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
                                TArgs &A) {
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
-  const int k = ctx->cr_ri;
-  if (ctx->cr_rows[k].cap < (size_t)(m * nf * NB) * 16 + 64 || ctx->cr_codes[k].cap < (size_t)(m * nf * NB) * 4 + 64)
+  if (ctx->cr_rows.cap < (size_t)(m * nf * NB) * 16 + 64 || ctx->cr_codes.cap < (size_t)(m * nf * NB) * 4 + 64)
     return arg_fail(ctx, MH_E_STATE, "corruption rows not allocated");
-  uint4 *rows = (uint4 *)ctx->cr_rows[k].p;
-  uint32_t *codes = (uint32_t *)ctx->cr_codes[k].p;
-  if (cr_rows_same()) {
-    MH_TRY(launch_cr_rows(ctx, st, m, nf, rlen, cc, rows, codes));
-  } else {
-    if (!ctx->crstream) {
-      HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->crstream, hipStreamNonBlocking));
-      HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_crw, hipEventDisableTiming));
-    }
-    for (int i = 0; i < 2; i++) {
-      if (!ctx->ev_rows[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_rows[i], hipEventDisableTiming));
-      if (!ctx->ev_rfree[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_rfree[i], hipEventDisableTiming));
-    }
-    if (ctx->rfree_rec[k]) HIPCHK(ctx, hipStreamWaitEvent(ctx->crstream, ctx->ev_rfree[k], 0));
-    hipStream_t ss = ctx->stage_stream;
-    ctx->stage_stream = ctx->crstream;
-    MH_TRY(launch_cr_rows(ctx, ctx->crstream, m, nf, rlen, cc, rows, codes));
-    ctx->stage_stream = ss;
-    HIPCHK(ctx, hipEventRecord(ctx->ev_rows[k], ctx->crstream));
-    HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_rows[k], 0));
-  }
+  uint4 *rows = (uint4 *)ctx->cr_rows.p;
+  uint32_t *codes = (uint32_t *)ctx->cr_codes.p;
+  MH_TRY(launch_cr_rows(ctx, st, m, nf, rlen, cc, rows, codes));
   A.crow = rows;
   A.ccode = codes;
   A.nb = (int32_t)NB;
   return MH_OK;
-}
-// after the writer that read the current set (queued on `st`): the set is free once it has run; with the row pass on
-// crstream the next unit takes the other set (on the writer stream one set serves every unit, in stream order)
-static int32_t cr_rows_release(mh_ctx *ctx, hipStream_t st) {
-  if (cr_rows_same()) return MH_OK;
-  const int k = ctx->cr_ri;
-  if (ctx->ev_rfree[k]) {
-    HIPCHK(ctx, hipEventRecord(ctx->ev_rfree[k], st));
-    ctx->rfree_rec[k] = true;
-  }
-  ctx->cr_ri ^= 1;
-  return MH_OK;
-}
-
-// MH_CR_OVERLAP=1: the direct writer's corruption passes run on their own stream beside the next units' writers
-// (one 1024-thread workgroup per CU, so the writers' workgroups fit beside it) instead of after every writer
-static bool cr_overlap() {
-  static const bool v = getenv("MH_CR_OVERLAP") && atoi(getenv("MH_CR_OVERLAP"));
-  return v;
 }
 
 // the corruption pass over one emission's records (on stream `st`, after its writer)
@@ -1960,35 +1686,28 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
   if (ncu <= 0) ncu = 256;
-  // per-file workgroups (two files): each stages one file's tables (MH_CR_PERFILE=0, experiments: both)
-  static const bool pf_env = !(getenv("MH_CR_PERFILE") && atoi(getenv("MH_CR_PERFILE")) == 0);
-  const bool pf = pf_env && nf == 2;
+  // per-file workgroups (two files): each stages one file's tables
+  const bool pf = nf == 2;
   const size_t lds = (size_t)(pf ? 1 : 2) * rlen * (CB_ROW + 2 * cc.n_bq) + 256 + 16;   // (+16: the walk reads pairs c + 1 <= n_bq + 1)
   const bool lds_tab = lds <= 150 * 1024 && !getenv("MH_CR_GLOBAL");   // MH_CR_GLOBAL: tables from global (tests)
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_CAPACITY, "too many reads in one emission for the corruption pass");
-  int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
-  if (cr_overlap()) per_cu = 1;                           // room for the writers beside it
-  if (getenv("MH_CR_PER_CU")) per_cu = std::max(1, atoi(getenv("MH_CR_PER_CU")));
+  const int per_cu = lds_tab ? (lds <= 78 * 1024 ? 2 : 1) : 2;   // 1024-thread workgroups
   // per-file workgroups of 512 threads (4 waves per SIMD, up to 128 VGPRs: the full-block path's phases keep their
-  // fifteen LDS reads in flight); at 1024 threads (MH_CR_THR=1024, 64 VGPRs) that path spills and takes 8.3 instead
-  // of 5.6-5.8 ms per chr1 unit (profiles/r03/experiments_r03.txt)
-  static const int cr_thr = getenv("MH_CR_THR") ? atoi(getenv("MH_CR_THR")) : 512;
-  const int thr = lds_tab && pf && cr_thr == 512 ? 512 : CI_THREADS;
+  // fifteen LDS reads in flight); at 1024 threads (64 VGPRs) that path spills and takes 8.3 instead of 5.6-5.8 ms per
+  // chr1 unit (profiles/r03/experiments_r03.txt)
+  const int thr = lds_tab && pf ? 512 : CI_THREADS;
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
   if (grid < 1) grid = 1;
   if (pf) grid = (grid + 1) & ~(int64_t)1;   // even: workgroup pairs (file 0, file 1)
-  static const int32_t cr_dbg = getenv("MH_CR_DBG") ? atoi(getenv("MH_CR_DBG")) : 0;
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc, cr_dbg};
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
   if (!crec_ready) {   // (the fused writer wrote the record words itself)
     hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
     HIPCHK(ctx, hipGetLastError());
   }
-  if (lds_tab && pf && cr_thr == 512)
+  if (lds_tab && pf)
     hipLaunchKernelGGL((k_cr_inplace<true, true, 512>), dim3((unsigned)grid), dim3(512), lds, st, A);
-  else if (lds_tab && pf)
-    hipLaunchKernelGGL((k_cr_inplace<true, true, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else if (lds_tab)
     hipLaunchKernelGGL((k_cr_inplace<true, false, CI_THREADS>), dim3((unsigned)grid), dim3(CI_THREADS), lds, st, A);
   else
@@ -2077,11 +1796,8 @@ static int ew_dbg_env() {
   return v;
 }
 // qname rows: a multiple of 16 bytes plus 4 (an odd number of dwords), so wave 0's lanes (one qname row per template)
-// writing the same column land on 32 different LDS banks instead of 8 (MH_EW_QPAD: A/B, 0 = the old multiple of 16)
-static int32_t ed_qpad() {
-  static const int v = getenv("MH_EW_QPAD") ? atoi(getenv("MH_EW_QPAD")) : 4;
-  return v;
-}
+// writing the same column land on 32 different LDS banks instead of 8
+constexpr int32_t ED_QPAD = 4;
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows = false) {
   const bool staged = !(ew_dbg_env() & 256) && !rows;   // (256: seam chunks stored by the seam pass, no LDS for them)
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
@@ -2124,9 +1840,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *d_mid = small + 256 + 4096;
   QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
-  // the direct writer (corruption too, unless MH_CORRUPT_LDS asks for the LDS-image writer: experiments): record
-  // offsets from per-tile prefixes; the LDS-image writer reads per-template offsets
-  const bool direct = !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS"));
+  // the direct writer (corruption too; mh_set_emit_mode(1) forces the LDS-image writer): record offsets from per-tile
+  // prefixes; the LDS-image writer reads per-template offsets
+  const bool direct = !ctx->emit_lds_only;
   const int64_t ntiles = (m + ED_T - 1) / ED_T;
 
   // ---- measure + tile prefixes (skipped when mh_emit_prepare already ran them for this unit) ------------------------
@@ -2281,8 +1997,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
-  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ed_qpad();
-  const bool cr_rows = ctx->corrupt_on && cr_rows_env() && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
+  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ED_QPAD;
+  const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
@@ -2309,8 +2025,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
                                               : ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at;
     if (ctx->gate && gate_here && ctx->job > 0) {
       const uint32_t want = ctx->sample_state ? ctx->job : ctx->job + 1;
-      if (gate_debug()) fprintf(stderr, "mh gate: writer %d of job %u waits for %u\n", ctx->writers_in_job, ctx->job,
-                                want);
       HIPCHK(ctx, hipStreamWaitValue32(ctx->wstream, ctx->gate, want, hipStreamWaitValueGte, 0xffffffffu));
       if (want > ctx->gate_waited) ctx->gate_waited = want;
     }
@@ -2327,26 +2041,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
                                  : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
-    if (cr_rows) MH_TRY(cr_rows_release(ctx, ctx->wstream));
     stage_end(ctx);
     hipStream_t tail = ctx->wstream;   // the stream whose last work is this unit's last
-    if (ctx->corrupt_on && !cr_rows) {
-      if (cr_overlap()) {   // the corruption pass on its own stream, beside the next units' writers
-        if (!ctx->crstream) {
-          HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->crstream, hipStreamNonBlocking));
-          HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_crw, hipEventDisableTiming));
-        }
-        HIPCHK(ctx, hipEventRecord(ctx->ev_crw, ctx->wstream));
-        HIPCHK(ctx, hipStreamWaitEvent(ctx->crstream, ctx->ev_crw, 0));
-        tail = ctx->crstream;
-        ctx->stage_stream = tail;
-        ctx->cr_pending = true;
-      }
+    if (ctx->corrupt_on && !cr_rows)   // (tables too large for the row pass's LDS): in place after the writer
       MH_TRY(launch_cr_inplace(ctx, tail, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p,
                                (char *)ctx->out1.p, (char *)ctx->out2.p, write_fastq2 ? 2 : 1,
                                (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc, nullptr, true));
-      ctx->stage_stream = ctx->wstream;
-    }
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, tail));
@@ -2512,10 +2212,6 @@ int32_t sync_async_fill(mh_ctx *ctx) {
 int32_t output_reset(mh_ctx *ctx) {
   ctx->used1 = ctx->used2 = 0;
   ctx->res1 = ctx->res2 = 0;
-  if (ctx->cr_pending) {   // the next writers overwrite the arenas: after the queued corruption passes
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, ctx->ev_writer, 0));
-    ctx->cr_pending = false;
-  }
   if (ctx->async_pending) {
     hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, (int64_t)0,
                        (int64_t)0);
@@ -2571,12 +2267,11 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
   const int32_t head = (int32_t)(((prefix.size() + mid.size() + 10 + 16) + 15) / 16 * 16);
   int32_t rb = 0;
-  bool direct = head_fits && !ctx->emit_lds_only && !(ctx->corrupt_on && getenv("MH_CORRUPT_LDS")) &&
-                win_stride <= 16 * 3 * ED_GMAX && m < (int64_t)UINT32_MAX && m > 0 && !getenv("MH_EMIT_SYNC");
+  bool direct = head_fits && !ctx->emit_lds_only && win_stride <= 16 * 3 * ED_GMAX && m < (int64_t)UINT32_MAX && m > 0;
   if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
-  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ed_qpad();
-  const bool cr_rows = ctx->corrupt_on && cr_rows_env() && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
+  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ED_QPAD;
+  const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
@@ -2679,7 +2374,6 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
                                : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
-  if (cr_rows) MH_TRY(cr_rows_release(ctx, ws));
   stage_end(ctx);
   // the unit's totals (cnt digits added), its base (the fill before it) and the fill after it
   hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (int64_t *)ctx->d_used.p, (int64_t *)stat, write_fastq2);

@@ -162,11 +162,6 @@ struct mh_ctx {
   // FASTQ writer stream: mh_emit_reads returns once its writer is queued here; every other entry point first makes
   // the main stream wait for the last queued writer (ev_writer)
   hipStream_t wstream = nullptr;
-  // corruption stream (MH_CR_OVERLAP): each unit's k_cr_inplace waits for its writer (ev_crw) and runs beside the next
-  // units' writers; ev_writer is then recorded after the corruption pass, and writers into a reset arena wait for it
-  hipStream_t crstream = nullptr;
-  hipEvent_t ev_crw = nullptr;
-  bool cr_pending = false;
   // a batch between mh_sample_units_begin and _end (mh_sample.hip SampleState); writers queued meanwhile wait, with
   // the gate on, for the begun batch's sort (gate >= job) instead of the next one's (gate >= job + 1)
   std::shared_ptr<void> sample_state;
@@ -264,12 +259,9 @@ struct mh_ctx {
   // asynchronous emission (mh_emit_async): measure, offsets, writer and corruption queued on the writer stream; the
   // arena fill lives on the device (d_used) until a call needs it on the host (sync_async_fill)
   mh::DevBuf d_used;                     // int64[2]
-  // corruption rows (MH_CR_ROWS): per block 15 qualities | 2-bit codes; two sets, each unit's row pass on crstream
-  // (after the writer two units back has released the set: ev_rfree) beside the previous unit's writer
-  mh::DevBuf cr_rows[2], cr_codes[2];
-  hipEvent_t ev_rows[2] = {nullptr, nullptr}, ev_rfree[2] = {nullptr, nullptr};
-  bool rfree_rec[2] = {false, false};
-  int cr_ri = 0;
+  // corruption rows (the direct writer's mode): per block 15 qualities | 2-bit codes; one set, the row pass and its
+  // writer in stream order on the writer stream
+  mh::DevBuf cr_rows, cr_codes;
   mh::DevBuf scan_partials_w;            // look-back scratch of the writer stream's scans
   mh::DevBuf rb_tmp;                     // read_part_bound's prefix sums
   bool async_pending = false;            // units queued asynchronously whose fill is not in used1 / used2 yet
@@ -323,7 +315,6 @@ int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FAS
 // a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
 int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set, uint32_t &gate);
 int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, uint32_t gate);
-bool gate_debug();                                  // MH_GATE_DEBUG: trace gate waits and writes
 void gate_open(mh_ctx *ctx);                        // release every writer waiting on the gate
 void gate_open_for(mh_ctx *ctx, uint32_t need);     // ... if a wait is about to depend on a writer needing `need`
 int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value);   // stream-ordered gate write (sampling)

@@ -43,11 +43,7 @@ namespace {
 
 constexpr uint32_t MT_UP = 0x80000000u, MT_LO = 0x7fffffffu, MT_A = 0x9908b0dfu;
 constexpr int64_t SEG_WORDS_DEFAULT = 624 * 640;   // outputs per segment (fewer, longer segments: the jump is the cost)
-// MH_SEG_TWISTS (experiments): segment length in 624-word twists
-static int64_t seg_words() {
-  static const int64_t w = getenv("MH_SEG_TWISTS") ? 624 * std::max(1, atoi(getenv("MH_SEG_TWISTS"))) : SEG_WORDS_DEFAULT;
-  return w;
-}
+static int64_t seg_words() { return SEG_WORDS_DEFAULT; }
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
@@ -121,13 +117,13 @@ constexpr int JB = 16;                  // set bits per batch of the jump
 // is stored twice (slot s and s + 2048), so x_{k+w}, x_{k+w+208}, x_{k+w+416} sit at (k mod 2048) + w + {0, 208,
 // 416} with no wrap: one address add per set bit (the three reads use immediate offsets), and a batch's unused
 // bit slots read a zero block instead of being masked out.  26 KB of LDS.
-__global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys, int dbg) {
+__global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const uint32_t *polys) {
   __shared__ uint32_t cb[2 * CB_WORDS + 624];
   __shared__ uint32_t gp[624];
   const SegJob job = jobs[blockIdx.x];
   const int t = threadIdx.x;
   mt_seed_lds(cb, job.seed);   // x_0 .. x_623
-  if (job.k > 0 && !(dbg & 1)) {
+  if (job.k > 0) {
     const uint32_t *g = polys + (int64_t)job.k * 624;
     for (int i = t; i < 624; i += 256) {
       gp[i] = g[i];
@@ -190,10 +186,10 @@ __global__ void __launch_bounds__(256) k_mt_segments(const SegJob *jobs, const u
   }
   uint32_t *st0 = cb, *st1 = cb + 624;
   uint32_t *out = job.out + job.start;
-  const int64_t cnt = (dbg & 2) ? 0 : job.count;
+  const int64_t cnt = job.count;
   for (int64_t base = 0; base < cnt; base += 624) {
     mt_twist_block(st0, st1, [&](int k, uint32_t w) {
-      if (base + k < cnt && !(dbg & 4)) out[base + k] = w;
+      if (base + k < cnt) out[base + k] = w;
     });
     uint32_t *tmp = st0; st0 = st1; st1 = tmp;
   }
@@ -1019,7 +1015,7 @@ int32_t mt_stream_words(mh_ctx *ctx, hipStream_t st, uint32_t seed, int64_t firs
   MH_TRY(ensure(ctx, jobs_buf, sizeof(SegJob) * jobs.size() + 64));
   HIPCHK(ctx, hipMemcpyAsync(jobs_buf.p, jobs.data(), sizeof(SegJob) * jobs.size(), hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)jobs_buf.p,
-                     (const uint32_t *)ctx->jump_polys.p, 0);
+                     (const uint32_t *)ctx->jump_polys.p);
   HIPCHK(ctx, hipGetLastError());
   SYNCCHK(ctx, hipStreamSynchronize(st));   // the host job table goes out of scope
   return MH_OK;
@@ -1055,11 +1051,10 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   hipStream_t st = ctx->stream;
   *done = false;
   // Chunks shrink with the draw index: a chunk's margin (in draws) is about mask(i) / its words, so sizing chunks as
-  // i / MH_DEC_DIV words (a power of two, MH_DEC_MINW .. DC_CHUNK) keeps margins from collapsing as i falls.
+  // i / 128 words (a power of two, 64 .. DC_CHUNK) keeps margins from collapsing as i falls.
   // Starts: the exact one for each unit's first chunk, then the expected accepts (rate (i+1)/(mask+1)).
-  const int64_t div = getenv("MH_DEC_DIV") ? std::max(1LL, atoll(getenv("MH_DEC_DIV"))) : 128;
-  const int64_t minw = getenv("MH_DEC_MINW") ? std::min<int64_t>(DC_CHUNK, std::max(64LL, atoll(getenv("MH_DEC_MINW"))))
-                                             : 64;
+  const int64_t div = 128;
+  const int64_t minw = 64;
   std::vector<ChunkJob> cj;
   std::vector<int64_t> s0;
   std::vector<int32_t> first(dec.size() + 1, 0);
@@ -1091,8 +1086,8 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     return MH_OK;
   }
   const int32_t U = (int32_t)dec.size();
-  // the tail of each unit: its chunks from the first one expected to start below MH_DEC_TAIL draws
-  const int64_t tail_at = getenv("MH_DEC_TAIL") ? atoll(getenv("MH_DEC_TAIL")) : (int64_t)1 << 15;   // TODO tune
+  // the tail of each unit: its chunks from the first one expected to start below 2^15 draws
+  const int64_t tail_at = (int64_t)1 << 15;
   std::vector<int32_t> tail_c(U, -1);
   for (int32_t u = 0; u < U; u++)
     for (int32_t c = first[u]; c < first[u + 1] && tail_at > 0; c++)
@@ -1139,7 +1134,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
   const unsigned grid = (unsigned)std::min<int64_t>(C, 4096);
   // pass 1 over every chunk, then passes over the queued chunks (resolve + recount), PASS_BATCH per host check
   constexpr int MAX_PASSES = 64;
-  const int PASS_BATCH = getenv("MH_DEC_BATCH") ? std::max(1, atoi(getenv("MH_DEC_BATCH"))) : 8;   // diagnostics
+  const int PASS_BATCH = 8;
   hipLaunchKernelGGL(k_decode_chunks<false>, dim3(grid), dim3(DC_THREADS), 0, st, (const ChunkJob *)d_jobs,
                      (const int32_t *)nullptr, (const int32_t *)nullptr, (int32_t)C, (const int64_t *)d_s0, d_count,
                      d_margin);
@@ -1166,25 +1161,6 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
     HIPCHK(ctx, hipMemcpyAsync(hs + 32, cur, 4, hipMemcpyDeviceToHost, st));
     SYNCCHK(ctx, hipStreamSynchronize(st));
     const int32_t h_ntodo = (int32_t)(hs[32] & 0xffffffff);
-    if (getenv("MH_DEC_VERBOSE")) fprintf(stderr, "decode: %d passes, %d chunks still queued of %lld\n", passes,
-                                          h_ntodo, (long long)C);
-    if (getenv("MH_DEC_VERBOSE") && atoi(getenv("MH_DEC_VERBOSE")) >= 2 && h_ntodo > 0) {   // where they are
-      std::vector<int32_t> q(h_ntodo);
-      std::vector<int64_t> hs(C);
-      HIPCHK(ctx, hipMemcpy(q.data(), d_todo, 4 * (size_t)h_ntodo, hipMemcpyDeviceToHost));
-      HIPCHK(ctx, hipMemcpy(hs.data(), d_s0, 8 * (size_t)C, hipMemcpyDeviceToHost));
-      int hist[40] = {0};
-      for (int32_t c : q) {
-        int64_t s = hs[c];
-        int b2 = 0;
-        while (s > 1 && b2 < 39) { s >>= 1; b2++; }
-        hist[b2]++;
-      }
-      fprintf(stderr, "  queued by log2(start):");
-      for (int b2 = 0; b2 < 40; b2++)
-        if (hist[b2]) fprintf(stderr, " %d:%d", b2, hist[b2]);
-      fprintf(stderr, "\n");
-    }
     if (h_ntodo == 0) {   // the last pass counted nothing: the starts in s1 are the sequential ones
       conv = true;
       break;
@@ -1227,33 +1203,16 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // workgroups that do fit beside them made the steps slower — WGS 1.18 vs 1.37 G/s, chr1 1.30 vs 1.50 — so the
 // default tuning stays.)  9 key bits per onesweep pass instead of the tuning's 8, the same workgroups: a 64 M-draw
 // batch's 27-bit keys in 3 passes instead of 4 (WGS 1.591 vs 1.576 G/s, two alternations; 10 bits 1.577, 11 bits
-// 1.569).  MH_SORT_BITS = 8 / 10 / 11: A/B.
-template <unsigned B>
-using SortBitsCfg = rocprim::radix_sort_config<
+// 1.569).
+using SortCfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, B,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 9,
                                         rocprim::block_radix_rank_algorithm::match>>;
-static int sort_bits() {
-  static const int v = getenv("MH_SORT_BITS") ? atoi(getenv("MH_SORT_BITS")) : 9;
-  return v;
-}
 template <class KIn>
 static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
                             size_t n, unsigned end_bit, hipStream_t st) {
   const rocprim::counting_iterator<uint32_t> iota(0u);
-  switch (sort_bits()) {
-    case 9:
-      return rocprim::radix_sort_pairs<SortBitsCfg<9>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
-                                                       end_bit, st);
-    case 10:
-      return rocprim::radix_sort_pairs<SortBitsCfg<10>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
-                                                        end_bit, st);
-    case 11:
-      return rocprim::radix_sort_pairs<SortBitsCfg<11>>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u,
-                                                        end_bit, st);
-    default:
-      return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
-  }
+  return rocprim::radix_sort_pairs<SortCfg>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
 }
 
 struct BatchPerm {
@@ -1439,10 +1398,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
   MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
   MH_TRY(ensure(ctx, ctx->s[11], 8 * 1024));
-  // sampling lanes for the per-unit stages: up to MH_LANES (default 2; 4 lets more of the sampling run beside the FASTQ
-  // writers, which then take longer: 3.45 against 2.73 ms per launch), at most one per unit
-  static const int lanes_env = getenv("MH_LANES") ? atoi(getenv("MH_LANES")) : 2;
-  int n_lanes = getenv("MH_ONE_LANE") ? 1 : std::max(1, std::min({lanes_env, (int)n_units, ctx->gate ? 2 : 4}));
+  // sampling lanes for the per-unit stages: two (four let more of the sampling run beside the FASTQ writers, which
+  // then take longer: 3.45 against 2.73 ms per launch), at most one per unit
+  int n_lanes = std::max(1, std::min(2, (int)n_units));
   const bool two_lanes = n_lanes > 1;
   // lanes 2 and 3 get their streams on first use only: the box runs with 4 hardware queues per process
   // (GPU_MAX_HW_QUEUES), and streams beyond that share queues — a sampling lane sharing the writer's queue would
@@ -1511,7 +1469,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
       HIPCHK(ctx, hipMemcpyAsync(d_dec, dec.data(), sizeof(DecJob) * dec.size(), hipMemcpyHostToDevice, st));
       stage_begin(ctx, "sample_mt_segments");
       hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)d_jobs,
-                         (const uint32_t *)ctx->jump_polys.p, getenv("MH_MT_DBG") ? atoi(getenv("MH_MT_DBG")) : 0);
+                         (const uint32_t *)ctx->jump_polys.p);
       HIPCHK(ctx, hipGetLastError());
       stage_end(ctx);
       stage_begin(ctx, "sample_shuffle_decode");
@@ -1543,12 +1501,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
 
   // ---- per-unit parallel stages (stream-ordered, shared scratch) ------------------------------------------------
   // units alternate between the two lanes; the second lane forks after the word streams and joins before readback.
-  // MH_STAGE_WAIT=1 (experiments): they start only once the FASTQ writers queued earlier (the previous job's) have
-  // drained.  The radix sorts and look-back scans of these stages run several times slower beside a bandwidth-bound
-  // writer than alone, but waiting leaves the writer stream idle instead: the same step time on the pool (14.8 ms
-  // either way), so by default they overlap.
-  static const bool stage_wait = getenv("MH_STAGE_WAIT") && atoi(getenv("MH_STAGE_WAIT"));
-  if (stage_wait && ctx->writer_pending) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_writer, 0));
+  // (They overlap the FASTQ writers queued earlier: the radix sorts and look-back scans run several times slower beside
+  // a bandwidth-bound writer than alone, but waiting for the writers to drain left the writer stream idle instead —
+  // the same step time, round 2.)
   if (two_lanes) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
@@ -1558,10 +1513,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   int32_t last[4] = {-1, -1, -1, -1};
   for (int32_t u = 0, k = 0; u < n_units; u++)
     if (plan[u].n > 0) last[k++ % n_lanes] = u;
-  // the batch-wide permutation (default; MH_PERM_UNIT=1: one sort per unit).  With the writer gate the batch's one
-  // sort releases the previous job's gated writers (they wait until it has run alone on the chip)
-  static const bool perm_unit = getenv("MH_PERM_UNIT") && atoi(getenv("MH_PERM_UNIT"));
-  const bool batch = !perm_unit && rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) && n_units <= PK_UNITS;
+  // the batch-wide permutation (one sort per unit when the batch's draws exceed 2^31).  With the writer gate the
+  // batch's one sort releases the previous job's gated writers (they wait until it has run alone on the chip)
+  const bool batch = rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) && n_units <= PK_UNITS;
   // Up to four units (two per lane): every unit's sort first, then the rest, each unit with its own sort buffers, so
   // the gate opens after the sorts alone.  More units: unit after unit.
   const bool split = ctx->gate && !batch && n_units <= mh_ctx::N_USORT;
@@ -1590,11 +1544,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
         HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_xjoin[l - 2], 0));
       }
     }
-    // 2. one sort of every unit's (target, step), heads, chase (main stream).  MH_SORT_WAIT=1 (A/B): the sort starts
-    // only once the FASTQ writers queued so far have drained (its 1024-thread workgroups otherwise start one by one
-    // between writer workgroups, and the early ones hold their CUs spinning on the look-back)
-    static const bool sort_wait = getenv("MH_SORT_WAIT") && atoi(getenv("MH_SORT_WAIT"));
-    if (sort_wait && ctx->writer_pending) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_writer, 0));
+    // 2. one sort of every unit's (target, step), heads, chase (main stream)
     stage_begin(ctx, "sample_permutation");
     std::vector<int64_t> uo(n_units), un(n_units);
     for (int32_t u = 0; u < n_units; u++) {

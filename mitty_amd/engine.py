@@ -6,7 +6,6 @@ the haplotype is spliced on the device once and kept resident for all of that co
 segments — and then emitted one by one, in the reference's unit order, into the device FASTQ arenas.
 """
 import logging
-import os
 
 from mitty_amd import _native
 
@@ -17,8 +16,7 @@ RNG_MODES = {'mitty': _native.MH_RNG_MITTY, 'philox': _native.MH_RNG_PHILOX}
 
 class Engine:
   SLOTS_PER_REGION = 64
-  # units prepared ahead of their writers (of the library's 16 emission buffer sets); MH_EMIT_AHEAD: A/B
-  EMIT_SETS = max(1, min(16, int(os.environ.get('MH_EMIT_AHEAD', '4'))))
+  EMIT_SETS = 4   # units prepared ahead of their writers (of the library's 16 emission buffer sets)
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
 
   def __init__(self, device=0):
@@ -86,8 +84,7 @@ class Engine:
     between sampling, measuring and writing) and a PendingUnits comes back at once; its resolve() gives the list
     (the units' bytes land in the arenas in unit order, as on the synchronous path).
     """
-    if not os.environ.get('MH_SPLICE_ONE_LANE'):
-      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
+    self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
     if lazy:
       for s in set(slots):   # the qname bound for the writer's room, while the splice's results are fresh
@@ -113,7 +110,7 @@ class Engine:
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
-                              write_fastq2, unit_key=seed, wait=bool(os.environ.get('MH_PREP_WAIT')))
+                              write_fastq2, unit_key=seed, wait=False)
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
@@ -135,8 +132,7 @@ class Engine:
 
     def begin(k):
       units = batches[k]
-      if not os.environ.get('MH_SPLICE_ONE_LANE'):
-        self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
+      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
       slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
       base = (k % 3) * self.TPL_BATCH + 3 * self.TPL_BATCH   # three generations in flight (writers, end, begin)
       ids[k] = [base + i for i in range(len(units))]
@@ -177,8 +173,7 @@ class Engine:
   def sample_only(self, units, soa_of, p, rlen, cum_tlen, tpl_base, rng='mitty'):
     """The sampling half of run_units: units [(ps, ri, cpy, rng_seed)] sampled together into template sets
     tpl_base + k.  Returns the template counts (emit_only emits them later)."""
-    if not os.environ.get('MH_SPLICE_ONE_LANE'):
-      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
+    self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
     return [int(x) for x in self.ctx.sample_units([tpl_base + k for k in range(len(units))], slots,
                                                   [u[3] for u in units], p, rlen, cum_tlen, RNG_MODES[rng])]

@@ -774,13 +774,13 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
   vdf = vcfio.load_variants_soa(G.path('data/syn.vcf'), 'S1', G.path('data/syn.bed'))
   seqs = mfasta.read_fasta(G.path('data/syn.fa'))
   outs = []
-  for lds in (False, True):
-    if lds:
-      monkeypatch.setenv('MH_CORRUPT_LDS', '1')
-    else:
-      monkeypatch.delenv('MH_CORRUPT_LDS', raising=False)
+  # (the direct writer with rc or forward-only haplotypes — mirrored mate-1 windows — and the LDS-image writer + the
+  # in-place pass, mh_set_emit_mode(1))
+  for fwd, lds in ((0, False), (1, False), (0, True)):
+    monkeypatch.setenv('MH_HAP_FWD', str(fwd))
     eng = Engine(0)
     try:
+      eng.ctx.set_emit_mode(1 if lds else 0)
       eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 9)
       for ri in range(len(vdf)):
         chrom, s0, e = vdf[ri]['region']
@@ -790,10 +790,11 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
       outs.append(eng.ctx.fetch_output())
     finally:
       eng.close()
-  (d1, d2), (l1, l2) = outs
-  assert len(d1) > 10000
-  G.check_same(d1, l1, 'fastq1')
-  G.check_same(d2, l2, 'fastq2')
+  (l1, l2) = outs[-1]
+  assert len(l1) > 10000
+  for k, (d1, d2) in enumerate(outs[:-1]):
+    G.check_same(d1, l1, 'fastq1 (variant {})'.format(k))
+    G.check_same(d2, l2, 'fastq2 (variant {})'.format(k))
 
 
 @pytest.mark.parametrize('tables,write2,fwd', [('lds', True, 0), ('global', True, 0), ('lds', False, 0),
