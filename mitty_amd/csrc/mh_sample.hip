@@ -26,12 +26,11 @@
 #include <cstdlib>
 #include <cstring>
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
+#include "mh_sort.h"
 
 namespace mh {
 
@@ -1198,21 +1197,13 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
-// The permutation's (target, step) sort: rocprim's LSD onesweep radix sort.  (Its gfx950 tuning runs 1024-thread
-// sort workgroups, which find no room on a CU beside the FASTQ writers and wait for them to drain; 256-thread onesweep
-// workgroups that do fit beside them made the steps slower — WGS 1.18 vs 1.37 G/s, chr1 1.30 vs 1.50 — so the
-// default tuning stays.)  9 key bits per onesweep pass instead of the tuning's 8, the same workgroups: a 64 M-draw
-// batch's 27-bit keys in 3 passes instead of 4 (WGS 1.591 vs 1.576 G/s, two alternations; 10 bits 1.577, 11 bits
-// 1.569).
-using SortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 9,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+// The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (8-bit digits, 256-thread
+// workgroups).  (Round 3 ran rocprim's onesweep with 1024-thread workgroups, which found no room on a CU beside the
+// FASTQ writers and waited for them to drain.)
 template <class KIn>
 static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
                             size_t n, unsigned end_bit, hipStream_t st) {
-  const rocprim::counting_iterator<uint32_t> iota(0u);
-  return rocprim::radix_sort_pairs<SortCfg>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
+  return lsd_sort_pairs_iota(tmp, tmp_bytes, keys_in, keys_out, vals_out, (int64_t)n, end_bit, st);
 }
 
 struct BatchPerm {

@@ -145,6 +145,84 @@ __global__ void __launch_bounds__(256) k_tile3(Args A) {
   }
 }
 
+// K tiles per 256-thread workgroup, software-pipelined: tile i+1's window gathers (3 x 16 B per thread, registers)
+// are issued before tile i's store sweep and land in the other LDS buffer after it
+template <int K>
+__global__ void __launch_bounds__(256) k_pipe(Args A) {
+  __shared__ __attribute__((aligned(16))) char win[2][32 * 2 * WS + 64];
+  __shared__ int32_t rel[2][2][33];
+  const int tid = threadIdx.x;
+  const int64_t nt_all = (A.n + 31) / 32;
+  const int64_t tile0 = (int64_t)blockIdx.x * K;
+  auto gather = [&](int64_t tile, uint4 *v) {
+    const int64_t t0 = tile * 32;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int s = tid + 256 * k;             // slot: window s / 11, chunk s % 11
+      const int w = s / 11, c = s - 11 * w, j = w >> 1;
+      const bool ok = tile < nt_all && s < 704 && t0 + j < A.n;
+      const int64_t p = ok ? ((w & 1) ? A.pos1[t0 + j] : A.pos0[t0 + j]) : 0;
+      v[k] = *(const uint4 *)(A.hap + (p & ~(int64_t)15) + 16 * c);
+    }
+  };
+  auto put = [&](int b, const uint4 *v) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int s = tid + 256 * k;
+      if (s < 704) *(uint4 *)(win[b] + (s / 11) * WS + 16 * (s % 11)) = v[k];
+    }
+  };
+  auto offsets = [&](int b, int64_t tile) {
+    if (tid < 2 && tile < nt_all) {
+      const int64_t t0 = tile * 32;
+      const int nt = (int)(A.n - t0 < 32 ? A.n - t0 : 32);
+      const int32_t *rl = tid ? A.rlen2 : A.rlen1;
+      int32_t o = 0;
+      for (int j = 0; j < nt; j++) {
+        rel[b][tid][j] = o;
+        o += rl[t0 + j];
+      }
+      rel[b][tid][nt] = o;
+    }
+  };
+  uint4 v[3];
+  gather(tile0, v);
+  offsets(0, tile0);
+  put(0, v);
+  __syncthreads();
+  for (int i = 0; i < K; i++) {
+    const int64_t tile = tile0 + i;
+    if (tile >= nt_all) break;
+    const int b = i & 1;
+    if (i + 1 < K) {
+      gather(tile + 1, v);
+      offsets(b ^ 1, tile + 1);
+    }
+    const int64_t t0 = tile * 32;
+    const int nt = (int)(A.n - t0 < 32 ? A.n - t0 : 32);
+    for (int f = 0; f < 2; f++) {
+      char *out = f ? A.out2 : A.out1;
+      const int64_t g0 = (f ? A.tb2 : A.tb1)[tile];
+      const int32_t span = rel[b][f][nt];
+      const int64_t c0 = g0 >> 4, c1 = (g0 + span) >> 4;
+      for (int64_t c = c0 + tid; c < c1; c += 256) {
+        const int32_t x = (int32_t)((c << 4) - g0);
+        int lo = 0, hi = nt;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (rel[b][f][mid] <= (x < 0 ? 0 : x)) lo = mid; else hi = mid;
+        }
+        const int32_t y = (x < 0 ? 0 : x) - rel[b][f][lo];
+        uint4 q;
+        __builtin_memcpy(&q, win[b] + (lo * 2 + f) * WS + (y % 150), 16);
+        *(uint4 *)(out + (c << 4)) = q;
+      }
+    }
+    if (i + 1 < K) put(b ^ 1, v);
+    __syncthreads();
+  }
+}
+
 int main(int argc, char **argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 2926000;
   std::vector<int64_t> Hs = {250000000, 124000000};
@@ -212,7 +290,8 @@ int main(int argc, char **argv) {
         int mode, T;
       };
       std::vector<V> vs = T == 32 ? std::vector<V>{{"tile3", 0, 32}, {"tile4", 0, 32}, {"stores", 1, 32},
-                                                    {"gathers", 2, 32}}
+                                                    {"gathers", 2, 32}, {"pipe2", 0, 32}, {"pipe4", 0, 32},
+                                                    {"pipe8", 0, 32}}
                                   : std::vector<V>{{"tile4x2", 0, 64}};
       for (const V &v : vs) {
         Args A{d_p0, d_p1, d_rl1, d_rl2, d_tb1, d_tb2, d_hap, d_o1, d_o2, n, v.mode};
@@ -221,6 +300,12 @@ int main(int argc, char **argv) {
           CK(hipEventRecord(e0, 0));
           if (!strcmp(v.name, "tile3"))
             hipLaunchKernelGGL(k_tile3, dim3((unsigned)nt), dim3(256), 0, 0, A);
+          else if (!strcmp(v.name, "pipe2"))
+            hipLaunchKernelGGL(k_pipe<2>, dim3((unsigned)((nt + 1) / 2)), dim3(256), 0, 0, A);
+          else if (!strcmp(v.name, "pipe4"))
+            hipLaunchKernelGGL(k_pipe<4>, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, 0, A);
+          else if (!strcmp(v.name, "pipe8"))
+            hipLaunchKernelGGL(k_pipe<8>, dim3((unsigned)((nt + 7) / 8)), dim3(256), 0, 0, A);
           else if (T == 32)
             hipLaunchKernelGGL((k_tile<32, 256, 4>), dim3((unsigned)nt), dim3(256), 0, 0, A);
           else

@@ -1,15 +1,20 @@
-# Interleaved A/B of env settings on the steady-state bench (VARS = space-separated KEY=VAL settings, X=0 = default)
-mkdir -p gpurun_out/ab
+#!/bin/bash
+# A/B of environment variants on one bench line, alternating REPS times in one call.
+# usage (inside gpurun): TAG=name REPS=2 BENCH_ARGS="--steps 8 --warmup 2" scripts/gpu_ab.sh 'base:' 'fwd:MH_HAP_FWD=1' ...
+# Each argument is label:ENV=V ENV2=V2 (env may be empty).  Prints value, ms/step and writer ms per run; JSON lines in
+# gpurun_out/ab_$TAG/.
+set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-for rep in ${REPS:-1 2}; do
-  for v in ${VARS}; do
-    echo -n "$v: "
-    env $v timeout -k 10 120 python bench.py --steps 6 --warmup 2 --no-cpu-baseline 2>/dev/null > gpurun_out/ab/o.log || exit 1
-    python3 -c "import json;d=json.loads(open('gpurun_out/ab/o.log').read().strip().splitlines()[-1]);print(round(d['ms_per_step'],2),d['stage_ms']['sample_shuffle_decode'])"
+TAG=${TAG:-ab}
+REPS=${REPS:-2}
+BENCH_ARGS=${BENCH_ARGS:---steps 8 --warmup 2}
+O=gpurun_out/ab_$TAG
+mkdir -p $O
+for rep in $(seq 1 $REPS); do
+  for v in "$@"; do
+    label=${v%%:*}
+    envs=${v#*:}
+    env $envs timeout -k 10 300 python -u bench.py $BENCH_ARGS --no-cpu-baseline --no-e2e > $O/${label}_$rep.json 2> $O/${label}_$rep.err || exit $?
+    python3 -c "import json; d=[json.loads(l) for l in open('$O/${label}_$rep.json') if l.startswith('{')][-1]; r=d['roofline']; print('$label', $rep, round(d['value']/1e9,4), round(d['ms_per_step'],2), 'writer', round(r['avg_launch_ms'],4))"
   done
 done
-if [ -n "$PROF" ]; then
-  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-  env $PROF timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab/prof.log 2>&1
-  grep -h "decode" gpurun_out/ab/prof/*stats.csv | cut -c1-160
-fi

@@ -6,6 +6,8 @@ cd "$GRAFT_REPO_ROOT"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py -k "forward_haplotype or philox_corruption_vs_numpy or writer_gate_pipelined" > /tmp/r04b_pytest.log 2>&1; rc=$?; tail -3 /tmp/r04b_pytest.log; [ $rc -eq 0 ] || exit $rc
 O=gpurun_out/r04b
 mkdir -p $O
+timeout -k 10 120 ./scripts/calib_writer > $O/calib_writer.json || exit $?
+cat $O/calib_writer.json
 run() {   # tag, env...
   local tag=$1; shift
   env "$@" timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-e2e > $O/b_$tag.json 2> $O/b_$tag.err || return $?
