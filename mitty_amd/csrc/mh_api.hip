@@ -933,8 +933,18 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
   if ((fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
+  // the two files' copies on two streams (two DMA engines side by side), file 2's after everything the main stream
+  // waits for (the writers)
+  const bool both = fq1 && len1 && fq2 && len2;
+  if (both) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+  }
   if (fq1 && len1) HIPCHK(ctx, hipMemcpyAsync(fq1, (char *)ctx->out1.p + off1, len1, hipMemcpyDeviceToHost, ctx->stream));
-  if (fq2 && len2) HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost, ctx->stream));
+  if (fq2 && len2)
+    HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost,
+                               both ? ctx->stream2 : ctx->stream));
+  if (both) SYNCCHK(ctx, hipStreamSynchronize(ctx->stream2));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
