@@ -658,7 +658,7 @@ struct QHead {
 // The output sweeps of a 32-template tile whose strings and metadata are in LDS: LPR lanes per record (record
 // r = file f, template j), passes over the tile's NF * ED_T records.  gbase: arena offset of the tile's first byte per
 // file; span: the tile's bytes per file.
-template <int NF, int LPR, int CR>
+template <int NF, int LPR, int CR, int FL>
 __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64_t gbase[2], const int32_t span[2],
                                           int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena,
                                           int32_t dbg) {
@@ -728,6 +728,41 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
   // no faster than the full one)
   if (staged) {
     if (dbg & 64) lds_barrier(); else __syncthreads();
+  }
+  if (FL) {
+    // flat sweep (FL): the tile's whole chunks per file in address order, consecutive lanes on consecutive chunks (a
+    // wave-instruction stores 1 KiB of contiguous lines instead of 16 records' 64-byte pieces); a chunk's record is
+    // the last one starting before the chunk's end (binary search over the tile's record starts), its seam or part
+    // as in the record-major sweep below
+    for (int f = 0; f < NF; f++) {
+      const int64_t g0 = gbase[f];
+      char *const out = arena[f];
+      const int64_t cend = (g0 + span[f]) >> 4;
+      for (int64_t cg = ((g0 + 15) >> 4) + tid; cg < cend; cg += ED_THREADS) {
+        const int32_t x = (int32_t)((cg << 4) - g0);
+        int lo = 0, hi = nt - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (meta[mid].rel[f] <= x + 15) lo = mid; else hi = mid - 1;
+        }
+        const DMeta &M = meta[lo];
+        const int32_t x0 = x - M.rel[f];
+        const int32_t sb = M.sb, tl = sb + M.S[f];
+        const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
+        if (b >= 0 && !staged) continue;                        // seam chunk, stored by the seam pass
+        uint4 v;
+        if (CR != 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
+          v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);
+        } else {
+          const int32_t src = b >= 0 ? o_s + ((f * ED_T + lo) * 4 + b) * 16
+                                     : (x0 + 16 <= sb ? M.qb + x0
+                                                      : (x0 + 16 <= tl ? M.bb[f] + (x0 - sb) : M.tb[f] + (x0 - tl)));
+          v = lds_load16(smem, (uint32_t)src);
+        }
+        *(uint4 *)(out + (cg << 4)) = v;
+      }
+    }
+    return;
   }
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
@@ -821,7 +856,7 @@ struct TArgs {
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
-template <int NF, int LPR, int CR>
+template <int NF, int LPR, int CR, int FL>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
@@ -1079,16 +1114,16 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   }
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
-  if (!(A.dbg & 1)) ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena, A.dbg);
+  if (!(A.dbg & 1)) ed_output<NF, LPR, CR, FL>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena, A.dbg);
 }
 
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
 // waves per SIMD instead of eight — and the launch of 184 k workgroups costs only ~0.35 ms of a 2.6 ms chr1-unit
 // writer (MH_EW_DBG=32), so there is no persistent variant.)
-template <int NF, int LPR, int CR>
+template <int NF, int LPR, int CR, int FL>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
   if (A.dbg & 32) return;   // (experiments: the launch alone)
-  emit_tile<NF, LPR, CR>(A, qh, blockIdx.x);
+  emit_tile<NF, LPR, CR, FL>(A, qh, blockIdx.x);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -1798,6 +1833,20 @@ static int ew_dbg_env() {
 // qname rows: a multiple of 16 bytes plus 4 (an odd number of dwords), so wave 0's lanes (one qname row per template)
 // writing the same column land on 32 different LDS banks instead of 8
 constexpr int32_t ED_QPAD = 4;
+// the direct writer's instantiation: CR mode (0 perfect, 1 in-place corruption after it, 2 corruption rows), one or
+// two files; MH_EW_FLAT=1 (experiment): the flat output sweep
+using EwKernel = void (*)(TArgs, QHead);
+static EwKernel ew_kernel(int cr, bool two) {
+  static const bool flat = getenv("MH_EW_FLAT") && atoi(getenv("MH_EW_FLAT"));
+  if (flat)
+    return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 1> : k_emit_tiles<1, 8, 2, 1>)
+           : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 1> : k_emit_tiles<1, 8, 1, 1>)
+                     : (two ? k_emit_tiles<2, 4, 0, 1> : k_emit_tiles<1, 8, 0, 1>);
+  return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 0> : k_emit_tiles<1, 8, 2, 0>)
+         : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 0> : k_emit_tiles<1, 8, 1, 0>)
+                   : (two ? k_emit_tiles<2, 4, 0, 0> : k_emit_tiles<1, 8, 0, 0>);
+}
+
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows = false) {
   const bool staged = !(ew_dbg_env() & 256) && !rows;   // (256: seam chunks stored by the seam pass, no LDS for them)
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
@@ -2036,9 +2085,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
             qstride, ew_dbg};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
-    auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
-               : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
-                                 : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
+    auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -2369,9 +2416,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
           ew_dbg_env()};
   if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
   stage_begin(ctx, "emit_write");
-  auto kfn = cr_rows           ? (write_fastq2 ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
-             : ctx->corrupt_on ? (write_fastq2 ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
-                               : (write_fastq2 ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
+  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
