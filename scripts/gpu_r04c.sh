@@ -18,7 +18,6 @@ python3 -c "import json; d=json.load(open('$O/verify.json')); print('verify', d[
 timeout -k 10 120 ./scripts/calib_writer > $O/calib_writer.json || exit $?
 cat $O/calib_writer.json
 TAG=r04c REPS=2 bash scripts/gpu_ab.sh 'base:' 'fwd:MH_HAP_FWD=1' 'tail4:MH_WRITER_GATE_TAIL=4' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'flatfwd:MH_EW_FLAT=1 MH_HAP_FWD=1' || exit $?
-TAG=r04c_dbg REPS=1 bash scripts/gpu_ab.sh 'dbg1:MH_EW_DBG=1' 'dbg8:MH_EW_DBG=8' 'dbg16:MH_EW_DBG=16' 'dbg9:MH_EW_DBG=9' 'dbg32:MH_EW_DBG=32' || exit $?
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-e2e > $O/prof.log 2>&1 || exit $?
