@@ -906,9 +906,46 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       rcw[k] = A.ccode[g];
     }
   }
+  if (A.dbg & 512) {
+    // (MH_EW_GATHER4, experiment) every thread gathers: window slots s = tid + 256 k (window s / chunks, chunk
+    // s % chunks of the tile's 64 windows), issued before anything else so wave 0's metadata loads and formatting
+    // overlap them; no redundant loads for unused chunks
+    uint4 wv[6];
+    int32_t dst[6];
+    bool rv[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const int s_ = tid + ED_THREADS * k;
+      const bool inr = s_ < 2 * ED_T * chunks;
+      const int w = inr ? s_ / chunks : 0, c = s_ - chunks * w, jg = w >> 1, sg = w & 1;
+      const bool kg = inr && jg < nt;
+      const int64_t pg = kg ? (sg ? A.pos1[t0 + jg] : A.pos0[t0 + jg]) : h.p_min;
+      int64_t ag = pg - h.p_min, eg = pg + A.rlen - h.p_min;
+      if (eg > h.hap_len) eg = h.hap_len;
+      if (ag > h.hap_len) ag = h.hap_len;
+      const int64_t lg = eg > ag ? eg - ag : 0;
+      const bool rev = sg && h.rc == nullptr;
+      const int64_t a2g = sg && !rev ? h.hap_len - ag - lg : ag;
+      const int64_t a16 = a2g & ~(int64_t)15;
+      const int32_t cmax = lg > 0 ? (int32_t)(((a2g + lg - 1) >> 4) - (a16 >> 4)) : 0;
+      const bool u = kg && a16 + 16 * c < a2g + lg;
+      wv[k] = *(const uint4 *)((sg && !rev ? h.rc : h.hap) + a16 + (u ? 16 * c : 0));
+      dst[k] = u ? o_win + w * win_stride + 16 * (rev ? cmax - c : c) : o_dump;
+      rv[k] = rev;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      if (tid + ED_THREADS * k >= 2 * ED_T * chunks) break;
+      uint4 v = wv[k];
+      if (rv[k])
+        v = make_uint4(comp4(__builtin_bswap32(v.w)), comp4(__builtin_bswap32(v.z)), comp4(__builtin_bswap32(v.y)),
+                       comp4(__builtin_bswap32(v.x)));
+      *(uint4 *)(smem + dst[k]) = v;
+    }
+  }
   for (int i = tid; i < TL; i += ED_THREADS)
     smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
-  if (tid >= 64 && !(A.dbg & 16)) {
+  if (tid >= 64 && !(A.dbg & (16 | 512))) {
     // waves 1-3: the gathers (three threads per mate window), all in flight together; an unused chunk re-reads the
     // first one
     const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
@@ -1827,7 +1864,8 @@ static int64_t digit_sum_host(int64_t K) {
 // dynamic LDS of k_emit_tiles: metadata, windows, qname buffers, T, seam chunks, dump
 // MH_EW_DBG (experiments, k_emit_tiles' TArgs.dbg)
 static int ew_dbg_env() {
-  static const int v = getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0;
+  static const int v = (getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0) |
+                       (getenv("MH_EW_GATHER4") && atoi(getenv("MH_EW_GATHER4")) ? 512 : 0);
   return v;
 }
 // qname rows: a multiple of 16 bytes plus 4 (an odd number of dwords), so wave 0's lanes (one qname row per template)

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04c
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_parity.py -k "templates_golden or templates_vs_oracle or batched_units or forward_haplotype or flat_sweep or writer_gate_pipelined or scan_timeout or chr1_templates or unit_vs_oracle_2mbp" \
+  tests/test_gpu_parity.py -k "templates_golden or templates_vs_oracle or batched_units or forward_haplotype or writer_variants or writer_gate_pipelined or scan_timeout or chr1_templates or unit_vs_oracle_2mbp" \
   tests/test_gpu_rccl.py > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" $O/pytest.log | tail -3; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
@@ -17,7 +17,7 @@ rc=$?; echo "verify rc=$rc"; tail -2 $O/verify.err; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json; d=json.load(open('$O/verify.json')); print('verify', d['verify'])"
 timeout -k 10 120 ./scripts/calib_writer > $O/calib_writer.json || exit $?
 cat $O/calib_writer.json
-TAG=r04c REPS=2 bash scripts/gpu_ab.sh 'base:' 'fwd:MH_HAP_FWD=1' 'tail4:MH_WRITER_GATE_TAIL=4' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'flatfwd:MH_EW_FLAT=1 MH_HAP_FWD=1' || exit $?
+TAG=r04c REPS=1 bash scripts/gpu_ab.sh 'base:' 'fwd:MH_HAP_FWD=1' 'tail4:MH_WRITER_GATE_TAIL=4' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'flatfwd:MH_EW_FLAT=1 MH_HAP_FWD=1' 'g4:MH_EW_GATHER4=1' 'g4flat:MH_EW_GATHER4=1 MH_EW_FLAT=1' || exit $?
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-e2e > $O/prof.log 2>&1 || exit $?

@@ -363,12 +363,14 @@ def test_unit_vs_oracle_forward_haplotype(native, monkeypatch, model):
   _unit_vs_oracle(1_200_000, 4000000001, model, n_seed=7, rate=8e-3, start0=98_765)
 
 
-@pytest.mark.parametrize('fwd', [0, 1])
-def test_unit_vs_oracle_flat_sweep(native, monkeypatch, fwd):
-  """The writer's flat output sweep (MH_EW_FLAT=1: a tile's chunks in address order, each chunk's record found by a
-  binary search over the record starts), with rc and forward-only haplotypes: byte-identical to the oracle, dense
-  variants (long qnames, many seams) and an offset region."""
-  monkeypatch.setenv('MH_EW_FLAT', '1')
+@pytest.mark.parametrize('flat,fwd,g4', [(1, 0, 0), (1, 1, 0), (0, 0, 1), (0, 1, 1), (1, 1, 1)])
+def test_unit_vs_oracle_writer_variants(native, monkeypatch, flat, fwd, g4):
+  """Writer variants: the flat output sweep (MH_EW_FLAT=1: a tile's chunks in address order, each chunk's record
+  found by a binary search over the record starts), every thread gathering (MH_EW_GATHER4=1), with rc and
+  forward-only haplotypes: byte-identical to the oracle, dense variants (long qnames, many seams) and an offset
+  region."""
+  monkeypatch.setenv('MH_EW_FLAT', str(flat))
+  monkeypatch.setenv('MH_EW_GATHER4', str(g4))
   monkeypatch.setenv('MH_HAP_FWD', str(fwd))
   assert _unit_vs_oracle(2_000_000, 23, 'hiseq-X-v2.5-Garvan') > 10000
   _unit_vs_oracle(1_000_000, 4000000002, '1kg-pcr-free', n_seed=9, rate=8e-3, start0=54_321)
