@@ -278,6 +278,12 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   ctx->gate_at = ge ? atoi(ge) : -1;
   const char *hf = getenv("MH_HAP_FWD");
   ctx->hap_fwd = hf && atoi(hf) != 0;
+  const char *ef = getenv("MH_EW_FLAT");
+  ctx->ew_flat = ef && atoi(ef) != 0;
+  const char *ed = getenv("MH_EW_DBG"), *eg = getenv("MH_EW_GATHER4");
+  ctx->ew_dbg = (ed ? atoi(ed) : 0) | (eg && atoi(eg) ? 512 : 0);
+  const char *so = getenv("MH_SORT");
+  ctx->sort_lsd = so && !strcmp(so, "lsd");
   const char *gt = getenv("MH_WRITER_GATE_TAIL");
   ctx->gate_tail = gt ? std::max(0, atoi(gt)) : 0;
   int can_wait = 0;

@@ -1862,20 +1862,13 @@ static int64_t digit_sum_host(int64_t K) {
 }
 
 // dynamic LDS of k_emit_tiles: metadata, windows, qname buffers, T, seam chunks, dump
-// MH_EW_DBG (experiments, k_emit_tiles' TArgs.dbg)
-static int ew_dbg_env() {
-  static const int v = (getenv("MH_EW_DBG") ? atoi(getenv("MH_EW_DBG")) : 0) |
-                       (getenv("MH_EW_GATHER4") && atoi(getenv("MH_EW_GATHER4")) ? 512 : 0);
-  return v;
-}
 // qname rows: a multiple of 16 bytes plus 4 (an odd number of dwords), so wave 0's lanes (one qname row per template)
 // writing the same column land on 32 different LDS banks instead of 8
 constexpr int32_t ED_QPAD = 4;
 // the direct writer's instantiation: CR mode (0 perfect, 1 in-place corruption after it, 2 corruption rows), one or
-// two files; MH_EW_FLAT=1 (experiment): the flat output sweep
+// two files, the flat output sweep (mh_ctx::ew_flat, experiment)
 using EwKernel = void (*)(TArgs, QHead);
-static EwKernel ew_kernel(int cr, bool two) {
-  static const bool flat = getenv("MH_EW_FLAT") && atoi(getenv("MH_EW_FLAT"));
+static EwKernel ew_kernel(int cr, bool two, bool flat) {
   if (flat)
     return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 1> : k_emit_tiles<1, 8, 2, 1>)
            : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 1> : k_emit_tiles<1, 8, 1, 1>)
@@ -1885,8 +1878,8 @@ static EwKernel ew_kernel(int cr, bool two) {
                    : (two ? k_emit_tiles<2, 4, 0, 0> : k_emit_tiles<1, 8, 0, 0>);
 }
 
-static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows = false) {
-  const bool staged = !(ew_dbg_env() & 256) && !rows;   // (256: seam chunks stored by the seam pass, no LDS for them)
+static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows, int32_t dbg) {
+  const bool staged = !(dbg & 256) && !rows;   // (256: seam chunks stored by the seam pass, no LDS for them)
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
@@ -2086,7 +2079,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
   const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows, ctx->ew_dbg);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -2117,13 +2110,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     }
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
-    const int ew_dbg = ew_dbg_env();
+    const int ew_dbg = ctx->ew_dbg;
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
             qstride, ew_dbg};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
-    auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
+    auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -2357,7 +2350,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
   const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows, ctx->ew_dbg);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
   if (!direct || lds_d > 64 * 1024) {
@@ -2451,10 +2444,10 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   stage_end(ctx);
   TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
           (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride,
-          ew_dbg_env()};
+          ctx->ew_dbg};
   if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
   stage_begin(ctx, "emit_write");
-  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
+  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);

@@ -251,6 +251,10 @@ struct mh_ctx {
   // forward-only haplotypes (MH_HAP_FWD=1, experiment): no reverse-complement copy; the writer reverse-complements
   // mate-1 windows into LDS itself
   bool hap_fwd = false;
+  // experiments read once per context (mh_create), so tests switch them per context: MH_EW_FLAT (flat output sweep),
+  // MH_EW_DBG / MH_EW_GATHER4 (the writer's TArgs.dbg bits), MH_SORT=lsd (the hand-written permutation sort)
+  bool ew_flat = false, sort_lsd = false;
+  int32_t ew_dbg = 0;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas

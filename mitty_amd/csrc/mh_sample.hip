@@ -32,6 +32,9 @@
 #include "mh_scan.h"
 #include "mh_sort.h"
 
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
 namespace mh {
 
 namespace jump {
@@ -1197,13 +1200,20 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
-// The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (8-bit digits, 256-thread
-// workgroups).  (Round 3 ran rocprim's onesweep with 1024-thread workgroups, which found no room on a CU beside the
-// FASTQ writers and waited for them to drain.)
+// The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (7-bit digits, 256-thread
+// workgroups sized to fit beside the FASTQ writers), or rocprim's onesweep (1024-thread workgroups, which wait for
+// whole CUs beside the writers; 9 key bits per pass: a 64 M-draw batch's 27-bit keys in 3 passes).  Until the
+// hand-written sort has run on the GPU, rocprim stays the default (MH_SORT=lsd selects the other).
+using SortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>>;
 template <class KIn>
-static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
-                            size_t n, unsigned end_bit, hipStream_t st) {
-  return lsd_sort_pairs_iota(tmp, tmp_bytes, keys_in, keys_out, vals_out, (int64_t)n, end_bit, st);
+static hipError_t perm_sort(bool lsd, void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out,
+                            uint32_t *vals_out, size_t n, unsigned end_bit, hipStream_t st) {
+  if (lsd) return lsd_sort_pairs_iota(tmp, tmp_bytes, keys_in, keys_out, vals_out, (int64_t)n, end_bit, st);
+  const rocprim::counting_iterator<uint32_t> iota(0u);
+  return rocprim::radix_sort_pairs<SortCfg>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
 }
 
 struct BatchPerm {
@@ -1270,9 +1280,9 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       unsigned end_bit = 1;
       while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
       size_t tmp = 0;
-      HIPCHK(ctx, perm_sort(nullptr, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
+      HIPCHK(ctx, perm_sort(ctx->sort_lsd, nullptr, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
-      HIPCHK(ctx, perm_sort(perm_tmp.p, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
+      HIPCHK(ctx, perm_sort(ctx->sort_lsd, perm_tmp.p, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
       hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                          (const uint32_t *)sv, nxt);
@@ -1556,9 +1566,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     unsigned end_bit = 1;
     while (end_bit < 32 && ((int64_t)1 << end_bit) < j_total) end_bit++;
     size_t tmp = 0;
-    HIPCHK(ctx, perm_sort(nullptr, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
+    HIPCHK(ctx, perm_sort(ctx->sort_lsd, nullptr, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     MH_TRY(ensure(ctx, ctx->pb_tmp, tmp + 256));
-    HIPCHK(ctx, perm_sort(ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
+    HIPCHK(ctx, perm_sort(ctx->sort_lsd, ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
     MH_TRY(gate_release(ctx, st, ctx->job));   // the previous job's gated writers may go

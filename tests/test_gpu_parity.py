@@ -376,9 +376,12 @@ def test_unit_vs_oracle_writer_variants(native, monkeypatch, flat, fwd, g4):
   _unit_vs_oracle(1_000_000, 4000000002, '1kg-pcr-free', n_seed=9, rate=8e-3, start0=54_321)
 
 
-def test_batched_units_vs_oracle(native):
+@pytest.mark.parametrize('sort', ['rocprim', 'lsd'])
+def test_batched_units_vs_oracle(native, monkeypatch, sort):
   """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
-  reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated."""
+  reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated.  The permutation's sort by
+  rocprim's onesweep and by the hand-written LSD radix sort (MH_SORT=lsd, mh_sort.h)."""
+  monkeypatch.setenv('MH_SORT', sort)
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from oracle import oracle as O
