@@ -4,7 +4,7 @@
 # usage: scripts/gpurun_wait.sh TIMEOUT 'command'
 T=$1
 shift
-for i in $(seq 1 20); do
+for i in $(seq 1 ${MAX_TRIES:-60}); do
   out=$(timeout $((T + 900)) /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
   rc=$?
   if echo "$out" | grep -q "status=transient rc=None charged=0.0s\|status=transient rc=None charged=Nones"; then
@@ -15,5 +15,5 @@ for i in $(seq 1 20); do
   echo "$out" | grep -v "^\[gpurun\] every call"
   exit $rc
 done
-echo "[wait] gave up after 20 attempts" >&2
+echo "[wait] gave up after ${MAX_TRIES:-60} attempts" >&2
 exit 3
