@@ -135,6 +135,16 @@ int32_t mh_sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_i
                               const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                               int32_t rng_mode);
 int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
+/* mh_sample_units without the host wait at its end: each unit's last stages (its part of the permutation chase, its
+ * template lengths and compaction; readgenerate.py:129-159 per unit) are queued in unit order on a second stream,
+ * and the unit's template set is resolved when first used (mh_use_templates, mh_templates_count, or any entry
+ * point other than the emission ones), so the first unit's FASTQ writer can start while later units still sample.
+ * The same templates as mh_sample_units. */
+int32_t mh_sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                              int32_t rng_mode);
+/* Templates kept in set tpl_id (waits for an asynchronous unit's tail). */
+int32_t mh_templates_count(mh_ctx *ctx, int32_t tpl_id, int64_t *n);
 /* Make template set `tpl_id` the current one (used by mh_emit_reads / mh_get_templates). */
 int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id);
 int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id);

@@ -21,7 +21,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free',
-           'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_begin', 'mh_sample_units_end',
+           'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_begin', 'mh_sample_units_end', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
@@ -143,6 +143,8 @@ def lib():
   _sig(L, 'mh_sample_units', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32, c_vp])
   _sig(L, 'mh_sample_units_begin', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32])
   _sig(L, 'mh_sample_units_end', [c_vp, c_i32, c_vp])
+  _sig(L, 'mh_sample_units_async', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32])
+  _sig(L, 'mh_templates_count', [c_vp, c_i32, c_vp])
   _sig(L, 'mh_use_templates', [c_vp, c_i32])
   _sig(L, 'mh_release_templates', [c_vp, c_i32])
   _sig(L, 'mh_mt_window_at', [ctypes.c_uint32, c_u64, c_vp])
@@ -474,6 +476,22 @@ class Context:
     out = np.zeros(max(n_units, 1), dtype=np.int64)
     self._chk(self._L.mh_sample_units_end(self._h, int(n_units), _ptr(out)))
     return out[:n_units]
+
+  def sample_units_async(self, tpl_ids, slots, seeds, p, rlen, cum_tlen, rng_mode=MH_RNG_MITTY):
+    """sample_units whose per-unit tails run on without a host wait; template_count(id) (or use_templates) waits
+    for one unit."""
+    ids = np.ascontiguousarray(tpl_ids, dtype=np.int32)
+    sl = np.ascontiguousarray(slots, dtype=np.int32)
+    sd = np.ascontiguousarray(seeds, dtype=np.uint64)
+    ct = np.ascontiguousarray(cum_tlen, dtype=np.float64)
+    self._chk(self._L.mh_sample_units_async(self._h, len(ids), _ptr(ids), _ptr(sl), _ptr(sd), float(p), int(rlen),
+                                            _ptr(ct), len(ct), int(rng_mode)))
+    return len(ids)
+
+  def template_count(self, tpl_id):
+    n = c_i64()
+    self._chk(self._L.mh_templates_count(self._h, int(tpl_id), ctypes.byref(n)))
+    return n.value
 
   def use_templates(self, tpl_id):
     self._chk(self._L.mh_use_templates(self._h, int(tpl_id)))

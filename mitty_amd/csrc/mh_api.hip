@@ -194,11 +194,19 @@ void stages_collect(mh_ctx *ctx) {
 
 using namespace mh;
 
-#define CTX_GUARD_NOJOIN(ctx)                                              \
+// the emission entry points: they run beside a batch's asynchronous tail (their template set was resolved by
+// mh_use_templates; their scratch is not the tail's)
+#define CTX_GUARD_EMIT(ctx)                                                \
   do {                                                                     \
     if (!(ctx)) return MH_E_ARG;                                           \
     hipError_t _e = hipSetDevice((ctx)->device);                           \
     if (_e != hipSuccess) return hip_fail((ctx), _e, "hipSetDevice", __FILE__, __LINE__); \
+  } while (0)
+// every other entry point first resolves a pending asynchronous tail (it may share the batch scratch)
+#define CTX_GUARD_NOJOIN(ctx)                                              \
+  do {                                                                     \
+    CTX_GUARD_EMIT(ctx);                                                   \
+    MH_TRY(tpl_resolve_all(ctx));                                          \
   } while (0)
 // every entry point but the emission ones: the main stream first waits for the last queued FASTQ writer
 #define CTX_GUARD(ctx)                                                     \
@@ -343,7 +351,9 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &e : ctx->res_ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
+  ctx->tail_state.reset();
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->h_units) (void)hipHostFree(ctx->h_units);
   for (auto &e : ctx->eset) {
     release(e.recs); release(e.off); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
@@ -741,10 +751,32 @@ int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n) {
   return sample_units_end(ctx, n_units, out_n);
 }
 
-int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id) {
-  if (!ctx) return MH_E_ARG;
+int32_t mh_sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
+                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
+                              int32_t rng_mode) {
+  CTX_GUARD_NOJOIN(ctx);
+  std::vector<int64_t> pmin, pmax;
+  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
+  return sample_units_async(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen,
+                            rng_mode);
+}
+
+int32_t mh_templates_count(mh_ctx *ctx, int32_t tpl_id, int64_t *n) {
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->tsets.find(tpl_id);
-  if (it == ctx->tsets.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  if (it == ctx->tsets.end()) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  MH_TRY(tpl_resolve(ctx, it->second));
+  if (!it->second.valid) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  if (n) *n = it->second.n;
+  return MH_OK;
+}
+
+int32_t mh_use_templates(mh_ctx *ctx, int32_t tpl_id) {
+  CTX_GUARD_EMIT(ctx);
+  auto it = ctx->tsets.find(tpl_id);
+  if (it == ctx->tsets.end()) return arg_fail(ctx, MH_E_STATE, "unknown template set");
+  MH_TRY(tpl_resolve(ctx, it->second));
+  if (!it->second.valid) return arg_fail(ctx, MH_E_STATE, "unknown template set");
   ctx->cur_tpl = tpl_id;
   return MH_OK;
 }
@@ -867,7 +899,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
 
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
@@ -877,7 +909,7 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
 
 int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                         int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || (!out_kept) != (!out_b1) || (!out_kept) != (!out_b2))
@@ -889,7 +921,7 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
@@ -901,7 +933,7 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
 int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                         int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                         int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
@@ -926,7 +958,7 @@ int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end,
 }
 
 int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   MH_TRY(sync_async_fill(ctx));
   if (b1) *b1 = ctx->used1;
   if (b2) *b2 = ctx->used2;
@@ -956,12 +988,12 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
 }
 
 int32_t mh_output_reset(mh_ctx *ctx) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   return output_reset(ctx);
 }
 
 int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t *out_bytes) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (rlen <= 0 || !out_bytes) return arg_fail(ctx, MH_E_ARG, "bad arguments");
@@ -970,7 +1002,7 @@ int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t
 
 int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int32_t *ticket) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !ticket) return arg_fail(ctx, MH_E_ARG, "bad arguments");
@@ -979,7 +1011,7 @@ int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
 
 int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2,
                        int64_t *out_base1, int64_t *out_base2) {
-  CTX_GUARD_NOJOIN(ctx);
+  CTX_GUARD_EMIT(ctx);
   int64_t r[5];
   MH_TRY(emit_result(ctx, ticket, r));
   if (out_kept) *out_kept = r[0];

@@ -98,6 +98,7 @@ struct TplSet {
   int64_t n = 0;
   int32_t rlen = 0;
   bool valid = false;
+  int32_t pend = -1;   // unit index in ctx->tail_state while the batch's asynchronous tail has not been resolved
 };
 
 struct Contig {
@@ -165,6 +166,10 @@ struct mh_ctx {
   // a batch between mh_sample_units_begin and _end (mh_sample.hip SampleState); writers queued meanwhile wait, with
   // the gate on, for the begun batch's sort (gate >= job) instead of the next one's (gate >= job + 1)
   std::shared_ptr<void> sample_state;
+  // a batch whose per-unit tail (chase, template lengths, compaction) is queued on stream2 without a host wait
+  // (mh_sample_units_async): its template sets are resolved one by one (tpl_resolve) as they are used
+  std::shared_ptr<void> tail_state;
+  int64_t *h_units = nullptr, *d_units = nullptr;   // mapped host memory: per unit m, status, flag, done
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
   // Writer gate.  The permutation's radix sort cannot run beside a FASTQ writer (its workgroups need a whole CU and
@@ -351,6 +356,13 @@ int32_t sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
                            int32_t n_tlen, int32_t rng_mode);
 int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
+int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
+                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                           int32_t n_tlen, int32_t rng_mode);
+// a template set of an asynchronous tail: wait for its unit (host), read its count, run the rare exact fix-up, and
+// order the main stream after it; no-op for a resolved set
+int32_t tpl_resolve(mh_ctx *ctx, TplSet &ts);
+int32_t tpl_resolve_all(mh_ctx *ctx);
 
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)

@@ -754,9 +754,10 @@ __global__ void __launch_bounds__(256) k_perm_heads(int64_t n, const uint32_t *K
   nxt[b] = s;   // buckets without a head keep the -1 of the memset
 }
 
-__global__ void __launch_bounds__(256) k_perm_chase(int64_t n, const uint32_t *K, const uint32_t *V,
+// sorted entries [k0, n): one unit's range of the batch sort (its keys are its own: K[n] starts another unit) or all
+__global__ void __launch_bounds__(256) k_perm_chase(int64_t k0, int64_t n, const uint32_t *K, const uint32_t *V,
                                                     const int32_t *nxt, const int64_t *ts, int64_t *out) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = k0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const uint32_t b = K[k], p = V[k];
   int64_t q = b;
@@ -1298,8 +1299,8 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   const int64_t *ts_use = bp && rng_mode == MH_RNG_MITTY && n > 1 ? bp->tsh + u.j_off : ts;
   if (permute) {
     stage_begin(ctx, "sample_permutation");
-    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
-                       (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)ts, ts_shuf);
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (int64_t)0, n,
+                       (const uint32_t *)sk, (const uint32_t *)sv, (const int32_t *)nxt, (const int64_t *)ts, ts_shuf);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     ts_use = ts_shuf;
@@ -1334,6 +1335,13 @@ struct SampleState {
   int64_t *d_m = nullptr, *d_status = nullptr;
   uint32_t *d_flags = nullptr;
   BatchPerm bp{nullptr, nullptr};
+  // the asynchronous tail (sample_units_async): per unit, its tail's end on stream2; units not yet resolved
+  std::vector<hipEvent_t> ev;
+  int32_t n_pending = 0;
+  ~SampleState() {
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 // First half: plan, word streams, shuffle decode, geometric scans and — batch path — the permutation's sort and
@@ -1346,6 +1354,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
       return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seeds[u]) + " is out of range 0 - 4294967295");
   if (n_tlen <= 0 || n_tlen > 8192) return arg_fail(ctx, MH_E_ARG, "cum_tlen must have 1..8192 entries");
   if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
+  MH_TRY(tpl_resolve_all(ctx));   // the previous batch's asynchronous tail reads the batch buffers this one refills
   ctx->job++;   // a new job: its writers count from 0 for the gate, and it opens the previous job's gate
   ctx->writers_in_job = 0;
   ctx->job_units = n_units;
@@ -1626,8 +1635,8 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
     const uint32_t *sk = (const uint32_t *)ctx->pb[3].p, *sv = (const uint32_t *)ctx->pb[4].p;
     const int32_t *nxt = (const int32_t *)ctx->pb[5].p;
     stage_begin(ctx, "sample_permutation");
-    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total, sk, sv, nxt,
-                       (const int64_t *)bp.ts, bp.tsh);
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, (int64_t)0, j_total,
+                       sk, sv, nxt, (const int64_t *)bp.ts, bp.tsh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     // 3. every unit's template lengths, compaction and file order (lanes)
@@ -1694,6 +1703,128 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
     if (out_n) out_n[u] = ts.n;
   }
   return MH_OK;
+}
+
+// One unit's tail results into mapped host memory (plain vector stores; the host reads them after the unit's event).
+__global__ void k_unit_result(const int64_t *m, const int64_t *status, const uint32_t *flag, int64_t *out) {
+  if (threadIdx.x == 0) {
+    out[0] = *m;
+    out[1] = *status;
+    out[2] = (int64_t)*flag;
+  }
+}
+
+// The batch tail without a host wait: per unit, in unit order on stream2, its range of the batch chase
+// ([j_off, j_off + n + 4) of the sorted entries: a unit's keys are its own), its template lengths and compaction, its
+// results into mapped host memory and an event.  The writer of unit 0 then waits for unit 0's tail only, not for the
+// whole batch's chase and compactions (the writer stream's idle gap at batch boundaries).  Template sets
+// stay pending (TplSet.pend) until tpl_resolve.
+static int32_t sample_tail_async(mh_ctx *ctx, const std::shared_ptr<SampleState> &Sp) {
+  SampleState &S = *Sp;
+  std::vector<UnitPlan> &plan = S.plan;
+  const int32_t n_units = S.n_units;
+  hipStream_t st = ctx->stream, l1 = ctx->stream2;
+  const BatchPerm &bp = S.bp;
+  const uint32_t *sk = (const uint32_t *)ctx->pb[3].p, *sv = (const uint32_t *)ctx->pb[4].p;
+  const int32_t *nxt = (const int32_t *)ctx->pb[5].p;
+  HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
+  HIPCHK(ctx, hipStreamWaitEvent(l1, ctx->ev_fork, 0));
+  S.ev.assign(n_units, nullptr);
+  for (int32_t u = 0; u < n_units; u++) {
+    UnitPlan &q = plan[u];
+    TplSet &ts = *q.out;
+    if (q.n == 0) {
+      ts.n = 0;
+      ts.rlen = S.rlen;
+      ts.valid = true;
+      continue;
+    }
+    ctx->stage_stream = l1;
+    stage_begin(ctx, "sample_permutation");
+    const int64_t k0 = q.j_off, k1 = q.j_off + q.n + 4;
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(k1 - k0, 256, INT32_MAX)), dim3(256), 0, l1, k0, k1, sk, sv, nxt,
+                       (const int64_t *)bp.ts, bp.tsh);
+    stage_end(ctx);
+    ctx->stage_stream = nullptr;
+    HIPCHK(ctx, hipGetLastError());
+    MH_TRY(finish_unit(ctx, q, S.words, S.jall + q.j_off, S.p, S.rlen, S.d_cum, S.n_tlen, S.rng_mode, false,
+                       S.d_m + u, S.d_flags + u, 1, 0, 2, nullptr, &bp));
+    hipLaunchKernelGGL(k_unit_result, dim3(1), dim3(64), 0, l1, (const int64_t *)(S.d_m + u),
+                       (const int64_t *)(S.d_status + u), (const uint32_t *)(S.d_flags + u), ctx->d_units + 4 * u);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventCreateWithFlags(&S.ev[u], hipEventDisableTiming));
+    HIPCHK(ctx, hipEventRecord(S.ev[u], l1));
+    ts.pend = u;
+    S.n_pending++;
+  }
+  stage_end(ctx);
+  if (S.n_pending) ctx->tail_state = Sp;
+  return MH_OK;
+}
+
+int32_t tpl_resolve(mh_ctx *ctx, TplSet &ts) {
+  if (ts.pend < 0) return MH_OK;
+  const int32_t u = ts.pend;
+  ts.pend = -1;
+  auto Sp = std::static_pointer_cast<SampleState>(ctx->tail_state);
+  if (!Sp || u >= Sp->n_units || Sp->plan[u].out != &ts)
+    return arg_fail(ctx, MH_E_STATE, "template set of a lost sampling batch");
+  SampleState &S = *Sp;
+  UnitPlan &q = S.plan[u];
+  hipStream_t st = ctx->stream;
+  SYNCCHK(ctx, hipEventSynchronize(S.ev[u]));
+  const volatile int64_t *r = ctx->h_units + 4 * u;
+  int64_t m = r[0];
+  const int64_t status = r[1];
+  const uint32_t flag = (uint32_t)r[2];
+  HIPCHK(ctx, hipStreamWaitEvent(st, S.ev[u], 0));   // (the main stream's work on this set comes after its tail)
+  if (status != 0 || flag != 0) {   // rare exact fix-up, as in sample_tail
+    if (S.rng_mode == MH_RNG_MITTY && status != 0) {
+      hipLaunchKernelGGL(k_shuffle_decode, dim3(1), dim3(SD_THREADS), 0, st, q.s_shuf, q.n, S.jall + q.j_off);
+      HIPCHK(ctx, hipGetLastError());
+    }
+    MH_TRY(ensure(ctx, ctx->s[12], 8 * (size_t)S.nn));
+    HIPCHK(ctx, hipMemsetAsync(S.d_flags + u, 0, 4, st));
+    MH_TRY(finish_unit(ctx, q, S.words, S.jall + q.j_off, S.p, S.rlen, S.d_cum, S.n_tlen, S.rng_mode, flag != 0,
+                       S.d_m + u, S.d_flags + u));
+    HIPCHK(ctx, hipMemcpyAsync(&m, S.d_m + u, 8, hipMemcpyDeviceToHost, st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+    ctx->fixups++;
+  }
+  ts.n = m;
+  ts.rlen = S.rlen;
+  ts.valid = true;
+  if (--S.n_pending == 0) ctx->tail_state.reset();
+  return MH_OK;
+}
+
+int32_t tpl_resolve_all(mh_ctx *ctx) {
+  auto Sp = std::static_pointer_cast<SampleState>(ctx->tail_state);
+  if (!Sp) return MH_OK;
+  for (UnitPlan &q : Sp->plan)
+    if (q.out && q.out->pend >= 0) MH_TRY(tpl_resolve(ctx, *q.out));
+  return MH_OK;
+}
+
+int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
+                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
+                           int32_t n_tlen, int32_t rng_mode) {
+  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
+  if (!ctx->h_units) {
+    if (hipHostMalloc((void **)&ctx->h_units, 32 * (size_t)PK_UNITS, hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess) {
+      ctx->h_units = nullptr;
+      return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+    }
+    void *d = nullptr;
+    HIPCHK(ctx, hipHostGetDevicePointer(&d, ctx->h_units, 0));
+    ctx->d_units = (int64_t *)d;
+  }
+  auto S = std::make_shared<SampleState>();
+  MH_TRY(sample_head(ctx, *S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
+  // the per-unit path (Philox, oversized batches) and a one-unit batch (no second lane) end as sample_units does
+  if (!S->batch || !S->two_lanes) return sample_tail(ctx, *S, nullptr);
+  return sample_tail_async(ctx, S);
 }
 
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,

@@ -93,15 +93,18 @@ class Engine:
     # batch's FASTQ writers (still queued on their own stream) to finish reading theirs
     base = self._tpl_base
     self._tpl_base = self.TPL_BATCH - base
-    ns = self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
-                               RNG_MODES[rng])
+    # the units' last sampling stages run on without a host wait; each unit's template set is resolved when its
+    # emission first uses it (unit 0's writer does not wait for the whole batch's tail)
+    self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
+                                cum_tlen, RNG_MODES[rng])
     if lazy and on_unit is None:
-      tickets = []
+      tickets, ns = [], []
       for k, (ps, ri, cpy, seed) in enumerate(units):
         self.ctx.use_templates(base + k)
+        ns.append(self.ctx.template_count(base + k))
         tickets.append(self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
                                            self._regions[ri][0], cpy, write_fastq2, unit_key=seed))
-      return PendingUnits(self.ctx, [int(x) for x in ns], tickets)
+      return PendingUnits(self.ctx, ns, tickets)
     out = []
     # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
     # stream): the writers drain while the caller moves on to the next batch
@@ -115,9 +118,10 @@ class Engine:
         self.ctx.use_templates(base + k)
         kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
                                            self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
-        out.append((int(ns[k]), kept, b1, b2))
+        n = self.ctx.template_count(base + k)
+        out.append((n, kept, b1, b2))
         if on_unit is not None:
-          on_unit(ps, int(ns[k]), kept, b1, b2)
+          on_unit(ps, n, kept, b1, b2)
     return out
 
   def run_batches_lookahead(self, batches, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,

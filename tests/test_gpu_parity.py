@@ -415,6 +415,46 @@ def test_batched_units_vs_oracle(native, monkeypatch, sort):
   assert fix <= 1
 
 
+def test_async_tail_equals_sync_templates(native):
+  """mh_sample_units_async: the units' tails queued on the second stream and resolved one by one, in any order (a
+  count, an export — any non-emission entry point resolves every pending set — or the next batch's sampling), give
+  the same template sets as mh_sample_units."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 30.0)
+  L = 6_000_000
+  seq = synth.contig(L, 31)
+  copies = synth.copies_soa(synth.variants(seq, 32))
+  units = [(0, c, 4100 + k) for k, c in enumerate([0, 1, 0, 1, 1])]
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('3', 0, L), seq)
+    eng.haplotypes([(0, 0), (0, 1)])
+    slots = [eng.haplotype(0, c, copies[c])[0] for _, c, _ in units]
+    seeds = [sd for _, _, sd in units]
+    ns = eng.ctx.sample_units(list(range(5)), slots, seeds, p, 150, mdl['cum_tlen'])
+    want = [eng.ctx.templates_export(i) for i in range(5)]
+    assert min(ns) > 1000
+    for rep in range(2):
+      eng.ctx.sample_units_async(list(range(10, 15)), slots, seeds, p, 150, mdl['cum_tlen'])
+      if rep == 0:
+        for i in (2, 0, 4):   # out of order, one at a time
+          assert eng.ctx.template_count(10 + i) == ns[i]
+        got = [eng.ctx.templates_export(10 + i) for i in range(5)]   # (resolves 1 and 3 too)
+      else:   # nothing resolved before the next batch's sampling: its start resolves them
+        eng.ctx.sample_units_async(list(range(20, 25)), slots, seeds, p, 150, mdl['cum_tlen'])
+        got = [eng.ctx.templates_export(10 + i) for i in range(5)] + \
+              [eng.ctx.templates_export(20 + i) for i in range(5)]
+      for k, g in enumerate(got):
+        w = want[k % 5]
+        assert len(g[0]) == ns[k % 5]
+        for a, b in zip(g, w):
+          assert np.array_equal(a, b), (rep, k)
+  finally:
+    eng.close()
+
+
 def test_resident_variants_and_buffer_reuse(native):
   """Haplotypes spliced from resident variant sets (mh_upload_variants) equal the host-array path, and rebuilding
   after a drop (the released buffers are reused, holding another copy's bytes) gives the same nodes, bytes and
