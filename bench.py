@@ -111,6 +111,9 @@ def parse():
                        'before batch k\'s writers, which wait for that sort (MH_WRITER_GATE=0); phased = sample every '
                        'unit of the step, then emit every unit (phased-sync: and the step starts after the previous '
                        'step\'s writers)')
+  ap.add_argument('--sync-tail', action='store_true',
+                  help='wgs batch pipeline: the host waits for each batch\'s whole sampling (mh_sample_units) instead '
+                       'of resolving its units one by one (mh_sample_units_async)')
   ap.add_argument('--emit-chunk-bytes', type=float, default=24e9,
                   help='wgs phased: FASTQ arenas recycled after about this many bytes')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
@@ -546,6 +549,7 @@ def run_genome(a, rank, world, local):
   if a.pipeline == 'lookahead':
     os.environ.setdefault('MH_WRITER_GATE', '0')   # read when the library context is created
   eng = Engine(local)
+  eng.async_tail = not a.sync_tail
   copies = {}
   for ri in regions:
     name, length = contigs[ri]

@@ -18,6 +18,7 @@ class Engine:
   SLOTS_PER_REGION = 64
   EMIT_SETS = 4   # units prepared ahead of their writers (of the library's 16 emission buffer sets)
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
+  async_tail = True     # run_units: mh_sample_units_async (False: mh_sample_units, the host waits for the batch)
 
   def __init__(self, device=0):
     self.ctx = _native.Context(device)
@@ -95,8 +96,12 @@ class Engine:
     self._tpl_base = self.TPL_BATCH - base
     # the units' last sampling stages run on without a host wait; each unit's template set is resolved when its
     # emission first uses it (unit 0's writer does not wait for the whole batch's tail)
-    self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
-                                cum_tlen, RNG_MODES[rng])
+    if self.async_tail:
+      self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
+                                  cum_tlen, RNG_MODES[rng])
+    else:
+      self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
+                            RNG_MODES[rng])
     if lazy and on_unit is None:
       tickets, ns = [], []
       for k, (ps, ri, cpy, seed) in enumerate(units):
