@@ -17,6 +17,9 @@ rc=$?; echo "verify rc=$rc"; tail -2 $O/verify.err; [ $rc -eq 0 ] || exit $rc
 python3 -c "import json; d=json.load(open('$O/verify.json')); print('verify', d['verify'])"
 timeout -k 10 120 ./scripts/calib_writer > $O/calib_writer.json || exit $?
 cat $O/calib_writer.json
+timeout -k 10 120 python3 scripts/calib_d2h.py > $O/calib_d2h.json || exit $?
+HSA_ENABLE_SDMA=0 timeout -k 10 120 python3 scripts/calib_d2h.py >> $O/calib_d2h.json || exit $?
+cat $O/calib_d2h.json
 TAG=r04c REPS=1 bash scripts/gpu_ab.sh 'base:' 'synctail: -- --sync-tail' 'fwd:MH_HAP_FWD=1' 'tail4:MH_WRITER_GATE_TAIL=4' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'flatfwd:MH_EW_FLAT=1 MH_HAP_FWD=1' 'g4:MH_EW_GATHER4=1' 'g4flat:MH_EW_GATHER4=1 MH_EW_FLAT=1' 'lsd:MH_SORT=lsd' 'lsdtail4:MH_SORT=lsd MH_WRITER_GATE_TAIL=4' 'base2:' || exit $?
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
