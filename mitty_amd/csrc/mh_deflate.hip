@@ -7,9 +7,10 @@
 // matches inside the slice): wave w < 7 ends its block with an empty stored block (a sync flush, 5 bytes) so the
 // next slice's bits start on a byte boundary, and the slices' bytes simply concatenate; wave 7's block is final.
 //   parse   greedy LZ77 over the slice, 64 positions per step: every lane looks up its position (a 2^11-entry hash of
-//           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1); the
-//           first lane with a MIN_MATCH-byte match ends the step's literals, its match is extended by the whole wave
-//           (up to 258 bytes), then the positions passed are hashed in;
+//           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1) and
+//           extends its match up to 32 bytes; a walk over the lanes takes every match the step's positions start
+//           (literals between them; a match of 32+ bytes is extended by the whole wave, up to 258, and ends the
+//           step), then the positions passed are hashed in;
 //   pass 1  the parse, counting symbol frequencies;
 //   codes   lane 0: length-limited Huffman lengths (15 bits; 7 for the code-length code), canonical codes, the
 //           dynamic header (mh_deflate.h, host-testable);
@@ -127,11 +128,19 @@ __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, 
   __builtin_amdgcn_wave_barrier();
 }
 
-// One step of the parse at `cur` (wave-uniform): returns the next position; sets the number of literals `nlit`
-// (positions cur .. cur + nlit - 1) and, when has_match, the match (mlen, mdist) at cur + nlit.
+// One step of the parse at `cur` (wave-uniform): every lane looks for a match at its position (cand: an earlier
+// position), extends it by itself up to LX bytes, and a greedy walk over the lanes (wave-uniform, one iteration per
+// match) picks the tokens: literals up to the next lane with a match, that match, and on after its end — so a step
+// takes every match that starts in its 64 positions, not only the first (records with many short matches, e.g.
+// BAM, took one step per match).  A match that reached LX is extended by the whole wave (64 bytes per round, up to
+// MAX_MATCH) and ends the step.  Per lane: lit (a literal token at this position), ms (a match starts here: mlen,
+// mdist).  The later lanes' candidates were looked up before this step's earlier positions were hashed in: the
+// tokens differ from a position-by-position greedy parse, never in validity (every match is verified).
+constexpr int LX = 32;
 struct Step {
-  int next, nlit, mlen, mdist;
-  bool has_match;
+  int next;                // the position after the step's last token
+  uint64_t lit, ms;        // lanes holding a literal / starting a match
+  int mlen, mdist;         // this lane's match (ms lanes)
 };
 
 __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane) {
@@ -146,35 +155,63 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
       if (j >= 0 && match7(s, p, w, j)) cand = j;
     }
   }
-  const uint64_t bal = __ballot(cand >= 0);
+  int len = 0;
+  bool capped = false;
+  if (cand >= 0) {   // the lane's own extension, four bytes at a time, up to LX (or the end of the slice)
+    const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH;
+    const int lim = cap < LX ? cap : LX;
+    len = MIN_MATCH;
+    while (len < lim) {
+      const uint32_t x = load4(s, p + len) ^ load4(s, cand + len);
+      if (x) {
+        len += (int)(__builtin_ctz(x) >> 3);
+        break;
+      }
+      len += 4;
+    }
+    if (len > lim) len = lim;
+    capped = len == LX && lim < cap;
+  }
+  const uint64_t M = __ballot(cand >= 0), C = __ballot(capped);
+  const int W = S - cur < 64 ? S - cur : 64;
   Step st;
-  const int lim = S - cur < 64 ? S - cur : 64;
-  if (bal == 0) {
-    st.nlit = lim;
-    st.has_match = false;
-    st.mlen = st.mdist = 0;
-    st.next = cur + lim;
-    return st;
+  st.lit = st.ms = 0;
+  int x = 0;
+  for (;;) {   // wave-uniform greedy walk: x = the lane of the next token
+    const uint64_t rest = x < 64 ? M & (~0ull << x) : 0ull;
+    const int m = rest ? __builtin_ctzll(rest) : 64;
+    const int me = m < W ? m : W;
+    if (me > x) st.lit |= (me - x >= 64 ? ~0ull : ((1ull << (me - x)) - 1ull)) << x;
+    if (m >= W) {
+      st.next = cur + W;
+      break;
+    }
+    st.ms |= 1ull << m;
+    int L = __builtin_amdgcn_readlane(len, m);
+    if ((C >> m) & 1ull) {   // a long match: the whole wave extends it, and the step ends with it
+      const int q = cur + m, j = __builtin_amdgcn_readlane(cand, m);
+      const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
+      for (;;) {
+        const int k = L + lane;
+        const bool eq = k < cap && s[q + k] == s[j + k];
+        const uint64_t ne = ~__ballot(eq);
+        const int run = ne ? __builtin_ctzll(ne) : 64;
+        L += run;
+        if (run < 64 || L >= cap) break;
+      }
+      if (L > cap) L = cap;
+      if (lane == m) len = L;
+      st.next = q + L;
+      break;
+    }
+    x = m + L;
+    if (x >= W) {
+      st.next = cur + x;
+      break;
+    }
   }
-  const int f = __builtin_ctzll(bal);
-  const int q = cur + f;
-  const int j = __shfl(cand, f, 64);
-  const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
-  int len = MIN_MATCH;
-  for (;;) {   // the whole wave extends the match, 64 bytes per round
-    const int k = len + lane;
-    const bool eq = k < cap && s[q + k] == s[j + k];
-    const uint64_t ne = ~__ballot(eq);
-    const int run = ne ? __builtin_ctzll(ne) : 64;
-    len += run;
-    if (run < 64 || len >= cap) break;
-  }
-  if (len > cap) len = cap;
-  st.nlit = f;
-  st.has_match = true;
   st.mlen = len;
-  st.mdist = q - j;
-  st.next = q + len;
+  st.mdist = p - cand;
   return st;
 }
 
@@ -187,12 +224,12 @@ __device__ __forceinline__ void hash_in(const uint8_t *s, int S, int a, int b, u
   __builtin_amdgcn_wave_barrier();
 }
 
-// the symbols of one step, pass 1: literal frequencies (LDS atomics, one per literal lane) and the match's
+// the symbols of one step, pass 1: literal and match frequencies (LDS atomics, one per token lane)
 __device__ __forceinline__ void count_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, int lane) {
-  if (lane < st.nlit) atomicAdd(&W.lf[s[cur + lane]], 1u);
-  if (st.has_match && lane == 0) {
-    W.lf[257 + len_code(st.mlen)]++;
-    W.dfq[dist_code(st.mdist)]++;
+  if ((st.lit >> lane) & 1ull) atomicAdd(&W.lf[s[cur + lane]], 1u);
+  if ((st.ms >> lane) & 1ull) {
+    atomicAdd(&W.lf[257 + len_code(st.mlen)], 1u);
+    atomicAdd(&W.dfq[dist_code(st.mdist)], 1u);
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
@@ -238,34 +275,29 @@ __device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t 
   bw.bitpos = end;
 }
 
-// the codes of one step, pass 2
+// the codes of one step, pass 2: every token lane's code (a literal's, or a match's length and distance codes with
+// their extra bits: <= 48 bits), placed in lane order = position order
 __device__ __forceinline__ void encode_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, BitWave &bw,
                                             int lane) {
   uint64_t v = 0;
   int n = 0;
-  if (lane < st.nlit) {
+  if ((st.lit >> lane) & 1ull) {
     const uint32_t c = s[cur + lane];
     v = W.lcode[c];
     n = W.llen[c];
+  } else if ((st.ms >> lane) & 1ull) {
+    const int lc = len_code(st.mlen), dc = dist_code(st.mdist);
+    const int le = len_extra(lc), de = dist_extra(dc);
+    v = W.lcode[257 + lc];
+    n = W.llen[257 + lc];
+    v |= (uint64_t)(st.mlen - len_base(lc)) << n;
+    n += le;
+    v |= (uint64_t)W.dcode[dc] << n;
+    n += W.dlen[dc];
+    v |= (uint64_t)(st.mdist - dist_base(dc)) << n;
+    n += de;
   }
   put_bits(bw, W.stage, v, n, lane);
-  if (st.has_match) {
-    v = 0;
-    n = 0;
-    if (lane == 0) {
-      const int lc = len_code(st.mlen), dc = dist_code(st.mdist);
-      const int le = len_extra(lc), de = dist_extra(dc);
-      v = W.lcode[257 + lc];
-      n = W.llen[257 + lc];
-      v |= (uint64_t)(st.mlen - len_base(lc)) << n;
-      n += le;
-      v |= (uint64_t)W.dcode[dc] << n;
-      n += W.dlen[dc];
-      v |= (uint64_t)(st.mdist - dist_base(dc)) << n;
-      n += de;
-    }
-    put_bits(bw, W.stage, v, n, lane);
-  }
 }
 
 __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, int64_t n_in, int64_t b0, int64_t nb,

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4, second call: the full-size WGS step byte-checked unit by unit (bench --verify), the remaining writer /
+# gate / sort arms, and the tumor/normal + BAM line (device deflate of BAM records).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04d
+mkdir -p $O
+timeout -k 10 700 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --verify > $O/verify.json 2> $O/verify.err
+rc=$?; echo "verify rc=$rc"; tail -2 $O/verify.err; [ $rc -eq 0 ] || exit $rc
+python3 -c "import json; d=json.load(open('$O/verify.json')); print('verify', d['verify'])"
+timeout -k 10 300 python -u bench.py --tumor-normal > $O/tn.json 2> $O/tn.err || exit $?
+python3 -c "import json; d=json.load(open('$O/tn.json')); print('tn', d['value'], d['ms_per_step'], d['bam_file_gpu'], d['with_bam_file']['value'])" || true
+TAG=r04d REPS=1 bash scripts/gpu_ab.sh 'base:' 'tail4:MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'g4:MH_EW_GATHER4=1' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'base2:' || exit $?
+echo done
