@@ -165,10 +165,9 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
   return ok;
 }
 
-bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
-               const std::vector<int64_t> &coff, std::string &err) {
-  std::string s("BAI\1", 4);
-  put32(s, (uint32_t)n_refs);
+bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPlan &plan, std::string &err) {
+  plan.refs.assign((size_t)std::max(n_refs, 0), BaiRef{});
+  if (threads < 1) threads = 1;
   int64_t i = 0;
   for (int32_t tid = 0; tid < n_refs; tid++) {
     if (i < n && recs[i].tid < tid) {
@@ -176,67 +175,126 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
       return false;
     }
     int64_t j = i;
-    while (j < n && recs[j].tid == tid) j++;
-    if (j == i) {   // no records on this reference
-      put32(s, 0);
-      put32(s, 0);
-      continue;
+    {   // the reference's records: a binary search (records are sorted by tid)
+      int64_t lo = i, hi = n;
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (recs[mid].tid <= tid) lo = mid + 1; else hi = mid;
+      }
+      j = lo;
     }
-    // bins: runs of consecutive records with the same bin form one chunk; adjacent chunks of a bin merge.  Indexed by
-    // bin number (at most 37449, SAM spec §5.3), written in ascending order (a std::map per record cost ~4x more)
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> bins(37450);
-    std::vector<uint64_t> lin;
-    for (int64_t k = i; k < j; k++) {
-      const uint64_t vb = voffset(coff, soff[k]), ve = voffset(coff, soff[k + 1]);
-      if (recs[k].bin >= 37450u) {
-        err = "BAI: bin number out of range";
+    BaiRef &R = plan.refs[tid];
+    R.i = i;
+    R.j = j;
+    if (j == i) continue;
+    // pieces of the record range on threads: each its runs (record order) and its linear index (first record per
+    // window); the pieces are then joined in order
+    const int64_t nr = j - i;
+    const int T = (int)std::min<int64_t>(threads, std::max<int64_t>(1, nr / 65536));
+    std::vector<std::vector<BaiRun>> runs(T);
+    std::vector<std::vector<int64_t>> lins(T);
+    std::vector<char> bad(T, 0);
+    auto work = [&](int t) {
+      const int64_t a = i + nr * t / T, b = i + nr * (t + 1) / T;
+      auto &rr = runs[t];
+      auto &lin = lins[t];
+      for (int64_t k = a; k < b; k++) {
+        const BaiRec &r = recs[k];
+        if (r.tid != tid || r.beg < 0) {   // (the binary search above assumed sorted records)
+          bad[t] = 2;
+          return;
+        }
+        if (r.bin >= 37450u) {
+          bad[t] = 1;
+          return;
+        }
+        if (!rr.empty() && rr.back().bin == r.bin && rr.back().ke == k)
+          rr.back().ke = k + 1;
+        else
+          rr.push_back(BaiRun{r.bin, k, k + 1});
+        const int64_t w0 = r.beg >> 14, w1 = (int64_t)(r.end - 1) >> 14;
+        if ((int64_t)lin.size() <= w1) lin.resize(w1 + 1, -1);
+        for (int64_t w = w0; w <= w1; w++)
+          if (lin[w] < 0) lin[w] = k;
+      }
+    };
+    if (T == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> pool;
+      for (int t = 0; t < T; t++) pool.emplace_back(work, t);
+      for (auto &th : pool) th.join();
+    }
+    for (int t = 0; t < T; t++)
+      if (bad[t]) {
+        err = bad[t] == 1 ? "BAI: bin number out of range" : "BAI: records not coordinate-sorted";
         return false;
       }
-      auto &ch = bins[recs[k].bin];
-      if (!ch.empty() && ch.back().second == vb)
-        ch.back().second = ve;
-      else
-        ch.emplace_back(vb, ve);
-      const int64_t w0 = recs[k].beg >> 14, w1 = (recs[k].end - 1) >> 14;
-      if ((int64_t)lin.size() <= w1) lin.resize(w1 + 1, UINT64_MAX);
-      for (int64_t w = w0; w <= w1; w++)
-        if (lin[w] == UINT64_MAX) lin[w] = vb;
-    }
-    uint32_t n_bins = 0;
-    for (const auto &ch : bins) n_bins += ch.empty() ? 0u : 1u;
-    put32(s, n_bins + 1);
-    for (uint32_t b = 0; b < (uint32_t)bins.size(); b++) {
-      if (bins[b].empty()) continue;
-      put32(s, b);
-      put32(s, (uint32_t)bins[b].size());
-      for (auto &c : bins[b]) {
-        put64(s, c.first);
-        put64(s, c.second);
+    std::vector<BaiRun> all;
+    for (int t = 0; t < T; t++)
+      for (const BaiRun &r : runs[t]) {
+        if (!all.empty() && all.back().bin == r.bin && all.back().ke == r.kb)
+          all.back().ke = r.ke;   // a run cut by the pieces
+        else
+          all.push_back(r);
       }
-    }
-    // pseudo-bin 37450: (first record, end of last record), (mapped, unmapped)
-    put32(s, 37450);
-    put32(s, 2);
-    put64(s, voffset(coff, soff[i]));
-    put64(s, voffset(coff, soff[j]));
-    put64(s, (uint64_t)(j - i));
-    put64(s, 0);
-    // linear index: windows with no overlapping record take the next window's offset (the last one set so far
-    // going backwards), i.e. the first record that can overlap anything at or after them
-    uint64_t next = voffset(coff, soff[j]);
-    for (int64_t w = (int64_t)lin.size() - 1; w >= 0; w--) {
-      if (lin[w] == UINT64_MAX)
-        lin[w] = next;
-      else
-        next = lin[w];
-    }
-    put32(s, (uint32_t)lin.size());
-    for (uint64_t v : lin) put64(s, v);
+    std::stable_sort(all.begin(), all.end(), [](const BaiRun &x, const BaiRun &y) { return x.bin < y.bin; });
+    R.runs = std::move(all);
+    size_t nw = 0;
+    for (int t = 0; t < T; t++) nw = std::max(nw, lins[t].size());
+    R.lin.assign(nw, -1);
+    for (int t = 0; t < T; t++)   // the earliest piece that set a window holds its first record
+      for (size_t w = 0; w < lins[t].size(); w++)
+        if (R.lin[w] < 0 && lins[t][w] >= 0) R.lin[w] = lins[t][w];
     i = j;
   }
   if (i != n) {
     err = "BAI: record tid outside the header's references";
     return false;
+  }
+  return true;
+}
+
+bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *soff, const std::vector<int64_t> &coff,
+              std::string &err) {
+  std::string s("BAI\1", 4);
+  put32(s, (uint32_t)plan.refs.size());
+  for (const BaiRef &R : plan.refs) {
+    if (R.j == R.i) {   // no records on this reference
+      put32(s, 0);
+      put32(s, 0);
+      continue;
+    }
+    uint32_t n_bins = 0;
+    for (size_t r = 0; r < R.runs.size(); r++) n_bins += (r == 0 || R.runs[r].bin != R.runs[r - 1].bin) ? 1u : 0u;
+    put32(s, n_bins + 1);
+    for (size_t r = 0; r < R.runs.size();) {
+      size_t e = r;
+      while (e < R.runs.size() && R.runs[e].bin == R.runs[r].bin) e++;
+      put32(s, R.runs[r].bin);
+      put32(s, (uint32_t)(e - r));
+      for (; r < e; r++) {
+        put64(s, voffset(coff, soff[R.runs[r].kb]));
+        put64(s, voffset(coff, soff[R.runs[r].ke]));
+      }
+    }
+    // pseudo-bin 37450: (first record, end of last record), (mapped, unmapped)
+    put32(s, 37450);
+    put32(s, 2);
+    put64(s, voffset(coff, soff[R.i]));
+    put64(s, voffset(coff, soff[R.j]));
+    put64(s, (uint64_t)(R.j - R.i));
+    put64(s, 0);
+    // linear index: windows with no overlapping record take the next window's offset (the last one set so far
+    // going backwards), i.e. the first record that can overlap anything at or after them
+    std::vector<uint64_t> lin(R.lin.size());
+    uint64_t next = voffset(coff, soff[R.j]);
+    for (int64_t w = (int64_t)lin.size() - 1; w >= 0; w--) {
+      if (R.lin[w] >= 0) next = voffset(coff, soff[R.lin[w]]);
+      lin[w] = next;
+    }
+    put32(s, (uint32_t)lin.size());
+    for (uint64_t v : lin) put64(s, v);
   }
   put64(s, 0);   // n_no_coor
   FILE *fp = fopen(path, "wb");
@@ -248,6 +306,13 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
   ok = (fclose(fp) == 0) && ok;
   if (!ok) err = std::string("BAI write failed: ") + path;
   return ok;
+}
+
+bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
+               const std::vector<int64_t> &coff, std::string &err) {
+  BaiPlan plan;
+  const int threads = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  return bai_plan(n_refs, n, recs, threads, plan, err) && bai_emit(path, plan, soff, coff, err);
 }
 
 }  // namespace mh

@@ -40,6 +40,25 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
 bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
                const std::vector<int64_t> &rec_block_coff, std::string &err);
 
+// The BAI in two halves, so the per-record half runs before the blocks' file offsets are known (beside the device
+// deflate): bai_plan, on `threads` threads, finds per reference the chunks (runs of consecutive records in one bin)
+// and the linear index as record indices; bai_emit maps them to virtual offsets and writes the file.
+struct BaiRun {
+  uint32_t bin;
+  int64_t kb, ke;   // records [kb, ke)
+};
+struct BaiRef {
+  int64_t i = 0, j = 0;        // the reference's records [i, j)
+  std::vector<BaiRun> runs;    // by bin, then record order
+  std::vector<int64_t> lin;    // per 16 kbp window: the first record overlapping it, or -1
+};
+struct BaiPlan {
+  std::vector<BaiRef> refs;
+};
+bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPlan &plan, std::string &err);
+bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *soff, const std::vector<int64_t> &rec_block_coff,
+              std::string &err);
+
 // virtual offset of data offset u
 inline uint64_t voffset(const std::vector<int64_t> &coff, int64_t u) {
   const int64_t b = u / BGZF_BLOCK;
