@@ -1,7 +1,9 @@
 // mh_api.hip — the C ABI (include/mitty_hip.h): context, buffers, argument checks, dispatch to the subsystems.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -1289,44 +1291,145 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
   MH_TRY(bam_sort(ctx));
   const int64_t n = B.n_rec;
-  // the sorted records deflated on the device (k_bgzf_blocks), then only the compressed bytes cross PCIe
+  // the BAI's per-record half on the device (chunks and linear windows; only their offsets cross PCIe)
+  BaiPlan plan;
+  std::vector<int64_t> offs;
+  bool dev_plan = false;
+  if (bai_path) MH_TRY(bam_bai_plan(ctx, plan, offs, &dev_plan));
+  // the sorted records deflated on the device (k_bgzf_blocks) piece by piece; a writer thread copies each packed
+  // piece out (stream2, two page-locked 64 MiB slots) and writes it while the next piece deflates
   std::vector<int64_t> boff;
   int64_t nz = 0;
+  struct Piece {
+    int64_t off, len;
+    hipEvent_t ev;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Piece> pieces;
+  bool fin = false;
   // gz_out is sized for the whole BAM (GBs): released on every exit, never kept beside the next job's buffers
-  struct GzRelease {
+  struct Guard {
     mh_ctx *c;
-    uint8_t *pin = nullptr;
-    ~GzRelease() {
-      if (pin) (void)hipHostFree(pin);
+    uint8_t *pin[2] = {nullptr, nullptr};
+    std::vector<Piece> *pc;
+    ~Guard() {
+      for (uint8_t *p : pin)
+        if (p) (void)hipHostFree(p);
+      for (Piece &x : *pc)
+        if (x.ev) (void)hipEventDestroy(x.ev);
       release(c->gz_out);
     }
-  } gz_guard{ctx};
+  } guard{ctx, {nullptr, nullptr}, &pieces};
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
-  MH_TRY(bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
-                     (int64_t)ctx->gz_out.cap, &nz, &boff));
+  const int64_t SLOT_B = (int64_t)1 << 26;
+  for (auto &p : guard.pin) HIPCHK(ctx, hipHostMalloc((void **)&p, (size_t)SLOT_B, hipHostMallocDefault));
   const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
                                            B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
-  // D2H through a page-locked 64 MiB piece (allocated once per call)
-  HIPCHK(ctx, hipHostMalloc((void **)&gz_guard.pin, (size_t)1 << 26, hipHostMallocDefault));
-  uint8_t *const pin = gz_guard.pin;
-  auto fetch = [&](int64_t o, int64_t len) -> const uint8_t * {
-    return hipMemcpy(pin, z + o, (size_t)len, hipMemcpyDeviceToHost) == hipSuccess ? pin : nullptr;
-  };
-  std::vector<int64_t> coff;
+  std::atomic<int> werr{(int)hipSuccess};   // (set by either thread)
   std::string err;
-  const bool wrote = bgzf_write_blocks(bam_path, hdr, 6, nz, boff, fetch, coff, err);
+  bool wrote = false;
+  int64_t data_pos = 0, end_pos = 0;
+  std::thread writer([&]() {
+    (void)hipSetDevice(ctx->device);
+    size_t item = 0;
+    int64_t in_item = 0;
+    // the next sub-piece (<= 64 MiB) of the queued pieces, waiting for the deflate to queue it
+    auto take = [&](int64_t *o, int64_t *m, hipEvent_t *ev) -> bool {
+      std::unique_lock<std::mutex> lk(mu);
+      for (;;) {
+        while (item < pieces.size() && in_item >= pieces[item].len) {
+          item++;
+          in_item = 0;
+        }
+        if (item < pieces.size()) break;
+        if (fin) return false;
+        cv.wait(lk);
+      }
+      const Piece &p = pieces[item];
+      *o = p.off + in_item;
+      *m = std::min(SLOT_B, p.len - in_item);
+      *ev = p.ev;
+      in_item += *m;
+      return true;
+    };
+    auto issue = [&](int s, int64_t *len) -> bool {   // a copy into slot s on stream2, behind its piece's pack
+      int64_t o, m;
+      hipEvent_t ev;
+      if (!take(&o, &m, &ev)) return false;
+      hipError_t e = hipStreamWaitEvent(ctx->stream2, ev, 0);
+      if (e == hipSuccess) e = hipMemcpyAsync(guard.pin[s], z + o, (size_t)m, hipMemcpyDeviceToHost, ctx->stream2);
+      if (e != hipSuccess) {
+        werr = (int)e;
+        return false;
+      }
+      *len = m;
+      return true;
+    };
+    int cur = 0;
+    int64_t len_cur = 0, len_next = 0;
+    bool have = issue(0, &len_cur);
+    auto next = [&](const uint8_t **buf, int64_t *len) -> bool {
+      if (!have || werr.load() != (int)hipSuccess) return false;
+      hipError_t e = hipStreamSynchronize(ctx->stream2);   // slot cur is in (and nothing else is in flight)
+      if (e != hipSuccess) {
+        werr = (int)e;
+        return false;
+      }
+      const int s = cur;
+      *buf = guard.pin[s];
+      *len = len_cur;
+      have = issue(s ^ 1, &len_next);   // the following sub-piece into the other slot, while this one is written
+      len_cur = len_next;
+      cur = s ^ 1;
+      return true;
+    };
+    wrote = bgzf_write_stream(bam_path, hdr, 6, next, &data_pos, &end_pos, err);
+    if (!wrote) {   // drain what is in flight before the slots go
+      (void)hipStreamSynchronize(ctx->stream2);
+    }
+  });
+  const std::function<void(int64_t, int64_t)> on_piece = [&](int64_t off, int64_t bytes) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ev, ctx->stream) != hipSuccess) {
+      if (ev) (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    pieces.push_back(Piece{off, ev ? bytes : 0, ev});
+    if (!ev) werr = (int)hipErrorUnknown;
+    cv.notify_one();
+  };
+  const int32_t rc = bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
+                                 (int64_t)ctx->gz_out.cap, &nz, &boff, &on_piece);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    fin = true;
+    cv.notify_one();
+  }
+  writer.join();
+  if (rc != MH_OK) return rc;
+  if (werr.load() != (int)hipSuccess) return hip_fail(ctx, (hipError_t)werr.load(), "BAM D2H", __FILE__, __LINE__);
   if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
+  if (end_pos - data_pos != nz) return arg_fail(ctx, MH_E_STATE, "BAM: compressed bytes written differ (internal)");
+  std::vector<int64_t> coff(boff.size());
+  for (size_t b = 0; b < boff.size(); b++) coff[b] = data_pos + boff[b];
   if (bai_path) {
-    std::vector<int64_t> soff((size_t)n + 1, 0);
-    std::vector<BaiRec> info((size_t)n + 1);
-    MH_TRY(bam_fetch_sorted(ctx, nullptr, soff.data(), (int32_t *)info.data()));
-    if (!bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
-      return arg_fail(ctx, MH_E_ARG, err);
+    if (dev_plan) {
+      if (!bai_emit(bai_path, plan, offs.data(), coff, err)) return arg_fail(ctx, MH_E_ARG, err);
+    } else {   // outside the device plan's checks: the host plan (and its errors)
+      std::vector<int64_t> soff((size_t)n + 1, 0);
+      std::vector<BaiRec> info((size_t)n + 1);
+      MH_TRY(bam_fetch_sorted(ctx, nullptr, soff.data(), (int32_t *)info.data()));
+      if (!bai_write(bai_path, (int32_t)B.ref_names.size(), n, info.data(), soff.data(), coff, err))
+        return arg_fail(ctx, MH_E_ARG, err);
+    }
   }
   if (out_records) *out_records = n;
   if (out_bytes) *out_bytes = B.bytes;
-  if (out_file_bytes) *out_file_bytes = coff.empty() ? 0 : coff.back() + 28;
+  if (out_file_bytes) *out_file_bytes = end_pos + 28;
   return MH_OK;
 }
 

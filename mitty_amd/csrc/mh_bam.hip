@@ -18,6 +18,9 @@
 // read's tid / pos, TLEN 0, no tags, qname = file 1's read name.  bin = reg2bin(pos, bam_endpos) as htslib sets it.
 #include <rocprim/device/device_radix_sort.hpp>
 
+#include <algorithm>
+
+#include "mh_bgzf.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
 
@@ -785,9 +788,166 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
   return MH_OK;
 }
 
+// ---- the BAI's device plan -----------------------------------------------------------------------------------
+namespace {
+
+// per record: the 16 kbp windows it overlaps take its index unless the record before already overlaps them (that
+// one is earlier: a window's first record wins, with few atomics per window); a reference's window count
+__global__ void k_bai_mark(const RInfo *info, int64_t n, const int64_t *woff, int32_t n_refs, uint32_t *lin,
+                           uint32_t *nwin, int32_t *bad) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const RInfo r = info[k];
+  if (r.tid < 0 || r.tid >= n_refs || r.beg < 0 || r.bin >= 37450u) {
+    atomicOr(bad, 1);
+    return;
+  }
+  const int64_t w0 = r.beg >> 14, w1 = (int64_t)(r.end - 1) >> 14;
+  if (w1 < 0) return;
+  if (w1 >= woff[r.tid + 1] - woff[r.tid]) {
+    atomicOr(bad, 2);
+    return;
+  }
+  int64_t from = w0;
+  if (k > 0) {
+    const RInfo q = info[k - 1];
+    if (q.tid > r.tid || (q.tid == r.tid && q.beg > r.beg)) atomicOr(bad, 4);   // (the store is sorted)
+    if (q.tid == r.tid && q.end - 1 >= q.beg) {
+      const int64_t p0 = q.beg >> 14, p1 = (int64_t)(q.end - 1) >> 14;
+      if (p0 <= w0 && p1 >= w0) from = p1 + 1;   // windows [w0, p1] already have an earlier record
+    }
+  }
+  uint32_t *L = lin + woff[r.tid];
+  for (int64_t w = from; w <= w1; w++) atomicMin(&L[w], (uint32_t)k);
+  atomicMax(&nwin[r.tid], (uint32_t)(w1 + 1));
+}
+
+__device__ __forceinline__ bool run_start(const RInfo *info, int64_t k) {
+  return k == 0 || info[k - 1].tid != info[k].tid || info[k - 1].bin != info[k].bin;
+}
+struct LoadRunStart {
+  const RInfo *info;
+  int64_t n;
+  __device__ int64_t operator()(int64_t k) const { return k < n && run_start(info, k) ? 1 : 0; }
+};
+struct StoreRunStart {
+  uint32_t *runs;
+  __device__ void operator()(int64_t k, int64_t incl, int64_t ex) const {
+    if (incl != ex) runs[ex] = (uint32_t)k;
+  }
+};
+
+// the plan's offsets: per run (tid << 32 | bin, offset of its first record, offset of its end, records), then per
+// window the offset of its first record (-1: none)
+__global__ void k_bai_gather(const RInfo *info, const int64_t *soff, const uint32_t *runs, int64_t n_runs, int64_t n,
+                             const uint32_t *lin, int64_t n_win, int64_t *out_runs, int64_t *out_win) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_runs) {
+    const int64_t kb = runs[i], ke = i + 1 < n_runs ? (int64_t)runs[i + 1] : n;
+    const RInfo r = info[kb];
+    out_runs[4 * i] = ((int64_t)r.tid << 32) | (int64_t)r.bin;
+    out_runs[4 * i + 1] = soff[kb];
+    out_runs[4 * i + 2] = soff[ke];
+    out_runs[4 * i + 3] = ke - kb;
+  }
+  if (i < n_win) out_win[i] = lin[i] == 0xffffffffu ? -1 : soff[lin[i]];
+}
+
+}  // namespace
+
+int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, bool *ok) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  *ok = false;
+  const int64_t n = B.n_rec;
+  const int32_t n_refs = (int32_t)B.ref_names.size();
+  plan.refs.assign((size_t)n_refs, BaiRef{});
+  offs.clear();
+  if (n == 0) {
+    *ok = true;
+    return MH_OK;
+  }
+  if (!B.sorted) return arg_fail(ctx, MH_E_STATE, "BAI plan of an unsorted store (internal)");
+  std::vector<int64_t> woff((size_t)n_refs + 1, 0);
+  for (int32_t t = 0; t < n_refs; t++) woff[t + 1] = woff[t] + (B.ref_len[t] >> 14) + 1;
+  const int64_t n_win = woff[n_refs];
+  MH_TRY(ensure(ctx, B.bai_lin, 4 * (size_t)n_win + 4 * (size_t)n_refs + 8 * (size_t)(n_refs + 1) + 64));
+  uint32_t *lin = (uint32_t *)B.bai_lin.p, *nwin = lin + n_win;
+  int64_t *d_woff = (int64_t *)(((uintptr_t)(nwin + n_refs) + 7) & ~(uintptr_t)7);
+  MH_TRY(ensure(ctx, B.bai_runs, 4 * (size_t)n + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 72);
+  int64_t *total = (int64_t *)((char *)ctx->d_small.p + 80);
+  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(n)));
+  int64_t *hs = pinned_small(ctx);
+  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  stage_begin(ctx, "bam_bai_plan");
+  HIPCHK(ctx, hipMemsetAsync(lin, 0xff, 4 * (size_t)n_win, st));
+  HIPCHK(ctx, hipMemsetAsync(nwin, 0, 4 * (size_t)n_refs, st));
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_woff, woff.data(), 8 * woff.size(), hipMemcpyHostToDevice, st));
+  const RInfo *info = (const RInfo *)B.sinfo.p;
+  hipLaunchKernelGGL(k_bai_mark, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, info, n,
+                     (const int64_t *)d_woff, n_refs, lin, nwin, bad);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadRunStart{info, n}, StoreRunStart{(uint32_t *)B.bai_runs.p},
+                                       ctx->scan_partials.p, total));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 28, total, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 29, bad, 4, hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  const int64_t n_runs = hs[28];
+  const int32_t f = (int32_t)(hs[29] & 0xffffffff);
+  if (f) {   // outside the device plan's checks: the host plans (and reports what it finds)
+    stage_end(ctx);
+    return MH_OK;
+  }
+  MH_TRY(ensure(ctx, B.bai_out, 8 * (size_t)(4 * n_runs + n_win) + 64));
+  int64_t *out_runs = (int64_t *)B.bai_out.p, *out_win = out_runs + 4 * n_runs;
+  const int64_t m = n_runs > n_win ? n_runs : n_win;
+  hipLaunchKernelGGL(k_bai_gather, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, info,
+                     (const int64_t *)B.soff.p, (const uint32_t *)B.bai_runs.p, n_runs, n, (const uint32_t *)lin, n_win,
+                     out_runs, out_win);
+  HIPCHK(ctx, hipGetLastError());
+  std::vector<int64_t> hr(4 * (size_t)n_runs), hw((size_t)n_win);
+  std::vector<uint32_t> hn((size_t)n_refs);
+  HIPCHK(ctx, hipMemcpyAsync(hr.data(), out_runs, 8 * hr.size(), hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hw.data(), out_win, 8 * hw.size(), hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hn.data(), nwin, 4 * hn.size(), hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  stage_end(ctx);
+  // offs: the runs' (first, end) offsets, then the windows'
+  offs.resize(2 * (size_t)n_runs + (size_t)n_win);
+  for (int64_t r = 0; r < n_runs; r++) {
+    offs[2 * r] = hr[4 * r + 1];
+    offs[2 * r + 1] = hr[4 * r + 2];
+  }
+  for (int64_t w = 0; w < n_win; w++) offs[2 * n_runs + w] = hw[w];
+  for (int64_t r0 = 0; r0 < n_runs;) {   // the runs of one reference are consecutive (the store is sorted)
+    const int32_t t = (int32_t)(hr[4 * r0] >> 32);
+    int64_t r1 = r0;
+    BaiRef &R = plan.refs[t];
+    if (R.n != 0) return MH_OK;   // (a reference's runs apart: not sorted — the host plan reports it)
+    while (r1 < n_runs && (int32_t)(hr[4 * r1] >> 32) == t) {
+      R.n += hr[4 * r1 + 3];
+      R.runs.push_back(BaiRun{(uint32_t)(hr[4 * r1] & 0xffffffff), 2 * r1, 2 * r1 + 1});
+      r1++;
+    }
+    R.vi = 2 * r0;
+    R.vj = 2 * (r1 - 1) + 1;
+    std::stable_sort(R.runs.begin(), R.runs.end(), [](const BaiRun &x, const BaiRun &y) { return x.bin < y.bin; });
+    R.lin.assign(hn[t], -1);
+    for (uint32_t w = 0; w < hn[t]; w++)
+      if (hw[woff[t] + w] >= 0) R.lin[w] = 2 * n_runs + woff[t] + w;
+    r0 = r1;
+  }
+  *ok = true;
+  return MH_OK;
+}
+
 void bam_release(BamStore &B) {
   for (DevBuf *b : {&B.names, &B.name_off, &B.nl1, &B.nl2, &B.tpl, &B.roff, &B.recs, &B.key, &B.val, &B.info,
-                    &B.key2, &B.val2, &B.sort_tmp, &B.soff, &B.srecs, &B.sinfo, &B.in1, &B.in2})
+                    &B.key2, &B.val2, &B.sort_tmp, &B.soff, &B.srecs, &B.sinfo, &B.in1, &B.in2, &B.bai_lin,
+                    &B.bai_runs, &B.bai_out})
     release(*b);
   B.n_rec = B.bytes = 0;
   B.n_files = 0;

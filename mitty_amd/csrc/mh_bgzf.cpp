@@ -165,6 +165,37 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
   return ok;
 }
 
+bool bgzf_write_stream(const char *path, const std::string &header, int level,
+                       const std::function<bool(const uint8_t **, int64_t *)> &next, int64_t *data_pos,
+                       int64_t *end_pos, std::string &err) {
+  FILE *fp = fopen(path, "wb");
+  if (!fp) {
+    err = std::string("cannot open ") + path;
+    return false;
+  }
+  int64_t pos = 0;
+  bool ok = true;
+  std::string blk;
+  for (size_t h = 0; h < header.size() && ok; h += BGZF_BLOCK) {
+    const int64_t m = std::min<int64_t>(BGZF_BLOCK, (int64_t)(header.size() - h));
+    ok = bgzf_block((const uint8_t *)header.data() + h, m, level, blk) && fwrite(blk.data(), 1, blk.size(), fp) ==
+         blk.size();
+    pos += (int64_t)blk.size();
+  }
+  *data_pos = pos;
+  const uint8_t *buf = nullptr;
+  int64_t len = 0;
+  while (ok && next(&buf, &len)) {
+    ok = fwrite(buf, 1, (size_t)len, fp) == (size_t)len;
+    pos += len;
+  }
+  *end_pos = pos;
+  ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
+  ok = (fclose(fp) == 0) && ok;
+  if (!ok && err.empty()) err = std::string("BGZF write failed: ") + path;
+  return ok;
+}
+
 bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPlan &plan, std::string &err) {
   plan.refs.assign((size_t)std::max(n_refs, 0), BaiRef{});
   if (threads < 1) threads = 1;
@@ -184,8 +215,9 @@ bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPla
       j = lo;
     }
     BaiRef &R = plan.refs[tid];
-    R.i = i;
-    R.j = j;
+    R.n = j - i;
+    R.vi = i;
+    R.vj = j;
     if (j == i) continue;
     // pieces of the record range on threads: each its runs (record order) and its linear index (first record per
     // window); the pieces are then joined in order
@@ -256,11 +288,11 @@ bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPla
 }
 
 bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *soff, const std::vector<int64_t> &coff,
-              std::string &err) {
+              std::string &err) {   // (soff: the offsets array the plan's positions index)
   std::string s("BAI\1", 4);
   put32(s, (uint32_t)plan.refs.size());
   for (const BaiRef &R : plan.refs) {
-    if (R.j == R.i) {   // no records on this reference
+    if (R.n == 0) {   // no records on this reference
       put32(s, 0);
       put32(s, 0);
       continue;
@@ -281,14 +313,14 @@ bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *soff, const 
     // pseudo-bin 37450: (first record, end of last record), (mapped, unmapped)
     put32(s, 37450);
     put32(s, 2);
-    put64(s, voffset(coff, soff[R.i]));
-    put64(s, voffset(coff, soff[R.j]));
-    put64(s, (uint64_t)(R.j - R.i));
+    put64(s, voffset(coff, soff[R.vi]));
+    put64(s, voffset(coff, soff[R.vj]));
+    put64(s, (uint64_t)R.n);
     put64(s, 0);
     // linear index: windows with no overlapping record take the next window's offset (the last one set so far
     // going backwards), i.e. the first record that can overlap anything at or after them
     std::vector<uint64_t> lin(R.lin.size());
-    uint64_t next = voffset(coff, soff[R.j]);
+    uint64_t next = voffset(coff, soff[R.vj]);
     for (int64_t w = (int64_t)lin.size() - 1; w >= 0; w--) {
       if (R.lin[w] >= 0) next = voffset(coff, soff[R.lin[w]]);
       lin[w] = next;

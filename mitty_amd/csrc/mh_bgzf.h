@@ -36,6 +36,13 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
                        const std::function<const uint8_t *(int64_t, int64_t)> &fetch,
                        std::vector<int64_t> &rec_block_coff, std::string &err);
 
+// The same file with the data blocks handed over as they are ready: next(&buf, &len) gives the next piece of BGZF
+// bytes (false: no more).  *data_pos = the data's file offset (after the header block(s)), *end_pos = the EOF
+// marker's.
+bool bgzf_write_stream(const char *path, const std::string &header, int level,
+                       const std::function<bool(const uint8_t **, int64_t *)> &next, int64_t *data_pos,
+                       int64_t *end_pos, std::string &err);
+
 // BAI for n sorted records whose data offsets are soff[0..n] (soff[n] = end), given the block map from bgzf_write.
 bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,
                const std::vector<int64_t> &rec_block_coff, std::string &err);
@@ -43,20 +50,23 @@ bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, 
 // The BAI in two halves, so the per-record half runs before the blocks' file offsets are known (beside the device
 // deflate): bai_plan, on `threads` threads, finds per reference the chunks (runs of consecutive records in one bin)
 // and the linear index as record indices; bai_emit maps them to virtual offsets and writes the file.
+// Every position below indexes bai_emit's `offs` array: the records' data offsets (bai_plan: offs = soff, positions
+// = record indices) or a compact array of just the offsets the index needs (the device plan, mh_bam.hip).
 struct BaiRun {
   uint32_t bin;
-  int64_t kb, ke;   // records [kb, ke)
+  int64_t kb, ke;   // a chunk: from the offset at kb to the offset at ke (records [kb, ke) for bai_plan)
 };
 struct BaiRef {
-  int64_t i = 0, j = 0;        // the reference's records [i, j)
+  int64_t n = 0;               // records on the reference
+  int64_t vi = 0, vj = 0;      // positions of its first record's offset and of its end
   std::vector<BaiRun> runs;    // by bin, then record order
-  std::vector<int64_t> lin;    // per 16 kbp window: the first record overlapping it, or -1
+  std::vector<int64_t> lin;    // per 16 kbp window: the position of its first overlapping record's offset, or -1
 };
 struct BaiPlan {
   std::vector<BaiRef> refs;
 };
 bool bai_plan(int32_t n_refs, int64_t n, const BaiRec *recs, int threads, BaiPlan &plan, std::string &err);
-bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *soff, const std::vector<int64_t> &rec_block_coff,
+bool bai_emit(const char *path, const BaiPlan &plan, const int64_t *offs, const std::vector<int64_t> &rec_block_coff,
               std::string &err);
 
 // virtual offset of data offset u

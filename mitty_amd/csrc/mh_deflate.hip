@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(256) k_bgzf_pack(const uint8_t *in, int64_t b0
 }  // namespace
 
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
-                    int64_t *used, std::vector<int64_t> *boff) {
+                    int64_t *used, std::vector<int64_t> *boff, const std::function<void(int64_t, int64_t)> *on_piece) {
   *used = 0;
   const int64_t nb_all = (n + BLOCK - 1) / BLOCK;
   if (boff) boff->assign((size_t)nb_all + 1, 0);
@@ -525,6 +525,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
                        (const uint8_t *)ctx->gz_slots.p, (const DfBlockInfo *)ctx->gz_info.p,
                        (const int64_t *)ctx->gz_off.p, d_out + w);
     HIPCHK(ctx, hipGetLastError());
+    if (on_piece) (*on_piece)(w, bytes);
     w += bytes;
   }
   SYNCCHK(ctx, hipStreamSynchronize(st));

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -125,6 +126,7 @@ struct BamStore {
   DevBuf roff, recs;           // record offsets [n_rec + 1] / bytes (input order)
   DevBuf key, val, info;       // sort key, record index, BAI info per record
   DevBuf key2, val2, sort_tmp, soff, srecs, sinfo;   // sorted
+  DevBuf bai_lin, bai_runs, bai_out;                  // the BAI's device plan (mh_bam.hip bam_bai_plan)
   int64_t n_rec = 0, bytes = 0;
   int32_t n_files = 0;
   bool sorted = false;         // srecs/soff/sinfo hold the current store in coordinate order
@@ -369,8 +371,11 @@ int32_t tpl_resolve_all(mh_ctx *ctx);
 int32_t sync_async_fill(mh_ctx *ctx);
 int32_t sync_writers(mh_ctx *ctx);   // the writer stream and the corruption stream drained (host wait)
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
-                    int64_t *used, std::vector<int64_t> *boff = nullptr);   // BGZF blocks of a device buffer (no EOF
-                    // marker), mh_deflate.hip; boff: each block's offset in d_out (+ the end), for a BAI
+                    int64_t *used, std::vector<int64_t> *boff = nullptr,
+                    const std::function<void(int64_t, int64_t)> *on_piece = nullptr);
+                    // BGZF blocks of a device buffer (no EOF marker), mh_deflate.hip; boff: each block's offset in
+                    // d_out (+ the end), for a BAI; on_piece(offset, bytes): a piece of d_out is queued on `st` (the
+                    // caller may copy it out behind that point while the next piece deflates)
 int64_t bgzf_device_bound(int64_t n);
 int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
 int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);
@@ -389,6 +394,11 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
 int32_t bam_sort(mh_ctx *ctx, const void *pa = nullptr);
 int32_t bam_undirect(mh_ctx *ctx);
 int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
+struct BaiPlan;
+// The BAI's per-record half on the device (sorted store): chunks and linear index as positions in `offs`, the
+// compact array of the data offsets they need.  *ok = false (and MH_OK) when the records are outside what the
+// device plan checks (a record past its reference's length, an unsorted store): the caller then plans on the host.
+int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, bool *ok);
 void bam_release(BamStore &B);
 int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count);
 int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_t *d1, int64_t len1, int64_t t_base,
