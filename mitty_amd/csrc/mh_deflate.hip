@@ -9,8 +9,8 @@
 //   parse   greedy LZ77 over the slice, 64 positions per step: every lane looks up its position (a 2^11-entry hash of
 //           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1) and
 //           extends its match up to 32 bytes; a walk over the lanes takes every match the step's positions start
-//           (literals between them; a match of 32+ bytes is extended by the whole wave, up to 258, and ends the
-//           step), then the positions passed are hashed in;
+//           (literals between them; a match of 32+ bytes is extended by the whole wave, up to 258), then the
+//           positions passed are hashed in;
 //   pass 1  the parse, counting symbol frequencies;
 //   codes   lane 0: length-limited Huffman lengths (15 bits; 7 for the code-length code), canonical codes, the
 //           dynamic header (mh_deflate.h, host-testable);
@@ -133,7 +133,7 @@ __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, 
 // match) picks the tokens: literals up to the next lane with a match, that match, and on after its end — so a step
 // takes every match that starts in its 64 positions, not only the first (records with many short matches, e.g.
 // BAM, took one step per match).  A match that reached LX is extended by the whole wave (64 bytes per round, up to
-// MAX_MATCH) and ends the step.  Per lane: lit (a literal token at this position), ms (a match starts here: mlen,
+// MAX_MATCH).  Per lane: lit (a literal token at this position), ms (a match starts here: mlen,
 // mdist).  The later lanes' candidates were looked up before this step's earlier positions were hashed in: the
 // tokens differ from a position-by-position greedy parse, never in validity (every match is verified).
 constexpr int LX = 32;
@@ -188,7 +188,7 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
     }
     st.ms |= 1ull << m;
     int L = __builtin_amdgcn_readlane(len, m);
-    if ((C >> m) & 1ull) {   // a long match: the whole wave extends it, and the step ends with it
+    if ((C >> m) & 1ull) {   // a long match: the whole wave extends it
       const int q = cur + m, j = __builtin_amdgcn_readlane(cand, m);
       const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
       for (;;) {
@@ -201,8 +201,6 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
       }
       if (L > cap) L = cap;
       if (lane == m) len = L;
-      st.next = q + L;
-      break;
     }
     x = m + L;
     if (x >= W) {

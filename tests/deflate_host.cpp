@@ -1,7 +1,7 @@
 // Host check of the single-thread parts of the device BGZF compressor (mitty_amd/csrc/mh_deflate.h: Huffman code
 // lengths, canonical codes, the dynamic block header, CRC-32 combination).  Test infrastructure: compresses a file
 // into BGZF with a sequential restatement of mh_deflate.hip's parse (64-position steps, hash of earlier steps, run
-// candidate, MIN_MATCH-byte matches, eight slices per block with sync flushes) and the shared header code; tests/test_deflate_cpu.py then
+// candidate, MIN_MATCH-byte matches, every match a step's positions start, eight slices per block with sync flushes) and the shared header code; tests/test_deflate_cpu.py then
 // inflates the output with Python's zlib.  usage: deflate_host IN OUT
 #include <cstdio>
 #include <cstring>
@@ -24,40 +24,60 @@ struct Tok {
   int len, dist;    // else a match
 };
 
-// mh_deflate.hip's parse, one step = 64 positions
+int g_steps = 0;   // parse steps (the device's cost unit), reported on stderr
+
+// mh_deflate.hip's parse, one step = 64 positions: every position's candidate from the table as it was at the
+// step's start (or the run at distance 1), each extended alone up to LX bytes; a greedy walk takes the step's
+// matches in order (literals between); a match that reached LX is extended to its end
 std::vector<Tok> parse(const uint8_t *s, int S) {
+  constexpr int LX = 32;
   std::vector<uint32_t> ht(1 << HB, 0);
   std::vector<Tok> out;
   for (int cur = 0; cur < S;) {
-    int f = -1, j = -1;
-    for (int l = 0; l < 64 && f < 0; l++) {
+    g_steps++;
+    const int W = S - cur < 64 ? S - cur : 64;
+    int cand[64], len[64];
+    bool capped[64];
+    for (int l = 0; l < 64; l++) {
       const int p = cur + l;
-      if (p + MIN_MATCH > S) continue;
+      cand[l] = -1;
+      len[l] = 0;
+      capped[l] = false;
+      if (l >= W || p + MIN_MATCH > S) continue;
       const uint32_t w = load4(s, p);
       auto match = [&](int c) { return std::memcmp(s + p, s + c, MIN_MATCH) == 0; };
       if (p >= 1 && match(p - 1)) {
-        f = l;
-        j = p - 1;
+        cand[l] = p - 1;
       } else {
         const int c = (int)ht[hash4(w)] - 1;
-        if (c >= 0 && match(c)) {
-          f = l;
-          j = c;
-        }
+        if (c >= 0 && match(c)) cand[l] = c;
+      }
+      if (cand[l] >= 0) {
+        const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH, lim = cap < LX ? cap : LX;
+        int L = MIN_MATCH;
+        while (L < lim && s[p + L] == s[cand[l] + L]) L++;
+        len[l] = L;
+        capped[l] = L == LX && lim < cap;
       }
     }
-    const int lim = S - cur < 64 ? S - cur : 64;
-    int next;
-    if (f < 0) {
-      for (int l = 0; l < lim; l++) out.push_back({s[cur + l], 0, 0});
-      next = cur + lim;
-    } else {
-      for (int l = 0; l < f; l++) out.push_back({s[cur + l], 0, 0});
-      const int q = cur + f, cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
-      int len = MIN_MATCH;
-      while (len < cap && s[q + len] == s[j + len]) len++;
-      out.push_back({-1, len, q - j});
-      next = q + len;
+    int x = 0, next = cur + W;
+    while (x < W) {
+      int m = x;
+      while (m < W && cand[m] < 0) m++;
+      for (int l = x; l < m; l++) out.push_back({s[cur + l], 0, 0});
+      if (m >= W) {
+        next = cur + W;
+        break;
+      }
+      const int q = cur + m, j = cand[m];
+      int L = len[m];
+      if (capped[m]) {
+        const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
+        while (L < cap && s[q + L] == s[j + L]) L++;
+      }
+      out.push_back({-1, L, q - j});
+      x = m + L;
+      next = cur + x;
     }
     for (int k = cur; k < next; k++)
       if (k + HASH_BYTES <= S) {
@@ -183,5 +203,6 @@ int main(int argc, char **argv) {
   if (!fo) return 2;
   fwrite(out.data(), 1, out.size(), fo);
   fclose(fo);
+  fprintf(stderr, "steps %d\n", g_steps);
   return 0;
 }
