@@ -289,6 +289,9 @@ int32_t mh_fasta_open(const char *path, const char *names, mh_fasta **out);
 const char *mh_fasta_error(const mh_fasta *f);
 int32_t mh_fasta_count(const mh_fasta *f, int32_t *n);
 int32_t mh_fasta_contig(const mh_fasta *f, int32_t i, const char **name, const char **seq, int64_t *len);
+/* Contig i's sequence bytes (mh_fasta_contig's len of them) into dst, joined by threads from the mapped file (a
+ * plain regular file) or copied (gzip input, FIFOs); without the library's own copy of the sequence. */
+int32_t mh_fasta_copy(const mh_fasta *f, int32_t i, char *dst);
 int32_t mh_fasta_close(mh_fasta *f);
 
 /* ---- compressed FASTQ sink: host-side BGZF (gzip-compatible members of <= 65280 input

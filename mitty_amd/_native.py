@@ -27,7 +27,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
-           'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_close']
+           'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_copy', 'mh_fasta_close']
 
 
 class NativeError(RuntimeError):
@@ -124,6 +124,7 @@ def lib():
   _sig(L, 'mh_fasta_error', [c_vp], ctypes.c_char_p)
   _sig(L, 'mh_fasta_count', [c_vp, ctypes.POINTER(c_i32)])
   _sig(L, 'mh_fasta_contig', [c_vp, c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(c_vp), P_i64])
+  _sig(L, 'mh_fasta_copy', [c_vp, c_i32, c_vp])
   _sig(L, 'mh_fasta_close', [c_vp])
   _sig(L, 'mh_output_size', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_output_fetch', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64])
@@ -276,6 +277,16 @@ class PinnedBuffer:
       pass
 
 
+# an uninitialised bytes object of n bytes and its buffer (CPython's PyBytes_FromStringAndSize(NULL, n): filled once,
+# before anything else sees it, as a C extension would)
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_bytes_ptr = ctypes.pythonapi.PyBytes_AsString
+_bytes_ptr.restype = ctypes.c_void_p
+_bytes_ptr.argtypes = [ctypes.py_object]
+
+
 def read_fasta(path, names=None):
   """Host FASTA reader (mh_fasta.cpp): {contig name: bytes}, only `names` when given."""
   L = lib()
@@ -291,9 +302,13 @@ def read_fasta(path, names=None):
     L.mh_fasta_count(h, ctypes.byref(n))
     out = {}
     for i in range(n.value):
-      nm, sq, ln = ctypes.c_char_p(), c_vp(), c_i64()
-      L.mh_fasta_contig(h, i, ctypes.byref(nm), ctypes.byref(sq), ctypes.byref(ln))
-      out[nm.value.decode()] = bytes((ctypes.c_char * ln.value).from_address(sq.value)) if ln.value else b''
+      nm, ln = ctypes.c_char_p(), c_i64()
+      L.mh_fasta_contig(h, i, ctypes.byref(nm), None, ctypes.byref(ln))
+      # the bytes object's own buffer filled by the library's threads (one pass over the file, no second copy)
+      b = _new_bytes(None, ln.value) if ln.value else b''
+      if ln.value:
+        L.mh_fasta_copy(h, i, _bytes_ptr(b))
+      out[nm.value.decode()] = b
     return out
   finally:
     if h:
