@@ -421,6 +421,9 @@ def run_tumor_normal(a):
     'host_cpus': os.cpu_count()}), flush=True)
 
 
+SPLIT_KEYS = ('setup_s', 'parse_s', 'run_s', 'gpu_s', 'flush_s', 'fetch_s', 'write_s', 'close_s')
+
+
 def end_to_end(a, seq, recs, model, kept_per_job):
   """The whole generate-reads command on chr1: FASTA and VCF parsed by the host readers, the GPU job, FASTQ pulled to
   page-locked memory and written to /dev/null (readgenerate.process_multi_threaded).  Input files are written first
@@ -444,11 +447,11 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     vcfio.load_variants_soa(vcf, 'SYN', bed)
     t2 = time.perf_counter()
     st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
-                                             seed=a.seed)
+                                             seed=a.seed, stage_times=True)
     t3 = time.perf_counter()
     out = {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
            'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
-           'split_s': {k: round(st[k], 3) for k in ('setup_s', 'fetch_s', 'write_s')},
+           'split_s': {k: round(st[k], 3) for k in SPLIT_KEYS}, 'stages_ms': st.get('stages_ms'),
            'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
                    'page-locked memory, written to /dev/null; seconds = the whole command'}
     if a.e2e_gz:   # the same with both files BGZF-compressed (what `.gz` output names cost): on the GPU, then on host
@@ -457,11 +460,11 @@ def end_to_end(a, seq, recs, model, kept_per_job):
         t4 = time.perf_counter()
         st = readgenerate.process_multi_threaded(fa, vcf, 'SYN', bed, mod, mdl, a.coverage, '/dev/null', '/dev/null',
                                                  seed=a.seed, compress=True, gz_level=1, gz_threads=threads,
-                                                 gz_device=dev)
+                                                 gz_device=dev, stage_times=True)
         t5 = time.perf_counter()
         out[key] = {'seconds': t5 - t4, 'value': st['kept'] / (t5 - t4), 'unit': 'templates/s',
                     'gz_bytes': st['written1'] + st['written2'],
-                    'split_s': {k: round(st[k], 3) for k in ('setup_s', 'fetch_s', 'write_s')},
+                    'split_s': {k: round(st[k], 3) for k in SPLIT_KEYS}, 'stages_ms': st.get('stages_ms'),
                     'note': 'the same command with BGZF output, deflated ' +
                             ('on the GPU from the arenas (mh_output_bgzf), then D2H of the compressed bytes' if dev else
                              'by the host pool (level 1, {} threads) after D2H'.format(threads))}

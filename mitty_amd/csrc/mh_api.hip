@@ -976,6 +976,7 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
   // the two files' copies on two streams (two DMA engines side by side), file 2's after everything the main stream
   // waits for (the writers)
   const bool both = fq1 && len1 && fq2 && len2;
+  stage_begin(ctx, "output_d2h");
   if (both) {
     HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
@@ -984,7 +985,11 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
   if (fq2 && len2)
     HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost,
                                both ? ctx->stream2 : ctx->stream));
-  if (both) SYNCCHK(ctx, hipStreamSynchronize(ctx->stream2));
+  if (both) {
+    HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  }
+  stage_end(ctx);
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
@@ -1504,11 +1509,15 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
   if (len == 0) return MH_OK;
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(len)));
   int64_t u = 0;
+  stage_begin(ctx, "bgzf_deflate");
   MH_TRY(bgzf_device(ctx, ctx->stream, src, len, (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &u));
+  stage_end(ctx);
   *used = u;
   if (!out) return MH_OK;   // (the size only)
   if (u > cap) return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
+  stage_begin(ctx, "bgzf_d2h");
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
+  stage_end(ctx);
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }

@@ -69,13 +69,15 @@ def get_data_for_workers(model, vcf, seed):
 def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                            fastq1_fname, fastq2_fname, threads=2, seed=7, device=0, rng='mitty', corrupt_seed=None,
                            flush_bytes=1 << 30, max_batch_units=32, max_batch_draws=200_000_000, compress=None,
-                           gz_level=6, gz_threads=8, gz_device=True):
+                           gz_level=6, gz_threads=8, gz_device=True, stage_times=False):
   """Generate reads for every (region, copy, pass) unit and write FASTQ (reference readgenerate.py:76-126).
 
   compress: None = BGZF for file names ending in '.gz' (FastqSink), True / False forces it; gz_device: deflated on
   the GPU (mh_output_bgzf) straight from the arenas, else on gz_threads host threads at gz_level.  Returns a stats
-  dict (templates sampled, kept, bytes, seconds; setup_s = inputs parsed and loaded, fetch_s = waiting for the GPU
-  and its D2H (deflate included), write_s = waiting for the file writes to free a staging slot).
+  dict (templates sampled, kept, bytes, seconds; setup_s = inputs parsed (parse_s) and loaded, run_s = the unit loop
+  = gpu_s + flush_s, flush_s = fetch_s (waiting for the GPU and its D2H, deflate included) + write_s (waiting for
+  the file writes to free a staging slot) + bookkeeping, close_s = files closed and the engine released).
+  stage_times: also the device's per-stage times (stages_ms: e.g. bgzf_deflate, bgzf_d2h, output_d2h, emit).
   """
   t0 = time.time()
   read_model = read_module.read_model_params(model, coverage)
@@ -83,7 +85,10 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   seqs = mfasta.read_fasta(fasta_fname, names={r['region'][0] for r in vdf})
   units = list(get_data_for_workers(read_model, vdf, seed))
   logger.debug('{} passes will be made'.format(len(units)))
+  t_parse = time.time()
   eng = Engine(device)
+  if stage_times:
+    eng.ctx.enable_timing(True)
   if corrupt_seed is not None:
     import numpy as np
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), corrupt_seed)
@@ -91,7 +96,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     chrom, s0, e = reg['region']
     eng.load_region(ri, reg['region'], mfasta.fetch(seqs, chrom, s0, e))
   stats = {'units': len(units), 'templates': 0, 'kept': 0, 'bytes1': 0, 'bytes2': 0, 'setup_s': time.time() - t0,
-           'fetch_s': 0.0, 'write_s': 0.0}
+           'parse_s': t_parse - t0, 'fetch_s': 0.0, 'write_s': 0.0, 'flush_s': 0.0}
   write2 = fastq2_fname is not None
   fp1 = FastqSink(fastq1_fname, gz_level, gz_threads, compress)   # '.gz' names get BGZF output
   fp2 = FastqSink(fastq2_fname, gz_level, gz_threads, compress) if write2 else None
@@ -107,6 +112,13 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
   GZ_CHUNK = 4096 * 0xff00   # whole BGZF blocks: the members equal one compression of the whole arena
 
   def flush(ps, n, kept, b1, b2):
+    tfl = time.time()
+    try:
+      _flush(ps, n, kept, b1, b2)
+    finally:
+      stats['flush_s'] += time.time() - tfl
+
+  def _flush(ps, n, kept, b1, b2):
     stats['templates'] += n
     stats['kept'] += kept
     stats['bytes1'] += b1
@@ -141,6 +153,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
           pw.submit(slot, [d1 if n1 else None, d2 if n2 else None])
       eng.ctx.reset_output()
 
+  t_run = time.time()
   try:
     # batches of units sampled together (their MT19937 streams run concurrently); order of emission unchanged
     batch, batch_draws = [], 0
@@ -156,6 +169,16 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
         logger.debug('Units {}..{}: {:0.3f}s'.format(batch[0][0], batch[-1][0], time.time() - t1))
         batch, batch_draws = [], 0
   finally:
+    # run_s: the unit loop (GPU job + flushes); gpu_s = run_s - flush_s: splice, sampling and emission as the host
+    # sees them
+    stats['run_s'] = time.time() - t_run
+    stats['gpu_s'] = stats['run_s'] - stats['flush_s']
+    if stage_times:
+      agg = {}
+      for name, ms in eng.ctx.stage_times():
+        agg[name] = agg.get(name, 0.0) + ms
+      stats['stages_ms'] = {k: round(v, 2) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])}
+    t_close = time.time()
     try:
       tw = time.time()
       pw.close()
@@ -169,6 +192,7 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
         for b in slot:
           b.free()
   stats['written1'], stats['written2'] = fp1.written, fp2.written if fp2 else 0
+  stats['close_s'] = time.time() - t_close
   stats['seconds'] = time.time() - t0
   return stats
 
