@@ -314,6 +314,14 @@ int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out
 int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used);
 int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t len, char *out, int64_t cap,
                              int64_t *used);
+/* Both arenas' bytes [offset, offset + n_f) deflated (file 1, then file 2) with each file's compressed bytes copied
+ * to out_f on a second stream behind its deflate: returns once the deflates are done (used_f = compressed bytes),
+ * the copies still in flight; mh_output_bgzf_wait(ticket) waits for them (before out_f is read or reused).  Two
+ * calls may be outstanding (the device buffer has two halves): the pipelined form of mh_output_bgzf_range for the
+ * `.gz` sinks (readgenerate.py:233-253's writes), one range's copies overlapping the next range's deflate. */
+int32_t mh_output_bgzf_pair(mh_ctx *ctx, int64_t offset, int64_t n1, int64_t n2, char *out1, int64_t cap1,
+                            char *out2, int64_t cap2, int64_t *used1, int64_t *used2, int32_t *ticket);
+int32_t mh_output_bgzf_wait(mh_ctx *ctx, int32_t ticket);
 
 /* ---- corrupt-reads over existing FASTQ (readcorrupt.multi_process, readcorrupt.py:18-118; cli.py:144-157) -----
  * The complete templates of the host buffers (file 2 optional) are corrupted with the model set by

@@ -25,7 +25,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
-           'mh_output_bgzf_range',
+           'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_copy', 'mh_fasta_close']
 
@@ -85,6 +85,9 @@ def lib():
   _sig(L, 'mh_bgzf_compress_gpu', [c_vp, c_vp, c_i64, c_vp, c_i64, P_i64])
   _sig(L, 'mh_output_bgzf', [c_vp, c_i32, c_vp, c_i64, P_i64])
   _sig(L, 'mh_output_bgzf_range', [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, P_i64])
+  _sig(L, 'mh_output_bgzf_pair', [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, P_i64, P_i64,
+                                  ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_output_bgzf_wait', [c_vp, c_i32])
   _sig(L, 'mh_expand_variant', [c_i64, c_i64, c_i64, c_i64, c_i32, c_i64, P_i64, ctypes.POINTER(c_i32), P_i64, P_i64])
   _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
@@ -700,6 +703,24 @@ class Context:
       self._chk(self._L.mh_output_bgzf_range(self._h, f, off, n, c_vp(pins[f].ptr), cap, ctypes.byref(used)))
       out.append(pins[f].view(used.value))
     return out
+
+  def output_bgzf_pair(self, pins, off, n1, n2):
+    """Both arenas' [off, off + n_f) BGZF-compressed on the GPU, the compressed bytes copied into page-locked staging
+    (pins: [PinnedBuffer, PinnedBuffer]) behind the deflates: returns (ticket, memoryviews) at once; the views hold
+    the bytes after output_bgzf_wait(ticket)."""
+    caps = []
+    for f, n in enumerate((n1, n2)):
+      cap = n + (n // 0xff00 + 2) * 40 + 64 if n > 0 else 0   # every block stored, at worst
+      pins[f].reserve(max(cap, 1))
+      caps.append(cap)
+    u1, u2, t = c_i64(), c_i64(), c_i32()
+    self._chk(self._L.mh_output_bgzf_pair(self._h, int(off), int(n1), int(n2), c_vp(pins[0].ptr) if n1 > 0 else None,
+                                          caps[0], c_vp(pins[1].ptr) if n2 > 0 else None, caps[1], ctypes.byref(u1),
+                                          ctypes.byref(u2), ctypes.byref(t)))
+    return t.value, [pins[0].view(u1.value), pins[1].view(u2.value)]
+
+  def output_bgzf_wait(self, ticket):
+    self._chk(self._L.mh_output_bgzf_wait(self._h, int(ticket)))
 
   def output_bgzf_pinned(self, pins):
     """Both arenas BGZF-compressed on the GPU into page-locked staging (pins: [PinnedBuffer, PinnedBuffer]);

@@ -354,6 +354,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   ctx->tail_state.reset();
+  for (hipEvent_t e : ctx->ev_gz)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->h_units) (void)hipHostFree(ctx->h_units);
   for (auto &e : ctx->eset) {
@@ -1519,6 +1521,75 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->gz_out.p, u, hipMemcpyDeviceToHost, ctx->stream));
   stage_end(ctx);
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_output_bgzf_pair(mh_ctx *ctx, int64_t offset, int64_t n1, int64_t n2, char *out1, int64_t cap1,
+                            char *out2, int64_t cap2, int64_t *used1, int64_t *used2, int32_t *ticket) {
+  CTX_GUARD(ctx);
+  if (!used1 || !used2 || !ticket || offset < 0 || n1 < 0 || n2 < 0 || (n1 && !out1) || (n2 && !out2))
+    return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  MH_TRY(sync_async_fill(ctx));
+  MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
+  if ((n1 && offset + n1 > ctx->used1) || (n2 && offset + n2 > ctx->used2))
+    return arg_fail(ctx, MH_E_ARG, "range outside the arena");
+  *used1 = *used2 = 0;
+  *ticket = -1;
+  const int64_t b1 = n1 ? bgzf_device_bound(n1) : 0, b2 = n2 ? bgzf_device_bound(n2) : 0;
+  const int64_t need = (b1 + b2 + 255) & ~(int64_t)255;
+  if (need == 0) return MH_OK;
+  for (int h = 0; h < 2; h++)
+    if (!ctx->ev_gz[h]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_gz[h], hipEventDisableTiming));
+  if ((int64_t)ctx->gz_out.cap / 2 < need) {   // (growing frees the old halves: their copies first)
+    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream2));
+    ctx->gz_pending[0] = ctx->gz_pending[1] = false;
+    MH_TRY(ensure(ctx, ctx->gz_out, 2 * (size_t)need));
+  }
+  const int h = ctx->gz_half;
+  if (ctx->gz_pending[h]) {   // the call two back copied out of this half
+    SYNCCHK(ctx, hipEventSynchronize(ctx->ev_gz[h]));
+    ctx->gz_pending[h] = false;
+  }
+  uint8_t *base = (uint8_t *)ctx->gz_out.p + (size_t)h * (ctx->gz_out.cap / 2);
+  const uint8_t *src[2] = {(const uint8_t *)ctx->out1.p + offset, (const uint8_t *)ctx->out2.p + offset};
+  const int64_t nn[2] = {n1, n2}, cap[2] = {cap1, cap2}, off[2] = {0, b1};
+  char *out[2] = {out1, out2};
+  int64_t *used[2] = {used1, used2};
+  for (int f = 0; f < 2; f++) {
+    if (nn[f] == 0) continue;
+    int64_t u = 0;
+    stage_begin(ctx, "bgzf_deflate");
+    MH_TRY(bgzf_device(ctx, ctx->stream, src[f], nn[f], base + off[f], f ? b2 : b1, &u));
+    stage_end(ctx);
+    if (u > cap[f]) {
+      SYNCCHK(ctx, hipStreamSynchronize(ctx->stream2));
+      return arg_fail(ctx, MH_E_CAPACITY, "output buffer too small");
+    }
+    *used[f] = u;
+    // the copy behind the deflate on the second stream: it overlaps the next deflate
+    HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+    ctx->stage_stream = ctx->stream2;
+    stage_begin(ctx, "bgzf_d2h");
+    HIPCHK(ctx, hipMemcpyAsync(out[f], base + off[f], (size_t)u, hipMemcpyDeviceToHost, ctx->stream2));
+    stage_end(ctx);
+    ctx->stage_stream = nullptr;
+  }
+  HIPCHK(ctx, hipEventRecord(ctx->ev_gz[h], ctx->stream2));
+  ctx->gz_pending[h] = true;
+  ctx->gz_half = h ^ 1;
+  *ticket = h;
+  return MH_OK;
+}
+
+int32_t mh_output_bgzf_wait(mh_ctx *ctx, int32_t ticket) {
+  CTX_GUARD_EMIT(ctx);
+  if (ticket < 0) return MH_OK;
+  if (ticket > 1) return arg_fail(ctx, MH_E_ARG, "bad ticket");
+  if (ctx->gz_pending[ticket]) {
+    SYNCCHK(ctx, hipEventSynchronize(ctx->ev_gz[ticket]));
+    ctx->gz_pending[ticket] = false;
+  }
   return MH_OK;
 }
 

@@ -219,6 +219,10 @@ struct mh_ctx {
   mh::DevBuf pb[6];     // batch-wide permutation: ts, shuffled ts, global keys, sorted keys, sorted steps, heads
   mh::DevBuf pb_tmp;    // its radix sort scratch
   mh::DevBuf gz_slots, gz_info, gz_off, gz_scan, gz_out, gz_in;   // device BGZF (mh_deflate.hip)
+  // mh_output_bgzf_pair: gz_out in two halves used by alternate calls; per half the event after its copies (stream2)
+  hipEvent_t ev_gz[2] = {nullptr, nullptr};
+  bool gz_pending[2] = {false, false};
+  int gz_half = 0;
   mh::DevBuf nrun_tmp;  // unsorted N-run boundaries
   mh::DevBuf dec_buf;   // chunk-parallel shuffle decode: chunk jobs, starts, counts, work list
   int64_t dec_passes = 0;   // count passes of the last chunk-parallel decode (diagnostics)

@@ -127,18 +127,28 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
     if u1 + u2 >= flush_bytes or ps == len(units) - 1:
       if gz_device and all(s is None or s.gz for s in sinks):
         # BGZF members deflated on the GPU from the arenas (chunks of whole 0xff00-byte blocks), then D2H of the
-        # compressed bytes only
+        # compressed bytes only: a chunk's copies run behind its deflates on a second stream, beside the next
+        # chunk's deflates, and the chunk goes to the writers once they are in
+        pending = None
         for off in range(0, max(u1, u2), GZ_CHUNK):
           slot = nslot[0] % 2
           nslot[0] += 1
           tw = time.time()
-          pw.wait(slot)
+          pw.wait(slot)   # the writes of this slot's previous chunk
           tf = time.time()
           n1, n2 = max(0, min(GZ_CHUNK, u1 - off)), max(0, min(GZ_CHUNK, u2 - off))
-          z1, z2 = eng.ctx.output_bgzf_range_pinned(pins[slot], off, n1, n2)
+          ticket, z = eng.ctx.output_bgzf_pair(pins[slot], off, n1, n2)
+          if pending is not None:
+            eng.ctx.output_bgzf_wait(pending[0])
+            pw.submit(*pending[1:])
+          pending = (ticket, slot, [z[0] if n1 else None, z[1] if n2 else None], [n1, n2])
           stats['write_s'] += tf - tw
           stats['fetch_s'] += time.time() - tf
-          pw.submit(slot, [z1 if n1 else None, z2 if n2 else None], [n1, n2])
+        if pending is not None:
+          tf = time.time()
+          eng.ctx.output_bgzf_wait(pending[0])
+          pw.submit(*pending[1:])
+          stats['fetch_s'] += time.time() - tf
       else:
         for off in range(0, max(u1, u2), CHUNK):
           slot = nslot[0] % 2
