@@ -209,6 +209,13 @@ int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);
 /* Copy arena bytes [offset, offset+len) of file 1 / file 2 to host (either host pointer may be NULL). */
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t offset1, char *fq1, int64_t len1, int64_t offset2, char *fq2,
                         int64_t len2);
+/* The same copies queued (file 1 and file 2 on two streams, after the queued writers) without a host wait: the
+ * bytes are in fq1 / fq2 after mh_output_fetch_wait(ticket).  Two fetches may be in flight, so the DMA engines stay
+ * busy while the host writes the previous chunk (readgenerate.py:233-253's file writes).  mh_output_reset waits for
+ * pending fetches. */
+int32_t mh_output_fetch_async(mh_ctx *ctx, int64_t offset1, char *fq1, int64_t len1, int64_t offset2, char *fq2,
+                              int64_t len2, int32_t *ticket);
+int32_t mh_output_fetch_wait(mh_ctx *ctx, int32_t ticket);
 int32_t mh_output_reset(mh_ctx *ctx);
 /* Page-locked host memory for mh_output_fetch destinations (D2H at full link rate; the FASTQ sink writes from it). */
 int32_t mh_host_alloc(int64_t bytes, void **out);

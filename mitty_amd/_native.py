@@ -25,7 +25,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
-           'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait',
+           'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait', 'mh_output_fetch_async',
+           'mh_output_fetch_wait',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
            'mh_fasta_open', 'mh_fasta_error', 'mh_fasta_count', 'mh_fasta_contig', 'mh_fasta_copy', 'mh_fasta_close']
 
@@ -88,6 +89,8 @@ def lib():
   _sig(L, 'mh_output_bgzf_pair', [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, P_i64, P_i64,
                                   ctypes.POINTER(c_i32)])
   _sig(L, 'mh_output_bgzf_wait', [c_vp, c_i32])
+  _sig(L, 'mh_output_fetch_async', [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.POINTER(c_i32)])
+  _sig(L, 'mh_output_fetch_wait', [c_vp, c_i32])
   _sig(L, 'mh_expand_variant', [c_i64, c_i64, c_i64, c_i64, c_i32, c_i64, P_i64, ctypes.POINTER(c_i32), P_i64, P_i64])
   _sig(L, 'mh_sample_templates', [c_vp, c_i32, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
   _sig(L, 'mh_sample_templates_span', [c_vp, c_i64, c_i64, c_dbl, c_i32, c_vp, c_i32, c_u64, c_i32, P_i64])
@@ -664,6 +667,19 @@ class Context:
     self._chk(self._L.mh_output_fetch(self._h, off1, c_vp(pins[0].ptr) if n1 > 0 else None, n1, off2,
                                       c_vp(pins[1].ptr) if n2 > 0 else None, n2))
     return pins[0].view(n1), pins[1].view(n2)
+
+  def fetch_range_async(self, pins, off1, n1, off2, n2):
+    """fetch_range_pinned without the wait: returns (ticket, memoryviews); the bytes are in after
+    fetch_wait(ticket)."""
+    pins[0].reserve(max(n1, 1))
+    pins[1].reserve(max(n2, 1))
+    t = c_i32()
+    self._chk(self._L.mh_output_fetch_async(self._h, off1, c_vp(pins[0].ptr) if n1 > 0 else None, n1, off2,
+                                            c_vp(pins[1].ptr) if n2 > 0 else None, n2, ctypes.byref(t)))
+    return t.value, (pins[0].view(n1), pins[1].view(n2))
+
+  def fetch_wait(self, ticket):
+    self._chk(self._L.mh_output_fetch_wait(self._h, int(ticket)))
 
   def fetch_output_pinned(self, pins):
     """The whole arenas into page-locked staging (pins: [PinnedBuffer, PinnedBuffer], grown as needed); returns

@@ -356,6 +356,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   ctx->tail_state.reset();
   for (hipEvent_t e : ctx->ev_gz)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev_fetch)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->h_units) (void)hipHostFree(ctx->h_units);
   for (auto &e : ctx->eset) {
@@ -996,8 +998,51 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
   return MH_OK;
 }
 
+int32_t mh_output_fetch_async(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2,
+                              int64_t len2, int32_t *ticket) {
+  CTX_GUARD(ctx);
+  MH_TRY(sync_async_fill(ctx));
+  if (!ticket || (fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
+      (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
+    return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
+  for (int t = 0; t < 2; t++)
+    if (!ctx->ev_fetch[t]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_fetch[t], hipEventDisableTiming));
+  const int t = ctx->fetch_next;
+  if (ctx->fetch_pending[t]) return arg_fail(ctx, MH_E_STATE, "two fetches in flight: wait for one first");
+  // file 1 on the main stream (after the writers it waits for), file 2 on the second stream behind the same point
+  stage_begin(ctx, "output_d2h");
+  HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+  if (fq1 && len1) HIPCHK(ctx, hipMemcpyAsync(fq1, (char *)ctx->out1.p + off1, len1, hipMemcpyDeviceToHost, ctx->stream));
+  if (fq2 && len2) HIPCHK(ctx, hipMemcpyAsync(fq2, (char *)ctx->out2.p + off2, len2, hipMemcpyDeviceToHost, ctx->stream2));
+  HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  stage_end(ctx);
+  HIPCHK(ctx, hipEventRecord(ctx->ev_fetch[t], ctx->stream));
+  ctx->fetch_pending[t] = true;
+  ctx->fetch_next = t ^ 1;
+  *ticket = t;
+  return MH_OK;
+}
+
+int32_t mh_output_fetch_wait(mh_ctx *ctx, int32_t ticket) {
+  CTX_GUARD_EMIT(ctx);
+  if (ticket < 0) return MH_OK;
+  if (ticket > 1) return arg_fail(ctx, MH_E_ARG, "bad ticket");
+  if (ctx->fetch_pending[ticket]) {
+    SYNCCHK(ctx, hipEventSynchronize(ctx->ev_fetch[ticket]));
+    ctx->fetch_pending[ticket] = false;
+  }
+  return MH_OK;
+}
+
 int32_t mh_output_reset(mh_ctx *ctx) {
   CTX_GUARD_EMIT(ctx);
+  for (int t = 0; t < 2; t++)   // copies still reading the arenas finish before they are refilled
+    if (ctx->fetch_pending[t]) {
+      SYNCCHK(ctx, hipEventSynchronize(ctx->ev_fetch[t]));
+      ctx->fetch_pending[t] = false;
+    }
   return output_reset(ctx);
 }
 

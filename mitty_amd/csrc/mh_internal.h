@@ -221,6 +221,9 @@ struct mh_ctx {
   mh::DevBuf gz_slots, gz_info, gz_off, gz_scan, gz_out, gz_in;   // device BGZF (mh_deflate.hip)
   // mh_output_bgzf_pair: gz_out in two halves used by alternate calls; per half the event after its copies (stream2)
   hipEvent_t ev_gz[2] = {nullptr, nullptr};
+  hipEvent_t ev_fetch[2] = {nullptr, nullptr};   // mh_output_fetch_async: per ticket, after both files' copies
+  bool fetch_pending[2] = {false, false};
+  int fetch_next = 0;
   bool gz_pending[2] = {false, false};
   int gz_half = 0;
   mh::DevBuf nrun_tmp;  // unsorted N-run boundaries

@@ -150,6 +150,8 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
           pw.submit(*pending[1:])
           stats['fetch_s'] += time.time() - tf
       else:
+        # two chunks' copies in flight: chunk k's D2H is queued before chunk k - 1 goes to the writers
+        pending = None
         for off in range(0, max(u1, u2), CHUNK):
           slot = nslot[0] % 2
           nslot[0] += 1
@@ -157,10 +159,18 @@ def process_multi_threaded(fasta_fname, vcf_fname, sample_name, bed_fname, read_
           pw.wait(slot)   # the writes of this slot's previous chunk
           tf = time.time()
           n1, n2 = max(0, min(CHUNK, u1 - off)), max(0, min(CHUNK, u2 - off))
-          d1, d2 = eng.ctx.fetch_range_pinned(pins[slot], off, n1, off, n2)
+          ticket, (d1, d2) = eng.ctx.fetch_range_async(pins[slot], off, n1, off, n2)
+          if pending is not None:
+            eng.ctx.fetch_wait(pending[0])
+            pw.submit(*pending[1:])
+          pending = (ticket, slot, [d1 if n1 else None, d2 if n2 else None])
           stats['write_s'] += tf - tw
           stats['fetch_s'] += time.time() - tf
-          pw.submit(slot, [d1 if n1 else None, d2 if n2 else None])
+        if pending is not None:
+          tf = time.time()
+          eng.ctx.fetch_wait(pending[0])
+          pw.submit(*pending[1:])
+          stats['fetch_s'] += time.time() - tf
       eng.ctx.reset_output()
 
   t_run = time.time()
