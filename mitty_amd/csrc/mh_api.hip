@@ -290,8 +290,8 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   ctx->hap_fwd = hf && atoi(hf) != 0;
   const char *ef = getenv("MH_EW_FLAT");
   ctx->ew_flat = ef && atoi(ef) != 0;
-  const char *ed = getenv("MH_EW_DBG"), *eg = getenv("MH_EW_GATHER4");
-  ctx->ew_dbg = (ed ? atoi(ed) : 0) | (eg && atoi(eg) ? 512 : 0);
+  const char *eg = getenv("MH_EW_GATHER4");
+  ctx->ew_dbg = eg && atoi(eg) ? 512 : 0;   // (EW_GATHER4)
   const char *so = getenv("MH_SORT");
   ctx->sort_lsd = so && !strcmp(so, "lsd");
   const char *gt = getenv("MH_WRITER_GATE_TAIL");

@@ -266,7 +266,7 @@ struct mh_ctx {
   // mate-1 windows into LDS itself
   bool hap_fwd = false;
   // experiments read once per context (mh_create), so tests switch them per context: MH_EW_FLAT (flat output sweep),
-  // MH_EW_DBG / MH_EW_GATHER4 (the writer's TArgs.dbg bits), MH_SORT=lsd (the hand-written permutation sort)
+  // MH_EW_GATHER4 (the writer's TArgs.dbg bit EW_GATHER4), MH_SORT=lsd (the hand-written permutation sort)
   bool ew_flat = false, sort_lsd = false;
   int32_t ew_dbg = 0;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
