@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4, second call: the full-size WGS step byte-checked unit by unit (bench --verify), the remaining writer /
-# gate / sort arms, and the tumor/normal + BAM line (device deflate of BAM records).
+# Round 4, second call: the full-size WGS step byte-checked unit by unit (bench --verify)
+# and the tumor/normal + BAM line (device deflate of BAM records), the RCCL line at one GPU.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04d
@@ -12,5 +12,4 @@ timeout -k 10 300 python -u bench.py --tumor-normal > $O/tn.json 2> $O/tn.err ||
 python3 -c "import json; d=json.load(open('$O/tn.json')); print('tn', d['value'], d['ms_per_step'], d['bam_file_gpu'], d['with_bam_file']['value'])" || true
 MH_DIST_BACKEND=nccl timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-e2e > $O/nccl1.json 2> $O/nccl1.err || exit $?
 python3 -c "import json; d=[json.loads(l) for l in open('$O/nccl1.json') if l.startswith('{')][-1]; print('nccl1', d['value'], d.get('collective_backend'), d.get('world_size_seen'))" || true
-TAG=r04d REPS=1 bash scripts/gpu_ab.sh 'base:' 'tail4:MH_WRITER_GATE_TAIL=4' 'flat:MH_EW_FLAT=1' 'g4:MH_EW_GATHER4=1' 'fwdtail4:MH_HAP_FWD=1 MH_WRITER_GATE_TAIL=4' 'copyorder: -- --unit-order copy' 'fwdcopy:MH_HAP_FWD=1 -- --unit-order copy' 'base2:' || exit $?
 echo done
