@@ -739,7 +739,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
         const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
         if (b >= 0 && !staged) continue;                        // seam chunk, stored by the seam pass
         uint4 v;
-        if (CR != 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
+        if (CR < 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
           v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);
         } else {
           const int32_t src = b >= 0 ? o_s + ((f * ED_T + lo) * 4 + b) * 16
@@ -769,7 +769,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       uint4 v;
-      if (CR != 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
+      if (CR < 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
         v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);   // inside T's '~' run: no LDS read
       } else {
         const int32_t src = b >= 0 ? o_s + (r * 4 + b) * 16
@@ -817,7 +817,13 @@ struct TArgs {
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
   const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
+  CorruptCfg cc;            // CR 3: the rows computed in the writer (its tables from global memory)
 };
+
+// one corruption row slot (defined with k_cr_cols below)
+__device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, const uint16_t *fp16,
+                                        const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
+                                        int cnt, uint4 *qo_, uint32_t *code_);
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
 // array of nodes would be placed in scratch)
@@ -854,7 +860,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
   // seam chunks through LDS (in order with the others); CR 2 stores them from the seam pass (4 KB less LDS: with the
   // per-record T strings that is 5 instead of 4 workgroups per CU, 0.77 vs 0.73 G/s on the corrupt bench)
-  const bool staged = !(A.dbg & EW_SEAM_PASS) && CR != 2;
+  const bool staged = !(A.dbg & EW_SEAM_PASS) && CR < 2;
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
@@ -868,7 +874,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   // CR 2: the tile's row slots (file f, template j, block b: slot f * ED_T * nb + j * nb + b), the first RK per thread
   // loaded before the gathers so they are in flight with them
   constexpr int RK = 3;
-  const int32_t nb = CR == 2 ? A.nb : 1, nsl = NF * ED_T * nb;
+  const int32_t nb = CR >= 2 ? A.nb : 1, nsl = NF * ED_T * nb;
   auto slot_g = [&](int32_t sl, int *sf, int *sj, int *sb_) -> int64_t {
     const int f = sl / (ED_T * nb), rem = sl - f * ED_T * nb, j = rem / nb;
     *sf = f;
@@ -1062,7 +1068,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
                                 : h.rc ? (int32_t)((h.hap_len - a - S) & 15) : (int32_t)((-(a + S)) & 15);
         mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + lead;
         mt.S[fr] = S;
-        mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
+        mt.tb[fr] = CR >= 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
         if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
           mt.qb = qb;
@@ -1080,13 +1086,59 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
     }
   }
+  // CR 3: the tile's row slots computed here, as k_cr_cols computes them (slot s: block s / (NF * ED_T), then file,
+  // then template, so a wave's lanes share a block and its table rows; the tables are read from global memory)
+  auto slot3 = [&](int32_t sl, int *sf, int *sj, int *sb_) __attribute__((always_inline)) {
+    const int b = sl / (NF * ED_T), rem = sl - b * (NF * ED_T), f = rem / ED_T;
+    *sf = f;
+    *sj = rem - f * ED_T;
+    *sb_ = b;
+  };
+  auto compute3 = [&](int32_t sl, uint4 *q, uint32_t *code) __attribute__((always_inline)) {
+    int f, j, b;
+    slot3(sl, &f, &j, &b);
+    *q = make_uint4(0u, 0u, 0u, 0u);
+    *code = 0u;
+    if (j >= nt) return;
+    const int n0 = ED_CRB * b, cnt = A.rlen - n0 < ED_CRB ? A.rlen - n0 : ED_CRB;
+    const int64_t tt = t0 + j + A.cc.t_base, row = (int64_t)f * A.cc.max_bp + n0;
+    cr_slot(A.cc.bk + row * CB_ROW, A.cc.TP + row * A.cc.n_bq, A.cc.Fp16, A.cc, make_uint2(A.cc.k0, A.cc.k1),
+            (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, q, code);
+  };
+  if (CR == 3) {
+    static_assert(RK == 3, "the fused rows' registers");
+    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
+    uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
+#pragma nounroll
+    for (int k = 0; k < RK; k++) {   // one copy of the row code; the results into named registers (k is uniform)
+      uint4 q = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t c = 0u;
+      if (tid + k * ED_THREADS < nsl) compute3(tid + k * ED_THREADS, &q, &c);
+      if (k == 0) {
+        r0 = q;
+        w0 = c;
+      } else if (k == 1) {
+        r1 = q;
+        w1 = c;
+      } else {
+        r2 = q;
+        w2 = c;
+      }
+    }
+    rq[0] = r0;
+    rq[1] = r1;
+    rq[2] = r2;
+    rcw[0] = w0;
+    rcw[1] = w1;
+    rcw[2] = w2;
+  }
   __syncthreads();
-  if (CR == 2) {
+  if (CR >= 2) {
     // each row slot of a kept record: its qualities into the record's T, its substitutions into the window
     // (base_rot[b][code - 1], illumina.py:131-136,159-160); block 0 also writes T's separators
     auto lay = [&](int32_t sl, uint4 q, uint32_t code) {
       int f, j, b;
-      (void)slot_g(sl, &f, &j, &b);
+      if (CR == 3) slot3(sl, &f, &j, &b); else (void)slot_g(sl, &f, &j, &b);
       if (j >= nt) return;
       const DMeta &M = meta[j];
       if (M.len[f] == 0) return;
@@ -1125,9 +1177,16 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     for (int k = 0; k < RK; k++)
       if (tid + k * ED_THREADS < nsl) lay(tid + k * ED_THREADS, rq[k], rcw[k]);
     for (int32_t sl = tid + RK * ED_THREADS; sl < nsl; sl += ED_THREADS) {   // (records of more than 23 blocks)
-      int sf, sj, sbk;
-      const int64_t g = slot_g(sl, &sf, &sj, &sbk);
-      lay(sl, A.crow[g], A.ccode[g]);
+      if (CR == 3) {
+        uint4 q;
+        uint32_t code;
+        compute3(sl, &q, &code);
+        lay(sl, q, code);
+      } else {
+        int sf, sj, sbk;
+        const int64_t g = slot_g(sl, &sf, &sj, &sbk);
+        lay(sl, A.crow[g], A.ccode[g]);
+      }
     }
     __syncthreads();
   }
@@ -1576,6 +1635,76 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
   *code = cd;
 }
 
+// One corruption row slot: the qualities (+ 33) and substitution codes of block n0 / 15 of template (tl, th)'s file f
+// (cnt bases: a full block, or the short last one) — k_cr_cols' item, and the fused writer's (CR 3).  bk / t8p: the
+// bucket and threshold-pair rows of base n0 (LDS or global), fp16 the u16 substitution thresholds.
+__device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, const uint16_t *fp16,
+                                        const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
+                                        int cnt, uint4 *qo_, uint32_t *code_) {
+  const int n_bq = cc.n_bq;
+  if (cnt == CI_BLK) {
+    cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, qo_, code_);
+  } else {   // a short last block: the guarded per-base path
+    uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
+#pragma unroll
+    for (int g = 0; g < CI_BLK / 3; g++) {
+      if (3 * g < cnt) {
+        const uint4 r = philox4x32_10(
+            make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int j = 3 * g + k;
+          if (j < cnt) {
+            const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+            uint32_t amb;
+            const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+            const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
+            const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+            const bool sub = !amb && h2 < pth;
+            px |= (uint32_t)(amb || h2 == pth) << j;
+            ps |= (uint32_t)sub << j;
+            pc |= (uint32_t)(sub && c10 == 1023u) << j;
+            ch |= (c10 % 3u) << (2 * j);
+            qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
+          }
+        }
+      }
+    }
+    while (px) {
+      const int j = __builtin_ctz(px);
+      px &= px - 1;
+      const int n = n0 + j;
+      const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+      const int k = n % 3;
+      const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+      uint32_t amb;
+      const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+      const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
+                                       f, n, w, bq, amb);
+      const uint32_t sh = 8u * (uint32_t)(j & 3);
+      qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
+      const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+      ps |= (x >> 8) << j;
+      pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
+    }
+    while (pc) {
+      const int j = __builtin_ctz(pc);
+      pc &= pc - 1;
+      const uint4 c = philox4x32_10(
+          make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
+      ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
+    }
+    uint32_t code = 0;
+    while (ps) {
+      const int j = __builtin_ctz(ps);
+      ps &= ps - 1;
+      code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
+    }
+    *qo_ = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+    *code_ = code;
+  }
+}
+
 // The corruption rows: a workgroup per (block column, template chunk) stages only its column's tables (bucket rows
 // and threshold pairs of 15 positions of one file: 6.7 KB; a record-major pass staging a whole file's 67 KB was
 // LDS-bound at 4.3 ms per chr1 unit, round 3), so occupancy is bound by registers, not LDS; its threads take
@@ -1616,69 +1745,9 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
   uint32_t *const ocode = codes + (int64_t)col * A.m;
   for (int64_t t = tb + threadIdx.x; t < te; t += CC_THREADS) {
     const int64_t tt = t + cc.t_base;
-    const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
     uint4 qo;
     uint32_t code;
-    if (cnt == CI_BLK) {
-      cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, &qo, &code);
-    } else {   // a short last block: the guarded per-base path
-      uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
-#pragma unroll
-      for (int g = 0; g < CI_BLK / 3; g++) {
-        if (3 * g < cnt) {
-          const uint4 r = philox4x32_10(
-              make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            const int j = 3 * g + k;
-            if (j < cnt) {
-              const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-              uint32_t amb;
-              const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
-              const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
-              const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-              const bool sub = !amb && h2 < pth;
-              px |= (uint32_t)(amb || h2 == pth) << j;
-              ps |= (uint32_t)sub << j;
-              pc |= (uint32_t)(sub && c10 == 1023u) << j;
-              ch |= (c10 % 3u) << (2 * j);
-              qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
-            }
-          }
-        }
-      }
-      while (px) {
-        const int j = __builtin_ctz(px);
-        px &= px - 1;
-        const int n = n0 + j;
-        const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-        const int k = n % 3;
-        const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-        uint32_t amb;
-        const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
-        const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
-                                         f, n, w, bq, amb);
-        const uint32_t sh = 8u * (uint32_t)(j & 3);
-        qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
-        const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-        ps |= (x >> 8) << j;
-        pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
-      }
-      while (pc) {
-        const int j = __builtin_ctz(pc);
-        pc &= pc - 1;
-        const uint4 c = philox4x32_10(
-            make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
-        ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
-      }
-      code = 0;
-      while (ps) {
-        const int j = __builtin_ctz(ps);
-        ps &= ps - 1;
-        code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
-      }
-      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
-    }
+    cr_slot(bk, t8p, fp16, cc, key, (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, &qo, &code);
     orow[t] = qo;
     ocode[t] = code;
   }
@@ -1718,6 +1787,11 @@ static int32_t cr_rows_alloc(mh_ctx *ctx, int64_t m, int32_t nf, int64_t rlen) {
 // serves every unit, in stream order; the pass on a stream of its own beside the previous writer was within noise)
 static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
                                TArgs &A) {
+  if (ctx->cr_fused) {   // CR 3: the writer computes its tile's rows itself
+    A.cc = cc;
+    A.nb = (rlen + CI_BLK - 1) / CI_BLK;
+    return MH_OK;
+  }
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (ctx->cr_rows.cap < (size_t)(m * nf * NB) * 16 + 64 || ctx->cr_codes.cap < (size_t)(m * nf * NB) * 4 + 64)
     return arg_fail(ctx, MH_E_STATE, "corruption rows not allocated");
@@ -1850,6 +1924,7 @@ constexpr int32_t ED_QPAD = 4;
 // two files, the flat output sweep (mh_ctx::ew_flat, experiment)
 using EwKernel = void (*)(TArgs, QHead);
 static EwKernel ew_kernel(int cr, bool two, bool flat) {
+  if (cr == 3) return two ? k_emit_tiles<2, 4, 3, 0> : k_emit_tiles<1, 8, 3, 0>;
   if (flat)
     return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 1> : k_emit_tiles<1, 8, 2, 1>)
            : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 1> : k_emit_tiles<1, 8, 1, 1>)
@@ -2071,7 +2146,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   }
   if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
       cnt_base + m < (int64_t)UINT32_MAX) {
-    if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
+    if (cr_rows && !ctx->cr_fused) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
     // and the next job's sampling overlap it
     if (!writer_dep) {
@@ -2097,7 +2172,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
             qstride, ew_dbg};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
-    auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
+    auto kfn = ew_kernel(cr_rows ? (ctx->cr_fused ? 3 : 2) : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -2406,7 +2481,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on) cc = corrupt_cfg(ctx, unit_key, 0);
 
-  if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
+  if (cr_rows && !ctx->cr_fused) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
   hipStream_t ws = ctx->wstream;
   HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));   // the unit's templates (main stream) are ready
   HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
@@ -2428,7 +2503,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
           ctx->ew_dbg};
   if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
   stage_begin(ctx, "emit_write");
-  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
+  auto kfn = ew_kernel(cr_rows ? (ctx->cr_fused ? 3 : 2) : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);
