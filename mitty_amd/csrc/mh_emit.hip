@@ -821,9 +821,9 @@ struct TArgs {
 };
 
 // one corruption row slot (defined with k_cr_cols below)
-__device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, const uint16_t *fp16,
-                                        const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
-                                        int cnt, uint4 *qo_, uint32_t *code_);
+__device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const uint16_t *t8p, uint32_t otp,
+                                        const uint16_t *fp16, const CorruptCfg &cc, uint2 key, uint32_t tl,
+                                        uint32_t th, int f, int n0, int cnt, uint4 *qo_, uint32_t *code_);
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
 // array of nodes would be placed in scratch)
@@ -893,6 +893,52 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       rq[k] = A.crow[g];
       rcw[k] = A.ccode[g];
     }
+  }
+  // CR 3: the tile's row slots computed here, as k_cr_cols computes them (slot s: block s / (NF * ED_T), then file,
+  // then template, so a wave's lanes share a block and its table rows; the tables are read from global memory)
+  auto slot3 = [&](int32_t sl, int *sf, int *sj, int *sb_) __attribute__((always_inline)) {
+    const int b = sl / (NF * ED_T), rem = sl - b * (NF * ED_T), f = rem / ED_T;
+    *sf = f;
+    *sj = rem - f * ED_T;
+    *sb_ = b;
+  };
+  auto compute3 = [&](int32_t sl, uint4 *q, uint32_t *code) __attribute__((always_inline)) {
+    int f, j, b;
+    slot3(sl, &f, &j, &b);
+    *q = make_uint4(0u, 0u, 0u, 0u);
+    *code = 0u;
+    if (j >= nt) return;
+    const int n0 = ED_CRB * b, cnt = A.rlen - n0 < ED_CRB ? A.rlen - n0 : ED_CRB;
+    const int64_t tt = t0 + j + A.cc.t_base, row = (int64_t)f * A.cc.max_bp + n0;
+    cr_slot(A.cc.bk, (uint32_t)(row * CB_ROW), A.cc.TP, (uint32_t)(row * A.cc.n_bq), A.cc.Fp16, A.cc,
+            make_uint2(A.cc.k0, A.cc.k1), (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, q, code);
+  };
+  if (CR == 3) {
+    static_assert(RK == 3, "the fused rows' registers");
+    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
+    uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
+#pragma nounroll
+    for (int k = 0; k < RK; k++) {   // one copy of the row code; the results into named registers (k is uniform)
+      uint4 q = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t c = 0u;
+      if (tid + k * ED_THREADS < nsl) compute3(tid + k * ED_THREADS, &q, &c);
+      if (k == 0) {
+        r0 = q;
+        w0 = c;
+      } else if (k == 1) {
+        r1 = q;
+        w1 = c;
+      } else {
+        r2 = q;
+        w2 = c;
+      }
+    }
+    rq[0] = r0;
+    rq[1] = r1;
+    rq[2] = r2;
+    rcw[0] = w0;
+    rcw[1] = w1;
+    rcw[2] = w2;
   }
   if (A.dbg & EW_GATHER4) {
     // (MH_EW_GATHER4, experiment) every thread gathers: window slots s = tid + 256 k (window s / chunks, chunk
@@ -1086,52 +1132,6 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
     }
   }
-  // CR 3: the tile's row slots computed here, as k_cr_cols computes them (slot s: block s / (NF * ED_T), then file,
-  // then template, so a wave's lanes share a block and its table rows; the tables are read from global memory)
-  auto slot3 = [&](int32_t sl, int *sf, int *sj, int *sb_) __attribute__((always_inline)) {
-    const int b = sl / (NF * ED_T), rem = sl - b * (NF * ED_T), f = rem / ED_T;
-    *sf = f;
-    *sj = rem - f * ED_T;
-    *sb_ = b;
-  };
-  auto compute3 = [&](int32_t sl, uint4 *q, uint32_t *code) __attribute__((always_inline)) {
-    int f, j, b;
-    slot3(sl, &f, &j, &b);
-    *q = make_uint4(0u, 0u, 0u, 0u);
-    *code = 0u;
-    if (j >= nt) return;
-    const int n0 = ED_CRB * b, cnt = A.rlen - n0 < ED_CRB ? A.rlen - n0 : ED_CRB;
-    const int64_t tt = t0 + j + A.cc.t_base, row = (int64_t)f * A.cc.max_bp + n0;
-    cr_slot(A.cc.bk + row * CB_ROW, A.cc.TP + row * A.cc.n_bq, A.cc.Fp16, A.cc, make_uint2(A.cc.k0, A.cc.k1),
-            (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, q, code);
-  };
-  if (CR == 3) {
-    static_assert(RK == 3, "the fused rows' registers");
-    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
-    uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
-#pragma nounroll
-    for (int k = 0; k < RK; k++) {   // one copy of the row code; the results into named registers (k is uniform)
-      uint4 q = make_uint4(0u, 0u, 0u, 0u);
-      uint32_t c = 0u;
-      if (tid + k * ED_THREADS < nsl) compute3(tid + k * ED_THREADS, &q, &c);
-      if (k == 0) {
-        r0 = q;
-        w0 = c;
-      } else if (k == 1) {
-        r1 = q;
-        w1 = c;
-      } else {
-        r2 = q;
-        w2 = c;
-      }
-    }
-    rq[0] = r0;
-    rq[1] = r1;
-    rq[2] = r2;
-    rcw[0] = w0;
-    rcw[1] = w1;
-    rcw[2] = w2;
-  }
   __syncthreads();
   if (CR >= 2) {
     // each row slot of a kept record: its qualities into the record's T, its substitutions into the window
@@ -1231,16 +1231,21 @@ struct CiArgs {
 
 // The LDS-table BQ step of one base (k_cr_inplace's walk): bk = the base's bucket row, tp = its threshold-pair row.
 // Entries below h1 = w >> 16 (capped at 93); *amb when one equals h1, or three or more of the bucket's lie below it.
-__device__ __forceinline__ uint32_t cr_lds_walk(const uint8_t *bk, const uint16_t *tp, uint32_t w, uint32_t *amb) {
-  const uint32_t e = bk[w >> 24];
+// (base + 32-bit offset form: with global tables a uniform base and 32-bit lane offsets, not 64-bit lane pointers)
+__device__ __forceinline__ uint32_t cr_walk_at(const uint8_t *bk, uint32_t obk, const uint16_t *tp, uint32_t otp,
+                                               uint32_t w, uint32_t *amb) {
+  const uint32_t e = bk[obk + (w >> 24)];
   const uint32_t c = e & 0x7fu, fl = e >> 7;
-  const uint32_t pa = tp[c], pb = tp[c + 1];
+  const uint32_t pa = tp[otp + c], pb = tp[otp + c + 1];
   const uint32_t lo = (w >> 16) & 0xffu;
   const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = pb >> 8;
   const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
   const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
   *amb = b2 | (fl & (uint32_t)(vn == lo));
   return c + b0 + b1;
+}
+__device__ __forceinline__ uint32_t cr_lds_walk(const uint8_t *bk, const uint16_t *tp, uint32_t w, uint32_t *amb) {
+  return cr_walk_at(bk, 0u, tp, 0u, w, amb);
 }
 
 // One full 15-base block of a record with the tables in LDS: five triple draws, per base a BQ step and the U2
@@ -1556,7 +1561,8 @@ static_assert(ED_CRB == CI_BLK, "the writer's row blocks are the corruption bloc
 
 // One full block with the tables in LDS (cr_full_block's phases), into registers: qualities packed in qo (byte 15
 // zero), the codes of the substituted bases in *code.
-__device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t *tp, const uint16_t *fp,
+__device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, const uint16_t *tp, uint32_t otp,
+                                              const uint16_t *fp,
                                               const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
                                               uint4 *qo, uint32_t *code) {
   const int n_bq = cc.n_bq;
@@ -1571,12 +1577,12 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
     RW[g] = r.w;
   }
 #pragma unroll
-  for (int j = 0; j < CI_BLK; j++) E[j] = bk[j * CB_ROW + (W[j] >> 24)];
+  for (int j = 0; j < CI_BLK; j++) E[j] = bk[obk + (uint32_t)(j * CB_ROW) + (W[j] >> 24)];
 #pragma unroll
   for (int j = 0; j < CI_BLK; j++) {
-    const uint16_t *t = tp + j * n_bq + (E[j] & 0x7fu);
-    P[j] = t[0];
-    V2[j] = ((const uint8_t *)t)[3];
+    const uint32_t ti = otp + (uint32_t)(j * n_bq) + (E[j] & 0x7fu);
+    P[j] = tp[ti];
+    V2[j] = ((const uint8_t *)tp)[2 * ti + 3];   // (byte 3 from the pair's start: the next entry's high byte)
   }
   uint32_t ps = 0, px = 0;
 #pragma unroll
@@ -1608,7 +1614,7 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
     const int k = n % 3;
     const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
     uint32_t amb;
-    const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
+    const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), tp, otp + (uint32_t)(j * n_bq), w, &amb);
     const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
                                      w, bq, amb);
     const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
@@ -1638,12 +1644,12 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, const uint16_t 
 // One corruption row slot: the qualities (+ 33) and substitution codes of block n0 / 15 of template (tl, th)'s file f
 // (cnt bases: a full block, or the short last one) — k_cr_cols' item, and the fused writer's (CR 3).  bk / t8p: the
 // bucket and threshold-pair rows of base n0 (LDS or global), fp16 the u16 substitution thresholds.
-__device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, const uint16_t *fp16,
-                                        const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
-                                        int cnt, uint4 *qo_, uint32_t *code_) {
+__device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const uint16_t *t8p, uint32_t otp,
+                                        const uint16_t *fp16, const CorruptCfg &cc, uint2 key, uint32_t tl,
+                                        uint32_t th, int f, int n0, int cnt, uint4 *qo_, uint32_t *code_) {
   const int n_bq = cc.n_bq;
   if (cnt == CI_BLK) {
-    cr_block_rows(bk, t8p, fp16, cc, key, tl, th, f, n0, qo_, code_);
+    cr_block_rows(bk, obk, t8p, otp, fp16, cc, key, tl, th, f, n0, qo_, code_);
   } else {   // a short last block: the guarded per-base path
     uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
 #pragma unroll
@@ -1657,7 +1663,7 @@ __device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, 
           if (j < cnt) {
             const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
             uint32_t amb;
-            const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+            const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), t8p, otp + (uint32_t)(j * n_bq), w, &amb);
             const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
             const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
             const bool sub = !amb && h2 < pth;
@@ -1678,7 +1684,7 @@ __device__ __forceinline__ void cr_slot(const uint8_t *bk, const uint16_t *t8p, 
       const int k = n % 3;
       const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
       uint32_t amb;
-      const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, t8p + j * n_bq, w, &amb);
+      const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), t8p, otp + (uint32_t)(j * n_bq), w, &amb);
       const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
                                        f, n, w, bq, amb);
       const uint32_t sh = 8u * (uint32_t)(j & 3);
@@ -1747,7 +1753,7 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
     const int64_t tt = t + cc.t_base;
     uint4 qo;
     uint32_t code;
-    cr_slot(bk, t8p, fp16, cc, key, (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, &qo, &code);
+    cr_slot(bk, 0u, t8p, 0u, fp16, cc, key, (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, &qo, &code);
     orow[t] = qo;
     ocode[t] = code;
   }
