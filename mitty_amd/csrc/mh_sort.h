@@ -179,9 +179,16 @@ inline hipError_t lsd_sort_pairs_iota(void *tmp, size_t &tmp_bytes, const uint32
   void *scr = take(scan_lb_scratch_bytes<int64_t>(nc));
   int64_t *total = (int64_t *)take(64);
   const int passes = end_bit == 0 ? 1 : (int)((end_bit + RS_BITS - 1) / RS_BITS);
+  // the scan scratch sits inside tmp at an offset that moves with n, so the memory under it holds other sorts' keys:
+  // its look-back state starts fresh here (zeroed by the first pass's scan) and is dropped after the last pass, so
+  // no later scan takes this interior address for zeroed scratch with a running ticket
+  lb_forget(scr);
+  struct Forget {
+    const void *p;
+    ~Forget() { lb_forget(p); }
+  } forget{scr};
   const uint32_t *ksrc = keys_in, *vsrc = nullptr;
   for (int ps = 0; ps < passes; ps++) {
-    const bool last = ps == passes - 1;
     // the last pass writes the outputs; the ones before alternate so that it reads the other buffer
     const bool to_out = ((passes - 1 - ps) & 1) == 0;
     uint32_t *kd = to_out ? keys_out : k2, *vd = to_out ? vals_out : v2;
@@ -194,7 +201,6 @@ inline hipError_t lsd_sort_pairs_iota(void *tmp, size_t &tmp_bytes, const uint32
                        (const uint32_t *)off, tiles, kd, vd);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    (void)last;
     ksrc = kd;
     vsrc = vd;
   }

@@ -415,6 +415,42 @@ def test_batched_units_vs_oracle(native, monkeypatch, sort):
   assert fix <= 1
 
 
+def test_lsd_sort_repeated_batches(native, monkeypatch):
+  """The hand-written permutation sort (MH_SORT=lsd) over batches of different sizes and then the first batch again:
+  its look-back scan scratch sits inside the sort's buffer at an offset that moves with the batch size, so a batch
+  size seen before must not find stale scan state there (round 4: a timed-out look-back scan on the bench's second
+  step).  The repeat's templates equal the first run's, and rocprim's sort gives the same."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, _ = _native.read_model_params(150, 30.0)
+  L = 4_000_000
+  seq = synth.contig(L, 41)
+  copies = synth.copies_soa(synth.variants(seq, 42))
+  batches = [[(0, 0, 0, 501), (1, 0, 1, 502), (2, 0, 0, 503)], [(3, 0, 1, 601)], [(4, 0, 0, 701), (5, 0, 1, 702)]]
+  got = {}
+  for sort in ('lsd', 'rocprim'):
+    monkeypatch.setenv('MH_SORT', sort)
+    eng = Engine(0)
+    try:
+      eng.load_region(0, ('2', 0, L), seq)
+      runs = []
+      for k, b in enumerate(batches + [batches[0]]):
+        ns = eng.sample_only(b, lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 100 * k)
+        runs.append([eng.ctx.templates_export(100 * k + i) for i in range(len(b))])
+        assert min(ns) > 1000
+      got[sort] = runs
+    finally:
+      eng.close()
+  for a, b in zip(got['lsd'][0], got['lsd'][-1]):
+    for x, y in zip(a, b):
+      assert np.array_equal(x, y)
+  for ra, rb in zip(got['lsd'], got['rocprim']):
+    for a, b in zip(ra, rb):
+      for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
 def test_async_tail_equals_sync_templates(native):
   """mh_sample_units_async: the units' tails queued on the second stream and resolved one by one, in any order (a
   count, an export — any non-emission entry point resolves every pending set — or the next batch's sampling), give
