@@ -6,9 +6,9 @@
 // one eighth of the block as a deflate block of their own (dynamic Huffman codes from that slice's symbols,
 // matches inside the slice): wave w < 7 ends its block with an empty stored block (a sync flush, 5 bytes) so the
 // next slice's bits start on a byte boundary, and the slices' bytes simply concatenate; wave 7's block is final.
-//   parse   greedy LZ77 over the slice, 64 positions per step: every lane looks up its position (a 2^11-entry hash of
-//           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1) and
-//           extends its match up to 32 bytes; a walk over the lanes takes every match the step's positions start
+//   parse   greedy LZ77 over the slice, 256 positions per step: every position is looked up (a 2^11-entry hash of
+//           the next four bytes, holding positions of earlier steps, and the run candidate at distance 1) and its
+//           match extended up to 32 bytes; a walk over the positions takes every match the step's positions start
 //           (literals between them; a match of 32+ bytes is extended by the whole wave, up to 258), then the
 //           positions passed are hashed in;
 //   pass 1  the parse, counting symbol frequencies;
@@ -37,7 +37,10 @@ constexpr int SLICE = (BLOCK + DF_WAVES - 1) / DF_WAVES;   // 8160 input bytes p
 constexpr int HBITS = 11;
 constexpr int REGION = 9216;                // a slice's output bytes in the slot (more: the block is stored)
 constexpr int SLOT = DF_WAVES * REGION;
-constexpr int STAGE = 112;                  // staging words: 64 codes of <= 48 bits, a carried word, slack
+constexpr int DF_NP = 4;                    // parse positions per lane and step (a step covers 256 positions)
+// staging words: a step's codes (at most 256 literals of <= 15 bits: a match of <= 48 bits stands for >= 7
+// positions), a carried word, slack
+constexpr int STAGE = (64 * DF_NP * 15 + 31) / 32 + 8;
 
 struct CodeScratch {                        // while the codes are built (the hash table is idle then)
   uint32_t keys[512], A[NLIT];
@@ -128,79 +131,111 @@ __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, 
   __builtin_amdgcn_wave_barrier();
 }
 
-// One step of the parse at `cur` (wave-uniform): every lane looks for a match at its position (cand: an earlier
-// position), extends it by itself up to LX bytes, and a greedy walk over the lanes (wave-uniform, one iteration per
-// match) picks the tokens: literals up to the next lane with a match, that match, and on after its end — so a step
-// takes every match that starts in its 64 positions, not only the first (records with many short matches, e.g.
-// BAM, took one step per match).  A match that reached LX is extended by the whole wave (64 bytes per round, up to
-// MAX_MATCH).  Per lane: lit (a literal token at this position), ms (a match starts here: mlen,
-// mdist).  The later lanes' candidates were looked up before this step's earlier positions were hashed in: the
-// tokens differ from a position-by-position greedy parse, never in validity (every match is verified).
+// One step of the parse at `cur` (wave-uniform) covers DF_NP x 64 positions (lane l holds positions cur + 64 h + l,
+// h < DF_NP): every position looks for a match (cand: an earlier position) and extends it by itself up to LX bytes,
+// then a greedy walk over the positions (wave-uniform, one iteration per match) picks the tokens: literals up to the
+// next position with a match, that match, and on after its end — so a step takes every match that starts in its
+// positions (records with many short matches, e.g. BAM, took one step per match), and a step of literals covers
+// 256 bytes (random FASTQ bases are literals).  A match that reached LX is extended by the whole wave (64 bytes per
+// round, up to MAX_MATCH).  The later positions' candidates were looked up before this step's earlier positions
+// were hashed in: the tokens differ from a position-by-position greedy parse, never in validity (every match is
+// verified); the host restatement (tests/deflate_host.cpp) deflates the golden FASTQ to the same ratio with 3.6x
+// fewer steps than one match per step.
 constexpr int LX = 32;
 struct Step {
-  int next;                // the position after the step's last token
-  uint64_t lit, ms;        // lanes holding a literal / starting a match
-  int mlen, mdist;         // this lane's match (ms lanes)
+  int next;                          // the position after the step's last token
+  uint64_t lit[DF_NP], ms[DF_NP];    // positions 64 h + lane holding a literal / starting a match
+  int mlen[DF_NP], mdist[DF_NP];     // this lane's matches (ms positions)
 };
 
 __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane) {
-  const int p = cur + lane;
-  int cand = -1;
-  if (p + MIN_MATCH <= S) {
-    const uint32_t w = load4(s, p);
-    if (p >= 1 && match7(s, p, w, p - 1)) {
-      cand = p - 1;                                  // a run: distance 1
-    } else {
-      const int j = (int)ht[hash4(w)] - 1;           // a position of an earlier step (< cur <= p)
-      if (j >= 0 && match7(s, p, w, j)) cand = j;
-    }
-  }
-  int len = 0;
-  bool capped = false;
-  if (cand >= 0) {   // the lane's own extension, four bytes at a time, up to LX (or the end of the slice)
-    const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH;
-    const int lim = cap < LX ? cap : LX;
-    len = MIN_MATCH;
-    while (len < lim) {
-      const uint32_t x = load4(s, p + len) ^ load4(s, cand + len);
-      if (x) {
-        len += (int)(__builtin_ctz(x) >> 3);
-        break;
+  int cand[DF_NP], len[DF_NP];
+  uint64_t M[DF_NP], C[DF_NP];
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    const int p = cur + 64 * h + lane;
+    int c = -1;
+    if (p + MIN_MATCH <= S) {
+      const uint32_t w = load4(s, p);
+      if (p >= 1 && match7(s, p, w, p - 1)) {
+        c = p - 1;                                   // a run: distance 1
+      } else {
+        const int j = (int)ht[hash4(w)] - 1;         // a position of an earlier step (< cur <= p)
+        if (j >= 0 && match7(s, p, w, j)) c = j;
       }
-      len += 4;
     }
-    if (len > lim) len = lim;
-    capped = len == LX && lim < cap;
+    int L = 0;
+    bool capped = false;
+    if (c >= 0) {   // the position's own extension, four bytes at a time, up to LX (or the end of the slice)
+      const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH;
+      const int lim = cap < LX ? cap : LX;
+      L = MIN_MATCH;
+      while (L < lim) {
+        const uint32_t x = load4(s, p + L) ^ load4(s, c + L);
+        if (x) {
+          L += (int)(__builtin_ctz(x) >> 3);
+          break;
+        }
+        L += 4;
+      }
+      if (L > lim) L = lim;
+      capped = L == LX && lim < cap;
+    }
+    cand[h] = c;
+    len[h] = L;
+    M[h] = __ballot(c >= 0);
+    C[h] = __ballot(capped);
   }
-  const uint64_t M = __ballot(cand >= 0), C = __ballot(capped);
-  const int W = S - cur < 64 ? S - cur : 64;
+  const int NW = 64 * DF_NP;
+  const int W = S - cur < NW ? S - cur : NW;
   Step st;
-  st.lit = st.ms = 0;
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) st.lit[h] = st.ms[h] = 0;
   int x = 0;
-  for (;;) {   // wave-uniform greedy walk: x = the lane of the next token
-    const uint64_t rest = x < 64 ? M & (~0ull << x) : 0ull;
-    const int m = rest ? __builtin_ctzll(rest) : 64;
+  for (;;) {   // wave-uniform greedy walk: x = the position of the next token
+    int m = NW;
+#pragma unroll
+    for (int h = 0; h < DF_NP; h++)
+      if (m == NW && x < 64 * (h + 1)) {
+        const uint64_t r = x > 64 * h ? M[h] & (~0ull << (x - 64 * h)) : M[h];
+        if (r) m = 64 * h + __builtin_ctzll(r);
+      }
     const int me = m < W ? m : W;
-    if (me > x) st.lit |= (me - x >= 64 ? ~0ull : ((1ull << (me - x)) - 1ull)) << x;
+#pragma unroll
+    for (int h = 0; h < DF_NP; h++) {   // literals [x, me)
+      const int a = x > 64 * h ? x - 64 * h : 0, b = me < 64 * (h + 1) ? me - 64 * h : 64;
+      if (b > a) st.lit[h] |= (b - a >= 64 ? ~0ull : ((1ull << (b - a)) - 1ull)) << a;
+    }
     if (m >= W) {
       st.next = cur + W;
       break;
     }
-    st.ms |= 1ull << m;
-    int L = __builtin_amdgcn_readlane(len, m);
-    if ((C >> m) & 1ull) {   // a long match: the whole wave extends it
-      const int q = cur + m, j = __builtin_amdgcn_readlane(cand, m);
+    const int hm = m >> 6, l = m & 63;
+    int L = 0, jc = 0;
+    bool cp = false;
+#pragma unroll
+    for (int h = 0; h < DF_NP; h++)
+      if (h == hm) {
+        st.ms[h] |= 1ull << l;
+        L = __builtin_amdgcn_readlane(len[h], l);
+        jc = __builtin_amdgcn_readlane(cand[h], l);
+        cp = (C[h] >> l) & 1ull;
+      }
+    if (cp) {   // a long match: the whole wave extends it
+      const int q = cur + m;
       const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
       for (;;) {
         const int k = L + lane;
-        const bool eq = k < cap && s[q + k] == s[j + k];
+        const bool eq = k < cap && s[q + k] == s[jc + k];
         const uint64_t ne = ~__ballot(eq);
         const int run = ne ? __builtin_ctzll(ne) : 64;
         L += run;
         if (run < 64 || L >= cap) break;
       }
       if (L > cap) L = cap;
-      if (lane == m) len = L;
+#pragma unroll
+      for (int h = 0; h < DF_NP; h++)
+        if (h == hm && lane == l) len[h] = L;
     }
     x = m + L;
     if (x >= W) {
@@ -208,8 +243,11 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
       break;
     }
   }
-  st.mlen = len;
-  st.mdist = p - cand;
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    st.mlen[h] = len[h];
+    st.mdist[h] = cur + 64 * h + lane - cand[h];
+  }
   return st;
 }
 
@@ -222,12 +260,15 @@ __device__ __forceinline__ void hash_in(const uint8_t *s, int S, int a, int b, u
   __builtin_amdgcn_wave_barrier();
 }
 
-// the symbols of one step, pass 1: literal and match frequencies (LDS atomics, one per token lane)
+// the symbols of one step, pass 1: literal and match frequencies (LDS atomics, one per token position)
 __device__ __forceinline__ void count_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, int lane) {
-  if ((st.lit >> lane) & 1ull) atomicAdd(&W.lf[s[cur + lane]], 1u);
-  if ((st.ms >> lane) & 1ull) {
-    atomicAdd(&W.lf[257 + len_code(st.mlen)], 1u);
-    atomicAdd(&W.dfq[dist_code(st.mdist)], 1u);
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    if ((st.lit[h] >> lane) & 1ull) atomicAdd(&W.lf[s[cur + 64 * h + lane]], 1u);
+    if ((st.ms[h] >> lane) & 1ull) {
+      atomicAdd(&W.lf[257 + len_code(st.mlen[h])], 1u);
+      atomicAdd(&W.dfq[dist_code(st.mdist[h])], 1u);
+    }
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
@@ -241,19 +282,19 @@ struct BitWave {
   bool overflow;
 };
 
-// put each lane's (v, n) (n <= 57 bits: v < 2^n) in lane order after bitpos
-__device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t v, int n, int lane) {
-  int total;
-  const int excl = wave_sum_incl(n, total) - n;   // the bits before this lane's
-  const int r = (int)(bw.bitpos & 31) + excl;   // bit offset inside the staging strip
-  if (n) {
-    const int wi = r >> 5, sh = r & 31;
-    atomicOr(&stage[wi], (uint32_t)(v << sh));
-    const uint64_t hi = sh ? v >> (32 - sh) : v >> 32;
-    if (hi) atomicOr(&stage[wi + 1], (uint32_t)hi);
-    const uint64_t hi2 = sh ? (v >> (64 - sh)) : 0;
-    if (sh && (sh + n) > 64 && hi2) atomicOr(&stage[wi + 2], (uint32_t)hi2);
-  }
+// OR one code (v, n) into the staging strip at bit offset r
+__device__ __forceinline__ void stage_or(uint32_t *stage, uint64_t v, int n, int r) {
+  if (!n) return;
+  const int wi = r >> 5, sh = r & 31;
+  atomicOr(&stage[wi], (uint32_t)(v << sh));
+  const uint64_t hi = sh ? v >> (32 - sh) : v >> 32;
+  if (hi) atomicOr(&stage[wi + 1], (uint32_t)hi);
+  const uint64_t hi2 = sh ? (v >> (64 - sh)) : 0;
+  if (sh && (sh + n) > 64 && hi2) atomicOr(&stage[wi + 2], (uint32_t)hi2);
+}
+
+// the strip's completed words to the region after `total` more bits, the partial one carried
+__device__ __forceinline__ void flush_bits(BitWave &bw, uint32_t *stage, int total, int lane) {
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   const int64_t end = bw.bitpos + total;
@@ -267,35 +308,52 @@ __device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t 
   const uint32_t carry = stage[full];
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
-  for (int k = lane; k < STAGE; k += 64) stage[k] = k == 0 ? carry : 0u;
+  for (int k = lane; k <= full + 2 && k < STAGE; k += 64) stage[k] = k == 0 ? carry : 0u;   // (the words used)
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   bw.bitpos = end;
 }
 
-// the codes of one step, pass 2: every token lane's code (a literal's, or a match's length and distance codes with
-// their extra bits: <= 48 bits), placed in lane order = position order
+// put each lane's (v, n) (n <= 57 bits: v < 2^n) in lane order after bitpos
+__device__ __forceinline__ void put_bits(BitWave &bw, uint32_t *stage, uint64_t v, int n, int lane) {
+  int total;
+  const int excl = wave_sum_incl(n, total) - n;   // the bits before this lane's
+  stage_or(stage, v, n, (int)(bw.bitpos & 31) + excl);
+  flush_bits(bw, stage, total, lane);
+}
+
+// the codes of one step, pass 2: every token position's code (a literal's, or a match's length and distance codes
+// with their extra bits: <= 48 bits), placed in position order (h, then lane)
 __device__ __forceinline__ void encode_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, BitWave &bw,
                                             int lane) {
-  uint64_t v = 0;
-  int n = 0;
-  if ((st.lit >> lane) & 1ull) {
-    const uint32_t c = s[cur + lane];
-    v = W.lcode[c];
-    n = W.llen[c];
-  } else if ((st.ms >> lane) & 1ull) {
-    const int lc = len_code(st.mlen), dc = dist_code(st.mdist);
-    const int le = len_extra(lc), de = dist_extra(dc);
-    v = W.lcode[257 + lc];
-    n = W.llen[257 + lc];
-    v |= (uint64_t)(st.mlen - len_base(lc)) << n;
-    n += le;
-    v |= (uint64_t)W.dcode[dc] << n;
-    n += W.dlen[dc];
-    v |= (uint64_t)(st.mdist - dist_base(dc)) << n;
-    n += de;
+  int before = (int)(bw.bitpos & 31);
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    uint64_t v = 0;
+    int n = 0;
+    if ((st.lit[h] >> lane) & 1ull) {
+      const uint32_t c = s[cur + 64 * h + lane];
+      v = W.lcode[c];
+      n = W.llen[c];
+    } else if ((st.ms[h] >> lane) & 1ull) {
+      const int ml = st.mlen[h], md = st.mdist[h];
+      const int lc = len_code(ml), dc = dist_code(md);
+      const int le = len_extra(lc), de = dist_extra(dc);
+      v = W.lcode[257 + lc];
+      n = W.llen[257 + lc];
+      v |= (uint64_t)(ml - len_base(lc)) << n;
+      n += le;
+      v |= (uint64_t)W.dcode[dc] << n;
+      n += W.dlen[dc];
+      v |= (uint64_t)(md - dist_base(dc)) << n;
+      n += de;
+    }
+    int tot;
+    const int excl = wave_sum_incl(n, tot) - n;
+    stage_or(W.stage, v, n, before + excl);
+    before += tot;
   }
-  put_bits(bw, W.stage, v, n, lane);
+  flush_bits(bw, W.stage, before - (int)(bw.bitpos & 31), lane);
 }
 
 __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, int64_t n_in, int64_t b0, int64_t nb,

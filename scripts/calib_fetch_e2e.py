@@ -10,6 +10,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+  import torch
+  torch.empty(1, device='cuda')   # torch's HIP runtime first (it cannot start after the library's in one process)
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from mitty_amd.readmodel import get_read_model
@@ -62,7 +64,6 @@ def main():
     run('sync_one_file', sync_fetch, False)
     run('async_two_files', async_fetch)
     run('async_one_file', async_fetch, False)
-    import torch
     src = torch.empty(4 << 30, dtype=torch.uint8, device='cuda')
     src.fill_(3)
     tp = [torch.empty(CH, dtype=torch.uint8, pin_memory=True) for _ in range(2)]

@@ -4,6 +4,7 @@
 // candidate, MIN_MATCH-byte matches, every match a step's positions start, eight slices per block with sync flushes) and the shared header code; tests/test_deflate_cpu.py then
 // inflates the output with Python's zlib.  usage: deflate_host IN OUT
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -31,14 +32,15 @@ int g_steps = 0;   // parse steps (the device's cost unit), reported on stderr
 // matches in order (literals between); a match that reached LX is extended to its end
 std::vector<Tok> parse(const uint8_t *s, int S) {
   constexpr int LX = 32;
+  const int SW = getenv("DF_SW") ? atoi(getenv("DF_SW")) : 256;   // positions per step (mh_deflate.hip DF_NP x 64)
   std::vector<uint32_t> ht(1 << HB, 0);
   std::vector<Tok> out;
   for (int cur = 0; cur < S;) {
     g_steps++;
-    const int W = S - cur < 64 ? S - cur : 64;
-    int cand[64], len[64];
-    bool capped[64];
-    for (int l = 0; l < 64; l++) {
+    const int W = S - cur < SW ? S - cur : SW;
+    int cand[128], len[128];
+    bool capped[128];
+    for (int l = 0; l < SW; l++) {
       const int p = cur + l;
       cand[l] = -1;
       len[l] = 0;

@@ -49,7 +49,7 @@ def _child(rank, port, outdir, q):
     unit = (0, ri, cpy, seed)
     ns = be.sample([unit], lambda r, cc: vdf[r]['copies'][cc], rm['p'], rm['rlen'], rm['cum_tlen'], 'mitty')
     n = ns[0]
-    be._slots.append(be._slots[0])   # set 1 emits from the same haplotype
+    be._slots[1] = be._slots[0]   # set 1 emits from the same haplotype
     be.share(0, n, 0, rm['rlen'], into=1)
     res = []
     for k in (0, 1):
