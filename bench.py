@@ -736,7 +736,8 @@ def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
       for ri in sorted({u[0] for u in units}):
         offs[ri] = (fp.tell(), len(data[ri][0]))
         fp.write(bytes(data[ri][0]))
-    jobs = [((img,) + offs[ri], copies[ri][cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(ps),
+    # (ref bytes, region start, variants, p, rlen, cum_tlen, seed, stub, chrom, cpy): oracle._unit_digest's job
+    jobs = [((img,) + offs[ri], 0, copies[ri][cpy], p, rlen, model['cum_tlen'], s, 'SYN:0:{}'.format(ps),
              contigs[ri][0], cpy) for ps, (ri, cpy, s) in enumerate(units)]
     ref = {}
     th = threading.Thread(target=lambda: ref.update(enumerate(O.digest_jobs(jobs, workers))), daemon=True)

@@ -132,16 +132,15 @@ __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, 
 }
 
 // One step of the parse at `cur` (wave-uniform) covers DF_NP x 64 positions (lane l holds positions cur + 64 h + l,
-// h < DF_NP): every position looks for a match (cand: an earlier position) and extends it by itself up to LX bytes,
-// then a greedy walk over the positions (wave-uniform, one iteration per match) picks the tokens: literals up to the
-// next position with a match, that match, and on after its end — so a step takes every match that starts in its
-// positions (records with many short matches, e.g. BAM, took one step per match), and a step of literals covers
-// 256 bytes (random FASTQ bases are literals).  A match that reached LX is extended by the whole wave (64 bytes per
-// round, up to MAX_MATCH).  The later positions' candidates were looked up before this step's earlier positions
-// were hashed in: the tokens differ from a position-by-position greedy parse, never in validity (every match is
-// verified); the host restatement (tests/deflate_host.cpp) deflates the golden FASTQ to the same ratio with 3.6x
-// fewer steps than one match per step.
-constexpr int LX = 32;
+// h < DF_NP): every position looks for a match (cand: an earlier position), then a greedy walk over the positions
+// (wave-uniform, one iteration per match) picks the tokens: literals up to the next position with a match, that
+// match — extended by the whole wave, 64 bytes per round, up to MAX_MATCH — and on after its end.  So a step takes
+// every match its positions start (records with many short matches, e.g. BAM, took one step per match), and a
+// step of literals covers 256 bytes (random FASTQ bases are literals).  The later positions' candidates were looked
+// up before this step's earlier positions were hashed in: the tokens differ from a position-by-position greedy
+// parse, never in validity (every match is verified); the host restatement (tests/deflate_host.cpp) deflates the
+// golden FASTQ to the same ratio in 3.6x fewer steps than one match per step.  (Each position extending its own
+// candidate before the walk cost three times the time on runs of matches: round 4, `scripts/bgzf_rate.py`.)
 struct Step {
   int next;                          // the position after the step's last token
   uint64_t lit[DF_NP], ms[DF_NP];    // positions 64 h + lane holding a literal / starting a match
@@ -150,7 +149,7 @@ struct Step {
 
 __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane) {
   int cand[DF_NP], len[DF_NP];
-  uint64_t M[DF_NP], C[DF_NP];
+  uint64_t M[DF_NP];
 #pragma unroll
   for (int h = 0; h < DF_NP; h++) {
     const int p = cur + 64 * h + lane;
@@ -164,27 +163,9 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
         if (j >= 0 && match7(s, p, w, j)) c = j;
       }
     }
-    int L = 0;
-    bool capped = false;
-    if (c >= 0) {   // the position's own extension, four bytes at a time, up to LX (or the end of the slice)
-      const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH;
-      const int lim = cap < LX ? cap : LX;
-      L = MIN_MATCH;
-      while (L < lim) {
-        const uint32_t x = load4(s, p + L) ^ load4(s, c + L);
-        if (x) {
-          L += (int)(__builtin_ctz(x) >> 3);
-          break;
-        }
-        L += 4;
-      }
-      if (L > lim) L = lim;
-      capped = L == LX && lim < cap;
-    }
     cand[h] = c;
-    len[h] = L;
+    len[h] = 0;
     M[h] = __ballot(c >= 0);
-    C[h] = __ballot(capped);
   }
   const int NW = 64 * DF_NP;
   const int W = S - cur < NW ? S - cur : NW;
@@ -211,32 +192,29 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
       break;
     }
     const int hm = m >> 6, l = m & 63;
-    int L = 0, jc = 0;
-    bool cp = false;
+    int jc = 0;
 #pragma unroll
     for (int h = 0; h < DF_NP; h++)
       if (h == hm) {
         st.ms[h] |= 1ull << l;
-        L = __builtin_amdgcn_readlane(len[h], l);
         jc = __builtin_amdgcn_readlane(cand[h], l);
-        cp = (C[h] >> l) & 1ull;
       }
-    if (cp) {   // a long match: the whole wave extends it
-      const int q = cur + m;
-      const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
-      for (;;) {
-        const int k = L + lane;
-        const bool eq = k < cap && s[q + k] == s[jc + k];
-        const uint64_t ne = ~__ballot(eq);
-        const int run = ne ? __builtin_ctzll(ne) : 64;
-        L += run;
-        if (run < 64 || L >= cap) break;
-      }
-      if (L > cap) L = cap;
-#pragma unroll
-      for (int h = 0; h < DF_NP; h++)
-        if (h == hm && lane == l) len[h] = L;
+    // the match extended by the whole wave, 64 bytes per round (up to MAX_MATCH)
+    const int q = cur + m;
+    const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
+    int L = MIN_MATCH;
+    for (;;) {
+      const int k = L + lane;
+      const bool eq = k < cap && s[q + k] == s[jc + k];
+      const uint64_t ne = ~__ballot(eq);
+      const int run = ne ? __builtin_ctzll(ne) : 64;
+      L += run;
+      if (run < 64 || L >= cap) break;
     }
+    if (L > cap) L = cap;
+#pragma unroll
+    for (int h = 0; h < DF_NP; h++)
+      if (h == hm && lane == l) len[h] = L;
     x = m + L;
     if (x >= W) {
       st.next = cur + x;

@@ -27,24 +27,20 @@ struct Tok {
 
 int g_steps = 0;   // parse steps (the device's cost unit), reported on stderr
 
-// mh_deflate.hip's parse, one step = 64 positions: every position's candidate from the table as it was at the
-// step's start (or the run at distance 1), each extended alone up to LX bytes; a greedy walk takes the step's
-// matches in order (literals between); a match that reached LX is extended to its end
+// mh_deflate.hip's parse: one step covers SW = DF_NP x 64 positions; every position's candidate from the table as it
+// was at the step's start (or the run at distance 1); a greedy walk takes the step's matches in order (literals
+// between), each extended to its end
 std::vector<Tok> parse(const uint8_t *s, int S) {
-  constexpr int LX = 32;
   const int SW = getenv("DF_SW") ? atoi(getenv("DF_SW")) : 256;   // positions per step (mh_deflate.hip DF_NP x 64)
   std::vector<uint32_t> ht(1 << HB, 0);
   std::vector<Tok> out;
+  std::vector<int> cand(SW);
   for (int cur = 0; cur < S;) {
     g_steps++;
     const int W = S - cur < SW ? S - cur : SW;
-    int cand[128], len[128];
-    bool capped[128];
     for (int l = 0; l < SW; l++) {
       const int p = cur + l;
       cand[l] = -1;
-      len[l] = 0;
-      capped[l] = false;
       if (l >= W || p + MIN_MATCH > S) continue;
       const uint32_t w = load4(s, p);
       auto match = [&](int c) { return std::memcmp(s + p, s + c, MIN_MATCH) == 0; };
@@ -53,13 +49,6 @@ std::vector<Tok> parse(const uint8_t *s, int S) {
       } else {
         const int c = (int)ht[hash4(w)] - 1;
         if (c >= 0 && match(c)) cand[l] = c;
-      }
-      if (cand[l] >= 0) {
-        const int cap = S - p < MAX_MATCH ? S - p : MAX_MATCH, lim = cap < LX ? cap : LX;
-        int L = MIN_MATCH;
-        while (L < lim && s[p + L] == s[cand[l] + L]) L++;
-        len[l] = L;
-        capped[l] = L == LX && lim < cap;
       }
     }
     int x = 0, next = cur + W;
@@ -71,12 +60,9 @@ std::vector<Tok> parse(const uint8_t *s, int S) {
         next = cur + W;
         break;
       }
-      const int q = cur + m, j = cand[m];
-      int L = len[m];
-      if (capped[m]) {
-        const int cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
-        while (L < cap && s[q + L] == s[j + L]) L++;
-      }
+      const int q = cur + m, j = cand[m], cap = S - q < MAX_MATCH ? S - q : MAX_MATCH;
+      int L = MIN_MATCH;
+      while (L < cap && s[q + L] == s[j + L]) L++;
       out.push_back({-1, L, q - j});
       x = m + L;
       next = cur + x;
