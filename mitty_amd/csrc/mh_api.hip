@@ -227,7 +227,6 @@ CorruptCfg corrupt_cfg(const mh_ctx *ctx, uint64_t unit_key, int64_t t_base) {
   cc.bk = (const uint8_t *)(base + ctx->corrupt_bk_off);
   cc.T16 = (const uint16_t *)(base + ctx->corrupt_T16_off);
   cc.Fp16 = (const uint16_t *)(base + ctx->corrupt_Fp16_off);
-  cc.TP = (const uint16_t *)(base + ctx->corrupt_TP_off);
   return cc;
 }
 }  // namespace mh
@@ -289,12 +288,6 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   ctx->gate_at = ge ? atoi(ge) : -1;
   const char *hf = getenv("MH_HAP_FWD");
   ctx->hap_fwd = hf && atoi(hf) != 0;
-  const char *ef = getenv("MH_EW_FLAT");
-  ctx->ew_flat = ef && atoi(ef) != 0;
-  const char *eg = getenv("MH_EW_GATHER4");
-  ctx->ew_dbg = eg && atoi(eg) ? 512 : 0;   // (EW_GATHER4)
-  const char *cf = getenv("MH_CR_FUSED");
-  ctx->cr_fused = cf && atoi(cf) != 0;
   const char *so = getenv("MH_SORT");
   ctx->sort_lsd = so && !strcmp(so, "lsd");
   const char *gt = getenv("MH_WRITER_GATE_TAIL");
@@ -1132,23 +1125,12 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
       bk[r * mh::CB_ROW + k] = (uint8_t)((lo < 93 ? lo : 93) | (lo < 93 && g[k + 1] > lo ? 0x80 : 0));
     }
   }
-  // the threshold-pair rows (the row pass builds them in LDS per column; the fused writer reads them from here):
-  // entry k = T's low byte | the next entry's low byte << 8 when both share their high byte (else 0xff), the last
-  // of the first min(n_bq, 93) entries paired with 0xffff
-  std::vector<uint16_t> TP(nt);
-  const int lim_all = n_bq < 93 ? n_bq : 93;
-  for (size_t r = 0; r < (size_t)2 * max_bp; r++)
-    for (int k = 0; k < n_bq; k++) {
-      const uint32_t a = T16[r * n_bq + k], c = k + 1 < lim_all ? T16[r * n_bq + k + 1] : 0xffffu;
-      TP[r * n_bq + k] = (uint16_t)((a & 0xffu) | ((c >> 8) == (a >> 8) ? (c & 0xffu) << 8 : 0xff00u));
-    }
   auto al16 = [](size_t x) { return ((x + 15) / 16) * 16; };
   ctx->corrupt_guide_off = al16(8 * nt);
   ctx->corrupt_bk_off = al16(ctx->corrupt_guide_off + 2 * guide.size());
   ctx->corrupt_T16_off = al16(ctx->corrupt_bk_off + bk.size());
   ctx->corrupt_Fp16_off = al16(ctx->corrupt_T16_off + 2 * nt);
-  ctx->corrupt_TP_off = al16(ctx->corrupt_Fp16_off + 2 * 100);
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_TP_off + 2 * nt + 64));
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_Fp16_off + 2 * 100 + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
   char *base = (char *)ctx->corrupt_cum.p;
   HIPCHK(ctx, hipMemcpyAsync(base, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
@@ -1157,7 +1139,6 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_bk_off, bk.data(), bk.size(), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_T16_off, T16.data(), 2 * nt, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp16_off, Fp16.data(), 2 * 100, hipMemcpyHostToDevice, ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_TP_off, TP.data(), 2 * nt, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;

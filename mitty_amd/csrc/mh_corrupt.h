@@ -37,7 +37,6 @@ struct CorruptCfg {
   const uint8_t *bk = nullptr;       // [2][max_bp][CB_ROW]: min(entries below k / 256, 93) | 0x80 (one inside)
   const uint16_t *T16 = nullptr;     // [2][max_bp][n_bq]: min(floor(cum * 2^16), 65535)
   const uint16_t *Fp16 = nullptr;    // [100]: min(floor(phred_p * 2^16), 65535)
-  const uint16_t *TP = nullptr;      // [2][max_bp][n_bq]: threshold pairs (mh_set_corruption), the fused writer's
 };
 
 // a ^ b ^ k in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96; the compiler emits two v_xor_b32 for

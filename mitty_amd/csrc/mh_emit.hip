@@ -579,9 +579,6 @@ __global__ void __launch_bounds__(EW_THREADS) k_emit_write(HapView h, int64_t m,
 //         first and last chunks are byte stores of the tile's own bytes (the neighbouring tiles own the rest).
 // With corruption the records carry len(seq) placeholder qualities and the writer also leaves each record's
 // first-base offset for k_cr_inplace.
-// writer variants (TArgs.dbg; the bytes are the same): seam chunks stored by the seam pass (no LDS for them, 4 KB
-// less per workgroup; always with the corruption rows), and every thread gathering (MH_EW_GATHER4, experiment)
-constexpr int32_t EW_SEAM_PASS = 256, EW_GATHER4 = 512;
 constexpr int ED_T = 32;
 constexpr int ED_THREADS = 256;
 constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads of masked-out bytes stay in range)
@@ -649,7 +646,7 @@ struct QHead {
 // The output sweeps of a 32-template tile whose strings and metadata are in LDS: LPR lanes per record (record
 // r = file f, template j), passes over the tile's NF * ED_T records.  gbase: arena offset of the tile's first byte per
 // file; span: the tile's bytes per file.
-template <int NF, int LPR, int CR, int FL>
+template <int NF, int LPR, int CR>
 __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64_t gbase[2], const int32_t span[2],
                                           int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -717,41 +714,6 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
   // (an LDS-only barrier here — the ragged-edge byte stores above need not land before the chunk sweep — measured no
   // faster than the full one, round 3)
   if (staged) __syncthreads();
-  if (FL) {
-    // flat sweep (FL): the tile's whole chunks per file in address order, consecutive lanes on consecutive chunks (a
-    // wave-instruction stores 1 KiB of contiguous lines instead of 16 records' 64-byte pieces); a chunk's record is
-    // the last one starting before the chunk's end (binary search over the tile's record starts), its seam or part
-    // as in the record-major sweep below
-    for (int f = 0; f < NF; f++) {
-      const int64_t g0 = gbase[f];
-      char *const out = arena[f];
-      const int64_t cend = (g0 + span[f]) >> 4;
-      for (int64_t cg = ((g0 + 15) >> 4) + tid; cg < cend; cg += ED_THREADS) {
-        const int32_t x = (int32_t)((cg << 4) - g0);
-        int lo = 0, hi = nt - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (meta[mid].rel[f] <= x + 15) lo = mid; else hi = mid - 1;
-        }
-        const DMeta &M = meta[lo];
-        const int32_t x0 = x - M.rel[f];
-        const int32_t sb = M.sb, tl = sb + M.S[f];
-        const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
-        if (b >= 0 && !staged) continue;                        // seam chunk, stored by the seam pass
-        uint4 v;
-        if (CR < 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
-          v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);
-        } else {
-          const int32_t src = b >= 0 ? o_s + ((f * ED_T + lo) * 4 + b) * 16
-                                     : (x0 + 16 <= sb ? M.qb + x0
-                                                      : (x0 + 16 <= tl ? M.bb[f] + (x0 - sb) : M.tb[f] + (x0 - tl)));
-          v = lds_load16(smem, (uint32_t)src);
-        }
-        *(uint4 *)(out + (cg << 4)) = v;
-      }
-    }
-    return;
-  }
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
     const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
@@ -813,17 +775,10 @@ struct TArgs {
   int64_t cnt_base;         // templates kept before the emission's first one (cnt numbering)
   uint2 *crec;              // corruption: per record the first base's arena offset and S (k_cr_inplace's words)
   int32_t rlen, win_stride, head, qstride;
-  int32_t dbg;              // writer variants (same bytes): EW_SEAM_PASS, EW_GATHER4
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
   const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
-  CorruptCfg cc;            // CR 3: the rows computed in the writer (its tables from global memory)
 };
-
-// one corruption row slot (defined with k_cr_cols below)
-__device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const uint16_t *t8p, uint32_t otp,
-                                        const uint16_t *fp16, const CorruptCfg &cc, uint2 key, uint32_t tl,
-                                        uint32_t th, int f, int n0, int cnt, uint4 *qo_, uint32_t *code_);
 
 // node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
 // array of nodes would be placed in scratch)
@@ -844,7 +799,7 @@ __device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const u
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
-template <int NF, int LPR, int CR, int FL>
+template <int NF, int LPR, int CR>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
@@ -860,7 +815,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
   // seam chunks through LDS (in order with the others); CR 2 stores them from the seam pass (4 KB less LDS: with the
   // per-record T strings that is 5 instead of 4 workgroups per CU, 0.77 vs 0.73 G/s on the corrupt bench)
-  const bool staged = !(A.dbg & EW_SEAM_PASS) && CR < 2;
+  const bool staged = CR != 2;
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
@@ -874,7 +829,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   // CR 2: the tile's row slots (file f, template j, block b: slot f * ED_T * nb + j * nb + b), the first RK per thread
   // loaded before the gathers so they are in flight with them
   constexpr int RK = 3;
-  const int32_t nb = CR >= 2 ? A.nb : 1, nsl = NF * ED_T * nb;
+  const int32_t nb = CR == 2 ? A.nb : 1, nsl = NF * ED_T * nb;
   auto slot_g = [&](int32_t sl, int *sf, int *sj, int *sb_) -> int64_t {
     const int f = sl / (ED_T * nb), rem = sl - f * ED_T * nb, j = rem / nb;
     *sf = f;
@@ -894,92 +849,9 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       rcw[k] = A.ccode[g];
     }
   }
-  // CR 3: the tile's row slots computed here, as k_cr_cols computes them (slot s: block s / (NF * ED_T), then file,
-  // then template, so a wave's lanes share a block and its table rows; the tables are read from global memory)
-  auto slot3 = [&](int32_t sl, int *sf, int *sj, int *sb_) __attribute__((always_inline)) {
-    const int b = sl / (NF * ED_T), rem = sl - b * (NF * ED_T), f = rem / ED_T;
-    *sf = f;
-    *sj = rem - f * ED_T;
-    *sb_ = b;
-  };
-  auto compute3 = [&](int32_t sl, uint4 *q, uint32_t *code) __attribute__((always_inline)) {
-    int f, j, b;
-    slot3(sl, &f, &j, &b);
-    *q = make_uint4(0u, 0u, 0u, 0u);
-    *code = 0u;
-    if (j >= nt) return;
-    const int n0 = ED_CRB * b, cnt = A.rlen - n0 < ED_CRB ? A.rlen - n0 : ED_CRB;
-    const int64_t tt = t0 + j + A.cc.t_base, row = (int64_t)f * A.cc.max_bp + n0;
-    cr_slot(A.cc.bk, (uint32_t)(row * CB_ROW), A.cc.TP, (uint32_t)(row * A.cc.n_bq), A.cc.Fp16, A.cc,
-            make_uint2(A.cc.k0, A.cc.k1), (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, q, code);
-  };
-  if (CR == 3) {
-    static_assert(RK == 3, "the fused rows' registers");
-    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
-    uint32_t w0 = 0u, w1 = 0u, w2 = 0u;
-#pragma nounroll
-    for (int k = 0; k < RK; k++) {   // one copy of the row code; the results into named registers (k is uniform)
-      uint4 q = make_uint4(0u, 0u, 0u, 0u);
-      uint32_t c = 0u;
-      if (tid + k * ED_THREADS < nsl) compute3(tid + k * ED_THREADS, &q, &c);
-      if (k == 0) {
-        r0 = q;
-        w0 = c;
-      } else if (k == 1) {
-        r1 = q;
-        w1 = c;
-      } else {
-        r2 = q;
-        w2 = c;
-      }
-    }
-    rq[0] = r0;
-    rq[1] = r1;
-    rq[2] = r2;
-    rcw[0] = w0;
-    rcw[1] = w1;
-    rcw[2] = w2;
-  }
-  if (A.dbg & EW_GATHER4) {
-    // (MH_EW_GATHER4, experiment) every thread gathers: window slots s = tid + 256 k (window s / chunks, chunk
-    // s % chunks of the tile's 64 windows), issued before anything else so wave 0's metadata loads and formatting
-    // overlap them; no redundant loads for unused chunks
-    uint4 wv[6];
-    int32_t dst[6];
-    bool rv[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const int s_ = tid + ED_THREADS * k;
-      const bool inr = s_ < 2 * ED_T * chunks;
-      const int w = inr ? s_ / chunks : 0, c = s_ - chunks * w, jg = w >> 1, sg = w & 1;
-      const bool kg = inr && jg < nt;
-      const int64_t pg = kg ? (sg ? A.pos1[t0 + jg] : A.pos0[t0 + jg]) : h.p_min;
-      int64_t ag = pg - h.p_min, eg = pg + A.rlen - h.p_min;
-      if (eg > h.hap_len) eg = h.hap_len;
-      if (ag > h.hap_len) ag = h.hap_len;
-      const int64_t lg = eg > ag ? eg - ag : 0;
-      const bool rev = sg && h.rc == nullptr;
-      const int64_t a2g = sg && !rev ? h.hap_len - ag - lg : ag;
-      const int64_t a16 = a2g & ~(int64_t)15;
-      const int32_t cmax = lg > 0 ? (int32_t)(((a2g + lg - 1) >> 4) - (a16 >> 4)) : 0;
-      const bool u = kg && a16 + 16 * c < a2g + lg;
-      wv[k] = *(const uint4 *)((sg && !rev ? h.rc : h.hap) + a16 + (u ? 16 * c : 0));
-      dst[k] = u ? o_win + w * win_stride + 16 * (rev ? cmax - c : c) : o_dump;
-      rv[k] = rev;
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      if (tid + ED_THREADS * k >= 2 * ED_T * chunks) break;
-      uint4 v = wv[k];
-      if (rv[k])
-        v = make_uint4(comp4(__builtin_bswap32(v.w)), comp4(__builtin_bswap32(v.z)), comp4(__builtin_bswap32(v.y)),
-                       comp4(__builtin_bswap32(v.x)));
-      *(uint4 *)(smem + dst[k]) = v;
-    }
-  }
   for (int i = tid; i < TL; i += ED_THREADS)
     smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
-  if (tid >= 64 && !(A.dbg & EW_GATHER4)) {
+  if (tid >= 64) {
     // waves 1-3: the gathers (three threads per mate window), all in flight together; an unused chunk re-reads the
     // first one
     const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
@@ -1114,7 +986,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
                                 : h.rc ? (int32_t)((h.hap_len - a - S) & 15) : (int32_t)((-(a + S)) & 15);
         mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + lead;
         mt.S[fr] = S;
-        mt.tb[fr] = CR >= 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
+        mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
         if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
           mt.qb = qb;
@@ -1133,12 +1005,12 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     }
   }
   __syncthreads();
-  if (CR >= 2) {
+  if (CR == 2) {
     // each row slot of a kept record: its qualities into the record's T, its substitutions into the window
     // (base_rot[b][code - 1], illumina.py:131-136,159-160); block 0 also writes T's separators
     auto lay = [&](int32_t sl, uint4 q, uint32_t code) {
       int f, j, b;
-      if (CR == 3) slot3(sl, &f, &j, &b); else (void)slot_g(sl, &f, &j, &b);
+      (void)slot_g(sl, &f, &j, &b);
       if (j >= nt) return;
       const DMeta &M = meta[j];
       if (M.len[f] == 0) return;
@@ -1177,30 +1049,23 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     for (int k = 0; k < RK; k++)
       if (tid + k * ED_THREADS < nsl) lay(tid + k * ED_THREADS, rq[k], rcw[k]);
     for (int32_t sl = tid + RK * ED_THREADS; sl < nsl; sl += ED_THREADS) {   // (records of more than 23 blocks)
-      if (CR == 3) {
-        uint4 q;
-        uint32_t code;
-        compute3(sl, &q, &code);
-        lay(sl, q, code);
-      } else {
-        int sf, sj, sbk;
-        const int64_t g = slot_g(sl, &sf, &sj, &sbk);
-        lay(sl, A.crow[g], A.ccode[g]);
-      }
+      int sf, sj, sbk;
+      const int64_t g = slot_g(sl, &sf, &sj, &sbk);
+      lay(sl, A.crow[g], A.ccode[g]);
     }
     __syncthreads();
   }
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
-  ed_output<NF, LPR, CR, FL>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena);
+  ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena);
 }
 
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
 // waves per SIMD instead of eight — and the launch of 184 k workgroups costs only ~0.35 ms of a 2.6 ms chr1-unit
 // writer (round 3), so there is no persistent variant.)
-template <int NF, int LPR, int CR, int FL>
+template <int NF, int LPR, int CR>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
-  emit_tile<NF, LPR, CR, FL>(A, qh, blockIdx.x);
+  emit_tile<NF, LPR, CR>(A, qh, blockIdx.x);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -1642,8 +1507,10 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, c
 }
 
 // One corruption row slot: the qualities (+ 33) and substitution codes of block n0 / 15 of template (tl, th)'s file f
-// (cnt bases: a full block, or the short last one) — k_cr_cols' item, and the fused writer's (CR 3).  bk / t8p: the
-// bucket and threshold-pair rows of base n0 (LDS or global), fp16 the u16 substitution thresholds.
+// (cnt bases: a full block, or the short last one) — k_cr_cols' item.  bk / t8p: the bucket and threshold-pair
+// tables, obk / otp the offsets of base n0's rows in them (a 32-bit offset from a uniform base), fp16 the u16
+// substitution thresholds.  (The same item computed inside the writer instead of a pass before it — its tables then
+// in global memory, 115 VGPRs — was slower: 0.69 vs 0.78 G/s on configs[2], round 4.)
 __device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const uint16_t *t8p, uint32_t otp,
                                         const uint16_t *fp16, const CorruptCfg &cc, uint2 key, uint32_t tl,
                                         uint32_t th, int f, int n0, int cnt, uint4 *qo_, uint32_t *code_) {
@@ -1793,11 +1660,6 @@ static int32_t cr_rows_alloc(mh_ctx *ctx, int64_t m, int32_t nf, int64_t rlen) {
 // serves every unit, in stream order; the pass on a stream of its own beside the previous writer was within noise)
 static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf, int32_t rlen, const CorruptCfg &cc,
                                TArgs &A) {
-  if (ctx->cr_fused) {   // CR 3: the writer computes its tile's rows itself
-    A.cc = cc;
-    A.nb = (rlen + CI_BLK - 1) / CI_BLK;
-    return MH_OK;
-  }
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (ctx->cr_rows.cap < (size_t)(m * nf * NB) * 16 + 64 || ctx->cr_codes.cap < (size_t)(m * nf * NB) * 4 + 64)
     return arg_fail(ctx, MH_E_STATE, "corruption rows not allocated");
@@ -1927,21 +1789,16 @@ static int64_t digit_sum_host(int64_t K) {
 // writing the same column land on 32 different LDS banks instead of 8
 constexpr int32_t ED_QPAD = 4;
 // the direct writer's instantiation: CR mode (0 perfect, 1 in-place corruption after it, 2 corruption rows), one or
-// two files, the flat output sweep (mh_ctx::ew_flat, experiment)
+// two files
 using EwKernel = void (*)(TArgs, QHead);
-static EwKernel ew_kernel(int cr, bool two, bool flat) {
-  if (cr == 3) return two ? k_emit_tiles<2, 4, 3, 0> : k_emit_tiles<1, 8, 3, 0>;
-  if (flat)
-    return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 1> : k_emit_tiles<1, 8, 2, 1>)
-           : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 1> : k_emit_tiles<1, 8, 1, 1>)
-                     : (two ? k_emit_tiles<2, 4, 0, 1> : k_emit_tiles<1, 8, 0, 1>);
-  return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 0> : k_emit_tiles<1, 8, 2, 0>)
-         : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 0> : k_emit_tiles<1, 8, 1, 0>)
-                   : (two ? k_emit_tiles<2, 4, 0, 0> : k_emit_tiles<1, 8, 0, 0>);
+static EwKernel ew_kernel(int cr, bool two) {
+  return cr == 2 ? (two ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
+         : cr == 1 ? (two ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
+                   : (two ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
 }
 
-static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows, int32_t dbg) {
-  const bool staged = !(dbg & EW_SEAM_PASS) && !rows;   // (seam chunks stored by the seam pass: no LDS for them)
+static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows) {
+  const bool staged = !rows;   // (rows: the seam chunks stored by the seam pass, no LDS for them)
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
@@ -2141,7 +1998,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
   const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows, ctx->ew_dbg);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   QHead qh{};
   const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
   if (head_fits) {
@@ -2152,7 +2009,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   }
   if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
       cnt_base + m < (int64_t)UINT32_MAX) {
-    if (cr_rows && !ctx->cr_fused) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
+    if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
     // and the next job's sampling overlap it
     if (!writer_dep) {
@@ -2172,13 +2029,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     }
     ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
-    const int ew_dbg = ctx->ew_dbg;
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
-            qstride, ew_dbg};
+            qstride};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
-    auto kfn = ew_kernel(cr_rows ? (ctx->cr_fused ? 3 : 2) : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
+    auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
     hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ctx->wstream, A, qh);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -2412,7 +2268,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
   const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows, ctx->ew_dbg);
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
     return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
   if (!direct || lds_d > 64 * 1024) {
@@ -2487,7 +2343,7 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
   CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
   if (ctx->corrupt_on) cc = corrupt_cfg(ctx, unit_key, 0);
 
-  if (cr_rows && !ctx->cr_fused) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
+  if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
   hipStream_t ws = ctx->wstream;
   HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));   // the unit's templates (main stream) are ready
   HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
@@ -2505,11 +2361,10 @@ int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, c
                                   ctx->scan_partials_w.p, (E3 *)stat));
   stage_end(ctx);
   TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
-          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride,
-          ctx->ew_dbg};
+          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride};
   if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
   stage_begin(ctx, "emit_write");
-  auto kfn = ew_kernel(cr_rows ? (ctx->cr_fused ? 3 : 2) : ctx->corrupt_on ? 1 : 0, write_fastq2, ctx->ew_flat);
+  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
   hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
   HIPCHK(ctx, hipGetLastError());
   stage_end(ctx);

@@ -250,7 +250,6 @@ struct mh_ctx {
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
   size_t corrupt_guide_off = 0;   // byte offsets inside corrupt_cum: the search guide, the Philox-mode bucket table
   size_t corrupt_bk_off = 0, corrupt_T16_off = 0, corrupt_Fp16_off = 0;   // and the u16 tables T16, Fp16
-  size_t corrupt_TP_off = 0;                                               // and the threshold pairs
   uint64_t corrupt_seed = 0;
   // exact corruption stream of mh_corrupt_fastq (mh_corrupt_stream_seed / _state): 0 = Philox; 1 = the stream of
   // RandomState(cx_seed) from output cx_pos on; 2 = continuing the explicit state (cx_key, cx_kpos)
@@ -266,11 +265,9 @@ struct mh_ctx {
   // forward-only haplotypes (MH_HAP_FWD=1, experiment): no reverse-complement copy; the writer reverse-complements
   // mate-1 windows into LDS itself
   bool hap_fwd = false;
-  // experiments read once per context (mh_create), so tests switch them per context: MH_EW_FLAT (flat output sweep),
-  // MH_EW_GATHER4 (the writer's TArgs.dbg bit EW_GATHER4), MH_SORT=lsd (the hand-written permutation sort)
-  bool ew_flat = false, sort_lsd = false;
-  bool cr_fused = false;   // MH_CR_FUSED=1 (experiment): the corruption rows computed inside the writer (CR 3)
-  int32_t ew_dbg = 0;
+  // MH_SORT=lsd (the hand-written permutation sort instead of rocprim's, measured slower: DESIGN.md), read once per
+  // context (mh_create), so tests switch it per context
+  bool sort_lsd = false;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas

@@ -363,19 +363,6 @@ def test_unit_vs_oracle_forward_haplotype(native, monkeypatch, model):
   _unit_vs_oracle(1_200_000, 4000000001, model, n_seed=7, rate=8e-3, start0=98_765)
 
 
-@pytest.mark.parametrize('flat,fwd,g4', [(1, 0, 0), (1, 1, 0), (0, 0, 1), (0, 1, 1), (1, 1, 1)])
-def test_unit_vs_oracle_writer_variants(native, monkeypatch, flat, fwd, g4):
-  """Writer variants: the flat output sweep (MH_EW_FLAT=1: a tile's chunks in address order, each chunk's record
-  found by a binary search over the record starts), every thread gathering (MH_EW_GATHER4=1), with rc and
-  forward-only haplotypes: byte-identical to the oracle, dense variants (long qnames, many seams) and an offset
-  region."""
-  monkeypatch.setenv('MH_EW_FLAT', str(flat))
-  monkeypatch.setenv('MH_EW_GATHER4', str(g4))
-  monkeypatch.setenv('MH_HAP_FWD', str(fwd))
-  assert _unit_vs_oracle(2_000_000, 23, 'hiseq-X-v2.5-Garvan') > 10000
-  _unit_vs_oracle(1_000_000, 4000000002, '1kg-pcr-free', n_seed=9, rate=8e-3, start0=54_321)
-
-
 @pytest.mark.parametrize('sort', ['rocprim', 'lsd'])
 def test_batched_units_vs_oracle(native, monkeypatch, sort):
   """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
@@ -866,11 +853,10 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
   vdf = vcfio.load_variants_soa(G.path('data/syn.vcf'), 'S1', G.path('data/syn.bed'))
   seqs = mfasta.read_fasta(G.path('data/syn.fa'))
   outs = []
-  # (the direct writer with rc or forward-only haplotypes — mirrored mate-1 windows —, with the rows computed inside
-  # it (MH_CR_FUSED), and the LDS-image writer + the in-place pass, mh_set_emit_mode(1))
-  for fwd, fused, lds in ((0, 0, False), (1, 0, False), (0, 1, False), (0, 0, True)):
+  # (the direct writer with rc or forward-only haplotypes — mirrored mate-1 windows — and the LDS-image writer + the
+  # in-place pass, mh_set_emit_mode(1))
+  for fwd, lds in ((0, False), (1, False), (0, True)):
     monkeypatch.setenv('MH_HAP_FWD', str(fwd))
-    monkeypatch.setenv('MH_CR_FUSED', str(fused))
     eng = Engine(0)
     try:
       eng.ctx.set_emit_mode(1 if lds else 0)
@@ -891,20 +877,17 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
 
 
 @pytest.mark.parametrize('tables,write2,fwd', [('lds', True, 0), ('global', True, 0), ('lds', False, 0),
-                                               ('lds', True, 1), ('fused', True, 0), ('fused', False, 1)])
+                                               ('lds', True, 1)])
 def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2, fwd):
   """Philox-mode corruption (the writer's len(seq) layout + k_cr_inplace) byte for byte against the numpy
   restatement of the draw scheme with full 53-bit uniforms (tests/philox_ref.py) applied to the perfect reads of the
   same sampling.  No N in the genome, so every template is kept and cnt - 1 is the template index; the bucket table
-  from LDS and from global memory (MH_CR_GLOBAL), the rows computed inside the writer (MH_CR_FUSED), one and two
-  FASTQ files."""
+  from LDS and from global memory (MH_CR_GLOBAL), one and two FASTQ files."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from tests import philox_ref
   if tables == 'global':
     monkeypatch.setenv('MH_CR_GLOBAL', '1')
-  if tables == 'fused':
-    monkeypatch.setenv('MH_CR_FUSED', '1')
   if fwd:   # forward-only haplotypes: the corruption rows' substitutions land in the mirrored mate-1 windows
     monkeypatch.setenv('MH_HAP_FWD', '1')
   mdl = G.model('hiseq-X-v2.5-Garvan')
