@@ -758,7 +758,7 @@ def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
       for (ps, ri, cpy, _), (n, kept, x1, x2) in zip(batch, res):
         arr1, arr2 = eng.ctx.fetch_output_arrays(o1, x1, o2, x2)
         f1, f2 = hpool.submit(sha, arr1), hpool.submit(sha, arr2)
-        got[ps] = (n, x1, f1, x2, f2)
+        got[ps] = (kept, x1, f1, x2, f2)   # (the oracle digest's first field is the kept-template count)
         o1, o2 = o1 + x1, o2 + x2
       for ps in [u[0] for u in batch]:   # hashed before the arenas are reused
         n, x1, f1, x2, f2 = got[ps]
@@ -771,7 +771,7 @@ def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
       os.remove(f)
     os.rmdir(d)
   bad = [ps for ps in range(len(units)) if got.get(ps) != ref.get(ps)]
-  out = {'units': len(units), 'units_equal': len(units) - len(bad), 'templates': sum(v[0] for v in got.values()),
+  out = {'units': len(units), 'units_equal': len(units) - len(bad), 'templates_kept': sum(v[0] for v in got.values()),
          'fastq_bytes': sum(v[1] + v[3] for v in got.values()), 'oracle_workers': workers,
          'gpu_fetch_hash_s': round(t_gpu, 1), 'seconds': round(time.perf_counter() - t0, 1),
          'method': 'per unit: sha256 of both FASTQ ranges of the arenas (D2H after the unit\'s batch) vs the CPU '

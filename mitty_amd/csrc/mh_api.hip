@@ -1266,7 +1266,8 @@ int32_t mh_stage_times(mh_ctx *ctx, const char **names, double *ms, int32_t cap,
 int32_t mh_bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths) {
   CTX_GUARD(ctx);
   if (n_refs < 0 || (n_refs > 0 && (!names || !lengths))) return arg_fail(ctx, MH_E_ARG, "bad reference list");
-  bam_release(ctx->bam);
+  // a new store (counts reset by bam_set_refs); the device buffers stay for the next job, as everything else does
+  // (freeing and reallocating GBs of them per job stretched a 10-step configs[4] bench from 47 to 481 ms per step)
   return bam_set_refs(ctx, n_refs, names, lengths);
 }
 

@@ -27,4 +27,4 @@ def test_wgs_full_step_every_unit_equals_oracle():
   line = [x for x in r.stdout.splitlines() if x.startswith('{')][-1]
   v = json.loads(line)['verify']
   assert v['units'] == 100 and v['units_equal'] == 100, v
-  assert v['templates'] > 280_000_000 and v['fastq_bytes'] > 200e9, v
+  assert v['templates_kept'] > 280_000_000 and v['fastq_bytes'] > 200e9, v
