@@ -792,34 +792,52 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
 namespace {
 
 // per record: the 16 kbp windows it overlaps take its index unless the record before already overlaps them (that
-// one is earlier: a window's first record wins, with few atomics per window); a reference's window count
+// one is earlier: a window's first record wins, with few atomics per window); a reference's window count is the
+// wave's max per reference, one atomic per wave and reference (one per record, all on one word, took 200 ms for a
+// configs[4] store of 17 M records, round 4)
 __global__ void k_bai_mark(const RInfo *info, int64_t n, const int64_t *woff, int32_t n_refs, uint32_t *lin,
                            uint32_t *nwin, int32_t *bad) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const RInfo r = info[k];
-  if (r.tid < 0 || r.tid >= n_refs || r.beg < 0 || r.bin >= 37450u) {
-    atomicOr(bad, 1);
-    return;
-  }
-  const int64_t w0 = r.beg >> 14, w1 = (int64_t)(r.end - 1) >> 14;
-  if (w1 < 0) return;
-  if (w1 >= woff[r.tid + 1] - woff[r.tid]) {
-    atomicOr(bad, 2);
-    return;
-  }
-  int64_t from = w0;
-  if (k > 0) {
-    const RInfo q = info[k - 1];
-    if (q.tid > r.tid || (q.tid == r.tid && q.beg > r.beg)) atomicOr(bad, 4);   // (the store is sorted)
-    if (q.tid == r.tid && q.end - 1 >= q.beg) {
-      const int64_t p0 = q.beg >> 14, p1 = (int64_t)(q.end - 1) >> 14;
-      if (p0 <= w0 && p1 >= w0) from = p1 + 1;   // windows [w0, p1] already have an earlier record
+  const int lane = threadIdx.x & 63;
+  int mt = -1;          // this record's reference, when it has windows
+  uint32_t my = 0;      // its window count (last window + 1)
+  if (k < n) {
+    const RInfo r = info[k];
+    if (r.tid < 0 || r.tid >= n_refs || r.beg < 0 || r.bin >= 37450u) {
+      atomicOr(bad, 1);
+    } else {
+      const int64_t w0 = r.beg >> 14, w1 = (int64_t)(r.end - 1) >> 14;
+      if (w1 >= woff[r.tid + 1] - woff[r.tid]) {
+        atomicOr(bad, 2);
+      } else if (w1 >= 0) {
+        int64_t from = w0;
+        if (k > 0) {
+          const RInfo q = info[k - 1];
+          if (q.tid > r.tid || (q.tid == r.tid && q.beg > r.beg)) atomicOr(bad, 4);   // (the store is sorted)
+          if (q.tid == r.tid && q.end - 1 >= q.beg) {
+            const int64_t p0 = q.beg >> 14, p1 = (int64_t)(q.end - 1) >> 14;
+            if (p0 <= w0 && p1 >= w0) from = p1 + 1;   // windows [w0, p1] already have an earlier record
+          }
+        }
+        uint32_t *L = lin + woff[r.tid];
+        for (int64_t w = from; w <= w1; w++) atomicMin(&L[w], (uint32_t)k);
+        mt = r.tid;
+        my = (uint32_t)(w1 + 1);
+      }
     }
   }
-  uint32_t *L = lin + woff[r.tid];
-  for (int64_t w = from; w <= w1; w++) atomicMin(&L[w], (uint32_t)k);
-  atomicMax(&nwin[r.tid], (uint32_t)(w1 + 1));
+  uint64_t rem = __ballot(mt >= 0);
+  while (rem) {   // per reference present in the wave (sorted records: usually one), its max by a butterfly
+    const int t = __shfl(mt, __builtin_ctzll(rem), 64);
+    uint32_t v = mt == t ? my : 0u;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
+      v = o > v ? o : v;
+    }
+    if (lane == __builtin_ctzll(rem)) atomicMax(&nwin[t], v);
+    rem &= ~__ballot(mt == t);
+  }
 }
 
 __device__ __forceinline__ bool run_start(const RInfo *info, int64_t k) {

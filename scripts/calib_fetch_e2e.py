@@ -60,7 +60,39 @@ def main():
       eng.ctx.fetch_wait(pend)
       return moved
 
+    def async_timed(both):   # as the e2e leg runs it: stage timing on (each fetch is an 'output_d2h' stage)
+      eng.ctx.enable_timing(True)
+      try:
+        return async_fetch(both)
+      finally:
+        eng.ctx.enable_timing(False)
+
+    def async_writer(both):   # ... and each chunk handed to the two file-writer threads (/dev/null)
+      from mitty_amd.lib.fastq_stream import PairWriter
+      from mitty_amd.lib.fastq_stream import FastqSink
+      sinks = [FastqSink('/dev/null', 1, 1, False), FastqSink('/dev/null', 1, 1, False)]
+      pw = PairWriter(sinks)
+      moved, pend = 0, None
+      try:
+        for k, off in enumerate(range(0, min(u1, u2) - CH, CH)):
+          pw.wait(k % 2)
+          t, (d1, d2) = eng.ctx.fetch_range_async(pins[k % 2], off, CH, off, CH if both else 0)
+          if pend is not None:
+            eng.ctx.fetch_wait(pend[0])
+            pw.submit(*pend[1:])
+          pend = (t, k % 2, [d1, d2 if both else None])
+          moved += CH * (2 if both else 1)
+        eng.ctx.fetch_wait(pend[0])
+        pw.submit(*pend[1:])
+        pw.close()
+      finally:
+        for x in sinks:
+          x.close()
+      return moved
+
     run('sync_two_files', sync_fetch)
+    run('async_two_timed', async_timed)
+    run('async_two_writer', async_writer)
     run('sync_one_file', sync_fetch, False)
     run('async_two_files', async_fetch)
     run('async_one_file', async_fetch, False)
