@@ -328,7 +328,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
   for (auto &b : ctx->pb) release(b);
   release(ctx->pb_tmp);
-  release(ctx->gz_slots); release(ctx->gz_info); release(ctx->gz_off); release(ctx->gz_scan); release(ctx->gz_out);
+  release(ctx->gz_slots); release(ctx->gz_tok); release(ctx->gz_info); release(ctx->gz_off); release(ctx->gz_scan); release(ctx->gz_out);
   release(ctx->gz_in);
   for (auto &b : ctx->s) release(b);
   for (auto &b : ctx->lane2) release(b);

@@ -14,8 +14,9 @@
 //   pass 1  the parse, counting symbol frequencies;
 //   codes   lane 0: length-limited Huffman lengths (15 bits; 7 for the code-length code), canonical codes, the
 //           dynamic header (mh_deflate.h, host-testable);
-//   pass 2  the same parse again, each step's codes placed by a wave prefix sum of their bit lengths into an LDS
-//           staging strip, whole words flushed to the slice's region of the block's slot;
+//   pass 2  pass 1's tokens (kept per wave in global memory: each step's position masks and its matches), each
+//           step's codes placed by wave prefix sums of their bit lengths into an LDS staging strip, whole words
+//           flushed to the slice's region of the block's slot;
 //   CRC-32  every thread a 128-byte segment, combined over a tree (x^(8n) operators).
 // A block whose codes would not fit a BGZF block, or not be smaller than its bytes, is stored instead.
 // k_bgzf_pack then writes the blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets
@@ -38,6 +39,12 @@ constexpr int HBITS = 11;
 constexpr int REGION = 9216;                // a slice's output bytes in the slot (more: the block is stored)
 constexpr int SLOT = DF_WAVES * REGION;
 constexpr int DF_NP = 4;                    // parse positions per lane and step (a step covers 256 positions)
+// pass 1's tokens, kept for pass 2 (global memory, per wave): per step its end and position masks (TSW words), then
+// the matches packed (length | distance << 9).  A step covers >= 256 positions but the last, a match >= 7 bytes.
+constexpr int TSW = 1 + 4 * DF_NP;
+constexpr int TOK_STEPS = (SLICE + 64 * DF_NP - 1) / (64 * DF_NP) + 1;
+constexpr int TOK_MATCHES = SLICE / 7 + 1;
+constexpr int TOK_WORDS = ((TOK_STEPS * TSW + TOK_MATCHES) + 63) / 64 * 64;
 // staging words: a step's codes (at most 256 literals of <= 15 bits: a match of <= 48 bits stands for >= 7
 // positions), a carried word, slack
 constexpr int STAGE = (64 * DF_NP * 15 + 31) / 32 + 8;
@@ -334,8 +341,55 @@ __device__ __forceinline__ void encode_step(const uint8_t *s, int cur, const Ste
   flush_bits(bw, W.stage, before - (int)(bw.bitpos & 31), lane);
 }
 
+// pass 1: a step's tokens into the wave's token area (step record, then its matches in position order)
+__device__ __forceinline__ void keep_step(uint32_t *tok, int step, int *nm, const Step &st, int lane) {
+  uint32_t v = (uint32_t)st.next;
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    if (lane == 1 + 2 * h) v = (uint32_t)st.lit[h];
+    if (lane == 2 + 2 * h) v = (uint32_t)(st.lit[h] >> 32);
+    if (lane == 1 + 2 * DF_NP + 2 * h) v = (uint32_t)st.ms[h];
+    if (lane == 2 + 2 * DF_NP + 2 * h) v = (uint32_t)(st.ms[h] >> 32);
+  }
+  if (lane < TSW) tok[step * TSW + lane] = v;
+  uint32_t *mt = tok + TOK_STEPS * TSW;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  int base = *nm;
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    if ((st.ms[h] >> lane) & 1ull)
+      mt[base + __popcll(st.ms[h] & below)] = (uint32_t)st.mlen[h] | ((uint32_t)st.mdist[h] << 9);
+    base += __popcll(st.ms[h]);
+  }
+  *nm = base;
+}
+
+// pass 2: step `step` back from the token area (vector loads: the words pass 1 stored)
+__device__ __forceinline__ Step load_step(const uint32_t *tok, int step, int *nm, int lane) {
+  const uint32_t rv = tok[step * TSW + (lane < TSW ? lane : 0)];
+  Step st;
+  st.next = __builtin_amdgcn_readlane((int)rv, 0);
+  const uint32_t *mt = tok + TOK_STEPS * TSW;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  int base = *nm;
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    st.lit[h] = (uint32_t)__builtin_amdgcn_readlane((int)rv, 1 + 2 * h) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv, 2 + 2 * h) << 32);
+    st.ms[h] = (uint32_t)__builtin_amdgcn_readlane((int)rv, 1 + 2 * DF_NP + 2 * h) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv, 2 + 2 * DF_NP + 2 * h) << 32);
+    uint32_t m = 0;
+    if ((st.ms[h] >> lane) & 1ull) m = mt[base + __popcll(st.ms[h] & below)];
+    st.mlen[h] = (int)(m & 511u);
+    st.mdist[h] = (int)(m >> 9);
+    base += __popcll(st.ms[h]);
+  }
+  *nm = base;
+  return st;
+}
+
 __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, int64_t n_in, int64_t b0, int64_t nb,
-                                                            uint8_t *slots, DfBlockInfo *info) {
+                                                            uint8_t *slots, DfBlockInfo *info, uint32_t *tokens) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   BlockLds &L = *(BlockLds *)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -390,6 +444,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   const uint8_t *s = L.in + s0;
   const bool last = s0 + SLICE >= n;   // the final deflate block (later waves have empty slices)
   uint32_t *region = (uint32_t *)(slots + (size_t)blockIdx.x * SLOT + (size_t)wave * REGION);
+  uint32_t *tok = tokens + ((size_t)blockIdx.x * DF_WAVES + wave) * TOK_WORDS;
   int32_t out_len = 0;
   if (S > 0) {
     // pass 1: frequencies
@@ -398,9 +453,11 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     for (int i = lane; i < NDIST; i += 64) W.dfq[i] = 0;
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    int n_step = 0, n_match = 0;
     for (int cur = 0; cur < S;) {
       const Step st = parse_step(s, S, cur, W.ht, lane);
       count_step(s, cur, st, W, lane);
+      keep_step(tok, n_step++, &n_match, st, lane);
       hash_in(s, S, cur, st.next, W.ht, lane);
       cur = st.next;
     }
@@ -434,14 +491,13 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
     }
-    // pass 2: the same parse, encoded
-    for (int i = lane; i < (1 << HBITS); i += 64) W.ht[i] = 0;
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    for (int cur = 0; cur < S;) {
-      const Step st = parse_step(s, S, cur, W.ht, lane);
+    // pass 2: pass 1's tokens, encoded (no second parse)
+    __builtin_amdgcn_s_waitcnt(0);   // (pass 1's token stores are done)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    n_match = 0;
+    for (int cur = 0, k = 0; cur < S; k++) {
+      const Step st = load_step(tok, k, &n_match, lane);
       encode_step(s, cur, st, W, bw, lane);
-      hash_in(s, S, cur, st.next, W.ht, lane);
       cur = st.next;
     }
     // end of block; then either the final padding or a sync flush (empty stored block) to a byte boundary
@@ -532,6 +588,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
   if (boff) boff->assign((size_t)nb_all + 1, 0);
   const int64_t CH = 8192;   // blocks per launch (slots: CH x 72 KiB)
   MH_TRY(ensure(ctx, ctx->gz_slots, (size_t)CH * SLOT + 64));
+  MH_TRY(ensure(ctx, ctx->gz_tok, sizeof(uint32_t) * (size_t)CH * DF_WAVES * TOK_WORDS + 64));
   MH_TRY(ensure(ctx, ctx->gz_info, sizeof(DfBlockInfo) * (size_t)CH + 64));
   MH_TRY(ensure(ctx, ctx->gz_off, sizeof(int64_t) * (size_t)(CH + 1) + 64));
   MH_TRY(ensure(ctx, ctx->gz_scan, scan_lb_scratch_bytes<int64_t>(CH + 1)));
@@ -544,7 +601,7 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
   for (int64_t b0 = 0; b0 < nb_all; b0 += CH) {
     const int64_t nb = nb_all - b0 < CH ? nb_all - b0 : CH;
     hipLaunchKernelGGL(k_bgzf_blocks, dim3((unsigned)nb), dim3(DF_THREADS), lds, st, d_in, n, b0, nb,
-                       (uint8_t *)ctx->gz_slots.p, (DfBlockInfo *)ctx->gz_info.p);
+                       (uint8_t *)ctx->gz_slots.p, (DfBlockInfo *)ctx->gz_info.p, (uint32_t *)ctx->gz_tok.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, device_scan_sum<int64_t>(st, nb, LoadBlk{(const DfBlockInfo *)ctx->gz_info.p, nb},
                                          StoreBlk{(int64_t *)ctx->gz_off.p}, ctx->gz_scan.p, tot));

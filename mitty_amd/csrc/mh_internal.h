@@ -219,6 +219,7 @@ struct mh_ctx {
   mh::DevBuf pb[6];     // batch-wide permutation: ts, shuffled ts, global keys, sorted keys, sorted steps, heads
   mh::DevBuf pb_tmp;    // its radix sort scratch
   mh::DevBuf gz_slots, gz_info, gz_off, gz_scan, gz_out, gz_in;   // device BGZF (mh_deflate.hip)
+  mh::DevBuf gz_tok;                                               // ... its pass-1 tokens per wave
   // mh_output_bgzf_pair: gz_out in two halves used by alternate calls; per half the event after its copies (stream2)
   hipEvent_t ev_gz[2] = {nullptr, nullptr};
   hipEvent_t ev_fetch[2] = {nullptr, nullptr};   // mh_output_fetch_async: per ticket, after both files' copies
