@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <functional>
 #include <map>
+#include <mutex>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -384,6 +386,9 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
                     // d_out (+ the end), for a BAI; on_piece(offset, bytes): a piece of d_out is queued on `st` (the
                     // caller may copy it out behind that point while the next piece deflates)
 int64_t bgzf_device_bound(int64_t n);
+int gpu_numa_node(int dev);   // the NUMA node of the device's PCI function (sysfs), -1 when unknown
+std::mutex &host_allocs_mu();  // mh_host_alloc's node-bound registrations (address -> bytes)
+std::unordered_map<void *, size_t> &host_allocs();
 int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
 int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);
 int32_t output_reset(mh_ctx *ctx);
