@@ -74,6 +74,35 @@ struct BlockLds {
   WaveLds w[DF_WAVES];
 };
 
+// DF_PROF (calibration builds only: make prof): per-phase shader-clock sums of every wave's lane 0, read back by
+// mh_df_prof (scripts/calib_deflate.py).  Slots: 0 staging, 1 CRC, 2 parse, 3 count, 4 keep, 5 hash-in, 6 codes and
+// header, 7 token load, 8 encode, 9 end of block; 10 parse steps, 11 matches, 12 waves with a slice.
+#ifdef DF_PROF
+__device__ unsigned long long df_prof[16];
+struct DfProf {
+  uint64_t t, a[16];
+  __device__ void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    a[i] += now - t;
+    t = now;
+  }
+};
+#define DFP_BEGIN                          \
+  DfProf P_;                               \
+  for (int i_ = 0; i_ < 16; i_++) P_.a[i_] = 0; \
+  P_.t = __builtin_amdgcn_s_memtime()
+#define DFP(i) P_.mark(i)
+#define DFP_ADD(i, v) P_.a[i] += (uint64_t)(v)
+#define DFP_END \
+  if (lane == 0) \
+    for (int i_ = 0; i_ < 16; i_++) atomicAdd(&df_prof[i_], (unsigned long long)P_.a[i_])
+#else
+#define DFP_BEGIN
+#define DFP(i)
+#define DFP_ADD(i, v)
+#define DFP_END
+#endif
+
 struct DfBlockInfo {
   int32_t n;           // input bytes
   int32_t stored;      // 1: stored block (the slices' regions unused)
@@ -395,6 +424,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = b0 + blockIdx.x;
   if (blockIdx.x >= nb) return;
+  DFP_BEGIN;
   const int64_t start = b * BLOCK;
   const int n = (int)(n_in - start < BLOCK ? n_in - start : BLOCK);
   // stage the block (16-byte loads when the block starts 16-byte aligned, bytes otherwise) and the CRC table
@@ -421,6 +451,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   }
   if (tid == 0) L.stored = 0;
   __syncthreads();
+  DFP(0);
   // CRC-32 of the block: 128-byte segments, then a tree of combinations
   {
     const int a = tid * 128, e = a + 128 < n ? a + 128 : n;
@@ -437,6 +468,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
       __syncthreads();
     }
   }
+  DFP(1);
   // the wave's slice
   WaveLds &W = L.w[wave];
   const int s0 = wave * SLICE;
@@ -456,11 +488,18 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     int n_step = 0, n_match = 0;
     for (int cur = 0; cur < S;) {
       const Step st = parse_step(s, S, cur, W.ht, lane);
+      DFP(2);
       count_step(s, cur, st, W, lane);
+      DFP(3);
       keep_step(tok, n_step++, &n_match, st, lane);
+      DFP(4);
       hash_in(s, S, cur, st.next, W.ht, lane);
+      DFP(5);
       cur = st.next;
     }
+    DFP_ADD(10, n_step);
+    DFP_ADD(11, n_match);
+    DFP_ADD(12, 1);
     if (lane == 0) W.lf[256] = 1;   // end of block (a slice without matches: HDIST 1, one unused distance code)
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -494,10 +533,13 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     // pass 2: pass 1's tokens, encoded (no second parse)
     __builtin_amdgcn_s_waitcnt(0);   // (pass 1's token stores are done)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    DFP(6);
     n_match = 0;
     for (int cur = 0, k = 0; cur < S; k++) {
       const Step st = load_step(tok, k, &n_match, lane);
+      DFP(7);
       encode_step(s, cur, st, W, bw, lane);
+      DFP(8);
       cur = st.next;
     }
     // end of block; then either the final padding or a sync flush (empty stored block) to a byte boundary
@@ -528,6 +570,8 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     // stored also when the codes would not be smaller (random bytes): the output never exceeds bgzf_device_bound
     I.stored = (L.stored || HDR + tot + TRL > MAX_BSIZE || tot >= 5 + (int64_t)n) ? 1 : 0;
   }
+  DFP(9);
+  DFP_END;
 }
 
 __device__ __forceinline__ int64_t block_bytes(const DfBlockInfo &I) {
@@ -624,6 +668,14 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
   if (boff) (*boff)[nb_all] = w;
   return MH_OK;
 }
+
+#ifdef DF_PROF
+extern "C" int mh_df_prof(unsigned long long *out) {   // the sums since the last call (then zeroed)
+  unsigned long long z[16] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(df_prof), sizeof(z)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(df_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // worst-case output bytes for n input bytes (every block stored)
 int64_t bgzf_device_bound(int64_t n) { return n + ((n + BLOCK - 1) / BLOCK + 1) * (HDR + 5 + TRL) + 64; }

@@ -10,8 +10,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
-  import torch
-  torch.empty(1, device='cuda')   # torch's HIP runtime first (it cannot start after the library's in one process)
+  # --torch: torch's HIP runtime first (then the library runs on it: one libamdhip64 per process) and torch's own
+  # copies measured too; without it the library runs on /opt/rocm's runtime, as in bench.py
+  use_torch = '--torch' in sys.argv
+  if use_torch:
+    import torch
+    torch.empty(1, device='cuda')
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from mitty_amd.readmodel import get_read_model
@@ -96,6 +100,8 @@ def main():
     run('sync_one_file', sync_fetch, False)
     run('async_two_files', async_fetch)
     run('async_one_file', async_fetch, False)
+    if not use_torch:
+      return
     src = torch.empty(4 << 30, dtype=torch.uint8, device='cuda')
     src.fill_(3)
     tp = [torch.empty(CH, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
