@@ -317,8 +317,6 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   ctx->gate_at = ge ? atoi(ge) : -1;
   const char *hf = getenv("MH_HAP_FWD");
   ctx->hap_fwd = hf && atoi(hf) != 0;
-  const char *tc = getenv("MH_TAIL_CHASE");
-  ctx->tail_batch_chase = tc && !strcmp(tc, "batch");
   const char *so = getenv("MH_SORT");
   ctx->sort_lsd = so && !strcmp(so, "lsd");
   const char *gt = getenv("MH_WRITER_GATE_TAIL");

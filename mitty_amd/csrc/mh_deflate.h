@@ -55,11 +55,13 @@ __host__ __device__ inline uint32_t bit_reverse(uint32_t code, int len) {
 
 // Code lengths, at most `limit` bits, for the m used symbols whose keys (frequency << 9 | symbol) are in `keys`,
 // sorted ascending (the caller sorts: a wave-parallel sort on the device).  len[] must be zero for unused symbols;
-// A is scratch for m entries.  Single thread.  Huffman's algorithm in place over the frequency-sorted weights
+// A is scratch for m entries and count for 32 (LDS on the device: a thread-local array indexed at run time would be
+// scratch memory, a global-memory round trip per access).  Single thread.  Huffman's algorithm in place over the frequency-sorted weights
 // (Moffat & Katajainen, "In-place calculation of minimum-redundancy codes", 1995), then the depths above `limit`
 // folded back with the Kraft sum kept at 1, and the lengths handed out again in frequency order.  One used symbol
 // gets length 1.
-__host__ __device__ inline void huffman_from_sorted(const uint32_t *keys, int m, int limit, uint8_t *len, uint32_t *A) {
+__host__ __device__ inline void huffman_from_sorted(const uint32_t *keys, int m, int limit, uint8_t *len, uint32_t *A,
+                                                    int32_t *count) {
   if (m == 0) return;
   if (m == 1) {
     len[keys[0] & 511u] = 1;
@@ -104,7 +106,7 @@ __host__ __device__ inline void huffman_from_sorted(const uint32_t *keys, int m,
     used = 0;
   }
   // A[i]: the code length of the i-th least frequent symbol
-  int count[32] = {0};
+  for (int b = 0; b < 32; b++) count[b] = 0;
   for (int i = 0; i < m; i++) count[A[i] > 31 ? 31 : A[i]]++;
   int over = 0;
   for (int b = limit + 1; b < 32; b++) {
@@ -148,9 +150,11 @@ __host__ __device__ inline int sorted_keys_small(const uint32_t *f, int n, uint3
   return m;
 }
 
-// Canonical codes (bit-reversed for deflate's LSB-first bit order) from lengths.
-__host__ __device__ inline void canonical_codes(const uint8_t *len, int n, uint16_t *code) {
-  int count[16] = {0}, next[16];
+// Canonical codes (bit-reversed for deflate's LSB-first bit order) from lengths; count and next: 16 entries of
+// scratch each.  Single thread (the device builds the two main alphabets' codes wave-wide: mh_deflate.hip).
+__host__ __device__ inline void canonical_codes(const uint8_t *len, int n, uint16_t *code, int32_t *count,
+                                                int32_t *next) {
+  for (int b = 0; b < 16; b++) count[b] = 0;
   for (int s = 0; s < n; s++) count[len[s]]++;
   count[0] = 0;
   int c = 0;
@@ -186,6 +190,7 @@ struct HeaderScratch {
   uint8_t seq[NLIT + NDIST];
   uint32_t rl[NLIT + NDIST];
   uint32_t cf[NCL], keys[NCL], A[NCL];
+  int32_t count[32], next[16];
   uint8_t cl[NCL];
   uint16_t cc[NCL];
 };
@@ -243,8 +248,8 @@ __host__ __device__ inline void write_dynamic_header(BitSink &bs, const uint8_t 
   uint8_t *cl = H.cl;
   uint16_t *cc = H.cc;
   for (int i = 0; i < NCL; i++) cl[i] = 0;
-  huffman_from_sorted(H.keys, sorted_keys_small(cf, NCL, H.keys), 7, cl, H.A);
-  canonical_codes(cl, NCL, cc);
+  huffman_from_sorted(H.keys, sorted_keys_small(cf, NCL, H.keys), 7, cl, H.A, H.count);
+  canonical_codes(cl, NCL, cc, H.count, H.next);
   int hclen = NCL;
   while (hclen > 4 && cl[CL_ORDER[hclen - 1]] == 0) hclen--;
   bs.put((uint32_t)(hlit - 257), 5);
@@ -264,7 +269,7 @@ __host__ __device__ inline void write_dynamic_header(BitSink &bs, const uint8_t 
 constexpr uint32_t CRC_POLY = 0xedb88320u;
 
 // a * b modulo the CRC polynomial (reflected bit order)
-__host__ __device__ inline uint32_t crc_multmodp(uint32_t a, uint32_t b) {
+__host__ __device__ constexpr inline uint32_t crc_multmodp(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -290,6 +295,51 @@ __host__ __device__ inline uint32_t crc_x8n(uint64_t n) {
 // crc32(A || B) from crc32(A), crc32(B) and len(B)
 __host__ __device__ inline uint32_t crc_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   return crc_multmodp(crc_x8n(len_b), crc_a) ^ crc_b;
+}
+
+// CRC-32 of a block by segments (the device: one segment per thread).  The raw CRC (register starting at 0, no final
+// inversion) is linear, so raw(block) = XOR over segments i of raw(segment i) * x^(8 (n - end_i)), and
+// crc32 = ~(raw(block) ^ 0xffffffff * x^(8 n)).  With segments of CRC_SEG bytes, n = q CRC_SEG + r: a whole segment
+// i < q is scaled by x^(8 CRC_SEG (q - 1 - i)) and then, all together, by x^(8 r); the partial segment q is not
+// scaled.  The powers are compile-time tables.  CRC_SEG = 132 bytes (33 words): lanes' word loads at 132-byte
+// strides fall in different LDS banks (128 put every lane on one bank).
+constexpr int CRC_SEG = 132;
+constexpr int CRC_NSEG = (BLOCK + CRC_SEG - 1) / CRC_SEG;   // 495 (<= 512 threads)
+struct CrcPowers {
+  uint32_t seg[CRC_NSEG + 1];   // x^(8 CRC_SEG j)
+  uint32_t byte[CRC_SEG];       // x^(8 r)
+};
+constexpr CrcPowers make_crc_powers() {
+  CrcPowers t{};
+  uint32_t p = 1u << 31;   // x^0
+  for (int r = 0; r < CRC_SEG; r++) {
+    t.byte[r] = p;
+    p = crc_multmodp(1u << 23, p);   // * x^8
+  }
+  uint32_t q = 1u << 31;
+  for (int j = 0; j <= CRC_NSEG; j++) {
+    t.seg[j] = q;
+    q = crc_multmodp(p, q);          // * x^(8 CRC_SEG)
+  }
+  return t;
+}
+// the raw CRC register after byte b (table of 256 entries: the standard reflected table)
+__host__ __device__ inline uint32_t crc_raw_byte(uint32_t c, uint32_t b, const uint32_t *tab) {
+  return tab[(c ^ b) & 0xffu] ^ (c >> 8);
+}
+// crc32 of n bytes by the segment method (host restatement of the device's, checked against the direct CRC)
+__host__ inline uint32_t crc32_segments(const uint8_t *b, int n, const CrcPowers &P, const uint32_t *tab) {
+  const int q = n / CRC_SEG, r = n - q * CRC_SEG;
+  uint32_t acc = 0, tail = 0;
+  for (int i = 0; i * CRC_SEG < n; i++) {
+    const int a = i * CRC_SEG, e = a + CRC_SEG < n ? a + CRC_SEG : n;
+    uint32_t c = 0;
+    for (int k = a; k < e; k++) c = crc_raw_byte(c, b[k], tab);
+    if (i < q) acc ^= crc_multmodp(P.seg[q - 1 - i], c);
+    else tail = c;
+  }
+  const uint32_t raw = crc_multmodp(P.byte[r], acc) ^ tail;
+  return ~(crc_multmodp(crc_multmodp(P.seg[q], P.byte[r]), 0xffffffffu) ^ raw);
 }
 
 }  // namespace df

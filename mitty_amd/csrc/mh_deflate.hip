@@ -17,7 +17,8 @@
 //   pass 2  pass 1's tokens (kept per wave in global memory: each step's position masks and its matches), each
 //           step's codes placed by wave prefix sums of their bit lengths into an LDS staging strip, whole words
 //           flushed to the slice's region of the block's slot;
-//   CRC-32  every thread a 128-byte segment, combined over a tree (x^(8n) operators).
+//   CRC-32  every thread a 132-byte segment (slicing by 4), scaled to the block's end by compile-time powers of x,
+//           XOR-reduced.
 // A block whose codes would not fit a BGZF block, or not be smaller than its bytes, is stored instead.
 // k_bgzf_pack then writes the blocks (gzip header with the BC field, the slices' bytes, CRC32, ISIZE) at offsets
 // from a scan of their sizes.
@@ -51,6 +52,7 @@ constexpr int STAGE = (64 * DF_NP * 15 + 31) / 32 + 8;
 
 struct CodeScratch {                        // while the codes are built (the hash table is idle then)
   uint32_t keys[512], A[NLIT];
+  int32_t count[32];
   HeaderScratch H;
 };
 struct WaveLds {
@@ -68,15 +70,20 @@ static_assert(sizeof(CodeScratch) <= sizeof(uint32_t) * (1 << HBITS), "code scra
 
 struct BlockLds {
   uint8_t in[BLOCK + 64];                   // the block's input, zero-padded
-  uint32_t crc_tab[256];
-  uint32_t crc[DF_THREADS];
+  uint32_t crc_tab[4][256];                 // slicing-by-4 tables: byte i followed by k zero bytes
+  uint32_t crcw[DF_WAVES], crc_tail, crc;   // per-wave XOR of the scaled segment CRCs; the partial segment's; result
   int32_t stored;
   WaveLds w[DF_WAVES];
 };
+static_assert(sizeof(BlockLds) <= 160 * 1024, "LDS");
+static_assert(CRC_NSEG <= DF_THREADS, "a CRC segment per thread");
+
+__constant__ CrcPowers kCrcPow = make_crc_powers();
 
 // DF_PROF (calibration builds only: make prof): per-phase shader-clock sums of every wave's lane 0, read back by
-// mh_df_prof (scripts/calib_deflate.py).  Slots: 0 staging, 1 CRC, 2 parse, 3 count, 4 keep, 5 hash-in, 6 codes and
-// header, 7 token load, 8 encode, 9 end of block; 10 parse steps, 11 matches, 12 waves with a slice.
+// mh_df_prof (scripts/calib_deflate.py).  Slots: 0 staging, 1 CRC, 2 parse, 3 count, 4 keep, 5 hash-in, 6 pass-2
+// set-up (and the pass-1 tail), 7 token load, 8 encode, 9 end of block; 10 parse steps, 11 matches, 12 waves with a
+// slice; 13 literal/length codes, 14 distance codes, 15 header.
 #ifdef DF_PROF
 __device__ unsigned long long df_prof[16];
 struct DfProf {
@@ -144,9 +151,43 @@ __device__ void wave_sort(uint32_t *k, int n, int lane) {
     }
 }
 
-// Code lengths of one alphabet from the wave's frequencies (keys sorted by the whole wave, the rest on lane 0).
+// Canonical codes of one alphabet from its lengths, wave-wide: the count of each length by ballots, then each
+// symbol's rank among the earlier symbols of its length (per-length counts in registers: loops over the 15 lengths
+// unrolled)
+__device__ void wave_canonical(const uint8_t *len, int n, uint16_t *code, int lane) {
+  uint32_t cnt[16], next[16], run[16];
+#pragma unroll
+  for (int b = 0; b < 16; b++) cnt[b] = run[b] = 0;
+  for (int s0 = 0; s0 < n; s0 += 64) {
+    const int l = s0 + lane < n ? len[s0 + lane] : 0;
+#pragma unroll
+    for (int b = 1; b < 16; b++) cnt[b] += (uint32_t)__popcll(__ballot(l == b));
+  }
+  uint32_t c = 0;
+  next[0] = 0;
+#pragma unroll
+  for (int b = 1; b < 16; b++) {
+    c = (c + cnt[b - 1]) << 1;
+    next[b] = c;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int s0 = 0; s0 < n; s0 += 64) {
+    const int l = s0 + lane < n ? len[s0 + lane] : 0;
+    uint32_t cd = 0;
+#pragma unroll
+    for (int b = 1; b < 16; b++) {
+      const uint64_t bal = __ballot(l == b);
+      if (l == b) cd = next[b] + run[b] + (uint32_t)__popcll(bal & below);
+      run[b] += (uint32_t)__popcll(bal);
+    }
+    if (s0 + lane < n) code[s0 + lane] = l ? (uint16_t)(__builtin_bitreverse32(cd) >> (32 - l)) : (uint16_t)0;
+  }
+}
+
+// Code lengths of one alphabet from the wave's frequencies (keys sorted by the whole wave, the lengths on lane 0,
+// the codes wave-wide).
 __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, uint16_t *code, uint32_t *keys,
-                             uint32_t *A, int lane) {
+                             uint32_t *A, int32_t *count, int lane) {
   // keys of the used symbols, compacted in symbol order by a wave prefix count
   int base = 0;
   for (int s0 = 0; s0 < n; s0 += 64) {
@@ -159,10 +200,10 @@ __device__ void wave_huffman(const uint32_t *f, int n, int limit, uint8_t *len, 
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   wave_sort(keys, base, lane);
-  if (lane == 0) {
-    huffman_from_sorted(keys, base, limit, len, A);
-    canonical_codes(len, n, code);
-  }
+  if (lane == 0) huffman_from_sorted(keys, base, limit, len, A, count);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  wave_canonical(len, n, code, lane);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 }
@@ -444,28 +485,49 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   } else {
     for (int i = tid; i < BLOCK + 64; i += DF_THREADS) L.in[i] = i < n ? src[i] : 0;
   }
-  for (int i = tid; i < 256; i += DF_THREADS) {
-    uint32_t c = (uint32_t)i;
-    for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ CRC_POLY : c >> 1;
-    L.crc_tab[i] = c;
+  for (int i = tid; i < 4 * 256; i += DF_THREADS) {   // table k: byte i & 255, then k zero bytes
+    uint32_t c = (uint32_t)(i & 255);
+    for (int k = 0; k < 8 * (1 + (i >> 8)); k++) c = c & 1 ? (c >> 1) ^ CRC_POLY : c >> 1;
+    L.crc_tab[i >> 8][i & 255] = c;
   }
-  if (tid == 0) L.stored = 0;
+  if (tid == 0) {
+    L.stored = 0;
+    L.crc_tail = 0;
+  }
   __syncthreads();
   DFP(0);
-  // CRC-32 of the block: 128-byte segments, then a tree of combinations
+  // CRC-32 by segments (mh_deflate.h crc32_segments): thread t's raw CRC of bytes [132 t, 132 t + 132), four bytes
+  // per step (slicing by 4), scaled by the compile-time power for its distance to the block's end; an XOR reduction
   {
-    const int a = tid * 128, e = a + 128 < n ? a + 128 : n;
-    uint32_t c = 0xffffffffu;
-    for (int i = a; i < e; i++) c = L.crc_tab[(c ^ L.in[i]) & 0xffu] ^ (c >> 8);
-    L.crc[tid] = a < e ? ~c : 0u;
-    __syncthreads();
-    for (int h = 1; h < DF_THREADS; h <<= 1) {   // segment pairs (tid, tid + h) at tid % 2h == 0
-      if ((tid & (2 * h - 1)) == 0 && tid + h < DF_THREADS) {
-        const int ra = (tid + h) * 128;
-        const int rl = ra >= n ? 0 : (n - ra < 128 * h ? n - ra : 128 * h);   // bytes of the right part
-        if (rl > 0) L.crc[tid] = crc_combine(L.crc[tid], L.crc[tid + h], (uint64_t)rl);
+    const int q = n / CRC_SEG, r = n - q * CRC_SEG;
+    const int a = tid * CRC_SEG;
+    uint32_t c = 0;
+    if (a < n) {
+      const int e = a + CRC_SEG < n ? a + CRC_SEG : n;
+      const uint32_t *w = (const uint32_t *)(L.in + a);   // (a: a multiple of 4)
+      const int nw = (e - a) >> 2;
+      for (int k = 0; k < nw; k++) {
+        c ^= w[k];
+        c = L.crc_tab[3][c & 255u] ^ L.crc_tab[2][(c >> 8) & 255u] ^ L.crc_tab[1][(c >> 16) & 255u] ^
+            L.crc_tab[0][c >> 24];
       }
-      __syncthreads();
+      for (int k = a + 4 * nw; k < e; k++) c = crc_raw_byte(c, L.in[k], L.crc_tab[0]);
+      if (tid < q) {
+        c = crc_multmodp(kCrcPow.seg[q - 1 - tid], c);
+      } else {
+        L.crc_tail = c;   // the partial segment (thread q, when r > 0): not scaled
+        c = 0;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+    if (lane == 0) L.crcw[wave] = c;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t x = 0;
+      for (int k = 0; k < DF_WAVES; k++) x ^= L.crcw[k];
+      const uint32_t raw = crc_multmodp(kCrcPow.byte[r], x) ^ L.crc_tail;
+      L.crc = ~(crc_multmodp(crc_multmodp(kCrcPow.seg[q], kCrcPow.byte[r]), 0xffffffffu) ^ raw);
     }
   }
   DFP(1);
@@ -504,8 +566,11 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     // codes
-    wave_huffman(W.lf, NLIT, 15, W.llen, W.lcode, W.cs.keys, W.cs.A, lane);
-    wave_huffman(W.dfq, NDIST, 15, W.dlen, W.dcode, W.cs.keys, W.cs.A, lane);
+    DFP(6);
+    wave_huffman(W.lf, NLIT, 15, W.llen, W.lcode, W.cs.keys, W.cs.A, W.cs.count, lane);
+    DFP(13);
+    wave_huffman(W.dfq, NDIST, 15, W.dlen, W.dcode, W.cs.keys, W.cs.A, W.cs.count, lane);
+    DFP(14);
     // the header bits into hw (lane 0)
     int hbits = 0;
     if (lane == 0) {
@@ -518,6 +583,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
       for (int k = (int)bs.pos + (bs.nacc ? 1 : 0); k < (int)bs.pos + 8; k++) ((uint8_t *)W.hw)[k] = 0;
     }
     hbits = __shfl(hbits, 0, 64);
+    DFP(15);
     for (int k = lane; k < STAGE; k += 64) W.stage[k] = 0;
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -564,7 +630,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
   if (tid == 0) {
     DfBlockInfo &I = info[blockIdx.x];
     I.n = n;
-    I.crc = L.crc[0];
+    I.crc = L.crc;
     int64_t tot = 0;
     for (int w = 0; w < DF_WAVES; w++) tot += I.len[w];
     // stored also when the codes would not be smaller (random bytes): the output never exceeds bgzf_device_bound

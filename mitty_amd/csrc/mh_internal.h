@@ -271,7 +271,6 @@ struct mh_ctx {
   // MH_SORT=lsd (the hand-written permutation sort instead of rocprim's, measured slower: DESIGN.md), read once per
   // context (mh_create), so tests switch it per context
   bool sort_lsd = false;
-  bool tail_batch_chase = false;   // MH_TAIL_CHASE=batch (experiment): the async tail's chase batch-wide, not per unit
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas

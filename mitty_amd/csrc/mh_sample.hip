@@ -1727,13 +1727,6 @@ static int32_t sample_tail_async(mh_ctx *ctx, const std::shared_ptr<SampleState>
   const BatchPerm &bp = S.bp;
   const uint32_t *sk = (const uint32_t *)ctx->pb[3].p, *sv = (const uint32_t *)ctx->pb[4].p;
   const int32_t *nxt = (const int32_t *)ctx->pb[5].p;
-  if (ctx->tail_batch_chase) {   // (experiment) the whole batch's chase first, on the main stream
-    stage_begin(ctx, "sample_permutation");
-    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(S.j_total, 256, INT32_MAX)), dim3(256), 0, st, (int64_t)0,
-                       S.j_total, sk, sv, nxt, (const int64_t *)bp.ts, bp.tsh);
-    HIPCHK(ctx, hipGetLastError());
-    stage_end(ctx);
-  }
   HIPCHK(ctx, hipEventRecord(ctx->ev_fork, st));
   HIPCHK(ctx, hipStreamWaitEvent(l1, ctx->ev_fork, 0));
   S.ev.assign(n_units, nullptr);
@@ -1746,16 +1739,15 @@ static int32_t sample_tail_async(mh_ctx *ctx, const std::shared_ptr<SampleState>
       ts.valid = true;
       continue;
     }
-    if (!ctx->tail_batch_chase) {
-      ctx->stage_stream = l1;
-      stage_begin(ctx, "sample_permutation");
-      const int64_t k0 = q.j_off, k1 = q.j_off + q.n + 4;
-      hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(k1 - k0, 256, INT32_MAX)), dim3(256), 0, l1, k0, k1, sk, sv,
-                         nxt, (const int64_t *)bp.ts, bp.tsh);
-      stage_end(ctx);
-      ctx->stage_stream = nullptr;
-      HIPCHK(ctx, hipGetLastError());
-    }
+    // (the whole batch's chase on the main stream before the fork instead: the same step time, round 4's A/B)
+    ctx->stage_stream = l1;
+    stage_begin(ctx, "sample_permutation");
+    const int64_t k0 = q.j_off, k1 = q.j_off + q.n + 4;
+    hipLaunchKernelGGL(k_perm_chase, dim3(grid_for(k1 - k0, 256, INT32_MAX)), dim3(256), 0, l1, k0, k1, sk, sv, nxt,
+                       (const int64_t *)bp.ts, bp.tsh);
+    stage_end(ctx);
+    ctx->stage_stream = nullptr;
+    HIPCHK(ctx, hipGetLastError());
     MH_TRY(finish_unit(ctx, q, S.words, S.jall + q.j_off, S.p, S.rlen, S.d_cum, S.n_tlen, S.rng_mode, false,
                        S.d_m + u, S.d_flags + u, 1, 0, 2, nullptr, &bp));
     hipLaunchKernelGGL(k_unit_result, dim3(1), dim3(64), 0, l1, (const int64_t *)(S.d_m + u),

@@ -101,7 +101,7 @@ def main():
     run('async_two_files', async_fetch)
     run('async_one_file', async_fetch, False)
     if not use_torch:
-      return
+      raise StopIteration
     src = torch.empty(4 << 30, dtype=torch.uint8, device='cuda')
     src.fill_(3)
     tp = [torch.empty(CH, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
@@ -121,6 +121,8 @@ def main():
     for s in pins:
       s[0].free()
       s[1].free()
+  except StopIteration:
+    pass
   finally:
     eng.close()
   print(json.dumps(out), flush=True)

@@ -84,8 +84,9 @@ void codes(const uint32_t *f, int n, int limit, uint8_t *len, uint16_t *code) {
     if (f[s]) keys.push_back((f[s] << 9) | (uint32_t)s);
   }
   std::sort(keys.begin(), keys.end());
-  huffman_from_sorted(keys.data(), (int)keys.size(), limit, len, A.data());
-  canonical_codes(len, n, code);
+  int32_t count[32], next[16];
+  huffman_from_sorted(keys.data(), (int)keys.size(), limit, len, A.data(), count);
+  canonical_codes(len, n, code, count, next);
 }
 
 // one slice as a deflate block (final or followed by a sync flush); returns its bytes
@@ -164,13 +165,19 @@ int main(int argc, char **argv) {
       const int S = bn - s0 < SLICE ? bn - s0 : SLICE;
       z += slice_bits(blk + s0, S, s0 + SLICE >= bn);
     }
-    // CRC by 128-byte segments combined (the device's method) must equal the direct CRC
-    uint32_t c = 0;
-    for (int a = 0; a < bn; a += 128) {
-      const int e = a + 128 < bn ? a + 128 : bn;
-      c = a == 0 ? crc_bytes(blk, e) : crc_combine(c, crc_bytes(blk + a, e - a), (uint64_t)(e - a));
-    }
-    if (c != crc_bytes(blk, bn)) {
+    // CRC by segments (the device's method) must equal the direct CRC; so must the combination of two halves
+    static const CrcPowers P = make_crc_powers();
+    static uint32_t tab[256];
+    if (!tab[1])
+      for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ CRC_POLY : c >> 1;
+        tab[i] = c;
+      }
+    const uint32_t c = crc32_segments(blk, bn, P, tab);
+    const int half = bn / 2;
+    if (c != crc_bytes(blk, bn) ||
+        crc_combine(crc_bytes(blk, half), crc_bytes(blk + half, bn - half), (uint64_t)(bn - half)) != c) {
       fprintf(stderr, "crc combine mismatch in block %lld\n", (long long)b);
       return 1;
     }

@@ -438,13 +438,10 @@ def test_lsd_sort_repeated_batches(native, monkeypatch):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize('chase', ['unit', 'batch'])
-def test_async_tail_equals_sync_templates(native, monkeypatch, chase):
+def test_async_tail_equals_sync_templates(native):
   """mh_sample_units_async: the units' tails queued on the second stream and resolved one by one, in any order (a
   count, an export — any non-emission entry point resolves every pending set — or the next batch's sampling), give
-  the same template sets as mh_sample_units; the permutation chase per unit in the tail, or batch-wide before it
-  (MH_TAIL_CHASE=batch)."""
-  monkeypatch.setenv('MH_TAIL_CHASE', chase)
+  the same template sets as mh_sample_units."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   mdl = G.model('hiseq-X-v2.5-Garvan')
