@@ -220,6 +220,10 @@ int32_t mh_output_reset(mh_ctx *ctx);
 /* Page-locked host memory for mh_output_fetch destinations (D2H at full link rate; the FASTQ sink writes from it). */
 int32_t mh_host_alloc(int64_t bytes, void **out);
 int32_t mh_host_free(void *p);
+/* Device memory the library freed is kept in a process-wide cache (per device) for later requests, so a context
+ * created after another closed reuses blocks allocated while device memory was unfragmented; an allocation that
+ * fails empties the cache first.  This frees every cached block now (*freed_bytes: their total). */
+int32_t mh_device_cache_trim(int64_t *freed_bytes);
 
 /* rpc.generate_read for a batch of (p, l) on haplotype `slot`: positions, start/end nodes and the text fields.
  * Text outputs are concatenated; *_off arrays (n+1 entries) index them.  MH_E_CAPACITY if a text buffer is short

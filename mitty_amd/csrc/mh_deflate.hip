@@ -55,10 +55,14 @@ struct CodeScratch {                        // while the codes are built (the ha
   int32_t count[32];
   HeaderScratch H;
 };
+struct PackedCodes {                        // pass 2 (the hash table is idle then): code | length << 16
+  uint32_t l[NLIT], d[NDIST];
+};
 struct WaveLds {
   union {
     uint32_t ht[1 << HBITS];                // hash: position + 1 of the latest earlier position (atomicMax)
     CodeScratch cs;
+    PackedCodes pk;
   };
   uint32_t lf[NLIT], dfq[NDIST];
   uint8_t llen[NLIT], dlen[NDIST];
@@ -67,6 +71,7 @@ struct WaveLds {
   uint32_t hw[96];                          // the dynamic header's bits, as words
 };
 static_assert(sizeof(CodeScratch) <= sizeof(uint32_t) * (1 << HBITS), "code scratch inside the hash table");
+static_assert(sizeof(PackedCodes) <= sizeof(uint32_t) * (1 << HBITS), "packed codes inside the hash table");
 
 struct BlockLds {
   uint8_t in[BLOCK + 64];                   // the block's input, zero-padded
@@ -122,11 +127,7 @@ __device__ __forceinline__ uint32_t load4(const uint8_t *b, int x) {   // bytes 
   return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(x & 3));
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t w) { return (w * 2654435761u) >> (32 - HBITS); }
-// bytes p .. p+6 equal bytes c .. c+6 (MIN_MATCH = 7: two overlapping 4-byte words)
-__device__ __forceinline__ bool match7(const uint8_t *s, int p, uint32_t wp, int c) {
-  return load4(s, c) == wp && load4(s, c + 3) == load4(s, p + 3);
-}
-static_assert(MIN_MATCH == 7, "match7");
+static_assert(MIN_MATCH == 7, "words7: a match is checked as two overlapping 4-byte words");
 
 // Wave-wide ascending sort of n <= 320 keys in LDS (bitonic over the next power of two, padded with ~0u).
 __device__ void wave_sort(uint32_t *k, int n, int lane) {
@@ -223,23 +224,51 @@ struct Step {
   uint64_t lit[DF_NP], ms[DF_NP];    // positions 64 h + lane holding a literal / starting a match
   int mlen[DF_NP], mdist[DF_NP];     // this lane's matches (ms positions)
 };
+// what pass 1 keeps of a step's positions for its hash inserts and counts (no second look at the bytes)
+struct StepPos {
+  uint32_t hv[DF_NP];                // hash of the position's first four bytes (valid positions)
+  uint32_t lb[DF_NP];                // the position's byte
+};
 
-__device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane) {
+// bytes x .. x+3 and x+3 .. x+6 from three aligned words (the slice starts 4-byte aligned)
+__device__ __forceinline__ void words7(const uint32_t *wd, int x, uint32_t &w, uint32_t &w3) {
+  const int i = x >> 2, o = x & 3;
+  const uint32_t q0 = wd[i], q1 = wd[i + 1], q2 = wd[i + 2];
+  w = __builtin_amdgcn_alignbyte(q1, q0, (uint32_t)o);
+  w3 = o ? __builtin_amdgcn_alignbyte(q2, q1, (uint32_t)(o - 1)) : __builtin_amdgcn_alignbyte(q1, q0, 3u);
+}
+
+__device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, const uint32_t *ht, int lane,
+                                           StepPos &sp) {
+  const uint32_t *wd = (const uint32_t *)s;
   int cand[DF_NP], len[DF_NP];
   uint64_t M[DF_NP];
 #pragma unroll
   for (int h = 0; h < DF_NP; h++) {
     const int p = cur + 64 * h + lane;
     int c = -1;
+    uint32_t hv = 0, lb = 0;
     if (p + MIN_MATCH <= S) {
-      const uint32_t w = load4(s, p);
-      if (p >= 1 && match7(s, p, w, p - 1)) {
-        c = p - 1;                                   // a run: distance 1
+      uint32_t w, w3;
+      words7(wd, p, w, w3);   // bytes p .. p+6 (two overlapping words)
+      lb = w & 0xffu;
+      hv = hash4(w);
+      // a run (distance 1): bytes p-1 .. p+6 all equal
+      if (p >= 1 && w == lb * 0x01010101u && w3 == w && s[p - 1] == lb) {
+        c = p - 1;
       } else {
-        const int j = (int)ht[hash4(w)] - 1;         // a position of an earlier step (< cur <= p)
-        if (j >= 0 && match7(s, p, w, j)) c = j;
+        const int j = (int)ht[hv] - 1;                // a position of an earlier step (< cur <= p)
+        if (j >= 0) {
+          uint32_t cw, cw3;
+          words7(wd, j, cw, cw3);
+          if (cw == w && cw3 == w3) c = j;
+        }
       }
+    } else if (p < S) {
+      lb = s[p];
     }
+    sp.hv[h] = hv;
+    sp.lb[h] = lb;
     cand[h] = c;
     len[h] = 0;
     M[h] = __ballot(c >= 0);
@@ -306,20 +335,28 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
   return st;
 }
 
-// positions a .. b-1 into the hash table; lanes colliding on one entry keep the latest position (atomicMax), so
-// both passes see the same table
-__device__ __forceinline__ void hash_in(const uint8_t *s, int S, int a, int b, uint32_t *ht, int lane) {
-  for (int k = a + lane; k < b; k += 64)
+// the step's positions cur .. next-1 into the hash table (the hashes parse_step computed; positions past the step's
+// window, inside its last match, hashed here); lanes colliding on one entry keep the latest position (atomicMax), so
+// the table does not depend on the order of the inserts
+__device__ __forceinline__ void hash_in(const uint8_t *s, int S, int cur, int next, const StepPos &sp, uint32_t *ht,
+                                        int lane) {
+#pragma unroll
+  for (int h = 0; h < DF_NP; h++) {
+    const int p = cur + 64 * h + lane;
+    if (p < next && p + HASH_BYTES <= S)
+      atomicMax(&ht[p + MIN_MATCH <= S ? sp.hv[h] : hash4(load4(s, p))], (uint32_t)(p + 1));
+  }
+  for (int k = cur + 64 * DF_NP + lane; k < next; k += 64)
     if (k + HASH_BYTES <= S) atomicMax(&ht[hash4(load4(s, k))], (uint32_t)(k + 1));
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 }
 
 // the symbols of one step, pass 1: literal and match frequencies (LDS atomics, one per token position)
-__device__ __forceinline__ void count_step(const uint8_t *s, int cur, const Step &st, WaveLds &W, int lane) {
+__device__ __forceinline__ void count_step(const Step &st, const StepPos &sp, WaveLds &W, int lane) {
 #pragma unroll
   for (int h = 0; h < DF_NP; h++) {
-    if ((st.lit[h] >> lane) & 1ull) atomicAdd(&W.lf[s[cur + 64 * h + lane]], 1u);
+    if ((st.lit[h] >> lane) & 1ull) atomicAdd(&W.lf[sp.lb[h]], 1u);
     if ((st.ms[h] >> lane) & 1ull) {
       atomicAdd(&W.lf[257 + len_code(st.mlen[h])], 1u);
       atomicAdd(&W.dfq[dist_code(st.mdist[h])], 1u);
@@ -387,19 +424,20 @@ __device__ __forceinline__ void encode_step(const uint8_t *s, int cur, const Ste
     uint64_t v = 0;
     int n = 0;
     if ((st.lit[h] >> lane) & 1ull) {
-      const uint32_t c = s[cur + 64 * h + lane];
-      v = W.lcode[c];
-      n = W.llen[c];
+      const uint32_t c = W.pk.l[s[cur + 64 * h + lane]];
+      v = c & 0xffffu;
+      n = (int)(c >> 16);
     } else if ((st.ms[h] >> lane) & 1ull) {
       const int ml = st.mlen[h], md = st.mdist[h];
       const int lc = len_code(ml), dc = dist_code(md);
       const int le = len_extra(lc), de = dist_extra(dc);
-      v = W.lcode[257 + lc];
-      n = W.llen[257 + lc];
+      const uint32_t lk = W.pk.l[257 + lc], dk = W.pk.d[dc];
+      v = lk & 0xffffu;
+      n = (int)(lk >> 16);
       v |= (uint64_t)(ml - len_base(lc)) << n;
       n += le;
-      v |= (uint64_t)W.dcode[dc] << n;
-      n += W.dlen[dc];
+      v |= (uint64_t)(dk & 0xffffu) << n;
+      n += (int)(dk >> 16);
       v |= (uint64_t)(md - dist_base(dc)) << n;
       n += de;
     }
@@ -434,9 +472,12 @@ __device__ __forceinline__ void keep_step(uint32_t *tok, int step, int *nm, cons
   *nm = base;
 }
 
-// pass 2: step `step` back from the token area (vector loads: the words pass 1 stored)
-__device__ __forceinline__ Step load_step(const uint32_t *tok, int step, int *nm, int lane) {
-  const uint32_t rv = tok[step * TSW + (lane < TSW ? lane : 0)];
+// pass 2: a step's record word (lane l: word l of the step record), loaded a step ahead
+__device__ __forceinline__ uint32_t load_rec(const uint32_t *tok, int step, int lane) {
+  return tok[step * TSW + (lane < TSW ? lane : 0)];
+}
+// pass 2: the step from its record, its matches loaded from the token area (vector loads: the words pass 1 stored)
+__device__ __forceinline__ Step load_step(const uint32_t *tok, uint32_t rv, int *nm, int lane) {
   Step st;
   st.next = __builtin_amdgcn_readlane((int)rv, 0);
   const uint32_t *mt = tok + TOK_STEPS * TSW;
@@ -549,13 +590,14 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
     __builtin_amdgcn_wave_barrier();
     int n_step = 0, n_match = 0;
     for (int cur = 0; cur < S;) {
-      const Step st = parse_step(s, S, cur, W.ht, lane);
+      StepPos sp;
+      const Step st = parse_step(s, S, cur, W.ht, lane, sp);
       DFP(2);
-      count_step(s, cur, st, W, lane);
+      count_step(st, sp, W, lane);
       DFP(3);
       keep_step(tok, n_step++, &n_match, st, lane);
       DFP(4);
-      hash_in(s, S, cur, st.next, W.ht, lane);
+      hash_in(s, S, cur, st.next, sp, W.ht, lane);
       DFP(5);
       cur = st.next;
     }
@@ -596,13 +638,23 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
     }
-    // pass 2: pass 1's tokens, encoded (no second parse)
-    __builtin_amdgcn_s_waitcnt(0);   // (pass 1's token stores are done)
+    // pass 2: pass 1's tokens, encoded (no second parse); the packed codes over the idle hash table
+    for (int i = lane; i < NLIT; i += 64) W.pk.l[i] = (uint32_t)W.lcode[i] | ((uint32_t)W.llen[i] << 16);
+    if (lane < NDIST) W.pk.d[lane] = (uint32_t)W.dcode[lane] | ((uint32_t)W.dlen[lane] << 16);
+    __builtin_amdgcn_s_waitcnt(0);   // (pass 1's token stores are done; the tables are in place)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
     DFP(6);
     n_match = 0;
+    // step k + 1's record and matches are loaded while step k is encoded
+    Step nx = load_step(tok, load_rec(tok, 0, lane), &n_match, lane);
+    uint32_t rvn = n_step > 1 ? load_rec(tok, 1, lane) : 0u;
     for (int cur = 0, k = 0; cur < S; k++) {
-      const Step st = load_step(tok, k, &n_match, lane);
+      const Step st = nx;
+      if (k + 1 < n_step) {
+        nx = load_step(tok, rvn, &n_match, lane);
+        if (k + 2 < n_step) rvn = load_rec(tok, k + 2, lane);
+      }
       DFP(7);
       encode_step(s, cur, st, W, bw, lane);
       DFP(8);
