@@ -278,6 +278,7 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
   Step st;
 #pragma unroll
   for (int h = 0; h < DF_NP; h++) st.lit[h] = st.ms[h] = 0;
+  // (the walk's state is wave-uniform: readfirstlane keeps it in scalar registers)
   int x = 0;
   for (;;) {   // wave-uniform greedy walk: x = the position of the next token
     int m = NW;
@@ -287,6 +288,7 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
         const uint64_t r = x > 64 * h ? M[h] & (~0ull << (x - 64 * h)) : M[h];
         if (r) m = 64 * h + __builtin_ctzll(r);
       }
+    m = __builtin_amdgcn_readfirstlane(m);
     const int me = m < W ? m : W;
 #pragma unroll
     for (int h = 0; h < DF_NP; h++) {   // literals [x, me)
@@ -318,10 +320,11 @@ __device__ __forceinline__ Step parse_step(const uint8_t *s, int S, int cur, con
       if (run < 64 || L >= cap) break;
     }
     if (L > cap) L = cap;
+    L = __builtin_amdgcn_readfirstlane(L);
 #pragma unroll
     for (int h = 0; h < DF_NP; h++)
       if (h == hm && lane == l) len[h] = L;
-    x = m + L;
+    x = __builtin_amdgcn_readfirstlane(m + L);
     if (x >= W) {
       st.next = cur + x;
       break;
@@ -503,7 +506,9 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
                                                             uint8_t *slots, DfBlockInfo *info, uint32_t *tokens) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   BlockLds &L = *(BlockLds *)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave: readfirstlane tells the compiler it is uniform, so the slice bounds and the whole parse walk are scalar;
+  // derived from threadIdx.x it is taken as divergent and the walk runs as exec-masked vector code)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t b = b0 + blockIdx.x;
   if (blockIdx.x >= nb) return;
   DFP_BEGIN;
@@ -599,7 +604,7 @@ __global__ void __launch_bounds__(DF_THREADS) k_bgzf_blocks(const uint8_t *in, i
       DFP(4);
       hash_in(s, S, cur, st.next, sp, W.ht, lane);
       DFP(5);
-      cur = st.next;
+      cur = __builtin_amdgcn_readfirstlane(st.next);
     }
     DFP_ADD(10, n_step);
     DFP_ADD(11, n_match);

@@ -585,6 +585,40 @@ constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads
 constexpr int ED_CRB = 15;   // bases per corruption block (CI_BLK)
 constexpr int ED_GMAX = 7;   // window chunks per gather thread (3 threads per mate): up to 21 chunks, rlen <= 321
 
+// EW_PROF (calibration builds only: make prof): per-phase shader-clock sums of k_emit_tiles' waves (lane 0), read
+// back by mh_ew_prof (scripts/calib_writer_phases.py).  Slots: 0 wave 0's formatting, 1 waves 1-3's gathers (sum of
+// the three), 2 / 3 their waits at the barrier, 4 the corruption rows' layering (all waves), 5 the seam sweep (with
+// its barrier), 6 the chunk sweep; 7 tiles.
+#ifdef EW_PROF
+__device__ unsigned long long ew_prof[16];
+struct EwProf {
+  uint64_t t, a[8];
+  __device__ void mark(int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    a[i] += now - t;
+    t = now;
+  }
+};
+#define EWP_PARAM , EwProf &P_
+#define EWP_ARG , P_
+#define EWP_BEGIN                                 \
+  EwProf P_;                                      \
+  for (int i_ = 0; i_ < 8; i_++) P_.a[i_] = 0;    \
+  P_.t = __builtin_amdgcn_s_memtime()
+#define EWP(i) P_.mark(i)
+#define EWP_END                                                                          \
+  if ((threadIdx.x & 63) == 0) {                                                         \
+    if (threadIdx.x == 0) P_.a[7] = 1;                                                   \
+    for (int i_ = 0; i_ < 8; i_++) atomicAdd(&ew_prof[i_], (unsigned long long)P_.a[i_]); \
+  }
+#else
+#define EWP_PARAM
+#define EWP_ARG
+#define EWP_BEGIN
+#define EWP(i)
+#define EWP_END
+#endif
+
 struct DMeta {
   int32_t rel[2];    // record start relative to the tile's first byte, per file
   int32_t len[2];    // record length per file (0: template dropped by the N filter)
@@ -648,7 +682,8 @@ struct QHead {
 // file; span: the tile's bytes per file.
 template <int NF, int LPR, int CR>
 __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64_t gbase[2], const int32_t span[2],
-                                          int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena) {
+                                          int32_t o_t, int32_t TL, int32_t o_s, bool staged, char *const *arena
+                                          EWP_PARAM) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   constexpr int RPP = ED_THREADS / LPR;                        // records per pass
@@ -714,6 +749,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
   // (an LDS-only barrier here — the ragged-edge byte stores above need not land before the chunk sweep — measured no
   // faster than the full one, round 3)
   if (staged) __syncthreads();
+  EWP(5);
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
     const int f = NF == 2 ? r / ED_T : 0, j = r % ED_T;
@@ -741,6 +777,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       *(uint4 *)(out + (cg << 4)) = v;
     }
   }
+  EWP(6);
 }
 
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t v) {
@@ -822,6 +859,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t TS = (A.rlen + 4 + 15) / 16 * 16;   // (a read 16 bytes past a T lands in the next one or the pad)
   const int32_t o_tr = o_dump + 16 + ED_PAD;
   const int tid = threadIdx.x;
+  EWP_BEGIN;
   const int Lp = qh.lp, Lm = qh.lm;
   const int64_t t0 = tile * ED_T;
   const int nt = (int)(t0 + ED_T < A.m ? ED_T : A.m - t0);
@@ -1004,7 +1042,9 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
     }
   }
+  EWP(tid < 64 ? 0 : 1);
   __syncthreads();
+  EWP(tid < 64 ? 2 : 3);
   if (CR == 2) {
     // each row slot of a kept record: its qualities into the record's T, its substitutions into the window
     // (base_rot[b][code - 1], illumina.py:131-136,159-160); block 0 also writes T's separators
@@ -1054,10 +1094,12 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       lay(sl, A.crow[g], A.ccode[g]);
     }
     __syncthreads();
+    EWP(4);
   }
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
-  ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena);
+  ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena EWP_ARG);
+  EWP_END;
 }
 
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
@@ -1752,6 +1794,15 @@ HapView view_of(const Hap &h) {
 }
 
 }  // namespace
+
+#ifdef EW_PROF
+extern "C" int mh_ew_prof(unsigned long long *out) {   // the sums since the last call (then zeroed)
+  unsigned long long z[16] = {0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ew_prof), sizeof(z)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(ew_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 
 int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept) {
   auto tit = ctx->tsets.find(ctx->cur_tpl);
