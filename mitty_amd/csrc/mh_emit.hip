@@ -949,6 +949,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
+#ifndef EW_CALIB_NOFMT   // (calibration builds only, `make variant V=NOFMT`: the reads parts left unwritten)
     if (keep) {
       ReadInfo ri;
       ri.n0 = n0;
@@ -988,6 +989,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
       if (fr == 1) smem[o] = '\n';
     }
+#endif
     // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
     const int32_t lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
     const int32_t ik = wave_incl_scan(keep && fr == 0 ? 1 : 0);
@@ -1026,6 +1028,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
         mt.S[fr] = S;
         mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
+#ifndef EW_CALIB_NOHEAD
         if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
           mt.qb = qb;
           mt.sb = sb;
@@ -1035,6 +1038,12 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
           for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
           for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
         }
+#else
+        if (fr == 0) {
+          mt.qb = qb;
+          mt.sb = sb;
+        }
+#endif
       }
       if (CR == 1 && (NF == 2 || fr == 0)) {   // the record's first base, for the corruption pass (S = 0: dropped)
         const uint64_t so = (uint64_t)((fr ? g1 : g0) + rel + sb);
