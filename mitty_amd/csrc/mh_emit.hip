@@ -585,6 +585,10 @@ constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads
 constexpr int ED_CRB = 15;   // bases per corruption block (CI_BLK)
 constexpr int ED_GMAX = 7;   // window chunks per gather thread (3 threads per mate): up to 21 chunks, rlen <= 321
 
+#if defined(EW_CALIB_SEAMINLINE) && !defined(EW_SEAM_INLINE)   // (make variant V=SEAMINLINE: the A/B build)
+#define EW_SEAM_INLINE
+#endif
+
 // EW_PROF (calibration builds only: make prof): per-phase shader-clock sums of k_emit_tiles' waves (lane 0), read
 // back by mh_ew_prof (scripts/calib_writer_phases.py).  Slots: 0 wave 0's formatting, 1 waves 1-3's gathers (sum of
 // the three), 2 / 3 their waits at the barrier, 4 the corruption rows' layering (all waves), 5 the seam sweep (with
@@ -677,6 +681,41 @@ struct QHead {
   __device__ __forceinline__ uint8_t at(int i) const { return (uint8_t)(w[i >> 2] >> (8 * (i & 3))); }
 };
 
+// the 16 bytes at record offsets x0 .. x0+15 of record (j, f) — previous record's T end | Q | B | T — merged per dword
+// with byte masks (v_bfi)
+template <int CR>
+__device__ __forceinline__ uint4 seam_chunk(const char *smem, const DMeta *meta, int j, int f, int32_t x0,
+                                            int32_t o_t, int32_t TL) {
+  const DMeta &M = meta[j];
+  const int32_t rel = M.rel[f], sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f], tb = M.tb[f],
+                tn = M.tn[f];
+  int32_t pte = o_t + TL;                                   // end of the previous record's T
+  if (CR && x0 < 0 && rel > 0)                              // the previous kept record of this file in the tile
+    for (int pj = j - 1; pj >= 0; pj--)
+      if (meta[pj].len[f] > 0) {
+        pte = meta[pj].tb[f] + meta[pj].tn[f];
+        break;
+      }
+  const uint4 vp = lds_load16(smem, (uint32_t)(pte + (x0 < 0 ? x0 : -16)));
+  const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
+  int32_t yb = x0 - sb;
+  yb = yb < -16 ? -16 : (yb > S ? S : yb);
+  const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
+  int32_t yt = x0 - tl;
+  yt = yt < -16 ? -16 : (yt > tn ? tn : yt);
+  const uint4 vt = lds_load16(smem, (uint32_t)(tb + yt));
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int32_t x = x0 + 4 * k;
+    const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
+    uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
+    v = (u4get(vq, k) & mq) | (v & ~mq);
+    w[k] = (u4get(vp, k) & mp) | (v & ~mp);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // The output sweeps of a 32-template tile whose strings and metadata are in LDS: LPR lanes per record (record
 // r = file f, template j), passes over the tile's NF * ED_T records.  gbase: arena offset of the tile's first byte per
 // file; span: the tile's bytes per file.
@@ -700,9 +739,12 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
     if (L == 0) continue;
     const int32_t rel = M.rel[f];
     const int64_t ga = gbase[f] + rel;                        // arena offset of the record's first byte
-    const int32_t sb = M.sb, S = M.S[f], tl = sb + S, qb = M.qb, bb = M.bb[f], tb = M.tb[f], tn = M.tn[f];
+    const int32_t sb = M.sb, S = M.S[f], tl = sb + S;
     const int b = q;
     const bool tile_end = rel + L == span[f];
+#ifdef EW_SEAM_INLINE
+    if (rel != 0 && !tile_end) continue;   // (only the tile's ragged edges here: the other seams in the chunk sweep)
+#endif
     const int32_t spb = b == 0 ? 0 : b == 1 ? sb : b == 2 ? tl : L;
     const int64_t cg = (ga + spb) >> 4;
     bool skip = (b == 3 && !tile_end) || ((ga + spb) & 15) == 0;   // aligned: both sides are pure chunks
@@ -711,44 +753,26 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
     skip |= b > 2 && ((ga + tl) & 15) != 0 && ((ga + tl) >> 4) == cg;
     if (skip) continue;
     const int32_t x0 = (int32_t)((cg << 4) - ga);
-    // the 16 bytes at record offsets x0 .. x0+15: previous record's T end | Q | B | T
-    int32_t pte = o_t + TL;                                   // end of the previous record's T
-    if (CR && x0 < 0 && rel > 0)                              // the previous kept record of this file in the tile
-      for (int pj = j - 1; pj >= 0; pj--)
-        if (meta[pj].len[f] > 0) {
-          pte = meta[pj].tb[f] + meta[pj].tn[f];
-          break;
-        }
-    const uint4 vp = lds_load16(smem, (uint32_t)(pte + (x0 < 0 ? x0 : -16)));
-    const uint4 vq = lds_load16(smem, (uint32_t)(qb + (x0 < -16 ? -16 : (x0 > sb ? sb : x0))));
-    int32_t yb = x0 - sb;
-    yb = yb < -16 ? -16 : (yb > S ? S : yb);
-    const uint4 vb = lds_load16(smem, (uint32_t)(bb + yb));
-    int32_t yt = x0 - tl;
-    yt = yt < -16 ? -16 : (yt > tn ? tn : yt);
-    const uint4 vt = lds_load16(smem, (uint32_t)(tb + yt));
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int32_t x = x0 + 4 * k;
-      const uint32_t mb = lt_mask(x, tl), mq = lt_mask(x, sb), mp = lt_mask(x, 0);
-      uint32_t v = (u4get(vb, k) & mb) | (u4get(vt, k) & ~mb);
-      v = (u4get(vq, k) & mq) | (v & ~mq);
-      w[k] = (u4get(vp, k) & mp) | (v & ~mp);
-    }
     const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;        // tile start: the previous tile owns the rest
     const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
+#ifdef EW_SEAM_INLINE
+    if (lo == 0 && hi == 16) continue;                          // a whole seam chunk: the chunk sweep's
+#endif
+    const uint4 wv = seam_chunk<CR>(smem, meta, j, f, x0, o_t, TL);
     if (lo == 0 && hi == 16) {
-      if (staged) *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-      else *(uint4 *)(arena[f] + (cg << 4)) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (staged) *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = wv;
+      else *(uint4 *)(arena[f] + (cg << 4)) = wv;
     } else {
+      const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
       char *g = arena[f] + (cg << 4);
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
+#ifndef EW_SEAM_INLINE
   // (an LDS-only barrier here — the ragged-edge byte stores above need not land before the chunk sweep — measured no
   // faster than the full one, round 3)
   if (staged) __syncthreads();
+#endif
   EWP(5);
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
@@ -765,8 +789,14 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
     for (int64_t cg = c0 + q; x0 + 16 <= L; cg += LPR, x0 += 16 * LPR) {
       const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
-      if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
       uint4 v;
+#ifdef EW_SEAM_INLINE
+      if (b >= 0) {
+        v = seam_chunk<CR>(smem, meta, j, f, x0, o_t, TL);
+      } else
+#else
+      if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
+#endif
       if (CR < 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
         v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);   // inside T's '~' run: no LDS read
       } else {
@@ -852,7 +882,11 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
   // seam chunks through LDS (in order with the others); CR 2 stores them from the seam pass (4 KB less LDS: with the
   // per-record T strings that is 5 instead of 4 workgroups per CU, 0.77 vs 0.73 G/s on the corrupt bench)
+#ifdef EW_SEAM_INLINE
+  const bool staged = false;
+#else
   const bool staged = CR != 2;
+#endif
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
@@ -1858,7 +1892,11 @@ static EwKernel ew_kernel(int cr, bool two) {
 }
 
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows) {
+#ifdef EW_SEAM_INLINE
+  const bool staged = false;   // (the seam chunks computed in the chunk sweep)
+#else
   const bool staged = !rows;   // (rows: the seam chunks stored by the seam pass, no LDS for them)
+#endif
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
