@@ -585,10 +585,6 @@ constexpr int ED_PAD = 32;   // LDS padding around every string (unaligned reads
 constexpr int ED_CRB = 15;   // bases per corruption block (CI_BLK)
 constexpr int ED_GMAX = 7;   // window chunks per gather thread (3 threads per mate): up to 21 chunks, rlen <= 321
 
-#if defined(EW_CALIB_SEAMINLINE) && !defined(EW_SEAM_INLINE)   // (make variant V=SEAMINLINE: the A/B build)
-#define EW_SEAM_INLINE
-#endif
-
 // EW_PROF (calibration builds only: make prof): per-phase shader-clock sums of k_emit_tiles' waves (lane 0), read
 // back by mh_ew_prof (scripts/calib_writer_phases.py).  Slots: 0 wave 0's formatting, 1 waves 1-3's gathers (sum of
 // the three), 2 / 3 their waits at the barrier, 4 the corruption rows' layering (all waves), 5 the seam sweep (with
@@ -742,9 +738,6 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
     const int32_t sb = M.sb, S = M.S[f], tl = sb + S;
     const int b = q;
     const bool tile_end = rel + L == span[f];
-#ifdef EW_SEAM_INLINE
-    if (rel != 0 && !tile_end) continue;   // (only the tile's ragged edges here: the other seams in the chunk sweep)
-#endif
     const int32_t spb = b == 0 ? 0 : b == 1 ? sb : b == 2 ? tl : L;
     const int64_t cg = (ga + spb) >> 4;
     bool skip = (b == 3 && !tile_end) || ((ga + spb) & 15) == 0;   // aligned: both sides are pure chunks
@@ -755,9 +748,6 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
     const int32_t x0 = (int32_t)((cg << 4) - ga);
     const int32_t lo = (rel == 0 && x0 < 0) ? -x0 : 0;        // tile start: the previous tile owns the rest
     const int32_t hi = b == 3 ? L - x0 : 16;                    // tile end: the next tile owns the rest
-#ifdef EW_SEAM_INLINE
-    if (lo == 0 && hi == 16) continue;                          // a whole seam chunk: the chunk sweep's
-#endif
     const uint4 wv = seam_chunk<CR>(smem, meta, j, f, x0, o_t, TL);
     if (lo == 0 && hi == 16) {
       if (staged) *(uint4 *)(smem + o_s + (r * 4 + b) * 16) = wv;
@@ -768,11 +758,10 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       for (int k = lo; k < hi; k++) g[k] = (char)(w[k >> 2] >> (8 * (k & 3)));
     }
   }
-#ifndef EW_SEAM_INLINE
   // (an LDS-only barrier here — the ragged-edge byte stores above need not land before the chunk sweep — measured no
-  // faster than the full one, round 3)
+  // faster than the full one, round 3; merging the seam chunks in the chunk sweep instead of staging them, with no
+  // second barrier and 4 KB less LDS, measured 1.5 % slower on the WGS line, round 4)
   if (staged) __syncthreads();
-#endif
   EWP(5);
   // every full chunk of each record: one unaligned LDS read (or a seam) and one aligned 16-byte store
   for (int r = tid / LPR; r < NF * ED_T; r += RPP) {
@@ -790,13 +779,7 @@ __device__ __forceinline__ void ed_output(const DMeta *meta, int nt, const int64
       const int b = x0 < 0 ? 0 : (x0 < sb && x0 + 16 > sb) ? 1 : (x0 < tl && x0 + 16 > tl) ? 2 : -1;
       if (b == 0 && rel == 0) continue;                         // ragged tile start, already written
       uint4 v;
-#ifdef EW_SEAM_INLINE
-      if (b >= 0) {
-        v = seam_chunk<CR>(smem, meta, j, f, x0, o_t, TL);
-      } else
-#else
       if (b >= 0 && !staged) continue;                          // seam chunk, stored by the seam pass
-#endif
       if (CR < 2 && b < 0 && x0 >= tl + 3 && x0 + 16 <= tl + TL - 1) {
         v = make_uint4(0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu, 0x7e7e7e7eu);   // inside T's '~' run: no LDS read
       } else {
@@ -882,11 +865,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   const int32_t o_s = o_t + (A.rlen + 4 + 2 * ED_PAD + 15) / 16 * 16;
   // seam chunks through LDS (in order with the others); CR 2 stores them from the seam pass (4 KB less LDS: with the
   // per-record T strings that is 5 instead of 4 workgroups per CU, 0.77 vs 0.73 G/s on the corrupt bench)
-#ifdef EW_SEAM_INLINE
-  const bool staged = false;
-#else
   const bool staged = CR != 2;
-#endif
   const int32_t o_dump = o_s + (staged ? NF * ED_T * 4 * 16 : 0);   // 16-byte sink for unused gathers
   const int32_t TL = A.rlen + 4;                      // T = '\n+\n' + rlen '~' + '\n' (readgenerate.py:229)
   // CR 2: per record its own T ('\n+\n' + S qualities + '\n') at o_tr + record * TS, laid from the corruption rows
@@ -983,6 +962,10 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
+#ifdef EW_CALIB_NOFMT2   // (calibration: the nodes loaded, their words kept, nothing formatted)
+    if (keep) smem[o_q + jf * qstride + head] = (char)(q0.a ^ q1.a ^ q2.a ^ q3.a ^ q0.b ^ q1.b ^ q2.b ^ q3.b);
+#define EW_CALIB_NOFMT
+#endif
 #ifndef EW_CALIB_NOFMT   // (calibration builds only, `make variant V=NOFMT`: the reads parts left unwritten)
     if (keep) {
       ReadInfo ri;
@@ -1892,11 +1875,7 @@ static EwKernel ew_kernel(int cr, bool two) {
 }
 
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows) {
-#ifdef EW_SEAM_INLINE
-  const bool staged = false;   // (the seam chunks computed in the chunk sweep)
-#else
   const bool staged = !rows;   // (rows: the seam chunks stored by the seam pass, no LDS for them)
-#endif
   const size_t TS = (size_t)((rlen + 4 + 15) / 16 * 16);   // CR 2: a T per record (emit_tile)
   return ((sizeof(DMeta) * ED_T + ED_PAD + 15) / 16) * 16 + (size_t)ED_T * 2 * win_stride + ED_PAD +
          (size_t)ED_T * qstride + ED_PAD + (size_t)((rlen + 4 + 2 * ED_PAD + 15) / 16 * 16) +
