@@ -54,14 +54,9 @@ def _rank(rank, world, port, layout, model_name, outdir):
 
 @pytest.mark.parametrize('world,layout', [(2, None), (2, 'slice'), (3, 'slice')])
 def test_distributed_output_identical_to_single_process(tmp_path, world, layout):
-  import socket
-  import torch.multiprocessing as mp
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
+  from tests._spawn import spawn_with_port
   model = 'hiseq-X-v2.5-Garvan'
-  mp.start_processes(_rank, args=(world, port, layout, model, str(tmp_path)), nprocs=world, join=True,
-                     start_method='spawn')
+  spawn_with_port(_rank, lambda port: (world, port, layout, model, str(tmp_path)), world)
   G.check_same(open(tmp_path / 'r1.fq', 'rb').read(), G.fastq_bytes('e2e_{}.r1.fq.gz'.format(model)))
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_{}.r2.fq.gz'.format(model)))
 
@@ -71,12 +66,8 @@ def test_distributed_gz_output(tmp_path, names):
   """'.gz' outputs (decided per file, as the single-GPU FastqSink decides): BGZF pieces at all-reduced offsets + EOF
   marker; each file decompresses (or reads) to the single-process bytes."""
   import gzip
-  import socket
-  import torch.multiprocessing as mp
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
-  mp.start_processes(_rank_gz, args=(2, port, str(tmp_path), names), nprocs=2, join=True, start_method='spawn')
+  from tests._spawn import spawn_with_port
+  spawn_with_port(_rank_gz, lambda port: (2, port, str(tmp_path), names), 2)
   model = 'hiseq-X-v2.5-Garvan'
   for k, fn in enumerate(names):
     raw = open(str(tmp_path / fn), 'rb').read()
@@ -140,10 +131,8 @@ def test_wgs_plan_four_ranks(tmp_path):
   synth.write_vcf(g['vcf'], seqs, {n: data[ri][1] for ri, (n, _) in enumerate(contigs)})
   with open(g['bed'], 'w') as fp:
     fp.write(''.join('{}\t0\t{}\n'.format(n, L) for n, L in contigs))
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
-  mp.start_processes(_rank_wgs, args=(4, port, g, str(tmp_path)), nprocs=4, join=True, start_method='spawn')
+  from tests._spawn import spawn_with_port
+  spawn_with_port(_rank_wgs, lambda port: (4, port, g, str(tmp_path)), 4)
   _, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
   units = O.unit_digests(dict(seqs), O.load_variant_file(g['vcf'], 'SYN', g['bed']), 'SYN', mdl, 30.0, 7, workers=4)
   assert len(units) == 100 and len({u[1] for u in units}) == 25

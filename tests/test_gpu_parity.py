@@ -1062,23 +1062,15 @@ def test_template_broadcast_packing_round_trip(native):
   device buffer (pos0 | pos1 | fo0 at 0 / 8n / 16n, the RCCL payload) and into a host buffer (the gloo payload),
   imported into another template set, emit the same FASTQ bytes as the sampled set; share() itself under a one-rank
   gloo group.  Runs in a spawned process (torch and libmitty_hip in one process need torch loaded first)."""
-  import socket
-  import torch.multiprocessing as mp
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
-  mp.start_processes(_packing_worker, args=(port,), nprocs=1, join=True, start_method='spawn')
+  from tests._spawn import spawn_with_port
+  spawn_with_port(_packing_worker, lambda port: (port,), 1)
 
 
 @pytest.mark.parametrize('layout', ['lpt', 'slice'])
 def test_distributed_two_ranks_one_gpu(native, tmp_path, layout):
   """Two ranks (gloo for the int64 exchanges, both on GPU 0) write the reference --threads 1 files."""
-  import socket
-  import torch.multiprocessing as mp
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
-  mp.start_processes(_gpu_rank, args=(2, port, layout, str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+  from tests._spawn import spawn_with_port
+  spawn_with_port(_gpu_rank, lambda port: (2, port, layout, str(tmp_path)), 2)
   G.check_same(open(tmp_path / 'r1.fq', 'rb').read(), G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'))
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz'))
 

@@ -9,7 +9,6 @@ the lengths; the bench runs the same plan at scale 1).  Reference: readgenerate.
 """
 import hashlib
 import os
-import socket
 
 import pytest
 
@@ -65,13 +64,10 @@ def _rank(rank, world, port, g, outdir, names=('r1.fq', 'r2.fq')):
 
 
 def _run(world, g, outdir, names=('r1.fq', 'r2.fq')):
-  import torch.multiprocessing as mp
-  with socket.socket() as s:
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
+  from tests._spawn import spawn_with_port
   os.makedirs(outdir, exist_ok=True)
   gg = {k: v for k, v in g.items() if k in ('fa', 'vcf', 'bed')}
-  mp.start_processes(_rank, args=(world, port, gg, outdir, names), nprocs=world, join=True, start_method='spawn')
+  spawn_with_port(_rank, lambda port: (world, port, gg, outdir, names), world)
 
 
 def _check_units(fname, units, which):
