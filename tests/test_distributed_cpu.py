@@ -118,8 +118,6 @@ def test_wgs_plan_four_ranks(tmp_path):
   """The whole-genome plan (GRCh37's 25 contigs, one BED interval each, 100 units dealt by LPT; the bench's and
   configs[3]'s shape) over 4 gloo ranks, at lengths x0.0005: the files equal the oracle's units in unit order."""
   import hashlib
-  import socket
-  import torch.multiprocessing as mp
   from mitty_amd import synth
   from mitty_amd.readmodel import get_read_model
   from oracle import oracle as O
