@@ -101,6 +101,9 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
+  ap.add_argument('--hip-runtime', default='rocm', choices=['rocm', 'torch'],
+                  help='the HIP runtime the library runs on at N = 1 without a process group: rocm = /opt/rocm\'s, '
+                       'which libmitty_hip.so links; torch = the copy torch ships (loaded first), as at N > 1')
   ap.add_argument('--unit-order', default='ps', choices=['ps', 'copy'],
                   help='wgs: the order a rank emits its units in: ps = the reference\'s unit order; copy = grouped by '
                        '(region, copy), so both passes of a haplotype run back to back (the arena bytes per unit are '
@@ -500,7 +503,7 @@ def run_genome(a, rank, world, local):
   per batch), an all-reduce of the counts closing each step."""
   # a process group at N > 1, and at N = 1 when MH_DIST_BACKEND names one (the RCCL path exercised on one GPU)
   use_pg = world > 1 or bool(os.environ.get('MH_DIST_BACKEND'))
-  if use_pg:
+  if use_pg or a.hip_runtime == 'torch':
     # torch before libmitty_hip: a process holds ONE HIP runtime, and whichever library loads first provides it
     # (ours needs libamdhip64.so.7, which torch's copy satisfies; torch's own libamdhip64.so would not reuse ours)
     import torch  # noqa: F401
