@@ -101,6 +101,9 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
+  ap.add_argument('--unit0-in-chunk', action='store_true',
+                  help='wgs: a batch\'s unit 0 prepared with the next units before its writer is queued (round 4\'s '
+                       'default before the A/B; the default queues unit 0\'s writer first)')
   ap.add_argument('--hip-runtime', default='rocm', choices=['rocm', 'torch'],
                   help='the HIP runtime the library runs on at N = 1 without a process group: rocm = /opt/rocm\'s, '
                        'which libmitty_hip.so links; torch = the copy torch ships (loaded first), as at N > 1')
@@ -556,6 +559,7 @@ def run_genome(a, rank, world, local):
     os.environ.setdefault('MH_WRITER_GATE', '0')   # read when the library context is created
   eng = Engine(local)
   eng.async_tail = not a.sync_tail
+  eng.unit0_alone = not a.unit0_in_chunk
   copies = {}
   for ri in regions:
     name, length = contigs[ri]

@@ -19,6 +19,7 @@ class Engine:
   EMIT_SETS = 4   # units prepared ahead of their writers (of the library's 16 emission buffer sets)
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
   async_tail = True     # run_units: mh_sample_units_async (False: mh_sample_units, the host waits for the batch)
+  unit0_alone = True    # run_units: unit 0's measure and writer queued before the next units are prepared
 
   def __init__(self, device=0):
     self.ctx = _native.Context(device)
@@ -112,9 +113,14 @@ class Engine:
       return PendingUnits(self.ctx, ns, tickets)
     out = []
     # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
-    # stream): the writers drain while the caller moves on to the next batch
-    for c0 in range(0, len(units), self.EMIT_SETS):
-      chunk = list(enumerate(units))[c0:c0 + self.EMIT_SETS]
+    # stream): the writers drain while the caller moves on to the next batch.  Unit 0 goes alone: preparing a unit
+    # waits for its sampling tail, so at a batch boundary the idle writer stream would otherwise wait for the tails
+    # and measure passes of the whole first chunk
+    order = list(enumerate(units))
+    k0 = 1 if self.unit0_alone and len(units) > 1 else 0
+    chunks = ([order[:1]] if k0 else []) + [order[c0:c0 + self.EMIT_SETS]
+                                            for c0 in range(k0, len(units), self.EMIT_SETS)]
+    for chunk in chunks:
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
