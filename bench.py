@@ -101,9 +101,6 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
-  ap.add_argument('--sample-ahead', action=argparse.BooleanOptionalAction, default=False,
-                  help='wgs: the next batch\'s splice and sampling queued as soon as this batch\'s measure passes are '
-                       '(before its writers), so they run beside the whole batch\'s writers')
   ap.add_argument('--unit0-in-chunk', action='store_true',
                   help='wgs: a batch\'s unit 0 prepared with the next units before its writer is queued (round 4\'s '
                        'default before the A/B; the default queues unit 0\'s writer first)')
@@ -563,8 +560,6 @@ def run_genome(a, rank, world, local):
   eng = Engine(local)
   eng.async_tail = not a.sync_tail
   eng.unit0_alone = not a.unit0_in_chunk
-  if a.sample_ahead:
-    eng.EMIT_SETS = 15   # every unit of a batch prepared before the next batch's sampling (16 emission sets)
   copies = {}
   for ri in regions:
     name, length = contigs[ri]
@@ -583,11 +578,6 @@ def run_genome(a, rank, world, local):
 
   tpl_flip = [0]
   soa_of = lambda r, c: copies[r][c]
-
-  def ahead_hook(bi):   # --sample-ahead: batch bi + 1 sampled once batch bi's measure passes are queued
-    if not a.sample_ahead or bi + 1 >= len(batches):
-      return None
-    return lambda: eng.sample_ahead(batches[bi + 1], soa_of, p, rlen, model['cum_tlen'], a.rng)
 
   def step_phased():
     if a.pipeline == 'phased-sync':
@@ -634,14 +624,14 @@ def run_genome(a, rank, world, local):
       return step_phased()
     eng.drop_haplotypes()
     res = []
-    for bi, batch in enumerate(batches):
+    for batch in batches:
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
       # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it.  --async-emit: the batch's
       # measure passes and writers are queued without a host round trip per unit (mh_emit_async), so the host moves
       # on to the next batch's splice and sampling while they run
       eng.ctx.reset_output()
-      res.append(eng.run_units(batch, soa_of, p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
-                               lazy=a.async_emit, on_prepared=ahead_hook(bi)))
+      res.append(eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
+                               lazy=a.async_emit))
     res = [u for r in res for u in (r.resolve() if hasattr(r, 'resolve') else r)]
     kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
     if dist is not None:
@@ -767,14 +757,9 @@ def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
 
     eng.ctx.sync()
     eng.drop_haplotypes()
-    for bi, batch in enumerate(batches):
+    for batch in batches:
       eng.ctx.reset_output()
-      hook = None
-      if a.sample_ahead and bi + 1 < len(batches):   # (the step's order: the next batch sampled ahead)
-        hook = lambda nb=batches[bi + 1]: eng.sample_ahead(nb, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'],
-                                                          a.rng)
-      res = eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
-                          on_prepared=hook)
+      res = eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
       eng.ctx.sync()
       o1 = o2 = 0
       for (ps, ri, cpy, _), (n, kept, x1, x2) in zip(batch, res):

@@ -28,7 +28,6 @@ class Engine:
     self._haps = {}      # (ri, cpy) -> (slot, n_nodes, p_min, p_max)
     self._vsets = {}     # (ri, cpy) -> resident variant set id (upload_variants)
     self._tpl_base = 0
-    self._ahead = None   # (units, slots, base) of a batch sampled ahead (sample_ahead)
 
   def close(self):
     self.ctx.close()
@@ -73,15 +72,25 @@ class Engine:
     self._vsets.clear()
 
   def drop_haplotypes(self):
-    self._ahead = None
     for slot, *_ in self._haps.values():
       self.ctx.release_haplotype(slot)
     self._haps.clear()
 
-  def _sample(self, units, soa_of, p, rlen, cum_tlen, rng):
-    """Splice the units' haplotypes and queue their sampling; returns (haplotype slots, template-set id base)."""
+  def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
+                on_unit=None, lazy=False):
+    """Sample a batch of work units together, then emit them in order.
+
+    units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
+    unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
+    lazy: the pipelined path — every unit's emission is queued on the writer stream (mh_emit_async: no host round trip
+    between sampling, measuring and writing) and a PendingUnits comes back at once; its resolve() gives the list
+    (the units' bytes land in the arenas in unit order, as on the synchronous path).
+    """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
+    if lazy:
+      for s in set(slots):   # the qname bound for the writer's room, while the splice's results are fresh
+        self.ctx.read_bound(s, rlen)
     # template ids alternate between two ranges per batch, so this batch's sampling never waits for the previous
     # batch's FASTQ writers (still queued on their own stream) to finish reading theirs
     base = self._tpl_base
@@ -94,35 +103,6 @@ class Engine:
     else:
       self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
                             RNG_MODES[rng])
-    return slots, base
-
-  def sample_ahead(self, units, soa_of, p, rlen, cum_tlen, rng='mitty'):
-    """Queue the next batch's splice and sampling now (e.g. from run_units' on_prepared, once the current batch's
-    measure passes are queued, so the sampling runs beside the whole batch's writers); the run_units call for the same
-    units then emits them without sampling again."""
-    slots, base = self._sample(units, soa_of, p, rlen, cum_tlen, rng)
-    self._ahead = ([tuple(u) for u in units], slots, base)
-
-  def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None, lazy=False, on_prepared=None):
-    """Sample a batch of work units together, then emit them in order.
-
-    units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
-    unit's emission (e.g. to stream the arena to files).  on_prepared() runs once every unit's measure pass is queued
-    (before the last chunk's writers: e.g. sample_ahead for the next batch).  Returns [(n, kept, b1, b2)] per unit.
-    lazy: the pipelined path — every unit's emission is queued on the writer stream (mh_emit_async: no host round trip
-    between sampling, measuring and writing) and a PendingUnits comes back at once; its resolve() gives the list
-    (the units' bytes land in the arenas in unit order, as on the synchronous path).
-    """
-    ahead = self._ahead
-    self._ahead = None
-    if ahead is not None and ahead[0] == [tuple(u) for u in units]:
-      _, slots, base = ahead   # sampled by sample_ahead while the previous batch was emitted
-    else:
-      slots, base = self._sample(units, soa_of, p, rlen, cum_tlen, rng)
-    if lazy:
-      for s in set(slots):   # the qname bound for the writer's room, while the splice's results are fresh
-        self.ctx.read_bound(s, rlen)
     if lazy and on_unit is None:
       tickets, ns = [], []
       for k, (ps, ri, cpy, seed) in enumerate(units):
@@ -140,13 +120,11 @@ class Engine:
     k0 = 1 if self.unit0_alone and len(units) > 1 else 0
     chunks = ([order[:1]] if k0 else []) + [order[c0:c0 + self.EMIT_SETS]
                                             for c0 in range(k0, len(units), self.EMIT_SETS)]
-    for ci, chunk in enumerate(chunks):
+    for chunk in chunks:
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
                               write_fastq2, unit_key=seed, wait=False)
-      if on_prepared is not None and ci == len(chunks) - 1:
-        on_prepared()
       for k, (ps, ri, cpy, seed) in chunk:
         self.ctx.use_templates(base + k)
         kept, b1, b2 = self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
