@@ -639,29 +639,10 @@ __device__ __forceinline__ uint32_t lds_put_u(char *lds, uint32_t o, uint64_t v)
   }
   uint32_t x = (uint32_t)v;
   const int nd = ndig_u(x);
-#ifdef EW_CALIB_FMT2   // (A/B build: two digits per step, one 32-bit division by 100 and a 24-bit multiply)
-  uint32_t e = o + (uint32_t)nd;
-  while (x >= 100u) {
-    const uint32_t q = x / 100u, r = x - q * 100u;
-    const uint32_t t = __umul24(r, 103u) >> 10;   // r / 10 for r < 100
-    e -= 2;
-    lds[e] = (char)('0' + t);
-    lds[e + 1] = (char)('0' + r - 10u * t);
-    x = q;
-  }
-  if (x >= 10u) {
-    const uint32_t t = __umul24(x, 103u) >> 10;
-    lds[e - 2] = (char)('0' + t);
-    lds[e - 1] = (char)('0' + x - 10u * t);
-  } else {
-    lds[e - 1] = (char)('0' + x);
-  }
-#else
   for (int i = nd - 1; i >= 0; i--) {
     lds[o + i] = (char)('0' + x % 10u);
     x /= 10u;
   }
-#endif
   return o + nd;
 }
 __device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) {
@@ -1070,12 +1051,8 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
           mt.sb = sb;
           char *d = smem + qb;
           for (int i = 0; i < Lp; i++) d[i] = (char)qh.at(i);
-#ifdef EW_CALIB_FMT2
-          (void)lds_put_u(smem, (uint32_t)(qb + Lp), (uint64_t)(uint32_t)cnt);
-#else
           uint32_t x = (uint32_t)cnt;
           for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
-#endif
           for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
         }
 #else
