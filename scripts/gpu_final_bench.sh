@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4, final tree: the bench line (metric, CPU baseline, end to end), its kernel statistics under rocprofv3, the
+# The round's record: the bench line (metric, CPU baseline, end to end), its kernel statistics under rocprofv3, the
 # full-size byte check, configs[1] / [2] / [4] lines, the device deflate's kernel statistics, the RCCL N = 1 line.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04t
+O=gpurun_out/final_bench
 mkdir -p $O
 timeout -k 10 420 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
 python3 scripts/bsum.py $O/bench.json || true

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4, final tree: the whole GPU suite (parity, RCCL at world size 1, the 100-unit genome plan) and smoke().
+# The round's record: the whole GPU suite (parity, RCCL at world size 1, the 100-unit genome plan) and smoke().
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04s
+O=gpurun_out/final_suite
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 600 --timeout-method thread \
   > $O/pytest.log 2>&1
