@@ -128,7 +128,7 @@ def parse():
   return ap.parse_args()
 
 
-def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
+def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1', world=1):
   agg = {}
   for name, ms in stages:
     agg.setdefault(name, [0.0, 0])
@@ -157,8 +157,9 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1'):
   read_gbs = hap_bytes / (ew_ms * 1e-3) / 1e9 if ew_ms > 0 else None
   return {'kernel': kernel, 'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
           'frac': (achieved / PEAK_HBM_GBS) if achieved else None, 'traffic': traffic,
-          'traffic_source': ('PMC passes (FETCH_SIZE, WRITE_SIZE) of this workload, ' + traffic_src)
-                            if traffic_src else None,
+          'traffic_source': (('PMC passes (FETCH_SIZE, WRITE_SIZE) of this workload, ' if world == 1 else
+                              'borrowed from the N = 1 PMC passes of this workload (not measured at this N), ') +
+                             traffic_src) if traffic_src else None,
           'algorithmic_bytes_per_launch': alg_bytes / max(ew_n, 1),
           'avg_launch_ms': ew_ms / max(ew_n, 1),
           'read_bytes_per_launch': hap_bytes / max(ew_n, 1),
@@ -658,7 +659,7 @@ def run_genome(a, rank, world, local):
     kept_all, b1_all, b2_all, n_units = (int(x) for x in c.tolist())
     backend, seen = dist.get_backend(), dist.get_world_size()
   workload = 'wgs' if a.genome_scale == 1 else None
-  roof, stage_ms, span_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload)
+  roof, stage_ms, span_ms = roofline(stages, kept, b1, b2, rlen, kernel, steps, workload, world)
   cpu = e2e = None
   if world == 1 and not a.plan_share:
     seq1, recs1, _ = data[0]
