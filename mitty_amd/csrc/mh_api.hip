@@ -462,6 +462,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
   if (ctx->h_units) (void)hipHostFree(ctx->h_units);
+  for (uint8_t *p : ctx->h_bam_pin)
+    if (p) (void)hipHostFree(p);
   for (auto &e : ctx->eset) {
     release(e.recs); release(e.off); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
@@ -1506,22 +1508,22 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   std::condition_variable cv;
   std::vector<Piece> pieces;
   bool fin = false;
-  // gz_out is sized for the whole BAM (GBs): released on every exit, never kept beside the next job's buffers
+  // gz_out is sized for the whole BAM (GBs): released on every exit into the device block cache (the next job's
+  // buffers, or the next file's gz_out, take it from there)
   struct Guard {
     mh_ctx *c;
-    uint8_t *pin[2] = {nullptr, nullptr};
     std::vector<Piece> *pc;
     ~Guard() {
-      for (uint8_t *p : pin)
-        if (p) (void)hipHostFree(p);
       for (Piece &x : *pc)
         if (x.ev) (void)hipEventDestroy(x.ev);
-      release(c->gz_out);
+      release(c->gz_out);   // (to the device block cache: the next file's output buffer)
     }
-  } guard{ctx, {nullptr, nullptr}, &pieces};
+  } guard{ctx, &pieces};
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
   const int64_t SLOT_B = (int64_t)1 << 26;
-  for (auto &p : guard.pin) HIPCHK(ctx, hipHostMalloc((void **)&p, (size_t)SLOT_B, hipHostMallocDefault));
+  for (auto &p : ctx->h_bam_pin)
+    if (!p) HIPCHK(ctx, hipHostMalloc((void **)&p, (size_t)SLOT_B, hipHostMallocDefault));
+  uint8_t *const pin[2] = {ctx->h_bam_pin[0], ctx->h_bam_pin[1]};
   const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
                                            B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
@@ -1557,7 +1559,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
       hipEvent_t ev;
       if (!take(&o, &m, &ev)) return false;
       hipError_t e = hipStreamWaitEvent(ctx->stream2, ev, 0);
-      if (e == hipSuccess) e = hipMemcpyAsync(guard.pin[s], z + o, (size_t)m, hipMemcpyDeviceToHost, ctx->stream2);
+      if (e == hipSuccess) e = hipMemcpyAsync(pin[s], z + o, (size_t)m, hipMemcpyDeviceToHost, ctx->stream2);
       if (e != hipSuccess) {
         werr = (int)e;
         return false;
@@ -1576,7 +1578,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
         return false;
       }
       const int s = cur;
-      *buf = guard.pin[s];
+      *buf = pin[s];
       *len = len_cur;
       have = issue(s ^ 1, &len_next);   // the following sub-piece into the other slot, while this one is written
       len_cur = len_next;

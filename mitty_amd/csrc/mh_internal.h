@@ -293,6 +293,8 @@ struct mh_ctx {
   int8_t res_state[RES_N] = {};          // 0 free, 1 queued (event), 2 filled by the host (synchronous fallback)
   int32_t res_next = 0;
   int64_t *h_small = nullptr;            // pinned 4 KiB for small readbacks (no staged copy per value)
+  uint8_t *h_bam_pin[2] = {nullptr, nullptr};   // mh_bam_write_gpu's two 64 MiB D2H slots (kept: page-locking
+                                                // 128 MiB per BAM file cost ~13 ms)
 
   // timing
   bool timing = false;
