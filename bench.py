@@ -399,6 +399,11 @@ def run_tumor_normal(a):
   bam_file_s = time.perf_counter() - t0
   # the same file with the record blocks deflated on the device (mh_bam_write_gpu) and its BAI: the whole configs[4]
   # pipeline per step is then the timed step + this
+  # (twice: the first call also allocates the compressed-output buffer and the staging slots, which a per-step
+  # pipeline keeps; the second is the steady state the per-step figure below uses)
+  t0 = time.perf_counter()
+  eng.ctx.bam_write_gpu('/dev/null', '@HD\tVN:1.0\tSO:coordinate\n', bai_path='/dev/null')
+  bam_gpu_first_s = time.perf_counter() - t0
   t0 = time.perf_counter()
   _, _, bam_gpu_file_bytes = eng.ctx.bam_write_gpu('/dev/null', '@HD\tVN:1.0\tSO:coordinate\n', bai_path='/dev/null')
   bam_gpu_s = time.perf_counter() - t0
@@ -417,9 +422,11 @@ def run_tumor_normal(a):
                'templates_per_step': kept // a.steps, 'bam_records_per_step': n_rec},
     'bam_bytes_per_step': bam_bytes, 'fastq_bytes_per_step': (b1 + b2) // a.steps,
     'bam_file_after_timing': {'seconds': bam_file_s, 'level': 1, 'threads': threads, 'sink': '/dev/null'},
-    'bam_file_gpu': {'seconds': bam_gpu_s, 'file_bytes': bam_gpu_file_bytes, 'sink': '/dev/null', 'bai': True,
+    'bam_file_gpu': {'seconds': bam_gpu_s, 'first_call_seconds': bam_gpu_first_s, 'file_bytes': bam_gpu_file_bytes,
+                     'sink': '/dev/null', 'bai': True,
                      'note': 'the record blocks deflated on the device (mh_bam_write_gpu), D2H of the compressed '
-                             'bytes, header block and BAI on the host'},
+                             'bytes, header block and BAI on the host; seconds = a second call (the buffers the '
+                             'first one allocated are reused), first_call_seconds = the first'},
     'with_bam_file': {'seconds_per_step': ms_per_step / 1e3 + bam_gpu_s,
                       'value': (kept / a.steps) / (ms_per_step / 1e3 + bam_gpu_s), 'unit': 'templates/s',
                       'note': 'the timed step (mix + BAM records sorted in HBM) plus the BAM file with BAI written '
