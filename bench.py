@@ -94,9 +94,11 @@ def parse():
   ap.add_argument('--batch-ramp', type=int, default=0,
                   help='wgs: the first K batches of a step are 2^-K, 2^-(K-1), .. of --batch-draws (the first writer '
                        'starts after a small batch is sampled, not a full one)')
-  ap.add_argument('--min-batches', type=int, default=4,
+  ap.add_argument('--min-batches', type=int, default=2,
                   help='wgs: at least this many batches per rank and step (a rank\'s share at N = 8 is ~1/8 of the '
-                       'genome: smaller batches keep its sampling beside its writers)')
+                       'genome: a second batch keeps its sampling beside its writers; rank 0\'s share timed alone, '
+                       'two batches against four: +6.8 %% at N = 8, +4 %% at N = 4, equal at N = 2, round 4; N = 1 '
+                       'has six by --batch-draws)')
   ap.add_argument('--plan-share', default=None, metavar='R/N',
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
