@@ -51,7 +51,9 @@ def parse():
   ap = argparse.ArgumentParser()
   ap.add_argument('--gpus', type=int, default=1)
   ap.add_argument('--steps', type=int, default=10)
-  ap.add_argument('--warmup', type=int, default=2)
+  # (the first bench process on a fresh box ran 13 % slow with 2 warm-up steps in three calls, and at the rate of the
+  # later processes with 40: profiles/r04/firstrun/)
+  ap.add_argument('--warmup', type=int, default=30)
   ap.add_argument('--model', default='hiseq-X-v2.5-Garvan')
   ap.add_argument('--coverage', type=float, default=30.0)
   ap.add_argument('--length', type=int, default=CHR1)
