@@ -78,11 +78,6 @@ def parse():
   ap.add_argument('--e2e-gz', action=argparse.BooleanOptionalAction, default=True,
                   help='end-to-end leg: also with BGZF-compressed output (host deflate, level 1)')
   ap.add_argument('--stages', action='store_true', help='print per-stage timings to stderr')
-  ap.add_argument('--emit-mode', type=int, default=0, help='0: direct writer, 1: LDS-image writer')
-  ap.add_argument('--async-emit', action='store_true',
-                  help='chr1: the pipelined emission path (mh_emit_async: measure, offsets and writer on the writer '
-                       'stream, no host readback) instead of the default (measure on the main stream); the same step '
-                       'time on the pool, with the writer sharing the chip with more of the sampling')
   ap.add_argument('--tumor-normal', action='store_true',
                   help='BASELINE configs[4] on one GPU: tumor 60x + normal 30x, 2x250 model (1kg-pcr-free), mixed '
                        'into one FASTQ pair, + the god-aligner BAM records built and coordinate-sorted in HBM')
@@ -95,9 +90,6 @@ def parse():
   ap.add_argument('--batch-draws', type=float, default=64e6,
                   help='wgs: units are sampled in batches of about this many template draws (a chr1 job is 30 M); '
                        'the FASTQ arenas are recycled per batch')
-  ap.add_argument('--batch-ramp', type=int, default=0,
-                  help='wgs: the first K batches of a step are 2^-K, 2^-(K-1), .. of --batch-draws (the first writer '
-                       'starts after a small batch is sampled, not a full one)')
   ap.add_argument('--min-batches', type=int, default=2,
                   help='wgs: at least this many batches per rank and step (a rank\'s share at N = 8 is ~1/8 of the '
                        'genome: a second batch keeps its sampling beside its writers; rank 0\'s share timed alone, '
@@ -107,27 +99,6 @@ def parse():
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
-  ap.add_argument('--unit0-in-chunk', action='store_true',
-                  help='wgs: a batch\'s unit 0 prepared with the next units before its writer is queued (round 4\'s '
-                       'default before the A/B; the default queues unit 0\'s writer first)')
-  ap.add_argument('--hip-runtime', default='rocm', choices=['rocm', 'torch'],
-                  help='the HIP runtime the library runs on at N = 1 without a process group: rocm = /opt/rocm\'s, '
-                       'which libmitty_hip.so links; torch = the copy torch ships (loaded first), as at N > 1')
-  ap.add_argument('--unit-order', default='ps', choices=['ps', 'copy'],
-                  help='wgs: the order a rank emits its units in: ps = the reference\'s unit order; copy = grouped by '
-                       '(region, copy), so both passes of a haplotype run back to back (the arena bytes per unit are '
-                       'the same; only their order in the step differs)')
-  ap.add_argument('--pipeline', default='batch', choices=['batch', 'lookahead', 'phased', 'phased-sync'],
-                  help='wgs: batch = sample a batch, emit it, next batch (the sampling of batch k+1 beside the '
-                       'writers of batch k); lookahead = batch k+1\'s sampling up to its permutation sort queued '
-                       'before batch k\'s writers, which wait for that sort (MH_WRITER_GATE=0); phased = sample every '
-                       'unit of the step, then emit every unit (phased-sync: and the step starts after the previous '
-                       'step\'s writers)')
-  ap.add_argument('--sync-tail', action='store_true',
-                  help='wgs batch pipeline: the host waits for each batch\'s whole sampling (mh_sample_units) instead '
-                       'of resolving its units one by one (mh_sample_units_async)')
-  ap.add_argument('--emit-chunk-bytes', type=float, default=24e9,
-                  help='wgs phased: FASTQ arenas recycled after about this many bytes')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
                   help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
                        '--threads 2)')
@@ -306,21 +277,16 @@ def run_chr1(a):
   eng.load_region(0, ('1', 0, a.length), seq)
   for cpy in range(len(copies)):   # inputs resident in HBM before timing: contig and both copies' variants
     eng.upload_variants(0, cpy, copies[cpy])
-  eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
+  kernel = 'k_emit_tiles'
 
   def step():
     # one chr1 job; consecutive jobs pipeline on the device (this job's splice and sampling run while the previous
     # job's last FASTQ writers drain); the timed region ends with a full synchronisation
     eng.drop_haplotypes()
     eng.ctx.reset_output()
-    pend = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
-                         rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=a.async_emit)
-
-    def get():
-      res = pend.resolve() if hasattr(pend, 'resolve') else pend
-      return sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)
-    return get
+    res = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
+                        rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
+    return lambda: (sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res))
 
   dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
   eng.close()
@@ -512,18 +478,17 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     os.rmdir(d)
 
 
-def plan_batches(mine, draws_of_region, target, min_batches=1, ramp=0):
+def plan_batches(mine, draws_of_region, target, min_batches=1):
   """A rank's units [(ps, ri, cpy, seed)] in batches of about `target` template draws (draws_of_region[ri] per
   unit), in ps order; at least `min_batches` batches when the rank has that many units (so its sampling of one batch
-  runs beside its writers of the previous one); the first `ramp` batches 2^-ramp, 2^-(ramp-1), .. of the size.
-  Returns (batches, the batch size used, the rank's draws)."""
+  runs beside its writers of the previous one).  Returns (batches, the batch size used, the rank's draws)."""
   total = sum(int(draws_of_region[u[1]]) for u in mine)
   size = min(target, total / max(1, min_batches))
   batches, cur, draws = [], [], 0
   for u in mine:
     cur.append(u)
     draws += int(draws_of_region[u[1]])
-    if draws >= size / 2 ** max(0, ramp - len(batches)):
+    if draws >= size:
       batches.append(cur)
       cur, draws = [], 0
   if cur:
@@ -537,7 +502,7 @@ def run_genome(a, rank, world, local):
   per batch), an all-reduce of the counts closing each step."""
   # a process group at N > 1, and at N = 1 when MH_DIST_BACKEND names one (the RCCL path exercised on one GPU)
   use_pg = world > 1 or bool(os.environ.get('MH_DIST_BACKEND'))
-  if use_pg or a.hip_runtime == 'torch':
+  if use_pg:
     # torch before libmitty_hip: a process holds ONE HIP runtime, and whichever library loads first provides it
     # (ours needs libamdhip64.so.7, which torch's copy satisfies; torch's own libamdhip64.so would not reuse ours)
     import torch  # noqa: F401
@@ -558,8 +523,6 @@ def run_genome(a, rank, world, local):
       sys.exit('bench.py: --plan-share R/N runs in one process (0 <= R < N)')
   pieces = D.plan_pieces(weights, plan_world, 'lpt')                  # 100 units: whole units by LPT at any N
   mine = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units) if pieces[ps][3] == plan_rank]
-  if a.unit_order == 'copy':
-    mine.sort(key=lambda u: (u[1], u[2], u[0]))
   regions = sorted({ri for _, ri, _, _ in mine})
   t_synth = time.perf_counter()
   data = synth.genome_regions(contigs, regions, workers=max(1, a.synth_workers // world))
@@ -586,11 +549,7 @@ def run_genome(a, rank, world, local):
     if dist.get_world_size() != world:
       sys.exit('bench.py: the process group has {} ranks, WORLD_SIZE={}'.format(dist.get_world_size(), world))
   from mitty_amd.engine import Engine
-  if a.pipeline == 'lookahead':
-    os.environ.setdefault('MH_WRITER_GATE', '0')   # read when the library context is created
   eng = Engine(local)
-  eng.async_tail = not a.sync_tail
-  eng.unit0_alone = not a.unit0_in_chunk
   copies = {}
   for ri in regions:
     name, length = contigs[ri]
@@ -598,72 +557,22 @@ def run_genome(a, rank, world, local):
     eng.load_region(ri, (name, 0, length), seq)
     for cpy in (0, 1):
       eng.upload_variants(ri, cpy, copies[ri][cpy])
-  eng.ctx.set_emit_mode(a.emit_mode)
-  kernel = 'k_emit_write' if a.emit_mode else 'k_emit_tiles'
+  kernel = 'k_emit_tiles'
   batches, batch_draws, mine_draws = plan_batches(mine, [L * p * 1.2 for _, L in contigs], a.batch_draws,
-                                                  a.min_batches, a.batch_ramp)
+                                                  a.min_batches)
   if dist is not None:
     import torch
     dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
 
-  tpl_flip = [0]
-  soa_of = lambda r, c: copies[r][c]
-
-  def step_phased():
-    if a.pipeline == 'phased-sync':
-      eng.ctx.sync()   # the previous step's writers drain before this step's sampling starts
-    eng.drop_haplotypes()
-    base = tpl_flip[0] = (1 << 20) - tpl_flip[0]   # template ids alternate per step (a step's writers may still run)
-    ids, k = [], 0
-    for batch in batches:   # every unit sampled first ...
-      eng.sample_only(batch, soa_of, p, rlen, model['cum_tlen'], base + k, a.rng)
-      ids.append(list(range(base + k, base + k + len(batch))))
-      k += len(batch)
-    kept = b1 = b2 = 0
-    units_all = [u for b in batches for u in b]
-    ids_all = [i for x in ids for i in x]
-    est = 0
-    c0 = 0
-    eng.ctx.reset_output()
-    for j, u in enumerate(units_all):   # ... then emitted in order, the arenas recycled every --emit-chunk-bytes
-      est += int(contigs[u[1]][1] * p * 740)   # ~L p templates of ~740 FASTQ bytes
-      if est >= a.emit_chunk_bytes or j == len(units_all) - 1:
-        for kp, x1, x2 in eng.emit_only(units_all[c0:j + 1], ids_all[c0:j + 1], soa_of, 'SYN', 0, True):
-          kept, b1, b2 = kept + kp, b1 + x1, b2 + x2
-        eng.ctx.reset_output()
-        c0, est = j + 1, 0
-    if dist is not None:
-      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
-      dist.all_reduce(counts)
-    return lambda: (kept, b1, b2)
-
-  def step_lookahead():
-    eng.drop_haplotypes()
-    res = eng.run_batches_lookahead(batches, soa_of, p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
-                                    on_batch=lambda k: eng.ctx.reset_output())
-    kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
-    if dist is not None:
-      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
-      dist.all_reduce(counts)
-    return lambda: (kept, b1, b2)
-
   def step():
-    if a.pipeline == 'lookahead':
-      return step_lookahead()
-    if a.pipeline != 'batch':
-      return step_phased()
     eng.drop_haplotypes()
     res = []
     for batch in batches:
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
-      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it.  --async-emit: the batch's
-      # measure passes and writers are queued without a host round trip per unit (mh_emit_async), so the host moves
-      # on to the next batch's splice and sampling while they run
+      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it
       eng.ctx.reset_output()
-      res.append(eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng,
-                               lazy=a.async_emit))
-    res = [u for r in res for u in (r.resolve() if hasattr(r, 'resolve') else r)]
+      res += eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
     kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
     if dist is not None:
       counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
@@ -731,7 +640,6 @@ def run_genome(a, rank, world, local):
                                             a.model, rlen, a.coverage, a.rng, world),
                'genome_bp': sum(L for _, L in contigs), 'read_model': a.model, 'coverage': a.coverage,
                'units': n_units, 'batches_rank0': len(batches), 'batch_draws': batch_draws,
-               'batch_ramp': a.batch_ramp, 'pipeline': a.pipeline,
                'templates_per_step': kept_all // steps,
                'parallelism': 'unit-shard (LPT) x{}'.format(world) if world > 1 else 'single GPU',
                'world_size_seen': seen, 'collective_backend': backend},

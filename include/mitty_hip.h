@@ -126,15 +126,6 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
 int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
                         const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                         int32_t rng_mode, int64_t *out_n);
-/* The batched form in two halves, so the next batch's permutation sort can be queued ahead of this batch's FASTQ
- * writers (the lookahead pipeline; readgenerate.py:102-115 runs units in worker processes instead): _begin queues
- * the word streams, the decode, the geometric scans and the sort; _end queues the rest and returns out_n as
- * mh_sample_units does.  One batch may be begun at a time; emissions may be queued in between (with the writer gate
- * on, their writers then wait for the begun batch's sort). */
-int32_t mh_sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
-                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                              int32_t rng_mode);
-int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
 /* mh_sample_units without the host wait at its end: each unit's last stages (its part of the permutation chase, its
  * template lengths and compaction; readgenerate.py:129-159 per unit) are queued in unit order on a second stream,
  * and the unit's template set is resolved when first used (mh_use_templates, mh_templates_count, or any entry
@@ -190,19 +181,6 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
 int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                         int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                         int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
-/* mh_emit_reads without a host round trip (the engine's pipelined path; same bytes, readgenerate.py:184-230): the
- * unit's measure pass, record offsets, writer and corruption are queued on the writer stream and the call returns a
- * ticket at once.  The unit lands in the arenas after the units queued before it (its base offsets come from the
- * device); room is reserved from mh_haplotype_read_bound.  mh_emit_result waits for the ticket's unit and returns its
- * kept count, bytes and base offsets per file (256 result slots: a ticket not read before its slot is handed out
- * again, 256 emissions later, is rejected as stale with MH_E_STATE). */
-int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
-                      int32_t write_fastq2, uint64_t unit_key, int32_t *out_ticket);
-int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2,
-                       int64_t *out_base1, int64_t *out_base2);
-/* An upper bound on the qname part of one read of length rlen from the haplotype in `slot` ('|' strand '|' POS '|'
- * rlen '|' CIGAR '|' v-list, readgenerate.py:223-225): the priciest window of nodes a read can span (rpc.py:119-160). */
-int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t *out_bytes);
 /* Templates in [t_begin, t_end) of the current set that survive the N filter (readgenerate.py:201-204). */
 int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end, int64_t *out_kept);
 int32_t mh_output_size(mh_ctx *ctx, int64_t *bytes1, int64_t *bytes2);

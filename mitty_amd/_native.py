@@ -20,8 +20,8 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_selftest_scan_fault',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_async', 'mh_emit_result', 'mh_haplotype_read_bound', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim',
-           'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_begin', 'mh_sample_units_end', 'mh_sample_units_async', 'mh_templates_count',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim',
+           'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
            'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
@@ -99,9 +99,6 @@ def lib():
   _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_emit_prepare', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_build_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
-  _sig(L, 'mh_emit_async', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, ctypes.POINTER(c_i32)])
-  _sig(L, 'mh_emit_result', [c_vp, c_i32, P_i64, P_i64, P_i64, P_i64, P_i64])
-  _sig(L, 'mh_haplotype_read_bound', [c_vp, c_i32, c_i32, ctypes.POINTER(c_i32)])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
@@ -149,8 +146,6 @@ def lib():
                              ctypes.POINTER(c_i32)])
   _sig(L, 'mh_enable_timing', [c_vp, c_i32])
   _sig(L, 'mh_sample_units', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32, c_vp])
-  _sig(L, 'mh_sample_units_begin', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32])
-  _sig(L, 'mh_sample_units_end', [c_vp, c_i32, c_vp])
   _sig(L, 'mh_sample_units_async', [c_vp, c_i32, c_vp, c_vp, c_vp, c_dbl, c_i32, c_vp, c_i32, c_i32])
   _sig(L, 'mh_templates_count', [c_vp, c_i32, c_vp])
   _sig(L, 'mh_use_templates', [c_vp, c_i32])
@@ -490,22 +485,6 @@ class Context:
                                       _ptr(ct), len(ct), int(rng_mode), _ptr(out)))
     return out[:len(ids)]
 
-  def sample_units_begin(self, tpl_ids, slots, seeds, p, rlen, cum_tlen, rng_mode=MH_RNG_MITTY):
-    """First half of sample_units (queued up to the permutation's sort); sample_units_end finishes it."""
-    ids = np.ascontiguousarray(tpl_ids, dtype=np.int32)
-    sl = np.ascontiguousarray(slots, dtype=np.int32)
-    sd = np.ascontiguousarray(seeds, dtype=np.uint64)
-    ct = np.ascontiguousarray(cum_tlen, dtype=np.float64)
-    self._chk(self._L.mh_sample_units_begin(self._h, len(ids), _ptr(ids), _ptr(sl), _ptr(sd), float(p), int(rlen),
-                                            _ptr(ct), len(ct), int(rng_mode)))
-    return len(ids)
-
-  def sample_units_end(self, n_units):
-    """The begun batch finished; returns templates kept per unit."""
-    out = np.zeros(max(n_units, 1), dtype=np.int64)
-    self._chk(self._L.mh_sample_units_end(self._h, int(n_units), _ptr(out)))
-    return out[:n_units]
-
   def sample_units_async(self, tpl_ids, slots, seeds, p, rlen, cum_tlen, rng_mode=MH_RNG_MITTY):
     """sample_units whose per-unit tails run on without a host wait; template_count(id) (or use_templates) waits
     for one unit."""
@@ -556,25 +535,6 @@ class Context:
     return fo0[:m], p0[:m], p1[:m]
 
   # ---- emission ----------------------------------------------------------------------------------------
-  def emit_async(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
-    """Queue one unit's emission (measure, offsets, writer, corruption) on the writer stream; returns a ticket for
-    emit_result."""
-    t = c_i32()
-    self._chk(self._L.mh_emit_async(self._h, int(slot), serial_stub.encode(), chrom.encode(), int(cpy),
-                                    1 if write_fastq2 else 0, int(unit_key), ctypes.byref(t)))
-    return t.value
-
-  def emit_result(self, ticket):
-    """(kept, bytes1, bytes2, base1, base2) of an emit_async ticket (waits for its unit)."""
-    r = [c_i64() for _ in range(5)]
-    self._chk(self._L.mh_emit_result(self._h, int(ticket), *[ctypes.byref(x) for x in r]))
-    return tuple(x.value for x in r)
-
-  def read_bound(self, slot, rlen):
-    out = c_i32()
-    self._chk(self._L.mh_haplotype_read_bound(self._h, int(slot), int(rlen), ctypes.byref(out)))
-    return out.value
-
   def emit_prepare(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, wait=True):
     """The measure pass and record offsets of the current templates (the next emit_reads of the same unit only
     queues the writer).  Returns (kept, bytes1, bytes2); with wait=False it returns None at once, without waiting

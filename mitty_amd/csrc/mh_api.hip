@@ -138,7 +138,6 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.cap >= bytes) return MH_OK;
   if (b.p) {
-    gate_open(ctx);
     MH_TRY(sync_writers(ctx));   // a queued FASTQ writer (or corruption pass) may still read or write it
     SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     lb_forget(b.p);
@@ -161,7 +160,6 @@ int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
   if (b.cap >= bytes) return MH_OK;
   DevBuf nb;
   MH_TRY(ensure(ctx, nb, bytes + bytes / 2));
-  gate_open(ctx);
   MH_TRY(sync_writers(ctx));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -186,48 +184,19 @@ void release_hap(Hap &h) {
   h.used_set = false;
 }
 
-int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set, uint32_t &gate) {
+int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set) {
   if (!ev) HIPCHK(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIPCHK(ctx, hipEventRecord(ev, ctx->wstream));
   set = true;
-  gate = ctx->gate_waited;
   return MH_OK;
 }
 
-int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, uint32_t gate) {
-  if (set) {
-    gate_open_for(ctx, gate);
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
-  }
-  return MH_OK;
-}
-
-
-static std::mutex g_gate_mu;   // gate_written is read-modify-written by both splice lanes (ensure -> gate_open)
-
-void gate_open(mh_ctx *ctx) {
-  if (!ctx->gate) return;
-  std::lock_guard<std::mutex> lk(g_gate_mu);
-  if (ctx->gate_waited <= ctx->gate_written) return;
-  (void)hipStreamWriteValue32(ctx->gstream, ctx->gate, ctx->gate_waited, 0);
-  ctx->gate_written = ctx->gate_waited;
-}
-
-void gate_open_for(mh_ctx *ctx, uint32_t need) {
-  if (ctx->gate && need > ctx->gate_written) gate_open(ctx);
-}
-
-int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value) {
-  if (!ctx->gate) return MH_OK;
-  std::lock_guard<std::mutex> lk(g_gate_mu);
-  if (value <= ctx->gate_written) return MH_OK;
-  HIPCHK(ctx, hipStreamWriteValue32(st, ctx->gate, value, 0));
-  ctx->gate_written = value;
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set) {
+  if (set) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
   return MH_OK;
 }
 
 int32_t sync_writers(mh_ctx *ctx) {
-  gate_open(ctx);
   SYNCCHK(ctx, hipStreamSynchronize(ctx->wstream));
   return MH_OK;
 }
@@ -262,7 +231,6 @@ int64_t *pinned_small(mh_ctx *ctx) {
 
 int32_t join_writer(mh_ctx *ctx) {
   if (!ctx->writer_pending) return MH_OK;
-  gate_open(ctx);
   HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_writer, 0));
   ctx->writer_pending = false;
   return MH_OK;
@@ -286,7 +254,6 @@ void stage_end(mh_ctx *ctx) {
 }
 
 void stages_collect(mh_ctx *ctx) {
-  gate_open(ctx);
   for (auto &s : ctx->pending) {
     (void)hipEventSynchronize(s.b);
     float ms = 0.f;
@@ -388,28 +355,8 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->max_cu = prop.multiProcessorCount;
-  // the writer gate (mh_internal.h): opt-in (MH_WRITER_GATE = the index of a job's first writer that waits; the
-  // bench measured 2-3 % shorter steps with 2 or 3, with slower writers), off when the device cannot wait on memory
-  const char *ge = getenv("MH_WRITER_GATE");
-  ctx->gate_at = ge ? atoi(ge) : -1;
-  const char *hf = getenv("MH_HAP_FWD");
-  ctx->hap_fwd = hf && atoi(hf) != 0;
   const char *so = getenv("MH_SORT");
   ctx->sort_lsd = so && !strcmp(so, "lsd");
-  const char *gt = getenv("MH_WRITER_GATE_TAIL");
-  ctx->gate_tail = gt ? std::max(0, atoi(gt)) : 0;
-  int can_wait = 0;
-  if (hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device) != hipSuccess) can_wait = 0;
-  (void)hipGetLastError();
-  if ((ctx->gate_at >= 0 || ctx->gate_tail > 0) && can_wait) {
-    void *g = nullptr;
-    if (hipStreamCreateWithFlags(&ctx->gstream, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&ctx->ev_sorted, hipEventDisableTiming) == hipSuccess &&
-        (hipExtMallocWithFlags(&g, 8, hipMallocSignalMemory) == hipSuccess || hipMalloc(&g, 64) == hipSuccess) &&
-        hipStreamWriteValue32(ctx->gstream, g, 0, 0) == hipSuccess && hipStreamSynchronize(ctx->gstream) == hipSuccess)
-      ctx->gate = (uint32_t *)g;
-    (void)hipGetLastError();
-  }
   *out = ctx;
   return MH_OK;
 }
@@ -417,7 +364,6 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
 int32_t mh_destroy(mh_ctx *ctx) {
   if (!ctx) return MH_OK;
   (void)hipSetDevice(ctx->device);
-  gate_open(ctx);
   (void)hipStreamSynchronize(ctx->wstream);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -441,20 +387,13 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &l : ctx->xlane)
     for (auto &b : l) release(b);
   for (auto &b : ctx->xscan) release(b);
-  for (auto &u : ctx->usort)
-    for (auto &b : u) release(b);
   release(ctx->scan_partials); release(ctx->scan_partials2); release(ctx->d_small);
   release(ctx->corrupt_cum); release(ctx->corrupt_phred);
   release(ctx->out1); release(ctx->out2);
-  release(ctx->d_used);
   release(ctx->cr_rows);
   release(ctx->cr_codes);
   release(ctx->scan_partials_w);
-  release(ctx->rb_tmp);
   for (auto &b : ctx->sl2) release(b);
-  for (auto &e : ctx->res_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->h_res) (void)hipHostFree(ctx->h_res);
   ctx->tail_state.reset();
   for (hipEvent_t e : ctx->ev_gz)
     if (e) (void)hipEventDestroy(e);
@@ -465,7 +404,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (uint8_t *p : ctx->h_bam_pin)
     if (p) (void)hipHostFree(p);
   for (auto &e : ctx->eset) {
-    release(e.recs); release(e.off); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
+    release(e.recs); release(e.off); release(e.strip); release(e.ovf); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
     if (e.rb) (void)hipEventDestroy(e.rb);
     if (e.h_stat) (void)hipHostFree(e.h_stat);
@@ -476,10 +415,6 @@ int32_t mh_destroy(mh_ctx *ctx) {
   bam_release(ctx->bam);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->gstream) (void)hipStreamSynchronize(ctx->gstream);
-  if (ctx->gate) (void)hipFree(ctx->gate);
-  if (ctx->ev_sorted) (void)hipEventDestroy(ctx->ev_sorted);
-  if (ctx->gstream) (void)hipStreamDestroy(ctx->gstream);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
   for (int l = 0; l < 2; l++) {
     if (ctx->xstream[l]) (void)hipStreamDestroy(ctx->xstream[l]);
@@ -612,15 +547,14 @@ static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, int64_t need, Hap **out)
       const Hap &s = ctx->hap_spare[best];
       r.hap = s.hap; r.rc = s.rc; r.keys = s.keys; r.ps = s.ps; r.pr = s.pr; r.op = s.op; r.oplen = s.oplen;
       r.nrun_s = s.nrun_s; r.nrun_e = s.nrun_e; r.nd = s.nd; r.bkt = s.bkt;
-      r.used = s.used; r.used_set = s.used_set; r.used_gate = s.used_gate;
+      r.used = s.used; r.used_set = s.used_set;
       ctx->hap_spare.erase(ctx->hap_spare.begin() + best);
       ctx->haps[slot] = r;
     }
   }
   Hap &h = ctx->haps[slot];
-  MH_TRY(wait_unused(ctx, h.used, h.used_set, h.used_gate));   // a queued writer may still read the old bytes
+  MH_TRY(wait_unused(ctx, h.used, h.used_set));   // a queued writer may still read the old bytes
   h.valid = false;
-  h.rb_rlen = h.rb_bytes = 0;
   *out = &h;
   return MH_OK;
 }
@@ -776,13 +710,12 @@ int32_t mh_release_haplotype(mh_ctx *ctx, int32_t slot) {
   if (it == ctx->haps.end()) return MH_OK;
   Hap &h = it->second;
   // keep the buffers for the next build (stream order protects them: every later user is on ctx->stream)
-  // a whole genome's haplotypes (25 regions x 2 copies) plus pipelined generations (asynchronous emission)
+  // a whole genome's haplotypes (25 regions x 2 copies) plus the generation the queued writers still read
   constexpr size_t SPARE_MAX = 128;
   if (ctx->hap_spare.size() < SPARE_MAX) {
     h.valid = false;
     ctx->hap_spare.push_back(h);
   } else {
-    gate_open(ctx);
     MH_TRY(sync_writers(ctx));
     SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
     release_hap(h);
@@ -844,21 +777,6 @@ int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, co
   MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
   return sample_units(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen, rng_mode,
                       out_n);
-}
-
-int32_t mh_sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
-                              const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                              int32_t rng_mode) {
-  CTX_GUARD_NOJOIN(ctx);
-  std::vector<int64_t> pmin, pmax;
-  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
-  return sample_units_begin(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen,
-                            rng_mode);
-}
-
-int32_t mh_sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n) {
-  CTX_GUARD_NOJOIN(ctx);
-  return sample_units_end(ctx, n_units, out_n);
 }
 
 int32_t mh_sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
@@ -987,7 +905,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
     for (int64_t i = 0; i < n; i++)
       if (fo0[i] != 0 && fo0[i] != 1) return arg_fail(ctx, MH_E_ARG, "file_order must be 0/1");
   TplSet &ts = ctx->tsets[tpl_id];
-  MH_TRY(wait_unused(ctx, ts.used, ts.used_set, ts.used_gate));   // a queued FASTQ writer may still read the old templates
+  MH_TRY(wait_unused(ctx, ts.used, ts.used_set));   // a queued FASTQ writer may still read the old templates
   ts.valid = false;
   MH_TRY(ensure(ctx, ts.fo0, n + 16));
   MH_TRY(ensure(ctx, ts.pos0, 8 * (n + 16)));
@@ -1069,7 +987,6 @@ int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end,
 
 int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
   CTX_GUARD_EMIT(ctx);
-  MH_TRY(sync_async_fill(ctx));
   if (b1) *b1 = ctx->used1;
   if (b2) *b2 = ctx->used2;
   return MH_OK;
@@ -1077,7 +994,6 @@ int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
 
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2, int64_t len2) {
   CTX_GUARD(ctx);
-  MH_TRY(sync_async_fill(ctx));
   if ((fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
@@ -1105,7 +1021,6 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
 int32_t mh_output_fetch_async(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2,
                               int64_t len2, int32_t *ticket) {
   CTX_GUARD(ctx);
-  MH_TRY(sync_async_fill(ctx));
   if (!ticket || (fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
@@ -1147,36 +1062,7 @@ int32_t mh_output_reset(mh_ctx *ctx) {
       SYNCCHK(ctx, hipEventSynchronize(ctx->ev_fetch[t]));
       ctx->fetch_pending[t] = false;
     }
-  return output_reset(ctx);
-}
-
-int32_t mh_haplotype_read_bound(mh_ctx *ctx, int32_t slot, int32_t rlen, int32_t *out_bytes) {
-  CTX_GUARD_EMIT(ctx);
-  auto it = ctx->haps.find(slot);
-  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
-  if (rlen <= 0 || !out_bytes) return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  return read_part_bound(ctx, it->second, rlen, out_bytes);
-}
-
-int32_t mh_emit_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
-                      int32_t write_fastq2, uint64_t unit_key, int32_t *ticket) {
-  CTX_GUARD_EMIT(ctx);
-  auto it = ctx->haps.find(slot);
-  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
-  if (!serial_stub || !chrom || !ticket) return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  return emit_async(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, ticket);
-}
-
-int32_t mh_emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2,
-                       int64_t *out_base1, int64_t *out_base2) {
-  CTX_GUARD_EMIT(ctx);
-  int64_t r[5];
-  MH_TRY(emit_result(ctx, ticket, r));
-  if (out_kept) *out_kept = r[0];
-  if (out_b1) *out_b1 = r[1];
-  if (out_b2) *out_b2 = r[2];
-  if (out_base1) *out_base1 = r[3];
-  if (out_base2) *out_base2 = r[4];
+  ctx->used1 = ctx->used2 = 0;
   return MH_OK;
 }
 
@@ -1442,7 +1328,6 @@ int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char 
 
 int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates) {
   CTX_GUARD(ctx);
-  MH_TRY(sync_async_fill(ctx));
   if (!templates) return arg_fail(ctx, MH_E_ARG, "null argument");
   int64_t u1 = 0, u2 = 0;
   const bool two = ctx->used2 > 0;
@@ -1636,7 +1521,6 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
 int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
                          int64_t *used1, int64_t *used2, int64_t *templates) {
   CTX_GUARD(ctx);
-  MH_TRY(sync_async_fill(ctx));
   if (!fq1 || len1 < 0 || (fq2 && len2 < 0) || t_base < 0 || !used1 || !used2 || !templates)
     return arg_fail(ctx, MH_E_ARG, "null argument");
   MH_TRY(stage_in(ctx, ctx->bam.in1, fq1, len1));
@@ -1695,7 +1579,6 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
                              int64_t *used) {
   CTX_GUARD(ctx);
   if ((file != 0 && file != 1) || !used || offset < 0 || len < 0) return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  MH_TRY(sync_async_fill(ctx));
   MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
   const int64_t n = file ? ctx->used2 : ctx->used1;
   if (offset > n || len > n - offset) return arg_fail(ctx, MH_E_ARG, "range outside the arena");
@@ -1722,7 +1605,6 @@ int32_t mh_output_bgzf_pair(mh_ctx *ctx, int64_t offset, int64_t n1, int64_t n2,
   CTX_GUARD(ctx);
   if (!used1 || !used2 || !ticket || offset < 0 || n1 < 0 || n2 < 0 || (n1 && !out1) || (n2 && !out2))
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  MH_TRY(sync_async_fill(ctx));
   MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
   if ((n1 && offset + n1 > ctx->used1) || (n2 && offset + n2 > ctx->used2))
     return arg_fail(ctx, MH_E_ARG, "range outside the arena");
@@ -1789,6 +1671,5 @@ int32_t mh_output_bgzf_wait(mh_ctx *ctx, int32_t ticket) {
 int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used) {
   CTX_GUARD(ctx);
   if ((file != 0 && file != 1) || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
-  MH_TRY(sync_async_fill(ctx));
   return mh_output_bgzf_range(ctx, file, 0, file ? ctx->used2 : ctx->used1, out, cap, used);
 }

@@ -263,32 +263,100 @@ struct QFixed {
 
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
-// Length of one read's part of the qname ('|' strand '|' pos '|' rlen '|' cigar '|' v1,v2,..; readgenerate.py:223-225)
-// for the read of length rlen at p whose start / end nodes are n0 (node nd0) .. n1.
-__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
-                                                 bool special, int64_t pos, int64_t p, int64_t rlen) {
-  int32_t L = 3 + ndig_s(pos) + 1 + ndig_s(rlen) + 1 + 1;
-  if (special) L += 1 + ndig_s(p - nd0.ps()) + 1 + ndig_s(rlen) + 1;
-  int32_t nv = 0;
-  for (int64_t k = n0; k <= n1; k++) {
-    const Node16 n = k == n0 ? nd0 : h.nd[k];
-    if (!special) L += ndig_s(node_count(n, p, rlen)) + 1;
-    if (n.code() != 0) {
-      L += ndig_s(node_v(n)) + (nv ? 1 : 0);
-      nv++;
+// The qname's reads part (readgenerate.py:223-225: per read in file order '|' strand '|' POS '|' rlen '|' CIGAR '|'
+// v1,v2,..; then the line's '\n'), formatted by k_emit_measure into a strip the writer copies: ED_SW bytes per
+// template (one line-aligned slot), longer parts (a read spanning many variants: ~0.06 % of 2x150 templates at
+// 1.3 variants/kbp) whole in an overflow area, the slot then holding the overflow offset.
+constexpr int ED_SW = 64;
+constexpr int MS_ROW = ED_SW + 4;   // LDS row per thread (an odd number of dwords: lanes' equal columns in distinct banks)
+
+struct Strip {
+  char *slot;                 // [m][ED_SW]
+  char *ovf;                  // overflow parts
+  int64_t ovf_cap;
+  unsigned long long *ovf_used;
+};
+
+// Byte sinks of the part formatter: the thread's LDS row (bytes past ED_SW only counted), or global memory.
+struct RowSink {
+  char *row;
+  int32_t o = 0;
+  __device__ __forceinline__ void put(char c) {
+    if (o < ED_SW) row[o] = c;
+    o++;
+  }
+  __device__ __forceinline__ void dec(int64_t v) {
+    if (v < 0) {
+      put('-');
+      v = -v;
+    }
+    if ((uint64_t)v > 0xffffffffull) {
+      auto put = [&](uint8_t c) { this->put((char)c); };
+      put_big((uint64_t)v);
+      return;
+    }
+    uint32_t x = (uint32_t)v;
+    const int nd = ndig_u(x);
+    for (int i = nd - 1; i >= 0; i--) {
+      if (o + i < ED_SW) row[o + i] = (char)('0' + x % 10u);
+      x /= 10u;
+    }
+    o += nd;
+  }
+};
+struct GlobalSink {
+  char *g;
+  int32_t o = 0;
+  __device__ __forceinline__ void put(char c) { g[o++] = c; }
+  __device__ __forceinline__ void dec(int64_t v) { o = (int32_t)(put_s(g + o, v) - g); }
+};
+
+// One read's part: '|' s '|' POS '|' rlen '|' CIGAR '|' v-list (rpc.py:144-160; the special '>p:nI' CIGAR of a read
+// inside an insertion, rpc.py:150-157); nodes n0 (nd0) .. n1.
+template <class Sink>
+__device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
+                                              const ReadInfo &r, int s, int64_t p, int64_t rlen) {
+  k.put('|');
+  k.put((char)('0' + s));
+  k.put('|');
+  k.dec(r.pos);
+  k.put('|');
+  k.dec(rlen);
+  k.put('|');
+  if (r.special) {
+    k.put('>');
+    k.dec(p - nd0.ps());
+    k.put(':');
+    k.dec(rlen);
+    k.put('I');
+  } else {
+    for (int64_t j = n0; j <= n1; j++) {
+      const Node16 n = j == n0 ? nd0 : h.nd[j];
+      k.dec(node_count(n, p, rlen));
+      k.put((char)n.op());
     }
   }
-  return L;
+  k.put('|');
+  bool first = true;
+  for (int64_t j = n0; j <= n1; j++) {
+    const Node16 n = j == n0 ? nd0 : h.nd[j];
+    if (n.code() == 0) continue;
+    if (!first) k.put(',');
+    k.dec(node_v(n));
+    first = false;
+  }
 }
 
 // One thread per template: start/end node of both mates, POS, the N filter (readgenerate.py:201-204), the qname
-// reads part's length (not its text: the writer formats it) and the record lengths without the cnt digits, into
-// Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the longest record
-// (+20) and the longest reads part + '\n' as maxima (one atomic per wave).
+// reads part (formatted into the strip when st.slot is set; else only measured) and the record lengths without the
+// cnt digits, into Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the
+// longest record (+20) and the longest reads part + '\n' as maxima (one atomic per wave); max_rec[1] = 1 when the
+// overflow area was too small.
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
-                                                      Rec *recs, int4 *tsum, int32_t *max_rec) {
+                                                      Rec *recs, int4 *tsum, int32_t *max_rec, Strip st) {
   __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
+  __shared__ __attribute__((aligned(16))) char s_row[256 * MS_ROW];
   const bool runs_lds = h.n_runs <= MS_RUNS;
   if (runs_lds)
     for (int i = threadIdx.x; i < h.n_runs; i += 256) {
@@ -322,14 +390,35 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
-      const int32_t l0 = read_part_len(h, nn0[0], r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
-      const int32_t l1 = read_part_len(h, nn0[1], r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
-      const int32_t rest = l0 + l1;
+      // the reads part in file order (reads[fo] = mate 0, readgenerate.py:207), formatted into this thread's row
+      // (selects, not r[sa]: a dynamically indexed private array would live in scratch memory)
+      const int sa = f0 == 0 ? 0 : 1;
+      const ReadInfo ra = sa ? r[1] : r[0], rb = sa ? r[0] : r[1];
+      const Node16 na = sa ? nn0[1] : nn0[0], nb = sa ? nn0[0] : nn0[1];
+      const int64_t pa = sa ? p[1] : p[0], pb = sa ? p[0] : p[1];
+      RowSink k{s_row + threadIdx.x * MS_ROW};
+      fmt_read_part(k, h, na, ra.n0, ra.n1, ra, sa, pa, rlen);
+      const int32_t la = k.o;
+      fmt_read_part(k, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen);
+      k.put('\n');
+      const int32_t rest = k.o - 1;
+      if (st.slot && k.o > ED_SW) {   // the whole part in the overflow area; the slot holds its offset
+        const unsigned long long at = atomicAdd(st.ovf_used, (unsigned long long)k.o);
+        if ((int64_t)(at + k.o) <= st.ovf_cap) {
+          GlobalSink g{st.ovf + at};
+          fmt_read_part(g, h, na, ra.n0, ra.n1, ra, sa, pa, rlen);
+          fmt_read_part(g, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen);
+          g.put('\n');
+          __builtin_memcpy(s_row + threadIdx.x * MS_ROW, &at, 8);   // (a 4-byte aligned row)
+        } else {
+          max_rec[1] = 1;
+        }
+      }
       const int32_t ql = q.prefix_len + q.mid_len + rest;
       const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
       const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
       const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
-      out.keep = 1 | ((f0 == 0 ? l0 : l1) << 1);   // kept; the first read's part length (where the second starts)
+      out.keep = 1 | (la << 1);   // kept; the first read's part length (where the second starts)
       out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
       out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
       out.rest = rest;
@@ -340,6 +429,21 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       s2 = out.len2;
     }
     recs[t] = out;
+  }
+  if (st.slot) {
+    // the wave's 64 rows to its 64 consecutive slots: 16-byte chunks, consecutive lanes on consecutive chunks
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t tw = (int64_t)blockIdx.x * blockDim.x + 64 * w;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int c = lane + 64 * i, row = c >> 2, col = (c & 3) * 16;
+      if (tw + row < m) {
+        uint4 v;
+        __builtin_memcpy(&v, s_row + (64 * w + row) * MS_ROW + col, 16);
+        *(uint4 *)(st.slot + (tw + row) * ED_SW + col) = v;
+      }
+    }
   }
   if (tsum != nullptr) {   // the tile = the 32 lanes of a wave half
 #pragma unroll
@@ -630,29 +734,6 @@ struct DMeta {
   int32_t tn[2];     // T length: rlen + 4, or S + 4 with corruption (qualities = len(seq))
 };
 
-// decimal text of v at byte offset o of the dynamic LDS block; returns the offset after it
-__device__ __forceinline__ uint32_t lds_put_u(char *lds, uint32_t o, uint64_t v) {
-  if (v > 0xffffffffull) {
-    auto put = [&](uint8_t c) { lds[o++] = (char)c; };
-    put_big(v);
-    return o;
-  }
-  uint32_t x = (uint32_t)v;
-  const int nd = ndig_u(x);
-  for (int i = nd - 1; i >= 0; i--) {
-    lds[o + i] = (char)('0' + x % 10u);
-    x /= 10u;
-  }
-  return o + nd;
-}
-__device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) {
-  if (v < 0) {
-    lds[o] = '-';
-    return lds_put_u(lds, o + 1, (uint64_t)(-v));
-  }
-  return lds_put_u(lds, o, (uint64_t)v);
-}
-
 // 16 bytes at an arbitrary byte offset of the dynamic LDS block: one ds_read_b128 (gfx950 reads LDS unaligned; was
 // five aligned dword reads + v_alignbyte).  (Offsets, not pointers: an integer round trip of an LDS pointer turns
 // its reads into flat loads.)
@@ -820,31 +901,15 @@ struct TArgs {
   const Rec *recs;          // k_emit_measure's records
   const E3 *tpre;           // per tile: kept templates and record bytes (no cnt digits) before it
   char *arena[2];
-  int64_t used[2];          // arena offset of the emission's first byte per file (synchronous path)
-  const int64_t *d_base;    // asynchronous path: the same offsets from the device (the fill before the unit)
+  int64_t used[2];          // arena offset of the emission's first byte per file
   int64_t cnt_base;         // templates kept before the emission's first one (cnt numbering)
   uint2 *crec;              // corruption: per record the first base's arena offset and S (k_cr_inplace's words)
   int32_t rlen, win_stride, head, qstride;
+  const char *slot, *ovf;   // k_emit_measure's strip: per template the qname reads part (Strip)
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
   const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
 };
-
-// node k of a read whose first four nodes q0..q3 (from node n0) are in registers (selects on the words: an indexed
-// array of nodes would be placed in scratch)
-#define NODE_AT(k)                                                                                       \
-  Node16 n;                                                                                              \
-  {                                                                                                      \
-    const int64_t i_ = (k) - n0;                                                                         \
-    if (i_ > 3) {                                                                                        \
-      const uint64_t *g_ = (const uint64_t *)(h.nd + (k));                                               \
-      n.a = g_[0];                                                                                       \
-      n.b = g_[1];                                                                                       \
-    } else {                                                                                             \
-      n.a = i_ == 0 ? q0.a : i_ == 1 ? q1.a : i_ == 2 ? q2.a : q3.a;                                     \
-      n.b = i_ == 0 ? q0.b : i_ == 1 ? q1.b : i_ == 2 ? q2.b : q3.b;                                     \
-    }                                                                                                    \
-  }
 
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
@@ -914,13 +979,10 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     if (eg > h.hap_len) eg = h.hap_len;
     if (ag > h.hap_len) ag = h.hap_len;
     const int64_t lg = eg > ag ? eg - ag : 0;
-    // mate 1: a forward range of the reverse-complement haplotype, or (forward-only haplotypes) the forward window
-    // reverse-complemented on its way into LDS: chunk c lands mirrored at 16 (cmax - c), bytes reversed
-    const bool rev = sg && h.rc == nullptr;
-    const int64_t a2g = sg && !rev ? h.hap_len - ag - lg : ag;
+    // mate 1: a forward range of the reverse-complement haplotype
+    const int64_t a2g = sg ? h.hap_len - ag - lg : ag;
     const int64_t a16 = a2g & ~(int64_t)15;
-    const uint8_t *hsrc = (sg && !rev ? h.rc : h.hap) + a16;
-    const int32_t cmax = lg > 0 ? (int32_t)(((a2g + lg - 1) >> 4) - (a16 >> 4)) : 0;
+    const uint8_t *hsrc = (sg ? h.rc : h.hap) + a16;
     uint4 wv[ED_GMAX];
     uint32_t use = 0;
 #pragma unroll
@@ -930,16 +992,19 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       use |= (uint32_t)u << k;
       wv[k] = *(const uint4 *)(hsrc + (u ? 16 * c : 0));
     }
+    // waves 1-2 also copy the tile's strip slots (the qname reads parts k_emit_measure formatted): 16 bytes each, to
+    // the qname buffer after its head room
+    const int js = g >> 2, cs = g & 3;
+    const bool ks = g < 4 * ED_T && js < nt;
+    uint4 sv = make_uint4(0, 0, 0, 0);
+    if (ks) sv = *(const uint4 *)(A.slot + (t0 + js) * ED_SW + 16 * cs);
     const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
 #pragma unroll
     for (int k = 0; k < ED_GMAX; k++) {
       const int c = q3 + 3 * k;
-      uint4 v = wv[k];
-      if (rev)
-        v = make_uint4(comp4(__builtin_bswap32(v.w)), comp4(__builtin_bswap32(v.z)), comp4(__builtin_bswap32(v.y)),
-                       comp4(__builtin_bswap32(v.x)));
-      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * (rev ? cmax - c : c) : o_dump)) = v;
+      *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * c : o_dump)) = wv[k];
     }
+    if (ks) __builtin_memcpy(smem + o_q + js * qstride + head + 16 * cs, &sv, 16);
   } else if (tid < 64) {
     // wave 0: lane = read (template jf, mate s)
     const int jf = tid >> 1, s = tid & 1;
@@ -949,64 +1014,25 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     const int fo = A.fo0[tf];
     const int fr = s == 0 ? fo : 1 - fo;   // the read's place in the qname = its file (reads[fo] = mate 0, :207)
     const int64_t rl = A.rlen;
-    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length, nodes
-    const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
+    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length
+    const int4 r0 = *(const int4 *)(A.recs + tf);
     const E3 P = A.tpre[tile];
-    const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
     const bool keep = valid && (r0.x & 1);
     const int32_t rest = r0.w;
-    // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
-    const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
-                 q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
     int64_t a = p - h.p_min, e = p + rl - h.p_min;   // the read's bases: hap[a, a + S)
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
-#ifdef EW_CALIB_NOFMT2   // (calibration: the nodes loaded, their words kept, nothing formatted)
-    if (keep) smem[o_q + jf * qstride + head] = (char)(q0.a ^ q1.a ^ q2.a ^ q3.a ^ q0.b ^ q1.b ^ q2.b ^ q3.b);
-#define EW_CALIB_NOFMT
-#endif
-#ifndef EW_CALIB_NOFMT   // (calibration builds only, `make variant V=NOFMT`: the reads parts left unwritten)
-    if (keep) {
-      ReadInfo ri;
-      ri.n0 = n0;
-      ri.n1 = n1;
-      read_place(h, q0, p, rl, ri);
-      // the read's part of the qname at its place (readgenerate.py:223-225); read 1 ends at `rest`, where the '\n' goes
-      uint32_t o = (uint32_t)(o_q + jf * qstride + head);
-      if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part
-      smem[o] = '|';
-      smem[o + 1] = (char)('0' + s);
-      smem[o + 2] = '|';
-      o = lds_put_s(smem, o + 3, ri.pos);
-      smem[o] = '|';
-      o = lds_put_s(smem, o + 1, rl);
-      smem[o++] = '|';
-      if (ri.special) {
-        smem[o] = '>';
-        o = lds_put_s(smem, o + 1, p - q0.ps());
-        smem[o] = ':';
-        o = lds_put_s(smem, o + 1, rl);
-        smem[o++] = 'I';
-      } else {
-        for (int64_t k = n0; k <= n1; k++) {
-          NODE_AT(k)
-          o = lds_put_s(smem, o, node_count(n, p, rl));
-          smem[o++] = (char)n.op();
-        }
-      }
-      smem[o++] = '|';
-      bool first = true;
-      for (int64_t k = n0; k <= n1; k++) {
-        NODE_AT(k)
-        if (n.code() == 0) continue;
-        if (!first) smem[o++] = ',';
-        o = lds_put_s(smem, o, node_v(n));
-        first = false;
-      }
-      if (fr == 1) smem[o] = '\n';
+    // a reads part longer than the strip slot: the whole part from the overflow area, into the buffer's second half
+    // (the slot copy of waves 1-2 lands in the first)
+    const bool ovf = keep && rest + 1 > ED_SW;
+    if (ovf && fr == 1) {
+      uint64_t at;
+      __builtin_memcpy(&at, A.slot + tf * ED_SW, 8);
+      char *d = smem + o_q + jf * qstride + head + ED_SW + head;
+      const char *src = A.ovf + at;
+      for (int i = 0; i <= rest; i++) d[i] = src[i];
     }
-#endif
     // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
     const int32_t lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
     const int32_t ik = wave_incl_scan(keep && fr == 0 ? 1 : 0);
@@ -1019,8 +1045,8 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     const int32_t tk = __shfl(ik, 63, 64), tb0 = __shfl(i0, 63, 64), tb1 = __shfl(i1, 63, 64);
     const int64_t K0 = A.cnt_base + P.kept;                          // templates kept before the tile
     const int64_t ds0 = digit_sum(K0) - digit_sum(A.cnt_base);       // cnt digits of the emission's records before it
-    const int64_t g0 = (A.d_base ? A.d_base[0] : A.used[0]) + P.b1 + ds0;
-    const int64_t g1 = (A.d_base ? A.d_base[1] : A.used[1]) + P.b2 + ds0;
+    const int64_t g0 = A.used[0] + P.b1 + ds0;
+    const int64_t g1 = A.used[1] + P.b2 + ds0;
     if (tid == 0) {
       const int64_t dst = digit_sum(K0 + tk) - digit_sum(K0);        // ... of the tile's records
       s_g[0] = g0;
@@ -1036,16 +1062,14 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       mt.len[fr] = keep ? lw + nd : 0;
       mt.rel[fr] = rel;
       const int32_t lh = Lp + nd + Lm;
-      const int32_t qb = o_q + jf * qstride + head - lh, sb = lh + rest + 1;
+      const int32_t qb = o_q + jf * qstride + (ovf ? ED_SW + head : 0) + head - lh, sb = lh + rest + 1;
       if (keep) {
-        // mate 1 reads the reverse complement forward: from rc at hap_len - a - S, or from the mirrored LDS window
-        const int32_t lead = !s ? (int32_t)(a & 15)
-                                : h.rc ? (int32_t)((h.hap_len - a - S) & 15) : (int32_t)((-(a + S)) & 15);
+        // mate 1 reads the reverse complement forward: from rc at hap_len - a - S
+        const int32_t lead = !s ? (int32_t)(a & 15) : (int32_t)((h.hap_len - a - S) & 15);
         mt.bb[fr] = o_win + (jf * 2 + s) * win_stride + lead;
         mt.S[fr] = S;
         mt.tb[fr] = CR == 2 ? o_tr + (NF == 2 ? jf * 2 + fr : jf) * TS : o_t;
         mt.tn[fr] = CR ? S + 4 : TL;
-#ifndef EW_CALIB_NOHEAD
         if (fr == 0) {   // the qname head ('@stub:' cnt '|chrom|cpy'), right-aligned before the reads part
           mt.qb = qb;
           mt.sb = sb;
@@ -1055,12 +1079,6 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
           for (int i = nd - 1; i >= 0; i--) { d[Lp + i] = (char)('0' + x % 10u); x /= 10u; }
           for (int i = 0; i < Lm; i++) d[Lp + nd + i] = (char)qh.at(Lp + i);
         }
-#else
-        if (fr == 0) {
-          mt.qb = qb;
-          mt.sb = sb;
-        }
-#endif
       }
       if (CR == 1 && (NF == 2 || fr == 0)) {   // the record's first base, for the corruption pass (S = 0: dropped)
         const uint64_t so = (uint64_t)((fr ? g1 : g0) + rel + sb);
@@ -1155,8 +1173,7 @@ struct CiArgs {
   const int8_t *fo0;
   const Rec *recs;
   const E3 *off;
-  char *arena[2];         // the emission's first byte per file (asynchronous: the arena start, plus d_base)
-  const int64_t *d_base;  // asynchronous emission: the emission's arena offsets from the device (else null)
+  char *arena[2];         // the emission's first byte per file
   const uint2 *crec;      // [m * nf] per record: k_cr_recs' packed offset and S
   int32_t rlen, nf, lh0;  // lh0: qname head bytes without the cnt digits ('@stub:' + '|chrom|cpy')
   CorruptCfg cc;
@@ -1293,7 +1310,7 @@ __global__ void __launch_bounds__(256) k_cr_recs(CiArgs A, uint2 *crec) {
     if (a > A.hap_len) a = A.hap_len;
     const uint32_t S = rc.x && e > a ? (uint32_t)(e - a) : 0u;
     // '@stub:' cnt '|chrom|cpy' reads-part '\n' | bases | '\n+\n' | qualities | '\n'
-    const uint64_t so = (uint64_t)((A.d_base ? A.d_base[f] : 0) + (f ? o.b2 : o.b1) + A.lh0 +
+    const uint64_t so = (uint64_t)((f ? o.b2 : o.b1) + A.lh0 +
                                    ndig_u((uint64_t)(o.kept + 1)) + rc.w + 1);
     crec[t * A.nf + f] = make_uint2((uint32_t)so, (uint32_t)(so >> 32) << 16 | S);
   }
@@ -1706,7 +1723,7 @@ static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf
   if (m <= 0) return MH_OK;
   const int64_t NB = (rlen + CI_BLK - 1) / CI_BLK;
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
-  CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, nullptr, rlen, nf, 0, cc};
+  CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, rlen, nf, 0, cc};
   stage_begin(ctx, "emit_corrupt_rows");
   const size_t lds_c = (size_t)CI_BLK * CB_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
   const int64_t gx = (m + CC_PER_WG - 1) / CC_PER_WG;
@@ -1744,7 +1761,7 @@ static int32_t cr_rows_prepare(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t n
 int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_t m, const int64_t *pos0,
                           const int64_t *pos1, const int8_t *fo0, const Rec *recs, const E3 *off, uint2 *crec,
                           char *o1, char *o2, int32_t nf, int32_t lh0, int32_t rlen, const CorruptCfg &cc,
-                          const int64_t *d_base = nullptr, bool crec_ready = false) {
+                          bool crec_ready = false) {
   if (m <= 0) return MH_OK;
   int ncu = 0;
   HIPCHK(ctx, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
@@ -1763,7 +1780,7 @@ int32_t launch_cr_inplace(mh_ctx *ctx, hipStream_t st, const HapView &hv, int64_
   int64_t grid = std::min<int64_t>((int64_t)ncu * per_cu, (m * nf * NB + thr - 1) / thr);
   if (grid < 1) grid = 1;
   if (pf) grid = (grid + 1) & ~(int64_t)1;   // even: workgroup pairs (file 0, file 1)
-  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, d_base, crec, rlen, nf, lh0, cc};
+  CiArgs A{hv.p_min, hv.hap_len, m, pos0, pos1, fo0, recs, off, {o1, o2}, crec, rlen, nf, lh0, cc};
   stage_begin(ctx, "emit_corrupt");
   if (!crec_ready) {   // (the fused writer wrote the record words itself)
     hipLaunchKernelGGL(k_cr_recs, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A, crec);
@@ -1815,7 +1832,7 @@ __global__ void k_rb_write(HapView h, int64_t n, const int64_t *p, const int64_t
 HapView view_of(const Hap &h) {
   return HapView{(const int64_t *)h.keys.p, (const int64_t *)h.ps.p, (const int64_t *)h.pr.p,
                  (const int64_t *)h.oplen.p, (const uint8_t *)h.op.p, h.n_nodes, (const uint8_t *)h.hap.p,
-                 h.rc_valid ? (const uint8_t *)h.rc.p : nullptr, (const int32_t *)h.bkt.p, (const Node16 *)h.nd.p, h.n_bkt, h.p_min,
+                 (const uint8_t *)h.rc.p, (const int32_t *)h.bkt.p, (const Node16 *)h.nd.p, h.n_bkt, h.p_min,
                  h.hap_len, (const int64_t *)h.nrun_s.p, (const int64_t *)h.nrun_e.p, h.n_runs};
 }
 
@@ -1890,7 +1907,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
   const TplSet &tp = tit->second;
   hipStream_t st = ctx->stream;
-  if (!prepare_only) MH_TRY(sync_async_fill(ctx));   // the arena fill of queued asynchronous units
   if (t_end < 0 || t_end > tp.n) t_end = tp.n;
   if (t_begin > t_end) t_begin = t_end;
   const int64_t m = t_end - t_begin;
@@ -1966,13 +1982,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       return arg_fail(ctx, MH_E_STATE, "more units prepared than emission buffer sets (emit the prepared units first)");
     }
     ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
-    if (es.busy) {
-      gate_open_for(ctx, es.done_gate);
-      HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
-    }
+    if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));
     if (m > ctx->eset_max_m) ctx->eset_max_m = m;
     const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
+    if (direct) {   // the qname reads parts: a slot per template, an overflow area of 8 bytes per template
+      MH_TRY(ensure(ctx, es.strip, (size_t)ED_SW * mm + 64));
+      MH_TRY(ensure(ctx, es.ovf, 8 * (size_t)mm + 4096));
+    }
     MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
     MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
     if (!direct) MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
@@ -1981,12 +1998,14 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     MH_TRY(ensure(ctx, es.stat, 64));
     char *stat = (char *)es.stat.p;        // per set: a deferred readback must not see the next unit's totals
     E3 *tot = (E3 *)stat;                  // [0, 24)
-    int32_t *max_rec = (int32_t *)(stat + 32);
+    int32_t *max_rec = (int32_t *)(stat + 32);   // [32, 48); the overflow area's fill at 48
     HIPCHK(ctx, hipMemsetAsync(stat, 0, 64, st));
     Rec *recs = (Rec *)es.recs.p;
     stage_begin(ctx, "emit_measure");
     hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
-                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec);
+                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec,
+                       Strip{direct ? (char *)es.strip.p : nullptr, (char *)es.ovf.p, (int64_t)es.ovf.cap,
+                             (unsigned long long *)(stat + 48)});
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     stage_begin(ctx, "emit_scan");
@@ -2038,6 +2057,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   es.prepared = false;
   const Rec *recs = (const Rec *)es.recs.p;
   const int32_t hmax = hm4[0], hslot = hm4[3];
+  const bool ovf_full = hm4[1] != 0;   // the strip's overflow area ran out: the LDS-image writer formats everything
 
   // ---- the writer ------------------------------------------------------------------------------------------------
   // arenas: append after what is already there
@@ -2072,8 +2092,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
-  // (hslot: the longest reads part + '\n' of the unit, from the measure pass)
-  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ED_QPAD;
+  // qname buffer per template (emit_tile): head room, the strip slot, and when a reads part is longer than a slot
+  // (hslot: the longest reads part + '\n' of the unit, from the measure pass) a second head room and the whole part
+  const int32_t qstride = head + ED_SW + (hslot > ED_SW ? head + (hslot + 15) / 16 * 16 : 0) + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   QHead qh{};
@@ -2084,7 +2105,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     qh.lp = (int32_t)prefix.size();
     qh.lm = (int32_t)mid.size();
   }
-  if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
+  if (direct && !ovf_full && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
       cnt_base + m < (int64_t)UINT32_MAX) {
     if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
@@ -2094,21 +2115,10 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
       writer_dep = ctx->ev_ready;
     }
     HIPCHK(ctx, hipStreamWaitEvent(ctx->wstream, writer_dep, 0));
-    // the writer gate: this job's writers from the gate_at-th on wait for the next job's sorts (mh_internal.h); with
-    // a batch begun ahead (mh_sample_units_begin: the lookahead pipeline) that batch is the next job and its sort is
-    // already queued, so they wait for gate >= job
-    const bool gate_here = ctx->gate_tail > 0 ? ctx->writers_in_job == std::max(0, ctx->job_units - ctx->gate_tail)
-                                              : ctx->gate_at >= 0 && ctx->writers_in_job == ctx->gate_at;
-    if (ctx->gate && gate_here && ctx->job > 0) {
-      const uint32_t want = ctx->sample_state ? ctx->job : ctx->job + 1;
-      HIPCHK(ctx, hipStreamWaitValue32(ctx->wstream, ctx->gate, want, hipStreamWaitValueGte, 0xffffffffu));
-      if (want > ctx->gate_waited) ctx->gate_waited = want;
-    }
-    ctx->writers_in_job++;
     ctx->stage_stream = ctx->wstream;
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
-            {ctx->used1, ctx->used2}, nullptr, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
-            qstride};
+            {ctx->used1, ctx->used2}, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
+            qstride, (const char *)es.strip.p, (const char *)es.ovf.p};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
     auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
@@ -2119,14 +2129,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     if (ctx->corrupt_on && !cr_rows)   // (tables too large for the row pass's LDS): in place after the writer
       MH_TRY(launch_cr_inplace(ctx, tail, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p,
                                (char *)ctx->out1.p, (char *)ctx->out2.p, write_fastq2 ? 2 : 1,
-                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc, nullptr, true));
+                               (int32_t)(prefix.size() + mid.size()), (int32_t)rlen, cc, true));
     stage_end(ctx);   // "emit"
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipEventRecord(es.done, tail));
-    es.done_gate = ctx->gate_waited;
     HIPCHK(ctx, hipEventRecord(ctx->ev_writer, tail));
-    MH_TRY(mark_used(ctx, h.used, h.used_set, h.used_gate));     // the haplotype and the templates stay live until then
-    MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
+    MH_TRY(mark_used(ctx, h.used, h.used_set));     // the haplotype and the templates stay live until then
+    MH_TRY(mark_used(ctx, tp.used, tp.used_set));
     es.busy = true;
     ctx->writer_pending = true;
   } else {
@@ -2163,308 +2172,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   *out_kept = ht.kept;
   *out_b1 = ht.b1;
   *out_b2 = write_fastq2 ? ht.b2 : 0;
-  return MH_OK;
-}
-
-// ---- asynchronous emission ------------------------------------------------------------------------------------
-// mh_emit_async queues a unit's measure pass, record offsets, writer (and corruption) on the writer stream and
-// returns at once: no host round trip separates sampling, measuring and writing.  Two things the synchronous path
-// reads back before queuing the writer come from elsewhere:
-//   * where the unit lands in the arenas: k_emit_advance takes the device-side fill (d_used) as the unit's base and
-//     adds the unit's totals, in stream order; the writer and the corruption pass read the base from the device;
-//   * how much room to reserve and the writer's per-template qname buffer: read_part_bound, an upper bound on one
-//     read's qname part (the longest window of the haplotype's nodes that a read can span, priced at its CIGAR and
-//     v-list digits), so a unit needs at most m * (head + cnt digits + 2 * bound + 1 + 2 * rlen + 5) bytes per file.
-// Results (kept, bytes, bases) come back through a pinned slot per ticket (mh_emit_result).
-static int ndig_host(int64_t v) {
-  int d = 1;
-  for (; v >= 10; v /= 10) d++;
-  return d;
-}
-
-struct LoadNodeCost {   // CIGAR entry (count <= max(oplen, rlen), op) + v-list entry (value, comma) of node k
-  const Node16 *nd;
-  int64_t rlen;
-  __device__ int64_t operator()(int64_t k) const {
-    const Node16 n = nd[k];
-    const int64_t ol = n.oplen();
-    int64_t c = ndig_u((uint64_t)(ol > rlen ? ol : rlen)) + 1;
-    if (n.code() != 0) c += ndig_s(node_v(n)) + 1;
-    return c;
-  }
-};
-struct StoreIncl {
-  int64_t *pre;
-  __device__ void operator()(int64_t k, int64_t incl, int64_t) const { pre[k] = incl; }
-};
-// the priciest window of nodes whose ps lie in [ps_k, ps_k + rlen - 1] (a read's nodes after its first one), and the
-// priciest single node (its first)
-__global__ void __launch_bounds__(256) k_window_cost(int64_t n, const Node16 *nd, const int64_t *pre, int64_t rlen,
-                                                     unsigned long long *mx) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int64_t lim = nd[k].ps() + rlen - 1;
-  int64_t lo = k, hi = n - 1;
-  while (lo < hi) {   // last node with ps <= lim (ps is non-decreasing)
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (nd[mid].ps() <= lim) lo = mid; else hi = mid - 1;
-  }
-  const int64_t before = k ? pre[k - 1] : 0;
-  atomicMax(mx, (unsigned long long)(pre[lo] - before));
-  atomicMax(mx + 1, (unsigned long long)(pre[k] - before));
-}
-
-int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out) {
-  if (h.rb_rlen == rlen && h.rb_bytes > 0) {
-    *out = h.rb_bytes;
-    return MH_OK;
-  }
-  hipStream_t st = ctx->stream;
-  int64_t nodes = 0;
-  unsigned long long mx[2] = {0, 0};
-  if (h.n_nodes > 0) {
-    MH_TRY(ensure(ctx, ctx->rb_tmp, 8 * (size_t)h.n_nodes + 64));
-    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(h.n_nodes)));
-    MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
-    unsigned long long *dmx = (unsigned long long *)((char *)ctx->d_small.p + 96);
-    int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 112);
-    HIPCHK(ctx, hipMemsetAsync(dmx, 0, 16, st));
-    HIPCHK(ctx, device_scan_sum<int64_t>(st, h.n_nodes, LoadNodeCost{(const Node16 *)h.nd.p, rlen},
-                                         StoreIncl{(int64_t *)ctx->rb_tmp.p}, ctx->scan_partials.p, tot));
-    hipLaunchKernelGGL(k_window_cost, dim3(grid_for(h.n_nodes, 256, INT32_MAX)), dim3(256), 0, st, h.n_nodes,
-                       (const Node16 *)h.nd.p, (const int64_t *)ctx->rb_tmp.p, (int64_t)rlen, dmx);
-    HIPCHK(ctx, hipGetLastError());
-    int64_t *hs = pinned_small(ctx);
-    if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
-    HIPCHK(ctx, hipMemcpyAsync(hs + 16, dmx, 16, hipMemcpyDeviceToHost, st));
-    SYNCCHK(ctx, hipStreamSynchronize(st));
-    mx[0] = (unsigned long long)hs[16];
-    mx[1] = (unsigned long long)hs[17];
-    nodes = (int64_t)(mx[0] + mx[1]);
-  }
-  // '|' strand '|' POS (< 2^40: 13 digits) '|' rlen '|' ... '|' + the special CIGAR ('>' offset ':' rlen 'I')
-  const int64_t b = 8 + 20 + 2 * (int64_t)ndig_host(rlen) + 24 + nodes;
-  if (b > (1 << 20)) return arg_fail(ctx, MH_E_CAPACITY, "qname bound too large");
-  h.rb_rlen = rlen;
-  h.rb_bytes = (int32_t)b;
-  *out = (int32_t)b;
-  return MH_OK;
-}
-
-// the unit's totals (stat[0..2]: the tile scan's kept and bytes without the cnt digits; the cnt digits of cnt = 1..kept
-// added), its base offsets (stat[6..7]: the device fill before it) and the device fill after it
-__global__ void k_emit_advance(int64_t *d_used, int64_t *stat, int32_t write2) {
-  const int64_t ds = digit_sum(stat[0]);
-  stat[1] += ds;
-  stat[2] = write2 ? stat[2] + ds : 0;
-  stat[6] = d_used[0];
-  stat[7] = d_used[1];
-  d_used[0] += stat[1];
-  d_used[1] += stat[2];
-}
-__global__ void k_set_used(int64_t *d_used, int64_t u1, int64_t u2) {
-  d_used[0] = u1;
-  d_used[1] = u2;
-}
-
-int32_t sync_async_fill(mh_ctx *ctx) {
-  if (!ctx->async_pending) return MH_OK;
-  gate_open(ctx);
-  SYNCCHK(ctx, hipStreamSynchronize(ctx->wstream));
-  int64_t u[2] = {0, 0};
-  HIPCHK(ctx, hipMemcpy(u, ctx->d_used.p, 16, hipMemcpyDeviceToHost));
-  ctx->used1 = u[0];
-  ctx->used2 = u[1];
-  ctx->async_pending = false;
-  ctx->res1 = ctx->res2 = 0;
-  return MH_OK;
-}
-
-// mh_output_reset: the arenas empty again; with asynchronous units queued, the device fill restarts from zero in
-// stream order (after their writers)
-int32_t output_reset(mh_ctx *ctx) {
-  ctx->used1 = ctx->used2 = 0;
-  ctx->res1 = ctx->res2 = 0;
-  if (ctx->async_pending) {
-    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, (int64_t)0,
-                       (int64_t)0);
-    HIPCHK(ctx, hipGetLastError());
-  }
-  return MH_OK;
-}
-
-// a ticket = result slot | the slot's generation << 8: a slot handed out again (a ticket nobody read, 256 emissions
-// later) invalidates the old ticket instead of answering it with another unit's results
-int32_t emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out) {
-  const int32_t t = ticket & (mh_ctx::RES_N - 1);
-  if (ticket < 0 || ctx->res_state[t] == 0) return arg_fail(ctx, MH_E_ARG, "unknown emission ticket");
-  if ((uint32_t)ticket >> 8 != ctx->res_gen[t])
-    return arg_fail(ctx, MH_E_STATE, "stale emission ticket (its result slot was reused by a later emission)");
-  gate_open(ctx);
-  if (ctx->res_state[t] == 1) SYNCCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));
-  const int64_t *r = ctx->h_res + 8 * t;
-  out[0] = r[0];
-  out[1] = r[1];
-  out[2] = r[2];
-  out[3] = r[6];
-  out[4] = r[7];
-  return MH_OK;
-}
-
-int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
-                   int32_t write_fastq2, uint64_t unit_key, int32_t *ticket) {
-  *ticket = -1;
-  auto tit = ctx->tsets.find(ctx->cur_tpl);
-  if (tit == ctx->tsets.end() || !tit->second.valid)
-    return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
-  const TplSet &tp = tit->second;
-  for (auto &e : ctx->eset)
-    if (e.prepared) return arg_fail(ctx, MH_E_STATE, "emit the prepared units before asynchronous emission");
-  if (!ctx->h_res) {
-    HIPCHK(ctx, hipHostMalloc((void **)&ctx->h_res, 64 * (size_t)mh_ctx::RES_N, hipHostMallocDefault));
-    for (auto &e : ctx->res_ev) HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  const int32_t t = ctx->res_next;
-  gate_open(ctx);
-  if (ctx->res_state[t] == 1) SYNCCHK(ctx, hipEventSynchronize(ctx->res_ev[t]));   // a ticket nobody read
-  ctx->res_next = (t + 1) % mh_ctx::RES_N;
-  ctx->res_state[t] = 0;
-  ctx->res_gen[t] = (ctx->res_gen[t] + 1) & 0x7fffff;
-  const int32_t tk = (int32_t)(ctx->res_gen[t] << 8) | t;
-  int64_t *res = ctx->h_res + 8 * t;
-  const int64_t m = tp.n, rlen = tp.rlen;
-  std::string prefix = std::string("@") + serial_stub + ":";
-  std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
-  QHead qh{};
-  const bool head_fits = prefix.size() + mid.size() <= sizeof(qh.w);
-  const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
-  const int32_t head = (int32_t)(((prefix.size() + mid.size() + 10 + 16) + 15) / 16 * 16);
-  int32_t rb = 0;
-  bool direct = head_fits && !ctx->emit_lds_only && win_stride <= 16 * 3 * ED_GMAX && m < (int64_t)UINT32_MAX && m > 0;
-  if (direct) MH_TRY(read_part_bound(ctx, h, (int32_t)rlen, &rb));
-  const int32_t hslot_b = 2 * rb + 1;   // both reads' parts and the qname's '\n'
-  const int32_t qstride = head + (hslot_b + 15) / 16 * 16 + 32 + ED_QPAD;
-  const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
-  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
-  if (ctx->corrupt_on && rlen > ctx->corrupt_max_bp)
-    return arg_fail(ctx, MH_E_ARG, "read length exceeds the BQ model's max_bp");
-  if (!direct || lds_d > 64 * 1024) {
-    // the synchronous path (its base is the host fill once the queued units are accounted for)
-    MH_TRY(sync_async_fill(ctx));
-    const int64_t b1 = ctx->used1, b2 = ctx->used2;
-    int64_t k = 0, x1 = 0, x2 = 0;
-    MH_TRY(emit_reads(ctx, h, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, false, &k, &x1, &x2));
-    res[0] = k;
-    res[1] = x1;
-    res[2] = x2;
-    res[6] = b1;
-    res[7] = b2;
-    ctx->res_state[t] = 2;
-    *ticket = tk;
-    return MH_OK;
-  }
-  std::string pm = prefix + mid;
-  std::memcpy(qh.w, pm.data(), pm.size());
-  qh.lp = (int32_t)prefix.size();
-  qh.lm = (int32_t)mid.size();
-
-  // room: an upper bound per file (qname line + bases + '\n+\n' + qualities + '\n')
-  const int64_t per_file = (int64_t)(prefix.size() + mid.size()) + ndig_host(m) + hslot_b + 2 * rlen + 5;
-  const int64_t U = m * per_file;
-  MH_TRY(ensure(ctx, ctx->d_used, 64));
-  if (!ctx->async_pending) {
-    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, ctx->used1,
-                       ctx->used2);
-    HIPCHK(ctx, hipGetLastError());
-    ctx->res1 = ctx->used1;
-    ctx->res2 = ctx->used2;
-    ctx->async_pending = true;
-  }
-  if ((int64_t)ctx->out1.cap < ctx->res1 + U + 64 || (write_fastq2 && (int64_t)ctx->out2.cap < ctx->res2 + U + 64)) {
-    // grow the arenas: everything queued lands first (a rare full synchronisation), then the fill restarts from the
-    // host's exact numbers.  The new size covers the reservations that were queued (a quarter more), so the next job
-    // of the same shape fits without another synchronisation.
-    const int64_t want1 = (ctx->res1 + U + 64) * 5 / 4, want2 = (ctx->res2 + U + 64) * 5 / 4;
-    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
-    MH_TRY(sync_async_fill(ctx));
-    MH_TRY(ensure_keep(ctx, ctx->out1, std::max(want1, ctx->used1 + U + 64), ctx->used1));
-    if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, std::max(want2, ctx->used2 + U + 64), ctx->used2));
-    SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
-    hipLaunchKernelGGL(k_set_used, dim3(1), dim3(1), 0, ctx->wstream, (int64_t *)ctx->d_used.p, ctx->used1,
-                       ctx->used2);
-    HIPCHK(ctx, hipGetLastError());
-    ctx->res1 = ctx->used1;
-    ctx->res2 = ctx->used2;
-    ctx->async_pending = true;
-  }
-  ctx->res1 += U;
-  if (write_fastq2) ctx->res2 += U;
-
-  const int32_t set = ctx->eset_i;
-  ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
-  EmitSet &es = ctx->eset[set];
-  const int64_t ntiles = (m + ED_T - 1) / ED_T;
-  if (m > ctx->eset_max_m) ctx->eset_max_m = m;
-  const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
-  MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
-  MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
-  MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
-  MH_TRY(ensure(ctx, ctx->scan_partials_w, scan_lb_scratch_bytes<E3>(ntiles)));
-  MH_TRY(ensure(ctx, es.stat, 64));
-  if (ctx->corrupt_on) MH_TRY(ensure(ctx, es.crrec, 16 * (size_t)m + 64));
-  char *stat = (char *)es.stat.p;
-  Rec *recs = (Rec *)es.recs.p;
-  const int64_t *pos0 = (const int64_t *)tp.pos0.p, *pos1 = (const int64_t *)tp.pos1.p;
-  const int8_t *fo0 = (const int8_t *)tp.fo0.p;
-  HapView hv = view_of(h);
-  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
-  if (ctx->corrupt_on) cc = corrupt_cfg(ctx, unit_key, 0);
-
-  if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
-  hipStream_t ws = ctx->wstream;
-  HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));   // the unit's templates (main stream) are ready
-  HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
-  ctx->stage_stream = ws;
-  stage_begin(ctx, "emit");
-  HIPCHK(ctx, hipMemsetAsync(stat, 0, 48, ws));
-  stage_begin(ctx, "emit_measure");
-  QFixed q{nullptr, nullptr, (int32_t)prefix.size(), (int32_t)mid.size()};
-  hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, ws, hv, m, pos0, pos1, fo0, rlen,
-                     q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, (int32_t *)(stat + 32));
-  HIPCHK(ctx, hipGetLastError());
-  stage_end(ctx);
-  stage_begin(ctx, "emit_scan");
-  HIPCHK(ctx, device_scan_sum<E3>(ws, ntiles, LoadTile{(const int4 *)es.tsum.p, ntiles}, StoreTile{(E3 *)es.tpre.p},
-                                  ctx->scan_partials_w.p, (E3 *)stat));
-  stage_end(ctx);
-  TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p}, {0, 0},
-          (const int64_t *)ctx->d_used.p, 0, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head, qstride};
-  if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
-  stage_begin(ctx, "emit_write");
-  auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);
-  hipLaunchKernelGGL(kfn, dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
-  HIPCHK(ctx, hipGetLastError());
-  stage_end(ctx);
-  // the unit's totals (cnt digits added), its base (the fill before it) and the fill after it
-  hipLaunchKernelGGL(k_emit_advance, dim3(1), dim3(1), 0, ws, (int64_t *)ctx->d_used.p, (int64_t *)stat, write_fastq2);
-  HIPCHK(ctx, hipGetLastError());
-  if (ctx->corrupt_on && !cr_rows)
-    MH_TRY(launch_cr_inplace(ctx, ws, hv, m, pos0, pos1, fo0, recs, nullptr, (uint2 *)es.crrec.p, (char *)ctx->out1.p,
-                             (char *)ctx->out2.p, write_fastq2 ? 2 : 1, (int32_t)(prefix.size() + mid.size()),
-                             (int32_t)rlen, cc, nullptr, true));
-  stage_end(ctx);   // "emit"
-  ctx->stage_stream = nullptr;
-  HIPCHK(ctx, hipMemcpyAsync(res, stat, 64, hipMemcpyDeviceToHost, ws));
-  HIPCHK(ctx, hipEventRecord(ctx->res_ev[t], ws));
-  ctx->res_state[t] = 1;
-  HIPCHK(ctx, hipEventRecord(es.done, ws));
-  es.done_gate = ctx->gate_waited;
-  HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ws));
-  MH_TRY(mark_used(ctx, h.used, h.used_set, h.used_gate));
-  MH_TRY(mark_used(ctx, tp.used, tp.used_set, tp.used_gate));
-  es.busy = true;
-  ctx->writer_pending = true;
-  *ticket = tk;
   return MH_OK;
 }
 

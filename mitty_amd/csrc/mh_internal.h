@@ -66,14 +66,11 @@ struct Hap {
   bool valid = false;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
-  mutable uint32_t used_gate = 0;      // the gate value that writer needs
   DevBuf hap, rc, keys, ps, pr, op, oplen, nrun_s, nrun_e;   // rc: reverse complement of hap (mate-1 reads)
-  bool rc_valid = false;       // rc built for this haplotype (not in forward-only mode: mh_ctx::hap_fwd)
   DevBuf nd;    // Node16 copy of the node arrays
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
-  int32_t rb_rlen = 0, rb_bytes = 0;   // read_part_bound's cache: the longest qname reads part of one read of rb_rlen
 };
 
 // One work unit's templates (illumina.generate_reads output), device-resident.
@@ -97,7 +94,6 @@ struct TplSet {
   mutable EmitPrep prep;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
-  mutable uint32_t used_gate = 0;      // the gate value that writer needs
   int64_t n = 0;
   int32_t rlen = 0;
   bool valid = false;
@@ -147,13 +143,13 @@ namespace mh {
 // units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
   DevBuf recs, off;            // per template: k_emit_measure's records; offsets (LDS-image writer only)
+  DevBuf strip, ovf;           // per template: the qname reads part (k_emit_measure -> k_emit_tiles), long ones
   DevBuf tsum, tpre;           // per 32-template tile: sums (kept, bytes per file) and their exclusive prefixes
   DevBuf crrec;                // corruption: per record the first base's offset and S (k_cr_recs)
   DevBuf stat;                 // the measure pass's totals (E3 at 0) and maxima (int32[4] at 32)
   int64_t *h_stat = nullptr;   // pinned: stat's readback (64 B), then the qname prefix (+64) and mid (+4160) staged
   hipEvent_t rb = nullptr;     // after that copy
   hipEvent_t done = nullptr;   // the last writer that read this set
-  uint32_t done_gate = 0;      // ... and the gate value it needs
   bool busy = false;
   bool prepared = false;       // holds a prepared unit whose writer is not queued yet
 };
@@ -167,32 +163,12 @@ struct mh_ctx {
   // FASTQ writer stream: mh_emit_reads returns once its writer is queued here; every other entry point first makes
   // the main stream wait for the last queued writer (ev_writer)
   hipStream_t wstream = nullptr;
-  // a batch between mh_sample_units_begin and _end (mh_sample.hip SampleState); writers queued meanwhile wait, with
-  // the gate on, for the begun batch's sort (gate >= job) instead of the next one's (gate >= job + 1)
-  std::shared_ptr<void> sample_state;
   // a batch whose per-unit tail (chase, template lengths, compaction) is queued on stream2 without a host wait
   // (mh_sample_units_async): its template sets are resolved one by one (tpl_resolve) as they are used
   std::shared_ptr<void> tail_state;
   int64_t *h_units = nullptr, *d_units = nullptr;   // mapped host memory: per unit m, status, flag, done
   hipEvent_t ev_ready = nullptr, ev_writer = nullptr;
   bool writer_pending = false;
-  // Writer gate.  The permutation's radix sort cannot run beside a FASTQ writer (its workgroups need a whole CU and
-  // wait until the writers drain), so the writers from a job's `gate_at`-th on wait on the device (hipStreamWaitValue32
-  // on `gate`) until the NEXT job's sampling has sorted (it writes its job number there): the sorts run alone in a short
-  // gap instead of after all the writers.  Any host wait for a writer first opens the gate (gate_open), so a job with
-  // no successor never waits.  Opt-in: MH_WRITER_GATE=k gates from a job's k-th writer (off by default).
-  hipStream_t gstream = nullptr;   // gate writes from the host side (never blocked)
-  hipEvent_t ev_sorted = nullptr;  // the first lane's last sort, for the gate write on the other lane
-  uint32_t *gate = nullptr;        // signal memory
-  uint32_t job = 0;                // sample_units calls so far (the current job's number)
-  uint32_t gate_waited = 0;        // the largest value a queued writer waits for
-  uint32_t gate_written = 0;       // the largest value a queued gate write stores
-  int32_t gate_at = -1;
-  int32_t gate_tail = 0;           // MH_WRITER_GATE_TAIL=D: the gate holds a job's last D writers instead
-  int32_t job_units = 0;           // units of the current job (the writers it will queue)
-  int32_t writers_in_job = 0;
-  static constexpr int N_USORT = 4;   // units of a batch sorted before any is chased (per unit: ts, keys, values, heads)
-  mh::DevBuf usort[N_USORT][4];
   // emission buffer sets in flight: a unit's measure pass refills the set the writer N_ESET units back read, so with
   // fewer sets than a batch's units the host (waiting for each unit's measure totals) is held until the batch's
   // writers are nearly done and the next batch's sampling cannot start beside them
@@ -265,9 +241,6 @@ struct mh_ctx {
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
-  // forward-only haplotypes (MH_HAP_FWD=1, experiment): no reverse-complement copy; the writer reverse-complements
-  // mate-1 windows into LDS itself
-  bool hap_fwd = false;
   // MH_SORT=lsd (the hand-written permutation sort instead of rocprim's, measured slower: DESIGN.md), read once per
   // context (mh_create), so tests switch it per context
   bool sort_lsd = false;
@@ -276,22 +249,10 @@ struct mh_ctx {
   // FASTQ arenas
   mh::DevBuf out1, out2;
   int64_t used1 = 0, used2 = 0;
-  // asynchronous emission (mh_emit_async): measure, offsets, writer and corruption queued on the writer stream; the
-  // arena fill lives on the device (d_used) until a call needs it on the host (sync_async_fill)
-  mh::DevBuf d_used;                     // int64[2]
   // corruption rows (the direct writer's mode): per block 15 qualities | 2-bit codes; one set, the row pass and its
   // writer in stream order on the writer stream
   mh::DevBuf cr_rows, cr_codes;
   mh::DevBuf scan_partials_w;            // look-back scratch of the writer stream's scans
-  mh::DevBuf rb_tmp;                     // read_part_bound's prefix sums
-  bool async_pending = false;            // units queued asynchronously whose fill is not in used1 / used2 yet
-  int64_t res1 = 0, res2 = 0;            // arena bytes reserved by queued asynchronous units (upper bounds)
-  static constexpr int RES_N = 256;      // result slots (tickets) in flight
-  int64_t *h_res = nullptr;              // pinned [RES_N][8]: E3 totals, bases (words 6, 7)
-  hipEvent_t res_ev[RES_N] = {};
-  uint32_t res_gen[RES_N] = {};          // generation of each slot (the ticket's high bits)
-  int8_t res_state[RES_N] = {};          // 0 free, 1 queued (event), 2 filled by the host (synchronous fallback)
-  int32_t res_next = 0;
   int64_t *h_small = nullptr;            // pinned 4 KiB for small readbacks (no staged copy per value)
   uint8_t *h_bam_pin[2] = {nullptr, nullptr};   // mh_bam_write_gpu's two 64 MiB D2H slots (kept: page-locking
                                                 // 128 MiB per BAM file cost ~13 ms)
@@ -335,11 +296,8 @@ void release(DevBuf &b);
 void release_hap(Hap &h);
 int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer
 // a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
-int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set, uint32_t &gate);
-int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, uint32_t gate);
-void gate_open(mh_ctx *ctx);                        // release every writer waiting on the gate
-void gate_open_for(mh_ctx *ctx, uint32_t need);     // ... if a wait is about to depend on a writer needing `need`
-int32_t gate_release(mh_ctx *ctx, hipStream_t st, uint32_t value);   // stream-ordered gate write (sampling)
+int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set);
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set);
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);
@@ -365,10 +323,6 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                      int32_t rng_mode, int64_t *out_n);
-int32_t sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
-                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                           int32_t n_tlen, int32_t rng_mode);
-int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n);
 int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
                            int32_t n_tlen, int32_t rng_mode);
@@ -379,7 +333,6 @@ int32_t tpl_resolve_all(mh_ctx *ctx);
 
 // FASTQ emission of the current template set's [t_begin, t_end) (mh_emit_reads); prepare_only: the measure pass and
 // record offsets only, kept for the next emit_reads of the same unit (mh_emit_prepare)
-int32_t sync_async_fill(mh_ctx *ctx);
 int32_t sync_writers(mh_ctx *ctx);   // the writer stream and the corruption stream drained (host wait)
 int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n, uint8_t *d_out, int64_t cap,
                     int64_t *used, std::vector<int64_t> *boff = nullptr,
@@ -391,12 +344,7 @@ int64_t bgzf_device_bound(int64_t n);
 int gpu_numa_node(int dev);   // the NUMA node of the device's PCI function (sysfs), -1 when unknown
 std::mutex &host_allocs_mu();  // mh_host_alloc's node-bound registrations (address -> bytes)
 std::unordered_map<void *, size_t> &host_allocs();
-int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure   // host used1 / used2 from the device fill after asynchronous emissions
-int32_t read_part_bound(mh_ctx *ctx, Hap &h, int32_t rlen, int32_t *out);
-int32_t output_reset(mh_ctx *ctx);
-int32_t emit_result(mh_ctx *ctx, int32_t ticket, int64_t *out);   // kept, bytes1, bytes2, base1, base2
-int32_t emit_async(mh_ctx *ctx, Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
-                   int32_t write_fastq2, uint64_t unit_key, int32_t *ticket);
+int64_t *pinned_small(mh_ctx *ctx);     // ctx->h_small (allocated on first use); nullptr on failure
 int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                    bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);

@@ -1195,10 +1195,7 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // `out`, file order.  `exact`: materialise the draws and recompute flagged ones on the host (rare path).
 // `lane` 1 runs on the second sampling stream with its own scratch (the units' stages are latency-bound, so two
 // units side by side fill the chip better than one after the other).
-// gate_role (the writer gate, mh_internal.h), right after the permutation's sort: 1 = record ev_sorted (the other
-// lane's last unit writes the gate), 2 = wait for ev_sorted then write the gate, 3 = write the gate.
-// phase: 0 = everything; 1 = the geometric scan and the sort (up to the gate); 2 = the rest.  `ub` (phases 1/2): the
-// unit's own ts, sorted keys, values and heads, so a lane can sort all its units before it chases any of them.
+// phase: 0 = everything; 1 = the geometric scan (and a per-unit sort); 2 = the rest.
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
 // The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (7-bit digits, 256-thread
@@ -1223,8 +1220,7 @@ struct BatchPerm {
 
 int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint32_t *jarr, double p, int32_t rlen,
                     const double *d_cum, int32_t n_tlen, int32_t rng_mode, bool exact, int64_t *d_m,
-                    uint32_t *d_flag, int lane = 0, int gate_role = 0, int phase = 0, mh::DevBuf *ub = nullptr,
-                    const BatchPerm *bp = nullptr) {
+                    uint32_t *d_flag, int lane = 0, int phase = 0, const BatchPerm *bp = nullptr) {
   hipStream_t st = lane == 0 ? ctx->stream : lane == 1 ? ctx->stream2 : ctx->xstream[lane - 2];
   ctx->stage_stream = lane ? st : nullptr;
   struct Restore {
@@ -1236,10 +1232,10 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   void *scan_partials = lane == 0 ? ctx->scan_partials.p : lane == 1 ? ctx->scan_partials2.p : ctx->xscan[lane - 2].p;
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
-  int64_t *ts = bp ? bp->ts + u.j_off : (int64_t *)(ub ? ub[0] : S4[0]).p;
+  int64_t *ts = bp ? bp->ts + u.j_off : (int64_t *)S4[0].p;
   int64_t *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
-  uint32_t *sk = (uint32_t *)(ub ? ub[1] : S4[4]).p, *sv = (uint32_t *)(ub ? ub[2] : S4[5]).p;
-  int32_t *nxt = (int32_t *)(ub ? ub[3] : S4[6]).p;
+  uint32_t *sk = (uint32_t *)S4[4].p, *sv = (uint32_t *)S4[5].p;
+  int32_t *nxt = (int32_t *)S4[6].p;
   const bool permute = rng_mode == MH_RNG_MITTY && n > 1 && !bp;
   uint8_t *keep = (uint8_t *)S4[3].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
@@ -1287,9 +1283,6 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
       hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                          (const uint32_t *)sv, nxt);
-      if (ctx->gate && gate_role == 1) HIPCHK(ctx, hipEventRecord(ctx->ev_sorted, st));
-      if (ctx->gate && gate_role == 2) HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_sorted, 0));
-      if (gate_role >= 2) MH_TRY(gate_release(ctx, st, ctx->job));
       HIPCHK(ctx, hipGetLastError());
       stage_end(ctx);
     }
@@ -1322,8 +1315,8 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
 
 }  // namespace
 
-// A batch's sampling state between its two halves (sample_units_begin / _end): the plan, the batch buffers and the
-// lanes.  The batch buffers are shared by every batch, so one batch is begun at a time.
+// A batch's sampling state between its two halves (sample_head / sample_tail): the plan, the batch buffers and the
+// lanes.  The batch buffers are shared by every batch.
 struct SampleState {
   std::vector<UnitPlan> plan;
   int32_t n_units = 0, rng_mode = 0, rlen = 0, n_tlen = 0, n_lanes = 1;
@@ -1345,7 +1338,7 @@ struct SampleState {
 };
 
 // First half: plan, word streams, shuffle decode, geometric scans and — batch path — the permutation's sort and
-// heads (the writer gate opens there); the per-unit path runs its units whole here.
+// heads; the per-unit path runs its units whole here.
 static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
                            int32_t n_tlen, int32_t rng_mode) {
@@ -1355,9 +1348,6 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   if (n_tlen <= 0 || n_tlen > 8192) return arg_fail(ctx, MH_E_ARG, "cum_tlen must have 1..8192 entries");
   if (rng_mode != MH_RNG_MITTY && rng_mode != MH_RNG_PHILOX) return arg_fail(ctx, MH_E_ARG, "unknown rng_mode");
   MH_TRY(tpl_resolve_all(ctx));   // the previous batch's asynchronous tail reads the batch buffers this one refills
-  ctx->job++;   // a new job: its writers count from 0 for the gate, and it opens the previous job's gate
-  ctx->writers_in_job = 0;
-  ctx->job_units = n_units;
   hipStream_t st = ctx->stream;
 
   // ---- plan ---------------------------------------------------------------------------------------------------
@@ -1390,7 +1380,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     q.j_off = j_total; j_total += q.n + 4;
     n_max = std::max(n_max, q.n);
     TplSet &ts = ctx->tsets[tpl_ids[u]];
-    MH_TRY(wait_unused(ctx, ts.used, ts.used_set, ts.used_gate));   // a queued FASTQ writer may still read the old templates
+    MH_TRY(wait_unused(ctx, ts.used, ts.used_set));   // a queued FASTQ writer may still read the old templates
     MH_TRY(ensure(ctx, ts.fo0, q.n + 16));
     MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
     MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));
@@ -1519,22 +1509,8 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
   }
-  // the writer gate opens after the last unit's sort on each lane (the lane whose last unit is queued last writes it)
-  int32_t last[4] = {-1, -1, -1, -1};
-  for (int32_t u = 0, k = 0; u < n_units; u++)
-    if (plan[u].n > 0) last[k++ % n_lanes] = u;
-  // the batch-wide permutation (one sort per unit when the batch's draws exceed 2^31).  With the writer gate the
-  // batch's one sort releases the previous job's gated writers (they wait until it has run alone on the chip)
+  // the batch-wide permutation (one sort per unit when the batch's draws exceed 2^31)
   const bool batch = rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) && n_units <= PK_UNITS;
-  // Up to four units (two per lane): every unit's sort first, then the rest, each unit with its own sort buffers, so
-  // the gate opens after the sorts alone.  More units: unit after unit.
-  const bool split = ctx->gate && !batch && n_units <= mh_ctx::N_USORT;
-  if (split)
-    for (int32_t u = 0; u < n_units; u++) {
-      const int64_t nu = plan[u].n + 1;
-      MH_TRY(ensure(ctx, ctx->usort[u][0], 8 * (size_t)nu));
-      for (int b = 1; b < 4; b++) MH_TRY(ensure(ctx, ctx->usort[u][b], 4 * (size_t)nu + 16));
-    }
   if (batch) {
     MH_TRY(ensure(ctx, ctx->pb[0], 8 * (size_t)j_total + 64));
     MH_TRY(ensure(ctx, ctx->pb[1], 8 * (size_t)j_total + 64));
@@ -1544,7 +1520,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     for (int32_t u = 0, k = 0; u < n_units; u++) {
       if (plan[u].n == 0) continue;
       MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                         d_flags + u, k++ % n_lanes, 0, 1, nullptr, &bp));
+                         d_flags + u, k++ % n_lanes, 1, &bp));
     }
     if (two_lanes) {
       HIPCHK(ctx, hipEventRecord(ctx->ev_join, ctx->stream2));
@@ -1580,23 +1556,16 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     HIPCHK(ctx, perm_sort(ctx->sort_lsd, ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
-    MH_TRY(gate_release(ctx, st, ctx->job));   // the previous job's gated writers may go
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     S.bp = bp;
-  } else
-  for (int ph = split ? 1 : 0; ph <= (split ? 2 : 0); ph++)
+  } else {
     for (int32_t u = 0, k = 0; u < n_units; u++) {
       if (plan[u].n == 0) continue;
-      const int lane = k++ % n_lanes;
-      int role = 0;
-      if (ctx->gate && u == last[lane] && ph != 2) {   // (at most two lanes with the gate)
-        const int other = n_lanes > 1 ? last[1 - lane] : -1;
-        role = other < 0 ? 3 : other < u ? 2 : 1;
-      }
       MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                         d_flags + u, lane, role, ph, split ? ctx->usort[u] : nullptr));
+                         d_flags + u, k++ % n_lanes));
     }
+  }
   S.plan = std::move(plan);
   S.n_units = n_units;
   S.rng_mode = rng_mode;
@@ -1648,7 +1617,7 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
     for (int32_t u = 0, k = 0; u < n_units; u++) {
       if (plan[u].n == 0) continue;
       MH_TRY(finish_unit(ctx, plan[u], words, jall + plan[u].j_off, p, rlen, d_cum, n_tlen, rng_mode, false, d_m + u,
-                         d_flags + u, k++ % n_lanes, 0, 2, nullptr, &bp));
+                         d_flags + u, k++ % n_lanes, 2, &bp));
     }
   }
   if (two_lanes) {
@@ -1659,7 +1628,6 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
       HIPCHK(ctx, hipStreamWaitEvent(st, ctx->ev_xjoin[l - 2], 0));
     }
   }
-  MH_TRY(gate_release(ctx, st, ctx->job));   // (no permutation: Philox mode, single-template units)
   std::vector<int64_t> hm(n_units), hstat(n_units);
   std::vector<uint32_t> hflag(n_units);
   // d_m, d_status, d_flags are consecutive in s[1] (20 bytes per unit): one readback into pinned memory
@@ -1749,7 +1717,7 @@ static int32_t sample_tail_async(mh_ctx *ctx, const std::shared_ptr<SampleState>
     ctx->stage_stream = nullptr;
     HIPCHK(ctx, hipGetLastError());
     MH_TRY(finish_unit(ctx, q, S.words, S.jall + q.j_off, S.p, S.rlen, S.d_cum, S.n_tlen, S.rng_mode, false,
-                       S.d_m + u, S.d_flags + u, 1, 0, 2, nullptr, &bp));
+                       S.d_m + u, S.d_flags + u, 1, 2, &bp));
     hipLaunchKernelGGL(k_unit_result, dim3(1), dim3(64), 0, l1, (const int64_t *)(S.d_m + u),
                        (const int64_t *)(S.d_status + u), (const uint32_t *)(S.d_flags + u), ctx->d_units + 4 * u);
     HIPCHK(ctx, hipGetLastError());
@@ -1810,7 +1778,6 @@ int32_t tpl_resolve_all(mh_ctx *ctx) {
 int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
                            int32_t n_tlen, int32_t rng_mode) {
-  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
   if (!ctx->h_units) {
     if (hipHostMalloc((void **)&ctx->h_units, 32 * (size_t)PK_UNITS, hipHostMallocMapped | hipHostMallocCoherent) !=
         hipSuccess) {
@@ -1831,30 +1798,9 @@ int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids,
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
                      int32_t rng_mode, int64_t *out_n) {
-  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
   SampleState S;
   MH_TRY(sample_head(ctx, S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
   return sample_tail(ctx, S, out_n);
-}
-
-// The two halves as separate calls, so a caller can queue the next batch's sort ahead of this batch's writers (the
-// lookahead pipeline): begin = sample_head, end = sample_tail.
-int32_t sample_units_begin(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
-                           const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                           int32_t n_tlen, int32_t rng_mode) {
-  if (ctx->sample_state) return arg_fail(ctx, MH_E_STATE, "a begun batch must be ended first (mh_sample_units_end)");
-  auto S = std::make_shared<SampleState>();
-  MH_TRY(sample_head(ctx, *S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
-  ctx->sample_state = S;
-  return MH_OK;
-}
-
-int32_t sample_units_end(mh_ctx *ctx, int32_t n_units, int64_t *out_n) {
-  auto S = std::static_pointer_cast<SampleState>(ctx->sample_state);
-  if (!S) return arg_fail(ctx, MH_E_STATE, "no begun batch (mh_sample_units_begin)");
-  if (n_units != S->n_units) return arg_fail(ctx, MH_E_ARG, "unit count differs from the begun batch's");
-  ctx->sample_state.reset();
-  return sample_tail(ctx, *S, out_n);
 }
 
 }  // namespace mh

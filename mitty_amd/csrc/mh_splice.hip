@@ -527,9 +527,8 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     stage_end(ctx);
   }
   // --- reverse complement (mate-1 reads) --------------------------------------------------------------------
-  h.rc_valid = !ctx->hap_fwd;
-  if (h.rc_valid) MH_TRY(ensure(ctx, h.rc, hap_len + 1024));
-  if (hap_len > 0 && h.rc_valid) {
+  MH_TRY(ensure(ctx, h.rc, hap_len + 1024));
+  if (hap_len > 0) {
     stage_begin(ctx, "splice_hap_rc");
     hipLaunchKernelGGL(k_hap_rc, dim3(grid_for((hap_len + 15) / 16, 256, INT32_MAX)), dim3(256), 0, st,
                        (const uint8_t *)h.hap.p, hap_len, (uint8_t *)h.rc.p);

@@ -291,9 +291,10 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
         sizes[i] = backend.measure(u, plan[i][1], plan[i][2], cpy, write2, useed, rng_range, bases.get(i, 0))
       stats['templates'] += (rng_range[1] - rng_range[0]) if S > 1 else ns[k_of[u]]
 
-  # plain files: every piece's offset from one all-reduce of the measured sizes; rank 0 sizes the files
+  # plain files: every piece's offset from one all-reduce of the measured sizes; rank 0 sizes the files.  Every rank
+  # joins (a flag all ranks share, not `sizes`: a rank that owns no pieces contributes zeros)
   off = [None, None]
-  if sizes:
+  if not all(gz[:len(fnames)]):
     sz = [0] * (2 * len(pieces))
     for i, (_, b1, b2) in sizes.items():
       sz[2 * i], sz[2 * i + 1] = b1, b2

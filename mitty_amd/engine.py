@@ -18,8 +18,6 @@ class Engine:
   SLOTS_PER_REGION = 64
   EMIT_SETS = 4   # units prepared ahead of their writers (of the library's 16 emission buffer sets)
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
-  async_tail = True     # run_units: mh_sample_units_async (False: mh_sample_units, the host waits for the batch)
-  unit0_alone = True    # run_units: unit 0's measure and writer queued before the next units are prepared
 
   def __init__(self, device=0):
     self.ctx = _native.Context(device)
@@ -77,47 +75,29 @@ class Engine:
     self._haps.clear()
 
   def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None, lazy=False):
+                on_unit=None):
     """Sample a batch of work units together, then emit them in order.
 
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
     unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
-    lazy: the pipelined path — every unit's emission is queued on the writer stream (mh_emit_async: no host round trip
-    between sampling, measuring and writing) and a PendingUnits comes back at once; its resolve() gives the list
-    (the units' bytes land in the arenas in unit order, as on the synchronous path).
     """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-    if lazy:
-      for s in set(slots):   # the qname bound for the writer's room, while the splice's results are fresh
-        self.ctx.read_bound(s, rlen)
     # template ids alternate between two ranges per batch, so this batch's sampling never waits for the previous
     # batch's FASTQ writers (still queued on their own stream) to finish reading theirs
     base = self._tpl_base
     self._tpl_base = self.TPL_BATCH - base
     # the units' last sampling stages run on without a host wait; each unit's template set is resolved when its
     # emission first uses it (unit 0's writer does not wait for the whole batch's tail)
-    if self.async_tail:
-      self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
-                                  cum_tlen, RNG_MODES[rng])
-    else:
-      self.ctx.sample_units([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen, cum_tlen,
-                            RNG_MODES[rng])
-    if lazy and on_unit is None:
-      tickets, ns = [], []
-      for k, (ps, ri, cpy, seed) in enumerate(units):
-        self.ctx.use_templates(base + k)
-        ns.append(self.ctx.template_count(base + k))
-        tickets.append(self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
-                                           self._regions[ri][0], cpy, write_fastq2, unit_key=seed))
-      return PendingUnits(self.ctx, ns, tickets)
+    self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
+                                cum_tlen, RNG_MODES[rng])
     out = []
     # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
     # stream): the writers drain while the caller moves on to the next batch.  Unit 0 goes alone: preparing a unit
     # waits for its sampling tail, so at a batch boundary the idle writer stream would otherwise wait for the tails
     # and measure passes of the whole first chunk
     order = list(enumerate(units))
-    k0 = 1 if self.unit0_alone and len(units) > 1 else 0
+    k0 = 1 if len(units) > 1 else 0
     chunks = ([order[:1]] if k0 else []) + [order[c0:c0 + self.EMIT_SETS]
                                             for c0 in range(k0, len(units), self.EMIT_SETS)]
     for chunk in chunks:
@@ -135,102 +115,9 @@ class Engine:
           on_unit(ps, n, kept, b1, b2)
     return out
 
-  def run_batches_lookahead(self, batches, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
-                            rng='mitty', on_batch=None):
-    """Batches of units [(ps, ri, cpy, rng_seed)] emitted in order with the next batch's sampling queued ahead:
-    batch k + 1's first half (word streams, decode, geometric scans, permutation sort: mh_sample_units_begin) is
-    queued before batch k's writers, so with the writer gate on (MH_WRITER_GATE=0) the sort runs alone between two
-    batches' writers and the rest of the sampling runs beside the writers.  on_batch(k) runs before batch k is
-    emitted (e.g. to recycle the arenas).  Returns [(n, kept, b1, b2)] per unit, in order."""
-    B = len(batches)
-    ids = [None] * B
-
-    def begin(k):
-      units = batches[k]
-      self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
-      slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-      base = (k % 3) * self.TPL_BATCH + 3 * self.TPL_BATCH   # three generations in flight (writers, end, begin)
-      ids[k] = [base + i for i in range(len(units))]
-      self.ctx.sample_units_begin(ids[k], slots, [u[3] for u in units], p, rlen, cum_tlen, RNG_MODES[rng])
-
-    out = []
-    if B == 0:
-      return out
-    begin(0)
-    ns = [None] * B
-    ns[0] = self.ctx.sample_units_end(len(batches[0]))
-    if B > 1:
-      begin(1)
-    for k in range(B):
-      if on_batch is not None:
-        on_batch(k)
-      units = batches[k]
-      slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-      for c0 in range(0, len(units), self.EMIT_SETS):
-        chunk = list(range(c0, min(c0 + self.EMIT_SETS, len(units))))
-        for i in chunk:
-          ps, ri, cpy, seed = units[i]
-          self.ctx.use_templates(ids[k][i])
-          self.ctx.emit_prepare(slots[i], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
-                                write_fastq2, unit_key=seed, wait=False)
-        for i in chunk:
-          ps, ri, cpy, seed = units[i]
-          self.ctx.use_templates(ids[k][i])
-          kept, b1, b2 = self.ctx.emit_reads(slots[i], '{}:{}:{}'.format(sample_name, worker_id, ps),
-                                             self._regions[ri][0], cpy, write_fastq2, unit_key=seed)
-          out.append((int(ns[k][i]), kept, b1, b2))
-      if k + 1 < B:
-        ns[k + 1] = self.ctx.sample_units_end(len(batches[k + 1]))
-      if k + 2 < B:
-        begin(k + 2)
-    return out
-
-  def sample_only(self, units, soa_of, p, rlen, cum_tlen, tpl_base, rng='mitty'):
-    """The sampling half of run_units: units [(ps, ri, cpy, rng_seed)] sampled together into template sets
-    tpl_base + k.  Returns the template counts (emit_only emits them later)."""
-    self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
-    slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-    return [int(x) for x in self.ctx.sample_units([tpl_base + k for k in range(len(units))], slots,
-                                                  [u[3] for u in units], p, rlen, cum_tlen, RNG_MODES[rng])]
-
-  def emit_only(self, units, tpl_ids, soa_of, sample_name, worker_id=0, write_fastq2=True):
-    """The emission half: units [(ps, ri, cpy, rng_seed)] whose templates are in sets tpl_ids, measured and written
-    in order (measure passes of up to EMIT_SETS units, then their writers queued back to back).  Returns
-    [(kept, b1, b2)] per unit."""
-    slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
-    out = []
-    for c0 in range(0, len(units), self.EMIT_SETS):
-      chunk = list(range(c0, min(c0 + self.EMIT_SETS, len(units))))
-      for k in chunk:
-        ps, ri, cpy, seed = units[k]
-        self.ctx.use_templates(tpl_ids[k])
-        self.ctx.emit_prepare(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
-                              write_fastq2, unit_key=seed, wait=False)
-      for k in chunk:
-        ps, ri, cpy, seed = units[k]
-        self.ctx.use_templates(tpl_ids[k])
-        out.append(self.ctx.emit_reads(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps),
-                                       self._regions[ri][0], cpy, write_fastq2, unit_key=seed))
-    return out
-
   def run_unit(self, ps, ri, cpy, rng_seed, soa, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,
                rng='mitty'):
     """One work unit: sample templates, emit FASTQ.  Returns (n_templates, kept, bytes1, bytes2)."""
     return self.run_units([(ps, ri, cpy, rng_seed)], lambda a, b: soa, p, rlen, cum_tlen, sample_name, worker_id,
                           write_fastq2, rng)[0]
 
-
-class PendingUnits:
-  """Emissions queued by Engine.run_units(lazy=True): resolve() waits for them and returns [(n, kept, b1, b2)]
-  (and keeps each unit's arena bases in .bases)."""
-
-  def __init__(self, ctx, ns, tickets):
-    self.ctx, self.ns, self.tickets = ctx, ns, tickets
-    self.result, self.bases = None, None
-
-  def resolve(self):
-    if self.result is None:
-      rs = [self.ctx.emit_result(t) for t in self.tickets]
-      self.result = [(n, r[0], r[1], r[2]) for n, r in zip(self.ns, rs)]
-      self.bases = [(r[3], r[4]) for r in rs]
-    return self.result

@@ -149,13 +149,52 @@ def test_bench_batch_plan():
   import bench
   units = [(ps, ps % 5, ps % 2, 100 + ps) for ps in range(40)]
   draws = [10.0, 20.0, 30.0, 40.0, 50.0]
-  for target, mb, ramp in ((100.0, 1, 0), (1e9, 4, 0), (100.0, 4, 2), (25.0, 1, 0)):
-    b, size, total = bench.plan_batches(units, draws, target, mb, ramp)
+  for target, mb in ((100.0, 1), (1e9, 4), (100.0, 4), (25.0, 1)):
+    b, size, total = bench.plan_batches(units, draws, target, mb)
     assert [u for x in b for u in x] == units
     assert total == sum(draws[u[1]] for u in units)
     assert size == min(target, total / mb)
     assert len(b) >= min(mb, len(units))
-    for x in b[:-1]:   # every batch but the last reaches its size (the ramp's first ones a fraction of it)
-      assert sum(draws[u[1]] for u in x) >= size / 2 ** ramp
-  b, _, _ = bench.plan_batches(units, draws, 100.0, 1, 2)
-  assert sum(draws[u[1]] for u in b[0]) < sum(draws[u[1]] for u in b[2])
+    for x in b[:-1]:   # every batch but the last reaches its size
+      assert sum(draws[u[1]] for u in x) >= size
+
+
+def _rank_few_units(rank, world, port, bed, outdir):
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    from mitty_amd.readmodel import get_read_model
+    from tests.dist_host import OracleBackend
+    c = G.load_json('e2e_config.json')['hiseq-X-v2.5-Garvan']
+    mod, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+    st = D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], bed, mod, mdl,
+                                      c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
+                                      seed=c['seed'], backend=OracleBackend(), layout='lpt')
+    assert st['units'] == 4 and st['pieces'] == (0 if rank == 4 else 1), (rank, st)
+  finally:
+    dist.destroy_process_group()
+
+
+def test_lpt_fewer_units_than_ranks(tmp_path):
+  """LPT with fewer units than ranks (one diploid region, two passes: 4 units on 5 gloo ranks): the rank that owns no
+  piece still joins every collective (the size all-reduce, the barriers, the totals), and the files equal the
+  one-process run's (a rank-local condition had decided whether a rank joined the size all-reduce)."""
+  from tests._spawn import spawn_with_port
+  from mitty_amd.readmodel import get_read_model
+  from tests.dist_host import OracleBackend
+  bed = str(tmp_path / 'one.bed')
+  with open(bed, 'w') as fp:
+    fp.write('1\t1000\t40000\n')
+  spawn_with_port(_rank_few_units, lambda port: (5, port, bed, str(tmp_path)), 5)
+  c = G.load_json('e2e_config.json')['hiseq-X-v2.5-Garvan']
+  mod, mdl = get_read_model('hiseq-X-v2.5-Garvan.pkl')
+  one = tmp_path / 'one'
+  one.mkdir()
+  D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], bed, mod, mdl, c['coverage'],
+                               str(one / 'r1.fq'), str(one / 'r2.fq'), seed=c['seed'], backend=OracleBackend())
+  for f in ('r1.fq', 'r2.fq'):
+    a, b = open(tmp_path / f, 'rb').read(), open(one / f, 'rb').read()
+    assert len(a) > 10000
+    G.check_same(a, b)

@@ -353,16 +353,6 @@ def test_unit_vs_oracle_nine_digit_positions(native, emit_mode):
                          emit_mode=emit_mode) > 10000
 
 
-@pytest.mark.parametrize('model', G.MODELS)
-def test_unit_vs_oracle_forward_haplotype(native, monkeypatch, model):
-  """Forward-only haplotypes (MH_HAP_FWD=1: no reverse-complement copy; the writer reverse-complements mate-1
-  windows into LDS, chunks mirrored): byte-identical to the oracle, with an offset region (reads cut by the haplotype
-  end, ragged window starts)."""
-  monkeypatch.setenv('MH_HAP_FWD', '1')
-  assert _unit_vs_oracle(2_000_000, 17, model) > 10000
-  _unit_vs_oracle(1_200_000, 4000000001, model, n_seed=7, rate=8e-3, start0=98_765)
-
-
 @pytest.mark.parametrize('sort', ['rocprim', 'lsd'])
 def test_batched_units_vs_oracle(native, monkeypatch, sort):
   """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
@@ -423,7 +413,10 @@ def test_lsd_sort_repeated_batches(native, monkeypatch):
       eng.load_region(0, ('2', 0, L), seq)
       runs = []
       for k, b in enumerate(batches + [batches[0]]):
-        ns = eng.sample_only(b, lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 100 * k)
+        eng.haplotypes([(ri, cpy) for _, ri, cpy, _ in b])
+        slots = [eng.haplotype(ri, cpy, copies[cpy])[0] for _, ri, cpy, _ in b]
+        ns = eng.ctx.sample_units([100 * k + i for i in range(len(b))], slots, [u[3] for u in b], p, 150,
+                                  mdl['cum_tlen'])
         runs.append([eng.ctx.templates_export(100 * k + i) for i in range(len(b))])
         assert min(ns) > 1000
       got[sort] = runs
@@ -853,10 +846,8 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
   vdf = vcfio.load_variants_soa(G.path('data/syn.vcf'), 'S1', G.path('data/syn.bed'))
   seqs = mfasta.read_fasta(G.path('data/syn.fa'))
   outs = []
-  # (the direct writer with rc or forward-only haplotypes — mirrored mate-1 windows — and the LDS-image writer + the
-  # in-place pass, mh_set_emit_mode(1))
-  for fwd, lds in ((0, False), (1, False), (0, True)):
-    monkeypatch.setenv('MH_HAP_FWD', str(fwd))
+  # (the direct writer and the LDS-image writer + the in-place pass, mh_set_emit_mode(1))
+  for lds in (False, True):
     eng = Engine(0)
     try:
       eng.ctx.set_emit_mode(1 if lds else 0)
@@ -876,9 +867,8 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
     G.check_same(d2, l2, 'fastq2 (variant {})'.format(k))
 
 
-@pytest.mark.parametrize('tables,write2,fwd', [('lds', True, 0), ('global', True, 0), ('lds', False, 0),
-                                               ('lds', True, 1)])
-def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2, fwd):
+@pytest.mark.parametrize('tables,write2', [('lds', True), ('global', True), ('lds', False)])
+def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2):
   """Philox-mode corruption (the writer's len(seq) layout + k_cr_inplace) byte for byte against the numpy
   restatement of the draw scheme with full 53-bit uniforms (tests/philox_ref.py) applied to the perfect reads of the
   same sampling.  No N in the genome, so every template is kept and cnt - 1 is the template index; the bucket table
@@ -888,8 +878,6 @@ def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, wri
   from tests import philox_ref
   if tables == 'global':
     monkeypatch.setenv('MH_CR_GLOBAL', '1')
-  if fwd:   # forward-only haplotypes: the corruption rows' substitutions land in the mirrored mate-1 windows
-    monkeypatch.setenv('MH_HAP_FWD', '1')
   mdl = G.model('hiseq-X-v2.5-Garvan')
   p, _ = _native.read_model_params(150, 30.0)
   seq = synth.contig(400_000, 5, n_gaps=False)
@@ -920,48 +908,6 @@ def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, wri
     assert lc[3::4][:len(ts)] == want_q
     n_sub += sum(x != y for x, y in zip(la[1::4], want_s))
   assert n_sub > 100
-
-
-@pytest.mark.parametrize('corrupt,write2', [(False, True), (True, True), (False, False)])
-def test_async_emission_matches_sync(native, corrupt, write2):
-  """The pipelined path (Engine.run_units(lazy=True): mh_emit_async — measure, offsets, writer and corruption on the
-  writer stream, arena bases from the device) writes the synchronous path's bytes, over two consecutive jobs of three
-  units (two contigs with N runs, both copies), with the arena reset between them as the bench does, and reports the
-  same counts; a synchronous job afterwards appends where the asynchronous fill ended."""
-  from mitty_amd import _native, synth
-  from mitty_amd.engine import Engine
-  mdl = G.model('hiseq-X-v2.5-Garvan')
-  p, _ = _native.read_model_params(150, 30.0)
-  seqs = [synth.contig(1_500_000, 41), synth.contig(900_000, 42)]
-  copies = [synth.copies_soa(synth.variants(sq, 43 + i)) for i, sq in enumerate(seqs)]
-  units = [(0, 0, 0, 501), (1, 0, 1, 502), (2, 1, 0, 503)]
-  outs = []
-  for lazy in (False, True):
-    eng = Engine(0)
-    try:
-      if corrupt:
-        eng.ctx.set_corruption(True, mdl['cum_bq_mat'], 10 ** (-np.arange(100) / 10), 11)
-      for ri, sq in enumerate(seqs):
-        eng.load_region(ri, (str(ri + 1), 0, len(sq)), sq)
-      got = []
-      for job in range(2):
-        eng.drop_haplotypes()
-        eng.ctx.reset_output()
-        r = eng.run_units(units, lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'S', 0, write2, lazy=lazy)
-        r = r.resolve() if lazy else r
-        got.append((r, eng.ctx.fetch_output()))
-      # a synchronous job after the asynchronous ones appends at the device fill
-      r3 = eng.run_units(units[:1], lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'S', 0, write2)
-      got.append((r3, eng.ctx.fetch_output()))
-      outs.append(got)
-    finally:
-      eng.close()
-  for (rs, (a1, a2)), (ra, (b1, b2)) in zip(outs[0], outs[1]):
-    assert rs == ra
-    assert sum(x[1] for x in rs) > 10000
-    G.check_same(a1, b1, 'fastq1')
-    G.check_same(a2, b2, 'fastq2')
-  assert outs[0][0][1][0] == outs[0][1][1][0]   # the two jobs write the same bytes after the reset
 
 
 # ---- multi-GPU slices (SURVEY.md §8(e)) ---------------------------------------------------------------------------
@@ -1486,48 +1432,6 @@ def test_philox_sampling_properties(native):
     eng.close()
 
 
-@pytest.mark.parametrize('knob,value', [('MH_WRITER_GATE', '2'), ('MH_WRITER_GATE_TAIL', '1'),
-                                        ('MH_WRITER_GATE_TAIL', '3')])
-def test_writer_gate_pipelined_jobs(native, monkeypatch, knob, value):
-  """The opt-in writer gate (MH_WRITER_GATE=2: a job's writers from the third on wait on the device until the next
-  job has sorted; each batch's units sorted before any is chased; MH_WRITER_GATE_TAIL=D: a job's last D writers wait):
-  three 4-unit jobs queued back to back, the arenas read only at the end, equal three times the oracle's job
-  (reference unit order, qname serials 0..3)."""
-  monkeypatch.setenv(knob, value)
-  from mitty_amd import _native, synth
-  from mitty_amd.engine import Engine
-  from oracle import oracle as O
-  mdl = G.model('hiseq-X-v2.5-Garvan')
-  rlen = int(mdl['mean_rlen'])
-  p, passes = _native.read_model_params(rlen, 30.0)
-  length = 1_500_000
-  seq = synth.contig(length, 3)
-  copies = synth.copies_soa(synth.variants(seq, 4))
-  units = _native.work_units(7, [2], passes)
-  assert len(units) == 4
-  want1, want2 = b'', b''
-  for ps, (ri, cpy, s) in enumerate(units):
-    _, o1, o2 = O.generate_unit_soa(seq, 0, copies[cpy], p, rlen, mdl['cum_tlen'], s, 'SYN:0:{}'.format(ps), '7', cpy)
-    want1 += o1
-    want2 += o2
-  eng = Engine(0)
-  try:
-    eng.load_region(0, ('7', 0, length), seq)
-    for cpy in range(2):
-      eng.upload_variants(0, cpy, copies[cpy])
-    job = [(ps, 0, cpy, s) for ps, (ri, cpy, s) in enumerate(units)]
-    for rnd in range(2):   # the first round grows every buffer (growth opens the gate); the second is checked
-      eng.ctx.reset_output()
-      for _ in range(3):
-        eng.drop_haplotypes()
-        eng.run_units(job, lambda r, c: copies[c], p, rlen, mdl['cum_tlen'], 'SYN')
-    d1, d2 = eng.ctx.fetch_output()
-  finally:
-    eng.close()
-  G.check_same(d1, want1 * 3, 'file 1 differs')
-  G.check_same(d2, want2 * 3, 'file 2 differs')
-
-
 # ---- device BGZF (mh_deflate.hip; SURVEY.md §8(f) rank 4) ----------------------------------------------------------
 def _bgzf_members(z):
   """The BGZF members of z: (BSIZE, ISIZE) each, checking the gzip header and the BC extra field."""
@@ -1605,46 +1509,6 @@ def test_device_bgzf_arena_ranges_equal_whole_arena(native):
       eng.ctx.output_bgzf_range_pinned(part, u1 - 10, 20, 0)   # past the arena
   finally:
     eng.close()
-
-
-@pytest.mark.parametrize('gate', [None, '0'])
-def test_lookahead_batches_match_run_units(native, monkeypatch, gate):
-  """The lookahead pipeline (batch k+1's sampling up to its sort queued before batch k's writers, the writers gated on
-  that sort: Engine.run_batches_lookahead over mh_sample_units_begin / _end) writes the same FASTQ, byte for byte,
-  as batch after batch through run_units — three regions, 12 units in batches of 4, 5 and 3."""
-  from mitty_amd import _native, synth
-  from mitty_amd.engine import Engine
-  mdl = G.model('hiseq-X-v2.5-Garvan')
-  p, passes = _native.read_model_params(mdl['mean_rlen'], 30.0)
-  lens = [1_500_000, 800_000, 2_000_000]
-  seqs = [synth.contig(L, 40 + i) for i, L in enumerate(lens)]
-  copies = [synth.copies_soa(synth.variants(s, 50 + i), 0, len(s)) for i, s in enumerate(seqs)]
-  units = [(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(_native.work_units(9, [2] * len(lens), passes))]
-  batches = [units[:4], units[4:9], units[9:]]
-  soa_of = lambda r, c: copies[r][c]
-
-  def run(lookahead):
-    if lookahead and gate is not None:
-      monkeypatch.setenv('MH_WRITER_GATE', gate)
-    else:
-      monkeypatch.delenv('MH_WRITER_GATE', raising=False)
-    eng = Engine(0)
-    try:
-      for ri, s in enumerate(seqs):
-        eng.load_region(ri, (str(ri + 1), 0, len(s)), s)
-      eng.ctx.reset_output()
-      if lookahead:
-        res = eng.run_batches_lookahead(batches, soa_of, p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')
-      else:
-        res = [r for b in batches for r in eng.run_units(b, soa_of, p, mdl['mean_rlen'], mdl['cum_tlen'], 'SYN')]
-      return res, eng.ctx.fetch_output()
-    finally:
-      eng.close()
-  r0, (a1, a2) = run(False)
-  r1, (b1, b2) = run(True)
-  assert r0 == r1
-  G.check_same(b1, a1, 'file 1 differs')
-  G.check_same(b2, a2, 'file 2 differs')
 
 
 def test_scan_timeout_is_reported(ctx, native):
