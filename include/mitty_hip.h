@@ -236,6 +236,14 @@ int32_t mh_bam_sort(mh_ctx *ctx);
 int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes);
 int32_t mh_bam_reset(mh_ctx *ctx);
+/* Bounded HBM for the record store (the reference's `samtools sort -m 2G` spills to temporary files,
+ * god_aligner.py:100-116): once the records held in HBM would pass `bytes` (0 = no limit, the default; an allocation
+ * that fails spills too), they move to host memory in input order.  Keys, offsets and BAI info of every record stay
+ * in HBM, so the coordinate sort is still one device sort; mh_bam_write / _gpu assemble the sorted stream on the
+ * host window by window (the GPU writer deflates each window on the device).  The file is byte-identical to the
+ * unbounded store's.  mh_bam_spilled: bytes and host blocks spilled so far. */
+int32_t mh_bam_set_capacity(mh_ctx *ctx, int64_t bytes);
+int32_t mh_bam_spilled(mh_ctx *ctx, int64_t *bytes, int64_t *blocks);
 /* mh_bam_write_gpu: mh_bam_write with the record blocks deflated on the device (mh_deflate.hip: dynamic-Huffman BGZF
  *   blocks of the sorted store in HBM, 0xff00 input bytes each, the header's block deflated on the host at level 6):
  *   only the compressed bytes cross PCIe.  Replaces the same pysam.sort / pysam.index pair (god_aligner.py:117-131);

@@ -24,7 +24,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
+           'mh_bam_records', 'mh_bam_set_capacity', 'mh_bam_spilled', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait', 'mh_output_fetch_async',
            'mh_output_fetch_wait',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
@@ -108,6 +108,8 @@ def lib():
   _sig(L, 'mh_bam_add_fastq', [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_bam_add_output', [c_vp, c_i64, P_i64])
   _sig(L, 'mh_bam_records', [c_vp, P_i64, P_i64])
+  _sig(L, 'mh_bam_set_capacity', [c_vp, c_i64])
+  _sig(L, 'mh_bam_spilled', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
   _sig(L, 'mh_bam_write_gpu', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, P_i64, P_i64, P_i64])
@@ -738,6 +740,16 @@ class Context:
     t = c_i64()
     self._chk(self._L.mh_bam_add_output(self._h, int(max_templates), ctypes.byref(t)))
     return t.value
+
+  def bam_set_capacity(self, nbytes):
+    """HBM budget of the BAM record store (0: no limit); records past it spill to host memory."""
+    self._chk(self._L.mh_bam_set_capacity(self._h, int(nbytes)))
+
+  def bam_spilled(self):
+    """(bytes, host blocks) of the record store spilled to host memory."""
+    b, k = c_i64(), c_i64()
+    self._chk(self._L.mh_bam_spilled(self._h, ctypes.byref(b), ctypes.byref(k)))
+    return b.value, k.value
 
   def bam_records(self):
     n, b = c_i64(), c_i64()

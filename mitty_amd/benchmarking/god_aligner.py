@@ -82,12 +82,16 @@ def header_text(hdr, sorted_by='coordinate'):
 
 
 def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max_templates=None,
-                           sample_name='Seven', device=0, level=6, chunk_bytes=1 << 30, gpu_bgzf=False):
+                           sample_name='Seven', device=0, level=6, chunk_bytes=1 << 30, gpu_bgzf=False,
+                           hbm_capacity=0):
   """god_aligner.process_multi_threaded (:44-131): `bam_fname` (coordinate-sorted BAM) + `bam_fname.bai`.
 
   As in the reference, max_templates stops after template index max_templates, i.e. max_templates + 1 templates.
   `threads` sizes the BGZF deflate pool; gpu_bgzf: the record blocks deflated on the device instead
-  (mh_bam_write_gpu: the same BAM stream, only the compressed bytes leave the GPU).
+  (mh_bam_write_gpu: the same BAM stream, only the compressed bytes leave the GPU).  hbm_capacity: record bytes held
+  in HBM before they spill to host memory (0: no limit) — the reference sorts with `samtools sort -m 2G`, an external
+  merge sort in bounded memory (god_aligner.py:100-116); here only the records' bytes leave HBM, their keys stay and
+  are sorted on the device, and the sorted stream is assembled on the host (mh_bam_set_capacity).
   """
   rg_id = base64.b64encode(' '.join(sys.argv).encode('ascii'))
   hdr = construct_header(fasta + '.ann', rg_id=rg_id, sample=sample_name)
@@ -95,6 +99,7 @@ def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max
   ctx = _native.Context(device)
   try:
     ctx.bam_set_refs([s['SN'] for s in hdr['SQ']], [s['LN'] for s in hdr['SQ']])
+    ctx.bam_set_capacity(hbm_capacity)
     limit = None if max_templates is None else max_templates + 1
     n_t = stream_templates(fastq1, fastq2, lambda b1, b2, want, done: ctx.bam_add_fastq(b1, b2, want),
                            chunk_bytes, limit)
@@ -103,7 +108,9 @@ def process_multi_threaded(fasta, bam_fname, fastq1, fastq2=None, threads=1, max
     else:
       n_rec, n_bytes = ctx.bam_write(bam_fname, header_text(hdr), level=level, threads=max(threads, 1),
                                      bai_path=bam_fname + '.bai')
+    spilled = ctx.bam_spilled()
   finally:
     ctx.close()
   logger.debug('Processed {} templates ({} records) in {:0.2f}s'.format(n_t, n_rec, time.time() - t0))
-  return {'templates': n_t, 'records': n_rec, 'bam_bytes_uncompressed': n_bytes, 'seconds': time.time() - t0}
+  return {'templates': n_t, 'records': n_rec, 'bam_bytes_uncompressed': n_bytes, 'seconds': time.time() - t0,
+          'spilled_bytes': spilled[0], 'spill_blocks': spilled[1]}

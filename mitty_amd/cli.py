@@ -141,14 +141,17 @@ def read_corruption(modelfile, fastq1_in, fastq1_out, seed, fastq2_in, fastq2_ou
 @click.option('--threads', default=2)
 @click.option('--device', default=0, help='HIP device ordinal')
 @click.option('--gpu-bgzf', is_flag=True, help='Deflate the BAM record blocks on the GPU (additive option)')
-def god_aligner(fasta, bam, sample_name, fastq1, fastq2, max_templates, threads, device, gpu_bgzf):
+@click.option('--hbm-gb', type=float, default=0.0,
+              help='BAM records held in HBM before they spill to host memory, GB (0: no limit; additive option, the '
+                   'counterpart of the reference\'s samtools sort -m)')
+def god_aligner(fasta, bam, sample_name, fastq1, fastq2, max_templates, threads, device, gpu_bgzf, hbm_gb):
   """Given a FASTA.ann file and FASTQ made of simulated reads,
      construct a perfectly aligned BAM from them (reference cli.py:183-204).
 
      Note: The program uses the fasta.ann file to construct the BAM header"""
   from mitty_amd.benchmarking import god_aligner as god
   god.process_multi_threaded(fasta, bam, fastq1, fastq2, threads, max_templates, sample_name, device=device,
-                             gpu_bgzf=gpu_bgzf)
+                             gpu_bgzf=gpu_bgzf, hbm_capacity=int(hbm_gb * 1e9))
 
 
 def main():

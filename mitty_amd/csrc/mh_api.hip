@@ -1342,6 +1342,13 @@ int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes) {
   return MH_OK;
 }
 
+int32_t mh_bam_spilled(mh_ctx *ctx, int64_t *bytes, int64_t *blocks) {
+  if (!ctx) return MH_E_ARG;
+  if (bytes) *bytes = ctx->bam.spilled;
+  if (blocks) *blocks = (int64_t)ctx->bam.spill.size();
+  return MH_OK;
+}
+
 int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len, int32_t level,
                      int32_t threads, const char *bai_path, int64_t *out_records, int64_t *out_bytes) {
   CTX_GUARD(ctx);
@@ -1367,6 +1374,96 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
   if (out_bytes) *out_bytes = B.bytes;
   return MH_OK;
 }
+
+}  // extern "C"
+
+// A spilled store's sorted record stream deflated on the device window by window: the host assembles window i + 1
+// (bam_assemble, a thread of its own) while window i goes H2D and through bgzf_device into ctx->gz_out.  Windows
+// are whole numbers of BGZF blocks, so the blocks — and the file — are the ones one deflate of the whole stream
+// makes.  Window size: the store's capacity (bounded HBM) rounded down to blocks, at most 8192 blocks (535 MB).
+static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t *nz, std::vector<int64_t> *boff,
+                                   const std::function<void(int64_t, int64_t)> &on_piece) {
+  BamStore &B = ctx->bam;
+  MH_TRY(bam_spill(ctx));   // (the records still in HBM: every record is then on the host)
+  BamHostOrder o;
+  MH_TRY(bam_host_order(ctx, o));
+  const int64_t cap_blocks = B.cap > 0 ? B.cap / BGZF_BLOCK : 8192;
+  const int64_t W = std::max<int64_t>(1, std::min<int64_t>(8192, cap_blocks)) * BGZF_BLOCK;
+  const int64_t n_win = (B.bytes + W - 1) / W;
+  uint8_t *pin[2] = {nullptr, nullptr};
+  struct PinGuard {
+    uint8_t **p;
+    ~PinGuard() {
+      for (int s = 0; s < 2; s++)
+        if (p[s]) (void)hipHostFree(p[s]);
+    }
+  } pguard{pin};
+  for (int s = 0; s < 2; s++) HIPCHK(ctx, hipHostMalloc((void **)&pin[s], (size_t)W, hipHostMallocDefault));
+  MH_TRY(ensure(ctx, B.in1, (size_t)W + 64));
+  MH_TRY(ensure(ctx, B.in2, (size_t)W + 64));
+  uint8_t *dwin[2] = {(uint8_t *)B.in1.p, (uint8_t *)B.in2.p};
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t ready = 0;            // windows assembled
+  int64_t freed = 2;            // windows whose staging slot may be refilled (slot of window i: i & 1)
+  bool stop = false;
+  std::thread asm_th([&]() {
+    for (int64_t i = 0; i < n_win; i++) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || i < freed; });
+        if (stop) return;
+      }
+      const int64_t w0 = i * W, w1 = std::min(B.bytes, w0 + W);
+      bam_assemble(B, o, w0, w1, pin[i & 1], 16);
+      std::lock_guard<std::mutex> lk(mu);
+      ready = i + 1;
+      cv.notify_all();
+    }
+  });
+  struct Join {
+    std::thread *t;
+    std::mutex *m;
+    std::condition_variable *c;
+    bool *stop;
+    ~Join() {
+      {
+        std::lock_guard<std::mutex> lk(*m);
+        *stop = true;
+        c->notify_all();
+      }
+      t->join();
+    }
+  } join{&asm_th, &mu, &cv, &stop};
+  boff->assign(1, 0);
+  int64_t zpos = 0;
+  std::vector<int64_t> bw;
+  for (int64_t i = 0; i < n_win; i++) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return ready > i; });
+    }
+    const int s = (int)(i & 1);
+    const int64_t len = std::min(B.bytes, (i + 1) * W) - i * W;
+    HIPCHK(ctx, hipMemcpyAsync(dwin[s], pin[s], (size_t)len, hipMemcpyHostToDevice, ctx->stream));
+    const std::function<void(int64_t, int64_t)> piece = [&](int64_t off, int64_t bytes) { on_piece(zpos + off, bytes); };
+    int64_t used = 0;
+    MH_TRY(bgzf_device(ctx, ctx->stream, dwin[s], len, (uint8_t *)ctx->gz_out.p + zpos,
+                       (int64_t)ctx->gz_out.cap - zpos, &used, &bw, &piece));   // (returns with the stream drained)
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      freed = i + 3;   // slot s (its H2D is done) takes window i + 2
+      cv.notify_all();
+    }
+    boff->pop_back();
+    for (int64_t x : bw) boff->push_back(zpos + x);
+    zpos += used;
+  }
+  *nz = zpos;
+  return MH_OK;
+}
+
+extern "C" {
 
 int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
                          const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes) {
@@ -1487,8 +1584,10 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     if (!ev) werr = (int)hipErrorUnknown;
     cv.notify_one();
   };
-  const int32_t rc = bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes, (uint8_t *)ctx->gz_out.p,
-                                 (int64_t)ctx->gz_out.cap, &nz, &boff, &on_piece);
+  const int32_t rc = B.spilled > 0 ? bam_deflate_spilled(ctx, &nz, &boff, on_piece)
+                                    : bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes,
+                                                  (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &nz, &boff,
+                                                  &on_piece);
   {
     std::lock_guard<std::mutex> lk(mu);
     fin = true;
@@ -1535,8 +1634,16 @@ int32_t mh_bam_sort(mh_ctx *ctx) {
   return bam_sort(ctx);
 }
 
+int32_t mh_bam_set_capacity(mh_ctx *ctx, int64_t bytes) {
+  if (!ctx) return MH_E_ARG;
+  if (bytes < 0) return arg_fail(ctx, MH_E_ARG, "capacity must be >= 0");
+  ctx->bam.cap = bytes;
+  return MH_OK;
+}
+
 int32_t mh_bam_reset(mh_ctx *ctx) {
   if (!ctx) return MH_E_ARG;
+  bam_free_spill(ctx->bam);
   ctx->bam.n_rec = ctx->bam.bytes = 0;
   ctx->bam.n_files = 0;
   ctx->bam.sorted = false;

@@ -19,6 +19,9 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
 
 #include "mh_bgzf.h"
 #include "mh_internal.h"
@@ -512,6 +515,18 @@ __global__ void __launch_bounds__(256) k_bam_gather(const uint8_t *src, const in
   if (gl == 0) sinfo[k] = info[r];
 }
 
+// a spilled store: only the BAI info is gathered in sorted order on the device (the bytes are assembled on the host)
+__global__ void k_bam_sinfo(const uint32_t *val, int64_t n, const RInfo *info, RInfo *sinfo, int32_t *bad) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t r = val[k];
+  if (r >= (uint64_t)n) {
+    atomicOr(bad, 2);
+    return;
+  }
+  sinfo[k] = info[r];
+}
+
 }  // namespace
 
 // the record kernels' bounds flag (1: k_bam_write place / bytes, 2: a sort value outside [0, n), 4: k_bam_gather bytes)
@@ -551,6 +566,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
   B.n_files = 0;
   B.sorted = false;
   B.direct = false;
+  bam_free_spill(B);
   B.refs_set = true;
   return MH_OK;
 }
@@ -634,7 +650,7 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
   int64_t add_bytes = 0;
   HIPCHK(ctx, hipMemcpyAsync(&add_bytes, tot, 8, hipMemcpyDeviceToHost, st));
   SYNCCHK(ctx, hipStreamSynchronize(st));
-  if (sorted_direct && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX) {
+  if (sorted_direct && B.n_rec == 0 && n_rec < (int64_t)UINT32_MAX && (B.cap <= 0 || add_bytes <= B.cap)) {
     // the whole input is here (the context's own arenas) and the store is empty: sort first, then every record is
     // written once, straight to its coordinate-sorted place (no input-order copy, no gather)
     MH_TRY(ensure(ctx, B.key, sizeof(uint64_t) * n_rec));
@@ -656,14 +672,21 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
     *templates = T;
     return MH_OK;
   }
-  MH_TRY(ensure_keep(ctx, B.recs, B.bytes + add_bytes + 64, B.bytes));
+  // bounded HBM: the resident records go to the host first when these would pass the capacity (or do not fit)
+  if (B.cap > 0 && B.bytes > B.spilled && B.bytes - B.spilled + add_bytes > B.cap) MH_TRY(bam_spill(ctx));
+  if (ensure_keep(ctx, B.recs, B.bytes - B.spilled + add_bytes + 64, B.bytes - B.spilled) != MH_OK) {
+    if (B.bytes == B.spilled) return MH_E_OOM;   // (nothing to spill: the error stands)
+    ctx->err.clear();
+    MH_TRY(bam_spill(ctx));
+    MH_TRY(ensure_keep(ctx, B.recs, add_bytes + 64, 0));
+  }
   MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n_rec), sizeof(uint64_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n_rec), sizeof(uint32_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n_rec), sizeof(RInfo) * B.n_rec));
   stage_begin(ctx, "bam_write");
   hipLaunchKernelGGL(k_bam_write<BW_G>, dim3(grid_for(n_rec * BW_G, 256, INT32_MAX)), dim3(256), 0, st, a,
                      (const BamTpl *)B.tpl.p, n_rec, nf, (const uint32_t *)nullptr, (const int64_t *)roff,
-                     (uint8_t *)B.recs.p,
+                     (uint8_t *)B.recs.p - B.spilled,   // (offsets are the store's; recs holds [spilled, bytes))
                      (uint64_t *)B.key.p + B.n_rec, (uint32_t *)B.val.p + B.n_rec, (RInfo *)B.info.p + B.n_rec,
                      B.n_rec, B.bytes + add_bytes, bad);
   HIPCHK(ctx, hipGetLastError());
@@ -710,10 +733,27 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
   HIPCHK(ctx, device_scan<int64_t>(st, n + 1, LoadSortedSize{(const uint32_t *)B.val2.p, (const int64_t *)B.roff.p, n},
                                    StoreOff64{(int64_t *)B.soff.p, 0}, OpSum{}, (int64_t)0,
                                    (int64_t *)ctx->scan_partials.p, (int64_t *)ctx->d_small.p));
-  MH_TRY(ensure(ctx, B.srecs, B.bytes + 64));
   MH_TRY(ensure(ctx, B.sinfo, sizeof(RInfo) * n));
   int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 68);
   HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  if (B.spilled > 0) {   // spilled records: the sorted bytes are assembled on the host when written
+    hipLaunchKernelGGL(k_bam_sinfo, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint32_t *)B.val2.p,
+                       n, (const RInfo *)B.info.p, (RInfo *)B.sinfo.p, bad);
+    HIPCHK(ctx, hipGetLastError());
+    MH_TRY(bam_check_bounds(ctx, bad, "k_bam_sinfo"));
+    {
+      int64_t *hs = pinned_small(ctx);
+      if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+      HIPCHK(ctx, hipMemcpyAsync(hs + 24, (const int64_t *)B.soff.p + n, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs + 25, (const int64_t *)B.roff.p + n, 8, hipMemcpyDeviceToHost, st));
+      SYNCCHK(ctx, hipStreamSynchronize(st));
+      if (hs[24] != B.bytes || hs[25] != B.bytes)
+        return arg_fail(ctx, MH_E_STATE, "BAM store: record offsets do not add up to the store's size (internal)");
+    }
+    B.sorted = true;
+    return MH_OK;
+  }
+  MH_TRY(ensure(ctx, B.srecs, B.bytes + 64));
   {   // the offsets must close on the store's byte count (a record-size mismatch would send the copies astray)
     int64_t *hs = pinned_small(ctx);
     if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
@@ -781,11 +821,87 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
   const int64_t n = B.n_rec;
   if (n == 0) return MH_OK;
   static_assert(sizeof(RInfo) == 16, "RInfo layout");
+  if (recs && B.spilled > 0) {   // the sorted stream assembled from the host blocks
+    MH_TRY(bam_spill(ctx));
+    BamHostOrder o;
+    MH_TRY(bam_host_order(ctx, o));
+    bam_assemble(B, o, 0, B.bytes, recs, 16);
+    recs = nullptr;
+  }
   if (recs) HIPCHK(ctx, hipMemcpyAsync(recs, B.srecs.p, B.bytes, hipMemcpyDeviceToHost, st));
   if (soff) HIPCHK(ctx, hipMemcpyAsync(soff, B.soff.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, st));
   if (info) HIPCHK(ctx, hipMemcpyAsync(info, B.sinfo.p, sizeof(RInfo) * n, hipMemcpyDeviceToHost, st));
   SYNCCHK(ctx, hipStreamSynchronize(st));
   return MH_OK;
+}
+
+// ---- bounded HBM: spilled records -----------------------------------------------------------------------------
+int32_t bam_spill(mh_ctx *ctx) {
+  BamStore &B = ctx->bam;
+  if (B.direct) MH_TRY(bam_undirect(ctx));
+  const int64_t len = B.bytes - B.spilled;
+  if (len <= 0) return MH_OK;
+  uint8_t *p = (uint8_t *)malloc((size_t)len);
+  if (!p) return arg_fail(ctx, MH_E_OOM, "host memory for spilled BAM records (" + std::to_string(len) + " bytes)");
+  stage_begin(ctx, "bam_spill");
+  if (hipMemcpyAsync(p, B.recs.p, (size_t)len, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    free(p);
+    return hip_fail(ctx, hipGetLastError(), "BAM spill D2H", __FILE__, __LINE__);
+  }
+  stage_end(ctx);
+  B.spill.push_back(BamStore::HostBlock{p, B.spilled, B.bytes});
+  B.spilled = B.bytes;
+  B.sorted = false;
+  return MH_OK;
+}
+
+int32_t bam_host_order(mh_ctx *ctx, BamHostOrder &o) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  const int64_t n = B.n_rec;
+  if (!B.sorted) return arg_fail(ctx, MH_E_STATE, "BAM store not sorted (internal)");
+  o.val.resize((size_t)n + 1);
+  o.roff.resize((size_t)n + 1);
+  o.soff.resize((size_t)n + 1);
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(o.val.data(), B.val2.p, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(o.roff.data(), B.roff.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(o.soff.data(), B.soff.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost, st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+  } else {
+    o.roff[0] = o.soff[0] = 0;
+  }
+  return MH_OK;
+}
+
+void bam_assemble(const BamStore &B, const BamHostOrder &o, int64_t w0, int64_t w1, uint8_t *dst, int threads) {
+  const int64_t n = B.n_rec;
+  if (w1 <= w0 || n == 0) return;
+  // sorted records overlapping [w0, w1): k0 = the one holding byte w0, k1 = the first starting at or after w1
+  const int64_t k0 = std::upper_bound(o.soff.begin(), o.soff.begin() + n + 1, w0) - o.soff.begin() - 1;
+  const int64_t k1 = std::lower_bound(o.soff.begin(), o.soff.begin() + n + 1, w1) - o.soff.begin();
+  const int64_t nk = k1 - k0;
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, nk / 4096));
+  auto part = [&](int t) {
+    const int64_t a = k0 + nk * t / T, b = k0 + nk * (t + 1) / T;
+    size_t blk = 0;
+    for (int64_t k = a; k < b; k++) {
+      const uint32_t r = o.val[k];
+      const int64_t src = o.roff[r], len = o.roff[r + 1] - src, s = o.soff[k];
+      const int64_t lo = std::max(s, w0), hi = std::min(s + len, w1);
+      if (hi <= lo) continue;
+      if (!(B.spill[blk].b0 <= src && src < B.spill[blk].b1))   // the host block holding the record (whole records)
+        blk = std::upper_bound(B.spill.begin(), B.spill.end(), src,
+                               [](int64_t x, const BamStore::HostBlock &h) { return x < h.b0; }) - B.spill.begin() - 1;
+      const BamStore::HostBlock &h = B.spill[blk];
+      std::memcpy(dst + (lo - w0), h.p + (src - h.b0) + (lo - s), (size_t)(hi - lo));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(part, t);
+  part(0);
+  for (auto &x : th) x.join();
 }
 
 // ---- the BAI's device plan -----------------------------------------------------------------------------------
@@ -962,7 +1078,14 @@ int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, boo
   return MH_OK;
 }
 
+void bam_free_spill(BamStore &B) {
+  for (auto &h : B.spill) free(h.p);
+  B.spill.clear();
+  B.spilled = 0;
+}
+
 void bam_release(BamStore &B) {
+  bam_free_spill(B);
   for (DevBuf *b : {&B.names, &B.name_off, &B.nl1, &B.nl2, &B.tpl, &B.roff, &B.recs, &B.key, &B.val, &B.info,
                     &B.key2, &B.val2, &B.sort_tmp, &B.soff, &B.srecs, &B.sinfo, &B.in1, &B.in2, &B.bai_lin,
                     &B.bai_runs, &B.bai_out})

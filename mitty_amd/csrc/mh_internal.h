@@ -127,8 +127,19 @@ struct BamStore {
   DevBuf bai_lin, bai_runs, bai_out;                  // the BAI's device plan (mh_bam.hip bam_bai_plan)
   int64_t n_rec = 0, bytes = 0;
   int32_t n_files = 0;
-  bool sorted = false;         // srecs/soff/sinfo hold the current store in coordinate order
+  bool sorted = false;         // soff/sinfo (and srecs unless spilled) hold the current store in coordinate order
   bool direct = false;         // ... written there straight from the parse (no input-order copy in recs yet)
+  // Bounded HBM (mh_bam_set_capacity): the records' bytes beyond `cap` leave HBM.  The store's input-order prefix
+  // [0, spilled) lives in host blocks; recs holds [spilled, bytes).  Keys, offsets and BAI info of every record stay
+  // in HBM (~36 B per record), so the coordinate sort is one device sort of the keys; the sorted byte stream is
+  // assembled on the host window by window and deflated on the device (mh_bam_write_gpu) or the host.
+  int64_t cap = 0;             // record bytes held in HBM before a spill (0: no limit)
+  struct HostBlock {
+    uint8_t *p;
+    int64_t b0, b1;            // the store's input-order bytes [b0, b1)
+  };
+  std::vector<HostBlock> spill;
+  int64_t spilled = 0;
 };
 
 struct StageTime {
@@ -356,12 +367,22 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
 int32_t bam_sort(mh_ctx *ctx, const void *pa = nullptr);
 int32_t bam_undirect(mh_ctx *ctx);
 int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
+int32_t bam_spill(mh_ctx *ctx);   // the device-resident records to a host block (input order)
+// the sorted store's byte stream [w0, w1) into dst (host), from the host blocks (every record spilled); the sorted
+// order (val2), input offsets (roff) and sorted offsets (soff) as host copies (bam_host_order)
+struct BamHostOrder {
+  std::vector<uint32_t> val;
+  std::vector<int64_t> roff, soff;
+};
+int32_t bam_host_order(mh_ctx *ctx, BamHostOrder &o);
+void bam_assemble(const BamStore &B, const BamHostOrder &o, int64_t w0, int64_t w1, uint8_t *dst, int threads);
 struct BaiPlan;
 // The BAI's per-record half on the device (sorted store): chunks and linear index as positions in `offs`, the
 // compact array of the data offsets they need.  *ok = false (and MH_OK) when the records are outside what the
 // device plan checks (a record past its reference's length, an unsorted store): the caller then plans on the host.
 int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, bool *ok);
 void bam_release(BamStore &B);
+void bam_free_spill(BamStore &B);
 int32_t newline_index(mh_ctx *ctx, const uint8_t *b, int64_t len, DevBuf &nl, int64_t *count);
 int32_t corrupt_fastq(mh_ctx *ctx, const uint8_t *d0, int64_t len0, const uint8_t *d1, int64_t len1, int64_t t_base,
                       int64_t *used0, int64_t *used1, int64_t *templates);

@@ -1102,6 +1102,65 @@ def test_god_aligner_bam_vs_oracle(native, model, tmp_path):
     _god_check(bam2, b1, b2)
 
 
+@pytest.mark.parametrize('gpu_bgzf', [False, True])
+@pytest.mark.parametrize('model', G.MODELS)
+def test_god_aligner_spilled_store_vs_oracle(native, model, gpu_bgzf, tmp_path):
+  """Bounded HBM (mh_bam_set_capacity, the counterpart of the reference's `samtools sort -m 2G`, god_aligner.py:100-116):
+  a 150 kB record budget with 64 kB input chunks spills the store to host memory many times over; the coordinate
+  sort still runs on the device (keys stay in HBM) and the sorted stream is assembled on the host, window by window
+  (one BGZF block per window at this budget, deflated on the device for gpu_bgzf).  The BAM and its BAI equal the
+  unbounded store's byte for byte, and the oracle's records and index (oracle/god.py)."""
+  from mitty_amd.benchmarking import god_aligner as ga
+  fa = _god_setup(tmp_path)
+  fq1, fq2, b1, b2 = _god_inputs(model, tmp_path)
+  a, b = str(tmp_path / 'a.bam'), str(tmp_path / 'b.bam')
+  sa = ga.process_multi_threaded(fa, a, fq1, fq2, threads=2, chunk_bytes=65536, gpu_bgzf=gpu_bgzf)
+  sb = ga.process_multi_threaded(fa, b, fq1, fq2, threads=2, chunk_bytes=65536, gpu_bgzf=gpu_bgzf,
+                                 hbm_capacity=150_000)
+  assert sa['spill_blocks'] == 0 and sb['spill_blocks'] > 5 and sb['spilled_bytes'] == sb['bam_bytes_uncompressed']
+  assert sb['bam_bytes_uncompressed'] > 10 * 150_000
+  assert open(a, 'rb').read() == open(b, 'rb').read()
+  assert open(a + '.bai', 'rb').read() == open(b + '.bai', 'rb').read()
+  _god_check(b, b1, b2)
+
+
+def test_god_aligner_spill_from_device_arenas(native, tmp_path):
+  """The configs[4] path (records straight from the FASTQ arenas, mh_bam_add_output) over a bounded store: two
+  generate-reads jobs appended (the second add spills the first's records), the device-deflated file equal to the
+  unbounded store's."""
+  from mitty_amd.engine import Engine
+  from mitty_amd.lib import fasta as mfasta, vcfio
+  from mitty_amd.readmodel import get_read_model
+  from mitty_amd.simulation import readgenerate
+  c = G.load_json('e2e_config.json')['1kg-pcr-free']
+  mod, mdl = get_read_model('1kg-pcr-free.pkl')
+  rm = mod.read_model_params(mdl, c['coverage'])
+  vdf = vcfio.load_variants_soa(G.path(c['vcf']), c['sample'], G.path(c['bed']))
+  seqs = mfasta.read_fasta(G.path(c['fasta']))
+  units = [(ps, w['region_idx'], w['region_cpy'], w['rng_seed'])
+           for ps, w in enumerate(readgenerate.get_data_for_workers(rm, vdf, c['seed']))]
+  out = {}
+  for cap in (0, 200_000):
+    eng = Engine(0)
+    try:
+      for ri, reg in enumerate(vdf):
+        eng.load_region(ri, reg['region'], mfasta.fetch(seqs, *reg['region']))
+      eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
+      eng.ctx.bam_set_capacity(cap)
+      for job in range(2):
+        eng.ctx.reset_output()
+        eng.run_units(units, lambda r, cp: vdf[r]['copies'][cp], rm['p'], rm['rlen'], rm['cum_tlen'],
+                      'S{}'.format(job))
+        eng.ctx.bam_add_output()
+      bam = str(tmp_path / 'c{}.bam'.format(cap))
+      eng.ctx.bam_write_gpu(bam, '@HD\tVN:1.0\tSO:coordinate\n', bai_path=bam + '.bai')
+      out[cap] = (open(bam, 'rb').read(), open(bam + '.bai', 'rb').read(), eng.ctx.bam_spilled())
+    finally:
+      eng.close()
+  assert out[0][2] == (0, 0) and out[200_000][2][1] >= 2
+  assert out[0][0] == out[200_000][0] and out[0][1] == out[200_000][1]
+
+
 def test_god_aligner_rejects_sequence_quality_mismatch(native, tmp_path):
   """pysam's AlignedSegment raises ValueError('quality and sequence mismatch') in write_perfect_reads; so do we."""
   from mitty_amd.benchmarking import god_aligner as ga
