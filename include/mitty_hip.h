@@ -244,6 +244,16 @@ int32_t mh_bam_reset(mh_ctx *ctx);
  * unbounded store's.  mh_bam_spilled: bytes and host blocks spilled so far. */
 int32_t mh_bam_set_capacity(mh_ctx *ctx, int64_t bytes);
 int32_t mh_bam_spilled(mh_ctx *ctx, int64_t *bytes, int64_t *blocks);
+/* Store pieces across ranks (configs[4] on N GPUs: each rank builds the BAM records of its FASTQ pieces, rank 0's
+ * store takes them in piece order and sorts and writes once — the reference's pysam.cat of the workers' fragments
+ * before one sort, god_aligner.py:63-68,100-108).  mh_bam_export copies records [r0, r1) of the store in input order:
+ * their bytes, the r1 - r0 + 1 record offsets (absolute), the sort keys and the BAI info (4 x int32 per record); any
+ * pointer may be host or device memory, or NULL to skip.  mh_bam_import appends n records given the same way
+ * (offsets with any base); ties in the coordinate order keep the import order. */
+int32_t mh_bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *roff, uint64_t *keys,
+                      int32_t *info);
+int32_t mh_bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *keys, const int32_t *info,
+                      int64_t n);
 /* mh_bam_write_gpu: mh_bam_write with the record blocks deflated on the device (mh_deflate.hip: dynamic-Huffman BGZF
  *   blocks of the sorted store in HBM, 0xff00 input bytes each, the header's block deflated on the host at level 6):
  *   only the compressed bytes cross PCIe.  Replaces the same pysam.sort / pysam.index pair (god_aligner.py:117-131);

@@ -24,7 +24,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_set_capacity', 'mh_bam_spilled', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
+           'mh_bam_records', 'mh_bam_set_capacity', 'mh_bam_spilled', 'mh_bam_export', 'mh_bam_import', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait', 'mh_output_fetch_async',
            'mh_output_fetch_wait',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
@@ -110,6 +110,8 @@ def lib():
   _sig(L, 'mh_bam_records', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_bam_set_capacity', [c_vp, c_i64])
   _sig(L, 'mh_bam_spilled', [c_vp, P_i64, P_i64])
+  _sig(L, 'mh_bam_export', [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_bam_import', [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64])
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
   _sig(L, 'mh_bam_write_gpu', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, P_i64, P_i64, P_i64])
@@ -336,6 +338,15 @@ def device_count():
   n = c_i32(0)
   lib().mh_device_count(ctypes.byref(n))
   return n.value
+
+
+def bam_piece_layout(n, nbytes):
+  """Byte offsets of a packed BAM store piece (n records, nbytes of records): records at 0, then (8-aligned) the
+  n + 1 record offsets, the n sort keys and the n BAI infos (4 x int32); returns (o_roff, o_key, o_info, total)."""
+  o_roff = (int(nbytes) + 7) & ~7
+  o_key = o_roff + 8 * (n + 1)
+  o_info = o_key + 8 * n
+  return o_roff, o_key, o_info, o_info + 16 * n
 
 
 def _ptr(a):
@@ -750,6 +761,25 @@ class Context:
     b, k = c_i64(), c_i64()
     self._chk(self._L.mh_bam_spilled(self._h, ctypes.byref(b), ctypes.byref(k)))
     return b.value, k.value
+
+  def bam_export(self, r0, r1, nbytes, ptr=None):
+    """Records [r0, r1) of the store (nbytes of record bytes) packed (bam_piece_layout) at address ptr (host or
+    device), or into a new uint8 array (returned)."""
+    n = int(r1 - r0)
+    o_roff, o_key, o_info, total = bam_piece_layout(n, nbytes)
+    out = None
+    if ptr is None:
+      out = np.empty(max(total, 8), np.uint8)
+      ptr = out.ctypes.data
+    self._chk(self._L.mh_bam_export(self._h, int(r0), int(r1), c_vp(ptr), c_vp(ptr + o_roff), c_vp(ptr + o_key),
+                                    c_vp(ptr + o_info)))
+    return out
+
+  def bam_import(self, n, nbytes, ptr):
+    """Append a packed piece (bam_export's layout) at address ptr (host or device) to the store."""
+    o_roff, o_key, o_info, _ = bam_piece_layout(n, nbytes)
+    self._chk(self._L.mh_bam_import(self._h, c_vp(ptr), c_vp(ptr + o_roff), c_vp(ptr + o_key), c_vp(ptr + o_info),
+                                    int(n)))
 
   def bam_records(self):
     n, b = c_i64(), c_i64()

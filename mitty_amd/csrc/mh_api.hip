@@ -1342,6 +1342,19 @@ int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes) {
   return MH_OK;
 }
 
+int32_t mh_bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *roff, uint64_t *keys,
+                      int32_t *info) {
+  CTX_GUARD(ctx);
+  return bam_export(ctx, r0, r1, recs, roff, keys, info);
+}
+
+int32_t mh_bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *keys, const int32_t *info,
+                      int64_t n) {
+  CTX_GUARD(ctx);
+  if (n < 0 || (n > 0 && (!roff || !keys || !info))) return arg_fail(ctx, MH_E_ARG, "null argument");
+  return bam_import(ctx, recs, roff, keys, info, n);
+}
+
 int32_t mh_bam_spilled(mh_ctx *ctx, int64_t *bytes, int64_t *blocks) {
   if (!ctx) return MH_E_ARG;
   if (bytes) *bytes = ctx->bam.spilled;

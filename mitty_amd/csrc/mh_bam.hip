@@ -835,6 +835,77 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
   return MH_OK;
 }
 
+// ---- store pieces across ranks (configs[4] on N GPUs) ----------------------------------------------------------
+__global__ void k_bam_import_idx(int64_t *roff, int64_t n, int64_t r0, int64_t base, uint32_t *val, int64_t vbase) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n) roff[i] = roff[i] - r0 + base;
+  if (i < n) val[i] = (uint32_t)(vbase + i);
+}
+
+int32_t bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *roff, uint64_t *key, int32_t *info) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  if (B.direct) MH_TRY(bam_undirect(ctx));   // (the direct write's sorted order becomes the input order)
+  if (r0 < 0 || r1 < r0 || r1 > B.n_rec) return arg_fail(ctx, MH_E_ARG, "record range outside the store");
+  const int64_t n = r1 - r0;
+  int64_t ab[2] = {0, 0};
+  HIPCHK(ctx, hipMemcpyAsync(ab, (const int64_t *)B.roff.p + r0, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(ab + 1, (const int64_t *)B.roff.p + r1, 8, hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  if (recs) {   // the bytes [ab[0], ab[1]): the spilled part from the host blocks, the rest from HBM
+    int64_t a = ab[0];
+    for (const auto &h : B.spill) {
+      if (a >= ab[1] || h.b1 <= a) continue;
+      const int64_t e = std::min(h.b1, ab[1]);
+      HIPCHK(ctx, hipMemcpyAsync(recs + (a - ab[0]), h.p + (a - h.b0), (size_t)(e - a), hipMemcpyDefault, st));
+      a = e;
+    }
+    if (a < ab[1])
+      HIPCHK(ctx, hipMemcpyAsync(recs + (a - ab[0]), (const uint8_t *)B.recs.p + (a - B.spilled), (size_t)(ab[1] - a),
+                                 hipMemcpyDefault, st));
+  }
+  if (roff) HIPCHK(ctx, hipMemcpyAsync(roff, (const int64_t *)B.roff.p + r0, 8 * (size_t)(n + 1), hipMemcpyDefault, st));
+  if (key && n) HIPCHK(ctx, hipMemcpyAsync(key, (const uint64_t *)B.key.p + r0, 8 * (size_t)n, hipMemcpyDefault, st));
+  if (info && n) HIPCHK(ctx, hipMemcpyAsync(info, (const RInfo *)B.info.p + r0, sizeof(RInfo) * n, hipMemcpyDefault, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  return MH_OK;
+}
+
+int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *key, const int32_t *info,
+                   int64_t n) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  if (B.direct) MH_TRY(bam_undirect(ctx));
+  if (n <= 0) return MH_OK;
+  if (B.n_rec + n >= (int64_t)UINT32_MAX) return arg_fail(ctx, MH_E_CAPACITY, "more than 2^32 records in one BAM");
+  int64_t ab[2] = {0, 0};
+  HIPCHK(ctx, hipMemcpyAsync(ab, roff, 8, hipMemcpyDefault, st));
+  HIPCHK(ctx, hipMemcpyAsync(ab + 1, roff + n, 8, hipMemcpyDefault, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  const int64_t add = ab[1] - ab[0];
+  if (add < 0) return arg_fail(ctx, MH_E_ARG, "record offsets decrease");
+  if (B.cap > 0 && B.bytes > B.spilled && B.bytes - B.spilled + add > B.cap) MH_TRY(bam_spill(ctx));
+  MH_TRY(ensure_keep(ctx, B.recs, B.bytes - B.spilled + add + 64, B.bytes - B.spilled));
+  MH_TRY(ensure_keep(ctx, B.roff, sizeof(int64_t) * (B.n_rec + n + 1), sizeof(int64_t) * (B.n_rec + 1)));
+  MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n), sizeof(uint64_t) * B.n_rec));
+  MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n), sizeof(uint32_t) * B.n_rec));
+  MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n), sizeof(RInfo) * B.n_rec));
+  if (add) HIPCHK(ctx, hipMemcpyAsync((uint8_t *)B.recs.p + (B.bytes - B.spilled), recs, (size_t)add, hipMemcpyDefault, st));
+  int64_t *ro = (int64_t *)B.roff.p + B.n_rec;
+  HIPCHK(ctx, hipMemcpyAsync(ro, roff, 8 * (size_t)(n + 1), hipMemcpyDefault, st));
+  HIPCHK(ctx, hipMemcpyAsync((uint64_t *)B.key.p + B.n_rec, key, 8 * (size_t)n, hipMemcpyDefault, st));
+  HIPCHK(ctx, hipMemcpyAsync((RInfo *)B.info.p + B.n_rec, info, sizeof(RInfo) * n, hipMemcpyDefault, st));
+  hipLaunchKernelGGL(k_bam_import_idx, dim3(grid_for(n + 1, 256, INT32_MAX)), dim3(256), 0, st, ro, n, ab[0], B.bytes,
+                     (uint32_t *)B.val.p + B.n_rec, B.n_rec);
+  HIPCHK(ctx, hipGetLastError());
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  B.n_rec += n;
+  B.bytes += add;
+  B.sorted = false;
+  return MH_OK;
+}
+
 // ---- bounded HBM: spilled records -----------------------------------------------------------------------------
 int32_t bam_spill(mh_ctx *ctx) {
   BamStore &B = ctx->bam;

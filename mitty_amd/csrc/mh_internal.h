@@ -367,7 +367,10 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
 int32_t bam_sort(mh_ctx *ctx, const void *pa = nullptr);
 int32_t bam_undirect(mh_ctx *ctx);
 int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
-int32_t bam_spill(mh_ctx *ctx);   // the device-resident records to a host block (input order)
+int32_t bam_spill(mh_ctx *ctx);
+int32_t bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *roff, uint64_t *key, int32_t *info);
+int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *key, const int32_t *info,
+                   int64_t n);   // the device-resident records to a host block (input order)
 // the sorted store's byte stream [w0, w1) into dst (host), from the host blocks (every record spilled); the sorted
 // order (val2), input offsets (roff) and sorted offsets (soff) as host copies (bam_host_order)
 struct BamHostOrder {

@@ -17,8 +17,14 @@ illumina.py:56-58), so the path shards without any data-path collective:
   (~4.5x smaller) until an all-reduce of the compressed sizes places them.  The files are byte-identical to the
   single-GPU run (= reference --threads 1) at any GPU count.
 
-The collectives carry a few int64 per piece; no sequence data crosses xGMI.  Outputs must be regular files
-(ranks write at offsets); FIFOs / process substitution need the single-GPU path.
+The collectives carry a few int64 per piece; no sequence data crosses xGMI for the FASTQ files.  Outputs must be
+regular files (ranks write at offsets); FIFOs / process substitution need the single-GPU path.
+
+With a BAM output (configs[4]: the god-aligner's perfect BAM of the generated reads), every rank also turns each of
+its pieces into BAM records on its own GPU as the piece is emitted (parse, encode, keys: mh_bam_add_output on the
+arenas), and rank 0's store takes the pieces in piece order (RCCL point-to-point on device buffers; gloo on host
+arrays), sorts the keys once and writes the BAM and BAI — the reference's pysam.cat of the workers' fragments before
+one sort (god_aligner.py:63-68,100-108).  The BAM equals the one-GPU god-aligner's over the same FASTQ, byte for byte.
 
 A process holds one HIP runtime: torch must load before libmitty_hip.so (mitty_amd._native does that itself when
 WORLD_SIZE > 1), otherwise torch brings its own runtime and whichever of the two initialises second sees no GPU.
@@ -199,17 +205,39 @@ class DeviceBackend:
   def reset_output(self):
     self.eng.ctx.reset_output()
 
+  # ---- the BAM leg: per piece the records of the arenas, packed (_native.bam_piece_layout); rank 0's store ----
+  def bam_piece(self, refs):
+    ctx = self.eng.ctx
+    ctx.bam_set_refs([r[0] for r in refs], [r[1] for r in refs])
+    ctx.bam_add_output()
+    n, nb = ctx.bam_records()
+    return n, nb, ctx.bam_export(0, n, nb)
+
+  def bam_begin(self, refs, capacity=0):
+    ctx = self.eng.ctx
+    ctx.bam_set_refs([r[0] for r in refs], [r[1] for r in refs])
+    ctx.bam_set_capacity(capacity)
+
+  def bam_import(self, n, nb, ptr):
+    self.eng.ctx.bam_import(n, nb, ptr)
+
+  def bam_write(self, path, header_text, bai=True):
+    return self.eng.ctx.bam_write_gpu(path, header_text, bai_path=path + '.bai' if bai else None)
+
   def close(self):
     self.eng.close()
 
 
 def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                                fastq1_fname, fastq2_fname, seed=7, rng='mitty', corrupt_seed=None, backend=None,
-                               group=None, max_batch_draws=200_000_000, layout=None):
+                               group=None, max_batch_draws=200_000_000, layout=None, bam_fname=None,
+                               bam_header_text=None, bam_refs=None, bam_capacity=0):
   """process_multi_threaded (readgenerate.py:76-126) over the ranks of the default process group.
 
   `backend` defaults to DeviceBackend(LOCAL_RANK); tests pass a host stand-in to exercise the orchestration with
   the gloo backend on CPU.  Returns this rank's stats plus the job totals.
+  bam_fname: also the god-aligner's BAM (+ .bai) of the reads, header bam_header_text, @SQ bam_refs [(name, length)]
+  (god_aligner.construct_header from the FASTA's .ann); bam_capacity: rank 0's record bytes in HBM before a spill.
   """
   import torch.distributed as dist
   from mitty_amd.simulation.readgenerate import get_data_for_workers
@@ -312,6 +340,7 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
   # the arenas are recycled after every piece -------------------------------------------------------------------
   fds = [os.open(fn, os.O_WRONLY) if not gz[f] else None for f, fn in enumerate(fnames)]
   held = {}   # piece index -> compressed bytes per gz file
+  bam_held = {}   # piece index -> (records, record bytes, packed piece)
   raw = [0, 0]
   try:
     for i in sorted(plan):
@@ -331,6 +360,8 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
         for f in plain:
           _pwrite_all(fds[f], data[f], off[f][i])
       held[i] = [backend.fetch_gz(f, rs[f]) if gz[f] else None for f in range(len(fnames))]
+      if bam_fname is not None:
+        bam_held[i] = backend.bam_piece(bam_refs)
   finally:
     for fd in fds:
       if fd is not None:
@@ -363,12 +394,59 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       finally:
         os.close(fd)
   held.clear()
+  if bam_fname is not None:
+    stats['bam_records'] = _bam_merge(backend, pieces, bam_held, rank, world, group, bam_fname, bam_header_text,
+                                      bam_refs, bam_capacity)
   tot = allreduce_i64([stats['templates'], stats['kept']] + raw, group)
   if world > 1:
     dist.barrier(group)
   stats.update({'job_templates': tot[0], 'job_kept': tot[1], 'bytes1': tot[2], 'bytes2': tot[3] if write2 else 0,
                 'seconds': time.time() - t0, 'rank': rank, 'world': world})
   return stats
+
+
+def _bam_merge(backend, pieces, bam_held, rank, world, group, bam_fname, header_text, refs, capacity):
+  """Rank 0's store takes every piece's records in piece order (its own from memory, the others' over the process
+  group: point-to-point, RCCL on device buffers under 'nccl'), then sorts and writes the BAM + BAI once.  The ranks
+  hold their packed pieces until then.  Returns the BAM's record count on rank 0 (0 elsewhere)."""
+  import torch
+  from mitty_amd import _native
+  sz = [0] * (2 * len(pieces))
+  for i, (n, nb, _) in bam_held.items():
+    sz[2 * i], sz[2 * i + 1] = n, nb
+  sz = allreduce_i64(sz, group)
+  dev = None
+  if world > 1:
+    import torch.distributed as dist
+    dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
+  if rank == 0:
+    backend.bam_begin(refs, capacity)
+  total = 0
+  for i in range(len(pieces)):
+    n, nb = sz[2 * i], sz[2 * i + 1]
+    if n == 0:
+      continue
+    owner = pieces[i][3]
+    size = _native.bam_piece_layout(n, nb)[3]
+    if owner == rank:
+      buf = bam_held.pop(i)[2]
+      if rank == 0:
+        backend.bam_import(n, nb, buf.ctypes.data)
+      else:
+        t = torch.from_numpy(buf[:size])
+        dist.send(t.to(dev) if dev == 'cuda' else t, 0, group=group)
+    elif rank == 0:
+      t = torch.empty(size, dtype=torch.uint8, device=dev)
+      dist.recv(t, owner, group=group)
+      if dev == 'cuda':
+        torch.cuda.current_stream().synchronize()
+      backend.bam_import(n, nb, t.data_ptr())
+    total += n
+  if rank == 0:
+    backend.bam_write(bam_fname, header_text)
+  if world > 1:
+    dist.barrier(group)
+  return total if rank == 0 else 0
 
 
 def _pwrite_all(fd, data, off):

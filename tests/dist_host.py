@@ -83,8 +83,50 @@ class OracleBackend:
     pass
 
 
+  # ---- the BAM leg (DeviceBackend.bam_*): records from oracle/god.py, packed as mh_bam_export packs them ----------
+  def bam_piece(self, refs):
+    import numpy as np
+    from oracle import god
+    from mitty_amd import _native
+    ref_dict = {name: k for k, (name, _) in enumerate(refs)}
+    recs = god.god_records(bytes(self.arena[0]), bytes(self.arena[1]) if self.arena[1] else None, ref_dict)
+    enc = [god.encode(r) for r in recs]
+    n, nb = len(enc), sum(len(e) for e in enc)
+    o_roff, o_key, o_info, total = _native.bam_piece_layout(n, nb)
+    buf = np.zeros(max(total, 8), np.uint8)
+    buf[:nb] = np.frombuffer(b''.join(enc), np.uint8)
+    buf[o_roff:o_key].view(np.int64)[:] = np.concatenate([[0], np.cumsum([len(e) for e in enc])]).astype(np.int64)
+    buf[o_key:o_info].view(np.uint64)[:] = [r['reference_id'] << 33 | (r['pos'] + 1) << 1 | int(r['is_reverse'])
+                                            for r in recs]
+    buf[o_info:total].view(np.int32)[:] = np.array(
+        [[r['reference_id'], r['pos'], god.end_pos(r), god.reg2bin(r['pos'], god.end_pos(r))] for r in recs],
+        np.int32).reshape(-1) if n else []
+    return n, nb, buf
+
+  def bam_begin(self, refs, capacity=0):
+    self.bam = []   # (key, import order, record bytes)
+
+  def bam_import(self, n, nb, ptr):
+    import ctypes
+    import numpy as np
+    from mitty_amd import _native
+    o_roff, o_key, _, total = _native.bam_piece_layout(n, nb)
+    buf = np.frombuffer(ctypes.string_at(ptr, total), np.uint8)
+    roff = buf[o_roff:o_key].view(np.int64)
+    keys = buf[o_key:o_key + 8 * n].view(np.uint64)
+    for k in range(n):
+      self.bam.append((int(keys[k]), len(self.bam), bytes(buf[roff[k] - roff[0]:roff[k + 1] - roff[0]])))
+
+  def bam_write(self, path, header_text, bai=True):
+    """The sorted record stream, uncompressed (the stand-in checks the order, not the BGZF framing)."""
+    with open(path, 'wb') as fp:
+      for _, _, rec in sorted(self.bam, key=lambda x: (x[0], x[1])):
+        fp.write(rec)
+
+
 def _records(b):
   """FASTQ bytes -> records with the '@{stub}:{cnt}|' head stripped."""
   lines = b.split(b'\n')
   return [lines[i].split(b'|', 1)[1] + b'\n' + b'\n'.join(lines[i + 1:i + 4]) + b'\n'
           for i in range(0, len(lines) - 1, 4)]
+

@@ -198,3 +198,39 @@ def test_lpt_fewer_units_than_ranks(tmp_path):
     a, b = open(tmp_path / f, 'rb').read(), open(one / f, 'rb').read()
     assert len(a) > 10000
     G.check_same(a, b)
+
+
+def _rank_bam(rank, world, port, outdir, layout):
+  import torch.distributed as dist
+  os.environ['MASTER_ADDR'] = '127.0.0.1'
+  os.environ['MASTER_PORT'] = str(port)
+  dist.init_process_group('gloo', rank=rank, world_size=world)
+  try:
+    from mitty_amd.readmodel import get_read_model
+    from tests.dist_host import OracleBackend
+    c = G.load_json('e2e_config.json')['1kg-pcr-free']
+    mod, mdl = get_read_model('1kg-pcr-free.pkl')
+    st = D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
+                                      seed=c['seed'], backend=OracleBackend(), layout=layout,
+                                      bam_fname=os.path.join(outdir, 'g.bam'), bam_header_text='@HD\tVN:1.0\n',
+                                      bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)])
+    assert (st['bam_records'] > 0) == (rank == 0)
+  finally:
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,layout', [(1, None), (2, None), (3, 'slice')])
+def test_distributed_bam_leg(tmp_path, world, layout):
+  """The configs[4] BAM leg over gloo ranks (host stand-in backend: records from oracle/god.py): every rank builds
+  its pieces' records, rank 0 takes them in piece order and writes the coordinate-sorted stream — equal to the
+  god-aligner oracle's sorted records of the one-process FASTQ (ties in input order)."""
+  from tests._spawn import spawn_with_port
+  from oracle import god
+  spawn_with_port(_rank_bam, lambda port: (world, port, str(tmp_path), layout), world)
+  f1, f2 = open(tmp_path / 'r1.fq', 'rb').read(), open(tmp_path / 'r2.fq', 'rb').read()
+  G.check_same(f1, G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'))
+  want = b''.join(god.encode(r) for r in god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2})))
+  got = open(tmp_path / 'g.bam', 'rb').read()
+  assert len(want) > 100000
+  assert got == want

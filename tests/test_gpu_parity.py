@@ -945,7 +945,7 @@ def test_emit_slices_concatenate_to_unit(native, corrupt):
     eng.close()
 
 
-def _gpu_rank(rank, world, port, layout, outdir):
+def _gpu_rank(rank, world, port, layout, outdir, bam=False):
   import torch.distributed as dist
   os.environ['MASTER_ADDR'] = '127.0.0.1'
   os.environ['MASTER_PORT'] = str(port)
@@ -955,9 +955,13 @@ def _gpu_rank(rank, world, port, layout, outdir):
     from mitty_amd.readmodel import get_read_model
     c = G.load_json('e2e_config.json')['1kg-pcr-free']
     mod, mdl = get_read_model('1kg-pcr-free.pkl')
+    extra = {}
+    if bam:   # the configs[4] BAM leg: every rank's pieces as BAM records, merged and written by rank 0
+      extra = dict(bam_fname=os.path.join(outdir, 'g.bam'), bam_header_text='@HD\tVN:1.0\tSO:coordinate\n',
+                   bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)], bam_capacity=bam if bam is not True else 0)
     D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
                                  c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
-                                 seed=c['seed'], backend=D.DeviceBackend(0), layout=layout)
+                                 seed=c['seed'], backend=D.DeviceBackend(0), layout=layout, **extra)
   finally:
     dist.destroy_process_group()
 
@@ -1019,6 +1023,30 @@ def test_distributed_two_ranks_one_gpu(native, tmp_path, layout):
   spawn_with_port(_gpu_rank, lambda port: (2, port, layout, str(tmp_path)), 2)
   G.check_same(open(tmp_path / 'r1.fq', 'rb').read(), G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'))
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz'))
+
+
+@pytest.mark.parametrize('layout,cap', [('lpt', 0), ('slice', 300_000)])
+def test_distributed_bam_two_ranks_one_gpu(native, tmp_path, layout, cap):
+  """configs[4] across ranks: two ranks (gloo, both on GPU 0) each build the BAM records of their pieces on the
+  device; rank 0's store imports them in piece order (mh_bam_import) and writes BAM + BAI.  Equal byte for byte to
+  the one-rank run, and its records and index to the god-aligner oracle over the reference FASTQ; with a bounded
+  rank-0 store (cap) too."""
+  from tests._spawn import spawn_with_port
+  from oracle import god
+  one, two = tmp_path / 'one', tmp_path / 'two'
+  one.mkdir()
+  two.mkdir()
+  spawn_with_port(_gpu_rank, lambda port: (1, port, layout, str(one), True), 1)
+  spawn_with_port(_gpu_rank, lambda port: (2, port, layout, str(two), cap or True), 2)
+  f1, f2 = G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz')
+  G.check_same(open(two / 'r1.fq', 'rb').read(), f1)
+  a, b = open(one / 'g.bam', 'rb').read(), open(two / 'g.bam', 'rb').read()
+  assert a == b
+  assert open(one / 'g.bam.bai', 'rb').read() == open(two / 'g.bam.bai', 'rb').read()
+  _, recs, vo, vend = god.record_voffsets(b)
+  want = god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2}))
+  assert len(recs) == len(want) > 1000 and recs == [god.encode(r) for r in want]
+  assert open(two / 'g.bam.bai', 'rb').read() == god.bai(3, [god.decode(r) for r in recs], vo, vend)
 
 
 # ---- god-aligner BAM (SURVEY.md §8(a) A16) -------------------------------------------------------------------------
