@@ -65,9 +65,9 @@ def parse():
   ap.add_argument('--cpu-baseline-frac', type=float, default=0.25,
                   help='WGS leg of the CPU baseline: all 100 work units, each on the first FRAC of its region '
                        '(0 = skip)')
-  ap.add_argument('--cpu-workers', type=int, default=16,
-                  help='CPU baseline worker processes (the reference\'s --threads; 16 = the GPU box\'s CPU share '
-                       'for one GPU)')
+  ap.add_argument('--cpu-workers', type=int, default=100,
+                  help='CPU baseline worker processes, the reference\'s --threads (SURVEY.md §8(d): min(host cores, '
+                       '#units) = 100 for the WGS job); a second WGS leg runs 16 (one GPU\'s CPU share on the box)')
   ap.add_argument('--verify', action='store_true',
                   help='wgs, N = 1: after the timed steps, run one more step unit by unit and compare every unit\'s '
                        'FASTQ bytes (sha256 of its arena range, both files) with the CPU oracle\'s digests')
@@ -607,7 +607,9 @@ def run_genome(a, rank, world, local):
     if not a.no_cpu_baseline:
       legs = {}
       if a.cpu_baseline_frac > 0:
-        legs['wgs'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model)
+        legs['wgs'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, a.cpu_workers)
+        if min(a.cpu_workers, os.cpu_count() or 1) > 16:
+          legs['wgs_16'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, 16)
       if a.cpu_baseline_mbp > 0:
         legs['chr1'] = cpu_baseline(a, seq1, recs1, p, rlen, model, _native.work_units(a.seed, [2], passes))
       if a.cpu_config0:
@@ -773,14 +775,14 @@ def _cpu_pool_run(jobs, workers):
   return n, dt, n / busy if busy > 0 else None
 
 
-def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model):
+def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, n_workers):
   """The metric's workload on the CPU: the CPU oracle (oracle/mitty_oracle.c, a scalar port of the reference path)
   laid out like the reference's multiprocessing path (`readgenerate.process_multi_threaded`: worker processes pulling
   work units, readgenerate.py:76-126) over all 100 work units of the 30x WGS job, in --cpu-workers processes.  Bounded
   sample: each unit runs on the first --cpu-baseline-frac of its region (same variants, same seeds), so the sample
   has the full job's unit list and topology.  Rate = templates / (last unit's end - first unit's start)."""
   frac = a.cpu_baseline_frac
-  workers = max(1, min(a.cpu_workers, os.cpu_count() or 1))
+  workers = max(1, min(n_workers, os.cpu_count() or 1, len(units)))
   d = tempfile.mkdtemp(prefix='mh_cpu_', dir='/dev/shm' if os.path.isdir('/dev/shm') else None)
   img = os.path.join(d, 'ref.bin')
   try:
@@ -803,9 +805,9 @@ def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model):
   return {'value': n / dt, 'unit': 'templates/s', 'cores': workers, 'kind': 'port', 'per_core': per_core,
           'host_cpus': os.cpu_count(), 'workload': 'wgs',
           'sample': 'the 30x WGS job\'s {} work units (25 regions x 2 copies x 2 passes, the reference\'s unit order '
-                    'and seeds), each on the first {:.0%} of its region, in {} oracle worker processes ({} host CPUs '
-                    'visible; {} = the box\'s CPU share for one GPU): {} templates in {:.2f} s'.format(
-                        len(jobs), frac, workers, os.cpu_count(), a.cpu_workers, n, dt)}
+                    'and seeds), each on the first {:.0%} of its region, in {} oracle worker processes (min(host CPUs, '
+                    'units, {}); {} host CPUs visible): {} templates in {:.2f} s'.format(
+                        len(jobs), frac, workers, n_workers, os.cpu_count(), n, dt)}
 
 
 def synth_copies(recs, L):

@@ -300,6 +300,7 @@ CorruptCfg corrupt_cfg(const mh_ctx *ctx, uint64_t unit_key, int64_t t_base) {
   cc.bk = (const uint8_t *)(base + ctx->corrupt_bk_off);
   cc.T16 = (const uint16_t *)(base + ctx->corrupt_T16_off);
   cc.Fp16 = (const uint16_t *)(base + ctx->corrupt_Fp16_off);
+  cc.bkf = (const uint8_t *)(base + ctx->corrupt_bkf_off);
   return cc;
 }
 }  // namespace mh
@@ -355,8 +356,8 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->max_cu = prop.multiProcessorCount;
-  const char *so = getenv("MH_SORT");
-  ctx->sort_lsd = so && !strcmp(so, "lsd");
+  const char *so = getenv("MH_SORT");   // (A/B: MH_SORT=rocprim, the library's onesweep sort)
+  ctx->sort_lsd = !(so && !strcmp(so, "rocprim"));
   *out = ctx;
   return MH_OK;
 }
@@ -1105,7 +1106,7 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   // [k, k + 1) / 256 and g[k] < 93 (CB_ROW = CG_BUCKETS buckets of the 16-bit draw)
   static_assert(mh::CB_ROW == mh::CG_BUCKETS, "bucket table and guide share their buckets");
   std::vector<uint16_t> guide((size_t)2 * max_bp * (mh::CG_BUCKETS + 1));
-  std::vector<uint8_t> bk((size_t)2 * max_bp * mh::CB_ROW);
+  std::vector<uint8_t> bk((size_t)2 * max_bp * mh::CB_ROW), bkf((size_t)2 * max_bp * mh::CF_ROW);
   for (size_t r = 0; r < (size_t)2 * max_bp; r++) {
     const uint16_t *row = T16.data() + r * n_bq;
     uint16_t *g = guide.data() + r * (mh::CG_BUCKETS + 1);
@@ -1118,13 +1119,23 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
       const int lo = g[k];
       bk[r * mh::CB_ROW + k] = (uint8_t)((lo < 93 ? lo : 93) | (lo < 93 && g[k + 1] > lo ? 0x80 : 0));
     }
+    // the fine table: the same entry over buckets of 32 draw values
+    c = 0;
+    int64_t c1 = 0;
+    for (int k = 0; k < mh::CF_ROW; k++) {
+      while (c < n_bq && (uint32_t)row[c] < ((uint32_t)k << mh::CF_SHIFT)) c++;
+      if (c1 < c) c1 = c;
+      while (c1 < n_bq && (uint32_t)row[c1] < ((uint32_t)(k + 1) << mh::CF_SHIFT)) c1++;
+      bkf[r * mh::CF_ROW + k] = (uint8_t)((c < 93 ? c : 93) | (c < 93 && c1 > c ? 0x80 : 0));
+    }
   }
   auto al16 = [](size_t x) { return ((x + 15) / 16) * 16; };
   ctx->corrupt_guide_off = al16(8 * nt);
   ctx->corrupt_bk_off = al16(ctx->corrupt_guide_off + 2 * guide.size());
   ctx->corrupt_T16_off = al16(ctx->corrupt_bk_off + bk.size());
   ctx->corrupt_Fp16_off = al16(ctx->corrupt_T16_off + 2 * nt);
-  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_Fp16_off + 2 * 100 + 64));
+  ctx->corrupt_bkf_off = al16(ctx->corrupt_Fp16_off + 2 * 100);
+  MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_bkf_off + bkf.size() + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
   char *base = (char *)ctx->corrupt_cum.p;
   HIPCHK(ctx, hipMemcpyAsync(base, cum_bq, 8 * nt, hipMemcpyHostToDevice, ctx->stream));
@@ -1133,6 +1144,7 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_bk_off, bk.data(), bk.size(), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_T16_off, T16.data(), 2 * nt, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_Fp16_off, Fp16.data(), 2 * 100, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(base + ctx->corrupt_bkf_off, bkf.data(), bkf.size(), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->corrupt_phred.p, phred_p, 8 * 100, hipMemcpyHostToDevice, ctx->stream));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->corrupt_on = true;
@@ -1390,6 +1402,16 @@ int32_t mh_bam_write(mh_ctx *ctx, const char *bam_path, const char *header_text,
 
 }  // extern "C"
 
+// copies that mh_output_bgzf_pair left in flight out of gz_out's halves: done before anything else rewrites gz_out
+static int32_t gz_drain(mh_ctx *ctx) {
+  for (int h = 0; h < 2; h++)
+    if (ctx->gz_pending[h]) {
+      SYNCCHK(ctx, hipEventSynchronize(ctx->ev_gz[h]));
+      ctx->gz_pending[h] = false;
+    }
+  return MH_OK;
+}
+
 // A spilled store's sorted record stream deflated on the device window by window: the host assembles window i + 1
 // (bam_assemble, a thread of its own) while window i goes H2D and through bgzf_device into ctx->gz_out.  Windows
 // are whole numbers of BGZF blocks, so the blocks — and the file — are the ones one deflate of the whole stream
@@ -1398,6 +1420,7 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t *nz, std::vector<int64_t
                                    const std::function<void(int64_t, int64_t)> &on_piece) {
   BamStore &B = ctx->bam;
   MH_TRY(bam_spill(ctx));   // (the records still in HBM: every record is then on the host)
+  MH_TRY(bam_sort(ctx));    // (a no-op unless the spill undid a direct write's order)
   BamHostOrder o;
   MH_TRY(bam_host_order(ctx, o));
   const int64_t cap_blocks = B.cap > 0 ? B.cap / BGZF_BLOCK : 8192;
@@ -1514,6 +1537,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
       release(c->gz_out);   // (to the device block cache: the next file's output buffer)
     }
   } guard{ctx, &pieces};
+  MH_TRY(gz_drain(ctx));
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
   const int64_t SLOT_B = (int64_t)1 << 26;
   for (auto &p : ctx->h_bam_pin)
@@ -1679,6 +1703,7 @@ int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out
   if ((!in && len > 0) || len < 0 || !out || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   *used = 0;
   if (len == 0) return MH_OK;
+  MH_TRY(gz_drain(ctx));
   MH_TRY(ensure(ctx, ctx->gz_in, (size_t)len + 64));
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(len)));
   HIPCHK(ctx, hipMemcpyAsync(ctx->gz_in.p, in, len, hipMemcpyHostToDevice, ctx->stream));
@@ -1705,6 +1730,7 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
   const uint8_t *src = (const uint8_t *)(file ? ctx->out2.p : ctx->out1.p) + offset;
   *used = 0;
   if (len == 0) return MH_OK;
+  MH_TRY(gz_drain(ctx));
   MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(len)));
   int64_t u = 0;
   stage_begin(ctx, "bgzf_deflate");

@@ -823,6 +823,7 @@ int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *inf
   static_assert(sizeof(RInfo) == 16, "RInfo layout");
   if (recs && B.spilled > 0) {   // the sorted stream assembled from the host blocks
     MH_TRY(bam_spill(ctx));
+    MH_TRY(bam_sort(ctx));   // (a no-op unless the spill undid a direct write's order)
     BamHostOrder o;
     MH_TRY(bam_host_order(ctx, o));
     bam_assemble(B, o, 0, B.bytes, recs, 16);
@@ -922,8 +923,7 @@ int32_t bam_spill(mh_ctx *ctx) {
   }
   stage_end(ctx);
   B.spill.push_back(BamStore::HostBlock{p, B.spilled, B.bytes});
-  B.spilled = B.bytes;
-  B.sorted = false;
+  B.spilled = B.bytes;   // (the sort's order, offsets and info stay valid: only where the bytes live changed)
   return MH_OK;
 }
 

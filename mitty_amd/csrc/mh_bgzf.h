@@ -1,6 +1,7 @@
 // mh_bgzf.h — host side of the BAM writer: BGZF framing on a deflate thread pool and the BAI index (SAM/BAM
 // specification §4.1 / §5.2; the reference produces these through htslib via pysam.sort / pysam.index,
-// god_aligner.py:117-131).  Plain C++ (no HIP); compiled with g++ and linked against zlib.
+// god_aligner.py:117-131).  The BAI is a valid spec index of our own file, not byte-identical to htslib's output
+// (htslib's chunk merging and linear-index fill are not pinned here: no htslib in the image).  Plain C++ (no HIP); compiled with g++ and linked against zlib.
 #pragma once
 
 #include <cstdint>

@@ -25,6 +25,8 @@ namespace mh {
 
 constexpr int CG_BUCKETS = 256;   // search-guide buckets per BQ row: bucket k = draws in [k / 256, (k + 1) / 256)
 constexpr int CB_ROW = 256;       // Philox mode: bucket-table bytes per BQ row (h1 >> 8)
+constexpr int CF_SHIFT = 6;       // Philox mode, the row pass's fine table: bucket h1 >> 6 (1024 per row)
+constexpr int CF_ROW = 65536 >> CF_SHIFT;
 
 struct CorruptCfg {
   int32_t enable;
@@ -37,6 +39,8 @@ struct CorruptCfg {
   const uint8_t *bk = nullptr;       // [2][max_bp][CB_ROW]: min(entries below k / 256, 93) | 0x80 (one inside)
   const uint16_t *T16 = nullptr;     // [2][max_bp][n_bq]: min(floor(cum * 2^16), 65535)
   const uint16_t *Fp16 = nullptr;    // [100]: min(floor(phred_p * 2^16), 65535)
+  const uint8_t *bkf = nullptr;      // [2][max_bp][CF_ROW]: bk's entries over 1024 buckets (the row pass: a threshold
+                                     // inside the draw's bucket for ~2.2 % of draws instead of ~7 %)
 };
 
 // a ^ b ^ k in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96; the compiler emits two v_xor_b32 for

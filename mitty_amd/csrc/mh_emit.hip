@@ -914,7 +914,7 @@ struct TArgs {
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
-template <int NF, int LPR, int CR>
+template <int NF, int LPR, int CR, int GW>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
@@ -967,10 +967,11 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   }
   for (int i = tid; i < TL; i += ED_THREADS)
     smem[o_t + i] = (char)(i == 0 || i == 2 || i == TL - 1 ? '\n' : i == 1 ? '+' : '~');
-  if (tid >= 64) {
-    // waves 1-3: the gathers (three threads per mate window), all in flight together; an unused chunk re-reads the
-    // first one
-    const int g = tid - 64, pr = g / 3, q3 = g - 3 * pr;
+  if (tid >= 64 * (4 - GW)) {
+    // the last GW waves: the gathers (GW threads per mate window), all in flight together; an unused chunk re-reads
+    // the first one
+    constexpr int GM = (3 * ED_GMAX + GW - 1) / GW;
+    const int g = tid - 64 * (4 - GW), pr = g / GW, q3 = g - GW * pr;
     const int jg = pr >> 1, sg = pr & 1;
     const int64_t tg = t0 + (jg < nt ? jg : 0);
     const bool kg = jg < nt;
@@ -983,29 +984,30 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     const int64_t a2g = sg ? h.hap_len - ag - lg : ag;
     const int64_t a16 = a2g & ~(int64_t)15;
     const uint8_t *hsrc = (sg ? h.rc : h.hap) + a16;
-    uint4 wv[ED_GMAX];
+    uint4 wv[GM];
     uint32_t use = 0;
 #pragma unroll
-    for (int k = 0; k < ED_GMAX; k++) {
-      const int c = q3 + 3 * k;
+    for (int k = 0; k < GM; k++) {
+      const int c = q3 + GW * k;
       const bool u = kg && c < chunks && a16 + 16 * c < a2g + lg;
       use |= (uint32_t)u << k;
       wv[k] = *(const uint4 *)(hsrc + (u ? 16 * c : 0));
     }
-    // waves 1-2 also copy the tile's strip slots (the qname reads parts k_emit_measure formatted): 16 bytes each, to
-    // the qname buffer after its head room
+    // the first 128 gather threads also copy the tile's strip slots (the qname reads parts k_emit_measure
+    // formatted): 16 bytes each, to the qname buffer after its head room
     const int js = g >> 2, cs = g & 3;
     const bool ks = g < 4 * ED_T && js < nt;
     uint4 sv = make_uint4(0, 0, 0, 0);
     if (ks) sv = *(const uint4 *)(A.slot + (t0 + js) * ED_SW + 16 * cs);
     const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
 #pragma unroll
-    for (int k = 0; k < ED_GMAX; k++) {
-      const int c = q3 + 3 * k;
+    for (int k = 0; k < GM; k++) {
+      const int c = q3 + GW * k;
       *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * c : o_dump)) = wv[k];
     }
     if (ks) __builtin_memcpy(smem + o_q + js * qstride + head + 16 * cs, &sv, 16);
-  } else if (tid < 64) {
+  }
+  if (tid < 64) {
     // wave 0: lane = read (template jf, mate s)
     const int jf = tid >> 1, s = tid & 1;
     const bool valid = jf < nt;
@@ -1149,9 +1151,9 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
 // One workgroup per 32-template tile.  (A grid-stride loop over tiles kept ~140 VGPRs live across iterations — three
 // waves per SIMD instead of eight — and the launch of 184 k workgroups costs only ~0.35 ms of a 2.6 ms chr1-unit
 // writer (round 3), so there is no persistent variant.)
-template <int NF, int LPR, int CR>
+template <int NF, int LPR, int CR, int GW>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
-  emit_tile<NF, LPR, CR>(A, qh, blockIdx.x);
+  emit_tile<NF, LPR, CR, GW>(A, qh, blockIdx.x);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -1509,14 +1511,29 @@ static_assert(ED_CRB == CI_BLK, "the writer's row blocks are the corruption bloc
 // (k_emit_tiles<.., 2>) lays the qualities into per-record T strings in LDS and applies the codes to its windows, so
 // the corrupted records leave the writer in its aligned 16-byte stores (no partial-line rewrite afterwards).
 
-// One full block with the tables in LDS (cr_full_block's phases), into registers: qualities packed in qo (byte 15
-// zero), the codes of the substituted bases in *code.
-__device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, const uint16_t *tp, uint32_t otp,
-                                              const uint16_t *fp,
-                                              const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f, int n0,
-                                              uint4 *qo, uint32_t *code) {
+// The row pass's BQ step from the fine table (k_cr_cols' LDS): entries of row j below h1 (capped at 93) from the
+// bucket entry e = bkf[j][h1 >> CF_SHIFT]; a flagged bucket (a threshold inside it) walks the row's T16 entries from
+// there, *amb when one equals h1.  The same counts and ambiguity as cr_walk_at's 256-bucket table and its pairs.
+__device__ __forceinline__ uint32_t cr_fine_walk(uint32_t e, const uint16_t *t16, uint32_t lim, uint32_t h1,
+                                                 uint32_t *amb) {
+  uint32_t c = e & 0x7fu;
+  *amb = 0;
+  if (e & 0x80u) {
+    while (c < lim && t16[c] < h1) c++;
+    *amb = c < lim && t16[c] == h1;
+  }
+  return c;
+}
+
+// One full block with the fine table in LDS, into registers (cr_block_rows' outputs): per base one bucket byte and
+// the Fp16 of its BQ decide (about 98 % of draws); the flagged buckets and the U2 draws on a threshold go to the
+// per-lane loop after the block.  bkf: base n0's row (row j at bkf + j * CF_ROW); t16: its T16 row (j * n_bq).
+__device__ __forceinline__ void cr_block_rows_f(const uint8_t *bkf, const uint16_t *t16, const uint16_t *fp,
+                                                const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f,
+                                                int n0, uint4 *qo, uint32_t *code) {
   const int n_bq = cc.n_bq;
-  uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], P[CI_BLK], V2[CI_BLK], F[CI_BLK], BQ[CI_BLK];
+  const uint32_t lim = n_bq < 93 ? (uint32_t)n_bq : 93u;
+  uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], F[CI_BLK];
   const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
 #pragma unroll
   for (int g = 0; g < CI_BLK / 3; g++) {
@@ -1527,36 +1544,20 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, c
     RW[g] = r.w;
   }
 #pragma unroll
-  for (int j = 0; j < CI_BLK; j++) E[j] = bk[obk + (uint32_t)(j * CB_ROW) + (W[j] >> 24)];
+  for (int j = 0; j < CI_BLK; j++) E[j] = bkf[j * CF_ROW + (W[j] >> (16 + CF_SHIFT))];
+#pragma unroll
+  for (int j = 0; j < CI_BLK; j++) F[j] = fp[E[j] & 0x7fu];
+  uint32_t ps = 0, px = 0, qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0;
 #pragma unroll
   for (int j = 0; j < CI_BLK; j++) {
-    const uint32_t ti = otp + (uint32_t)(j * n_bq) + (E[j] & 0x7fu);
-    P[j] = tp[ti];
-    V2[j] = ((const uint8_t *)tp)[2 * ti + 3];   // (byte 3 from the pair's start: the next entry's high byte)
-  }
-  uint32_t ps = 0, px = 0;
-#pragma unroll
-  for (int j = 0; j < CI_BLK; j++) {
-    const uint32_t e = E[j], c = e & 0x7fu, fl = e >> 7, pa = P[j];
-    const uint32_t lo = (W[j] >> 16) & 0xffu;
-    const uint32_t v0 = pa & 0xffu, v1 = pa >> 8, v2 = V2[j];
-    const uint32_t b0 = fl & (uint32_t)(v0 < lo), b1 = b0 & (uint32_t)(v1 < lo), b2 = b1 & (uint32_t)(v2 < lo);
-    const uint32_t vn = b1 ? v2 : (b0 ? v1 : v0);
-    const uint32_t amb = b2 | (fl & (uint32_t)(vn == lo));
-    BQ[j] = c + b0 + b1;
-    px |= amb << j;
-    F[j] = fp[BQ[j]];
-  }
-  uint32_t qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0;
-#pragma unroll
-  for (int j = 0; j < CI_BLK; j++) {
-    const uint32_t amb = (px >> j) & 1u, pth = F[j], h2 = W[j] & 0xffffu;
-    ps |= (uint32_t)(!amb && h2 < pth) << j;
-    px |= (uint32_t)(h2 == pth) << j;
-    const uint32_t qv = (BQ[j] + 33u) << (8 * (j & 3));
+    const int32_t d = (int32_t)(W[j] & 0xffffu) - (int32_t)F[j];   // U2's top 16 bits against Fp16[bq]
+    ps |= ((uint32_t)d >> 31) << j;
+    px |= (uint32_t)(d == 0 || (E[j] & 0x80u)) << j;
+    const uint32_t qv = ((E[j] & 0x7fu) + 33u) << (8 * (j & 3));
     if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
   }
-  while (px) {   // rare: the full 53-bit decisions
+  ps &= ~px;
+  while (px) {   // rare: a threshold in the bucket (walk), then the 16-bit U2 decision or the full 53-bit ones
     const int j = __builtin_ctz(px);
     px &= px - 1;
     const int n = n0 + j;
@@ -1564,9 +1565,13 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, c
     const int k = n % 3;
     const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
     uint32_t amb;
-    const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), tp, otp + (uint32_t)(j * n_bq), w, &amb);
-    const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
-                                     w, bq, amb);
+    const uint32_t bq = cr_fine_walk(bkf[j * CF_ROW + (w >> (16 + CF_SHIFT))], t16 + j * n_bq, lim, w >> 16, &amb);
+    const uint32_t pth = fp[bq], h2 = w & 0xffffu;
+    uint32_t x;
+    if (amb || h2 == pth)
+      x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n, w, bq, amb);
+    else
+      x = bq | (h2 < pth ? 0x100u : 0u);
     const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
     if (j < 4) qd0 = (qd0 & mk) | qv; else if (j < 8) qd1 = (qd1 & mk) | qv; else if (j < 12) qd2 = (qd2 & mk) | qv;
     else qd3 = (qd3 & mk) | qv;
@@ -1591,77 +1596,6 @@ __device__ __forceinline__ void cr_block_rows(const uint8_t *bk, uint32_t obk, c
   *code = cd;
 }
 
-// One corruption row slot: the qualities (+ 33) and substitution codes of block n0 / 15 of template (tl, th)'s file f
-// (cnt bases: a full block, or the short last one) — k_cr_cols' item.  bk / t8p: the bucket and threshold-pair
-// tables, obk / otp the offsets of base n0's rows in them (a 32-bit offset from a uniform base), fp16 the u16
-// substitution thresholds.  (The same item computed inside the writer instead of a pass before it — its tables then
-// in global memory, 115 VGPRs — was slower: 0.69 vs 0.78 G/s on configs[2], round 4.)
-__device__ __forceinline__ void cr_slot(const uint8_t *bk, uint32_t obk, const uint16_t *t8p, uint32_t otp,
-                                        const uint16_t *fp16, const CorruptCfg &cc, uint2 key, uint32_t tl,
-                                        uint32_t th, int f, int n0, int cnt, uint4 *qo_, uint32_t *code_) {
-  const int n_bq = cc.n_bq;
-  if (cnt == CI_BLK) {
-    cr_block_rows(bk, obk, t8p, otp, fp16, cc, key, tl, th, f, n0, qo_, code_);
-  } else {   // a short last block: the guarded per-base path
-    uint32_t qd[4] = {0, 0, 0, 0}, px = 0, pc = 0, ps = 0, ch = 0;
-#pragma unroll
-    for (int g = 0; g < CI_BLK / 3; g++) {
-      if (3 * g < cnt) {
-        const uint4 r = philox4x32_10(
-            make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          const int j = 3 * g + k;
-          if (j < cnt) {
-            const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-            uint32_t amb;
-            const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), t8p, otp + (uint32_t)(j * n_bq), w, &amb);
-            const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
-            const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-            const bool sub = !amb && h2 < pth;
-            px |= (uint32_t)(amb || h2 == pth) << j;
-            ps |= (uint32_t)sub << j;
-            pc |= (uint32_t)(sub && c10 == 1023u) << j;
-            ch |= (c10 % 3u) << (2 * j);
-            qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
-          }
-        }
-      }
-    }
-    while (px) {
-      const int j = __builtin_ctz(px);
-      px &= px - 1;
-      const int n = n0 + j;
-      const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-      const int k = n % 3;
-      const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-      uint32_t amb;
-      const uint32_t bq = cr_walk_at(bk, obk + (uint32_t)(j * CB_ROW), t8p, otp + (uint32_t)(j * n_bq), w, &amb);
-      const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
-                                       f, n, w, bq, amb);
-      const uint32_t sh = 8u * (uint32_t)(j & 3);
-      qd[j >> 2] = (qd[j >> 2] & ~(0xffu << sh)) | (((x & 0xffu) + 33u) << sh);
-      const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
-      ps |= (x >> 8) << j;
-      pc |= (uint32_t)((x >> 8) && c10 == 1023u) << j;
-    }
-    while (pc) {
-      const int j = __builtin_ctz(pc);
-      pc &= pc - 1;
-      const uint4 c = philox4x32_10(
-          make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3), key);
-      ch = (ch & ~(3u << (2 * j))) | (__umulhi(c.x, 3u) << (2 * j));
-    }
-    uint32_t code = 0;
-    while (ps) {
-      const int j = __builtin_ctz(ps);
-      ps &= ps - 1;
-      code |= (((ch >> (2 * j)) & 3u) + 1u) << (2 * j);
-    }
-    *qo_ = make_uint4(qd[0], qd[1], qd[2], qd[3]);
-    *code_ = code;
-  }
-}
 
 // The corruption rows: a workgroup per (block column, template chunk) stages only its column's tables (bucket rows
 // and threshold pairs of 15 positions of one file: 6.7 KB; a record-major pass staging a whole file's 67 KB was
@@ -1678,34 +1612,70 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
   const int NB = (rlen + CI_BLK - 1) / CI_BLK;
   const int col = (int)blockIdx.y, f = col / NB, b = col - f * NB, n0 = CI_BLK * b;
   const int cnt = rlen - n0 < CI_BLK ? rlen - n0 : CI_BLK;
-  const uint32_t lim_all = n_bq < 93 ? (uint32_t)n_bq : 93u;
-  // LDS: bucket rows [15][CB_ROW] | Fp16[100] (256 B) | threshold low-byte pairs [15][n_bq] (+16)
-  const int32_t o_fp = CI_BLK * CB_ROW, o_t8 = o_fp + 256;
+  // LDS: fine bucket rows [15][CF_ROW] | Fp16[100] (256 B) | T16 rows [15][n_bq] (+16)
+  const int32_t o_fp = CI_BLK * CF_ROW, o_t16 = o_fp + 256;
   {
-    const uint4 *src = (const uint4 *)(cc.bk + ((int64_t)f * cc.max_bp + n0) * CB_ROW);
+    const uint4 *src = (const uint4 *)(cc.bkf + ((int64_t)f * cc.max_bp + n0) * CF_ROW);
     uint4 *dst = (uint4 *)ctab;
-    for (int i = threadIdx.x; i < cnt * CB_ROW / 16; i += CC_THREADS) dst[i] = src[i];
+    for (int i = threadIdx.x; i < cnt * CF_ROW / 16; i += CC_THREADS) dst[i] = src[i];
     const uint16_t *t16 = cc.T16 + ((int64_t)f * cc.max_bp + n0) * n_bq;
-    for (int i = threadIdx.x; i < cnt * n_bq; i += CC_THREADS) {
-      const int j = i % n_bq;
-      const uint32_t a = t16[i], c = j + 1 < (int)lim_all ? t16[i + 1] : 0xffffu;
-      ((uint16_t *)(ctab + o_t8))[i] = (uint16_t)((a & 0xffu) | ((c >> 8) == (a >> 8) ? (c & 0xffu) << 8 : 0xff00u));
-    }
+    for (int i = threadIdx.x; i < cnt * n_bq; i += CC_THREADS) ((uint16_t *)(ctab + o_t16))[i] = t16[i];
     for (int i = threadIdx.x; i < 100; i += CC_THREADS) ((uint16_t *)(ctab + o_fp))[i] = cc.Fp16[i];
   }
   __syncthreads();
-  const uint8_t *bk = ctab;
+  const uint8_t *bkf = ctab;
   const uint16_t *fp16 = (const uint16_t *)(ctab + o_fp);
-  const uint16_t *t8p = (const uint16_t *)(ctab + o_t8);
+  const uint16_t *t16 = (const uint16_t *)(ctab + o_t16);
+  const uint32_t lim = n_bq < 93 ? (uint32_t)n_bq : 93u;
   const uint2 key = make_uint2(cc.k0, cc.k1);
   const int64_t tb = (int64_t)blockIdx.x * per_wg, te = tb + per_wg < A.m ? tb + per_wg : A.m;
   uint4 *const orow = rows + (int64_t)col * A.m;
   uint32_t *const ocode = codes + (int64_t)col * A.m;
   for (int64_t t = tb + threadIdx.x; t < te; t += CC_THREADS) {
     const int64_t tt = t + cc.t_base;
+    const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
     uint4 qo;
     uint32_t code;
-    cr_slot(bk, 0u, t8p, 0u, fp16, cc, key, (uint32_t)tt, (uint32_t)(tt >> 32), f, n0, cnt, &qo, &code);
+    if (cnt == CI_BLK) {
+      cr_block_rows_f(bkf, t16, fp16, cc, key, tl, th, f, n0, &qo, &code);
+    } else {   // a short last block: per triple, per base (as corrupt_triple, into the slot)
+      uint32_t qd[4] = {0, 0, 0, 0}, cd = 0;
+#pragma unroll
+      for (int g = 0; g < CI_BLK / 3; g++) {
+        if (3 * g >= cnt) continue;
+        const uint4 r = philox4x32_10(
+            make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n0 / 3u + (uint32_t)g), cc.c3), key);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int j = 3 * g + k;
+          if (j >= cnt) continue;
+          const int n = n0 + j;
+          const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+          uint32_t amb;
+          uint32_t bq = cr_fine_walk(bkf[j * CF_ROW + (w >> (16 + CF_SHIFT))], t16 + j * n_bq, lim, w >> 16, &amb);
+          const uint32_t pth = fp16[bq], h2 = w & 0xffffu;
+          bool sub;
+          if (amb || h2 == pth) {
+            const uint32_t x = cq_exact(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th,
+                                        f, n, w, bq, amb);
+            bq = x & 0xffu;
+            sub = x >> 8;
+          } else {
+            sub = h2 < pth;
+          }
+          qd[j >> 2] |= (bq + 33u) << (8 * (j & 3));
+          if (sub) {
+            uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+            if (c10 == 1023u)
+              c10 = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)n, cc.c3),
+                                           key).x, 3u);
+            cd |= (c10 % 3u + 1u) << (2 * j);
+          }
+        }
+      }
+      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+      code = cd;
+    }
     orow[t] = qo;
     ocode[t] = code;
   }
@@ -1725,7 +1695,7 @@ static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
   CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, rlen, nf, 0, cc};
   stage_begin(ctx, "emit_corrupt_rows");
-  const size_t lds_c = (size_t)CI_BLK * CB_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
+  const size_t lds_c = (size_t)CI_BLK * CF_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
   const int64_t gx = (m + CC_PER_WG - 1) / CC_PER_WG;
   if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
   hipLaunchKernelGGL(k_cr_cols, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS), lds_c, st, A, rows, codes);
@@ -1886,9 +1856,14 @@ constexpr int32_t ED_QPAD = 4;
 // two files
 using EwKernel = void (*)(TArgs, QHead);
 static EwKernel ew_kernel(int cr, bool two) {
-  return cr == 2 ? (two ? k_emit_tiles<2, 4, 2> : k_emit_tiles<1, 8, 2>)
-         : cr == 1 ? (two ? k_emit_tiles<2, 4, 1> : k_emit_tiles<1, 8, 1>)
-                   : (two ? k_emit_tiles<2, 4, 0> : k_emit_tiles<1, 8, 0>);
+  static const bool gw4 = getenv("MH_EW_GW4") != nullptr;   // (A/B: every wave gathers)
+  if (gw4)
+    return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 4> : k_emit_tiles<1, 8, 2, 4>)
+           : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 4> : k_emit_tiles<1, 8, 1, 4>)
+                     : (two ? k_emit_tiles<2, 4, 0, 4> : k_emit_tiles<1, 8, 0, 4>);
+  return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 3> : k_emit_tiles<1, 8, 2, 3>)
+         : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 3> : k_emit_tiles<1, 8, 1, 3>)
+                   : (two ? k_emit_tiles<2, 4, 0, 3> : k_emit_tiles<1, 8, 0, 3>);
 }
 
 static size_t ed_lds_bytes(int32_t win_stride, int32_t qstride, int64_t rlen, int nf, bool rows) {

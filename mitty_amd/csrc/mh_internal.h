@@ -240,6 +240,7 @@ struct mh_ctx {
   int32_t corrupt_max_bp = 0, corrupt_n_bq = 0;
   size_t corrupt_guide_off = 0;   // byte offsets inside corrupt_cum: the search guide, the Philox-mode bucket table
   size_t corrupt_bk_off = 0, corrupt_T16_off = 0, corrupt_Fp16_off = 0;   // and the u16 tables T16, Fp16
+  size_t corrupt_bkf_off = 0;                                               // the row pass's fine bucket table
   uint64_t corrupt_seed = 0;
   // exact corruption stream of mh_corrupt_fastq (mh_corrupt_stream_seed / _state): 0 = Philox; 1 = the stream of
   // RandomState(cx_seed) from output cx_pos on; 2 = continuing the explicit state (cx_key, cx_kpos)

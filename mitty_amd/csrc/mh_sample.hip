@@ -1198,10 +1198,10 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // phase: 0 = everything; 1 = the geometric scan (and a per-unit sort); 2 = the rest.
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
-// The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (7-bit digits, 256-thread
-// workgroups sized to fit beside the FASTQ writers), or rocprim's onesweep (1024-thread workgroups, which wait for
-// whole CUs beside the writers; 9 key bits per pass: a 64 M-draw batch's 27-bit keys in 3 passes).  Until the
-// hand-written sort has run on the GPU, rocprim stays the default (MH_SORT=lsd selects the other).
+// The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (9-bit digits with the tile
+// counts folded into the scatter: a 64 M-draw batch's 27-bit keys in 3 passes, 256-thread workgroups sized to fit
+// beside the FASTQ writers).  MH_SORT=rocprim: rocprim's onesweep (1024-thread workgroups, which wait for whole CUs
+// beside the writers), kept for the A/B.
 using SortCfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 9,
@@ -1359,7 +1359,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     q.p_max = p_max[u];
     q.n = (int64_t)((double)(q.p_max - q.p_min) * p * 1.2);   // int((p_max - p_min) * p * 1.2)
     if (q.n < 0) q.n = 0;
-    if (q.n > ((int64_t)1 << 31) - 2) return arg_fail(ctx, MH_E_ARG, "region too large for one work unit");
+    // (< 2^30 draws: the permutation sort's look-back counts are 30-bit; a 2x150 30x unit of 2^30 draws is a
+    // 36 Gbp region)
+    if (q.n > ((int64_t)1 << 30) - 8) return arg_fail(ctx, MH_E_ARG, "region too large for one work unit");
     HostMT sr;
     sr.seed((uint32_t)seeds[u]);
     q.s_tloc = (uint32_t)sr.interval(0xfffffffeull);
@@ -1509,8 +1511,8 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     for (int l = 2; l < n_lanes; l++) HIPCHK(ctx, hipStreamWaitEvent(ctx->xstream[l - 2], ctx->ev_fork, 0));
   }
-  // the batch-wide permutation (one sort per unit when the batch's draws exceed 2^31)
-  const bool batch = rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 31) && n_units <= PK_UNITS;
+  // the batch-wide permutation (one sort per unit when the batch's draws exceed 2^30)
+  const bool batch = rng_mode == MH_RNG_MITTY && j_total < ((int64_t)1 << 30) && n_units <= PK_UNITS;
   if (batch) {
     MH_TRY(ensure(ctx, ctx->pb[0], 8 * (size_t)j_total + 64));
     MH_TRY(ensure(ctx, ctx->pb[1], 8 * (size_t)j_total + 64));

@@ -1,18 +1,18 @@
 // mh_sort.h — the permutation's stable (target, step) sort on gfx950: an LSD radix sort of u32 keys whose values are
 // the element indices (the Fisher-Yates steps, illumina.py:70 `shuffle_rng.shuffle(ts)`; DESIGN.md "Kernels").
 //
-// 7-bit digits, ceil(end_bit / 7) passes, each three steps:
-//   k_rs_count    one 256-thread workgroup per 2048-key tile: the tile's digit histogram (LDS atomics), written
-//                 digit-major (count[d * tiles + tile]), so one exclusive scan of the counts gives every
-//                 (digit, tile) its global output offset;
-//   scan          device_scan_sum (mh_scan.h's look-back scan) over the 128 x tiles counts;
-//   k_rs_scatter  the tile again: each wave ranks its 8 x 64 keys stably (per item row a match over the digit's 7
-//                 bits by ballots, a running per-wave digit count in LDS), waves combined per digit, the keys and
-//                 values laid out in LDS in digit order, then written out in that order (runs of one digit — 16 keys
-//                 on average, 64 bytes — land on consecutive addresses).
-// Sized to fit where a FASTQ writer workgroup retires: 256 threads and under 20 KB of LDS (the writer's is ~22 KB), so
-// the sort's workgroups take the CU slots the writers free (the library sort's 1024-thread workgroups waited for whole
-// CUs, round 3).  Stable: equal keys keep their input order, as rocprim's sort does.
+// 9-bit digits, ceil(end_bit / 9) passes (a 64 M-draw batch's 26-27-bit keys: 3), with the tile counts folded into
+// the scatter (decoupled look-back per digit), so a pass reads and writes every key and value once:
+//   k_rs_hist     every pass's digit histogram in one read of the input keys (LDS per workgroup, then one global
+//                 atomic per digit and workgroup); k_rs_starts turns each pass's histogram into digit starts;
+//   k_rs_onesweep one 256-thread workgroup per 2048-key tile, tiles taken in launch order from a ticket: each wave
+//                 ranks its 8 x 64 keys stably (per item row a match over the digit's 9 bits by ballots, a running
+//                 per-wave digit count in LDS); the tile publishes its per-digit counts, looks back over its
+//                 predecessors' (thread = digit, two digits per thread) until an inclusive prefix, publishes its own;
+//                 the keys and values are laid out in LDS in digit order and written out in that order (runs of one
+//                 digit land on consecutive addresses).
+// 256 threads and 28 KB of LDS, so the sort's workgroups take the CU slots a retiring FASTQ writer frees (the library
+// sort's 1024-thread workgroups waited for whole CUs).  Stable: equal keys keep their input order.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,51 +28,74 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;   // 2048 keys
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_BITS = 7;
+constexpr int RS_BITS = 9;
 constexpr uint32_t RS_BINS = 1u << RS_BITS, RS_MASK = RS_BINS - 1u;
+constexpr int RS_DPT = (int)RS_BINS / RS_THREADS;   // digits per thread (2)
+constexpr int RS_MAXP = 4;                          // passes (u32 keys: at most 4 x 9 bits)
+// look-back status word per (tile, digit): flag in the top two bits, the count (< 2^30) below
+constexpr uint32_t RS_AGG = 0x40000000u, RS_INC = 0x80000000u, RS_VAL = 0x3fffffffu;
 
-__global__ void __launch_bounds__(RS_THREADS) k_rs_count(const uint32_t *keys, int64_t n, int shift,
-                                                        uint32_t *count, int64_t tiles) {
-  __shared__ uint32_t h[RS_BINS];
-  const int tid = threadIdx.x;
-  if (tid < (int)RS_BINS) h[tid] = 0;
+__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint32_t *keys, int64_t n, int passes, uint32_t *ghist) {
+  __shared__ uint32_t h[RS_MAXP * RS_BINS];
+  for (int i = threadIdx.x; i < RS_MAXP * (int)RS_BINS; i += RS_THREADS) h[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
-#pragma unroll
-  for (int k = 0; k < RS_ITEMS; k++) {
-    const int64_t i = base + k * RS_THREADS + tid;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & RS_MASK], 1u);
+  for (int64_t i = (int64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * RS_THREADS) {
+    const uint32_t k = keys[i];
+    for (int p = 0; p < passes; p++) atomicAdd(&h[p * RS_BINS + ((k >> (RS_BITS * p)) & RS_MASK)], 1u);
   }
   __syncthreads();
-  if (tid < (int)RS_BINS) count[(int64_t)tid * tiles + blockIdx.x] = h[tid];
+  for (int i = threadIdx.x; i < passes * (int)RS_BINS; i += RS_THREADS)
+    if (h[i]) atomicAdd(&ghist[i], h[i]);
 }
 
-struct RsLoad {
-  const uint32_t *c;
-  int64_t n;
-  __device__ int64_t operator()(int64_t i) const { return i < n ? (int64_t)c[i] : 0; }
-};
-struct RsStore {
-  uint32_t *o;
-  __device__ void operator()(int64_t i, int64_t, int64_t ex) const { o[i] = (uint32_t)ex; }
-};
+// one workgroup per pass: its histogram -> exclusive digit starts, in place
+__global__ void __launch_bounds__(RS_THREADS) k_rs_starts(uint32_t *ghist) {
+  __shared__ int32_t wsum[RS_WAVES];
+  uint32_t *h = ghist + (size_t)blockIdx.x * RS_BINS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // thread t owns digits RS_DPT t .. RS_DPT t + RS_DPT - 1 (consecutive: the scan runs over the threads)
+  uint32_t v[RS_DPT], s = 0;
+#pragma unroll
+  for (int q = 0; q < RS_DPT; q++) {
+    v[q] = h[RS_DPT * tid + q];
+    s += v[q];
+  }
+  int total;
+  const int32_t incl = wave_sum_incl((int32_t)s, total);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int32_t pre = 0;
+#pragma unroll
+  for (int q = 0; q < RS_WAVES; q++) pre += q < w ? wsum[q] : 0;
+  uint32_t x = (uint32_t)(pre + incl) - s;
+#pragma unroll
+  for (int q = 0; q < RS_DPT; q++) {
+    h[RS_DPT * tid + q] = x;
+    x += v[q];
+  }
+}
 
-// keys_in / vals_in (null: the element index) -> keys_out / vals_out, stable by digit (key >> shift) & RS_MASK
-__global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint32_t *keys_in, const uint32_t *vals_in, int64_t n,
-                                                          int shift, const uint32_t *offs, int64_t tiles,
-                                                          uint32_t *keys_out, uint32_t *vals_out) {
+// keys_in / vals_in (null: the element index) -> keys_out / vals_out, stable by digit (key >> shift) & RS_MASK.
+// gstart: the pass's digit starts; status: [ticket (64 B)] [tiles x RS_BINS words], zeroed before the launch; fault:
+// the look-back scans' host-mapped fault word (a wait that never ends is reported, mh_scan.h).
+__global__ void __launch_bounds__(RS_THREADS) k_rs_onesweep(const uint32_t *keys_in, const uint32_t *vals_in,
+                                                           int64_t n, int shift, const uint32_t *gstart,
+                                                           uint32_t *status, uint32_t *keys_out, uint32_t *vals_out,
+                                                           uint32_t *fault) {
   __shared__ uint32_t wc[RS_WAVES][RS_BINS];   // per wave: running digit counts, then the wave's exclusive prefix
   __shared__ uint32_t ds[RS_BINS];             // the tile's digit starts (exclusive scan over digits)
   __shared__ uint32_t go[RS_BINS];             // the tile's global output offset per digit
   __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
+  __shared__ int32_t wsum[RS_WAVES];
+  __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid < (int)RS_BINS) {
-#pragma unroll
-    for (int q = 0; q < RS_WAVES; q++) wc[q][tid] = 0;
-    go[tid] = offs[(int64_t)tid * tiles + blockIdx.x];
-  }
+  uint32_t *ticket = status;
+  uint32_t *st = status + 16;
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  for (int i = tid; i < RS_WAVES * (int)RS_BINS; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE + (int64_t)w * (64 * RS_ITEMS);
+  const int64_t tile = s_tile;
+  const int64_t base = tile * RS_TILE + (int64_t)w * (64 * RS_ITEMS);
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint32_t key[RS_ITEMS], val[RS_ITEMS], rk[RS_ITEMS];
 #pragma unroll
@@ -101,27 +124,63 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint32_t *keys_
     if (ok && lane == leader) wc[w][d] = c0 + (uint32_t)__popcll(m);
   }
   __syncthreads();
-  // per digit (thread = digit; threads past the bins count 0): the waves' exclusive prefixes and the tile's count,
-  // then the digit starts
-  uint32_t t = 0;
-  if (tid < (int)RS_BINS) {
+  // per digit (thread t: digits RS_DPT t + q): the waves' exclusive prefixes and the tile's count; the count published
+  uint32_t t[RS_DPT], s = 0;
 #pragma unroll
-    for (int q = 0; q < RS_WAVES; q++) {
-      const uint32_t c = wc[q][tid];
-      wc[q][tid] = t;
-      t += c;
+  for (int q = 0; q < RS_DPT; q++) {
+    const int d = RS_DPT * tid + q;
+    uint32_t c = 0;
+#pragma unroll
+    for (int x = 0; x < RS_WAVES; x++) {
+      const uint32_t y = wc[x][d];
+      wc[x][d] = c;
+      c += y;
     }
+    t[q] = c;
+    s += c;
+    __hip_atomic_store(&st[tile * RS_BINS + d], (tile == 0 ? RS_INC : RS_AGG) | c, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
-  {
+  {   // the tile's digit starts: an exclusive scan of the counts over the digits
     int total;
-    const int32_t incl = wave_sum_incl((int32_t)t, total);   // (within the wave)
-    __shared__ int32_t wsum[RS_WAVES];
+    const int32_t incl = wave_sum_incl((int32_t)s, total);
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     int32_t pre = 0;
 #pragma unroll
     for (int q = 0; q < RS_WAVES; q++) pre += q < w ? wsum[q] : 0;
-    if (tid < (int)RS_BINS) ds[tid] = (uint32_t)(pre + incl) - t;
+    uint32_t x = (uint32_t)(pre + incl) - s;
+#pragma unroll
+    for (int q = 0; q < RS_DPT; q++) {
+      ds[RS_DPT * tid + q] = x;
+      x += t[q];
+    }
+  }
+  // look-back per digit: the predecessors' counts until an inclusive prefix
+#pragma unroll
+  for (int q = 0; q < RS_DPT; q++) {
+    const int d = RS_DPT * tid + q;
+    uint32_t pre = 0;
+    if (tile > 0) {
+      int64_t j = tile - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const uint32_t v = __hip_atomic_load(&st[j * RS_BINS + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v & (RS_INC | RS_AGG)) {
+          pre += v & RS_VAL;
+          if (v & RS_INC) break;
+          j--;
+          continue;
+        }
+        if (++spins > (1u << 24)) {   // never published (a broken ticket or status area): report, do not hang
+          if (fault) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(&st[tile * RS_BINS + d], RS_INC | (pre + t[q]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    go[d] = gstart[d] + pre;
   }
   __syncthreads();
 #pragma unroll
@@ -135,7 +194,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint32_t *keys_
     }
   }
   __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t t0 = tile * RS_TILE;
   const int nt = (int)(n - t0 < RS_TILE ? n - t0 : RS_TILE);
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; k++) {
@@ -151,10 +210,10 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_scatter(const uint32_t *keys_
   }
 }
 
-// Scratch for lsd_sort_pairs_iota: two key and value buffers, the counts, their offsets, the scan's scratch.
+// Scratch for lsd_sort_pairs_iota: two key and value buffers, the look-back status words, the histograms.
 inline size_t lsd_sort_tmp_bytes(int64_t n) {
-  const int64_t tiles = (n + RS_TILE - 1) / RS_TILE, nc = RS_BINS * (tiles < 1 ? 1 : tiles);
-  return 2 * 4 * (size_t)n + 2 * 4 * (size_t)nc + scan_lb_scratch_bytes<int64_t>(nc) + 2048;
+  const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
+  return 2 * 4 * (size_t)n + 4 * (size_t)(tiles < 1 ? 1 : tiles) * RS_BINS + 64 + 4 * RS_MAXP * RS_BINS + 2048;
 }
 
 // Stable sort of keys_in[0, n) over bits [0, end_bit), values = the element indices: keys_out / vals_out.  tmp null:
@@ -165,9 +224,9 @@ inline hipError_t lsd_sort_pairs_iota(void *tmp, size_t &tmp_bytes, const uint32
     tmp_bytes = lsd_sort_tmp_bytes(n);
     return hipSuccess;
   }
-  if (tmp_bytes < lsd_sort_tmp_bytes(n) || n < 0 || n >= ((int64_t)1 << 32) - 1) return hipErrorInvalidValue;
+  if (tmp_bytes < lsd_sort_tmp_bytes(n) || n < 0 || n >= ((int64_t)1 << 30)) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
-  const int64_t tiles = (n + RS_TILE - 1) / RS_TILE, nc = RS_BINS * tiles;
+  const int64_t tiles = (n + RS_TILE - 1) / RS_TILE;
   char *p = (char *)tmp;
   auto take = [&](size_t b) {
     char *q = p;
@@ -175,32 +234,25 @@ inline hipError_t lsd_sort_pairs_iota(void *tmp, size_t &tmp_bytes, const uint32
     return q;
   };
   uint32_t *k2 = (uint32_t *)take(4 * (size_t)n), *v2 = (uint32_t *)take(4 * (size_t)n);
-  uint32_t *cnt = (uint32_t *)take(4 * (size_t)nc), *off = (uint32_t *)take(4 * (size_t)nc);
-  void *scr = take(scan_lb_scratch_bytes<int64_t>(nc));
-  int64_t *total = (int64_t *)take(64);
+  const size_t st_bytes = 64 + 4 * (size_t)tiles * RS_BINS;
+  uint32_t *status = (uint32_t *)take(st_bytes);
+  uint32_t *ghist = (uint32_t *)take(4 * RS_MAXP * RS_BINS);
   const int passes = end_bit == 0 ? 1 : (int)((end_bit + RS_BITS - 1) / RS_BITS);
-  // the scan scratch sits inside tmp at an offset that moves with n, so the memory under it holds other sorts' keys:
-  // its look-back state starts fresh here (zeroed by the first pass's scan) and is dropped after the last pass, so
-  // no later scan takes this interior address for zeroed scratch with a running ticket
-  lb_forget(scr);
-  struct Forget {
-    const void *p;
-    ~Forget() { lb_forget(p); }
-  } forget{scr};
+  hipError_t e = hipMemsetAsync(ghist, 0, 4 * (size_t)passes * RS_BINS, st);
+  if (e != hipSuccess) return e;
+  const int64_t hg = tiles < 2048 ? tiles : 2048;
+  hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist);
+  hipLaunchKernelGGL(k_rs_starts, dim3((unsigned)passes), dim3(RS_THREADS), 0, st, ghist);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint32_t *ksrc = keys_in, *vsrc = nullptr;
   for (int ps = 0; ps < passes; ps++) {
     // the last pass writes the outputs; the ones before alternate so that it reads the other buffer
     const bool to_out = ((passes - 1 - ps) & 1) == 0;
     uint32_t *kd = to_out ? keys_out : k2, *vd = to_out ? vals_out : v2;
-    hipLaunchKernelGGL(k_rs_count, dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, ksrc, n, RS_BITS * ps, cnt, tiles);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    e = device_scan_sum<int64_t>(st, nc, RsLoad{cnt, nc}, RsStore{off}, scr, total);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, ksrc, vsrc, n, RS_BITS * ps,
-                       (const uint32_t *)off, tiles, kd, vd);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(status, 0, st_bytes, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rs_onesweep, dim3((unsigned)tiles), dim3(RS_THREADS), 0, st, ksrc, vsrc, n, RS_BITS * ps,
+                       (const uint32_t *)(ghist + (size_t)ps * RS_BINS), status, kd, vd, scan_fault_device());
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     ksrc = kd;
     vsrc = vd;
   }

@@ -218,7 +218,8 @@ def decode(rec):
 def bai(n_ref, recs, vo, vend):
   """BAI bytes for sorted decoded records with virtual offsets vo (and the end offset vend): runs of consecutive
   records in one bin are one chunk, adjacent chunks merge; linear index = first record overlapping each 16 kbp
-  window, empty windows take the next window's value; pseudo-bin 37450; n_no_coor = 0."""
+  window, empty windows take the next window's value; pseudo-bin 37450; n_no_coor = 0.  A valid spec §5.2 index of
+  the file, not claimed byte-identical to htslib's (parity unpinned)."""
   out = b'BAI\1' + struct.pack('<i', n_ref)
   ends = vo[1:] + [vend]
   i = 0

@@ -1,19 +1,16 @@
 #!/bin/bash
-# Submit one gpurun call, re-submitting only while the pool reports no free box / back-off (status=transient with
-# nothing run and nothing charged).  A call that ran on a box (any exit status) is never re-submitted.
-# usage: scripts/gpurun_wait.sh TIMEOUT 'command'
-T=$1
-shift
-for i in $(seq 1 ${MAX_TRIES:-60}); do
-  out=$(timeout $((T + 900)) /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
+# Run one gpurun command, waiting while the pool has no free box or slot (nothing ran, nothing charged: exit 3 or a
+# "transient" status).  A command that ran (any other outcome) is never repeated.
+#   scripts/gpurun_wait.sh LOG TIMEOUT 'command'
+LOG=$1; TO=$2; shift 2
+for i in $(seq 1 40); do
+  /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$LOG" 2>&1
   rc=$?
-  if echo "$out" | grep -q "status=transient rc=None charged=0.0s\|status=transient rc=None charged=Nones"; then
-    echo "[wait] attempt $i: no box ($(echo "$out" | grep -o 'no free box\|backing off\|stopped responding' | head -1)); sleeping" >&2
+  if [ $rc -eq 3 ] || grep -q "status=transient" "$LOG"; then
+    echo "[wait] attempt $i: no box ($(grep -o 'retry in [0-9]*s' "$LOG" | head -1)); sleeping" >> "$LOG.wait"
     sleep 90
     continue
   fi
-  echo "$out" | grep -v "^\[gpurun\] every call"
   exit $rc
 done
-echo "[wait] gave up after ${MAX_TRIES:-60} attempts" >&2
 exit 3

@@ -1,5 +1,6 @@
 """The BAI writer's host half (mh_bgzf.cpp bai_plan / bai_emit: per-record work on threads, then the virtual offsets)
-against the oracle's BAI (oracle/god.py bai, the SAM spec §5.2 layout of god_aligner.py:117-131's pysam.index) on
+against the oracle's BAI (oracle/god.py bai, a restatement of the SAM spec §5.2 index; it is a valid index of the
+same file, not claimed byte-identical to what pysam.index (god_aligner.py:117-131) would write) on
 synthetic sorted records: several references (one empty), runs of one bin cut across the thread pieces, records in
 higher-level bins, windows without records, and record offsets on BGZF block boundaries.  The library's C++ is
 compiled with a small driver (g++, zlib), no GPU."""

@@ -1146,7 +1146,7 @@ def test_god_aligner_spilled_store_vs_oracle(native, model, gpu_bgzf, tmp_path):
   sb = ga.process_multi_threaded(fa, b, fq1, fq2, threads=2, chunk_bytes=65536, gpu_bgzf=gpu_bgzf,
                                  hbm_capacity=150_000)
   assert sa['spill_blocks'] == 0 and sb['spill_blocks'] > 5 and sb['spilled_bytes'] == sb['bam_bytes_uncompressed']
-  assert sb['bam_bytes_uncompressed'] > 10 * 150_000
+  assert sb['bam_bytes_uncompressed'] > 5 * 150_000
   assert open(a, 'rb').read() == open(b, 'rb').read()
   assert open(a + '.bai', 'rb').read() == open(b + '.bai', 'rb').read()
   _god_check(b, b1, b2)
