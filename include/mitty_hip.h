@@ -66,6 +66,11 @@ int32_t mh_sync(mh_ctx *ctx);
  * never publishes; returns MH_E_STATE when the timed-out wait was reported (the expected result), then checks that a
  * correct scan after it succeeds. */
 int32_t mh_selftest_scan_fault(mh_ctx *ctx);
+/* Self-test of the permutation's radix sort (mh_sort.h; the stable (target, step) sort that replaces replaying
+ * illumina.py:70's shuffle): keys[0, n) (host) sorted on the device over bits [0, end_bit); keys_out / vals_out (host,
+ * n each) get the sorted keys and their input indices, equal keys in input order. */
+int32_t mh_selftest_sort(mh_ctx *ctx, const uint32_t *keys, int64_t n, int32_t end_bit, uint32_t *keys_out,
+                         uint32_t *vals_out);
 
 /* ---- host-side helpers that mirror the reference's scalar logic ---------------------------------------- */
 int32_t mh_read_model_params(int64_t mean_rlen, double coverage, double *p, int64_t *passes);

@@ -17,7 +17,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
-           'mh_selftest_scan_fault',
+           'mh_selftest_scan_fault', 'mh_selftest_sort',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim',
@@ -72,6 +72,7 @@ def lib():
   _sig(L, 'mh_last_error', [c_vp], ctypes.c_char_p)
   _sig(L, 'mh_sync', [c_vp])
   _sig(L, 'mh_selftest_scan_fault', [c_vp])
+  _sig(L, 'mh_selftest_sort', [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp])
   _sig(L, 'mh_read_model_params', [c_i64, c_dbl, ctypes.POINTER(c_dbl), P_i64])
   _sig(L, 'mh_work_units', [c_u64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, P_i64])
   _sig(L, 'mh_upload_contig', [c_vp, c_i32, c_vp, c_i64])
@@ -904,6 +905,14 @@ class Context:
 
   def sync(self):
     self._chk(self._L.mh_sync(self._h))
+
+  def selftest_sort(self, keys, end_bit):
+    """mh_selftest_sort: (sorted keys, input indices) of a u32 array by the library's LSD radix sort."""
+    import numpy as np
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    ko, vo = np.empty_like(k), np.empty_like(k)
+    self._chk(self._L.mh_selftest_sort(self._h, k.ctypes.data, k.size, int(end_bit), ko.ctypes.data, vo.ctypes.data))
+    return ko, vo
 
   def selftest_scan_fault(self):
     """(return code, message) of mh_selftest_scan_fault: MH_E_STATE when a timed-out look-back scan is reported."""

@@ -22,6 +22,7 @@
 #include "mh_corrupt.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
+#include "mh_sort.h"
 
 namespace mh {
 namespace jump {
@@ -95,13 +96,43 @@ void *cache_take(size_t bytes, size_t *cap) {
   return nullptr;
 }
 
+// (A/B, round 5: MH_ARENA_GB=N reserves one N GiB block on the first allocation and carves every later request
+// from it, bump-allocated, 2 MiB aligned; such blocks go back to the cache, never to hipFree)
+struct Arena {
+  char *base = nullptr;
+  size_t size = 0, used = 0;
+  bool tried = false;
+};
+Arena g_arena;
+bool in_arena(void *p) {
+  return g_arena.base && (char *)p >= g_arena.base && (char *)p < g_arena.base + g_arena.size;
+}
+void *arena_take(size_t bytes, size_t *cap) {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  if (!g_arena.tried) {
+    g_arena.tried = true;
+    const char *e = getenv("MH_ARENA_GB");
+    const size_t gb = e ? (size_t)atoll(e) : 0;
+    if (gb && hipMalloc((void **)&g_arena.base, gb << 30) == hipSuccess) g_arena.size = gb << 30;
+    else g_arena.base = nullptr;
+    (void)hipGetLastError();
+  }
+  if (!g_arena.base) return nullptr;
+  const size_t c = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+  if (g_arena.used + c > g_arena.size) return nullptr;
+  void *p = g_arena.base + g_arena.used;
+  g_arena.used += c;
+  *cap = c;
+  return p;
+}
+
 int64_t cache_trim(int dev) {   // dev < 0: every device's blocks
   std::vector<std::pair<void *, int>> out;
   int64_t freed = 0;
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (auto it = g_cache.begin(); it != g_cache.end();)
-      if (dev < 0 || it->second.dev == dev) {
+      if ((dev < 0 || it->second.dev == dev) && !in_arena(it->second.p)) {
         out.push_back({it->second.p, it->second.dev});
         freed += (int64_t)it->first;
         it = g_cache.erase(it);
@@ -121,6 +152,7 @@ int64_t cache_trim(int dev) {   // dev < 0: every device's blocks
 
 hipError_t dev_alloc(void **p, size_t bytes, size_t *cap) {
   if ((*p = cache_take(bytes, cap))) return hipSuccess;
+  if ((*p = arena_take(bytes, cap))) return hipSuccess;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) {   // the cache's blocks back to the device, then once more
     (void)hipGetLastError();
@@ -449,6 +481,32 @@ struct StoreCheck {   // element i's exclusive prefix must be i
 // A look-back scan whose tile 0 never runs (device_scan_sum's skip_tile0): every waiting tile times out, the fault
 // word is set, and the synchronisation after it fails with MH_E_STATE — the expected result.  A correct scan after it
 // then succeeds (the word was cleared).
+int32_t mh_selftest_sort(mh_ctx *ctx, const uint32_t *keys, int64_t n, int32_t end_bit, uint32_t *keys_out,
+                         uint32_t *vals_out) {
+  CTX_GUARD(ctx);
+  if (n < 0 || (n > 0 && (!keys || !keys_out || !vals_out)) || end_bit < 0 || end_bit > 32)
+    return arg_fail(ctx, MH_E_ARG, "bad sort arguments");
+  hipStream_t st = ctx->stream;
+  size_t tmp = 0;
+  HIPCHK(ctx, lsd_sort_pairs_iota(nullptr, tmp, nullptr, nullptr, nullptr, n, (unsigned)end_bit, st));
+  DevBuf b;
+  const size_t kb = (4 * (size_t)n + 255) & ~(size_t)255;
+  MH_TRY(ensure(ctx, b, 3 * kb + tmp + 256));
+  uint32_t *dk = (uint32_t *)b.p, *ko = (uint32_t *)((char *)b.p + kb), *vo = (uint32_t *)((char *)b.p + 2 * kb);
+  const int32_t rc = [&]() -> int32_t {
+    if (n) HIPCHK(ctx, hipMemcpyAsync(dk, keys, 4 * (size_t)n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, lsd_sort_pairs_iota((char *)b.p + 3 * kb, tmp, dk, ko, vo, n, (unsigned)end_bit, st));
+    if (n) {
+      HIPCHK(ctx, hipMemcpyAsync(keys_out, ko, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(vals_out, vo, 4 * (size_t)n, hipMemcpyDeviceToHost, st));
+    }
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+    return MH_OK;
+  }();
+  release(b);
+  return rc;
+}
+
 int32_t mh_selftest_scan_fault(mh_ctx *ctx) {
   CTX_GUARD(ctx);
   hipStream_t st = ctx->stream;

@@ -225,7 +225,7 @@ __device__ __forceinline__ int count_N_runs(const int64_t *rs, const int64_t *re
 }
 
 // Number of 'N' in hap[a, b), capped at 3 (the filter only needs > 2).
-__device__ int count_N(const HapView &h, int64_t a, int64_t b) {
+__device__ __forceinline__ int count_N(const HapView &h, int64_t a, int64_t b) {
   if (h.n_runs == 0 || b <= a) return 0;
   int64_t r = upper_bound(h.nre, h.n_runs, a);   // first run with end > a
   int64_t c = 0;
@@ -259,7 +259,11 @@ struct QFixed {
   const char *prefix;   // "@{stub}:"
   const char *mid;      // "|{chrom}|{cpy}"
   int32_t prefix_len, mid_len;
+  uint4 tail;           // "|{rlen}|{rlen}=|": what follows POS in the part of a read inside one '=' node
+  int32_t tail_len;     // (0: no such shortcut, rlen of more than 5 digits)
 };
+
+__device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
@@ -268,7 +272,6 @@ constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: s
 // template (one line-aligned slot), longer parts (a read spanning many variants: ~0.06 % of 2x150 templates at
 // 1.3 variants/kbp) whole in an overflow area, the slot then holding the overflow offset.
 constexpr int ED_SW = 64;
-constexpr int MS_ROW = ED_SW + 4;   // LDS row per thread (an odd number of dwords: lanes' equal columns in distinct banks)
 
 struct Strip {
   char *slot;                 // [m][ED_SW]
@@ -277,7 +280,11 @@ struct Strip {
   unsigned long long *ovf_used;
 };
 
-// Byte sinks of the part formatter: the thread's LDS row (bytes past ED_SW only counted), or global memory.
+// Byte sinks of the part formatter.  RowSink: the thread's LDS row (bytes past ED_SW only counted).  Digits go in
+// as one packed 8-byte store, fixed text as one 16-byte store (unaligned LDS access), so a row keeps ED_RSLACK bytes
+// of slack past ED_SW for stores that start inside it.
+constexpr int ED_RSLACK = 16;
+constexpr int MS_ROW = ED_SW + ED_RSLACK + 4;   // an odd number of dwords: lanes' equal columns in distinct banks
 struct RowSink {
   char *row;
   int32_t o = 0;
@@ -285,41 +292,109 @@ struct RowSink {
     if (o < ED_SW) row[o] = c;
     o++;
   }
+  // x < 10^8 as n decimal digits (leading zeros when n exceeds its length), most significant first
+  __device__ __forceinline__ void digits(uint32_t x, int n) {
+    uint64_t acc = 0;
+    for (int i = 0; i < n; i++) {
+      acc = (acc << 8) | (uint64_t)('0' + x % 10u);
+      x /= 10u;
+    }
+    if (o < ED_SW) __builtin_memcpy(row + o, &acc, 8);
+    o += n;
+  }
   __device__ __forceinline__ void dec(int64_t v) {
     if (v < 0) {
       put('-');
       v = -v;
     }
-    if ((uint64_t)v > 0xffffffffull) {
+    const uint64_t u = (uint64_t)v;
+    if (u < 100000000ull) {
+      digits((uint32_t)u, ndig_u(u));
+    } else if (u < 10000000000000000ull) {
+      const uint64_t h = u / 100000000ull;
+      digits((uint32_t)h, ndig_u(h));
+      digits((uint32_t)(u - h * 100000000ull), 8);
+    } else {
       auto put = [&](uint8_t c) { this->put((char)c); };
-      put_big((uint64_t)v);
-      return;
+      put_big(u);
     }
-    uint32_t x = (uint32_t)v;
-    const int nd = ndig_u(x);
-    for (int i = nd - 1; i >= 0; i--) {
-      if (o + i < ED_SW) row[o + i] = (char)('0' + x % 10u);
-      x /= 10u;
-    }
-    o += nd;
+  }
+  // n <= 16 bytes of fixed text
+  __device__ __forceinline__ void text(const uint4 &t, int n) {
+    if (o < ED_SW) __builtin_memcpy(row + o, &t, 16);
+    o += n;
   }
 };
 struct GlobalSink {
   char *g;
   int32_t o = 0;
   __device__ __forceinline__ void put(char c) { g[o++] = c; }
+  __device__ __forceinline__ void text(const uint4 &t, int n) {
+    for (int i = 0; i < n; i++) g[o++] = (char)(u4get(t, i >> 2) >> (8 * (i & 3)));
+  }
   __device__ __forceinline__ void dec(int64_t v) { o = (int32_t)(put_s(g + o, v) - g); }
 };
 
+// A read's first three nodes, loaded together (clamped to the last node) as soon as its start node is known: the end
+// node and the reads part come from them without a chain of dependent loads (a read spans at most three nodes
+// unless it covers two variants: ~4 % of 2x150 reads at 1.3 variants/kbp, which load the rest).
+struct Nodes3 {
+  Node16 a, b, c;
+  __device__ __forceinline__ Node16 at(const HapView &h, int64_t n0, int64_t j) const {
+    const int64_t d = j - n0;
+    if (d > 2) return h.nd[j];
+    Node16 o;   // (field by field: a select of whole structs would go through scratch memory)
+    o.a = d == 0 ? a.a : d == 1 ? b.a : c.a;
+    o.b = d == 0 ? a.b : d == 1 ? b.b : c.b;
+    return o;
+  }
+};
+__device__ __forceinline__ Nodes3 nodes3(const HapView &h, int64_t n0) {
+  const int64_t last = h.n_nodes - 1;
+  return Nodes3{h.nd[n0], h.nd[n0 + 1 < last ? n0 + 1 : last], h.nd[n0 + 2 < last ? n0 + 2 : last]};
+}
+// c ? x : y field by field (a select of whole structs would put both in scratch memory)
+__device__ __forceinline__ Nodes3 sel3(bool c, const Nodes3 &x, const Nodes3 &y) {
+  Nodes3 o;
+  o.a.a = c ? x.a.a : y.a.a;
+  o.a.b = c ? x.a.b : y.a.b;
+  o.b.a = c ? x.b.a : y.b.a;
+  o.b.b = c ? x.b.b : y.b.b;
+  o.c.a = c ? x.c.a : y.c.a;
+  o.c.b = c ? x.c.b : y.c.b;
+  return o;
+}
+// node_walk from n0 over the preloaded nodes
+__device__ __forceinline__ int64_t node_walk3(const HapView &h, const Nodes3 &q, int64_t n0, int64_t x) {
+  const int64_t last = h.n_nodes - 1;
+  if (n0 + 1 > last || q.b.key() > x) return n0;
+  if (n0 + 2 > last || q.c.key() > x) return n0 + 1;
+  return node_walk(h, n0 + 2, x);
+}
+
+// rpc.get_begin_end_nodes (rpc.py:119-130) with the first three nodes preloaded, then POS / sequence range
+__device__ __forceinline__ void place_read(const HapView &h, int64_t p, int64_t rlen, ReadInfo &r, Nodes3 &q) {
+  r.n0 = node_upper(h, p) - 1;
+  q = nodes3(h, r.n0);
+  r.n1 = node_walk3(h, q, r.n0, p + rlen - 1);
+  read_place(h, q.a, p, rlen, r);
+}
+
 // One read's part: '|' s '|' POS '|' rlen '|' CIGAR '|' v-list (rpc.py:144-160; the special '>p:nI' CIGAR of a read
-// inside an insertion, rpc.py:150-157); nodes n0 (nd0) .. n1.
+// inside an insertion, rpc.py:150-157); nodes n0 .. n1 (the first three preloaded in q).
 template <class Sink>
-__device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
-                                              const ReadInfo &r, int s, int64_t p, int64_t rlen) {
+__device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const Nodes3 q, int64_t n0, int64_t n1,
+                                              const ReadInfo &r, int s, int64_t p, int64_t rlen, const QFixed &qf) {
+  const Node16 nd0 = q.a;
   k.put('|');
   k.put((char)('0' + s));
   k.put('|');
   k.dec(r.pos);
+  // a read inside one '=' node (most of them): CIGAR '{rlen}=', no v-list — the rest is the fixed tail
+  if (qf.tail_len && n0 == n1 && !r.special && nd0.code() == 0 && node_count(nd0, p, rlen) == rlen) {
+    k.text(qf.tail, qf.tail_len);
+    return;
+  }
   k.put('|');
   k.dec(rlen);
   k.put('|');
@@ -331,7 +406,7 @@ __device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const N
     k.put('I');
   } else {
     for (int64_t j = n0; j <= n1; j++) {
-      const Node16 n = j == n0 ? nd0 : h.nd[j];
+      const Node16 n = q.at(h, n0, j);
       k.dec(node_count(n, p, rlen));
       k.put((char)n.op());
     }
@@ -339,7 +414,7 @@ __device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const N
   k.put('|');
   bool first = true;
   for (int64_t j = n0; j <= n1; j++) {
-    const Node16 n = j == n0 ? nd0 : h.nd[j];
+    const Node16 n = q.at(h, n0, j);
     if (n.code() == 0) continue;
     if (!first) k.put(',');
     k.dec(node_v(n));
@@ -370,16 +445,12 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int32_t sk = 0, s1 = 0, s2 = 0;   // this template's share of the tile sums
   if (t < m) {
     ReadInfo r[2];
-    Node16 nn0[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-#pragma unroll
-    for (int s = 0; s < 2; s++) {   // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range
-      r[s].n0 = node_upper(h, p[s]) - 1;
-      r[s].n1 = node_walk(h, r[s].n0, p[s] + rlen - 1);
-      nn0[s] = h.nd[r[s].n0];
-      read_place(h, nn0[s], p[s], rlen, r[s]);
-    }
+    // (two named node sets, not an array: an indexed array of them went to scratch memory)
+    Nodes3 q0, q1;
+    place_read(h, p[0], rlen, r[0], q0);
+    place_read(h, p[1], rlen, r[1], q1);
     int keep;
     if (runs_lds) {
       keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
@@ -394,20 +465,20 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       // (selects, not r[sa]: a dynamically indexed private array would live in scratch memory)
       const int sa = f0 == 0 ? 0 : 1;
       const ReadInfo ra = sa ? r[1] : r[0], rb = sa ? r[0] : r[1];
-      const Node16 na = sa ? nn0[1] : nn0[0], nb = sa ? nn0[0] : nn0[1];
+      const Nodes3 na = sel3(sa, q1, q0), nb = sel3(sa, q0, q1);
       const int64_t pa = sa ? p[1] : p[0], pb = sa ? p[0] : p[1];
       RowSink k{s_row + threadIdx.x * MS_ROW};
-      fmt_read_part(k, h, na, ra.n0, ra.n1, ra, sa, pa, rlen);
+      fmt_read_part(k, h, na, ra.n0, ra.n1, ra, sa, pa, rlen, q);
       const int32_t la = k.o;
-      fmt_read_part(k, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen);
+      fmt_read_part(k, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
       k.put('\n');
       const int32_t rest = k.o - 1;
       if (st.slot && k.o > ED_SW) {   // the whole part in the overflow area; the slot holds its offset
         const unsigned long long at = atomicAdd(st.ovf_used, (unsigned long long)k.o);
         if ((int64_t)(at + k.o) <= st.ovf_cap) {
           GlobalSink g{st.ovf + at};
-          fmt_read_part(g, h, na, ra.n0, ra.n1, ra, sa, pa, rlen);
-          fmt_read_part(g, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen);
+          fmt_read_part(g, h, na, ra.n0, ra.n1, ra, sa, pa, rlen, q);
+          fmt_read_part(g, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
           g.put('\n');
           __builtin_memcpy(s_row + threadIdx.x * MS_ROW, &at, 8);   // (a 4-byte aligned row)
         } else {
@@ -431,8 +502,11 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     recs[t] = out;
   }
   if (st.slot) {
-    // the wave's 64 rows to its 64 consecutive slots: 16-byte chunks, consecutive lanes on consecutive chunks
-    __syncthreads();
+    // the wave's 64 rows to its 64 consecutive slots: 16-byte chunks, consecutive lanes on consecutive chunks (a wave
+    // reads only its own rows: its LDS writes complete, no workgroup barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t tw = (int64_t)blockIdx.x * blockDim.x + 64 * w;
 #pragma unroll
@@ -749,7 +823,6 @@ __device__ __forceinline__ uint32_t lt_mask(int32_t x0, int32_t n) {
   return (uint32_t)((1ull << (8 * k)) - 1ull);
 }
 
-__device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // qname head constants by value (kernel arguments: uniform indexing reads them through the scalar cache)
 struct QHead {
@@ -1905,7 +1978,16 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   int32_t *err = (int32_t *)(small + 36);
   char *d_prefix = small + 256;
   char *d_mid = small + 256 + 4096;
-  QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
+  QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size(), make_uint4(0, 0, 0, 0), 0};
+  {   // the fixed tail of a read inside one '=' node: "|{rlen}|{rlen}=|"
+    const std::string r = std::to_string(rlen), t = "|" + r + "|" + r + "=|";
+    if (t.size() <= 16) {
+      char b[16] = {0};
+      memcpy(b, t.data(), t.size());
+      memcpy(&q.tail, b, 16);
+      q.tail_len = (int32_t)t.size();
+    }
+  }
   HapView hv = view_of(h);
   // the direct writer (corruption too; mh_set_emit_mode(1) forces the LDS-image writer): record offsets from per-tile
   // prefixes; the LDS-image writer reads per-template offsets

@@ -5,14 +5,17 @@
 // the scatter (decoupled look-back per digit), so a pass reads and writes every key and value once:
 //   k_rs_hist     every pass's digit histogram in one read of the input keys (LDS per workgroup, then one global
 //                 atomic per digit and workgroup); k_rs_starts turns each pass's histogram into digit starts;
-//   k_rs_onesweep one 256-thread workgroup per 2048-key tile, tiles taken in launch order from a ticket: each wave
-//                 ranks its 8 x 64 keys stably (per item row a match over the digit's 9 bits by ballots, a running
+//   k_rs_onesweep one 512-thread workgroup per 8192-key tile, tiles taken in launch order from a ticket: each wave
+//                 ranks its 16 x 64 keys stably (per item row a match over the digit's 9 bits by ballots, a running
 //                 per-wave digit count in LDS); the tile publishes its per-digit counts, looks back over its
-//                 predecessors' (thread = digit, two digits per thread) until an inclusive prefix, publishes its own;
-//                 the keys and values are laid out in LDS in digit order and written out in that order (runs of one
-//                 digit land on consecutive addresses).
-// 256 threads and 28 KB of LDS, so the sort's workgroups take the CU slots a retiring FASTQ writer frees (the library
-// sort's 1024-thread workgroups waited for whole CUs).  Stable: equal keys keep their input order.
+//                 predecessors' (thread = digit) until an inclusive prefix, publishes its own; the keys, then the
+//                 values, are laid out in LDS in digit order and written out in that order (runs of one digit land
+//                 on consecutive addresses: 16 keys per digit and tile on average).
+// Round 5 measured the 2048-key tile at ~1 ms per pass of 67 M keys in isolation (~1 TB/s): per key, a quarter of a
+// status word to clear, publish and look back over, and 16-byte runs per digit.  The 8192-key tile quarters both.
+// 512 threads and ~50 KB of LDS (keys and values staged in turn through one buffer): small enough to take the CU
+// slots a retiring FASTQ writer frees (the library sort's 1024-thread workgroups waited for whole CUs).  Stable:
+// equal keys keep their input order.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -24,18 +27,20 @@
 
 namespace mh {
 
-constexpr int RS_THREADS = 256;
-constexpr int RS_ITEMS = 8;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;   // 2048 keys
+constexpr int RS_THREADS = 512;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;   // 8192 keys
 constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_BITS = 9;
 constexpr uint32_t RS_BINS = 1u << RS_BITS, RS_MASK = RS_BINS - 1u;
-constexpr int RS_DPT = (int)RS_BINS / RS_THREADS;   // digits per thread (2)
+constexpr int RS_DPT = (int)RS_BINS / RS_THREADS;   // digits per thread (1)
+static_assert(RS_DPT >= 1 && RS_DPT * RS_THREADS == (int)RS_BINS, "every thread owns whole digits");
 constexpr int RS_MAXP = 4;                          // passes (u32 keys: at most 4 x 9 bits)
 // look-back status word per (tile, digit): flag in the top two bits, the count (< 2^30) below
 constexpr uint32_t RS_AGG = 0x40000000u, RS_INC = 0x80000000u, RS_VAL = 0x3fffffffu;
 
-__global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint32_t *keys, int64_t n, int passes, uint32_t *ghist) {
+static __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint32_t *keys, int64_t n, int passes,
+                                                              uint32_t *ghist) {
   __shared__ uint32_t h[RS_MAXP * RS_BINS];
   for (int i = threadIdx.x; i < RS_MAXP * (int)RS_BINS; i += RS_THREADS) h[i] = 0;
   __syncthreads();
@@ -49,7 +54,7 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_hist(const uint32_t *keys, in
 }
 
 // one workgroup per pass: its histogram -> exclusive digit starts, in place
-__global__ void __launch_bounds__(RS_THREADS) k_rs_starts(uint32_t *ghist) {
+static __global__ void __launch_bounds__(RS_THREADS) k_rs_starts(uint32_t *ghist) {
   __shared__ int32_t wsum[RS_WAVES];
   uint32_t *h = ghist + (size_t)blockIdx.x * RS_BINS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -78,14 +83,14 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_starts(uint32_t *ghist) {
 // keys_in / vals_in (null: the element index) -> keys_out / vals_out, stable by digit (key >> shift) & RS_MASK.
 // gstart: the pass's digit starts; status: [ticket (64 B)] [tiles x RS_BINS words], zeroed before the launch; fault:
 // the look-back scans' host-mapped fault word (a wait that never ends is reported, mh_scan.h).
-__global__ void __launch_bounds__(RS_THREADS) k_rs_onesweep(const uint32_t *keys_in, const uint32_t *vals_in,
-                                                           int64_t n, int shift, const uint32_t *gstart,
-                                                           uint32_t *status, uint32_t *keys_out, uint32_t *vals_out,
-                                                           uint32_t *fault) {
+static __global__ void __launch_bounds__(RS_THREADS) k_rs_onesweep(const uint32_t *keys_in, const uint32_t *vals_in,
+                                                                  int64_t n, int shift, const uint32_t *gstart,
+                                                                  uint32_t *status, uint32_t *keys_out, uint32_t *vals_out,
+                                                                  uint32_t *fault) {
   __shared__ uint32_t wc[RS_WAVES][RS_BINS];   // per wave: running digit counts, then the wave's exclusive prefix
   __shared__ uint32_t ds[RS_BINS];             // the tile's digit starts (exclusive scan over digits)
   __shared__ uint32_t go[RS_BINS];             // the tile's global output offset per digit
-  __shared__ uint32_t sk[RS_TILE], sv[RS_TILE];
+  __shared__ uint32_t sb[RS_TILE];             // keys, then values, in digit order
   __shared__ int32_t wsum[RS_WAVES];
   __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -95,20 +100,17 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_onesweep(const uint32_t *keys
   for (int i = tid; i < RS_WAVES * (int)RS_BINS; i += RS_THREADS) (&wc[0][0])[i] = 0;
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t base = tile * RS_TILE + (int64_t)w * (64 * RS_ITEMS);
+  const int64_t t0 = tile * RS_TILE;
+  const int nt = (int)(n - t0 < RS_TILE ? n - t0 : RS_TILE);   // keys in this tile
+  const int wb = w * (64 * RS_ITEMS) + lane;                      // item k of this lane: tile key wb + 64 k
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint32_t key[RS_ITEMS], val[RS_ITEMS], rk[RS_ITEMS];
+  uint32_t key[RS_ITEMS], rk[RS_ITEMS];   // (the values are loaded when they are laid out: fewer registers)
 #pragma unroll
-  for (int k = 0; k < RS_ITEMS; k++) {   // element order in the wave: item row k, then lane
-    const int64_t i = base + 64 * k + lane;
-    const bool ok = i < n;
-    key[k] = ok ? keys_in[i] : 0xffffffffu;
-    val[k] = ok ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-  }
+  for (int k = 0; k < RS_ITEMS; k++)   // element order in the wave: item row k, then lane
+    key[k] = wb + 64 * k < nt ? keys_in[t0 + wb + 64 * k] : 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; k++) {
-    const int64_t i = base + 64 * k + lane;
-    const bool ok = i < n;
+    const bool ok = wb + 64 * k < nt;
     const uint32_t d = (key[k] >> shift) & RS_MASK;
     uint64_t m = __ballot(ok);   // lanes holding the same digit (invalid lanes match nobody)
 #pragma unroll
@@ -183,31 +185,41 @@ __global__ void __launch_bounds__(RS_THREADS) k_rs_onesweep(const uint32_t *keys
     go[d] = gstart[d] + pre;
   }
   __syncthreads();
+  // each item's place in the tile's digit order (rk becomes it), then the keys through LDS: thread t writes places
+  // t, t + RS_THREADS, ... and keeps each one's output index for the values
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; k++) {
-    const int64_t i = base + 64 * k + lane;
-    if (i < n) {
+    if (wb + 64 * k < nt) {
       const uint32_t d = (key[k] >> shift) & RS_MASK;
-      const uint32_t pos = ds[d] + wc[w][d] + rk[k];
-      sk[pos] = key[k];
-      sv[pos] = val[k];
+      rk[k] = ds[d] + wc[w][d] + rk[k];
+      sb[rk[k]] = key[k];
     }
   }
   __syncthreads();
-  const int64_t t0 = tile * RS_TILE;
-  const int nt = (int)(n - t0 < RS_TILE ? n - t0 : RS_TILE);
+  uint32_t oi[RS_ITEMS];
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; k++) {
     const int p = k * RS_THREADS + tid;
+    oi[k] = 0xffffffffu;
     if (p < nt) {
-      const uint32_t kk = sk[p], d = (kk >> shift) & RS_MASK;
+      const uint32_t kk = sb[p], d = (kk >> shift) & RS_MASK;
       const uint32_t o = go[d] + (uint32_t)p - ds[d];
       if ((int64_t)o < n) {   // (always: a guard against a broken offset table, never a stray write)
         keys_out[o] = kk;
-        vals_out[o] = sv[p];
+        oi[k] = o;
       }
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; k++) {
+    const int li = wb + 64 * k;
+    if (li < nt) sb[rk[k]] = vals_in ? vals_in[t0 + li] : (uint32_t)(t0 + li);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; k++)
+    if (oi[k] != 0xffffffffu) vals_out[oi[k]] = sb[k * RS_THREADS + tid];
 }
 
 // Scratch for lsd_sort_pairs_iota: two key and value buffers, the look-back status words, the histograms.

@@ -11,11 +11,11 @@
 //                                   from the resident contig / alt pool; k_hap_rc the reverse complement;
 //   7. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
 // Node arrays are SoA in HBM: keys (search key, ps+1 for 'D' as rpc.py:127), ps, pr, op, oplen.
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
+#include "mh_sort.h"
 
 namespace mh {
 
@@ -283,8 +283,14 @@ __device__ __forceinline__ uint32_t n_bits4(uint32_t w) {
 }
 // One pass over the haplotype for the run boundaries, 64 positions per thread: boundaries are rare, so each is
 // appended to an unsorted list through an atomic counter (cap entries kept, all counted); sorted afterwards.
-__global__ void __launch_bounds__(256) k_nrun_find(const uint8_t *hap, int64_t len, int64_t cap, int64_t *rs,
-                                                   int64_t *re, unsigned long long *cnt) {
+__global__ void __launch_bounds__(256) k_widen_u32(const uint32_t *a, int64_t n, int64_t *out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = a[i];
+}
+
+// (positions as u32: the caller refuses haplotypes of 2^32 - 1 bases or more)
+__global__ void __launch_bounds__(256) k_nrun_find(const uint8_t *hap, int64_t len, int64_t cap, uint32_t *rs,
+                                                   uint32_t *re, unsigned long long *cnt) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t k0 = c * 64;
   if (k0 > len) return;
@@ -304,12 +310,12 @@ __global__ void __launch_bounds__(256) k_nrun_find(const uint8_t *hap, int64_t l
   uint64_t st = nm & ~sh & pos, en = sh & ~nm & pos;
   while (st) {
     const unsigned long long i = atomicAdd(cnt, 1ull);
-    if ((int64_t)i < cap) rs[i] = k0 + __builtin_ctzll(st);
+    if ((int64_t)i < cap) rs[i] = (uint32_t)(k0 + __builtin_ctzll(st));
     st &= st - 1;
   }
   while (en) {
     const unsigned long long i = atomicAdd(cnt + 1, 1ull);
-    if ((int64_t)i < cap) re[i] = k0 + __builtin_ctzll(en);
+    if ((int64_t)i < cap) re[i] = (uint32_t)(k0 + __builtin_ctzll(en));
     en &= en - 1;
   }
 }
@@ -498,6 +504,10 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
                                             : "SNP/INS alt length inconsistent with its op");
   }
   int64_t p_min = ps0;
+  if (hap_len >= ((int64_t)1 << 32) - 1) {   // (the N-run boundaries are sorted as u32 positions)
+    stage_end(ctx);
+    return arg_fail(ctx, MH_E_ARG, "haplotype of 2^32 - 1 bases or more");
+  }
   MH_TRY(ensure(ctx, h.hap, hap_len + 1024));   // emission gathers whole 16-byte chunks past the last base
   // --- node-search buckets and the AoS node copy (the byte fill below and emission search through them) --------
   {
@@ -542,7 +552,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     unsigned long long hc[2] = {0, 0};
     for (int attempt = 0; attempt < 2; attempt++) {
       MH_TRY(ensure(ctx, b_nrun, 16 * (size_t)cap + 64));
-      int64_t *us = (int64_t *)b_nrun.p, *ue = us + cap;
+      uint32_t *us = (uint32_t *)b_nrun.p, *ue = us + cap;
       HIPCHK(ctx, hipMemsetAsync(cnt, 0, 16, st));
       const int64_t nel = hap_len / 64 + 1;
       hipLaunchKernelGGL(k_nrun_find, dim3(grid_for(nel, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)h.hap.p,
@@ -564,17 +574,23 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     MH_TRY(ensure(ctx, h.nrun_s, 8 * (nr + 1)));
     MH_TRY(ensure(ctx, h.nrun_e, 8 * (nr + 1)));
     if (nr > 0) {
+      // both boundary lists sorted by the library's LSD sort (mh_sort.h; the values, element indices, unused),
+      // then widened to the i64 lists the measure pass searches
       unsigned bits = 1;
-      while (bits < 63 && ((int64_t)1 << bits) <= hap_len) bits++;
-      int64_t *us = (int64_t *)b_nrun.p, *ue = us + cap;
+      while (bits < 32 && ((int64_t)1 << bits) <= hap_len) bits++;
+      const uint32_t *us = (const uint32_t *)b_nrun.p, *ue = us + cap;
       size_t tmp = 0;
-      HIPCHK(ctx, rocprim::radix_sort_keys(nullptr, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p, (size_t)nr, 0u,
-                                           bits, st));
-      MH_TRY(ensure(ctx, b_perm, tmp + 256));
-      HIPCHK(ctx, rocprim::radix_sort_keys(b_perm.p, tmp, (const uint64_t *)us, (uint64_t *)h.nrun_s.p,
-                                           (size_t)nr, 0u, bits, st));
-      HIPCHK(ctx, rocprim::radix_sort_keys(b_perm.p, tmp, (const uint64_t *)ue, (uint64_t *)h.nrun_e.p,
-                                           (size_t)nr, 0u, bits, st));
+      HIPCHK(ctx, lsd_sort_pairs_iota(nullptr, tmp, us, nullptr, nullptr, nr, bits, st));
+      const size_t kb = (8 * (size_t)nr + 255) & ~(size_t)255;
+      MH_TRY(ensure(ctx, b_perm, tmp + 2 * kb + 256));
+      uint32_t *sk = (uint32_t *)b_perm.p, *sv = (uint32_t *)((char *)b_perm.p + kb);
+      void *stmp = (char *)b_perm.p + 2 * kb;
+      for (int e = 0; e < 2; e++) {
+        HIPCHK(ctx, lsd_sort_pairs_iota(stmp, tmp, e ? ue : us, sk, sv, nr, bits, st));
+        hipLaunchKernelGGL(k_widen_u32, dim3(grid_for(nr, 256, 65535)), dim3(256), 0, st, (const uint32_t *)sk, nr,
+                           (int64_t *)(e ? h.nrun_e.p : h.nrun_s.p));
+        HIPCHK(ctx, hipGetLastError());
+      }
     }
   }
   stage_end(ctx);
