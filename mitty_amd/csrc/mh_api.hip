@@ -388,8 +388,6 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->max_cu = prop.multiProcessorCount;
-  const char *so = getenv("MH_SORT");   // (A/B: MH_SORT=rocprim, the library's onesweep sort)
-  ctx->sort_lsd = !(so && !strcmp(so, "rocprim"));
   *out = ctx;
   return MH_OK;
 }

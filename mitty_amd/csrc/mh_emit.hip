@@ -281,9 +281,9 @@ struct Strip {
 };
 
 // Byte sinks of the part formatter.  RowSink: the thread's LDS row (bytes past ED_SW only counted).  Digits go in
-// as one packed 8-byte store, fixed text as one 16-byte store (unaligned LDS access), so a row keeps ED_RSLACK bytes
-// of slack past ED_SW for stores that start inside it.
-constexpr int ED_RSLACK = 16;
+// as one packed 8-byte store, fixed text as 8-byte stores (unaligned LDS access), so a row keeps ED_RSLACK bytes of
+// slack past ED_SW for stores that start inside it.
+constexpr int ED_RSLACK = 8;
 constexpr int MS_ROW = ED_SW + ED_RSLACK + 4;   // an odd number of dwords: lanes' equal columns in distinct banks
 struct RowSink {
   char *row;
@@ -321,7 +321,9 @@ struct RowSink {
   }
   // n <= 16 bytes of fixed text
   __device__ __forceinline__ void text(const uint4 &t, int n) {
-    if (o < ED_SW) __builtin_memcpy(row + o, &t, 16);
+    const uint64_t a = t.x | ((uint64_t)t.y << 32), b = t.z | ((uint64_t)t.w << 32);
+    if (o < ED_SW) __builtin_memcpy(row + o, &a, 8);
+    if (o + 8 < ED_SW && n > 8) __builtin_memcpy(row + o + 8, &b, 8);
     o += n;
   }
 };
@@ -352,17 +354,6 @@ struct Nodes3 {
 __device__ __forceinline__ Nodes3 nodes3(const HapView &h, int64_t n0) {
   const int64_t last = h.n_nodes - 1;
   return Nodes3{h.nd[n0], h.nd[n0 + 1 < last ? n0 + 1 : last], h.nd[n0 + 2 < last ? n0 + 2 : last]};
-}
-// c ? x : y field by field (a select of whole structs would put both in scratch memory)
-__device__ __forceinline__ Nodes3 sel3(bool c, const Nodes3 &x, const Nodes3 &y) {
-  Nodes3 o;
-  o.a.a = c ? x.a.a : y.a.a;
-  o.a.b = c ? x.a.b : y.a.b;
-  o.b.a = c ? x.b.a : y.b.a;
-  o.b.b = c ? x.b.b : y.b.b;
-  o.c.a = c ? x.c.a : y.c.a;
-  o.c.b = c ? x.c.b : y.c.b;
-  return o;
 }
 // node_walk from n0 over the preloaded nodes
 __device__ __forceinline__ int64_t node_walk3(const HapView &h, const Nodes3 &q, int64_t n0, int64_t x) {
@@ -444,41 +435,50 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int32_t nbytes = 0;
   int32_t sk = 0, s1 = 0, s2 = 0;   // this template's share of the tile sums
   if (t < m) {
-    ReadInfo r[2];
-    const int64_t p[2] = {pos0[t], pos1[t]};
+    const int64_t p0 = pos0[t], p1 = pos1[t];
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-    // (two named node sets, not an array: an indexed array of them went to scratch memory)
-    Nodes3 q0, q1;
-    place_read(h, p[0], rlen, r[0], q0);
-    place_read(h, p[1], rlen, r[1], q1);
-    int keep;
-    if (runs_lds) {
-      keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
-             count_N_runs(s_rs, s_re, h.n_runs, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
-    } else {
-      keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
-             count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    // the reads part in file order (reads[fo] = mate 0, readgenerate.py:207): mate sa's part first.  One read at a
+    // time — its start/end nodes, POS, N count, and its part formatted into this thread's LDS row — so only one read's
+    // nodes are live (fewer registers, more waves: the pass waits on its random node loads).  A template the N filter
+    // drops is formatted too and ignored.
+    const int sa = f0 == 0 ? 0 : 1;
+    const int64_t pa = sa ? p1 : p0, pb = sa ? p0 : p1;
+    RowSink k{s_row + threadIdx.x * MS_ROW};
+    ReadInfo ra, rb;
+    int nna, nnb;
+    {
+      Nodes3 qa;
+      place_read(h, pa, rlen, ra, qa);
+      nna = runs_lds ? count_N_runs(s_rs, s_re, h.n_runs, ra.hap_a, ra.hap_a + ra.seq_len)
+                     : count_N(h, ra.hap_a, ra.hap_a + ra.seq_len);
+      fmt_read_part(k, h, qa, ra.n0, ra.n1, ra, sa, pa, rlen, q);
     }
-    Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
+    const int32_t la = k.o;
+    {
+      Nodes3 qb;
+      place_read(h, pb, rlen, rb, qb);
+      nnb = runs_lds ? count_N_runs(s_rs, s_re, h.n_runs, rb.hap_a, rb.hap_a + rb.seq_len)
+                     : count_N(h, rb.hap_a, rb.hap_a + rb.seq_len);
+      fmt_read_part(k, h, qb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
+    }
+    k.put('\n');
+    const int keep = nna <= 2 && nnb <= 2;
+    // mate-indexed (selects, not an indexed array: a dynamically indexed private array would live in scratch memory)
+    const int32_t n0m0 = (int32_t)(sa ? rb.n0 : ra.n0), n0m1 = (int32_t)(sa ? ra.n0 : rb.n0);
+    const int32_t n1m0 = (int32_t)(sa ? rb.n1 : ra.n1), n1m1 = (int32_t)(sa ? ra.n1 : rb.n1);
+    Rec out{0, 0, 0, 0, {n0m0, n0m1}, {n1m0, n1m1}};
     if (keep) {
-      // the reads part in file order (reads[fo] = mate 0, readgenerate.py:207), formatted into this thread's row
-      // (selects, not r[sa]: a dynamically indexed private array would live in scratch memory)
-      const int sa = f0 == 0 ? 0 : 1;
-      const ReadInfo ra = sa ? r[1] : r[0], rb = sa ? r[0] : r[1];
-      const Nodes3 na = sel3(sa, q1, q0), nb = sel3(sa, q0, q1);
-      const int64_t pa = sa ? p[1] : p[0], pb = sa ? p[0] : p[1];
-      RowSink k{s_row + threadIdx.x * MS_ROW};
-      fmt_read_part(k, h, na, ra.n0, ra.n1, ra, sa, pa, rlen, q);
-      const int32_t la = k.o;
-      fmt_read_part(k, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
-      k.put('\n');
       const int32_t rest = k.o - 1;
       if (st.slot && k.o > ED_SW) {   // the whole part in the overflow area; the slot holds its offset
         const unsigned long long at = atomicAdd(st.ovf_used, (unsigned long long)k.o);
         if ((int64_t)(at + k.o) <= st.ovf_cap) {
           GlobalSink g{st.ovf + at};
-          fmt_read_part(g, h, na, ra.n0, ra.n1, ra, sa, pa, rlen, q);
-          fmt_read_part(g, h, nb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
+          Nodes3 qx;
+          ReadInfo rx;
+          place_read(h, pa, rlen, rx, qx);
+          fmt_read_part(g, h, qx, rx.n0, rx.n1, rx, sa, pa, rlen, q);
+          place_read(h, pb, rlen, rx, qx);
+          fmt_read_part(g, h, qx, rx.n0, rx.n1, rx, 1 - sa, pb, rlen, q);
           g.put('\n');
           __builtin_memcpy(s_row + threadIdx.x * MS_ROW, &at, 8);   // (a 4-byte aligned row)
         } else {
@@ -486,8 +486,7 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
         }
       }
       const int32_t ql = q.prefix_len + q.mid_len + rest;
-      const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
-      const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
+      const int32_t s_f1 = ra.seq_len, s_f2 = rb.seq_len;   // file 1 holds mate sa
       const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
       out.keep = 1 | (la << 1);   // kept; the first read's part length (where the second starts)
       out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
@@ -1929,11 +1928,6 @@ constexpr int32_t ED_QPAD = 4;
 // two files
 using EwKernel = void (*)(TArgs, QHead);
 static EwKernel ew_kernel(int cr, bool two) {
-  static const bool gw4 = getenv("MH_EW_GW4") != nullptr;   // (A/B: every wave gathers)
-  if (gw4)
-    return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 4> : k_emit_tiles<1, 8, 2, 4>)
-           : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 4> : k_emit_tiles<1, 8, 1, 4>)
-                     : (two ? k_emit_tiles<2, 4, 0, 4> : k_emit_tiles<1, 8, 0, 4>);
   return cr == 2 ? (two ? k_emit_tiles<2, 4, 2, 3> : k_emit_tiles<1, 8, 2, 3>)
          : cr == 1 ? (two ? k_emit_tiles<2, 4, 1, 3> : k_emit_tiles<1, 8, 1, 3>)
                    : (two ? k_emit_tiles<2, 4, 0, 3> : k_emit_tiles<1, 8, 0, 3>);

@@ -253,9 +253,6 @@ struct mh_ctx {
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
-  // MH_SORT=lsd (the hand-written permutation sort instead of rocprim's, measured slower: DESIGN.md), read once per
-  // context (mh_create), so tests switch it per context
-  bool sort_lsd = false;
   bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
 
   // FASTQ arenas

@@ -16,8 +16,7 @@
 //                     and the unit is redone with those draws recomputed by the host libm
 //   k_perm_*          the permutation the swaps produce, without replaying them: steps radix-sorted by target,
 //                     then a chase per step (see k_perm_heads)
-//   tlen scan         one look-back scan: tl = searchsorted(cum_tlen, U) clipped to rlen, keep te < p_max, and the
-//                     kept templates compacted
+//   k_tlen + scan     tl = searchsorted(cum_tlen (LDS), U) clipped to rlen; keep te < p_max; compaction
 //   file order        fo0[k] = byte (k & 3) of word k >> 2, & 1 (randint(2, dtype=int8) buffering), written
 //                     by the compaction's store
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
@@ -33,8 +32,6 @@
 #include "mh_scan.h"
 #include "mh_sort.h"
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 namespace mh {
 
@@ -843,81 +840,45 @@ struct StoreTs {
 };
 
 // ---- template length, compaction, file order ----------------------------------------------------------------
-// One look-back scan: its load draws the template length (tl = searchsorted(cum_tlen, U, 'left') clipped to rlen,
-// illumina.py:72-77) and keeps te = ts + tl < p_max; its store places the kept template (positions and file-order
-// bit) at its exclusive prefix, with ts / te carried in registers.  The search starts from a guide (the first index
-// whose cum >= g / TL_GUIDE for U's bucket g) and steps forward: the same index as the binary search, ~1-2 loads.
-constexpr int TL_GUIDE = 4096;
-constexpr int TL_LDS = 2048;   // tables of up to this many entries are staged in LDS (the read models have 1000)
-struct TlenCarry {
-  int64_t ts, te;
-};
-__device__ __forceinline__ double *tl_cum_lds() {
-  __shared__ double t[TL_LDS];
-  return t;
-}
-__device__ __forceinline__ uint16_t *tl_guide_lds() {
-  __shared__ uint16_t g[TL_GUIDE];
-  return g;
-}
-struct LoadTlen {
-  const uint32_t *w;
-  const double *cum;
-  const int32_t *guide;
-  int32_t n_tlen;
-  int64_t rlen, p_max;
-  const int64_t *ts;
-  using Carry = TlenCarry;
-  __device__ void prepare() const {
-    if (n_tlen > TL_LDS) return;
-    double *c = tl_cum_lds();
-    uint16_t *g = tl_guide_lds();
-    for (int i = threadIdx.x; i < n_tlen; i += blockDim.x) c[i] = cum[i];
-    for (int i = threadIdx.x; i < TL_GUIDE; i += blockDim.x) g[i] = (uint16_t)guide[i];
-  }
-  __device__ int64_t operator()(int64_t k, TlenCarry &c) const {
+constexpr int TLEN_PER = 8;
+__global__ void __launch_bounds__(256) k_tlen(int64_t n, const uint32_t *w, const double *cum_tlen, int32_t n_tlen,
+                                              int64_t rlen, int64_t p_max, const int64_t *ts, int64_t *te,
+                                              uint8_t *keep) {
+  extern __shared__ __attribute__((aligned(16))) double s_cum[];
+  for (int i = threadIdx.x; i < n_tlen; i += blockDim.x) s_cum[i] = cum_tlen[i];
+  __syncthreads();
+  // TLEN_PER draws per thread (lane-strided): the table is staged once per TLEN_PER * 256 draws
+  for (int q = 0; q < TLEN_PER; q++) {
+    const int64_t k = ((int64_t)blockIdx.x * TLEN_PER + q) * blockDim.x + threadIdx.x;
+    if (k >= n) return;
     const double u = mt_double(w, k);
-    const int b = (int)(u * TL_GUIDE);
-    int32_t lo;
-    if (n_tlen <= TL_LDS) {
-      const double *cl = tl_cum_lds();
-      lo = tl_guide_lds()[b];
-      while (lo < n_tlen && cl[lo] < u) lo++;
-    } else {
-      lo = guide[b];
-      while (lo < n_tlen && cum[lo] < u) lo++;
+    int32_t lo = 0, hi = n_tlen;                        // searchsorted(side='left')
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (s_cum[mid] < u) lo = mid + 1; else hi = mid;
     }
-    c.ts = ts[k];
-    c.te = c.ts + (lo < rlen ? rlen : (int64_t)lo);   // tl.clip(rlen)
-    return c.te < p_max;
+    const int64_t tl = lo < rlen ? rlen : lo;           // tl.clip(rlen)
+    const int64_t e = ts[k] + tl;
+    te[k] = e;
+    keep[k] = e < p_max;
   }
+}
+struct LoadKeep {
+  const uint8_t *keep;
+  __device__ int64_t operator()(int64_t k) const { return keep[k]; }
 };
 // the kept template's place excl: its positions, and its file-order bit (fo0[k] = byte (k & 3) of word k >> 2, & 1:
 // randint(2, dtype=int8) buffering, illumina.py:80 — the k-th kept template takes the k-th draw)
 struct StoreCompact {
-  int64_t *pos0, *pos1;
-  int64_t rlen;
-  const uint32_t *wfo;
-  int8_t *fo0;
-  __device__ void operator()(int64_t, int64_t incl, int64_t excl, const TlenCarry &c) const {
-    if (incl == excl) return;   // not kept
-    pos0[excl] = c.ts;
-    pos1[excl] = c.te - rlen;
+  const uint8_t *keep; const int64_t *ts, *te; int64_t *pos0, *pos1; int64_t rlen;
+  const uint32_t *wfo; int8_t *fo0;
+  __device__ void operator()(int64_t k, int64_t, int64_t excl) const {
+    if (!keep[k]) return;
+    pos0[excl] = ts[k];
+    pos1[excl] = te[k] - rlen;
     fo0[excl] = (int8_t)((wfo[excl >> 2] >> (8 * (excl & 3))) & 1u);
   }
 };
-// host: cum_tlen followed by its guide (int32 [TL_GUIDE]), the layout LoadTlen reads
-inline void tlen_table(const double *cum, int32_t n_tlen, std::vector<char> &out) {
-  out.resize(8 * (size_t)n_tlen + 4 * (size_t)TL_GUIDE);
-  memcpy(out.data(), cum, 8 * (size_t)n_tlen);
-  int32_t *g = (int32_t *)(out.data() + 8 * (size_t)n_tlen);
-  int32_t i = 0;
-  for (int b = 0; b < TL_GUIDE; b++) {
-    const double x = (double)b / TL_GUIDE;
-    while (i < n_tlen && cum[i] < x) i++;
-    g[b] = i;
-  }
-}
 
 // ---- Philox4x32-10 fast mode ------------------------------------------------------------------------------
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
@@ -1236,19 +1197,12 @@ int32_t decode_parallel(mh_ctx *ctx, const std::vector<DecJob> &dec, int64_t *d_
 // bp (the batch-wide permutation): phase 1 writes the unit's ts into bp_ts + j_off, phase 2 takes its shuffled ts
 // from bp_tsh + j_off; the unit's own sort and chase are skipped
 // The permutation's (target, step) sort: the hand-written LSD radix sort of mh_sort.h (9-bit digits with the tile
-// counts folded into the scatter: a 64 M-draw batch's 27-bit keys in 3 passes, 256-thread workgroups sized to fit
-// beside the FASTQ writers).  MH_SORT=rocprim: rocprim's onesweep (1024-thread workgroups, which wait for whole CUs
-// beside the writers), kept for the A/B.
-using SortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 9,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+// counts folded into the scatter: a 64 M-draw batch's 27-bit keys in 3 passes, 512-thread workgroups that fit beside
+// the FASTQ writers; round 5's A/B against rocprim's onesweep: within noise).
 template <class KIn>
-static hipError_t perm_sort(bool lsd, void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out,
-                            uint32_t *vals_out, size_t n, unsigned end_bit, hipStream_t st) {
-  if (lsd) return lsd_sort_pairs_iota(tmp, tmp_bytes, keys_in, keys_out, vals_out, (int64_t)n, end_bit, st);
-  const rocprim::counting_iterator<uint32_t> iota(0u);
-  return rocprim::radix_sort_pairs<SortCfg>(tmp, tmp_bytes, keys_in, keys_out, iota, vals_out, n, 0u, end_bit, st);
+static hipError_t perm_sort(void *tmp, size_t &tmp_bytes, KIn keys_in, uint32_t *keys_out, uint32_t *vals_out,
+                            size_t n, unsigned end_bit, hipStream_t st) {
+  return lsd_sort_pairs_iota(tmp, tmp_bytes, keys_in, keys_out, vals_out, (int64_t)n, end_bit, st);
 }
 
 struct BatchPerm {
@@ -1270,10 +1224,11 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   const int64_t n = u.n;
   const uint32_t *w_tloc = words + u.w_tloc, *w_tlen = words + u.w_tlen, *w_fo = words + u.w_fo;
   int64_t *ts = bp ? bp->ts + u.j_off : (int64_t *)S4[0].p;
-  int64_t *ts_shuf = (int64_t *)S4[1].p;
+  int64_t *ts_shuf = (int64_t *)S4[1].p, *te = (int64_t *)S4[2].p;
   uint32_t *sk = (uint32_t *)S4[4].p, *sv = (uint32_t *)S4[5].p;
   int32_t *nxt = (int32_t *)S4[6].p;
   const bool permute = rng_mode == MH_RNG_MITTY && n > 1 && !bp;
+  uint8_t *keep = (uint8_t *)S4[3].p;
   int64_t *flag_idx = (int64_t *)ctx->s[11].p;
   int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 128 + 64 * lane);
   const double log_q = std::log(1.0 - p);
@@ -1313,9 +1268,9 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       unsigned end_bit = 1;
       while (end_bit < 32 && ((int64_t)1 << end_bit) < n) end_bit++;
       size_t tmp = 0;
-      HIPCHK(ctx, perm_sort(ctx->sort_lsd, nullptr, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
+      HIPCHK(ctx, perm_sort(nullptr, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       MH_TRY(ensure(ctx, perm_tmp, tmp + 256));
-      HIPCHK(ctx, perm_sort(ctx->sort_lsd, perm_tmp.p, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
+      HIPCHK(ctx, perm_sort(perm_tmp.p, tmp, jarr, sk, sv, (size_t)n, end_bit, st));
       HIPCHK(ctx, hipMemsetAsync(nxt, 0xff, 4 * (size_t)n, st));
       hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, (const uint32_t *)sk,
                          (const uint32_t *)sv, nxt);
@@ -1336,11 +1291,14 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   }
 
   stage_begin(ctx, "sample_tlen_compact");
-  HIPCHK(ctx, device_scan_sum<int64_t>(st, n,
-                                       LoadTlen{w_tlen, d_cum, (const int32_t *)(d_cum + n_tlen), n_tlen,
-                                                (int64_t)rlen, u.p_max, ts_use},
-                                       StoreCompact{(int64_t *)u.out->pos0.p, (int64_t *)u.out->pos1.p,
-                                                    (int64_t)rlen, w_fo, (int8_t *)u.out->fo0.p},
+  hipLaunchKernelGGL(k_tlen, dim3(grid_for((n + TLEN_PER - 1) / TLEN_PER, 256, INT32_MAX)), dim3(256), 8 * n_tlen, st,
+                     n, w_tlen, d_cum, n_tlen,
+                     (int64_t)rlen, u.p_max, ts_use, te, keep);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
+                                       StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p,
+                                                    (int64_t *)u.out->pos1.p, (int64_t)rlen, w_fo,
+                                                    (int8_t *)u.out->fo0.p},
                                        scan_partials, d_m));
   stage_end(ctx);
   return MH_OK;
@@ -1427,6 +1385,8 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   MH_TRY(ensure(ctx, ctx->s[3], 4 * (size_t)j_total + 64));
   MH_TRY(ensure(ctx, ctx->s[4], 8 * nn));
   MH_TRY(ensure(ctx, ctx->s[5], 8 * nn));
+  MH_TRY(ensure(ctx, ctx->s[6], 8 * nn));
+  MH_TRY(ensure(ctx, ctx->s[7], nn));
   MH_TRY(ensure(ctx, ctx->s[8], 4 * (nn + 1)));
   MH_TRY(ensure(ctx, ctx->s[9], 4 * (nn + 1)));
   MH_TRY(ensure(ctx, ctx->s[10], 4 * nn));
@@ -1449,13 +1409,15 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     mh::DevBuf *L = l == 1 ? ctx->lane2 : ctx->xlane[l - 2];
     MH_TRY(ensure(ctx, L[0], 8 * nn));
     MH_TRY(ensure(ctx, L[1], 8 * nn));
+    MH_TRY(ensure(ctx, L[2], 8 * nn));
+    MH_TRY(ensure(ctx, L[3], nn));
     MH_TRY(ensure(ctx, L[4], 4 * (nn + 1)));
     MH_TRY(ensure(ctx, L[5], 4 * (nn + 1)));
     MH_TRY(ensure(ctx, L[6], 4 * nn));
     MH_TRY(ensure(ctx, l == 1 ? ctx->scan_partials2 : ctx->xscan[l - 2],
                   std::max<size_t>(16 * scan_partials_count(nn + 1) + 64, scan_lb_scratch_bytes<int64_t>(nn + 1))));
   }
-  MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 4 * (size_t)TL_GUIDE + 64));
+  MH_TRY(ensure(ctx, ctx->s[13], 8 * (size_t)n_tlen + 64));
   MH_TRY(ensure(ctx, ctx->s[1], 64 * (size_t)n_units + 64));          // per-unit m, flags, decode status
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   MH_TRY(ensure(ctx, ctx->scan_partials, std::max<size_t>(16 * scan_partials_count(nn + 1) + 64,
@@ -1466,9 +1428,7 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   int64_t *d_status = d_m + n_units;                                    // [n_units]
   uint32_t *d_flags = (uint32_t *)(d_status + n_units);                 // [n_units]
   HIPCHK(ctx, hipMemsetAsync(ctx->s[1].p, 0, 64 * (size_t)n_units + 64, st));
-  std::vector<char> tl_tab;
-  tlen_table(cum_tlen, n_tlen, tl_tab);
-  HIPCHK(ctx, hipMemcpyAsync(d_cum, tl_tab.data(), tl_tab.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_cum, cum_tlen, 8 * n_tlen, hipMemcpyHostToDevice, st));
 
   stage_begin(ctx, "sample");
   // ---- word streams ------------------------------------------------------------------------------------------
@@ -1584,9 +1544,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     unsigned end_bit = 1;
     while (end_bit < 32 && ((int64_t)1 << end_bit) < j_total) end_bit++;
     size_t tmp = 0;
-    HIPCHK(ctx, perm_sort(ctx->sort_lsd, nullptr, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
+    HIPCHK(ctx, perm_sort(nullptr, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     MH_TRY(ensure(ctx, ctx->pb_tmp, tmp + 256));
-    HIPCHK(ctx, perm_sort(ctx->sort_lsd, ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
+    HIPCHK(ctx, perm_sort(ctx->pb_tmp.p, tmp, gk, sk, sv, (size_t)j_total, end_bit, st));
     hipLaunchKernelGGL(k_perm_heads, dim3(grid_for(j_total, 256, INT32_MAX)), dim3(256), 0, st, j_total,
                        (const uint32_t *)sk, (const uint32_t *)sv, nxt);
     HIPCHK(ctx, hipGetLastError());

@@ -10,7 +10,6 @@
 
 #include <cstdint>
 #include <mutex>
-#include <type_traits>
 #include <unordered_map>
 
 namespace mh {
@@ -262,34 +261,6 @@ inline uint32_t scan_fault_take() {
   return v;
 }
 
-// A Load with a member type Carry hands per-element state to its Store (load(i, carry), store(i, incl, excl, carry)),
-// held in registers between the two: what the load computed is not recomputed or round-tripped through HBM.
-struct NoCarry {};
-template <class L, class = void>
-struct carry_of {
-  using type = NoCarry;
-};
-template <class L>
-struct carry_of<L, std::void_t<typename L::Carry>> {
-  using type = typename L::Carry;
-};
-// A Load with prepare() stages what it reads (tables into LDS) before the first load; the kernel then synchronises.
-template <class L, class = void>
-struct has_prepare : std::false_type {};
-template <class L>
-struct has_prepare<L, std::void_t<decltype(std::declval<const L &>().prepare())>> : std::true_type {};
-
-template <typename T, typename Load, typename C>
-__device__ __forceinline__ T load_c(const Load &load, int64_t i, C &c) {
-  if constexpr (std::is_same_v<C, NoCarry>) return load(i);
-  else return load(i, c);
-}
-template <typename T, typename Store, typename C>
-__device__ __forceinline__ void store_c(const Store &store, int64_t i, const T &incl, const T &ex, const C &c) {
-  if constexpr (std::is_same_v<C, NoCarry>) store(i, incl, ex);
-  else store(i, incl, ex, c);
-}
-
 template <typename T, typename Load, typename Store>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, Store store, uint64_t *scratch,
                                                          int64_t nt, T *total, uint32_t ticket_base, uint32_t epoch,
@@ -303,21 +274,18 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
   uint64_t *agg = scratch + 8, *inc = agg + (size_t)K * nt;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_tile = (int64_t)(uint32_t)(atomicAdd(ticket, 1u) - ticket_base);
-  if constexpr (has_prepare<Load>::value) load.prepare();
   __syncthreads();
   const int64_t tile = s_tile;
   // wave w owns elements [tile * LB_TILE + w * 64 * LB_ITEMS, +64 * LB_ITEMS): item k of lane l is element
   // w * 64 * LB_ITEMS + 64 k + l (coalesced loads and stores), scanned with one wave scan per item
   const int64_t base = tile * LB_TILE + (int64_t)wave * 64 * LB_ITEMS + lane;
-  using C = typename carry_of<Load>::type;
   T v[LB_ITEMS];
-  C cr[LB_ITEMS];
   T carry{};
   // every item loaded before any is scanned: the loads' latencies overlap instead of alternating with the shuffles
 #pragma unroll
   for (int k = 0; k < LB_ITEMS; k++) {
     const int64_t i = base + 64 * k;
-    v[k] = i < n ? load_c<T>(load, i, cr[k]) : T{};
+    v[k] = i < n ? load(i) : T{};
   }
 #pragma unroll
   for (int k = 0; k < LB_ITEMS; k++) {
@@ -398,7 +366,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lb(int64_t n, Load load, 
     T ex = shfl_up_t(incl, 1);
     if (lane == 0) ex = prev;
     prev = shfl_idx_t(incl, 63);
-    if (i < n) store_c<T>(store, i, incl, ex, cr[k]);
+    if (i < n) store(i, incl, ex);
   }
   if (tile == nt - 1 && tid == SCAN_THREADS - 1) *total = off + v[LB_ITEMS - 1];
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment variants on one bench line, alternating REPS times in one call.
-# usage (inside gpurun): TAG=name REPS=2 BENCH_ARGS="--steps 8 --warmup 2" scripts/gpu_ab.sh 'base:' 'lsd:MH_SORT=lsd' ...
+# usage (inside gpurun): TAG=name REPS=2 BENCH_ARGS="--steps 8 --warmup 2" scripts/gpu_ab.sh 'base:' 'x:MH_LIB=path/to/other/libmitty_hip.so' ...
 # Each argument is label:ENV=V ENV2=V2 (env may be empty), optionally followed by ' -- ' and extra bench arguments.  Prints value, ms/step and writer ms per run; JSON lines in
 # gpurun_out/ab_$TAG/.
 set -o pipefail

@@ -353,12 +353,10 @@ def test_unit_vs_oracle_nine_digit_positions(native, emit_mode):
                          emit_mode=emit_mode) > 10000
 
 
-@pytest.mark.parametrize('sort', ['rocprim', 'lsd'])
-def test_batched_units_vs_oracle(native, monkeypatch, sort):
-  """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes), emitted in the
-  reference's unit order: the arena equals the oracle's per-unit FASTQ concatenated.  The permutation's sort by
-  rocprim's onesweep and by the hand-written LSD radix sort (MH_SORT=lsd, mh_sort.h)."""
-  monkeypatch.setenv('MH_SORT', sort)
+def test_batched_units_vs_oracle(native):
+  """Several units sampled in one batch (jump-ahead segments for every stream, concurrent decodes, the batch-wide
+  permutation sort of mh_sort.h), emitted in the reference's unit order: the arena equals the oracle's per-unit FASTQ
+  concatenated."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from oracle import oracle as O
@@ -392,11 +390,11 @@ def test_batched_units_vs_oracle(native, monkeypatch, sort):
   assert fix <= 1
 
 
-def test_lsd_sort_repeated_batches(native, monkeypatch):
-  """The hand-written permutation sort (MH_SORT=lsd) over batches of different sizes and then the first batch again:
-  its look-back scan scratch sits inside the sort's buffer at an offset that moves with the batch size, so a batch
-  size seen before must not find stale scan state there (round 4: a timed-out look-back scan on the bench's second
-  step).  The repeat's templates equal the first run's, and rocprim's sort gives the same."""
+def test_lsd_sort_repeated_batches(native):
+  """The permutation sort (mh_sort.h) over batches of different sizes and then the first batch again: its look-back
+  status words sit inside the sort's buffer at an offset that moves with the batch size, so a batch size seen before
+  must not find stale status there (round 4: a timed-out look-back scan on the bench's second step).  The repeat's
+  templates equal the first run's, and every batch's equal a one-unit-at-a-time run's."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   mdl = G.model('hiseq-X-v2.5-Garvan')
@@ -406,8 +404,7 @@ def test_lsd_sort_repeated_batches(native, monkeypatch):
   copies = synth.copies_soa(synth.variants(seq, 42))
   batches = [[(0, 0, 0, 501), (1, 0, 1, 502), (2, 0, 0, 503)], [(3, 0, 1, 601)], [(4, 0, 0, 701), (5, 0, 1, 702)]]
   got = {}
-  for sort in ('lsd', 'rocprim'):
-    monkeypatch.setenv('MH_SORT', sort)
+  for mode in ('batch', 'single'):
     eng = Engine(0)
     try:
       eng.load_region(0, ('2', 0, L), seq)
@@ -415,17 +412,21 @@ def test_lsd_sort_repeated_batches(native, monkeypatch):
       for k, b in enumerate(batches + [batches[0]]):
         eng.haplotypes([(ri, cpy) for _, ri, cpy, _ in b])
         slots = [eng.haplotype(ri, cpy, copies[cpy])[0] for _, ri, cpy, _ in b]
-        ns = eng.ctx.sample_units([100 * k + i for i in range(len(b))], slots, [u[3] for u in b], p, 150,
-                                  mdl['cum_tlen'])
+        if mode == 'batch':
+          ns = eng.ctx.sample_units([100 * k + i for i in range(len(b))], slots, [u[3] for u in b], p, 150,
+                                    mdl['cum_tlen'])
+        else:
+          ns = [eng.ctx.sample_units([100 * k + i], [sl], [u[3]], p, 150, mdl['cum_tlen'])[0]
+                for i, (sl, u) in enumerate(zip(slots, b))]
         runs.append([eng.ctx.templates_export(100 * k + i) for i in range(len(b))])
         assert min(ns) > 1000
-      got[sort] = runs
+      got[mode] = runs
     finally:
       eng.close()
-  for a, b in zip(got['lsd'][0], got['lsd'][-1]):
+  for a, b in zip(got['batch'][0], got['batch'][-1]):
     for x, y in zip(a, b):
       assert np.array_equal(x, y)
-  for ra, rb in zip(got['lsd'], got['rocprim']):
+  for ra, rb in zip(got['batch'], got['single']):
     for a, b in zip(ra, rb):
       for x, y in zip(a, b):
         assert np.array_equal(x, y)
