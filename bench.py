@@ -237,7 +237,8 @@ def main():
     sys.exit('bench.py: --gpus {} but WORLD_SIZE={}: the launcher and the flag disagree'.format(a.gpus, world))
   rank = int(os.environ.get('RANK', '0'))
   local = int(os.environ.get('LOCAL_RANK', '0'))
-  a.prime_s = prime_hbm(a, local)
+  global PRIME_S
+  a.prime_s = PRIME_S = prime_hbm(a, local)
   if a.tumor_normal or a.workload == 'chr1':
     if world != 1:
       sys.exit('bench.py: --tumor-normal and --workload chr1 are one-GPU configs')
@@ -259,6 +260,15 @@ def prime_hbm(a, local):
   sys.stderr.write(r.stdout)
   return round(time.perf_counter() - t0, 2)
 
+
+PRIME_S = None   # the priming pass's seconds in this process (None: it did not run)
+
+
+def hbm_setup():
+  """Whether this process's GPU was primed (scripts/prime_hbm.py in a child process before the first GPU call) and the
+  pass's seconds: on a fresh box the first process to use the GPU ran 2-13 % slower throughout without it (DESIGN.md
+  "the first process")."""
+  return {'primed': PRIME_S is not None, 'prime_hbm_s': PRIME_S}
 
 def run_chr1(a):
   import numpy as np
@@ -336,7 +346,7 @@ def run_chr1(a):
     'span_ms': span_ms,
     'stage_note': STAGE_NOTE,
     'fastq_bytes_per_template': (b1 + b2) / max(kept, 1),
-    'setup_s': {'prime_hbm': getattr(a, 'prime_s', None)},
+    'setup_s': hbm_setup(),
     'host_cpus': os.cpu_count(),
   }
   print(json.dumps(out), flush=True)
@@ -429,7 +439,7 @@ def run_tumor_normal(a):
                       'note': 'the timed step (mix + BAM records sorted in HBM) plus the BAM file with BAI written '
                               'from them (bam_file_gpu), per step'},
     'stage_ms': {k: round(v / a.steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])},
-    'setup_s': {'prime_hbm': getattr(a, 'prime_s', None)},
+    'setup_s': hbm_setup(),
     'host_cpus': os.cpu_count()}), flush=True)
 
 
@@ -464,6 +474,7 @@ def end_to_end(a, seq, recs, model, kept_per_job):
     out = {'seconds': t3 - t2, 'value': st['kept'] / (t3 - t2), 'unit': 'templates/s', 'templates': st['kept'],
            'fastq_bytes': st['bytes1'] + st['bytes2'], 'fasta_parse_s': t1 - t0, 'vcf_parse_s': t2 - t1,
            'split_s': {k: round(st[k], 3) for k in SPLIT_KEYS}, 'stages_ms': st.get('stages_ms'),
+           'primed': hbm_setup()['primed'],
            'note': 'generate-reads chr1 end to end: host FASTA (249 MB) + VCF parse, GPU job, FASTQ D2H to '
                    'page-locked memory, written to /dev/null; seconds = the whole command'}
     if a.e2e_gz:   # the same with both files BGZF-compressed (what `.gz` output names cost): on the GPU, then on host
@@ -475,7 +486,7 @@ def end_to_end(a, seq, recs, model, kept_per_job):
                                                  gz_device=dev, stage_times=True)
         t5 = time.perf_counter()
         out[key] = {'seconds': t5 - t4, 'value': st['kept'] / (t5 - t4), 'unit': 'templates/s',
-                    'gz_bytes': st['written1'] + st['written2'],
+                    'gz_bytes': st['written1'] + st['written2'], 'primed': hbm_setup()['primed'],
                     'split_s': {k: round(st[k], 3) for k in SPLIT_KEYS}, 'stages_ms': st.get('stages_ms'),
                     'note': 'the same command with BGZF output, deflated ' +
                             ('on the GPU from the arenas (mh_output_bgzf), then D2H of the compressed bytes' if dev else
@@ -663,7 +674,7 @@ def run_genome(a, rank, world, local):
     'span_ms': span_ms,
     'stage_note': STAGE_NOTE,
     'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
-    'setup_s': {'synth_inputs': round(t_synth, 2), 'prime_hbm': getattr(a, 'prime_s', None)},
+    'setup_s': dict(synth_inputs=round(t_synth, 2), **hbm_setup()),
     'host_cpus': os.cpu_count(),
   }
   if a.plan_share:   # not the metric line: one rank's share of an N-rank plan, timed alone

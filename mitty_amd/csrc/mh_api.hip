@@ -96,43 +96,13 @@ void *cache_take(size_t bytes, size_t *cap) {
   return nullptr;
 }
 
-// (A/B, round 5: MH_ARENA_GB=N reserves one N GiB block on the first allocation and carves every later request
-// from it, bump-allocated, 2 MiB aligned; such blocks go back to the cache, never to hipFree)
-struct Arena {
-  char *base = nullptr;
-  size_t size = 0, used = 0;
-  bool tried = false;
-};
-Arena g_arena;
-bool in_arena(void *p) {
-  return g_arena.base && (char *)p >= g_arena.base && (char *)p < g_arena.base + g_arena.size;
-}
-void *arena_take(size_t bytes, size_t *cap) {
-  std::lock_guard<std::mutex> lk(g_cache_mu);
-  if (!g_arena.tried) {
-    g_arena.tried = true;
-    const char *e = getenv("MH_ARENA_GB");
-    const size_t gb = e ? (size_t)atoll(e) : 0;
-    if (gb && hipMalloc((void **)&g_arena.base, gb << 30) == hipSuccess) g_arena.size = gb << 30;
-    else g_arena.base = nullptr;
-    (void)hipGetLastError();
-  }
-  if (!g_arena.base) return nullptr;
-  const size_t c = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-  if (g_arena.used + c > g_arena.size) return nullptr;
-  void *p = g_arena.base + g_arena.used;
-  g_arena.used += c;
-  *cap = c;
-  return p;
-}
-
 int64_t cache_trim(int dev) {   // dev < 0: every device's blocks
   std::vector<std::pair<void *, int>> out;
   int64_t freed = 0;
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (auto it = g_cache.begin(); it != g_cache.end();)
-      if ((dev < 0 || it->second.dev == dev) && !in_arena(it->second.p)) {
+      if (dev < 0 || it->second.dev == dev) {
         out.push_back({it->second.p, it->second.dev});
         freed += (int64_t)it->first;
         it = g_cache.erase(it);
@@ -152,7 +122,6 @@ int64_t cache_trim(int dev) {   // dev < 0: every device's blocks
 
 hipError_t dev_alloc(void **p, size_t bytes, size_t *cap) {
   if ((*p = cache_take(bytes, cap))) return hipSuccess;
-  if ((*p = arena_take(bytes, cap))) return hipSuccess;
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) {   // the cache's blocks back to the device, then once more
     (void)hipGetLastError();

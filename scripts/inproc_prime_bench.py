@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.join(REPO, 'scripts'))
 import prime_hbm  # noqa: E402
 
 saved = sys.argv[1:]
-sys.argv = ['prime_hbm.py', '0', '8']
+sys.argv = ['prime_hbm.py', '0', '8', os.environ.get('PRIME_WRITE', '1')]
 prime_hbm.main()
 sys.argv = [os.path.join(REPO, 'bench.py')] + saved
 runpy.run_path(os.path.join(REPO, 'bench.py'), run_name='__main__')
