@@ -404,7 +404,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (uint8_t *p : ctx->h_bam_pin)
     if (p) (void)hipHostFree(p);
   for (auto &e : ctx->eset) {
-    release(e.recs); release(e.off); release(e.strip); release(e.ovf); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
+    release(e.recs); release(e.off); release(e.tsum); release(e.tpre); release(e.stat); release(e.crrec);
     (void)hipEventDestroy(e.done);
     if (e.rb) (void)hipEventDestroy(e.rb);
     if (e.h_stat) (void)hipHostFree(e.h_stat);
@@ -1368,8 +1368,25 @@ int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates
   if (!templates) return arg_fail(ctx, MH_E_ARG, "null argument");
   int64_t u1 = 0, u2 = 0;
   const bool two = ctx->used2 > 0;
-  return bam_add(ctx, (const uint8_t *)ctx->out1.p, ctx->used1, two ? (const uint8_t *)ctx->out2.p : nullptr,
-                 two ? ctx->used2 : 0, max_templates, &u1, &u2, templates, true);
+  const uint8_t *a1 = (const uint8_t *)ctx->out1.p, *a2 = two ? (const uint8_t *)ctx->out2.p : nullptr;
+  if (ctx->bam.cap <= 0)
+    return bam_add(ctx, a1, ctx->used1, a2, two ? ctx->used2 : 0, max_templates, &u1, &u2, templates, true);
+  // bounded HBM (mh_bam_set_capacity): the arenas in pieces of cap / 2048 templates (a template's records are well
+  // under 2 KiB: 2x250 reads with their qnames ~1 KiB), so the store spills between pieces and stays near the bound
+  const int64_t per = std::max<int64_t>(1, ctx->bam.cap / 2048);
+  int64_t o1 = 0, o2 = 0, tot = 0;
+  while (max_templates < 0 || tot < max_templates) {
+    const int64_t lim = max_templates < 0 ? per : std::min(per, max_templates - tot);
+    int64_t t = 0;
+    MH_TRY(bam_add(ctx, a1 + o1, ctx->used1 - o1, two ? a2 + o2 : nullptr, two ? ctx->used2 - o2 : 0, lim, &u1, &u2,
+                   &t, false));
+    if (t == 0) break;
+    o1 += u1;
+    o2 += u2;
+    tot += t;
+  }
+  *templates = tot;
+  return MH_OK;
 }
 
 int32_t mh_bam_records(mh_ctx *ctx, int64_t *n_records, int64_t *bytes) {

@@ -259,170 +259,34 @@ struct QFixed {
   const char *prefix;   // "@{stub}:"
   const char *mid;      // "|{chrom}|{cpy}"
   int32_t prefix_len, mid_len;
-  uint4 tail;           // "|{rlen}|{rlen}=|": what follows POS in the part of a read inside one '=' node
-  int32_t tail_len;     // (0: no such shortcut, rlen of more than 5 digits)
 };
-
-__device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
-// The qname's reads part (readgenerate.py:223-225: per read in file order '|' strand '|' POS '|' rlen '|' CIGAR '|'
-// v1,v2,..; then the line's '\n'), formatted by k_emit_measure into a strip the writer copies: ED_SW bytes per
-// template (one line-aligned slot), longer parts (a read spanning many variants: ~0.06 % of 2x150 templates at
-// 1.3 variants/kbp) whole in an overflow area, the slot then holding the overflow offset.
-constexpr int ED_SW = 64;
-
-struct Strip {
-  char *slot;                 // [m][ED_SW]
-  char *ovf;                  // overflow parts
-  int64_t ovf_cap;
-  unsigned long long *ovf_used;
-};
-
-// Byte sinks of the part formatter.  RowSink: the thread's LDS row (bytes past ED_SW only counted).  Digits go in
-// as one packed 8-byte store, fixed text as 8-byte stores (unaligned LDS access), so a row keeps ED_RSLACK bytes of
-// slack past ED_SW for stores that start inside it.
-constexpr int ED_RSLACK = 8;
-constexpr int MS_ROW = ED_SW + ED_RSLACK + 4;   // an odd number of dwords: lanes' equal columns in distinct banks
-struct RowSink {
-  char *row;
-  int32_t o = 0;
-  __device__ __forceinline__ void put(char c) {
-    if (o < ED_SW) row[o] = c;
-    o++;
-  }
-  // x < 10^8 as n decimal digits (leading zeros when n exceeds its length), most significant first
-  __device__ __forceinline__ void digits(uint32_t x, int n) {
-    uint64_t acc = 0;
-    for (int i = 0; i < n; i++) {
-      acc = (acc << 8) | (uint64_t)('0' + x % 10u);
-      x /= 10u;
-    }
-    if (o < ED_SW) __builtin_memcpy(row + o, &acc, 8);
-    o += n;
-  }
-  __device__ __forceinline__ void dec(int64_t v) {
-    if (v < 0) {
-      put('-');
-      v = -v;
-    }
-    const uint64_t u = (uint64_t)v;
-    if (u < 100000000ull) {
-      digits((uint32_t)u, ndig_u(u));
-    } else if (u < 10000000000000000ull) {
-      const uint64_t h = u / 100000000ull;
-      digits((uint32_t)h, ndig_u(h));
-      digits((uint32_t)(u - h * 100000000ull), 8);
-    } else {
-      auto put = [&](uint8_t c) { this->put((char)c); };
-      put_big(u);
+__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
+                                                 bool special, int64_t pos, int64_t p, int64_t rlen) {
+  int32_t L = 3 + ndig_s(pos) + 1 + ndig_s(rlen) + 1 + 1;
+  if (special) L += 1 + ndig_s(p - nd0.ps()) + 1 + ndig_s(rlen) + 1;
+  int32_t nv = 0;
+  for (int64_t k = n0; k <= n1; k++) {
+    const Node16 n = k == n0 ? nd0 : h.nd[k];
+    if (!special) L += ndig_s(node_count(n, p, rlen)) + 1;
+    if (n.code() != 0) {
+      L += ndig_s(node_v(n)) + (nv ? 1 : 0);
+      nv++;
     }
   }
-  // n <= 16 bytes of fixed text
-  __device__ __forceinline__ void text(const uint4 &t, int n) {
-    const uint64_t a = t.x | ((uint64_t)t.y << 32), b = t.z | ((uint64_t)t.w << 32);
-    if (o < ED_SW) __builtin_memcpy(row + o, &a, 8);
-    if (o + 8 < ED_SW && n > 8) __builtin_memcpy(row + o + 8, &b, 8);
-    o += n;
-  }
-};
-struct GlobalSink {
-  char *g;
-  int32_t o = 0;
-  __device__ __forceinline__ void put(char c) { g[o++] = c; }
-  __device__ __forceinline__ void text(const uint4 &t, int n) {
-    for (int i = 0; i < n; i++) g[o++] = (char)(u4get(t, i >> 2) >> (8 * (i & 3)));
-  }
-  __device__ __forceinline__ void dec(int64_t v) { o = (int32_t)(put_s(g + o, v) - g); }
-};
-
-// A read's first three nodes, loaded together (clamped to the last node) as soon as its start node is known: the end
-// node and the reads part come from them without a chain of dependent loads (a read spans at most three nodes
-// unless it covers two variants: ~4 % of 2x150 reads at 1.3 variants/kbp, which load the rest).
-struct Nodes3 {
-  Node16 a, b, c;
-  __device__ __forceinline__ Node16 at(const HapView &h, int64_t n0, int64_t j) const {
-    const int64_t d = j - n0;
-    if (d > 2) return h.nd[j];
-    Node16 o;   // (field by field: a select of whole structs would go through scratch memory)
-    o.a = d == 0 ? a.a : d == 1 ? b.a : c.a;
-    o.b = d == 0 ? a.b : d == 1 ? b.b : c.b;
-    return o;
-  }
-};
-__device__ __forceinline__ Nodes3 nodes3(const HapView &h, int64_t n0) {
-  const int64_t last = h.n_nodes - 1;
-  return Nodes3{h.nd[n0], h.nd[n0 + 1 < last ? n0 + 1 : last], h.nd[n0 + 2 < last ? n0 + 2 : last]};
-}
-// node_walk from n0 over the preloaded nodes
-__device__ __forceinline__ int64_t node_walk3(const HapView &h, const Nodes3 &q, int64_t n0, int64_t x) {
-  const int64_t last = h.n_nodes - 1;
-  if (n0 + 1 > last || q.b.key() > x) return n0;
-  if (n0 + 2 > last || q.c.key() > x) return n0 + 1;
-  return node_walk(h, n0 + 2, x);
-}
-
-// rpc.get_begin_end_nodes (rpc.py:119-130) with the first three nodes preloaded, then POS / sequence range
-__device__ __forceinline__ void place_read(const HapView &h, int64_t p, int64_t rlen, ReadInfo &r, Nodes3 &q) {
-  r.n0 = node_upper(h, p) - 1;
-  q = nodes3(h, r.n0);
-  r.n1 = node_walk3(h, q, r.n0, p + rlen - 1);
-  read_place(h, q.a, p, rlen, r);
-}
-
-// One read's part: '|' s '|' POS '|' rlen '|' CIGAR '|' v-list (rpc.py:144-160; the special '>p:nI' CIGAR of a read
-// inside an insertion, rpc.py:150-157); nodes n0 .. n1 (the first three preloaded in q).
-template <class Sink>
-__device__ __forceinline__ void fmt_read_part(Sink &k, const HapView &h, const Nodes3 q, int64_t n0, int64_t n1,
-                                              const ReadInfo &r, int s, int64_t p, int64_t rlen, const QFixed &qf) {
-  const Node16 nd0 = q.a;
-  k.put('|');
-  k.put((char)('0' + s));
-  k.put('|');
-  k.dec(r.pos);
-  // a read inside one '=' node (most of them): CIGAR '{rlen}=', no v-list — the rest is the fixed tail
-  if (qf.tail_len && n0 == n1 && !r.special && nd0.code() == 0 && node_count(nd0, p, rlen) == rlen) {
-    k.text(qf.tail, qf.tail_len);
-    return;
-  }
-  k.put('|');
-  k.dec(rlen);
-  k.put('|');
-  if (r.special) {
-    k.put('>');
-    k.dec(p - nd0.ps());
-    k.put(':');
-    k.dec(rlen);
-    k.put('I');
-  } else {
-    for (int64_t j = n0; j <= n1; j++) {
-      const Node16 n = q.at(h, n0, j);
-      k.dec(node_count(n, p, rlen));
-      k.put((char)n.op());
-    }
-  }
-  k.put('|');
-  bool first = true;
-  for (int64_t j = n0; j <= n1; j++) {
-    const Node16 n = q.at(h, n0, j);
-    if (n.code() == 0) continue;
-    if (!first) k.put(',');
-    k.dec(node_v(n));
-    first = false;
-  }
+  return L;
 }
 
 // One thread per template: start/end node of both mates, POS, the N filter (readgenerate.py:201-204), the qname
-// reads part (formatted into the strip when st.slot is set; else only measured) and the record lengths without the
-// cnt digits, into Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the
-// longest record (+20) and the longest reads part + '\n' as maxima (one atomic per wave); max_rec[1] = 1 when the
-// overflow area was too small.
+// reads part's length (not its text: the writer formats it) and the record lengths without the cnt digits, into
+// Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the longest record
+// (+20) and the longest reads part + '\n' as maxima (one atomic per wave).
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
-                                                      Rec *recs, int4 *tsum, int32_t *max_rec, Strip st) {
+                                                      Rec *recs, int4 *tsum, int32_t *max_rec) {
   __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
-  __shared__ __attribute__((aligned(16))) char s_row[256 * MS_ROW];
   const bool runs_lds = h.n_runs <= MS_RUNS;
   if (runs_lds)
     for (int i = threadIdx.x; i < h.n_runs; i += 256) {
@@ -435,60 +299,35 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int32_t nbytes = 0;
   int32_t sk = 0, s1 = 0, s2 = 0;   // this template's share of the tile sums
   if (t < m) {
-    const int64_t p0 = pos0[t], p1 = pos1[t];
+    ReadInfo r[2];
+    Node16 nn0[2];
+    const int64_t p[2] = {pos0[t], pos1[t]};
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-    // the reads part in file order (reads[fo] = mate 0, readgenerate.py:207): mate sa's part first.  One read at a
-    // time — its start/end nodes, POS, N count, and its part formatted into this thread's LDS row — so only one read's
-    // nodes are live (fewer registers, more waves: the pass waits on its random node loads).  A template the N filter
-    // drops is formatted too and ignored.
-    const int sa = f0 == 0 ? 0 : 1;
-    const int64_t pa = sa ? p1 : p0, pb = sa ? p0 : p1;
-    RowSink k{s_row + threadIdx.x * MS_ROW};
-    ReadInfo ra, rb;
-    int nna, nnb;
-    {
-      Nodes3 qa;
-      place_read(h, pa, rlen, ra, qa);
-      nna = runs_lds ? count_N_runs(s_rs, s_re, h.n_runs, ra.hap_a, ra.hap_a + ra.seq_len)
-                     : count_N(h, ra.hap_a, ra.hap_a + ra.seq_len);
-      fmt_read_part(k, h, qa, ra.n0, ra.n1, ra, sa, pa, rlen, q);
+#pragma unroll
+    for (int s = 0; s < 2; s++) {   // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range
+      r[s].n0 = node_upper(h, p[s]) - 1;
+      r[s].n1 = node_walk(h, r[s].n0, p[s] + rlen - 1);
+      nn0[s] = h.nd[r[s].n0];
+      read_place(h, nn0[s], p[s], rlen, r[s]);
     }
-    const int32_t la = k.o;
-    {
-      Nodes3 qb;
-      place_read(h, pb, rlen, rb, qb);
-      nnb = runs_lds ? count_N_runs(s_rs, s_re, h.n_runs, rb.hap_a, rb.hap_a + rb.seq_len)
-                     : count_N(h, rb.hap_a, rb.hap_a + rb.seq_len);
-      fmt_read_part(k, h, qb, rb.n0, rb.n1, rb, 1 - sa, pb, rlen, q);
+    int keep;
+    if (runs_lds) {
+      keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+             count_N_runs(s_rs, s_re, h.n_runs, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
+    } else {
+      keep = count_N(h, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
+             count_N(h, r[1].hap_a, r[1].hap_a + r[1].seq_len) <= 2;
     }
-    k.put('\n');
-    const int keep = nna <= 2 && nnb <= 2;
-    // mate-indexed (selects, not an indexed array: a dynamically indexed private array would live in scratch memory)
-    const int32_t n0m0 = (int32_t)(sa ? rb.n0 : ra.n0), n0m1 = (int32_t)(sa ? ra.n0 : rb.n0);
-    const int32_t n1m0 = (int32_t)(sa ? rb.n1 : ra.n1), n1m1 = (int32_t)(sa ? ra.n1 : rb.n1);
-    Rec out{0, 0, 0, 0, {n0m0, n0m1}, {n1m0, n1m1}};
+    Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
-      const int32_t rest = k.o - 1;
-      if (st.slot && k.o > ED_SW) {   // the whole part in the overflow area; the slot holds its offset
-        const unsigned long long at = atomicAdd(st.ovf_used, (unsigned long long)k.o);
-        if ((int64_t)(at + k.o) <= st.ovf_cap) {
-          GlobalSink g{st.ovf + at};
-          Nodes3 qx;
-          ReadInfo rx;
-          place_read(h, pa, rlen, rx, qx);
-          fmt_read_part(g, h, qx, rx.n0, rx.n1, rx, sa, pa, rlen, q);
-          place_read(h, pb, rlen, rx, qx);
-          fmt_read_part(g, h, qx, rx.n0, rx.n1, rx, 1 - sa, pb, rlen, q);
-          g.put('\n');
-          __builtin_memcpy(s_row + threadIdx.x * MS_ROW, &at, 8);   // (a 4-byte aligned row)
-        } else {
-          max_rec[1] = 1;
-        }
-      }
+      const int32_t l0 = read_part_len(h, nn0[0], r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
+      const int32_t l1 = read_part_len(h, nn0[1], r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
+      const int32_t rest = l0 + l1;
       const int32_t ql = q.prefix_len + q.mid_len + rest;
-      const int32_t s_f1 = ra.seq_len, s_f2 = rb.seq_len;   // file 1 holds mate sa
+      const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
+      const int32_t s_f2 = f0 == 0 ? r[1].seq_len : r[0].seq_len;
       const int32_t q1 = corrupt ? s_f1 : (int32_t)rlen, q2 = corrupt ? s_f2 : (int32_t)rlen;
-      out.keep = 1 | (la << 1);   // kept; the first read's part length (where the second starts)
+      out.keep = 1 | ((f0 == 0 ? l0 : l1) << 1);   // kept; the first read's part length (where the second starts)
       out.len1 = ql + 1 + s_f1 + 3 + q1 + 1;
       out.len2 = ql + 1 + s_f2 + 3 + q2 + 1;
       out.rest = rest;
@@ -499,24 +338,6 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
       s2 = out.len2;
     }
     recs[t] = out;
-  }
-  if (st.slot) {
-    // the wave's 64 rows to its 64 consecutive slots: 16-byte chunks, consecutive lanes on consecutive chunks (a wave
-    // reads only its own rows: its LDS writes complete, no workgroup barrier)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t tw = (int64_t)blockIdx.x * blockDim.x + 64 * w;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int c = lane + 64 * i, row = c >> 2, col = (c & 3) * 16;
-      if (tw + row < m) {
-        uint4 v;
-        __builtin_memcpy(&v, s_row + (64 * w + row) * MS_ROW + col, 16);
-        *(uint4 *)(st.slot + (tw + row) * ED_SW + col) = v;
-      }
-    }
   }
   if (tsum != nullptr) {   // the tile = the 32 lanes of a wave half
 #pragma unroll
@@ -822,6 +643,7 @@ __device__ __forceinline__ uint32_t lt_mask(int32_t x0, int32_t n) {
   return (uint32_t)((1ull << (8 * k)) - 1ull);
 }
 
+__device__ __forceinline__ uint32_t u4get(const uint4 &v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
 // qname head constants by value (kernel arguments: uniform indexing reads them through the scalar cache)
 struct QHead {
@@ -977,7 +799,6 @@ struct TArgs {
   int64_t cnt_base;         // templates kept before the emission's first one (cnt numbering)
   uint2 *crec;              // corruption: per record the first base's arena offset and S (k_cr_inplace's words)
   int32_t rlen, win_stride, head, qstride;
-  const char *slot, *ovf;   // k_emit_measure's strip: per template the qname reads part (Strip)
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
   const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
@@ -986,6 +807,42 @@ struct TArgs {
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
 // read from the shared string for S + 4 bytes, whose last one k_cr_inplace turns into the '\n' (and the
 // placeholders into qualities) when it corrupts the record.
+__device__ __forceinline__ uint32_t lds_put_u(char *lds, uint32_t o, uint64_t v) {
+  if (v > 0xffffffffull) {
+    auto put = [&](uint8_t c) { lds[o++] = (char)c; };
+    put_big(v);
+    return o;
+  }
+  uint32_t x = (uint32_t)v;
+  const int nd = ndig_u(x);
+  for (int i = nd - 1; i >= 0; i--) {
+    lds[o + i] = (char)('0' + x % 10u);
+    x /= 10u;
+  }
+  return o + nd;
+}
+__device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) {
+  if (v < 0) {
+    lds[o] = '-';
+    return lds_put_u(lds, o + 1, (uint64_t)(-v));
+  }
+  return lds_put_u(lds, o, (uint64_t)v);
+}
+
+#define NODE_AT(k)                                                                                       \
+  Node16 n;                                                                                              \
+  {                                                                                                      \
+    const int64_t i_ = (k) - n0;                                                                         \
+    if (i_ > 3) {                                                                                        \
+      const uint64_t *g_ = (const uint64_t *)(h.nd + (k));                                               \
+      n.a = g_[0];                                                                                       \
+      n.b = g_[1];                                                                                       \
+    } else {                                                                                             \
+      n.a = i_ == 0 ? q0.a : i_ == 1 ? q1.a : i_ == 2 ? q2.a : q3.a;                                     \
+      n.b = i_ == 0 ? q0.b : i_ == 1 ? q1.b : i_ == 2 ? q2.b : q3.b;                                     \
+    }                                                                                                    \
+  }
+
 template <int NF, int LPR, int CR, int GW>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1065,19 +922,12 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       use |= (uint32_t)u << k;
       wv[k] = *(const uint4 *)(hsrc + (u ? 16 * c : 0));
     }
-    // the first 128 gather threads also copy the tile's strip slots (the qname reads parts k_emit_measure
-    // formatted): 16 bytes each, to the qname buffer after its head room
-    const int js = g >> 2, cs = g & 3;
-    const bool ks = g < 4 * ED_T && js < nt;
-    uint4 sv = make_uint4(0, 0, 0, 0);
-    if (ks) sv = *(const uint4 *)(A.slot + (t0 + js) * ED_SW + 16 * cs);
     const int32_t slot = o_win + (jg * 2 + sg) * win_stride;
 #pragma unroll
     for (int k = 0; k < GM; k++) {
       const int c = q3 + GW * k;
       *(uint4 *)(smem + (((use >> k) & 1) ? slot + 16 * c : o_dump)) = wv[k];
     }
-    if (ks) __builtin_memcpy(smem + o_q + js * qstride + head + 16 * cs, &sv, 16);
   }
   if (tid < 64) {
     // wave 0: lane = read (template jf, mate s)
@@ -1088,24 +938,57 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     const int fo = A.fo0[tf];
     const int fr = s == 0 ? fo : 1 - fo;   // the read's place in the qname = its file (reads[fo] = mate 0, :207)
     const int64_t rl = A.rlen;
-    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length
-    const int4 r0 = *(const int4 *)(A.recs + tf);
+    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length, nodes
+    const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
     const E3 P = A.tpre[tile];
+    const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
     const bool keep = valid && (r0.x & 1);
     const int32_t rest = r0.w;
+    // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
+    const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
+                 q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
     int64_t a = p - h.p_min, e = p + rl - h.p_min;   // the read's bases: hap[a, a + S)
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
-    // a reads part longer than the strip slot: the whole part from the overflow area, into the buffer's second half
-    // (the slot copy of waves 1-2 lands in the first)
-    const bool ovf = keep && rest + 1 > ED_SW;
-    if (ovf && fr == 1) {
-      uint64_t at;
-      __builtin_memcpy(&at, A.slot + tf * ED_SW, 8);
-      char *d = smem + o_q + jf * qstride + head + ED_SW + head;
-      const char *src = A.ovf + at;
-      for (int i = 0; i <= rest; i++) d[i] = src[i];
+    if (keep) {
+      ReadInfo ri;
+      ri.n0 = n0;
+      ri.n1 = n1;
+      read_place(h, q0, p, rl, ri);
+      // the read's part of the qname at its place (readgenerate.py:223-225); read 1 ends at `rest`, where the '\n' goes
+      uint32_t o = (uint32_t)(o_q + jf * qstride + head);
+      if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part
+      smem[o] = '|';
+      smem[o + 1] = (char)('0' + s);
+      smem[o + 2] = '|';
+      o = lds_put_s(smem, o + 3, ri.pos);
+      smem[o] = '|';
+      o = lds_put_s(smem, o + 1, rl);
+      smem[o++] = '|';
+      if (ri.special) {
+        smem[o] = '>';
+        o = lds_put_s(smem, o + 1, p - q0.ps());
+        smem[o] = ':';
+        o = lds_put_s(smem, o + 1, rl);
+        smem[o++] = 'I';
+      } else {
+        for (int64_t k = n0; k <= n1; k++) {
+          NODE_AT(k)
+          o = lds_put_s(smem, o, node_count(n, p, rl));
+          smem[o++] = (char)n.op();
+        }
+      }
+      smem[o++] = '|';
+      bool first = true;
+      for (int64_t k = n0; k <= n1; k++) {
+        NODE_AT(k)
+        if (n.code() == 0) continue;
+        if (!first) smem[o++] = ',';
+        o = lds_put_s(smem, o, node_v(n));
+        first = false;
+      }
+      if (fr == 1) smem[o] = '\n';
     }
     // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
     const int32_t lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
@@ -1136,7 +1019,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       mt.len[fr] = keep ? lw + nd : 0;
       mt.rel[fr] = rel;
       const int32_t lh = Lp + nd + Lm;
-      const int32_t qb = o_q + jf * qstride + (ovf ? ED_SW + head : 0) + head - lh, sb = lh + rest + 1;
+      const int32_t qb = o_q + jf * qstride + head - lh, sb = lh + rest + 1;
       if (keep) {
         // mate 1 reads the reverse complement forward: from rc at hap_len - a - S
         const int32_t lead = !s ? (int32_t)(a & 15) : (int32_t)((h.hap_len - a - S) & 15);
@@ -1972,16 +1855,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   int32_t *err = (int32_t *)(small + 36);
   char *d_prefix = small + 256;
   char *d_mid = small + 256 + 4096;
-  QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size(), make_uint4(0, 0, 0, 0), 0};
-  {   // the fixed tail of a read inside one '=' node: "|{rlen}|{rlen}=|"
-    const std::string r = std::to_string(rlen), t = "|" + r + "|" + r + "=|";
-    if (t.size() <= 16) {
-      char b[16] = {0};
-      memcpy(b, t.data(), t.size());
-      memcpy(&q.tail, b, 16);
-      q.tail_len = (int32_t)t.size();
-    }
-  }
+  QFixed q{d_prefix, d_mid, (int32_t)prefix.size(), (int32_t)mid.size()};
   HapView hv = view_of(h);
   // the direct writer (corruption too; mh_set_emit_mode(1) forces the LDS-image writer): record offsets from per-tile
   // prefixes; the LDS-image writer reads per-template offsets
@@ -2037,10 +1911,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     if (m > ctx->eset_max_m) ctx->eset_max_m = m;
     const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
     MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
-    if (direct) {   // the qname reads parts: a slot per template, an overflow area of 8 bytes per template
-      MH_TRY(ensure(ctx, es.strip, (size_t)ED_SW * mm + 64));
-      MH_TRY(ensure(ctx, es.ovf, 8 * (size_t)mm + 4096));
-    }
     MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
     MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
     if (!direct) MH_TRY(ensure(ctx, es.off, sizeof(E3) * (m + 1)));
@@ -2054,9 +1924,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     Rec *recs = (Rec *)es.recs.p;
     stage_begin(ctx, "emit_measure");
     hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
-                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec,
-                       Strip{direct ? (char *)es.strip.p : nullptr, (char *)es.ovf.p, (int64_t)es.ovf.cap,
-                             (unsigned long long *)(stat + 48)});
+                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     stage_begin(ctx, "emit_scan");
@@ -2108,7 +1976,6 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   es.prepared = false;
   const Rec *recs = (const Rec *)es.recs.p;
   const int32_t hmax = hm4[0], hslot = hm4[3];
-  const bool ovf_full = hm4[1] != 0;   // the strip's overflow area ran out: the LDS-image writer formats everything
 
   // ---- the writer ------------------------------------------------------------------------------------------------
   // arenas: append after what is already there
@@ -2143,9 +2010,9 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   char *o1 = (char *)ctx->out1.p + ctx->used1;
   char *o2 = write_fastq2 ? (char *)ctx->out2.p + ctx->used2 : nullptr;
   const int32_t head = (int32_t)(((q.prefix_len + q.mid_len + 10 + 16) + 15) / 16 * 16);
-  // qname buffer per template (emit_tile): head room, the strip slot, and when a reads part is longer than a slot
-  // (hslot: the longest reads part + '\n' of the unit, from the measure pass) a second head room and the whole part
-  const int32_t qstride = head + ED_SW + (hslot > ED_SW ? head + (hslot + 15) / 16 * 16 : 0) + 32 + ED_QPAD;
+  // qname buffer per template (emit_tile): head room, then the reads part (hslot: the longest reads part + '\n' of
+  // the unit, from the measure pass)
+  const int32_t qstride = head + (hslot > 16 ? (hslot + 15) / 16 * 16 : 16) + 32 + ED_QPAD;
   const bool cr_rows = ctx->corrupt_on && cr_rows_lds(write_fastq2 ? 2 : 1, rlen, ctx->corrupt_n_bq);
   const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, write_fastq2 ? 2 : 1, cr_rows);
   QHead qh{};
@@ -2156,7 +2023,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     qh.lp = (int32_t)prefix.size();
     qh.lm = (int32_t)mid.size();
   }
-  if (direct && !ovf_full && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
+  if (direct && head_fits && win_stride <= 16 * 3 * ED_GMAX && lds_d <= 64 * 1024 &&
       cnt_base + m < (int64_t)UINT32_MAX) {
     if (cr_rows) MH_TRY(cr_rows_alloc(ctx, m, write_fastq2 ? 2 : 1, rlen));
     // the direct writer, queued on the writer stream: the call returns while it runs, so the next unit's measure pass
@@ -2169,7 +2036,7 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     ctx->stage_stream = ctx->wstream;
     TArgs A{hv, m, pos0, pos1, fo0, recs, (const E3 *)es.tpre.p, {(char *)ctx->out1.p, (char *)ctx->out2.p},
             {ctx->used1, ctx->used2}, cnt_base, (uint2 *)es.crrec.p, (int32_t)rlen, win_stride, head,
-            qstride, (const char *)es.strip.p, (const char *)es.ovf.p};
+            qstride};
     if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ctx->wstream, m, write_fastq2 ? 2 : 1, (int32_t)rlen, cc, A));
     stage_begin(ctx, "emit_write");   // (after the row pass: the stage times the writer alone)
     auto kfn = ew_kernel(cr_rows ? 2 : ctx->corrupt_on ? 1 : 0, write_fastq2);

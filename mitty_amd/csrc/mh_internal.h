@@ -154,7 +154,6 @@ namespace mh {
 // units (on the writer stream) overlap the measure passes of later ones and the next job's sampling (main stream).
 struct EmitSet {
   DevBuf recs, off;            // per template: k_emit_measure's records; offsets (LDS-image writer only)
-  DevBuf strip, ovf;           // per template: the qname reads part (k_emit_measure -> k_emit_tiles), long ones
   DevBuf tsum, tpre;           // per 32-template tile: sums (kept, bytes per file) and their exclusive prefixes
   DevBuf crrec;                // corruption: per record the first base's offset and S (k_cr_recs)
   DevBuf stat;                 // the measure pass's totals (E3 at 0) and maxima (int32[4] at 32)

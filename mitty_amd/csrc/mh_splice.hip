@@ -283,6 +283,37 @@ __device__ __forceinline__ uint32_t n_bits4(uint32_t w) {
 }
 // One pass over the haplotype for the run boundaries, 64 positions per thread: boundaries are rare, so each is
 // appended to an unsorted list through an atomic counter (cap entries kept, all counted); sorted afterwards.
+// Both N-run boundary lists of a haplotype (blockIdx.x: 0 starts, 1 ends; n distinct positions each, n <= NR_LDS)
+// sorted in LDS by one workgroup (bitonic over the next power of two, padded with 0xffffffff) and widened to the i64
+// lists the measure pass searches: one launch instead of two radix sorts' dozen (a genome has ~50 haplotypes per step,
+// each with a few dozen N runs).
+constexpr int NR_LDS = 8192;
+__global__ void __launch_bounds__(1024) k_nrun_sort_small(const uint32_t *us, const uint32_t *ue, int64_t n,
+                                                          int64_t *os, int64_t *oe) {
+  __shared__ uint32_t v[NR_LDS];
+  const uint32_t *a = blockIdx.x ? ue : us;
+  int64_t *o = blockIdx.x ? oe : os;
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v[i] = i < n ? a[i] : 0xffffffffu;
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t x = v[i], y = v[l];
+          if (((i & k) == 0) == (x > y)) {
+            v[i] = y;
+            v[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) o[i] = v[i];
+}
+
 __global__ void __launch_bounds__(256) k_widen_u32(const uint32_t *a, int64_t n, int64_t *out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = a[i];
@@ -573,7 +604,11 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     h.n_runs = nr;
     MH_TRY(ensure(ctx, h.nrun_s, 8 * (nr + 1)));
     MH_TRY(ensure(ctx, h.nrun_e, 8 * (nr + 1)));
-    if (nr > 0) {
+    if (nr > 0 && nr <= NR_LDS) {
+      hipLaunchKernelGGL(k_nrun_sort_small, dim3(2), dim3(1024), 0, st, (const uint32_t *)b_nrun.p,
+                         (const uint32_t *)b_nrun.p + cap, nr, (int64_t *)h.nrun_s.p, (int64_t *)h.nrun_e.p);
+      HIPCHK(ctx, hipGetLastError());
+    } else if (nr > 0) {
       // both boundary lists sorted by the library's LSD sort (mh_sort.h; the values, element indices, unused),
       // then widened to the i64 lists the measure pass searches
       unsigned bits = 1;

@@ -1288,7 +1288,8 @@ def test_tumor_normal_mix_god_aligner(native, tmp_path):
   """BASELINE configs[4] in small: a normal (sample S0, 6x) and a tumor (S1, 12x, the VCF's other sample) run of the
   2x250 model into the same device arenas — the mix is the two runs' FASTQ one after the other, each sample named in
   its qnames (Readme.md:14-16) — then the perfect BAM built from the arenas (parse, encode, coordinate sort in HBM).
-  The FASTQ equals the oracle's two runs concatenated; the BAM records equal the oracle god-aligner's over it."""
+  The FASTQ equals the oracle's two runs concatenated; the BAM records equal the oracle god-aligner's over it, and a
+  store bounded far below the records' size (spilled to host memory) writes the same BAM and BAI."""
   from mitty_amd.engine import Engine
   from mitty_amd.lib import fasta as mfasta, vcfio
   from mitty_amd.readmodel import get_read_model
@@ -1330,8 +1331,19 @@ def test_tumor_normal_mix_god_aligner(native, tmp_path):
     eng.ctx.bam_add_fastq(want1, want2)
     bam2 = str(tmp_path / 'tn2.bam')
     eng.ctx.bam_write(bam2, '@HD\tVN:1.0\n')
+    # the same mix into a store bounded to 40 kB (mh_bam_set_capacity): the arenas go in pieces, the store spills
+    # between them, and the file (BAM and BAI) is the unbounded store's, byte for byte
+    eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
+    eng.ctx.bam_set_capacity(40_000)
+    assert eng.ctx.bam_add_output() == want1.count(b'\n') // 4
+    assert eng.ctx.bam_spilled()[1] > 5
+    bam3 = str(tmp_path / 'tn3.bam')
+    eng.ctx.bam_write(bam3, '@HD\tVN:1.0\n', bai_path=bam3 + '.bai')
+    eng.ctx.bam_set_capacity(0)
   finally:
     eng.close()
+  assert open(bam3, 'rb').read() == open(bam, 'rb').read()
+  assert open(bam3 + '.bai', 'rb').read() == open(bam + '.bai', 'rb').read()
   refs = {'1': 0, '2': 1, '3': 2}
   _, recs, _, _ = god.record_voffsets(open(bam, 'rb').read())
   assert recs == [god.encode(r) for r in god.sorted_stream(god.god_records(want1, want2, refs))]
