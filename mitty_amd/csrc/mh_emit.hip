@@ -263,13 +263,40 @@ struct QFixed {
 
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
-__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Node16 &nd0, int64_t n0, int64_t n1,
+// A read's first three nodes, loaded together (clamped to the last node) as soon as its start node is known: its end
+// node and its qname part's length come from them without a chain of dependent loads (a 2x150 read spans more than
+// three nodes only when it covers two variants, which load the rest).
+struct Nodes3 {
+  Node16 a, b, c;
+  __device__ __forceinline__ Node16 at(const HapView &h, int64_t n0, int64_t j) const {
+    const int64_t d = j - n0;
+    if (d > 2) return h.nd[j];
+    Node16 o;   // (field by field: a select of whole structs would go through scratch memory)
+    o.a = d == 0 ? a.a : d == 1 ? b.a : c.a;
+    o.b = d == 0 ? a.b : d == 1 ? b.b : c.b;
+    return o;
+  }
+};
+__device__ __forceinline__ Nodes3 nodes3(const HapView &h, int64_t n0) {
+  const int64_t last = h.n_nodes - 1;
+  return Nodes3{h.nd[n0], h.nd[n0 + 1 < last ? n0 + 1 : last], h.nd[n0 + 2 < last ? n0 + 2 : last]};
+}
+// node_walk from n0 over the preloaded nodes
+__device__ __forceinline__ int64_t node_walk3(const HapView &h, const Nodes3 &q, int64_t n0, int64_t x) {
+  const int64_t last = h.n_nodes - 1;
+  if (n0 + 1 > last || q.b.key() > x) return n0;
+  if (n0 + 2 > last || q.c.key() > x) return n0 + 1;
+  return node_walk(h, n0 + 2, x);
+}
+
+__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Nodes3 q, int64_t n0, int64_t n1,
                                                  bool special, int64_t pos, int64_t p, int64_t rlen) {
+  const Node16 nd0 = q.a;
   int32_t L = 3 + ndig_s(pos) + 1 + ndig_s(rlen) + 1 + 1;
   if (special) L += 1 + ndig_s(p - nd0.ps()) + 1 + ndig_s(rlen) + 1;
   int32_t nv = 0;
   for (int64_t k = n0; k <= n1; k++) {
-    const Node16 n = k == n0 ? nd0 : h.nd[k];
+    const Node16 n = q.at(h, n0, k);
     if (!special) L += ndig_s(node_count(n, p, rlen)) + 1;
     if (n.code() != 0) {
       L += ndig_s(node_v(n)) + (nv ? 1 : 0);
@@ -300,16 +327,17 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
   int32_t sk = 0, s1 = 0, s2 = 0;   // this template's share of the tile sums
   if (t < m) {
     ReadInfo r[2];
-    Node16 nn0[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-#pragma unroll
-    for (int s = 0; s < 2; s++) {   // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range
-      r[s].n0 = node_upper(h, p[s]) - 1;
-      r[s].n1 = node_walk(h, r[s].n0, p[s] + rlen - 1);
-      nn0[s] = h.nd[r[s].n0];
-      read_place(h, nn0[s], p[s], rlen, r[s]);
-    }
+    // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range (two named node sets, not an array: an
+    // indexed array of them went to scratch memory)
+    r[0].n0 = node_upper(h, p[0]) - 1;
+    r[1].n0 = node_upper(h, p[1]) - 1;
+    const Nodes3 q0 = nodes3(h, r[0].n0), q1 = nodes3(h, r[1].n0);
+    r[0].n1 = node_walk3(h, q0, r[0].n0, p[0] + rlen - 1);
+    r[1].n1 = node_walk3(h, q1, r[1].n0, p[1] + rlen - 1);
+    read_place(h, q0.a, p[0], rlen, r[0]);
+    read_place(h, q1.a, p[1], rlen, r[1]);
     int keep;
     if (runs_lds) {
       keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
@@ -320,8 +348,8 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
-      const int32_t l0 = read_part_len(h, nn0[0], r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
-      const int32_t l1 = read_part_len(h, nn0[1], r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
+      const int32_t l0 = read_part_len(h, q0, r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
+      const int32_t l1 = read_part_len(h, q1, r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
       const int32_t rest = l0 + l1;
       const int32_t ql = q.prefix_len + q.mid_len + rest;
       const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
