@@ -1244,9 +1244,11 @@ __device__ __forceinline__ void cr_full_block(const uint8_t *bk, const uint16_t 
     const int j = __builtin_ctz(px);
     px &= px - 1;
     const int n = n0 + j;
-    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-    const int k = n % 3;
-    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+    // the base's word from the block's draws (a select chain: W is in registers; recomputing its Philox draw cost
+    // ~100 instructions per pass of this loop, which a wave takes whenever one of its lanes has a flagged base)
+    uint32_t w = W[0];
+#pragma unroll
+    for (int i = 1; i < CI_BLK; i++) w = j == i ? W[i] : w;
     uint32_t amb;
     const uint32_t bq = cr_lds_walk(bk + j * CB_ROW, tp + j * n_bq, w, &amb);
     const uint32_t x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n,
