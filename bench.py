@@ -268,7 +268,9 @@ def hbm_setup():
   """Whether this process's GPU was primed (scripts/prime_hbm.py in a child process before the first GPU call) and the
   pass's seconds: on a fresh box the first process to use the GPU ran 2-13 % slower throughout without it (DESIGN.md
   "the first process")."""
-  return {'primed': PRIME_S is not None, 'prime_hbm_s': PRIME_S}
+  return {'primed': PRIME_S is not None, 'prime_hbm_s': PRIME_S,
+          'unprimed_first_process': 'a first GPU process on a newly taken box runs 0-10 % (median ~5 %) slower '
+                                    'throughout without the pass: profiles/r05/fresh_box_ab.json'}
 
 def run_chr1(a):
   import numpy as np

@@ -48,13 +48,13 @@ int32_t arg_fail(mh_ctx *ctx, int32_t code, const std::string &msg) {
   return code;
 }
 
-bool scan_fault_pending() {
+bool scan_fault_pending(const mh_ctx *ctx) {
   const uint32_t *h = scan_fault_host();
-  return h && __atomic_load_n(h, __ATOMIC_ACQUIRE) != 0;
+  return h && __atomic_load_n(h + (ctx ? ctx->fault_slot : 0), __ATOMIC_ACQUIRE) != 0;
 }
 
 int32_t scan_fault_fail(mh_ctx *ctx) {
-  (void)scan_fault_take();
+  (void)scan_fault_take(ctx ? ctx->fault_slot : 0);
   return arg_fail(ctx, MH_E_STATE, "a look-back scan's wait timed out (a broken ticket base or scratch): its offsets "
                                    "are wrong");
 }
@@ -275,6 +275,7 @@ using namespace mh;
 #define CTX_GUARD_EMIT(ctx)                                                \
   do {                                                                     \
     if (!(ctx)) return MH_E_ARG;                                           \
+    scan_fault_slot = (ctx)->fault_slot;                                   \
     hipError_t _e = hipSetDevice((ctx)->device);                           \
     if (_e != hipSuccess) return hip_fail((ctx), _e, "hipSetDevice", __FILE__, __LINE__); \
   } while (0)
@@ -332,6 +333,11 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
   if (device < 0 || device >= n) return MH_E_ARG;
   mh_ctx *ctx = new mh_ctx();
   ctx->device = device;
+  {   // its own scan-fault word (slots 1 .. SCAN_FAULT_SLOTS - 1, reused round-robin past that many contexts)
+    static std::atomic<int> next{0};
+    ctx->fault_slot = 1 + next++ % (SCAN_FAULT_SLOTS - 1);
+    (void)scan_fault_take(ctx->fault_slot);
+  }
   // the FASTQ writers (bandwidth-bound, long) yield to the main stream's latency-bound sampling kernels
   int prio_lo = 0, prio_hi = 0;
   (void)hipSetDevice(device);

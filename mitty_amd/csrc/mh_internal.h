@@ -166,6 +166,7 @@ struct EmitSet {
 }  // namespace mh
 
 struct mh_ctx {
+  int fault_slot = 0;   // this context's look-back scan fault word (mh_scan.h)
   int device = 0;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;   // second sampling lane: per-unit finish stages of odd units run here
@@ -292,9 +293,9 @@ int32_t scan_fault_fail(mh_ctx *ctx);
 #define SYNCCHK(ctx, call)                                                    \
   do {                                                                        \
     HIPCHK(ctx, call);                                                        \
-    if (::mh::scan_fault_pending()) return ::mh::scan_fault_fail(ctx);        \
+    if (::mh::scan_fault_pending(ctx)) return ::mh::scan_fault_fail(ctx);     \
   } while (0)
-bool scan_fault_pending();
+bool scan_fault_pending(const mh_ctx *ctx);
 
 // Grow `b` to hold at least `bytes`; contents are NOT preserved.
 int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);

@@ -42,7 +42,7 @@ void jump_poly_words(uint64_t L, int64_t k, uint32_t *out624);
 namespace {
 
 constexpr uint32_t MT_UP = 0x80000000u, MT_LO = 0x7fffffffu, MT_A = 0x9908b0dfu;
-constexpr int64_t SEG_WORDS_DEFAULT = 624 * 640;   // outputs per segment (fewer, longer segments: the jump is the cost)
+constexpr int64_t SEG_WORDS_DEFAULT = 624 * 640;   // outputs per segment (twice as long: within noise, round 5)
 static int64_t seg_words() { return SEG_WORDS_DEFAULT; }
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {

@@ -233,14 +233,19 @@ __device__ __forceinline__ uint64_t lb_get(const uint64_t *w) {
 
 // scratch: [ticket (64 B)] [aggregate words K x nt] [inclusive words K x nt], zeroed when new; ticket_base: the
 // ticket counter's value when this launch starts; epoch: this launch's tag (1 .. 2^16 - 1)
-// A host-mapped word every look-back scan reports a timed-out wait to (a broken ticket base or scratch: the scan's
-// sums are then wrong).  The host reads it after a synchronisation (scan_fault_take) and fails the call with
-// MH_E_STATE instead of returning the wrong offsets as success.
+// Host-mapped words a look-back scan reports a timed-out wait to (a broken ticket base or scratch: the scan's sums
+// are then wrong), one per context: the host reads its context's word after a synchronisation (scan_fault_take) and
+// fails the call with MH_E_STATE instead of returning the wrong offsets as success, and a fault in one context does
+// not fail another's calls.  The word a launch reports to is the calling thread's current context's
+// (scan_fault_slot, set by every entry point's guard); slot 0 serves launches outside any context.
+constexpr int SCAN_FAULT_SLOTS = 256;
+inline thread_local int scan_fault_slot = 0;
 inline uint32_t *scan_fault_host() {
   static uint32_t *w = [] {
     uint32_t *p = nullptr;
-    if (hipHostMalloc((void **)&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (uint32_t *)nullptr;
-    p[0] = 0;
+    if (hipHostMalloc((void **)&p, 4 * SCAN_FAULT_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return (uint32_t *)nullptr;
+    for (int i = 0; i < SCAN_FAULT_SLOTS; i++) p[i] = 0;
     return p;
   }();
   return w;
@@ -251,13 +256,13 @@ inline uint32_t *scan_fault_device() {
     if (!h || hipHostGetDevicePointer((void **)&p, h, 0) != hipSuccess) return (uint32_t *)nullptr;
     return p;
   }();
-  return d;
+  return d ? d + scan_fault_slot : nullptr;
 }
-// 1 when a look-back scan timed out since the last call (the word is cleared)
-inline uint32_t scan_fault_take() {
+// 1 when a look-back scan of this slot timed out since the last call (the word is cleared)
+inline uint32_t scan_fault_take(int slot) {
   uint32_t *h = scan_fault_host();
   if (!h) return 0;
-  const uint32_t v = __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL);
+  const uint32_t v = __atomic_exchange_n(h + slot, 0u, __ATOMIC_ACQ_REL);
   return v;
 }
 
