@@ -1966,14 +1966,13 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
                                       ctx->scan_partials.p, tot));
     stage_end(ctx);
     if (defer) {
-      HIPCHK(ctx, hipMemcpyAsync(es.h_stat, tot, sizeof(E3), hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync((char *)es.h_stat + 32, max_rec, 16, hipMemcpyDeviceToHost, st));
+      // the totals (stat + 0) and the maxima (stat + 32) in one copy: a small copy costs a blit launch
+      HIPCHK(ctx, hipMemcpyAsync(es.h_stat, stat, 48, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipEventRecord(es.rb, st));
     } else {
       int64_t *hs = pinned_small(ctx);
       if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
-      HIPCHK(ctx, hipMemcpyAsync(hs, tot, sizeof(E3), hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(hs + 4, max_rec, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs, stat, 48, hipMemcpyDeviceToHost, st));   // totals at + 0, maxima at + 32
       SYNCCHK(ctx, hipStreamSynchronize(st));
       std::memcpy(&ht, hs, sizeof(E3));
       std::memcpy(hm4, hs + 4, sizeof(hm4));

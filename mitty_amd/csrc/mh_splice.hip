@@ -314,6 +314,15 @@ __global__ void __launch_bounds__(1024) k_nrun_sort_small(const uint32_t *us, co
   for (int i = threadIdx.x; i < n; i += blockDim.x) o[i] = v[i];
 }
 
+// ps of the first node, ps and oplen of the last, into out[0..2] (one readback with the splice's error word)
+__global__ void k_splice_ends(const int64_t *ps, const int64_t *nl, int64_t n_nodes, int64_t *out) {
+  if (threadIdx.x == 0) {
+    out[0] = ps[0];
+    out[1] = ps[n_nodes - 1];
+    out[2] = nl[n_nodes - 1];
+  }
+}
+
 __global__ void __launch_bounds__(256) k_widen_u32(const uint32_t *a, int64_t n, int64_t *out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = a[i];
@@ -518,17 +527,18 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     n_nodes++;
     hap_len += len;
   }
-  // p_min / p_max (readgenerate.py:192): ps of the first node; ps + oplen of the last
+  // p_min / p_max (readgenerate.py:192): ps of the first node; ps + oplen of the last — gathered beside the error
+  // word by one thread and read back in one copy (each small copy is a blit launch of its own)
   int64_t *hs = hs_lane;
-  HIPCHK(ctx, hipMemcpyAsync(hs + 8, ps, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hs + 9, ps + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hs + 10, nl + n_nodes - 1, 8, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(k_splice_ends, dim3(1), dim3(64), 0, st, (const int64_t *)ps, (const int64_t *)nl, n_nodes,
+                     (int64_t *)(small + 96));
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipMemcpyAsync(hs + 8, small + 64, 64, hipMemcpyDeviceToHost, st));   // err at + 64, ends at + 96
 
   // --- haplotype bytes ---------------------------------------------------------------------------------------
-  HIPCHK(ctx, hipMemcpyAsync(hs + 11, err, 4, hipMemcpyDeviceToHost, st));
   SYNCCHK(ctx, hipStreamSynchronize(st));
-  const int64_t ps0 = hs[8], psl = hs[9], nll = hs[10];
-  const int32_t herr = (int32_t)(hs[11] & 0xffffffff);
+  const int64_t ps0 = hs[12], psl = hs[13], nll = hs[14];
+  const int32_t herr = (int32_t)(hs[8] & 0xffffffff);
   if (herr) {
     stage_end(ctx);
     return arg_fail(ctx, MH_E_ARG, herr & 1 ? "variant beyond the end of the fetched reference region"
