@@ -238,9 +238,14 @@ __device__ __forceinline__ void hap_fill_chunk(int64_t o0, int64_t hap_len, int6
 
 // A workgroup fills FILL_SPAN bytes; its nodes (from the last one keyed below its first bucket to the first one
 // past its last bucket) are staged in LDS first, so every chunk's search is an LDS binary search.
-__global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, int64_t p_min, int64_t n_nodes, const Node16 *nd,
+// ends: the splice's {ps of the first node, ...} (k_splice_ends) and err its error word: a spliced node list with an
+// error is not filled (its sources may point anywhere); the host reports the error after its one synchronisation
+__global__ void __launch_bounds__(256) k_hap_fill(int64_t hap_len, const int64_t *ends, const int32_t *err,
+                                                  int64_t n_nodes, const Node16 *nd,
                                                   const int64_t *src, const int32_t *bkt, int64_t n_bkt,
                                                   const uint8_t *contig, const uint8_t *alt_pool, uint8_t *hap) {
+  if (*err) return;
+  const int64_t p_min = ends[0];
   __shared__ Node16 s_nd[FILL_NODES];
   __shared__ int64_t s_src[FILL_NODES];
   __shared__ int64_t s_lo, s_hi;
@@ -390,10 +395,11 @@ __global__ void __launch_bounds__(256) k_node_pack(int64_t n, const int64_t *ps,
 
 // Node-search buckets: bkt[k] = first node whose key is >= p_min + (k << NODE_BKT_SHIFT) (lower_bound), so the
 // searchsorted of rpc.get_begin_end_nodes (rpc.py:127-130) only scans the few keys of one bucket.
-__global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64_t n, int64_t p_min, int64_t n_bkt,
-                                                      int32_t *bkt) {
+__global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64_t n, const int64_t *ends,
+                                                      int64_t n_bkt, int32_t *bkt) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > n_bkt) return;
+  const int64_t p_min = ends[0];   // (k_splice_ends)
   const int64_t x = p_min + (k << NODE_BKT_SHIFT);
   int64_t lo = 0, hi = n;
   while (lo < hi) {
@@ -534,17 +540,12 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
                      (int64_t *)(small + 96));
   HIPCHK(ctx, hipGetLastError());
   HIPCHK(ctx, hipMemcpyAsync(hs + 8, small + 64, 64, hipMemcpyDeviceToHost, st));   // err at + 64, ends at + 96
+  // (read after the N-run count's synchronisation below: the kernels in between take p_min from the device and
+  // skip an erroneous splice)
+  const int64_t *d_ends = (const int64_t *)(small + 96);
+  int64_t p_min = 0, p_last = 0, nl_last = 0;
 
   // --- haplotype bytes ---------------------------------------------------------------------------------------
-  SYNCCHK(ctx, hipStreamSynchronize(st));
-  const int64_t ps0 = hs[12], psl = hs[13], nll = hs[14];
-  const int32_t herr = (int32_t)(hs[8] & 0xffffffff);
-  if (herr) {
-    stage_end(ctx);
-    return arg_fail(ctx, MH_E_ARG, herr & 1 ? "variant beyond the end of the fetched reference region"
-                                            : "SNP/INS alt length inconsistent with its op");
-  }
-  int64_t p_min = ps0;
   if (hap_len >= ((int64_t)1 << 32) - 1) {   // (the N-run boundaries are sorted as u32 positions)
     stage_end(ctx);
     return arg_fail(ctx, MH_E_ARG, "haplotype of 2^32 - 1 bases or more");
@@ -565,14 +566,14 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     const int64_t n_bkt = ((hap_len + 2048) >> NODE_BKT_SHIFT) + 1;   // keys reach at most p_min + hap_len + 1
     MH_TRY(ensure(ctx, h.bkt, 4 * (n_bkt + 2)));
     hipLaunchKernelGGL(k_node_buckets, dim3(grid_for(n_bkt + 1, 256, INT32_MAX)), dim3(256), 0, st,
-                       (const int64_t *)h.keys.p, n_nodes, p_min, n_bkt, (int32_t *)h.bkt.p);
+                       (const int64_t *)h.keys.p, n_nodes, d_ends, n_bkt, (int32_t *)h.bkt.p);
     HIPCHK(ctx, hipGetLastError());
     h.n_bkt = n_bkt;
   }
   if (hap_len > 0) {
     stage_begin(ctx, "splice_hap_copy");
     hipLaunchKernelGGL(k_hap_fill, dim3((unsigned)((hap_len + FILL_SPAN - 1) / FILL_SPAN)), dim3(256), 0, st, hap_len,
-                       p_min, n_nodes, (const Node16 *)h.nd.p, (const int64_t *)nsrc, (const int32_t *)h.bkt.p,
+                       d_ends, (const int32_t *)err, n_nodes, (const Node16 *)h.nd.p, (const int64_t *)nsrc, (const int32_t *)h.bkt.p,
                        h.n_bkt, (const uint8_t *)c.seq.p, d_pool, (uint8_t *)h.hap.p);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
@@ -594,15 +595,26 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
     for (int attempt = 0; attempt < 2; attempt++) {
       MH_TRY(ensure(ctx, b_nrun, 16 * (size_t)cap + 64));
       uint32_t *us = (uint32_t *)b_nrun.p, *ue = us + cap;
-      HIPCHK(ctx, hipMemsetAsync(cnt, 0, 16, st));
+      if (attempt) HIPCHK(ctx, hipMemsetAsync(cnt, 0, 16, st));   // (the first time: zeroed with `small`)
       const int64_t nel = hap_len / 64 + 1;
       hipLaunchKernelGGL(k_nrun_find, dim3(grid_for(nel, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)h.hap.p,
                          hap_len, cap, us, ue, cnt);
       HIPCHK(ctx, hipGetLastError());
-      HIPCHK(ctx, hipMemcpyAsync(hs + 12, cnt, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs + 16, cnt, 16, hipMemcpyDeviceToHost, st));
       SYNCCHK(ctx, hipStreamSynchronize(st));
-      hc[0] = (unsigned long long)hs[12];
-      hc[1] = (unsigned long long)hs[13];
+      if (attempt == 0) {   // the splice's error word and node ends, read back before the haplotype bytes
+        const int32_t herr = (int32_t)(hs[8] & 0xffffffff);
+        if (herr) {
+          stage_end(ctx);
+          return arg_fail(ctx, MH_E_ARG, herr & 1 ? "variant beyond the end of the fetched reference region"
+                                                  : "SNP/INS alt length inconsistent with its op");
+        }
+        p_min = hs[12];
+        p_last = hs[13];
+        nl_last = hs[14];
+      }
+      hc[0] = (unsigned long long)hs[16];
+      hc[1] = (unsigned long long)hs[17];
       if ((int64_t)hc[0] <= cap && (int64_t)hc[1] <= cap) break;
       cap = (int64_t)std::max(hc[0], hc[1]);   // more boundaries than room: once more with room for all
     }
@@ -642,7 +654,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
 
   h.n_nodes = n_nodes;
   h.p_min = p_min;
-  h.p_max = psl + nll;
+  h.p_max = p_last + nl_last;
   h.hap_len = hap_len;
   h.ref_start_pos = rs;
   h.valid = true;
