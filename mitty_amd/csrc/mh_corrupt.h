@@ -44,11 +44,10 @@ struct CorruptCfg {
 };
 
 // a ^ b ^ k in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96; the compiler emits two v_xor_b32 for
-// it).  k is wave-uniform (the Philox key schedule), so it is passed in an SGPR.
+// a ^ b ^ k).  The builtin, not inline asm: the compiler then knows the instruction's hazards (the asm form was
+// padded with s_nop, ~38 per block of the corruption rows) and schedules around it.
 __device__ __forceinline__ uint32_t xor3_vvs(uint32_t a, uint32_t b, uint32_t k) {
-  uint32_t d;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
-  return d;
+  return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {

@@ -1510,15 +1510,41 @@ __device__ __forceinline__ uint32_t cr_fine_walk(uint32_t e, const uint16_t *t16
   return c;
 }
 
-// One full block with the fine table in LDS, into registers (cr_block_rows' outputs): per base one bucket byte and
-// the Fp16 of its BQ decide (about 98 % of draws); the flagged buckets and the U2 draws on a threshold go to the
-// per-lane loop after the block.  bkf: base n0's row (row j at bkf + j * CF_ROW); t16: its T16 row (j * n_bq).
-__device__ __forceinline__ void cr_block_rows_f(const uint8_t *bkf, const uint16_t *t16, const uint16_t *fp,
-                                                const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f,
-                                                int n0, uint4 *qo, uint32_t *code) {
-  const int n_bq = cc.n_bq;
-  const uint32_t lim = n_bq < 93 ? (uint32_t)n_bq : 93u;
-  uint32_t W[CI_BLK], RW[CI_BLK / 3], E[CI_BLK], F[CI_BLK];
+// One flagged draw (a threshold inside its bucket, or U2 on Fp16[bq]) of base n0 + j, resolved alone: its triple's
+// draw again, the walk from the bucket entry, then the 16-bit U2 decision or the full 53-bit ones.  Returns the
+// quality byte (bq + 33) | the base's substitution code << 8 (choice + 1, 0: the base stays).  n0 is a multiple of 3
+// (15 * block).
+__device__ __forceinline__ uint32_t cr_px_resolve(const uint8_t *bkf, const uint16_t *t16, const uint16_t *fp,
+                                                  const CorruptCfg &cc, uint2 key, uint32_t tl, uint32_t th, int f,
+                                                  int n0, int j, uint32_t lim) {
+  const int n = n0 + j;
+  const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
+  const int k = j % 3;
+  const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
+  uint32_t amb;
+  const uint32_t bq = cr_fine_walk(bkf[j * CF_ROW + (w >> (16 + CF_SHIFT))], t16 + j * cc.n_bq, lim, w >> 16, &amb);
+  const uint32_t pth = fp[bq], h2 = w & 0xffffu;
+  const uint32_t x = amb || h2 == pth ? cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1,
+                                                      cc.c3, tl, th, f, n, w, bq, amb)
+                                      : bq | (h2 < pth ? 0x100u : 0u);
+  uint32_t code = 0;
+  if (x >> 8) {
+    const uint32_t c10 = (r.w >> (10 * k)) & 1023u;
+    code = 1u + (c10 == 1023u ? __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)n,
+                                                                   cc.c3), key).x, 3u)
+                              : c10 % 3u);
+  }
+  return ((x & 0xffu) + 33u) | code << 8;
+}
+
+// A full block's fast step with the fine table in LDS, into registers: per base one bucket byte and the Fp16 of its
+// BQ decide (about 98 % of draws).  Qualities + 33 into qd[4] (the flagged bases' bytes are placeholders), the
+// substituted bases into *ps, the flagged ones (left to the caller: cr_px_resolve) into *px; RW: the triples' fourth
+// words (the choice bits).  bkf: base n0's row (row j at bkf + j * CF_ROW).
+__device__ __forceinline__ void cr_block_fast(const uint8_t *bkf, const uint16_t *fp, const CorruptCfg &cc, uint2 key,
+                                              uint32_t tl, uint32_t th, int f, int n0, uint32_t *qd, uint32_t *ps_o,
+                                              uint32_t *px_o, uint32_t *RW) {
+  uint32_t W[CI_BLK], E[CI_BLK], F[CI_BLK];
   const uint32_t cw = ((uint32_t)f << 16) | (uint32_t)n0 / 3u;
 #pragma unroll
   for (int g = 0; g < CI_BLK / 3; g++) {
@@ -1541,29 +1567,22 @@ __device__ __forceinline__ void cr_block_rows_f(const uint8_t *bkf, const uint16
     const uint32_t qv = ((E[j] & 0x7fu) + 33u) << (8 * (j & 3));
     if (j < 4) qd0 |= qv; else if (j < 8) qd1 |= qv; else if (j < 12) qd2 |= qv; else qd3 |= qv;
   }
-  ps &= ~px;
-  while (px) {   // rare: a threshold in the bucket (walk), then the 16-bit U2 decision or the full 53-bit ones
-    const int j = __builtin_ctz(px);
-    px &= px - 1;
-    const int n = n0 + j;
-    const uint4 r = philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | ((uint32_t)n / 3u), cc.c3), key);
-    const int k = n % 3;
-    const uint32_t w = k == 0 ? r.x : k == 1 ? r.y : r.z;
-    uint32_t amb;
-    const uint32_t bq = cr_fine_walk(bkf[j * CF_ROW + (w >> (16 + CF_SHIFT))], t16 + j * n_bq, lim, w >> 16, &amb);
-    const uint32_t pth = fp[bq], h2 = w & 0xffffu;
-    uint32_t x;
-    if (amb || h2 == pth)
-      x = cq_exact_body(cc.cum, cc.phred, cc.guide, cc.max_bp, cc.n_bq, cc.k0, cc.k1, cc.c3, tl, th, f, n, w, bq, amb);
-    else
-      x = bq | (h2 < pth ? 0x100u : 0u);
-    const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = ((x & 0xffu) + 33u) << sh;
-    if (j < 4) qd0 = (qd0 & mk) | qv; else if (j < 8) qd1 = (qd1 & mk) | qv; else if (j < 12) qd2 = (qd2 & mk) | qv;
-    else qd3 = (qd3 & mk) | qv;
-    ps |= (x >> 8) << j;
-  }
-  *qo = make_uint4(qd0, qd1, qd2, qd3);
+  qd[0] = qd0;
+  qd[1] = qd1;
+  qd[2] = qd2;
+  qd[3] = qd3;
+  *ps_o = ps & ~px;
+  *px_o = px;
+}
+
+// The block's substitution codes (2 bits per base: choice + 1) from the triples' choice bits: randint(0, 3) as
+// c10 % 3, or (c10 == 1023, rejected) the base's own draw (t, f | 0x8000, n)
+__device__ __forceinline__ uint32_t cr_block_codes(uint32_t ps, const uint32_t *RW, const CorruptCfg &cc, uint2 key,
+                                                   uint32_t tl, uint32_t th, int f, int n0) {
   uint32_t cd = 0;
+#ifdef EW_CALIB_NOPS
+  ps = 0;
+#endif
   while (ps) {
     const int j = __builtin_ctz(ps);
     ps &= ps - 1;
@@ -1571,14 +1590,14 @@ __device__ __forceinline__ void cr_block_rows_f(const uint8_t *bkf, const uint16
     const uint32_t rw = g == 0 ? RW[0] : g == 1 ? RW[1] : g == 2 ? RW[2] : g == 3 ? RW[3] : RW[4];
     const uint32_t c10 = (rw >> (10 * k)) & 1023u;
     uint32_t chv;
-    if (c10 == 1023u)   // rejected: the base's own draw (t, f | 0x8000, n)
+    if (c10 == 1023u)
       chv = __umulhi(philox4x32_10(make_uint4(tl, th, ((uint32_t)f << 16) | 0x8000u | (uint32_t)(n0 + j), cc.c3),
                                    key).x, 3u);
     else
       chv = c10 % 3u;
     cd |= (chv + 1u) << (2 * j);
   }
-  *code = cd;
+  return cd;
 }
 
 
@@ -1587,9 +1606,29 @@ __device__ __forceinline__ void cr_block_rows_f(const uint8_t *bkf, const uint16
 // LDS-bound at 4.3 ms per chr1 unit, round 3), so occupancy is bound by registers, not LDS; its threads take
 // consecutive templates, so the slots it writes are contiguous.  The items, stream and decisions of k_cr_inplace,
 // over every block of every record up to rlen.
+//
+// The flagged draws (~2.2 % of draws: ~21 per wave and block) are resolved by the whole wave at once (round 5): a
+// lane looping over its own flagged bases ran the wave for the busiest of its 64 lanes (~2.2 Philox draws and walks
+// per block, a third of the kernel's vector instructions); instead each wave lists its (lane, base) items in LDS,
+// one lane takes one item (its draw, walk and decision), and writes the quality byte and the substitution bit back
+// into the owner's LDS slot.  A wave with more than CC_PX_CAP items (none seen; the tables would need far more
+// thresholds per bucket) resolves them lane by lane as before.
 constexpr int CC_THREADS = 256;
+constexpr int CC_WAVES = CC_THREADS / 64;
 constexpr int CC_PER_WG = 16 * CC_THREADS;   // templates per workgroup (2048 or 8192: within noise)
-__global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes) {
+constexpr int CC_PX_CAP = 64;
+struct CcWave {
+  uint4 qd[64];
+  uint32_t code[64];
+  uint16_t item[CC_PX_CAP];   // lane | base << 6
+};
+// the column tables' LDS, then the waves' item areas (16-aligned)
+__host__ __device__ constexpr size_t cc_tables_lds(int32_t n_bq) {
+  return ((size_t)CI_BLK * CF_ROW + 256 + (size_t)CI_BLK * n_bq * 2 + 15) / 16 * 16;
+}
+
+// at most 80 VGPRs (6 waves per SIMD; 87 unbounded, 5 waves): 2.7 % faster, one spilled word outside the loop
+__global__ void __launch_bounds__(CC_THREADS) __attribute__((amdgpu_waves_per_eu(6))) k_cr_cols(CiArgs A, uint4 *rows, uint32_t *codes) {
   const int32_t per_wg = CC_PER_WG;
   extern __shared__ __attribute__((aligned(16))) uint8_t ctab[];
   const CorruptCfg &cc = A.cc;
@@ -1597,7 +1636,7 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
   const int NB = (rlen + CI_BLK - 1) / CI_BLK;
   const int col = (int)blockIdx.y, f = col / NB, b = col - f * NB, n0 = CI_BLK * b;
   const int cnt = rlen - n0 < CI_BLK ? rlen - n0 : CI_BLK;
-  // LDS: fine bucket rows [15][CF_ROW] | Fp16[100] (256 B) | T16 rows [15][n_bq] (+16)
+  // LDS: fine bucket rows [15][CF_ROW] | Fp16[100] (256 B) | T16 rows [15][n_bq] | the waves' CcWave areas
   const int32_t o_fp = CI_BLK * CF_ROW, o_t16 = o_fp + 256;
   {
     const uint4 *src = (const uint4 *)(cc.bkf + ((int64_t)f * cc.max_bp + n0) * CF_ROW);
@@ -1611,19 +1650,82 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
   const uint8_t *bkf = ctab;
   const uint16_t *fp16 = (const uint16_t *)(ctab + o_fp);
   const uint16_t *t16 = (const uint16_t *)(ctab + o_t16);
+  const int lane = (int)(threadIdx.x & 63);
+  CcWave &cw = ((CcWave *)(ctab + cc_tables_lds(n_bq)))[threadIdx.x >> 6];
   const uint32_t lim = n_bq < 93 ? (uint32_t)n_bq : 93u;
   const uint2 key = make_uint2(cc.k0, cc.k1);
   const int64_t tb = (int64_t)blockIdx.x * per_wg, te = tb + per_wg < A.m ? tb + per_wg : A.m;
   uint4 *const orow = rows + (int64_t)col * A.m;
   uint32_t *const ocode = codes + (int64_t)col * A.m;
-  for (int64_t t = tb + threadIdx.x; t < te; t += CC_THREADS) {
+  // every wave runs the workgroup's trip count (the flagged draws are resolved wave-wide): lanes past te compute
+  // and store nothing
+  for (int64_t t0 = tb; t0 < te; t0 += CC_THREADS) {
+    const int64_t t = t0 + threadIdx.x;
+    const bool act = t < te;
     const int64_t tt = t + cc.t_base;
     const uint32_t tl = (uint32_t)tt, th = (uint32_t)(tt >> 32);
     uint4 qo;
     uint32_t code;
     if (cnt == CI_BLK) {
-      cr_block_rows_f(bkf, t16, fp16, cc, key, tl, th, f, n0, &qo, &code);
+      uint32_t qd[4], ps, px, RW[CI_BLK / 3];
+      cr_block_fast(bkf, fp16, cc, key, tl, th, f, n0, qd, &ps, &px, RW);
+      code = cr_block_codes(ps, RW, cc, key, tl, th, f, n0);   // the fast bases' codes (RW dies here)
+      if (!act) px = 0;
+#ifdef EW_CALIB_NOPX
+      px = 0;
+#endif
+      if (__ballot(px != 0)) {   // wave-uniform
+        // list the wave's flagged (lane, base) items
+        int total = 0;
+        for (uint32_t m = px;;) {
+          const uint64_t bal = __ballot(m != 0);
+          if (!bal) break;
+          if (m) {
+            const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (pos < CC_PX_CAP) cw.item[pos] = (uint16_t)(lane | __builtin_ctz(m) << 6);
+            m &= m - 1;
+          }
+          total += (int)__popcll(bal);
+        }
+        if (total <= CC_PX_CAP) {
+          cw.qd[lane] = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+          cw.code[lane] = code;
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+          if (lane < total) {
+            const uint32_t it = cw.item[lane];
+            const int src = (int)(it & 63u), j = (int)(it >> 6);
+            const int64_t ts = tt - lane + src;
+            const uint32_t x = cr_px_resolve(bkf, t16, fp16, cc, key, (uint32_t)ts, (uint32_t)(ts >> 32), f, n0, j, lim);
+            ((uint8_t *)&cw.qd[src])[j] = (uint8_t)x;
+            if (x >> 8) atomicOr(&cw.code[src], (x >> 8) << (2 * j));
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+          const uint4 q = cw.qd[lane];
+          qd[0] = q.x;
+          qd[1] = q.y;
+          qd[2] = q.z;
+          qd[3] = q.w;
+          code = cw.code[lane];
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
+        } else {
+          while (px) {   // the lane's own flagged bases, one by one
+            const int j = __builtin_ctz(px);
+            px &= px - 1;
+            const uint32_t x = cr_px_resolve(bkf, t16, fp16, cc, key, tl, th, f, n0, j, lim);
+            const uint32_t sh = 8u * (uint32_t)(j & 3), mk = ~(0xffu << sh), qv = (x & 0xffu) << sh;
+            if (j < 4) qd[0] = (qd[0] & mk) | qv; else if (j < 8) qd[1] = (qd[1] & mk) | qv;
+            else if (j < 12) qd[2] = (qd[2] & mk) | qv; else qd[3] = (qd[3] & mk) | qv;
+            code |= (x >> 8) << (2 * j);
+          }
+        }
+      }
+      qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
     } else {   // a short last block: per triple, per base (as corrupt_triple, into the slot)
+      if (!act) continue;
       uint32_t qd[4] = {0, 0, 0, 0}, cd = 0;
 #pragma unroll
       for (int g = 0; g < CI_BLK / 3; g++) {
@@ -1661,8 +1763,10 @@ __global__ void __launch_bounds__(CC_THREADS) k_cr_cols(CiArgs A, uint4 *rows, u
       qo = make_uint4(qd[0], qd[1], qd[2], qd[3]);
       code = cd;
     }
-    orow[t] = qo;
-    ocode[t] = code;
+    if (act) {
+      orow[t] = qo;
+      ocode[t] = code;
+    }
   }
 }
 
@@ -1680,7 +1784,7 @@ static int32_t launch_cr_rows(mh_ctx *ctx, hipStream_t st, int64_t m, int32_t nf
   if (m * nf * NB >= ((int64_t)1 << 31)) return arg_fail(ctx, MH_E_STATE, "corruption rows: bad shape");
   CiArgs A{0, 0, m, nullptr, nullptr, nullptr, nullptr, nullptr, {nullptr, nullptr}, nullptr, rlen, nf, 0, cc};
   stage_begin(ctx, "emit_corrupt_rows");
-  const size_t lds_c = (size_t)CI_BLK * CF_ROW + 256 + (size_t)CI_BLK * cc.n_bq * 2 + 16;
+  const size_t lds_c = cc_tables_lds(cc.n_bq) + CC_WAVES * sizeof(CcWave);
   const int64_t gx = (m + CC_PER_WG - 1) / CC_PER_WG;
   if (gx >= INT32_MAX || nf * NB > 65535) return arg_fail(ctx, MH_E_CAPACITY, "corruption rows: grid");
   hipLaunchKernelGGL(k_cr_cols, dim3((unsigned)gx, (unsigned)(nf * NB)), dim3(CC_THREADS), lds_c, st, A, rows, codes);
