@@ -1166,6 +1166,7 @@ int32_t mh_set_corruption(mh_ctx *ctx, int32_t enable, const double *cum_bq, int
   ctx->corrupt_T16_off = al16(ctx->corrupt_bk_off + bk.size());
   ctx->corrupt_Fp16_off = al16(ctx->corrupt_T16_off + 2 * nt);
   ctx->corrupt_bkf_off = al16(ctx->corrupt_Fp16_off + 2 * 100);
+  MH_TRY(sync_writers(ctx));   // queued writers and row passes may still read the previous tables
   MH_TRY(ensure(ctx, ctx->corrupt_cum, ctx->corrupt_bkf_off + bkf.size() + 64));
   MH_TRY(ensure(ctx, ctx->corrupt_phred, 8 * 100));
   char *base = (char *)ctx->corrupt_cum.p;
