@@ -150,8 +150,8 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1', world=1
 def corrupt_roofline(stages, kept, b1, b2, rlen):
   """The corruption pass, timed by HIP events on the writer stream.  Default (corruption rows): k_cr_cols, stage
   'emit_corrupt_rows', before each writer — per 15-base block one 16-byte row slot and one 4-byte code word written
-  (20 B per 15 bases); the writer (stage 'emit_write') lays them into the records.  MH_CR_ROWS=0: k_cr_recs +
-  k_cr_inplace, stage 'emit_corrupt', after each writer — per base one read (the block's bases) and one quality
+  (20 B per 15 bases); the writer (stage 'emit_write') lays them into the records.  In place (tables too large for
+  the row pass's LDS, or the LDS-image writer): k_cr_recs + k_cr_inplace, stage 'emit_corrupt', after each writer — per base one read (the block's bases) and one quality
   written, the substituted bases written back (4.7 % under hiseq-X-v2.5-Garvan), 8 bytes of record word read and one
   '\n' per record.  Either is bound by VALU issue (Philox rounds and the table walk), not by HBM."""
   rows = any(k == 'emit_corrupt_rows' for k, _ in stages)
