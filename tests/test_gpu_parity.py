@@ -868,25 +868,28 @@ def test_corruption_direct_writer_matches_lds_writer(native, monkeypatch, model)
     G.check_same(d2, l2, 'fastq2 (variant {})'.format(k))
 
 
-@pytest.mark.parametrize('tables,write2', [('lds', True), ('global', True), ('lds', False), ('stress', True)])
+@pytest.mark.parametrize('tables,write2', [('lds', True), ('global', True), ('lds', False), ('stress', True),
+                                           ('rlen250', True)])
 def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, write2):
   """Philox-mode corruption (the writer's len(seq) layout + k_cr_inplace) byte for byte against the numpy
   restatement of the draw scheme with full 53-bit uniforms (tests/philox_ref.py) applied to the perfect reads of the
   same sampling.  No N in the genome, so every template is kept and cnt - 1 is the template index; the bucket table
   from LDS and from global memory (MH_CR_GLOBAL), one and two FASTQ files.  'stress': a BQ table of 93 random
   thresholds per position, so ~9 % of draws land in a bucket holding one — waves with more flagged draws than the
-  row pass's LDS item list (its per-lane fallback), walks of several entries and the exact decisions all run."""
+  row pass's LDS item list (its per-lane fallback), walks of several entries and the exact decisions all run.
+  'rlen250': 2x250 reads of 1kg-pcr-free (16 full blocks and a short one of 10 bases per read)."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   from tests import philox_ref
   if tables == 'global':
     monkeypatch.setenv('MH_CR_GLOBAL', '1')
-  mdl = G.model('hiseq-X-v2.5-Garvan')
+  mdl = G.model('1kg-pcr-free' if tables == 'rlen250' else 'hiseq-X-v2.5-Garvan')
+  rlen = int(mdl['mean_rlen'])
   cum = mdl['cum_bq_mat']
   if tables == 'stress':
     cum = np.sort(np.random.default_rng(5).random(cum.shape), axis=2)
     cum[:, :, -1] = 1.0
-  p, _ = _native.read_model_params(150, 30.0)
+  p, _ = _native.read_model_params(rlen, 30.0)
   seq = synth.contig(400_000, 5, n_gaps=False)
   copies = synth.copies_soa(synth.variants(seq, 6))
   phred = 10 ** (-np.arange(100) / 10)
@@ -897,7 +900,7 @@ def test_philox_corruption_vs_numpy_restatement(native, monkeypatch, tables, wri
       if corrupt:
         eng.ctx.set_corruption(True, cum, phred, 3_000_000_099)
       eng.load_region(0, ('1', 0, len(seq)), seq)
-      eng.run_unit(0, 0, 1, 4711, copies[1], p, 150, mdl['cum_tlen'], 'S', write_fastq2=write2)
+      eng.run_unit(0, 0, 1, 4711, copies[1], p, rlen, mdl['cum_tlen'], 'S', write_fastq2=write2)
       outs.append(eng.ctx.fetch_output())
     finally:
       eng.close()
