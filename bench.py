@@ -65,9 +65,10 @@ def parse():
   ap.add_argument('--cpu-baseline-frac', type=float, default=0.25,
                   help='WGS leg of the CPU baseline: all 100 work units, each on the first FRAC of its region '
                        '(0 = skip)')
-  ap.add_argument('--cpu-workers', type=int, default=100,
+  ap.add_argument('--cpu-workers', type=int, default=0,
                   help='CPU baseline worker processes, the reference\'s --threads (SURVEY.md §8(d): min(host cores, '
-                       '#units) = 100 for the WGS job); a second WGS leg runs 16 (one GPU\'s CPU share on the box)')
+                       '#units)); 0 = the CPU share this process may use, measured (affinity, cgroup cpu.max); a side '
+                       'leg runs one process per unit (100) on that share, labelled')
   ap.add_argument('--verify', action='store_true',
                   help='wgs, N = 1: after the timed steps, run one more step unit by unit and compare every unit\'s '
                        'FASTQ bytes (sha256 of its arena range, both files) with the CPU oracle\'s digests')
@@ -144,7 +145,11 @@ def roofline(stages, kept, b1, b2, rlen, kernel, steps, workload='chr1', world=1
           'avg_launch_ms': ew_ms / max(ew_n, 1),
           'read_bytes_per_launch': hap_bytes / max(ew_n, 1),
           'read_only_achieved': read_gbs,
-          'read_only_frac': read_gbs / PEAK_HBM_GBS if read_gbs else None}, stage_ms, span_ms
+          'read_only_frac': read_gbs / PEAK_HBM_GBS if read_gbs else None,
+          # the north star's "HBM-read roofline" counts only the haplotype bytes read; the kernel also writes the FASTQ
+          # (W per template against R = 2 rlen read), so at the full 8 TB/s for R + W its read-only fraction would be
+          # R / (R + W): the highest read_only_frac this byte mix allows (DESIGN.md, round-6 performance)
+          'read_only_ceiling': hap_bytes / alg_bytes if alg_bytes else None}, stage_ms, span_ms
 
 
 def corrupt_roofline(stages, kept, b1, b2, rlen):
@@ -628,10 +633,16 @@ def run_genome(a, rank, world, local):
       e2e = end_to_end(a, seq1, recs1, model, None)
     if not a.no_cpu_baseline:
       legs = {}
+      share = effective_cpus()
       if a.cpu_baseline_frac > 0:
-        legs['wgs'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, a.cpu_workers)
-        if min(a.cpu_workers, os.cpu_count() or 1) > 16:
-          legs['wgs_16'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, 16)
+        # headline: one worker per usable core (min(cores, units)); side leg: one process per unit on
+        # the same share (time-shared), labelled
+        w = a.cpu_workers or share[0]
+        legs['wgs'] = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, w, share)
+        if len(units) > w:
+          side = cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, len(units), share)
+          side['note'] = 'one process per work unit, time-sharing the {} usable cores'.format(share[0])
+          legs['wgs_process_per_unit'] = side
       if a.cpu_baseline_mbp > 0:
         legs['chr1'] = cpu_baseline(a, seq1, recs1, p, rlen, model, _native.work_units(a.seed, [2], passes))
       if a.cpu_config0:
@@ -639,6 +650,11 @@ def run_genome(a, rank, world, local):
       cpu = legs.pop('wgs', None) or legs.pop('chr1', None)   # the metric's workload when it ran
       if cpu is not None:
         cpu.update(legs)
+        cpu['cpu_share'] = share[1]
+        ref = dict(REFERENCE_MEASURED)
+        if 'configs0' in legs:
+          ref['port_over_reference_configs0'] = legs['configs0']['value'] / ref['configs0_shape_threads2_templates_per_s']
+        cpu['reference_measured'] = ref
   if dist is not None:
     dist.destroy_process_group()
   if rank != 0:
@@ -697,7 +713,7 @@ def verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model):
   sys.path.insert(0, REPO)
   from oracle import oracle as O
   t0 = time.perf_counter()
-  workers = max(1, min(a.cpu_workers, os.cpu_count() or 1))
+  workers = max(1, a.cpu_workers or effective_cpus()[0])
   d = tempfile.mkdtemp(prefix='mh_verify_', dir='/dev/shm' if os.path.isdir('/dev/shm') else None)
   img = os.path.join(d, 'ref.bin')
   offs = {}
@@ -797,14 +813,56 @@ def _cpu_pool_run(jobs, workers):
   return n, dt, n / busy if busy > 0 else None
 
 
-def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, n_workers):
+def effective_cpus():
+  """The CPUs this process may actually use: the affinity mask, capped by the cgroup's CPU quota (cgroup v2
+  cpu.max, or v1 cpu.cfs_quota_us / cpu.cfs_period_us); without a quota, OMP_NUM_THREADS when the launcher sets it
+  (the GPU pool's per-job share).  Returns (cores, how) — `how` names what was read."""
+  aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+  quota, src = None, None
+  try:
+    with open('/sys/fs/cgroup/cpu.max') as fp:
+      q, per = fp.read().split()[:2]
+    if q != 'max':
+      quota, src = float(q) / float(per), 'cgroup v2 cpu.max {} {}'.format(q, per)
+  except (OSError, ValueError):
+    try:
+      with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fp:
+        q = int(fp.read())
+      with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fp:
+        per = int(fp.read())
+      if q > 0:
+        quota, src = q / per, 'cgroup v1 cfs quota {} / period {}'.format(q, per)
+    except (OSError, ValueError):
+      pass
+  parts = ['sched_getaffinity: {} CPUs'.format(aff), src or 'no cgroup CPU quota']
+  cores = aff
+  if quota is not None:
+    cores = max(1, min(aff, int(quota)))
+  else:
+    omp = os.environ.get('OMP_NUM_THREADS', '')
+    if omp.isdigit() and 0 < int(omp) < aff:
+      cores = int(omp)
+      parts.append('OMP_NUM_THREADS={} (the launcher\'s per-job CPU share)'.format(omp))
+  return cores, '; '.join(parts) + ' -> {} cores'.format(cores)
+
+
+# The reference's own rates, measured in the survey container (SURVEY.md §6: 8-vCPU Xeon, the reference with a
+# pysam shim, synthetic 2 Mbp genome): the port's configs[0] leg is quoted against the first
+REFERENCE_MEASURED = {
+  'configs0_shape_threads2_templates_per_s': 60.0e3,   # 1kg-pcr-free 2x250, --threads 2 (119,868 templates, 2.03 s)
+  'one_worker_templates_per_s': 43.7e3,                # hiseq-X-v2.5-Garvan 2x150, 1 worker (200,133 templates, 4.58 s)
+  'hardware': '8-vCPU Intel Xeon (survey container), the reference itself under a test-side pysam shim',
+  'source': 'SURVEY.md section 6'}
+
+
+def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, n_workers, share=None):
   """The metric's workload on the CPU: the CPU oracle (oracle/mitty_oracle.c, a scalar port of the reference path)
   laid out like the reference's multiprocessing path (`readgenerate.process_multi_threaded`: worker processes pulling
   work units, readgenerate.py:76-126) over all 100 work units of the 30x WGS job, in --cpu-workers processes.  Bounded
   sample: each unit runs on the first --cpu-baseline-frac of its region (same variants, same seeds), so the sample
   has the full job's unit list and topology.  Rate = templates / (last unit's end - first unit's start)."""
   frac = a.cpu_baseline_frac
-  workers = max(1, min(n_workers, os.cpu_count() or 1, len(units)))
+  workers = max(1, min(n_workers, len(units)))
   d = tempfile.mkdtemp(prefix='mh_cpu_', dir='/dev/shm' if os.path.isdir('/dev/shm') else None)
   img = os.path.join(d, 'ref.bin')
   try:
@@ -824,12 +882,12 @@ def cpu_baseline_wgs(a, contigs, data, units, p, rlen, model, n_workers):
     for f in glob.glob(os.path.join(d, '*')):
       os.remove(f)
     os.rmdir(d)
-  return {'value': n / dt, 'unit': 'templates/s', 'cores': workers, 'kind': 'port', 'per_core': per_core,
-          'host_cpus': os.cpu_count(), 'workload': 'wgs',
+  cores, how = share if share else (workers, 'workers')
+  return {'value': n / dt, 'unit': 'templates/s', 'cores': min(cores, workers), 'processes': workers, 'kind': 'port',
+          'per_core': per_core, 'host_cpus': os.cpu_count(), 'workload': 'wgs',
           'sample': 'the 30x WGS job\'s {} work units (25 regions x 2 copies x 2 passes, the reference\'s unit order '
-                    'and seeds), each on the first {:.0%} of its region, in {} oracle worker processes (min(host CPUs, '
-                    'units, {}); {} host CPUs visible): {} templates in {:.2f} s'.format(
-                        len(jobs), frac, workers, n_workers, os.cpu_count(), n, dt)}
+                    'and seeds), each on the first {:.0%} of its region, in {} oracle worker processes on this '
+                    'process\'s CPU share ({}): {} templates in {:.2f} s'.format(len(jobs), frac, workers, how, n, dt)}
 
 
 def synth_copies(recs, L):

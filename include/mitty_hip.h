@@ -207,6 +207,10 @@ int32_t mh_host_free(void *p);
  * created after another closed reuses blocks allocated while device memory was unfragmented; an allocation that
  * fails empties the cache first.  This frees every cached block now (*freed_bytes: their total). */
 int32_t mh_device_cache_trim(int64_t *freed_bytes);
+/* Bytes of the library's device blocks in use (not in the cache), process-wide, and their peak since the last reset
+ * (reset_peak != 0: the peak restarts from the current value after it is read).  Lets a caller check a bound such
+ * as mh_bam_set_capacity's. */
+int32_t mh_device_live_bytes(int64_t *live, int64_t *peak, int32_t reset_peak);
 
 /* rpc.generate_read for a batch of (p, l) on haplotype `slot`: positions, start/end nodes and the text fields.
  * Text outputs are concatenated; *_off arrays (n+1 entries) index them.  MH_E_CAPACITY if a text buffer is short
@@ -384,8 +388,17 @@ int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624);
 /* Emission kernel choice: 0 = direct writer (default; falls back to 1 for a unit whose qname reads part exceeds
  * 256 bytes, with fused corruption, or for sample names too long for its LDS layout), 1 = LDS-image writer always. */
 int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode);
-/* Fisher-Yates swap-index decode: 0 = chunk-parallel (default; falls back to 1 when the chunk starts do not reach
- * their fixed point), 1 = block-sequential always. */
+/* Fisher-Yates swap-index decode and its exact fallbacks, a bit set (0 = the default):
+ *   MH_DEC_SEQUENTIAL  the block-sequential decode always (by default it runs only when the chunk-parallel decode's
+ *                      starts do not reach their fixed point);
+ *   MH_DEC_FORCE_FIXUP every unit redone by the single-stream decode + per-unit permutation fix-up (by default only a
+ *                      unit whose decode ran out of words);
+ *   MH_DEC_FORCE_GEO   every unit redone with every geometric draw recomputed by the host libm (by default only the
+ *                      draws whose quotient lies within 1e-12 of an integer, illumina.py:66-76).
+ * The forcing bits exist so the tests can pin these rare paths against the oracle; they never change the output. */
+#define MH_DEC_SEQUENTIAL 1
+#define MH_DEC_FORCE_FIXUP 2
+#define MH_DEC_FORCE_GEO 4
 int32_t mh_set_decode_mode(mh_ctx *ctx, int32_t mode);
 /* Units the context redid on the exact sequential fallback path (decode out of words / near-integer quotient). */
 int32_t mh_fixup_count(mh_ctx *ctx, int64_t *n);

@@ -20,7 +20,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_selftest_scan_fault', 'mh_selftest_sort',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim', 'mh_device_live_bytes',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
@@ -140,6 +140,7 @@ def lib():
   _sig(L, 'mh_host_alloc', [c_i64, ctypes.POINTER(c_vp)])
   _sig(L, 'mh_host_free', [c_vp])
   _sig(L, 'mh_device_cache_trim', [ctypes.POINTER(c_i64)])
+  _sig(L, 'mh_device_live_bytes', [ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_i32])
   _sig(L, 'mh_read_batch', [c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                             c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64, c_vp, c_i64, c_vp, P_i64])
   _sig(L, 'mh_set_corruption', [c_vp, c_i32, c_vp, c_i32, c_i32, c_vp, c_u64])
@@ -327,6 +328,14 @@ def device_cache_trim():
   f = c_i64()
   lib().mh_device_cache_trim(ctypes.byref(f))
   return f.value
+
+
+def device_live_bytes(reset_peak=False):
+  """(live, peak) bytes of the library's device blocks in use (mh_device_live_bytes); reset_peak restarts the peak
+  from the live value after reading it."""
+  a, b = c_i64(), c_i64()
+  lib().mh_device_live_bytes(ctypes.byref(a), ctypes.byref(b), 1 if reset_peak else 0)
+  return a.value, b.value
 
 
 def bgzf_eof():

@@ -53,6 +53,10 @@ bool scan_fault_pending(const mh_ctx *ctx) {
   return h && __atomic_load_n(h + (ctx ? ctx->fault_slot : 0), __ATOMIC_ACQUIRE) != 0;
 }
 
+// a library thread working for ctx (the splice's second lane): its look-back scans report to ctx's fault word, which
+// its synchronisations (SYNCCHK) check — the entry-point guard sets this only for the calling thread
+void lane_thread_enter(mh_ctx *ctx) { scan_fault_slot = ctx->fault_slot; }
+
 int32_t scan_fault_fail(mh_ctx *ctx) {
   (void)scan_fault_take(ctx ? ctx->fault_slot : 0);
   return arg_fail(ctx, MH_E_STATE, "a look-back scan's wait timed out (a broken ticket base or scratch): its offsets "
@@ -72,8 +76,18 @@ struct CachedBlock {
 };
 std::mutex g_cache_mu;
 std::multimap<size_t, CachedBlock> g_cache;   // by capacity
+// bytes of the library's device blocks in use (handed out, not in the cache), and their peak (mh_device_live_bytes)
+std::atomic<int64_t> g_live{0}, g_live_peak{0};
+
+void live_add(int64_t d) {
+  const int64_t v = g_live.fetch_add(d) + d;
+  int64_t pk = g_live_peak.load();
+  while (v > pk && !g_live_peak.compare_exchange_weak(pk, v)) {
+  }
+}
 
 void cache_put(void *p, size_t cap) {
+  live_add(-(int64_t)cap);
   int dev = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceSynchronize();   // (what hipFree does: no kernel still reads or writes the block)
@@ -121,7 +135,10 @@ int64_t cache_trim(int dev) {   // dev < 0: every device's blocks
 }
 
 hipError_t dev_alloc(void **p, size_t bytes, size_t *cap) {
-  if ((*p = cache_take(bytes, cap))) return hipSuccess;
+  if ((*p = cache_take(bytes, cap))) {
+    live_add((int64_t)*cap);
+    return hipSuccess;
+  }
   hipError_t e = hipMalloc(p, bytes);
   if (e != hipSuccess) {   // the cache's blocks back to the device, then once more
     (void)hipGetLastError();
@@ -129,8 +146,12 @@ hipError_t dev_alloc(void **p, size_t bytes, size_t *cap) {
     (void)hipGetDevice(&dev);
     if (cache_trim(dev) > 0) e = hipMalloc(p, bytes);
   }
-  if (e == hipSuccess) *cap = bytes;
-  else *p = nullptr;
+  if (e == hipSuccess) {
+    *cap = bytes;
+    live_add((int64_t)bytes);
+  } else {
+    *p = nullptr;
+  }
   return e;
 }
 }  // namespace
@@ -485,15 +506,32 @@ int32_t mh_selftest_scan_fault(mh_ctx *ctx) {
   hipStream_t st = ctx->stream;
   const int64_t n = 2 * (int64_t)LB_TILE + 5;
   MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(n)));
+  MH_TRY(ensure(ctx, ctx->scan_partials2, scan_lb_scratch_bytes<int64_t>(n)));
   MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
   int64_t *tot = (int64_t *)((char *)ctx->d_small.p + 160);
   int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 168);
-  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
-  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadOne{}, StoreCheck{bad}, ctx->scan_partials.p, tot, true));
-  const int32_t rc = [&]() -> int32_t {
-    SYNCCHK(ctx, hipStreamSynchronize(st));
+  // the faulting scan on `s`, then its synchronisation: MH_E_STATE expected
+  auto fault_once = [&](hipStream_t s, void *scratch) -> int32_t {
+    HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, s));
+    HIPCHK(ctx, device_scan_sum<int64_t>(s, n, LoadOne{}, StoreCheck{bad}, scratch, tot, true));
+    SYNCCHK(ctx, hipStreamSynchronize(s));
     return MH_OK;
-  }();
+  };
+  // 1. from a lane thread (as the splice's second lane, mh_build_haplotypes_vset): its launches must report to this
+  // context's fault word, not to slot 0
+  int32_t rc_lane = MH_OK;
+  std::thread t1([&]() {
+    lane_thread_enter(ctx);
+    if (hipSetDevice(ctx->device) != hipSuccess) {
+      rc_lane = MH_E_HIP;
+      return;
+    }
+    rc_lane = fault_once(ctx->stream2, ctx->scan_partials2.p);
+  });
+  t1.join();
+  if (rc_lane != MH_E_STATE) return arg_fail(ctx, MH_E_HIP, "the timed-out scan of a lane thread was not reported");
+  // 2. from the calling thread
+  const int32_t rc = fault_once(st, ctx->scan_partials.p);
   if (rc != MH_E_STATE) return arg_fail(ctx, MH_E_HIP, "the timed-out scan was not reported");
   const std::string msg = ctx->err;
   HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
@@ -670,6 +708,7 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
       const VarSet &v1 = ctx->vsets[vsets[i0 + 1]];
       int32_t rc1 = MH_OK;
       std::thread t1([&]() {   // nothing may escape the lane's thread (std::terminate): errors become codes
+        lane_thread_enter(ctx);
         try {
           const hipError_t e = hipSetDevice(ctx->device);
           if (e != hipSuccess) {
@@ -1269,6 +1308,13 @@ int32_t mh_device_cache_trim(int64_t *freed_bytes) {
   return MH_OK;
 }
 
+int32_t mh_device_live_bytes(int64_t *live, int64_t *peak, int32_t reset_peak) {
+  if (live) *live = mh::g_live.load();
+  if (peak) *peak = mh::g_live_peak.load();
+  if (reset_peak) mh::g_live_peak.store(mh::g_live.load());
+  return MH_OK;
+}
+
 int32_t mh_host_free(void *p) {
   if (!p) return MH_OK;
   size_t n = 0;
@@ -1306,8 +1352,10 @@ int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode) {
 }
 
 int32_t mh_set_decode_mode(mh_ctx *ctx, int32_t mode) {
-  if (!ctx || mode < 0 || mode > 1) return MH_E_ARG;
-  ctx->decode_sequential = mode == 1;
+  if (!ctx || mode < 0 || mode > (MH_DEC_SEQUENTIAL | MH_DEC_FORCE_FIXUP | MH_DEC_FORCE_GEO)) return MH_E_ARG;
+  ctx->decode_sequential = (mode & MH_DEC_SEQUENTIAL) != 0;
+  ctx->force_fixup = (mode & MH_DEC_FORCE_FIXUP) != 0;
+  ctx->force_geo = (mode & MH_DEC_FORCE_GEO) != 0;
   return MH_OK;
 }
 
@@ -1461,19 +1509,29 @@ static int32_t gz_drain(mh_ctx *ctx) {
   return MH_OK;
 }
 
+// Window of a spilled store's deflate: a quarter of the store's capacity (two staging windows in HBM and two ring
+// slots of compressed output, each about a window: together about the capacity), whole BGZF blocks, at most 8192
+// blocks (535 MB)
+static int64_t spill_window(const BamStore &B) {
+  const int64_t cap_blocks = B.cap > 0 ? B.cap / 4 / BGZF_BLOCK : 8192;
+  return std::max<int64_t>(1, std::min<int64_t>(8192, cap_blocks)) * BGZF_BLOCK;
+}
+
 // A spilled store's sorted record stream deflated on the device window by window: the host assembles window i + 1
-// (bam_assemble, a thread of its own) while window i goes H2D and through bgzf_device into ctx->gz_out.  Windows
-// are whole numbers of BGZF blocks, so the blocks — and the file — are the ones one deflate of the whole stream
-// makes.  Window size: the store's capacity (bounded HBM) rounded down to blocks, at most 8192 blocks (535 MB).
-static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t *nz, std::vector<int64_t> *boff,
-                                   const std::function<void(int64_t, int64_t)> &on_piece) {
+// (bam_assemble, a thread of its own) while window i goes H2D and through bgzf_device into ring slot i & 1 of
+// ctx->gz_out (ring bytes per slot; pieces are reported at their ring offsets, the block offsets in `boff` are the
+// stream's).  Before window i overwrites its slot, slot_free(i) returns once the compressed pieces of window i - 2 have
+// left the device.  Windows are whole numbers of BGZF blocks, so the blocks — and the file — are the ones one deflate
+// of the whole stream makes.
+static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::vector<int64_t> *boff,
+                                   const std::function<void(int64_t, int64_t)> &on_piece,
+                                   const std::function<int32_t(int64_t)> &slot_free) {
   BamStore &B = ctx->bam;
   MH_TRY(bam_spill(ctx));   // (the records still in HBM: every record is then on the host)
   MH_TRY(bam_sort(ctx));    // (a no-op unless the spill undid a direct write's order)
   BamHostOrder o;
   MH_TRY(bam_host_order(ctx, o));
-  const int64_t cap_blocks = B.cap > 0 ? B.cap / BGZF_BLOCK : 8192;
-  const int64_t W = std::max<int64_t>(1, std::min<int64_t>(8192, cap_blocks)) * BGZF_BLOCK;
+  const int64_t W = spill_window(B);
   const int64_t n_win = (B.bytes + W - 1) / W;
   uint8_t *pin[2] = {nullptr, nullptr};
   struct PinGuard {
@@ -1531,10 +1589,12 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t *nz, std::vector<int64_t
     const int s = (int)(i & 1);
     const int64_t len = std::min(B.bytes, (i + 1) * W) - i * W;
     HIPCHK(ctx, hipMemcpyAsync(dwin[s], pin[s], (size_t)len, hipMemcpyHostToDevice, ctx->stream));
-    const std::function<void(int64_t, int64_t)> piece = [&](int64_t off, int64_t bytes) { on_piece(zpos + off, bytes); };
+    MH_TRY(slot_free(i));   // ring slot s: window i - 2's compressed pieces copied out
+    const int64_t zb = s * ring;
+    const std::function<void(int64_t, int64_t)> piece = [&](int64_t off, int64_t bytes) { on_piece(zb + off, bytes); };
     int64_t used = 0;
-    MH_TRY(bgzf_device(ctx, ctx->stream, dwin[s], len, (uint8_t *)ctx->gz_out.p + zpos,
-                       (int64_t)ctx->gz_out.cap - zpos, &used, &bw, &piece));   // (returns with the stream drained)
+    MH_TRY(bgzf_device(ctx, ctx->stream, dwin[s], len, (uint8_t *)ctx->gz_out.p + zb, ring, &used, &bw,
+                       &piece));   // (returns with the stream drained)
     {
       std::lock_guard<std::mutex> lk(mu);
       freed = i + 3;   // slot s (its H2D is done) takes window i + 2
@@ -1587,7 +1647,9 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     }
   } guard{ctx, &pieces};
   MH_TRY(gz_drain(ctx));
-  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)bgzf_device_bound(B.bytes)));
+  // a spilled (bounded) store deflates window by window into two ring slots; otherwise one buffer for the whole file
+  const int64_t ring = B.spilled > 0 ? bgzf_device_bound(spill_window(B)) : 0;
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)(ring ? 2 * ring : bgzf_device_bound(B.bytes))));
   const int64_t SLOT_B = (int64_t)1 << 26;
   for (auto &p : ctx->h_bam_pin)
     if (!p) HIPCHK(ctx, hipHostMalloc((void **)&p, (size_t)SLOT_B, hipHostMallocDefault));
@@ -1597,14 +1659,16 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
   std::atomic<int> werr{(int)hipSuccess};   // (set by either thread)
   std::string err;
-  bool wrote = false;
+  bool wrote = false, writer_done = false;
+  size_t pieces_out = 0;   // pieces whose bytes have all been copied off the device (the ring's slots reuse them)
   int64_t data_pos = 0, end_pos = 0;
   std::thread writer([&]() {
     (void)hipSetDevice(ctx->device);
     size_t item = 0;
     int64_t in_item = 0;
+    size_t slot_piece[2] = {0, 0};   // per staging slot: 1 + the piece its sub-piece ends, or 0
     // the next sub-piece (<= 64 MiB) of the queued pieces, waiting for the deflate to queue it
-    auto take = [&](int64_t *o, int64_t *m, hipEvent_t *ev) -> bool {
+    auto take = [&](int64_t *o, int64_t *m, hipEvent_t *ev, size_t *ends) -> bool {
       std::unique_lock<std::mutex> lk(mu);
       for (;;) {
         while (item < pieces.size() && in_item >= pieces[item].len) {
@@ -1620,12 +1684,13 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
       *m = std::min(SLOT_B, p.len - in_item);
       *ev = p.ev;
       in_item += *m;
+      *ends = in_item >= p.len ? item + 1 : 0;
       return true;
     };
     auto issue = [&](int s, int64_t *len) -> bool {   // a copy into slot s on stream2, behind its piece's pack
       int64_t o, m;
       hipEvent_t ev;
-      if (!take(&o, &m, &ev)) return false;
+      if (!take(&o, &m, &ev, &slot_piece[s])) return false;
       hipError_t e = hipStreamWaitEvent(ctx->stream2, ev, 0);
       if (e == hipSuccess) e = hipMemcpyAsync(pin[s], z + o, (size_t)m, hipMemcpyDeviceToHost, ctx->stream2);
       if (e != hipSuccess) {
@@ -1646,6 +1711,11 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
         return false;
       }
       const int s = cur;
+      if (slot_piece[s]) {   // that piece's last bytes are off the device: its ring space may be refilled
+        std::lock_guard<std::mutex> lk(mu);
+        pieces_out = std::max(pieces_out, slot_piece[s]);
+        cv.notify_all();
+      }
       *buf = pin[s];
       *len = len_cur;
       have = issue(s ^ 1, &len_next);   // the following sub-piece into the other slot, while this one is written
@@ -1657,6 +1727,9 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     if (!wrote) {   // drain what is in flight before the slots go
       (void)hipStreamSynchronize(ctx->stream2);
     }
+    std::lock_guard<std::mutex> lk(mu);
+    writer_done = true;
+    cv.notify_all();
   });
   const std::function<void(int64_t, int64_t)> on_piece = [&](int64_t off, int64_t bytes) {
     hipEvent_t ev = nullptr;
@@ -1668,16 +1741,26 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     std::lock_guard<std::mutex> lk(mu);
     pieces.push_back(Piece{off, ev ? bytes : 0, ev});
     if (!ev) werr = (int)hipErrorUnknown;
-    cv.notify_one();
+    cv.notify_all();
   };
-  const int32_t rc = B.spilled > 0 ? bam_deflate_spilled(ctx, &nz, &boff, on_piece)
+  std::vector<size_t> win_end;   // win_end[i]: pieces queued before window i
+  const std::function<int32_t(int64_t)> slot_free = [&](int64_t i) -> int32_t {
+    std::unique_lock<std::mutex> lk(mu);
+    win_end.push_back(pieces.size());
+    if (i < 2) return MH_OK;
+    const size_t need = win_end[(size_t)i - 1];   // every piece of windows <= i - 2
+    cv.wait(lk, [&] { return pieces_out >= need || writer_done || werr.load() != (int)hipSuccess; });
+    if (pieces_out < need) return arg_fail(ctx, MH_E_STATE, "BAM writer stopped before the deflate ring drained");
+    return MH_OK;
+  };
+  const int32_t rc = B.spilled > 0 ? bam_deflate_spilled(ctx, ring, &nz, &boff, on_piece, slot_free)
                                     : bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes,
                                                   (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &nz, &boff,
                                                   &on_piece);
   {
     std::lock_guard<std::mutex> lk(mu);
     fin = true;
-    cv.notify_one();
+    cv.notify_all();
   }
   writer.join();
   if (rc != MH_OK) return rc;

@@ -887,7 +887,13 @@ int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const 
   const int64_t add = ab[1] - ab[0];
   if (add < 0) return arg_fail(ctx, MH_E_ARG, "record offsets decrease");
   if (B.cap > 0 && B.bytes > B.spilled && B.bytes - B.spilled + add > B.cap) MH_TRY(bam_spill(ctx));
-  MH_TRY(ensure_keep(ctx, B.recs, B.bytes - B.spilled + add + 64, B.bytes - B.spilled));
+  if (ensure_keep(ctx, B.recs, B.bytes - B.spilled + add + 64, B.bytes - B.spilled) != MH_OK) {
+    // (as bam_add: when the records do not fit beside the resident ones, the resident ones go to the host first)
+    if (B.bytes == B.spilled) return MH_E_OOM;
+    ctx->err.clear();
+    MH_TRY(bam_spill(ctx));
+    MH_TRY(ensure_keep(ctx, B.recs, add + 64, 0));
+  }
   MH_TRY(ensure_keep(ctx, B.roff, sizeof(int64_t) * (B.n_rec + n + 1), sizeof(int64_t) * (B.n_rec + 1)));
   MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n), sizeof(uint64_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n), sizeof(uint32_t) * B.n_rec));

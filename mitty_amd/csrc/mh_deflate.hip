@@ -754,7 +754,9 @@ int32_t bgzf_device(mh_ctx *ctx, hipStream_t st, const uint8_t *d_in, int64_t n,
   *used = 0;
   const int64_t nb_all = (n + BLOCK - 1) / BLOCK;
   if (boff) boff->assign((size_t)nb_all + 1, 0);
-  const int64_t CH = 8192;   // blocks per launch (slots: CH x 72 KiB)
+  // blocks per launch (slots: CH x 72 KiB); no more than the input has, so a small window (a bounded BAM store's)
+  // does not allocate the scratch of 8192 blocks
+  const int64_t CH = std::max<int64_t>(1, std::min<int64_t>(8192, nb_all));
   MH_TRY(ensure(ctx, ctx->gz_slots, (size_t)CH * SLOT + 64));
   MH_TRY(ensure(ctx, ctx->gz_tok, sizeof(uint32_t) * (size_t)CH * DF_WAVES * TOK_WORDS + 64));
   MH_TRY(ensure(ctx, ctx->gz_info, sizeof(DfBlockInfo) * (size_t)CH + 64));

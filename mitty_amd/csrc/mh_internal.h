@@ -253,7 +253,9 @@ struct mh_ctx {
 
   // emission: emit_lds_only forces the LDS-image writer (A/B and fallback testing)
   bool emit_lds_only = false;
-  bool decode_sequential = false;   // mh_set_decode_mode(1): block-sequential shuffle decode only
+  bool decode_sequential = false;   // MH_DEC_SEQUENTIAL: block-sequential shuffle decode only
+  bool force_fixup = false;         // MH_DEC_FORCE_FIXUP: every unit through the single-stream decode fix-up
+  bool force_geo = false;           // MH_DEC_FORCE_GEO: every unit's geometric draws recomputed on the host
 
   // FASTQ arenas
   mh::DevBuf out1, out2;

@@ -1248,15 +1248,28 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
       hipLaunchKernelGGL(k_geo_array, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, n, w_tloc, p, log_q, fl, g);
       HIPCHK(ctx, hipMemcpyAsync(&nflag, d_flag, 4, hipMemcpyDeviceToHost, st));
       SYNCCHK(ctx, hipStreamSynchronize(st));
-      if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
-      std::vector<int64_t> idx(nflag);
-      if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
-      for (int64_t k : idx) {
-        uint32_t ww[2];
-        HIPCHK(ctx, hipMemcpy(ww, w_tloc + 2 * k, 8, hipMemcpyDeviceToHost));
+      auto host_geo = [&](const uint32_t *ww) {   // numpy legacy_random_geometric_inversion on the host libm
         double U = (((int32_t)(ww[0] >> 5)) * 67108864.0 + ((int32_t)(ww[1] >> 6))) / 9007199254740992.0;
-        int64_t gv = (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));   // the reference's libm
-        HIPCHK(ctx, hipMemcpy(g + k, &gv, 8, hipMemcpyHostToDevice));
+        return (int64_t)std::ceil(std::log1p(-U) / std::log(1.0 - p));
+      };
+      if (ctx->force_geo && p < 0.333333333333333333333333) {
+        // MH_DEC_FORCE_GEO (tests): every draw of the unit from the host libm, so this path is pinned against the
+        // oracle on whole units, not only on the rare draws the device flags
+        std::vector<uint32_t> hw(2 * (size_t)n);
+        std::vector<int64_t> hg((size_t)n);
+        HIPCHK(ctx, hipMemcpy(hw.data(), w_tloc, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < n; k++) hg[k] = host_geo(hw.data() + 2 * k);
+        HIPCHK(ctx, hipMemcpy(g, hg.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+      } else {
+        if (nflag > 1024) return arg_fail(ctx, MH_E_ARG, "too many near-integer geometric quotients");
+        std::vector<int64_t> idx(nflag);
+        if (nflag) HIPCHK(ctx, hipMemcpy(idx.data(), flag_idx, 8 * nflag, hipMemcpyDeviceToHost));
+        for (int64_t k : idx) {
+          uint32_t ww[2];
+          HIPCHK(ctx, hipMemcpy(ww, w_tloc + 2 * k, 8, hipMemcpyDeviceToHost));
+          int64_t gv = host_geo(ww);   // the reference's libm
+          HIPCHK(ctx, hipMemcpy(g + k, &gv, 8, hipMemcpyHostToDevice));
+        }
       }
       HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
       HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
@@ -1644,7 +1657,11 @@ static int32_t sample_tail(mh_ctx *ctx, SampleState &S, int64_t *out_n) {
   // ---- rare exact fix-ups: decode out of words (sequential stream), near-integer geometric quotients ------------
   for (int32_t u = 0; u < n_units; u++) {
     UnitPlan &q = plan[u];
-    if (q.n == 0 || (hstat[u] == 0 && hflag[u] == 0)) continue;
+    if (q.n == 0) continue;
+    // MH_DEC_FORCE_FIXUP / _GEO (tests): take the fallback for every unit
+    if (ctx->force_fixup) hstat[u] = 1;
+    if (ctx->force_geo) hflag[u] = 1;
+    if (hstat[u] == 0 && hflag[u] == 0) continue;
     if (rng_mode == MH_RNG_MITTY && hstat[u] != 0) {
       hipLaunchKernelGGL(k_shuffle_decode, dim3(1), dim3(SD_THREADS), 0, st, q.s_shuf, q.n, jall + q.j_off);
       HIPCHK(ctx, hipGetLastError());
@@ -1739,8 +1756,8 @@ int32_t tpl_resolve(mh_ctx *ctx, TplSet &ts) {
   SYNCCHK(ctx, hipEventSynchronize(S.ev[u]));
   const volatile int64_t *r = ctx->h_units + 4 * u;
   int64_t m = r[0];
-  const int64_t status = r[1];
-  const uint32_t flag = (uint32_t)r[2];
+  const int64_t status = ctx->force_fixup ? 1 : r[1];                // MH_DEC_FORCE_FIXUP (tests)
+  const uint32_t flag = ctx->force_geo ? 1u : (uint32_t)r[2];         // MH_DEC_FORCE_GEO (tests)
   HIPCHK(ctx, hipStreamWaitEvent(st, S.ev[u], 0));   // (the main stream's work on this set comes after its tail)
   if (status != 0 || flag != 0) {   // rare exact fix-up, as in sample_tail
     if (S.rng_mode == MH_RNG_MITTY && status != 0) {

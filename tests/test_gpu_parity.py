@@ -62,22 +62,65 @@ def test_templates_vs_oracle(native, model, span, seed):
   assert np.array_equal(r[1]['pos'], p1)
 
 
-@pytest.mark.parametrize('tail,div', [('0', '1'), ('0', '128'), ('4096', '512'), ('300000', '128'),
-                                      ('100000000', '128')])
-def test_templates_decode_tail_vs_oracle(native, monkeypatch, tail, div):
-  """The shuffle decode's tail cutoff (MH_DEC_TAIL: draws below it are decoded by k_decode_tail after the count
-  passes; 0 = no tail, 1e8 = the whole unit) and chunk sizing (MH_DEC_DIV: chunk words ~ i / div) never change the
-  templates."""
+DEC_MODES = {'sequential': 1, 'force_fixup': 2, 'force_geo': 4, 'all': 7}
+
+
+@pytest.mark.parametrize('mode', sorted(DEC_MODES))
+def test_templates_forced_fallbacks_vs_oracle(native, mode):
+  """The exact fallbacks that keep the templates bit-exact when the fast path cannot, each forced through the C ABI
+  (mh_set_decode_mode) on a 12 Mbp unit (illumina.py:66-76): the block-sequential decode (k_shuffle_decode2), the
+  single-stream decode + per-unit permutation fix-up (k_shuffle_decode, finish_unit), and every geometric draw
+  recomputed by the host libm (finish_unit's exact path).  Array-equal to the oracle; the fix-up modes must have run."""
   from mitty_amd.simulation import illumina
   from oracle import oracle as O
-  monkeypatch.setenv('MH_DEC_TAIL', tail)
-  monkeypatch.setenv('MH_DEC_DIV', div)
   mdl = G.model('hiseq-X-v2.5-Garvan')
   rm = illumina.read_model_params(mdl, 30.0)
-  r = illumina.generate_reads(rm, 500, 500 + 12_000_000, 2024)
+  ctx = illumina.device_context()
+  fix0 = ctx.fixup_count()
+  ctx.set_decode_mode(DEC_MODES[mode])
+  try:
+    r = illumina.generate_reads(rm, 500, 500 + 12_000_000, 2024)
+  finally:
+    ctx.set_decode_mode(0)
+  fixed = ctx.fixup_count() - fix0
   fo, p0, p1 = O.generate_templates(rm['p'], int(rm['rlen']), mdl['cum_tlen'], 500, 500 + 12_000_000, 2024)
   assert np.array_equal(r[0]['pos'], p0) and np.array_equal(r[1]['pos'], p1)
   assert np.array_equal(r[0]['file_order'], fo)
+  assert fixed == (0 if mode == 'sequential' else 1)
+
+
+@pytest.mark.parametrize('mode', sorted(DEC_MODES))
+def test_batched_units_forced_fallbacks_vs_oracle(native, mode):
+  """The same forced fallbacks on a batched multi-unit job (the batch permutation, the asynchronous per-unit tails
+  resolved by the emission): every unit's FASTQ equal to the oracle's, every unit redone by the fix-up modes."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 30.0)
+  L = 3_000_000
+  seq = synth.contig(L, 71)
+  copies = synth.copies_soa(synth.variants(seq, 72))
+  units = _native.work_units(5, [2], passes)
+  eng = Engine(0)
+  try:
+    eng.ctx.set_decode_mode(DEC_MODES[mode])
+    eng.load_region(0, ('7', 0, L), seq)
+    res = eng.run_units([(ps, ri, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)], lambda r, c: copies[c], p,
+                        150, mdl['cum_tlen'], 'SYN')
+    d1, d2 = eng.ctx.fetch_output()
+    fix = eng.ctx.fixup_count()
+  finally:
+    eng.close()
+  o1, o2 = [], []
+  for ps, (ri, cpy, sd) in enumerate(units):
+    k, b1, b2 = O.generate_unit_soa(seq, 0, copies[cpy], p, 150, mdl['cum_tlen'], sd, 'SYN:0:{}'.format(ps), '7', cpy)
+    assert res[ps][1] == k and k > 1000
+    o1.append(b1)
+    o2.append(b2)
+  G.check_same(d1, b''.join(o1))
+  G.check_same(d2, b''.join(o2))
+  assert fix == (0 if mode == 'sequential' else len(units))
 
 
 def test_templates_high_coverage_vs_oracle(native):
@@ -387,7 +430,7 @@ def test_batched_units_vs_oracle(native):
     o2.append(b2)
   G.check_same(d1, b''.join(o1))
   G.check_same(d2, b''.join(o2))
-  assert fix <= 1
+  assert fix <= 1   # (the exact fallbacks are forced and pinned in test_*_forced_fallbacks_vs_oracle)
 
 
 def test_lsd_sort_repeated_batches(native):
@@ -523,9 +566,10 @@ def test_resident_variants_and_buffer_reuse(native):
       G.check_same(d2, e2, 'fastq2 copy {}'.format(cpy))
 
 
-def test_two_lane_splice_matches_one_lane(native, monkeypatch):
+def test_two_lane_splice_matches_one_lane(native):
   """Both copies spliced side by side (mh_build_haplotypes_vset: second stream, second host thread, its own scratch)
-  give the nodes, haplotype bytes and FASTQ of one-at-a-time builds, over two contigs and a rebuild after a drop."""
+  give the nodes, haplotype bytes and FASTQ of one-at-a-time builds (mh_build_haplotype_vset per copy), over two
+  contigs and a rebuild after a drop."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   mdl = G.model('hiseq-X-v2.5-Garvan')
@@ -533,12 +577,9 @@ def test_two_lane_splice_matches_one_lane(native, monkeypatch):
   seqs = [synth.contig(3_000_000, 51), synth.contig(2_000_000, 52)]
   copies = [synth.copies_soa(synth.variants(sq, 53 + i)) for i, sq in enumerate(seqs)]
   units = [(0, 0, 0, 61), (1, 0, 1, 62), (2, 1, 0, 63), (3, 1, 1, 64)]
+  keys = [(ri, cpy) for ri in (0, 1) for cpy in (0, 1)]
 
   def run(one_lane):
-    if one_lane:
-      monkeypatch.setenv('MH_SPLICE_ONE_LANE', '1')
-    else:
-      monkeypatch.delenv('MH_SPLICE_ONE_LANE', raising=False)
     eng = Engine(0)
     try:
       for ri, sq in enumerate(seqs):
@@ -549,8 +590,13 @@ def test_two_lane_splice_matches_one_lane(native, monkeypatch):
       for _ in range(2):
         eng.drop_haplotypes()
         eng.ctx.reset_output()
+        if one_lane:   # every copy built alone first, so run_units' two-lane build finds nothing to do
+          for ri, cpy in keys:
+            eng.haplotype(ri, cpy, None)
+        else:
+          eng.haplotypes(keys)
         res = eng.run_units(units, lambda ri, c: copies[ri][c], p, 150, mdl['cum_tlen'], 'SYN')
-        nodes = [eng.ctx.get_nodes(*eng.haplotype(ri, cpy, None)[:2]) for ri in (0, 1) for cpy in (0, 1)]
+        nodes = [eng.ctx.get_nodes(*eng.haplotype(ri, cpy, None)[:2]) for ri, cpy in keys]
         out.append((res, nodes, eng.ctx.fetch_output()))
       return out
     finally:
@@ -608,9 +654,10 @@ def test_pipelined_jobs_match_isolated_runs(native):
   G.check_same(b2, a2, 'fastq2')
 
 
-def test_deferred_prepare_matches_waiting_prepare(native, monkeypatch):
-  """mh_emit_prepare with null outputs (no host round trip; totals read back when the writer is queued) gives the
-  bytes and counts of the waiting form, and the waiting form's returned totals are the writer's."""
+def test_deferred_prepare_matches_waiting_prepare(native):
+  """mh_emit_prepare with null outputs (no host round trip; totals read back when the writer is queued), with
+  outputs (the waiting form) and no prepare at all (emit_reads measures itself) give the same bytes and counts, and
+  the waiting form's returned totals are the writer's."""
   from mitty_amd import _native, synth
   from mitty_amd.engine import Engine
   mdl = G.model('hiseq-X-v2.5-Garvan')
@@ -618,37 +665,37 @@ def test_deferred_prepare_matches_waiting_prepare(native, monkeypatch):
   L = 3_000_000
   seq = synth.contig(L, 41)
   copies = synth.copies_soa(synth.variants(seq, 42))
-  units = [(0, 0, 0, 51), (1, 0, 1, 52), (2, 0, 0, 53), (3, 0, 1, 54)]
+  units = [(0, 0, 51), (1, 1, 52), (2, 0, 53), (3, 1, 54)]
 
-  def run(wait):
-    if wait:
-      monkeypatch.setenv('MH_PREP_WAIT', '1')
-    else:
-      monkeypatch.delenv('MH_PREP_WAIT', raising=False)
+  def run(form):
     eng = Engine(0)
     try:
       eng.load_region(0, ('1', 0, L), seq)
-      res = eng.run_units(units, lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'SYN')
+      res = []
+      for ps, cpy, sd in units:
+        slot = eng.haplotype(0, cpy, copies[cpy])[0]
+        eng.ctx.sample_units([ps], [slot], [sd], p, 150, mdl['cum_tlen'])
+        eng.ctx.use_templates(ps)
+        stub = 'SYN:0:{}'.format(ps)
+        got = None
+        if form == 'wait':
+          got = eng.ctx.emit_prepare(slot, stub, '1', cpy, True, unit_key=sd)
+        elif form == 'deferred':
+          assert eng.ctx.emit_prepare(slot, stub, '1', cpy, True, unit_key=sd, wait=False) is None
+        r = eng.ctx.emit_reads(slot, stub, '1', cpy, True, unit_key=sd)
+        if got is not None:
+          assert got == r
+        res.append(r)
       return res, eng.ctx.fetch_output()
     finally:
       eng.close()
 
-  res_w, (w1, w2) = run(True)
-  res_d, (d1, d2) = run(False)
-  assert res_w == res_d and all(r[1] > 1000 for r in res_w)
-  G.check_same(d1, w1, 'fastq1')
-  G.check_same(d2, w2, 'fastq2')
-  # the waiting form's totals equal what the writer then reports
-  eng = Engine(0)
-  try:
-    eng.load_region(0, ('1', 0, L), seq)
-    slot = eng.haplotype(0, 0, copies[0])[0]
-    eng.ctx.sample_units([0], [slot], [51], p, 150, mdl['cum_tlen'])
-    eng.ctx.use_templates(0)
-    got = eng.ctx.emit_prepare(slot, 'SYN:0:0', '1', 0, True, unit_key=51)
-    assert got == eng.ctx.emit_reads(slot, 'SYN:0:0', '1', 0, True, unit_key=51)
-  finally:
-    eng.close()
+  res_w, (w1, w2) = run('wait')
+  for form in ('deferred', 'none'):
+    res_d, (d1, d2) = run(form)
+    assert res_w == res_d and all(r[0] > 1000 for r in res_w)
+    G.check_same(d1, w1, 'fastq1 ' + form)
+    G.check_same(d2, w2, 'fastq2 ' + form)
 
 
 # ---- the bench configuration (BASELINE configs[1]) at full size -----------------------------------------------------
@@ -1163,9 +1210,9 @@ def test_god_aligner_spilled_store_vs_oracle(native, model, gpu_bgzf, tmp_path):
 
 
 def test_god_aligner_spill_from_device_arenas(native, tmp_path):
-  """The configs[4] path (records straight from the FASTQ arenas, mh_bam_add_output) over a bounded store: two
-  generate-reads jobs appended (the second add spills the first's records), the device-deflated file equal to the
-  unbounded store's."""
+  """The configs[4] path (records straight from the FASTQ arenas, mh_bam_add_output) over a bounded store: four
+  generate-reads jobs appended (each add spills the records before it), the device-deflated file equal to the
+  unbounded store's, and the write's device memory held near the bound."""
   from mitty_amd.engine import Engine
   from mitty_amd.lib import fasta as mfasta, vcfio
   from mitty_amd.readmodel import get_read_model
@@ -1185,18 +1232,32 @@ def test_god_aligner_spill_from_device_arenas(native, tmp_path):
         eng.load_region(ri, reg['region'], mfasta.fetch(seqs, *reg['region']))
       eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
       eng.ctx.bam_set_capacity(cap)
-      for job in range(2):
+      for job in range(4):
         eng.ctx.reset_output()
         eng.run_units(units, lambda r, cp: vdf[r]['copies'][cp], rm['p'], rm['rlen'], rm['cum_tlen'],
                       'S{}'.format(job))
         eng.ctx.bam_add_output()
       bam = str(tmp_path / 'c{}.bam'.format(cap))
+      eng.ctx.bam_sort()
+      native.device_cache_trim()
+      live0, _ = native.device_live_bytes(reset_peak=True)
       eng.ctx.bam_write_gpu(bam, '@HD\tVN:1.0\tSO:coordinate\n', bai_path=bam + '.bai')
-      out[cap] = (open(bam, 'rb').read(), open(bam + '.bai', 'rb').read(), eng.ctx.bam_spilled())
+      peak = native.device_live_bytes()[1] - live0
+      out[cap] = (open(bam, 'rb').read(), open(bam + '.bai', 'rb').read(), eng.ctx.bam_spilled(), peak,
+                  eng.ctx.bam_records())
     finally:
       eng.close()
   assert out[0][2] == (0, 0) and out[200_000][2][1] >= 2
   assert out[0][0] == out[200_000][0] and out[0][1] == out[200_000][1]
+  # the bounded store's write stays near its bound: two staging windows and two deflate ring slots of
+  # one BGZF block each at this budget (a quarter of 200 kB is less than a 0xff00-byte block) plus the deflate's
+  # per-launch scratch for that block — not an output buffer for the whole record stream, as the unbounded store has
+  rec_bytes = out[200_000][4][1]
+  peaks = 'record bytes {}, write peak bounded {} / unbounded {}'.format(rec_bytes, out[200_000][3], out[0][3])
+  print(peaks)
+  assert rec_bytes > 2_500_000, peaks
+  assert out[200_000][3] < 1_000_000, peaks
+  assert out[0][3] > rec_bytes, peaks   # (the unbounded store: one output buffer for the whole file)
 
 
 def test_god_aligner_rejects_sequence_quality_mismatch(native, tmp_path):
