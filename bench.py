@@ -87,6 +87,9 @@ def parse():
                        'memory and the file is assembled window by window (mh_bam_set_capacity)')
   ap.add_argument('--tn-length', type=int, default=50_000_000,
                   help='--tumor-normal: contig length (a chr1 job at 90x of 2x250 does not fit one GPU with its BAM)')
+  ap.add_argument('--tn-genome', action='store_true',
+                  help='--tumor-normal --gpus N: the whole synthetic GRCh37 (lengths x --genome-scale) instead of one '
+                       '--tn-length contig')
   ap.add_argument('--workload', default='wgs', choices=['wgs', 'chr1'],
                   help='wgs: whole synthetic GRCh37 at every N (the metric; configs[3]); chr1: configs[1], N = 1')
   ap.add_argument('--genome-scale', type=float, default=1.0,
@@ -244,9 +247,12 @@ def main():
   local = int(os.environ.get('LOCAL_RANK', '0'))
   global PRIME_S
   a.prime_s = PRIME_S = prime_hbm(a, local)
+  if a.tumor_normal and world > 1:
+    run_tumor_normal_ranks(a, rank, world, local)
+    return
   if a.tumor_normal or a.workload == 'chr1':
     if world != 1:
-      sys.exit('bench.py: --tumor-normal and --workload chr1 are one-GPU configs')
+      sys.exit('bench.py: --workload chr1 is a one-GPU config')
     run_tumor_normal(a) if a.tumor_normal else run_chr1(a)
     return
   run_genome(a, rank, world, local)
@@ -447,6 +453,156 @@ def run_tumor_normal(a):
                               'from them (bam_file_gpu), per step'},
     'stage_ms': {k: round(v / a.steps, 3) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])},
     'setup_s': hbm_setup(),
+    'host_cpus': os.cpu_count()}), flush=True)
+
+
+def run_tumor_normal_ranks(a, rank, world, local):
+  """BASELINE configs[4] on N GPUs (one process per GPU, RCCL): the normal (30x) and tumor (60x) samples' work units
+  (2x250, 1kg-pcr-free) dealt to the ranks by LPT; per step every rank generates its units into its arenas, turns
+  them into BAM records on its GPU, partitions the records by coordinate range and the all-to-all (RCCL over xGMI)
+  moves each to its range's rank, which sorts its range in HBM (mitty_amd.distributed: no rank merges the others'
+  records).  After the timed steps the BAM and BAI are written once, every rank deflating its range's blocks on its
+  GPU (the per-step file leg in the line)."""
+  import torch
+  import torch.distributed as tdist
+  from mitty_amd import _native, synth
+  from mitty_amd import distributed as D
+  from mitty_amd.readmodel import get_read_model
+  _, model = get_read_model('1kg-pcr-free.pkl')
+  rlen = int(model['mean_rlen'])
+  contigs = synth.genome_contigs(a.genome_scale) if a.tn_genome else [('1', a.tn_length)]
+  samples = []
+  units = []   # (sample, ri, cpy, seed, ps)
+  for k, (name, cov) in enumerate((('NORMAL', 30.0), ('TUMOR', 60.0))):
+    p, passes = _native.read_model_params(rlen, cov)
+    samples.append((name, p))
+    for ps, (ri, cpy, s) in enumerate(_native.work_units(a.seed + k, [2] * len(contigs), passes)):
+      units.append((k, ri, cpy, s, ps))
+  weights = [contigs[ri][1] * samples[k][1] for k, ri, _, _, _ in units]
+  pieces = D.plan_pieces(weights, world, 'lpt')
+  mine = [i for i, pc in enumerate(pieces) if pc[3] == rank]
+  regions = sorted({units[i][1] for i in mine})
+  t_synth = time.perf_counter()
+  data = synth.genome_regions(contigs, regions, workers=max(1, a.synth_workers // world))
+  tumor = {ri: synth.copies_soa(synth.variants(data[ri][0], 3000 + ri)) for ri in regions}
+  t_synth = time.perf_counter() - t_synth
+  local = local % max(1, torch.cuda.device_count())
+  torch.cuda.set_device(local)
+  tdist.init_process_group(os.environ.get('MH_DIST_BACKEND', 'nccl'))
+  be = D.DeviceBackend(local)
+  eng = be.eng
+  for ri in regions:
+    name, length = contigs[ri]
+    seq, _, normal = data[ri]
+    for k, copies in enumerate((normal, tumor[ri])):
+      eng.load_region(2 * ri + k, (name, 0, length), seq)
+      for cpy in (0, 1):
+        eng.upload_variants(2 * ri + k, cpy, copies[cpy])
+  soa = lambda r, c: (data[r // 2][2] if r % 2 == 0 else tumor[r // 2])[c]
+  # this rank's batches: its units of one sample at a time (one read model per sampling batch), ~a.batch_draws each
+  batches = []
+  for k in (0, 1):
+    cur, draws = [], 0
+    for i in mine:
+      sk, ri, cpy, s, ps = units[i]
+      if sk != k:
+        continue
+      cur.append(i)
+      draws += contigs[ri][1] * samples[k][1] * 1.2
+      if draws >= a.batch_draws:
+        batches.append((k, cur))
+        cur, draws = [], 0
+    if cur:
+      batches.append((k, cur))
+  rounds = int(D._allgather_i64([len(batches)], world, None)[:, 0].max())   # (the exchange is collective)
+  refs = [(name, L) for name, L in contigs]
+  splitters = D.range_splitters([(name, 0, L) for name, L in contigs], refs, world)
+  cap = int(a.bam_hbm_gb * (1 << 30))
+  stats = {}
+  dev = 'cuda' if tdist.get_backend() == 'nccl' else 'cpu'
+  counts = torch.zeros(3, dtype=torch.int64, device=dev)
+
+  def step():
+    eng.drop_haplotypes()
+    be.bam_begin(refs, cap)
+    kept = b1 = b2 = 0
+    for r in range(rounds):
+      part = None
+      if r < len(batches):
+        k, idx = batches[r]
+        eng.ctx.reset_output()
+        res = eng.run_units([(units[i][4], 2 * units[i][1] + k, units[i][2], units[i][3]) for i in idx], soa,
+                            samples[k][1], rlen, model['cum_tlen'], samples[k][0], 0, True, 'mitty')
+        kept += sum(x[1] for x in res)
+        b1 += sum(x[2] for x in res)
+        b2 += sum(x[3] for x in res)
+        part = be.bam_partition(splitters, idx[0] << 32)
+      D._bam_exchange(be, part, world, None, stats)
+    be.rctx.bam_sort()
+    counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
+    tdist.all_reduce(counts)
+    return lambda: (kept, b1, b2)
+
+  for _ in range(a.warmup):
+    step()
+  eng.ctx.sync()
+  be.rctx.sync()
+  torch.cuda.synchronize()
+  tdist.barrier()
+  t0 = time.perf_counter()
+  kept = b1 = b2 = 0
+  for _ in range(a.steps):
+    k_, x1, x2 = step()()
+    kept, b1, b2 = kept + k_, b1 + x1, b2 + x2
+  eng.ctx.sync()
+  be.rctx.sync()
+  torch.cuda.synchronize()
+  tdist.barrier()
+  dt = time.perf_counter() - t0
+  t = torch.tensor([dt], dtype=torch.float64, device=dev)
+  tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+  dt = float(t.item())
+  n_rec, nbytes = be.bam_range()
+  tot = D.allreduce_i64([kept, b1, b2, n_rec, nbytes])
+  # the BAM file and its BAI from the last step's ranges (each rank deflates its blocks on its GPU)
+  path = os.path.join('/dev/shm' if os.path.isdir('/dev/shm') else tempfile.gettempdir(),
+                      'mh_tn_{}.bam'.format(os.environ.get('MASTER_PORT', '0')))
+  tdist.barrier()
+  t1 = time.perf_counter()
+  D._bam_write_ranges(be, rank, world, None, path, '@HD\tVN:1.0\tSO:coordinate\n', refs)
+  tdist.barrier()
+  file_s = time.perf_counter() - t1
+  file_bytes = os.path.getsize(path) if rank == 0 else 0
+  if rank == 0:
+    os.remove(path)
+    os.remove(path + '.bai')
+  be.close()
+  tdist.destroy_process_group()
+  if rank != 0:
+    return
+  ms_per_step = dt / a.steps * 1e3
+  per_step = tot[0] / a.steps
+  print(json.dumps({
+    'metric': 'paired 2x250 templates/s, tumor 60x + normal 30x mixed, + god-aligner BAM records sorted in HBM, '
+              '{} GPUs'.format(world),
+    'value': tot[0] / dt, 'unit': 'templates/s', 'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+    'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
+    'dtype': 'int64+u8', 'data': 'synthetic contigs + two independent synthetic variant sets (mitty_amd.synth)',
+    'config': {'workload': 'generate-reads tumor/normal mix (BASELINE configs[4]) on {} GPUs: {}'.format(
+                   world, 'whole GRCh37 (lengths x{})'.format(a.genome_scale) if a.tn_genome
+                   else '{} bp contig'.format(a.tn_length)),
+               'read_model': '1kg-pcr-free', 'coverage': {'TUMOR': 60, 'NORMAL': 30}, 'units': len(units),
+               'templates_per_step': per_step, 'bam_records_per_step': tot[3], 'rounds_per_step': rounds,
+               'parallelism': 'unit-shard (LPT) x{}, BAM by coordinate range (all-to-all)'.format(world),
+               'collective_backend': os.environ.get('MH_DIST_BACKEND', 'nccl')},
+    'bam_bytes_per_step': tot[4], 'fastq_bytes_per_step': (tot[1] + tot[2]) // a.steps,
+    'bam_store': {'hbm_capacity_bytes_per_rank': cap or None},
+    'bam_file_ranges': {'seconds': file_s, 'file_bytes': file_bytes, 'bai': True,
+                        'note': 'every rank deflates the blocks that start in its range on its GPU into a part file, '
+                                'the parts are copied into one BAM at their offsets, the BAI joined on rank 0'},
+    'with_bam_file': {'seconds_per_step': ms_per_step / 1e3 + file_s,
+                      'value': per_step / (ms_per_step / 1e3 + file_s), 'unit': 'templates/s'},
+    'setup_s': dict(synth_inputs=round(t_synth, 2), **hbm_setup()),
     'host_cpus': os.cpu_count()}), flush=True)
 
 

@@ -252,6 +252,10 @@ int32_t mh_bam_reset(mh_ctx *ctx);
  * host window by window (the GPU writer deflates each window on the device).  The file is byte-identical to the
  * unbounded store's.  mh_bam_spilled: bytes and host blocks spilled so far. */
 int32_t mh_bam_set_capacity(mh_ctx *ctx, int64_t bytes);
+/* Spilled records to unlinked temporary files in `dir` (mapped: the page cache holds them, and the kernel may write
+ * them back under memory pressure — samtools sort's temporary files) instead of anonymous host memory; NULL or ""
+ * = host memory (the default). */
+int32_t mh_bam_set_spill_dir(mh_ctx *ctx, const char *dir);
 int32_t mh_bam_spilled(mh_ctx *ctx, int64_t *bytes, int64_t *blocks);
 /* Store pieces across ranks (configs[4] on N GPUs: each rank builds the BAM records of its FASTQ pieces, rank 0's
  * store takes them in piece order and sorts and writes once — the reference's pysam.cat of the workers' fragments
@@ -270,6 +274,39 @@ int32_t mh_bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, con
  *   BAM file's size. */
 int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
                          const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes);
+/* ---- configs[4] across ranks: one coordinate range per rank (god_aligner.py:63-68,100-116: its workers' fragments,
+ * `samtools sort -m 2G -@N`'s external merge and pysam.index, without a single merging process) ------------------
+ *   mh_bam_partition       the store's records (one FASTQ piece's) by destination rank: dest = the number of the
+ *                          n_dest - 1 ascending `splitters` <= the record's sort key.  Packed into a library buffer,
+ *                          one segment per destination at seg_off[d] (n_dest + 1 entries), each laid out as records
+ *                          (seg_bytes[d], 8-aligned), seg_n[d] + 1 record offsets from the segment's records, seg_n[d]
+ *                          sort keys, seg_n[d] BAI infos (4 x int32), seg_n[d] ties (tie_base + the record's input
+ *                          index: the global input order); input order inside each segment
+ *   mh_bam_partition_fetch the packed segments to `out` (host or device memory, >= seg_off[n_dest] bytes)
+ *   mh_bam_import_tie      mh_bam_import with each record's tie: equal sort keys are ordered by tie, so pieces may
+ *                          arrive in any order (every import of the store gives ties, or none does)
+ *   mh_bam_sorted_head     the first `len` bytes of the sorted record stream (host memory)
+ *   mh_bam_write_part      the sorted stream from byte `skip`, then `tail` (host bytes: the head of the next ranks'
+ *                          ranges), deflated on the device into 0xff00-byte BGZF blocks and written to `path`: the
+ *                          header's block(s) first when header_len >= 0, the EOF marker when `eof`.  *out_blocks data
+ *                          blocks starting at *out_data_pos in the file, *out_bytes = the file's size; boff (>= blocks
+ *                          + 1 entries, or NULL) = each block's offset from *out_data_pos.  With skip = the bytes that
+ *                          complete the previous rank's last block, the parts concatenated are the one-rank file.
+ *   mh_bam_bai_runs        the BAI's raw plan of the sorted store (two calls: NULL arrays for the sizes): per run of
+ *                          consecutive records in one bin, (tid << 32 | bin, first record's data offset, end offset,
+ *                          records); per 16 kbp window of every reference (n_win in all) its first overlapping record's
+ *                          data offset or -1; per reference its window count.  Ranks' plans join into one BAI. */
+int32_t mh_bam_partition(mh_ctx *ctx, const uint64_t *splitters, int32_t n_dest, uint64_t tie_base, int64_t *seg_off,
+                         int64_t *seg_n, int64_t *seg_bytes);
+int32_t mh_bam_partition_fetch(mh_ctx *ctx, void *out, int64_t cap);
+int32_t mh_bam_import_tie(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *keys,
+                          const int32_t *info, const uint64_t *ties, int64_t n);
+int32_t mh_bam_sorted_head(mh_ctx *ctx, int64_t len, uint8_t *out);
+int32_t mh_bam_write_part(mh_ctx *ctx, const char *path, const char *header_text, int64_t header_len, int64_t skip,
+                          const uint8_t *tail, int64_t tail_len, int32_t eof, int64_t *out_blocks, int64_t *out_data_pos,
+                          int64_t *out_bytes, int64_t *boff, int64_t boff_cap);
+int32_t mh_bam_bai_runs(mh_ctx *ctx, int64_t *n_runs, int64_t *runs, int64_t runs_cap, int64_t *n_win, int64_t *win,
+                        int64_t win_cap, int64_t *ref_nwin);
 
 /* ---- VCF ingest (vcfio.load_variant_file / split_copies / parse, vcfio.py:51-126) ------
  * Host-only (no device): mh_vcf_open parses a plain or bgzipped VCF for one sample; mh_vcf_region runs the BED

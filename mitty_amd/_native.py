@@ -24,7 +24,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
-           'mh_bam_records', 'mh_bam_set_capacity', 'mh_bam_spilled', 'mh_bam_export', 'mh_bam_import', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
+           'mh_bam_records', 'mh_bam_set_capacity', 'mh_bam_set_spill_dir', 'mh_bam_spilled', 'mh_bam_export', 'mh_bam_import', 'mh_bam_sort', 'mh_bam_write', 'mh_bam_write_gpu', 'mh_bam_reset', 'mh_bam_partition', 'mh_bam_partition_fetch', 'mh_bam_import_tie', 'mh_bam_sorted_head', 'mh_bam_write_part', 'mh_bam_bai_runs', 'mh_corrupt_fastq', 'mh_bgzf_compress', 'mh_bgzf_eof', 'mh_bgzf_compress_device', 'mh_bgzf_compress_gpu', 'mh_output_bgzf',
            'mh_output_bgzf_range', 'mh_output_bgzf_pair', 'mh_output_bgzf_wait', 'mh_output_fetch_async',
            'mh_output_fetch_wait',
            'mh_vcf_open', 'mh_vcf_error', 'mh_vcf_close', 'mh_vcf_region', 'mh_vcf_copy', 'mh_vcf_filter',
@@ -113,6 +113,14 @@ def lib():
   _sig(L, 'mh_bam_spilled', [c_vp, P_i64, P_i64])
   _sig(L, 'mh_bam_export', [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp])
   _sig(L, 'mh_bam_import', [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64])
+  _sig(L, 'mh_bam_partition', [c_vp, c_vp, c_i32, ctypes.c_uint64, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_bam_set_spill_dir', [c_vp, ctypes.c_char_p])
+  _sig(L, 'mh_bam_partition_fetch', [c_vp, c_vp, c_i64])
+  _sig(L, 'mh_bam_import_tie', [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64])
+  _sig(L, 'mh_bam_sorted_head', [c_vp, c_i64, c_vp])
+  _sig(L, 'mh_bam_write_part', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i64, c_vp, c_i64, c_i32, P_i64,
+                                P_i64, P_i64, c_vp, c_i64])
+  _sig(L, 'mh_bam_bai_runs', [c_vp, P_i64, c_vp, c_i64, P_i64, c_vp, c_i64, c_vp])
   _sig(L, 'mh_bam_write', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_i32, ctypes.c_char_p, P_i64,
                            P_i64])
   _sig(L, 'mh_bam_write_gpu', [c_vp, ctypes.c_char_p, ctypes.c_char_p, c_i64, ctypes.c_char_p, P_i64, P_i64, P_i64])
@@ -357,6 +365,13 @@ def bam_piece_layout(n, nbytes):
   o_key = o_roff + 8 * (n + 1)
   o_info = o_key + 8 * n
   return o_roff, o_key, o_info, o_info + 16 * n
+
+
+def bam_part_layout(n, nbytes):
+  """Byte offsets of one destination's segment of mh_bam_partition (n records, nbytes of records): the packed piece
+  of bam_piece_layout, then n ties (uint64); returns (o_roff, o_key, o_info, o_tie, total)."""
+  o_roff, o_key, o_info, o_tie = bam_piece_layout(n, nbytes)
+  return o_roff, o_key, o_info, o_tie, o_tie + 8 * n
 
 
 def _ptr(a):
@@ -766,6 +781,10 @@ class Context:
     """HBM budget of the BAM record store (0: no limit); records past it spill to host memory."""
     self._chk(self._L.mh_bam_set_capacity(self._h, int(nbytes)))
 
+  def bam_set_spill_dir(self, path):
+    """Spill to unlinked temporary files in `path` (None: host memory)."""
+    self._chk(self._L.mh_bam_set_spill_dir(self._h, None if path is None else path.encode()))
+
   def bam_spilled(self):
     """(bytes, host blocks) of the record store spilled to host memory."""
     b, k = c_i64(), c_i64()
@@ -814,6 +833,57 @@ class Context:
 
   def bam_reset(self):
     self._chk(self._L.mh_bam_reset(self._h))
+
+  def bam_partition(self, splitters, tie_base):
+    """The store's records by destination rank (mh_bam_partition): returns (segment offsets [n_dest + 1], records
+    [n_dest], record bytes [n_dest]); the packed segments stay in the library until bam_partition_fetch."""
+    sp = np.ascontiguousarray(splitters, dtype=np.uint64)
+    nd = len(sp) + 1
+    off, n, nb = np.zeros(nd + 1, np.int64), np.zeros(nd, np.int64), np.zeros(nd, np.int64)
+    self._chk(self._L.mh_bam_partition(self._h, _ptr(sp) if len(sp) else None, nd, int(tie_base), _ptr(off), _ptr(n),
+                                       _ptr(nb)))
+    return off, n, nb
+
+  def bam_partition_fetch(self, ptr, cap):
+    """The packed segments to address ptr (host or device memory, cap bytes)."""
+    self._chk(self._L.mh_bam_partition_fetch(self._h, c_vp(ptr), int(cap)))
+
+  def bam_import_tie(self, n, nbytes, ptr):
+    """Append a segment of mh_bam_partition (bam_part_layout) at address ptr (host or device) with its ties."""
+    o_roff, o_key, o_info, o_tie, _ = bam_part_layout(n, nbytes)
+    self._chk(self._L.mh_bam_import_tie(self._h, c_vp(ptr), c_vp(ptr + o_roff), c_vp(ptr + o_key),
+                                        c_vp(ptr + o_info), c_vp(ptr + o_tie), int(n)))
+
+  def bam_sorted_head(self, n):
+    out = np.empty(max(int(n), 1), np.uint8)
+    self._chk(self._L.mh_bam_sorted_head(self._h, int(n), _ptr(out)))
+    return out[:int(n)].tobytes()
+
+  def bam_write_part(self, path, header_text=None, skip=0, tail=b'', eof=False):
+    """The sorted stream from `skip` plus `tail`, as BGZF blocks deflated on the device, to `path` (mh_bam_write_part).
+    Returns (blocks, data_pos, file bytes, block offsets [blocks + 1] from data_pos)."""
+    nb, dp, fb = c_i64(), c_i64(), c_i64()
+    h = header_text.encode() if header_text is not None else b''
+    t = np.frombuffer(tail, np.uint8) if len(tail) else None
+    args = (self._h, path.encode(), h, len(h) if header_text is not None else -1, int(skip), _ptr(t), len(tail),
+            1 if eof else 0, ctypes.byref(nb), ctypes.byref(dp), ctypes.byref(fb))
+    n_bytes = self.bam_records()[1]
+    cap = (n_bytes - int(skip) + len(tail)) // 0xff00 + 2
+    boff = np.zeros(cap, np.int64)
+    self._chk(self._L.mh_bam_write_part(*args, _ptr(boff), cap))
+    return nb.value, dp.value, fb.value, boff[:nb.value + 1]
+
+  def bam_bai_runs(self, n_refs):
+    """The BAI's raw plan of the sorted store (mh_bam_bai_runs): (runs int64 [n_runs, 4], windows int64 [n_win],
+    per-reference window counts)."""
+    nr, nw = c_i64(), c_i64()
+    self._chk(self._L.mh_bam_bai_runs(self._h, ctypes.byref(nr), None, 0, ctypes.byref(nw), None, 0, None))
+    runs = np.zeros(max(4 * nr.value, 4), np.int64)
+    win = np.zeros(max(nw.value, 1), np.int64)
+    rn = np.zeros(max(n_refs, 1), np.int64)
+    self._chk(self._L.mh_bam_bai_runs(self._h, ctypes.byref(nr), _ptr(runs), len(runs), ctypes.byref(nw), _ptr(win),
+                                      len(win), _ptr(rn)))
+    return runs[:4 * nr.value].reshape(-1, 4), win[:nw.value], rn[:n_refs]
 
   def bam_sort(self):
     """Coordinate-sort the record store in HBM (mh_bam_write reuses the result)."""

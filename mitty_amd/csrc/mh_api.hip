@@ -1522,8 +1522,10 @@ static int64_t spill_window(const BamStore &B) {
 // ctx->gz_out (ring bytes per slot; pieces are reported at their ring offsets, the block offsets in `boff` are the
 // stream's).  Before window i overwrites its slot, slot_free(i) returns once the compressed pieces of window i - 2 have
 // left the device.  Windows are whole numbers of BGZF blocks, so the blocks — and the file — are the ones one deflate
-// of the whole stream makes.
-static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::vector<int64_t> *boff,
+// of the whole stream makes.  The stream deflated is the sorted stream from byte `skip`, then `tail` (a range's part
+// of a file, mh_bam_write_part).
+static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t skip, const uint8_t *tail, int64_t tail_len,
+                                   int64_t *nz, std::vector<int64_t> *boff,
                                    const std::function<void(int64_t, int64_t)> &on_piece,
                                    const std::function<int32_t(int64_t)> &slot_free) {
   BamStore &B = ctx->bam;
@@ -1532,7 +1534,8 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::
   BamHostOrder o;
   MH_TRY(bam_host_order(ctx, o));
   const int64_t W = spill_window(B);
-  const int64_t n_win = (B.bytes + W - 1) / W;
+  const int64_t nb = B.bytes - skip, L = nb + tail_len;   // the stream: sorted [skip, bytes), then the tail
+  const int64_t n_win = (L + W - 1) / W;
   uint8_t *pin[2] = {nullptr, nullptr};
   struct PinGuard {
     uint8_t **p;
@@ -1557,8 +1560,12 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::
         cv.wait(lk, [&] { return stop || i < freed; });
         if (stop) return;
       }
-      const int64_t w0 = i * W, w1 = std::min(B.bytes, w0 + W);
-      bam_assemble(B, o, w0, w1, pin[i & 1], 16);
+      const int64_t v0 = i * W, v1 = std::min(L, v0 + W);
+      if (std::min(v1, nb) > v0) bam_assemble(B, o, skip + v0, skip + std::min(v1, nb), pin[i & 1], 16);
+      if (v1 > nb) {
+        const int64_t t0 = std::max(v0, nb);
+        std::memcpy(pin[i & 1] + (t0 - v0), tail + (t0 - nb), (size_t)(v1 - t0));
+      }
       std::lock_guard<std::mutex> lk(mu);
       ready = i + 1;
       cv.notify_all();
@@ -1587,7 +1594,7 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::
       cv.wait(lk, [&] { return ready > i; });
     }
     const int s = (int)(i & 1);
-    const int64_t len = std::min(B.bytes, (i + 1) * W) - i * W;
+    const int64_t len = std::min(L, (i + 1) * W) - i * W;
     HIPCHK(ctx, hipMemcpyAsync(dwin[s], pin[s], (size_t)len, hipMemcpyHostToDevice, ctx->stream));
     MH_TRY(slot_free(i));   // ring slot s: window i - 2's compressed pieces copied out
     const int64_t zb = s * ring;
@@ -1608,24 +1615,21 @@ static int32_t bam_deflate_spilled(mh_ctx *ctx, int64_t ring, int64_t *nz, std::
   return MH_OK;
 }
 
-extern "C" {
-
-int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
-                         const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes) {
-  CTX_GUARD(ctx);
-  BamStore &B = ctx->bam;
-  if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
-  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
-  MH_TRY(bam_sort(ctx));
-  const int64_t n = B.n_rec;
-  // the BAI's per-record half on the device (chunks and linear windows; only their offsets cross PCIe)
-  BaiPlan plan;
-  std::vector<int64_t> offs;
-  bool dev_plan = false;
-  if (bai_path) MH_TRY(bam_bai_plan(ctx, plan, offs, &dev_plan));
-  // the sorted records deflated on the device (k_bgzf_blocks) piece by piece; a writer thread copies each packed
-  // piece out (stream2, two page-locked 64 MiB slots) and writes it while the next piece deflates
+// The sorted store's record stream deflated on the device and written to `path`: the header's block(s) first (hdr
+// null: none), the stream from byte `skip` followed by `tail` (tail_len bytes, host memory) cut into 0xff00-byte BGZF
+// blocks, the EOF marker when `eof`.  A writer thread copies each packed piece out (stream2, two page-locked 64 MiB
+// slots) and writes it while the next piece deflates.  boff: the data blocks' offsets from data_pos (nblocks + 1).
+struct BamPart {
+  int64_t data_pos = 0, end_pos = 0, nz = 0;
   std::vector<int64_t> boff;
+};
+static int32_t bam_write_gpu_impl(mh_ctx *ctx, const char *path, const std::string *hdr, int64_t skip,
+                                  const uint8_t *tail, int64_t tail_len, bool eof, BamPart &P) {
+  BamStore &B = ctx->bam;
+  MH_TRY(bam_sort(ctx));
+  if (skip < 0 || skip > B.bytes || tail_len < 0 || (tail_len > 0 && !tail))
+    return arg_fail(ctx, MH_E_ARG, "BAM part: skip or tail out of range");
+  std::vector<int64_t> &boff = P.boff;
   int64_t nz = 0;
   struct Piece {
     int64_t off, len;
@@ -1647,21 +1651,21 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     }
   } guard{ctx, &pieces};
   MH_TRY(gz_drain(ctx));
+  const int64_t L = B.bytes - skip + tail_len;
   // a spilled (bounded) store deflates window by window into two ring slots; otherwise one buffer for the whole file
   const int64_t ring = B.spilled > 0 ? bgzf_device_bound(spill_window(B)) : 0;
-  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)(ring ? 2 * ring : bgzf_device_bound(B.bytes))));
+  MH_TRY(ensure(ctx, ctx->gz_out, (size_t)(ring ? 2 * ring : bgzf_device_bound(L))));
   const int64_t SLOT_B = (int64_t)1 << 26;
   for (auto &p : ctx->h_bam_pin)
     if (!p) HIPCHK(ctx, hipHostMalloc((void **)&p, (size_t)SLOT_B, hipHostMallocDefault));
   uint8_t *const pin[2] = {ctx->h_bam_pin[0], ctx->h_bam_pin[1]};
-  const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
-                                           B.ref_names, B.ref_len);
   const uint8_t *z = (const uint8_t *)ctx->gz_out.p;
   std::atomic<int> werr{(int)hipSuccess};   // (set by either thread)
   std::string err;
   bool wrote = false, writer_done = false;
   size_t pieces_out = 0;   // pieces whose bytes have all been copied off the device (the ring's slots reuse them)
   int64_t data_pos = 0, end_pos = 0;
+  const std::string no_header;
   std::thread writer([&]() {
     (void)hipSetDevice(ctx->device);
     size_t item = 0;
@@ -1723,7 +1727,7 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
       cur = s ^ 1;
       return true;
     };
-    wrote = bgzf_write_stream(bam_path, hdr, 6, next, &data_pos, &end_pos, err);
+    wrote = bgzf_write_stream(path, hdr ? *hdr : no_header, 6, next, &data_pos, &end_pos, err, eof);
     if (!wrote) {   // drain what is in flight before the slots go
       (void)hipStreamSynchronize(ctx->stream2);
     }
@@ -1753,10 +1757,22 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
     if (pieces_out < need) return arg_fail(ctx, MH_E_STATE, "BAM writer stopped before the deflate ring drained");
     return MH_OK;
   };
-  const int32_t rc = B.spilled > 0 ? bam_deflate_spilled(ctx, ring, &nz, &boff, on_piece, slot_free)
-                                    : bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p, B.bytes,
-                                                  (uint8_t *)ctx->gz_out.p, (int64_t)ctx->gz_out.cap, &nz, &boff,
-                                                  &on_piece);
+  int32_t rc = MH_OK;
+  if (B.spilled > 0) {
+    rc = bam_deflate_spilled(ctx, ring, skip, tail, tail_len, &nz, &boff, on_piece, slot_free);
+  } else {
+    // the tail after the sorted records (srecs keeps its bytes), then one deflate of [skip, bytes + tail_len)
+    if (tail_len > 0) {
+      rc = ensure_keep(ctx, B.srecs, (size_t)(B.bytes + tail_len + 64), (size_t)B.bytes);
+      if (rc == MH_OK &&
+          hipMemcpyAsync((uint8_t *)B.srecs.p + B.bytes, tail, (size_t)tail_len, hipMemcpyHostToDevice, ctx->stream) !=
+              hipSuccess)
+        rc = hip_fail(ctx, hipGetLastError(), "BAM part tail H2D", __FILE__, __LINE__);
+    }
+    if (rc == MH_OK)
+      rc = bgzf_device(ctx, ctx->stream, (const uint8_t *)B.srecs.p + skip, L, (uint8_t *)ctx->gz_out.p,
+                       (int64_t)ctx->gz_out.cap, &nz, &boff, &on_piece);
+  }
   {
     std::lock_guard<std::mutex> lk(mu);
     fin = true;
@@ -1767,8 +1783,34 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   if (werr.load() != (int)hipSuccess) return hip_fail(ctx, (hipError_t)werr.load(), "BAM D2H", __FILE__, __LINE__);
   if (!wrote) return arg_fail(ctx, MH_E_ARG, err);
   if (end_pos - data_pos != nz) return arg_fail(ctx, MH_E_STATE, "BAM: compressed bytes written differ (internal)");
-  std::vector<int64_t> coff(boff.size());
-  for (size_t b = 0; b < boff.size(); b++) coff[b] = data_pos + boff[b];
+  P.data_pos = data_pos;
+  P.end_pos = end_pos;
+  P.nz = nz;
+  return MH_OK;
+}
+
+extern "C" {
+
+int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_text, int64_t header_len,
+                         const char *bai_path, int64_t *out_records, int64_t *out_bytes, int64_t *out_file_bytes) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (!bam_path || (header_len > 0 && !header_text)) return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  MH_TRY(bam_sort(ctx));
+  const int64_t n = B.n_rec;
+  // the BAI's per-record half on the device (chunks and linear windows; only their offsets cross PCIe)
+  BaiPlan plan;
+  std::vector<int64_t> offs;
+  bool dev_plan = false;
+  if (bai_path) MH_TRY(bam_bai_plan(ctx, plan, offs, &dev_plan));
+  const std::string hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len),
+                                           B.ref_names, B.ref_len);
+  BamPart P;
+  MH_TRY(bam_write_gpu_impl(ctx, bam_path, &hdr, 0, nullptr, 0, true, P));
+  std::vector<int64_t> coff(P.boff.size());
+  for (size_t b = 0; b < P.boff.size(); b++) coff[b] = P.data_pos + P.boff[b];
+  std::string err;
   if (bai_path) {
     if (dev_plan) {
       if (!bai_emit(bai_path, plan, offs.data(), coff, err)) return arg_fail(ctx, MH_E_ARG, err);
@@ -1782,7 +1824,97 @@ int32_t mh_bam_write_gpu(mh_ctx *ctx, const char *bam_path, const char *header_t
   }
   if (out_records) *out_records = n;
   if (out_bytes) *out_bytes = B.bytes;
-  if (out_file_bytes) *out_file_bytes = end_pos + 28;
+  if (out_file_bytes) *out_file_bytes = P.end_pos + 28;
+  return MH_OK;
+}
+
+int32_t mh_bam_write_part(mh_ctx *ctx, const char *path, const char *header_text, int64_t header_len, int64_t skip,
+                          const uint8_t *tail, int64_t tail_len, int32_t eof, int64_t *out_blocks, int64_t *out_data_pos,
+                          int64_t *out_bytes, int64_t *boff, int64_t boff_cap) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (!path || !out_blocks || !out_data_pos || !out_bytes || (header_len > 0 && !header_text))
+    return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  std::string hdr;
+  if (header_len >= 0)
+    hdr = bam_header_bytes(std::string(header_text ? header_text : "", (size_t)header_len), B.ref_names, B.ref_len);
+  BamPart P;
+  MH_TRY(bam_write_gpu_impl(ctx, path, header_len >= 0 ? &hdr : nullptr, skip, tail, tail_len, eof != 0, P));
+  const int64_t nb = (int64_t)P.boff.size() - 1;
+  *out_blocks = nb;
+  *out_data_pos = P.data_pos;
+  *out_bytes = P.end_pos + (eof ? 28 : 0);
+  if (boff) {
+    if (boff_cap < nb + 1) return arg_fail(ctx, MH_E_CAPACITY, "block offset array too small");
+    std::memcpy(boff, P.boff.data(), 8 * (size_t)(nb + 1));
+  }
+  return MH_OK;
+}
+
+int32_t mh_bam_partition(mh_ctx *ctx, const uint64_t *splitters, int32_t n_dest, uint64_t tie_base, int64_t *seg_off,
+                         int64_t *seg_n, int64_t *seg_bytes) {
+  CTX_GUARD(ctx);
+  if (n_dest < 1 || (n_dest > 1 && !splitters) || !seg_off || !seg_n || !seg_bytes)
+    return arg_fail(ctx, MH_E_ARG, "null argument");
+  if (!ctx->bam.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
+  return bam_partition(ctx, splitters, n_dest, tie_base, seg_off, seg_n, seg_bytes);
+}
+
+int32_t mh_bam_partition_fetch(mh_ctx *ctx, void *out, int64_t cap) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if ((!out && B.send_bytes > 0) || cap < B.send_bytes) return arg_fail(ctx, MH_E_CAPACITY, "partition buffer too small");
+  if (B.send_bytes > 0) HIPCHK(ctx, hipMemcpyAsync(out, B.send.p, (size_t)B.send_bytes, hipMemcpyDefault, ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_bam_import_tie(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *keys,
+                          const int32_t *info, const uint64_t *ties, int64_t n) {
+  CTX_GUARD(ctx);
+  if (n < 0 || (n > 0 && (!roff || !keys || !info || !ties))) return arg_fail(ctx, MH_E_ARG, "null argument");
+  return bam_import(ctx, recs, roff, keys, info, n, ties);
+}
+
+int32_t mh_bam_sorted_head(mh_ctx *ctx, int64_t len, uint8_t *out) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (len < 0 || len > B.bytes || (len > 0 && !out)) return arg_fail(ctx, MH_E_ARG, "bad head length");
+  MH_TRY(bam_sort(ctx));
+  if (len == 0) return MH_OK;
+  if (B.spilled > 0) {
+    MH_TRY(bam_spill(ctx));
+    MH_TRY(bam_sort(ctx));
+    BamHostOrder o;
+    MH_TRY(bam_host_order(ctx, o));
+    bam_assemble(B, o, 0, len, out, 4);
+    return MH_OK;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(out, B.srecs.p, (size_t)len, hipMemcpyDeviceToHost, ctx->stream));
+  SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return MH_OK;
+}
+
+int32_t mh_bam_bai_runs(mh_ctx *ctx, int64_t *n_runs, int64_t *runs, int64_t runs_cap, int64_t *n_win, int64_t *win,
+                        int64_t win_cap, int64_t *ref_nwin) {
+  CTX_GUARD(ctx);
+  BamStore &B = ctx->bam;
+  if (!n_runs || !n_win) return arg_fail(ctx, MH_E_ARG, "null argument");
+  MH_TRY(bam_sort(ctx));
+  std::vector<int64_t> hr, hw, woff;
+  std::vector<uint32_t> hn;
+  bool ok = false;
+  MH_TRY(bam_bai_raw(ctx, hr, hw, hn, woff, &ok));
+  if (!ok) return arg_fail(ctx, MH_E_STATE, "BAI plan: records outside the references' lengths or not sorted");
+  *n_runs = (int64_t)hr.size() / 4;
+  *n_win = (int64_t)hw.size();
+  if (!runs || !win || !ref_nwin) return MH_OK;   // (the sizes only)
+  if (runs_cap < (int64_t)hr.size() || win_cap < (int64_t)hw.size()) return arg_fail(ctx, MH_E_CAPACITY, "BAI arrays");
+  std::memcpy(runs, hr.data(), 8 * hr.size());
+  std::memcpy(win, hw.data(), 8 * hw.size());
+  for (size_t t = 0; t < hn.size(); t++) ref_nwin[t] = hn[t];
+  (void)B;
   return MH_OK;
 }
 
@@ -1803,6 +1935,12 @@ int32_t mh_bam_sort(mh_ctx *ctx) {
   return bam_sort(ctx);
 }
 
+int32_t mh_bam_set_spill_dir(mh_ctx *ctx, const char *dir) {
+  if (!ctx) return MH_E_ARG;
+  ctx->bam.spill_dir = dir ? dir : "";
+  return MH_OK;
+}
+
 int32_t mh_bam_set_capacity(mh_ctx *ctx, int64_t bytes) {
   if (!ctx) return MH_E_ARG;
   if (bytes < 0) return arg_fail(ctx, MH_E_ARG, "capacity must be >= 0");
@@ -1817,6 +1955,7 @@ int32_t mh_bam_reset(mh_ctx *ctx) {
   ctx->bam.n_files = 0;
   ctx->bam.sorted = false;
   ctx->bam.direct = false;
+  ctx->bam.use_tie = false;
   return MH_OK;
 }
 

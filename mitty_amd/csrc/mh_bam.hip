@@ -17,6 +17,8 @@
 // ('>p:nI' -> 'nI'), MAPQ 60, flag = reverse | paired / proper / read1 / read2 for two files, mate = the other
 // read's tid / pos, TLEN 0, no tags, qname = file 1's read name.  bin = reg2bin(pos, bam_endpos) as htslib sets it.
 #include <rocprim/device/device_radix_sort.hpp>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -26,6 +28,7 @@
 #include "mh_bgzf.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
+#include "mh_sort.h"
 
 namespace mh {
 namespace {
@@ -465,6 +468,11 @@ __global__ void k_bam_keys(const BamTpl *tpl, int64_t n_rec, int32_t nr, uint64_
   val[i] = (uint32_t)i;
 }
 
+__global__ void k_gather_key(const uint64_t *key, const uint32_t *val, int64_t n, uint64_t *out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) out[k] = key[val[k]];
+}
+
 // sorted position k <- record val[k]
 struct LoadSortedSize {
   const uint32_t *val;
@@ -566,6 +574,7 @@ int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64
   B.n_files = 0;
   B.sorted = false;
   B.direct = false;
+  B.use_tie = false;
   bam_free_spill(B);
   B.refs_set = true;
   return MH_OK;
@@ -720,11 +729,31 @@ int32_t bam_sort(mh_ctx *ctx, const void *pa) {
   MH_TRY(ensure(ctx, B.val2, sizeof(uint32_t) * n));
   size_t tmp = 0;
   stage_begin(ctx, "bam_sort");
-  HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, (uint64_t *)B.key.p, (uint64_t *)B.key2.p, (uint32_t *)B.val.p,
-                                        (uint32_t *)B.val2.p, (size_t)n, 0u, end_bit, st));
+  const uint64_t *kin = (const uint64_t *)B.key.p;
+  const uint32_t *vin = (const uint32_t *)B.val.p;
+  if (B.use_tie) {
+    // records from several ranks: first in their global input order (the tie), then the stable key sort — equal
+    // keys keep the one-rank store's input order, whatever order the pieces arrived in
+    MH_TRY(ensure(ctx, B.tie2, sizeof(uint64_t) * n));
+    MH_TRY(ensure(ctx, B.tval, sizeof(uint32_t) * n));
+    MH_TRY(ensure(ctx, B.tkey, sizeof(uint64_t) * n));
+    size_t t2 = 0;
+    HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, t2, (uint64_t *)B.tie.p, (uint64_t *)B.tie2.p, (uint32_t *)B.val.p,
+                                          (uint32_t *)B.tval.p, (size_t)n, 0u, 64u, st));
+    MH_TRY(ensure(ctx, B.sort_tmp, t2 + 256));
+    HIPCHK(ctx, rocprim::radix_sort_pairs(B.sort_tmp.p, t2, (uint64_t *)B.tie.p, (uint64_t *)B.tie2.p,
+                                          (uint32_t *)B.val.p, (uint32_t *)B.tval.p, (size_t)n, 0u, 64u, st));
+    hipLaunchKernelGGL(k_gather_key, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint64_t *)B.key.p,
+                       (const uint32_t *)B.tval.p, n, (uint64_t *)B.tkey.p);
+    HIPCHK(ctx, hipGetLastError());
+    kin = (const uint64_t *)B.tkey.p;
+    vin = (const uint32_t *)B.tval.p;
+  }
+  HIPCHK(ctx, rocprim::radix_sort_pairs(nullptr, tmp, kin, (uint64_t *)B.key2.p, vin, (uint32_t *)B.val2.p, (size_t)n,
+                                        0u, end_bit, st));
   MH_TRY(ensure(ctx, B.sort_tmp, tmp + 256));
-  HIPCHK(ctx, rocprim::radix_sort_pairs(B.sort_tmp.p, tmp, (uint64_t *)B.key.p, (uint64_t *)B.key2.p,
-                                        (uint32_t *)B.val.p, (uint32_t *)B.val2.p, (size_t)n, 0u, end_bit, st));
+  HIPCHK(ctx, rocprim::radix_sort_pairs(B.sort_tmp.p, tmp, kin, (uint64_t *)B.key2.p, vin, (uint32_t *)B.val2.p,
+                                        (size_t)n, 0u, end_bit, st));
   stage_end(ctx);
   // sorted offsets, then the gather
   MH_TRY(ensure(ctx, B.soff, sizeof(int64_t) * (n + 1)));
@@ -873,12 +902,16 @@ int32_t bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *
 }
 
 int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *key, const int32_t *info,
-                   int64_t n) {
+                   int64_t n, const uint64_t *tie) {
   BamStore &B = ctx->bam;
   hipStream_t st = ctx->stream;
   if (!B.refs_set) return arg_fail(ctx, MH_E_STATE, "call mh_bam_set_refs first");
   if (B.direct) MH_TRY(bam_undirect(ctx));
   if (n <= 0) return MH_OK;
+  // ties: the records' global input order (pieces from several ranks, in any order); every import of a store gives
+  // them or none does
+  if (B.n_rec == 0) B.use_tie = tie != nullptr;
+  if (B.use_tie != (tie != nullptr)) return arg_fail(ctx, MH_E_ARG, "BAM import: tie order given for some pieces only");
   if (B.n_rec + n >= (int64_t)UINT32_MAX) return arg_fail(ctx, MH_E_CAPACITY, "more than 2^32 records in one BAM");
   int64_t ab[2] = {0, 0};
   HIPCHK(ctx, hipMemcpyAsync(ab, roff, 8, hipMemcpyDefault, st));
@@ -898,6 +931,10 @@ int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const 
   MH_TRY(ensure_keep(ctx, B.key, sizeof(uint64_t) * (B.n_rec + n), sizeof(uint64_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.val, sizeof(uint32_t) * (B.n_rec + n), sizeof(uint32_t) * B.n_rec));
   MH_TRY(ensure_keep(ctx, B.info, sizeof(RInfo) * (B.n_rec + n), sizeof(RInfo) * B.n_rec));
+  if (tie) {
+    MH_TRY(ensure_keep(ctx, B.tie, sizeof(uint64_t) * (B.n_rec + n), sizeof(uint64_t) * B.n_rec));
+    HIPCHK(ctx, hipMemcpyAsync((uint64_t *)B.tie.p + B.n_rec, tie, 8 * (size_t)n, hipMemcpyDefault, st));
+  }
   if (add) HIPCHK(ctx, hipMemcpyAsync((uint8_t *)B.recs.p + (B.bytes - B.spilled), recs, (size_t)add, hipMemcpyDefault, st));
   int64_t *ro = (int64_t *)B.roff.p + B.n_rec;
   HIPCHK(ctx, hipMemcpyAsync(ro, roff, 8 * (size_t)(n + 1), hipMemcpyDefault, st));
@@ -919,16 +956,32 @@ int32_t bam_spill(mh_ctx *ctx) {
   if (B.direct) MH_TRY(bam_undirect(ctx));
   const int64_t len = B.bytes - B.spilled;
   if (len <= 0) return MH_OK;
-  uint8_t *p = (uint8_t *)malloc((size_t)len);
+  uint8_t *p = nullptr;
+  const bool mapped = !B.spill_dir.empty();
+  if (mapped) {   // an unlinked temporary file (samtools sort -m's temporary files): the kernel may write it back
+    std::string tmpl = B.spill_dir + "/mitty_bam_spill_XXXXXX";
+    std::vector<char> path(tmpl.begin(), tmpl.end());
+    path.push_back('\0');
+    const int fd = mkstemp(path.data());
+    if (fd < 0) return arg_fail(ctx, MH_E_ARG, "BAM spill: cannot create a file in " + B.spill_dir);
+    unlink(path.data());
+    void *m = MAP_FAILED;
+    if (ftruncate(fd, (off_t)len) == 0) m = mmap(nullptr, (size_t)len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return arg_fail(ctx, MH_E_OOM, "BAM spill: cannot map " + std::to_string(len) + " bytes");
+    p = (uint8_t *)m;
+  } else {
+    p = (uint8_t *)malloc((size_t)len);
+  }
   if (!p) return arg_fail(ctx, MH_E_OOM, "host memory for spilled BAM records (" + std::to_string(len) + " bytes)");
   stage_begin(ctx, "bam_spill");
   if (hipMemcpyAsync(p, B.recs.p, (size_t)len, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    free(p);
+    if (mapped) munmap(p, (size_t)len); else free(p);
     return hip_fail(ctx, hipGetLastError(), "BAM spill D2H", __FILE__, __LINE__);
   }
   stage_end(ctx);
-  B.spill.push_back(BamStore::HostBlock{p, B.spilled, B.bytes});
+  B.spill.push_back(BamStore::HostBlock{p, B.spilled, B.bytes, mapped});
   B.spilled = B.bytes;   // (the sort's order, offsets and info stay valid: only where the bytes live changed)
   return MH_OK;
 }
@@ -1068,64 +1121,16 @@ __global__ void k_bai_gather(const RInfo *info, const int64_t *soff, const uint3
 
 int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, bool *ok) {
   BamStore &B = ctx->bam;
-  hipStream_t st = ctx->stream;
   *ok = false;
-  const int64_t n = B.n_rec;
   const int32_t n_refs = (int32_t)B.ref_names.size();
   plan.refs.assign((size_t)n_refs, BaiRef{});
   offs.clear();
-  if (n == 0) {
-    *ok = true;
-    return MH_OK;
-  }
-  if (!B.sorted) return arg_fail(ctx, MH_E_STATE, "BAI plan of an unsorted store (internal)");
-  std::vector<int64_t> woff((size_t)n_refs + 1, 0);
-  for (int32_t t = 0; t < n_refs; t++) woff[t + 1] = woff[t] + (B.ref_len[t] >> 14) + 1;
-  const int64_t n_win = woff[n_refs];
-  MH_TRY(ensure(ctx, B.bai_lin, 4 * (size_t)n_win + 4 * (size_t)n_refs + 8 * (size_t)(n_refs + 1) + 64));
-  uint32_t *lin = (uint32_t *)B.bai_lin.p, *nwin = lin + n_win;
-  int64_t *d_woff = (int64_t *)(((uintptr_t)(nwin + n_refs) + 7) & ~(uintptr_t)7);
-  MH_TRY(ensure(ctx, B.bai_runs, 4 * (size_t)n + 64));
-  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
-  int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 72);
-  int64_t *total = (int64_t *)((char *)ctx->d_small.p + 80);
-  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(n)));
-  int64_t *hs = pinned_small(ctx);
-  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
-  stage_begin(ctx, "bam_bai_plan");
-  HIPCHK(ctx, hipMemsetAsync(lin, 0xff, 4 * (size_t)n_win, st));
-  HIPCHK(ctx, hipMemsetAsync(nwin, 0, 4 * (size_t)n_refs, st));
-  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
-  HIPCHK(ctx, hipMemcpyAsync(d_woff, woff.data(), 8 * woff.size(), hipMemcpyHostToDevice, st));
-  const RInfo *info = (const RInfo *)B.sinfo.p;
-  hipLaunchKernelGGL(k_bai_mark, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, info, n,
-                     (const int64_t *)d_woff, n_refs, lin, nwin, bad);
-  HIPCHK(ctx, hipGetLastError());
-  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadRunStart{info, n}, StoreRunStart{(uint32_t *)B.bai_runs.p},
-                                       ctx->scan_partials.p, total));
-  HIPCHK(ctx, hipMemcpyAsync(hs + 28, total, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hs + 29, bad, 4, hipMemcpyDeviceToHost, st));
-  SYNCCHK(ctx, hipStreamSynchronize(st));
-  const int64_t n_runs = hs[28];
-  const int32_t f = (int32_t)(hs[29] & 0xffffffff);
-  if (f) {   // outside the device plan's checks: the host plans (and reports what it finds)
-    stage_end(ctx);
-    return MH_OK;
-  }
-  MH_TRY(ensure(ctx, B.bai_out, 8 * (size_t)(4 * n_runs + n_win) + 64));
-  int64_t *out_runs = (int64_t *)B.bai_out.p, *out_win = out_runs + 4 * n_runs;
-  const int64_t m = n_runs > n_win ? n_runs : n_win;
-  hipLaunchKernelGGL(k_bai_gather, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, info,
-                     (const int64_t *)B.soff.p, (const uint32_t *)B.bai_runs.p, n_runs, n, (const uint32_t *)lin, n_win,
-                     out_runs, out_win);
-  HIPCHK(ctx, hipGetLastError());
-  std::vector<int64_t> hr(4 * (size_t)n_runs), hw((size_t)n_win);
-  std::vector<uint32_t> hn((size_t)n_refs);
-  HIPCHK(ctx, hipMemcpyAsync(hr.data(), out_runs, 8 * hr.size(), hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hw.data(), out_win, 8 * hw.size(), hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipMemcpyAsync(hn.data(), nwin, 4 * hn.size(), hipMemcpyDeviceToHost, st));
-  SYNCCHK(ctx, hipStreamSynchronize(st));
-  stage_end(ctx);
+  std::vector<int64_t> hr, hw, woff;
+  std::vector<uint32_t> hn;
+  bool raw_ok = false;
+  MH_TRY(bam_bai_raw(ctx, hr, hw, hn, woff, &raw_ok));
+  if (!raw_ok) return MH_OK;   // (outside the device plan's checks: the host plans and reports what it finds)
+  const int64_t n_runs = (int64_t)hr.size() / 4, n_win = (int64_t)hw.size();
   // offs: the runs' (first, end) offsets, then the windows'
   offs.resize(2 * (size_t)n_runs + (size_t)n_win);
   for (int64_t r = 0; r < n_runs; r++) {
@@ -1155,8 +1160,245 @@ int32_t bam_bai_plan(mh_ctx *ctx, BaiPlan &plan, std::vector<int64_t> &offs, boo
   return MH_OK;
 }
 
+// ---- range partition across ranks (configs[4] on N GPUs: every rank sorts and writes one coordinate range) --------
+namespace {
+
+constexpr int PART_MAX = 1024;   // destinations (ranks)
+
+// dest = the number of splitters <= key (splitters ascending): the coordinate range the record belongs to
+__global__ void k_part_dest(const uint64_t *key, int64_t n, const uint64_t *split, int32_t n_split, uint32_t *dest) {
+  __shared__ uint64_t s[PART_MAX];
+  for (int i = threadIdx.x; i < n_split; i += blockDim.x) s[i] = split[i];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = key[i];
+  int lo = 0, hi = n_split;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s[mid] <= k) lo = mid + 1; else hi = mid;
+  }
+  dest[i] = (uint32_t)lo;
+}
+
+// start[d] = the first position of the dest-sorted records whose destination is >= d (d = 0..n_dest)
+__global__ void k_part_starts(const uint32_t *dk, int64_t n, int32_t n_dest, int64_t *start) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n) return;
+  const int32_t lo = k == 0 ? 0 : (int32_t)dk[k - 1] + 1, hi = k == n ? n_dest : (int32_t)dk[k];
+  for (int32_t d = lo; d <= hi; d++) start[d] = k;
+}
+
+// a segment's layout (bam_part_layout in _native.py): records, 8-aligned; n + 1 record offsets from the segment's
+// records; n keys; n BAI infos; n ties
+struct PartSeg {
+  int64_t o_roff, o_key, o_info, o_tie, total;
+};
+__host__ __device__ inline PartSeg part_layout(int64_t n, int64_t nb) {
+  PartSeg g;
+  g.o_roff = (nb + 7) & ~(int64_t)7;
+  g.o_key = g.o_roff + 8 * (n + 1);
+  g.o_info = g.o_key + 8 * n;
+  g.o_tie = g.o_info + 16 * n;
+  g.total = g.o_tie + 8 * n;
+  return g;
+}
+
+// 32 lanes per record (as k_bam_gather): sorted-by-destination position k holds input record ord[k]; its bytes,
+// offset, key, info and tie go to its destination's segment
+__global__ void __launch_bounds__(256) k_part_write(const uint8_t *src, const int64_t *roff, const uint32_t *ord,
+                                                    const uint32_t *dk, const int64_t *soff, const int64_t *start,
+                                                    const int64_t *seg, const uint64_t *key, const RInfo *info,
+                                                    uint64_t tie_base, int64_t n, uint8_t *out, int64_t src_bytes,
+                                                    int64_t out_cap, int32_t *bad) {
+  constexpr int G = 32;
+  const int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int gl = threadIdx.x & (G - 1);
+  if (k >= n) return;
+  const uint32_t r = ord[k], d = dk[k];
+  if (r >= (uint64_t)n) {
+    if (gl == 0) atomicOr(bad, 2);
+    return;
+  }
+  const int64_t s0 = start[d], s1 = start[d + 1], nd = s1 - s0, sb = soff[s0];
+  const PartSeg g = part_layout(nd, soff[s1] - sb);
+  uint8_t *base = out + seg[d];
+  const int64_t a = roff[r], len = roff[r + 1] - a, o = soff[k] - sb;
+  if (a < 0 || len < 0 || a + len > src_bytes || seg[d] + g.total > out_cap || o < 0 || o + len > g.o_roff) {
+    if (gl == 0) atomicOr(bad, 4);
+    return;
+  }
+  const uint8_t *__restrict__ sp = src + a;
+  uint8_t *__restrict__ dp = base + o;
+  for (int64_t j0 = 0; j0 < len; j0 += 8 * G) {
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t j = j0 + gl + G * u;
+      v[u] = j < len ? sp[j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t j = j0 + gl + G * u;
+      if (j < len) dp[j] = v[u];
+    }
+  }
+  if (gl == 0) {
+    const int64_t j = k - s0;
+    int64_t *ro = (int64_t *)(base + g.o_roff);
+    ro[j] = o;
+    if (j == nd - 1) ro[nd] = o + len;
+    ((uint64_t *)(base + g.o_key))[j] = key[r];
+    ((RInfo *)(base + g.o_info))[j] = info[r];
+    ((uint64_t *)(base + g.o_tie))[j] = tie_base + r;
+  }
+}
+
+}  // namespace
+
+int32_t bam_partition(mh_ctx *ctx, const uint64_t *split, int32_t n_dest, uint64_t tie_base, int64_t *seg_off,
+                      int64_t *seg_n, int64_t *seg_bytes) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  if (n_dest < 1 || n_dest > PART_MAX) return arg_fail(ctx, MH_E_ARG, "partition: 1..1024 destinations");
+  for (int32_t i = 1; i + 1 < n_dest; i++)
+    if (split[i] < split[i - 1]) return arg_fail(ctx, MH_E_ARG, "partition: splitters not ascending");
+  if (B.direct) MH_TRY(bam_undirect(ctx));   // (input order = the direct write's sorted order: ties keep their order)
+  if (B.spilled > 0) return arg_fail(ctx, MH_E_STATE, "partition: the store has spilled (stage pieces unbounded)");
+  const int64_t n = B.n_rec;
+  if (n >= ((int64_t)1 << 30)) return arg_fail(ctx, MH_E_CAPACITY, "partition: more than 2^30 records in one piece");
+  MH_TRY(ensure(ctx, B.part_split, 8 * (size_t)n_dest + 64));
+  MH_TRY(ensure(ctx, B.part_dest, 4 * (size_t)n + 64));
+  MH_TRY(ensure(ctx, B.part_dk, 4 * (size_t)n + 64));
+  MH_TRY(ensure(ctx, B.part_ord, 4 * (size_t)n + 64));
+  MH_TRY(ensure(ctx, B.part_soff, 8 * (size_t)(n + 1) + 64));
+  MH_TRY(ensure(ctx, B.part_start, 8 * (size_t)(n_dest + 1) + 64));
+  MH_TRY(ensure(ctx, B.part_seg, 8 * (size_t)(n_dest + 1) + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int64_t *hs = pinned_small(ctx);
+  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  std::vector<int64_t> start((size_t)n_dest + 1, 0), sb((size_t)n_dest + 1, 0);
+  if (n > 0) {
+    if (n_dest > 1)
+      HIPCHK(ctx, hipMemcpyAsync(B.part_split.p, split, 8 * (size_t)(n_dest - 1), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_part_dest, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, (const uint64_t *)B.key.p, n,
+                       (const uint64_t *)B.part_split.p, n_dest - 1, (uint32_t *)B.part_dest.p);
+    HIPCHK(ctx, hipGetLastError());
+    // stable by destination (the records' input order kept inside each destination)
+    unsigned end_bit = 1;
+    while ((1u << end_bit) < (unsigned)n_dest) end_bit++;
+    size_t tmp = 0;
+    HIPCHK(ctx, lsd_sort_pairs_iota(nullptr, tmp, nullptr, nullptr, nullptr, n, end_bit, st));
+    MH_TRY(ensure(ctx, B.part_tmp, tmp + 256));
+    HIPCHK(ctx, lsd_sort_pairs_iota(B.part_tmp.p, tmp, (const uint32_t *)B.part_dest.p, (uint32_t *)B.part_dk.p,
+                                    (uint32_t *)B.part_ord.p, n, end_bit, st));
+    MH_TRY(ensure(ctx, ctx->scan_partials, sizeof(int64_t) * scan_partials_count(n + 1) + 64));
+    HIPCHK(ctx, device_scan<int64_t>(st, n + 1, LoadSortedSize{(const uint32_t *)B.part_ord.p, (const int64_t *)B.roff.p, n},
+                                     StoreOff64{(int64_t *)B.part_soff.p, 0}, OpSum{}, (int64_t)0,
+                                     (int64_t *)ctx->scan_partials.p, (int64_t *)ctx->d_small.p));
+    hipLaunchKernelGGL(k_part_starts, dim3(grid_for(n + 1, 256, INT32_MAX)), dim3(256), 0, st,
+                       (const uint32_t *)B.part_dk.p, n, n_dest, (int64_t *)B.part_start.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(start.data(), B.part_start.p, 8 * start.size(), hipMemcpyDeviceToHost, st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+    for (int32_t d = 0; d <= n_dest; d++)
+      HIPCHK(ctx, hipMemcpyAsync(&sb[d], (const int64_t *)B.part_soff.p + start[d], 8, hipMemcpyDeviceToHost, st));
+    SYNCCHK(ctx, hipStreamSynchronize(st));
+    if (start[n_dest] != n || sb[n_dest] != B.bytes)
+      return arg_fail(ctx, MH_E_STATE, "partition: record counts or offsets do not add up (internal)");
+  }
+  std::vector<int64_t> seg((size_t)n_dest + 1, 0);
+  for (int32_t d = 0; d < n_dest; d++) {
+    seg_n[d] = start[d + 1] - start[d];
+    seg_bytes[d] = sb[d + 1] - sb[d];
+    seg[d + 1] = seg[d] + part_layout(seg_n[d], seg_bytes[d]).total;
+  }
+  for (int32_t d = 0; d <= n_dest; d++) seg_off[d] = seg[d];
+  MH_TRY(ensure(ctx, B.send, (size_t)seg[n_dest] + 64));
+  B.send_bytes = seg[n_dest];
+  if (n > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(B.part_seg.p, seg.data(), 8 * seg.size(), hipMemcpyHostToDevice, st));
+    int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 76);
+    HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+    hipLaunchKernelGGL(k_part_write, dim3(grid_for(n * 32, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)B.recs.p,
+                       (const int64_t *)B.roff.p, (const uint32_t *)B.part_ord.p, (const uint32_t *)B.part_dk.p,
+                       (const int64_t *)B.part_soff.p, (const int64_t *)B.part_start.p, (const int64_t *)B.part_seg.p,
+                       (const uint64_t *)B.key.p, (const RInfo *)B.info.p, tie_base, n, (uint8_t *)B.send.p,
+                       B.bytes, seg[n_dest], bad);
+    HIPCHK(ctx, hipGetLastError());
+    MH_TRY(bam_check_bounds(ctx, bad, "k_part_write"));
+  }
+  return MH_OK;
+}
+
+int32_t bam_bai_raw(mh_ctx *ctx, std::vector<int64_t> &runs, std::vector<int64_t> &win, std::vector<uint32_t> &nwin,
+                    std::vector<int64_t> &woff, bool *ok) {
+  BamStore &B = ctx->bam;
+  hipStream_t st = ctx->stream;
+  *ok = false;
+  const int64_t n = B.n_rec;
+  const int32_t n_refs = (int32_t)B.ref_names.size();
+  woff.assign((size_t)n_refs + 1, 0);
+  for (int32_t t = 0; t < n_refs; t++) woff[t + 1] = woff[t] + (B.ref_len[t] >> 14) + 1;
+  const int64_t n_win = woff[n_refs];
+  runs.clear();
+  win.assign((size_t)n_win, -1);
+  nwin.assign((size_t)n_refs, 0);
+  if (n == 0) {
+    *ok = true;
+    return MH_OK;
+  }
+  if (!B.sorted) return arg_fail(ctx, MH_E_STATE, "BAI plan of an unsorted store (internal)");
+  MH_TRY(ensure(ctx, B.bai_lin, 4 * (size_t)n_win + 4 * (size_t)n_refs + 8 * (size_t)(n_refs + 1) + 64));
+  uint32_t *lin = (uint32_t *)B.bai_lin.p, *dn = lin + n_win;
+  int64_t *d_woff = (int64_t *)(((uintptr_t)(dn + n_refs) + 7) & ~(uintptr_t)7);
+  MH_TRY(ensure(ctx, B.bai_runs, 4 * (size_t)n + 64));
+  MH_TRY(ensure(ctx, ctx->d_small, 8192 + 256));
+  int32_t *bad = (int32_t *)((char *)ctx->d_small.p + 72);
+  int64_t *total = (int64_t *)((char *)ctx->d_small.p + 80);
+  MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<int64_t>(n)));
+  int64_t *hs = pinned_small(ctx);
+  if (!hs) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  stage_begin(ctx, "bam_bai_plan");
+  HIPCHK(ctx, hipMemsetAsync(lin, 0xff, 4 * (size_t)n_win, st));
+  HIPCHK(ctx, hipMemsetAsync(dn, 0, 4 * (size_t)n_refs, st));
+  HIPCHK(ctx, hipMemsetAsync(bad, 0, 4, st));
+  HIPCHK(ctx, hipMemcpyAsync(d_woff, woff.data(), 8 * woff.size(), hipMemcpyHostToDevice, st));
+  const RInfo *info = (const RInfo *)B.sinfo.p;
+  hipLaunchKernelGGL(k_bai_mark, dim3(grid_for(n, 256, INT32_MAX)), dim3(256), 0, st, info, n,
+                     (const int64_t *)d_woff, n_refs, lin, dn, bad);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadRunStart{info, n}, StoreRunStart{(uint32_t *)B.bai_runs.p},
+                                       ctx->scan_partials.p, total));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 28, total, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(hs + 29, bad, 4, hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  const int64_t n_runs = hs[28];
+  if ((int32_t)(hs[29] & 0xffffffff)) {   // outside the device plan's checks
+    stage_end(ctx);
+    return MH_OK;
+  }
+  MH_TRY(ensure(ctx, B.bai_out, 8 * (size_t)(4 * n_runs + n_win) + 64));
+  int64_t *out_runs = (int64_t *)B.bai_out.p, *out_win = out_runs + 4 * n_runs;
+  const int64_t m = n_runs > n_win ? n_runs : n_win;
+  hipLaunchKernelGGL(k_bai_gather, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, info,
+                     (const int64_t *)B.soff.p, (const uint32_t *)B.bai_runs.p, n_runs, n, (const uint32_t *)lin, n_win,
+                     out_runs, out_win);
+  HIPCHK(ctx, hipGetLastError());
+  runs.resize(4 * (size_t)n_runs);
+  HIPCHK(ctx, hipMemcpyAsync(runs.data(), out_runs, 8 * runs.size(), hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(win.data(), out_win, 8 * win.size(), hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(nwin.data(), dn, 4 * nwin.size(), hipMemcpyDeviceToHost, st));
+  SYNCCHK(ctx, hipStreamSynchronize(st));
+  stage_end(ctx);
+  *ok = true;
+  return MH_OK;
+}
+
 void bam_free_spill(BamStore &B) {
-  for (auto &h : B.spill) free(h.p);
+  for (auto &h : B.spill) {
+    if (h.mapped) munmap(h.p, (size_t)(h.b1 - h.b0)); else free(h.p);
+  }
   B.spill.clear();
   B.spilled = 0;
 }
@@ -1165,8 +1407,11 @@ void bam_release(BamStore &B) {
   bam_free_spill(B);
   for (DevBuf *b : {&B.names, &B.name_off, &B.nl1, &B.nl2, &B.tpl, &B.roff, &B.recs, &B.key, &B.val, &B.info,
                     &B.key2, &B.val2, &B.sort_tmp, &B.soff, &B.srecs, &B.sinfo, &B.in1, &B.in2, &B.bai_lin,
-                    &B.bai_runs, &B.bai_out})
+                    &B.bai_runs, &B.bai_out, &B.tie, &B.tie2, &B.tval, &B.tkey, &B.part_dest, &B.part_dk,
+                    &B.part_ord, &B.part_soff, &B.part_start, &B.part_seg, &B.part_split, &B.part_tmp, &B.send})
     release(*b);
+  B.use_tie = false;
+  B.send_bytes = 0;
   B.n_rec = B.bytes = 0;
   B.n_files = 0;
   B.refs_set = false;

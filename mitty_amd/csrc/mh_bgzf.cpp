@@ -167,7 +167,7 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
 
 bool bgzf_write_stream(const char *path, const std::string &header, int level,
                        const std::function<bool(const uint8_t **, int64_t *)> &next, int64_t *data_pos,
-                       int64_t *end_pos, std::string &err) {
+                       int64_t *end_pos, std::string &err, bool eof) {
   FILE *fp = fopen(path, "wb");
   if (!fp) {
     err = std::string("cannot open ") + path;
@@ -190,7 +190,7 @@ bool bgzf_write_stream(const char *path, const std::string &header, int level,
     pos += len;
   }
   *end_pos = pos;
-  ok = ok && fwrite(BGZF_EOF, 1, 28, fp) == 28;
+  ok = ok && (!eof || fwrite(BGZF_EOF, 1, 28, fp) == 28);
   ok = (fclose(fp) == 0) && ok;
   if (!ok && err.empty()) err = std::string("BGZF write failed: ") + path;
   return ok;

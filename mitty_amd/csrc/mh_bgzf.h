@@ -40,9 +40,10 @@ bool bgzf_write_blocks(const char *path, const std::string &header, int level, i
 // The same file with the data blocks handed over as they are ready: next(&buf, &len) gives the next piece of BGZF
 // bytes (false: no more).  *data_pos = the data's file offset (after the header block(s)), *end_pos = the EOF
 // marker's.
+// eof false: no EOF marker (a part of a file other writers complete, mh_bam_write_part).
 bool bgzf_write_stream(const char *path, const std::string &header, int level,
                        const std::function<bool(const uint8_t **, int64_t *)> &next, int64_t *data_pos,
-                       int64_t *end_pos, std::string &err);
+                       int64_t *end_pos, std::string &err, bool eof = true);
 
 // BAI for n sorted records whose data offsets are soff[0..n] (soff[n] = end), given the block map from bgzf_write.
 bool bai_write(const char *path, int32_t n_refs, int64_t n, const BaiRec *recs, const int64_t *soff,

@@ -125,6 +125,12 @@ struct BamStore {
   DevBuf key, val, info;       // sort key, record index, BAI info per record
   DevBuf key2, val2, sort_tmp, soff, srecs, sinfo;   // sorted
   DevBuf bai_lin, bai_runs, bai_out;                  // the BAI's device plan (mh_bam.hip bam_bai_plan)
+  // ranks (configs[4] on N GPUs): each record's global input index (tie), which orders equal keys when records
+  // arrive from several ranks (use_tie); the range partition's scratch and packed segments (mh_bam_partition)
+  DevBuf tie, tie2, tval, tkey;
+  DevBuf part_dest, part_dk, part_ord, part_soff, part_start, part_seg, part_split, part_tmp, send;
+  bool use_tie = false;
+  int64_t send_bytes = 0;
   int64_t n_rec = 0, bytes = 0;
   int32_t n_files = 0;
   bool sorted = false;         // soff/sinfo (and srecs unless spilled) hold the current store in coordinate order
@@ -137,9 +143,11 @@ struct BamStore {
   struct HostBlock {
     uint8_t *p;
     int64_t b0, b1;            // the store's input-order bytes [b0, b1)
+    bool mapped = false;       // an unlinked temporary file mapped in (spill_dir), else malloc
   };
   std::vector<HostBlock> spill;
   int64_t spilled = 0;
+  std::string spill_dir;       // mh_bam_set_spill_dir: spill to files there (the page cache, not anonymous memory)
 };
 
 struct StageTime {
@@ -367,10 +375,18 @@ int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2,
 int32_t bam_sort(mh_ctx *ctx, const void *pa = nullptr);
 int32_t bam_undirect(mh_ctx *ctx);
 int32_t bam_fetch_sorted(mh_ctx *ctx, uint8_t *recs, int64_t *soff, int32_t *info);
-int32_t bam_spill(mh_ctx *ctx);
+int32_t bam_spill(mh_ctx *ctx);   // the device-resident records to a host block (input order)
 int32_t bam_export(mh_ctx *ctx, int64_t r0, int64_t r1, uint8_t *recs, int64_t *roff, uint64_t *key, int32_t *info);
 int32_t bam_import(mh_ctx *ctx, const uint8_t *recs, const int64_t *roff, const uint64_t *key, const int32_t *info,
-                   int64_t n);   // the device-resident records to a host block (input order)
+                   int64_t n, const uint64_t *tie = nullptr);
+// the store's records by destination rank: dest = the number of splitters <= the record's key; packed per
+// destination (bam_part_layout, input order inside each) into B.send; seg_off[d] / seg_n[d] / seg_bytes[d]
+int32_t bam_partition(mh_ctx *ctx, const uint64_t *split, int32_t n_dest, uint64_t tie_base, int64_t *seg_off,
+                      int64_t *seg_n, int64_t *seg_bytes);
+// the raw device BAI plan of the sorted store (per run: tid << 32 | bin, first offset, end offset, records; per window
+// its first record's offset or -1; per reference its window count); *ok false: outside the device plan's checks
+int32_t bam_bai_raw(mh_ctx *ctx, std::vector<int64_t> &runs, std::vector<int64_t> &win, std::vector<uint32_t> &nwin,
+                    std::vector<int64_t> &woff, bool *ok);
 // the sorted store's byte stream [w0, w1) into dst (host), from the host blocks (every record spilled); the sorted
 // order (val2), input offsets (roff) and sorted offsets (soff) as host copies (bam_host_order)
 struct BamHostOrder {

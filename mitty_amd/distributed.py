@@ -20,11 +20,28 @@ illumina.py:56-58), so the path shards without any data-path collective:
 The collectives carry a few int64 per piece; no sequence data crosses xGMI for the FASTQ files.  Outputs must be
 regular files (ranks write at offsets); FIFOs / process substitution need the single-GPU path.
 
-With a BAM output (configs[4]: the god-aligner's perfect BAM of the generated reads), every rank also turns each of
-its pieces into BAM records on its own GPU as the piece is emitted (parse, encode, keys: mh_bam_add_output on the
-arenas), and rank 0's store takes the pieces in piece order (RCCL point-to-point on device buffers; gloo on host
-arrays), sorts the keys once and writes the BAM and BAI — the reference's pysam.cat of the workers' fragments before
-one sort (god_aligner.py:63-68,100-108).  The BAM equals the one-GPU god-aligner's over the same FASTQ, byte for byte.
+With a BAM output (configs[4]: the god-aligner's perfect BAM of the generated reads), the coordinate order is cut
+into one range per rank (range_splitters: the BED regions' bases in @SQ order, split evenly — templates start
+uniformly over the regions, illumina.py:66-76), and no rank merges the others' records:
+
+* as each piece is emitted, its rank turns it into BAM records on its GPU (mh_bam_add_output on the arenas) and
+  partitions them by range (mh_bam_partition: packed per destination, each record with its global input index as a
+  tie); one all-to-all per round of pieces (RCCL on device buffers under 'nccl', gloo on host arrays) moves every
+  record to its range's rank, whose store (a second HIP context) imports it (mh_bam_import_tie);
+* each rank sorts its range on its GPU (equal keys by tie: the one-rank store's input order) and deflates it into
+  BGZF blocks cut where the one-rank file cuts them (every 0xff00 bytes of the whole sorted stream: a rank skips the
+  bytes that complete the previous rank's last block and appends the head of the next ranks' ranges —
+  mh_bam_write_part), into a part file of its own; an all-gather of the parts' sizes places them, and every rank
+  copies its part into the BAM at its offset (rank 0's part starts with the header, the last ends with the EOF);
+* the BAI: every rank's raw plan of its range (mh_bam_bai_runs: runs of one bin, first record per 16 kbp window) in
+  virtual offsets of the final file, gathered to rank 0 and joined (runs cut at a range boundary are one run again)
+  into the one-rank index.
+
+The bounded store (mh_bam_set_capacity, `bam_capacity`) applies to every rank's range: records past it spill to host
+memory (or, with `bam_spill_dir`, to unlinked temporary files, as `samtools sort -m` does), so a rank's memory
+follows its range, not the job — the reference's workers' fragments, cat, `samtools sort -m 2G -@N` and
+pysam.index (god_aligner.py:63-68,100-116).  The BAM and BAI equal the one-GPU god-aligner's over the same FASTQ,
+byte for byte.
 
 A process holds one HIP runtime: torch must load before libmitty_hip.so (mitty_amd._native does that itself when
 WORLD_SIZE > 1), otherwise torch brings its own runtime and whichever of the two initialises second sees no GPU.
@@ -205,39 +222,65 @@ class DeviceBackend:
   def reset_output(self):
     self.eng.ctx.reset_output()
 
-  # ---- the BAM leg: per piece the records of the arenas, packed (_native.bam_piece_layout); rank 0's store ----
-  def bam_piece(self, refs):
+  # ---- the BAM leg (configs[4]): each piece's records partitioned by coordinate range (this context's store
+  # stages one piece at a time); this rank's range in a store of its own (a second context on the same GPU) ----
+  def bam_begin(self, refs, capacity=0, spill_dir=None):
+    from mitty_amd import _native
+    names, lens = [r[0] for r in refs], [r[1] for r in refs]
+    self.eng.ctx.bam_set_refs(names, lens)
+    self.eng.ctx.bam_set_capacity(0)
+    if getattr(self, 'rctx', None) is None:
+      self.rctx = _native.Context(self.eng.device)
+    self.rctx.bam_set_refs(names, lens)
+    self.rctx.bam_set_capacity(capacity)
+    if spill_dir is not None:
+      self.rctx.bam_set_spill_dir(spill_dir)
+
+  def bam_partition(self, splitters, tie_base):
+    """The arenas' records (this piece) by range -> (segment offsets, records, record bytes) per destination."""
     ctx = self.eng.ctx
-    ctx.bam_set_refs([r[0] for r in refs], [r[1] for r in refs])
+    ctx.bam_reset()
     ctx.bam_add_output()
-    n, nb = ctx.bam_records()
-    return n, nb, ctx.bam_export(0, n, nb)
+    return ctx.bam_partition(splitters, tie_base)
 
-  def bam_begin(self, refs, capacity=0):
-    ctx = self.eng.ctx
-    ctx.bam_set_refs([r[0] for r in refs], [r[1] for r in refs])
-    ctx.bam_set_capacity(capacity)
+  def bam_partition_into(self, t):
+    """The packed segments into torch tensor t (host or device)."""
+    self.eng.ctx.bam_partition_fetch(t.data_ptr(), t.numel())
 
-  def bam_import(self, n, nb, ptr):
-    self.eng.ctx.bam_import(n, nb, ptr)
+  def bam_import_segment(self, t, off, n, nb):
+    self.rctx.bam_import_tie(n, nb, t.data_ptr() + off)
 
-  def bam_write(self, path, header_text, bai=True):
-    return self.eng.ctx.bam_write_gpu(path, header_text, bai_path=path + '.bai' if bai else None)
+  def bam_range(self):
+    """(records, bytes) of this rank's range."""
+    return self.rctx.bam_records()
+
+  def bam_head(self, n):
+    return self.rctx.bam_sorted_head(n)
+
+  def bam_write_part(self, path, header_text, skip, tail, eof):
+    return self.rctx.bam_write_part(path, header_text, skip, tail, eof)
+
+  def bam_bai_runs(self, n_refs):
+    return self.rctx.bam_bai_runs(n_refs)
 
   def close(self):
+    if getattr(self, 'rctx', None) is not None:
+      self.rctx.close()
+      self.rctx = None
     self.eng.close()
 
 
 def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, read_module, model, coverage,
                                fastq1_fname, fastq2_fname, seed=7, rng='mitty', corrupt_seed=None, backend=None,
                                group=None, max_batch_draws=200_000_000, layout=None, bam_fname=None,
-                               bam_header_text=None, bam_refs=None, bam_capacity=0):
+                               bam_header_text=None, bam_refs=None, bam_capacity=0, bam_spill_dir=None):
   """process_multi_threaded (readgenerate.py:76-126) over the ranks of the default process group.
 
   `backend` defaults to DeviceBackend(LOCAL_RANK); tests pass a host stand-in to exercise the orchestration with
   the gloo backend on CPU.  Returns this rank's stats plus the job totals.
   bam_fname: also the god-aligner's BAM (+ .bai) of the reads, header bam_header_text, @SQ bam_refs [(name, length)]
-  (god_aligner.construct_header from the FASTA's .ann); bam_capacity: rank 0's record bytes in HBM before a spill.
+  (god_aligner.construct_header from the FASTA's .ann); bam_capacity: each rank's range store's record bytes in HBM
+  before a spill; bam_spill_dir: spill to unlinked temporary files there instead of host memory.
   """
   import torch.distributed as dist
   from mitty_amd.simulation.readgenerate import get_data_for_workers
@@ -337,13 +380,25 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
       dist.barrier(group)
 
   # ---- phase B: each piece emitted, then written at its offset (plain) or deflated on the device and held (gz);
-  # the arenas are recycled after every piece -------------------------------------------------------------------
+  # the arenas are recycled after every piece.  With a BAM, the pieces go in rounds (the k-th piece of every rank),
+  # each round closed by one all-to-all of the pieces' records to their coordinate ranges' ranks ------------------
   fds = [os.open(fn, os.O_WRONLY) if not gz[f] else None for f, fn in enumerate(fnames)]
   held = {}   # piece index -> compressed bytes per gz file
-  bam_held = {}   # piece index -> (records, record bytes, packed piece)
   raw = [0, 0]
+  order = sorted(plan)
+  rounds = len(order)
+  splitters = None
+  if bam_fname is not None:
+    rounds = max(sum(1 for pc in pieces if pc[3] == r) for r in range(world)) if pieces else 0
+    splitters = range_splitters([vdf[ri]['region'] for ri in range(len(vdf))], bam_refs, world)
+    backend.bam_begin(bam_refs, bam_capacity, bam_spill_dir)
+    stats['bam_rounds'] = rounds
   try:
-    for i in sorted(plan):
+    for r in range(rounds):
+      i = order[r] if r < len(order) else None
+      if i is None:   # (a rank with fewer pieces: an empty contribution to the round's exchange)
+        _bam_exchange(backend, None, world, group, stats)
+        continue
       k, stub, chrom, cpy, useed, rng_range, base = plan[i]
       backend.reset_output()
       kept, r1, r2 = backend.emit(k, stub, chrom, cpy, write2, useed, rng_range, base)
@@ -360,8 +415,8 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
         for f in plain:
           _pwrite_all(fds[f], data[f], off[f][i])
       held[i] = [backend.fetch_gz(f, rs[f]) if gz[f] else None for f in range(len(fnames))]
-      if bam_fname is not None:
-        bam_held[i] = backend.bam_piece(bam_refs)
+      if bam_fname is not None:   # the piece's records to their ranges (tie: piece index, record index)
+        _bam_exchange(backend, backend.bam_partition(splitters, i << 32), world, group, stats)
   finally:
     for fd in fds:
       if fd is not None:
@@ -395,8 +450,7 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
         os.close(fd)
   held.clear()
   if bam_fname is not None:
-    stats['bam_records'] = _bam_merge(backend, pieces, bam_held, rank, world, group, bam_fname, bam_header_text,
-                                      bam_refs, bam_capacity)
+    stats['bam_records'] = _bam_write_ranges(backend, rank, world, group, bam_fname, bam_header_text, bam_refs)
   tot = allreduce_i64([stats['templates'], stats['kept']] + raw, group)
   if world > 1:
     dist.barrier(group)
@@ -405,48 +459,264 @@ def generate_reads_distributed(fasta_fname, vcf_fname, sample_name, bed_fname, r
   return stats
 
 
-def _bam_merge(backend, pieces, bam_held, rank, world, group, bam_fname, header_text, refs, capacity):
-  """Rank 0's store takes every piece's records in piece order (its own from memory, the others' over the process
-  group: point-to-point, RCCL on device buffers under 'nccl'), then sorts and writes the BAM + BAI once.  The ranks
-  hold their packed pieces until then.  Returns the BAM's record count on rank 0 (0 elsewhere)."""
+BGZF_BLOCK = 0xff00   # uncompressed bytes per BGZF block (htslib's BGZF_BLOCK_SIZE; mh_bgzf.h)
+
+
+def sort_key(tid, pos0):
+  """The god-aligner store's coordinate key of a record at (tid, 0-based pos) on the forward strand
+  (samtools sort's order: tid, pos + 1, is_reverse)."""
+  return (int(tid) << 33) | ((int(pos0) + 1) << 1)
+
+
+def range_splitters(regions, refs, world):
+  """world - 1 ascending sort keys that cut the coordinate order into `world` ranges of about equal bases of the BED
+  regions (templates start uniformly over the regions: illumina.py:66-76, geometric gaps); range d holds the keys
+  k with splitters[d - 1] <= k < splitters[d].  regions: [(chrom, start0, end)]; refs: the @SQ [(name, length)]."""
+  tid = {name: t for t, (name, _) in enumerate(refs)}
+  segs = sorted((tid[c], s0, e) for c, s0, e in regions if c in tid and e > s0)
+  total = sum(e - s0 for _, s0, e in segs)
+  out = []
+  for d in range(1, world):
+    want, acc = total * d // world, 0
+    key = sort_key(len(refs), 0)   # (past every record: an empty range)
+    for t, s0, e in segs:
+      if acc + (e - s0) > want:
+        key = sort_key(t, s0 + (want - acc))
+        break
+      acc += e - s0
+    out.append(max(key, out[-1]) if out else key)
+  return out
+
+
+def _bam_exchange(backend, part, world, group, stats):
+  """One round: every rank's packed segments (backend.bam_partition: offsets, records and record bytes per
+  destination; None = nothing this round) to their destinations (all-to-all, RCCL on device buffers under 'nccl',
+  gloo on host tensors), imported into the receiving ranks' range stores."""
   import torch
   from mitty_amd import _native
-  sz = [0] * (2 * len(pieces))
-  for i, (n, nb, _) in bam_held.items():
-    sz[2 * i], sz[2 * i + 1] = n, nb
-  sz = allreduce_i64(sz, group)
-  dev = None
+  if part is None:   # an empty segment per destination (its layout: the one record offset, 0)
+    off, seg_n, seg_b = 8 * np.arange(world + 1, dtype=np.int64), np.zeros(world, np.int64), np.zeros(world, np.int64)
+  else:
+    off, seg_n, seg_b = part
+  if world == 1:
+    t = torch.empty(max(int(off[-1]), 8), dtype=torch.uint8)
+    if part is not None:
+      backend.bam_partition_into(t)
+      backend.bam_import_segment(t, 0, int(seg_n[0]), int(seg_b[0]))
+    stats['bam_sent'] = stats.get('bam_sent', 0) + int(seg_n.sum())
+    return
+  import torch.distributed as dist
+  dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
+  # sizes first: (records, record bytes) per destination, all-to-all
+  sz = torch.tensor(np.stack([seg_n, seg_b], 1).reshape(-1), dtype=torch.int64, device=dev)
+  rs = torch.empty(2 * world, dtype=torch.int64, device=dev)
+  dist.all_to_all_single(rs, sz, group=group)
+  rs = rs.cpu().numpy().reshape(world, 2)
+  tot_in = [int(_native.bam_part_layout(int(n), int(nb))[4]) for n, nb in rs]
+  tot_out = [int(off[d + 1] - off[d]) for d in range(world)]
+  send = (torch.empty if part is not None else torch.zeros)(max(int(off[-1]), 8), dtype=torch.uint8, device=dev)
+  if part is not None and int(off[-1]) > 0:
+    backend.bam_partition_into(send)
+  recv = torch.empty(max(sum(tot_in), 8), dtype=torch.uint8, device=dev)
+  dist.all_to_all_single(recv[:sum(tot_in)], send[:int(off[-1])], tot_in, tot_out, group=group)
+  if dev == 'cuda':
+    torch.cuda.current_stream().synchronize()
+  o = 0
+  for s in range(world):
+    n, nb = int(rs[s][0]), int(rs[s][1])
+    if n:
+      backend.bam_import_segment(recv, o, n, nb)
+    o += tot_in[s]
+  stats['bam_sent'] = stats.get('bam_sent', 0) + int(seg_n.sum())
+  stats['bam_received'] = stats.get('bam_received', 0) + int(rs[:, 0].sum())
+
+
+def _allgather_i64(vals, world, group):
+  """Every rank's int64 vector (same length), as a [world, len] array (an all-reduce of a zero-padded slot each)."""
+  import torch.distributed as dist
+  vals = [int(v) for v in vals]
+  if world == 1:
+    return np.array([vals], np.int64)
+  rank = dist.get_rank(group)
+  buf = [0] * (world * len(vals))
+  buf[rank * len(vals):(rank + 1) * len(vals)] = vals
+  return np.array(allreduce_i64(buf, group), np.int64).reshape(world, len(vals))
+
+
+def _allgather_bytes(data, cap, world, group):
+  """Every rank's bytes (at most cap), as a list."""
+  import torch
+  import torch.distributed as dist
+  if world == 1:
+    return [bytes(data)]
+  dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
+  t = torch.zeros(cap + 8, dtype=torch.uint8)
+  t[:8] = torch.from_numpy(np.array([len(data)], np.int64).view(np.uint8))
+  if len(data):
+    t[8:8 + len(data)] = torch.from_numpy(np.frombuffer(data, np.uint8).copy())
+  t = t.to(dev)
+  out = [torch.empty_like(t) for _ in range(world)]
+  dist.all_gather(out, t, group=group)
+  res = []
+  for x in out:
+    x = x.cpu().numpy()
+    n = int(x[:8].view(np.int64)[0])
+    res.append(x[8:8 + n].tobytes())
+  return res
+
+
+def _bam_write_ranges(backend, rank, world, group, bam_fname, header_text, refs):
+  """Each rank's range sorted and deflated where the one-rank file cuts its blocks, the parts placed by an
+  all-gather of their sizes and copied into the BAM; the BAI joined on rank 0 from every rank's raw plan.  Returns
+  the BAM's record count."""
+  n_rec, nbytes = backend.bam_range()
+  tab = _allgather_i64([n_rec, nbytes], world, group)
+  U = np.concatenate([[0], np.cumsum(tab[:, 1])])   # each range's first byte in the whole sorted stream
+  total = int(U[-1])
+  B = BGZF_BLOCK
+  skip = [min(int(tab[r, 1]), (-int(U[r])) % B) for r in range(world)]
+  heads = _allgather_bytes(backend.bam_head(min(B, nbytes)), B, world, group)
+  # the tail: the next ranges' first bytes up to the end of this rank's last block (or of the stream)
+  tail = b''
+  own = nbytes - skip[rank]
+  if own > 0:
+    nb_local = (own + B - 1) // B
+    end = min(total, int(U[rank]) + skip[rank] + nb_local * B)
+    need, r = end - int(U[rank + 1]), rank + 1
+    while need > 0 and r < world:
+      take = heads[r][:need]
+      tail += take
+      need -= len(take)
+      r += 1
+    assert need <= 0, 'BAM ranges: the next ranges\' heads do not complete the last block'
+  part = '{}.part{}'.format(bam_fname, rank)
+  nblk, data_pos, fbytes, boff = backend.bam_write_part(part, header_text if rank == 0 else None, skip[rank], tail,
+                                                        rank == world - 1)
+  z = int(boff[-1]) if len(boff) else 0
+  lastz = int(boff[-1] - boff[-2]) if nblk > 0 else 0
+  pt = _allgather_i64([fbytes, data_pos, nblk, z, lastz], world, group)
+  part_off = np.concatenate([[0], np.cumsum(pt[:, 0])])
   if world > 1:
     import torch.distributed as dist
-    dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
-  if rank == 0:
-    backend.bam_begin(refs, capacity)
-  total = 0
-  for i in range(len(pieces)):
-    n, nb = sz[2 * i], sz[2 * i + 1]
-    if n == 0:
-      continue
-    owner = pieces[i][3]
-    size = _native.bam_piece_layout(n, nb)[3]
-    if owner == rank:
-      buf = bam_held.pop(i)[2]
-      if rank == 0:
-        backend.bam_import(n, nb, buf.ctypes.data)
-      else:
-        t = torch.from_numpy(buf[:size])
-        dist.send(t.to(dev) if dev == 'cuda' else t, 0, group=group)
-    elif rank == 0:
-      t = torch.empty(size, dtype=torch.uint8, device=dev)
-      dist.recv(t, owner, group=group)
-      if dev == 'cuda':
-        torch.cuda.current_stream().synchronize()
-      backend.bam_import(n, nb, t.data_ptr())
-    total += n
-  if rank == 0:
-    backend.bam_write(bam_fname, header_text)
-  if world > 1:
+    if rank == 0:
+      with open(bam_fname, 'wb') as fp:
+        fp.truncate(int(part_off[-1]))
     dist.barrier(group)
-  return total if rank == 0 else 0
+  elif rank == 0:
+    open(bam_fname, 'wb').close()
+  fd_in, fd_out = os.open(part, os.O_RDONLY), os.open(bam_fname, os.O_WRONLY)
+  try:
+    o, n = int(part_off[rank]), int(fbytes)
+    src = 0
+    while src < n:
+      m = os.copy_file_range(fd_in, fd_out, n - src, src, o + src)
+      if m <= 0:
+        raise OSError('copy_file_range: no progress copying {} into {}'.format(part, bam_fname))
+      src += m
+  finally:
+    os.close(fd_in)
+    os.close(fd_out)
+    os.remove(part)
+  # the BAI: this range's raw plan in the final file's virtual offsets
+  b0 = [(int(U[r]) + skip[r]) // B for r in range(world)]
+
+  def coff(b):   # the file offset of (whole-stream) block b
+    lb = b - b0[rank]
+    if 0 <= lb < nblk:
+      return int(part_off[rank] + data_pos + boff[lb])
+    for r in range(world):
+      if pt[r, 2] > 0 and b == b0[r]:
+        return int(part_off[r] + pt[r, 1])
+      if pt[r, 2] > 0 and b == b0[r] + pt[r, 2] - 1:
+        return int(part_off[r] + pt[r, 1] + pt[r, 3] - pt[r, 4])
+    if b * B >= total:   # the end of the stream: the EOF block's offset
+      return int(part_off[world - 1] + pt[world - 1, 1] + pt[world - 1, 3])
+    raise RuntimeError('BAI: block {} is not a block this range can reference'.format(b))
+
+  def voff(u):
+    b = u // B
+    return (coff(b) << 16) | (u - b * B)
+
+  runs, win, rnwin = backend.bam_bai_runs(len(refs))
+  base = int(U[rank])
+  plan = {'runs': [(int(t) >> 32, int(t) & 0xffffffff, int(a) + base, int(e) + base, voff(int(a) + base),
+                    voff(int(e) + base), int(c)) for t, a, e, c in runs],
+          'win': {}, 'nwin': [int(x) for x in rnwin]}
+  wo = np.concatenate([[0], np.cumsum([(ln >> 14) + 1 for _, ln in refs])])
+  for t in range(len(refs)):
+    ws = win[wo[t]:wo[t] + int(rnwin[t])]
+    plan['win'][t] = [(w, voff(int(x) + base)) for w, x in enumerate(ws) if x >= 0]
+  plans = _gather_to0(plan, rank, world, group)
+  if rank == 0:
+    with open(bam_fname + '.bai', 'wb') as fp:
+      fp.write(bai_join(plans, len(refs)))
+  if world > 1:
+    import torch.distributed as dist
+    dist.barrier(group)
+  return int(tab[:, 0].sum())
+
+
+def _gather_to0(obj, rank, world, group):
+  if world == 1:
+    return [obj]
+  import torch.distributed as dist
+  out = [None] * world if rank == 0 else None
+  dist.gather_object(obj, out, dst=0, group=group)
+  return out
+
+
+def bai_join(plans, n_refs):
+  """The BAI (SAM spec §5.2, as mh_bgzf.cpp bai_emit writes it) from the ranks' plans in range order.  A plan:
+  'runs' [(tid, bin, first data offset, end offset, first voffset, end voffset, records)] in record order, 'win'
+  {tid: [(window, voffset of its first record)]}, 'nwin' [window count per tid].  Runs of one bin that meet at a
+  range boundary are one run (as the one-rank plan finds them); each reference's runs are then ordered by bin
+  (stable); a window's first record is the first range's that has one."""
+  import struct
+  out = bytearray(b'BAI\x01')
+  out += struct.pack('<i', n_refs)
+  for t in range(n_refs):
+    runs = []   # [bin, ub, ue, vb, ve, n]
+    for p in plans:
+      for (tid, b, ub, ue, vb, ve, c) in p['runs']:
+        if tid != t:
+          continue
+        if runs and runs[-1][0] == b and runs[-1][2] == ub:
+          runs[-1][2], runs[-1][4], runs[-1][5] = ue, ve, runs[-1][5] + c
+        else:
+          runs.append([b, ub, ue, vb, ve, c])
+    if not runs:
+      out += struct.pack('<ii', 0, 0)
+      continue
+    n = sum(r[5] for r in runs)
+    vi, vj = runs[0][3], runs[-1][4]
+    ordered = sorted(runs, key=lambda r: r[0])   # (stable)
+    bins = []
+    for r in ordered:
+      if bins and bins[-1][0] == r[0]:
+        bins[-1][1].append((r[3], r[4]))
+      else:
+        bins.append((r[0], [(r[3], r[4])]))
+    out += struct.pack('<i', len(bins) + 1)
+    for b, chunks in bins:
+      out += struct.pack('<Ii', b, len(chunks))
+      for vb, ve in chunks:
+        out += struct.pack('<QQ', vb, ve)
+    out += struct.pack('<IiQQQQ', 37450, 2, vi, vj, n, 0)
+    nw = max(p['nwin'][t] for p in plans)
+    lin = [-1] * nw
+    for p in plans:
+      for w, v in p['win'].get(t, []):
+        if lin[w] < 0:
+          lin[w] = v
+    nxt = vj
+    for w in range(nw - 1, -1, -1):
+      if lin[w] >= 0:
+        nxt = lin[w]
+      lin[w] = nxt
+    out += struct.pack('<i', nw)
+    out += struct.pack('<{}Q'.format(nw), *lin)
+  out += struct.pack('<Q', 0)
+  return bytes(out)
 
 
 def _pwrite_all(fd, data, off):

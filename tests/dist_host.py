@@ -2,6 +2,8 @@
 orchestration of mitty_amd.distributed (plan, slice counts, cnt bases, file offsets, pwrite) runs with gloo on CPU.
 Every oracle record is a kept template, and the stand-in renumbers cnt from the base it is given, so a wrong
 cnt_base or offset shows up as a byte difference against the single-process output."""
+import numpy as np
+
 from oracle import oracle as O
 
 
@@ -83,45 +85,97 @@ class OracleBackend:
     pass
 
 
-  # ---- the BAM leg (DeviceBackend.bam_*): records from oracle/god.py, packed as mh_bam_export packs them ----------
-  def bam_piece(self, refs):
+  # ---- the BAM leg (DeviceBackend.bam_*): records from oracle/god.py, partitioned and packed as mh_bam_partition
+  # packs them; the range store sorted by (key, tie); parts as host BGZF (zlib) cut every 0xff00 bytes ----------
+  def bam_begin(self, refs, capacity=0, spill_dir=None):
+    self.refs = refs
+    self.bam = []   # the range store: (key, tie, record bytes, BAI info)
+
+  def bam_partition(self, splitters, tie_base):
+    import bisect
     import numpy as np
     from oracle import god
     from mitty_amd import _native
-    ref_dict = {name: k for k, (name, _) in enumerate(refs)}
+    ref_dict = {name: k for k, (name, _) in enumerate(self.refs)}
     recs = god.god_records(bytes(self.arena[0]), bytes(self.arena[1]) if self.arena[1] else None, ref_dict)
-    enc = [god.encode(r) for r in recs]
-    n, nb = len(enc), sum(len(e) for e in enc)
-    o_roff, o_key, o_info, total = _native.bam_piece_layout(n, nb)
-    buf = np.zeros(max(total, 8), np.uint8)
-    buf[:nb] = np.frombuffer(b''.join(enc), np.uint8)
-    buf[o_roff:o_key].view(np.int64)[:] = np.concatenate([[0], np.cumsum([len(e) for e in enc])]).astype(np.int64)
-    buf[o_key:o_info].view(np.uint64)[:] = [r['reference_id'] << 33 | (r['pos'] + 1) << 1 | int(r['is_reverse'])
-                                            for r in recs]
-    buf[o_info:total].view(np.int32)[:] = np.array(
-        [[r['reference_id'], r['pos'], god.end_pos(r), god.reg2bin(r['pos'], god.end_pos(r))] for r in recs],
-        np.int32).reshape(-1) if n else []
-    return n, nb, buf
+    segs = [[] for _ in range(len(splitters) + 1)]
+    for i, r in enumerate(recs):
+      key = r['reference_id'] << 33 | (r['pos'] + 1) << 1 | int(r['is_reverse'])
+      info = (r['reference_id'], r['pos'], god.end_pos(r), god.reg2bin(r['pos'], god.end_pos(r)))
+      segs[bisect.bisect_right(splitters, key)].append((key, tie_base + i, god.encode(r), info))
+    out, off = [], [0]
+    for seg in segs:
+      n, nb = len(seg), sum(len(e) for _, _, e, _ in seg)
+      o_roff, o_key, o_info, o_tie, total = _native.bam_part_layout(n, nb)
+      buf = np.zeros(total, np.uint8)
+      buf[:nb] = np.frombuffer(b''.join(e for _, _, e, _ in seg), np.uint8)
+      buf[o_roff:o_key].view(np.int64)[:] = np.concatenate([[0], np.cumsum([len(e) for _, _, e, _ in seg])])
+      buf[o_key:o_info].view(np.uint64)[:] = [k for k, _, _, _ in seg]
+      buf[o_info:o_tie].view(np.int32)[:] = np.array([x for *_, x in seg], np.int32).reshape(-1) if n else []
+      buf[o_tie:total].view(np.uint64)[:] = [t for _, t, _, _ in seg]
+      out.append(buf.tobytes())
+      off.append(off[-1] + total)
+    self._send = b''.join(out)
+    return (np.array(off, np.int64), np.array([len(x) for x in segs], np.int64),
+            np.array([sum(len(e) for _, _, e, _ in x) for x in segs], np.int64))
 
-  def bam_begin(self, refs, capacity=0):
-    self.bam = []   # (key, import order, record bytes)
+  def bam_partition_into(self, t):
+    t.numpy()[:len(self._send)] = np.frombuffer(self._send, np.uint8)
 
-  def bam_import(self, n, nb, ptr):
-    import ctypes
-    import numpy as np
+  def bam_import_segment(self, t, off, n, nb):
     from mitty_amd import _native
-    o_roff, o_key, _, total = _native.bam_piece_layout(n, nb)
-    buf = np.frombuffer(ctypes.string_at(ptr, total), np.uint8)
+    o_roff, o_key, o_info, o_tie, total = _native.bam_part_layout(n, nb)
+    buf = t.numpy()[off:off + total]
     roff = buf[o_roff:o_key].view(np.int64)
-    keys = buf[o_key:o_key + 8 * n].view(np.uint64)
+    keys, ties = buf[o_key:o_info].view(np.uint64), buf[o_tie:total].view(np.uint64)
+    info = buf[o_info:o_tie].view(np.int32).reshape(-1, 4)
     for k in range(n):
-      self.bam.append((int(keys[k]), len(self.bam), bytes(buf[roff[k] - roff[0]:roff[k + 1] - roff[0]])))
+      self.bam.append((int(keys[k]), int(ties[k]), bytes(buf[roff[k]:roff[k + 1]]), tuple(int(x) for x in info[k])))
 
-  def bam_write(self, path, header_text, bai=True):
-    """The sorted record stream, uncompressed (the stand-in checks the order, not the BGZF framing)."""
+  def _sorted(self):
+    return sorted(self.bam, key=lambda x: (x[0], x[1]))
+
+  def bam_range(self):
+    return len(self.bam), sum(len(x[2]) for x in self.bam)
+
+  def bam_head(self, n):
+    return b''.join(x[2] for x in self._sorted())[:n]
+
+  def bam_write_part(self, path, header_text, skip, tail, eof):
+    from oracle import god
+    from mitty_amd import _native
+    data = b''.join(x[2] for x in self._sorted())[skip:] + tail
+    hz = b''
+    if header_text is not None:
+      hz = _native.bgzf_compress(god.header_bytes(header_text, [{'SN': n, 'LN': ln} for n, ln in self.refs]))
+    blocks = [_native.bgzf_compress(data[o:o + 0xff00]) for o in range(0, len(data), 0xff00)]
+    boff = np.concatenate([[0], np.cumsum([len(z) for z in blocks])]).astype(np.int64)
     with open(path, 'wb') as fp:
-      for _, _, rec in sorted(self.bam, key=lambda x: (x[0], x[1])):
-        fp.write(rec)
+      fp.write(hz + b''.join(blocks) + (_native.bgzf_eof() if eof else b''))
+    return len(blocks), len(hz), len(hz) + int(boff[-1]) + (28 if eof else 0), boff
+
+  def bam_bai_runs(self, n_refs):
+    """mh_bam_bai_runs' arrays from the sorted records (runs of one bin in record order; first record per window)."""
+    recs = self._sorted()
+    soff = np.concatenate([[0], np.cumsum([len(x[2]) for x in recs])]).astype(np.int64)
+    runs = []
+    for k, x in enumerate(recs):
+      tid, _, _, b = x[3]
+      if runs and runs[-1][0] == (tid << 32 | b) and runs[-1][2] == soff[k]:
+        runs[-1][2] = soff[k + 1]
+        runs[-1][3] += 1
+      else:
+        runs.append([tid << 32 | b, soff[k], soff[k + 1], 1])
+    wo = np.concatenate([[0], np.cumsum([(ln >> 14) + 1 for _, ln in self.refs])])
+    win = np.full(int(wo[-1]), -1, np.int64)
+    nwin = np.zeros(n_refs, np.int64)
+    for k, x in enumerate(recs):
+      tid, beg, end, _ = x[3]
+      for w in range(beg >> 14, ((end - 1) >> 14) + 1):
+        if win[wo[tid] + w] < 0:
+          win[wo[tid] + w] = soff[k]
+      nwin[tid] = max(nwin[tid], ((end - 1) >> 14) + 1)
+    return np.array(runs, np.int64).reshape(-1, 4), win, nwin
 
 
 def _records(b):

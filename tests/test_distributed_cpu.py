@@ -215,22 +215,67 @@ def _rank_bam(rank, world, port, outdir, layout):
                                       seed=c['seed'], backend=OracleBackend(), layout=layout,
                                       bam_fname=os.path.join(outdir, 'g.bam'), bam_header_text='@HD\tVN:1.0\n',
                                       bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)])
-    assert (st['bam_records'] > 0) == (rank == 0)
+    assert st['bam_records'] > 1000 and st['bam_rounds'] >= 1
   finally:
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,layout', [(1, None), (2, None), (3, 'slice')])
+@pytest.mark.parametrize('world,layout', [(1, None), (2, None), (3, 'slice'), (4, 'lpt')])
 def test_distributed_bam_leg(tmp_path, world, layout):
-  """The configs[4] BAM leg over gloo ranks (host stand-in backend: records from oracle/god.py): every rank builds
-  its pieces' records, rank 0 takes them in piece order and writes the coordinate-sorted stream — equal to the
-  god-aligner oracle's sorted records of the one-process FASTQ (ties in input order)."""
+  """The configs[4] BAM leg over gloo ranks (host stand-in backend: records from oracle/god.py, host BGZF): every
+  rank partitions its pieces' records by coordinate range and the all-to-all moves them to their range's rank; each
+  rank sorts its range (equal keys by tie = global input order), writes the part of the file whose blocks start in
+  its range (header on rank 0, the next ranges' heads completing its last block, EOF on the last rank); the parts
+  are placed by their sizes and the BAI joined from the ranks' plans.  The file is the one-process BGZF of the
+  god-aligner oracle's sorted stream, cut every 0xff00 bytes, and the BAI the oracle's over its virtual offsets."""
+  import numpy as np
   from tests._spawn import spawn_with_port
   from oracle import god
+  from mitty_amd import _native
   spawn_with_port(_rank_bam, lambda port: (world, port, str(tmp_path), layout), world)
   f1, f2 = open(tmp_path / 'r1.fq', 'rb').read(), open(tmp_path / 'r2.fq', 'rb').read()
   G.check_same(f1, G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'))
-  want = b''.join(god.encode(r) for r in god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2})))
+  stream = b''.join(god.encode(r) for r in god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2})))
+  assert len(stream) > 10 * 0xff00
+  refs = [('1', 50000), ('2', 20000), ('3', 8000)]
+  want = (_native.bgzf_compress(god.header_bytes('@HD\tVN:1.0\n', [{'SN': n, 'LN': ln} for n, ln in refs])) +
+          b''.join(_native.bgzf_compress(stream[o:o + 0xff00]) for o in range(0, len(stream), 0xff00)) +
+          _native.bgzf_eof())
   got = open(tmp_path / 'g.bam', 'rb').read()
-  assert len(want) > 100000
   assert got == want
+  _, recs, vo, vend = god.record_voffsets(got)
+  assert open(tmp_path / 'g.bam.bai', 'rb').read() == god.bai(3, [god.decode(r) for r in recs], vo, vend)
+  assert not [f for f in os.listdir(tmp_path) if '.part' in f]
+
+
+def test_range_splitters_and_bai_join():
+  """range_splitters: ascending keys at equal shares of the regions' bases (in @SQ order); bai_join of one plan is
+  bai_emit's layout (checked against god.bai on a tiny sorted set), and a run cut by a range boundary joins again."""
+  import numpy as np
+  from oracle import god
+  refs = [('1', 50000), ('2', 20000), ('3', 8000)]
+  sp = D.range_splitters([('2', 0, 20000), ('1', 0, 50000), ('3', 0, 8000)], refs, 3)
+  assert sp == [D.sort_key(0, 26000), D.sort_key(1, 2000)]
+  assert D.range_splitters([('1', 0, 10)], refs, 1) == []
+  assert D.range_splitters([('1', 0, 4)], refs, 8) == sorted(D.range_splitters([('1', 0, 4)], refs, 8))
+  # records: (tid, pos, end, bin) and voffsets; the same set as one plan or cut in two
+  recs = [dict(reference_id=0, pos=p, cigarstring='100M', bin=god.reg2bin(p, p + 100)) for p in (10, 20, 16380, 40000)]
+  vo = [100 << 16, 100 << 16 | 50, 100 << 16 | 90, 300 << 16]
+  vend = 300 << 16 | 70
+  ends = vo[1:] + [vend]
+
+  def plan(ks):
+    runs, win, nw = [], {}, 0
+    for k in ks:
+      r = recs[k]
+      if runs and runs[-1][1] == r['bin'] and runs[-1][3] == k:
+        runs[-1][3], runs[-1][5], runs[-1][6] = k + 1, ends[k], runs[-1][6] + 1
+      else:
+        runs.append([0, r['bin'], k, k + 1, vo[k], ends[k], 1])
+      for w in range(r['pos'] >> 14, ((r['pos'] + 99) >> 14) + 1):
+        win.setdefault(w, vo[k])
+      nw = max(nw, ((r['pos'] + 99) >> 14) + 1)
+    return {'runs': [tuple(x) for x in runs], 'win': {0: sorted(win.items())}, 'nwin': [nw, 0, 0]}
+  want = god.bai(3, recs, vo, vend)
+  assert D.bai_join([plan(range(4))], 3) == want
+  assert D.bai_join([plan([0]), plan([1, 2]), plan([3])], 3) == want

@@ -1002,7 +1002,7 @@ def test_emit_slices_concatenate_to_unit(native, corrupt):
     eng.close()
 
 
-def _gpu_rank(rank, world, port, layout, outdir, bam=False):
+def _gpu_rank(rank, world, port, layout, outdir, bam=False, spill_dir=None):
   import torch.distributed as dist
   os.environ['MASTER_ADDR'] = '127.0.0.1'
   os.environ['MASTER_PORT'] = str(port)
@@ -1013,9 +1013,10 @@ def _gpu_rank(rank, world, port, layout, outdir, bam=False):
     c = G.load_json('e2e_config.json')['1kg-pcr-free']
     mod, mdl = get_read_model('1kg-pcr-free.pkl')
     extra = {}
-    if bam:   # the configs[4] BAM leg: every rank's pieces as BAM records, merged and written by rank 0
+    if bam:   # the configs[4] BAM leg: every rank sorts and writes one coordinate range
       extra = dict(bam_fname=os.path.join(outdir, 'g.bam'), bam_header_text='@HD\tVN:1.0\tSO:coordinate\n',
-                   bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)], bam_capacity=bam if bam is not True else 0)
+                   bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)], bam_capacity=bam if bam is not True else 0,
+                   bam_spill_dir=spill_dir)
     D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
                                  c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
                                  seed=c['seed'], backend=D.DeviceBackend(0), layout=layout, **extra)
@@ -1082,28 +1083,45 @@ def test_distributed_two_ranks_one_gpu(native, tmp_path, layout):
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz'))
 
 
-@pytest.mark.parametrize('layout,cap', [('lpt', 0), ('slice', 300_000)])
-def test_distributed_bam_two_ranks_one_gpu(native, tmp_path, layout, cap):
-  """configs[4] across ranks: two ranks (gloo, both on GPU 0) each build the BAM records of their pieces on the
-  device; rank 0's store imports them in piece order (mh_bam_import) and writes BAM + BAI.  Equal byte for byte to
-  the one-rank run, and its records and index to the god-aligner oracle over the reference FASTQ; with a bounded
-  rank-0 store (cap) too."""
+@pytest.mark.parametrize('world,layout,cap,disk', [(2, 'lpt', 0, False), (2, 'slice', 300_000, False),
+                                                  (3, 'lpt', 200_000, True)])
+def test_distributed_bam_ranks_one_gpu(native, tmp_path, world, layout, cap, disk):
+  """configs[4] across ranks without a merging rank: 2 or 3 ranks (gloo, all on GPU 0) each build the BAM records of
+  their pieces on the device and partition them by coordinate range (mh_bam_partition); the all-to-all moves every
+  record to its range's rank, which sorts its range (ties by global input order), deflates the blocks that start in
+  it on the device (mh_bam_write_part) and contributes its BAI plan.  BAM and BAI equal the one-GPU god-aligner's
+  file (mh_bam_write_gpu over the same FASTQ, one store) byte for byte, and the records and index the oracle's; with
+  bounded range stores (cap) spilling to host memory or to temporary files (disk)."""
   from tests._spawn import spawn_with_port
   from oracle import god
-  one, two = tmp_path / 'one', tmp_path / 'two'
+  one, many = tmp_path / 'one', tmp_path / 'many'
   one.mkdir()
-  two.mkdir()
-  spawn_with_port(_gpu_rank, lambda port: (1, port, layout, str(one), True), 1)
-  spawn_with_port(_gpu_rank, lambda port: (2, port, layout, str(two), cap or True), 2)
+  many.mkdir()
+  spill = str(tmp_path / 'spill') if disk else None
+  if disk:
+    os.mkdir(spill)
+  spawn_with_port(_gpu_rank, lambda port: (world, port, layout, str(many), cap or True, spill), world)
   f1, f2 = G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz')
-  G.check_same(open(two / 'r1.fq', 'rb').read(), f1)
-  a, b = open(one / 'g.bam', 'rb').read(), open(two / 'g.bam', 'rb').read()
+  G.check_same(open(many / 'r1.fq', 'rb').read(), f1)
+  # the one-store reference: the god-aligner's own GPU writer over the same FASTQ
+  from mitty_amd.engine import Engine
+  eng = Engine(0)
+  try:
+    eng.ctx.bam_set_refs(['1', '2', '3'], [50000, 20000, 8000])
+    eng.ctx.bam_add_fastq(f1, f2)
+    eng.ctx.bam_write_gpu(str(one / 'g.bam'), '@HD\tVN:1.0\tSO:coordinate\n', bai_path=str(one / 'g.bam.bai'))
+  finally:
+    eng.close()
+  a, b = open(one / 'g.bam', 'rb').read(), open(many / 'g.bam', 'rb').read()
   assert a == b
-  assert open(one / 'g.bam.bai', 'rb').read() == open(two / 'g.bam.bai', 'rb').read()
+  assert open(one / 'g.bam.bai', 'rb').read() == open(many / 'g.bam.bai', 'rb').read()
   _, recs, vo, vend = god.record_voffsets(b)
   want = god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2}))
   assert len(recs) == len(want) > 1000 and recs == [god.encode(r) for r in want]
-  assert open(two / 'g.bam.bai', 'rb').read() == god.bai(3, [god.decode(r) for r in recs], vo, vend)
+  assert open(many / 'g.bam.bai', 'rb').read() == god.bai(3, [god.decode(r) for r in recs], vo, vend)
+  assert not [f for f in os.listdir(many) if '.part' in f]
+  if disk:
+    assert os.listdir(spill) == []   # (the spill files were unlinked when mapped)
 
 
 # ---- god-aligner BAM (SURVEY.md §8(a) A16) -------------------------------------------------------------------------
