@@ -498,14 +498,14 @@ def _bam_exchange(backend, part, world, group, stats):
     off, seg_n, seg_b = 8 * np.arange(world + 1, dtype=np.int64), np.zeros(world, np.int64), np.zeros(world, np.int64)
   else:
     off, seg_n, seg_b = part
-  if world == 1:
+  import torch.distributed as dist
+  if not (dist.is_available() and dist.is_initialized()):   # one process, no group: straight into the range store
     t = torch.empty(max(int(off[-1]), 8), dtype=torch.uint8)
     if part is not None:
       backend.bam_partition_into(t)
       backend.bam_import_segment(t, 0, int(seg_n[0]), int(seg_b[0]))
     stats['bam_sent'] = stats.get('bam_sent', 0) + int(seg_n.sum())
     return
-  import torch.distributed as dist
   dev = 'cuda' if dist.get_backend(group) == 'nccl' else 'cpu'
   # sizes first: (records, record bytes) per destination, all-to-all
   sz = torch.tensor(np.stack([seg_n, seg_b], 1).reshape(-1), dtype=torch.int64, device=dev)

@@ -7,7 +7,9 @@ runtime per process, DESIGN.md "Multi-GPU"):
   emit the same bytes, equal to the CPU oracle's unit;
 * allreduce_i64 on cuda tensors;
 * generate_reads_distributed under the nccl group (its piece-size / file-offset all-reduce runs through RCCL): the
-  files equal the golden reference FASTQ.
+  files equal the golden reference FASTQ;
+* its configs[4] BAM leg under the nccl group (records partitioned into cuda tensors, RCCL all-to-all, imported from
+  device memory): records and BAI equal the god-aligner oracle's.
 """
 import os
 import socket
@@ -67,6 +69,16 @@ def _child(rank, port, outdir, q):
                                       c['coverage'], os.path.join(outdir, 'r1.fq'), os.path.join(outdir, 'r2.fq'),
                                       seed=c['seed'])
     out['dist_stats'] = {k: st[k] for k in ('world', 'units', 'job_kept')}
+    # the configs[4] BAM leg under the nccl group: each piece's records partitioned into a cuda tensor, moved by
+    # RCCL's all-to-all, imported into the range store from device memory
+    c = G.load_json('e2e_config.json')['1kg-pcr-free']
+    mod, mdl = get_read_model('1kg-pcr-free.pkl')
+    st = D.generate_reads_distributed(G.path(c['fasta']), G.path(c['vcf']), c['sample'], G.path(c['bed']), mod, mdl,
+                                      c['coverage'], os.path.join(outdir, 'b1.fq'), os.path.join(outdir, 'b2.fq'),
+                                      seed=c['seed'], bam_fname=os.path.join(outdir, 'g.bam'),
+                                      bam_header_text='@HD\tVN:1.0\tSO:coordinate\n',
+                                      bam_refs=[('1', 50000), ('2', 20000), ('3', 8000)])
+    out['bam_stats'] = {k: st[k] for k in ('bam_records', 'bam_rounds', 'bam_received')}
     q.put(out)
   except BaseException as ex:   # noqa: BLE001 — reported to the parent
     import traceback
@@ -109,3 +121,12 @@ def test_rccl_world_one(tmp_path):
   assert out['dist_stats']['world'] == 1
   G.check_same(open(tmp_path / 'r1.fq', 'rb').read(), G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r1.fq.gz'))
   G.check_same(open(tmp_path / 'r2.fq', 'rb').read(), G.fastq_bytes('e2e_hiseq-X-v2.5-Garvan.r2.fq.gz'))
+  # the BAM leg over RCCL: records and BAI = the god-aligner oracle's over the reference FASTQ
+  from oracle import god
+  f1, f2 = G.fastq_bytes('e2e_1kg-pcr-free.r1.fq.gz'), G.fastq_bytes('e2e_1kg-pcr-free.r2.fq.gz')
+  b = open(tmp_path / 'g.bam', 'rb').read()
+  _, recs, vo, vend = god.record_voffsets(b)
+  want = god.sorted_stream(god.god_records(f1, f2, {'1': 0, '2': 1, '3': 2}))
+  assert out['bam_stats']['bam_records'] == out['bam_stats']['bam_received'] == len(recs) == len(want) > 1000
+  assert recs == [god.encode(r) for r in want]
+  assert open(tmp_path / 'g.bam.bai', 'rb').read() == god.bai(3, [god.decode(r) for r in recs], vo, vend)
