@@ -105,6 +105,10 @@ def parse():
   ap.add_argument('--plan-share', default=None, metavar='R/N',
                   help='wgs, one GPU, no process group: time only rank R\'s units of the N-rank LPT plan (a projection '
                        'of one rank of an N-GPU run; the JSON says so and is not the metric line)')
+  ap.add_argument('--emit-mode', type=int, default=0, choices=[0, 2, 3],
+                  help='0: every unit queued with no host readback (measure pass, tile scan, k_emit_tiles chained on '
+                       'the device); 2: the host reads each unit\'s totals before its writer (round 5); 3: the '
+                       'single-pass writer k_emit_fused (no measure pass)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
                   help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
@@ -297,7 +301,7 @@ def run_chr1(a):
   copies = synth.copies_soa(recs)
   units = _native.work_units(a.seed, [2], passes)
 
-  eng = Engine(0)
+  eng = Engine(0, a.emit_mode)
   if a.corrupt:
     eng.ctx.set_corruption(True, model['cum_bq_mat'], 10 ** (-np.arange(100) / 10), a.seed)
   eng.load_region(0, ('1', 0, a.length), seq)
@@ -732,7 +736,7 @@ def run_genome(a, rank, world, local):
     if dist.get_world_size() != world:
       sys.exit('bench.py: the process group has {} ranks, WORLD_SIZE={}'.format(dist.get_world_size(), world))
   from mitty_amd.engine import Engine
-  eng = Engine(local)
+  eng = Engine(local, a.emit_mode)
   copies = {}
   for ri in regions:
     name, length = contigs[ri]
@@ -750,12 +754,13 @@ def run_genome(a, rank, world, local):
 
   def step():
     eng.drop_haplotypes()
-    res = []
     for batch in batches:
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
-      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it
+      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it; their totals are collected
+      # once, at the end of the step (no host wait on a writer before then)
       eng.ctx.reset_output()
-      res += eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
+      eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True)
+    res = eng.collect()
     kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
     if dist is not None:
       counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))

@@ -178,6 +178,19 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
 int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_bytes1, int64_t *out_bytes2);
+/* mh_emit_reads for a whole unit of the current template set, queued with no host wait (the same bytes at the same
+ * arena offsets): the single-pass writer (k_emit_fused) finds each read's nodes, applies the N filter, measures and
+ * numbers the records and takes every 32-template tile's arena offset from a decoupled look-back over the launch's
+ * earlier tiles; the unit's end offsets pass to the next queued unit on the device.  No measure pass, no tile scan,
+ * no readback between units (readgenerate.py:184-230's worker loop, whose outputs are appended in order).  Units the
+ * single-pass writer does not cover (mh_set_emit_mode 1 or 2, qname heads over 96 bytes, reads over 321 bp, the
+ * in-place corruption) take mh_emit_reads' path inside the call.
+ *   mh_emit_collect  waits for the queued units and returns their (kept, bytes1, bytes2), 3 int64 per unit in queue
+ *                    order (out NULL: *n_units only); every entry point that reads or appends to the arenas
+ *                    (fetches, sizes, mh_emit_reads, BGZF, BAM, corrupt) first resolves the queued units itself. */
+int32_t mh_emit_reads_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                            int32_t write_fastq2, uint64_t unit_key);
+int32_t mh_emit_collect(mh_ctx *ctx, int64_t *out, int64_t cap, int64_t *n_units);
 /* The byte sizes a slice [t_begin, t_end) of the current template set will emit (t_end < 0: the whole set), without
  * writing it: the measure pass and its totals only (kept templates, bytes per FASTQ file), no buffer set held.  The
  * multi-GPU writer (mitty_amd/distributed.py) all-reduces these to place every piece in the files before any piece is
@@ -422,8 +435,10 @@ int32_t mh_enable_timing(mh_ctx *ctx, int32_t on);
 /* Host computation of the MT19937 window (x_J .. x_{J+623}, untempered) of the stream seeded with `seed`, via the
  * jump polynomial x^J mod P — the same math the device segments use (tests compare it with the plain recurrence). */
 int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624);
-/* Emission kernel choice: 0 = direct writer (default; falls back to 1 for a unit whose qname reads part exceeds
- * 256 bytes, with fused corruption, or for sample names too long for its LDS layout), 1 = LDS-image writer always. */
+/* Emission kernel choice: 0 = default (mh_emit_reads_async: the single-pass writer where it applies; otherwise and
+ * for mh_emit_reads the measure pass + direct tile writer, falling back to the LDS-image writer for sample names or
+ * records too long for its LDS layout), 1 = LDS-image writer always, 2 = never the single-pass writer (the measure
+ * pass + direct tile writer: the two-pass path, for tests and A/B). */
 int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode);
 /* Fisher-Yates swap-index decode and its exact fallbacks, a bit set (0 = the default):
  *   MH_DEC_SEQUENTIAL  the block-sequential decode always (by default it runs only when the chunk-parallel decode's

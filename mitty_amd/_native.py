@@ -20,7 +20,7 @@ EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_
            'mh_selftest_scan_fault', 'mh_selftest_sort',
            'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
-           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim', 'mh_device_live_bytes',
+           'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_reads_async', 'mh_emit_collect', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim', 'mh_device_live_bytes',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
            'mh_use_templates', 'mh_release_templates', 'mh_mt_window_at', 'mh_fixup_count', 'mh_set_emit_mode', 'mh_set_decode_mode',
            'mh_emit_reads_range', 'mh_emit_measure', 'mh_count_kept', 'mh_bam_set_refs', 'mh_bam_add_fastq', 'mh_bam_add_output',
@@ -99,6 +99,8 @@ def lib():
   _sig(L, 'mh_get_templates', [c_vp, c_vp, c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_emit_reads', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_emit_prepare', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, P_i64, P_i64, P_i64])
+  _sig(L, 'mh_emit_reads_async', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64])
+  _sig(L, 'mh_emit_collect', [c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_build_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
@@ -546,7 +548,8 @@ class Context:
     self._chk(self._L.mh_release_templates(self._h, int(tpl_id)))
 
   def set_emit_mode(self, mode):
-    """0: direct writer (default), 1: LDS-image writer."""
+    """0: default (the single-pass writer for emit_async, measure pass + direct writer for emit_reads), 1: LDS-image
+    writer, 2: never the single-pass writer (the two-pass path)."""
     self._chk(self._L.mh_set_emit_mode(self._h, int(mode)))
 
   def set_decode_mode(self, mode):
@@ -601,6 +604,20 @@ class Context:
                                             int(t_range[1]), int(cnt_base), ctypes.byref(k), ctypes.byref(b1),
                                             ctypes.byref(b2)))
     return k.value, b1.value, b2.value
+
+  def emit_async(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0):
+    """Queue the emission of the whole current template set (mh_emit_reads_async: the single-pass writer, no host
+    wait); emit_collect returns its (kept, bytes1, bytes2) with those of the other queued units."""
+    self._chk(self._L.mh_emit_reads_async(self._h, slot, serial_stub.encode(), chrom.encode(), int(cpy),
+                                          1 if write_fastq2 else 0, int(unit_key)))
+
+  def emit_collect(self):
+    """Wait for the queued emissions; [(kept, bytes1, bytes2)] per unit, in queue order."""
+    n = c_i64()
+    self._chk(self._L.mh_emit_collect(self._h, None, 0, ctypes.byref(n)))
+    out = np.zeros(3 * max(n.value, 1), np.int64)
+    self._chk(self._L.mh_emit_collect(self._h, _ptr(out), n.value, ctypes.byref(n)))
+    return [tuple(int(x) for x in out[3 * i:3 * i + 3]) for i in range(n.value)]
 
   def emit_measure(self, slot, serial_stub, chrom, cpy, write_fastq2=True, unit_key=0, t_range=None, cnt_base=0):
     """(kept, bytes1, bytes2) that emit_reads with the same arguments will produce, without writing anything."""

@@ -58,7 +58,11 @@ bool scan_fault_pending(const mh_ctx *ctx) {
 void lane_thread_enter(mh_ctx *ctx) { scan_fault_slot = ctx->fault_slot; }
 
 int32_t scan_fault_fail(mh_ctx *ctx) {
-  (void)scan_fault_take(ctx ? ctx->fault_slot : 0);
+  const uint32_t v = scan_fault_take(ctx ? ctx->fault_slot : 0);
+  // bits 2 and 4: the single-pass FASTQ writer (k_emit_fused) found a read's qname part past the splice's bound, or
+  // a tile past the arena it was given; it stored nothing wrong there, but the unit's output is incomplete
+  if (v & 2u) return arg_fail(ctx, MH_E_STATE, "single-pass writer: a qname part exceeded the splice's bound (internal)");
+  if (v & 4u) return arg_fail(ctx, MH_E_STATE, "single-pass writer: the arena reservation was too small (internal)");
   return arg_fail(ctx, MH_E_STATE, "a look-back scan's wait timed out (a broken ticket base or scratch): its offsets "
                                    "are wrong");
 }
@@ -456,6 +460,7 @@ const char *mh_last_error(const mh_ctx *ctx) { return ctx ? ctx->err.c_str() : "
 
 int32_t mh_sync(mh_ctx *ctx) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
   return MH_OK;
 }
@@ -999,6 +1004,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
 int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                       int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   CTX_GUARD_EMIT(ctx);
+  MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
@@ -1009,6 +1015,7 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
 int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
                         int32_t write_fastq2, uint64_t unit_key, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   CTX_GUARD_EMIT(ctx);
+  MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || (!out_kept) != (!out_b1) || (!out_kept) != (!out_b2))
@@ -1021,12 +1028,45 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
                             int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end,
                             int64_t cnt_base, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2) {
   CTX_GUARD_EMIT(ctx);
+  MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (t_begin < 0 || t_end < t_begin || cnt_base < 0) return arg_fail(ctx, MH_E_ARG, "bad template range");
   return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,
                     false, out_kept, out_b1, out_b2);
+}
+
+int32_t mh_emit_reads_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
+                            int32_t write_fastq2, uint64_t unit_key) {
+  CTX_GUARD_EMIT(ctx);
+  auto it = ctx->haps.find(slot);
+  if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (!serial_stub || !chrom) return arg_fail(ctx, MH_E_ARG, "null argument");
+  bool queued = false;
+  MH_TRY(emit_unit_async(ctx, it->second, serial_stub, chrom, cpy, write_fastq2, unit_key, &queued));
+  if (queued) return MH_OK;
+  // a unit the single-pass writer does not cover: the two-pass path at the arenas' exact ends, its totals queued
+  // in order with the others
+  MH_TRY(lazy_resolve(ctx));
+  int64_t k = 0, b1 = 0, b2 = 0;
+  MH_TRY(emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, false, &k, &b1,
+                    &b2));
+  ctx->lazy.push_back(mh_ctx::LazyUnit{-1, ctx->lazy_gen, {k, b1, b2}});
+  return MH_OK;
+}
+
+int32_t mh_emit_collect(mh_ctx *ctx, int64_t *out, int64_t cap, int64_t *n_units) {
+  CTX_GUARD_EMIT(ctx);
+  if (!n_units) return arg_fail(ctx, MH_E_ARG, "null argument");
+  MH_TRY(lazy_resolve(ctx));
+  const int64_t n = (int64_t)ctx->lazy_done.size() / 3;
+  *n_units = n;
+  if (!out) return MH_OK;   // (the count only: the totals stay for the next call)
+  if (cap < n) return arg_fail(ctx, MH_E_CAPACITY, "mh_emit_collect: room for " + std::to_string(n) + " units needed");
+  std::memcpy(out, ctx->lazy_done.data(), sizeof(int64_t) * 3 * (size_t)n);
+  ctx->lazy_done.clear();
+  return MH_OK;
 }
 
 int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, const char *chrom, int64_t cpy,
@@ -1058,6 +1098,7 @@ int32_t mh_count_kept(mh_ctx *ctx, int32_t slot, int64_t t_begin, int64_t t_end,
 
 int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
   CTX_GUARD_EMIT(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if (b1) *b1 = ctx->used1;
   if (b2) *b2 = ctx->used2;
   return MH_OK;
@@ -1065,6 +1106,7 @@ int32_t mh_output_size(mh_ctx *ctx, int64_t *b1, int64_t *b2) {
 
 int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2, int64_t len2) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if ((fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
@@ -1092,6 +1134,7 @@ int32_t mh_output_fetch(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int6
 int32_t mh_output_fetch_async(mh_ctx *ctx, int64_t off1, char *fq1, int64_t len1, int64_t off2, char *fq2,
                               int64_t len2, int32_t *ticket) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if (!ticket || (fq1 && (off1 < 0 || len1 < 0 || off1 + len1 > ctx->used1)) ||
       (fq2 && (off2 < 0 || len2 < 0 || off2 + len2 > ctx->used2)))
     return arg_fail(ctx, MH_E_ARG, "fetch range outside the arena");
@@ -1134,6 +1177,11 @@ int32_t mh_output_reset(mh_ctx *ctx) {
       ctx->fetch_pending[t] = false;
     }
   ctx->used1 = ctx->used2 = 0;
+  // the single-pass chain starts again from the empty arenas; units still queued keep their totals for
+  // mh_emit_collect but no longer move the arenas
+  ctx->chain_open = false;
+  ctx->lazy_gen++;
+  ctx->used_ub1 = ctx->used_ub2 = 0;
   return MH_OK;
 }
 
@@ -1346,8 +1394,10 @@ int32_t mh_mt_window_at(uint32_t seed, uint64_t offset, uint32_t *out624) {
 }
 
 int32_t mh_set_emit_mode(mh_ctx *ctx, int32_t mode) {
-  if (!ctx || mode < 0 || mode > 1) return MH_E_ARG;
+  if (!ctx || mode < 0 || mode > 3) return MH_E_ARG;
   ctx->emit_lds_only = mode == 1;
+  ctx->emit_two_pass = mode == 2;
+  ctx->emit_single = mode == 3;
   return MH_OK;
 }
 
@@ -1420,6 +1470,7 @@ int32_t mh_bam_add_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char 
 
 int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if (!templates) return arg_fail(ctx, MH_E_ARG, "null argument");
   int64_t u1 = 0, u2 = 0;
   const bool two = ctx->used2 > 0;
@@ -1921,6 +1972,7 @@ int32_t mh_bam_bai_runs(mh_ctx *ctx, int64_t *n_runs, int64_t *runs, int64_t run
 int32_t mh_corrupt_fastq(mh_ctx *ctx, const char *fq1, int64_t len1, const char *fq2, int64_t len2, int64_t t_base,
                          int64_t *used1, int64_t *used2, int64_t *templates) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if (!fq1 || len1 < 0 || (fq2 && len2 < 0) || t_base < 0 || !used1 || !used2 || !templates)
     return arg_fail(ctx, MH_E_ARG, "null argument");
   MH_TRY(stage_in(ctx, ctx->bam.in1, fq1, len1));
@@ -1994,6 +2046,7 @@ int32_t mh_bgzf_compress_gpu(mh_ctx *ctx, const char *in, int64_t len, char *out
 int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t len, char *out, int64_t cap,
                              int64_t *used) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if ((file != 0 && file != 1) || !used || offset < 0 || len < 0) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
   const int64_t n = file ? ctx->used2 : ctx->used1;
@@ -2020,6 +2073,7 @@ int32_t mh_output_bgzf_range(mh_ctx *ctx, int32_t file, int64_t offset, int64_t 
 int32_t mh_output_bgzf_pair(mh_ctx *ctx, int64_t offset, int64_t n1, int64_t n2, char *out1, int64_t cap1,
                             char *out2, int64_t cap2, int64_t *used1, int64_t *used2, int32_t *ticket) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if (!used1 || !used2 || !ticket || offset < 0 || n1 < 0 || n2 < 0 || (n1 && !out1) || (n2 && !out2))
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
   MH_TRY(sync_writers(ctx));   // the writers (and corruption passes) of the arena's last units
@@ -2087,6 +2141,7 @@ int32_t mh_output_bgzf_wait(mh_ctx *ctx, int32_t ticket) {
 
 int32_t mh_output_bgzf(mh_ctx *ctx, int32_t file, char *out, int64_t cap, int64_t *used) {
   CTX_GUARD(ctx);
+  MH_TRY(lazy_resolve(ctx));
   if ((file != 0 && file != 1) || !used) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   return mh_output_bgzf_range(ctx, file, 0, file ? ctx->used2 : ctx->used1, out, cap, used);
 }

@@ -830,6 +830,16 @@ struct TArgs {
   const uint4 *crow;        // corruption rows (CR 2, k_cr_rows): per block of 15 bases its qualities + 33, and
   const uint32_t *ccode;    //   its 2-bit substitution codes; slot (file * nb + block) * m + template
   int32_t nb;               // blocks per record row
+  // the single-pass writer (k_emit_fused): no measure pass, its tiles' prefixes by a decoupled look-back
+  uint64_t *lb;             // look-back scratch: ticket word (64 B), then 3 aggregate and 3 inclusive words per tile
+  int64_t ntiles;
+  uint32_t tbase, epoch;    // the ticket counter's value at launch; this launch's epoch (mh_scan.h lb_reserve)
+  uint32_t *fault;          // the context's fault word: 1 look-back timeout, 2 qname row overflow, 4 arena overflow
+  const int64_t *cur_in;    // arena ends after the previous unit of the chain (null: used[])
+  int64_t *cur_out;         // after this unit: kept, end of file 1, end of file 2 (device cursor; the last tile)
+  int64_t *res;             // kept, bytes 1, bytes 2, end 1, end 2 (mapped host memory; the last tile)
+  int64_t cap[2];           // arena capacities (bytes)
+  int32_t hcap;             // qname row room for the reads part and its '\n'
 };
 
 // CR: the corrupt layout — len(seq) qualities per record (illumina.corrupt_single_read, illumina.py:140-162): T is
@@ -871,11 +881,16 @@ __device__ __forceinline__ uint32_t lds_put_s(char *lds, uint32_t o, int64_t v) 
     }                                                                                                    \
   }
 
-template <int NF, int LPR, int CR, int GW>
+// FU: the single-pass writer — wave 0 finds each read's nodes, applies the N filter and measures the records itself
+// (what k_emit_measure wrote to Rec), publishes the tile's sums and takes its prefix by a decoupled look-back over
+// the earlier tiles of the launch (mh_scan.h's status words), instead of reading the measure pass's records and the
+// tile scan's prefixes.
+template <int NF, int LPR, int CR, int GW, bool FU = false>
 __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const int64_t tile) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int64_t s_g[2];      // arena offset of the tile's first byte per file
   __shared__ int32_t s_span[2];   // the tile's bytes per file
+  __shared__ int32_t s_skip;      // FU: the tile's records would pass the arena's end (reported, nothing stored)
   // LDS layout (byte offsets): meta | pad | windows [ED_T][2][win_stride] | pad | qname buffers [ED_T][qstride] |
   // pad | T | pad | seam chunks [NF][ED_T][4] x 16 B | dump (16 B)
   DMeta *meta = (DMeta *)smem;
@@ -966,27 +981,97 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
     const int fo = A.fo0[tf];
     const int fr = s == 0 ? fo : 1 - fo;   // the read's place in the qname = its file (reads[fo] = mate 0, :207)
     const int64_t rl = A.rlen;
-    // the measure pass's record: keep | first part length << 1, record lengths, both parts' length, nodes
-    const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
-    const E3 P = A.tpre[tile];
-    const int64_t n0 = s ? r1.y : r1.x, n1 = s ? r1.w : r1.z;
-    const bool keep = valid && (r0.x & 1);
-    const int32_t rest = r0.w;
-    // the read's nodes: the first four loaded together (a 150-bp read spans one to three at 1.3 variants/kbp)
-    const Node16 q0 = h.nd[n0], q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0], q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0],
-                 q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
     int64_t a = p - h.p_min, e = p + rl - h.p_min;   // the read's bases: hap[a, a + S)
     if (e > h.hap_len) e = h.hap_len;
     if (a > h.hap_len) a = h.hap_len;
     const int32_t S = (int32_t)(e > a ? e - a : 0);
-    if (keep) {
-      ReadInfo ri;
+    int64_t n0, n1;
+    Node16 q0, q1, q2, q3;   // the read's nodes: the first four loaded together (a 150-bp read spans one to three)
+    ReadInfo ri;
+    bool keep;
+    int32_t rest, flen, lw;  // both reads' qname parts; the file-1 read's part (where the other starts); record bytes
+    E3 P;                    // kept templates and record bytes (no cnt digits) before the tile
+    if constexpr (FU) {
+      // rpc.get_begin_end_nodes (rpc.py:119-130): the start node by the bucketed search, the end node from the four
+      // nodes loaded at once (further only past them)
+      n0 = node_upper(h, p) - 1;
+      const int64_t last = h.n_nodes - 1;
+      q0 = h.nd[n0];
+      q1 = h.nd[n0 + 1 < last ? n0 + 1 : last];
+      q2 = h.nd[n0 + 2 < last ? n0 + 2 : last];
+      q3 = h.nd[n0 + 3 < last ? n0 + 3 : last];
+      const int64_t x = p + rl - 1;
+      n1 = n0;
+      if (n0 + 1 <= last && q1.key() <= x) {
+        n1 = n0 + 1;
+        if (n0 + 2 <= last && q2.key() <= x) {
+          n1 = n0 + 2;
+          if (n0 + 3 <= last && q3.key() <= x) n1 = node_walk(h, n0 + 3, x);
+        }
+      }
       ri.n0 = n0;
       ri.n1 = n1;
       read_place(h, q0, p, rl, ri);
+      // the read's qname part length (readgenerate.py:223-225; k_emit_measure's read_part_len)
+      int32_t L = 3 + ndig_s(ri.pos) + 1 + ndig_s(rl) + 1 + 1;
+      if (ri.special) L += 1 + ndig_s(p - q0.ps()) + 1 + ndig_s(rl) + 1;
+      int32_t nv = 0;
+      for (int64_t k = n0; k <= n1; k++) {
+        NODE_AT(k)
+        if (!ri.special) L += ndig_s(node_count(n, p, rl)) + 1;
+        if (n.code() != 0) {
+          L += ndig_s(node_v(n)) + (nv ? 1 : 0);
+          nv++;
+        }
+      }
+      // the N filter (readgenerate.py:201-204) over both mates: the pair's two lanes exchange their verdicts and parts
+      const int kr = count_N(h, a, a + S) <= 2;
+      const int ko = __shfl_xor(kr, 1, 64);
+      const int32_t Lo = __shfl_xor(L, 1, 64);
+      keep = valid && kr && ko;
+      rest = L + Lo;
+      flen = fr == 0 ? L : Lo;
+      lw = keep ? Lp + Lm + rest + 1 + S + 3 + (CR ? S : (int32_t)rl) + 1 : 0;
+      P = E3{0, 0, 0};
+    } else {
+      // the measure pass's record: keep | first part length << 1, record lengths, both parts' length, nodes
+      const int4 r0 = *(const int4 *)(A.recs + tf), r1 = *(const int4 *)((const char *)(A.recs + tf) + 16);
+      P = A.tpre[tile];
+      n0 = s ? r1.y : r1.x;
+      n1 = s ? r1.w : r1.z;
+      keep = valid && (r0.x & 1);
+      rest = r0.w;
+      flen = r0.x >> 1;
+      lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
+      q0 = h.nd[n0];
+      q1 = h.nd[n0 + 1 <= n1 ? n0 + 1 : n0];
+      q2 = h.nd[n0 + 2 <= n1 ? n0 + 2 : n0];
+      q3 = h.nd[n0 + 3 <= n1 ? n0 + 3 : n0];
+      ri.n0 = n0;
+      ri.n1 = n1;
+      if (keep) read_place(h, q0, p, rl, ri);
+    }
+    // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
+    const int32_t ik = wave_incl_scan(keep && fr == 0 ? 1 : 0);
+    const int32_t i0 = wave_incl_scan(fr == 0 ? lw : 0);
+    const int32_t i1 = wave_incl_scan(fr == 1 ? lw : 0);
+    const int32_t tk = __shfl(ik, 63, 64), tb0 = __shfl(i0, 63, 64), tb1 = __shfl(i1, 63, 64);
+    const int lane = tid;
+    uint64_t *const lb_agg = FU ? A.lb + 8 : nullptr, *const lb_inc = FU ? lb_agg + 3 * A.ntiles : nullptr;
+    if constexpr (FU) {   // the tile's sums out first: later tiles' look-backs wait for them, not for the formatting
+      const int64_t tv = lane == 0 ? tk : lane == 1 ? tb0 : tb1;
+      if (lane < 3) lb_put((tile == 0 ? lb_inc : lb_agg) + (size_t)lane * A.ntiles + tile, tv, tile == 0 ? 2u : 1u,
+                           A.epoch);
+    }
+    bool fmt = keep;
+    if (FU && keep && rest + 1 > A.hcap) {   // (the splice's bound was wrong: reported, the row never overrun)
+      fmt = false;
+      if (A.fault) __hip_atomic_fetch_or(A.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (fmt) {
       // the read's part of the qname at its place (readgenerate.py:223-225); read 1 ends at `rest`, where the '\n' goes
       uint32_t o = (uint32_t)(o_q + jf * qstride + head);
-      if (fr == 1) o += (uint32_t)(r0.x >> 1);   // after the first read's part
+      if (fr == 1) o += (uint32_t)flen;   // after the first read's part
       smem[o] = '|';
       smem[o + 1] = (char)('0' + s);
       smem[o + 2] = '|';
@@ -1018,26 +1103,111 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
       }
       if (fr == 1) smem[o] = '\n';
     }
-    // this read's record (file fr) without the cnt digits; the wave's inclusive sums of (kept, bytes per file)
-    const int32_t lw = keep ? (fr == 0 ? r0.y : r0.z) : 0;
-    const int32_t ik = wave_incl_scan(keep && fr == 0 ? 1 : 0);
-    const int32_t i0 = wave_incl_scan(fr == 0 ? lw : 0);
-    const int32_t i1 = wave_incl_scan(fr == 1 ? lw : 0);
-    // sums over the tile's templates before this one (the inclusive value of lane 2 jf - 1) and the tile's totals
+    int64_t u0 = A.used[0], u1 = A.used[1];   // arena offsets of the emission's first byte
+    if constexpr (FU) {
+      // the look-back (mh_scan.h k_scan_lb's, three fields): lane l reads tile j - l's words; the nearest tile with an
+      // inclusive prefix ends the walk, the aggregates after it are summed
+      if (tile > 0) {
+        // (lane l reads tiles j - LB_TPL l - t, t < LB_TPL: a wave step covers 64 LB_TPL tiles; four tiles per lane
+        // measured slower than one: 2.47 against 1.92 ms per chr1-size unit alone, the polls' traffic)
+        constexpr int LB_TPL = 1;
+        E3 prefix{0, 0, 0};
+        for (int64_t j = tile - 1;; j -= 64 * LB_TPL) {
+          bool is_inc = false, ok = false;
+          E3 val{0, 0, 0};
+          uint32_t spins = 0;
+          while (!ok) {
+            // this lane's tiles, nearest first: aggregates summed up to the first inclusive prefix (taken, then stop)
+            bool ready = true, hit = false;
+            E3 v{0, 0, 0};
+#pragma unroll
+            for (int t = 0; t < LB_TPL; t++) {
+              const int64_t jj = j - LB_TPL * lane - t;
+              uint64_t wi[3], wa[3];
+#pragma unroll
+              for (int k = 0; k < 3; k++) {
+                wi[k] = jj >= 0 ? lb_get(lb_inc + (size_t)k * A.ntiles + jj) : 0;
+                wa[k] = jj >= 0 ? lb_get(lb_agg + (size_t)k * A.ntiles + jj) : 0;
+              }
+              if (jj < 0 || hit) continue;
+              bool all_inc = true, all_agg = true;
+#pragma unroll
+              for (int k = 0; k < 3; k++) {
+                all_inc &= lb_flag(wi[k], A.epoch) == 2u;
+                all_agg &= lb_flag(wa[k], A.epoch) == 1u;
+              }
+              const uint64_t *w = all_inc ? wi : wa;
+              if (all_inc || all_agg) {
+                v = v + E3{(int64_t)(w[0] >> LB_VAL_SHIFT), (int64_t)(w[1] >> LB_VAL_SHIFT),
+                           (int64_t)(w[2] >> LB_VAL_SHIFT)};
+                hit = all_inc;
+              } else {
+                ready = false;
+              }
+            }
+            if (ready) {
+              ok = true;
+              is_inc = hit || j - LB_TPL * lane < 0;   // (past tile 0: nothing further back)
+              val = v;
+            } else if (++spins > (1u << 24)) {   // (a bound on the wait: reported, never a hung GPU)
+              ok = is_inc = true;
+              if (A.fault) __hip_atomic_fetch_or(A.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+              __builtin_amdgcn_s_sleep(1);
+            }
+          }
+          const uint64_t bal = __ballot(is_inc);
+          const int first = bal ? __builtin_ctzll(bal) : 64;   // nearest lane whose tiles reach an inclusive prefix
+          if (lane > first) val = E3{0, 0, 0};
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) val = val + shfl_xor_t(val, d);
+          prefix = prefix + val;
+          if (first < 64) break;
+        }
+        P = prefix;
+        const E3 mine = prefix + E3{tk, tb0, tb1};
+        const int64_t mv = lane == 0 ? mine.kept : lane == 1 ? mine.b1 : mine.b2;
+        if (lane < 3) lb_put(lb_inc + (size_t)lane * A.ntiles + tile, mv, 2u, A.epoch);
+      }
+    }
+    if (A.cur_out) {   // a chained unit (mh_emit_reads_async): no host readback between units
+      if (A.cur_in) {  // where the previous unit's writer ended
+        u0 = A.cur_in[1];
+        u1 = A.cur_in[2];
+      }
+      if (tile == A.ntiles - 1 && lane == 0) {   // the unit's totals: the next unit's start, the host's readback
+        const E3 T = P + E3{tk, tb0, tb1};
+        const int64_t ds = digit_sum(A.cnt_base + T.kept) - digit_sum(A.cnt_base);
+        const int64_t b1 = T.b1 + ds, b2 = NF == 2 ? T.b2 + ds : 0;
+        A.cur_out[0] = T.kept;
+        A.cur_out[1] = u0 + b1;
+        A.cur_out[2] = u1 + b2;
+        A.res[0] = T.kept;
+        A.res[1] = b1;
+        A.res[2] = b2;
+        A.res[3] = u0 + b1;
+        A.res[4] = u1 + b2;
+      }
+    }
+    // sums over the tile's templates before this one (the inclusive value of lane 2 jf - 1)
     const int src = jf ? 2 * jf - 1 : 0;
     int32_t xk = __shfl(ik, src, 64), x0 = __shfl(i0, src, 64), x1 = __shfl(i1, src, 64);
     if (jf == 0) xk = x0 = x1 = 0;
-    const int32_t tk = __shfl(ik, 63, 64), tb0 = __shfl(i0, 63, 64), tb1 = __shfl(i1, 63, 64);
     const int64_t K0 = A.cnt_base + P.kept;                          // templates kept before the tile
     const int64_t ds0 = digit_sum(K0) - digit_sum(A.cnt_base);       // cnt digits of the emission's records before it
-    const int64_t g0 = A.used[0] + P.b1 + ds0;
-    const int64_t g1 = A.used[1] + P.b2 + ds0;
+    const int64_t g0 = u0 + P.b1 + ds0;
+    const int64_t g1 = u1 + P.b2 + ds0;
     if (tid == 0) {
       const int64_t dst = digit_sum(K0 + tk) - digit_sum(K0);        // ... of the tile's records
       s_g[0] = g0;
       s_g[1] = g1;
       s_span[0] = (int32_t)(tb0 + dst);
       s_span[1] = (int32_t)(tb1 + dst);
+      s_skip = 0;
+      if (FU && (g0 + tb0 + dst > A.cap[0] || (NF == 2 && g1 + tb1 + dst > A.cap[1]))) {
+        s_skip = 1;
+        if (A.fault) __hip_atomic_fetch_or(A.fault, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
     if (valid) {
       DMeta &mt = meta[jf];
@@ -1127,6 +1297,7 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
   }
   const int64_t gbase[2] = {s_g[0], s_g[1]};
   const int32_t span[2] = {s_span[0], s_span[1]};
+  if (FU && s_skip) return;
   ed_output<NF, LPR, CR>(meta, nt, gbase, span, o_t, TL, o_s, staged, A.arena EWP_ARG);
   EWP_END;
 }
@@ -1137,6 +1308,16 @@ __device__ __forceinline__ void emit_tile(const TArgs &A, const QHead &qh, const
 template <int NF, int LPR, int CR, int GW>
 __global__ void __launch_bounds__(ED_THREADS) k_emit_tiles(TArgs A, QHead qh) {
   emit_tile<NF, LPR, CR, GW>(A, qh, blockIdx.x);
+}
+
+// The single-pass writer: tiles numbered by an atomic ticket in the order they start (HIP promises no dispatch
+// order), so every tile a look-back waits for is already running.
+template <int NF, int LPR, int CR, int GW>
+__global__ void __launch_bounds__(ED_THREADS) k_emit_fused(TArgs A, QHead qh) {
+  __shared__ int64_t s_tile;
+  if (threadIdx.x == 0) s_tile = (int64_t)(uint32_t)(atomicAdd((uint32_t *)A.lb, 1u) - A.tbase);
+  __syncthreads();
+  emit_tile<NF, LPR, CR, GW, true>(A, qh, s_tile);
 }
 
 // ---- BQ corruption of the emitted records (illumina.corrupt_template, illumina.py:139-162) ---------------------
@@ -2223,6 +2404,214 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
   *out_kept = ht.kept;
   *out_b1 = ht.b1;
   *out_b2 = write_fastq2 ? ht.b2 : 0;
+  return MH_OK;
+}
+
+// ---- the single-pass writer's host side -----------------------------------------------------------------------
+using EfKernel = void (*)(TArgs, QHead);
+static EfKernel ef_kernel(int cr, bool two) {
+  return cr == 2 ? (two ? k_emit_fused<2, 4, 2, 3> : k_emit_fused<1, 8, 2, 3>)
+                 : (two ? k_emit_fused<2, 4, 0, 3> : k_emit_fused<1, 8, 0, 3>);
+}
+static int32_t ndig_host(int64_t v) {
+  int32_t d = 1;
+  for (; v >= 10; v /= 10) d++;
+  return d;
+}
+
+int32_t emit_unit_async(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, bool *queued) {
+  *queued = false;
+  auto tit = ctx->tsets.find(ctx->cur_tpl);
+  if (tit == ctx->tsets.end() || !tit->second.valid)
+    return arg_fail(ctx, MH_E_STATE, "no templates: call mh_sample_templates / mh_use_templates first");
+  const TplSet &tp = tit->second;
+  const int64_t m = tp.n, rlen = tp.rlen;
+  const int32_t nf = write_fastq2 ? 2 : 1;
+  const std::string prefix = std::string("@") + serial_stub + ":";
+  const std::string mid = std::string("|") + chrom + "|" + std::to_string(cpy);
+  // what the single-pass writer covers (the rest takes emit_reads: the LDS-image writer, long names, reads past
+  // the windows the splice bounded, the in-place corruption)
+  if (ctx->emit_lds_only || ctx->emit_two_pass || !h.bound_valid || m >= (int64_t)UINT32_MAX) return MH_OK;
+  int w = 0;
+  while (w < PB_NW && PB_W[w] < rlen) w++;
+  QHead qh{};
+  if (w == PB_NW || prefix.size() + mid.size() > sizeof(qh.w)) return MH_OK;
+  const bool cr_rows = ctx->corrupt_on && cr_rows_lds(nf, rlen, ctx->corrupt_n_bq);
+  if (ctx->corrupt_on && (!cr_rows || rlen > ctx->corrupt_max_bp)) return MH_OK;
+  // a read's qname part: '|' s '|' POS '|' rlen '|' + its nodes' CIGAR and v_list bytes (the splice's bound) + '|'
+  const int32_t part_b = 3 + std::max(ndig_host(h.pos_max), 2) + 1 + ndig_host(rlen) + 1 + 1 + h.part_w[w];
+  const int32_t hslot = 2 * part_b + 1;   // both reads' parts + '\n'
+  const int32_t win_stride = (int32_t)(((rlen + 31) / 16) * 16);
+  const int32_t head = (int32_t)(((prefix.size() + mid.size() + 10 + 16) + 15) / 16 * 16);
+  const int32_t hrow = (hslot + 15) / 16 * 16;
+  const int32_t qstride = head + hrow + 32 + ED_QPAD;
+  const size_t lds_d = ed_lds_bytes(win_stride, qstride, rlen, nf, cr_rows);
+  if (win_stride > 16 * 3 * ED_GMAX || lds_d > 64 * 1024) return MH_OK;
+  // the default: the measure pass and the tile scan queued on the main stream, the writer on the writer stream, the
+  // unit's offsets and totals passed on the device (no readback); mh_set_emit_mode(3): the single-pass writer
+  const bool single = ctx->emit_single;
+  if (!single && m > 0 && ctx->eset[ctx->eset_i].prepared) return MH_OK;   // (a prepared unit holds the next set)
+  *queued = true;
+  if ((int64_t)ctx->lazy.size() >= mh_ctx::LZ_SLOTS) MH_TRY(lazy_resolve(ctx));   // (the result slots are full)
+  if (m == 0) {
+    ctx->lazy.push_back(mh_ctx::LazyUnit{-1, ctx->lazy_gen, {0, 0, 0}});
+    return MH_OK;
+  }
+  if (!ctx->h_lazy) {
+    if (hipHostMalloc((void **)&ctx->h_lazy, 64 * (size_t)mh_ctx::LZ_SLOTS,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      ctx->h_lazy = nullptr;
+      return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+    }
+    void *d = nullptr;
+    HIPCHK(ctx, hipHostGetDevicePointer(&d, ctx->h_lazy, 0));
+    ctx->d_lazy = (int64_t *)d;
+  }
+  MH_TRY(ensure(ctx, ctx->d_cur, 32 * (size_t)(mh_ctx::LZ_SLOTS + 1)));
+  // arenas: room for the chain's upper bound (every record at the bound: the longest qname part twice, both reads)
+  if (!ctx->chain_open) {
+    ctx->used_ub1 = ctx->used1;
+    ctx->used_ub2 = ctx->used2;
+  }
+  const int64_t rec_b = (int64_t)(prefix.size() + mid.size()) + ndig_host(m) + hslot + 2 * rlen + 5;
+  const int64_t add = m * rec_b;
+  MH_TRY(ensure_keep(ctx, ctx->out1, ctx->used_ub1 + add + 64, ctx->used_ub1));
+  if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, ctx->used_ub2 + add + 64, ctx->used_ub2));
+  const int64_t ntiles = (m + ED_T - 1) / ED_T;
+  const size_t lb_need = 64 + 48 * (size_t)ntiles + 64;
+  int32_t set = -1;
+  if (single) {
+    MH_TRY(ensure(ctx, ctx->fused_lb, lb_need));
+  } else {
+    set = ctx->eset_i;
+    EmitSet &es = ctx->eset[set];
+    ctx->eset_i = (ctx->eset_i + 1) % mh_ctx::N_ESET;
+    if (m > ctx->eset_max_m) ctx->eset_max_m = m;
+    const int64_t mm = ctx->eset_max_m, mt = (mm + ED_T - 1) / ED_T;
+    MH_TRY(ensure(ctx, es.recs, sizeof(Rec) * mm));
+    MH_TRY(ensure(ctx, es.tsum, sizeof(int4) * (size_t)mt));
+    MH_TRY(ensure(ctx, es.tpre, sizeof(E3) * (size_t)mt));
+    MH_TRY(ensure(ctx, es.stat, 64));
+    MH_TRY(ensure(ctx, ctx->scan_partials, scan_lb_scratch_bytes<E3>(ntiles)));
+  }
+  CorruptCfg cc{0, nullptr, nullptr, 0, 0, 0, 0, 0, 0};
+  if (cr_rows) {
+    cc = corrupt_cfg(ctx, unit_key, 0);
+    MH_TRY(cr_rows_alloc(ctx, m, nf, rlen));
+  }
+  // (every allocation above may drain the writers; from here on nothing does)
+  const std::string pm = prefix + mid;
+  std::memcpy(qh.w, pm.data(), pm.size());
+  qh.lp = (int32_t)prefix.size();
+  qh.lm = (int32_t)mid.size();
+  const int64_t seq = ctx->lazy_seq;
+  const int32_t rslot = (int32_t)(seq % mh_ctx::LZ_SLOTS);
+  int64_t *d_cur = (int64_t *)ctx->d_cur.p;
+  hipStream_t ws = ctx->wstream;
+  uint32_t tbase = 0, epoch = 0;
+  if (single) HIPCHK(ctx, lb_reserve(ws, ctx->fused_lb.p, lb_need, (uint32_t)ntiles, &tbase, &epoch));
+  TArgs A{};
+  A.h = view_of(h);
+  A.m = m;
+  A.pos0 = (const int64_t *)tp.pos0.p;
+  A.pos1 = (const int64_t *)tp.pos1.p;
+  A.fo0 = (const int8_t *)tp.fo0.p;
+  A.arena[0] = (char *)ctx->out1.p;
+  A.arena[1] = (char *)ctx->out2.p;
+  A.used[0] = ctx->used1;
+  A.used[1] = ctx->used2;
+  A.cnt_base = 0;
+  A.rlen = (int32_t)rlen;
+  A.win_stride = win_stride;
+  A.head = head;
+  A.qstride = qstride;
+  A.nb = 1;
+  A.lb = single ? (uint64_t *)ctx->fused_lb.p : nullptr;
+  A.ntiles = ntiles;
+  A.tbase = tbase;
+  A.epoch = epoch;
+  A.fault = scan_fault_device();
+  A.cur_in = ctx->chain_open ? d_cur + 4 * (seq % (mh_ctx::LZ_SLOTS + 1)) : nullptr;
+  A.cur_out = d_cur + 4 * ((seq + 1) % (mh_ctx::LZ_SLOTS + 1));
+  A.res = ctx->d_lazy + 8 * rslot;
+  A.cap[0] = (int64_t)ctx->out1.cap;
+  A.cap[1] = write_fastq2 ? (int64_t)ctx->out2.cap : 0;
+  A.hcap = hrow;
+  // the writer waits for what the main stream has queued (this unit's templates: its sampling tail was joined there
+  // by tpl_resolve; its measure pass and tile scan), not for any host readback
+  stage_begin(ctx, "emit");
+  if (!single) {
+    EmitSet &es = ctx->eset[set];
+    hipStream_t st = ctx->stream;
+    if (es.busy) HIPCHK(ctx, hipStreamWaitEvent(st, es.done, 0));   // the writer that last read the set
+    char *stat = (char *)es.stat.p;   // (its maxima are not read: the splice's bound sizes the rows)
+    stage_begin(ctx, "emit_measure");
+    hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A.h, m, A.pos0, A.pos1,
+                       A.fo0, rlen, QFixed{nullptr, nullptr, qh.lp, qh.lm}, (int32_t)ctx->corrupt_on,
+                       (Rec *)es.recs.p, (int4 *)es.tsum.p, (int32_t *)(stat + 32));
+    HIPCHK(ctx, hipGetLastError());
+    stage_end(ctx);
+    stage_begin(ctx, "emit_scan");
+    HIPCHK(ctx, device_scan_sum<E3>(st, ntiles, LoadTile{(const int4 *)es.tsum.p, ntiles},
+                                    StoreTile{(E3 *)es.tpre.p}, ctx->scan_partials.p, (E3 *)stat));
+    stage_end(ctx);
+    A.recs = (const Rec *)es.recs.p;
+    A.tpre = (const E3 *)es.tpre.p;
+  }
+  HIPCHK(ctx, hipEventRecord(ctx->ev_ready, ctx->stream));
+  HIPCHK(ctx, hipStreamWaitEvent(ws, ctx->ev_ready, 0));
+  ctx->stage_stream = ws;
+  if (cr_rows) MH_TRY(cr_rows_prepare(ctx, ws, m, nf, (int32_t)rlen, cc, A));
+  stage_begin(ctx, "emit_write");
+  hipLaunchKernelGGL(single ? ef_kernel(cr_rows ? 2 : 0, write_fastq2 != 0) : ew_kernel(cr_rows ? 2 : 0, write_fastq2),
+                     dim3((unsigned)ntiles), dim3(ED_THREADS), lds_d, ws, A, qh);
+  HIPCHK(ctx, hipGetLastError());
+  stage_end(ctx);
+  stage_end(ctx);   // "emit"
+  ctx->stage_stream = nullptr;
+  if (!single) {
+    HIPCHK(ctx, hipEventRecord(ctx->eset[set].done, ws));
+    ctx->eset[set].busy = true;
+  }
+  HIPCHK(ctx, hipEventRecord(ctx->ev_writer, ws));
+  MH_TRY(mark_used(ctx, h.used, h.used_set));     // the haplotype and the templates stay live until then
+  MH_TRY(mark_used(ctx, tp.used, tp.used_set));
+  ctx->writer_pending = true;
+  ctx->chain_open = true;
+  ctx->used_ub1 += add;
+  if (write_fastq2) ctx->used_ub2 += add;
+  ctx->lazy_seq = seq + 1;
+  ctx->lazy.push_back(mh_ctx::LazyUnit{rslot, ctx->lazy_gen, {0, 0, 0}});
+  return MH_OK;
+}
+
+int32_t lazy_resolve(mh_ctx *ctx) {
+  if (ctx->lazy.empty()) return MH_OK;
+  MH_TRY(sync_writers(ctx));   // (SYNCCHK: a look-back timeout or a bound the writer found wrong fails here)
+  const volatile int64_t *r = ctx->h_lazy;
+  for (const auto &u : ctx->lazy) {
+    int64_t k = 0, b1 = 0, b2 = 0;
+    if (u.slot < 0) {
+      k = u.known[0];
+      b1 = u.known[1];
+      b2 = u.known[2];
+    } else {
+      const volatile int64_t *q = r + 8 * u.slot;
+      k = q[0];
+      b1 = q[1];
+      b2 = q[2];
+      if (u.gen == ctx->lazy_gen) {   // the chain's ends move the arenas
+        ctx->used1 = q[3];
+        ctx->used2 = q[4];
+      }
+    }
+    ctx->lazy_done.push_back(k);
+    ctx->lazy_done.push_back(b1);
+    ctx->lazy_done.push_back(b2);
+  }
+  ctx->lazy.clear();
+  ctx->chain_open = false;
   return MH_OK;
 }
 

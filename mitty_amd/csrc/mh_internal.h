@@ -62,6 +62,11 @@ __host__ __device__ int expand_variant(uint8_t o, int64_t vp, int64_t oplen, int
 
 constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
 
+// Read windows the splice bounds a read's qname part for (k_part_bound): the single-pass writer sizes its qname rows
+// and reserves arena bytes from the bound of the smallest window >= rlen, before any template is measured.
+constexpr int PB_NW = 8;
+constexpr int32_t PB_W[PB_NW] = {100, 125, 150, 175, 200, 250, 300, 321};
+
 struct Hap {
   bool valid = false;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
@@ -71,6 +76,11 @@ struct Hap {
   DevBuf bkt;   // node search buckets: bkt[k] = first node with key >= p_min + k * 2^NODE_BKT_SHIFT
   int64_t n_bkt = 0;
   int64_t n_nodes = 0, n_runs = 0, p_min = 0, p_max = 0, hap_len = 0, ref_start_pos = 0;
+  // k_part_bound: per window PB_W[w], the most bytes the nodes of one read add to its qname part (counts, ops,
+  // variant sizes); the largest POS a read can have
+  bool bound_valid = false;
+  int32_t part_w[PB_NW] = {0};
+  int64_t pos_max = 0;
 };
 
 // One work unit's templates (illumina.generate_reads output), device-resident.
@@ -268,6 +278,29 @@ struct mh_ctx {
   // FASTQ arenas
   mh::DevBuf out1, out2;
   int64_t used1 = 0, used2 = 0;
+  // single-pass emission (mh_emit_reads_async, k_emit_fused): units queued on the writer stream with no host wait.
+  // Each writer's last tile writes the unit's totals to mapped host memory (h_lazy, LZ_SLOTS slots of 8 words) and
+  // the arena ends to the device cursor ring (d_cur) the next unit's writer starts from.  While a chain is open the
+  // host knows only an upper bound of the arena ends (used_ub); lazy_resolve waits for the writers and makes
+  // used1/used2 exact again.  Units queued before an mh_output_reset belong to an older generation: their totals are
+  // still collected, their ends no longer move the arenas.
+  static constexpr int LZ_SLOTS = 4096;
+  int64_t *h_lazy = nullptr, *d_lazy = nullptr;
+  mh::DevBuf d_cur;                 // LZ_SLOTS + 1 cursors of 4 words: kept, end file 1, end file 2, -
+  mh::DevBuf fused_lb;              // the single-pass writer's look-back scratch (writer stream)
+  struct LazyUnit {
+    int32_t slot;                   // h_lazy slot (-1: totals already known, in `known`)
+    int64_t gen;
+    int64_t known[3];
+  };
+  std::vector<LazyUnit> lazy;       // queued, not resolved
+  std::vector<int64_t> lazy_done;   // resolved totals (3 per unit, queue order) for mh_emit_collect
+  int64_t lazy_seq = 0;             // units queued on the chain so far (cursor ring position)
+  int64_t lazy_gen = 0;
+  bool chain_open = false;
+  int64_t used_ub1 = 0, used_ub2 = 0;
+  bool emit_two_pass = false;       // mh_set_emit_mode(2): every unit through mh_emit_reads' path (host readbacks)
+  bool emit_single = false;         // mh_set_emit_mode(3): the single-pass writer (k_emit_fused)
   // corruption rows (the direct writer's mode): per block 15 qualities | 2-bit codes; one set, the row pass and its
   // writer in stream order on the writer stream
   mh::DevBuf cr_rows, cr_codes;
@@ -368,6 +401,12 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
                    int32_t write_fastq2, uint64_t unit_key, int64_t t_begin, int64_t t_end, int64_t cnt_base,
                    bool prepare_only, int64_t *out_kept, int64_t *out_b1, int64_t *out_b2);
 int32_t count_kept(mh_ctx *ctx, const Hap &h, int64_t t_begin, int64_t t_end, int64_t *out_kept);
+// One whole unit of the current template set through the single-pass writer, queued with no host wait (its totals
+// resolved by lazy_resolve).  *queued false (MH_OK): the unit does not qualify (the caller takes the two-pass path).
+int32_t emit_unit_async(mh_ctx *ctx, const Hap &h, const char *serial_stub, const char *chrom, int64_t cpy,
+                        int32_t write_fastq2, uint64_t unit_key, bool *queued);
+// Waits for the queued single-pass writers, moves their totals to lazy_done and makes used1/used2 exact.
+int32_t lazy_resolve(mh_ctx *ctx);
 
 int32_t bam_set_refs(mh_ctx *ctx, int32_t n_refs, const char *names, const int64_t *lengths);
 int32_t bam_add(mh_ctx *ctx, const uint8_t *d1, int64_t len1, const uint8_t *d2, int64_t len2, int64_t max_templates,

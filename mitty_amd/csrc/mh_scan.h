@@ -386,6 +386,26 @@ inline size_t scan_lb_scratch_bytes(int64_t n) {
 // scan_lb_scratch_bytes<T>(n) bytes of device memory.
 // skip_tile0 (self-test only, mh_selftest_scan_fault): the ticket base one below the counter and one workgroup
 // fewer, so tile 0 never publishes and every other tile's look-back times out (all accesses stay in range)
+// A launch's share of a look-back scratch buffer (`need` bytes, `tiles` tickets): the scratch zeroed on `st` when new,
+// grown or out of epochs; the ticket counter's value when the launch starts and its epoch.  (device_scan_sum, and
+// the single-pass FASTQ writer, mh_emit.hip)
+inline hipError_t lb_reserve(hipStream_t st, void *scratch, size_t need, uint32_t tiles, uint32_t *base,
+                             uint32_t *epoch) {
+  std::lock_guard<std::mutex> lk(lb_mu());
+  LbScratchState &S = lb_states()[scratch];
+  if (S.zeroed < need || S.epoch >= (1u << LB_EPOCH_BITS) - 1) {   // new (or grown) scratch, or epochs used up
+    hipError_t e = hipMemsetAsync(scratch, 0, need, st);
+    if (e != hipSuccess) return e;
+    S.zeroed = need;
+    S.ticket = 0;
+    S.epoch = 0;
+  }
+  *base = S.ticket;
+  *epoch = ++S.epoch;
+  S.ticket += tiles;
+  return hipSuccess;
+}
+
 template <typename T, typename Load, typename Store>
 inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store store, void *scratch, T *total,
                                   bool skip_tile0 = false) {
@@ -395,18 +415,9 @@ inline hipError_t device_scan_sum(hipStream_t st, int64_t n, Load load, Store st
   const size_t need = scan_lb_scratch_bytes<T>(n);
   uint32_t base, epoch;
   {
-    std::lock_guard<std::mutex> lk(lb_mu());
-    LbScratchState &S = lb_states()[scratch];
-    if (S.zeroed < need || S.epoch >= (1u << LB_EPOCH_BITS) - 1) {   // new (or grown) scratch, or epochs used up
-      hipError_t e = hipMemsetAsync(scratch, 0, need, st);
-      if (e != hipSuccess) return e;
-      S.zeroed = need;
-      S.ticket = 0;
-      S.epoch = 0;
-    }
-    base = S.ticket - (skip_tile0 ? 1u : 0u);
-    epoch = ++S.epoch;
-    S.ticket += (uint32_t)(skip_tile0 ? nt - 1 : nt);
+    hipError_t e = lb_reserve(st, scratch, need, (uint32_t)(skip_tile0 ? nt - 1 : nt), &base, &epoch);
+    if (e != hipSuccess) return e;
+    if (skip_tile0) base -= 1u;
   }
   hipLaunchKernelGGL((k_scan_lb<T, Load, Store>), dim3((unsigned)(skip_tile0 ? nt - 1 : nt)), dim3(SCAN_THREADS), 0,
                      st, n, load, store, (uint64_t *)scratch, nt, total, base, epoch, scan_fault_device());

@@ -12,6 +12,8 @@
 //   7. N-run extraction          -> sorted [start, end) runs of 'N' so the N-filter never re-reads bases.
 // Node arrays are SoA in HBM: keys (search key, ps+1 for 'D' as rpc.py:127), ps, pr, op, oplen.
 
+#include <cstring>
+
 #include "mh_device.h"
 #include "mh_internal.h"
 #include "mh_scan.h"
@@ -393,6 +395,92 @@ __global__ void __launch_bounds__(256) k_node_pack(int64_t n, const int64_t *ps,
   nd[i] = Node16{(a & 0xffffffffffull) | code << 40 | (l & 0x3fffffull) << 42, (b & 0xffffffffffull) | (l >> 22) << 40};
 }
 
+__device__ __forceinline__ int32_t pb_ndig(int64_t v) {   // (no 64-bit division: it is a long VALU routine)
+  int32_t d = 1;
+  for (int64_t p = 10; v >= p && d < 18; p *= 10) d++;
+  return d;
+}
+// Bytes node n adds to a read's qname part under window W (rpc.py:146-147): its CIGAR count and op — a count is
+// min(p + l - ps, oplen) - max(0, p - ps) <= min(oplen, l), a deletion's is its length — and, for a variant, its size
+// in v_list (X: 0, I: +oplen, D: -oplen) with a comma.
+__device__ __forceinline__ int32_t pb_node_cost(const Node16 &n, int32_t W) {
+  const int c = n.code();
+  const int64_t ol = n.oplen();
+  const int32_t cnt = pb_ndig(c == 3 ? ol : (ol < W ? ol : W)) + 1;
+  return cnt + (c == 0 ? 0 : c == 1 ? 2 : c == 2 ? pb_ndig(ol) + 1 : pb_ndig(ol) + 2);
+}
+
+// The qname-part bound of the single-pass writer (k_emit_fused).  A read at p whose start node is j (key_j <= p <
+// key_{j+1}) ends in the last node with key <= p + rlen - 1 < key_{j+1} + rlen - 1 (rpc.py:119-130), so its nodes'
+// bytes are at most node j's plus those of every node k > j with key_k <= key_{j+1} + W - 2, W >= rlen; a read inside
+// an insertion (rpc.py:152-156) writes '>' off ':' l 'I' instead of its count.  Per window the maximum over j, and the
+// largest POS (p - ps + pr < pr + oplen), into out_w[PB_NW] / *out_pos (zeroed).
+__global__ void __launch_bounds__(256) k_part_bound(const Node16 *nd, int64_t n, int32_t *out_w,
+                                                    unsigned long long *out_pos) {
+  __shared__ int32_t s_w[4][PB_NW];
+  __shared__ unsigned long long s_p[4];
+  int32_t best[PB_NW];
+  unsigned long long pm = 0;
+#pragma unroll
+  for (int w = 0; w < PB_NW; w++) best[w] = 0;
+  // (a grid-stride loop over few workgroups, one atomic per workgroup and window: one per wave, ~10 k waves on the
+  // same nine words, serialised at the memory side and took ~0.26 ms per chr1 haplotype)
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const Node16 a = nd[j];
+    const int64_t ol = a.oplen();
+    int32_t c[PB_NW];
+#pragma unroll
+    for (int w = 0; w < PB_NW; w++) {
+      c[w] = pb_node_cost(a, PB_W[w]);
+      if (a.code() == 2) {   // (special: the count replaced by '>' off ':' l 'I', off < oplen, l <= W)
+        const int32_t sp = 3 + pb_ndig(ol) + pb_ndig(PB_W[w]) + pb_ndig(ol) + 1;
+        if (sp > c[w]) c[w] = sp;
+      }
+    }
+    if (j + 1 < n) {
+      const int64_t base = nd[j + 1].key();
+      for (int64_t k = j + 1; k < n; k++) {
+        const Node16 b = nd[k];
+        const int64_t key = b.key();
+        if (key > base + PB_W[PB_NW - 1] - 2) break;
+#pragma unroll
+        for (int w = 0; w < PB_NW; w++)
+          if (key <= base + PB_W[w] - 2) c[w] += pb_node_cost(b, PB_W[w]);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < PB_NW; w++) best[w] = c[w] > best[w] ? c[w] : best[w];
+    const unsigned long long e = (unsigned long long)(a.pr() + (ol > 1 ? ol : 1));
+    pm = e > pm ? e : pm;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+#pragma unroll
+    for (int w = 0; w < PB_NW; w++) {
+      const int32_t o = __shfl_xor(best[w], d, 64);
+      best[w] = o > best[w] ? o : best[w];
+    }
+    const unsigned long long o = __shfl_xor(pm, d, 64);
+    pm = o > pm ? o : pm;
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int w = 0; w < PB_NW; w++) s_w[wv][w] = best[w];
+    s_p[wv] = pm;
+  }
+  __syncthreads();
+  if (threadIdx.x < PB_NW) {
+    int32_t m = 0;
+    for (int k = 0; k < 4; k++) m = s_w[k][threadIdx.x] > m ? s_w[k][threadIdx.x] : m;
+    atomicMax(out_w + threadIdx.x, m);
+  } else if (threadIdx.x == PB_NW) {
+    unsigned long long m = 0;
+    for (int k = 0; k < 4; k++) m = s_p[k] > m ? s_p[k] : m;
+    atomicMax(out_pos, m);
+  }
+}
+
 // Node-search buckets: bkt[k] = first node whose key is >= p_min + (k << NODE_BKT_SHIFT) (lower_bound), so the
 // searchsorted of rpc.get_begin_end_nodes (rpc.py:127-130) only scans the few keys of one bucket.
 __global__ void __launch_bounds__(256) k_node_buckets(const int64_t *keys, int64_t n, const int64_t *ends,
@@ -469,6 +557,7 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
   const int64_t n_var = v.n;
   const int64_t nv = n_var > 0 ? n_var : 1;
   const int64_t node_cap = 2 * n_var + 1;
+  h.bound_valid = false;
 
   stage_begin(ctx, "splice");
   const int64_t *d_pos = (const int64_t *)v.pos.p, *d_oplen = (const int64_t *)v.oplen.p;
@@ -569,6 +658,13 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
                        (const int64_t *)h.keys.p, n_nodes, d_ends, n_bkt, (int32_t *)h.bkt.p);
     HIPCHK(ctx, hipGetLastError());
     h.n_bkt = n_bkt;
+    // the single-pass writer's qname-part bounds, read back with the N-run counts below (small + 160 / + 192)
+    if (n_nodes > 0) {
+      hipLaunchKernelGGL(k_part_bound, dim3(grid_for(n_nodes, 256, 512)), dim3(256), 0, st,
+                         (const Node16 *)h.nd.p, n_nodes, (int32_t *)(small + 160),
+                         (unsigned long long *)(small + 192));
+      HIPCHK(ctx, hipGetLastError());
+    }
   }
   if (hap_len > 0) {
     stage_begin(ctx, "splice_hap_copy");
@@ -600,7 +696,8 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
       hipLaunchKernelGGL(k_nrun_find, dim3(grid_for(nel, 256, INT32_MAX)), dim3(256), 0, st, (const uint8_t *)h.hap.p,
                          hap_len, cap, us, ue, cnt);
       HIPCHK(ctx, hipGetLastError());
-      HIPCHK(ctx, hipMemcpyAsync(hs + 16, cnt, 16, hipMemcpyDeviceToHost, st));
+      // the counts (small + 128) and k_part_bound's results (small + 160 .. 200) -> hs + 16 .. 25
+      HIPCHK(ctx, hipMemcpyAsync(hs + 16, cnt, 72, hipMemcpyDeviceToHost, st));
       SYNCCHK(ctx, hipStreamSynchronize(st));
       if (attempt == 0) {   // the splice's error word and node ends, read back before the haplotype bytes
         const int32_t herr = (int32_t)(hs[8] & 0xffffffff);
@@ -612,6 +709,9 @@ int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const Var
         p_min = hs[12];
         p_last = hs[13];
         nl_last = hs[14];
+        std::memcpy(h.part_w, hs + 20, sizeof(h.part_w));
+        h.pos_max = hs[24];
+        h.bound_valid = true;
       }
       hc[0] = (unsigned long long)hs[16];
       hc[1] = (unsigned long long)hs[17];

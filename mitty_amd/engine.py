@@ -16,16 +16,26 @@ RNG_MODES = {'mitty': _native.MH_RNG_MITTY, 'philox': _native.MH_RNG_PHILOX}
 
 class Engine:
   SLOTS_PER_REGION = 64
-  EMIT_SETS = 4   # units prepared ahead of their writers (of the library's 16 emission buffer sets)
   TPL_BATCH = 1 << 20   # template-set ids: [0, TPL_BATCH) and [TPL_BATCH, 2 * TPL_BATCH), alternating per batch
 
-  def __init__(self, device=0):
+  EMIT_SETS = 4   # the two-pass path: units prepared ahead of their writers (of the library's 16 emission buffer sets)
+
+  def __init__(self, device=0, emit_mode=0):
+    """emit_mode (mh_set_emit_mode): 0 every unit queued with no host readback (mh_emit_reads_async: measure pass,
+    tile scan and writer chained on the device); 3 the same through the single-pass writer (k_emit_fused); 2 the
+    two-pass path with the host reading each unit's totals before its writer (round 5's flow; A/B and tests); 1 the
+    LDS-image writer."""
     self.ctx = _native.Context(device)
     self.device = device
+    self.emit_mode = emit_mode
+    if emit_mode:
+      self.ctx.set_emit_mode(emit_mode)
     self._regions = {}   # ri -> region tuple (contig uploaded)
     self._haps = {}      # (ri, cpy) -> (slot, n_nodes, p_min, p_max)
     self._vsets = {}     # (ri, cpy) -> resident variant set id (upload_variants)
     self._tpl_base = 0
+    self._lazy_n = []    # template counts of the units queued by run_units and not yet collected
+    self._two_pass_done = []
 
   def close(self):
     self.ctx.close()
@@ -75,11 +85,12 @@ class Engine:
     self._haps.clear()
 
   def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None):
+                on_unit=None, lazy=False):
     """Sample a batch of work units together, then emit them in order.
 
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
-    unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit.
+    unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit; lazy=True returns None
+    and leaves the units' results to collect(), so the caller queues the next batch while these writers run.
     """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
@@ -91,11 +102,29 @@ class Engine:
     # emission first uses it (unit 0's writer does not wait for the whole batch's tail)
     self.ctx.sample_units_async([base + k for k in range(len(units))], slots, [u[3] for u in units], p, rlen,
                                 cum_tlen, RNG_MODES[rng])
+    # every unit's writer queued as soon as its templates are resolved (mh_emit_reads_async: the single-pass writer,
+    # no measure pass and no readback between units); the writers drain while the caller moves on
+    if self.emit_mode in (1, 2):
+      return self._emit_two_pass(units, slots, base, sample_name, worker_id, write_fastq2, on_unit, lazy)
     out = []
+    for k, (ps, ri, cpy, seed) in enumerate(units):
+      self.ctx.use_templates(base + k)
+      self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
+                          write_fastq2, unit_key=seed)
+      self._lazy_n.append(self.ctx.template_count(base + k))
+      if on_unit is not None:
+        done = self.collect()
+        out += done
+        on_unit(ps, *done[-1])
+    if on_unit is not None:
+      return out
+    return None if lazy else self.collect()
+
+  def _emit_two_pass(self, units, slots, base, sample_name, worker_id, write_fastq2, on_unit, lazy):
     # measure passes of up to EMIT_SETS units first (main stream), then their writers queued back to back (writer
-    # stream): the writers drain while the caller moves on to the next batch.  Unit 0 goes alone: preparing a unit
-    # waits for its sampling tail, so at a batch boundary the idle writer stream would otherwise wait for the tails
-    # and measure passes of the whole first chunk
+    # stream).  Unit 0 goes alone: preparing a unit waits for its sampling tail, so at a batch boundary the idle
+    # writer stream would otherwise wait for the tails and measure passes of the whole first chunk
+    out = []
     order = list(enumerate(units))
     k0 = 1 if len(units) > 1 else 0
     chunks = ([order[:1]] if k0 else []) + [order[c0:c0 + self.EMIT_SETS]
@@ -113,6 +142,21 @@ class Engine:
         out.append((n, kept, b1, b2))
         if on_unit is not None:
           on_unit(ps, n, kept, b1, b2)
+    if lazy:
+      self._two_pass_done += out
+      return None
+    return out
+
+  def collect(self):
+    """[(n, kept, b1, b2)] of every unit queued by run_units since the last collect (waits for their writers)."""
+    if self.emit_mode in (1, 2):
+      out, self._two_pass_done = self._two_pass_done, []
+      return out
+    res = self.ctx.emit_collect()
+    if len(res) != len(self._lazy_n):
+      raise RuntimeError('emit_collect returned {} units for {} queued'.format(len(res), len(self._lazy_n)))
+    out = [(n,) + tuple(r) for n, r in zip(self._lazy_n, res)]
+    self._lazy_n = []
     return out
 
   def run_unit(self, ps, ri, cpy, rng_seed, soa, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True,

@@ -1721,3 +1721,127 @@ def test_lsd_sort_equals_stable_argsort(ctx, bits):
     order = np.argsort(k, kind='stable')
     assert np.array_equal(vo, order.astype(np.uint32)), (bits, n)
     assert np.array_equal(ko, k[order]), (bits, n)
+
+
+# ---- the single-pass writer (k_emit_fused) ---------------------------------------------------------------------
+def _dense_records(seq, seed, start0, end):
+  """Variants far denser than any VCF (test input): one every 2-12 bp; 60 % SNVs, 20 % insertions (2 % of them
+  300-700 bp, so reads fall inside them: '>p:nI'), 20 % deletions (2 % of them 200-1500 bp: 4-digit CIGAR counts),
+  GT 0|1 / 1|0 / 1|1.  Reads then span tens of nodes (the writer's node loop past its four preloaded nodes)."""
+  rs = np.random.RandomState(seed)
+  arr = np.frombuffer(seq, dtype=np.uint8)
+  pos0 = start0 + np.cumsum(rs.randint(2, 13, size=(end - start0) // 4))
+  pos0 = pos0[pos0 < end - 2000]
+  pos0 = pos0[arr[pos0] != ord('N')]
+  n = len(pos0)
+  kind = rs.choice(3, size=n, p=[0.6, 0.2, 0.2])
+  ln = 1 + rs.geometric(0.35, size=n)
+  big = rs.rand(n) < 0.02
+  ln[big & (kind == 1)] = rs.randint(300, 701, size=int((big & (kind == 1)).sum()))
+  ln[big & (kind == 2)] = rs.randint(200, 1501, size=int((big & (kind == 2)).sum()))
+  gt = np.array([[0, 1], [1, 0], [1, 1]], dtype=np.int8)[rs.choice(3, size=n)]
+  ref_len = np.where(kind == 2, ln + 1, 1).astype(np.int64)
+  acgt = np.frombuffer(b'ACGT', dtype=np.uint8)
+  alts = []
+  for i in range(n):
+    b = seq[pos0[i]:pos0[i] + 1]
+    if kind[i] == 0:
+      alts.append(b'A' if b != b'A' else b'C')
+    elif kind[i] == 1:
+      alts.append(b + acgt[rs.randint(0, 4, size=int(ln[i]))].tobytes())
+    else:
+      alts.append(b)
+  return {'pos': pos0.astype(np.int64) + 1, 'ref_len': ref_len, 'alt': alts, 'gt': gt}
+
+
+@pytest.mark.parametrize('model', G.MODELS)
+def test_single_pass_writer_dense_variants_vs_oracle(native, model):
+  """mh_emit_reads_async's two writers — the chained two-pass path (mode 0: measure pass, tile scan and writer
+  queued with no host readback, offsets passed on the device) and the single-pass writer (mode 3, k_emit_fused: no
+  measure pass, tile offsets by a decoupled look-back) — with qname rows and arena reservation sized by the splice's
+  bound (k_part_bound), on haplotypes far denser than any VCF, both read models (2x150, 2x250), N runs, reads inside
+  long insertions.  Every unit's FASTQ equal to the oracle's (readgenerate.py:184-230, rpc.py:119-160) and to the
+  host-readback path's (mode 2) bytes; the queued units' totals equal; the single-pass run had no measure pass."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model(model)
+  rlen = int(mdl['mean_rlen'])
+  p, passes = _native.read_model_params(rlen, 30.0)
+  L = 400_000
+  seq = synth.contig(L, 31)
+  copies = synth.copies_soa(_dense_records(seq, 32, 0, L))
+  units = _native.work_units(9, [2], passes)
+  job = [(ps, 0, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)]
+  outs = {}
+  for mode in (0, 2, 3):
+    eng = Engine(0)
+    try:
+      eng.ctx.set_emit_mode(mode)
+      eng.ctx.enable_timing(True)
+      eng.load_region(0, ('3', 0, L), seq)
+      res = eng.run_units(job, lambda r, c: copies[c], p, rlen, mdl['cum_tlen'], 'DNS')
+      d1, d2 = eng.ctx.fetch_output()
+      names = {nm for nm, _ in eng.ctx.stage_times()}
+    finally:
+      eng.close()
+    outs[mode] = (res, d1, d2)
+    assert ('emit_measure' in names) == (mode != 3), names
+  for mode in (2, 3):
+    assert outs[0][0] == outs[mode][0]
+    G.check_same(outs[0][1], outs[mode][1])
+    G.check_same(outs[0][2], outs[mode][2])
+  o1, o2 = [], []
+  for ps, _, cpy, sd in job:
+    k, b1, b2 = O.generate_unit_soa(seq, 0, copies[cpy], p, rlen, mdl['cum_tlen'], sd, 'DNS:0:{}'.format(ps), '3', cpy)
+    assert outs[0][0][ps][1] == k and k > 500
+    o1.append(b1)
+    o2.append(b2)
+  G.check_same(outs[0][1], b''.join(o1))
+  G.check_same(outs[0][2], b''.join(o2))
+  assert b'>' in outs[0][1] and b'I|' in outs[0][1]   # reads inside long insertions were among them
+
+
+@pytest.mark.parametrize('mode', [0, 3])
+def test_single_pass_writer_chain_across_resets_and_fallback(native, mode):
+  """Units queued on the single-pass chain across an mh_output_reset (the next chain starts at 0; the earlier units'
+  totals still collected in order), a unit the single-pass writer does not take (a sample name too long for its
+  qname head: the two-pass path inside mh_emit_reads_async, at the chain's exact end) and an arena fetch in the middle
+  (which resolves the chain): the bytes after each reset equal the oracle's concatenation."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 30.0)
+  L = 600_000
+  seq = synth.contig(L, 41)
+  copies = synth.copies_soa(synth.variants(seq, 42))
+  units = _native.work_units(17, [2], passes)
+  job = [(ps, 0, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)]
+  long_name = 'S' * 120
+  eng = Engine(0, mode)
+  try:
+    eng.load_region(0, ('2', 0, L), seq)
+    eng.run_units(job[:2], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'A', lazy=True)
+    first = eng.ctx.fetch_output()
+    eng.ctx.reset_output()
+    eng.run_units(job[2:], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'A', lazy=True)
+    eng.run_units(job[:1], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], long_name, lazy=True)
+    eng.run_units(job[1:2], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'A', lazy=True)
+    res = eng.collect()
+    second = eng.ctx.fetch_output()
+  finally:
+    eng.close()
+
+  def oracle(part, name):
+    o = [O.generate_unit_soa(seq, 0, copies[cpy], p, 150, mdl['cum_tlen'], sd, '{}:0:{}'.format(name, ps), '2', cpy)
+         for ps, _, cpy, sd in part]
+    return o
+
+  o_first = oracle(job[:2], 'A')
+  o_second = oracle(job[2:], 'A') + oracle(job[:1], long_name) + oracle(job[1:2], 'A')
+  assert [r[1:] for r in res] == [(k, len(b1), len(b2)) for k, b1, b2 in o_first + o_second]
+  G.check_same(first[0], b''.join(o[1] for o in o_first))
+  G.check_same(first[1], b''.join(o[2] for o in o_first))
+  G.check_same(second[0], b''.join(o[1] for o in o_second))
+  G.check_same(second[1], b''.join(o[2] for o in o_second))
