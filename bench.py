@@ -26,6 +26,7 @@ carries `cpu_baseline` (the CPU oracle on the host cores, and the configs[0] CPU
 (the whole `generate-reads` command on chr1: files in, FASTQ to /dev/null).
 """
 import argparse
+import collections
 import glob
 import json
 import os
@@ -179,6 +180,28 @@ def corrupt_roofline(stages, kept, b1, b2, rlen):
           'bases_per_s': bases / (ms * 1e-3) if ms > 0 else None}
 
 
+class LazyCounts:
+  """The (kept, bytes1, bytes2) of units queued with Engine.run_units(lazy=True), read after the timed region: a step
+  returns getter(n) for its n units, so no step waits for its writers (the next step's splice and sampling run
+  beside them, as the reference's worker pool runs the next units while earlier ones are written)."""
+
+  def __init__(self, eng):
+    self.eng = eng
+    self.q = collections.deque()
+
+  def getter(self, n):
+    memo = []
+
+    def get():   # (getters are called in step order; each reads its units once)
+      if not memo:
+        while len(self.q) < n:
+          self.q.extend(self.eng.collect())
+        res = [self.q.popleft() for _ in range(n)]
+        memo.append((sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res)))
+      return memo[0]
+    return get
+
+
 def timed(step, steps, warmup, eng, dist):
   def barrier():
     if dist is not None:
@@ -309,14 +332,16 @@ def run_chr1(a):
     eng.upload_variants(0, cpy, copies[cpy])
   kernel = 'k_emit_tiles'
 
+  counts = LazyCounts(eng)
+
   def step():
     # one chr1 job; consecutive jobs pipeline on the device (this job's splice and sampling run while the previous
     # job's last FASTQ writers drain); the timed region ends with a full synchronisation
     eng.drop_haplotypes()
     eng.ctx.reset_output()
-    res = eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
-                        rlen, model['cum_tlen'], 'SYN', 0, True, a.rng)
-    return lambda: (sum(r[1] for r in res), sum(r[2] for r in res), sum(r[3] for r in res))
+    eng.run_units([(ps, ri, cpy, s) for ps, (ri, cpy, s) in enumerate(units)], lambda r, c: copies[c], p,
+                  rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True)
+    return counts.getter(len(units))
 
   dt, kept, b1, b2, stages = timed(step, a.steps, a.warmup, eng, None)
   eng.close()
@@ -752,20 +777,27 @@ def run_genome(a, rank, world, local):
     dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
 
+  lazy = LazyCounts(eng)
+  n_mine = sum(len(b) for b in batches)
+  prev = []
+
   def step():
     eng.drop_haplotypes()
     for batch in batches:
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
-      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it; their totals are collected
-      # once, at the end of the step (no host wait on a writer before then)
+      # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it; no host wait on a writer
+      # anywhere in the step (the totals are read after the timed region, or at the step's end with N > 1)
       eng.ctx.reset_output()
       eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True)
-    res = eng.collect()
-    kept, b1, b2 = sum(u[1] for u in res), sum(u[2] for u in res), sum(u[3] for u in res)
+    get = lazy.getter(n_mine)
     if dist is not None:
-      counts.copy_(torch.tensor([kept, b1, b2], dtype=torch.int64))
-      dist.all_reduce(counts)   # RCCL over xGMI: the job's template / byte totals (file offsets in the file writer)
-    return lambda: (kept, b1, b2)
+      # RCCL over xGMI: the previous step's template / byte totals (file offsets in the file writer), all-reduced once
+      # this step's units are queued — its writers have run beside this step's sampling, so no rank waits on them
+      if prev:
+        counts.copy_(torch.tensor(list(prev.pop()()), dtype=torch.int64))
+        dist.all_reduce(counts)
+      prev.append(get)
+    return get
 
   steps, warmup = a.steps, a.warmup
   dt, kept, b1, b2, stages = timed(step, steps, warmup, eng, dist)
