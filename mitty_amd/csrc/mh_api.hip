@@ -405,7 +405,7 @@ int32_t mh_destroy(mh_ctx *ctx) {
   for (auto &h : ctx->hap_spare) release_hap(h);
   for (auto &kv : ctx->vsets) release_vars(kv.second);
   for (auto &kv : ctx->tsets) {
-    release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1);
+    release(kv.second.fo0); release(kv.second.pos0); release(kv.second.pos1); release(kv.second.n0);
     if (kv.second.used) (void)hipEventDestroy(kv.second.used);
   }
   release(ctx->jump_polys); release(ctx->perm_tmp); release(ctx->nrun_tmp); release(ctx->dec_buf);
@@ -807,8 +807,9 @@ int32_t mh_sample_templates(mh_ctx *ctx, int32_t slot, double p, int32_t rlen, c
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
   if (!cum_tlen || !out_n || rlen <= 0 || !(p > 0.0 && p <= 1.0)) return arg_fail(ctx, MH_E_ARG, "bad arguments");
   const int32_t id = -1;
+  const NodeIdx ni = node_idx_of(it->second);
   MH_TRY(sample_units(ctx, 1, &id, &it->second.p_min, &it->second.p_max, &seed, p, rlen, cum_tlen, n_tlen, rng_mode,
-                      out_n));
+                      out_n, &ni));
   ctx->cur_tpl = id;
   return MH_OK;
 }
@@ -827,12 +828,13 @@ int32_t mh_sample_templates_span(mh_ctx *ctx, int64_t p_min, int64_t p_max, doub
 
 static int32_t unit_spans(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
                           const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                          std::vector<int64_t> &pmin, std::vector<int64_t> &pmax) {
+                          std::vector<int64_t> &pmin, std::vector<int64_t> &pmax, std::vector<NodeIdx> &nidx) {
   if (n_units < 0 || (n_units > 0 && (!tpl_ids || !slots || !seeds)) || !cum_tlen || rlen <= 0 ||
       !(p > 0.0 && p <= 1.0))
     return arg_fail(ctx, MH_E_ARG, "bad arguments");
   pmin.resize(n_units);
   pmax.resize(n_units);
+  nidx.resize(n_units);
   for (int32_t u = 0; u < n_units; u++) {
     if (tpl_ids[u] < 0) return arg_fail(ctx, MH_E_ARG, "template set ids must be >= 0");
     for (int32_t v = 0; v < u; v++)
@@ -841,6 +843,7 @@ static int32_t unit_spans(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, 
     if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
     pmin[u] = it->second.p_min;
     pmax[u] = it->second.p_max;
+    nidx[u] = node_idx_of(it->second);
   }
   return MH_OK;
 }
@@ -850,9 +853,10 @@ int32_t mh_sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, co
                         int32_t rng_mode, int64_t *out_n) {
   CTX_GUARD_NOJOIN(ctx);   // orders itself against queued writers (Hap/TplSet used events)
   std::vector<int64_t> pmin, pmax;
-  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
+  std::vector<NodeIdx> nidx;
+  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax, nidx));
   return sample_units(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen, rng_mode,
-                      out_n);
+                      out_n, nidx.data());
 }
 
 int32_t mh_sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int32_t *slots,
@@ -860,9 +864,10 @@ int32_t mh_sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_i
                               int32_t rng_mode) {
   CTX_GUARD_NOJOIN(ctx);
   std::vector<int64_t> pmin, pmax;
-  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax));
+  std::vector<NodeIdx> nidx;
+  MH_TRY(unit_spans(ctx, n_units, tpl_ids, slots, seeds, p, rlen, cum_tlen, pmin, pmax, nidx));
   return sample_units_async(ctx, n_units, tpl_ids, pmin.data(), pmax.data(), seeds, p, rlen, cum_tlen, n_tlen,
-                            rng_mode);
+                            rng_mode, nidx.data());
 }
 
 int32_t mh_templates_count(mh_ctx *ctx, int32_t tpl_id, int64_t *n) {
@@ -890,7 +895,7 @@ int32_t mh_release_templates(mh_ctx *ctx, int32_t tpl_id) {
   auto it = ctx->tsets.find(tpl_id);
   if (it == ctx->tsets.end()) return MH_OK;
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));
-  release(it->second.fo0); release(it->second.pos0); release(it->second.pos1);
+  release(it->second.fo0); release(it->second.pos0); release(it->second.pos1); release(it->second.n0);
   if (it->second.used) (void)hipEventDestroy(it->second.used);
   ctx->tsets.erase(it);
   if (ctx->cur_tpl == tpl_id) ctx->cur_tpl = -1;
@@ -906,6 +911,7 @@ int32_t mh_set_templates(mh_ctx *ctx, const int8_t *fo0, const int64_t *pos0, co
   TplSet &ts = ctx->tsets[-1];
   MH_TRY(ensure(ctx, ts.fo0, n + 1));
   MH_TRY(ensure(ctx, ts.pos0, 8 * (n + 1)));
+  ts.has_n0 = false;   // (no start nodes: the measure pass searches)
   MH_TRY(ensure(ctx, ts.pos1, 8 * (n + 1)));
   if (n) {
     HIPCHK(ctx, hipMemcpyAsync(ts.fo0.p, fo0, n, hipMemcpyHostToDevice, ctx->stream));
@@ -985,6 +991,7 @@ int32_t mh_templates_import(mh_ctx *ctx, int32_t tpl_id, int32_t on_device, cons
   ts.valid = false;
   MH_TRY(ensure(ctx, ts.fo0, n + 16));
   MH_TRY(ensure(ctx, ts.pos0, 8 * (n + 16)));
+  ts.has_n0 = false;   // (no start nodes: the measure pass searches)
   MH_TRY(ensure(ctx, ts.pos1, 8 * (n + 16)));
   const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (n) {

@@ -263,40 +263,39 @@ struct QFixed {
 
 constexpr int MS_RUNS = 128;  // N runs staged in LDS by k_emit_measure (more: searched in global memory)
 
-// A read's first three nodes, loaded together (clamped to the last node) as soon as its start node is known: its end
-// node and its qname part's length come from them without a chain of dependent loads (a 2x150 read spans more than
-// three nodes only when it covers two variants, which load the rest).
-struct Nodes3 {
-  Node16 a, b, c;
-  __device__ __forceinline__ Node16 at(const HapView &h, int64_t n0, int64_t j) const {
-    const int64_t d = j - n0;
-    if (d > 2) return h.nd[j];
+// Six consecutive nodes from k0 (clamped to the last node) in registers: with the start node of mate 0 known (the
+// sampling side's packed index), both mates' start and end nodes and their qname parts usually come from these six
+// (96 bytes, one random access) — mate 1 starts tl - rlen bases after mate 0, a few hundred bases.  (Round 5 loaded
+// three nodes per mate after a bucket search each: 237 -> 222 us per chr1-size unit alone.)
+struct Nodes6 {
+  Node16 v0, v1, v2, v3, v4, v5;
+  int64_t k0;
+  __device__ __forceinline__ Node16 at(const HapView &h, int64_t k) const {
+    const int64_t d = k - k0;
+    if (d < 0 || d > 5) return h.nd[k];
     Node16 o;   // (field by field: a select of whole structs would go through scratch memory)
-    o.a = d == 0 ? a.a : d == 1 ? b.a : c.a;
-    o.b = d == 0 ? a.b : d == 1 ? b.b : c.b;
+    o.a = d == 0 ? v0.a : d == 1 ? v1.a : d == 2 ? v2.a : d == 3 ? v3.a : d == 4 ? v4.a : v5.a;
+    o.b = d == 0 ? v0.b : d == 1 ? v1.b : d == 2 ? v2.b : d == 3 ? v3.b : d == 4 ? v4.b : v5.b;
     return o;
   }
+  // searchsorted(keys, x, 'right') - 1 from node k (key_k <= x)
+  __device__ __forceinline__ int64_t walk(const HapView &h, int64_t k, int64_t x) const {
+    while (k + 1 < h.n_nodes && at(h, k + 1).key() <= x) k++;
+    return k;
+  }
 };
-__device__ __forceinline__ Nodes3 nodes3(const HapView &h, int64_t n0) {
+__device__ __forceinline__ Nodes6 nodes6(const HapView &h, int64_t k0) {
   const int64_t last = h.n_nodes - 1;
-  return Nodes3{h.nd[n0], h.nd[n0 + 1 < last ? n0 + 1 : last], h.nd[n0 + 2 < last ? n0 + 2 : last]};
+  auto c = [&](int64_t d) { return h.nd[k0 + d < last ? k0 + d : last]; };
+  return Nodes6{c(0), c(1), c(2), c(3), c(4), c(5), k0};
 }
-// node_walk from n0 over the preloaded nodes
-__device__ __forceinline__ int64_t node_walk3(const HapView &h, const Nodes3 &q, int64_t n0, int64_t x) {
-  const int64_t last = h.n_nodes - 1;
-  if (n0 + 1 > last || q.b.key() > x) return n0;
-  if (n0 + 2 > last || q.c.key() > x) return n0 + 1;
-  return node_walk(h, n0 + 2, x);
-}
-
-__device__ __forceinline__ int32_t read_part_len(const HapView &h, const Nodes3 q, int64_t n0, int64_t n1,
-                                                 bool special, int64_t pos, int64_t p, int64_t rlen) {
-  const Node16 nd0 = q.a;
+__device__ __forceinline__ int32_t read_part_len6(const HapView &h, const Nodes6 &q, int64_t n0, int64_t n1,
+                                                  bool special, int64_t pos, int64_t p, int64_t rlen) {
   int32_t L = 3 + ndig_s(pos) + 1 + ndig_s(rlen) + 1 + 1;
-  if (special) L += 1 + ndig_s(p - nd0.ps()) + 1 + ndig_s(rlen) + 1;
+  if (special) L += 1 + ndig_s(p - q.at(h, n0).ps()) + 1 + ndig_s(rlen) + 1;
   int32_t nv = 0;
   for (int64_t k = n0; k <= n1; k++) {
-    const Node16 n = q.at(h, n0, k);
+    const Node16 n = q.at(h, k);
     if (!special) L += ndig_s(node_count(n, p, rlen)) + 1;
     if (n.code() != 0) {
       L += ndig_s(node_v(n)) + (nv ? 1 : 0);
@@ -309,10 +308,13 @@ __device__ __forceinline__ int32_t read_part_len(const HapView &h, const Nodes3 
 // One thread per template: start/end node of both mates, POS, the N filter (readgenerate.py:201-204), the qname
 // reads part's length (not its text: the writer formats it) and the record lengths without the cnt digits, into
 // Rec; per 32-template tile the sums (kept, bytes file 1, bytes file 2) into tsum (null: none); the longest record
-// (+20) and the longest reads part + '\n' as maxima (one atomic per wave).
+// (+20) and the longest reads part + '\n' as maxima (one atomic per wave).  n0a (null: none): mate 0's start node per
+// template from the sampling side (StoreCompact), checked against its nodes before use — then one random access of
+// six nodes serves both mates (Nodes6) instead of two bucket searches and two three-node loads (222 -> ... us per
+// chr1-size unit alone, round 6).
 __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, const int64_t *pos0, const int64_t *pos1,
                                                       const int8_t *fo0, int64_t rlen, QFixed q, int32_t corrupt,
-                                                      Rec *recs, int4 *tsum, int32_t *max_rec) {
+                                                      Rec *recs, int4 *tsum, int32_t *max_rec, const int32_t *n0a) {
   __shared__ int64_t s_rs[MS_RUNS], s_re[MS_RUNS];   // the N runs, when they fit
   const bool runs_lds = h.n_runs <= MS_RUNS;
   if (runs_lds)
@@ -329,15 +331,26 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     ReadInfo r[2];
     const int64_t p[2] = {pos0[t], pos1[t]};
     const int f0 = fo0[t];   // file f holds mate (f == fo0 ? 0 : 1)
-    // rpc.get_begin_end_nodes (rpc.py:119-130), then POS / sequence range (two named node sets, not an array: an
-    // indexed array of them went to scratch memory)
-    r[0].n0 = node_upper(h, p[0]) - 1;
-    r[1].n0 = node_upper(h, p[1]) - 1;
-    const Nodes3 q0 = nodes3(h, r[0].n0), q1 = nodes3(h, r[1].n0);
-    r[0].n1 = node_walk3(h, q0, r[0].n0, p[0] + rlen - 1);
-    r[1].n1 = node_walk3(h, q1, r[1].n0, p[1] + rlen - 1);
-    read_place(h, q0.a, p[0], rlen, r[0]);
-    read_place(h, q1.a, p[1], rlen, r[1]);
+    // rpc.get_begin_end_nodes (rpc.py:119-130): mate 0's start node from the sampling side's index when it checks
+    // out (searchsorted - 1: key <= p0 < next key), else by the bucketed search; six nodes from there in registers;
+    // mate 1 (p1 >= p0 for every sampled template) walks on from mate 0's start node
+    int64_t a0 = n0a ? (int64_t)n0a[t] : -1;
+    Nodes6 q6;
+    bool ok = false;
+    if (a0 >= 0 && a0 < h.n_nodes) {
+      q6 = nodes6(h, a0);
+      ok = q6.v0.key() <= p[0] && (a0 + 1 >= h.n_nodes || q6.v1.key() > p[0]);
+    }
+    if (!ok) {
+      a0 = node_upper(h, p[0]) - 1;
+      q6 = nodes6(h, a0);
+    }
+    r[0].n0 = a0;
+    r[0].n1 = q6.walk(h, a0, p[0] + rlen - 1);
+    r[1].n0 = p[1] >= p[0] ? q6.walk(h, a0, p[1]) : node_upper(h, p[1]) - 1;
+    r[1].n1 = q6.walk(h, r[1].n0, p[1] + rlen - 1);
+    read_place(h, q6.at(h, r[0].n0), p[0], rlen, r[0]);
+    read_place(h, q6.at(h, r[1].n0), p[1], rlen, r[1]);
     int keep;
     if (runs_lds) {
       keep = count_N_runs(s_rs, s_re, h.n_runs, r[0].hap_a, r[0].hap_a + r[0].seq_len) <= 2 &&
@@ -348,8 +361,8 @@ __global__ void __launch_bounds__(256) k_emit_measure(HapView h, int64_t m, cons
     }
     Rec out{0, 0, 0, 0, {(int32_t)r[0].n0, (int32_t)r[1].n0}, {(int32_t)r[0].n1, (int32_t)r[1].n1}};
     if (keep) {
-      const int32_t l0 = read_part_len(h, q0, r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
-      const int32_t l1 = read_part_len(h, q1, r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
+      const int32_t l0 = read_part_len6(h, q6, r[0].n0, r[0].n1, r[0].special, r[0].pos, p[0], rlen);
+      const int32_t l1 = read_part_len6(h, q6, r[1].n0, r[1].n1, r[1].special, r[1].pos, p[1], rlen);
       const int32_t rest = l0 + l1;
       const int32_t ql = q.prefix_len + q.mid_len + rest;
       const int32_t s_f1 = f0 == 0 ? r[0].seq_len : r[1].seq_len;
@@ -2239,7 +2252,8 @@ int32_t emit_reads(mh_ctx *ctx, const Hap &h, int32_t slot, const char *serial_s
     Rec *recs = (Rec *)es.recs.p;
     stage_begin(ctx, "emit_measure");
     hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, hv, m, pos0, pos1, fo0,
-                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec);
+                       rlen, q, (int32_t)ctx->corrupt_on, recs, (int4 *)es.tsum.p, max_rec,
+                       tp.has_n0 ? (const int32_t *)tp.n0.p + t_begin : nullptr);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     stage_begin(ctx, "emit_scan");
@@ -2549,7 +2563,8 @@ int32_t emit_unit_async(mh_ctx *ctx, const Hap &h, const char *serial_stub, cons
     stage_begin(ctx, "emit_measure");
     hipLaunchKernelGGL(k_emit_measure, dim3(grid_for(m, 256, INT32_MAX)), dim3(256), 0, st, A.h, m, A.pos0, A.pos1,
                        A.fo0, rlen, QFixed{nullptr, nullptr, qh.lp, qh.lm}, (int32_t)ctx->corrupt_on,
-                       (Rec *)es.recs.p, (int4 *)es.tsum.p, (int32_t *)(stat + 32));
+                       (Rec *)es.recs.p, (int4 *)es.tsum.p, (int32_t *)(stat + 32),
+                       tp.has_n0 ? (const int32_t *)tp.n0.p : nullptr);
     HIPCHK(ctx, hipGetLastError());
     stage_end(ctx);
     stage_begin(ctx, "emit_scan");

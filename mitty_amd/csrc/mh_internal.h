@@ -62,6 +62,38 @@ __host__ __device__ int expand_variant(uint8_t o, int64_t vp, int64_t oplen, int
 
 constexpr int NODE_BKT_SHIFT = 8;   // 256 bp per node-search bucket (~0.7 nodes per bucket at 1.3 variants/kbp)
 
+// A haplotype's node search (searchsorted(keys, x, 'right'), rpc.py:127-130) for the sampling side: the geometric
+// cumsum's store finds each draw's start node while the positions are still in sorted order (neighbouring draws, the
+// same buckets: cached), and packs it into the position's top bits (TS_NODE_SHIFT), so the shuffle carries it for free
+// and the measure pass starts from it instead of searching in shuffled order.  nd == nullptr: no node index.
+constexpr int TS_NODE_SHIFT = 40;                                  // positions < 2^40 (Node16's own bound)
+constexpr int64_t TS_POS_MASK = ((int64_t)1 << TS_NODE_SHIFT) - 1;
+struct NodeIdx {
+  const Node16 *nd = nullptr;
+  const int32_t *bkt = nullptr;
+  int64_t n_bkt = 0, n_nodes = 0, p_min = 0;
+};
+__device__ __forceinline__ int64_t node_idx_upper(const NodeIdx &h, int64_t x) {
+  int64_t k = (x - h.p_min) >> NODE_BKT_SHIFT, lo = 0, hi = h.n_nodes;
+  if (k >= 0) {
+    if (k >= h.n_bkt) k = h.n_bkt - 1;
+    lo = h.bkt[k];
+    hi = k + 1 < h.n_bkt ? h.bkt[k + 1] : h.n_nodes;
+  }
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (h.nd[mid].key() <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+struct Hap;
+inline NodeIdx node_idx_of(const Hap &h);
+// the packed word: position | (start node + 1) << TS_NODE_SHIFT (0: none)
+__device__ __forceinline__ int64_t ts_pack(const NodeIdx &h, int64_t v) {
+  if (!h.nd || v < 0 || v > TS_POS_MASK || h.n_nodes >= ((int64_t)1 << (63 - TS_NODE_SHIFT)) - 1) return v;
+  return v | node_idx_upper(h, v) << TS_NODE_SHIFT;   // (upper_bound = start node + 1)
+}
+
 // Read windows the splice bounds a read's qname part for (k_part_bound): the single-pass writer sizes its qname rows
 // and reserves arena bytes from the bound of the smallest window >= rlen, before any template is measured.
 constexpr int PB_NW = 8;
@@ -82,6 +114,17 @@ struct Hap {
   int32_t part_w[PB_NW] = {0};
   int64_t pos_max = 0;
 };
+inline NodeIdx node_idx_of(const Hap &h) {
+  NodeIdx n;
+  if (h.valid && h.n_nodes > 0 && h.nd.p && h.bkt.p) {
+    n.nd = (const Node16 *)h.nd.p;
+    n.bkt = (const int32_t *)h.bkt.p;
+    n.n_bkt = h.n_bkt;
+    n.n_nodes = h.n_nodes;
+    n.p_min = h.p_min;
+  }
+  return n;
+}
 
 // One work unit's templates (illumina.generate_reads output), device-resident.
 // mh_emit_prepare's results for a template set: the measure pass and record offsets already in buffer set `set`
@@ -101,6 +144,8 @@ struct EmitPrep {
 
 struct TplSet {
   DevBuf fo0, pos0, pos1;
+  DevBuf n0;                           // int32 per template: mate 0's start node (-1: unknown), when has_n0
+  bool has_n0 = false;
   mutable EmitPrep prep;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
@@ -372,12 +417,13 @@ void release_vars(VarSet &v);
 // lane 0: ctx->stream and the shared scratch; lane 1: ctx->stream2 and sl2 (a second host thread)
 int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t ref_start_pos, const VarSet &v, int lane = 0);
 
+// nidx: per unit its haplotype's node search (the start nodes then travel packed in the positions), or null
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                     int32_t rng_mode, int64_t *out_n);
+                     int32_t rng_mode, int64_t *out_n, const NodeIdx *nidx = nullptr);
 int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                           int32_t n_tlen, int32_t rng_mode);
+                           int32_t n_tlen, int32_t rng_mode, const NodeIdx *nidx = nullptr);
 // a template set of an asynchronous tail: wait for its unit (host), read its count, run the rare exact fix-up, and
 // order the main stream after it; no-op for a resolved set
 int32_t tpl_resolve(mh_ctx *ctx, TplSet &ts);

@@ -834,9 +834,9 @@ __global__ void k_geo_array(int64_t n, const uint32_t *w, double p, double log_q
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) g[k] = geometric_draw(mt_double(w, k), p, log_q, fl, k);
 }
-struct StoreTs {
-  int64_t *ts; int64_t add;
-  __device__ void operator()(int64_t k, int64_t incl, int64_t) const { ts[k] = incl + add; }
+struct StoreTs {   // ts = cumsum + p_min + 1, with its start node packed in (NodeIdx, mh_internal.h) when known
+  int64_t *ts; int64_t add; NodeIdx ni;
+  __device__ void operator()(int64_t k, int64_t incl, int64_t) const { ts[k] = ts_pack(ni, incl + add); }
 };
 
 // ---- template length, compaction, file order ----------------------------------------------------------------
@@ -858,7 +858,7 @@ __global__ void __launch_bounds__(256) k_tlen(int64_t n, const uint32_t *w, cons
       if (s_cum[mid] < u) lo = mid + 1; else hi = mid;
     }
     const int64_t tl = lo < rlen ? rlen : lo;           // tl.clip(rlen)
-    const int64_t e = ts[k] + tl;
+    const int64_t e = (ts[k] & TS_POS_MASK) + tl;
     te[k] = e;
     keep[k] = e < p_max;
   }
@@ -872,9 +872,12 @@ struct LoadKeep {
 struct StoreCompact {
   const uint8_t *keep; const int64_t *ts, *te; int64_t *pos0, *pos1; int64_t rlen;
   const uint32_t *wfo; int8_t *fo0;
+  int32_t *n0;   // mate 0's start node, unpacked from ts (null: the set keeps none)
   __device__ void operator()(int64_t k, int64_t, int64_t excl) const {
     if (!keep[k]) return;
-    pos0[excl] = ts[k];
+    const int64_t v = ts[k];
+    pos0[excl] = v & TS_POS_MASK;
+    if (n0) n0[excl] = (int32_t)(v >> TS_NODE_SHIFT) - 1;
     pos1[excl] = te[k] - rlen;
     fo0[excl] = (int8_t)((wfo[excl >> 2] >> (8 * (excl & 3))) & 1u);
   }
@@ -1038,6 +1041,7 @@ int32_t mt_state_words(mh_ctx *ctx, hipStream_t st, const uint32_t *key624, int3
 namespace {
 
 struct UnitPlan {
+  NodeIdx ni;   // the unit's haplotype nodes (start nodes packed into ts), or none
   int64_t p_min, p_max, n, n_fo_words, n_shuf_words;
   uint32_t s_tloc, s_tlen, s_shuf, s_fo;
   int64_t w_tloc, w_tlen, w_fo, w_shuf;   // word offsets in the batch word buffer
@@ -1239,7 +1243,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   if (phase != 2) {
     stage_begin(ctx, "sample_geometric_scan");
     if (!exact) {
-      HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1},
+      HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadGeo{w_tloc, p, log_q, fl}, StoreTs{ts, u.p_min + 1, u.ni},
                                            scan_partials, tot));
     } else {
       int64_t *g = (int64_t *)ctx->s[12].p;
@@ -1272,7 +1276,7 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
         }
       }
       HIPCHK(ctx, hipMemsetAsync(d_flag, 0, 4, st));
-      HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1}, OpSum{}, (int64_t)0,
+      HIPCHK(ctx, device_scan<int64_t>(st, n, LoadArr{g}, StoreTs{ts, u.p_min + 1, u.ni}, OpSum{}, (int64_t)0,
                                        (int64_t *)scan_partials, tot));
     }
     stage_end(ctx);
@@ -1313,7 +1317,8 @@ int32_t finish_unit(mh_ctx *ctx, UnitPlan &u, const uint32_t *words, const uint3
   HIPCHK(ctx, device_scan_sum<int64_t>(st, n, LoadKeep{keep},
                                        StoreCompact{keep, ts_use, te, (int64_t *)u.out->pos0.p,
                                                     (int64_t *)u.out->pos1.p, (int64_t)rlen, w_fo,
-                                                    (int8_t *)u.out->fo0.p},
+                                                    (int8_t *)u.out->fo0.p,
+                                                    u.out->has_n0 ? (int32_t *)u.out->n0.p : nullptr},
                                        scan_partials, d_m));
   stage_end(ctx);
   return MH_OK;
@@ -1347,7 +1352,7 @@ struct SampleState {
 // heads; the per-unit path runs its units whole here.
 static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                           int32_t n_tlen, int32_t rng_mode) {
+                           int32_t n_tlen, int32_t rng_mode, const NodeIdx *nidx) {
   for (int32_t u = 0; u < n_units; u++)
     if (seeds[u] > 0xffffffffull)
       return arg_fail(ctx, MH_E_SEED, "Seed value " + std::to_string(seeds[u]) + " is out of range 0 - 4294967295");
@@ -1392,6 +1397,9 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     MH_TRY(ensure(ctx, ts.fo0, q.n + 16));
     MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
     MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));
+    q.ni = nidx ? nidx[u] : NodeIdx{};
+    ts.has_n0 = q.ni.nd != nullptr;
+    if (ts.has_n0) MH_TRY(ensure(ctx, ts.n0, 4 * (q.n + 16)));
     ts.valid = false;
     q.out = &ts;
   }
@@ -1789,7 +1797,7 @@ int32_t tpl_resolve_all(mh_ctx *ctx) {
 
 int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
                            const int64_t *p_max, const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen,
-                           int32_t n_tlen, int32_t rng_mode) {
+                           int32_t n_tlen, int32_t rng_mode, const NodeIdx *nidx) {
   if (!ctx->h_units) {
     if (hipHostMalloc((void **)&ctx->h_units, 32 * (size_t)PK_UNITS, hipHostMallocMapped | hipHostMallocCoherent) !=
         hipSuccess) {
@@ -1801,7 +1809,7 @@ int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids,
     ctx->d_units = (int64_t *)d;
   }
   auto S = std::make_shared<SampleState>();
-  MH_TRY(sample_head(ctx, *S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
+  MH_TRY(sample_head(ctx, *S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode, nidx));
   // the per-unit path (Philox, oversized batches) and a one-unit batch (no second lane) end as sample_units does
   if (!S->batch || !S->two_lanes) return sample_tail(ctx, *S, nullptr);
   return sample_tail_async(ctx, S);
@@ -1809,9 +1817,9 @@ int32_t sample_units_async(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids,
 
 int32_t sample_units(mh_ctx *ctx, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min, const int64_t *p_max,
                      const uint64_t *seeds, double p, int32_t rlen, const double *cum_tlen, int32_t n_tlen,
-                     int32_t rng_mode, int64_t *out_n) {
+                     int32_t rng_mode, int64_t *out_n, const NodeIdx *nidx) {
   SampleState S;
-  MH_TRY(sample_head(ctx, S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode));
+  MH_TRY(sample_head(ctx, S, n_units, tpl_ids, p_min, p_max, seeds, p, rlen, cum_tlen, n_tlen, rng_mode, nidx));
   return sample_tail(ctx, S, out_n);
 }
 
