@@ -1488,11 +1488,20 @@ int32_t mh_bam_add_output(mh_ctx *ctx, int64_t max_templates, int64_t *templates
   // under 2 KiB: 2x250 reads with their qnames ~1 KiB), so the store spills between pieces and stays near the bound
   const int64_t per = std::max<int64_t>(1, ctx->bam.cap / 2048);
   int64_t o1 = 0, o2 = 0, tot = 0;
+  // each piece indexes a byte window of about its own records (4 KiB per template, doubled when a window holds no
+  // whole template), not the whole rest of the arenas: the newline index of every piece over the remainder made the
+  // bounded add quadratic in arena / piece
+  int64_t win = per * 4096;
   while (max_templates < 0 || tot < max_templates) {
     const int64_t lim = max_templates < 0 ? per : std::min(per, max_templates - tot);
+    const int64_t r1 = ctx->used1 - o1, r2 = two ? ctx->used2 - o2 : 0;
+    const int64_t l1 = std::min(r1, win), l2 = std::min(r2, win);
     int64_t t = 0;
-    MH_TRY(bam_add(ctx, a1 + o1, ctx->used1 - o1, two ? a2 + o2 : nullptr, two ? ctx->used2 - o2 : 0, lim, &u1, &u2,
-                   &t, false));
+    MH_TRY(bam_add(ctx, a1 + o1, l1, two ? a2 + o2 : nullptr, l2, lim, &u1, &u2, &t, false));
+    if (t == 0 && (l1 < r1 || l2 < r2)) {   // (a template longer than the window: a wider one)
+      win *= 2;
+      continue;
+    }
     if (t == 0) break;
     o1 += u1;
     o2 += u2;

@@ -17,7 +17,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python3 scripts/bsum.py $O/bench_prof.json prof || true
 timeout -k 10 600 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e --verify > $O/verify.json 2> $O/verify.err
 rc=$?; echo "verify rc=$rc"; [ $rc -eq 0 ] || { tail -3 $O/verify.err; exit $rc; }
-python3 -c "import json; d=json.load(open('$O/verify.json')); v=d['verify']; print('verify', v['units'], v['units_equal'], v['templates'])"
+python3 -c "import json; d=json.load(open('$O/verify.json')); v=d['verify']; print('verify', v['units'], v['units_equal'], v['templates_kept'])"
 timeout -k 10 300 python -u bench.py --tumor-normal > $O/tn.json 2> $O/tn.err || exit $?
 python3 -c "import json; d=json.load(open('$O/tn.json')); print('tn', round(d['ms_per_step'],2), d['value'], d['bam_file_gpu']['seconds'], d['with_bam_file']['value'])" || true
 timeout -k 10 300 python -u bench.py --workload chr1 --corrupt --no-cpu-baseline --no-e2e > $O/corrupt.json 2> $O/corrupt.err || exit $?
