@@ -806,6 +806,7 @@ def run_genome(a, rank, world, local):
     if world != 1 or a.plan_share or a.rng != 'mitty':
       sys.exit('bench.py: --verify is the N = 1, rng=mitty WGS line')
     verify = verify_wgs(a, eng, batches, copies, contigs, data, units, p, rlen, model)
+  live, peak = _native.device_live_bytes()   # the library's device blocks in use (not its block cache), and their peak
   eng.close()
   kept_all, b1_all, b2_all, n_units = kept, b1, b2, len(mine)
   backend, seen = None, 1
@@ -885,6 +886,7 @@ def run_genome(a, rank, world, local):
     'span_ms': span_ms,
     'stage_note': STAGE_NOTE,
     'fastq_bytes_per_template': (b1_all + b2_all) / max(kept_all, 1),
+    'device_peak_gib': round(peak / 2 ** 30, 1),
     'setup_s': dict(synth_inputs=round(t_synth, 2), **hbm_setup()),
     'host_cpus': os.cpu_count(),
   }

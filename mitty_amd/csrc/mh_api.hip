@@ -182,10 +182,10 @@ int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes) {
   return MH_OK;
 }
 
-int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep) {
+int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep, int32_t grow_shift) {
   if (b.cap >= bytes) return MH_OK;
   DevBuf nb;
-  MH_TRY(ensure(ctx, nb, bytes + bytes / 2));
+  MH_TRY(ensure(ctx, nb, bytes + (bytes >> grow_shift)));
   MH_TRY(sync_writers(ctx));   // the old buffer's queued writers finish first
   if (b.p && keep) HIPCHK(ctx, hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
   SYNCCHK(ctx, hipStreamSynchronize(ctx->stream));

@@ -2490,8 +2490,15 @@ int32_t emit_unit_async(mh_ctx *ctx, const Hap &h, const char *serial_stub, cons
   }
   const int64_t rec_b = (int64_t)(prefix.size() + mid.size()) + ndig_host(m) + hslot + 2 * rlen + 5;
   const int64_t add = m * rec_b;
-  MH_TRY(ensure_keep(ctx, ctx->out1, ctx->used_ub1 + add + 64, ctx->used_ub1));
-  if (write_fastq2) MH_TRY(ensure_keep(ctx, ctx->out2, ctx->used_ub2 + add + 64, ctx->used_ub2));
+  // a growth reserves for the rest of the sampled batch too (its units' draws bound their templates), by an eighth
+  // more, not by half: one reallocation per batch size instead of one every few units, and no superseded arenas
+  // piling up in the device block cache
+  ctx->batch_left = std::max<int64_t>(0, ctx->batch_left - tp.n_draws);
+  const int64_t rest = ctx->batch_left * rec_b;
+  if ((int64_t)ctx->out1.cap < ctx->used_ub1 + add + 64)
+    MH_TRY(ensure_keep(ctx, ctx->out1, ctx->used_ub1 + add + rest + 64, ctx->used_ub1, 3));
+  if (write_fastq2 && (int64_t)ctx->out2.cap < ctx->used_ub2 + add + 64)
+    MH_TRY(ensure_keep(ctx, ctx->out2, ctx->used_ub2 + add + rest + 64, ctx->used_ub2, 3));
   const int64_t ntiles = (m + ED_T - 1) / ED_T;
   const size_t lb_need = 64 + 48 * (size_t)ntiles + 64;
   int32_t set = -1;

@@ -150,6 +150,7 @@ struct TplSet {
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
   mutable bool used_set = false;
   int64_t n = 0;
+  int64_t n_draws = 0;   // the unit's template draws (n <= n_draws), known when sampling is queued
   int32_t rlen = 0;
   bool valid = false;
   int32_t pend = -1;   // unit index in ctx->tail_state while the batch's asynchronous tail has not been resolved
@@ -344,6 +345,7 @@ struct mh_ctx {
   int64_t lazy_gen = 0;
   bool chain_open = false;
   int64_t used_ub1 = 0, used_ub2 = 0;
+  int64_t batch_left = 0;           // draws of the last sampled batch's units not emitted yet (arena reservation)
   bool emit_two_pass = false;       // mh_set_emit_mode(2): every unit through mh_emit_reads' path (host readbacks)
   bool emit_single = false;         // mh_set_emit_mode(3): the single-pass writer (k_emit_fused)
   // corruption rows (the direct writer's mode): per block 15 qualities | 2-bit codes; one set, the row pass and its
@@ -387,8 +389,9 @@ bool scan_fault_pending(const mh_ctx *ctx);
 
 // Grow `b` to hold at least `bytes`; contents are NOT preserved.
 int32_t ensure(mh_ctx *ctx, DevBuf &b, size_t bytes);
-// Grow preserving the first `keep` bytes (stream-ordered copy).
-int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep);
+// Grow preserving the first `keep` bytes (stream-ordered copy); the new capacity is bytes + bytes >> grow_shift (and
+// ensure's eighth).
+int32_t ensure_keep(mh_ctx *ctx, DevBuf &b, size_t bytes, size_t keep, int32_t grow_shift = 1);
 void release(DevBuf &b);
 void release_hap(Hap &h);
 int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer

@@ -1398,12 +1398,15 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     MH_TRY(ensure(ctx, ts.pos0, 8 * (q.n + 16)));
     MH_TRY(ensure(ctx, ts.pos1, 8 * (q.n + 16)));
     q.ni = nidx ? nidx[u] : NodeIdx{};
+    ts.n_draws = q.n;
     ts.has_n0 = q.ni.nd != nullptr;
     if (ts.has_n0) MH_TRY(ensure(ctx, ts.n0, 4 * (q.n + 16)));
     ts.valid = false;
     q.out = &ts;
   }
   const int64_t nn = n_max + 1;
+  ctx->batch_left = 0;
+  for (const UnitPlan &q : plan) ctx->batch_left += q.n;
   MH_TRY(ensure(ctx, ctx->s[0], 4 * (size_t)words_total + 64));
   MH_TRY(ensure(ctx, ctx->s[3], 4 * (size_t)j_total + 64));
   MH_TRY(ensure(ctx, ctx->s[4], 8 * nn));
