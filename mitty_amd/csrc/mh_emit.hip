@@ -2610,7 +2610,12 @@ int32_t emit_unit_async(mh_ctx *ctx, const Hap &h, const char *serial_stub, cons
 
 int32_t lazy_resolve(mh_ctx *ctx) {
   if (ctx->lazy.empty()) return MH_OK;
-  MH_TRY(sync_writers(ctx));   // (SYNCCHK: a look-back timeout or a bound the writer found wrong fails here)
+  const int32_t rc = sync_writers(ctx);   // (SYNCCHK: a look-back timeout or a bound the writer found wrong fails here)
+  if (rc != MH_OK) {   // the queued units' totals and ends are not to be trusted: dropped with the chain
+    ctx->lazy.clear();
+    ctx->chain_open = false;
+    return rc;
+  }
   const volatile int64_t *r = ctx->h_lazy;
   for (const auto &u : ctx->lazy) {
     int64_t k = 0, b1 = 0, b2 = 0;

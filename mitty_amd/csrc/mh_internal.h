@@ -96,8 +96,8 @@ __device__ __forceinline__ int64_t ts_pack(const NodeIdx &h, int64_t v) {
 
 // Read windows the splice bounds a read's qname part for (k_part_bound): the single-pass writer sizes its qname rows
 // and reserves arena bytes from the bound of the smallest window >= rlen, before any template is measured.
-constexpr int PB_NW = 8;
-constexpr int32_t PB_W[PB_NW] = {100, 125, 150, 175, 200, 250, 300, 321};
+constexpr int PB_NW = 4;   // (eight windows cost 35 us per chr1 haplotype, rebuilt every step)
+constexpr int32_t PB_W[PB_NW] = {100, 150, 250, 321};
 
 struct Hap {
   bool valid = false;
