@@ -1845,3 +1845,43 @@ def test_single_pass_writer_chain_across_resets_and_fallback(native, mode):
   G.check_same(first[1], b''.join(o[2] for o in o_first))
   G.check_same(second[0], b''.join(o[1] for o in o_second))
   G.check_same(second[1], b''.join(o[2] for o in o_second))
+
+
+@pytest.mark.parametrize('mode', [1, 2])
+def test_emit_async_fallback_modes_vs_oracle(native, mode):
+  """mh_emit_reads_async for units it hands to mh_emit_reads' path inside the call (mh_set_emit_mode 1: the LDS-image
+  writer; 2: the two-pass path with its host readback), queued among chained units of the default mode: the totals
+  come back in queue order from mh_emit_collect and the arenas hold the oracle's bytes; mh_emit_collect with too
+  little room fails (MH_E_CAPACITY) and keeps the totals for the next call."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 30.0)
+  L = 400_000
+  seq = synth.contig(L, 51)
+  copies = synth.copies_soa(synth.variants(seq, 52))
+  units = _native.work_units(23, [2], passes)
+  job = [(ps, 0, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)]
+  eng = Engine(0)
+  try:
+    eng.load_region(0, ('4', 0, L), seq)
+    eng.run_units(job[:1], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'F', lazy=True)
+    eng.ctx.set_emit_mode(mode)
+    eng.run_units(job[1:3], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'F', lazy=True)
+    eng.ctx.set_emit_mode(0)
+    eng.run_units(job[3:], lambda r, c: copies[c], p, 150, mdl['cum_tlen'], 'F', lazy=True)
+    import ctypes
+    n = ctypes.c_int64()
+    out = np.zeros(3, np.int64)
+    rc = eng.ctx._L.mh_emit_collect(eng.ctx._h, out.ctypes.data_as(ctypes.c_void_p), 1, ctypes.byref(n))
+    assert rc == native.MH_E_CAPACITY and n.value == len(job), (rc, n.value)
+    res = eng.collect()
+    d1, d2 = eng.ctx.fetch_output()
+  finally:
+    eng.close()
+  o = [O.generate_unit_soa(seq, 0, copies[cpy], p, 150, mdl['cum_tlen'], sd, 'F:0:{}'.format(ps), '4', cpy)
+       for ps, _, cpy, sd in job]
+  assert [r[1:] for r in res] == [(k, len(b1), len(b2)) for k, b1, b2 in o]
+  G.check_same(d1, b''.join(x[1] for x in o))
+  G.check_same(d2, b''.join(x[2] for x in o))
