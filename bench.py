@@ -110,6 +110,12 @@ def parse():
                   help='0: every unit queued with no host readback (measure pass, tile scan, k_emit_tiles chained on '
                        'the device); 2: the host reads each unit\'s totals before its writer (round 5); 3: the '
                        'single-pass writer k_emit_fused (no measure pass)')
+  ap.add_argument('--prefetch', action=argparse.BooleanOptionalAction, default=True,
+                  help='wgs: splice the next batch\'s haplotypes while the current batch is written '
+                       '(mh_prefetch_haplotypes_vset) instead of at the next batch\'s start (+1.2 %%, 4 of 4 same-box '
+                       'alternations, profiles/r06/experiments/haplotype_prefetch_ab)')
+  ap.add_argument('--prefetch-after', type=int, default=0,
+                  help='--prefetch: once this unit of the batch is queued (-1: before the first; 0 measured best)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
                   help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
@@ -782,13 +788,19 @@ def run_genome(a, rank, world, local):
   prev = []
 
   def step():
-    eng.drop_haplotypes()
-    for batch in batches:
+    eng.drop_haplotypes()   # (with --prefetch: this step's first batch's haplotypes were built during the previous step)
+    for i, batch in enumerate(batches):
       # the batch's writers append to empty arenas: they run after the previous batch's writers on the writer
       # stream, so a batch's FASTQ is complete in HBM before the next one overwrites it; no host wait on a writer
-      # anywhere in the step (the totals are read after the timed region, or at the step's end with N > 1)
+      # anywhere in the step (the totals are read after the timed region, or at the step's end with N > 1).  With
+      # --prefetch the next batch's haplotypes are spliced while this one is written (for the last batch: the next
+      # step's first batch, a fresh build kept for it) — every haplotype is still built once per step
+      last = i + 1 == len(batches)
+      nxt = batches[0] if last else batches[i + 1]
       eng.ctx.reset_output()
-      eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True)
+      eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True,
+                    prefetch=[(ri, cpy) for _, ri, cpy, _ in nxt] if a.prefetch else None, prefetch_next_step=last,
+                    prefetch_after=a.prefetch_after)
     get = lazy.getter(n_mine)
     if dist is not None:
       # RCCL over xGMI: the previous step's template / byte totals (file offsets in the file writer), all-reduced once

@@ -101,6 +101,17 @@ int32_t mh_build_haplotype_vset(mh_ctx *ctx, int32_t slot, int32_t contig_id, in
 int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
                                  const int64_t *ref_starts, const int32_t *vsets, int64_t *out_n_nodes,
                                  int64_t *out_p_min, int64_t *out_p_max);
+/* mh_build_haplotypes_vset for the NEXT batch while the current one is still being sampled and written: the call
+ * takes the slots' buffers and returns; a host thread of the context issues the splices on a stream of their own (the
+ * context's fourth, created on first use) with their own scratch, so nothing waits for the pending sampling tail
+ * (mh_sample_units_async) or for queued measure passes.  That thread is joined, and the main stream waits for the
+ * splices, before the first use of a prefetched haplotype (emission from its slot) and in every entry point that
+ * resolves the sampling tail (sampling, builds, releases...), which also report a failed splice.  The slots must be
+ * free (MH_E_ARG for a live slot); the haplotypes are byte-identical to a build (mh_get_nodes reads their nodes).
+ * (The reference builds each work unit's haplotype inside its worker, readgenerate.py:190; this only moves the
+ * build earlier in the pipeline.) */
+int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
+                                    const int64_t *ref_starts, const int32_t *vsets);
 int32_t mh_release_variants(mh_ctx *ctx, int32_t vset);
 /* Copy a slot's node list back (arrays sized n_nodes; seq bytes of node k = hap[ps[k]-p_min .. +oplen) for
  * non-'D' nodes).  Any pointer may be NULL. */

@@ -18,7 +18,7 @@ MH_RNG_MITTY, MH_RNG_PHILOX = 0, 1
 # Every exported symbol of include/mitty_hip.h (tests check the library exports all of them).
 EXPORTS = ['mh_version', 'mh_device_count', 'mh_create', 'mh_destroy', 'mh_last_error', 'mh_sync',
            'mh_selftest_scan_fault', 'mh_selftest_sort',
-           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
+           'mh_read_model_params', 'mh_work_units', 'mh_upload_contig', 'mh_build_haplotype', 'mh_upload_variants', 'mh_build_haplotype_vset', 'mh_build_haplotypes_vset', 'mh_prefetch_haplotypes_vset', 'mh_release_variants', 'mh_get_nodes',
            'mh_release_haplotype', 'mh_expand_variant', 'mh_sample_templates', 'mh_sample_templates_span', 'mh_set_templates',
            'mh_get_templates', 'mh_templates_export', 'mh_templates_import', 'mh_emit_reads', 'mh_emit_prepare', 'mh_emit_reads_async', 'mh_emit_collect', 'mh_output_size', 'mh_output_fetch', 'mh_output_reset', 'mh_host_alloc', 'mh_host_free', 'mh_device_cache_trim', 'mh_device_live_bytes',
            'mh_read_batch', 'mh_set_corruption', 'mh_set_corruption_stream', 'mh_get_corruption_stream', 'mh_stage_times', 'mh_enable_timing', 'mh_sample_units', 'mh_sample_units_async', 'mh_templates_count',
@@ -102,6 +102,7 @@ def lib():
   _sig(L, 'mh_emit_reads_async', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64])
   _sig(L, 'mh_emit_collect', [c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_build_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_prefetch_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
@@ -480,6 +481,15 @@ class Context:
     self._chk(self._L.mh_build_haplotypes_vset(self._h, n, _ptr(s), _ptr(c), _ptr(r), _ptr(v), _ptr(nn), _ptr(pmin),
                                                _ptr(pmax)))
     return [(int(nn[i]), int(pmin[i]), int(pmax[i])) for i in range(n)]
+
+  def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+    """build_haplotypes_vset for the next batch, beside the current one (mh_prefetch_haplotypes_vset: returns at once;
+    the splices run on the context's prefetch thread and stream, joined before the slots are used); the slots must be
+    free."""
+    n = len(slots)
+    a = lambda xs, t: np.ascontiguousarray(np.asarray(xs, dtype=t))
+    s, c, r, v = a(slots, np.int32), a(contig_ids, np.int32), a(ref_starts, np.int64), a(vsets, np.int32)
+    self._chk(self._L.mh_prefetch_haplotypes_vset(self._h, n, _ptr(s), _ptr(c), _ptr(r), _ptr(v)))
 
   def release_variants(self, vset):
     self._chk(self._L.mh_release_variants(self._h, int(vset)))

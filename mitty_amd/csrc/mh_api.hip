@@ -217,8 +217,28 @@ int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set) {
   return MH_OK;
 }
 
-int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set) {
-  if (set) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, hipStream_t st) {
+  if (set) HIPCHK(ctx, hipStreamWaitEvent(st ? st : ctx->stream, ev, 0));
+  return MH_OK;
+}
+
+// the prefetch thread joined (its failure reported here) and the main stream after the prefetched splices
+// (mh_prefetch_haplotypes_vset): before any use of a prefetched Hap
+int32_t join_prefetch(mh_ctx *ctx) {
+  if (ctx->pf_thread.joinable()) {
+    ctx->pf_thread.join();
+    if (ctx->pf_rc != MH_OK) {   // (its message is in ctx->err)
+      const int32_t rc = ctx->pf_rc;
+      ctx->pf_rc = MH_OK;
+      ctx->prefetch_pending = false;
+      for (auto &kv : ctx->haps) kv.second.prefetched = false;
+      return rc;
+    }
+  }
+  if (!ctx->prefetch_pending) return MH_OK;
+  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_prefetch, 0));
+  for (auto &kv : ctx->haps) kv.second.prefetched = false;
+  ctx->prefetch_pending = false;
   return MH_OK;
 }
 
@@ -309,6 +329,7 @@ using namespace mh;
   do {                                                                     \
     CTX_GUARD_EMIT(ctx);                                                   \
     MH_TRY(tpl_resolve_all(ctx));                                          \
+    MH_TRY(join_prefetch(ctx));                                            \
   } while (0)
 // every entry point but the emission ones: the main stream first waits for the last queued FASTQ writer
 #define CTX_GUARD(ctx)                                                     \
@@ -394,10 +415,12 @@ int32_t mh_create(int32_t device, mh_ctx **out) {
 
 int32_t mh_destroy(mh_ctx *ctx) {
   if (!ctx) return MH_OK;
+  if (ctx->pf_thread.joinable()) ctx->pf_thread.join();
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->wstream);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
   for (auto x : ctx->xstream)
     if (x) (void)hipStreamSynchronize(x);
   for (auto &kv : ctx->contigs) release(kv.second.seq);
@@ -425,12 +448,14 @@ int32_t mh_destroy(mh_ctx *ctx) {
   release(ctx->cr_codes);
   release(ctx->scan_partials_w);
   for (auto &b : ctx->sl2) release(b);
+  for (auto &b : ctx->sl3) release(b);
   ctx->tail_state.reset();
   for (hipEvent_t e : ctx->ev_gz)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->ev_fetch)
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+  if (ctx->h_small3) (void)hipHostFree(ctx->h_small3);
   if (ctx->h_units) (void)hipHostFree(ctx->h_units);
   for (uint8_t *p : ctx->h_bam_pin)
     if (p) (void)hipHostFree(p);
@@ -447,6 +472,8 @@ int32_t mh_destroy(mh_ctx *ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+  if (ctx->ev_prefetch) (void)hipEventDestroy(ctx->ev_prefetch);
+  if (ctx->pstream) (void)hipStreamDestroy(ctx->pstream);
   for (int l = 0; l < 2; l++) {
     if (ctx->xstream[l]) (void)hipStreamDestroy(ctx->xstream[l]);
     if (ctx->ev_xjoin[l]) (void)hipEventDestroy(ctx->ev_xjoin[l]);
@@ -607,7 +634,7 @@ int32_t mh_upload_contig(mh_ctx *ctx, int32_t contig_id, const char *seq, int64_
 // the smallest whose haplotype buffer holds `need` bytes, else the largest (grown by the build) — else fresh ones
 // (the pool grows to the generations a pipelined job needs); the main stream waits for the slot's last writer.  Best
 // fit keeps a whole genome's haplotypes (50 of very different lengths) rebuilding without a hipMalloc / hipFree.
-static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, int64_t need, Hap **out) {
+static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, int64_t need, Hap **out, hipStream_t st = nullptr) {
   if (!ctx->haps.count(slot)) {
     int best = -1, big = -1;
     for (int i = 0; i < (int)ctx->hap_spare.size(); i++) {
@@ -628,7 +655,7 @@ static int32_t hap_for_build(mh_ctx *ctx, int32_t slot, int64_t need, Hap **out)
     }
   }
   Hap &h = ctx->haps[slot];
-  MH_TRY(wait_unused(ctx, h.used, h.used_set));   // a queued writer may still read the old bytes
+  MH_TRY(wait_unused(ctx, h.used, h.used_set, st));   // a queued writer may still read the old bytes
   h.valid = false;
   *out = &h;
   return MH_OK;
@@ -743,6 +770,75 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
       if (out_p_max) out_p_max[i0 + j] = hp[j]->p_max;
     }
   }
+  return MH_OK;
+}
+
+// The next batch's haplotypes while the current batch's sampling tails, measure passes and FASTQ writers run (the
+// splice off the batch boundary's critical path).  On the calling thread: each slot's buffers (hap_for_build, the
+// prefetch stream waiting for the writer that last read a reused buffer); then a host thread of the context issues
+// the splices one after the other on the prefetch stream (created on first use, the context's fourth) with scratch
+// and a pinned readback block of their own, and waits on their readbacks, so the call returns at once and neither
+// waits for the pending sampling tail nor for the main stream's queued measure passes.  join_prefetch (every entry
+// point that resolves the sampling tail, and emission from a prefetched slot) joins that thread and makes the main
+// stream wait for the splices.  The slots must be free (a live slot may be read by queued work).
+int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
+                                    const int64_t *ref_starts, const int32_t *vsets) {
+  CTX_GUARD_EMIT(ctx);
+  MH_TRY(join_prefetch(ctx));   // (an earlier prefetch's thread)
+  if (n < 0 || (n > 0 && (!slots || !contig_ids || !ref_starts || !vsets))) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  for (int32_t i = 0; i < n; i++) {
+    if (!ctx->contigs.count(contig_ids[i])) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
+    if (vsets[i] < 0 || !ctx->vsets.count(vsets[i])) return arg_fail(ctx, MH_E_STATE, "unknown variant set id");
+    if (ctx->haps.count(slots[i])) return arg_fail(ctx, MH_E_ARG, "prefetch into a live haplotype slot");
+    for (int32_t j = 0; j < i; j++)
+      if (slots[j] == slots[i]) return arg_fail(ctx, MH_E_ARG, "a slot appears twice");
+  }
+  if (n == 0) return MH_OK;
+  if (!ctx->pstream) {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    HIPCHK(ctx, hipStreamCreateWithPriority(&ctx->pstream, hipStreamNonBlocking, hi));
+    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_prefetch, hipEventDisableTiming));
+  }
+  if (!ctx->h_small3 && hipHostMalloc((void **)&ctx->h_small3, 4096, hipHostMallocDefault) != hipSuccess) {
+    ctx->h_small3 = nullptr;
+    return arg_fail(ctx, MH_E_OOM, "pinned host memory");
+  }
+  struct Job {
+    Hap *h;
+    const Contig *c;
+    int64_t rs;
+    const VarSet *v;
+  };
+  std::vector<Job> jobs;
+  for (int32_t i = 0; i < n; i++) {
+    const Contig &c = ctx->contigs[contig_ids[i]];
+    Hap *hp = nullptr;
+    MH_TRY(hap_for_build(ctx, slots[i], c.len + (c.len >> 6) + (1 << 20), &hp, ctx->pstream));
+    hp->prefetched = true;   // (Hap references stay valid while other slots are inserted: node-based map)
+    jobs.push_back(Job{hp, &c, ref_starts[i], &ctx->vsets[vsets[i]]});
+  }
+  ctx->prefetch_pending = true;
+  ctx->pf_rc = MH_OK;
+  ctx->pf_thread = std::thread([ctx, jobs]() {   // nothing may escape the thread (std::terminate): errors become codes
+    int32_t rc = MH_OK;
+    lane_thread_enter(ctx);
+    try {
+      const hipError_t e = hipSetDevice(ctx->device);
+      if (e != hipSuccess) rc = hip_fail(ctx, e, "hipSetDevice (prefetch)", __FILE__, __LINE__);
+      for (size_t k = 0; k < jobs.size() && rc == MH_OK; k++)
+        rc = splice_build(ctx, *jobs[k].h, *jobs[k].c, jobs[k].rs, *jobs[k].v, 2);
+      const hipError_t e2 = hipEventRecord(ctx->ev_prefetch, ctx->pstream);
+      if (rc == MH_OK && e2 != hipSuccess) rc = hip_fail(ctx, e2, "hipEventRecord (prefetch)", __FILE__, __LINE__);
+    } catch (const std::bad_alloc &) {
+      rc = arg_fail(ctx, MH_E_OOM, "host memory (prefetch)");
+    } catch (const std::exception &x) {
+      rc = arg_fail(ctx, MH_E_STATE, std::string("prefetch: ") + x.what());
+    } catch (...) {
+      rc = arg_fail(ctx, MH_E_STATE, "prefetch: unknown exception");
+    }
+    ctx->pf_rc = rc;
+  });
   return MH_OK;
 }
 
@@ -1014,6 +1110,7 @@ int32_t mh_emit_reads(mh_ctx *ctx, int32_t slot, const char *serial_stub, const 
   MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (it->second.prefetched) MH_TRY(join_prefetch(ctx));   // (its splice was queued on the prefetch stream)
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
   return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, false, out_kept,
                     out_b1, out_b2);
@@ -1025,6 +1122,7 @@ int32_t mh_emit_prepare(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
   MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (it->second.prefetched) MH_TRY(join_prefetch(ctx));   // (its splice was queued on the prefetch stream)
   if (!serial_stub || !chrom || (!out_kept) != (!out_b1) || (!out_kept) != (!out_b2))
     return arg_fail(ctx, MH_E_ARG, "null argument");
   return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, 0, -1, 0, true, out_kept,
@@ -1038,6 +1136,7 @@ int32_t mh_emit_reads_range(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
   MH_TRY(lazy_resolve(ctx));   // (appends at the arenas' exact ends)
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (it->second.prefetched) MH_TRY(join_prefetch(ctx));   // (its splice was queued on the prefetch stream)
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (t_begin < 0 || t_end < t_begin || cnt_base < 0) return arg_fail(ctx, MH_E_ARG, "bad template range");
   return emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,
@@ -1049,6 +1148,7 @@ int32_t mh_emit_reads_async(mh_ctx *ctx, int32_t slot, const char *serial_stub, 
   CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (it->second.prefetched) MH_TRY(join_prefetch(ctx));   // (its splice was queued on the prefetch stream)
   if (!serial_stub || !chrom) return arg_fail(ctx, MH_E_ARG, "null argument");
   bool queued = false;
   MH_TRY(emit_unit_async(ctx, it->second, serial_stub, chrom, cpy, write_fastq2, unit_key, &queued));
@@ -1082,6 +1182,7 @@ int32_t mh_emit_measure(mh_ctx *ctx, int32_t slot, const char *serial_stub, cons
   CTX_GUARD_EMIT(ctx);
   auto it = ctx->haps.find(slot);
   if (it == ctx->haps.end() || !it->second.valid) return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+  if (it->second.prefetched) MH_TRY(join_prefetch(ctx));   // (its splice was queued on the prefetch stream)
   if (!serial_stub || !chrom || !out_kept || !out_b1 || !out_b2) return arg_fail(ctx, MH_E_ARG, "null argument");
   if (t_begin < 0 || (t_end >= 0 && t_end < t_begin) || cnt_base < 0) return arg_fail(ctx, MH_E_ARG, "bad template range");
   MH_TRY(emit_reads(ctx, it->second, slot, serial_stub, chrom, cpy, write_fastq2, unit_key, t_begin, t_end, cnt_base,

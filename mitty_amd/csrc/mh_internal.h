@@ -10,6 +10,7 @@
 #include <unordered_map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mitty_hip.h"
@@ -113,6 +114,7 @@ struct Hap {
   bool bound_valid = false;
   int32_t part_w[PB_NW] = {0};
   int64_t pos_max = 0;
+  bool prefetched = false;   // built by mh_prefetch_haplotypes_vset, not yet joined (join_prefetch)
 };
 inline NodeIdx node_idx_of(const Hap &h) {
   NodeIdx n;
@@ -295,6 +297,15 @@ struct mh_ctx {
   mh::DevBuf xscan[2];
   hipEvent_t ev_xjoin[2] = {nullptr, nullptr};
   mh::DevBuf sl2[8];   // the splice's second lane: anchor, accepted, ref_before, node src, small, partials, N runs, sort
+  // mh_prefetch_haplotypes_vset: the next batch's splices issued by a host thread of the context on a stream of their
+  // own (the fourth: GPU_MAX_HW_QUEUES is 4) with their own scratch and pinned readback block
+  hipStream_t pstream = nullptr;
+  hipEvent_t ev_prefetch = nullptr;   // after the last prefetched splice
+  bool prefetch_pending = false;      // some Hap has prefetched set
+  std::thread pf_thread;              // the host thread issuing the prefetched splices (their readbacks wait there)
+  int32_t pf_rc = 0;                  // its result
+  mh::DevBuf sl3[8];
+  int64_t *h_small3 = nullptr;
   mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
   mh::DevBuf d_small;        // device small scalars
 
@@ -397,7 +408,8 @@ void release_hap(Hap &h);
 int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FASTQ writer
 // a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
 int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set);
-int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set);
+int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, hipStream_t st = nullptr);   // st: ctx->stream when null
+int32_t join_prefetch(mh_ctx *ctx);   // the prefetch thread joined, the main stream after its splices
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);

@@ -538,22 +538,23 @@ void release_vars(VarSet &v) {
 
 int32_t splice_build(mh_ctx *ctx, Hap &h, const Contig &c, int64_t rs, const VarSet &v, int lane) {
   // lane 1 (mh_build_haplotypes_vset's second copy, on a host thread of its own): the second stream and its own
-  // scratch, no stage timing
+  // scratch, no stage timing; lane 2 (mh_prefetch_haplotypes_vset's thread): the prefetch stream and its own scratch
   const bool l1 = lane != 0;
-  hipStream_t st = l1 ? ctx->stream2 : ctx->stream;
-  DevBuf &b_anchor = l1 ? ctx->sl2[0] : ctx->s[6], &b_acc = l1 ? ctx->sl2[1] : ctx->s[7];
-  DevBuf &b_refb = l1 ? ctx->sl2[2] : ctx->s[8], &b_nsrc = l1 ? ctx->sl2[3] : ctx->s[9];
-  DevBuf &b_small = l1 ? ctx->sl2[4] : ctx->d_small, &b_part = l1 ? ctx->sl2[5] : ctx->scan_partials;
-  DevBuf &b_nrun = l1 ? ctx->sl2[6] : ctx->nrun_tmp, &b_perm = l1 ? ctx->sl2[7] : ctx->perm_tmp;
+  hipStream_t st = lane == 2 ? ctx->pstream : l1 ? ctx->stream2 : ctx->stream;
+  DevBuf *sl = lane == 2 ? ctx->sl3 : ctx->sl2;
+  DevBuf &b_anchor = l1 ? sl[0] : ctx->s[6], &b_acc = l1 ? sl[1] : ctx->s[7];
+  DevBuf &b_refb = l1 ? sl[2] : ctx->s[8], &b_nsrc = l1 ? sl[3] : ctx->s[9];
+  DevBuf &b_small = l1 ? sl[4] : ctx->d_small, &b_part = l1 ? sl[5] : ctx->scan_partials;
+  DevBuf &b_nrun = l1 ? sl[6] : ctx->nrun_tmp, &b_perm = l1 ? sl[7] : ctx->perm_tmp;
   auto stage_begin = [&](mh_ctx *cx, const char *name) {
     if (!l1) ::mh::stage_begin(cx, name);
   };
   auto stage_end = [&](mh_ctx *cx) {
     if (!l1) ::mh::stage_end(cx);
   };
-  int64_t *hs_base = pinned_small(ctx);
+  int64_t *hs_base = lane == 2 ? ctx->h_small3 : pinned_small(ctx);
   if (!hs_base) return arg_fail(ctx, MH_E_OOM, "pinned host memory");
-  int64_t *const hs_lane = hs_base + (l1 ? 256 : 0);
+  int64_t *const hs_lane = hs_base + (lane == 1 ? 256 : 0);
   const int64_t n_var = v.n;
   const int64_t nv = n_var > 0 ? n_var : 1;
   const int64_t node_cap = 2 * n_var + 1;

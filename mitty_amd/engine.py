@@ -32,6 +32,8 @@ class Engine:
       self.ctx.set_emit_mode(emit_mode)
     self._regions = {}   # ri -> region tuple (contig uploaded)
     self._haps = {}      # (ri, cpy) -> (slot, n_nodes, p_min, p_max)
+    self._pre = {}       # (ri, cpy) -> (slot, ...) prefetched for the next step (adopted by drop_haplotypes)
+    self._gen = {}       # (ri, cpy) -> the generation (0 / 1) of its last slot: a new build takes the other one
     self._vsets = {}     # (ri, cpy) -> resident variant set id (upload_variants)
     self._tpl_base = 0
     self._lazy_n = []    # template counts of the units queued by run_units and not yet collected
@@ -50,11 +52,17 @@ class Engine:
     self.ctx.upload_variants(vset, soa)
     self._vsets[(ri, cpy)] = vset
 
+  def _slot(self, key):
+    """A slot for a new build of key: the generation its last slot did not use (that one may still be live)."""
+    g = 1 - self._gen.get(key, 1)
+    self._gen[key] = g
+    return key[0] * self.SLOTS_PER_REGION + 2 * g + key[1]
+
   def haplotype(self, ri, cpy, soa):
     key = (ri, cpy)
     if key not in self._haps:
       region = self._regions[ri]
-      slot = ri * self.SLOTS_PER_REGION + cpy
+      slot = self._slot(key)
       if key in self._vsets:
         n_nodes, p_min, p_max = self.ctx.build_haplotype_vset(slot, ri, region[1] + 1, self._vsets[key])
       else:
@@ -67,12 +75,27 @@ class Engine:
     time side by side (mh_build_haplotypes_vset); keys already built are kept."""
     todo = [k for k in dict.fromkeys(keys) if k not in self._haps and k in self._vsets]
     if todo:
-      slots = [ri * self.SLOTS_PER_REGION + cpy for ri, cpy in todo]
+      slots = [self._slot(k) for k in todo]
       res = self.ctx.build_haplotypes_vset(slots, [ri for ri, _ in todo],
                                            [self._regions[ri][1] + 1 for ri, _ in todo],
                                            [self._vsets[k] for k in todo])
       for k, slot, r in zip(todo, slots, res):
         self._haps[k] = (slot,) + tuple(r)
+
+  def prefetch(self, keys, next_step=False):
+    """Build the haplotypes of the next batch while the current one is sampled and written
+    (mh_prefetch_haplotypes_vset: returns at once, the splices off the batch boundary's critical path).  Keys already
+    built are kept, unless next_step: then every key gets a fresh build (into its other slot generation), kept apart
+    until drop_haplotypes adopts them for the next step."""
+    todo = [k for k in dict.fromkeys(keys) if k in self._vsets and k not in self._pre and
+            (next_step or k not in self._haps)]
+    if not todo:
+      return
+    slots = [self._slot(k) for k in todo]
+    self.ctx.prefetch_haplotypes_vset(slots, [ri for ri, _ in todo], [self._regions[ri][1] + 1 for ri, _ in todo],
+                                      [self._vsets[k] for k in todo])
+    for k, slot in zip(todo, slots):   # (n_nodes, p_min, p_max: not known until the splice has run; get_nodes)
+      (self._pre if next_step else self._haps)[k] = (slot, None, None, None)
 
   def drop_variants(self):
     for vset in self._vsets.values():
@@ -80,17 +103,21 @@ class Engine:
     self._vsets.clear()
 
   def drop_haplotypes(self):
+    """Release the haplotypes; those prefetched for the next step (prefetch(..., next_step=True)) become current."""
     for slot, *_ in self._haps.values():
       self.ctx.release_haplotype(slot)
-    self._haps.clear()
+    self._haps, self._pre = self._pre, {}
 
   def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None, lazy=False):
+                on_unit=None, lazy=False, prefetch=None, prefetch_next_step=False, prefetch_after=0):
     """Sample a batch of work units together, then emit them in order.
 
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
     unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit; lazy=True returns None
     and leaves the units' results to collect(), so the caller queues the next batch while these writers run.
+    prefetch: the next batch's (ri, cpy) keys, built (Engine.prefetch) once unit `prefetch_after` is queued (-1:
+    before unit 0) instead of at the next batch's start; unit 0 measured best (its wait for the batch's head is over,
+    and the splices have the rest of the batch to finish before the next head needs them).
     """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
@@ -107,11 +134,16 @@ class Engine:
     if self.emit_mode in (1, 2):
       return self._emit_two_pass(units, slots, base, sample_name, worker_id, write_fastq2, on_unit, lazy)
     out = []
+    at = min(prefetch_after, len(units) - 1) if prefetch else -1
+    if prefetch and prefetch_after < 0:   # (before unit 0: beside this batch's sampling head)
+      self.prefetch(prefetch, prefetch_next_step)
     for k, (ps, ri, cpy, seed) in enumerate(units):
       self.ctx.use_templates(base + k)
       self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
                           write_fastq2, unit_key=seed)
       self._lazy_n.append(self.ctx.template_count(base + k))
+      if k == at:
+        self.prefetch(prefetch, prefetch_next_step)
       if on_unit is not None:
         done = self.collect()
         out += done

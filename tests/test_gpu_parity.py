@@ -433,6 +433,69 @@ def test_batched_units_vs_oracle(native):
   assert fix <= 1   # (the exact fallbacks are forced and pinned in test_*_forced_fallbacks_vs_oracle)
 
 
+def test_prefetched_haplotypes_vs_build(native):
+  """Engine.run_units(prefetch=...) as `bench.py --prefetch` runs it: the next batch's haplotypes spliced by the
+  context's prefetch thread on its own stream (mh_prefetch_haplotypes_vset) while the current batch is sampled and
+  written, and the next step's first batch as a fresh build kept across drop_haplotypes.  Two steps of three batches:
+  every batch's FASTQ equal to the same run with every haplotype built at its batch's start, the first step equal to
+  the oracle's; a prefetch into a live slot is refused."""
+  from mitty_amd import _native, synth
+  from mitty_amd.engine import Engine
+  from oracle import oracle as O
+  mdl = G.model('hiseq-X-v2.5-Garvan')
+  p, passes = _native.read_model_params(150, 10.0)
+  lens = [3_000_000, 2_000_000, 2_500_000]
+  regions = [(str(7 + i), 0, L) for i, L in enumerate(lens)]
+  seqs = [synth.contig(L, 51 + i) for i, L in enumerate(lens)]
+  copies = [synth.copies_soa(synth.variants(s, 61 + i)) for i, s in enumerate(seqs)]
+  units = _native.work_units(77, [2] * len(lens), passes)
+  job = [(ps, ri, cpy, sd) for ps, (ri, cpy, sd) in enumerate(units)]
+  batches = [[u for u in job if u[1] == ri] for ri in range(len(lens))]
+
+  def run(prefetch):
+    eng = Engine(0)
+    outs = []
+    try:
+      for ri, (reg, sq) in enumerate(zip(regions, seqs)):
+        eng.load_region(ri, reg, sq)
+        for cpy in (0, 1):
+          eng.upload_variants(ri, cpy, copies[ri][cpy])
+      for step in range(2):
+        eng.drop_haplotypes()
+        for i, batch in enumerate(batches):
+          last = i + 1 == len(batches)
+          nxt = batches[0] if last else batches[i + 1]
+          eng.ctx.reset_output()
+          res = eng.run_units(batch, lambda r, c: copies[r][c], p, 150, mdl['cum_tlen'], 'PF',
+                              prefetch=[(ri, cpy) for _, ri, cpy, _ in nxt] if prefetch else None,
+                              prefetch_next_step=last, prefetch_after=0)
+          outs.append((res, eng.ctx.fetch_output()))
+      if prefetch:
+        live = eng._haps[(0, 0)][0]
+        with pytest.raises(ValueError):   # (MH_E_ARG: a live slot)
+          eng.ctx.prefetch_haplotypes_vset([live], [0], [1], [eng._vsets[(0, 0)]])
+    finally:
+      eng.close()
+    return outs
+
+  a, b = run(True), run(False)
+  assert len(a) == len(b) == 2 * len(batches)
+  for (ra, (a1, a2)), (rb, (b1, b2)) in zip(a, b):
+    assert ra == rb
+    G.check_same(a1, b1)
+    G.check_same(a2, b2)
+  for i, batch in enumerate(batches):   # the first step against the oracle
+    o1, o2 = [], []
+    for ps, ri, cpy, sd in batch:
+      k, x1, x2 = O.generate_unit_soa(seqs[ri], 0, copies[ri][cpy], p, 150, mdl['cum_tlen'], sd, 'PF:0:{}'.format(ps),
+                                      regions[ri][0], cpy)
+      o1.append(x1)
+      o2.append(x2)
+    G.check_same(a[i][1][0], b''.join(o1))
+    G.check_same(a[i][1][1], b''.join(o2))
+    assert a[i][1][0] == a[len(batches) + i][1][0]   # (the second step repeats the first)
+
+
 def test_lsd_sort_repeated_batches(native):
   """The permutation sort (mh_sort.h) over batches of different sizes and then the first batch again: its look-back
   status words sit inside the sort's buffer at an offset that moves with the batch size, so a batch size seen before
