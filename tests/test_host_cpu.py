@@ -490,3 +490,48 @@ def test_rpc_variant_helpers_chain_equals_node_list_oracle():
       got.append((samp_pos, ref_pos, '=', len(seq) - off, seq[off:], None))
     want = [tuple(n) for n in O.create_node_list(seq.encode(), rs, vl)]
     assert got == want, (vl, got, want)
+
+
+def test_engine_prefetch_slot_generations():
+  """Engine's haplotype slots (no GPU: a stand-in context records the calls): a prefetch for the next step builds
+  every key afresh into the slot generation its live slot does not use, kept apart until drop_haplotypes releases the
+  current ones and adopts them; a prefetch within a step skips keys already built; builds alternate generations, so
+  a key's new slot is never its live one (mh_prefetch_haplotypes_vset refuses live slots)."""
+  from mitty_amd.engine import Engine
+
+  class Ctx:
+    def __init__(self):
+      self.live, self.calls = set(), []
+
+    def build_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+      assert not self.live & set(slots)
+      self.live |= set(slots)
+      self.calls.append(('build', tuple(slots)))
+      return [(3, 1, 9)] * len(slots)
+
+    def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+      assert not self.live & set(slots)
+      self.live |= set(slots)
+      self.calls.append(('prefetch', tuple(slots)))
+
+    def release_haplotype(self, slot):
+      self.live.remove(slot)
+
+  eng = Engine.__new__(Engine)
+  eng.ctx = Ctx()
+  eng._regions = {0: ('1', 0, 100), 1: ('2', 0, 100)}
+  eng._vsets = {(0, 0): 0, (0, 1): 1, (1, 0): 64, (1, 1): 65}
+  eng._haps, eng._pre, eng._gen = {}, {}, {}
+  a, b = [(0, 0), (0, 1)], [(1, 0), (1, 1)]
+  eng.haplotypes(a)                        # step 1, batch 0
+  eng.prefetch(b)                          # batch 1 during batch 0
+  eng.prefetch(b)                          # (already built: nothing)
+  eng.prefetch(a, next_step=True)          # the next step's batch 0 during the last batch: fresh builds
+  assert eng.ctx.calls == [('build', (0, 1)), ('prefetch', (64, 65)), ('prefetch', (2, 3))]
+  assert set(eng._haps) == set(a + b) and set(eng._pre) == set(a)
+  eng.drop_haplotypes()                    # step 2: the prefetched ones become current, the rest released
+  assert eng.ctx.live == {2, 3} and set(eng._haps) == set(a) and not eng._pre
+  eng.haplotypes(a + b)                    # a kept (built during step 1), b rebuilt in its other generation
+  assert eng.ctx.calls[-1] == ('build', (66, 67))
+  eng.prefetch(a, next_step=True)
+  assert eng.ctx.calls[-1] == ('prefetch', (0, 1))
