@@ -111,11 +111,15 @@ def parse():
                        'the device); 2: the host reads each unit\'s totals before its writer (round 5); 3: the '
                        'single-pass writer k_emit_fused (no measure pass)')
   ap.add_argument('--prefetch', action=argparse.BooleanOptionalAction, default=True,
-                  help='wgs: splice the next batch\'s haplotypes while the current batch is written '
-                       '(mh_prefetch_haplotypes_vset) instead of at the next batch\'s start (+1.2 %%, 4 of 4 same-box '
-                       'alternations, profiles/r06/experiments/haplotype_prefetch_ab)')
+                  help='wgs: splice the next batch\'s haplotypes and generate its MT19937 word streams while the '
+                       'current batch is written (mh_prefetch_haplotypes_vset) instead of at the next batch\'s start '
+                       '(+1.8 %%, 4 of 4 same-box alternations, profiles/r06/experiments/haplotype_prefetch_ab)')
   ap.add_argument('--prefetch-after', type=int, default=0,
                   help='--prefetch: once this unit of the batch is queued (-1: before the first; 0 measured best)')
+  ap.add_argument('--prefetch-last-after', type=int, default=-1,
+                  help='--prefetch, the step\'s last batch (the next step\'s first batch prefetched): after this unit '
+                       '(-1, before its first: the last batch is short and the next step\'s first batch has many '
+                       'haplotypes; +1.2 %% over 0, profiles/r06/experiments/haplotype_prefetch_ab/words_last_batch)')
   ap.add_argument('--synth-workers', type=int, default=8, help='processes building the synthetic inputs')
   ap.add_argument('--cpu-config0', action=argparse.BooleanOptionalAction, default=True,
                   help='N = 1: also time the CPU oracle on BASELINE configs[0] (hg001.bed: 2 x 1 Mbp, 1kg-pcr-free, '
@@ -799,8 +803,8 @@ def run_genome(a, rank, world, local):
       nxt = batches[0] if last else batches[i + 1]
       eng.ctx.reset_output()
       eng.run_units(batch, lambda r, c: copies[r][c], p, rlen, model['cum_tlen'], 'SYN', 0, True, a.rng, lazy=True,
-                    prefetch=[(ri, cpy) for _, ri, cpy, _ in nxt] if a.prefetch else None, prefetch_next_step=last,
-                    prefetch_after=a.prefetch_after)
+                    prefetch=nxt if a.prefetch else None, prefetch_next_step=last,
+                    prefetch_after=a.prefetch_last_after if last else a.prefetch_after)
     get = lazy.getter(n_mine)
     if dist is not None:
       # RCCL over xGMI: the previous step's template / byte totals (file offsets in the file writer), all-reduced once

@@ -104,14 +104,18 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
 /* mh_build_haplotypes_vset for the NEXT batch while the current one is still being sampled and written: the call
  * takes the slots' buffers and returns; a host thread of the context issues the splices on a stream of their own (the
  * context's fourth, created on first use) with their own scratch, so nothing waits for the pending sampling tail
- * (mh_sample_units_async) or for queued measure passes.  That thread is joined, and the main stream waits for the
- * splices, before the first use of a prefetched haplotype (emission from its slot) and in every entry point that
- * resolves the sampling tail (sampling, builds, releases...), which also report a failed splice.  The slots must be
- * free (MH_E_ARG for a live slot); the haplotypes are byte-identical to a build (mh_get_nodes reads their nodes).
- * (The reference builds each work unit's haplotype inside its worker, readgenerate.py:190; this only moves the
- * build earlier in the pipeline.) */
+ * (mh_sample_units_async) or for queued measure passes.  Given the next batch's units (n_units > 0: each unit's
+ * haplotype slot — prefetched here or live — and seed, and p as mh_sample_units takes them, rng mode mitty), the same
+ * thread then generates their MT19937 word streams into a buffer of their own; mh_sample_units(_async) of a batch
+ * with exactly those units, spans and p takes that buffer instead of generating them (the same words).  That thread is
+ * joined, and the main stream waits for its work, before the first use of a prefetched haplotype (emission from its
+ * slot) and in every entry point that resolves the sampling tail (sampling, builds, releases...), which also report a
+ * failed splice.  The slots must be free (MH_E_ARG for a live slot); the haplotypes are byte-identical to a build.
+ * (The reference builds each work unit's haplotype and draws its streams inside its worker, readgenerate.py:190,
+ * illumina.py:43-110; this only moves that work earlier in the pipeline.) */
 int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
-                                    const int64_t *ref_starts, const int32_t *vsets);
+                                    const int64_t *ref_starts, const int32_t *vsets, int32_t n_units,
+                                    const int32_t *unit_slots, const uint64_t *unit_seeds, double p);
 int32_t mh_release_variants(mh_ctx *ctx, int32_t vset);
 /* Copy a slot's node list back (arrays sized n_nodes; seq bytes of node k = hap[ps[k]-p_min .. +oplen) for
  * non-'D' nodes).  Any pointer may be NULL. */

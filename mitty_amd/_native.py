@@ -102,7 +102,7 @@ def lib():
   _sig(L, 'mh_emit_reads_async', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64])
   _sig(L, 'mh_emit_collect', [c_vp, c_vp, c_i64, P_i64])
   _sig(L, 'mh_build_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
-  _sig(L, 'mh_prefetch_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp])
+  _sig(L, 'mh_prefetch_haplotypes_vset', [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_dbl])
   _sig(L, 'mh_emit_reads_range', [c_vp, c_i32, ctypes.c_char_p, ctypes.c_char_p, c_i64, c_i32, c_u64, c_i64, c_i64,
                                    c_i64, P_i64, P_i64, P_i64])
   _sig(L, 'mh_count_kept', [c_vp, c_i32, c_i64, c_i64, P_i64])
@@ -482,14 +482,17 @@ class Context:
                                                _ptr(pmax)))
     return [(int(nn[i]), int(pmin[i]), int(pmax[i])) for i in range(n)]
 
-  def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+  def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets, unit_slots=(), unit_seeds=(), p=1.0):
     """build_haplotypes_vset for the next batch, beside the current one (mh_prefetch_haplotypes_vset: returns at once;
     the splices run on the context's prefetch thread and stream, joined before the slots are used); the slots must be
-    free."""
-    n = len(slots)
+    free.  unit_slots / unit_seeds / p: the next batch's units, whose MT19937 word streams the same thread generates
+    for the sample_units call that matches them."""
+    n, nu = len(slots), len(unit_slots)
     a = lambda xs, t: np.ascontiguousarray(np.asarray(xs, dtype=t))
     s, c, r, v = a(slots, np.int32), a(contig_ids, np.int32), a(ref_starts, np.int64), a(vsets, np.int32)
-    self._chk(self._L.mh_prefetch_haplotypes_vset(self._h, n, _ptr(s), _ptr(c), _ptr(r), _ptr(v)))
+    us, ud = a(unit_slots, np.int32), a(unit_seeds, np.uint64)
+    self._chk(self._L.mh_prefetch_haplotypes_vset(self._h, n, _ptr(s), _ptr(c), _ptr(r), _ptr(v), nu, _ptr(us),
+                                                  _ptr(ud), float(p)))
 
   def release_variants(self, vset):
     self._chk(self._L.mh_release_variants(self._h, int(vset)))

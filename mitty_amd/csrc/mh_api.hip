@@ -773,8 +773,9 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
   return MH_OK;
 }
 
-// The next batch's haplotypes while the current batch's sampling tails, measure passes and FASTQ writers run (the
-// splice off the batch boundary's critical path).  On the calling thread: each slot's buffers (hap_for_build, the
+// The next batch's haplotypes — and, given its units, its MT19937 word streams — while the current batch's sampling
+// tails, measure passes and FASTQ writers run (the splice and the word generation off the batch boundary's critical
+// path).  On the calling thread: each slot's buffers (hap_for_build, the
 // prefetch stream waiting for the writer that last read a reused buffer); then a host thread of the context issues
 // the splices one after the other on the prefetch stream (created on first use, the context's fourth) with scratch
 // and a pinned readback block of their own, and waits on their readbacks, so the call returns at once and neither
@@ -782,10 +783,13 @@ int32_t mh_build_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, c
 // point that resolves the sampling tail, and emission from a prefetched slot) joins that thread and makes the main
 // stream wait for the splices.  The slots must be free (a live slot may be read by queued work).
 int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots, const int32_t *contig_ids,
-                                    const int64_t *ref_starts, const int32_t *vsets) {
+                                    const int64_t *ref_starts, const int32_t *vsets, int32_t n_units,
+                                    const int32_t *unit_slots, const uint64_t *unit_seeds, double p) {
   CTX_GUARD_EMIT(ctx);
   MH_TRY(join_prefetch(ctx));   // (an earlier prefetch's thread)
   if (n < 0 || (n > 0 && (!slots || !contig_ids || !ref_starts || !vsets))) return arg_fail(ctx, MH_E_ARG, "bad arguments");
+  if (n_units < 0 || (n_units > 0 && (!unit_slots || !unit_seeds || !(p > 0.0 && p <= 1.0))))
+    return arg_fail(ctx, MH_E_ARG, "bad unit arguments");
   for (int32_t i = 0; i < n; i++) {
     if (!ctx->contigs.count(contig_ids[i])) return arg_fail(ctx, MH_E_STATE, "unknown contig id");
     if (vsets[i] < 0 || !ctx->vsets.count(vsets[i])) return arg_fail(ctx, MH_E_STATE, "unknown variant set id");
@@ -793,7 +797,7 @@ int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots
     for (int32_t j = 0; j < i; j++)
       if (slots[j] == slots[i]) return arg_fail(ctx, MH_E_ARG, "a slot appears twice");
   }
-  if (n == 0) return MH_OK;
+  if (n == 0 && n_units == 0) return MH_OK;
   if (!ctx->pstream) {
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
@@ -818,9 +822,19 @@ int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots
     hp->prefetched = true;   // (Hap references stay valid while other slots are inserted: node-based map)
     jobs.push_back(Job{hp, &c, ref_starts[i], &ctx->vsets[vsets[i]]});
   }
+  // the units' haplotypes: prefetched above (spans known once spliced) or live
+  std::vector<const Hap *> uh(n_units);
+  for (int32_t u = 0; u < n_units; u++) {
+    auto it = ctx->haps.find(unit_slots[u]);
+    if (it == ctx->haps.end() || (!it->second.valid && !it->second.prefetched))
+      return arg_fail(ctx, MH_E_STATE, "empty haplotype slot");
+    uh[u] = &it->second;
+  }
+  std::vector<uint64_t> useeds(unit_seeds, unit_seeds + n_units);
+  ctx->pf_words.valid = false;
   ctx->prefetch_pending = true;
   ctx->pf_rc = MH_OK;
-  ctx->pf_thread = std::thread([ctx, jobs]() {   // nothing may escape the thread (std::terminate): errors become codes
+  ctx->pf_thread = std::thread([ctx, jobs, uh, useeds, p]() {   // nothing may escape the thread: errors become codes
     int32_t rc = MH_OK;
     lane_thread_enter(ctx);
     try {
@@ -828,6 +842,14 @@ int32_t mh_prefetch_haplotypes_vset(mh_ctx *ctx, int32_t n, const int32_t *slots
       if (e != hipSuccess) rc = hip_fail(ctx, e, "hipSetDevice (prefetch)", __FILE__, __LINE__);
       for (size_t k = 0; k < jobs.size() && rc == MH_OK; k++)
         rc = splice_build(ctx, *jobs[k].h, *jobs[k].c, jobs[k].rs, *jobs[k].v, 2);
+      if (rc == MH_OK && !uh.empty()) {   // the next batch's word streams (sample_head takes them when it matches)
+        std::vector<int64_t> pmin(uh.size()), pmax(uh.size());
+        for (size_t u = 0; u < uh.size(); u++) {
+          pmin[u] = uh[u]->p_min;
+          pmax[u] = uh[u]->p_max;
+        }
+        rc = prefetch_words(ctx, ctx->pstream, (int32_t)uh.size(), pmin.data(), pmax.data(), useeds.data(), p);
+      }
       const hipError_t e2 = hipEventRecord(ctx->ev_prefetch, ctx->pstream);
       if (rc == MH_OK && e2 != hipSuccess) rc = hip_fail(ctx, e2, "hipEventRecord (prefetch)", __FILE__, __LINE__);
     } catch (const std::bad_alloc &) {

@@ -100,6 +100,17 @@ __device__ __forceinline__ int64_t ts_pack(const NodeIdx &h, int64_t v) {
 constexpr int PB_NW = 4;   // (eight windows cost 35 us per chr1 haplotype, rebuilt every step)
 constexpr int32_t PB_W[PB_NW] = {100, 150, 250, 321};
 
+// The next sampling batch's word streams, generated on the prefetch stream into their own buffer (prefetch_words);
+// sample_head takes the buffer when its batch has the same units (seeds, spans) and p
+struct PrefetchedWords {
+  bool valid = false;
+  double p = 0.0;
+  std::vector<uint64_t> seeds;
+  std::vector<int64_t> p_min, p_max;
+  int64_t words_total = 0;
+  DevBuf buf, jobs;
+};
+
 struct Hap {
   bool valid = false;
   mutable hipEvent_t used = nullptr;   // after the last FASTQ writer that reads it (writer stream)
@@ -306,6 +317,7 @@ struct mh_ctx {
   int32_t pf_rc = 0;                  // its result
   mh::DevBuf sl3[8];
   int64_t *h_small3 = nullptr;
+  mh::PrefetchedWords pf_words;       // the next batch's MT19937 word streams (prefetch_words), or none
   mh::DevBuf pinned_small;   // host-visible small readback area (hipHostMalloc)
   mh::DevBuf d_small;        // device small scalars
 
@@ -409,7 +421,12 @@ int32_t join_writer(mh_ctx *ctx);   // main stream waits for the last queued FAS
 // a resource a queued FASTQ writer reads: mark it (writer stream) / make the main stream wait before overwriting it
 int32_t mark_used(mh_ctx *ctx, hipEvent_t &ev, bool &set);
 int32_t wait_unused(mh_ctx *ctx, hipEvent_t ev, bool set, hipStream_t st = nullptr);   // st: ctx->stream when null
-int32_t join_prefetch(mh_ctx *ctx);   // the prefetch thread joined, the main stream after its splices
+int32_t join_prefetch(mh_ctx *ctx);
+// The MT19937 word streams of a sampling batch (units' spans and seeds, p; rng mode mitty) generated on `st` into
+// ctx->pf_words (the prefetch thread, after the next batch's splices); skipped (no error) while the jump polynomials
+// the batch needs are not resident yet
+int32_t prefetch_words(mh_ctx *ctx, hipStream_t st, int32_t n_units, const int64_t *p_min, const int64_t *p_max,
+                       const uint64_t *seeds, double p);   // the prefetch thread joined, the main stream after its splices
 
 // Stage timing (HIP events on ctx->stream).
 void stage_begin(mh_ctx *ctx, const char *name);

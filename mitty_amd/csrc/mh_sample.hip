@@ -21,6 +21,7 @@
 //                     by the compaction's store
 // The single-stream decode (k_shuffle_decode: MT19937 fused with the decode in one workgroup) remains as the exact
 // fallback for a unit whose decode ran out of pre-generated words.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1348,6 +1349,49 @@ struct SampleState {
   }
 };
 
+// One unit's draws and its four word streams' seeds and offsets in the batch word buffer (readgenerate's
+// illumina.generate_reads: int((p_max - p_min) * p * 1.2) draws; the seeds from the unit's RandomState)
+static void plan_unit_words(UnitPlan &q, int64_t p_min, int64_t p_max, uint64_t seed, double p, int32_t rng_mode,
+                            int64_t &words_total) {
+  q.p_min = p_min;
+  q.p_max = p_max;
+  q.n = (int64_t)((double)(q.p_max - q.p_min) * p * 1.2);   // int((p_max - p_min) * p * 1.2)
+  if (q.n < 0) q.n = 0;
+  HostMT sr;
+  sr.seed((uint32_t)seed);
+  q.s_tloc = (uint32_t)sr.interval(0xfffffffeull);
+  q.s_tlen = (uint32_t)sr.interval(0xfffffffeull);
+  q.s_shuf = (uint32_t)sr.interval(0xfffffffeull);
+  q.s_fo = (uint32_t)sr.interval(0xfffffffeull);
+  q.n_fo_words = (q.n + 3) / 4 + 1;
+  q.n_shuf_words = rng_mode == MH_RNG_MITTY ? shuffle_words_alloc(q.n) : 0;
+  auto take = [&](int64_t cnt) {   // 16-byte aligned stream offsets (vector loads in the decode)
+    int64_t at = words_total;
+    words_total = (words_total + cnt + 4 + 3) & ~(int64_t)3;
+    return at;
+  };
+  q.w_tloc = take(2 * q.n);
+  q.w_tlen = take(2 * q.n);
+  q.w_fo = take(q.n_fo_words);
+  q.w_shuf = take(q.n_shuf_words);
+}
+
+// The unit's four MT19937 streams as jump-ahead segments into `words`
+static void unit_seg_jobs(uint32_t *words, const UnitPlan &q, std::vector<SegJob> &jobs, int64_t &kmax) {
+  const int64_t SEG_WORDS = seg_words();
+  auto add_stream = [&](uint32_t *out, int64_t count, uint32_t seed) {
+    for (int64_t k = 0; k * SEG_WORDS < count; k++) {
+      int64_t s0 = k * SEG_WORDS;
+      jobs.push_back(SegJob{out, s0, std::min(SEG_WORDS, count - s0), seed, (int32_t)k});
+      kmax = std::max(kmax, k);
+    }
+  };
+  add_stream(words + q.w_tloc, 2 * q.n, q.s_tloc);
+  add_stream(words + q.w_tlen, 2 * q.n, q.s_tlen);
+  add_stream(words + q.w_fo, q.n_fo_words, q.s_fo);
+  add_stream(words + q.w_shuf, q.n_shuf_words, q.s_shuf);
+}
+
 // First half: plan, word streams, shuffle decode, geometric scans and — batch path — the permutation's sort and
 // heads; the per-unit path runs its units whole here.
 static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const int32_t *tpl_ids, const int64_t *p_min,
@@ -1366,30 +1410,10 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   int64_t words_total = 0, j_total = 0, n_max = 1;
   for (int32_t u = 0; u < n_units; u++) {
     UnitPlan &q = plan[u];
-    q.p_min = p_min[u];
-    q.p_max = p_max[u];
-    q.n = (int64_t)((double)(q.p_max - q.p_min) * p * 1.2);   // int((p_max - p_min) * p * 1.2)
-    if (q.n < 0) q.n = 0;
+    plan_unit_words(q, p_min[u], p_max[u], seeds[u], p, rng_mode, words_total);
     // (< 2^30 draws: the permutation sort's look-back counts are 30-bit; a 2x150 30x unit of 2^30 draws is a
     // 36 Gbp region)
     if (q.n > ((int64_t)1 << 30) - 8) return arg_fail(ctx, MH_E_ARG, "region too large for one work unit");
-    HostMT sr;
-    sr.seed((uint32_t)seeds[u]);
-    q.s_tloc = (uint32_t)sr.interval(0xfffffffeull);
-    q.s_tlen = (uint32_t)sr.interval(0xfffffffeull);
-    q.s_shuf = (uint32_t)sr.interval(0xfffffffeull);
-    q.s_fo = (uint32_t)sr.interval(0xfffffffeull);
-    q.n_fo_words = (q.n + 3) / 4 + 1;
-    q.n_shuf_words = rng_mode == MH_RNG_MITTY ? shuffle_words_alloc(q.n) : 0;
-    auto take = [&](int64_t cnt) {   // 16-byte aligned stream offsets (vector loads in the decode)
-      int64_t at = words_total;
-      words_total = (words_total + cnt + 4 + 3) & ~(int64_t)3;
-      return at;
-    };
-    q.w_tloc = take(2 * q.n);
-    q.w_tlen = take(2 * q.n);
-    q.w_fo = take(q.n_fo_words);
-    q.w_shuf = take(q.n_shuf_words);
     q.j_off = j_total; j_total += q.n + 4;
     n_max = std::max(n_max, q.n);
     TplSet &ts = ctx->tsets[tpl_ids[u]];
@@ -1407,6 +1431,15 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
   const int64_t nn = n_max + 1;
   ctx->batch_left = 0;
   for (const UnitPlan &q : plan) ctx->batch_left += q.n;
+  // this batch's word streams generated ahead by the prefetch thread (prefetch_words, same plan): its buffer becomes
+  // the batch's (the previous batch's tails, which read the old one, were resolved above)
+  PrefetchedWords &pw = ctx->pf_words;
+  const bool have_words = rng_mode == MH_RNG_MITTY && pw.valid && pw.p == p && pw.seeds.size() == (size_t)n_units &&
+                          std::equal(pw.seeds.begin(), pw.seeds.end(), seeds) &&
+                          std::equal(pw.p_min.begin(), pw.p_min.end(), p_min) &&
+                          std::equal(pw.p_max.begin(), pw.p_max.end(), p_max) && pw.words_total == words_total;
+  pw.valid = false;
+  if (have_words) std::swap(ctx->s[0], pw.buf);
   MH_TRY(ensure(ctx, ctx->s[0], 4 * (size_t)words_total + 64));
   MH_TRY(ensure(ctx, ctx->s[3], 4 * (size_t)j_total + 64));
   MH_TRY(ensure(ctx, ctx->s[4], 8 * nn));
@@ -1463,20 +1496,10 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
     std::vector<DecJob> dec;
     int64_t kmax = 0;
     const int64_t SEG_WORDS = seg_words();
-    auto add_stream = [&](uint32_t *out, int64_t count, uint32_t seed) {
-      for (int64_t k = 0; k * SEG_WORDS < count; k++) {
-        int64_t s0 = k * SEG_WORDS;
-        jobs.push_back(SegJob{out, s0, std::min(SEG_WORDS, count - s0), seed, (int32_t)k});
-        kmax = std::max(kmax, k);
-      }
-    };
     for (int32_t u = 0; u < n_units; u++) {
       UnitPlan &q = plan[u];
       if (q.n == 0) continue;
-      add_stream(words + q.w_tloc, 2 * q.n, q.s_tloc);
-      add_stream(words + q.w_tlen, 2 * q.n, q.s_tlen);
-      add_stream(words + q.w_fo, q.n_fo_words, q.s_fo);
-      add_stream(words + q.w_shuf, q.n_shuf_words, q.s_shuf);
+      unit_seg_jobs(words, q, jobs, kmax);
       dec.push_back(DecJob{words + q.w_shuf, q.n_shuf_words, q.n, jall + q.j_off, d_status + u});
     }
     if (!jobs.empty()) {
@@ -1486,11 +1509,13 @@ static int32_t sample_head(mh_ctx *ctx, SampleState &S, int32_t n_units, const i
       DecJob *d_dec = (DecJob *)((char *)ctx->s[2].p + ((sizeof(SegJob) * jobs.size() + 15) / 16) * 16);
       HIPCHK(ctx, hipMemcpyAsync(d_jobs, jobs.data(), sizeof(SegJob) * jobs.size(), hipMemcpyHostToDevice, st));
       HIPCHK(ctx, hipMemcpyAsync(d_dec, dec.data(), sizeof(DecJob) * dec.size(), hipMemcpyHostToDevice, st));
-      stage_begin(ctx, "sample_mt_segments");
-      hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)d_jobs,
-                         (const uint32_t *)ctx->jump_polys.p);
-      HIPCHK(ctx, hipGetLastError());
-      stage_end(ctx);
+      if (!have_words) {
+        stage_begin(ctx, "sample_mt_segments");
+        hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)d_jobs,
+                           (const uint32_t *)ctx->jump_polys.p);
+        HIPCHK(ctx, hipGetLastError());
+        stage_end(ctx);
+      }
       stage_begin(ctx, "sample_shuffle_decode");
       bool done = false;
       if (!ctx->decode_sequential) MH_TRY(decode_parallel(ctx, dec, d_status, &done));
@@ -1795,6 +1820,38 @@ int32_t tpl_resolve_all(mh_ctx *ctx) {
   if (!Sp) return MH_OK;
   for (UnitPlan &q : Sp->plan)
     if (q.out && q.out->pend >= 0) MH_TRY(tpl_resolve(ctx, *q.out));
+  return MH_OK;
+}
+
+int32_t prefetch_words(mh_ctx *ctx, hipStream_t st, int32_t n_units, const int64_t *p_min, const int64_t *p_max,
+                       const uint64_t *seeds, double p) {
+  PrefetchedWords &pw = ctx->pf_words;
+  pw.valid = false;
+  std::vector<UnitPlan> plan(n_units);
+  int64_t words_total = 0;
+  for (int32_t u = 0; u < n_units; u++) {
+    plan_unit_words(plan[u], p_min[u], p_max[u], seeds[u], p, MH_RNG_MITTY, words_total);
+    if (plan[u].n > ((int64_t)1 << 30) - 8) return MH_OK;   // (sample_head reports it)
+  }
+  MH_TRY(ensure(ctx, pw.buf, 4 * (size_t)words_total + 64));
+  std::vector<SegJob> jobs;
+  int64_t kmax = 0;
+  for (const UnitPlan &q : plan)
+    if (q.n > 0) unit_seg_jobs((uint32_t *)pw.buf.p, q, jobs, kmax);
+  // the jump polynomials are the main thread's (ensure_polys): without them resident the batch is not prefetched
+  if (jobs.empty() || ctx->jump_k < kmax + 1 || ctx->jump_seg != seg_words()) return MH_OK;
+  MH_TRY(ensure(ctx, pw.jobs, sizeof(SegJob) * jobs.size() + 64));
+  HIPCHK(ctx, hipMemcpyAsync(pw.jobs.p, jobs.data(), sizeof(SegJob) * jobs.size(), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_mt_segments, dim3((unsigned)jobs.size()), dim3(256), 0, st, (const SegJob *)pw.jobs.p,
+                     (const uint32_t *)ctx->jump_polys.p);
+  HIPCHK(ctx, hipGetLastError());
+  SYNCCHK(ctx, hipStreamSynchronize(st));   // (the job table's host copy lives until here)
+  pw.p = p;
+  pw.seeds.assign(seeds, seeds + n_units);
+  pw.p_min.assign(p_min, p_min + n_units);
+  pw.p_max.assign(p_max, p_max + n_units);
+  pw.words_total = words_total;
+  pw.valid = true;
   return MH_OK;
 }
 

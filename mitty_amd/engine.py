@@ -82,20 +82,26 @@ class Engine:
       for k, slot, r in zip(todo, slots, res):
         self._haps[k] = (slot,) + tuple(r)
 
-  def prefetch(self, keys, next_step=False):
-    """Build the haplotypes of the next batch while the current one is sampled and written
-    (mh_prefetch_haplotypes_vset: returns at once, the splices off the batch boundary's critical path).  Keys already
-    built are kept, unless next_step: then every key gets a fresh build (into its other slot generation), kept apart
-    until drop_haplotypes adopts them for the next step."""
+  def prefetch(self, units, next_step=False, p=None, rng='mitty'):
+    """Build the haplotypes of the next batch's units [(ps, ri, cpy, seed)] while the current one is sampled and
+    written, and (given p, rng 'mitty') their MT19937 word streams (mh_prefetch_haplotypes_vset: returns at once, the
+    splices and the word generation off the batch boundary's critical path).  Keys already built are kept, unless
+    next_step: then every key gets a fresh build (into its other slot generation), kept apart until drop_haplotypes
+    adopts them for the next step."""
+    keys = [(ri, cpy) for _, ri, cpy, _ in units]
     todo = [k for k in dict.fromkeys(keys) if k in self._vsets and k not in self._pre and
             (next_step or k not in self._haps)]
-    if not todo:
-      return
     slots = [self._slot(k) for k in todo]
-    self.ctx.prefetch_haplotypes_vset(slots, [ri for ri, _ in todo], [self._regions[ri][1] + 1 for ri, _ in todo],
-                                      [self._vsets[k] for k in todo])
     for k, slot in zip(todo, slots):   # (n_nodes, p_min, p_max: not known until the splice has run; get_nodes)
       (self._pre if next_step else self._haps)[k] = (slot, None, None, None)
+    home = self._pre if next_step else self._haps
+    words = p is not None and rng == 'mitty' and all(k in home for k in keys)
+    if not todo and not words:
+      return
+    self.ctx.prefetch_haplotypes_vset(slots, [ri for ri, _ in todo], [self._regions[ri][1] + 1 for ri, _ in todo],
+                                      [self._vsets[k] for k in todo],
+                                      [home[k][0] for k in keys] if words else (),
+                                      [u[3] for u in units] if words else (), p if words else 1.0)
 
   def drop_variants(self):
     for vset in self._vsets.values():
@@ -115,9 +121,10 @@ class Engine:
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
     unit's emission (e.g. to stream the arena to files).  Returns [(n, kept, b1, b2)] per unit; lazy=True returns None
     and leaves the units' results to collect(), so the caller queues the next batch while these writers run.
-    prefetch: the next batch's (ri, cpy) keys, built (Engine.prefetch) once unit `prefetch_after` is queued (-1:
-    before unit 0) instead of at the next batch's start; unit 0 measured best (its wait for the batch's head is over,
-    and the splices have the rest of the batch to finish before the next head needs them).
+    prefetch: the next batch's units [(ps, ri, cpy, seed)] (same p and rng), whose haplotypes and word streams are
+    built (Engine.prefetch) once unit `prefetch_after` is queued (-1: before unit 0) instead of at the next batch's
+    start; unit 0 measured best (its wait for the batch's head is over, and the prefetch has the rest of the batch to
+    finish before the next head needs it).
     """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])
     slots = [self.haplotype(ri, cpy, soa_of(ri, cpy))[0] for _, ri, cpy, _ in units]
@@ -136,14 +143,14 @@ class Engine:
     out = []
     at = min(prefetch_after, len(units) - 1) if prefetch else -1
     if prefetch and prefetch_after < 0:   # (before unit 0: beside this batch's sampling head)
-      self.prefetch(prefetch, prefetch_next_step)
+      self.prefetch(prefetch, prefetch_next_step, p, rng)
     for k, (ps, ri, cpy, seed) in enumerate(units):
       self.ctx.use_templates(base + k)
       self.ctx.emit_async(slots[k], '{}:{}:{}'.format(sample_name, worker_id, ps), self._regions[ri][0], cpy,
                           write_fastq2, unit_key=seed)
       self._lazy_n.append(self.ctx.template_count(base + k))
       if k == at:
-        self.prefetch(prefetch, prefetch_next_step)
+        self.prefetch(prefetch, prefetch_next_step, p, rng)
       if on_unit is not None:
         done = self.collect()
         out += done

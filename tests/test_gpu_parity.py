@@ -467,7 +467,7 @@ def test_prefetched_haplotypes_vs_build(native):
           nxt = batches[0] if last else batches[i + 1]
           eng.ctx.reset_output()
           res = eng.run_units(batch, lambda r, c: copies[r][c], p, 150, mdl['cum_tlen'], 'PF',
-                              prefetch=[(ri, cpy) for _, ri, cpy, _ in nxt] if prefetch else None,
+                              prefetch=nxt if prefetch else None,
                               prefetch_next_step=last, prefetch_after=0)
           outs.append((res, eng.ctx.fetch_output()))
       if prefetch:

@@ -509,7 +509,7 @@ def test_engine_prefetch_slot_generations():
       self.calls.append(('build', tuple(slots)))
       return [(3, 1, 9)] * len(slots)
 
-    def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets):
+    def prefetch_haplotypes_vset(self, slots, contig_ids, ref_starts, vsets, unit_slots=(), unit_seeds=(), p=1.0):
       assert not self.live & set(slots)
       self.live |= set(slots)
       self.calls.append(('prefetch', tuple(slots)))
@@ -523,15 +523,16 @@ def test_engine_prefetch_slot_generations():
   eng._vsets = {(0, 0): 0, (0, 1): 1, (1, 0): 64, (1, 1): 65}
   eng._haps, eng._pre, eng._gen = {}, {}, {}
   a, b = [(0, 0), (0, 1)], [(1, 0), (1, 1)]
+  ua, ub = [(0, ri, cpy, 5) for ri, cpy in a], [(0, ri, cpy, 5) for ri, cpy in b]
   eng.haplotypes(a)                        # step 1, batch 0
-  eng.prefetch(b)                          # batch 1 during batch 0
-  eng.prefetch(b)                          # (already built: nothing)
-  eng.prefetch(a, next_step=True)          # the next step's batch 0 during the last batch: fresh builds
+  eng.prefetch(ub)                         # batch 1 during batch 0
+  eng.prefetch(ub)                         # (already built: nothing)
+  eng.prefetch(ua, next_step=True)         # the next step's batch 0 during the last batch: fresh builds
   assert eng.ctx.calls == [('build', (0, 1)), ('prefetch', (64, 65)), ('prefetch', (2, 3))]
   assert set(eng._haps) == set(a + b) and set(eng._pre) == set(a)
   eng.drop_haplotypes()                    # step 2: the prefetched ones become current, the rest released
   assert eng.ctx.live == {2, 3} and set(eng._haps) == set(a) and not eng._pre
   eng.haplotypes(a + b)                    # a kept (built during step 1), b rebuilt in its other generation
   assert eng.ctx.calls[-1] == ('build', (66, 67))
-  eng.prefetch(a, next_step=True)
+  eng.prefetch(ua, next_step=True)
   assert eng.ctx.calls[-1] == ('prefetch', (0, 1))
