@@ -114,8 +114,10 @@ def parse():
                   help='wgs: splice the next batch\'s haplotypes and generate its MT19937 word streams while the '
                        'current batch is written (mh_prefetch_haplotypes_vset) instead of at the next batch\'s start '
                        '(+1.8 %%, 4 of 4 same-box alternations, profiles/r06/experiments/haplotype_prefetch_ab)')
-  ap.add_argument('--prefetch-after', type=int, default=0,
-                  help='--prefetch: once this unit of the batch is queued (-1: before the first; 0 measured best)')
+  ap.add_argument('--prefetch-after', type=int, default=1,
+                  help='--prefetch: once this unit of the batch is queued (-1: before the first; 1 measured best: '
+                       '+2.2 %% over 0 and +0.6 %% over -1, 4 of 4 alternations, '
+                       'profiles/r06/experiments/haplotype_prefetch_ab/placement)')
   ap.add_argument('--prefetch-last-after', type=int, default=-1,
                   help='--prefetch, the step\'s last batch (the next step\'s first batch prefetched): after this unit '
                        '(-1, before its first: the last batch is short and the next step\'s first batch has many '

@@ -115,7 +115,7 @@ class Engine:
     self._haps, self._pre = self._pre, {}
 
   def run_units(self, units, soa_of, p, rlen, cum_tlen, sample_name, worker_id=0, write_fastq2=True, rng='mitty',
-                on_unit=None, lazy=False, prefetch=None, prefetch_next_step=False, prefetch_after=0):
+                on_unit=None, lazy=False, prefetch=None, prefetch_next_step=False, prefetch_after=1):
     """Sample a batch of work units together, then emit them in order.
 
     units: [(ps, ri, cpy, rng_seed)]; soa_of(ri, cpy) -> variant SoA.  on_unit(ps, n, kept, b1, b2) runs after each
@@ -123,7 +123,7 @@ class Engine:
     and leaves the units' results to collect(), so the caller queues the next batch while these writers run.
     prefetch: the next batch's units [(ps, ri, cpy, seed)] (same p and rng), whose haplotypes and word streams are
     built (Engine.prefetch) once unit `prefetch_after` is queued (-1: before unit 0) instead of at the next batch's
-    start; unit 0 measured best (its wait for the batch's head is over, and the prefetch has the rest of the batch to
+    start; unit 1 measured best (the wait for the batch's head is over, and the prefetch has the rest of the batch to
     finish before the next head needs it).
     """
     self.haplotypes([(ri, cpy) for _, ri, cpy, _ in units])

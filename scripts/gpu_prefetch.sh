@@ -1,5 +1,5 @@
 #!/bin/bash
-# word-stream prefetch: the step's last batch prefetching before its first unit vs after it, against none
+# prefetch placement: after unit 0 (default; the step's last batch before unit 0) vs before unit 0 in every batch
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=prefetch5 REPS=4 BENCH_ARGS="--steps 10 --warmup 10" bash scripts/gpu_ab.sh 'pfw:' 'pfwl: -- --prefetch-last-after -1' 'nopf: -- --no-prefetch' || exit $?
+TAG=prefetch7 REPS=4 BENCH_ARGS="--steps 10 --warmup 10" bash scripts/gpu_ab.sh 'def:' 'm1all: -- --prefetch-after -1' 'a1: -- --prefetch-after 1' || exit $?
